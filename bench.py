@@ -1,0 +1,221 @@
+"""bench.py -- batched permission checks/s on MI355X (one process per GPU, snapshot replicas).
+
+Workload (BASELINE.json metric "permission checks/sec + GTEPS @1B tuples"): the synthetic
+Drive-like tuple graph (SURVEY.md 8d, C2/C4 generator; 8 layered group levels, power-law
+out-degrees, Zipf-ish popularity, seed 20250131) generated directly in HBM, and per GPU a
+1,000,000-check batch of doc#viewer@user queries (50% positive by random walks, 50% uniform,
+max_depth drawn from {0 (global), 1..10}, global max_read_depth 10).  A "step" is one
+kg_check_batch_device call over the whole batch (queries resident in HBM).
+
+Multi-GPU: `torch.distributed.run --nproc-per-node N bench.py --gpus N`: each rank builds the
+same snapshot on its GPU and checks its own batch (weak scaling, no data-path collective;
+SURVEY.md 8e "replicas").  Timing: barrier + synchronize on both sides of exactly K steps, max
+over ranks; rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--tuples", type=float, default=1e9, help="synthetic graph size (tuples)")
+    ap.add_argument("--batch", type=int, default=1_000_000, help="checks per step per GPU")
+    ap.add_argument("--global-depth", type=int, default=10)
+    ap.add_argument("--seed", type=int, default=20250131)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline time budget (0 = skip)")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    import torch
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", rank=rank, world_size=world)
+    torch.cuda.set_device(local)
+
+    from keto_amd import _lib
+    from keto_amd.engine import Snapshot
+    L = _lib.load()
+
+    t_build = time.time()
+    snap = Snapshot.synthetic(int(a.tuples), seed=a.seed, device=local)
+    info = snap.info()
+    t_build = time.time() - t_build
+
+    B = a.batch
+    dq = torch.empty((B, 7), dtype=torch.int32, device=f"cuda:{local}")
+    _lib.check(L.kg_synth_queries(snap.handle, 1000 + rank, B, dq.data_ptr()), "kg_synth_queries")
+    dout = torch.empty(B, dtype=torch.uint8, device=f"cuda:{local}")
+    derr = torch.empty(B, dtype=torch.int32, device=f"cuda:{local}")
+    stream = torch.cuda.current_stream(local).cuda_stream
+
+    def step(st=None):
+        rc = L.kg_check_batch_device(snap.handle, dq.data_ptr(), B, a.global_depth, dout.data_ptr(), derr.data_ptr(),
+                                     C.byref(st) if st is not None else None, C.c_void_p(stream))
+        _lib.check(rc, "kg_check_batch_device")
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    stats = [_lib.kg_stats() for _ in range(a.steps)]
+    lat = []
+    t0 = time.perf_counter()
+    for k in range(a.steps):
+        s0 = time.perf_counter()
+        step(stats[k])  # stats => the call waits for its batch: per-batch latency
+        lat.append(time.perf_counter() - s0)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    res = dout.cpu().numpy()
+    errs = derr.cpu().numpy()
+    assert (errs == 0).all() and (res <= 1).all(), "unexpected errors in the synthetic batch"
+    edges = sum(s.edges_read for s in stats)
+    if dist:
+        t = torch.tensor([float(edges)], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t)
+        edges = t.item()
+    l_bytes = np.array([8 * s.light_rows_opened + 4 * s.light_edges_read + 16 * s.light_probes for s in stats], float)
+    l_ms = np.array([s.light_ms for s in stats], float)
+    achieved = float(l_bytes.mean() / (l_ms.mean() * 1e-3) / 1e9)
+    traffic = pmc_traffic(int(a.tuples), B)
+
+    value = world * B * a.steps / elapsed
+    out = {
+        "metric": "permission checks/sec (batched check, synthetic Drive-like graph)",
+        "value": value,
+        "unit": "checks/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": elapsed / a.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic (device-generated Drive-like tuple graph, seed %d)" % a.seed,
+        "config": {"workload": "C2/C4 generator @ %.3g tuples, %d checks/step/GPU, max_read_depth %d"
+                               % (a.tuples, B, a.global_depth),
+                   "tuples": info["rows"], "nodes": info["nodes"], "set_edges": info["set_edges"],
+                   "batch_per_gpu": B, "global_max_read_depth": a.global_depth, "parallelism": f"replica{world}"},
+        "gteps": edges / elapsed / 1e9,
+        "p99_batch_ms": float(np.percentile(np.array(lat) * 1e3, 99)),
+        "allowed_fraction": float(res.mean()),
+        "tiers": {"light": int(stats[-1].n_light), "heavy": int(stats[-1].n_heavy),
+                  "general": int(stats[-1].n_general)},
+        "snapshot_build_s": t_build,
+        "roofline": {"kernel": "k_light", "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "bytes_model": "8*rows_opened + 4*edges_read + 16*direct_probes (per k_light launch)",
+                     "launch_ms": float(l_ms.mean()), "bytes_per_launch": float(l_bytes.mean())},
+    }
+    if rank == 0 and world == 1 and a.cpu_seconds > 0:
+        out["cpu_baseline"] = cpu_baseline(snap, dq, a)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+def pmc_traffic(tuples: int, batch: int):
+    """HBM bytes per k_light launch from the committed rocprofv3 --pmc pass (profiles/), if one
+    was taken on this exact workload; else None."""
+    p = os.path.join(ROOT, "profiles", "pmc_k_light.json")
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        if int(d.get("tuples", -1)) == tuples and int(d.get("batch", -1)) == batch:
+            return d.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def cpu_baseline(snap, dq, a) -> dict:
+    """The C restatement of the reference engine (oracle, sequential Go DFS schedule with visited
+    sets) over the same row index, on a bounded sample of the same batch."""
+    from keto_amd import _lib
+    from oracle.oracle import POLICY_DFS, Oracle
+    L = _lib.load()
+    info = snap.info()
+    nn, nr = info["nodes"], info["rows"]
+    row_off = np.zeros(nn + 1, np.uint64)
+    row_subj = np.zeros(nr, np.uint32)
+    nd = [np.zeros(nn, np.uint32) for _ in range(3)]
+    p = lambda x: x.ctypes.data_as(C.c_void_p)
+    _lib.check(L.kg_snapshot_export_csr(snap.handle, p(row_off), p(row_subj), p(nd[0]), p(nd[1]), p(nd[2])),
+               "kg_snapshot_export_csr")
+    threads = max(1, min(a.cpu_threads, os.cpu_count() or 1))
+    o = Oracle.from_csr(0, nd[0], nd[1], nd[2], row_off, row_subj, nthreads=threads)
+    del row_subj
+    q = dq[:200_000].cpu().numpy().view(np.uint32)
+    node = q[:, 1].copy()  # synthetic docs: node id == object id
+    subj = q[:, 4].copy()
+    dep = q[:, 6].view(np.int32).copy()
+
+    def run(n, th):
+        t = time.perf_counter()
+        o.check_nodes_batch(node[:n], subj[:n], dep[:n], a.global_depth, POLICY_DFS, th)
+        return time.perf_counter() - t
+
+    res = {}
+    for th, budget in ((threads, a.cpu_seconds), (1, a.cpu_seconds / 3)):
+        n = 256
+        t = run(n, th)
+        while t < budget / 8 and n < len(node):
+            n = min(len(node), n * 4)
+            t = run(n, th)
+        res[th] = (n / t, n, t)
+    v, n, t = res[threads]
+    return {"value": v, "unit": "checks/s", "cores": threads, "kind": "port",
+            "sample": f"first {n} checks of the rank-0 batch on the same graph ({t:.1f} s), sequential Go-order DFS "
+                      f"with visited sets (oracle/keto_oracle.c POLICY_DFS), {threads} host threads",
+            "value_1thread": res[1][0], "host_cpu": host_cpu()}
+
+
+def host_cpu() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip() + f" (nproc {os.cpu_count()})"
+    except OSError:
+        pass
+    return f"nproc {os.cpu_count()}"
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,187 @@
+/*
+ * ketogpu.h -- C ABI of libketogpu.so, the MI355X (gfx950) batched permission-check engine.
+ *
+ * This is the drop-in boundary for Ory Keto's check / expand hot path.  A Go host binds it
+ * through cgo; the Python host in keto_amd/ binds it through ctypes.
+ * Plain C types only: dense u32 ids, POD structs, caller-owned input/output buffers.
+ *
+ * Every entry point names the reference interface it replaces (paths relative to the
+ * reference checkout, ryukinix/keto @ 2025-01-31):
+ *
+ *   kg_snapshot_create   relationtuple.Manager.GetRelationTuples  internal/relationtuple/definitions.go:19-25
+ *                        + Persister.GetRelationTuples           internal/persistence/sql/relationtuples.go:203-244
+ *                        + namespace AST / config                internal/namespace/ast/ast_definitions.go:5-68,
+ *                                                                internal/check/engine.go:209-229 (astRelationFor)
+ *   kg_check_batch       check.Engine.CheckIsMember (looped)      internal/check/engine.go:54-60
+ *                        check.Engine.CheckRelationTuple          internal/check/engine.go:65-80
+ *                        (new BatchCheck, SURVEY.md 8b: equals a loop of CheckIsMember)
+ *   kg_expand_batch      expand.Engine.BuildTree                  internal/expand/engine.go:35-104
+ *   kg_last_error        herodot / errors.WithStack message text  internal/check/engine.go:228, rewrites.go:15-17
+ *
+ * Id spaces (the caller interns strings; the reference maps strings to UUIDv5 first,
+ * internal/persistence/sql/uuid_mapping.go:31-66 -- a dense id per UUID is equivalent):
+ *   namespace ids  < 65535, relation ids < 65535 (global over namespaces),
+ *   object ids     < 2^31-1, one space for objects AND subject ids (both are UUIDs upstream).
+ * Rows must be passed in shard_id order (the order GetRelationTuples returns them).
+ */
+#ifndef KETOGPU_H
+#define KETOGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KG_SUBJECT_ID 0xFFFFFFFFu /* kg_tuple.sns value marking a SubjectID subject (id in sobj) */
+
+/* One relation tuple ns:obj#rel@subject (internal/relationtuple/definitions.go:46-57). */
+typedef struct {
+  uint32_t ns, obj, rel;    /* namespace, object, relation                         */
+  uint32_t sns, sobj, srel; /* subject set (sns,sobj,srel), or sns = KG_SUBJECT_ID */
+} kg_tuple;
+
+/* A check request: the tuple to test plus the request max-depth (<= 0 means "use global"),
+ * exactly the arguments of CheckIsMember(ctx, tuple, restDepth). */
+typedef struct {
+  kg_tuple t;
+  int32_t max_depth;
+} kg_query;
+
+/* An expand root: a subject set, or a subject id (sns = KG_SUBJECT_ID) -- BuildTree's Subject. */
+typedef struct {
+  uint32_t sns, sobj, srel;
+  int32_t max_depth;
+} kg_set;
+
+/* Interning metadata. */
+typedef struct {
+  uint32_t n_namespaces;
+  uint32_t n_relations;
+  uint32_t wildcard_rel; /* id of the "..." relation (engine.go:40), or 0xFFFFFFFF */
+} kg_dict;
+
+/* Compiled namespace configuration (the OPL / ast.Relation rewrites).
+ * rw nodes: kind 0 = or, 1 = and (SubjectSetRewrite), 2 = ComputedSubjectSet(rel),
+ *           3 = TupleToSubjectSet(rel, crel), 4 = InvertResult (its one child in child[first]).
+ * Children of node i are child[first .. first+count).  Relation j of namespace rel_ns[j]
+ * named rel_rel[j] has rewrite root rel_root[j] (-1: declared without rewrite).
+ * ns_has_rel[ns] != 0 when the namespace is configured with at least one relation
+ * (engine.go:219-228: otherwise every relation is accepted without rewrite). */
+typedef struct {
+  int32_t kind, rel, crel, first, count;
+} kg_rw_node;
+
+typedef struct {
+  uint32_t n_ns;
+  const uint8_t* ns_has_rel;
+  uint32_t n_rel;
+  const uint32_t* rel_ns;
+  const uint32_t* rel_rel;
+  const int32_t* rel_root;
+  uint32_t n_rw;
+  const kg_rw_node* rw;
+  uint32_t n_child;
+  const int32_t* child;
+} kg_rewrite_prog;
+
+/* Per-batch counters; the algorithmic-byte model of SURVEY.md 8d is
+ * B = 8*rows_opened + 4*edges_read + 16*direct_probes + 16*frontier_hbm. */
+typedef struct {
+  uint64_t rows_opened;
+  uint64_t edges_read;
+  uint64_t direct_probes;
+  uint64_t frontier_hbm;
+  uint64_t n_light, n_heavy, n_general; /* queries finished per engine tier */
+  uint64_t light_rows_opened, light_edges_read, light_probes; /* k_light's share of the counters */
+  double kernel_ms;                     /* device time of the whole batch (HIP events)  */
+  double light_ms;                      /* device time of the k_light launch             */
+} kg_stats;
+
+/* Per-query outputs of kg_check_batch. */
+#define KG_NOT_MEMBER 0
+#define KG_IS_MEMBER 1
+#define KG_ERROR 2
+
+/* err_code values (mirror the reference's error sources). */
+#define KG_ERR_NONE 0
+#define KG_ERR_RELATION_NOT_FOUND 1 /* engine.go:228  relation %q not found            */
+#define KG_ERR_NOT_IMPLEMENTED 2    /* rewrites.go:15-17 not implemented                */
+#define KG_ERR_REWRITE_CYCLE 3      /* computed-subject-set cycle (reference recurses forever) */
+#define KG_ERR_RESOURCE 4           /* exceeded an engine capacity                       */
+
+/* Expand output: pre-order records.  type 1 = union, 2 = leaf (ketoapi TreeNodeUnion/Leaf).
+ * Root r of the batch owns records [root_off[r], root_off[r+1]); an empty range = nil tree. */
+typedef struct {
+  uint8_t type;
+  uint8_t is_set;  /* 1: subject set (ns,obj,rel); 0: subject id in obj */
+  uint16_t pad;
+  uint32_t ns, obj, rel;
+  uint32_t n_children;
+} kg_tree_node;
+
+typedef struct {
+  kg_tree_node* nodes;
+  uint64_t n_nodes;
+  uint64_t* root_off; /* n_roots + 1 entries */
+  uint64_t n_roots;
+} kg_tree_buf;
+
+typedef struct kg_snapshot kg_snapshot;
+
+/* Synthetic "Drive-like" tuple graph generated on the device.
+ * Deterministic in (seed, index); kg_snapshot_export returns its rows. */
+typedef struct {
+  uint64_t n_tuples_target; /* ~total tuples (docs#viewer + group#member)           */
+  uint64_t seed;
+  uint32_t n_layers;        /* group layers (8)                                    */
+  uint32_t max_degree;      /* out-degree truncation (1e5)                        */
+  float set_fraction;       /* fraction of group#member subjects that are subject sets */
+  float doc_set_fraction;   /* fraction of doc#viewer subjects that are L0 groups  */
+} kg_synth_params;
+
+/* ---- snapshot --------------------------------------------------------------------------- */
+int kg_snapshot_create(const kg_tuple* rows, size_t n, const kg_dict* dict, const kg_rewrite_prog* prog,
+                       int device, kg_snapshot** out);
+int kg_snapshot_synthetic(const kg_synth_params* params, int device, kg_snapshot** out);
+void kg_snapshot_destroy(kg_snapshot* s);
+/* sizes: [0]=nodes [1]=rows [2]=set edges [3]=device bytes */
+int kg_snapshot_info(const kg_snapshot* s, uint64_t* info4);
+/* Namespace / relation / object ids the synthetic generator uses:
+ * ids6 = {ns_doc, ns_group, ns_user(unused for ids), rel_viewer, rel_member, n_objects}. */
+int kg_synth_ids(const kg_snapshot* s, uint32_t* ids6);
+/* Copies the snapshot's rows back (shard order) as kg_tuple, for oracle cross-checks.
+ * rows may be NULL to query the count. */
+int64_t kg_snapshot_export(const kg_snapshot* s, kg_tuple* rows, uint64_t cap);
+/* Copies the row index back: row_off[nodes+1], row_subj[rows] (tagged: bit31 = subject set ->
+ * node id, else subject id), node triples nd_ns/nd_obj/nd_rel[nodes].  For the CPU baseline. */
+int kg_snapshot_export_csr(const kg_snapshot* s, uint64_t* row_off, uint32_t* row_subj, uint32_t* nd_ns,
+                           uint32_t* nd_obj, uint32_t* nd_rel);
+
+/* ---- check ------------------------------------------------------------------------------ */
+/* Host buffers: q[n] in, out[n] (KG_NOT_MEMBER / KG_IS_MEMBER / KG_ERROR), err_code[n] (may be
+ * NULL), stats (may be NULL).  Synchronous. */
+int kg_check_batch(kg_snapshot* s, const kg_query* q, size_t n, int32_t global_max_depth, uint8_t* out,
+                   uint32_t* err_code, kg_stats* stats);
+/* Device-resident variant: d_q / d_out / d_err are device pointers (HBM), stream is a
+ * hipStream_t (NULL = the snapshot's stream).  Asynchronous unless stats != NULL. */
+int kg_check_batch_device(kg_snapshot* s, const kg_query* d_q, size_t n, int32_t global_max_depth,
+                          uint8_t* d_out, uint32_t* d_err, kg_stats* stats, void* stream);
+/* Device-side synthetic check batch for a synthetic snapshot: 50% positive (reverse walks) and
+ * 50% uniform doc#viewer@user queries, max_depth in {0,1..10}.  d_q is a device buffer. */
+int kg_synth_queries(kg_snapshot* s, uint64_t seed, size_t n, kg_query* d_q);
+
+/* ---- expand ----------------------------------------------------------------------------- */
+int kg_expand_batch(kg_snapshot* s, const kg_set* roots, size_t n, int32_t global_max_depth, kg_tree_buf* out);
+void kg_tree_free(kg_tree_buf* t);
+
+/* ---- errors ----------------------------------------------------------------------------- */
+/* Thread-local text of the last failing call; returns its length. */
+size_t kg_last_error(char* buf, size_t len);
+const char* kg_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KETOGPU_H */

@@ -1,0 +1,123 @@
+"""ctypes binding of libketogpu.so (include/ketogpu.h).  Fails loudly when the HIP library is
+missing -- there is no CPU fallback on the product path."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libketogpu.so")
+
+KG_SUBJECT_ID = 0xFFFFFFFF
+KG_NOT_MEMBER, KG_IS_MEMBER, KG_ERROR = 0, 1, 2
+KG_ERR_NONE, KG_ERR_RELATION_NOT_FOUND, KG_ERR_NOT_IMPLEMENTED, KG_ERR_REWRITE_CYCLE, KG_ERR_RESOURCE = 0, 1, 2, 3, 4
+
+
+class kg_tuple(C.Structure):
+    _fields_ = [(n, C.c_uint32) for n in ("ns", "obj", "rel", "sns", "sobj", "srel")]
+
+
+class kg_query(C.Structure):
+    _fields_ = [("t", kg_tuple), ("max_depth", C.c_int32)]
+
+
+class kg_set(C.Structure):
+    _fields_ = [("sns", C.c_uint32), ("sobj", C.c_uint32), ("srel", C.c_uint32), ("max_depth", C.c_int32)]
+
+
+class kg_dict(C.Structure):
+    _fields_ = [("n_namespaces", C.c_uint32), ("n_relations", C.c_uint32), ("wildcard_rel", C.c_uint32)]
+
+
+class kg_rw_node(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in ("kind", "rel", "crel", "first", "count")]
+
+
+class kg_rewrite_prog(C.Structure):
+    _fields_ = [("n_ns", C.c_uint32), ("ns_has_rel", C.c_void_p), ("n_rel", C.c_uint32), ("rel_ns", C.c_void_p),
+                ("rel_rel", C.c_void_p), ("rel_root", C.c_void_p), ("n_rw", C.c_uint32), ("rw", C.c_void_p),
+                ("n_child", C.c_uint32), ("child", C.c_void_p)]
+
+
+class kg_stats(C.Structure):
+    _fields_ = [("rows_opened", C.c_uint64), ("edges_read", C.c_uint64), ("direct_probes", C.c_uint64),
+                ("frontier_hbm", C.c_uint64), ("n_light", C.c_uint64), ("n_heavy", C.c_uint64),
+                ("n_general", C.c_uint64), ("light_rows_opened", C.c_uint64), ("light_edges_read", C.c_uint64),
+                ("light_probes", C.c_uint64), ("kernel_ms", C.c_double), ("light_ms", C.c_double)]
+
+    def as_dict(self) -> dict:
+        return {n: getattr(self, n) for n, _ in self._fields_}
+
+
+class kg_tree_node(C.Structure):
+    _fields_ = [("type", C.c_uint8), ("is_set", C.c_uint8), ("pad", C.c_uint16), ("ns", C.c_uint32),
+                ("obj", C.c_uint32), ("rel", C.c_uint32), ("n_children", C.c_uint32)]
+
+
+class kg_tree_buf(C.Structure):
+    _fields_ = [("nodes", C.POINTER(kg_tree_node)), ("n_nodes", C.c_uint64), ("root_off", C.POINTER(C.c_uint64)),
+                ("n_roots", C.c_uint64)]
+
+
+class kg_synth_params(C.Structure):
+    _fields_ = [("n_tuples_target", C.c_uint64), ("seed", C.c_uint64), ("n_layers", C.c_uint32),
+                ("max_degree", C.c_uint32), ("set_fraction", C.c_float), ("doc_set_fraction", C.c_float)]
+
+
+# every symbol include/ketogpu.h declares
+EXPORTS = ["kg_snapshot_create", "kg_snapshot_synthetic", "kg_snapshot_destroy", "kg_snapshot_info", "kg_synth_ids",
+           "kg_snapshot_export", "kg_snapshot_export_csr", "kg_check_batch", "kg_check_batch_device", "kg_synth_queries", "kg_expand_batch",
+           "kg_tree_free", "kg_last_error", "kg_version"]
+
+
+class KetoGPUError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def load(path: str = LIB_PATH):
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise KetoGPUError(f"libketogpu.so not found at {path}: build it with `python -m keto_amd.build` "
+                           "(there is no CPU fallback)")
+    L = C.CDLL(path)
+    vp, sz, i32, u32, u64 = C.c_void_p, C.c_size_t, C.c_int32, C.c_uint32, C.c_uint64
+    L.kg_snapshot_create.argtypes = [vp, sz, C.POINTER(kg_dict), C.POINTER(kg_rewrite_prog), C.c_int, C.POINTER(vp)]
+    L.kg_snapshot_synthetic.argtypes = [C.POINTER(kg_synth_params), C.c_int, C.POINTER(vp)]
+    L.kg_snapshot_destroy.argtypes = [vp]
+    L.kg_snapshot_destroy.restype = None
+    L.kg_snapshot_info.argtypes = [vp, vp]
+    L.kg_synth_ids.argtypes = [vp, vp]
+    L.kg_snapshot_export.argtypes = [vp, vp, u64]
+    L.kg_snapshot_export.restype = C.c_int64
+    L.kg_snapshot_export_csr.argtypes = [vp, vp, vp, vp, vp, vp]
+    L.kg_snapshot_export_csr.restype = C.c_int
+    L.kg_check_batch.argtypes = [vp, vp, sz, i32, vp, vp, C.POINTER(kg_stats)]
+    L.kg_check_batch_device.argtypes = [vp, vp, sz, i32, vp, vp, C.POINTER(kg_stats), vp]
+    L.kg_synth_queries.argtypes = [vp, u64, sz, vp]
+    L.kg_expand_batch.argtypes = [vp, vp, sz, i32, C.POINTER(kg_tree_buf)]
+    L.kg_tree_free.argtypes = [C.POINTER(kg_tree_buf)]
+    L.kg_tree_free.restype = None
+    L.kg_last_error.argtypes = [C.c_char_p, sz]
+    L.kg_last_error.restype = sz
+    L.kg_version.restype = C.c_char_p
+    for name in ("kg_snapshot_create", "kg_snapshot_synthetic", "kg_snapshot_info", "kg_synth_ids", "kg_check_batch",
+                 "kg_check_batch_device", "kg_synth_queries", "kg_expand_batch"):
+        getattr(L, name).restype = C.c_int
+    _lib = L
+    return L
+
+
+def last_error() -> str:
+    buf = C.create_string_buffer(2048)
+    load().kg_last_error(buf, 2048)
+    return buf.value.decode(errors="replace")
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise KetoGPUError(f"{what} failed ({rc}): {last_error()}")

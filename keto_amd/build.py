@@ -1,0 +1,63 @@
+"""Builds libketogpu.so in-tree with hipcc for gfx950 (no torch types cross the C ABI)."""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+LIB_DIR = os.path.join(HERE, "lib")
+LIB = os.path.join(LIB_DIR, "libketogpu.so")
+SOURCES = ["kg_abi.cpp", "kg_snapshot.hip", "kg_check.hip", "kg_interp.hip", "kg_expand.hip"]
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("KG_OFFLOAD_ARCH", "gfx950")
+
+
+def sources():
+    return [os.path.join(CSRC, s) for s in SOURCES if os.path.exists(os.path.join(CSRC, s))]
+
+
+def stale() -> bool:
+    if not os.path.exists(LIB):
+        return True
+    t = os.path.getmtime(LIB)
+    deps = sources() + [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
+    deps.append(os.path.join(ROOT, "include", "ketogpu.h"))
+    return any(os.path.getmtime(p) > t for p in deps)
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if not force and not stale():
+        return LIB
+    os.makedirs(LIB_DIR, exist_ok=True)
+    objs = []
+    jobs = []
+    for src in sources():
+        obj = os.path.join(LIB_DIR, os.path.basename(src) + ".o")
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-c", "-x", "hip", src, "-o", obj,
+               "-I", os.path.join(ROOT, "include"), "-Wall", "-Wno-unused-function", "-Wno-unused-result"]
+        jobs.append((cmd, src))
+        objs.append(obj)
+    procs = [(subprocess.Popen(c, stdout=subprocess.PIPE, stderr=subprocess.STDOUT), s) for c, s in jobs]
+    failed = False
+    for p, s in procs:
+        out, _ = p.communicate()
+        if p.returncode != 0 or verbose:
+            sys.stderr.write(out.decode(errors="replace"))
+        if p.returncode != 0:
+            failed = True
+    if failed:
+        raise RuntimeError("hipcc failed")
+    tmp = LIB + ".tmp"
+    subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs + ["-lpthread"],
+                   check=True)
+    os.replace(tmp, LIB)
+    for o in objs:
+        os.remove(o)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose="-v" in sys.argv))

@@ -1,0 +1,219 @@
+// kg_abi.cpp -- the extern "C" boundary of libketogpu.so (declared in include/ketogpu.h).
+// No exception crosses the ABI; every failure returns non-zero and sets kg_last_error().
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+
+#include "kg_snapshot.h"
+
+namespace kg {
+static thread_local std::string g_err;
+
+int set_error(int code, const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+void clear_error() { g_err.clear(); }
+}  // namespace kg
+
+using kg::Snapshot;
+using kg::set_error;
+
+#define KG_GUARD_BEGIN try {
+#define KG_GUARD_END                                          \
+  }                                                           \
+  catch (const std::bad_alloc&) {                             \
+    return set_error(-4, "host allocation failed");           \
+  }                                                           \
+  catch (const std::exception& ex) {                          \
+    return set_error(-5, "internal error: %s", ex.what());    \
+  }                                                           \
+  catch (...) {                                               \
+    return set_error(-5, "internal error");                   \
+  }
+
+extern "C" {
+
+const char* kg_version(void) { return "ketogpu 0.1 (gfx950)"; }
+
+size_t kg_last_error(char* buf, size_t len) {
+  const std::string& e = kg::g_err;
+  if (buf && len) {
+    size_t n = e.size() < len - 1 ? e.size() : len - 1;
+    memcpy(buf, e.data(), n);
+    buf[n] = 0;
+  }
+  return e.size();
+}
+
+int kg_snapshot_create(const kg_tuple* rows, size_t n, const kg_dict* dict, const kg_rewrite_prog* prog, int device,
+                       kg_snapshot** out) {
+  KG_GUARD_BEGIN
+  if (!out) return set_error(-2, "out is NULL");
+  *out = nullptr;
+  if (n && !rows) return set_error(-2, "rows is NULL");
+  Snapshot* s = new Snapshot();
+  int rc = s->init_device(device);
+  if (!rc) rc = s->create_from_tuples(rows, n, dict, prog);
+  if (rc) {
+    delete s;
+    return rc;
+  }
+  *out = reinterpret_cast<kg_snapshot*>(s);
+  kg::clear_error();
+  return 0;
+  KG_GUARD_END
+}
+
+int kg_snapshot_synthetic(const kg_synth_params* params, int device, kg_snapshot** out) {
+  KG_GUARD_BEGIN
+  if (!out || !params) return set_error(-2, "NULL argument");
+  *out = nullptr;
+  Snapshot* s = new Snapshot();
+  int rc = s->init_device(device);
+  if (!rc) rc = s->create_synthetic(params);
+  if (rc) {
+    delete s;
+    return rc;
+  }
+  *out = reinterpret_cast<kg_snapshot*>(s);
+  return 0;
+  KG_GUARD_END
+}
+
+void kg_snapshot_destroy(kg_snapshot* s) { delete reinterpret_cast<Snapshot*>(s); }
+
+int kg_snapshot_info(const kg_snapshot* sp, uint64_t* info4) {
+  if (!sp || !info4) return set_error(-2, "NULL argument");
+  const Snapshot* s = reinterpret_cast<const Snapshot*>(sp);
+  info4[0] = s->ds.n_nodes;
+  info4[1] = s->h_row_off_last;
+  info4[2] = s->n_set_edges;
+  info4[3] = s->device_bytes;
+  return 0;
+}
+
+int kg_synth_ids(const kg_snapshot* sp, uint32_t* ids6) {
+  if (!sp || !ids6) return set_error(-2, "NULL argument");
+  const Snapshot* s = reinterpret_cast<const Snapshot*>(sp);
+  if (!s->is_synth) return set_error(-2, "not a synthetic snapshot");
+  const kg::SynthLayout& L = s->synth;
+  ids6[0] = L.ns_doc;
+  ids6[1] = L.ns_group;
+  ids6[2] = L.ns_user;
+  ids6[3] = L.rel_viewer;
+  ids6[4] = L.rel_member;
+  ids6[5] = L.n_docs + L.n_groups + L.n_users;
+  return 0;
+}
+
+int64_t kg_snapshot_export(const kg_snapshot* sp, kg_tuple* rows, uint64_t cap) {
+  KG_GUARD_BEGIN
+  if (!sp) return set_error(-2, "NULL snapshot");
+  Snapshot* s = const_cast<Snapshot*>(reinterpret_cast<const Snapshot*>(sp));
+  std::lock_guard<std::mutex> lk(s->mu);
+  hipSetDevice(s->device);
+  return s->export_rows(rows, cap);
+  KG_GUARD_END
+}
+
+int kg_snapshot_export_csr(const kg_snapshot* sp, uint64_t* row_off, uint32_t* row_subj, uint32_t* nd_ns,
+                           uint32_t* nd_obj, uint32_t* nd_rel) {
+  KG_GUARD_BEGIN
+  if (!sp) return set_error(-2, "NULL snapshot");
+  Snapshot* s = const_cast<Snapshot*>(reinterpret_cast<const Snapshot*>(sp));
+  std::lock_guard<std::mutex> lk(s->mu);
+  HIPC(hipSetDevice(s->device));
+  size_t nn = s->ds.n_nodes;
+  if (row_off) HIPC(hipMemcpy(row_off, s->ds.row_off, (nn + 1) * 8, hipMemcpyDeviceToHost));
+  if (row_subj && s->h_row_off_last)
+    HIPC(hipMemcpy(row_subj, s->ds.row_subj, s->h_row_off_last * 4, hipMemcpyDeviceToHost));
+  if (nn && nd_ns) HIPC(hipMemcpy(nd_ns, s->ds.nd_ns, nn * 4, hipMemcpyDeviceToHost));
+  if (nn && nd_obj) HIPC(hipMemcpy(nd_obj, s->ds.nd_obj, nn * 4, hipMemcpyDeviceToHost));
+  if (nn && nd_rel) HIPC(hipMemcpy(nd_rel, s->ds.nd_rel, nn * 4, hipMemcpyDeviceToHost));
+  return 0;
+  KG_GUARD_END
+}
+
+int kg_check_batch_device(kg_snapshot* sp, const kg_query* d_q, size_t n, int32_t global_max_depth, uint8_t* d_out,
+                          uint32_t* d_err, kg_stats* stats, void* stream) {
+  KG_GUARD_BEGIN
+  if (!sp) return set_error(-2, "NULL snapshot");
+  Snapshot* s = reinterpret_cast<Snapshot*>(sp);
+  std::lock_guard<std::mutex> lk(s->mu);
+  return kg::check_batch_device(s, d_q, n, global_max_depth, d_out, d_err, stats, (hipStream_t)stream);
+  KG_GUARD_END
+}
+
+int kg_check_batch(kg_snapshot* sp, const kg_query* q, size_t n, int32_t global_max_depth, uint8_t* out,
+                   uint32_t* err_code, kg_stats* stats) {
+  KG_GUARD_BEGIN
+  if (!sp) return set_error(-2, "NULL snapshot");
+  if (n && (!q || !out)) return set_error(-2, "NULL buffer");
+  Snapshot* s = reinterpret_cast<Snapshot*>(sp);
+  std::lock_guard<std::mutex> lk(s->mu);
+  HIPC(hipSetDevice(s->device));
+  if (n == 0) {
+    if (stats) memset(stats, 0, sizeof *stats);
+    return 0;
+  }
+  kg_query* d_q = nullptr;
+  uint8_t* d_out = nullptr;
+  uint32_t* d_err = nullptr;
+  HIPC(hipMalloc(&d_q, n * sizeof(kg_query)));
+  HIPC(hipMalloc(&d_out, n));
+  HIPC(hipMalloc(&d_err, n * 4));
+  int rc = 0;
+  if (hipMemcpyAsync(d_q, q, n * sizeof(kg_query), hipMemcpyHostToDevice, s->stream) != hipSuccess)
+    rc = set_error(-1, "H2D copy failed");
+  if (!rc) rc = kg::check_batch_device(s, d_q, n, global_max_depth, d_out, d_err, stats, s->stream);
+  if (!rc && hipMemcpyAsync(out, d_out, n, hipMemcpyDeviceToHost, s->stream) != hipSuccess)
+    rc = set_error(-1, "D2H copy failed");
+  if (!rc && err_code && hipMemcpyAsync(err_code, d_err, n * 4, hipMemcpyDeviceToHost, s->stream) != hipSuccess)
+    rc = set_error(-1, "D2H copy failed");
+  if (!rc) {
+    hipError_t e = hipStreamSynchronize(s->stream);
+    if (e != hipSuccess) rc = set_error(-1, "batch failed: %s", hipGetErrorString(e));
+  }
+  hipFree(d_q);
+  hipFree(d_out);
+  hipFree(d_err);
+  return rc;
+  KG_GUARD_END
+}
+
+int kg_synth_queries(kg_snapshot* sp, uint64_t seed, size_t n, kg_query* d_q) {
+  KG_GUARD_BEGIN
+  if (!sp) return set_error(-2, "NULL snapshot");
+  Snapshot* s = reinterpret_cast<Snapshot*>(sp);
+  std::lock_guard<std::mutex> lk(s->mu);
+  return kg::synth_queries(s, seed, n, d_q);
+  KG_GUARD_END
+}
+
+int kg_expand_batch(kg_snapshot* sp, const kg_set* roots, size_t n, int32_t global_max_depth, kg_tree_buf* out) {
+  (void)sp;
+  (void)roots;
+  (void)n;
+  (void)global_max_depth;
+  if (out) memset(out, 0, sizeof *out);
+  return set_error(KG_ERR_NOT_IMPLEMENTED, "kg_expand_batch: not implemented yet");
+}
+
+void kg_tree_free(kg_tree_buf* t) {
+  if (!t) return;
+  free(t->nodes);
+  free(t->root_off);
+  memset(t, 0, sizeof *t);
+}
+
+}  // extern "C"

@@ -1,0 +1,67 @@
+// kg_snapshot.h -- host-side snapshot object and error plumbing (not part of the C ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <mutex>
+#include <vector>
+
+#include "../../include/ketogpu.h"
+#include "kg_internal.h"
+
+namespace kg {
+
+constexpr int KG_ERR_RESOURCE_CODE = -4;
+
+// Thread-local last error (kg_last_error).  Returns `code` so callers can `return set_error(...)`.
+int set_error(int code, const char* fmt, ...);
+void clear_error();
+
+#define HIPC(expr)                                                                               \
+  do {                                                                                           \
+    hipError_t _e = (expr);                                                                      \
+    if (_e != hipSuccess) return ::kg::set_error(-1, "%s: %s (%s:%d)", #expr, hipGetErrorString(_e), \
+                                                 __FILE__, __LINE__);                            \
+  } while (0)
+
+struct Snapshot {
+  int device = -1;
+  int n_cu = 256;
+  hipStream_t stream = nullptr;
+  std::mutex mu;  // one batch at a time per snapshot (one stream)
+  DevSnap ds{};
+  uint32_t wildcard_rel = NONE;
+  bool has_program = false;
+  bool is_synth = false;
+  SynthLayout synth{};
+  uint64_t h_row_off_last = 0, n_set_edges = 0, device_bytes = 0;
+  std::vector<void*> allocs;
+  // host mirrors (host-tuple path)
+  std::vector<uint32_t> h_nd_ns, h_nd_obj, h_nd_rel, h_row_subj;
+  std::vector<uint64_t> h_row_off, h_adj_off;
+  std::vector<uint8_t> h_relflags;
+  std::vector<int32_t> h_relroot;
+  std::vector<RwNode> h_rw;
+  std::vector<int32_t> h_rwchild;
+  // per-batch scratch (grown on demand, owned by the snapshot)
+  void* scratch = nullptr;
+  size_t scratch_bytes = 0;
+  void* heavy_pool = nullptr;
+  size_t heavy_pool_bytes = 0;
+
+  ~Snapshot();
+  int init_device(int dev);
+  int alloc(void** p, size_t bytes);
+  int create_from_tuples(const kg_tuple* rows, size_t n, const kg_dict* dict, const kg_rewrite_prog* prog);
+  int create_synthetic(const kg_synth_params* p);
+  int upload_program(const kg_dict* dict, const kg_rewrite_prog* prog);
+  int build_hash_tables();
+  uint8_t host_relflag(uint32_t ns, uint32_t rel) const;
+  int64_t export_rows(kg_tuple* out, uint64_t cap);
+};
+
+// kg_check.hip
+int check_batch_device(Snapshot* s, const kg_query* d_q, size_t n, int32_t global_max_depth, uint8_t* d_out,
+                       uint32_t* d_err, kg_stats* stats, hipStream_t stream);
+int synth_queries(Snapshot* s, uint64_t seed, size_t n, kg_query* d_q);
+
+}  // namespace kg

@@ -1,0 +1,484 @@
+// kg_snapshot.hip -- snapshot construction: host tuples or the device-side synthetic generator
+// -> HBM-resident CSR + hash tables (layout in kg_internal.h).
+//
+// Replaces the read side of the SQL persister for the check path:
+//   Persister.GetRelationTuples  internal/persistence/sql/relationtuples.go:203-244
+//     (WHERE ns/obj/rel [/subject] ORDER BY shard_id) -> rows are laid out per (ns,obj,rel) in the
+//     order given (the caller passes shard_id order), so expansion order == the reference's.
+//   checkDirect's exact-tuple query (engine.go:159-163) -> dset hash probe.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cstring>
+#include <memory>
+#include <vector>
+
+#include "kg_internal.h"
+#include "kg_snapshot.h"
+
+namespace kg {
+
+// ------------------------------------------------------------------ device hash-table builders
+__global__ void k_dset_insert_rows(uint64_t* dset, uint64_t mask, const uint64_t* row_off, const uint32_t* row_subj,
+                                   uint32_t n_nodes) {
+  uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= n_nodes) return;
+  for (uint64_t i = row_off[v]; i < row_off[v + 1]; i++) {
+    uint64_t key = dset_key(v, row_subj[i]);
+    uint64_t b = mix64(key) & mask;
+    for (;;) {
+      uint64_t* bucket = dset + b * DSET_BUCKET;
+      bool done = false;
+      for (int s = 0; s < DSET_BUCKET; s++) {
+        unsigned long long old = atomicCAS((unsigned long long*)&bucket[s], (unsigned long long)EMPTY64,
+                                           (unsigned long long)key);
+        if (old == EMPTY64 || old == key) {
+          done = true;
+          break;
+        }
+      }
+      if (done) break;
+      b = (b + 1) & mask;
+    }
+  }
+}
+
+__global__ void k_nmap_insert(uint64_t* keys, uint32_t* vals, uint64_t mask, const uint32_t* nd_ns,
+                              const uint32_t* nd_obj, const uint32_t* nd_rel, uint32_t n_nodes) {
+  uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= n_nodes) return;
+  uint64_t key = nmap_key(nd_ns[v], nd_rel[v], nd_obj[v]);
+  uint64_t i = mix64(key) & mask;
+  for (;;) {
+    unsigned long long old =
+        atomicCAS((unsigned long long*)&keys[i], (unsigned long long)EMPTY64, (unsigned long long)key);
+    if (old == EMPTY64 || old == key) {
+      vals[i] = v;
+      return;
+    }
+    i = (i + 1) & mask;
+  }
+}
+
+// ------------------------------------------------------------------ synthetic generator kernels
+__global__ void k_synth_degrees(SynthLayout L, uint32_t n_nodes, uint64_t* deg, uint64_t* setdeg) {
+  uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= n_nodes) return;
+  uint32_t d = synth_degree(L, v);
+  uint32_t s = 0;
+  for (uint32_t e = 0; e < d; e++) s += (synth_subject(L, v, e) & SET_BIT) ? 1u : 0u;
+  deg[v] = d;
+  setdeg[v] = s;
+}
+
+__global__ void k_synth_fill(SynthLayout L, uint32_t n_nodes, const uint64_t* row_off, const uint64_t* adj_off,
+                             uint32_t* row_subj, uint32_t* adj, uint32_t* nd_ns, uint32_t* nd_obj, uint32_t* nd_rel) {
+  uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= n_nodes) return;
+  uint64_t r = row_off[v], a = adj_off[v];
+  uint32_t d = (uint32_t)(row_off[v + 1] - r);
+  for (uint32_t e = 0; e < d; e++) {
+    uint32_t s = synth_subject(L, v, e);
+    row_subj[r + e] = s;
+    if (s & SET_BIT) adj[a++] = s & ~SET_BIT;
+  }
+  bool doc = v < L.n_docs;
+  nd_ns[v] = doc ? L.ns_doc : L.ns_group;
+  nd_obj[v] = v;
+  nd_rel[v] = doc ? L.rel_viewer : L.rel_member;
+}
+
+// ------------------------------------------------------------------ Snapshot
+static uint64_t pow2_at_least(uint64_t x) {
+  uint64_t c = 1;
+  while (c < x) c <<= 1;
+  return c;
+}
+
+Snapshot::~Snapshot() {
+  if (device >= 0) hipSetDevice(device);
+  for (void* p : allocs) hipFree(p);
+  if (stream) hipStreamDestroy(stream);
+}
+
+int Snapshot::alloc(void** p, size_t bytes) {
+  if (bytes == 0) bytes = 16;
+  hipError_t e = hipMalloc(p, bytes);
+  if (e != hipSuccess) return set_error(KG_ERR_RESOURCE_CODE, "hipMalloc(%zu) failed: %s", bytes, hipGetErrorString(e));
+  allocs.push_back(*p);
+  device_bytes += bytes;
+  return 0;
+}
+
+int Snapshot::init_device(int dev) {
+  device = dev;
+  hipError_t e = hipSetDevice(dev);
+  if (e != hipSuccess) return set_error(-1, "hipSetDevice(%d): %s", dev, hipGetErrorString(e));
+  e = hipStreamCreateWithFlags(&stream, hipStreamNonBlocking);
+  if (e != hipSuccess) return set_error(-1, "hipStreamCreate: %s", hipGetErrorString(e));
+  int cus = 0;
+  hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  n_cu = cus > 0 ? cus : 256;
+  return 0;
+}
+
+// Hash tables: dset sized for load <= 0.5 over 8-key buckets; nmap for load <= 0.5.
+int Snapshot::build_hash_tables() {
+  uint64_t n_rows = h_row_off_last;
+  uint64_t buckets = pow2_at_least(std::max<uint64_t>(1, (n_rows * 2 + DSET_BUCKET - 1) / DSET_BUCKET));
+  uint64_t* dset = nullptr;
+  if (alloc((void**)&dset, buckets * DSET_BUCKET * 8)) return -1;
+  HIPC(hipMemsetAsync(dset, 0xFF, buckets * DSET_BUCKET * 8, stream));
+  uint64_t slots = pow2_at_least(std::max<uint64_t>(16, (uint64_t)ds.n_nodes * 2));
+  uint64_t* nk = nullptr;
+  uint32_t* nv = nullptr;
+  if (alloc((void**)&nk, slots * 8) || alloc((void**)&nv, slots * 4)) return -1;
+  HIPC(hipMemsetAsync(nk, 0xFF, slots * 8, stream));
+  uint32_t grid = (ds.n_nodes + 255) / 256;
+  if (ds.n_nodes) {
+    hipLaunchKernelGGL(k_dset_insert_rows, dim3(grid), dim3(256), 0, stream, dset, buckets - 1, ds.row_off,
+                       ds.row_subj, ds.n_nodes);
+    HIPC(hipGetLastError());
+    hipLaunchKernelGGL(k_nmap_insert, dim3(grid), dim3(256), 0, stream, nk, nv, slots - 1, ds.nd_ns, ds.nd_obj,
+                       ds.nd_rel, ds.n_nodes);
+    HIPC(hipGetLastError());
+  }
+  ds.dset = dset;
+  ds.dset_mask = buckets - 1;
+  ds.nmap_keys = nk;
+  ds.nmap_vals = nv;
+  ds.nmap_mask = slots - 1;
+  HIPC(hipStreamSynchronize(stream));
+  return 0;
+}
+
+// Upload the rewrite program and the (ns,rel) flag table (dense n_ns x n_rel).
+int Snapshot::upload_program(const kg_dict* dict, const kg_rewrite_prog* prog) {
+  ds.n_ns = std::max<uint32_t>(dict ? dict->n_namespaces : 0, prog ? prog->n_ns : 0);
+  ds.n_rel = dict ? dict->n_relations : 0;
+  if (prog)
+    for (uint32_t j = 0; j < prog->n_rel; j++) {
+      ds.n_rel = std::max(ds.n_rel, prog->rel_rel[j] + 1);
+      ds.n_ns = std::max(ds.n_ns, prog->rel_ns[j] + 1);
+    }
+  has_program = false;
+  if (prog)
+    for (uint32_t i = 0; i < prog->n_ns; i++) has_program |= prog->ns_has_rel[i] != 0;
+  ds.relflags = nullptr;
+  ds.relroot = nullptr;
+  ds.rw = nullptr;
+  ds.rwchild = nullptr;
+  ds.n_rw = 0;
+  if (!has_program) return 0;
+  if ((uint64_t)ds.n_ns * ds.n_rel > (64ull << 20))
+    return set_error(KG_ERR_RESOURCE_CODE, "namespace x relation table too large (%u x %u)", ds.n_ns, ds.n_rel);
+  size_t nt = (size_t)ds.n_ns * ds.n_rel;
+  h_relflags.assign(nt, 0);
+  h_relroot.assign(nt, -1);
+  for (uint32_t ns = 0; ns < prog->n_ns; ns++)
+    if (prog->ns_has_rel[ns])
+      for (uint32_t r = 0; r < ds.n_rel; r++) h_relflags[(size_t)ns * ds.n_rel + r] = 2;  // undeclared -> error
+  for (uint32_t j = 0; j < prog->n_rel; j++) {
+    size_t at = (size_t)prog->rel_ns[j] * ds.n_rel + prog->rel_rel[j];
+    if (prog->rel_ns[j] < prog->n_ns && !prog->ns_has_rel[prog->rel_ns[j]]) continue;
+    h_relflags[at] = prog->rel_root[j] >= 0 ? 1 : 0;
+    h_relroot[at] = prog->rel_root[j];
+  }
+  h_rw.assign((const RwNode*)prog->rw, (const RwNode*)prog->rw + prog->n_rw);
+  h_rwchild.assign(prog->child, prog->child + prog->n_child);
+  uint8_t* rf;
+  int32_t* rr;
+  RwNode* rw;
+  int32_t* rc;
+  if (alloc((void**)&rf, nt) || alloc((void**)&rr, nt * 4) || alloc((void**)&rw, (h_rw.size() + 1) * sizeof(RwNode)) ||
+      alloc((void**)&rc, (h_rwchild.size() + 1) * 4))
+    return -1;
+  HIPC(hipMemcpy(rf, h_relflags.data(), nt, hipMemcpyHostToDevice));
+  HIPC(hipMemcpy(rr, h_relroot.data(), nt * 4, hipMemcpyHostToDevice));
+  if (!h_rw.empty()) HIPC(hipMemcpy(rw, h_rw.data(), h_rw.size() * sizeof(RwNode), hipMemcpyHostToDevice));
+  if (!h_rwchild.empty()) HIPC(hipMemcpy(rc, h_rwchild.data(), h_rwchild.size() * 4, hipMemcpyHostToDevice));
+  ds.relflags = rf;
+  ds.relroot = rr;
+  ds.rw = rw;
+  ds.rwchild = rc;
+  ds.n_rw = (uint32_t)h_rw.size();
+  return 0;
+}
+
+uint8_t Snapshot::host_relflag(uint32_t ns, uint32_t rel) const {
+  if (!has_program || ns >= ds.n_ns || rel >= ds.n_rel) return 0;
+  return h_relflags[(size_t)ns * ds.n_rel + rel];
+}
+
+// ------------------------------------------------------------------ host interning map
+namespace {
+struct HostMap {  // (u64 key) -> u32, open addressing
+  std::vector<uint64_t> k;
+  std::vector<uint32_t> v;
+  uint64_t mask = 0, n = 0;
+  void init(uint64_t cap) {
+    uint64_t c = pow2_at_least(std::max<uint64_t>(16, cap * 2));
+    k.assign(c, EMPTY64);
+    v.assign(c, 0);
+    mask = c - 1;
+    n = 0;
+  }
+  void grow() {
+    std::vector<uint64_t> ok;
+    std::vector<uint32_t> ov;
+    ok.swap(k);
+    ov.swap(v);
+    init(ok.size());
+    for (size_t i = 0; i < ok.size(); i++)
+      if (ok[i] != EMPTY64) put(ok[i], ov[i]);
+  }
+  // returns existing value or inserts val
+  uint32_t put(uint64_t key, uint32_t val) {
+    if ((n + 1) * 2 > k.size()) grow();
+    uint64_t i = mix64(key) & mask;
+    while (k[i] != EMPTY64) {
+      if (k[i] == key) return v[i];
+      i = (i + 1) & mask;
+    }
+    k[i] = key;
+    v[i] = val;
+    n++;
+    return val;
+  }
+};
+}  // namespace
+
+int Snapshot::create_from_tuples(const kg_tuple* rows, size_t n, const kg_dict* dict, const kg_rewrite_prog* prog) {
+  wildcard_rel = dict ? dict->wildcard_rel : NONE;
+  ds.wildcard_rel = wildcard_rel;
+  // 1. intern nodes (ns, obj, rel) in first-appearance order
+  HostMap m;
+  m.init(n + 16);
+  std::vector<uint32_t> lhs(n), sub(n);
+  auto intern = [&](uint32_t ns, uint32_t obj, uint32_t rel) -> uint32_t {
+    uint32_t id = (uint32_t)h_nd_ns.size();
+    uint32_t got = m.put(nmap_key(ns, rel, obj), id);
+    if (got == id) {
+      h_nd_ns.push_back(ns);
+      h_nd_obj.push_back(obj);
+      h_nd_rel.push_back(rel);
+    }
+    return got;
+  };
+  for (size_t i = 0; i < n; i++) {
+    const kg_tuple& t = rows[i];
+    if (t.ns >= 0xFFFF || t.rel >= 0xFFFF || t.obj >= 0x7FFFFFFF)
+      return set_error(-2, "tuple %zu: id out of range", i);
+    lhs[i] = intern(t.ns, t.obj, t.rel);
+    if (t.sns == KG_SUBJECT_ID) {
+      if (t.sobj >= 0x7FFFFFFF) return set_error(-2, "tuple %zu: subject id out of range", i);
+      sub[i] = t.sobj;
+    } else {
+      if (t.sns >= 0xFFFF || t.srel >= 0xFFFF || t.sobj >= 0x7FFFFFFF)
+        return set_error(-2, "tuple %zu: subject set id out of range", i);
+      sub[i] = SET_BIT | intern(t.sns, t.sobj, t.srel);
+    }
+  }
+  uint32_t nn = (uint32_t)h_nd_ns.size();
+  ds.n_nodes = nn;
+  // 2. rows per node in tuple (shard) order: counting sort
+  h_row_off.assign((size_t)nn + 1, 0);
+  h_adj_off.assign((size_t)nn + 1, 0);
+  for (size_t i = 0; i < n; i++) {
+    h_row_off[lhs[i] + 1]++;
+    uint32_t s = sub[i];
+    if ((s & SET_BIT) && h_nd_rel[s & ~SET_BIT] != wildcard_rel) h_adj_off[lhs[i] + 1]++;
+  }
+  for (uint32_t v = 0; v < nn; v++) {
+    h_row_off[v + 1] += h_row_off[v];
+    h_adj_off[v + 1] += h_adj_off[v];
+  }
+  h_row_subj.assign(n, 0);
+  std::vector<uint32_t> adj(h_adj_off[nn]);
+  {
+    std::vector<uint64_t> fr(h_row_off.begin(), h_row_off.end() - 1), fa(h_adj_off.begin(), h_adj_off.end() - 1);
+    for (size_t i = 0; i < n; i++) {
+      uint32_t s = sub[i], v = lhs[i];
+      h_row_subj[fr[v]++] = s;
+      if ((s & SET_BIT) && h_nd_rel[s & ~SET_BIT] != wildcard_rel) adj[fa[v]++] = s & ~SET_BIT;
+    }
+  }
+  h_row_off_last = h_row_off[nn];
+  // 3. program + purity closure
+  if (upload_program(dict, prog)) return -1;
+  std::vector<uint8_t> flags;
+  if (has_program) {
+    flags.assign(nn, 0);
+    std::vector<uint32_t> work;
+    for (uint32_t v = 0; v < nn; v++) {
+      uint8_t rf = host_relflag(h_nd_ns[v], h_nd_rel[v]);
+      if (rf & 1) flags[v] |= NF_REWRITE;
+      if (rf & 2) flags[v] |= NF_ERR;
+      if (rf) {
+        flags[v] |= NF_IMPURE;
+        work.push_back(v);
+      }
+    }
+    // reverse set-adjacency: a node is impure when an impure node is reachable from it
+    std::vector<uint64_t> roff((size_t)nn + 1, 0);
+    for (uint32_t c : adj) roff[c + 1]++;
+    for (uint32_t v = 0; v < nn; v++) roff[v + 1] += roff[v];
+    std::vector<uint32_t> radj(adj.size());
+    {
+      std::vector<uint64_t> f(roff.begin(), roff.end() - 1);
+      for (uint32_t v = 0; v < nn; v++)
+        for (uint64_t i = h_adj_off[v]; i < h_adj_off[v + 1]; i++) radj[f[adj[i]]++] = v;
+    }
+    while (!work.empty()) {
+      uint32_t c = work.back();
+      work.pop_back();
+      for (uint64_t i = roff[c]; i < roff[c + 1]; i++) {
+        uint32_t p = radj[i];
+        if (!(flags[p] & NF_IMPURE)) {
+          flags[p] |= NF_IMPURE;
+          work.push_back(p);
+        }
+      }
+    }
+  }
+  // 4. upload
+  uint64_t *d_ro, *d_ao;
+  uint32_t *d_rs, *d_adj, *d_ns, *d_obj, *d_rel;
+  if (alloc((void**)&d_ro, ((size_t)nn + 1) * 8) || alloc((void**)&d_ao, ((size_t)nn + 1) * 8) ||
+      alloc((void**)&d_rs, n * 4) || alloc((void**)&d_adj, adj.size() * 4) || alloc((void**)&d_ns, (size_t)nn * 4) ||
+      alloc((void**)&d_obj, (size_t)nn * 4) || alloc((void**)&d_rel, (size_t)nn * 4))
+    return -1;
+  HIPC(hipMemcpy(d_ro, h_row_off.data(), ((size_t)nn + 1) * 8, hipMemcpyHostToDevice));
+  HIPC(hipMemcpy(d_ao, h_adj_off.data(), ((size_t)nn + 1) * 8, hipMemcpyHostToDevice));
+  if (n) HIPC(hipMemcpy(d_rs, h_row_subj.data(), n * 4, hipMemcpyHostToDevice));
+  if (!adj.empty()) HIPC(hipMemcpy(d_adj, adj.data(), adj.size() * 4, hipMemcpyHostToDevice));
+  if (nn) {
+    HIPC(hipMemcpy(d_ns, h_nd_ns.data(), (size_t)nn * 4, hipMemcpyHostToDevice));
+    HIPC(hipMemcpy(d_obj, h_nd_obj.data(), (size_t)nn * 4, hipMemcpyHostToDevice));
+    HIPC(hipMemcpy(d_rel, h_nd_rel.data(), (size_t)nn * 4, hipMemcpyHostToDevice));
+  }
+  ds.row_off = d_ro;
+  ds.adj_off = d_ao;
+  ds.row_subj = d_rs;
+  ds.adj = d_adj;
+  ds.nd_ns = d_ns;
+  ds.nd_obj = d_obj;
+  ds.nd_rel = d_rel;
+  n_set_edges = adj.size();
+  ds.nflags = nullptr;
+  if (has_program) {
+    uint8_t* d_f;
+    if (alloc((void**)&d_f, nn + 1)) return -1;
+    if (nn) HIPC(hipMemcpy(d_f, flags.data(), nn, hipMemcpyHostToDevice));
+    ds.nflags = d_f;
+  }
+  return build_hash_tables();
+}
+
+int Snapshot::create_synthetic(const kg_synth_params* p) {
+  SynthLayout L{};
+  uint64_t T = p->n_tuples_target ? p->n_tuples_target : 10000000ull;
+  L.seed = p->seed;
+  L.n_layers = p->n_layers ? p->n_layers : 8;
+  L.n_docs = (uint32_t)std::max<uint64_t>(1, T / 8);
+  L.group_per_layer = (uint32_t)std::max<uint64_t>(1, T / 16 / L.n_layers);
+  L.n_groups = L.group_per_layer * L.n_layers;
+  L.n_users = (uint32_t)std::max<uint64_t>(1, T / 10);
+  L.max_degree = p->max_degree ? p->max_degree : 100000;
+  L.set_frac = p->set_fraction > 0 ? p->set_fraction : 0.25f;
+  L.doc_set_frac = p->doc_set_fraction > 0 ? p->doc_set_fraction : 0.5f;
+  // interned ids used by the generator: rel 0 is "..." (reserved like keto_amd.mapper.Interner)
+  L.ns_doc = 0;
+  L.ns_group = 1;
+  L.ns_user = 2;
+  L.rel_viewer = 1;
+  L.rel_member = 2;
+  if ((uint64_t)L.n_docs + L.n_groups + L.n_users >= 0x7FFFFFFFull) return set_error(-2, "synthetic graph too large");
+  synth = L;
+  is_synth = true;
+  wildcard_rel = 0;
+  ds.wildcard_rel = 0;
+  uint32_t nn = L.n_docs + L.n_groups;
+  ds.n_nodes = nn;
+  uint64_t *deg, *setdeg, *d_ro, *d_ao;
+  if (alloc((void**)&d_ro, ((size_t)nn + 1) * 8) || alloc((void**)&d_ao, ((size_t)nn + 1) * 8)) return -1;
+  HIPC(hipMalloc(&deg, ((size_t)nn + 1) * 8));
+  HIPC(hipMalloc(&setdeg, ((size_t)nn + 1) * 8));
+  uint32_t grid = (nn + 255) / 256;
+  hipLaunchKernelGGL(k_synth_degrees, dim3(grid), dim3(256), 0, stream, L, nn, deg, setdeg);
+  HIPC(hipGetLastError());
+  HIPC(hipMemsetAsync(deg + nn, 0, 8, stream));
+  HIPC(hipMemsetAsync(setdeg + nn, 0, 8, stream));
+  size_t tmp_bytes = 0;
+  HIPC(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, deg, d_ro, nn + 1, stream));
+  void* tmp;
+  HIPC(hipMalloc(&tmp, tmp_bytes + 16));
+  HIPC(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, deg, d_ro, nn + 1, stream));
+  HIPC(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, setdeg, d_ao, nn + 1, stream));
+  uint64_t tot[2];
+  HIPC(hipMemcpyAsync(&tot[0], d_ro + nn, 8, hipMemcpyDeviceToHost, stream));
+  HIPC(hipMemcpyAsync(&tot[1], d_ao + nn, 8, hipMemcpyDeviceToHost, stream));
+  HIPC(hipStreamSynchronize(stream));
+  hipFree(tmp);
+  hipFree(deg);
+  hipFree(setdeg);
+  uint32_t *d_rs, *d_adj, *d_ns, *d_obj, *d_rel;
+  if (alloc((void**)&d_rs, tot[0] * 4) || alloc((void**)&d_adj, tot[1] * 4) || alloc((void**)&d_ns, (size_t)nn * 4) ||
+      alloc((void**)&d_obj, (size_t)nn * 4) || alloc((void**)&d_rel, (size_t)nn * 4))
+    return -1;
+  hipLaunchKernelGGL(k_synth_fill, dim3(grid), dim3(256), 0, stream, L, nn, d_ro, d_ao, d_rs, d_adj, d_ns, d_obj,
+                     d_rel);
+  HIPC(hipGetLastError());
+  ds.row_off = d_ro;
+  ds.adj_off = d_ao;
+  ds.row_subj = d_rs;
+  ds.adj = d_adj;
+  ds.nd_ns = d_ns;
+  ds.nd_obj = d_obj;
+  ds.nd_rel = d_rel;
+  ds.nflags = nullptr;  // no rewrites configured: every node pure
+  h_row_off_last = tot[0];
+  n_set_edges = tot[1];
+  kg_dict dict{3, 3, 0};
+  if (upload_program(&dict, nullptr)) return -1;
+  return build_hash_tables();
+}
+
+int64_t Snapshot::export_rows(kg_tuple* out, uint64_t cap) {
+  uint64_t n = h_row_off_last;
+  if (!out) return (int64_t)n;
+  if (cap < n) return set_error(-3, "export buffer too small (%llu < %llu)", (unsigned long long)cap,
+                                (unsigned long long)n);
+  uint32_t nn = ds.n_nodes;
+  std::vector<uint64_t> off((size_t)nn + 1);
+  std::vector<uint32_t> subj(n), ns(nn), obj(nn), rel(nn);
+  HIPC(hipMemcpy(off.data(), ds.row_off, ((size_t)nn + 1) * 8, hipMemcpyDeviceToHost));
+  if (n) HIPC(hipMemcpy(subj.data(), ds.row_subj, n * 4, hipMemcpyDeviceToHost));
+  if (nn) {
+    HIPC(hipMemcpy(ns.data(), ds.nd_ns, (size_t)nn * 4, hipMemcpyDeviceToHost));
+    HIPC(hipMemcpy(obj.data(), ds.nd_obj, (size_t)nn * 4, hipMemcpyDeviceToHost));
+    HIPC(hipMemcpy(rel.data(), ds.nd_rel, (size_t)nn * 4, hipMemcpyDeviceToHost));
+  }
+  for (uint32_t v = 0; v < nn; v++)
+    for (uint64_t i = off[v]; i < off[v + 1]; i++) {
+      kg_tuple& t = out[i];
+      t.ns = ns[v];
+      t.obj = obj[v];
+      t.rel = rel[v];
+      uint32_t s = subj[i];
+      if (s & SET_BIT) {
+        uint32_t c = s & ~SET_BIT;
+        t.sns = ns[c];
+        t.sobj = obj[c];
+        t.srel = rel[c];
+      } else {
+        t.sns = KG_SUBJECT_ID;
+        t.sobj = s;
+        t.srel = 0;
+      }
+    }
+  return (int64_t)n;
+}
+
+}  // namespace kg

@@ -1,0 +1,279 @@
+"""Host-side mirror of the reference's check / expand engine surface, running on the MI355X
+library through the C ABI.
+
+Reference interfaces mirrored (paths relative to the reference checkout):
+  check.NewEngine / Engine.CheckIsMember / CheckRelationTuple   internal/check/engine.go:42-80
+  Engine.BatchCheck (new)                         == a loop of CheckIsMember
+  expand.Engine.BuildTree                                       internal/expand/engine.go:35-104
+  config.Provider.MaxReadDepth (default 5, 1..65535)            internal/driver/config/provider.go:160-162
+  checkgroup.Result{Membership, Err}                            internal/check/checkgroup/definitions.go:46-69
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _lib
+from .ketoapi import RelationTuple, SubjectSet, Tree, TREE_LEAF, TREE_UNION
+from .mapper import Interner, Mapper, SUBJECT_ID
+from .namespace import Namespace, Program, compile_program
+
+MEMBERSHIP_UNKNOWN, IS_MEMBER, NOT_MEMBER = 0, 1, 2  # checkgroup.Membership
+
+ERR_TEXT = {
+    _lib.KG_ERR_RELATION_NOT_FOUND: "relation not found",       # engine.go:228
+    _lib.KG_ERR_NOT_IMPLEMENTED: "not implemented",             # rewrites.go:15-17
+    _lib.KG_ERR_REWRITE_CYCLE: "computed subject-set rewrite cycle",
+    _lib.KG_ERR_RESOURCE: "engine capacity exceeded",
+}
+
+
+class CheckError(RuntimeError):
+    def __init__(self, code: int):
+        super().__init__(ERR_TEXT.get(code, f"error {code}"))
+        self.code = code
+
+
+@dataclass
+class Result:
+    membership: int
+    err: Optional[CheckError] = None
+
+
+@dataclass
+class Config:
+    max_read_depth: int = 5
+    namespaces: List[Namespace] = field(default_factory=list)
+
+    def __post_init__(self):
+        if not 1 <= self.max_read_depth <= 65535:  # embedx/config.schema.json:308-315
+            raise ValueError("max_read_depth must be in [1, 65535]")
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+class Snapshot:
+    """An HBM-resident, immutable snapshot of the relation tuples (rows in shard order)."""
+
+    def __init__(self, tuples: np.ndarray, interner: Interner, program: Optional[Program] = None, device: int = 0,
+                 _handle=None):
+        L = _lib.load()
+        self.interner = interner
+        self.device = device
+        self._h = C.c_void_p()
+        if _handle is not None:
+            self._h = _handle
+            return
+        t = np.ascontiguousarray(tuples, dtype=np.uint32).reshape(-1, 6)
+        d = _lib.kg_dict(interner.n_namespaces, interner.n_relations, interner.wildcard_rel)
+        prog_c = None
+        self._keep = []
+        if program is not None and not program.empty:
+            arrs = [np.ascontiguousarray(program.ns_has_rel, np.uint8), np.ascontiguousarray(program.rel_ns, np.uint32),
+                    np.ascontiguousarray(program.rel_rel, np.uint32), np.ascontiguousarray(program.rel_root, np.int32),
+                    np.ascontiguousarray(program.rw, np.int32).reshape(-1, 5),
+                    np.ascontiguousarray(program.child, np.int32)]
+            self._keep = arrs
+            prog_c = _lib.kg_rewrite_prog(len(arrs[0]), _ptr(arrs[0]), len(arrs[1]), _ptr(arrs[1]), _ptr(arrs[2]),
+                                          _ptr(arrs[3]), arrs[4].shape[0], _ptr(arrs[4]), len(arrs[5]), _ptr(arrs[5]))
+        rc = L.kg_snapshot_create(_ptr(t), t.shape[0], C.byref(d), C.byref(prog_c) if prog_c is not None else None,
+                                  device, C.byref(self._h))
+        _lib.check(rc, "kg_snapshot_create")
+
+    @classmethod
+    def synthetic(cls, n_tuples: int, seed: int = 20250131, device: int = 0, n_layers: int = 8,
+                  max_degree: int = 100000, set_fraction: float = 0.25, doc_set_fraction: float = 0.5) -> "Snapshot":
+        L = _lib.load()
+        p = _lib.kg_synth_params(n_tuples, seed, n_layers, max_degree, set_fraction, doc_set_fraction)
+        h = C.c_void_p()
+        _lib.check(L.kg_snapshot_synthetic(C.byref(p), device, C.byref(h)), "kg_snapshot_synthetic")
+        it = Interner()  # ids used by the generator: ns doc=0 group=1 user=2; rel ...=0 viewer=1 member=2
+        for s in ("doc", "group", "user"):
+            it.ns_id(s)
+        for r in ("viewer", "member"):
+            it.rel_id(r)
+        snap = cls(None, it, device=device, _handle=h)
+        return snap
+
+    @property
+    def handle(self):
+        return self._h
+
+    def info(self) -> dict:
+        a = np.zeros(4, np.uint64)
+        _lib.check(_lib.load().kg_snapshot_info(self._h, _ptr(a)), "kg_snapshot_info")
+        return {"nodes": int(a[0]), "rows": int(a[1]), "set_edges": int(a[2]), "device_bytes": int(a[3])}
+
+    def synth_ids(self) -> dict:
+        a = np.zeros(6, np.uint32)
+        _lib.check(_lib.load().kg_synth_ids(self._h, _ptr(a)), "kg_synth_ids")
+        return dict(zip(["ns_doc", "ns_group", "ns_user", "rel_viewer", "rel_member", "n_objects"], map(int, a)))
+
+    def export(self) -> np.ndarray:
+        L = _lib.load()
+        n = L.kg_snapshot_export(self._h, None, 0)
+        if n < 0:
+            raise _lib.KetoGPUError(_lib.last_error())
+        out = np.zeros((n, 6), np.uint32)
+        got = L.kg_snapshot_export(self._h, _ptr(out), n)
+        if got != n:
+            raise _lib.KetoGPUError(_lib.last_error())
+        return out
+
+    def close(self) -> None:
+        if self._h:
+            _lib.load().kg_snapshot_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def queries_array(q6: np.ndarray, max_depths) -> np.ndarray:
+    """(n,6) tuple ids + per-query max depth -> (n,7) uint32 kg_query rows."""
+    q6 = np.asarray(q6, np.uint32).reshape(-1, 6)
+    out = np.zeros((q6.shape[0], 7), np.uint32)
+    out[:, :6] = q6
+    out[:, 6] = np.broadcast_to(np.asarray(max_depths, np.int64), (q6.shape[0],)).astype(np.int32).view(np.uint32)
+    return out
+
+
+class Engine:
+    """check.Engine: permission checks against a snapshot."""
+
+    def __init__(self, snapshot: Snapshot, config: Optional[Config] = None):
+        self.snapshot = snapshot
+        self.config = config or Config()
+        self.last_stats: Optional[dict] = None
+
+    # ---- batched (the hot path)
+    def batch_check_ids(self, q: np.ndarray, with_stats: bool = False) -> Tuple[np.ndarray, np.ndarray]:
+        """q: (n,7) uint32 kg_query rows.  Returns (result u8 [0 not member, 1 member, 2 error], err u32)."""
+        q = np.ascontiguousarray(q, np.uint32).reshape(-1, 7)
+        n = q.shape[0]
+        out = np.zeros(n, np.uint8)
+        err = np.zeros(n, np.uint32)
+        st = _lib.kg_stats()
+        rc = _lib.load().kg_check_batch(self.snapshot.handle, _ptr(q), n, self.config.max_read_depth, _ptr(out),
+                                        _ptr(err), C.byref(st) if with_stats else None)
+        _lib.check(rc, "kg_check_batch")
+        self.last_stats = st.as_dict() if with_stats else None
+        return out, err
+
+    def batch_check(self, tuples: Sequence[RelationTuple], max_depths) -> Tuple[List[bool], List[Optional[CheckError]]]:
+        """BatchCheck(ctx, []*RelationTuple, maxDepth []int) ([]bool, []error) -- SURVEY.md 8b."""
+        it = self.snapshot.interner
+        q = queries_array(np.asarray([it.tuple_ids(t) for t in tuples], np.uint32).reshape(-1, 6), max_depths)
+        out, err = self.batch_check_ids(q)
+        allowed = [bool(o == _lib.KG_IS_MEMBER) for o in out]
+        errs = [CheckError(int(e)) if o == _lib.KG_ERROR else None for o, e in zip(out, err)]
+        return allowed, errs
+
+    # ---- single-query API of the reference
+    def check_relation_tuple(self, t: RelationTuple, rest_depth: int) -> Result:
+        allowed, errs = self.batch_check([t], [rest_depth])
+        if errs[0] is not None:
+            return Result(MEMBERSHIP_UNKNOWN, errs[0])
+        return Result(IS_MEMBER if allowed[0] else NOT_MEMBER)
+
+    def check_is_member(self, t: RelationTuple, rest_depth: int) -> bool:
+        r = self.check_relation_tuple(t, rest_depth)
+        if r.err is not None:
+            raise r.err
+        return r.membership == IS_MEMBER
+
+
+class ExpandEngine:
+    """expand.Engine: subject-set trees."""
+
+    def __init__(self, snapshot: Snapshot, config: Optional[Config] = None):
+        self.snapshot = snapshot
+        self.config = config or Config()
+
+    def build_trees_ids(self, roots: np.ndarray) -> List[Optional[np.ndarray]]:
+        """roots: (n,4) uint32 kg_set rows (sns, sobj, srel, max_depth).  Returns per root the pre-order
+        records (m, 6) = (type, is_set, ns, obj, rel, n_children), or None for a nil tree."""
+        roots = np.ascontiguousarray(roots, np.uint32).reshape(-1, 4)
+        buf = _lib.kg_tree_buf()
+        L = _lib.load()
+        rc = L.kg_expand_batch(self.snapshot.handle, _ptr(roots), roots.shape[0], self.config.max_read_depth,
+                               C.byref(buf))
+        _lib.check(rc, "kg_expand_batch")
+        try:
+            n = int(buf.n_nodes)
+            recs = np.ctypeslib.as_array(C.cast(buf.nodes, C.POINTER(C.c_uint32)), shape=(n * 5,)).reshape(n, 5) \
+                if n else np.zeros((0, 5), np.uint32)
+            offs = np.ctypeslib.as_array(buf.root_off, shape=(roots.shape[0] + 1,)).copy()
+            out: List[Optional[np.ndarray]] = []
+            for r in range(roots.shape[0]):
+                a, b = int(offs[r]), int(offs[r + 1])
+                if a == b:
+                    out.append(None)
+                    continue
+                seg = recs[a:b]
+                rec = np.zeros((b - a, 6), np.int64)
+                rec[:, 0] = seg[:, 0] & 0xFF
+                rec[:, 1] = (seg[:, 0] >> 8) & 0xFF
+                rec[:, 2:5] = seg[:, 1:4]
+                rec[:, 5] = seg[:, 4]
+                out.append(rec)
+            return out
+        finally:
+            L.kg_tree_free(C.byref(buf))
+
+    def build_tree(self, subject, rest_depth: int) -> Optional[Tree]:
+        """BuildTree(ctx, subject, restDepth): subject is a SubjectSet or a subject-id string."""
+        it = self.snapshot.interner
+        if isinstance(subject, SubjectSet):
+            row = [*it.subject_set_ids(subject), rest_depth]
+        else:
+            row = [SUBJECT_ID, it.obj_id(subject), 0, rest_depth]
+        row[3] = np.int32(row[3]).view(np.uint32)
+        rec = self.build_trees_ids(np.asarray([row], np.uint32))[0]
+        return records_to_tree(rec, it)
+
+
+def records_to_tree(rec: Optional[np.ndarray], it: Interner) -> Optional[Tree]:
+    if rec is None or len(rec) == 0:
+        return None
+    pos = 0
+
+    def walk() -> Tree:
+        nonlocal pos
+        r = rec[pos]
+        pos += 1
+        t = Tree(TREE_UNION if int(r[0]) == 1 else TREE_LEAF, it.subject_from_ids(bool(r[1]), int(r[2]), int(r[3]),
+                                                                                  int(r[4])))
+        for _ in range(int(r[5])):
+            t.children.append(walk())
+        return t
+
+    return walk()
+
+
+class Registry:
+    """Test/embedding convenience mirroring driver.Registry's engine wiring
+    (internal/driver/registry_default.go:180-192): tuples + namespaces -> snapshot + engines."""
+
+    def __init__(self, tuples: Sequence[RelationTuple], namespaces: Sequence[Namespace] = (), max_read_depth: int = 5,
+                 device: int = 0, interner: Optional[Interner] = None):
+        self.interner = interner or Interner()
+        self.config = Config(max_read_depth, list(namespaces))
+        self.program = compile_program(list(namespaces), self.interner)
+        arr = self.interner.tuples_array(tuples)
+        self.snapshot = Snapshot(arr, self.interner, self.program, device)
+        self.mapper = Mapper(self.interner, list(namespaces) if namespaces else None)
+
+    def permission_engine(self) -> Engine:
+        return Engine(self.snapshot, self.config)
+
+    def expand_engine(self) -> ExpandEngine:
+        return ExpandEngine(self.snapshot, self.config)

@@ -1,0 +1,134 @@
+"""GPU parity tests for batched checks: the HIP path through the C ABI against the CPU oracle
+and the reference's golden vectors.  Bit-exact (integer decisions)."""
+import numpy as np
+import pytest
+
+from golden_cases import Case, all_cases
+from keto_amd.engine import Config, Engine, Registry, Snapshot, queries_array
+from keto_amd.ketoapi import RelationTuple
+from keto_amd.mapper import Interner, SUBJECT_ID
+from oracle.oracle import POLICY_CANONICAL, POLICY_DFS, Oracle
+
+pytestmark = pytest.mark.gpu
+
+CHECK_CASES = all_cases("checks")
+
+
+@pytest.mark.parametrize("fn,case", CHECK_CASES, ids=[f"{f}:{c['name']}" for f, c in CHECK_CASES])
+def test_golden_checks(fn, case):
+    c = Case(case)
+    reg = Registry(c.tuples, c.namespaces, interner=c.it)
+    e = reg.permission_engine()
+    for chk in case["checks"]:
+        e.config.max_read_depth = chk["global_max_depth"]
+        got = e.check_is_member(RelationTuple.from_string(chk["tuple"]), chk["max_depth"])
+        assert got == chk["allowed"], chk
+
+
+def random_graph(rng, n_obj=60, n_rows=400, n_ns=3, n_rel=3, p_set=0.45, p_wild=0.1, n_users=40):
+    it = Interner()
+    nss = [f"n{i}" for i in range(n_ns)]
+    rels = [f"r{i}" for i in range(n_rel)]
+    tuples = []
+    for _ in range(n_rows):
+        ns, obj, rel = rng.choice(nss), f"o{rng.integers(n_obj)}", rng.choice(rels)
+        if rng.random() < p_set:
+            srel = "..." if rng.random() < p_wild else rng.choice(rels)
+            s = f"{rng.choice(nss)}:o{rng.integers(n_obj)}#{srel}"
+        else:
+            s = f"u{rng.integers(n_users)}"
+        tuples.append(RelationTuple.from_string(f"{ns}:{obj}#{rel}@{s}"))
+    return it, tuples, nss, rels
+
+
+def random_queries(rng, nss, rels, n, n_obj=60, n_users=40, p_setq=0.15):
+    qs = []
+    for _ in range(n):
+        if rng.random() < p_setq:
+            s = f"({rng.choice(nss)}:o{rng.integers(n_obj)}#{rng.choice(rels)})"
+        else:
+            s = f"u{rng.integers(n_users + 5)}"  # a few unknown subjects
+        qs.append(RelationTuple.from_string(f"{rng.choice(nss)}:o{rng.integers(n_obj + 3)}#{rng.choice(rels)}@{s}"))
+    return qs
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_random_graphs_vs_oracle(seed):
+    rng = np.random.default_rng(seed)
+    it, tuples, nss, rels = random_graph(rng, n_obj=40 + 20 * seed, n_rows=200 + 150 * seed)
+    reg = Registry(tuples, [], interner=it)
+    qs = random_queries(rng, nss, rels, 3000, n_obj=40 + 20 * seed)
+    depths = rng.integers(-1, 9, len(qs))
+    q6 = np.asarray([it.tuple_ids(t) for t in qs], np.uint32)
+    oracle = Oracle(it.tuples_array(tuples), it.wildcard_rel)
+    for gmax in (1, 3, 5, 8):
+        e = Engine(reg.snapshot, Config(gmax))
+        out, err = e.batch_check_ids(queries_array(q6, depths))
+        exp, oerr, _ = oracle.check_batch(q6, depths, gmax, POLICY_CANONICAL)
+        assert (err == 0).all() and (oerr == 0).all()
+        bad = np.nonzero(out != exp)[0]
+        assert bad.size == 0, [(str(qs[i]), int(depths[i]), int(out[i]), int(exp[i])) for i in bad[:10]]
+        # schedule sensitivity: queries where the Go DFS schedule agrees are bit-exact with it too
+        dfs, _, _ = oracle.check_batch(q6, depths, gmax, POLICY_DFS)
+        inv = dfs == exp
+        assert (out[inv] == dfs[inv]).all()
+
+
+def test_heavy_path_overflow_star():
+    # one query reaching > LDS capacity (512 visited) forces the workgroup (HBM bitmap) tier
+    tuples = [RelationTuple.from_string(f"g:root#m@(g:c{i}#m)") for i in range(3000)]
+    tuples += [RelationTuple.from_string(f"g:c{i}#m@(g:d{i % 700}#m)") for i in range(3000)]
+    tuples += [RelationTuple.from_string("g:d699#m@target"), RelationTuple.from_string("g:c5#m@near")]
+    reg = Registry(tuples, [])
+    e = reg.permission_engine()
+    it = reg.interner
+    qs = [RelationTuple.from_string(s) for s in
+          ["g:root#m@target", "g:root#m@near", "g:root#m@nobody", "g:c1#m@target", "g:d699#m@target"]]
+    q6 = np.asarray([it.tuple_ids(t) for t in qs], np.uint32)
+    oracle = Oracle(it.tuples_array(tuples), it.wildcard_rel)
+    for gmax in (2, 3, 4, 6):
+        e.config.max_read_depth = gmax
+        out, _ = e.batch_check_ids(queries_array(q6, 0), with_stats=True)
+        exp, _, _ = oracle.check_batch(q6, np.zeros(len(qs), np.int32), gmax)
+        assert list(out) == list(exp), (gmax, out, exp)
+    assert e.last_stats["n_heavy"] >= 1
+
+
+def test_empty_and_unknown():
+    reg = Registry([RelationTuple.from_string("a:b#c@d")], [])
+    e = reg.permission_engine()
+    out, err = e.batch_check_ids(np.zeros((0, 7), np.uint32))
+    assert out.shape == (0,)
+    assert e.check_is_member(RelationTuple.from_string("a:b#c@d"), 0)
+    assert not e.check_is_member(RelationTuple.from_string("a:b#c@zzz"), 0)
+    assert not e.check_is_member(RelationTuple.from_string("x:y#z@d"), 0)  # unknown namespace -> false
+
+
+def _torch():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+@pytest.mark.parametrize("n_tuples,gmax", [(200_000, 10), (300_000, 5)])
+def test_synthetic_graph_vs_oracle(n_tuples, gmax):
+    torch = _torch()
+    from keto_amd import _lib
+    snap = Snapshot.synthetic(n_tuples, seed=20250131)
+    n = 20000
+    dq = torch.empty((n, 7), dtype=torch.int32, device="cuda")
+    _lib.check(_lib.load().kg_synth_queries(snap.handle, 7, n, dq.data_ptr()), "kg_synth_queries")
+    e = Engine(snap, Config(gmax))
+    q = dq.cpu().numpy().view(np.uint32)
+    out, err = e.batch_check_ids(q, with_stats=True)
+    assert (err == 0).all()
+    rows = snap.export()
+    oracle = Oracle(rows, 0)
+    exp, _, _ = oracle.check_batch(q[:, :6], q[:, 6].view(np.int32), gmax, POLICY_CANONICAL, nthreads=8)
+    assert (out == exp).all(), np.nonzero(out != exp)[0][:10]
+    frac = out.mean()
+    assert 0.05 < frac < 0.95  # both answers occur
+    # layered generator => every query is schedule-invariant
+    dfs, _, _ = oracle.check_batch(q[:, :6], q[:, 6].view(np.int32), gmax, POLICY_DFS, nthreads=8)
+    assert (dfs == exp).all()

@@ -1,0 +1,97 @@
+"""CPU tests: host logic, tuple codec, namespace compiler, and the C-ABI library surface
+(load + exports only; no compute call without a GPU)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from keto_amd.ketoapi import MalformedInput, RelationTuple, SubjectSet, Tree
+from keto_amd.mapper import Interner, Mapper, NamespaceNotFound, SUBJECT_ID
+from keto_amd.namespace import (ComputedSubjectSet, InvertResult, Namespace, Relation, SubjectSetRewrite,
+                                TupleToSubjectSet, compile_program, namespace_from_json, namespace_to_json)
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_tuple_string_roundtrip():
+    # ketoapi/enc_string.go:13-95
+    t = RelationTuple.from_string("doc:readme#editor@(group:dev#member)")
+    assert t.subject_set == SubjectSet("group", "dev", "member")
+    assert str(t) == "doc:readme#editor@(group:dev#member)"
+    t2 = RelationTuple.from_string("doc:folder#parent@doc:folder_c#...")
+    assert t2.subject_set == SubjectSet("doc", "folder_c", "...")
+    t3 = RelationTuple.from_string("videos:/cats/1.mp4#view@*")
+    assert t3.subject_id == "*" and t3.object == "/cats/1.mp4"
+    assert RelationTuple.from_string(":directory#access@user").namespace == ""
+    for bad in ["nocolon", "ns:obj", "ns:obj#rel"]:
+        with pytest.raises(MalformedInput):
+            RelationTuple.from_string(bad)
+
+
+def test_interner_shared_uuid_space():
+    it = Interner()
+    a = it.tuple_ids(RelationTuple.from_string("n:user#rel@user"))
+    assert a[1] == a[4]  # object "user" and subject id "user" share the id (one UUID space)
+    assert a[3] == SUBJECT_ID
+    assert it.rel_name(it.wildcard_rel) == "..."
+    assert it.uuid_of("x") == it.uuid_of("x")
+
+
+def test_mapper_unknown_namespace():
+    it = Interner()
+    m = Mapper(it, [Namespace("known")])
+    m.from_tuple(RelationTuple.from_string("known:o#r@s"))
+    with pytest.raises(NamespaceNotFound):
+        m.from_tuple(RelationTuple.from_string("unknown:o#r@s"))
+    with pytest.raises(NamespaceNotFound):
+        m.from_tuple(RelationTuple.from_string("known:o#r@(unknown:o#r)"))
+
+
+def test_namespace_json_roundtrip_and_compile():
+    js = {"name": "acl", "relations": [
+        {"name": "allow"}, {"name": "deny"},
+        {"name": "access", "rewrite": {"operator": "and", "children": [
+            {"relation": "allow"}, {"inverted": {"relation": "deny"}},
+            {"relation": "parent", "computed_subject_set_relation": "access"}]}}]}
+    ns = namespace_from_json(js)
+    assert isinstance(ns.relations[2].rewrite.children[1], InvertResult)
+    assert namespace_from_json(namespace_to_json(ns)) == ns
+    it = Interner()
+    p = compile_program([ns], it)
+    assert p.ns_has_rel[it.ns_id("acl")] == 1
+    assert list(p.rel_root) == [-1, -1, 0]
+    kinds = list(p.rw[:, 0])
+    assert kinds == [1, 2, 4, 2, 3]  # and, computed, not, computed(deny), ttu
+    # single child without operator is wrapped into an "or" (ast_definitions.go:59-68)
+    ns2 = namespace_from_json({"name": "d", "relations": [{"name": "v", "rewrite": {"relation": "o"}}]})
+    assert ns2.relations[0].rewrite.operation == "or"
+
+
+def test_tree_json_roundtrip():
+    t = Tree("union", SubjectSet("a", "b", "c"), [Tree("leaf", "u")])
+    assert Tree.from_json(t.to_json()) == t
+
+
+def test_library_exports_every_declared_symbol():
+    from keto_amd import _lib
+    from keto_amd.build import build
+    build()  # cross-compiles for gfx950 on a CPU-only host too
+    with open(os.path.join(ROOT, "include", "ketogpu.h")) as f:
+        hdr = f.read()
+    declared = set(re.findall(r"\b(kg_[a-z_]+)\s*\(", hdr))
+    assert declared == set(_lib.EXPORTS), declared ^ set(_lib.EXPORTS)
+    L = _lib.load()
+    for name in declared:
+        assert hasattr(L, name), name
+    assert L.kg_version().startswith(b"ketogpu")
+
+
+def test_library_reports_errors_without_gpu():
+    from keto_amd import _lib
+    L = _lib.load()
+    h = ctypes.c_void_p()
+    rc = L.kg_snapshot_create(None, 0, None, None, 0, None)
+    assert rc != 0
+    assert "NULL" in _lib.last_error()
