@@ -1,0 +1,232 @@
+// kg_bfs.h -- wave64 building blocks shared by the check kernels (device only).
+//
+// wave_bfs_run(): level-synchronous, depth-bounded BFS of ONE wave over the set-adjacency CSR,
+// starting from a deduplicated root set at rest depth d0.  It answers, for rewrite-free nodes,
+// the reference's checkIsAllowed recursion (internal/check/engine.go:183-207):
+//   level k node at rest depth d = d0-k:  checkDirect(d-1)   -> probe the exact tuple if d >= 1
+//                                          checkExpandSubject -> children at d-1, if d >= 2
+// with the group rule "first IsMember wins" (checkgroup/concurrent_checkgroup.go:104-115) as the
+// early exit.  Marking every node at its shallowest level gives the schedule-free answer
+// (SURVEY.md 8a); storage is either the wave's LDS (fast tier, bounded) or a per-slot HBM
+// bitmap + list (unbounded tier).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "kg_internal.h"
+
+namespace kg {
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
+__device__ __forceinline__ uint32_t nmap_find(const DevSnap& s, uint32_t ns, uint32_t rel, uint32_t obj) {
+  if (ns >= 0xFFFFu || rel >= 0xFFFFu || obj >= 0x7FFFFFFFu) return NONE;
+  uint64_t key = nmap_key(ns, rel, obj);
+  uint64_t i = mix64(key) & s.nmap_mask;
+  for (;;) {
+    uint64_t k = s.nmap_keys[i];
+    if (k == key) return s.nmap_vals[i];
+    if (k == EMPTY64) return NONE;
+    i = (i + 1) & s.nmap_mask;
+  }
+}
+
+// checkDirect: does the exact tuple (node, subject) exist?  One 64-B bucket per probe.
+__device__ __forceinline__ bool dset_probe(const DevSnap& s, uint32_t node, uint32_t subj) {
+  uint64_t key = dset_key(node, subj);
+  uint64_t b = mix64(key) & s.dset_mask;
+  for (;;) {
+    const ulonglong2* p = reinterpret_cast<const ulonglong2*>(s.dset + b * DSET_BUCKET);
+    ulonglong2 a0 = p[0], a1 = p[1], a2 = p[2], a3 = p[3];
+    if (a0.x == key || a0.y == key || a1.x == key || a1.y == key || a2.x == key || a2.y == key || a3.x == key ||
+        a3.y == key)
+      return true;
+    if (a3.y == EMPTY64) return false;  // buckets fill front to back
+    b = (b + 1) & s.dset_mask;
+  }
+}
+
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t x, uint32_t* total) {
+  int lane = lane_id();
+  uint32_t v = x;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    uint32_t y = __shfl_up(v, off, 64);
+    if (lane >= off) v += y;
+  }
+  *total = __shfl(v, 63, 64);
+  return v - x;
+}
+
+__device__ __forceinline__ void wave_append(bool pred, uint32_t val, uint32_t* list, uint32_t* count) {
+  uint64_t m = __ballot(pred);
+  if (!m) return;
+  int lane = lane_id();
+  int leader = __ffsll((unsigned long long)m) - 1;
+  uint32_t base = 0;
+  if (lane == leader) base = atomicAdd(count, (uint32_t)__popcll(m));
+  base = __shfl(base, leader, 64);
+  if (pred) list[base + __popcll(m & ((1ull << lane) - 1))] = val;
+}
+
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
+  uint32_t lo = __shfl((uint32_t)v, src, 64), hi = __shfl((uint32_t)(v >> 32), src, 64);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ uint32_t lanes_below(uint64_t m) { return __popcll(m & ((1ull << lane_id()) - 1)); }
+
+// largest j in [0, n) with pref[j] <= e (pref non-decreasing, pref[0] = 0)
+__device__ __forceinline__ int owner_search(const uint32_t* pref, int n, uint32_t e) {
+  int lo = 0, hi = n;
+  while (hi - lo > 1) {
+    int mid = (lo + hi) >> 1;
+    if (pref[mid] <= e) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// ------------------------------------------------------------------ per-wave BFS storage
+constexpr int VIS_LOG2 = 10;  // LDS visited-hash slots per wave
+constexpr int VIS = 1 << VIS_LOG2;
+constexpr int LIST = 512;  // LDS BFS list per wave (visited cap; hash load <= 0.5)
+
+struct WaveLds {
+  uint32_t vis[VIS];
+  uint32_t list[LIST];
+  uint32_t pref[64];
+};
+
+struct LdsStore {
+  WaveLds* L;
+  __device__ uint32_t* list() const { return L->list; }
+  __device__ uint32_t* pref() const { return L->pref; }
+  __device__ uint64_t cap() const { return LIST; }
+  __device__ void reset() {
+    const int lane = lane_id();
+    for (int i = lane * 4; i < VIS; i += 256) *reinterpret_cast<uint4*>(&L->vis[i]) = make_uint4(NONE, NONE, NONE, NONE);
+    __builtin_amdgcn_wave_barrier();
+  }
+  __device__ bool insert(uint32_t key) {
+    uint32_t h = (key * 2654435761u) >> (32 - VIS_LOG2);
+    for (;;) {
+      uint32_t old = atomicCAS(&L->vis[h], NONE, key);
+      if (old == NONE) return true;
+      if (old == key) return false;
+      h = (h + 1) & (VIS - 1);
+    }
+  }
+  __device__ void sync() { __builtin_amdgcn_wave_barrier(); }
+  __device__ void finish(uint32_t) {}
+};
+
+// HBM tier: visited bitmap (n_nodes bits, left all-clear between runs) + BFS list; LDS prefix.
+struct GlobalStore {
+  uint32_t* bm;
+  uint32_t* lst;
+  uint64_t capacity;
+  uint32_t* pf;
+  __device__ uint32_t* list() const { return lst; }
+  __device__ uint32_t* pref() const { return pf; }
+  __device__ uint64_t cap() const { return capacity; }
+  __device__ void reset() {}
+  __device__ bool insert(uint32_t key) {
+    uint32_t bit = 1u << (key & 31);
+    return !(atomicOr(&bm[key >> 5], bit) & bit);
+  }
+  __device__ void sync() {
+    // list entries written by other lanes of this wave must be visible to its loads
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  }
+  __device__ void finish(uint32_t n) {
+    sync();
+    for (uint32_t i = lane_id(); i < n; i += 64) atomicAnd(&bm[lst[i] >> 5], 0u);
+    sync();
+  }
+};
+
+struct BfsStats {
+  unsigned long long rows = 0, edges = 0, probes = 0;
+};
+
+enum : int { BFS_N = 0, BFS_M = 1, BFS_OVERFLOW = 2 };
+
+// Each lane offers at most one candidate root; deduplicated roots are appended to the list.
+// Returns false on overflow (the caller gives up on this store tier).
+template <class Store>
+__device__ __forceinline__ bool wave_add_roots(Store& st, bool offer, uint32_t node, uint32_t& n_list) {
+  const bool fresh = offer && st.insert(node);
+  const uint64_t m = __ballot(fresh);
+  const uint32_t cnt = __popcll(m);
+  if (n_list + cnt > st.cap()) return false;
+  if (fresh) st.list()[n_list + lanes_below(m)] = node;
+  n_list += cnt;
+  return true;
+}
+
+template <class Store>
+__device__ int wave_bfs_run(const DevSnap& s, Store& st, uint32_t n_roots, int d0, uint32_t subj, BfsStats& bs) {
+  const int lane = lane_id();
+  uint32_t* list = st.list();
+  uint32_t* pref = st.pref();
+  uint32_t lvl_b = 0, lvl_e = n_roots, n_list = n_roots;
+  int res = BFS_N;
+  st.sync();
+  for (int k = 0; lvl_b < lvl_e; k++) {
+    const int d = d0 - k;       // rest depth of this level's checkIsAllowed calls
+    if (d < 1) break;           // checkDirect needs d-1 >= 0
+    const bool expand = d >= 2; // children need d-1 >= 1 to probe anything
+    for (uint32_t base = lvl_b; base < lvl_e; base += 64) {
+      const uint32_t i = base + lane;
+      const bool valid = i < lvl_e;
+      const uint32_t node = valid ? list[i] : 0;
+      uint64_t rb = 0, re = 0;
+      if (valid && expand) {
+        rb = s.adj_off[node];
+        re = s.adj_off[node + 1];
+      }
+      const bool h = valid && dset_probe(s, node, subj);
+      const uint64_t nvalid = __ballot(valid);
+      bs.probes += __popcll(nvalid);
+      if (__ballot(h)) {
+        res = BFS_M;
+        break;
+      }
+      if (!expand) continue;
+      bs.rows += __popcll(nvalid);
+      uint32_t total;
+      const uint32_t excl = wave_excl_scan((uint32_t)(re - rb), &total);
+      pref[lane] = excl;
+      __builtin_amdgcn_wave_barrier();
+      bs.edges += total;
+      for (uint32_t eb = 0; eb < total; eb += 64) {
+        const uint32_t e = eb + lane;
+        const bool act = e < total;
+        const int own = act ? owner_search(pref, 64, e) : 0;
+        const uint64_t src_b = shfl64(rb, own);
+        uint32_t child = NONE;
+        if (act) child = s.adj[src_b + (e - pref[own])];
+        const bool fresh = act && st.insert(child);
+        const uint64_t m = __ballot(fresh);
+        const uint32_t cnt = __popcll(m);
+        if (n_list + cnt > st.cap()) {
+          res = BFS_OVERFLOW;
+          break;
+        }
+        if (fresh) list[n_list + lanes_below(m)] = child;
+        n_list += cnt;
+      }
+      __builtin_amdgcn_wave_barrier();
+      if (res != BFS_N) break;
+    }
+    if (res != BFS_N) break;
+    st.sync();
+    lvl_b = lvl_e;
+    lvl_e = n_list;
+  }
+  st.finish((uint32_t)min<uint64_t>(n_list, st.cap()));
+  return res;
+}
+
+}  // namespace kg

@@ -23,79 +23,12 @@
 
 #include <algorithm>
 
+#include "kg_bfs.h"
 #include "kg_internal.h"
+#include "kg_interp.h"
 #include "kg_snapshot.h"
 
 namespace kg {
-
-// ------------------------------------------------------------------ device helpers
-__device__ __forceinline__ uint32_t nmap_find(const DevSnap& s, uint32_t ns, uint32_t rel, uint32_t obj) {
-  if (ns >= 0xFFFFu || rel >= 0xFFFFu || obj >= 0x7FFFFFFFu) return NONE;
-  uint64_t key = nmap_key(ns, rel, obj);
-  uint64_t i = mix64(key) & s.nmap_mask;
-  for (;;) {
-    uint64_t k = s.nmap_keys[i];
-    if (k == key) return s.nmap_vals[i];
-    if (k == EMPTY64) return NONE;
-    i = (i + 1) & s.nmap_mask;
-  }
-}
-
-// checkDirect: does the exact tuple (node, subject) exist?  One 64-B bucket per probe.
-__device__ __forceinline__ bool dset_probe(const DevSnap& s, uint32_t node, uint32_t subj) {
-  uint64_t key = dset_key(node, subj);
-  uint64_t b = mix64(key) & s.dset_mask;
-  for (;;) {
-    const ulonglong2* p = reinterpret_cast<const ulonglong2*>(s.dset + b * DSET_BUCKET);
-    ulonglong2 a0 = p[0], a1 = p[1], a2 = p[2], a3 = p[3];
-    if (a0.x == key || a0.y == key || a1.x == key || a1.y == key || a2.x == key || a2.y == key || a3.x == key ||
-        a3.y == key)
-      return true;
-    if (a3.y == EMPTY64) return false;  // buckets fill front to back
-    b = (b + 1) & s.dset_mask;
-  }
-}
-
-__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
-
-__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t x, uint32_t* total) {
-  int lane = lane_id();
-  uint32_t v = x;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    uint32_t y = __shfl_up(v, off, 64);
-    if (lane >= off) v += y;
-  }
-  *total = __shfl(v, 63, 64);
-  return v - x;
-}
-
-__device__ __forceinline__ void wave_append(bool pred, uint32_t val, uint32_t* list, uint32_t* count) {
-  uint64_t m = __ballot(pred);
-  if (!m) return;
-  int lane = lane_id();
-  int leader = __ffsll((unsigned long long)m) - 1;
-  uint32_t base = 0;
-  if (lane == leader) base = atomicAdd(count, (uint32_t)__popcll(m));
-  base = __shfl(base, leader, 64);
-  if (pred) list[base + __popcll(m & ((1ull << lane) - 1))] = val;
-}
-
-__device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
-  uint32_t lo = __shfl((uint32_t)v, src, 64), hi = __shfl((uint32_t)(v >> 32), src, 64);
-  return ((uint64_t)hi << 32) | lo;
-}
-
-// largest j in [0, n) with pref[j] <= e (pref non-decreasing, pref[0] = 0)
-__device__ __forceinline__ int owner_search(const uint32_t* pref, int n, uint32_t e) {
-  int lo = 0, hi = n;  // invariant: pref[lo] <= e, answer in [lo, hi)
-  while (hi - lo > 1) {
-    int mid = (lo + hi) >> 1;
-    if (pref[mid] <= e) lo = mid;
-    else hi = mid;
-  }
-  return lo;
-}
 
 // Counters: [0] rows_opened [1] edges_read [2] probes [3] frontier_hbm [4] light [5] heavy [6] general
 enum { ST_ROWS = 0, ST_EDGES, ST_PROBES, ST_FHBM, ST_LIGHT, ST_HEAVY, ST_GENERAL, ST_LROWS, ST_LEDGES, ST_LPROBES, ST_N };
@@ -106,6 +39,7 @@ struct Ctl {
   uint32_t heavy_head, giant_head, gen_head, pad0;
   uint32_t heads[8 * 32];  // per-XCD dequeue heads, one 128-B line each
   unsigned long long st[ST_N];
+  InterpCtl ic;
 };
 
 // ------------------------------------------------------------------ k_resolve
@@ -147,34 +81,14 @@ __global__ __launch_bounds__(256) void k_resolve(DevSnap s, const kg_query* __re
 }
 
 // ------------------------------------------------------------------ k_light
-constexpr int LWAVES = 4;     // waves per workgroup (256 threads)
-constexpr int VIS_LOG2 = 10;  // LDS visited-hash slots per wave
-constexpr int VIS = 1 << VIS_LOG2;
-constexpr int LIST = 512;     // LDS BFS list per wave; level k = list[lvl_b, lvl_e)
-constexpr int VIS_MAX = LIST; // visited cap (load <= 0.5 on the hash)
+constexpr int LWAVES = 4;  // waves per workgroup (256 threads)
 
-struct LightLds {
-  uint32_t vis[VIS];
-  uint32_t list[LIST];
-  uint32_t pref[64];
-};
-
-__device__ __forceinline__ bool vis_insert(uint32_t* vis, uint32_t key) {
-  uint32_t h = (key * 2654435761u) >> (32 - VIS_LOG2);
-  for (;;) {
-    uint32_t old = atomicCAS(&vis[h], NONE, key);
-    if (old == NONE) return true;
-    if (old == key) return false;
-    h = (h + 1) & (VIS - 1);
-  }
-}
-
-// Dequeue one light query index; per-XCD heads over [0, count) split into 8 ranges.
-__device__ __forceinline__ uint32_t dequeue(Ctl* ctl, uint32_t count, uint32_t& head_sel) {
-  while (head_sel < 8 + 8) {
-    uint32_t h = (head_sel) & 7;
+// Dequeue one work index; per-XCD heads over [0, count) split into 8 ranges.
+__device__ __forceinline__ uint32_t dequeue(uint32_t* heads, uint32_t count, uint32_t& head_sel, uint32_t head0) {
+  while (head_sel < head0 + 8) {
+    uint32_t h = head_sel & 7;
     uint32_t lo = (uint32_t)((uint64_t)count * h / 8), hi = (uint32_t)((uint64_t)count * (h + 1) / 8);
-    uint32_t k = atomicAdd(&ctl->heads[h * 32], 1u);
+    uint32_t k = atomicAdd(&heads[h * 32], 1u);
     if (lo + k < hi) return lo + k;
     head_sel++;
   }
@@ -184,94 +98,37 @@ __device__ __forceinline__ uint32_t dequeue(Ctl* ctl, uint32_t count, uint32_t& 
 __global__ __launch_bounds__(256) void k_light(DevSnap s, const RQuery* __restrict__ rq,
                                                const uint32_t* __restrict__ light_list, uint8_t* __restrict__ out,
                                                uint32_t* __restrict__ err, uint32_t* heavy_list, Ctl* ctl) {
-  __shared__ LightLds lds_all[LWAVES];
+  __shared__ WaveLds lds_all[LWAVES];
   const int wave = threadIdx.x >> 6, lane = lane_id();
-  LightLds& L = lds_all[wave];
+  LdsStore st{&lds_all[wave]};
   const uint32_t count = ctl->light_count;
-  uint32_t head_sel = blockIdx.x & 7;  // XCD label (speed only, never correctness)
-  unsigned long long st_rows = 0, st_edges = 0, st_probes = 0, st_done = 0;
+  const uint32_t head0 = blockIdx.x & 7;  // XCD label (speed only, never correctness)
+  uint32_t head_sel = head0;
+  BfsStats bs;
+  unsigned long long st_done = 0;
   for (;;) {
     uint32_t li = 0;
-    if (lane == 0) li = dequeue(ctl, count, head_sel);
+    if (lane == 0) li = dequeue(ctl->heads, count, head_sel, head0);
     li = __shfl(li, 0, 64);
     if (li == NONE) break;
     const uint32_t qi = light_list[li];
     const RQuery q = rq[qi];
-    // reset the visited hash (4 KiB = 4 x 1 KiB wave stores)
-    for (int i = lane * 4; i < VIS; i += 256) *reinterpret_cast<uint4*>(&L.vis[i]) = make_uint4(NONE, NONE, NONE, NONE);
-    __builtin_amdgcn_wave_barrier();
-    if (lane == 0) {
-      vis_insert(L.vis, q.node);
-      L.list[0] = q.node;
-    }
-    __builtin_amdgcn_wave_barrier();
-    uint32_t lvl_b = 0, lvl_e = 1, n_list = 1;
-    bool hit = false, overflow = false;
-    for (int k = 0;; k++) {
-      const int d = q.depth - k;  // rest depth of this level's checkIsAllowed calls
-      if (d < 1) break;           // direct needs d-1 >= 0
-      const bool expand = d >= 2; // children need d-1 >= 1 to probe anything
-      for (uint32_t base = lvl_b; base < lvl_e; base += 64) {
-        const uint32_t i = base + lane;
-        const bool valid = i < lvl_e;
-        const uint32_t node = valid ? L.list[i] : 0;
-        uint64_t rb = 0, re = 0;
-        if (valid && expand) {
-          rb = s.adj_off[node];
-          re = s.adj_off[node + 1];
-        }
-        const bool h = valid && dset_probe(s, node, q.subj);
-        const uint64_t nvalid = __ballot(valid);
-        st_probes += __popcll(nvalid);
-        if (__ballot(h)) {
-          hit = true;
-          break;
-        }
-        if (!expand) continue;
-        st_rows += __popcll(nvalid);
-        uint32_t total;
-        const uint32_t len = (uint32_t)(re - rb);
-        const uint32_t excl = wave_excl_scan(len, &total);
-        L.pref[lane] = excl;
-        __builtin_amdgcn_wave_barrier();
-        st_edges += total;
-        for (uint32_t eb = 0; eb < total; eb += 64) {
-          const uint32_t e = eb + lane;
-          const bool act = e < total;
-          uint32_t child = NONE;
-          int own = act ? owner_search(L.pref, 64, e) : 0;
-          const uint64_t src_b = shfl64(rb, own);
-          if (act) child = s.adj[src_b + (e - L.pref[own])];
-          const bool fresh = act && vis_insert(L.vis, child);
-          const uint64_t m = __ballot(fresh);
-          const uint32_t cnt = __popcll(m);
-          if (n_list + cnt > VIS_MAX) {
-            overflow = true;
-            break;
-          }
-          if (fresh) L.list[n_list + __popcll(m & ((1ull << lane) - 1))] = child;
-          n_list += cnt;
-        }
-        __builtin_amdgcn_wave_barrier();
-        if (overflow) break;
-      }
-      if (hit || overflow) break;
-      lvl_b = lvl_e;
-      lvl_e = n_list;
-      if (lvl_b == lvl_e) break;
-    }
-    if (overflow) {
+    st.reset();
+    uint32_t n = 0;
+    wave_add_roots(st, lane == 0, q.node, n);
+    const int r = wave_bfs_run(s, st, n, q.depth, q.subj, bs);
+    if (r == BFS_OVERFLOW) {
       if (lane == 0) heavy_list[atomicAdd(&ctl->heavy_count, 1u)] = qi;
     } else if (lane == 0) {
-      out[qi] = hit ? KG_IS_MEMBER : KG_NOT_MEMBER;
+      out[qi] = r == BFS_M ? KG_IS_MEMBER : KG_NOT_MEMBER;
       if (err) err[qi] = KG_ERR_NONE;
       st_done++;
     }
   }
   if (lane == 0) {
-    atomicAdd(&ctl->st[ST_LROWS], st_rows);
-    atomicAdd(&ctl->st[ST_LEDGES], st_edges);
-    atomicAdd(&ctl->st[ST_LPROBES], st_probes);
+    atomicAdd(&ctl->st[ST_LROWS], bs.rows);
+    atomicAdd(&ctl->st[ST_LEDGES], bs.edges);
+    atomicAdd(&ctl->st[ST_LPROBES], bs.probes);
     atomicAdd(&ctl->st[ST_LIGHT], st_done);
   }
 }
@@ -380,7 +237,7 @@ __global__ __launch_bounds__(256) void k_heavy(DevSnap s, const RQuery* __restri
       if (lvl_b == lvl_e) break;
     }
     __syncthreads();
-    const uint32_t n_list = min<uint64_t>(sh_n, cap);
+    const uint32_t n_list = (uint32_t)min((uint64_t)sh_n, cap);
     if (tid == 0) {
       if (sh_over && !sh_hit) {
         giant_list[atomicAdd(giant_count, 1u)] = qi;
@@ -390,8 +247,13 @@ __global__ __launch_bounds__(256) void k_heavy(DevSnap s, const RQuery* __restri
         st_done++;
       }
     }
-    // clear this query's bits (every set bit in a touched word belongs to this query)
-    for (uint32_t i = tid; i < n_list; i += 256) atomicAnd(&bm[list[i] >> 5], 0u);
+    // clear this query's bits (every set bit in a touched word belongs to this query); after an
+    // overflow some set bits have no list entry, so the whole slot bitmap is cleared instead
+    if (sh_over) {
+      for (uint64_t w = tid; w < words_per_slot; w += 256) bm[w] = 0u;
+    } else {
+      for (uint32_t i = tid; i < n_list; i += 256) atomicAnd(&bm[list[i] >> 5], 0u);
+    }
     __syncthreads();
   }
   if (tid == 0) {
@@ -446,12 +308,6 @@ int synth_queries(Snapshot* s, uint64_t seed, size_t n, kg_query* d_q) {
   return 0;
 }
 
-// k_general lives in kg_interp.hip
-int launch_general(Snapshot* s, const RQuery* rq, const uint32_t* gen_list, const uint32_t* gen_count,
-                   uint32_t* gen_head, uint8_t* out, uint32_t* err, unsigned long long* st_general,
-                   unsigned long long* st_rows, unsigned long long* st_edges, unsigned long long* st_probes,
-                   hipStream_t stream);
-
 // ------------------------------------------------------------------ batch driver
 static size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 
@@ -461,10 +317,11 @@ int check_batch_device(Snapshot* s, const kg_query* d_q, size_t n, int32_t globa
   if (n > 0x7FFFFFFFull) return set_error(-2, "batch too large");
   HIPC(hipSetDevice(s->device));
   if (!stream) stream = s->stream;
-  // scratch: rq[n] | light[n] | gen[n] | heavy[n] | giant[n] | Ctl
+  // scratch: rq[n] | light[n] | gen[n] | heavy[n] | giant[n] | p2[n] | Ctl
   size_t off_rq = 0, off_light = align_up(off_rq + n * sizeof(RQuery)), off_gen = align_up(off_light + n * 4),
          off_heavy = align_up(off_gen + n * 4), off_giant = align_up(off_heavy + n * 4),
-         off_ctl = align_up(off_giant + n * 4), total = align_up(off_ctl + sizeof(Ctl));
+         off_p2 = align_up(off_giant + n * 4), off_ctl = align_up(off_p2 + n * 4),
+         total = align_up(off_ctl + sizeof(Ctl));
   if (total > s->scratch_bytes) {
     if (s->scratch) hipFree(s->scratch);
     s->scratch = nullptr;
@@ -478,6 +335,7 @@ int check_batch_device(Snapshot* s, const kg_query* d_q, size_t n, int32_t globa
   uint32_t* gen = (uint32_t*)(base + off_gen);
   uint32_t* heavy = (uint32_t*)(base + off_heavy);
   uint32_t* giant = (uint32_t*)(base + off_giant);
+  uint32_t* p2 = (uint32_t*)(base + off_p2);
   Ctl* ctl = (Ctl*)(base + off_ctl);
   // heavy pool: H slots of (bitmap + cap list) + one giant slot (bitmap + n_nodes list)
   const uint64_t nn = std::max<uint32_t>(s->ds.n_nodes, 1);
@@ -523,9 +381,17 @@ int check_batch_device(Snapshot* s, const kg_query* d_q, size_t n, int32_t globa
     hipLaunchKernelGGL(k_heavy, dim3(1), dim3(256), 0, stream, s->ds, rq, giant, &ctl->giant_count, &ctl->giant_head,
                        d_out, d_err, gb, words, gl, nn, giant /*never overflows*/, &ctl->pad0, ctl);
     HIPC(hipGetLastError());
-    if (launch_general(s, rq, gen, &ctl->gen_count, &ctl->gen_head, d_out, d_err, &ctl->st[ST_GENERAL],
-                       &ctl->st[ST_ROWS], &ctl->st[ST_EDGES], &ctl->st[ST_PROBES], stream))
-      return -1;
+    if (s->has_program) {
+      InterpCtl ic{};
+      ic.gen_count = &ctl->gen_count;
+      ic.p2_list = p2;
+      ic.st_general = &ctl->st[ST_GENERAL];
+      ic.st_rows = &ctl->st[ST_ROWS];
+      ic.st_edges = &ctl->st[ST_EDGES];
+      ic.st_probes = &ctl->st[ST_PROBES];
+      HIPC(hipMemcpyAsync(&ctl->ic, &ic, sizeof ic, hipMemcpyHostToDevice, stream));
+      if (launch_general(s, d_q, rq, gen, &ctl->gen_count, &ctl->ic, d_out, d_err, stream)) return -1;
+    }
   }
   if (stats) {
     HIPC(hipEventRecord(e1, stream));

@@ -47,6 +47,9 @@ struct Snapshot {
   size_t scratch_bytes = 0;
   void* heavy_pool = nullptr;
   size_t heavy_pool_bytes = 0;
+  void* interp_pool = nullptr;
+  size_t interp_pool_bytes = 0;
+  uint64_t batch_seq = 0;
 
   ~Snapshot();
   int init_device(int dev);

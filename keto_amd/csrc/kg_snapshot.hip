@@ -99,6 +99,9 @@ static uint64_t pow2_at_least(uint64_t x) {
 Snapshot::~Snapshot() {
   if (device >= 0) hipSetDevice(device);
   for (void* p : allocs) hipFree(p);
+  if (scratch) hipFree(scratch);
+  if (heavy_pool) hipFree(heavy_pool);
+  if (interp_pool) hipFree(interp_pool);
   if (stream) hipStreamDestroy(stream);
 }
 
