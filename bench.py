@@ -181,28 +181,33 @@ def cpu_baseline(snap, dq, a) -> dict:
     threads = max(1, min(a.cpu_threads, os.cpu_count() or 1))
     o = Oracle.from_csr(0, nd[0], nd[1], nd[2], row_off, row_subj, nthreads=threads)
     del row_subj
-    q = dq[:200_000].cpu().numpy().view(np.uint32)
+    q = dq.cpu().numpy().view(np.uint32)
     node = q[:, 1].copy()  # synthetic docs: node id == object id
     subj = q[:, 4].copy()
     dep = q[:, 6].view(np.int32).copy()
 
-    def run(n, th):
+    def run(n, th, passes=1):
         t = time.perf_counter()
-        o.check_nodes_batch(node[:n], subj[:n], dep[:n], a.global_depth, POLICY_DFS, th)
+        for _ in range(passes):
+            o.check_nodes_batch(node[:n], subj[:n], dep[:n], a.global_depth, POLICY_DFS, th)
         return time.perf_counter() - t
 
     res = {}
     for th, budget in ((threads, a.cpu_seconds), (1, a.cpu_seconds / 3)):
-        n = 256
+        n, passes = 256, 1
         t = run(n, th)
-        while t < budget / 8 and n < len(node):
+        while t < budget / 4 and n < len(node):  # grow the sample of distinct checks first
             n = min(len(node), n * 4)
             t = run(n, th)
-        res[th] = (n / t, n, t)
-    v, n, t = res[threads]
+        if t < budget / 2:  # then repeat it to reach ~budget seconds of CPU work
+            passes = max(1, int(budget / max(t, 1e-6)))
+            t = run(n, th, passes)
+        res[th] = (n * passes / t, n, passes, t)
+    v, n, passes, t = res[threads]
     return {"value": v, "unit": "checks/s", "cores": threads, "kind": "port",
-            "sample": f"first {n} checks of the rank-0 batch on the same graph ({t:.1f} s), sequential Go-order DFS "
-                      f"with visited sets (oracle/keto_oracle.c POLICY_DFS), {threads} host threads",
+            "sample": f"{passes} pass(es) over the first {n} checks of the rank-0 batch on the same graph "
+                      f"({t:.1f} s), sequential Go-order DFS with visited sets (oracle/keto_oracle.c POLICY_DFS), "
+                      f"{threads} host threads",
             "value_1thread": res[1][0], "host_cpu": host_cpu()}
 
 

@@ -201,12 +201,13 @@ int kg_synth_queries(kg_snapshot* sp, uint64_t seed, size_t n, kg_query* d_q) {
 }
 
 int kg_expand_batch(kg_snapshot* sp, const kg_set* roots, size_t n, int32_t global_max_depth, kg_tree_buf* out) {
-  (void)sp;
-  (void)roots;
-  (void)n;
-  (void)global_max_depth;
-  if (out) memset(out, 0, sizeof *out);
-  return set_error(KG_ERR_NOT_IMPLEMENTED, "kg_expand_batch: not implemented yet");
+  KG_GUARD_BEGIN
+  if (!sp || !out) return set_error(-2, "NULL argument");
+  if (n && !roots) return set_error(-2, "roots is NULL");
+  Snapshot* s = reinterpret_cast<Snapshot*>(sp);
+  std::lock_guard<std::mutex> lk(s->mu);
+  return kg::expand_batch(s, roots, n, global_max_depth, out);
+  KG_GUARD_END
 }
 
 void kg_tree_free(kg_tree_buf* t) {

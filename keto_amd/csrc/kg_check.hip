@@ -62,8 +62,7 @@ __global__ __launch_bounds__(256) void k_resolve(DevSnap s, const kg_query* __re
     }
     int32_t d = x.max_depth;
     if (d <= 0 || global < d) d = global;  // engine.go:68-70
-    uint8_t rf = 0;
-    if (s.relflags && x.t.ns < s.n_ns && x.t.rel < s.n_rel) rf = s.relflags[(size_t)x.t.ns * s.n_rel + x.t.rel];
+    const uint8_t rf = relflag(s, x.t.ns, x.t.rel);
     if (node == NONE) {
       route = rf ? ROUTE_GENERAL : ROUTE_DONE;
     } else {

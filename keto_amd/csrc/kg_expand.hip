@@ -1,0 +1,434 @@
+// kg_expand.hip -- batched expand trees (expand.Engine.BuildTree, internal/expand/engine.go:35-104).
+//
+// BuildTree is a sequential pre-order DFS with ONE visited set per request (created at the root,
+// graph_utils.go:35-50): a subject set already visited returns nil, a set without rows returns
+// nil, rest depth <= 1 turns a set with rows into a Leaf, otherwise a Union whose children are the
+// row subjects in shard order (nil children become Leaf{row subject}).  The depth clamp
+// (engine.go:37-39) is re-applied per level but is the identity below the root (children get
+// d-1 >= 1).
+//
+// One wave64 per root.  Every row subject yields exactly one child record, so a Union's child
+// count (its row length) is known when it is emitted and the output is a single pre-order stream.
+// Order only matters for subject sets that will be EXPANDED (unvisited, rows non-empty, d-1 >= 2):
+// everything before the first such candidate in a 64-wide row chunk is emitted in parallel as
+// leaves, candidates are visited strictly in row order.  Output streams go to 1024-record chunks
+// of an HBM arena (bump allocator), then a compaction kernel lays each root out contiguously.
+// Visited sets live in LDS (pass 1); roots that outgrow LDS rerun with an HBM bitmap (pass 2).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "kg_bfs.h"
+#include "kg_internal.h"
+#include "kg_snapshot.h"
+
+namespace kg {
+
+constexpr uint32_t CHUNK = 256;  // records per arena chunk
+
+struct ExpFrame {
+  uint32_t node;
+  uint32_t cursor;
+  int32_t d;
+  uint32_t pad;
+};
+
+struct ExpCtl {
+  uint32_t arena_head;   // next free chunk
+  uint32_t overflow;     // arena exhausted
+  uint32_t p2_count, p2_head;
+  uint32_t head;         // pass-1 dequeue
+  uint32_t pad[3];
+  unsigned long long records;
+};
+
+// Per-root result of the DFS: first chunk and record count (0 records = nil tree).
+struct RootOut {
+  uint32_t first_chunk;
+  uint32_t count;
+};
+
+struct Stream {
+  kg_tree_node* arena;
+  uint32_t* next;  // chunk -> next chunk
+  uint32_t n_chunks;
+  ExpCtl* ctl;
+  uint32_t first, cur, pos;  // wave-uniform
+  bool ok;
+};
+
+__device__ __forceinline__ uint32_t alloc_chunk(Stream& S) {
+  uint32_t c = 0;
+  if (lane_id() == 0) c = atomicAdd(&S.ctl->arena_head, 1u);
+  c = __shfl(c, 0, 64);
+  if (c >= S.n_chunks) {
+    if (lane_id() == 0) S.ctl->overflow = 1;
+    S.ok = false;
+    return NONE;
+  }
+  if (lane_id() == 0) S.next[c] = NONE;
+  return c;
+}
+
+// Lanes with `pred` append one record each, in lane order, to the wave's stream.
+__device__ __forceinline__ void emit(Stream& S, bool pred, const kg_tree_node& r) {
+  const uint64_t m = __ballot(pred);
+  if (!m || !S.ok) return;
+  const uint32_t cnt = __popcll(m);
+  const uint32_t rank = lanes_below(m);
+  uint32_t room = CHUNK - S.pos;
+  uint32_t nxt = NONE;
+  if (cnt > room) {
+    nxt = alloc_chunk(S);
+    if (!S.ok) return;
+    if (lane_id() == 0) S.next[S.cur] = nxt;
+  }
+  if (pred) {
+    if (rank < room) S.arena[(size_t)S.cur * CHUNK + S.pos + rank] = r;
+    else S.arena[(size_t)nxt * CHUNK + (rank - room)] = r;
+  }
+  if (cnt > room) {
+    S.cur = nxt;
+    S.pos = cnt - room;
+  } else {
+    S.pos += cnt;
+  }
+}
+
+__device__ __forceinline__ kg_tree_node rec_set(const DevSnap& s, uint8_t type, uint32_t node, uint32_t nch) {
+  kg_tree_node r;
+  r.type = type;
+  r.is_set = 1;
+  r.pad = 0;
+  r.ns = s.nd_ns[node];
+  r.obj = s.nd_obj[node];
+  r.rel = s.nd_rel[node];
+  r.n_children = nch;
+  return r;
+}
+__device__ __forceinline__ kg_tree_node rec_subject(const DevSnap& s, uint32_t sub) {
+  if (sub & SET_BIT) return rec_set(s, 2, sub & ~SET_BIT, 0);
+  kg_tree_node r;
+  r.type = 2;
+  r.is_set = 0;
+  r.pad = 0;
+  r.ns = KG_SUBJECT_ID;
+  r.obj = sub;
+  r.rel = 0;
+  r.n_children = 0;
+  return r;
+}
+
+enum : int { EXP_OK = 0, EXP_OVERFLOW = 1, EXP_ARENA = 2 };
+
+template <class Store>
+__device__ int expand_root(const DevSnap& s, Store& st, const kg_set& root, int32_t global, ExpFrame* stack,
+                           Stream& S, uint32_t& n_records) {
+  const int lane = lane_id();
+  S.ok = true;
+  S.pos = 0;
+  S.first = S.cur = alloc_chunk(S);
+  n_records = 0;
+  if (!S.ok) return EXP_ARENA;
+  int32_t d = root.max_depth;
+  if (d <= 0 || global < d) d = global;  // engine.go:37-39
+  if (root.sns == KG_SUBJECT_ID) {       // SubjectID -> Leaf
+    emit(S, lane == 0, rec_subject(s, root.sobj < 0x7FFFFFFFu ? root.sobj : 0x7FFFFFFFu));
+    n_records = 1;
+    return S.ok ? EXP_OK : EXP_ARENA;
+  }
+  const uint32_t rn = nmap_find(s, root.sns, root.srel, root.sobj);
+  if (rn == NONE) return EXP_OK;  // no rows anywhere: nil
+  st.reset();
+  uint32_t n_vis = 0;
+  wave_add_roots(st, lane == 0, rn, n_vis);  // marks the root visited
+  const uint64_t rb0 = s.row_off[rn], re0 = s.row_off[rn + 1];
+  if (rb0 == re0) {
+    st.finish(n_vis);
+    return EXP_OK;  // no rows: nil
+  }
+  if (d <= 1) {
+    emit(S, lane == 0, rec_set(s, 2, rn, 0));
+    st.finish(n_vis);
+    n_records = 1;
+    return S.ok ? EXP_OK : EXP_ARENA;
+  }
+  emit(S, lane == 0, rec_set(s, 1, rn, (uint32_t)(re0 - rb0)));
+  uint32_t count = 1;
+  int sp = 0;
+  ExpFrame F{rn, 0, d, 0};
+  int status = EXP_OK;
+  for (;;) {
+    const uint64_t rb = s.row_off[F.node], re = s.row_off[F.node + 1];
+    const bool can_expand = F.d - 1 >= 2;
+    bool pushed = false;
+    while (rb + F.cursor < re) {
+      const uint64_t i = rb + F.cursor + lane;
+      const bool valid = i < re;
+      const uint32_t sub = valid ? s.row_subj[i] : 0;
+      bool cand = false;
+      uint64_t crb = 0, cre = 0;
+      if (valid && can_expand && (sub & SET_BIT)) {
+        const uint32_t c = sub & ~SET_BIT;
+        crb = s.row_off[c];
+        cre = s.row_off[c + 1];
+        cand = cre > crb;
+      }
+      const uint64_t mc = __ballot(cand);
+      const uint32_t p = mc ? (uint32_t)(__ffsll((unsigned long long)mc) - 1) : 64u;
+      // everything before the first candidate: leaves (and marks, order-free for non-candidates)
+      const bool leaf = valid && (uint32_t)lane < p;
+      // d-1 <= 1: child sets become leaves but BuildTree still marks them visited, which a later
+      // (shallower) encounter elsewhere in the tree observes.  Sets without rows need no mark:
+      // any encounter of them is a leaf.  SubjectIDs are never marked (engine.go:41-45).
+      if (!can_expand && !wave_add_roots(st, leaf && (sub & SET_BIT), sub & ~SET_BIT, n_vis)) {
+        status = EXP_OVERFLOW;
+        break;
+      }
+      emit(S, leaf, rec_subject(s, sub));
+      count += __popcll(__ballot(leaf));
+      if (!S.ok) return EXP_ARENA;
+      if (p == 64u) {
+        F.cursor += (uint32_t)min<uint64_t>(64, re - (rb + F.cursor));
+        continue;
+      }
+      // candidate at lane p, in order
+      const uint32_t csub = __shfl(sub, (int)p, 64);
+      const uint32_t cnode = csub & ~SET_BIT;
+      const uint32_t clen = (uint32_t)(__shfl((uint32_t)(cre - crb), (int)p, 64));
+      F.cursor += p + 1;
+      const uint32_t before = n_vis;
+      if (!wave_add_roots(st, lane == 0, cnode, n_vis)) {
+        status = EXP_OVERFLOW;
+        break;
+      }
+      if (n_vis == before) {  // already visited: BuildTree -> nil -> Leaf{row subject}
+        emit(S, lane == 0, rec_subject(s, csub));
+        count++;
+        if (!S.ok) return EXP_ARENA;
+        continue;
+      }
+      emit(S, lane == 0, rec_set(s, 1, cnode, clen));
+      count++;
+      if (!S.ok) return EXP_ARENA;
+      if (sp >= 0x7FFF) {
+        status = EXP_OVERFLOW;
+        break;
+      }
+      if (lane == 0) stack[sp] = F;
+      sp++;
+      F = ExpFrame{cnode, 0, F.d - 1, 0};
+      pushed = true;
+      break;
+    }
+    if (status != EXP_OK) break;
+    if (pushed) continue;
+    if (sp == 0) break;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    sp--;
+    F = stack[sp];
+  }
+  st.finish((uint32_t)min<uint64_t>(n_vis, st.cap()));
+  n_records = count;
+  return status;
+}
+
+
+
+__global__ __launch_bounds__(256) void k_expand_lds(DevSnap s, const kg_set* __restrict__ roots, uint32_t n,
+                                                    int32_t global, ExpCtl* ctl, RootOut* outs, kg_tree_node* arena,
+                                                    uint32_t* next, uint32_t n_chunks, ExpFrame* stacks,
+                                                    uint32_t stack_cap, uint32_t* p2_list) {
+  __shared__ WaveLds lds_all[4];
+  const int wave = threadIdx.x >> 6, lane = lane_id();
+  LdsStore st{&lds_all[wave]};
+  ExpFrame* stack = stacks + (size_t)(blockIdx.x * 4 + wave) * stack_cap;
+  Stream S{arena, next, n_chunks, ctl, 0, 0, 0, true};
+  unsigned long long recs = 0;
+  for (;;) {
+    uint32_t ri = 0;
+    if (lane == 0) ri = atomicAdd(&ctl->head, 1u);
+    ri = __shfl(ri, 0, 64);
+    if (ri >= n) break;
+    uint32_t nr = 0;
+    const int r = expand_root(s, st, roots[ri], global, stack, S, nr);
+    if (lane == 0) {
+      if (r == EXP_OVERFLOW) {
+        p2_list[atomicAdd(&ctl->p2_count, 1u)] = ri;
+        outs[ri] = RootOut{NONE, 0};
+      } else {
+        outs[ri] = RootOut{S.first, nr};
+        recs += nr;
+      }
+    }
+  }
+  if (lane == 0) atomicAdd(&ctl->records, recs);
+}
+
+// Pass 2: HBM bitmap visited sets; marks are always recorded in the list so they can be cleared.
+__global__ __launch_bounds__(64) void k_expand_hbm(DevSnap s, const kg_set* __restrict__ roots, int32_t global,
+                                                   ExpCtl* ctl, RootOut* outs, kg_tree_node* arena, uint32_t* next,
+                                                   uint32_t n_chunks, ExpFrame* stacks, uint32_t stack_cap,
+                                                   const uint32_t* p2_list, uint32_t* bitmaps, uint64_t words,
+                                                   uint32_t* lists, uint64_t cap) {
+  __shared__ uint32_t pref[64];
+  const int lane = lane_id();
+  GlobalStore st{bitmaps + (size_t)blockIdx.x * words, lists + (size_t)blockIdx.x * cap, cap, pref};
+  ExpFrame* stack = stacks + (size_t)blockIdx.x * stack_cap;
+  Stream S{arena, next, n_chunks, ctl, 0, 0, 0, true};
+  unsigned long long recs = 0;
+  const uint32_t count = ctl->p2_count;
+  for (;;) {
+    uint32_t k = 0;
+    if (lane == 0) k = atomicAdd(&ctl->p2_head, 1u);
+    k = __shfl(k, 0, 64);
+    if (k >= count) break;
+    const uint32_t ri = p2_list[k];
+    uint32_t nr = 0;
+    const int r = expand_root(s, st, roots[ri], global, stack, S, nr);
+    if (lane == 0) {
+      outs[ri] = r == EXP_OK ? RootOut{S.first, nr} : RootOut{NONE, 0xFFFFFFFFu};
+      recs += nr;
+    }
+  }
+  if (lane == 0) atomicAdd(&ctl->records, recs);
+}
+
+__global__ void k_expand_compact(const RootOut* outs, uint32_t n, const uint64_t* off, const kg_tree_node* arena,
+                                 const uint32_t* next, kg_tree_node* dst) {
+  const uint32_t r = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= n) return;
+  uint32_t c = outs[r].first_chunk, left = outs[r].count;
+  uint64_t o = off[r];
+  while (left > 0 && c != NONE) {
+    const uint32_t take = left < CHUNK ? left : CHUNK;
+    for (uint32_t i = lane; i < take; i += 64) dst[o + i] = arena[(size_t)c * CHUNK + i];
+    o += take;
+    left -= take;
+    c = next[c];
+  }
+}
+
+int expand_batch(Snapshot* s, const kg_set* roots, size_t n, int32_t global, kg_tree_buf* out) {
+  memset(out, 0, sizeof *out);
+  if (global < 1) global = 5;
+  out->root_off = (uint64_t*)calloc(n + 1, 8);
+  out->n_roots = n;
+  if (!out->root_off) return set_error(-4, "host allocation failed");
+  if (n == 0) return 0;
+  HIPC(hipSetDevice(s->device));
+  hipStream_t stream = s->stream;
+  // device buffers for this call
+  const uint32_t stack_cap = (uint32_t)std::min<int64_t>(0x8000, (int64_t)global + 2);
+  const uint32_t grid1 = (uint32_t)s->n_cu * 2, slots1 = grid1 * 4;
+  const uint64_t nn = std::max<uint32_t>(s->ds.n_nodes, 1), words = (nn + 31) / 32 + 1;
+  const uint32_t slots2 = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(32, (2ull << 30) / ((words + nn) * 4)));
+  uint32_t n_chunks = (uint32_t)std::min<uint64_t>(1u << 22, std::max<uint64_t>(4096, n * 2 + slots1));
+  kg_set* d_roots = nullptr;
+  ExpCtl* ctl = nullptr;
+  RootOut* outs = nullptr;
+  ExpFrame* stacks = nullptr;
+  uint32_t *p2 = nullptr, *bm = nullptr, *lists = nullptr;
+  kg_tree_node *arena = nullptr, *dst = nullptr;
+  uint32_t* next = nullptr;
+  uint64_t* d_off = nullptr;
+  int rc = 0;
+  auto fail = [&](const char* what, hipError_t e) { rc = set_error(-1, "%s: %s", what, hipGetErrorString(e)); };
+  hipError_t e;
+  if ((e = hipMalloc(&d_roots, n * sizeof(kg_set))) != hipSuccess) fail("hipMalloc", e);
+  if (!rc && (e = hipMalloc(&ctl, sizeof(ExpCtl))) != hipSuccess) fail("hipMalloc", e);
+  if (!rc && (e = hipMalloc(&outs, n * sizeof(RootOut))) != hipSuccess) fail("hipMalloc", e);
+  if (!rc && (e = hipMalloc(&stacks, (size_t)(slots1 + slots2) * stack_cap * sizeof(ExpFrame))) != hipSuccess)
+    fail("hipMalloc", e);
+  if (!rc && (e = hipMalloc(&p2, n * 4)) != hipSuccess) fail("hipMalloc", e);
+  if (!rc && (e = hipMalloc(&bm, (size_t)slots2 * (words + nn) * 4)) != hipSuccess) fail("hipMalloc", e);
+  if (!rc) {
+    lists = bm + (size_t)slots2 * words;
+    if ((e = hipMemcpyAsync(d_roots, roots, n * sizeof(kg_set), hipMemcpyHostToDevice, stream)) != hipSuccess)
+      fail("H2D", e);
+  }
+  ExpCtl h{};
+  for (int attempt = 0; !rc; attempt++) {
+    if (arena) hipFree(arena), arena = nullptr;
+    if (next) hipFree(next), next = nullptr;
+    if ((e = hipMalloc(&arena, (size_t)n_chunks * CHUNK * sizeof(kg_tree_node))) != hipSuccess) {
+      fail("hipMalloc(arena)", e);
+      break;
+    }
+    if ((e = hipMalloc(&next, (size_t)n_chunks * 4)) != hipSuccess) {
+      fail("hipMalloc", e);
+      break;
+    }
+    // every attempt starts from clear visited bitmaps (an arena overflow aborts roots mid-way)
+    if ((e = hipMemsetAsync(bm, 0, (size_t)slots2 * words * 4, stream)) != hipSuccess ||
+        (e = hipMemsetAsync(ctl, 0, sizeof(ExpCtl), stream)) != hipSuccess) {
+      fail("memset", e);
+      break;
+    }
+    hipLaunchKernelGGL(k_expand_lds, dim3(grid1), dim3(256), 0, stream, s->ds, d_roots, (uint32_t)n, global, ctl, outs,
+                       arena, next, n_chunks, stacks, stack_cap, p2);
+    hipLaunchKernelGGL(k_expand_hbm, dim3(slots2), dim3(64), 0, stream, s->ds, d_roots, global, ctl, outs, arena, next,
+                       n_chunks, stacks + (size_t)slots1 * stack_cap, stack_cap, p2, bm, words, lists, nn);
+    if ((e = hipGetLastError()) != hipSuccess) {
+      fail("launch", e);
+      break;
+    }
+    if ((e = hipMemcpyAsync(&h, ctl, sizeof h, hipMemcpyDeviceToHost, stream)) != hipSuccess ||
+        (e = hipStreamSynchronize(stream)) != hipSuccess) {
+      fail("expand", e);
+      break;
+    }
+    if (!h.overflow) break;
+    if (n_chunks >= (1u << 30) || attempt > 8) {
+      rc = set_error(KG_ERR_RESOURCE, "expand output exceeds the arena");
+      break;
+    }
+    n_chunks *= 4;  // grow the arena and rerun (outputs are rewritten from scratch)
+  }
+  std::vector<RootOut> ho(n);
+  if (!rc && (e = hipMemcpy(ho.data(), outs, n * sizeof(RootOut), hipMemcpyDeviceToHost)) != hipSuccess)
+    fail("D2H", e);
+  if (!rc) {
+    for (size_t r = 0; r < n; r++) {
+      if (ho[r].count == 0xFFFFFFFFu) {
+        rc = set_error(KG_ERR_RESOURCE, "expand root %zu exceeded the stack", r);
+        break;
+      }
+      out->root_off[r + 1] = out->root_off[r] + ho[r].count;
+    }
+  }
+  const uint64_t total = rc ? 0 : out->root_off[n];
+  if (!rc && total) {
+    out->nodes = (kg_tree_node*)malloc(total * sizeof(kg_tree_node));
+    if (!out->nodes) rc = set_error(-4, "host allocation failed");
+    if (!rc && (e = hipMalloc(&dst, total * sizeof(kg_tree_node))) != hipSuccess) fail("hipMalloc", e);
+    if (!rc && (e = hipMalloc(&d_off, (n + 1) * 8)) != hipSuccess) fail("hipMalloc", e);
+    if (!rc && (e = hipMemcpyAsync(d_off, out->root_off, (n + 1) * 8, hipMemcpyHostToDevice, stream)) != hipSuccess)
+      fail("H2D", e);
+    if (!rc) {
+      hipLaunchKernelGGL(k_expand_compact, dim3((uint32_t)((n + 3) / 4)), dim3(256), 0, stream, outs, (uint32_t)n,
+                         d_off, arena, next, dst);
+      if ((e = hipMemcpyAsync(out->nodes, dst, total * sizeof(kg_tree_node), hipMemcpyDeviceToHost, stream)) !=
+              hipSuccess ||
+          (e = hipStreamSynchronize(stream)) != hipSuccess)
+        fail("compact", e);
+    }
+  }
+  out->n_nodes = total;
+  for (void* p : {(void*)d_roots, (void*)ctl, (void*)outs, (void*)stacks, (void*)p2, (void*)bm, (void*)arena,
+                  (void*)next, (void*)dst, (void*)d_off})
+    if (p) (void)hipFree(p);
+  if (rc) {
+    free(out->nodes);
+    free(out->root_off);
+    memset(out, 0, sizeof *out);
+  }
+  return rc;
+}
+
+}  // namespace kg

@@ -71,12 +71,22 @@ struct DevSnap {
   const uint32_t* nd_rel;
   // program: relation flags [n_ns * n_rel] (bit0 has rewrite, bit1 undeclared->error), roots
   uint32_t n_ns, n_rel;
+  const uint8_t* ns_has_rel;  // [n_ns]: configured with relations (unknown relation ids -> error)
   const uint8_t* relflags;
   const int32_t* relroot;
   const RwNode* rw;
   const int32_t* rwchild;
   uint32_t n_rw;
 };
+
+// astRelationFor (internal/check/engine.go:209-229) as flags: bit0 = has rewrite, bit1 = the
+// namespace is configured with relations and this one is not declared ("relation %q not found").
+// Unknown namespaces and namespaces without relations accept every relation without rewrite.
+__host__ __device__ __forceinline__ uint8_t relflag(const DevSnap& s, uint32_t ns, uint32_t rel) {
+  if (!s.relflags || ns >= s.n_ns) return 0;
+  if (rel >= s.n_rel) return s.ns_has_rel[ns] ? 2 : 0;
+  return s.relflags[(size_t)ns * s.n_rel + rel];
+}
 
 // Resolved query as stored in HBM by the mapping kernel.
 struct RQuery {

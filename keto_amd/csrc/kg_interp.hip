@@ -39,10 +39,6 @@ struct Frame {
 
 __device__ __forceinline__ bool decisive(uint32_t r) { return r == R_M || r == R_ERR; }
 
-__device__ __forceinline__ uint8_t relflag(const DevSnap& s, uint32_t ns, uint32_t rel) {
-  if (!s.relflags || ns >= s.n_ns || rel >= s.n_rel) return 0;
-  return s.relflags[(size_t)ns * s.n_rel + rel];
-}
 __device__ __forceinline__ int32_t relroot(const DevSnap& s, uint32_t ns, uint32_t rel) {
   return s.relroot[(size_t)ns * s.n_rel + rel];
 }

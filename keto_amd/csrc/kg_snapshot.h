@@ -66,5 +66,7 @@ struct Snapshot {
 int check_batch_device(Snapshot* s, const kg_query* d_q, size_t n, int32_t global_max_depth, uint8_t* d_out,
                        uint32_t* d_err, kg_stats* stats, hipStream_t stream);
 int synth_queries(Snapshot* s, uint64_t seed, size_t n, kg_query* d_q);
+// kg_expand.hip
+int expand_batch(Snapshot* s, const kg_set* roots, size_t n, int32_t global, kg_tree_buf* out);
 
 }  // namespace kg

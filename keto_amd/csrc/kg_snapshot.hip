@@ -169,6 +169,7 @@ int Snapshot::upload_program(const kg_dict* dict, const kg_rewrite_prog* prog) {
   if (prog)
     for (uint32_t i = 0; i < prog->n_ns; i++) has_program |= prog->ns_has_rel[i] != 0;
   ds.relflags = nullptr;
+  ds.ns_has_rel = nullptr;
   ds.relroot = nullptr;
   ds.rw = nullptr;
   ds.rwchild = nullptr;
@@ -190,13 +191,17 @@ int Snapshot::upload_program(const kg_dict* dict, const kg_rewrite_prog* prog) {
   }
   h_rw.assign((const RwNode*)prog->rw, (const RwNode*)prog->rw + prog->n_rw);
   h_rwchild.assign(prog->child, prog->child + prog->n_child);
-  uint8_t* rf;
+  std::vector<uint8_t> nshas(ds.n_ns, 0);
+  for (uint32_t ns = 0; ns < prog->n_ns && ns < ds.n_ns; ns++) nshas[ns] = prog->ns_has_rel[ns] ? 1 : 0;
+  uint8_t *rf, *nh;
   int32_t* rr;
   RwNode* rw;
   int32_t* rc;
   if (alloc((void**)&rf, nt) || alloc((void**)&rr, nt * 4) || alloc((void**)&rw, (h_rw.size() + 1) * sizeof(RwNode)) ||
-      alloc((void**)&rc, (h_rwchild.size() + 1) * 4))
+      alloc((void**)&rc, (h_rwchild.size() + 1) * 4) || alloc((void**)&nh, ds.n_ns + 1))
     return -1;
+  HIPC(hipMemcpy(nh, nshas.data(), ds.n_ns, hipMemcpyHostToDevice));
+  ds.ns_has_rel = nh;
   HIPC(hipMemcpy(rf, h_relflags.data(), nt, hipMemcpyHostToDevice));
   HIPC(hipMemcpy(rr, h_relroot.data(), nt * 4, hipMemcpyHostToDevice));
   if (!h_rw.empty()) HIPC(hipMemcpy(rw, h_rw.data(), h_rw.size() * sizeof(RwNode), hipMemcpyHostToDevice));
