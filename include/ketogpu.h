@@ -139,17 +139,22 @@ typedef struct {
   uint32_t max_degree;      /* out-degree truncation (1e5)                        */
   float set_fraction;       /* fraction of group#member subjects that are subject sets */
   float doc_set_fraction;   /* fraction of doc#viewer subjects that are L0 groups  */
+  uint32_t preset;          /* 0 = C2/C4 rewrite-free; 1 = C3 (+ folders, OPL view/edit/share) */
 } kg_synth_params;
 
 /* ---- snapshot --------------------------------------------------------------------------- */
 int kg_snapshot_create(const kg_tuple* rows, size_t n, const kg_dict* dict, const kg_rewrite_prog* prog,
                        int device, kg_snapshot** out);
-int kg_snapshot_synthetic(const kg_synth_params* params, int device, kg_snapshot** out);
+/* prog: the namespace program compiled against the generator's ids (ns doc=0 group=1 user=2
+ * folder=3; rel "..."=0 viewer=1 member=2 editor=3 owner=4 parents=5 blocked=6 view=7 edit=8
+ * share=9), or NULL for none.  keto_amd/synth.py builds both. */
+int kg_snapshot_synthetic(const kg_synth_params* params, const kg_rewrite_prog* prog, int device,
+                          kg_snapshot** out);
 void kg_snapshot_destroy(kg_snapshot* s);
 /* sizes: [0]=nodes [1]=rows [2]=set edges [3]=device bytes */
 int kg_snapshot_info(const kg_snapshot* s, uint64_t* info4);
-/* Namespace / relation / object ids the synthetic generator uses:
- * ids6 = {ns_doc, ns_group, ns_user(unused for ids), rel_viewer, rel_member, n_objects}. */
+/* Synthetic layout: ids6 = {n_docs, n_groups, n_users, n_folders, user_obj0, folder_obj0}
+ * (doc d = object d, group g = object n_docs+g, user u = object user_obj0+u). */
 int kg_synth_ids(const kg_snapshot* s, uint32_t* ids6);
 /* Copies the snapshot's rows back (shard order) as kg_tuple, for oracle cross-checks.
  * rows may be NULL to query the count. */

@@ -61,7 +61,8 @@ class kg_tree_buf(C.Structure):
 
 class kg_synth_params(C.Structure):
     _fields_ = [("n_tuples_target", C.c_uint64), ("seed", C.c_uint64), ("n_layers", C.c_uint32),
-                ("max_degree", C.c_uint32), ("set_fraction", C.c_float), ("doc_set_fraction", C.c_float)]
+                ("max_degree", C.c_uint32), ("set_fraction", C.c_float), ("doc_set_fraction", C.c_float),
+                ("preset", C.c_uint32)]
 
 
 # every symbol include/ketogpu.h declares
@@ -87,7 +88,8 @@ def load(path: str = LIB_PATH):
     L = C.CDLL(path)
     vp, sz, i32, u32, u64 = C.c_void_p, C.c_size_t, C.c_int32, C.c_uint32, C.c_uint64
     L.kg_snapshot_create.argtypes = [vp, sz, C.POINTER(kg_dict), C.POINTER(kg_rewrite_prog), C.c_int, C.POINTER(vp)]
-    L.kg_snapshot_synthetic.argtypes = [C.POINTER(kg_synth_params), C.c_int, C.POINTER(vp)]
+    L.kg_snapshot_synthetic.argtypes = [C.POINTER(kg_synth_params), C.POINTER(kg_rewrite_prog), C.c_int,
+                                        C.POINTER(vp)]
     L.kg_snapshot_destroy.argtypes = [vp]
     L.kg_snapshot_destroy.restype = None
     L.kg_snapshot_info.argtypes = [vp, vp]

@@ -74,13 +74,14 @@ int kg_snapshot_create(const kg_tuple* rows, size_t n, const kg_dict* dict, cons
   KG_GUARD_END
 }
 
-int kg_snapshot_synthetic(const kg_synth_params* params, int device, kg_snapshot** out) {
+int kg_snapshot_synthetic(const kg_synth_params* params, const kg_rewrite_prog* prog, int device,
+                          kg_snapshot** out) {
   KG_GUARD_BEGIN
   if (!out || !params) return set_error(-2, "NULL argument");
   *out = nullptr;
   Snapshot* s = new Snapshot();
   int rc = s->init_device(device);
-  if (!rc) rc = s->create_synthetic(params);
+  if (!rc) rc = s->create_synthetic(params, prog);
   if (rc) {
     delete s;
     return rc;
@@ -107,12 +108,12 @@ int kg_synth_ids(const kg_snapshot* sp, uint32_t* ids6) {
   const Snapshot* s = reinterpret_cast<const Snapshot*>(sp);
   if (!s->is_synth) return set_error(-2, "not a synthetic snapshot");
   const kg::SynthLayout& L = s->synth;
-  ids6[0] = L.ns_doc;
-  ids6[1] = L.ns_group;
-  ids6[2] = L.ns_user;
-  ids6[3] = L.rel_viewer;
-  ids6[4] = L.rel_member;
-  ids6[5] = L.n_docs + L.n_groups + L.n_users;
+  ids6[0] = L.n_docs;
+  ids6[1] = L.n_groups;
+  ids6[2] = L.n_users;
+  ids6[3] = L.n_folders;
+  ids6[4] = L.user_obj0;
+  ids6[5] = L.folder_obj0;
   return 0;
 }
 

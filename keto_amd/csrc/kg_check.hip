@@ -271,8 +271,17 @@ __global__ void k_synth_queries(SynthLayout L, DevSnap s, uint64_t seed, uint32_
   uint32_t doc = (uint32_t)(shash(seed, i, 7) % L.n_docs);
   int32_t md = (int32_t)(shash(seed, i, 8) % 11);  // 0 (-> global) or 1..10
   uint32_t user = NONE;
+  uint32_t rel = L.rel_viewer, start = doc;
+  if (L.preset == 1) {  // C3: view / edit / share, walks start at viewer / editor / owner rows
+    const uint32_t k = (uint32_t)(shash(seed, i, 11) % 3);
+    rel = k == 0 ? L.rel_view : (k == 1 ? L.rel_edit : L.rel_share);
+    const uint32_t want = (uint32_t)(shash(seed, i, 12) % 3);
+    const uint32_t wrel = want == 0 ? L.rel_viewer : (want == 1 ? L.rel_editor : L.rel_owner);
+    for (uint32_t b = 0; b < L.n_blocks; b++)
+      if (L.b[b].ns == L.ns_doc && L.b[b].rel == wrel) start = L.b[b].node0 + doc;
+  }
   if ((i & 1) == 0) {  // positive: walk down random rows until a subject id
-    uint32_t cur = doc;
+    uint32_t cur = start;
     for (int step = 0; step < 16; step++) {
       uint64_t b = s.row_off[cur], e = s.row_off[cur + 1];
       if (e == b) break;
@@ -284,11 +293,11 @@ __global__ void k_synth_queries(SynthLayout L, DevSnap s, uint64_t seed, uint32_
       cur = sub & ~SET_BIT;
     }
   }
-  if (user == NONE) user = L.n_docs + L.n_groups + (uint32_t)(shash(seed, i, 10) % L.n_users);
+  if (user == NONE) user = L.user_obj0 + (uint32_t)(shash(seed, i, 10) % L.n_users);
   kg_query x;
   x.t.ns = L.ns_doc;
   x.t.obj = doc;
-  x.t.rel = L.rel_viewer;
+  x.t.rel = rel;
   x.t.sns = KG_SUBJECT_ID;
   x.t.sobj = user;
   x.t.srel = 0;

@@ -97,62 +97,4 @@ struct RQuery {
 };
 enum : uint32_t { ROUTE_DONE = 0, ROUTE_LIGHT = 1, ROUTE_GENERAL = 2 };
 
-// ---------------------------------------------------------------- synthetic graph
-// Deterministic "Drive-like" generator: pure function of (seed, index) so
-// the device build and kg_snapshot_export / the oracle see the same rows.
-struct SynthLayout {
-  uint64_t seed;
-  uint32_t n_docs, n_groups, n_users, n_layers, group_per_layer;
-  uint32_t max_degree;
-  float set_frac, doc_set_frac;
-  // ids
-  uint32_t ns_doc, ns_group, ns_user, rel_viewer, rel_member;
-};
-
-__host__ __device__ __forceinline__ double u01(uint64_t h) { return (double)(h >> 11) * (1.0 / 9007199254740992.0); }
-__host__ __device__ __forceinline__ uint64_t shash(uint64_t seed, uint64_t a, uint64_t b) {
-  return mix64(seed ^ mix64(a * 0x9E3779B97F4A7C15ull + b * 0xD1B54A32D192ED03ull + 0x632BE59BD9B4E019ull));
-}
-// truncated power-law out-degree: floor((1-u)^(-1/(s-1))), s = 2.1 (groups, mean ~7.5) / 2.3 (docs, ~3.9)
-__host__ __device__ __forceinline__ uint32_t synth_degree(const SynthLayout& L, uint32_t node) {
-  bool doc = node < L.n_docs;
-  double u = u01(shash(L.seed, node, 0xDE6));
-  double inv = doc ? (1.0 / 1.3) : (1.0 / 1.1);
-  double k = floor(pow(1.0 - u, -inv));
-  if (k < 1) k = 1;
-  if (k > L.max_degree) k = L.max_degree;
-  return (uint32_t)k;
-}
-// log-uniform rank (Zipf(~1) popularity) mapped through an affine permutation of [0, n)
-__host__ __device__ __forceinline__ uint32_t synth_pick(uint64_t h, uint32_t n) {
-  double u = u01(h);
-  uint64_t r = (uint64_t)floor(exp(u * log((double)n + 1.0))) - 1;
-  if (r >= n) r = n - 1;
-  return (uint32_t)((r * 2654435761ull + 12345ull) % n);
-}
-__host__ __device__ __forceinline__ uint32_t synth_layer(const SynthLayout& L, uint32_t node) {
-  return (node - L.n_docs) / L.group_per_layer;
-}
-// Subject of tuple e of node: tagged (SET_BIT | group node) or a user object id.
-__host__ __device__ __forceinline__ uint32_t synth_subject(const SynthLayout& L, uint32_t node, uint32_t e) {
-  uint64_t h1 = shash(L.seed, ((uint64_t)node << 20) ^ e, 1);
-  uint64_t h2 = shash(L.seed, ((uint64_t)node << 20) ^ e, 2);
-  bool doc = node < L.n_docs;
-  uint32_t layer = doc ? 0 : synth_layer(L, node);
-  bool set;
-  uint32_t tgt_layer;
-  if (doc) {
-    set = u01(h1) < L.doc_set_frac;
-    tgt_layer = 0;
-  } else {
-    set = (layer + 1 < L.n_layers) && u01(h1) < L.set_frac;
-    tgt_layer = layer + 1;
-  }
-  if (set) {
-    uint32_t g = synth_pick(h2, L.group_per_layer);
-    return SET_BIT | (L.n_docs + tgt_layer * L.group_per_layer + g);
-  }
-  return L.n_docs + L.n_groups + synth_pick(h2, L.n_users);  // user object id
-}
-
 }  // namespace kg

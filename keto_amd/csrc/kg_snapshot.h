@@ -7,6 +7,7 @@
 
 #include "../../include/ketogpu.h"
 #include "kg_internal.h"
+#include "kg_synth.h"
 
 namespace kg {
 
@@ -55,7 +56,7 @@ struct Snapshot {
   int init_device(int dev);
   int alloc(void** p, size_t bytes);
   int create_from_tuples(const kg_tuple* rows, size_t n, const kg_dict* dict, const kg_rewrite_prog* prog);
-  int create_synthetic(const kg_synth_params* p);
+  int create_synthetic(const kg_synth_params* p, const kg_rewrite_prog* prog);
   int upload_program(const kg_dict* dict, const kg_rewrite_prog* prog);
   int build_hash_tables();
   uint8_t host_relflag(uint32_t ns, uint32_t rel) const;

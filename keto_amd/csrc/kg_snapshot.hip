@@ -16,6 +16,7 @@
 
 #include "kg_internal.h"
 #include "kg_snapshot.h"
+#include "kg_synth.h"
 
 namespace kg {
 
@@ -62,12 +63,20 @@ __global__ void k_nmap_insert(uint64_t* keys, uint32_t* vals, uint64_t mask, con
 }
 
 // ------------------------------------------------------------------ synthetic generator kernels
+// set-adjacency keeps subject sets except "..." ones (engine.go:123-126), like the host path
+__device__ __forceinline__ bool synth_is_adj(const SynthLayout& L, uint32_t sub) {
+  if (!(sub & SET_BIT)) return false;
+  uint32_t ns, obj, rel;
+  synth_node(L, sub & ~SET_BIT, ns, obj, rel);
+  return rel != 0;  // rel 0 == "..."
+}
+
 __global__ void k_synth_degrees(SynthLayout L, uint32_t n_nodes, uint64_t* deg, uint64_t* setdeg) {
   uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
   if (v >= n_nodes) return;
   uint32_t d = synth_degree(L, v);
   uint32_t s = 0;
-  for (uint32_t e = 0; e < d; e++) s += (synth_subject(L, v, e) & SET_BIT) ? 1u : 0u;
+  for (uint32_t e = 0; e < d; e++) s += synth_is_adj(L, synth_subject(L, v, e)) ? 1u : 0u;
   deg[v] = d;
   setdeg[v] = s;
 }
@@ -81,12 +90,28 @@ __global__ void k_synth_fill(SynthLayout L, uint32_t n_nodes, const uint64_t* ro
   for (uint32_t e = 0; e < d; e++) {
     uint32_t s = synth_subject(L, v, e);
     row_subj[r + e] = s;
-    if (s & SET_BIT) adj[a++] = s & ~SET_BIT;
+    if (synth_is_adj(L, s)) adj[a++] = s & ~SET_BIT;
   }
-  bool doc = v < L.n_docs;
-  nd_ns[v] = doc ? L.ns_doc : L.ns_group;
-  nd_obj[v] = v;
-  nd_rel[v] = doc ? L.rel_viewer : L.rel_member;
+  synth_node(L, v, nd_ns[v], nd_obj[v], nd_rel[v]);
+}
+
+// Purity closure on the device (the host path does it on the host): seed with the relation flags,
+// then propagate "impure" backwards over set-adjacency until a fixed point.
+__global__ void k_flags_init(DevSnap s, uint8_t* flags) {
+  uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= s.n_nodes) return;
+  const uint8_t rf = relflag(s, s.nd_ns[v], s.nd_rel[v]);
+  flags[v] = rf ? (uint8_t)(NF_IMPURE | ((rf & 1) ? NF_REWRITE : 0) | ((rf & 2) ? NF_ERR : 0)) : 0;
+}
+__global__ void k_flags_propagate(DevSnap s, uint8_t* flags, uint32_t* changed) {
+  uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= s.n_nodes || (flags[v] & NF_IMPURE)) return;
+  for (uint64_t i = s.adj_off[v]; i < s.adj_off[v + 1]; i++)
+    if (flags[s.adj[i]] & NF_IMPURE) {
+      flags[v] |= NF_IMPURE;
+      *changed = 1;
+      return;
+    }
 }
 
 // ------------------------------------------------------------------ Snapshot
@@ -384,36 +409,23 @@ int Snapshot::create_from_tuples(const kg_tuple* rows, size_t n, const kg_dict* 
   return build_hash_tables();
 }
 
-int Snapshot::create_synthetic(const kg_synth_params* p) {
+int Snapshot::create_synthetic(const kg_synth_params* p, const kg_rewrite_prog* prog) {
   SynthLayout L{};
-  uint64_t T = p->n_tuples_target ? p->n_tuples_target : 10000000ull;
-  L.seed = p->seed;
-  L.n_layers = p->n_layers ? p->n_layers : 8;
-  L.n_docs = (uint32_t)std::max<uint64_t>(1, T / 8);
-  L.group_per_layer = (uint32_t)std::max<uint64_t>(1, T / 16 / L.n_layers);
-  L.n_groups = L.group_per_layer * L.n_layers;
-  L.n_users = (uint32_t)std::max<uint64_t>(1, T / 10);
-  L.max_degree = p->max_degree ? p->max_degree : 100000;
-  L.set_frac = p->set_fraction > 0 ? p->set_fraction : 0.25f;
-  L.doc_set_frac = p->doc_set_fraction > 0 ? p->doc_set_fraction : 0.5f;
-  // interned ids used by the generator: rel 0 is "..." (reserved like keto_amd.mapper.Interner)
-  L.ns_doc = 0;
-  L.ns_group = 1;
-  L.ns_user = 2;
-  L.rel_viewer = 1;
-  L.rel_member = 2;
-  if ((uint64_t)L.n_docs + L.n_groups + L.n_users >= 0x7FFFFFFFull) return set_error(-2, "synthetic graph too large");
+  const uint64_t T = p->n_tuples_target ? p->n_tuples_target : 10000000ull;
+  if (p->preset > 1) return set_error(-2, "unknown synthetic preset %u", p->preset);
+  if (!synth_make_layout(L, T, p->seed, p->n_layers, p->max_degree, p->set_fraction, p->doc_set_fraction, p->preset))
+    return set_error(-2, "synthetic graph too large");
   synth = L;
   is_synth = true;
   wildcard_rel = 0;
   ds.wildcard_rel = 0;
-  uint32_t nn = L.n_docs + L.n_groups;
+  const uint32_t nn = L.n_nodes;
   ds.n_nodes = nn;
   uint64_t *deg, *setdeg, *d_ro, *d_ao;
   if (alloc((void**)&d_ro, ((size_t)nn + 1) * 8) || alloc((void**)&d_ao, ((size_t)nn + 1) * 8)) return -1;
   HIPC(hipMalloc(&deg, ((size_t)nn + 1) * 8));
   HIPC(hipMalloc(&setdeg, ((size_t)nn + 1) * 8));
-  uint32_t grid = (nn + 255) / 256;
+  const uint32_t grid = (nn + 255) / 256;
   hipLaunchKernelGGL(k_synth_degrees, dim3(grid), dim3(256), 0, stream, L, nn, deg, setdeg);
   HIPC(hipGetLastError());
   HIPC(hipMemsetAsync(deg + nn, 0, 8, stream));
@@ -428,9 +440,9 @@ int Snapshot::create_synthetic(const kg_synth_params* p) {
   HIPC(hipMemcpyAsync(&tot[0], d_ro + nn, 8, hipMemcpyDeviceToHost, stream));
   HIPC(hipMemcpyAsync(&tot[1], d_ao + nn, 8, hipMemcpyDeviceToHost, stream));
   HIPC(hipStreamSynchronize(stream));
-  hipFree(tmp);
-  hipFree(deg);
-  hipFree(setdeg);
+  HIPC(hipFree(tmp));
+  HIPC(hipFree(deg));
+  HIPC(hipFree(setdeg));
   uint32_t *d_rs, *d_adj, *d_ns, *d_obj, *d_rel;
   if (alloc((void**)&d_rs, tot[0] * 4) || alloc((void**)&d_adj, tot[1] * 4) || alloc((void**)&d_ns, (size_t)nn * 4) ||
       alloc((void**)&d_obj, (size_t)nn * 4) || alloc((void**)&d_rel, (size_t)nn * 4))
@@ -445,11 +457,28 @@ int Snapshot::create_synthetic(const kg_synth_params* p) {
   ds.nd_ns = d_ns;
   ds.nd_obj = d_obj;
   ds.nd_rel = d_rel;
-  ds.nflags = nullptr;  // no rewrites configured: every node pure
+  ds.nflags = nullptr;
   h_row_off_last = tot[0];
   n_set_edges = tot[1];
-  kg_dict dict{3, 3, 0};
-  if (upload_program(&dict, nullptr)) return -1;
+  kg_dict dict{4, 10, 0};
+  if (upload_program(&dict, prog)) return -1;
+  if (has_program) {
+    uint8_t* f;
+    uint32_t* changed;
+    if (alloc((void**)&f, (size_t)nn + 1)) return -1;
+    HIPC(hipMalloc(&changed, 4));
+    hipLaunchKernelGGL(k_flags_init, dim3(grid), dim3(256), 0, stream, ds, f);
+    for (int it = 0; it < 1000; it++) {
+      uint32_t h = 0;
+      HIPC(hipMemsetAsync(changed, 0, 4, stream));
+      hipLaunchKernelGGL(k_flags_propagate, dim3(grid), dim3(256), 0, stream, ds, f, changed);
+      HIPC(hipMemcpyAsync(&h, changed, 4, hipMemcpyDeviceToHost, stream));
+      HIPC(hipStreamSynchronize(stream));
+      if (!h) break;
+    }
+    HIPC(hipFree(changed));
+    ds.nflags = f;
+  }
   return build_hash_tables();
 }
 

@@ -65,39 +65,47 @@ class Snapshot:
         L = _lib.load()
         self.interner = interner
         self.device = device
+        self.program = program
+        self._keep = []
         self._h = C.c_void_p()
         if _handle is not None:
             self._h = _handle
             return
         t = np.ascontiguousarray(tuples, dtype=np.uint32).reshape(-1, 6)
         d = _lib.kg_dict(interner.n_namespaces, interner.n_relations, interner.wildcard_rel)
-        prog_c = None
-        self._keep = []
-        if program is not None and not program.empty:
-            arrs = [np.ascontiguousarray(program.ns_has_rel, np.uint8), np.ascontiguousarray(program.rel_ns, np.uint32),
-                    np.ascontiguousarray(program.rel_rel, np.uint32), np.ascontiguousarray(program.rel_root, np.int32),
-                    np.ascontiguousarray(program.rw, np.int32).reshape(-1, 5),
-                    np.ascontiguousarray(program.child, np.int32)]
-            self._keep = arrs
-            prog_c = _lib.kg_rewrite_prog(len(arrs[0]), _ptr(arrs[0]), len(arrs[1]), _ptr(arrs[1]), _ptr(arrs[2]),
-                                          _ptr(arrs[3]), arrs[4].shape[0], _ptr(arrs[4]), len(arrs[5]), _ptr(arrs[5]))
+        prog_c = self._prog(program)
         rc = L.kg_snapshot_create(_ptr(t), t.shape[0], C.byref(d), C.byref(prog_c) if prog_c is not None else None,
                                   device, C.byref(self._h))
         _lib.check(rc, "kg_snapshot_create")
 
+    def _prog(self, program: Optional[Program]):
+        self._keep = []
+        if program is None or program.empty:
+            return None
+        arrs = [np.ascontiguousarray(program.ns_has_rel, np.uint8), np.ascontiguousarray(program.rel_ns, np.uint32),
+                np.ascontiguousarray(program.rel_rel, np.uint32), np.ascontiguousarray(program.rel_root, np.int32),
+                np.ascontiguousarray(program.rw, np.int32).reshape(-1, 5), np.ascontiguousarray(program.child, np.int32)]
+        self._keep = arrs
+        return _lib.kg_rewrite_prog(len(arrs[0]), _ptr(arrs[0]), len(arrs[1]), _ptr(arrs[1]), _ptr(arrs[2]),
+                                    _ptr(arrs[3]), arrs[4].shape[0], _ptr(arrs[4]), len(arrs[5]), _ptr(arrs[5]))
+
     @classmethod
     def synthetic(cls, n_tuples: int, seed: int = 20250131, device: int = 0, n_layers: int = 8,
-                  max_degree: int = 100000, set_fraction: float = 0.25, doc_set_fraction: float = 0.5) -> "Snapshot":
+                  max_degree: int = 100000, set_fraction: float = 0.25, doc_set_fraction: float = 0.5,
+                  preset: int = 0) -> "Snapshot":
+        """Device-generated Drive-like graph (keto_amd/csrc/kg_synth.h); preset 0 = C2/C4, 1 = C3."""
+        from . import synth
         L = _lib.load()
-        p = _lib.kg_synth_params(n_tuples, seed, n_layers, max_degree, set_fraction, doc_set_fraction)
+        it = synth.interner()
+        prog = synth.program(preset, it)
+        snap = cls(None, it, device=device, _handle=C.c_void_p())
+        p = _lib.kg_synth_params(n_tuples, seed, n_layers, max_degree, set_fraction, doc_set_fraction, preset)
+        prog_c = snap._prog(prog)
         h = C.c_void_p()
-        _lib.check(L.kg_snapshot_synthetic(C.byref(p), device, C.byref(h)), "kg_snapshot_synthetic")
-        it = Interner()  # ids used by the generator: ns doc=0 group=1 user=2; rel ...=0 viewer=1 member=2
-        for s in ("doc", "group", "user"):
-            it.ns_id(s)
-        for r in ("viewer", "member"):
-            it.rel_id(r)
-        snap = cls(None, it, device=device, _handle=h)
+        _lib.check(L.kg_snapshot_synthetic(C.byref(p), C.byref(prog_c) if prog_c is not None else None, device,
+                                           C.byref(h)), "kg_snapshot_synthetic")
+        snap._h = h
+        snap.program = prog
         return snap
 
     @property
@@ -112,7 +120,7 @@ class Snapshot:
     def synth_ids(self) -> dict:
         a = np.zeros(6, np.uint32)
         _lib.check(_lib.load().kg_synth_ids(self._h, _ptr(a)), "kg_synth_ids")
-        return dict(zip(["ns_doc", "ns_group", "ns_user", "rel_viewer", "rel_member", "n_objects"], map(int, a)))
+        return dict(zip(["n_docs", "n_groups", "n_users", "n_folders", "user_obj0", "folder_obj0"], map(int, a)))
 
     def export(self) -> np.ndarray:
         L = _lib.load()

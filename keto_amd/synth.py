@@ -1,0 +1,58 @@
+"""Synthetic Drive-like tuple graphs generated in HBM.
+
+The generator itself is device code (keto_amd/csrc/kg_synth.h); this module supplies the id
+scheme it assumes and, for preset C3, the OPL namespace program:
+
+    doc / folder:  view  = viewer | edit | parents.traverse(view)
+                   edit  = editor | owner | parents.traverse(edit)
+    doc:           share = view & !blocked
+"""
+from __future__ import annotations
+
+from typing import List
+
+from .mapper import Interner
+from .namespace import (ComputedSubjectSet, InvertResult, Namespace, Relation, SubjectSetRewrite,
+                        TupleToSubjectSet, compile_program)
+
+PRESET_C2 = 0
+PRESET_C3 = 1
+
+NAMESPACES = ["doc", "group", "user", "folder"]
+RELATIONS = ["viewer", "member", "editor", "owner", "parents", "blocked", "view", "edit", "share"]  # after "..."
+
+
+def interner() -> Interner:
+    it = Interner()  # rel 0 = "..."
+    for n in NAMESPACES:
+        it.ns_id(n)
+    for r in RELATIONS:
+        it.rel_id(r)
+    return it
+
+
+def c3_namespaces() -> List[Namespace]:
+    def view():
+        return SubjectSetRewrite([ComputedSubjectSet("viewer"), ComputedSubjectSet("edit"),
+                                  TupleToSubjectSet("parents", "view")])
+
+    def edit():
+        return SubjectSetRewrite([ComputedSubjectSet("editor"), ComputedSubjectSet("owner"),
+                                  TupleToSubjectSet("parents", "edit")])
+
+    plain = [Relation(r) for r in ("viewer", "editor", "owner", "parents")]
+    doc = Namespace("doc", plain + [Relation("blocked"), Relation("view", rewrite=view()),
+                                    Relation("edit", rewrite=edit()),
+                                    Relation("share", rewrite=SubjectSetRewrite(
+                                        [ComputedSubjectSet("view"), InvertResult(ComputedSubjectSet("blocked"))],
+                                        "and"))])
+    folder = Namespace("folder", [Relation(r) for r in ("viewer", "editor", "owner", "parents")] +
+                       [Relation("view", rewrite=view()), Relation("edit", rewrite=edit())])
+    group = Namespace("group", [Relation("member")])
+    return [doc, group, folder]
+
+
+def program(preset: int, it: Interner):
+    if preset == PRESET_C3:
+        return compile_program(c3_namespaces(), it)
+    return None
