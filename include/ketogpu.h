@@ -94,6 +94,7 @@ typedef struct {
   uint64_t direct_probes;
   uint64_t frontier_hbm;
   uint64_t n_light, n_heavy, n_general; /* queries finished per engine tier */
+  uint64_t n_medium;
   uint64_t light_rows_opened, light_edges_read, light_probes; /* k_light's share of the counters */
   double kernel_ms;                     /* device time of the whole batch (HIP events)  */
   double light_ms;                      /* device time of the k_light launch             */

@@ -31,12 +31,14 @@
 namespace kg {
 
 // Counters: [0] rows_opened [1] edges_read [2] probes [3] frontier_hbm [4] light [5] heavy [6] general
-enum { ST_ROWS = 0, ST_EDGES, ST_PROBES, ST_FHBM, ST_LIGHT, ST_HEAVY, ST_GENERAL, ST_LROWS, ST_LEDGES, ST_LPROBES, ST_N };
+enum { ST_ROWS = 0, ST_EDGES, ST_PROBES, ST_FHBM, ST_LIGHT, ST_HEAVY, ST_GENERAL, ST_LROWS, ST_LEDGES, ST_LPROBES,
+       ST_MEDIUM, ST_N };
 
 // Device-side counters/heads (zeroed per batch).
 struct Ctl {
   uint32_t light_count, gen_count, heavy_count, giant_count;
   uint32_t heavy_head, giant_head, gen_head, pad0;
+  uint32_t medium_count, medium_head, pad1[2];
   uint32_t heads[8 * 32];  // per-XCD dequeue heads, one 128-B line each
   unsigned long long st[ST_N];
   InterpCtl ic;
@@ -69,7 +71,12 @@ __global__ __launch_bounds__(256) void k_resolve(DevSnap s, const kg_query* __re
       bool impure = s.nflags && (s.nflags[node] & NF_IMPURE);
       route = impure ? ROUTE_GENERAL : ROUTE_LIGHT;
     }
-    rq[i] = RQuery{node, subj, d, route};
+    uint32_t rb = 0, rl = 0;
+    if (node != NONE) {
+      rb = (uint32_t)s.adj_off[node];
+      rl = (uint32_t)(s.adj_off[node + 1] - s.adj_off[node]);
+    }
+    rq[i] = RQuery{node, subj, d, route, rb, rl};
     if (route == ROUTE_DONE) {
       out[i] = KG_NOT_MEMBER;
       if (err) err[i] = KG_ERR_NONE;
@@ -94,12 +101,111 @@ __device__ __forceinline__ uint32_t dequeue(uint32_t* heads, uint32_t count, uin
   return NONE;
 }
 
+// Per-wave LDS of k_light: visited hash of EXPANDED nodes and the BFS list with inlined rows.
+// Nodes of the last level that can still be probed (rest depth 1) are probed on discovery and
+// never stored, so the list only holds nodes that will be expanded.
+constexpr int LX_VLOG2 = 9;
+constexpr int LX_VIS = 1 << LX_VLOG2;
+constexpr int LX_LIST = 256;  // hash load <= 0.5
+struct LightLds {
+  uint32_t vis[LX_VIS];
+  uint32_t node[LX_LIST];
+  uint32_t beg[LX_LIST];
+  uint32_t len[LX_LIST];
+  uint32_t pref[64];
+};
+
+__device__ __forceinline__ bool lx_insert(uint32_t* vis, uint32_t key) {
+  uint32_t h = (key * 2654435761u) >> (32 - LX_VLOG2);
+  for (;;) {
+    uint32_t old = atomicCAS(&vis[h], NONE, key);
+    if (old == NONE) return true;
+    if (old == key) return false;
+    h = (h + 1) & (LX_VIS - 1);
+  }
+}
+
+// One query, one wave.  Level k (rest depth d = D-k >= 2) holds the nodes to expand: every one of
+// them was already probed (checkDirect at d-1) when it was discovered.  Per level, ONE dependent
+// HBM round trip: the rows of the frontier (adjx, children + their own rows inline).
+// Returns BFS_M / BFS_N / BFS_OVERFLOW.
+__device__ __forceinline__ int light_query(const DevSnap& s, LightLds& L, const RQuery& q, BfsStats& bs) {
+  const int lane = lane_id();
+  for (int i = lane * 4; i < LX_VIS; i += 256) *reinterpret_cast<uint4*>(&L.vis[i]) = make_uint4(NONE, NONE, NONE, NONE);
+  // the root: checkDirect(D-1) (D >= 1 always)
+  bs.probes++;
+  bool hit = false;
+  if (lane == 0) hit = dset_probe(s, q.node, q.subj);
+  if (__shfl((int)hit, 0, 64)) return BFS_M;
+  if (q.depth < 2) return BFS_N;
+  __builtin_amdgcn_wave_barrier();
+  if (lane == 0) {
+    lx_insert(L.vis, q.node);
+    L.node[0] = q.node;
+    L.beg[0] = q.beg;
+    L.len[0] = q.len;
+  }
+  __builtin_amdgcn_wave_barrier();
+  uint32_t lvl_b = 0, lvl_e = 1, n = 1;
+  for (int k = 0; lvl_b < lvl_e; k++) {
+    const int d = q.depth - k;        // >= 2: expand; children sit at d-1 >= 1 and get probed
+    const bool keep = d - 1 >= 2;     // children will themselves be expanded -> list them
+    for (uint32_t base = lvl_b; base < lvl_e; base += 64) {
+      const uint32_t i = base + lane;
+      const bool valid = i < lvl_e;
+      const uint32_t b = valid ? L.beg[i] : 0u;
+      const uint32_t ln = valid ? L.len[i] : 0u;
+      bs.rows += __popcll(__ballot(valid));
+      uint32_t total;
+      const uint32_t excl = wave_excl_scan(ln, &total);
+      L.pref[lane] = excl;
+      __builtin_amdgcn_wave_barrier();
+      bs.edges += total;
+      for (uint32_t eb = 0; eb < total; eb += 64) {
+        const uint32_t e = eb + lane;
+        const bool act = e < total;
+        const int own = act ? owner_search(L.pref, 64, e) : 0;
+        const uint32_t ob = __shfl(b, own, 64);
+        AdjX x{NONE, 0, 0, 0};
+        if (act) x = s.adjx[ob + (e - L.pref[own])];
+        // checkDirect(d-2) of the child: once per node when it will be expanded (first-mark
+        // dedup), unconditionally on the last level (no visited state is kept for it)
+        bool h;
+        if (keep) {
+          const bool fresh = act && lx_insert(L.vis, x.node);
+          h = fresh && dset_probe(s, x.node, q.subj);
+          const uint64_t m = __ballot(fresh);
+          const uint32_t cnt = __popcll(m);
+          bs.probes += cnt;
+          if (n + cnt > LX_LIST) return __ballot(h) ? BFS_M : BFS_OVERFLOW;
+          if (fresh) {
+            const uint32_t at = n + lanes_below(m);
+            L.node[at] = x.node;
+            L.beg[at] = x.begin;
+            L.len[at] = x.len;
+          }
+          n += cnt;
+        } else {
+          h = act && dset_probe(s, x.node, q.subj);
+          bs.probes += __popcll(__ballot(act));
+        }
+        if (__ballot(h)) return BFS_M;
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+    lvl_b = lvl_e;
+    lvl_e = n;
+    if (!keep) break;
+  }
+  return BFS_N;
+}
+
 __global__ __launch_bounds__(256) void k_light(DevSnap s, const RQuery* __restrict__ rq,
                                                const uint32_t* __restrict__ light_list, uint8_t* __restrict__ out,
                                                uint32_t* __restrict__ err, uint32_t* heavy_list, Ctl* ctl) {
-  __shared__ WaveLds lds_all[LWAVES];
+  __shared__ LightLds lds_all[LWAVES];
   const int wave = threadIdx.x >> 6, lane = lane_id();
-  LdsStore st{&lds_all[wave]};
+  LightLds& L = lds_all[wave];
   const uint32_t count = ctl->light_count;
   const uint32_t head0 = blockIdx.x & 7;  // XCD label (speed only, never correctness)
   uint32_t head_sel = head0;
@@ -112,12 +218,10 @@ __global__ __launch_bounds__(256) void k_light(DevSnap s, const RQuery* __restri
     if (li == NONE) break;
     const uint32_t qi = light_list[li];
     const RQuery q = rq[qi];
-    st.reset();
-    uint32_t n = 0;
-    wave_add_roots(st, lane == 0, q.node, n);
-    const int r = wave_bfs_run(s, st, n, q.depth, q.subj, bs);
+    const int r = light_query(s, L, q, bs);
+    __builtin_amdgcn_wave_barrier();
     if (r == BFS_OVERFLOW) {
-      if (lane == 0) heavy_list[atomicAdd(&ctl->heavy_count, 1u)] = qi;
+      if (lane == 0) heavy_list[atomicAdd(&ctl->medium_count, 1u)] = qi;  // -> workgroup LDS tier
     } else if (lane == 0) {
       out[qi] = r == BFS_M ? KG_IS_MEMBER : KG_NOT_MEMBER;
       if (err) err[qi] = KG_ERR_NONE;
@@ -132,10 +236,11 @@ __global__ __launch_bounds__(256) void k_light(DevSnap s, const RQuery* __restri
   }
 }
 
-// ------------------------------------------------------------------ k_heavy
-// One 256-lane workgroup per overflowed query.  Per-slot HBM state: visited bitmap (n_nodes bits)
-// and the BFS list (cap entries).  A query whose list would exceed cap is forwarded to the
-// "giant" pass (same kernel, one slot, cap = n_nodes).
+// ------------------------------------------------------------------ workgroup tiers
+// Queries whose visited set outgrew one wave's LDS: one 256-lane workgroup per query, same BFS.
+//   k_wg<WgLds>  visited hash (8192 slots) + BFS list (4096) in LDS          ("medium")
+//   k_wg<WgHbm>  visited bitmap (n_nodes bits) + BFS list in HBM per slot     ("heavy", "giant")
+// Overflow forwards the query to the next tier's list.
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t* wsum, uint32_t* total) {
   const int lane = lane_id(), wave = threadIdx.x >> 6;
   uint32_t wt;
@@ -153,115 +258,175 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t* wsum, 
   return e + off;
 }
 
-__global__ __launch_bounds__(256) void k_heavy(DevSnap s, const RQuery* __restrict__ rq, const uint32_t* hlist,
-                                               const uint32_t* hcount_p, uint32_t* hhead, uint8_t* __restrict__ out,
-                                               uint32_t* __restrict__ err, uint32_t* bitmaps, uint64_t words_per_slot,
-                                               uint32_t* lists, uint64_t cap, uint32_t* giant_list,
-                                               uint32_t* giant_count, Ctl* ctl) {
-  __shared__ uint32_t sh_qi, sh_n, sh_hit, sh_over;
-  __shared__ uint32_t pref[256];
-  __shared__ uint32_t wsum[4];
-  const int tid = threadIdx.x;
-  uint32_t* bm = bitmaps + (uint64_t)blockIdx.x * words_per_slot;
-  uint32_t* list = lists + (uint64_t)blockIdx.x * cap;
-  unsigned long long st_rows = 0, st_edges = 0, st_probes = 0, st_fh = 0, st_done = 0;
-  const uint32_t hcount = *hcount_p;
-  for (;;) {
-    if (tid == 0) sh_qi = atomicAdd(hhead, 1u);
+struct WgLds {
+  static constexpr int VLOG2 = 13;
+  static constexpr uint32_t VSLOTS = 1u << VLOG2;
+  static constexpr uint32_t CAP = 4096;  // hash load <= 0.5
+  uint32_t* vis;
+  uint32_t* lst;
+  __device__ uint32_t* list() const { return lst; }
+  __device__ uint64_t cap() const { return CAP; }
+  __device__ void reset() {
+    for (uint32_t i = threadIdx.x * 4; i < VSLOTS; i += 1024)
+      *reinterpret_cast<uint4*>(&vis[i]) = make_uint4(NONE, NONE, NONE, NONE);
     __syncthreads();
-    const uint32_t hi = sh_qi;
-    if (hi >= hcount) break;
-    const uint32_t qi = hlist[hi];
-    const RQuery q = rq[qi];
-    if (tid == 0) {
-      list[0] = q.node;
-      atomicOr(&bm[q.node >> 5], 1u << (q.node & 31));
-      sh_n = 1;
-      sh_hit = 0;
-      sh_over = 0;
+  }
+  __device__ bool insert(uint32_t key) {
+    uint32_t h = (key * 2654435761u) >> (32 - VLOG2);
+    for (;;) {
+      uint32_t old = atomicCAS(&vis[h], NONE, key);
+      if (old == NONE) return true;
+      if (old == key) return false;
+      h = (h + 1) & (VSLOTS - 1);
+    }
+  }
+  __device__ void finish(uint32_t, bool) {}
+};
+
+struct WgHbm {
+  uint32_t* bm;
+  uint32_t* lst;
+  uint64_t capacity, words;
+  __device__ uint32_t* list() const { return lst; }
+  __device__ uint64_t cap() const { return capacity; }
+  __device__ void reset() {}
+  __device__ bool insert(uint32_t key) {
+    uint32_t bit = 1u << (key & 31);
+    return !(atomicOr(&bm[key >> 5], bit) & bit);
+  }
+  // every set bit in a touched word belongs to this query; after an overflow some set bits have no
+  // list entry, so the whole slot bitmap is cleared instead
+  __device__ void finish(uint32_t n, bool overflow) {
+    if (overflow) {
+      for (uint64_t w = threadIdx.x; w < words; w += 256) bm[w] = 0u;
+    } else {
+      for (uint32_t i = threadIdx.x; i < n; i += 256) atomicAnd(&bm[lst[i] >> 5], 0u);
     }
     __syncthreads();
-    uint32_t lvl_b = 0, lvl_e = 1;
-    for (int k = 0;; k++) {
-      const int d = q.depth - k;
-      if (d < 1) break;
-      const bool expand = d >= 2;
+  }
+};
+
+struct WgShared {
+  uint32_t qi, n, hit, over;
+  uint32_t pref[256];
+  uint32_t wsum[4];
+};
+
+template <class St>
+__device__ void wg_run(const DevSnap& s, St& st, WgShared& sh, const RQuery* __restrict__ rq, const uint32_t* qlist,
+                       uint32_t qcount, uint32_t* qhead, uint8_t* __restrict__ out, uint32_t* __restrict__ err,
+                       uint32_t* next_list, uint32_t* next_count, Ctl* ctl, int st_idx) {
+  const int tid = threadIdx.x;
+  uint32_t* list = st.list();
+  unsigned long long st_rows = 0, st_edges = 0, st_probes = 0, st_fh = 0, st_done = 0;
+  for (;;) {
+    if (tid == 0) sh.qi = atomicAdd(qhead, 1u);
+    __syncthreads();
+    const uint32_t hi = sh.qi;
+    if (hi >= qcount) break;
+    const uint32_t qi = qlist[hi];
+    const RQuery q = rq[qi];
+    st.reset();
+    if (tid == 0) {
+      st.insert(q.node);
+      list[0] = q.node;
+      sh.n = 1;
+      sh.over = 0;
+      sh.hit = dset_probe(s, q.node, q.subj) ? 1u : 0u;  // root: checkDirect(D-1)
+      st_probes++;
+    }
+    __syncthreads();
+    // The list holds nodes to EXPAND (rest depth >= 2); children are probed when discovered and
+    // kept only if they will be expanded themselves (same scheme as k_light).
+    uint32_t lvl_b = 0, lvl_e = (q.depth >= 2 && !sh.hit) ? 1u : 0u;
+    for (int k = 0; lvl_b < lvl_e; k++) {
+      const int d = q.depth - k;     // >= 2
+      const bool keep = d - 1 >= 2;
       for (uint32_t base = lvl_b; base < lvl_e; base += 256) {
         const uint32_t i = base + tid;
         const bool valid = i < lvl_e;
         const uint32_t node = valid ? list[i] : 0;
         uint64_t rb = 0, re = 0;
-        if (valid && expand) {
+        if (valid) {
           rb = s.adj_off[node];
           re = s.adj_off[node + 1];
-        }
-        if (valid && dset_probe(s, node, q.subj)) sh_hit = 1;
-        if (tid == 0) {
-          uint32_t nv = min(256u, lvl_e - base);
-          st_probes += nv;
-          st_fh += nv;
-          if (expand) st_rows += nv;
+          st_rows++;
+          st_fh++;
         }
         uint32_t total;
-        const uint32_t excl = block_excl_scan(expand ? (uint32_t)(re - rb) : 0u, wsum, &total);
-        pref[tid] = excl;
+        const uint32_t excl = block_excl_scan((uint32_t)(re - rb), sh.wsum, &total);
+        sh.pref[tid] = excl;
         __syncthreads();
-        if (sh_hit) break;
         if (tid == 0) st_edges += total;
         for (uint32_t eb = 0; eb < total; eb += 256) {
           const uint32_t e = eb + tid;
           if (e < total) {
-            int own = owner_search(pref, 256, e);
-            uint64_t src = 0;
-            // rb of the owner: recompute from its node (owner lane's rb is in another wave)
-            uint32_t onode = list[base + own];
-            src = s.adj_off[onode] + (e - pref[own]);
-            uint32_t child = s.adj[src];
-            uint32_t bit = 1u << (child & 31);
-            uint32_t old = atomicOr(&bm[child >> 5], bit);
-            if (!(old & bit)) {
-              uint32_t pos = atomicAdd(&sh_n, 1u);
-              if (pos < cap) list[pos] = child;
-              else sh_over = 1;
+            const int own = owner_search(sh.pref, 256, e);
+            const uint32_t onode = list[base + own];  // the owner's row start lives in another wave
+            const uint32_t child = s.adj[s.adj_off[onode] + (e - sh.pref[own])];
+            if (keep) {
+              if (st.insert(child)) {
+                st_probes++;
+                if (dset_probe(s, child, q.subj)) sh.hit = 1;
+                const uint32_t pos = atomicAdd(&sh.n, 1u);
+                if (pos < st.cap()) list[pos] = child;
+                else sh.over = 1;
+              }
+            } else {
+              st_probes++;
+              if (dset_probe(s, child, q.subj)) sh.hit = 1;
             }
           }
         }
         __syncthreads();
-        if (sh_over) break;
+        if (sh.hit || sh.over) break;
       }
       __syncthreads();
-      if (sh_hit || sh_over) break;
+      if (sh.hit || sh.over || !keep) break;
       lvl_b = lvl_e;
-      lvl_e = sh_n;
-      if (lvl_b == lvl_e) break;
+      lvl_e = sh.n;
     }
     __syncthreads();
-    const uint32_t n_list = (uint32_t)min((uint64_t)sh_n, cap);
+    const bool overflow = sh.over && !sh.hit;
     if (tid == 0) {
-      if (sh_over && !sh_hit) {
-        giant_list[atomicAdd(giant_count, 1u)] = qi;
+      if (overflow) {
+        next_list[atomicAdd(next_count, 1u)] = qi;
       } else {
-        out[qi] = sh_hit ? KG_IS_MEMBER : KG_NOT_MEMBER;
+        out[qi] = sh.hit ? KG_IS_MEMBER : KG_NOT_MEMBER;
         if (err) err[qi] = KG_ERR_NONE;
         st_done++;
       }
     }
-    // clear this query's bits (every set bit in a touched word belongs to this query); after an
-    // overflow some set bits have no list entry, so the whole slot bitmap is cleared instead
-    if (sh_over) {
-      for (uint64_t w = tid; w < words_per_slot; w += 256) bm[w] = 0u;
-    } else {
-      for (uint32_t i = tid; i < n_list; i += 256) atomicAnd(&bm[list[i] >> 5], 0u);
-    }
-    __syncthreads();
+    st.finish((uint32_t)min((uint64_t)sh.n, st.cap()), sh.over != 0);
   }
+  atomicAdd(&ctl->st[ST_ROWS], st_rows);  // per-thread counters (rows/probes counted per lane)
+  atomicAdd(&ctl->st[ST_PROBES], st_probes);
+  if (st_idx == ST_HEAVY) atomicAdd(&ctl->st[ST_FHBM], st_fh);
   if (tid == 0) {
-    atomicAdd(&ctl->st[ST_ROWS], st_rows);
     atomicAdd(&ctl->st[ST_EDGES], st_edges);
-    atomicAdd(&ctl->st[ST_PROBES], st_probes);
-    atomicAdd(&ctl->st[ST_FHBM], st_fh);
-    atomicAdd(&ctl->st[ST_HEAVY], st_done);
+    atomicAdd(&ctl->st[st_idx], st_done);
   }
+}
+
+__global__ __launch_bounds__(256) void k_medium(DevSnap s, const RQuery* __restrict__ rq, const uint32_t* qlist,
+                                                const uint32_t* qcount_p, uint32_t* qhead, uint8_t* __restrict__ out,
+                                                uint32_t* __restrict__ err, uint32_t* next_list, uint32_t* next_count,
+                                                Ctl* ctl) {
+  __shared__ uint32_t vis[WgLds::VSLOTS];
+  __shared__ uint32_t lst[WgLds::CAP];
+  __shared__ WgShared sh;
+  WgLds st{vis, lst};
+  wg_run(s, st, sh, rq, qlist, *qcount_p, qhead, out, err, next_list, next_count, ctl, ST_MEDIUM);
+}
+
+__global__ __launch_bounds__(256) void k_heavy(DevSnap s, const RQuery* __restrict__ rq, const uint32_t* qlist,
+                                               const uint32_t* qcount_p, uint32_t* qhead, uint8_t* __restrict__ out,
+                                               uint32_t* __restrict__ err, uint32_t* bitmaps, uint64_t words_per_slot,
+                                               uint32_t* lists, uint64_t cap, uint32_t* next_list,
+                                               uint32_t* next_count, Ctl* ctl) {
+  __shared__ WgShared sh;
+  WgHbm st{bitmaps + (uint64_t)blockIdx.x * words_per_slot, lists + (uint64_t)blockIdx.x * cap, cap, words_per_slot};
+  wg_run(s, st, sh, rq, qlist, *qcount_p, qhead, out, err, next_list, next_count, ctl, ST_HEAVY);
 }
 
 // ------------------------------------------------------------------ synthetic queries
@@ -325,11 +490,11 @@ int check_batch_device(Snapshot* s, const kg_query* d_q, size_t n, int32_t globa
   if (n > 0x7FFFFFFFull) return set_error(-2, "batch too large");
   HIPC(hipSetDevice(s->device));
   if (!stream) stream = s->stream;
-  // scratch: rq[n] | light[n] | gen[n] | heavy[n] | giant[n] | p2[n] | Ctl
+  // scratch: rq[n] | light[n] | gen[n] | medium[n] | heavy[n] | giant[n] | p2[n] | Ctl
   size_t off_rq = 0, off_light = align_up(off_rq + n * sizeof(RQuery)), off_gen = align_up(off_light + n * 4),
-         off_heavy = align_up(off_gen + n * 4), off_giant = align_up(off_heavy + n * 4),
-         off_p2 = align_up(off_giant + n * 4), off_ctl = align_up(off_p2 + n * 4),
-         total = align_up(off_ctl + sizeof(Ctl));
+         off_med = align_up(off_gen + n * 4), off_heavy = align_up(off_med + n * 4),
+         off_giant = align_up(off_heavy + n * 4), off_p2 = align_up(off_giant + n * 4),
+         off_ctl = align_up(off_p2 + n * 4), total = align_up(off_ctl + sizeof(Ctl));
   if (total > s->scratch_bytes) {
     if (s->scratch) hipFree(s->scratch);
     s->scratch = nullptr;
@@ -341,6 +506,7 @@ int check_batch_device(Snapshot* s, const kg_query* d_q, size_t n, int32_t globa
   RQuery* rq = (RQuery*)(base + off_rq);
   uint32_t* light = (uint32_t*)(base + off_light);
   uint32_t* gen = (uint32_t*)(base + off_gen);
+  uint32_t* medium = (uint32_t*)(base + off_med);
   uint32_t* heavy = (uint32_t*)(base + off_heavy);
   uint32_t* giant = (uint32_t*)(base + off_giant);
   uint32_t* p2 = (uint32_t*)(base + off_p2);
@@ -378,11 +544,15 @@ int check_batch_device(Snapshot* s, const kg_query* d_q, size_t n, int32_t globa
     hipLaunchKernelGGL(k_resolve, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, stream, s->ds, d_q, (uint32_t)n,
                        global_max_depth, rq, d_out, d_err, light, gen, ctl);
     HIPC(hipGetLastError());
-    const uint32_t light_grid = (uint32_t)std::min<uint64_t>((uint64_t)s->n_cu * 6, (n + 3) / 4 + 8);
+    // 7 workgroups of 4 waves per CU: LDS 21 KiB/WG and 71 VGPRs both allow 28 waves/CU
+    const uint32_t light_grid = (uint32_t)std::min<uint64_t>((uint64_t)s->n_cu * 7, (n + 3) / 4 + 8);
     if (stats) HIPC(hipEventRecord(l0, stream));
-    hipLaunchKernelGGL(k_light, dim3(light_grid), dim3(256), 0, stream, s->ds, rq, light, d_out, d_err, heavy, ctl);
+    hipLaunchKernelGGL(k_light, dim3(light_grid), dim3(256), 0, stream, s->ds, rq, light, d_out, d_err, medium, ctl);
     HIPC(hipGetLastError());
     if (stats) HIPC(hipEventRecord(l1, stream));
+    hipLaunchKernelGGL(k_medium, dim3((uint32_t)s->n_cu * 3), dim3(256), 0, stream, s->ds, rq, medium,
+                       &ctl->medium_count, &ctl->medium_head, d_out, d_err, heavy, &ctl->heavy_count, ctl);
+    HIPC(hipGetLastError());
     hipLaunchKernelGGL(k_heavy, dim3(H), dim3(256), 0, stream, s->ds, rq, heavy, &ctl->heavy_count, &ctl->heavy_head,
                        d_out, d_err, hb, words, hl, cap_h, giant, &ctl->giant_count, ctl);
     HIPC(hipGetLastError());
@@ -422,6 +592,7 @@ int check_batch_device(Snapshot* s, const kg_query* d_q, size_t n, int32_t globa
     stats->light_ms = lms;
     stats->frontier_hbm = h.st[ST_FHBM];
     stats->n_light = h.st[ST_LIGHT];
+    stats->n_medium = h.st[ST_MEDIUM];
     stats->n_heavy = h.st[ST_HEAVY];
     stats->n_general = h.st[ST_GENERAL];
     stats->kernel_ms = ms;

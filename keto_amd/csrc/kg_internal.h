@@ -52,12 +52,19 @@ struct RwNode {
 };
 enum { RW_OR = 0, RW_AND = 1, RW_COMPUTED = 2, RW_TTU = 3, RW_NOT = 4 };
 
+// Set-adjacency edge with the child's own row inlined (begin/len into adj/adjx), so a BFS level
+// needs one dependent HBM round trip instead of two (no adj_off lookup per discovered node).
+struct AdjX {
+  uint32_t node, begin, len, pad;
+};
+
 // Everything a kernel needs, passed by value.
 struct DevSnap {
   uint32_t n_nodes;
   uint32_t wildcard_rel;
   const uint64_t* adj_off;
   const uint32_t* adj;
+  const AdjX* adjx;  // parallel to adj
   const uint64_t* row_off;
   const uint32_t* row_subj;
   const uint64_t* dset;
@@ -94,6 +101,7 @@ struct RQuery {
   uint32_t subj;   // tagged subject or NONE
   int32_t depth;   // clamped rest depth
   uint32_t route;  // ROUTE_*
+  uint32_t beg, len;  // root's set-adjacency row
 };
 enum : uint32_t { ROUTE_DONE = 0, ROUTE_LIGHT = 1, ROUTE_GENERAL = 2 };
 

@@ -62,6 +62,15 @@ __global__ void k_nmap_insert(uint64_t* keys, uint32_t* vals, uint64_t mask, con
   }
 }
 
+__global__ void k_build_adjx(const uint32_t* adj, const uint64_t* adj_off, uint64_t n_edges, AdjX* adjx) {
+  for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < n_edges;
+       e += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t c = adj[e];
+    const uint64_t b = adj_off[c], x = adj_off[c + 1];
+    adjx[e] = AdjX{c, (uint32_t)b, (uint32_t)(x - b), 0u};
+  }
+}
+
 // ------------------------------------------------------------------ synthetic generator kernels
 // set-adjacency keeps subject sets except "..." ones (engine.go:123-126), like the host path
 __device__ __forceinline__ bool synth_is_adj(const SynthLayout& L, uint32_t sub) {
@@ -153,6 +162,15 @@ int Snapshot::init_device(int dev) {
 
 // Hash tables: dset sized for load <= 0.5 over 8-key buckets; nmap for load <= 0.5.
 int Snapshot::build_hash_tables() {
+  // inlined child rows for the BFS (indices are u32: up to 2^32-1 set edges per snapshot)
+  if (n_set_edges >= 0xFFFFFFFFull) return set_error(KG_ERR_RESOURCE_CODE, "more than 2^32-1 subject-set edges");
+  AdjX* adjx = nullptr;
+  if (alloc((void**)&adjx, (n_set_edges + 1) * sizeof(AdjX))) return -1;
+  if (n_set_edges) {
+    hipLaunchKernelGGL(k_build_adjx, dim3(2048), dim3(256), 0, stream, ds.adj, ds.adj_off, n_set_edges, adjx);
+    HIPC(hipGetLastError());
+  }
+  ds.adjx = adjx;
   uint64_t n_rows = h_row_off_last;
   uint64_t buckets = pow2_at_least(std::max<uint64_t>(1, (n_rows * 2 + DSET_BUCKET - 1) / DSET_BUCKET));
   uint64_t* dset = nullptr;

@@ -213,3 +213,25 @@ def test_relation_not_found_and_cycle():
     assert r.err is not None and r.err.code == 3
     r = e.check_relation_tuple(RelationTuple.from_string("d:x#nope@u"), 0)
     assert r.err is not None and r.err.code == 1
+
+
+@pytest.mark.parametrize("n_tuples,gmax", [(150_000, 10), (250_000, 5)])
+def test_synthetic_c3_rewrites_vs_oracle(n_tuples, gmax):
+    """Config C3: the Drive-like graph + folder forest + OPL view/edit/share (interpreter path)."""
+    torch = _torch()
+    from keto_amd import _lib
+    snap = Snapshot.synthetic(n_tuples, seed=20250131, preset=1)
+    n = 6000
+    dq = torch.empty((n, 7), dtype=torch.int32, device="cuda")
+    _lib.check(_lib.load().kg_synth_queries(snap.handle, 11, n, dq.data_ptr()), "kg_synth_queries")
+    e = Engine(snap, Config(gmax))
+    q = dq.cpu().numpy().view(np.uint32)
+    out, err = e.batch_check_ids(q, with_stats=True)
+    assert e.last_stats["n_general"] == n
+    oracle = Oracle(snap.export(), 0, snap.program)
+    exp, oerr, _ = oracle.check_batch(q[:, :6], q[:, 6].view(np.int32), gmax, POLICY_CANONICAL, nthreads=8)
+    bad = np.nonzero((out != exp) | (err.astype(np.int64) != oerr))[0]
+    assert bad.size == 0, [(q[i].tolist(), int(out[i]), int(exp[i]), int(err[i]), int(oerr[i])) for i in bad[:8]]
+    assert 0.05 < (out == 1).mean() < 0.95 and (out == 2).sum() == 0
+    dfs, _, _ = oracle.check_batch(q[:, :6], q[:, 6].view(np.int32), gmax, POLICY_DFS, nthreads=8)
+    assert (dfs == exp).all()  # rewrites sit outside every visited scope: schedule-invariant
