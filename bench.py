@@ -40,7 +40,22 @@ def parse():
     ap.add_argument("--seed", type=int, default=20250131)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline time budget (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--preset", type=int, default=0,
+                    help="0 = C2/C4 rewrite-free (headline); 1 = C3 (OPL view/edit/share via the rewrite interpreter)")
     return ap.parse_args()
+
+
+def aggregate(dist, elapsed: float, edges: float, device=None):
+    """Whole-job numbers over ranks: elapsed = MAX over ranks (the job ends with its slowest
+    rank), edges = SUM.  Replicas exchange nothing else."""
+    if dist is None:
+        return elapsed, edges
+    import torch
+    t = torch.tensor([elapsed, -edges], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    e = torch.tensor([edges], dtype=torch.float64, device=device)
+    dist.all_reduce(e, op=dist.ReduceOp.SUM)
+    return float(t[0].item()), float(e[0].item())
 
 
 def main():
@@ -61,7 +76,7 @@ def main():
     L = _lib.load()
 
     t_build = time.time()
-    snap = Snapshot.synthetic(int(a.tuples), seed=a.seed, device=local)
+    snap = Snapshot.synthetic(int(a.tuples), seed=a.seed, device=local, preset=a.preset)
     info = snap.info()
     t_build = time.time() - t_build
 
@@ -95,19 +110,10 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-
     res = dout.cpu().numpy()
     errs = derr.cpu().numpy()
     assert (errs == 0).all() and (res <= 1).all(), "unexpected errors in the synthetic batch"
-    edges = sum(s.edges_read for s in stats)
-    if dist:
-        t = torch.tensor([float(edges)], dtype=torch.float64, device=f"cuda:{local}")
-        dist.all_reduce(t)
-        edges = t.item()
+    elapsed, edges = aggregate(dist, elapsed, float(sum(s.edges_read for s in stats)), f"cuda:{local}")
     l_bytes = np.array([8 * s.light_rows_opened + 4 * s.light_edges_read + 16 * s.light_probes for s in stats], float)
     l_ms = np.array([s.light_ms for s in stats], float)
     achieved = float(l_bytes.mean() / (l_ms.mean() * 1e-3) / 1e9)
@@ -127,8 +133,9 @@ def main():
         "vs_baseline": None,
         "dtype": "u32",
         "data": "synthetic (device-generated Drive-like tuple graph, seed %d)" % a.seed,
-        "config": {"workload": "C2/C4 generator @ %.3g tuples, %d checks/step/GPU, max_read_depth %d"
-                               % (a.tuples, B, a.global_depth),
+        "config": {"workload": "%s generator @ %.3g tuples, %d checks/step/GPU, max_read_depth %d"
+                               % ("C2/C4" if a.preset == 0 else "C3 (OPL view/edit/share)", a.tuples, B,
+                                  a.global_depth),
                    "tuples": info["rows"], "nodes": info["nodes"], "set_edges": info["set_edges"],
                    "batch_per_gpu": B, "global_max_read_depth": a.global_depth, "parallelism": f"replica{world}"},
         "gteps": edges / elapsed / 1e9,

@@ -22,19 +22,20 @@ __device__ __forceinline__ uint32_t nmap_find(const DevSnap& s, uint32_t ns, uin
   if (ns >= 0xFFFFu || rel >= 0xFFFFu || obj >= 0x7FFFFFFFu) return NONE;
   uint64_t key = nmap_key(ns, rel, obj);
   uint64_t i = mix64(key) & s.nmap_mask;
-  for (;;) {
+  for (uint64_t p = 0; p <= s.nmap_mask; p++) {  // load <= 0.5: ends at an empty slot long before
     uint64_t k = s.nmap_keys[i];
     if (k == key) return s.nmap_vals[i];
     if (k == EMPTY64) return NONE;
     i = (i + 1) & s.nmap_mask;
   }
+  return NONE;
 }
 
 // checkDirect: does the exact tuple (node, subject) exist?  One 64-B bucket per probe.
 __device__ __forceinline__ bool dset_probe(const DevSnap& s, uint32_t node, uint32_t subj) {
   uint64_t key = dset_key(node, subj);
   uint64_t b = mix64(key) & s.dset_mask;
-  for (;;) {
+  for (uint64_t n = 0; n <= s.dset_mask; n++) {  // load <= 0.5: nearly always the first bucket
     const ulonglong2* p = reinterpret_cast<const ulonglong2*>(s.dset + b * DSET_BUCKET);
     ulonglong2 a0 = p[0], a1 = p[1], a2 = p[2], a3 = p[3];
     if (a0.x == key || a0.y == key || a1.x == key || a1.y == key || a2.x == key || a2.y == key || a3.x == key ||
@@ -43,6 +44,7 @@ __device__ __forceinline__ bool dset_probe(const DevSnap& s, uint32_t node, uint
     if (a3.y == EMPTY64) return false;  // buckets fill front to back
     b = (b + 1) & s.dset_mask;
   }
+  return false;
 }
 
 __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t x, uint32_t* total) {
@@ -107,14 +109,17 @@ struct LdsStore {
     for (int i = lane * 4; i < VIS; i += 256) *reinterpret_cast<uint4*>(&L->vis[i]) = make_uint4(NONE, NONE, NONE, NONE);
     __builtin_amdgcn_wave_barrier();
   }
+  // Bounded probe: callers check the list cap after every 64-wide step, so the table never holds
+  // more than LIST + 64 < VIS keys; the bound only guarantees termination.
   __device__ bool insert(uint32_t key) {
     uint32_t h = (key * 2654435761u) >> (32 - VIS_LOG2);
-    for (;;) {
+    for (int p = 0; p < VIS; p++) {
       uint32_t old = atomicCAS(&L->vis[h], NONE, key);
       if (old == NONE) return true;
       if (old == key) return false;
       h = (h + 1) & (VIS - 1);
     }
+    return true;
   }
   __device__ void sync() { __builtin_amdgcn_wave_barrier(); }
   __device__ void finish(uint32_t) {}

@@ -115,14 +115,18 @@ struct LightLds {
   uint32_t pref[64];
 };
 
+// Bounded LDS hash insert. The list cap (256) keeps the table <= ~63% full (each chunk adds at
+// most 64 before the cap check), so the bound is a safety net: a full table reports "fresh" and
+// the caller's cap check turns the query into an overflow instead of spinning.
 __device__ __forceinline__ bool lx_insert(uint32_t* vis, uint32_t key) {
   uint32_t h = (key * 2654435761u) >> (32 - LX_VLOG2);
-  for (;;) {
+  for (int p = 0; p < LX_VIS; p++) {
     uint32_t old = atomicCAS(&vis[h], NONE, key);
     if (old == NONE) return true;
     if (old == key) return false;
     h = (h + 1) & (LX_VIS - 1);
   }
+  return true;
 }
 
 // One query, one wave.  Level k (rest depth d = D-k >= 2) holds the nodes to expand: every one of
@@ -271,14 +275,16 @@ struct WgLds {
       *reinterpret_cast<uint4*>(&vis[i]) = make_uint4(NONE, NONE, NONE, NONE);
     __syncthreads();
   }
-  __device__ bool insert(uint32_t key) {
+  // 1 = inserted, 0 = already present, -1 = table full (bounded: never spins)
+  __device__ int insert(uint32_t key) {
     uint32_t h = (key * 2654435761u) >> (32 - VLOG2);
-    for (;;) {
+    for (uint32_t p = 0; p < VSLOTS; p++) {
       uint32_t old = atomicCAS(&vis[h], NONE, key);
-      if (old == NONE) return true;
-      if (old == key) return false;
+      if (old == NONE) return 1;
+      if (old == key) return 0;
       h = (h + 1) & (VSLOTS - 1);
     }
+    return -1;
   }
   __device__ void finish(uint32_t, bool) {}
 };
@@ -290,9 +296,9 @@ struct WgHbm {
   __device__ uint32_t* list() const { return lst; }
   __device__ uint64_t cap() const { return capacity; }
   __device__ void reset() {}
-  __device__ bool insert(uint32_t key) {
+  __device__ int insert(uint32_t key) {
     uint32_t bit = 1u << (key & 31);
-    return !(atomicOr(&bm[key >> 5], bit) & bit);
+    return (atomicOr(&bm[key >> 5], bit) & bit) ? 0 : 1;
   }
   // every set bit in a touched word belongs to this query; after an overflow some set bits have no
   // list entry, so the whole slot bitmap is cleared instead
@@ -328,7 +334,7 @@ __device__ void wg_run(const DevSnap& s, St& st, WgShared& sh, const RQuery* __r
     const RQuery q = rq[qi];
     st.reset();
     if (tid == 0) {
-      st.insert(q.node);
+      (void)st.insert(q.node);
       list[0] = q.node;
       sh.n = 1;
       sh.over = 0;
@@ -359,13 +365,19 @@ __device__ void wg_run(const DevSnap& s, St& st, WgShared& sh, const RQuery* __r
         __syncthreads();
         if (tid == 0) st_edges += total;
         for (uint32_t eb = 0; eb < total; eb += 256) {
+          if (*(volatile uint32_t*)&sh.over || *(volatile uint32_t*)&sh.hit) break;  // decided: stop early
           const uint32_t e = eb + tid;
           if (e < total) {
             const int own = owner_search(sh.pref, 256, e);
             const uint32_t onode = list[base + own];  // the owner's row start lives in another wave
             const uint32_t child = s.adj[s.adj_off[onode] + (e - sh.pref[own])];
             if (keep) {
-              if (st.insert(child)) {
+              // capacity first: once the list is full nothing more is inserted (a full LDS hash
+              // would otherwise make the insert probe forever)
+              const int ins = (*(volatile uint32_t*)&sh.n < st.cap()) ? st.insert(child) : -1;
+              if (ins < 0) {
+                sh.over = 1;
+              } else if (ins > 0) {
                 st_probes++;
                 if (dset_probe(s, child, q.subj)) sh.hit = 1;
                 const uint32_t pos = atomicAdd(&sh.n, 1u);

@@ -100,7 +100,13 @@ __device__ int interp_query(const DevSnap& s, Store& st, const kg_query& oq, con
   // multi-root BFS over pure roots at rest depth d0
   auto bfs = [&](uint32_t n_roots, int d0) -> int { return wave_bfs_run(s, st, n_roots, d0, subj, bs); };
 
-  for (;;) {
+  // every step pushes a frame (bounded by STACK_CAP), advances a cursor or returns a result;
+  // the step cap is a termination guarantee against engine bugs, never reached on valid input
+  for (uint64_t steps = 0;; steps++) {
+    if (steps > (1ull << 34)) {
+      err = KG_ERR_RESOURCE;
+      return R_ERR;
+    }
     bool done = false;
     uint32_t res = R_N;
     switch (F.kind) {

@@ -28,7 +28,7 @@ __global__ void k_dset_insert_rows(uint64_t* dset, uint64_t mask, const uint64_t
   for (uint64_t i = row_off[v]; i < row_off[v + 1]; i++) {
     uint64_t key = dset_key(v, row_subj[i]);
     uint64_t b = mix64(key) & mask;
-    for (;;) {
+    for (uint64_t n = 0; n <= mask; n++) {  // sized for load <= 0.5: always finds room
       uint64_t* bucket = dset + b * DSET_BUCKET;
       bool done = false;
       for (int s = 0; s < DSET_BUCKET; s++) {
@@ -51,7 +51,7 @@ __global__ void k_nmap_insert(uint64_t* keys, uint32_t* vals, uint64_t mask, con
   if (v >= n_nodes) return;
   uint64_t key = nmap_key(nd_ns[v], nd_rel[v], nd_obj[v]);
   uint64_t i = mix64(key) & mask;
-  for (;;) {
+  for (uint64_t n = 0; n <= mask; n++) {  // sized for load <= 0.5: always finds room
     unsigned long long old =
         atomicCAS((unsigned long long*)&keys[i], (unsigned long long)EMPTY64, (unsigned long long)key);
     if (old == EMPTY64 || old == key) {

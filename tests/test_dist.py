@@ -1,0 +1,48 @@
+"""Multi-rank path on CPU (gloo, world_size 2): bench.py's replica aggregation (max elapsed over
+ranks, summed edges) -- the only cross-rank exchange of the replica mode."""
+import os
+import socket
+import sys
+
+import pytest
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, q):
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+    import bench
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    elapsed, edges = bench.aggregate(dist, elapsed=1.0 + rank, edges=10.0 * (rank + 1))
+    q.put((rank, elapsed, edges))
+    dist.destroy_process_group()
+
+
+def test_replica_aggregation_gloo_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(120)
+        assert p.exitcode == 0
+    got = sorted(q.get(timeout=10) for _ in range(2))
+    assert got == [(0, 2.0, 30.0), (1, 2.0, 30.0)]
+
+
+def test_single_rank_passthrough():
+    sys.path.insert(0, ROOT)
+    import bench
+    assert bench.aggregate(None, 3.5, 7.0) == (3.5, 7.0)

@@ -91,7 +91,31 @@ def test_heavy_path_overflow_star():
         out, _ = e.batch_check_ids(queries_array(q6, 0), with_stats=True)
         exp, _, _ = oracle.check_batch(q6, np.zeros(len(qs), np.int32), gmax)
         assert list(out) == list(exp), (gmax, out, exp)
-    assert e.last_stats["n_heavy"] >= 1
+    assert e.last_stats["n_medium"] + e.last_stats["n_heavy"] >= 1
+
+
+def test_workgroup_tiers_lds_and_hbm():
+    # > 256 expanded nodes leaves the wave tier; > 4096 leaves the LDS workgroup tier for the HBM one
+    tuples = [RelationTuple.from_string(f"g:root#m@(g:c{i}#m)") for i in range(5000)]
+    tuples += [RelationTuple.from_string(f"g:c{i}#m@(g:d{i % 1500}#m)") for i in range(5000)]
+    tuples += [RelationTuple.from_string(f"g:d{i}#m@(g:e{i % 400}#m)") for i in range(1500)]
+    tuples += [RelationTuple.from_string("g:e399#m@target"), RelationTuple.from_string("g:d7#m@mid")]
+    reg = Registry(tuples, [])
+    e = reg.permission_engine()
+    it = reg.interner
+    qs = [RelationTuple.from_string(s) for s in
+          ["g:root#m@target", "g:root#m@mid", "g:root#m@none", "g:c3#m@target", "g:c7#m@mid", "g:d3#m@target"]]
+    q6 = np.asarray([it.tuple_ids(t) for t in qs], np.uint32)
+    oracle = Oracle(it.tuples_array(tuples), it.wildcard_rel)
+    tiers = {"n_medium": 0, "n_heavy": 0}
+    for gmax in (2, 3, 4, 5, 6):
+        e.config.max_read_depth = gmax
+        out, _ = e.batch_check_ids(queries_array(q6, 0), with_stats=True)
+        exp, _, _ = oracle.check_batch(q6, np.zeros(len(qs), np.int32), gmax)
+        assert list(out) == list(exp), (gmax, out, exp)
+        for k in tiers:
+            tiers[k] += e.last_stats[k]
+    assert tiers["n_medium"] >= 1 and tiers["n_heavy"] >= 1, tiers
 
 
 def test_empty_and_unknown():
