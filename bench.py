@@ -42,7 +42,58 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--preset", type=int, default=0,
                     help="0 = C2/C4 rewrite-free (headline); 1 = C3 (OPL view/edit/share via the rewrite interpreter)")
+    ap.add_argument("--mode", choices=["check", "expand"], default="check",
+                    help="expand = config C5: batched BuildTree of hot group#member roots")
+    ap.add_argument("--roots", type=int, default=100_000, help="expand roots per step (C5)")
     return ap.parse_args()
+
+
+def bench_expand(a):
+    """Config C5: full subject-set trees for the most popular group#member roots at max_read_depth
+    (SURVEY.md 8d), one kg_expand_batch call per step (trees delivered to host memory)."""
+    import torch
+    from keto_amd import _lib
+    from keto_amd.engine import Snapshot
+    L = _lib.load()
+    torch.cuda.set_device(0)
+    snap = Snapshot.synthetic(int(a.tuples), seed=a.seed, device=0)
+    ids = snap.synth_ids()
+    n_docs, n_groups = ids["n_docs"], ids["n_groups"]
+    gpl = n_groups // 8
+    r = np.arange(a.roots, dtype=np.uint64)
+    layer, rank = r % 8, r // 8
+    node = n_docs + layer * gpl + (rank * 2654435761 + 12345) % gpl  # popularity rank -> group (kg_synth.h)
+    roots = np.zeros((a.roots, 4), np.uint32)
+    roots[:, 0] = 1  # ns group
+    roots[:, 1] = node.astype(np.uint32)  # group object id == node id
+    roots[:, 2] = 2  # rel member
+    roots[:, 3] = 0  # request depth 0 -> global
+    depth = a.global_depth if a.global_depth != 10 else 5
+
+    def step():
+        buf = _lib.kg_tree_buf()
+        _lib.check(L.kg_expand_batch(snap.handle, roots.ctypes.data_as(C.c_void_p), a.roots, depth, C.byref(buf)),
+                   "kg_expand_batch")
+        res = (buf.n_nodes, buf.kernel_ms)
+        L.kg_tree_free(C.byref(buf))
+        return res
+
+    for _ in range(a.warmup):
+        step()
+    t0 = time.perf_counter()
+    nodes, kms = 0, 0.0
+    for _ in range(a.steps):
+        n, k = step()
+        nodes += n
+        kms += k
+    el = time.perf_counter() - t0
+    out = {"metric": "expand trees/sec (batched BuildTree, hot group#member roots)", "value": a.roots * a.steps / el,
+           "unit": "trees/s", "n_gpus": 1, "steps": a.steps, "warmup": a.warmup, "ms_per_step": el / a.steps * 1e3,
+           "higher_is_better": True, "dtype": "u32", "data": "synthetic (device-generated, seed %d)" % a.seed,
+           "config": {"workload": "C5: %d hot roots @ %.3g tuples, max_read_depth %d" % (a.roots, a.tuples, depth)},
+           "tree_nodes_per_step": nodes / a.steps, "tree_nodes_per_s": nodes / el,
+           "kernel_ms_per_step": kms / a.steps, "trees_per_s_kernel_only": a.roots * a.steps / (kms * 1e-3)}
+    print(json.dumps(out), flush=True)
 
 
 def aggregate(dist, elapsed: float, edges: float, device=None):
@@ -60,6 +111,8 @@ def aggregate(dist, elapsed: float, edges: float, device=None):
 
 def main():
     a = parse()
+    if a.mode == "expand":
+        return bench_expand(a)
     import torch
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))

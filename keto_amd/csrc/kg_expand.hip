@@ -353,6 +353,9 @@ int expand_batch(Snapshot* s, const kg_set* roots, size_t n, int32_t global, kg_
       fail("H2D", e);
   }
   ExpCtl h{};
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  for (auto& x : ev)
+    if (!rc && (e = hipEventCreate(&x)) != hipSuccess) fail("hipEventCreate", e);
   for (int attempt = 0; !rc; attempt++) {
     if (arena) hipFree(arena), arena = nullptr;
     if (next) hipFree(next), next = nullptr;
@@ -370,10 +373,12 @@ int expand_batch(Snapshot* s, const kg_set* roots, size_t n, int32_t global, kg_
       fail("memset", e);
       break;
     }
+    (void)hipEventRecord(ev[0], stream);
     hipLaunchKernelGGL(k_expand_lds, dim3(grid1), dim3(256), 0, stream, s->ds, d_roots, (uint32_t)n, global, ctl, outs,
                        arena, next, n_chunks, stacks, stack_cap, p2);
     hipLaunchKernelGGL(k_expand_hbm, dim3(slots2), dim3(64), 0, stream, s->ds, d_roots, global, ctl, outs, arena, next,
                        n_chunks, stacks + (size_t)slots1 * stack_cap, stack_cap, p2, bm, words, lists, nn);
+    (void)hipEventRecord(ev[1], stream);
     if ((e = hipGetLastError()) != hipSuccess) {
       fail("launch", e);
       break;
@@ -411,8 +416,10 @@ int expand_batch(Snapshot* s, const kg_set* roots, size_t n, int32_t global, kg_
     if (!rc && (e = hipMemcpyAsync(d_off, out->root_off, (n + 1) * 8, hipMemcpyHostToDevice, stream)) != hipSuccess)
       fail("H2D", e);
     if (!rc) {
+      (void)hipEventRecord(ev[2], stream);
       hipLaunchKernelGGL(k_expand_compact, dim3((uint32_t)((n + 3) / 4)), dim3(256), 0, stream, outs, (uint32_t)n,
                          d_off, arena, next, dst);
+      (void)hipEventRecord(ev[3], stream);
       if ((e = hipMemcpyAsync(out->nodes, dst, total * sizeof(kg_tree_node), hipMemcpyDeviceToHost, stream)) !=
               hipSuccess ||
           (e = hipStreamSynchronize(stream)) != hipSuccess)
@@ -420,6 +427,14 @@ int expand_batch(Snapshot* s, const kg_set* roots, size_t n, int32_t global, kg_
     }
   }
   out->n_nodes = total;
+  if (!rc) {
+    float a = 0, b = 0;
+    (void)hipEventElapsedTime(&a, ev[0], ev[1]);
+    if (total) (void)hipEventElapsedTime(&b, ev[2], ev[3]);
+    out->kernel_ms = (double)a + (double)b;
+  }
+  for (auto& x : ev)
+    if (x) (void)hipEventDestroy(x);
   for (void* p : {(void*)d_roots, (void*)ctl, (void*)outs, (void*)stacks, (void*)p2, (void*)bm, (void*)arena,
                   (void*)next, (void*)dst, (void*)d_off})
     if (p) (void)hipFree(p);
