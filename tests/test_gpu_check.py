@@ -100,11 +100,16 @@ def test_workgroup_tiers_lds_and_hbm():
     tuples += [RelationTuple.from_string(f"g:c{i}#m@(g:d{i % 1500}#m)") for i in range(5000)]
     tuples += [RelationTuple.from_string(f"g:d{i}#m@(g:e{i % 400}#m)") for i in range(1500)]
     tuples += [RelationTuple.from_string("g:e399#m@target"), RelationTuple.from_string("g:d7#m@mid")]
+    # a second root with ~1000 expanded nodes: beyond the wave tier, inside the LDS workgroup tier
+    tuples += [RelationTuple.from_string(f"g:r2#m@(g:f{i}#m)") for i in range(1000)]
+    tuples += [RelationTuple.from_string(f"g:f{i}#m@(g:h{i % 100}#m)") for i in range(1000)]
+    tuples += [RelationTuple.from_string("g:h99#m@deep")]
     reg = Registry(tuples, [])
     e = reg.permission_engine()
     it = reg.interner
     qs = [RelationTuple.from_string(s) for s in
-          ["g:root#m@target", "g:root#m@mid", "g:root#m@none", "g:c3#m@target", "g:c7#m@mid", "g:d3#m@target"]]
+          ["g:root#m@target", "g:root#m@mid", "g:root#m@none", "g:c3#m@target", "g:c7#m@mid", "g:d3#m@target",
+           "g:r2#m@deep", "g:r2#m@none"]]
     q6 = np.asarray([it.tuple_ids(t) for t in qs], np.uint32)
     oracle = Oracle(it.tuples_array(tuples), it.wildcard_rel)
     tiers = {"n_medium": 0, "n_heavy": 0}
