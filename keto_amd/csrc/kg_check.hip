@@ -22,8 +22,11 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
+#include <cstring>
 
 #include "kg_bfs.h"
+#include "kg_grid.h"
 #include "kg_internal.h"
 #include "kg_interp.h"
 #include "kg_snapshot.h"
@@ -52,6 +55,7 @@ __global__ __launch_bounds__(256) void k_resolve(DevSnap s, const kg_query* __re
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   bool valid = i < n;
   uint32_t route = ROUTE_DONE;
+  bool did_probe = false;
   if (valid) {
     kg_query x = q[i];
     uint32_t node = nmap_find(s, x.t.ns, x.t.rel, x.t.obj);
@@ -72,15 +76,25 @@ __global__ __launch_bounds__(256) void k_resolve(DevSnap s, const kg_query* __re
       route = impure ? ROUTE_GENERAL : ROUTE_LIGHT;
     }
     uint32_t rb = 0, rl = 0;
-    if (node != NONE) {
+    bool member = false;
+    did_probe = route == ROUTE_LIGHT;
+    if (route == ROUTE_LIGHT) {
+      // the root's checkDirect(D-1) (D >= 1 always) is thread-parallel here: a direct tuple or a
+      // depth that cannot reach any child (D < 2) finishes the query before the wave tier
       rb = (uint32_t)s.adj_off[node];
       rl = (uint32_t)(s.adj_off[node + 1] - s.adj_off[node]);
+      member = dset_probe(s, node, subj);
+      if (member || d < 2 || rl == 0) route = ROUTE_DONE;
     }
     rq[i] = RQuery{node, subj, d, route, rb, rl};
     if (route == ROUTE_DONE) {
-      out[i] = KG_NOT_MEMBER;
+      out[i] = member ? KG_IS_MEMBER : KG_NOT_MEMBER;
       if (err) err[i] = KG_ERR_NONE;
     }
+  }
+  {
+    const uint64_t probed = __ballot(valid && did_probe);
+    if (probed && lane_id() == 0) atomicAdd(&ctl->st[ST_PROBES], (unsigned long long)__popcll(probed));
   }
   wave_append(valid && route == ROUTE_LIGHT, i, light_list, &ctl->light_count);
   wave_append(valid && route == ROUTE_GENERAL, i, gen_list, &ctl->gen_count);
@@ -136,12 +150,7 @@ __device__ __forceinline__ bool lx_insert(uint32_t* vis, uint32_t key) {
 __device__ __forceinline__ int light_query(const DevSnap& s, LightLds& L, const RQuery& q, BfsStats& bs) {
   const int lane = lane_id();
   for (int i = lane * 4; i < LX_VIS; i += 256) *reinterpret_cast<uint4*>(&L.vis[i]) = make_uint4(NONE, NONE, NONE, NONE);
-  // the root: checkDirect(D-1) (D >= 1 always)
-  bs.probes++;
-  bool hit = false;
-  if (lane == 0) hit = dset_probe(s, q.node, q.subj);
-  if (__shfl((int)hit, 0, 64)) return BFS_M;
-  if (q.depth < 2) return BFS_N;
+  // the root was probed by k_resolve (checkDirect(D-1) missed, D >= 2, non-empty row)
   __builtin_amdgcn_wave_barrier();
   if (lane == 0) {
     lx_insert(L.vis, q.node);
@@ -151,6 +160,10 @@ __device__ __forceinline__ int light_query(const DevSnap& s, LightLds& L, const 
   }
   __builtin_amdgcn_wave_barrier();
   uint32_t lvl_b = 0, lvl_e = 1, n = 1;
+  // Children discovered in one 64-edge step are probed (checkDirect at their d-1) in the NEXT
+  // step, together with that step's row loads: each step is one HBM round trip for both.
+  bool pend = false;
+  uint32_t pend_node = 0;
   for (int k = 0; lvl_b < lvl_e; k++) {
     const int d = q.depth - k;        // >= 2: expand; children sit at d-1 >= 1 and get probed
     const bool keep = d - 1 >= 2;     // children will themselves be expanded -> list them
@@ -172,16 +185,15 @@ __device__ __forceinline__ int light_query(const DevSnap& s, LightLds& L, const 
         const uint32_t ob = __shfl(b, own, 64);
         AdjX x{NONE, 0, 0, 0};
         if (act) x = s.adjx[ob + (e - L.pref[own])];
-        // checkDirect(d-2) of the child: once per node when it will be expanded (first-mark
+        const bool h = pend && dset_probe(s, pend_node, q.subj);  // previous step's children
+        if (__ballot(h)) return BFS_M;
+        // children of this step: probed once per node when they will be expanded (first-mark
         // dedup), unconditionally on the last level (no visited state is kept for it)
-        bool h;
         if (keep) {
           const bool fresh = act && lx_insert(L.vis, x.node);
-          h = fresh && dset_probe(s, x.node, q.subj);
           const uint64_t m = __ballot(fresh);
           const uint32_t cnt = __popcll(m);
-          bs.probes += cnt;
-          if (n + cnt > LX_LIST) return __ballot(h) ? BFS_M : BFS_OVERFLOW;
+          if (n + cnt > LX_LIST) return BFS_OVERFLOW;  // the workgroup tier redoes the query
           if (fresh) {
             const uint32_t at = n + lanes_below(m);
             L.node[at] = x.node;
@@ -189,11 +201,12 @@ __device__ __forceinline__ int light_query(const DevSnap& s, LightLds& L, const 
             L.len[at] = x.len;
           }
           n += cnt;
+          pend = fresh;
         } else {
-          h = act && dset_probe(s, x.node, q.subj);
-          bs.probes += __popcll(__ballot(act));
+          pend = act;
         }
-        if (__ballot(h)) return BFS_M;
+        pend_node = x.node;
+        bs.probes += __popcll(__ballot(pend));
       }
       __builtin_amdgcn_wave_barrier();
     }
@@ -201,7 +214,8 @@ __device__ __forceinline__ int light_query(const DevSnap& s, LightLds& L, const 
     lvl_e = n;
     if (!keep) break;
   }
-  return BFS_N;
+  const bool h = pend && dset_probe(s, pend_node, q.subj);
+  return __ballot(h) ? BFS_M : BFS_N;
 }
 
 __global__ __launch_bounds__(256) void k_light(DevSnap s, const RQuery* __restrict__ rq,
@@ -523,25 +537,34 @@ int check_batch_device(Snapshot* s, const kg_query* d_q, size_t n, int32_t globa
   uint32_t* giant = (uint32_t*)(base + off_giant);
   uint32_t* p2 = (uint32_t*)(base + off_p2);
   Ctl* ctl = (Ctl*)(base + off_ctl);
-  // heavy pool: H slots of (bitmap + cap list) + one giant slot (bitmap + n_nodes list)
+  // heavy tier: KG_HEAVY_TIER=wg keeps the one-workgroup-per-query HBM tier (A/B measurement);
+  // the default is the grid tier (kg_grid.hip)
+  static const bool wg_heavy = [] {
+    const char* e = getenv("KG_HEAVY_TIER");
+    return e && strcmp(e, "wg") == 0;
+  }();
   const uint64_t nn = std::max<uint32_t>(s->ds.n_nodes, 1);
   const uint64_t words = (nn + 31) / 32 + 1;
   const uint64_t cap_h = std::min<uint64_t>(nn, 4u << 20);
-  const uint32_t H = (uint32_t)std::min<uint64_t>(2 * (uint64_t)s->n_cu, std::max<uint64_t>(
-                                                      1, (8ull << 30) / ((words + cap_h) * 4)));
-  const size_t pool = ((size_t)H * (words + cap_h) + (words + nn)) * 4;
-  if (pool > s->heavy_pool_bytes) {
-    if (s->heavy_pool) hipFree(s->heavy_pool);
-    s->heavy_pool = nullptr;
-    s->heavy_pool_bytes = 0;
-    HIPC(hipMalloc(&s->heavy_pool, pool));
-    HIPC(hipMemsetAsync(s->heavy_pool, 0, pool, stream));  // bitmaps start clear and are left clear
-    s->heavy_pool_bytes = pool;
+  uint32_t H = 0, *hb = nullptr, *hl = nullptr, *gb = nullptr, *gl = nullptr;
+  if (wg_heavy) {  // H slots of (bitmap + cap list) + one giant slot (bitmap + n_nodes list)
+    H = (uint32_t)std::min<uint64_t>(2 * (uint64_t)s->n_cu,
+                                     std::max<uint64_t>(1, (8ull << 30) / ((words + cap_h) * 4)));
+    const size_t pool = ((size_t)H * (words + cap_h) + (words + nn)) * 4;
+    if (pool > s->heavy_pool_bytes) {
+      if (s->heavy_pool) hipFree(s->heavy_pool);
+      s->heavy_pool = nullptr;
+      s->heavy_pool_bytes = 0;
+      HIPC(hipMalloc(&s->heavy_pool, pool));
+      HIPC(hipMemsetAsync(s->heavy_pool, 0, pool, stream));  // bitmaps start clear and are left clear
+      s->heavy_pool_bytes = pool;
+    }
+    hb = (uint32_t*)s->heavy_pool;
+    hl = hb + (size_t)H * words;
+    gb = hl + (size_t)H * cap_h;
+    gl = gb + words;
   }
-  uint32_t* hb = (uint32_t*)s->heavy_pool;
-  uint32_t* hl = hb + (size_t)H * words;
-  uint32_t* gb = hl + (size_t)H * cap_h;
-  uint32_t* gl = gb + words;
+  GridStats gs;
 
   hipEvent_t e0 = nullptr, e1 = nullptr, l0 = nullptr, l1 = nullptr;
   if (stats) {
@@ -565,12 +588,17 @@ int check_batch_device(Snapshot* s, const kg_query* d_q, size_t n, int32_t globa
     hipLaunchKernelGGL(k_medium, dim3((uint32_t)s->n_cu * 3), dim3(256), 0, stream, s->ds, rq, medium,
                        &ctl->medium_count, &ctl->medium_head, d_out, d_err, heavy, &ctl->heavy_count, ctl);
     HIPC(hipGetLastError());
-    hipLaunchKernelGGL(k_heavy, dim3(H), dim3(256), 0, stream, s->ds, rq, heavy, &ctl->heavy_count, &ctl->heavy_head,
-                       d_out, d_err, hb, words, hl, cap_h, giant, &ctl->giant_count, ctl);
-    HIPC(hipGetLastError());
-    hipLaunchKernelGGL(k_heavy, dim3(1), dim3(256), 0, stream, s->ds, rq, giant, &ctl->giant_count, &ctl->giant_head,
-                       d_out, d_err, gb, words, gl, nn, giant /*never overflows*/, &ctl->pad0, ctl);
-    HIPC(hipGetLastError());
+    if (wg_heavy) {
+      hipLaunchKernelGGL(k_heavy, dim3(H), dim3(256), 0, stream, s->ds, rq, heavy, &ctl->heavy_count,
+                         &ctl->heavy_head, d_out, d_err, hb, words, hl, cap_h, giant, &ctl->giant_count, ctl);
+      HIPC(hipGetLastError());
+      hipLaunchKernelGGL(k_heavy, dim3(1), dim3(256), 0, stream, s->ds, rq, giant, &ctl->giant_count,
+                         &ctl->giant_head, d_out, d_err, gb, words, gl, nn, giant /*never overflows*/, &ctl->pad0,
+                         ctl);
+      HIPC(hipGetLastError());
+    } else if (int rc = grid_tier(s, rq, heavy, &ctl->heavy_count, d_out, d_err, stream, &gs)) {
+      return rc;
+    }
     if (s->has_program) {
       InterpCtl ic{};
       ic.gen_count = &ctl->gen_count;
@@ -605,7 +633,11 @@ int check_batch_device(Snapshot* s, const kg_query* d_q, size_t n, int32_t globa
     stats->frontier_hbm = h.st[ST_FHBM];
     stats->n_light = h.st[ST_LIGHT];
     stats->n_medium = h.st[ST_MEDIUM];
-    stats->n_heavy = h.st[ST_HEAVY];
+    stats->n_heavy = wg_heavy ? h.st[ST_HEAVY] : gs.done;
+    stats->rows_opened += gs.rows;
+    stats->edges_read += gs.edges;
+    stats->direct_probes += gs.probes;
+    stats->frontier_hbm += gs.logged;
     stats->n_general = h.st[ST_GENERAL];
     stats->kernel_ms = ms;
   }

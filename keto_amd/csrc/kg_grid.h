@@ -1,0 +1,17 @@
+// kg_grid.h -- grid tier interface (kg_grid.hip), called by the batch driver (kg_check.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "kg_internal.h"
+
+namespace kg {
+
+struct GridStats {
+  unsigned long long rows = 0, edges = 0, probes = 0, done = 0, logged = 0;
+};
+
+struct Snapshot;
+int grid_tier(Snapshot* s, const RQuery* rq, const uint32_t* qlist, const uint32_t* d_count, uint8_t* out,
+              uint32_t* err, hipStream_t stream, GridStats* gs);
+
+}  // namespace kg

@@ -48,6 +48,10 @@ struct Snapshot {
   size_t scratch_bytes = 0;
   void* heavy_pool = nullptr;
   size_t heavy_pool_bytes = 0;
+  void* grid_pool = nullptr;  // grid tier: bitmaps | log | lens | offs | slots | ctl
+  size_t grid_pool_bytes = 0;
+  void* grid_scan_tmp = nullptr;
+  size_t grid_scan_tmp_bytes = 0;
   void* interp_pool = nullptr;
   size_t interp_pool_bytes = 0;
   uint64_t batch_seq = 0;

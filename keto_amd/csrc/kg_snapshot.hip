@@ -135,6 +135,8 @@ Snapshot::~Snapshot() {
   for (void* p : allocs) hipFree(p);
   if (scratch) hipFree(scratch);
   if (heavy_pool) hipFree(heavy_pool);
+  if (grid_pool) hipFree(grid_pool);
+  if (grid_scan_tmp) hipFree(grid_scan_tmp);
   if (interp_pool) hipFree(interp_pool);
   if (stream) hipStreamDestroy(stream);
 }
