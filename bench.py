@@ -194,8 +194,12 @@ def main():
         "gteps": edges / elapsed / 1e9,
         "p99_batch_ms": float(np.percentile(np.array(lat) * 1e3, 99)),
         "allowed_fraction": float(res.mean()),
-        "tiers": {"light": int(stats[-1].n_light), "heavy": int(stats[-1].n_heavy),
-                  "general": int(stats[-1].n_general)},
+        "tiers": {"light": int(stats[-1].n_light), "medium": int(stats[-1].n_medium),
+                  "heavy": int(stats[-1].n_heavy), "general": int(stats[-1].n_general)},
+        "work_per_batch": {"light": {"rows": int(stats[-1].light_rows_opened), "edges": int(stats[-1].light_edges_read),
+                                     "probes": int(stats[-1].light_probes)},
+                           "all": {"rows": int(stats[-1].rows_opened), "edges": int(stats[-1].edges_read),
+                                   "probes": int(stats[-1].direct_probes)}},
         "snapshot_build_s": t_build,
         "roofline": {"kernel": "k_light", "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

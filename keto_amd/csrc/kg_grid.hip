@@ -1,11 +1,13 @@
 // kg_grid.hip -- the grid tier: queries whose BFS outgrew the LDS workgroup tier (thousands to
 // millions of expanded nodes).  All of them advance together, level-synchronously, and every level
 // is spread edge-balanced over the whole GPU:
-//   F                append-only log of (slot, node) frontier entries; level L = F[lvl_b, lvl_e)
+//   F/RB/lens        append-only log of (slot, node, set-row start, set-row length) entries;
+//                    level L = log[lvl_b, lvl_e)
 //   bitmaps[slot]    visited set of each query (n_nodes bits), cleared from the log afterwards
-//   per level        row lengths -> device exclusive scan -> one thread per edge (binary search of
-//                    its entry), bit test-and-set, checkDirect probe at discovery, append if the
-//                    child will itself be expanded (rest depth >= 2)
+//   per level        device inclusive scan of the row lengths -> one thread per edge (LDS binary
+//                    search of its entry within a 2048-edge tile), checkDirect probe at discovery;
+//                    children that will themselves be expanded (rest depth >= 2, non-empty set
+//                    row, read inline from adjx) are bit-test-and-set and appended wave-aggregated
 // Semantics are those of k_light / k_medium (kg_check.hip): bounded reachability with every node
 // probed once at its shallowest depth.  A round that overflows the log is rerun with fewer slots.
 #include <hip/hip_runtime.h>
@@ -23,16 +25,20 @@ namespace kg {
 struct GridCtl {
   unsigned long long n;  // entries appended to the log
   uint32_t overflow, pad;
-  unsigned long long rows, edges, probes;
+  unsigned long long probes;
 };
 
-__global__ void k_grid_init(const RQuery* __restrict__ rq, const uint32_t* __restrict__ qlist, uint32_t base,
-                            uint32_t cnt, uint64_t* F, uint32_t* slot_q, uint32_t* slot_hit, uint32_t* bitmaps,
-                            uint64_t words, GridCtl* ctl) {
+// Log entry j: F[j] = slot << 32 | node, RB[j] = first adjx index of node's set row, lens[j] = its
+// length.  Only nodes with a non-empty set row are marked and logged; leaves are probed wherever
+// they are reached (a probe does not depend on the depth it is made at, so this is exact).
+__global__ void k_grid_init(DevSnap s, const RQuery* __restrict__ rq, const uint32_t* __restrict__ qlist,
+                            uint32_t base, uint32_t cnt, uint64_t* F, uint32_t* RB, uint64_t* lens, uint32_t* slot_q,
+                            uint32_t* slot_hit, uint32_t* bitmaps, uint64_t words, GridCtl* ctl) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i == 0) {
     ctl->n = cnt;
     ctl->overflow = 0;
+    ctl->probes = 0;
   }
   if (i >= cnt) return;
   const uint32_t qi = qlist[base + i];
@@ -41,57 +47,108 @@ __global__ void k_grid_init(const RQuery* __restrict__ rq, const uint32_t* __res
   slot_hit[i] = 0;  // the root was already probed (k_resolve)
   bitmaps[(size_t)i * words + (root >> 5)] |= 1u << (root & 31);
   F[i] = ((uint64_t)i << 32) | root;
+  RB[i] = (uint32_t)s.adj_off[root];
+  lens[i] = s.adj_off[root + 1] - s.adj_off[root];
 }
 
-__global__ void k_grid_rowlen(DevSnap s, const RQuery* __restrict__ rq, const uint64_t* __restrict__ F,
-                              uint64_t lvl_b, uint64_t n, int level, const uint32_t* slot_q,
-                              const uint32_t* slot_hit, uint64_t* lens) {
-  const uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-  if (j > n) return;
-  uint64_t len = 0;
-  if (j < n) {
-    const uint64_t f = F[lvl_b + j];
-    const uint32_t slot = (uint32_t)(f >> 32), node = (uint32_t)f;
-    const int d = rq[slot_q[slot]].depth - level;
-    if (d >= 2 && !slot_hit[slot]) len = s.adj_off[node + 1] - s.adj_off[node];
+// smallest j in [lo, hi) with incl[j] > e (incl = inclusive prefix sums of the level's row lengths)
+__device__ __forceinline__ uint64_t first_above(const uint64_t* incl, uint64_t lo, uint64_t hi, uint64_t e) {
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (incl[mid] > e) hi = mid;
+    else lo = mid + 1;
   }
-  lens[j] = len;
+  return lo;
 }
+
+// One thread per edge of the level, in tiles of GT edges per workgroup: the tile's entries'
+// row starts are staged in LDS so each edge finds its entry with an LDS binary search.
+constexpr uint32_t GT = 2048;
 
 __global__ __launch_bounds__(256) void k_grid_expand(DevSnap s, const RQuery* __restrict__ rq, uint64_t* F,
-                                                     uint64_t lvl_b, uint64_t n, const uint64_t* __restrict__ offs,
-                                                     uint64_t total, int level, const uint32_t* slot_q,
-                                                     uint32_t* slot_hit, uint32_t* bitmaps, uint64_t words,
-                                                     uint64_t cap, GridCtl* ctl) {
-  unsigned long long probes = 0;
-  for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < total;
-       e += (uint64_t)gridDim.x * blockDim.x) {
-    uint64_t lo = 0, hi = n;  // largest j with offs[j] <= e
-    while (hi - lo > 1) {
-      const uint64_t mid = (lo + hi) >> 1;
-      if (offs[mid] <= e) lo = mid;
-      else hi = mid;
+                                                     uint32_t* RB, uint64_t* lens, uint64_t lvl_b, uint64_t n,
+                                                     const uint64_t* __restrict__ incl, uint64_t total, int level,
+                                                     const uint32_t* __restrict__ slot_q, uint32_t* slot_hit,
+                                                     uint32_t* bitmaps, uint64_t words, uint64_t cap, GridCtl* ctl) {
+  __shared__ uint64_t s_beg[GT + 1];
+  __shared__ uint64_t s_j0, s_cnt;
+  const int lane = lane_id();
+  uint32_t probes = 0;
+  for (uint64_t t0 = (uint64_t)blockIdx.x * GT; t0 < total; t0 += (uint64_t)gridDim.x * GT) {
+    const uint64_t t1 = t0 + GT < total ? t0 + GT : total;
+    if (threadIdx.x == 0) {
+      const uint64_t j0 = first_above(incl, 0, n, t0);
+      s_j0 = j0;
+      s_cnt = first_above(incl, j0, n, t1 - 1) - j0 + 1;
     }
-    const uint64_t f = F[lvl_b + lo];
-    const uint32_t slot = (uint32_t)(f >> 32), node = (uint32_t)f;
-    if (*(volatile uint32_t*)&slot_hit[slot]) continue;
-    const RQuery q = rq[slot_q[slot]];
-    const int d = q.depth - level;  // >= 2 (rows of shallower nodes have length 0)
-    const uint32_t child = s.adj[s.adj_off[node] + (e - offs[lo])];
-    if (d - 1 >= 2) {  // child will be expanded: first mark + probe + log it
-      const uint32_t bit = 1u << (child & 31);
-      if (atomicOr(&bitmaps[(size_t)slot * words + (child >> 5)], bit) & bit) continue;
-      probes++;
-      if (dset_probe(s, child, q.subj)) atomicExch(&slot_hit[slot], 1u);
-      const unsigned long long at = atomicAdd(&ctl->n, 1ull);
-      if (at < cap) F[at] = ((uint64_t)slot << 32) | child;
-      else ctl->overflow = 1;
-    } else {  // last level: probe only
-      probes++;
-      if (dset_probe(s, child, q.subj)) atomicExch(&slot_hit[slot], 1u);
+    __syncthreads();
+    const uint64_t j0 = s_j0, cnt = s_cnt;
+    const bool use_lds = cnt <= GT;
+    if (use_lds)
+      for (uint32_t i = threadIdx.x; i <= cnt; i += 256) s_beg[i] = j0 + i == 0 ? 0 : incl[j0 + i - 1];
+    __syncthreads();
+    for (uint32_t k = 0; k < GT; k += 256) {
+      const uint64_t e = t0 + k + threadIdx.x;
+      bool act = e < t1, keep = false;
+      uint32_t slot = 0, child = 0, cb = 0, cl = 0;
+      if (act) {
+        uint64_t j, beg;
+        if (use_lds) {
+          uint32_t lo = 0, hi = (uint32_t)cnt;  // largest i < cnt with s_beg[i] <= e
+          while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (s_beg[mid] <= e) lo = mid;
+            else hi = mid;
+          }
+          j = j0 + lo;
+          beg = s_beg[lo];
+        } else {
+          j = first_above(incl, j0, j0 + cnt, e);
+          beg = incl[j] - lens[lvl_b + j];
+        }
+        slot = (uint32_t)(F[lvl_b + j] >> 32);
+        if (slot_hit[slot]) {
+          act = false;
+        } else {
+          const RQuery q = rq[slot_q[slot]];
+          const AdjX x = s.adjx[RB[lvl_b + j] + (e - beg)];
+          child = x.node;
+          cb = x.begin;
+          cl = x.len;
+          keep = cl > 0 && q.depth - level - 1 >= 2;  // child will itself be expanded
+          if (keep) {
+            const uint32_t bit = 1u << (child & 31);
+            if (atomicOr(&bitmaps[(size_t)slot * words + (child >> 5)], bit) & bit) act = false;
+          }
+          if (act) {
+            probes++;
+            if (dset_probe(s, child, q.subj)) atomicExch(&slot_hit[slot], 1u);
+          }
+        }
+      }
+      const bool app = act && keep;
+      const uint64_t m = __ballot(app);
+      if (m) {  // wave-aggregated append to the log
+        const int leader = __ffsll((unsigned long long)m) - 1;
+        unsigned long long base = 0;
+        if (lane == leader) base = atomicAdd(&ctl->n, (unsigned long long)__popcll(m));
+        base = shfl64(base, leader);
+        if (app) {
+          const unsigned long long at = base + lanes_below(m);
+          if (at < cap) {
+            F[at] = ((uint64_t)slot << 32) | child;
+            RB[at] = cb;
+            lens[at] = cl;
+          } else {
+            ctl->overflow = 1;
+          }
+        }
+      }
     }
+    __syncthreads();
   }
-  if (probes) atomicAdd(&ctl->probes, probes);
+  for (int off = 32; off; off >>= 1) probes += __shfl_xor(probes, off, 64);
+  if (lane == 0 && probes) atomicAdd(&ctl->probes, (unsigned long long)probes);
 }
 
 __global__ void k_grid_finish(const uint32_t* slot_q, const uint32_t* slot_hit, uint32_t cnt, uint8_t* out,
@@ -122,7 +179,7 @@ int grid_tier(Snapshot* s, const RQuery* rq, const uint32_t* qlist, const uint32
   // budget: <= 16 GiB of bitmaps, <= 1024 slots; log capacity >= n_nodes (a single query always fits)
   const uint32_t G0 = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(1024, (16ull << 30) / (words * 4)));
   const uint64_t cap = std::max<uint64_t>(nn + 1024, 64ull << 20);
-  const size_t need = (size_t)G0 * words * 4 + cap * 8 + (cap + 1) * 8 * 2 + (size_t)G0 * 8 + sizeof(GridCtl) + 4096;
+  const size_t need = (size_t)G0 * words * 4 + cap * (8 + 4 + 8 + 8) + (size_t)G0 * 8 + sizeof(GridCtl) + 4096;
   if (need > s->grid_pool_bytes) {
     if (s->grid_pool) HIPC(hipFree(s->grid_pool));
     s->grid_pool = nullptr;
@@ -138,16 +195,18 @@ int grid_tier(Snapshot* s, const RQuery* rq, const uint32_t* qlist, const uint32
   uint64_t* F = (uint64_t*)p;
   p += cap * 8;
   uint64_t* lens = (uint64_t*)p;
-  p += (cap + 1) * 8;
-  uint64_t* offs = (uint64_t*)p;
-  p += (cap + 1) * 8;
+  p += cap * 8;
+  uint64_t* incl = (uint64_t*)p;
+  p += cap * 8;
+  uint32_t* RB = (uint32_t*)p;
+  p += cap * 4;
   uint32_t* slot_q = (uint32_t*)p;
   uint32_t* slot_hit = slot_q + G0;
   p += (size_t)G0 * 8;
   GridCtl* ctl = (GridCtl*)(((uintptr_t)p + 255) & ~uintptr_t(255));
   // scan scratch sized for the largest level (cap entries)
   size_t tmp_bytes = 0;
-  HIPC(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, lens, offs, cap + 1, stream));
+  HIPC(hipcub::DeviceScan::InclusiveSum(nullptr, tmp_bytes, lens, incl, cap, stream));
   if (tmp_bytes > s->grid_scan_tmp_bytes) {
     if (s->grid_scan_tmp) HIPC(hipFree(s->grid_scan_tmp));
     HIPC(hipMalloc(&s->grid_scan_tmp, tmp_bytes + 256));
@@ -156,30 +215,26 @@ int grid_tier(Snapshot* s, const RQuery* rq, const uint32_t* qlist, const uint32
   uint32_t G = G0;
   for (uint32_t done = 0; done < count;) {
     const uint32_t cnt = std::min(G, count - done);
-    HIPC(hipMemsetAsync(&ctl->rows, 0, 3 * sizeof(unsigned long long), stream));
-    hipLaunchKernelGGL(k_grid_init, dim3((cnt + 255) / 256), dim3(256), 0, stream, rq, qlist, done, cnt, F, slot_q,
-                       slot_hit, bitmaps, words, ctl);
+    hipLaunchKernelGGL(k_grid_init, dim3((cnt + 255) / 256), dim3(256), 0, stream, s->ds, rq, qlist, done, cnt, F,
+                       RB, lens, slot_q, slot_hit, bitmaps, words, ctl);
     HIPC(hipGetLastError());
     uint64_t lvl_b = 0, lvl_e = cnt;
     GridCtl h{};
     for (int level = 0; lvl_b < lvl_e; level++) {
       const uint64_t n = lvl_e - lvl_b;
-      hipLaunchKernelGGL(k_grid_rowlen, dim3((uint32_t)((n + 256) / 256)), dim3(256), 0, stream, s->ds, rq, F, lvl_b,
-                         n, level, slot_q, slot_hit, lens);
-      HIPC(hipGetLastError());
       size_t tb = s->grid_scan_tmp_bytes;
-      HIPC(hipcub::DeviceScan::ExclusiveSum(s->grid_scan_tmp, tb, lens, offs, n + 1, stream));
+      HIPC(hipcub::DeviceScan::InclusiveSum(s->grid_scan_tmp, tb, lens + lvl_b, incl, n, stream));
       uint64_t total = 0;
-      HIPC(hipMemcpyAsync(&total, offs + n, 8, hipMemcpyDeviceToHost, stream));
+      HIPC(hipMemcpyAsync(&total, incl + n - 1, 8, hipMemcpyDeviceToHost, stream));
       HIPC(hipStreamSynchronize(stream));
       if (total == 0) break;
       if (gs) {
         gs->rows += n;
         gs->edges += total;
       }
-      const uint32_t grid = (uint32_t)std::min<uint64_t>((uint64_t)s->n_cu * 16, (total + 255) / 256);
-      hipLaunchKernelGGL(k_grid_expand, dim3(grid), dim3(256), 0, stream, s->ds, rq, F, lvl_b, n, offs, total, level,
-                         slot_q, slot_hit, bitmaps, words, cap, ctl);
+      const uint32_t grid = (uint32_t)std::min<uint64_t>((uint64_t)s->n_cu * 8, (total + GT - 1) / GT);
+      hipLaunchKernelGGL(k_grid_expand, dim3(grid), dim3(256), 0, stream, s->ds, rq, F, RB, lens, lvl_b, n, incl,
+                         total, level, slot_q, slot_hit, bitmaps, words, cap, ctl);
       HIPC(hipGetLastError());
       HIPC(hipMemcpyAsync(&h, ctl, sizeof h, hipMemcpyDeviceToHost, stream));
       HIPC(hipStreamSynchronize(stream));
