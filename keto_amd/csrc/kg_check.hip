@@ -41,8 +41,9 @@ enum { ST_ROWS = 0, ST_EDGES, ST_PROBES, ST_FHBM, ST_LIGHT, ST_HEAVY, ST_GENERAL
 struct Ctl {
   uint32_t light_count, gen_count, heavy_count, giant_count;
   uint32_t heavy_head, giant_head, gen_head, pad0;
-  uint32_t medium_count, medium_head, pad1[2];
-  uint32_t heads[8 * 32];  // per-XCD dequeue heads, one 128-B line each
+  uint32_t medium_count, medium_head, light2_count, pad1;
+  uint32_t heads[8 * 32];   // per-XCD dequeue heads, one 128-B line each (k_light<16>)
+  uint32_t heads2[8 * 32];  // (k_light<64>)
   unsigned long long st[ST_N];
   InterpCtl ic;
 };
@@ -103,99 +104,111 @@ __global__ __launch_bounds__(256) void k_resolve(DevSnap s, const kg_query* __re
 // ------------------------------------------------------------------ k_light
 constexpr int LWAVES = 4;  // waves per workgroup (256 threads)
 
-// Dequeue one work index; per-XCD heads over [0, count) split into 8 ranges.
-__device__ __forceinline__ uint32_t dequeue(uint32_t* heads, uint32_t count, uint32_t& head_sel, uint32_t head0) {
-  while (head_sel < head0 + 8) {
-    uint32_t h = head_sel & 7;
-    uint32_t lo = (uint32_t)((uint64_t)count * h / 8), hi = (uint32_t)((uint64_t)count * (h + 1) / 8);
-    uint32_t k = atomicAdd(&heads[h * 32], 1u);
-    if (lo + k < hi) return lo + k;
-    head_sel++;
-  }
-  return NONE;
-}
-
-// Per-wave LDS of k_light: visited hash of EXPANDED nodes and the BFS list with inlined rows.
-// Nodes of the last level that can still be probed (rest depth 1) are probed on discovery and
-// never stored, so the list only holds nodes that will be expanded.
-constexpr int LX_VLOG2 = 9;
-constexpr int LX_VIS = 1 << LX_VLOG2;
-constexpr int LX_LIST = 256;  // hash load <= 0.5
+// LDS of one light group (W lanes = one query): visited hash of EXPANDED nodes and the BFS list
+// with inlined rows.  Nodes of the last level that can still be probed (rest depth 1) are probed
+// on discovery and never stored, so the list only holds nodes that will be expanded.
+template <int W, int VLOG2, int LIST>
 struct LightLds {
-  uint32_t vis[LX_VIS];
-  uint32_t node[LX_LIST];
-  uint32_t beg[LX_LIST];
-  uint32_t len[LX_LIST];
-  uint32_t pref[64];
+  static constexpr int VIS = 1 << VLOG2;
+  uint32_t vis[VIS];
+  uint32_t node[LIST];
+  uint32_t beg[LIST];
+  uint32_t len[LIST];
+  uint32_t pref[W];
 };
 
-// Bounded LDS hash insert. The list cap (256) keeps the table <= ~63% full (each chunk adds at
-// most 64 before the cap check), so the bound is a safety net: a full table reports "fresh" and
-// the caller's cap check turns the query into an overflow instead of spinning.
+// Bounded LDS hash insert.  The list cap keeps the table <= ~63% full (each step adds at most W
+// before the cap check), so the bound is a safety net: a full table reports "fresh" and the
+// caller's cap check turns the query into an overflow instead of spinning.
+template <int VLOG2>
 __device__ __forceinline__ bool lx_insert(uint32_t* vis, uint32_t key) {
-  uint32_t h = (key * 2654435761u) >> (32 - LX_VLOG2);
-  for (int p = 0; p < LX_VIS; p++) {
+  constexpr uint32_t VIS = 1u << VLOG2;
+  uint32_t h = (key * 2654435761u) >> (32 - VLOG2);
+  for (uint32_t p = 0; p < VIS; p++) {
     uint32_t old = atomicCAS(&vis[h], NONE, key);
     if (old == NONE) return true;
     if (old == key) return false;
-    h = (h + 1) & (LX_VIS - 1);
+    h = (h + 1) & (VIS - 1);
   }
   return true;
 }
 
-// One query, one wave.  Level k (rest depth d = D-k >= 2) holds the nodes to expand: every one of
-// them was already probed (checkDirect at d-1) when it was discovered.  Per level, ONE dependent
-// HBM round trip: the rows of the frontier (adjx, children + their own rows inline).
+// Lane-group primitives: a wave64 holds 64/W independent groups of W lanes.
+template <int W>
+struct Group {
+  int lane, gl, gb;  // wave lane, lane within the group, first wave lane of the group
+  __device__ __forceinline__ Group() : lane(lane_id()), gl(lane_id() & (W - 1)), gb(lane_id() & ~(W - 1)) {}
+  __device__ __forceinline__ uint64_t ballot(bool p) const {
+    const uint64_t m = __ballot(p);
+    return W == 64 ? m : (m >> gb) & ((1ull << W) - 1);
+  }
+  __device__ __forceinline__ uint32_t below(uint64_t m) const { return __popcll(m & ((1ull << gl) - 1)); }
+  __device__ __forceinline__ uint32_t excl_scan(uint32_t x, uint32_t* total) const {
+    uint32_t v = x;
+#pragma unroll
+    for (int off = 1; off < W; off <<= 1) {
+      const uint32_t y = __shfl_up(v, off, W);
+      if (gl >= off) v += y;
+    }
+    *total = __shfl(v, W - 1, W);
+    return v - x;
+  }
+};
+
+// One query, one group of W lanes.  Level k (rest depth d = D-k >= 2) holds the nodes to expand:
+// every one of them was already probed (checkDirect at d-1) when it was discovered.  Children
+// discovered in one W-edge step are probed in the NEXT step, together with that step's row loads
+// (adjx: children + their own rows inline), so each step is one HBM round trip.
 // Returns BFS_M / BFS_N / BFS_OVERFLOW.
-__device__ __forceinline__ int light_query(const DevSnap& s, LightLds& L, const RQuery& q, BfsStats& bs) {
-  const int lane = lane_id();
-  for (int i = lane * 4; i < LX_VIS; i += 256) *reinterpret_cast<uint4*>(&L.vis[i]) = make_uint4(NONE, NONE, NONE, NONE);
+template <int W, int VLOG2, int LIST>
+__device__ __forceinline__ int light_query(const DevSnap& s, LightLds<W, VLOG2, LIST>& L, const Group<W>& g,
+                                           const RQuery& q, BfsStats& bs) {
+  constexpr int VIS = 1 << VLOG2;
+  for (int i = g.gl * 4; i < VIS; i += W * 4) *reinterpret_cast<uint4*>(&L.vis[i]) = make_uint4(NONE, NONE, NONE, NONE);
   // the root was probed by k_resolve (checkDirect(D-1) missed, D >= 2, non-empty row)
   __builtin_amdgcn_wave_barrier();
-  if (lane == 0) {
-    lx_insert(L.vis, q.node);
+  if (g.gl == 0) {
+    lx_insert<VLOG2>(L.vis, q.node);
     L.node[0] = q.node;
     L.beg[0] = q.beg;
     L.len[0] = q.len;
   }
   __builtin_amdgcn_wave_barrier();
   uint32_t lvl_b = 0, lvl_e = 1, n = 1;
-  // Children discovered in one 64-edge step are probed (checkDirect at their d-1) in the NEXT
-  // step, together with that step's row loads: each step is one HBM round trip for both.
   bool pend = false;
   uint32_t pend_node = 0;
   for (int k = 0; lvl_b < lvl_e; k++) {
-    const int d = q.depth - k;        // >= 2: expand; children sit at d-1 >= 1 and get probed
-    const bool keep = d - 1 >= 2;     // children will themselves be expanded -> list them
-    for (uint32_t base = lvl_b; base < lvl_e; base += 64) {
-      const uint32_t i = base + lane;
+    const int d = q.depth - k;     // >= 2: expand; children sit at d-1 >= 1 and get probed
+    const bool keep = d - 1 >= 2;  // children will themselves be expanded -> list them
+    for (uint32_t base = lvl_b; base < lvl_e; base += W) {
+      const uint32_t i = base + g.gl;
       const bool valid = i < lvl_e;
       const uint32_t b = valid ? L.beg[i] : 0u;
       const uint32_t ln = valid ? L.len[i] : 0u;
-      bs.rows += __popcll(__ballot(valid));
+      bs.rows += __popcll(g.ballot(valid));
       uint32_t total;
-      const uint32_t excl = wave_excl_scan(ln, &total);
-      L.pref[lane] = excl;
+      const uint32_t excl = g.excl_scan(ln, &total);
+      L.pref[g.gl] = excl;
       __builtin_amdgcn_wave_barrier();
       bs.edges += total;
-      for (uint32_t eb = 0; eb < total; eb += 64) {
-        const uint32_t e = eb + lane;
+      for (uint32_t eb = 0; eb < total; eb += W) {
+        const uint32_t e = eb + g.gl;
         const bool act = e < total;
-        const int own = act ? owner_search(L.pref, 64, e) : 0;
-        const uint32_t ob = __shfl(b, own, 64);
+        const int own = act ? owner_search(L.pref, W, e) : 0;
+        const uint32_t ob = __shfl(b, own, W);
         AdjX x{NONE, 0, 0, 0};
         if (act) x = s.adjx[ob + (e - L.pref[own])];
         const bool h = pend && dset_probe(s, pend_node, q.subj);  // previous step's children
-        if (__ballot(h)) return BFS_M;
+        if (g.ballot(h)) return BFS_M;
         // children of this step: probed once per node when they will be expanded (first-mark
         // dedup), unconditionally on the last level (no visited state is kept for it)
         if (keep) {
-          const bool fresh = act && lx_insert(L.vis, x.node);
-          const uint64_t m = __ballot(fresh);
+          const bool fresh = act && lx_insert<VLOG2>(L.vis, x.node);
+          const uint64_t m = g.ballot(fresh);
           const uint32_t cnt = __popcll(m);
-          if (n + cnt > LX_LIST) return BFS_OVERFLOW;  // the workgroup tier redoes the query
+          if (n + cnt > LIST) return BFS_OVERFLOW;  // the next tier redoes the query
           if (fresh) {
-            const uint32_t at = n + lanes_below(m);
+            const uint32_t at = n + g.below(m);
             L.node[at] = x.node;
             L.beg[at] = x.begin;
             L.len[at] = x.len;
@@ -206,7 +219,7 @@ __device__ __forceinline__ int light_query(const DevSnap& s, LightLds& L, const 
           pend = act;
         }
         pend_node = x.node;
-        bs.probes += __popcll(__ballot(pend));
+        bs.probes += __popcll(g.ballot(pend));
       }
       __builtin_amdgcn_wave_barrier();
     }
@@ -215,42 +228,73 @@ __device__ __forceinline__ int light_query(const DevSnap& s, LightLds& L, const 
     if (!keep) break;
   }
   const bool h = pend && dset_probe(s, pend_node, q.subj);
-  return __ballot(h) ? BFS_M : BFS_N;
+  return g.ballot(h) ? BFS_M : BFS_N;
 }
 
+// Dequeue up to `want` consecutive work indices for a wave; per-XCD heads over [0, count) split
+// into 8 ranges.  Returns the first index (NONE when all ranges are drained) and the number taken.
+__device__ __forceinline__ uint32_t dequeue_n(uint32_t* heads, uint32_t count, uint32_t& head_sel, uint32_t head0,
+                                              uint32_t want, uint32_t& got) {
+  while (head_sel < head0 + 8) {
+    uint32_t h = head_sel & 7;
+    uint32_t lo = (uint32_t)((uint64_t)count * h / 8), hi = (uint32_t)((uint64_t)count * (h + 1) / 8);
+    uint32_t k = atomicAdd(&heads[h * 32], want);
+    if (lo + k < hi) {
+      got = min(want, hi - (lo + k));
+      return lo + k;
+    }
+    head_sel++;
+  }
+  got = 0;
+  return NONE;
+}
+
+// Light tiers: k_light<16,...> runs four queries per wave (most light queries touch ~10 edges);
+// its overflow goes to k_light<64,...> (one query per wave, 4x the LDS), whose overflow goes to
+// the workgroup tier.  The groups of a wave advance in lockstep, one query each per round.
+template <int W, int VLOG2, int LIST>
 __global__ __launch_bounds__(256) void k_light(DevSnap s, const RQuery* __restrict__ rq,
-                                               const uint32_t* __restrict__ light_list, uint8_t* __restrict__ out,
-                                               uint32_t* __restrict__ err, uint32_t* heavy_list, Ctl* ctl) {
-  __shared__ LightLds lds_all[LWAVES];
-  const int wave = threadIdx.x >> 6, lane = lane_id();
-  LightLds& L = lds_all[wave];
-  const uint32_t count = ctl->light_count;
+                                               const uint32_t* __restrict__ qlist, const uint32_t* count_p,
+                                               uint32_t* heads, uint8_t* __restrict__ out,
+                                               uint32_t* __restrict__ err, uint32_t* next_list, uint32_t* next_count,
+                                               Ctl* ctl) {
+  constexpr int G = 256 / W, GW = 64 / W;  // groups per workgroup / per wave
+  __shared__ LightLds<W, VLOG2, LIST> lds_all[G];
+  const Group<W> g;
+  LightLds<W, VLOG2, LIST>& L = lds_all[threadIdx.x / W];
+  const uint32_t count = *count_p;
   const uint32_t head0 = blockIdx.x & 7;  // XCD label (speed only, never correctness)
   uint32_t head_sel = head0;
   BfsStats bs;
   unsigned long long st_done = 0;
   for (;;) {
-    uint32_t li = 0;
-    if (lane == 0) li = dequeue(ctl->heads, count, head_sel, head0);
-    li = __shfl(li, 0, 64);
-    if (li == NONE) break;
-    const uint32_t qi = light_list[li];
-    const RQuery q = rq[qi];
-    const int r = light_query(s, L, q, bs);
-    __builtin_amdgcn_wave_barrier();
-    if (r == BFS_OVERFLOW) {
-      if (lane == 0) heavy_list[atomicAdd(&ctl->medium_count, 1u)] = qi;  // -> workgroup LDS tier
-    } else if (lane == 0) {
-      out[qi] = r == BFS_M ? KG_IS_MEMBER : KG_NOT_MEMBER;
-      if (err) err[qi] = KG_ERR_NONE;
-      st_done++;
+    uint32_t first = 0, got = 0;
+    if (g.lane == 0) first = dequeue_n(heads, count, head_sel, head0, GW, got);
+    first = __shfl(first, 0, 64);
+    got = __shfl(got, 0, 64);
+    if (first == NONE) break;
+    const uint32_t gi = g.lane / W;
+    if (gi < got) {
+      const uint32_t qi = qlist[first + gi];
+      const RQuery q = rq[qi];
+      const int r = light_query<W, VLOG2, LIST>(s, L, g, q, bs);
+      __builtin_amdgcn_wave_barrier();
+      if (g.gl == 0) {
+        if (r == BFS_OVERFLOW) {
+          next_list[atomicAdd(next_count, 1u)] = qi;
+        } else {
+          out[qi] = r == BFS_M ? KG_IS_MEMBER : KG_NOT_MEMBER;
+          if (err) err[qi] = KG_ERR_NONE;
+          st_done++;
+        }
+      }
     }
   }
-  if (lane == 0) {
-    atomicAdd(&ctl->st[ST_LROWS], bs.rows);
-    atomicAdd(&ctl->st[ST_LEDGES], bs.edges);
-    atomicAdd(&ctl->st[ST_LPROBES], bs.probes);
-    atomicAdd(&ctl->st[ST_LIGHT], st_done);
+  if (g.gl == 0) {  // the narrow tier has its own counters (roofline of k_light<16>); wide -> shared
+    atomicAdd(&ctl->st[W == 16 ? ST_LROWS : ST_ROWS], bs.rows);
+    atomicAdd(&ctl->st[W == 16 ? ST_LEDGES : ST_EDGES], bs.edges);
+    atomicAdd(&ctl->st[W == 16 ? ST_LPROBES : ST_PROBES], bs.probes);
+    if (st_done) atomicAdd(&ctl->st[ST_LIGHT], st_done);
   }
 }
 
@@ -516,8 +560,9 @@ int check_batch_device(Snapshot* s, const kg_query* d_q, size_t n, int32_t globa
   if (n > 0x7FFFFFFFull) return set_error(-2, "batch too large");
   HIPC(hipSetDevice(s->device));
   if (!stream) stream = s->stream;
-  // scratch: rq[n] | light[n] | gen[n] | medium[n] | heavy[n] | giant[n] | p2[n] | Ctl
-  size_t off_rq = 0, off_light = align_up(off_rq + n * sizeof(RQuery)), off_gen = align_up(off_light + n * 4),
+  // scratch: rq[n] | light[n] | light2[n] | gen[n] | medium[n] | heavy[n] | giant[n] | p2[n] | Ctl
+  size_t off_rq = 0, off_light = align_up(off_rq + n * sizeof(RQuery)), off_light2 = align_up(off_light + n * 4),
+         off_gen = align_up(off_light2 + n * 4),
          off_med = align_up(off_gen + n * 4), off_heavy = align_up(off_med + n * 4),
          off_giant = align_up(off_heavy + n * 4), off_p2 = align_up(off_giant + n * 4),
          off_ctl = align_up(off_p2 + n * 4), total = align_up(off_ctl + sizeof(Ctl));
@@ -531,6 +576,7 @@ int check_batch_device(Snapshot* s, const kg_query* d_q, size_t n, int32_t globa
   char* base = (char*)s->scratch;
   RQuery* rq = (RQuery*)(base + off_rq);
   uint32_t* light = (uint32_t*)(base + off_light);
+  uint32_t* light2 = (uint32_t*)(base + off_light2);
   uint32_t* gen = (uint32_t*)(base + off_gen);
   uint32_t* medium = (uint32_t*)(base + off_med);
   uint32_t* heavy = (uint32_t*)(base + off_heavy);
@@ -579,12 +625,16 @@ int check_batch_device(Snapshot* s, const kg_query* d_q, size_t n, int32_t globa
     hipLaunchKernelGGL(k_resolve, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, stream, s->ds, d_q, (uint32_t)n,
                        global_max_depth, rq, d_out, d_err, light, gen, ctl);
     HIPC(hipGetLastError());
-    // 7 workgroups of 4 waves per CU: LDS 21 KiB/WG and 71 VGPRs both allow 28 waves/CU
-    const uint32_t light_grid = (uint32_t)std::min<uint64_t>((uint64_t)s->n_cu * 7, (n + 3) / 4 + 8);
+    // 7 workgroups of 4 waves per CU: ~21 KiB of LDS per workgroup allows 28 waves/CU
+    const uint32_t light_grid = (uint32_t)std::min<uint64_t>((uint64_t)s->n_cu * 7, (n + 15) / 16 + 8);
     if (stats) HIPC(hipEventRecord(l0, stream));
-    hipLaunchKernelGGL(k_light, dim3(light_grid), dim3(256), 0, stream, s->ds, rq, light, d_out, d_err, medium, ctl);
+    hipLaunchKernelGGL((k_light<16, 7, 64>), dim3(light_grid), dim3(256), 0, stream, s->ds, rq, light,
+                       &ctl->light_count, ctl->heads, d_out, d_err, light2, &ctl->light2_count, ctl);
     HIPC(hipGetLastError());
     if (stats) HIPC(hipEventRecord(l1, stream));
+    hipLaunchKernelGGL((k_light<64, 9, 256>), dim3((uint32_t)s->n_cu * 4), dim3(256), 0, stream, s->ds, rq, light2,
+                       &ctl->light2_count, ctl->heads2, d_out, d_err, medium, &ctl->medium_count, ctl);
+    HIPC(hipGetLastError());
     hipLaunchKernelGGL(k_medium, dim3((uint32_t)s->n_cu * 3), dim3(256), 0, stream, s->ds, rq, medium,
                        &ctl->medium_count, &ctl->medium_head, d_out, d_err, heavy, &ctl->heavy_count, ctl);
     HIPC(hipGetLastError());
