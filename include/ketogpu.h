@@ -155,6 +155,10 @@ int kg_snapshot_synthetic(const kg_synth_params* params, const kg_rewrite_prog* 
 void kg_snapshot_destroy(kg_snapshot* s);
 /* sizes: [0]=nodes [1]=rows [2]=set edges [3]=device bytes */
 int kg_snapshot_info(const kg_snapshot* s, uint64_t* info4);
+/* Engine knobs (no reference counterpart; tuning and tests).  key "tiers": where queries that
+ * overflow the wave tiers go -- 0 = grid tier (default), 1 = LDS workgroup tier then grid tier,
+ * 2 = LDS workgroup tier then one-workgroup-per-query HBM tier.  Results never depend on it. */
+int kg_snapshot_tune(kg_snapshot* s, const char* key, int64_t value);
 /* Synthetic layout: ids6 = {n_docs, n_groups, n_users, n_folders, user_obj0, folder_obj0}
  * (doc d = object d, group g = object n_docs+g, user u = object user_obj0+u). */
 int kg_synth_ids(const kg_snapshot* s, uint32_t* ids6);

@@ -66,7 +66,7 @@ class kg_synth_params(C.Structure):
 
 
 # every symbol include/ketogpu.h declares
-EXPORTS = ["kg_snapshot_create", "kg_snapshot_synthetic", "kg_snapshot_destroy", "kg_snapshot_info", "kg_synth_ids",
+EXPORTS = ["kg_snapshot_create", "kg_snapshot_synthetic", "kg_snapshot_destroy", "kg_snapshot_info", "kg_snapshot_tune", "kg_synth_ids",
            "kg_snapshot_export", "kg_snapshot_export_csr", "kg_check_batch", "kg_check_batch_device", "kg_synth_queries", "kg_expand_batch",
            "kg_tree_free", "kg_last_error", "kg_version"]
 
@@ -94,6 +94,7 @@ def load(path: str = LIB_PATH):
     L.kg_snapshot_destroy.restype = None
     L.kg_snapshot_info.argtypes = [vp, vp]
     L.kg_synth_ids.argtypes = [vp, vp]
+    L.kg_snapshot_tune.argtypes = [vp, C.c_char_p, C.c_int64]
     L.kg_snapshot_export.argtypes = [vp, vp, u64]
     L.kg_snapshot_export.restype = C.c_int64
     L.kg_snapshot_export_csr.argtypes = [vp, vp, vp, vp, vp, vp]
@@ -107,7 +108,7 @@ def load(path: str = LIB_PATH):
     L.kg_last_error.argtypes = [C.c_char_p, sz]
     L.kg_last_error.restype = sz
     L.kg_version.restype = C.c_char_p
-    for name in ("kg_snapshot_create", "kg_snapshot_synthetic", "kg_snapshot_info", "kg_synth_ids", "kg_check_batch",
+    for name in ("kg_snapshot_create", "kg_snapshot_synthetic", "kg_snapshot_info", "kg_snapshot_tune", "kg_synth_ids", "kg_check_batch",
                  "kg_check_batch_device", "kg_synth_queries", "kg_expand_batch"):
         getattr(L, name).restype = C.c_int
     _lib = L

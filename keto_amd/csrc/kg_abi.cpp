@@ -103,6 +103,18 @@ int kg_snapshot_info(const kg_snapshot* sp, uint64_t* info4) {
   return 0;
 }
 
+int kg_snapshot_tune(kg_snapshot* sp, const char* key, int64_t value) {
+  if (!sp || !key) return set_error(-2, "NULL argument");
+  Snapshot* s = reinterpret_cast<Snapshot*>(sp);
+  std::lock_guard<std::mutex> lk(s->mu);
+  if (strcmp(key, "tiers") == 0) {
+    if (value < 0 || value > 2) return set_error(-2, "tiers must be 0, 1 or 2");
+    s->tiers = (int)value;
+    return 0;
+  }
+  return set_error(-2, "unknown knob '%s'", key);
+}
+
 int kg_synth_ids(const kg_snapshot* sp, uint32_t* ids6) {
   if (!sp || !ids6) return set_error(-2, "NULL argument");
   const Snapshot* s = reinterpret_cast<const Snapshot*>(sp);

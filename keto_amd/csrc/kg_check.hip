@@ -44,9 +44,53 @@ struct Ctl {
   uint32_t medium_count, medium_head, light2_count, pad1;
   uint32_t heads[8 * 32];   // per-XCD dequeue heads, one 128-B line each (k_light<16>)
   uint32_t heads2[8 * 32];  // (k_light<64>)
+  uint32_t light8[8 * 32];  // per-XCD shard sizes of the light list (k_resolve appends)
   unsigned long long st[ST_N];
+  unsigned long long st8[8][16];  // per-XCD shards of the hot counters (block-reduced adds)
   InterpCtl ic;
 };
+
+// One device-scope atomic on a single word costs ~11 ns at the memory side and one word saturates
+// near 90 M updates/s (MI355X_MICROARCH.md, "dequeue"/"fanin"): counters and list appends are
+// reduced per workgroup and spread over 8 per-XCD shards.
+
+// Adds v[k] (summed over the workgroup) to counter shard (blockIdx & 7) of stat idx[k].
+// Every thread of the workgroup must call it.
+template <int N>
+__device__ void block_stats(Ctl* ctl, const int (&idx)[N], const unsigned long long (&v)[N]) {
+  __shared__ unsigned long long red[4][N];
+  const int lane = lane_id(), wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < N; k++) {
+    unsigned long long x = v[k];
+    for (int off = 32; off; off >>= 1) x += __shfl_xor(x, off, 64);
+    if (lane == 0) red[wave][k] = x;
+  }
+  __syncthreads();
+  if (threadIdx.x < N) {
+    const unsigned long long t = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+    if (t) atomicAdd(&ctl->st8[blockIdx.x & 7][idx[threadIdx.x]], t);
+  }
+  __syncthreads();
+}
+
+// Workgroup-aggregated append (one atomic per workgroup).  Every thread must call it.
+__device__ void block_append(bool pred, uint32_t val, uint32_t* list, uint32_t* count) {
+  __shared__ uint32_t wcnt[4], bbase;
+  const int lane = lane_id(), wave = threadIdx.x >> 6;
+  const uint64_t m = __ballot(pred);
+  if (lane == 0) wcnt[wave] = __popcll(m);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t t = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+    bbase = t ? atomicAdd(count, t) : 0u;
+  }
+  __syncthreads();
+  uint32_t off = bbase;
+  for (int w = 0; w < wave; w++) off += wcnt[w];
+  if (pred) list[off + lanes_below(m)] = val;
+  __syncthreads();
+}
 
 // ------------------------------------------------------------------ k_resolve
 __global__ __launch_bounds__(256) void k_resolve(DevSnap s, const kg_query* __restrict__ q, uint32_t n,
@@ -94,11 +138,14 @@ __global__ __launch_bounds__(256) void k_resolve(DevSnap s, const kg_query* __re
     }
   }
   {
-    const uint64_t probed = __ballot(valid && did_probe);
-    if (probed && lane_id() == 0) atomicAdd(&ctl->st[ST_PROBES], (unsigned long long)__popcll(probed));
+    const int idx[1] = {ST_PROBES};
+    const unsigned long long v[1] = {(valid && did_probe) ? 1ull : 0ull};
+    block_stats<1>(ctl, idx, v);
   }
-  wave_append(valid && route == ROUTE_LIGHT, i, light_list, &ctl->light_count);
-  wave_append(valid && route == ROUTE_GENERAL, i, gen_list, &ctl->gen_count);
+  // light list: 8 shards of capacity n (shard = blockIdx & 7), dequeued by k_light per XCD
+  const uint32_t h = blockIdx.x & 7;
+  block_append(valid && route == ROUTE_LIGHT, i, light_list + (size_t)h * n, &ctl->light8[h * 32]);
+  block_append(valid && route == ROUTE_GENERAL, i, gen_list, &ctl->gen_count);
 }
 
 // ------------------------------------------------------------------ k_light
@@ -231,14 +278,34 @@ __device__ __forceinline__ int light_query(const DevSnap& s, LightLds<W, VLOG2, 
   return g.ballot(h) ? BFS_M : BFS_N;
 }
 
-// Dequeue up to `want` consecutive work indices for a wave; per-XCD heads over [0, count) split
-// into 8 ranges.  Returns the first index (NONE when all ranges are drained) and the number taken.
-__device__ __forceinline__ uint32_t dequeue_n(uint32_t* heads, uint32_t count, uint32_t& head_sel, uint32_t head0,
+// A work list: either 8 shards (shard h = list[h*cap, h*cap + counts[32*h])) or one list of
+// counts[0] entries split into 8 ranges.  Range h is drained first by workgroups of XCD label h.
+struct WorkList {
+  const uint32_t* list;
+  const uint32_t* counts;
+  uint32_t cap;
+  uint32_t sharded;
+  __device__ void range(uint32_t h, uint32_t& b, uint32_t& e) const {
+    if (sharded) {
+      b = h * cap;
+      e = b + counts[h * 32];
+    } else {
+      const uint32_t c = counts[0];
+      b = (uint32_t)((uint64_t)c * h / 8);
+      e = (uint32_t)((uint64_t)c * (h + 1) / 8);
+    }
+  }
+};
+
+// Dequeue up to `want` consecutive work items for a wave from per-XCD heads.  Returns the first
+// list position (NONE when every range is drained) and the number taken.
+__device__ __forceinline__ uint32_t dequeue_n(const WorkList& wl, uint32_t* heads, uint32_t& head_sel, uint32_t head0,
                                               uint32_t want, uint32_t& got) {
   while (head_sel < head0 + 8) {
-    uint32_t h = head_sel & 7;
-    uint32_t lo = (uint32_t)((uint64_t)count * h / 8), hi = (uint32_t)((uint64_t)count * (h + 1) / 8);
-    uint32_t k = atomicAdd(&heads[h * 32], want);
+    const uint32_t h = head_sel & 7;
+    uint32_t lo, hi;
+    wl.range(h, lo, hi);
+    const uint32_t k = atomicAdd(&heads[h * 32], want);
     if (lo + k < hi) {
       got = min(want, hi - (lo + k));
       return lo + k;
@@ -253,8 +320,7 @@ __device__ __forceinline__ uint32_t dequeue_n(uint32_t* heads, uint32_t count, u
 // its overflow goes to k_light<64,...> (one query per wave, 4x the LDS), whose overflow goes to
 // the workgroup tier.  The groups of a wave advance in lockstep, one query each per round.
 template <int W, int VLOG2, int LIST>
-__global__ __launch_bounds__(256) void k_light(DevSnap s, const RQuery* __restrict__ rq,
-                                               const uint32_t* __restrict__ qlist, const uint32_t* count_p,
+__global__ __launch_bounds__(256) void k_light(DevSnap s, const RQuery* __restrict__ rq, WorkList wl,
                                                uint32_t* heads, uint8_t* __restrict__ out,
                                                uint32_t* __restrict__ err, uint32_t* next_list, uint32_t* next_count,
                                                Ctl* ctl) {
@@ -262,20 +328,19 @@ __global__ __launch_bounds__(256) void k_light(DevSnap s, const RQuery* __restri
   __shared__ LightLds<W, VLOG2, LIST> lds_all[G];
   const Group<W> g;
   LightLds<W, VLOG2, LIST>& L = lds_all[threadIdx.x / W];
-  const uint32_t count = *count_p;
   const uint32_t head0 = blockIdx.x & 7;  // XCD label (speed only, never correctness)
   uint32_t head_sel = head0;
   BfsStats bs;
   unsigned long long st_done = 0;
   for (;;) {
     uint32_t first = 0, got = 0;
-    if (g.lane == 0) first = dequeue_n(heads, count, head_sel, head0, GW, got);
+    if (g.lane == 0) first = dequeue_n(wl, heads, head_sel, head0, GW, got);
     first = __shfl(first, 0, 64);
     got = __shfl(got, 0, 64);
     if (first == NONE) break;
     const uint32_t gi = g.lane / W;
     if (gi < got) {
-      const uint32_t qi = qlist[first + gi];
+      const uint32_t qi = wl.list[first + gi];
       const RQuery q = rq[qi];
       const int r = light_query<W, VLOG2, LIST>(s, L, g, q, bs);
       __builtin_amdgcn_wave_barrier();
@@ -290,12 +355,13 @@ __global__ __launch_bounds__(256) void k_light(DevSnap s, const RQuery* __restri
       }
     }
   }
-  if (g.gl == 0) {  // the narrow tier has its own counters (roofline of k_light<16>); wide -> shared
-    atomicAdd(&ctl->st[W == 16 ? ST_LROWS : ST_ROWS], bs.rows);
-    atomicAdd(&ctl->st[W == 16 ? ST_LEDGES : ST_EDGES], bs.edges);
-    atomicAdd(&ctl->st[W == 16 ? ST_LPROBES : ST_PROBES], bs.probes);
-    if (st_done) atomicAdd(&ctl->st[ST_LIGHT], st_done);
-  }
+  // group-uniform counters: count each group once (its lane 0); the narrow tier has its own
+  // counters (roofline of k_light<16>), the wide tier adds to the shared ones
+  const bool lead = g.gl == 0;
+  const int idx[4] = {W == 16 ? ST_LROWS : ST_ROWS, W == 16 ? ST_LEDGES : ST_EDGES, W == 16 ? ST_LPROBES : ST_PROBES,
+                      ST_LIGHT};
+  const unsigned long long v[4] = {lead ? bs.rows : 0ull, lead ? bs.edges : 0ull, lead ? bs.probes : 0ull, st_done};
+  block_stats<4>(ctl, idx, v);
 }
 
 // ------------------------------------------------------------------ workgroup tiers
@@ -469,13 +535,9 @@ __device__ void wg_run(const DevSnap& s, St& st, WgShared& sh, const RQuery* __r
     }
     st.finish((uint32_t)min((uint64_t)sh.n, st.cap()), sh.over != 0);
   }
-  atomicAdd(&ctl->st[ST_ROWS], st_rows);  // per-thread counters (rows/probes counted per lane)
-  atomicAdd(&ctl->st[ST_PROBES], st_probes);
-  if (st_idx == ST_HEAVY) atomicAdd(&ctl->st[ST_FHBM], st_fh);
-  if (tid == 0) {
-    atomicAdd(&ctl->st[ST_EDGES], st_edges);
-    atomicAdd(&ctl->st[st_idx], st_done);
-  }
+  const int idx[5] = {ST_ROWS, ST_PROBES, ST_FHBM, ST_EDGES, st_idx};
+  const unsigned long long v[5] = {st_rows, st_probes, st_idx == ST_HEAVY ? st_fh : 0ull, st_edges, st_done};
+  block_stats<5>(ctl, idx, v);
 }
 
 __global__ __launch_bounds__(256) void k_medium(DevSnap s, const RQuery* __restrict__ rq, const uint32_t* qlist,
@@ -560,8 +622,8 @@ int check_batch_device(Snapshot* s, const kg_query* d_q, size_t n, int32_t globa
   if (n > 0x7FFFFFFFull) return set_error(-2, "batch too large");
   HIPC(hipSetDevice(s->device));
   if (!stream) stream = s->stream;
-  // scratch: rq[n] | light[n] | light2[n] | gen[n] | medium[n] | heavy[n] | giant[n] | p2[n] | Ctl
-  size_t off_rq = 0, off_light = align_up(off_rq + n * sizeof(RQuery)), off_light2 = align_up(off_light + n * 4),
+  // scratch: rq[n] | light[8n] (8 shards) | light2[n] | gen[n] | medium[n] | heavy[n] | giant[n] | p2[n] | Ctl
+  size_t off_rq = 0, off_light = align_up(off_rq + n * sizeof(RQuery)), off_light2 = align_up(off_light + 8 * n * 4),
          off_gen = align_up(off_light2 + n * 4),
          off_med = align_up(off_gen + n * 4), off_heavy = align_up(off_med + n * 4),
          off_giant = align_up(off_heavy + n * 4), off_p2 = align_up(off_giant + n * 4),
@@ -583,12 +645,9 @@ int check_batch_device(Snapshot* s, const kg_query* d_q, size_t n, int32_t globa
   uint32_t* giant = (uint32_t*)(base + off_giant);
   uint32_t* p2 = (uint32_t*)(base + off_p2);
   Ctl* ctl = (Ctl*)(base + off_ctl);
-  // heavy tier: KG_HEAVY_TIER=wg keeps the one-workgroup-per-query HBM tier (A/B measurement);
-  // the default is the grid tier (kg_grid.hip)
-  static const bool wg_heavy = [] {
-    const char* e = getenv("KG_HEAVY_TIER");
-    return e && strcmp(e, "wg") == 0;
-  }();
+  // tiers after k_light<64> (kg_snapshot_tune "tiers"): 0 grid; 1 LDS workgroup tier, then grid;
+  // 2 LDS workgroup tier, then HBM workgroup tier (one workgroup per query)
+  const bool use_medium = s->tiers >= 1, wg_heavy = s->tiers == 2;
   const uint64_t nn = std::max<uint32_t>(s->ds.n_nodes, 1);
   const uint64_t words = (nn + 31) / 32 + 1;
   const uint64_t cap_h = std::min<uint64_t>(nn, 4u << 20);
@@ -628,16 +687,20 @@ int check_batch_device(Snapshot* s, const kg_query* d_q, size_t n, int32_t globa
     // 7 workgroups of 4 waves per CU: ~21 KiB of LDS per workgroup allows 28 waves/CU
     const uint32_t light_grid = (uint32_t)std::min<uint64_t>((uint64_t)s->n_cu * 7, (n + 15) / 16 + 8);
     if (stats) HIPC(hipEventRecord(l0, stream));
-    hipLaunchKernelGGL((k_light<16, 7, 64>), dim3(light_grid), dim3(256), 0, stream, s->ds, rq, light,
-                       &ctl->light_count, ctl->heads, d_out, d_err, light2, &ctl->light2_count, ctl);
+    hipLaunchKernelGGL((k_light<16, 7, 64>), dim3(light_grid), dim3(256), 0, stream, s->ds, rq,
+                       WorkList{light, ctl->light8, (uint32_t)n, 1u}, ctl->heads, d_out, d_err, light2,
+                       &ctl->light2_count, ctl);
     HIPC(hipGetLastError());
     if (stats) HIPC(hipEventRecord(l1, stream));
-    hipLaunchKernelGGL((k_light<64, 9, 256>), dim3((uint32_t)s->n_cu * 4), dim3(256), 0, stream, s->ds, rq, light2,
-                       &ctl->light2_count, ctl->heads2, d_out, d_err, medium, &ctl->medium_count, ctl);
+    hipLaunchKernelGGL((k_light<64, 9, 256>), dim3((uint32_t)s->n_cu * 4), dim3(256), 0, stream, s->ds, rq,
+                       WorkList{light2, &ctl->light2_count, 0u, 0u}, ctl->heads2, d_out, d_err,
+                       use_medium ? medium : heavy, use_medium ? &ctl->medium_count : &ctl->heavy_count, ctl);
     HIPC(hipGetLastError());
-    hipLaunchKernelGGL(k_medium, dim3((uint32_t)s->n_cu * 3), dim3(256), 0, stream, s->ds, rq, medium,
-                       &ctl->medium_count, &ctl->medium_head, d_out, d_err, heavy, &ctl->heavy_count, ctl);
-    HIPC(hipGetLastError());
+    if (use_medium) {
+      hipLaunchKernelGGL(k_medium, dim3((uint32_t)s->n_cu * 3), dim3(256), 0, stream, s->ds, rq, medium,
+                         &ctl->medium_count, &ctl->medium_head, d_out, d_err, heavy, &ctl->heavy_count, ctl);
+      HIPC(hipGetLastError());
+    }
     if (wg_heavy) {
       hipLaunchKernelGGL(k_heavy, dim3(H), dim3(256), 0, stream, s->ds, rq, heavy, &ctl->heavy_count,
                          &ctl->heavy_head, d_out, d_err, hb, words, hl, cap_h, giant, &ctl->giant_count, ctl);
@@ -673,6 +736,8 @@ int check_batch_device(Snapshot* s, const kg_query* d_q, size_t n, int32_t globa
     hipEventDestroy(l1);
     Ctl h;
     HIPC(hipMemcpy(&h, ctl, sizeof(Ctl), hipMemcpyDeviceToHost));
+    for (int x = 0; x < 8; x++)
+      for (int k = 0; k < ST_N; k++) h.st[k] += h.st8[x][k];
     stats->rows_opened = h.st[ST_ROWS] + h.st[ST_LROWS];
     stats->edges_read = h.st[ST_EDGES] + h.st[ST_LEDGES];
     stats->direct_probes = h.st[ST_PROBES] + h.st[ST_LPROBES];

@@ -25,27 +25,50 @@ namespace kg {
 struct GridCtl {
   unsigned long long n;  // entries appended to the log
   uint32_t overflow, pad;
-  unsigned long long probes;
+  unsigned long long probes8[8][16];  // per-XCD shards (one 128-B line each)
 };
+
+// Visited sets of all slots in ONE open-addressing table of 64-bit keys
+//   epoch (16) | slot (16) | node (32)
+// Entries of older epochs (earlier rounds / batches) count as empty, so the table is never
+// cleared between rounds; it is zeroed once per 65535 rounds.  Within a round an entry never
+// changes once written, so a (possibly stale) plain load that shows this round's epoch is final.
+constexpr int GH_PROBES = 128;
+__device__ __forceinline__ int gh_insert(uint64_t* H, uint64_t mask, uint64_t key) {
+  const uint64_t ep = key >> 48;
+  uint64_t h = mix64(key & 0xFFFFFFFFFFFFull) & mask;
+  for (int p = 0; p < GH_PROBES; p++) {
+    uint64_t cur = H[h];
+    for (;;) {
+      if (cur == key) return 0;      // already visited
+      if ((cur >> 48) == ep) break;  // another key of this round: next slot
+      const uint64_t old = atomicCAS((unsigned long long*)&H[h], (unsigned long long)cur, (unsigned long long)key);
+      if (old == cur) return 1;      // inserted
+      cur = old;
+    }
+    h = (h + 1) & mask;
+  }
+  return -1;  // probe bound: the round is rerun with fewer slots
+}
 
 // Log entry j: F[j] = slot << 32 | node, RB[j] = first adjx index of node's set row, lens[j] = its
 // length.  Only nodes with a non-empty set row are marked and logged; leaves are probed wherever
 // they are reached (a probe does not depend on the depth it is made at, so this is exact).
 __global__ void k_grid_init(DevSnap s, const RQuery* __restrict__ rq, const uint32_t* __restrict__ qlist,
                             uint32_t base, uint32_t cnt, uint64_t* F, uint32_t* RB, uint64_t* lens, uint32_t* slot_q,
-                            uint32_t* slot_hit, uint32_t* bitmaps, uint64_t words, GridCtl* ctl) {
+                            uint32_t* slot_hit, uint64_t* H, uint64_t mask, uint64_t epoch, GridCtl* ctl) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i == 0) {
     ctl->n = cnt;
     ctl->overflow = 0;
-    ctl->probes = 0;
   }
+  if (i < 8 * 16) (&ctl->probes8[0][0])[i] = 0;
   if (i >= cnt) return;
   const uint32_t qi = qlist[base + i];
   const uint32_t root = rq[qi].node;
   slot_q[i] = qi;
   slot_hit[i] = 0;  // the root was already probed (k_resolve)
-  bitmaps[(size_t)i * words + (root >> 5)] |= 1u << (root & 31);
+  if (gh_insert(H, mask, (epoch << 48) | ((uint64_t)i << 32) | root) < 0) ctl->overflow = 1;
   F[i] = ((uint64_t)i << 32) | root;
   RB[i] = (uint32_t)s.adj_off[root];
   lens[i] = s.adj_off[root + 1] - s.adj_off[root];
@@ -69,9 +92,13 @@ __global__ __launch_bounds__(256) void k_grid_expand(DevSnap s, const RQuery* __
                                                      uint32_t* RB, uint64_t* lens, uint64_t lvl_b, uint64_t n,
                                                      const uint64_t* __restrict__ incl, uint64_t total, int level,
                                                      const uint32_t* __restrict__ slot_q, uint32_t* slot_hit,
-                                                     uint32_t* bitmaps, uint64_t words, uint64_t cap, GridCtl* ctl) {
+                                                     uint64_t* H, uint64_t mask, uint64_t epoch, uint64_t cap,
+                                                     GridCtl* ctl) {
   __shared__ uint64_t s_beg[GT + 1];
   __shared__ uint64_t s_j0, s_cnt;
+  __shared__ uint32_t s_wcnt[4];
+  __shared__ unsigned long long s_base;
+  const int wave = threadIdx.x >> 6;
   const int lane = lane_id();
   uint32_t probes = 0;
   for (uint64_t t0 = (uint64_t)blockIdx.x * GT; t0 < total; t0 += (uint64_t)gridDim.x * GT) {
@@ -117,8 +144,9 @@ __global__ __launch_bounds__(256) void k_grid_expand(DevSnap s, const RQuery* __
           cl = x.len;
           keep = cl > 0 && q.depth - level - 1 >= 2;  // child will itself be expanded
           if (keep) {
-            const uint32_t bit = 1u << (child & 31);
-            if (atomicOr(&bitmaps[(size_t)slot * words + (child >> 5)], bit) & bit) act = false;
+            const int ins = gh_insert(H, mask, (epoch << 48) | ((uint64_t)slot << 32) | child);
+            if (ins < 0) ctl->overflow = 1;
+            if (ins == 0) act = false;
           }
           if (act) {
             probes++;
@@ -126,29 +154,32 @@ __global__ __launch_bounds__(256) void k_grid_expand(DevSnap s, const RQuery* __
           }
         }
       }
+      // workgroup-aggregated append to the log: one atomic per 256 edges
       const bool app = act && keep;
       const uint64_t m = __ballot(app);
-      if (m) {  // wave-aggregated append to the log
-        const int leader = __ffsll((unsigned long long)m) - 1;
-        unsigned long long base = 0;
-        if (lane == leader) base = atomicAdd(&ctl->n, (unsigned long long)__popcll(m));
-        base = shfl64(base, leader);
-        if (app) {
-          const unsigned long long at = base + lanes_below(m);
-          if (at < cap) {
-            F[at] = ((uint64_t)slot << 32) | child;
-            RB[at] = cb;
-            lens[at] = cl;
-          } else {
-            ctl->overflow = 1;
-          }
+      if (lane == 0) s_wcnt[wave] = __popcll(m);
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        const uint32_t t = s_wcnt[0] + s_wcnt[1] + s_wcnt[2] + s_wcnt[3];
+        s_base = t ? atomicAdd(&ctl->n, (unsigned long long)t) : 0ull;
+      }
+      __syncthreads();
+      if (app) {
+        unsigned long long at = s_base + lanes_below(m);
+        for (int w = 0; w < wave; w++) at += s_wcnt[w];
+        if (at < cap) {
+          F[at] = ((uint64_t)slot << 32) | child;
+          RB[at] = cb;
+          lens[at] = cl;
+        } else {
+          ctl->overflow = 1;
         }
       }
+      __syncthreads();
     }
-    __syncthreads();
   }
   for (int off = 32; off; off >>= 1) probes += __shfl_xor(probes, off, 64);
-  if (lane == 0 && probes) atomicAdd(&ctl->probes, (unsigned long long)probes);
+  if (lane == 0 && probes) atomicAdd(&ctl->probes8[blockIdx.x & 7][wave], (unsigned long long)probes);
 }
 
 __global__ void k_grid_finish(const uint32_t* slot_q, const uint32_t* slot_hit, uint32_t cnt, uint8_t* out,
@@ -160,13 +191,6 @@ __global__ void k_grid_finish(const uint32_t* slot_q, const uint32_t* slot_hit, 
   if (err) err[qi] = KG_ERR_NONE;
 }
 
-__global__ void k_grid_clear(const uint64_t* F, uint64_t n, uint32_t* bitmaps, uint64_t words) {
-  for (uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j < n; j += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t f = F[j];
-    bitmaps[(size_t)(f >> 32) * words + ((uint32_t)f >> 5)] = 0u;
-  }
-}
-
 // Host driver: qlist / count live on the device (count is read back once).
 int grid_tier(Snapshot* s, const RQuery* rq, const uint32_t* qlist, const uint32_t* d_count, uint8_t* out,
               uint32_t* err, hipStream_t stream, GridStats* gs) {
@@ -175,23 +199,25 @@ int grid_tier(Snapshot* s, const RQuery* rq, const uint32_t* qlist, const uint32
   HIPC(hipStreamSynchronize(stream));
   if (count == 0) return 0;
   const uint64_t nn = std::max<uint32_t>(s->ds.n_nodes, 1);
-  const uint64_t words = (nn + 31) / 32 + 1;
-  // budget: <= 16 GiB of bitmaps, <= 1024 slots; log capacity >= n_nodes (a single query always fits)
-  const uint32_t G0 = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(1024, (16ull << 30) / (words * 4)));
+  // log capacity >= n_nodes (one slot alone always fits); hash >= 2x the log (load <= 0.5)
   const uint64_t cap = std::max<uint64_t>(nn + 1024, 64ull << 20);
-  const size_t need = (size_t)G0 * words * 4 + cap * (8 + 4 + 8 + 8) + (size_t)G0 * 8 + sizeof(GridCtl) + 4096;
+  uint64_t hcap = 1;
+  while (hcap < 2 * cap) hcap <<= 1;
+  const uint32_t G0 = 0xFFFF;  // slot field is 16 bits
+  const size_t need = hcap * 8 + cap * (8 + 4 + 8 + 8) + (size_t)G0 * 8 + sizeof(GridCtl) + 4096;
   if (need > s->grid_pool_bytes) {
     if (s->grid_pool) HIPC(hipFree(s->grid_pool));
     s->grid_pool = nullptr;
     s->grid_pool_bytes = 0;
     HIPC(hipMalloc(&s->grid_pool, need));
-    HIPC(hipMemsetAsync(s->grid_pool, 0, (size_t)G0 * words * 4, stream));  // bitmaps start (and stay) clear
+    HIPC(hipMemsetAsync(s->grid_pool, 0, hcap * 8, stream));  // epoch 0 = empty
     s->grid_pool_bytes = need;
+    s->grid_epoch = 0;
     s->grid_scan_tmp_bytes = 0;
   }
   char* p = (char*)s->grid_pool;
-  uint32_t* bitmaps = (uint32_t*)p;
-  p += (size_t)G0 * words * 4;
+  uint64_t* H = (uint64_t*)p;
+  p += hcap * 8;
   uint64_t* F = (uint64_t*)p;
   p += cap * 8;
   uint64_t* lens = (uint64_t*)p;
@@ -215,12 +241,19 @@ int grid_tier(Snapshot* s, const RQuery* rq, const uint32_t* qlist, const uint32
   uint32_t G = G0;
   for (uint32_t done = 0; done < count;) {
     const uint32_t cnt = std::min(G, count - done);
+    if (++s->grid_epoch == 0x10000) {  // epoch wrap: the table is zeroed once per 65535 rounds
+      HIPC(hipMemsetAsync(H, 0, hcap * 8, stream));
+      s->grid_epoch = 1;
+    }
+    const uint64_t epoch = s->grid_epoch;
     hipLaunchKernelGGL(k_grid_init, dim3((cnt + 255) / 256), dim3(256), 0, stream, s->ds, rq, qlist, done, cnt, F,
-                       RB, lens, slot_q, slot_hit, bitmaps, words, ctl);
+                       RB, lens, slot_q, slot_hit, H, hcap - 1, epoch, ctl);
     HIPC(hipGetLastError());
     uint64_t lvl_b = 0, lvl_e = cnt;
     GridCtl h{};
-    for (int level = 0; lvl_b < lvl_e; level++) {
+    HIPC(hipMemcpyAsync(&h, ctl, sizeof h, hipMemcpyDeviceToHost, stream));
+    HIPC(hipStreamSynchronize(stream));
+    for (int level = 0; lvl_b < lvl_e && !h.overflow; level++) {
       const uint64_t n = lvl_e - lvl_b;
       size_t tb = s->grid_scan_tmp_bytes;
       HIPC(hipcub::DeviceScan::InclusiveSum(s->grid_scan_tmp, tb, lens + lvl_b, incl, n, stream));
@@ -234,34 +267,26 @@ int grid_tier(Snapshot* s, const RQuery* rq, const uint32_t* qlist, const uint32
       }
       const uint32_t grid = (uint32_t)std::min<uint64_t>((uint64_t)s->n_cu * 8, (total + GT - 1) / GT);
       hipLaunchKernelGGL(k_grid_expand, dim3(grid), dim3(256), 0, stream, s->ds, rq, F, RB, lens, lvl_b, n, incl,
-                         total, level, slot_q, slot_hit, bitmaps, words, cap, ctl);
+                         total, level, slot_q, slot_hit, H, hcap - 1, epoch, cap, ctl);
       HIPC(hipGetLastError());
       HIPC(hipMemcpyAsync(&h, ctl, sizeof h, hipMemcpyDeviceToHost, stream));
       HIPC(hipStreamSynchronize(stream));
-      if (h.overflow) break;
       lvl_b = lvl_e;
       lvl_e = std::min<uint64_t>(h.n, cap);
     }
-    HIPC(hipMemcpyAsync(&h, ctl, sizeof h, hipMemcpyDeviceToHost, stream));
-    HIPC(hipStreamSynchronize(stream));
     hipLaunchKernelGGL(k_grid_finish, dim3((cnt + 255) / 256), dim3(256), 0, stream, slot_q, slot_hit, cnt, out, err,
                        &ctl->overflow);
     HIPC(hipGetLastError());
-    if (h.overflow) {
-      // some set bits have no log entry: clear the round's bitmaps wholesale, retry with fewer slots
-      HIPC(hipMemsetAsync(bitmaps, 0, (size_t)cnt * words * 4, stream));
-      if (G == 1) return set_error(KG_ERR_RESOURCE_CODE, "grid tier log overflow");
-      G = std::max<uint32_t>(1, G / 4);
+    if (h.overflow) {  // log or probe bound exceeded: rerun these queries with fewer slots
+      if (G == 1) return set_error(KG_ERR_RESOURCE_CODE, "grid tier capacity exceeded");
+      G = std::max<uint32_t>(1, std::min(G, cnt) / 4);
       continue;
     }
-    const uint64_t logged = std::min<uint64_t>(h.n, cap);
-    hipLaunchKernelGGL(k_grid_clear, dim3((uint32_t)std::min<uint64_t>(4096, (logged + 255) / 256)), dim3(256), 0,
-                       stream, F, logged, bitmaps, words);
-    HIPC(hipGetLastError());
     if (gs) {
-      gs->probes += h.probes;
+      for (int x = 0; x < 8; x++)
+        for (int k = 0; k < 16; k++) gs->probes += h.probes8[x][k];
       gs->done += cnt;
-      gs->logged += logged;
+      gs->logged += std::min<uint64_t>(h.n, cap);
     }
     done += cnt;
   }

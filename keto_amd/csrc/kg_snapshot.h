@@ -52,6 +52,8 @@ struct Snapshot {
   size_t grid_pool_bytes = 0;
   void* grid_scan_tmp = nullptr;
   size_t grid_scan_tmp_bytes = 0;
+  uint32_t grid_epoch = 0;
+  int tiers = 0;  // kg_snapshot_tune("tiers")  // grid tier visited-table epoch (kg_grid.hip)
   void* interp_pool = nullptr;
   size_t interp_pool_bytes = 0;
   uint64_t batch_seq = 0;

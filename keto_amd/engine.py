@@ -117,6 +117,10 @@ class Snapshot:
         _lib.check(_lib.load().kg_snapshot_info(self._h, _ptr(a)), "kg_snapshot_info")
         return {"nodes": int(a[0]), "rows": int(a[1]), "set_edges": int(a[2]), "device_bytes": int(a[3])}
 
+    def tune(self, key: str, value: int) -> None:
+        """Engine knobs (kg_snapshot_tune): "tiers" = 0 grid / 1 LDS workgroup + grid / 2 workgroup tiers."""
+        _lib.check(_lib.load().kg_snapshot_tune(self._h, key.encode(), int(value)), "kg_snapshot_tune")
+
     def synth_ids(self) -> dict:
         a = np.zeros(6, np.uint32)
         _lib.check(_lib.load().kg_synth_ids(self._h, _ptr(a)), "kg_synth_ids")

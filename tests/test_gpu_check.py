@@ -94,8 +94,10 @@ def test_heavy_path_overflow_star():
     assert e.last_stats["n_medium"] + e.last_stats["n_heavy"] >= 1
 
 
-def test_workgroup_tiers_lds_and_hbm():
-    # > 256 expanded nodes leaves the wave tier; > 4096 leaves the LDS workgroup tier for the HBM one
+@pytest.mark.parametrize("tiers", [0, 1, 2])
+def test_workgroup_tiers_lds_and_hbm(tiers):
+    # > 256 expanded nodes leaves the wave tiers; tiers=0 sends them to the grid tier, 1/2 first to
+    # the LDS workgroup tier (<= 4096 expanded nodes), then to the grid / HBM workgroup tier
     tuples = [RelationTuple.from_string(f"g:root#m@(g:c{i}#m)") for i in range(5000)]
     tuples += [RelationTuple.from_string(f"g:c{i}#m@(g:d{i % 1500}#m)") for i in range(5000)]
     tuples += [RelationTuple.from_string(f"g:d{i}#m@(g:e{i % 400}#m)") for i in range(1500)]
@@ -106,13 +108,14 @@ def test_workgroup_tiers_lds_and_hbm():
     tuples += [RelationTuple.from_string("g:h99#m@deep")]
     reg = Registry(tuples, [])
     e = reg.permission_engine()
+    e.snapshot.tune("tiers", tiers)
     it = reg.interner
     qs = [RelationTuple.from_string(s) for s in
           ["g:root#m@target", "g:root#m@mid", "g:root#m@none", "g:c3#m@target", "g:c7#m@mid", "g:d3#m@target",
            "g:r2#m@deep", "g:r2#m@none"]]
     q6 = np.asarray([it.tuple_ids(t) for t in qs], np.uint32)
     oracle = Oracle(it.tuples_array(tuples), it.wildcard_rel)
-    tiers = {"n_medium": 0, "n_heavy": 0}
+    tiers_mode, tiers = tiers, {"n_medium": 0, "n_heavy": 0}
     for gmax in (2, 3, 4, 5, 6):
         e.config.max_read_depth = gmax
         out, _ = e.batch_check_ids(queries_array(q6, 0), with_stats=True)
@@ -120,7 +123,7 @@ def test_workgroup_tiers_lds_and_hbm():
         assert list(out) == list(exp), (gmax, out, exp)
         for k in tiers:
             tiers[k] += e.last_stats[k]
-    assert tiers["n_medium"] >= 1 and tiers["n_heavy"] >= 1, tiers
+    assert tiers["n_heavy"] >= 1 and (tiers["n_medium"] >= 1) == (tiers_mode > 0), tiers
 
 
 def test_empty_and_unknown():
@@ -145,6 +148,7 @@ def test_synthetic_graph_vs_oracle(n_tuples, gmax):
     torch = _torch()
     from keto_amd import _lib
     snap = Snapshot.synthetic(n_tuples, seed=20250131)
+    snap.tune("tiers", 1 if gmax == 5 else 0)
     n = 20000
     dq = torch.empty((n, 7), dtype=torch.int32, device="cuda")
     _lib.check(_lib.load().kg_synth_queries(snap.handle, 7, n, dq.data_ptr()), "kg_synth_queries")
