@@ -70,6 +70,11 @@ __device__ __forceinline__ void wave_append(bool pred, uint32_t val, uint32_t* l
   if (pred) list[base + __popcll(m & ((1ull << lane) - 1))] = val;
 }
 
+__device__ __forceinline__ uint64_t shfl_up64(uint64_t v, int off) {
+  const uint32_t lo = __shfl_up((uint32_t)v, off, 64), hi = __shfl_up((uint32_t)(v >> 32), off, 64);
+  return ((uint64_t)hi << 32) | lo;
+}
+
 __device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
   uint32_t lo = __shfl((uint32_t)v, src, 64), hi = __shfl((uint32_t)(v >> 32), src, 64);
   return ((uint64_t)hi << 32) | lo;

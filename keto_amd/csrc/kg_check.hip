@@ -671,14 +671,10 @@ int check_batch_device(Snapshot* s, const kg_query* d_q, size_t n, int32_t globa
   }
   GridStats gs;
 
-  hipEvent_t e0 = nullptr, e1 = nullptr, l0 = nullptr, l1 = nullptr;
-  if (stats) {
-    HIPC(hipEventCreate(&e0));
-    HIPC(hipEventCreate(&e1));
-    HIPC(hipEventCreate(&l0));
-    HIPC(hipEventCreate(&l1));
-    HIPC(hipEventRecord(e0, stream));
-  }
+  if (stats && !s->ev[0])
+    for (auto& e : s->ev) HIPC(hipEventCreate(&e));
+  hipEvent_t e0 = s->ev[0], e1 = s->ev[1], l0 = s->ev[2], l1 = s->ev[3];
+  if (stats) HIPC(hipEventRecord(e0, stream));
   HIPC(hipMemsetAsync(ctl, 0, sizeof(Ctl), stream));
   if (n) {
     hipLaunchKernelGGL(k_resolve, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, stream, s->ds, d_q, (uint32_t)n,
@@ -709,7 +705,7 @@ int check_batch_device(Snapshot* s, const kg_query* d_q, size_t n, int32_t globa
                          &ctl->giant_head, d_out, d_err, gb, words, gl, nn, giant /*never overflows*/, &ctl->pad0,
                          ctl);
       HIPC(hipGetLastError());
-    } else if (int rc = grid_tier(s, rq, heavy, &ctl->heavy_count, d_out, d_err, stream, &gs)) {
+    } else if (int rc = grid_tier(s, rq, heavy, &ctl->heavy_count, global_max_depth, d_out, d_err, stream, &gs)) {
       return rc;
     }
     if (s->has_program) {
@@ -730,10 +726,6 @@ int check_batch_device(Snapshot* s, const kg_query* d_q, size_t n, int32_t globa
     float ms = 0, lms = 0;
     HIPC(hipEventElapsedTime(&ms, e0, e1));
     if (n) HIPC(hipEventElapsedTime(&lms, l0, l1));
-    hipEventDestroy(e0);
-    hipEventDestroy(e1);
-    hipEventDestroy(l0);
-    hipEventDestroy(l1);
     Ctl h;
     HIPC(hipMemcpy(&h, ctl, sizeof(Ctl), hipMemcpyDeviceToHost));
     for (int x = 0; x < 8; x++)

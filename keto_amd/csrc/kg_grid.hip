@@ -11,7 +11,6 @@
 // Semantics are those of k_light / k_medium (kg_check.hip): bounded reachability with every node
 // probed once at its shallowest depth.  A round that overflows the log is rerun with fewer slots.
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 
@@ -25,6 +24,8 @@ namespace kg {
 struct GridCtl {
   unsigned long long n;  // entries appended to the log
   uint32_t overflow, pad;
+  unsigned long long lvl_b, lvl_e, total;  // current level = log[lvl_b, lvl_e), its edge count
+  unsigned long long edges;                // edges over all levels (stats)
   unsigned long long probes8[8][16];  // per-XCD shards (one 128-B line each)
 };
 
@@ -61,6 +62,7 @@ __global__ void k_grid_init(DevSnap s, const RQuery* __restrict__ rq, const uint
   if (i == 0) {
     ctl->n = cnt;
     ctl->overflow = 0;
+    ctl->lvl_b = ctl->lvl_e = ctl->total = ctl->edges = 0;
   }
   if (i < 8 * 16) (&ctl->probes8[0][0])[i] = 0;
   if (i >= cnt) return;
@@ -84,13 +86,96 @@ __device__ __forceinline__ uint64_t first_above(const uint64_t* incl, uint64_t l
   return lo;
 }
 
+// ---- device-side level loop: no host round trip per level.
+// k_grid_advance: next level = entries logged by the previous one.
+__global__ void k_grid_advance(GridCtl* ctl, uint64_t cap) {
+  const unsigned long long e = ctl->n < cap ? ctl->n : cap;
+  ctl->lvl_b = ctl->lvl_e;
+  ctl->lvl_e = e;
+  ctl->total = 0;
+}
+
+// Inclusive scan of lens[lvl_b, lvl_e) -> incl[0, n) in three fixed-size launches (the level size
+// lives on the device): per-block chunk sums, one-block scan of the sums, per-block rescan.
+constexpr uint32_t SCAN_BLOCKS = 1024;
+
+__device__ __forceinline__ uint64_t block_sum64(uint64_t v, uint64_t* red) {
+  for (int off = 32; off; off >>= 1) v += __shfl_xor(v, off, 64);
+  if (lane_id() == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  const uint64_t t = red[0] + red[1] + red[2] + red[3];
+  __syncthreads();
+  return t;
+}
+
+__global__ __launch_bounds__(256) void k_grid_scan_reduce(const uint64_t* __restrict__ lens, const GridCtl* ctl,
+                                                          uint64_t* bsum) {
+  __shared__ uint64_t red[4];
+  const uint64_t lb = ctl->lvl_b, n = ctl->lvl_e - lb;
+  const uint64_t chunk = (n + SCAN_BLOCKS - 1) / SCAN_BLOCKS;
+  const uint64_t b0 = blockIdx.x * chunk, b1 = min(n, b0 + chunk);
+  uint64_t v = 0;
+  for (uint64_t j = b0 + threadIdx.x; j < b1; j += 256) v += lens[lb + j];
+  v = block_sum64(v, red);
+  if (threadIdx.x == 0) bsum[blockIdx.x] = v;
+}
+
+__global__ __launch_bounds__(SCAN_BLOCKS) void k_grid_scan_top(uint64_t* bsum, GridCtl* ctl) {
+  __shared__ uint64_t wsum[SCAN_BLOCKS / 64];
+  const int lane = lane_id(), wave = threadIdx.x >> 6;
+  const uint64_t x = bsum[threadIdx.x];
+  uint64_t v = x;
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint64_t y = shfl_up64(v, off);
+    if (lane >= off) v += y;
+  }
+  if (lane == 63) wsum[wave] = v;
+  __syncthreads();
+  uint64_t before = 0, tot = 0;
+  for (int w = 0; w < (int)(SCAN_BLOCKS / 64); w++) {
+    if (w < wave) before += wsum[w];
+    tot += wsum[w];
+  }
+  bsum[threadIdx.x] = before + v - x;  // exclusive block offsets
+  if (threadIdx.x == 0) {
+    ctl->total = tot;
+    ctl->edges += tot;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_grid_scan_apply(const uint64_t* __restrict__ lens, uint64_t* incl,
+                                                         const uint64_t* __restrict__ boff, const GridCtl* ctl) {
+  __shared__ uint64_t wsum[4];
+  const int lane = lane_id(), wave = threadIdx.x >> 6;
+  const uint64_t lb = ctl->lvl_b, n = ctl->lvl_e - lb;
+  const uint64_t chunk = (n + SCAN_BLOCKS - 1) / SCAN_BLOCKS;
+  const uint64_t b0 = blockIdx.x * chunk, b1 = min(n, b0 + chunk);
+  uint64_t carry = boff[blockIdx.x];
+  for (uint64_t t = b0; t < b1; t += 256) {
+    const uint64_t j = t + threadIdx.x;
+    const uint64_t x = j < b1 ? lens[lb + j] : 0;
+    uint64_t v = x;
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint64_t y = shfl_up64(v, off);
+      if (lane >= off) v += y;
+    }
+    if (lane == 63) wsum[wave] = v;
+    __syncthreads();
+    uint64_t before = carry;
+    for (int w = 0; w < wave; w++) before += wsum[w];
+    if (j < b1) incl[j] = before + v;
+    carry += wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    __syncthreads();
+  }
+}
+
 // One thread per edge of the level, in tiles of GT edges per workgroup: the tile's entries'
 // row starts are staged in LDS so each edge finds its entry with an LDS binary search.
 constexpr uint32_t GT = 2048;
 
 __global__ __launch_bounds__(256) void k_grid_expand(DevSnap s, const RQuery* __restrict__ rq, uint64_t* F,
-                                                     uint32_t* RB, uint64_t* lens, uint64_t lvl_b, uint64_t n,
-                                                     const uint64_t* __restrict__ incl, uint64_t total, int level,
+                                                     uint32_t* RB, uint64_t* lens,
+                                                     const uint64_t* __restrict__ incl, int level,
                                                      const uint32_t* __restrict__ slot_q, uint32_t* slot_hit,
                                                      uint64_t* H, uint64_t mask, uint64_t epoch, uint64_t cap,
                                                      GridCtl* ctl) {
@@ -100,6 +185,7 @@ __global__ __launch_bounds__(256) void k_grid_expand(DevSnap s, const RQuery* __
   __shared__ unsigned long long s_base;
   const int wave = threadIdx.x >> 6;
   const int lane = lane_id();
+  const uint64_t lvl_b = ctl->lvl_b, n = ctl->lvl_e - lvl_b, total = ctl->total;
   uint32_t probes = 0;
   for (uint64_t t0 = (uint64_t)blockIdx.x * GT; t0 < total; t0 += (uint64_t)gridDim.x * GT) {
     const uint64_t t1 = t0 + GT < total ? t0 + GT : total;
@@ -192,8 +278,8 @@ __global__ void k_grid_finish(const uint32_t* slot_q, const uint32_t* slot_hit, 
 }
 
 // Host driver: qlist / count live on the device (count is read back once).
-int grid_tier(Snapshot* s, const RQuery* rq, const uint32_t* qlist, const uint32_t* d_count, uint8_t* out,
-              uint32_t* err, hipStream_t stream, GridStats* gs) {
+int grid_tier(Snapshot* s, const RQuery* rq, const uint32_t* qlist, const uint32_t* d_count, int global_max_depth,
+              uint8_t* out, uint32_t* err, hipStream_t stream, GridStats* gs) {
   uint32_t count = 0;
   HIPC(hipMemcpyAsync(&count, d_count, 4, hipMemcpyDeviceToHost, stream));
   HIPC(hipStreamSynchronize(stream));
@@ -204,7 +290,7 @@ int grid_tier(Snapshot* s, const RQuery* rq, const uint32_t* qlist, const uint32
   uint64_t hcap = 1;
   while (hcap < 2 * cap) hcap <<= 1;
   const uint32_t G0 = 0xFFFF;  // slot field is 16 bits
-  const size_t need = hcap * 8 + cap * (8 + 4 + 8 + 8) + (size_t)G0 * 8 + sizeof(GridCtl) + 4096;
+  const size_t need = hcap * 8 + cap * (8 + 4 + 8 + 8) + (size_t)G0 * 8 + sizeof(GridCtl) + SCAN_BLOCKS * 8 + 4096;
   if (need > s->grid_pool_bytes) {
     if (s->grid_pool) HIPC(hipFree(s->grid_pool));
     s->grid_pool = nullptr;
@@ -213,7 +299,6 @@ int grid_tier(Snapshot* s, const RQuery* rq, const uint32_t* qlist, const uint32
     HIPC(hipMemsetAsync(s->grid_pool, 0, hcap * 8, stream));  // epoch 0 = empty
     s->grid_pool_bytes = need;
     s->grid_epoch = 0;
-    s->grid_scan_tmp_bytes = 0;
   }
   char* p = (char*)s->grid_pool;
   uint64_t* H = (uint64_t*)p;
@@ -230,14 +315,7 @@ int grid_tier(Snapshot* s, const RQuery* rq, const uint32_t* qlist, const uint32
   uint32_t* slot_hit = slot_q + G0;
   p += (size_t)G0 * 8;
   GridCtl* ctl = (GridCtl*)(((uintptr_t)p + 255) & ~uintptr_t(255));
-  // scan scratch sized for the largest level (cap entries)
-  size_t tmp_bytes = 0;
-  HIPC(hipcub::DeviceScan::InclusiveSum(nullptr, tmp_bytes, lens, incl, cap, stream));
-  if (tmp_bytes > s->grid_scan_tmp_bytes) {
-    if (s->grid_scan_tmp) HIPC(hipFree(s->grid_scan_tmp));
-    HIPC(hipMalloc(&s->grid_scan_tmp, tmp_bytes + 256));
-    s->grid_scan_tmp_bytes = tmp_bytes;
-  }
+  uint64_t* bsum = (uint64_t*)(((uintptr_t)(ctl + 1) + 255) & ~uintptr_t(255));  // SCAN_BLOCKS
   uint32_t G = G0;
   for (uint32_t done = 0; done < count;) {
     const uint32_t cnt = std::min(G, count - done);
@@ -249,30 +327,30 @@ int grid_tier(Snapshot* s, const RQuery* rq, const uint32_t* qlist, const uint32
     hipLaunchKernelGGL(k_grid_init, dim3((cnt + 255) / 256), dim3(256), 0, stream, s->ds, rq, qlist, done, cnt, F,
                        RB, lens, slot_q, slot_hit, H, hcap - 1, epoch, ctl);
     HIPC(hipGetLastError());
-    uint64_t lvl_b = 0, lvl_e = cnt;
+    // Levels run back to back on the device (sizes never come back to the host); the host looks
+    // at the log once per LEVELS_PER_SYNC levels to stop early on an empty level or an overflow.
+    // Level k expands nodes at rest depth D-k >= 2, so at most global_max_depth-1 levels exist.
+    constexpr int LEVELS_PER_SYNC = 16;
+    const int max_levels = std::max(1, global_max_depth - 1);
     GridCtl h{};
-    HIPC(hipMemcpyAsync(&h, ctl, sizeof h, hipMemcpyDeviceToHost, stream));
-    HIPC(hipStreamSynchronize(stream));
-    for (int level = 0; lvl_b < lvl_e && !h.overflow; level++) {
-      const uint64_t n = lvl_e - lvl_b;
-      size_t tb = s->grid_scan_tmp_bytes;
-      HIPC(hipcub::DeviceScan::InclusiveSum(s->grid_scan_tmp, tb, lens + lvl_b, incl, n, stream));
-      uint64_t total = 0;
-      HIPC(hipMemcpyAsync(&total, incl + n - 1, 8, hipMemcpyDeviceToHost, stream));
-      HIPC(hipStreamSynchronize(stream));
-      if (total == 0) break;
-      if (gs) {
-        gs->rows += n;
-        gs->edges += total;
+    for (int level = 0; level < max_levels;) {
+      const int stop = std::min(max_levels, level + LEVELS_PER_SYNC);
+      for (; level < stop; level++) {
+        hipLaunchKernelGGL(k_grid_advance, dim3(1), dim3(1), 0, stream, ctl, cap);
+        hipLaunchKernelGGL(k_grid_scan_reduce, dim3(SCAN_BLOCKS), dim3(256), 0, stream, lens, ctl, bsum);
+        hipLaunchKernelGGL(k_grid_scan_top, dim3(1), dim3(SCAN_BLOCKS), 0, stream, bsum, ctl);
+        hipLaunchKernelGGL(k_grid_scan_apply, dim3(SCAN_BLOCKS), dim3(256), 0, stream, lens, incl, bsum, ctl);
+        hipLaunchKernelGGL(k_grid_expand, dim3((uint32_t)s->n_cu * 8), dim3(256), 0, stream, s->ds, rq, F, RB, lens,
+                           incl, level, slot_q, slot_hit, H, hcap - 1, epoch, cap, ctl);
+        HIPC(hipGetLastError());
       }
-      const uint32_t grid = (uint32_t)std::min<uint64_t>((uint64_t)s->n_cu * 8, (total + GT - 1) / GT);
-      hipLaunchKernelGGL(k_grid_expand, dim3(grid), dim3(256), 0, stream, s->ds, rq, F, RB, lens, lvl_b, n, incl,
-                         total, level, slot_q, slot_hit, H, hcap - 1, epoch, cap, ctl);
-      HIPC(hipGetLastError());
       HIPC(hipMemcpyAsync(&h, ctl, sizeof h, hipMemcpyDeviceToHost, stream));
       HIPC(hipStreamSynchronize(stream));
-      lvl_b = lvl_e;
-      lvl_e = std::min<uint64_t>(h.n, cap);
+      if (h.overflow || std::min<uint64_t>(h.n, cap) == h.lvl_e) break;  // next level empty
+    }
+    if (gs) {
+      gs->rows += std::min<uint64_t>(h.n, cap);
+      gs->edges += h.edges;
     }
     hipLaunchKernelGGL(k_grid_finish, dim3((cnt + 255) / 256), dim3(256), 0, stream, slot_q, slot_hit, cnt, out, err,
                        &ctl->overflow);

@@ -48,11 +48,10 @@ struct Snapshot {
   size_t scratch_bytes = 0;
   void* heavy_pool = nullptr;
   size_t heavy_pool_bytes = 0;
-  void* grid_pool = nullptr;  // grid tier: bitmaps | log | lens | offs | slots | ctl
+  void* grid_pool = nullptr;  // grid tier: visited hash | log | slots | ctl | scan sums
   size_t grid_pool_bytes = 0;
-  void* grid_scan_tmp = nullptr;
-  size_t grid_scan_tmp_bytes = 0;
   uint32_t grid_epoch = 0;
+  hipEvent_t ev[4] = {};  // batch timing events (created on first use)
   int tiers = 0;  // kg_snapshot_tune("tiers")  // grid tier visited-table epoch (kg_grid.hip)
   void* interp_pool = nullptr;
   size_t interp_pool_bytes = 0;

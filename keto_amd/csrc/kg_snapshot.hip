@@ -136,7 +136,8 @@ Snapshot::~Snapshot() {
   if (scratch) hipFree(scratch);
   if (heavy_pool) hipFree(heavy_pool);
   if (grid_pool) hipFree(grid_pool);
-  if (grid_scan_tmp) hipFree(grid_scan_tmp);
+  for (auto& e : ev)
+    if (e) hipEventDestroy(e);
   if (interp_pool) hipFree(interp_pool);
   if (stream) hipStreamDestroy(stream);
 }

@@ -2,11 +2,11 @@ set -u
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
 python -c "import __graft_entry__ as g; g.build()" > gpurun_out/build.log 2>&1 || exit 4
-timeout -k 10 400 python -m pytest tests -m gpu -q -rs -x > gpurun_out/pytest8.log 2>&1; rc=$?; echo "pytest rc=$rc"
+timeout -k 10 400 python -m pytest tests -m gpu -q -rs -x > gpurun_out/pytest9.log 2>&1; rc=$?; echo "pytest rc=$rc"
 if [ $rc -ne 0 ]; then exit $rc; fi
-for t in 0 1 2; do
-timeout -k 10 200 python bench.py --tiers $t --tuples 1e9 --steps 5 --warmup 1 --cpu-seconds 0 > gpurun_out/bench_1b_t$t.log 2>&1; rc=$?; echo "bench1b tiers=$t rc=$rc"
+for t in 0 1; do
+timeout -k 10 200 python bench.py --tiers $t --tuples 1e9 --steps 5 --warmup 1 --cpu-seconds 0 > gpurun_out/bench_1b_i_t$t.log 2>&1; rc=$?; echo "bench1b tiers=$t rc=$rc"
 if [ $rc -ne 0 ]; then exit $rc; fi
 done
-timeout -k 10 240 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_1b_h -o run --output-format csv -- python3 bench.py --tuples 1e9 --steps 5 --warmup 1 --cpu-seconds 0 > gpurun_out/prof_1b_h.log 2>&1; rc=$?; echo "prof rc=$rc"
+timeout -k 10 240 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_1b_i -o run --output-format csv -- python3 bench.py --tuples 1e9 --steps 5 --warmup 1 --cpu-seconds 0 > gpurun_out/prof_1b_i.log 2>&1; rc=$?; echo "prof rc=$rc"
 exit $rc
