@@ -32,8 +32,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--tuples", type=float, default=1e9, help="synthetic graph size (tuples)")
     ap.add_argument("--batch", type=int, default=1_000_000, help="checks per step per GPU")
     ap.add_argument("--global-depth", type=int, default=10)
@@ -196,7 +196,7 @@ def main():
         "gteps": edges / elapsed / 1e9,
         "p99_batch_ms": float(np.percentile(np.array(lat) * 1e3, 99)),
         "allowed_fraction": float(res.mean()),
-        "tiers": {"light": int(stats[-1].n_light), "medium": int(stats[-1].n_medium),
+        "tiers": {"light": int(stats[-1].n_light), "wide": int(stats[-1].n_wide), "medium": int(stats[-1].n_medium),
                   "heavy": int(stats[-1].n_heavy), "general": int(stats[-1].n_general)},
         "work_per_batch": {"light": {"rows": int(stats[-1].light_rows_opened), "edges": int(stats[-1].light_edges_read),
                                      "probes": int(stats[-1].light_probes)},

@@ -97,7 +97,9 @@ typedef struct {
   uint64_t n_medium;
   uint64_t light_rows_opened, light_edges_read, light_probes; /* k_light's share of the counters */
   double kernel_ms;                     /* device time of the whole batch (HIP events)  */
-  double light_ms;                      /* device time of the k_light launch             */
+  double light_ms;                      /* device time of the k_light<16> launch         */
+  uint64_t n_wide;                      /* queries handed from k_light<16> to k_light<64> */
+  uint64_t n_grid;                      /* queries resolved by the grid tier             */
 } kg_stats;
 
 /* Per-query outputs of kg_check_batch. */
@@ -157,7 +159,9 @@ void kg_snapshot_destroy(kg_snapshot* s);
 int kg_snapshot_info(const kg_snapshot* s, uint64_t* info4);
 /* Engine knobs (no reference counterpart; tuning and tests).  key "tiers": where queries that
  * overflow the wave tiers go -- 0 = grid tier (default), 1 = LDS workgroup tier then grid tier,
- * 2 = LDS workgroup tier then one-workgroup-per-query HBM tier.  Results never depend on it. */
+ * 2 = LDS workgroup tier then one-workgroup-per-query HBM tier.  key "light": the first wave
+ * tier -- 0 = k_stream (many queries per wave over one FIFO, default), 1 = k_light<16> (four
+ * 16-lane groups per wave).  Results never depend on either. */
 int kg_snapshot_tune(kg_snapshot* s, const char* key, int64_t value);
 /* Synthetic layout: ids6 = {n_docs, n_groups, n_users, n_folders, user_obj0, folder_obj0}
  * (doc d = object d, group g = object n_docs+g, user u = object user_obj0+u). */
@@ -176,7 +180,9 @@ int kg_snapshot_export_csr(const kg_snapshot* s, uint64_t* row_off, uint32_t* ro
 int kg_check_batch(kg_snapshot* s, const kg_query* q, size_t n, int32_t global_max_depth, uint8_t* out,
                    uint32_t* err_code, kg_stats* stats);
 /* Device-resident variant: d_q / d_out / d_err are device pointers (HBM), stream is a
- * hipStream_t (NULL = the snapshot's stream).  Asynchronous unless stats != NULL. */
+ * hipStream_t (NULL = the snapshot's stream).  Returns once the batch is enqueued; when queries
+ * reach the grid tier the call waits for the wave tiers (the grid tier's size is read back), and
+ * with stats != NULL it waits for the whole batch. */
 int kg_check_batch_device(kg_snapshot* s, const kg_query* d_q, size_t n, int32_t global_max_depth,
                           uint8_t* d_out, uint32_t* d_err, kg_stats* stats, void* stream);
 /* Device-side synthetic check batch for a synthetic snapshot: 50% positive (reverse walks) and

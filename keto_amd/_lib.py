@@ -43,7 +43,8 @@ class kg_stats(C.Structure):
     _fields_ = [("rows_opened", C.c_uint64), ("edges_read", C.c_uint64), ("direct_probes", C.c_uint64),
                 ("frontier_hbm", C.c_uint64), ("n_light", C.c_uint64), ("n_heavy", C.c_uint64),
                 ("n_general", C.c_uint64), ("n_medium", C.c_uint64), ("light_rows_opened", C.c_uint64), ("light_edges_read", C.c_uint64),
-                ("light_probes", C.c_uint64), ("kernel_ms", C.c_double), ("light_ms", C.c_double)]
+                ("light_probes", C.c_uint64), ("kernel_ms", C.c_double), ("light_ms", C.c_double),
+                ("n_wide", C.c_uint64), ("n_grid", C.c_uint64)]
 
     def as_dict(self) -> dict:
         return {n: getattr(self, n) for n, _ in self._fields_}

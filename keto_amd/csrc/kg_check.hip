@@ -364,6 +364,238 @@ __global__ __launch_bounds__(256) void k_light(DevSnap s, const RQuery* __restri
   block_stats<4>(ctl, idx, v);
 }
 
+// ------------------------------------------------------------------ k_stream
+// The stream tier: one wave runs up to Q queries at once over ONE FIFO of row entries
+// (adjx begin, length, slot | generation | rest depth).  Every step takes the next 64 edges from
+// the FIFO head -- whatever queries they belong to -- so lanes stay busy however small the
+// queries are, and a finished query's slot is refilled at once (no lockstep rounds).
+//   * per query, FIFO order is BFS order (children are appended after every entry of the
+//     current level), so first-mark dedup marks each node at its shallowest depth, exactly as in
+//     k_light; the visited hash of a slot holds its expanded nodes
+//   * children found in one step are probed (checkDirect) in the next, together with that
+//     step's adjx loads: one HBM round trip per step for both
+//   * a query ends on a hit (IsMember), when it has no FIFO entry and no pending probe left
+//     (NotMember), or on overflow (visited cap, FIFO full, a row longer than LONG_ROW), which
+//     hands it to the next tier to be redone there
+//   * a finished slot bumps its generation: its FIFO entries and pending probes become stale
+constexpr uint32_t LONG_ROW = 2048;  // rows longer than this go to a wider tier
+constexpr uint32_t SF_HIT = 1, SF_OVER = 2;
+
+template <int Q, int VLOG2, int QC>
+struct StreamLds {
+  static constexpr int VIS = 1 << VLOG2;
+  uint32_t vis[Q * VIS];
+  uint32_t e_beg[QC], e_len[QC], e_meta[QC];  // meta = slot (4) | generation (12) | rest depth (16)
+  uint32_t pref[64];
+  uint32_t s_qi[Q], s_subj[Q], s_gen[Q], s_cnt[Q], s_ins[Q], s_flag[Q];
+};
+
+// 1 inserted, 0 present, -1 table full (bounded)
+template <int VLOG2>
+__device__ __forceinline__ int lx_insert3(uint32_t* vis, uint32_t key) {
+  constexpr uint32_t VIS = 1u << VLOG2;
+  uint32_t h = (key * 2654435761u) >> (32 - VLOG2);
+  for (uint32_t p = 0; p < VIS; p++) {
+    const uint32_t old = atomicCAS(&vis[h], NONE, key);
+    if (old == NONE) return 1;
+    if (old == key) return 0;
+    h = (h + 1) & (VIS - 1);
+  }
+  return -1;
+}
+
+__device__ __forceinline__ uint32_t wave_or(uint32_t v) {
+  for (int off = 32; off; off >>= 1) v |= __shfl_xor(v, off, 64);
+  return v;
+}
+
+template <int Q, int VLOG2, int QC>
+__global__ __launch_bounds__(256) void k_stream(DevSnap s, const RQuery* __restrict__ rq, WorkList wl,
+                                                uint32_t* heads, uint8_t* __restrict__ out,
+                                                uint32_t* __restrict__ err, uint32_t* next_list,
+                                                uint32_t* next_count, Ctl* ctl) {
+  using Lds = StreamLds<Q, VLOG2, QC>;
+  constexpr int VIS = Lds::VIS;
+  constexpr uint32_t INS_CAP = VIS * 5 / 8;  // expanded nodes per query (hash load <= 5/8)
+  static_assert(Q <= 16 && Q <= 64, "slot field is 4 bits");
+  __shared__ Lds lds_all[4];
+  Lds& L = lds_all[threadIdx.x >> 6];
+  const int lane = lane_id();
+  const uint32_t head0 = blockIdx.x & 7;  // XCD label (speed only, never correctness)
+  uint32_t head_sel = head0;
+  for (int i = lane; i < Q * VIS; i += 64) L.vis[i] = NONE;
+  if (lane < Q) {
+    L.s_gen[lane] = 0;
+    L.s_flag[lane] = 0;
+    L.s_cnt[lane] = 0;
+    L.s_ins[lane] = 0;
+  }
+  __builtin_amdgcn_wave_barrier();
+  uint32_t active = 0;  // wave-uniform: slots holding a query
+  bool drained = false;
+  uint32_t head = 0, tail = 0, head_off = 0;
+  bool pend = false;  // per lane: a child of the previous step awaiting its probe
+  uint32_t pend_node = 0, pend_slot = 0, pend_gen = 0;
+  unsigned long long st_rows = 0, st_edges = 0, st_probes = 0, st_done = 0;
+  for (;;) {
+    // ---- refill free slots (their root entries need FIFO room)
+    const uint32_t freem = ~active & ((1u << Q) - 1);
+    const uint32_t want = __popc(freem);
+    if (want && !drained && (tail - head) + want <= QC) {
+      uint32_t first = 0, got = 0;
+      if (lane == 0) first = dequeue_n(wl, heads, head_sel, head0, want, got);
+      first = __shfl(first, 0, 64);
+      got = __shfl(got, 0, 64);
+      if (first == NONE) {
+        drained = true;
+      } else {
+        uint32_t slot = 0;
+        if ((uint32_t)lane < got) {
+          uint32_t m = freem;
+          for (int k = 0; k < lane; k++) m &= m - 1;
+          slot = __ffs(m) - 1;
+          const uint32_t qi = wl.list[first + lane];
+          const RQuery q = rq[qi];
+          const uint32_t gen = L.s_gen[slot];
+          const bool over = q.depth > 0xFFFF || q.len > LONG_ROW;
+          L.s_qi[slot] = qi;
+          L.s_subj[slot] = q.subj;
+          L.s_flag[slot] = over ? SF_OVER : 0u;
+          L.s_cnt[slot] = 1;
+          L.s_ins[slot] = 1;
+          lx_insert3<VLOG2>(&L.vis[slot * VIS], q.node);
+          const uint32_t at = (tail + lane) % QC;
+          L.e_beg[at] = q.beg;
+          L.e_len[at] = over ? 0u : q.len;
+          L.e_meta[at] = (slot << 28) | ((gen & 0xFFF) << 16) | (uint32_t)(over ? 2 : q.depth);
+        }
+        active |= wave_or((uint32_t)lane < got ? 1u << slot : 0u);
+        tail += got;
+      }
+    }
+    if (active == 0 && (drained || tail == head)) {
+      if (drained) break;
+      continue;
+    }
+    __builtin_amdgcn_wave_barrier();
+    // ---- window: up to 64 FIFO entries from the head
+    const uint32_t avail = tail - head;
+    uint32_t ebeg = 0, elen = 0, emeta = 0;
+    bool live = false;
+    if ((uint32_t)lane < avail) {
+      const uint32_t at = (head + lane) % QC;
+      emeta = L.e_meta[at];
+      const uint32_t sl = emeta >> 28;
+      live = ((active >> sl) & 1) && ((emeta >> 16) & 0xFFF) == (L.s_gen[sl] & 0xFFF) &&
+             (L.s_flag[sl] & (SF_HIT | SF_OVER)) == 0;
+      ebeg = L.e_beg[at];
+      elen = live ? L.e_len[at] : 0u;
+      if (lane == 0) {
+        ebeg += head_off;
+        elen = live ? elen - head_off : 0u;
+      }
+    }
+    uint32_t total;
+    const uint32_t excl = wave_excl_scan(elen, &total);
+    L.pref[lane] = excl;
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t taken = min(total, 64u);
+    const bool consumed = (uint32_t)lane < avail && excl + elen <= taken;
+    const uint32_t ncons = __popcll(__ballot(consumed));  // a prefix of the window
+    if (consumed && live) {
+      atomicSub(&L.s_cnt[emeta >> 28], 1u);
+      st_rows++;
+    }
+    {
+      const uint32_t ex_n = __shfl(excl, ncons & 63, 64);
+      if (ncons < avail && ncons < 64 && ex_n < taken) head_off = (ncons == 0 ? head_off : 0u) + (taken - ex_n);
+      else if (ncons > 0) head_off = 0;
+    }
+    // ---- this step's edges; previous step's probes in flight together with them
+    const bool act = (uint32_t)lane < taken;
+    const int own = act ? owner_search(L.pref, 64, (uint32_t)lane) : 0;
+    const uint32_t ob = __shfl(ebeg, own, 64);
+    const uint32_t om = __shfl(emeta, own, 64);
+    AdjX x{NONE, 0, 0, 0};
+    if (act) x = s.adjx[ob + ((uint32_t)lane - L.pref[own])];
+    const bool pvalid = pend && L.s_gen[pend_slot] == pend_gen;
+    const bool h = pvalid && dset_probe(s, pend_node, L.s_subj[pend_slot]);
+    st_probes += pvalid ? 1 : 0;
+    if (h) atomicOr(&L.s_flag[pend_slot], SF_HIT);
+    head += ncons;
+    st_edges += (lane == 0) ? taken : 0u;
+    // ---- children: kept (rest >= 2, non-empty set row) ones are marked + appended; every new
+    // child is probed next step
+    const uint32_t slot = om >> 28, d = om & 0xFFFF;
+    const bool keepc = act && d >= 3 && x.len > 0;
+    bool fresh = false;
+    if (keepc) {
+      const int r = x.len > LONG_ROW ? -1 : lx_insert3<VLOG2>(&L.vis[slot * VIS], x.node);
+      if (r != 0) {
+        const uint32_t k = r > 0 ? atomicAdd(&L.s_ins[slot], 1u) : INS_CAP;
+        if (k >= INS_CAP) atomicOr(&L.s_flag[slot], SF_OVER);
+        else fresh = true;
+      }
+    }
+    const uint64_t am = __ballot(fresh);
+    const uint32_t room = QC - (tail - head);
+    const uint32_t pos = __popcll(am & ((1ull << lane) - 1));
+    bool appended = false;
+    if (fresh) {
+      if (pos < room) {
+        const uint32_t at = (tail + pos) % QC;
+        L.e_beg[at] = x.begin;
+        L.e_len[at] = x.len;
+        L.e_meta[at] = (om & 0xFFFF0000u) | (d - 1);
+        atomicAdd(&L.s_cnt[slot], 1u);
+        appended = true;
+      } else {
+        atomicOr(&L.s_flag[slot], SF_OVER);
+      }
+    }
+    tail += min((uint32_t)__popcll(am), room);
+    pend = act && (keepc ? appended : true);
+    pend_node = x.node;
+    pend_slot = slot;
+    pend_gen = act ? L.s_gen[slot] : 0u;
+    // ---- finished queries
+    const uint32_t pslots = wave_or(pend ? 1u << slot : 0u);
+    __builtin_amdgcn_wave_barrier();
+    bool done = false;
+    if (lane < Q && ((active >> lane) & 1)) {
+      const uint32_t f = L.s_flag[lane];
+      if (f & SF_HIT) {
+        done = true;
+        out[L.s_qi[lane]] = KG_IS_MEMBER;
+        if (err) err[L.s_qi[lane]] = KG_ERR_NONE;
+        st_done++;
+      } else if (f & SF_OVER) {
+        done = true;
+        next_list[atomicAdd(next_count, 1u)] = L.s_qi[lane];
+      } else if (L.s_cnt[lane] == 0 && !((pslots >> lane) & 1)) {
+        done = true;
+        out[L.s_qi[lane]] = KG_NOT_MEMBER;
+        if (err) err[L.s_qi[lane]] = KG_ERR_NONE;
+        st_done++;
+      }
+      if (done) L.s_gen[lane]++;  // stale: its FIFO entries and pending probes
+    }
+    const uint32_t freed = (uint32_t)__ballot(done) & ((1u << Q) - 1);
+    if (freed) {
+      active &= ~freed;
+      for (uint32_t m = freed; m; m &= m - 1) {
+        const uint32_t sl = __ffs(m) - 1;
+        for (int i = lane; i < VIS; i += 64) L.vis[sl * VIS + i] = NONE;
+      }
+      if (pend && ((freed >> pend_slot) & 1)) pend = false;
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  const int idx[4] = {ST_LROWS, ST_LEDGES, ST_LPROBES, ST_LIGHT};
+  const unsigned long long v[4] = {st_rows, st_edges, st_probes, st_done};
+  block_stats<4>(ctl, idx, v);
+}
+
 // ------------------------------------------------------------------ workgroup tiers
 // Queries whose visited set outgrew one wave's LDS: one 256-lane workgroup per query, same BFS.
 //   k_wg<WgLds>  visited hash (8192 slots) + BFS list (4096) in LDS          ("medium")
@@ -680,12 +912,20 @@ int check_batch_device(Snapshot* s, const kg_query* d_q, size_t n, int32_t globa
     hipLaunchKernelGGL(k_resolve, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, stream, s->ds, d_q, (uint32_t)n,
                        global_max_depth, rq, d_out, d_err, light, gen, ctl);
     HIPC(hipGetLastError());
-    // 7 workgroups of 4 waves per CU: ~21 KiB of LDS per workgroup allows 28 waves/CU
-    const uint32_t light_grid = (uint32_t)std::min<uint64_t>((uint64_t)s->n_cu * 7, (n + 15) / 16 + 8);
     if (stats) HIPC(hipEventRecord(l0, stream));
-    hipLaunchKernelGGL((k_light<16, 7, 64>), dim3(light_grid), dim3(256), 0, stream, s->ds, rq,
-                       WorkList{light, ctl->light8, (uint32_t)n, 1u}, ctl->heads, d_out, d_err, light2,
-                       &ctl->light2_count, ctl);
+    if (s->light_tier == 1) {
+      // 7 workgroups of 4 waves per CU: ~21 KiB of LDS per workgroup allows 28 waves/CU
+      const uint32_t light_grid = (uint32_t)std::min<uint64_t>((uint64_t)s->n_cu * 7, (n + 15) / 16 + 8);
+      hipLaunchKernelGGL((k_light<16, 7, 64>), dim3(light_grid), dim3(256), 0, stream, s->ds, rq,
+                         WorkList{light, ctl->light8, (uint32_t)n, 1u}, ctl->heads, d_out, d_err, light2,
+                         &ctl->light2_count, ctl);
+    } else {
+      // ~30 KiB of LDS per workgroup (8 slots x 512 B visited + 256-entry FIFO per wave): 5 per CU
+      const uint32_t grid = (uint32_t)std::min<uint64_t>((uint64_t)s->n_cu * 5, (n + 31) / 32 + 8);
+      hipLaunchKernelGGL((k_stream<8, 7, 256>), dim3(grid), dim3(256), 0, stream, s->ds, rq,
+                         WorkList{light, ctl->light8, (uint32_t)n, 1u}, ctl->heads, d_out, d_err, light2,
+                         &ctl->light2_count, ctl);
+    }
     HIPC(hipGetLastError());
     if (stats) HIPC(hipEventRecord(l1, stream));
     hipLaunchKernelGGL((k_light<64, 9, 256>), dim3((uint32_t)s->n_cu * 4), dim3(256), 0, stream, s->ds, rq,
@@ -741,6 +981,8 @@ int check_batch_device(Snapshot* s, const kg_query* d_q, size_t n, int32_t globa
     stats->n_light = h.st[ST_LIGHT];
     stats->n_medium = h.st[ST_MEDIUM];
     stats->n_heavy = wg_heavy ? h.st[ST_HEAVY] : gs.done;
+    stats->n_wide = h.light2_count;
+    stats->n_grid = gs.done;
     stats->rows_opened += gs.rows;
     stats->edges_read += gs.edges;
     stats->direct_probes += gs.probes;

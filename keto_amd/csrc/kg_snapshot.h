@@ -52,7 +52,8 @@ struct Snapshot {
   size_t grid_pool_bytes = 0;
   uint32_t grid_epoch = 0;
   hipEvent_t ev[4] = {};  // batch timing events (created on first use)
-  int tiers = 0;  // kg_snapshot_tune("tiers")  // grid tier visited-table epoch (kg_grid.hip)
+  int tiers = 0;       // kg_snapshot_tune("tiers")
+  int light_tier = 0;  // kg_snapshot_tune("light"): 0 k_stream, 1 k_light<16>  // grid tier visited-table epoch (kg_grid.hip)
   void* interp_pool = nullptr;
   size_t interp_pool_bytes = 0;
   uint64_t batch_seq = 0;
