@@ -39,6 +39,7 @@ def parse():
     ap.add_argument("--global-depth", type=int, default=10)
     ap.add_argument("--seed", type=int, default=20250131)
     ap.add_argument("--tiers", type=int, default=0, help="kg_snapshot_tune tiers (0 grid, 1 LDS-WG+grid, 2 WG)")
+    ap.add_argument("--wide", type=int, default=1, help="kg_snapshot_tune wide (k_light<64> tier on/off)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline time budget (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--preset", type=int, default=0,
@@ -132,6 +133,7 @@ def main():
     t_build = time.time()
     snap = Snapshot.synthetic(int(a.tuples), seed=a.seed, device=local, preset=a.preset)
     snap.tune("tiers", a.tiers)
+    snap.tune("wide", a.wide)
     info = snap.info()
     t_build = time.time() - t_build
 

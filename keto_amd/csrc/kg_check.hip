@@ -912,26 +912,33 @@ int check_batch_device(Snapshot* s, const kg_query* d_q, size_t n, int32_t globa
     hipLaunchKernelGGL(k_resolve, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, stream, s->ds, d_q, (uint32_t)n,
                        global_max_depth, rq, d_out, d_err, light, gen, ctl);
     HIPC(hipGetLastError());
+    uint32_t* const after_list = use_medium ? medium : heavy;
+    uint32_t* const after_count = use_medium ? &ctl->medium_count : &ctl->heavy_count;
+    // overflow of the first wave tier: k_light<64> (wide tier) or straight to the tiers after it
+    uint32_t* const ovf_list = s->wide_tier ? light2 : after_list;
+    uint32_t* const ovf_count = s->wide_tier ? &ctl->light2_count : after_count;
     if (stats) HIPC(hipEventRecord(l0, stream));
     if (s->light_tier == 1) {
       // 7 workgroups of 4 waves per CU: ~21 KiB of LDS per workgroup allows 28 waves/CU
       const uint32_t light_grid = (uint32_t)std::min<uint64_t>((uint64_t)s->n_cu * 7, (n + 15) / 16 + 8);
       hipLaunchKernelGGL((k_light<16, 7, 64>), dim3(light_grid), dim3(256), 0, stream, s->ds, rq,
-                         WorkList{light, ctl->light8, (uint32_t)n, 1u}, ctl->heads, d_out, d_err, light2,
-                         &ctl->light2_count, ctl);
+                         WorkList{light, ctl->light8, (uint32_t)n, 1u}, ctl->heads, d_out, d_err, ovf_list,
+                         ovf_count, ctl);
     } else {
       // ~30 KiB of LDS per workgroup (8 slots x 512 B visited + 256-entry FIFO per wave): 5 per CU
       const uint32_t grid = (uint32_t)std::min<uint64_t>((uint64_t)s->n_cu * 5, (n + 31) / 32 + 8);
       hipLaunchKernelGGL((k_stream<8, 7, 256>), dim3(grid), dim3(256), 0, stream, s->ds, rq,
-                         WorkList{light, ctl->light8, (uint32_t)n, 1u}, ctl->heads, d_out, d_err, light2,
-                         &ctl->light2_count, ctl);
+                         WorkList{light, ctl->light8, (uint32_t)n, 1u}, ctl->heads, d_out, d_err, ovf_list,
+                         ovf_count, ctl);
     }
     HIPC(hipGetLastError());
     if (stats) HIPC(hipEventRecord(l1, stream));
-    hipLaunchKernelGGL((k_light<64, 9, 256>), dim3((uint32_t)s->n_cu * 4), dim3(256), 0, stream, s->ds, rq,
-                       WorkList{light2, &ctl->light2_count, 0u, 0u}, ctl->heads2, d_out, d_err,
-                       use_medium ? medium : heavy, use_medium ? &ctl->medium_count : &ctl->heavy_count, ctl);
-    HIPC(hipGetLastError());
+    if (s->wide_tier) {
+      hipLaunchKernelGGL((k_light<64, 9, 256>), dim3((uint32_t)s->n_cu * 4), dim3(256), 0, stream, s->ds, rq,
+                         WorkList{light2, &ctl->light2_count, 0u, 0u}, ctl->heads2, d_out, d_err, after_list,
+                         after_count, ctl);
+      HIPC(hipGetLastError());
+    }
     if (use_medium) {
       hipLaunchKernelGGL(k_medium, dim3((uint32_t)s->n_cu * 3), dim3(256), 0, stream, s->ds, rq, medium,
                          &ctl->medium_count, &ctl->medium_head, d_out, d_err, heavy, &ctl->heavy_count, ctl);
@@ -966,8 +973,13 @@ int check_batch_device(Snapshot* s, const kg_query* d_q, size_t n, int32_t globa
     float ms = 0, lms = 0;
     HIPC(hipEventElapsedTime(&ms, e0, e1));
     if (n) HIPC(hipEventElapsedTime(&lms, l0, l1));
+    static_assert(sizeof(Ctl) <= 65536, "Ctl readback fits the pinned buffer");
+    void* hbuf = s->host_buf(sizeof(Ctl));
+    if (!hbuf) return set_error(-1, "pinned host buffer");
+    HIPC(hipMemcpyAsync(hbuf, ctl, sizeof(Ctl), hipMemcpyDeviceToHost, stream));
+    HIPC(hipStreamSynchronize(stream));
     Ctl h;
-    HIPC(hipMemcpy(&h, ctl, sizeof(Ctl), hipMemcpyDeviceToHost));
+    memcpy(&h, hbuf, sizeof(Ctl));
     for (int x = 0; x < 8; x++)
       for (int k = 0; k < ST_N; k++) h.st[k] += h.st8[x][k];
     stats->rows_opened = h.st[ST_ROWS] + h.st[ST_LROWS];

@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstring>
 
 #include "kg_bfs.h"
 #include "kg_grid.h"
@@ -280,9 +281,11 @@ __global__ void k_grid_finish(const uint32_t* slot_q, const uint32_t* slot_hit, 
 // Host driver: qlist / count live on the device (count is read back once).
 int grid_tier(Snapshot* s, const RQuery* rq, const uint32_t* qlist, const uint32_t* d_count, int global_max_depth,
               uint8_t* out, uint32_t* err, hipStream_t stream, GridStats* gs) {
-  uint32_t count = 0;
-  HIPC(hipMemcpyAsync(&count, d_count, 4, hipMemcpyDeviceToHost, stream));
+  uint32_t* hb = (uint32_t*)s->host_buf(sizeof(GridCtl) + 64);
+  if (!hb) return set_error(-1, "pinned host buffer");
+  HIPC(hipMemcpyAsync(hb, d_count, 4, hipMemcpyDeviceToHost, stream));
   HIPC(hipStreamSynchronize(stream));
+  const uint32_t count = hb[0];
   if (count == 0) return 0;
   const uint64_t nn = std::max<uint32_t>(s->ds.n_nodes, 1);
   // log capacity >= n_nodes (one slot alone always fits); hash >= 2x the log (load <= 0.5)
@@ -344,8 +347,9 @@ int grid_tier(Snapshot* s, const RQuery* rq, const uint32_t* qlist, const uint32
                            incl, level, slot_q, slot_hit, H, hcap - 1, epoch, cap, ctl);
         HIPC(hipGetLastError());
       }
-      HIPC(hipMemcpyAsync(&h, ctl, sizeof h, hipMemcpyDeviceToHost, stream));
+      HIPC(hipMemcpyAsync(hb, ctl, sizeof h, hipMemcpyDeviceToHost, stream));
       HIPC(hipStreamSynchronize(stream));
+      memcpy(&h, hb, sizeof h);
       if (h.overflow || std::min<uint64_t>(h.n, cap) == h.lvl_e) break;  // next level empty
     }
     if (gs) {

@@ -136,10 +136,17 @@ Snapshot::~Snapshot() {
   if (scratch) hipFree(scratch);
   if (heavy_pool) hipFree(heavy_pool);
   if (grid_pool) hipFree(grid_pool);
+  if (pinned) hipHostFree(pinned);
   for (auto& e : ev)
     if (e) hipEventDestroy(e);
   if (interp_pool) hipFree(interp_pool);
   if (stream) hipStreamDestroy(stream);
+}
+
+void* Snapshot::host_buf(size_t bytes) {
+  if (bytes > 65536) return nullptr;
+  if (!pinned && hipHostMalloc(&pinned, 65536, hipHostMallocDefault) != hipSuccess) pinned = nullptr;
+  return pinned;
 }
 
 int Snapshot::alloc(void** p, size_t bytes) {

@@ -95,8 +95,8 @@ def test_heavy_path_overflow_star():
     assert e.last_stats["n_medium"] + e.last_stats["n_heavy"] >= 1
 
 
-@pytest.mark.parametrize("tiers", [0, 1, 2])
-def test_workgroup_tiers_lds_and_hbm(tiers):
+@pytest.mark.parametrize("tiers,wide", [(0, 0), (0, 1), (1, 1), (2, 0)])
+def test_workgroup_tiers_lds_and_hbm(tiers, wide):
     # > 256 expanded nodes leaves the wave tiers; tiers=0 sends them to the grid tier, 1/2 first to
     # the LDS workgroup tier (<= 4096 expanded nodes), then to the grid / HBM workgroup tier
     tuples = [RelationTuple.from_string(f"g:root#m@(g:c{i}#m)") for i in range(5000)]
@@ -110,6 +110,7 @@ def test_workgroup_tiers_lds_and_hbm(tiers):
     reg = Registry(tuples, [])
     e = reg.permission_engine()
     e.snapshot.tune("tiers", tiers)
+    e.snapshot.tune("wide", wide)
     it = reg.interner
     qs = [RelationTuple.from_string(s) for s in
           ["g:root#m@target", "g:root#m@mid", "g:root#m@none", "g:c3#m@target", "g:c7#m@mid", "g:d3#m@target",
