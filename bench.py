@@ -39,7 +39,7 @@ def parse():
     ap.add_argument("--global-depth", type=int, default=10)
     ap.add_argument("--seed", type=int, default=20250131)
     ap.add_argument("--tiers", type=int, default=0, help="kg_snapshot_tune tiers (0 grid, 1 LDS-WG+grid, 2 WG)")
-    ap.add_argument("--wide", type=int, default=1, help="kg_snapshot_tune wide (k_light<64> tier on/off)")
+    ap.add_argument("--wide", type=int, default=0, help="kg_snapshot_tune wide (k_light<64> tier on/off)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline time budget (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--preset", type=int, default=0,
@@ -205,9 +205,9 @@ def main():
                            "all": {"rows": int(stats[-1].rows_opened), "edges": int(stats[-1].edges_read),
                                    "probes": int(stats[-1].direct_probes)}},
         "snapshot_build_s": t_build,
-        "roofline": {"kernel": "k_light", "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "roofline": {"kernel": "k_stream<8,7,256>", "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "bytes_model": "8*rows_opened + 4*edges_read + 16*direct_probes (per k_light launch)",
+                     "bytes_model": "8*rows_opened + 4*edges_read + 16*direct_probes (per k_stream launch; R/E/P counted in-kernel)",
                      "launch_ms": float(l_ms.mean()), "bytes_per_launch": float(l_bytes.mean())},
     }
     if rank == 0 and world == 1 and a.cpu_seconds > 0:
@@ -219,9 +219,9 @@ def main():
 
 
 def pmc_traffic(tuples: int, batch: int):
-    """HBM bytes per k_light launch from the committed rocprofv3 --pmc pass (profiles/), if one
+    """HBM bytes per k_stream launch from the committed rocprofv3 --pmc pass (profiles/), if one
     was taken on this exact workload; else None."""
-    p = os.path.join(ROOT, "profiles", "pmc_k_light.json")
+    p = os.path.join(ROOT, "profiles", "pmc_k_stream.json")
     try:
         with open(p) as f:
             d = json.load(f)

@@ -162,7 +162,7 @@ int kg_snapshot_info(const kg_snapshot* s, uint64_t* info4);
  * 2 = LDS workgroup tier then one-workgroup-per-query HBM tier.  key "light": the first wave
  * tier -- 0 = k_stream (many queries per wave over one FIFO, default), 1 = k_light<16> (four
  * 16-lane groups per wave).  key "wide": 1 = k_light<64> (one query per wave, 256 expanded
- * nodes) takes the first tier's overflow, 0 = the overflow goes straight on.  Results never
+ * nodes) takes the first tier's overflow, 0 = the overflow goes straight on (default).  Results never
  * depend on any of them. */
 int kg_snapshot_tune(kg_snapshot* s, const char* key, int64_t value);
 /* Synthetic layout: ids6 = {n_docs, n_groups, n_users, n_folders, user_obj0, folder_obj0}

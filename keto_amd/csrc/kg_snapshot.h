@@ -53,7 +53,7 @@ struct Snapshot {
   uint32_t grid_epoch = 0;
   hipEvent_t ev[4] = {};  // batch timing events (created on first use)
   void* pinned = nullptr;  // 64 KiB of pinned host memory for small device->host readbacks
-  int wide_tier = 1;       // kg_snapshot_tune("wide"): 1 = k_light<64> between k_stream and the rest
+  int wide_tier = 0;       // kg_snapshot_tune("wide"): 1 = k_light<64> between k_stream and the rest
   void* host_buf(size_t bytes);
   int tiers = 0;       // kg_snapshot_tune("tiers")
   int light_tier = 0;  // kg_snapshot_tune("light"): 0 k_stream, 1 k_light<16>  // grid tier visited-table epoch (kg_grid.hip)

@@ -32,7 +32,7 @@ def per_dispatch(d: str, kernel: str, counter: str):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--kernel", default="k_light")
+    ap.add_argument("--kernel", default="k_stream")
     ap.add_argument("--fetch", required=True)
     ap.add_argument("--write", required=True)
     ap.add_argument("--tuples", type=float, required=True)
