@@ -222,6 +222,7 @@ __device__ __forceinline__ int light_query(const DevSnap& s, LightLds<W, VLOG2, 
   }
   __builtin_amdgcn_wave_barrier();
   uint32_t lvl_b = 0, lvl_e = 1, n = 1;
+  const uint32_t qsig = subj_sig(q.subj);
   bool pend = false;
   uint32_t pend_node = 0;
   for (int k = 0; lvl_b < lvl_e; k++) {
@@ -265,6 +266,7 @@ __device__ __forceinline__ int light_query(const DevSnap& s, LightLds<W, VLOG2, 
         } else {
           pend = act;
         }
+        pend = pend && sig_maybe(x.sig, qsig);  // the signature rules out most misses
         pend_node = x.node;
         bs.probes += __popcll(g.ballot(pend));
       }
@@ -554,7 +556,7 @@ __global__ __launch_bounds__(256) void k_stream(DevSnap s, const RQuery* __restr
       }
     }
     tail += min((uint32_t)__popcll(am), room);
-    pend = act && (keepc ? appended : true);
+    pend = act && (keepc ? appended : true) && sig_maybe(x.sig, subj_sig(L.s_subj[slot]));
     pend_node = x.node;
     pend_slot = slot;
     pend_gen = act ? L.s_gen[slot] : 0u;

@@ -235,7 +235,7 @@ __global__ __launch_bounds__(256) void k_grid_expand(DevSnap s, const RQuery* __
             if (ins < 0) ctl->overflow = 1;
             if (ins == 0) act = false;
           }
-          if (act) {
+          if (act && sig_maybe(x.sig, subj_sig(q.subj))) {  // the signature rules out most misses
             probes++;
             if (dset_probe(s, child, q.subj)) atomicExch(&slot_hit[slot], 1u);
           }

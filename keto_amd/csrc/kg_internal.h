@@ -54,9 +54,23 @@ enum { RW_OR = 0, RW_AND = 1, RW_COMPUTED = 2, RW_TTU = 3, RW_NOT = 4 };
 
 // Set-adjacency edge with the child's own row inlined (begin/len into adj/adjx), so a BFS level
 // needs one dependent HBM round trip instead of two (no adj_off lookup per discovered node).
+// One set-adjacency edge with the child's own set row inlined (begin/len) and a 2-bit Bloom
+// signature of the child's direct subjects (its full row): a checkDirect probe whose subject bits
+// are not all present in the signature is a certain miss and is skipped.
 struct AdjX {
-  uint32_t node, begin, len, pad;
+  uint32_t node, begin, len, sig;
 };
+
+__host__ __device__ __forceinline__ uint32_t subj_sig(uint32_t subj) {
+  uint32_t h = subj * 0x9E3779B1u;
+  h ^= h >> 15;
+  h *= 0x85EBCA77u;
+  h ^= h >> 13;
+  return (1u << (h & 31)) | (1u << ((h >> 5) & 31));
+}
+__host__ __device__ __forceinline__ bool sig_maybe(uint32_t sig, uint32_t subj_mask) {
+  return (sig & subj_mask) == subj_mask;
+}
 
 // Everything a kernel needs, passed by value.
 struct DevSnap {

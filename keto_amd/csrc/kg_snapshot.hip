@@ -62,12 +62,22 @@ __global__ void k_nmap_insert(uint64_t* keys, uint32_t* vals, uint64_t mask, con
   }
 }
 
-__global__ void k_build_adjx(const uint32_t* adj, const uint64_t* adj_off, uint64_t n_edges, AdjX* adjx) {
+// Bloom signature of every node's full row (direct subjects, tagged like dset keys).
+__global__ void k_node_sig(const uint64_t* row_off, const uint32_t* row_subj, uint32_t n_nodes, uint32_t* sig) {
+  const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= n_nodes) return;
+  uint32_t m = 0;
+  for (uint64_t i = row_off[v], e = row_off[v + 1]; i < e && m != 0xFFFFFFFFu; i++) m |= subj_sig(row_subj[i]);
+  sig[v] = m;
+}
+
+__global__ void k_build_adjx(const uint32_t* adj, const uint64_t* adj_off, const uint32_t* sig, uint64_t n_edges,
+                             AdjX* adjx) {
   for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < n_edges;
        e += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t c = adj[e];
     const uint64_t b = adj_off[c], x = adj_off[c + 1];
-    adjx[e] = AdjX{c, (uint32_t)b, (uint32_t)(x - b), 0u};
+    adjx[e] = AdjX{c, (uint32_t)b, (uint32_t)(x - b), sig[c]};
   }
 }
 
@@ -177,8 +187,15 @@ int Snapshot::build_hash_tables() {
   AdjX* adjx = nullptr;
   if (alloc((void**)&adjx, (n_set_edges + 1) * sizeof(AdjX))) return -1;
   if (n_set_edges) {
-    hipLaunchKernelGGL(k_build_adjx, dim3(2048), dim3(256), 0, stream, ds.adj, ds.adj_off, n_set_edges, adjx);
+    uint32_t* sig = nullptr;
+    HIPC(hipMalloc(&sig, (size_t)ds.n_nodes * 4 + 4));
+    hipLaunchKernelGGL(k_node_sig, dim3((ds.n_nodes + 255) / 256), dim3(256), 0, stream, ds.row_off, ds.row_subj,
+                       ds.n_nodes, sig);
     HIPC(hipGetLastError());
+    hipLaunchKernelGGL(k_build_adjx, dim3(2048), dim3(256), 0, stream, ds.adj, ds.adj_off, sig, n_set_edges, adjx);
+    HIPC(hipGetLastError());
+    HIPC(hipStreamSynchronize(stream));
+    HIPC(hipFree(sig));
   }
   ds.adjx = adjx;
   uint64_t n_rows = h_row_off_last;
