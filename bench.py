@@ -40,6 +40,7 @@ def parse():
     ap.add_argument("--seed", type=int, default=20250131)
     ap.add_argument("--tiers", type=int, default=0, help="kg_snapshot_tune tiers (0 grid, 1 LDS-WG+grid, 2 WG)")
     ap.add_argument("--wide", type=int, default=0, help="kg_snapshot_tune wide (k_light<64> tier on/off)")
+    ap.add_argument("--back", type=int, default=1, help="kg_snapshot_tune back (backward tier + no-holder filter)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline time budget (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--preset", type=int, default=0,
@@ -134,6 +135,7 @@ def main():
     snap = Snapshot.synthetic(int(a.tuples), seed=a.seed, device=local, preset=a.preset)
     snap.tune("tiers", a.tiers)
     snap.tune("wide", a.wide)
+    snap.tune("back", a.back)
     info = snap.info()
     t_build = time.time() - t_build
 
@@ -199,11 +201,13 @@ def main():
         "p99_batch_ms": float(np.percentile(np.array(lat) * 1e3, 99)),
         "allowed_fraction": float(res.mean()),
         "tiers": {"light": int(stats[-1].n_light), "wide": int(stats[-1].n_wide), "medium": int(stats[-1].n_medium),
-                  "heavy": int(stats[-1].n_heavy), "general": int(stats[-1].n_general)},
+                  "back": int(stats[-1].n_back), "grid": int(stats[-1].n_grid), "heavy": int(stats[-1].n_heavy),
+                  "general": int(stats[-1].n_general), "no_holder": int(stats[-1].n_no_holder)},
         "work_per_batch": {"light": {"rows": int(stats[-1].light_rows_opened), "edges": int(stats[-1].light_edges_read),
                                      "probes": int(stats[-1].light_probes)},
                            "all": {"rows": int(stats[-1].rows_opened), "edges": int(stats[-1].edges_read),
-                                   "probes": int(stats[-1].direct_probes)}},
+                                   "probes": int(stats[-1].direct_probes)},
+                           "back": {"rows": int(stats[-1].back_rows), "edges": int(stats[-1].back_edges)}},
         "snapshot_build_s": t_build,
         "roofline": {"kernel": "k_stream<8,7,256>", "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

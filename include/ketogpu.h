@@ -100,6 +100,9 @@ typedef struct {
   double light_ms;                      /* device time of the k_light<16> launch         */
   uint64_t n_wide;                      /* queries handed from k_light<16> to k_light<64> */
   uint64_t n_grid;                      /* queries resolved by the grid tier             */
+  uint64_t n_back;                      /* queries resolved by the backward tier         */
+  uint64_t n_no_holder;                 /* queries answered NotMember by k_resolve: no row holds the subject */
+  uint64_t back_rows, back_edges;       /* backward tier: parent lists opened / parents read */
 } kg_stats;
 
 /* Per-query outputs of kg_check_batch. */
@@ -163,7 +166,9 @@ int kg_snapshot_info(const kg_snapshot* s, uint64_t* info4);
  * tier -- 0 = k_stream (many queries per wave over one FIFO, default), 1 = k_light<16> (four
  * 16-lane groups per wave).  key "wide": 1 = k_light<64> (one query per wave, 256 expanded
  * nodes) takes the first tier's overflow, 0 = the overflow goes straight on (default).  Results never
- * depend on any of them. */
+ * depend on any of them.  key "back": 1 = the backward tier (reverse search from the subject's
+ * holders, one workgroup per query) takes the wave tiers' overflow before the grid tier, and
+ * k_resolve answers queries whose subject no row holds (default); 0 = off. */
 int kg_snapshot_tune(kg_snapshot* s, const char* key, int64_t value);
 /* Synthetic layout: ids6 = {n_docs, n_groups, n_users, n_folders, user_obj0, folder_obj0}
  * (doc d = object d, group g = object n_docs+g, user u = object user_obj0+u). */

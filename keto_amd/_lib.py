@@ -44,7 +44,9 @@ class kg_stats(C.Structure):
                 ("frontier_hbm", C.c_uint64), ("n_light", C.c_uint64), ("n_heavy", C.c_uint64),
                 ("n_general", C.c_uint64), ("n_medium", C.c_uint64), ("light_rows_opened", C.c_uint64), ("light_edges_read", C.c_uint64),
                 ("light_probes", C.c_uint64), ("kernel_ms", C.c_double), ("light_ms", C.c_double),
-                ("n_wide", C.c_uint64), ("n_grid", C.c_uint64)]
+                ("n_wide", C.c_uint64), ("n_grid", C.c_uint64),
+                ("n_back", C.c_uint64), ("n_no_holder", C.c_uint64), ("back_rows", C.c_uint64),
+                ("back_edges", C.c_uint64)]
 
     def as_dict(self) -> dict:
         return {n: getattr(self, n) for n, _ in self._fields_}

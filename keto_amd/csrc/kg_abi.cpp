@@ -117,6 +117,11 @@ int kg_snapshot_tune(kg_snapshot* sp, const char* key, int64_t value) {
     s->wide_tier = (int)value;
     return 0;
   }
+  if (strcmp(key, "back") == 0) {
+    if (value < 0 || value > 1) return set_error(-2, "back must be 0 or 1");
+    s->back_tier = (int)value;
+    return 0;
+  }
   if (strcmp(key, "light") == 0) {
     if (value < 0 || value > 1) return set_error(-2, "light must be 0 or 1");
     s->light_tier = (int)value;

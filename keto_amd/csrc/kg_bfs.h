@@ -47,6 +47,20 @@ __device__ __forceinline__ bool dset_probe(const DevSnap& s, uint32_t node, uint
   return false;
 }
 
+// Holders of a tagged subject: hold[first, first+count) are the nodes whose row contains it.
+// Requires s.radj (reverse indexes built).  Unknown subject -> count 0.
+__device__ __forceinline__ uint2 holders_find(const DevSnap& s, uint32_t subj) {
+  if (subj == NONE) return make_uint2(0, 0);
+  uint64_t h = mix64(subj) & s.hmask;
+  for (uint64_t p = 0; p <= s.hmask; p++) {  // load <= 0.5
+    const uint32_t k = s.hkeys[h];
+    if (k == subj) return s.hvals[h];
+    if (k == NONE) break;
+    h = (h + 1) & s.hmask;
+  }
+  return make_uint2(0, 0);
+}
+
 __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t x, uint32_t* total) {
   int lane = lane_id();
   uint32_t v = x;

@@ -35,13 +35,15 @@ namespace kg {
 
 // Counters: [0] rows_opened [1] edges_read [2] probes [3] frontier_hbm [4] light [5] heavy [6] general
 enum { ST_ROWS = 0, ST_EDGES, ST_PROBES, ST_FHBM, ST_LIGHT, ST_HEAVY, ST_GENERAL, ST_LROWS, ST_LEDGES, ST_LPROBES,
-       ST_MEDIUM, ST_N };
+       ST_MEDIUM, ST_BROWS, ST_BEDGES, ST_BACK, ST_NOHOLD, ST_N };
+static_assert(ST_N <= 16, "per-XCD counter shards hold 16 counters");
 
 // Device-side counters/heads (zeroed per batch).
 struct Ctl {
   uint32_t light_count, gen_count, heavy_count, giant_count;
   uint32_t heavy_head, giant_head, gen_head, pad0;
   uint32_t medium_count, medium_head, light2_count, pad1;
+  uint32_t back_head, fwd_count, pad2[2];  // k_back dequeue head; its overflow (-> grid tier)
   uint32_t heads[8 * 32];   // per-XCD dequeue heads, one 128-B line each (k_light<16>)
   uint32_t heads2[8 * 32];  // (k_light<64>)
   uint32_t light8[8 * 32];  // per-XCD shard sizes of the light list (k_resolve appends)
@@ -96,11 +98,11 @@ __device__ void block_append(bool pred, uint32_t val, uint32_t* list, uint32_t* 
 __global__ __launch_bounds__(256) void k_resolve(DevSnap s, const kg_query* __restrict__ q, uint32_t n,
                                                  int32_t global, RQuery* __restrict__ rq, uint8_t* __restrict__ out,
                                                  uint32_t* __restrict__ err, uint32_t* light_list,
-                                                 uint32_t* gen_list, Ctl* ctl) {
+                                                 uint32_t* gen_list, int no_holder_filter, Ctl* ctl) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   bool valid = i < n;
   uint32_t route = ROUTE_DONE;
-  bool did_probe = false;
+  bool did_probe = false, no_holder = false;
   if (valid) {
     kg_query x = q[i];
     uint32_t node = nmap_find(s, x.t.ns, x.t.rel, x.t.obj);
@@ -130,6 +132,11 @@ __global__ __launch_bounds__(256) void k_resolve(DevSnap s, const kg_query* __re
       rl = (uint32_t)(s.adj_off[node + 1] - s.adj_off[node]);
       member = dset_probe(s, node, subj);
       if (member || d < 2 || rl == 0) route = ROUTE_DONE;
+      // a subject that no row holds cannot be reached from any root (checkDirect never hits)
+      if (route == ROUTE_LIGHT && no_holder_filter && holders_find(s, subj).y == 0) {
+        route = ROUTE_DONE;
+        no_holder = true;
+      }
     }
     rq[i] = RQuery{node, subj, d, route, rb, rl};
     if (route == ROUTE_DONE) {
@@ -138,9 +145,9 @@ __global__ __launch_bounds__(256) void k_resolve(DevSnap s, const kg_query* __re
     }
   }
   {
-    const int idx[1] = {ST_PROBES};
-    const unsigned long long v[1] = {(valid && did_probe) ? 1ull : 0ull};
-    block_stats<1>(ctl, idx, v);
+    const int idx[2] = {ST_PROBES, ST_NOHOLD};
+    const unsigned long long v[2] = {(valid && did_probe) ? 1ull : 0ull, no_holder ? 1ull : 0ull};
+    block_stats<2>(ctl, idx, v);
   }
   // light list: 8 shards of capacity n (shard = blockIdx & 7), dequeued by k_light per XCD
   const uint32_t h = blockIdx.x & 7;
@@ -411,7 +418,7 @@ __device__ __forceinline__ uint32_t wave_or(uint32_t v) {
   return v;
 }
 
-template <int Q, int VLOG2, int QC>
+template <int Q, int VLOG2, int QC, int CHUNK>
 __global__ __launch_bounds__(256) void k_stream(DevSnap s, const RQuery* __restrict__ rq, WorkList wl,
                                                 uint32_t* heads, uint8_t* __restrict__ out,
                                                 uint32_t* __restrict__ err, uint32_t* next_list,
@@ -434,7 +441,8 @@ __global__ __launch_bounds__(256) void k_stream(DevSnap s, const RQuery* __restr
   }
   __builtin_amdgcn_wave_barrier();
   uint32_t active = 0;  // wave-uniform: slots holding a query
-  bool drained = false;
+  bool drained = false;  // the work list is exhausted (the local chunk may still hold entries)
+  uint32_t c_first = 0, c_left = 0;  // wave-local chunk of list positions
   uint32_t head = 0, tail = 0, head_off = 0;
   bool pend = false;  // per lane: a child of the previous step awaiting its probe
   uint32_t pend_node = 0, pend_slot = 0, pend_gen = 0;
@@ -444,13 +452,20 @@ __global__ __launch_bounds__(256) void k_stream(DevSnap s, const RQuery* __restr
     const uint32_t freem = ~active & ((1u << Q) - 1);
     const uint32_t want = __popc(freem);
     if (want && !drained && (tail - head) + want <= QC) {
-      uint32_t first = 0, got = 0;
-      if (lane == 0) first = dequeue_n(wl, heads, head_sel, head0, want, got);
-      first = __shfl(first, 0, 64);
-      got = __shfl(got, 0, 64);
-      if (first == NONE) {
-        drained = true;
-      } else {
+      // the wave pulls CHUNK consecutive list entries per dequeue and refills from them: a refill
+      // per finished query would put one device-scope atomic per query on the per-XCD heads
+      if (c_left == 0) {
+        uint32_t got = 0;
+        if (lane == 0) c_first = dequeue_n(wl, heads, head_sel, head0, CHUNK, got);
+        c_first = __shfl(c_first, 0, 64);
+        c_left = __shfl(got, 0, 64);
+        if (c_first == NONE) drained = true;
+      }
+      const uint32_t got = min(want, c_left);
+      if (got) {
+        const uint32_t first = c_first;
+        c_first += got;
+        c_left -= got;
         uint32_t slot = 0;
         if ((uint32_t)lane < got) {
           uint32_t m = freem;
@@ -475,8 +490,8 @@ __global__ __launch_bounds__(256) void k_stream(DevSnap s, const RQuery* __restr
         tail += got;
       }
     }
-    if (active == 0 && (drained || tail == head)) {
-      if (drained) break;
+    if (active == 0 && ((drained && c_left == 0) || tail == head)) {
+      if (drained && c_left == 0) break;
       continue;
     }
     __builtin_amdgcn_wave_barrier();
@@ -795,6 +810,139 @@ __global__ __launch_bounds__(256) void k_heavy(DevSnap s, const RQuery* __restri
   wg_run(s, st, sh, rq, qlist, *qcount_p, qhead, out, err, next_list, next_count, ctl, ST_HEAVY);
 }
 
+// ------------------------------------------------------------------ k_back: the backward tier
+// Queries that outgrew the wave tiers are first tried BACKWARDS, one workgroup per query: the
+// reachability question of the rewrite-free path ("a path of <= D-1 subject-set hops from the
+// root to a node whose row holds the subject") is symmetric, and in a power-law
+// graph the set of nodes that can reach a rarely used subject is usually tiny while the set the
+// root reaches is huge.  Level 0 = the subject's holders (hold[] via the subject hash), level j =
+// their parents through reverse set-adjacency, j <= D-1; the root found at any level is a hit
+// (IsMember), an exhausted search is NotMember.  A visited set that outgrows LDS hands the query
+// on to the forward grid tier, which redoes it from scratch (results never depend on the tier).
+// Paths from a LIGHT root only cross rewrite-free nodes (k_resolve's routing), so any backward
+// path that reaches the root is a forward path of the same length.
+constexpr uint32_t BK_VLOG2 = 13, BK_VSLOTS = 1u << BK_VLOG2, BK_CAP = 4096;  // hash load <= 0.5
+
+struct BackShared {
+  uint32_t qi, n, hit, over;
+  uint32_t pref[256];
+  uint64_t rb[256];
+  uint32_t wsum[4];
+};
+
+__device__ __forceinline__ int bk_insert(uint32_t* vis, uint32_t key) {
+  uint32_t h = (key * 2654435761u) >> (32 - BK_VLOG2);
+  for (uint32_t p = 0; p < BK_VSLOTS; p++) {
+    const uint32_t old = atomicCAS(&vis[h], NONE, key);
+    if (old == NONE) return 1;
+    if (old == key) return 0;
+    h = (h + 1) & (BK_VSLOTS - 1);
+  }
+  return -1;
+}
+
+// Appends a newly seen node to the level list (capacity first, so the hash never fills).
+__device__ __forceinline__ void bk_add(uint32_t* vis, uint32_t* lst, BackShared& sh, uint32_t v) {
+  if (*(volatile uint32_t*)&sh.n >= BK_CAP) {
+    sh.over = 1;
+    return;
+  }
+  const int ins = bk_insert(vis, v);
+  if (ins < 0) {
+    sh.over = 1;
+  } else if (ins > 0) {
+    const uint32_t pos = atomicAdd(&sh.n, 1u);
+    if (pos < BK_CAP) lst[pos] = v;
+    else sh.over = 1;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_back(DevSnap s, const RQuery* __restrict__ rq, const uint32_t* qlist,
+                                              const uint32_t* qcount_p, uint32_t* qhead, uint8_t* __restrict__ out,
+                                              uint32_t* __restrict__ err, uint32_t* next_list, uint32_t* next_count,
+                                              Ctl* ctl) {
+  __shared__ uint32_t vis[BK_VSLOTS];
+  __shared__ uint32_t lst[BK_CAP];
+  __shared__ BackShared sh;
+  const int tid = threadIdx.x;
+  const uint32_t qcount = *qcount_p;
+  unsigned long long st_rows = 0, st_edges = 0, st_done = 0;
+  for (;;) {
+    if (tid == 0) sh.qi = atomicAdd(qhead, 1u);
+    __syncthreads();
+    const uint32_t hi = sh.qi;
+    if (hi >= qcount) break;
+    const uint32_t qi = qlist[hi];
+    const RQuery q = rq[qi];
+    const uint2 hr = holders_find(s, q.subj);
+    for (uint32_t i = tid * 4; i < BK_VSLOTS; i += 1024)
+      *reinterpret_cast<uint4*>(&vis[i]) = make_uint4(NONE, NONE, NONE, NONE);
+    if (tid == 0) {
+      sh.n = 0;
+      sh.hit = 0;
+      sh.over = hr.y > BK_CAP ? 1u : 0u;
+    }
+    __syncthreads();
+    if (!sh.over) {  // level 0: the holders (the root itself was probed by k_resolve)
+      for (uint32_t i = tid; i < hr.y; i += 256) {
+        const uint32_t v = s.hold[hr.x + i];
+        if (v == q.node) sh.hit = 1;
+        else bk_add(vis, lst, sh, v);
+      }
+    }
+    __syncthreads();
+    uint32_t lvl_b = 0, lvl_e = sh.n;
+    for (int j = 1; j <= q.depth - 1 && lvl_b < lvl_e && !sh.hit && !sh.over; j++) {
+      const bool keep = j < q.depth - 1;  // parents found here can still be expanded
+      for (uint32_t base = lvl_b; base < lvl_e; base += 256) {
+        const uint32_t i = base + tid;
+        uint64_t rb = 0, re = 0;
+        if (i < lvl_e) {
+          const uint32_t v = lst[i];
+          rb = s.radj_off[v];
+          re = s.radj_off[v + 1];
+          st_rows++;
+        }
+        sh.rb[tid] = rb;
+        uint32_t total;
+        const uint32_t excl = block_excl_scan((uint32_t)(re - rb), sh.wsum, &total);
+        sh.pref[tid] = excl;
+        __syncthreads();
+        if (tid == 0) st_edges += total;
+        for (uint32_t eb = 0; eb < total; eb += 256) {
+          if (*(volatile uint32_t*)&sh.over || *(volatile uint32_t*)&sh.hit) break;
+          const uint32_t e = eb + tid;
+          if (e < total) {
+            const int own = owner_search(sh.pref, 256, e);
+            const uint32_t p = s.radj[sh.rb[own] + (e - sh.pref[own])];
+            if (p == q.node) sh.hit = 1;
+            else if (keep) bk_add(vis, lst, sh, p);
+          }
+        }
+        __syncthreads();
+        if (sh.hit || sh.over) break;
+      }
+      __syncthreads();
+      lvl_b = lvl_e;
+      lvl_e = sh.n;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      if (sh.hit || !sh.over) {
+        out[qi] = sh.hit ? KG_IS_MEMBER : KG_NOT_MEMBER;
+        if (err) err[qi] = KG_ERR_NONE;
+        st_done++;
+      } else {
+        next_list[atomicAdd(next_count, 1u)] = qi;
+      }
+    }
+    __syncthreads();
+  }
+  const int idx[3] = {ST_BROWS, ST_BEDGES, ST_BACK};
+  const unsigned long long v[3] = {st_rows, st_edges, st_done};
+  block_stats<3>(ctl, idx, v);
+}
+
 // ------------------------------------------------------------------ synthetic queries
 __global__ void k_synth_queries(SynthLayout L, DevSnap s, uint64_t seed, uint32_t n, kg_query* q) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -911,8 +1059,9 @@ int check_batch_device(Snapshot* s, const kg_query* d_q, size_t n, int32_t globa
   if (stats) HIPC(hipEventRecord(e0, stream));
   HIPC(hipMemsetAsync(ctl, 0, sizeof(Ctl), stream));
   if (n) {
+    const bool use_back = s->back_tier && s->ds.radj;
     hipLaunchKernelGGL(k_resolve, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, stream, s->ds, d_q, (uint32_t)n,
-                       global_max_depth, rq, d_out, d_err, light, gen, ctl);
+                       global_max_depth, rq, d_out, d_err, light, gen, use_back ? 1 : 0, ctl);
     HIPC(hipGetLastError());
     uint32_t* const after_list = use_medium ? medium : heavy;
     uint32_t* const after_count = use_medium ? &ctl->medium_count : &ctl->heavy_count;
@@ -929,7 +1078,7 @@ int check_batch_device(Snapshot* s, const kg_query* d_q, size_t n, int32_t globa
     } else {
       // ~30 KiB of LDS per workgroup (8 slots x 512 B visited + 256-entry FIFO per wave): 5 per CU
       const uint32_t grid = (uint32_t)std::min<uint64_t>((uint64_t)s->n_cu * 5, (n + 31) / 32 + 8);
-      hipLaunchKernelGGL((k_stream<8, 7, 256>), dim3(grid), dim3(256), 0, stream, s->ds, rq,
+      hipLaunchKernelGGL((k_stream<8, 7, 256, 16>), dim3(grid), dim3(256), 0, stream, s->ds, rq,
                          WorkList{light, ctl->light8, (uint32_t)n, 1u}, ctl->heads, d_out, d_err, ovf_list,
                          ovf_count, ctl);
     }
@@ -954,8 +1103,18 @@ int check_batch_device(Snapshot* s, const kg_query* d_q, size_t n, int32_t globa
                          &ctl->giant_head, d_out, d_err, gb, words, gl, nn, giant /*never overflows*/, &ctl->pad0,
                          ctl);
       HIPC(hipGetLastError());
-    } else if (int rc = grid_tier(s, rq, heavy, &ctl->heavy_count, global_max_depth, d_out, d_err, stream, &gs)) {
-      return rc;
+    } else {
+      // backward tier first (k_back), its overflow -> forward grid tier
+      const uint32_t* fwd_list = heavy;
+      const uint32_t* fwd_count = &ctl->heavy_count;
+      if (use_back) {
+        hipLaunchKernelGGL(k_back, dim3((uint32_t)s->n_cu * 3), dim3(256), 0, stream, s->ds, rq, heavy,
+                           &ctl->heavy_count, &ctl->back_head, d_out, d_err, giant, &ctl->fwd_count, ctl);
+        HIPC(hipGetLastError());
+        fwd_list = giant;
+        fwd_count = &ctl->fwd_count;
+      }
+      if (int rc = grid_tier(s, rq, fwd_list, fwd_count, global_max_depth, d_out, d_err, stream, &gs)) return rc;
     }
     if (s->has_program) {
       InterpCtl ic{};
@@ -1002,6 +1161,10 @@ int check_batch_device(Snapshot* s, const kg_query* d_q, size_t n, int32_t globa
     stats->direct_probes += gs.probes;
     stats->frontier_hbm += gs.logged;
     stats->n_general = h.st[ST_GENERAL];
+    stats->n_back = h.st[ST_BACK];
+    stats->n_no_holder = h.st[ST_NOHOLD];
+    stats->back_rows = h.st[ST_BROWS];
+    stats->back_edges = h.st[ST_BEDGES];
     stats->kernel_ms = ms;
   }
   return 0;

@@ -58,7 +58,8 @@ __device__ __forceinline__ int gh_insert(uint64_t* H, uint64_t mask, uint64_t ke
 // they are reached (a probe does not depend on the depth it is made at, so this is exact).
 __global__ void k_grid_init(DevSnap s, const RQuery* __restrict__ rq, const uint32_t* __restrict__ qlist,
                             uint32_t base, uint32_t cnt, uint64_t* F, uint32_t* RB, uint64_t* lens, uint32_t* slot_q,
-                            uint32_t* slot_hit, uint64_t* H, uint64_t mask, uint64_t epoch, GridCtl* ctl) {
+                            uint2* slot_info, uint32_t* slot_hit, uint64_t* H, uint64_t mask, uint64_t epoch,
+                            GridCtl* ctl) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i == 0) {
     ctl->n = cnt;
@@ -68,8 +69,10 @@ __global__ void k_grid_init(DevSnap s, const RQuery* __restrict__ rq, const uint
   if (i < 8 * 16) (&ctl->probes8[0][0])[i] = 0;
   if (i >= cnt) return;
   const uint32_t qi = qlist[base + i];
-  const uint32_t root = rq[qi].node;
+  const RQuery q = rq[qi];
+  const uint32_t root = q.node;
   slot_q[i] = qi;
+  slot_info[i] = make_uint2(q.subj, (uint32_t)q.depth);
   slot_hit[i] = 0;  // the root was already probed (k_resolve)
   if (gh_insert(H, mask, (epoch << 48) | ((uint64_t)i << 32) | root) < 0) ctl->overflow = 1;
   F[i] = ((uint64_t)i << 32) | root;
@@ -87,18 +90,22 @@ __device__ __forceinline__ uint64_t first_above(const uint64_t* incl, uint64_t l
   return lo;
 }
 
-// ---- device-side level loop: no host round trip per level.
-// k_grid_advance: next level = entries logged by the previous one.
-__global__ void k_grid_advance(GridCtl* ctl, uint64_t cap) {
-  const unsigned long long e = ctl->n < cap ? ctl->n : cap;
-  ctl->lvl_b = ctl->lvl_e;
-  ctl->lvl_e = e;
-  ctl->total = 0;
+// ---- device-side level loop: no host round trip per level.  The next level is the entries
+// logged by the previous one: [previous lvl_e, min(n, cap)).  k_grid_scan_reduce computes those
+// bounds from GridCtl, k_grid_scan_top publishes them (lvl_b, lvl_e, total) for the rest of the
+// level.
+__device__ __forceinline__ void next_level(const GridCtl* ctl, uint64_t cap, uint64_t& lb, uint64_t& le) {
+  lb = ctl->lvl_e;
+  le = ctl->n < cap ? ctl->n : cap;
 }
 
 // Inclusive scan of lens[lvl_b, lvl_e) -> incl[0, n) in three fixed-size launches (the level size
-// lives on the device): per-block chunk sums, one-block scan of the sums, per-block rescan.
+// lives on the device): per-block chunk sums, one-block scan of the sums, per-block rescan.  The
+// rescan also records, for every GT-edge tile of the level, the entry holding its first edge
+// (tile_first), so k_grid_expand never binary-searches HBM.
 constexpr uint32_t SCAN_BLOCKS = 1024;
+constexpr uint32_t GT = 2048;               // edges per k_grid_expand tile
+constexpr uint64_t TILE_CAP = 1ull << 22;   // tiles with a tile_first entry (beyond: HBM search)
 
 __device__ __forceinline__ uint64_t block_sum64(uint64_t v, uint64_t* red) {
   for (int off = 32; off; off >>= 1) v += __shfl_xor(v, off, 64);
@@ -110,9 +117,11 @@ __device__ __forceinline__ uint64_t block_sum64(uint64_t v, uint64_t* red) {
 }
 
 __global__ __launch_bounds__(256) void k_grid_scan_reduce(const uint64_t* __restrict__ lens, const GridCtl* ctl,
-                                                          uint64_t* bsum) {
+                                                          uint64_t* bsum, uint64_t cap) {
   __shared__ uint64_t red[4];
-  const uint64_t lb = ctl->lvl_b, n = ctl->lvl_e - lb;
+  uint64_t lb, le;
+  next_level(ctl, cap, lb, le);
+  const uint64_t n = le - lb;
   const uint64_t chunk = (n + SCAN_BLOCKS - 1) / SCAN_BLOCKS;
   const uint64_t b0 = blockIdx.x * chunk, b1 = min(n, b0 + chunk);
   uint64_t v = 0;
@@ -121,8 +130,11 @@ __global__ __launch_bounds__(256) void k_grid_scan_reduce(const uint64_t* __rest
   if (threadIdx.x == 0) bsum[blockIdx.x] = v;
 }
 
-__global__ __launch_bounds__(SCAN_BLOCKS) void k_grid_scan_top(uint64_t* bsum, GridCtl* ctl) {
+__global__ __launch_bounds__(SCAN_BLOCKS) void k_grid_scan_top(uint64_t* bsum, GridCtl* ctl, uint64_t cap) {
   __shared__ uint64_t wsum[SCAN_BLOCKS / 64];
+  uint64_t lb, le;
+  next_level(ctl, cap, lb, le);
+  __syncthreads();  // every thread has read the previous bounds before thread 0 publishes
   const int lane = lane_id(), wave = threadIdx.x >> 6;
   const uint64_t x = bsum[threadIdx.x];
   uint64_t v = x;
@@ -139,13 +151,16 @@ __global__ __launch_bounds__(SCAN_BLOCKS) void k_grid_scan_top(uint64_t* bsum, G
   }
   bsum[threadIdx.x] = before + v - x;  // exclusive block offsets
   if (threadIdx.x == 0) {
+    ctl->lvl_b = lb;
+    ctl->lvl_e = le;
     ctl->total = tot;
     ctl->edges += tot;
   }
 }
 
 __global__ __launch_bounds__(256) void k_grid_scan_apply(const uint64_t* __restrict__ lens, uint64_t* incl,
-                                                         const uint64_t* __restrict__ boff, const GridCtl* ctl) {
+                                                         const uint64_t* __restrict__ boff, const GridCtl* ctl,
+                                                         uint32_t* tile_first) {
   __shared__ uint64_t wsum[4];
   const int lane = lane_id(), wave = threadIdx.x >> 6;
   const uint64_t lb = ctl->lvl_b, n = ctl->lvl_e - lb;
@@ -164,23 +179,28 @@ __global__ __launch_bounds__(256) void k_grid_scan_apply(const uint64_t* __restr
     __syncthreads();
     uint64_t before = carry;
     for (int w = 0; w < wave; w++) before += wsum[w];
-    if (j < b1) incl[j] = before + v;
+    if (j < b1) {
+      const uint64_t hi = before + v, lo = hi - x;  // entry j holds edges [lo, hi)
+      incl[j] = hi;
+      // tiles whose first edge lies in [lo, hi): exactly one entry writes each tile
+      for (uint64_t t = (lo + GT - 1) / GT; t * GT < hi && t < TILE_CAP; t++) tile_first[t] = (uint32_t)j;
+    }
     carry += wsum[0] + wsum[1] + wsum[2] + wsum[3];
     __syncthreads();
   }
 }
 
-// One thread per edge of the level, in tiles of GT edges per workgroup: the tile's entries'
-// row starts are staged in LDS so each edge finds its entry with an LDS binary search.
-constexpr uint32_t GT = 2048;
-
-__global__ __launch_bounds__(256) void k_grid_expand(DevSnap s, const RQuery* __restrict__ rq, uint64_t* F,
-                                                     uint32_t* RB, uint64_t* lens,
-                                                     const uint64_t* __restrict__ incl, int level,
-                                                     const uint32_t* __restrict__ slot_q, uint32_t* slot_hit,
+// One thread per edge of the level, in tiles of GT edges per workgroup: the tile's entries (edge
+// start, slot, adjx row start) are staged in LDS, so each edge finds its entry with an LDS binary
+// search; per-slot (subject, depth) come from one 8-B slot record.
+__global__ __launch_bounds__(256) void k_grid_expand(DevSnap s, uint64_t* F, uint32_t* RB, uint64_t* lens,
+                                                     const uint64_t* __restrict__ incl,
+                                                     const uint32_t* __restrict__ tile_first, int level,
+                                                     const uint2* __restrict__ slot_info, uint32_t* slot_hit,
                                                      uint64_t* H, uint64_t mask, uint64_t epoch, uint64_t cap,
                                                      GridCtl* ctl) {
-  __shared__ uint64_t s_beg[GT + 1];
+  __shared__ uint64_t s_beg[GT + 2];
+  __shared__ uint32_t s_slot[GT + 2], s_rb[GT + 2];
   __shared__ uint64_t s_j0, s_cnt;
   __shared__ uint32_t s_wcnt[4];
   __shared__ unsigned long long s_base;
@@ -191,22 +211,35 @@ __global__ __launch_bounds__(256) void k_grid_expand(DevSnap s, const RQuery* __
   for (uint64_t t0 = (uint64_t)blockIdx.x * GT; t0 < total; t0 += (uint64_t)gridDim.x * GT) {
     const uint64_t t1 = t0 + GT < total ? t0 + GT : total;
     if (threadIdx.x == 0) {
-      const uint64_t j0 = first_above(incl, 0, n, t0);
+      const uint64_t t = t0 / GT;
+      uint64_t j0, jl;
+      if (t + 1 < TILE_CAP) {
+        j0 = tile_first[t];
+        jl = t1 < total ? tile_first[t + 1] : n - 1;  // an entry at or after the tile's last edge
+      } else {
+        j0 = first_above(incl, 0, n, t0);
+        jl = first_above(incl, j0, n, t1 - 1);
+      }
       s_j0 = j0;
-      s_cnt = first_above(incl, j0, n, t1 - 1) - j0 + 1;
+      s_cnt = jl - j0 + 1;
     }
     __syncthreads();
     const uint64_t j0 = s_j0, cnt = s_cnt;
-    const bool use_lds = cnt <= GT;
+    const bool use_lds = cnt <= GT + 1;
     if (use_lds)
-      for (uint32_t i = threadIdx.x; i <= cnt; i += 256) s_beg[i] = j0 + i == 0 ? 0 : incl[j0 + i - 1];
+      for (uint32_t i = threadIdx.x; i < cnt; i += 256) {
+        s_beg[i] = j0 + i == 0 ? 0 : incl[j0 + i - 1];
+        s_slot[i] = (uint32_t)(F[lvl_b + j0 + i] >> 32);
+        s_rb[i] = RB[lvl_b + j0 + i];
+      }
     __syncthreads();
     for (uint32_t k = 0; k < GT; k += 256) {
       const uint64_t e = t0 + k + threadIdx.x;
       bool act = e < t1, keep = false;
       uint32_t slot = 0, child = 0, cb = 0, cl = 0;
       if (act) {
-        uint64_t j, beg;
+        uint64_t beg;
+        uint32_t rb;
         if (use_lds) {
           uint32_t lo = 0, hi = (uint32_t)cnt;  // largest i < cnt with s_beg[i] <= e
           while (hi - lo > 1) {
@@ -214,30 +247,32 @@ __global__ __launch_bounds__(256) void k_grid_expand(DevSnap s, const RQuery* __
             if (s_beg[mid] <= e) lo = mid;
             else hi = mid;
           }
-          j = j0 + lo;
           beg = s_beg[lo];
+          slot = s_slot[lo];
+          rb = s_rb[lo];
         } else {
-          j = first_above(incl, j0, j0 + cnt, e);
+          const uint64_t j = first_above(incl, j0, j0 + cnt, e);
           beg = incl[j] - lens[lvl_b + j];
+          slot = (uint32_t)(F[lvl_b + j] >> 32);
+          rb = RB[lvl_b + j];
         }
-        slot = (uint32_t)(F[lvl_b + j] >> 32);
         if (slot_hit[slot]) {
           act = false;
         } else {
-          const RQuery q = rq[slot_q[slot]];
-          const AdjX x = s.adjx[RB[lvl_b + j] + (e - beg)];
+          const uint2 si = slot_info[slot];  // (tagged subject, rest depth of the root)
+          const AdjX x = s.adjx[rb + (e - beg)];
           child = x.node;
           cb = x.begin;
           cl = x.len;
-          keep = cl > 0 && q.depth - level - 1 >= 2;  // child will itself be expanded
+          keep = cl > 0 && (int)si.y - level - 1 >= 2;  // child will itself be expanded
           if (keep) {
             const int ins = gh_insert(H, mask, (epoch << 48) | ((uint64_t)slot << 32) | child);
             if (ins < 0) ctl->overflow = 1;
             if (ins == 0) act = false;
           }
-          if (act && sig_maybe(x.sig, subj_sig(q.subj))) {  // the signature rules out most misses
+          if (act && sig_maybe(x.sig, subj_sig(si.x))) {  // the signature rules out most misses
             probes++;
-            if (dset_probe(s, child, q.subj)) atomicExch(&slot_hit[slot], 1u);
+            if (dset_probe(s, child, si.x)) atomicExch(&slot_hit[slot], 1u);
           }
         }
       }
@@ -293,7 +328,8 @@ int grid_tier(Snapshot* s, const RQuery* rq, const uint32_t* qlist, const uint32
   uint64_t hcap = 1;
   while (hcap < 2 * cap) hcap <<= 1;
   const uint32_t G0 = 0xFFFF;  // slot field is 16 bits
-  const size_t need = hcap * 8 + cap * (8 + 4 + 8 + 8) + (size_t)G0 * 8 + sizeof(GridCtl) + SCAN_BLOCKS * 8 + 4096;
+  const size_t need = hcap * 8 + cap * (8 + 4 + 8 + 8) + (size_t)G0 * 16 + TILE_CAP * 4 + sizeof(GridCtl) +
+                      SCAN_BLOCKS * 8 + 4096;
   if (need > s->grid_pool_bytes) {
     if (s->grid_pool) HIPC(hipFree(s->grid_pool));
     s->grid_pool = nullptr;
@@ -314,6 +350,10 @@ int grid_tier(Snapshot* s, const RQuery* rq, const uint32_t* qlist, const uint32
   p += cap * 8;
   uint32_t* RB = (uint32_t*)p;
   p += cap * 4;
+  uint32_t* tile_first = (uint32_t*)p;
+  p += TILE_CAP * 4;
+  uint2* slot_info = (uint2*)p;
+  p += (size_t)G0 * 8;
   uint32_t* slot_q = (uint32_t*)p;
   uint32_t* slot_hit = slot_q + G0;
   p += (size_t)G0 * 8;
@@ -328,7 +368,7 @@ int grid_tier(Snapshot* s, const RQuery* rq, const uint32_t* qlist, const uint32
     }
     const uint64_t epoch = s->grid_epoch;
     hipLaunchKernelGGL(k_grid_init, dim3((cnt + 255) / 256), dim3(256), 0, stream, s->ds, rq, qlist, done, cnt, F,
-                       RB, lens, slot_q, slot_hit, H, hcap - 1, epoch, ctl);
+                       RB, lens, slot_q, slot_info, slot_hit, H, hcap - 1, epoch, ctl);
     HIPC(hipGetLastError());
     // Levels run back to back on the device (sizes never come back to the host); the host looks
     // at the log once per LEVELS_PER_SYNC levels to stop early on an empty level or an overflow.
@@ -339,12 +379,12 @@ int grid_tier(Snapshot* s, const RQuery* rq, const uint32_t* qlist, const uint32
     for (int level = 0; level < max_levels;) {
       const int stop = std::min(max_levels, level + LEVELS_PER_SYNC);
       for (; level < stop; level++) {
-        hipLaunchKernelGGL(k_grid_advance, dim3(1), dim3(1), 0, stream, ctl, cap);
-        hipLaunchKernelGGL(k_grid_scan_reduce, dim3(SCAN_BLOCKS), dim3(256), 0, stream, lens, ctl, bsum);
-        hipLaunchKernelGGL(k_grid_scan_top, dim3(1), dim3(SCAN_BLOCKS), 0, stream, bsum, ctl);
-        hipLaunchKernelGGL(k_grid_scan_apply, dim3(SCAN_BLOCKS), dim3(256), 0, stream, lens, incl, bsum, ctl);
-        hipLaunchKernelGGL(k_grid_expand, dim3((uint32_t)s->n_cu * 8), dim3(256), 0, stream, s->ds, rq, F, RB, lens,
-                           incl, level, slot_q, slot_hit, H, hcap - 1, epoch, cap, ctl);
+        hipLaunchKernelGGL(k_grid_scan_reduce, dim3(SCAN_BLOCKS), dim3(256), 0, stream, lens, ctl, bsum, cap);
+        hipLaunchKernelGGL(k_grid_scan_top, dim3(1), dim3(SCAN_BLOCKS), 0, stream, bsum, ctl, cap);
+        hipLaunchKernelGGL(k_grid_scan_apply, dim3(SCAN_BLOCKS), dim3(256), 0, stream, lens, incl, bsum, ctl,
+                           tile_first);
+        hipLaunchKernelGGL(k_grid_expand, dim3((uint32_t)s->n_cu * 8), dim3(256), 0, stream, s->ds, F, RB, lens,
+                           incl, tile_first, level, slot_info, slot_hit, H, hcap - 1, epoch, cap, ctl);
         HIPC(hipGetLastError());
       }
       HIPC(hipMemcpyAsync(hb, ctl, sizeof h, hipMemcpyDeviceToHost, stream));

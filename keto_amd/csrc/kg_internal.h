@@ -12,6 +12,9 @@
 //   nmap                                  (ns,rel,obj) -> node id, for request mapping on device.
 //   nflags[n_nodes] u8                    bit0 IMPURE: a rewrite / undeclared relation is reachable
 //                                        through set-adjacency (needs the rewrite interpreter).
+//   radj_off[n_nodes+1] u64 / radj[] u32  reverse set-adjacency (parents), for the backward tier.
+//   hold[] u32 + subject hash             holders: the nodes whose row contains a given subject,
+//                                        grouped by subject (the backward tier's level 0).
 #pragma once
 #include <stdint.h>
 
@@ -52,11 +55,10 @@ struct RwNode {
 };
 enum { RW_OR = 0, RW_AND = 1, RW_COMPUTED = 2, RW_TTU = 3, RW_NOT = 4 };
 
-// Set-adjacency edge with the child's own row inlined (begin/len into adj/adjx), so a BFS level
-// needs one dependent HBM round trip instead of two (no adj_off lookup per discovered node).
 // One set-adjacency edge with the child's own set row inlined (begin/len) and a 2-bit Bloom
 // signature of the child's direct subjects (its full row): a checkDirect probe whose subject bits
-// are not all present in the signature is a certain miss and is skipped.
+// are not all present in the signature is a certain miss and is skipped.  A BFS level needs one
+// dependent HBM round trip instead of two (no adj_off lookup per discovered node).
 struct AdjX {
   uint32_t node, begin, len, sig;
 };
@@ -98,6 +100,13 @@ struct DevSnap {
   const RwNode* rw;
   const int32_t* rwchild;
   uint32_t n_rw;
+  // reverse indexes (backward tier, kg_check.hip k_back); radj == nullptr: not built
+  const uint64_t* radj_off;  // [n_nodes+1] parents of a node through set-adjacency
+  const uint32_t* radj;
+  const uint32_t* hold;      // holder nodes (rows containing a subject), grouped by subject
+  const uint32_t* hkeys;     // subject hash: tagged subject, NONE = empty slot
+  const uint2* hvals;        // (first index into hold, holder count)
+  uint64_t hmask;            // n_slots - 1
 };
 
 // astRelationFor (internal/check/engine.go:209-229) as flags: bit0 = has rewrite, bit1 = the

@@ -60,6 +60,7 @@ struct Snapshot {
   void* interp_pool = nullptr;
   size_t interp_pool_bytes = 0;
   uint64_t batch_seq = 0;
+  int back_tier = 1;  // kg_snapshot_tune("back"): backward tier + no-holder filter in k_resolve
 
   ~Snapshot();
   int init_device(int dev);
@@ -68,6 +69,7 @@ struct Snapshot {
   int create_synthetic(const kg_synth_params* p, const kg_rewrite_prog* prog);
   int upload_program(const kg_dict* dict, const kg_rewrite_prog* prog);
   int build_hash_tables();
+  int build_reverse();
   uint8_t host_relflag(uint32_t ns, uint32_t rel) const;
   int64_t export_rows(kg_tuple* out, uint64_t cap);
 };

@@ -81,6 +81,58 @@ __global__ void k_build_adjx(const uint32_t* adj, const uint64_t* adj_off, const
   }
 }
 
+// ------------------------------------------------------------------ reverse indexes
+// In-degree over set-adjacency, then parents filled through per-node cursors (order within a
+// parent list is irrelevant: the backward tier only asks "is the root reachable").
+__global__ void k_indeg(const uint32_t* adj, uint64_t n_edges, unsigned long long* deg) {
+  for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < n_edges; e += (uint64_t)gridDim.x * blockDim.x)
+    atomicAdd(&deg[adj[e]], 1ull);
+}
+__global__ void k_fill_radj(const uint64_t* adj_off, const uint32_t* adj, uint32_t n_nodes, unsigned long long* cur,
+                            uint32_t* radj) {
+  const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= n_nodes) return;
+  for (uint64_t i = adj_off[v], e = adj_off[v + 1]; i < e; i++) radj[atomicAdd(&cur[adj[i]], 1ull)] = v;
+}
+// (subject, node) pairs of every row entry, to be sorted by subject
+__global__ void k_row_nodes(const uint64_t* row_off, uint32_t n_nodes, uint32_t* node_of_row) {
+  const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= n_nodes) return;
+  for (uint64_t i = row_off[v], e = row_off[v + 1]; i < e; i++) node_of_row[i] = v;
+}
+__global__ void k_count_runs(const uint32_t* key, uint64_t n, unsigned long long* cnt) {
+  uint32_t c = 0;
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    c += (i == 0 || key[i] != key[i - 1]) ? 1u : 0u;
+  for (int off = 32; off; off >>= 1) c += __shfl_xor(c, off, 64);
+  if ((threadIdx.x & 63) == 0 && c) atomicAdd(cnt, (unsigned long long)c);
+}
+__device__ __forceinline__ uint64_t hold_slot(uint32_t key, uint64_t mask) { return mix64(key) & mask; }
+// run starts insert (subject -> first index); run ends then add the count
+__global__ void k_hold_insert(const uint32_t* key, uint64_t n, uint32_t* hkeys, uint2* hvals, uint64_t mask) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    if (i != 0 && key[i] == key[i - 1]) continue;
+    const uint32_t k = key[i];
+    for (uint64_t h = hold_slot(k, mask), p = 0; p <= mask; p++, h = (h + 1) & mask) {  // load <= 0.5
+      if (atomicCAS(&hkeys[h], NONE, k) == NONE) {
+        hvals[h].x = (uint32_t)i;
+        break;
+      }
+    }
+  }
+}
+__global__ void k_hold_count(const uint32_t* key, uint64_t n, const uint32_t* hkeys, uint2* hvals, uint64_t mask) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    if (i + 1 != n && key[i] == key[i + 1]) continue;
+    const uint32_t k = key[i];
+    for (uint64_t h = hold_slot(k, mask), p = 0; p <= mask; p++, h = (h + 1) & mask)
+      if (hkeys[h] == k) {
+        hvals[h].y = (uint32_t)(i + 1 - hvals[h].x);
+        break;
+      }
+  }
+}
+
 // ------------------------------------------------------------------ synthetic generator kernels
 // set-adjacency keeps subject sets except "..." ones (engine.go:123-126), like the host path
 __device__ __forceinline__ bool synth_is_adj(const SynthLayout& L, uint32_t sub) {
@@ -223,6 +275,78 @@ int Snapshot::build_hash_tables() {
   ds.nmap_vals = nv;
   ds.nmap_mask = slots - 1;
   HIPC(hipStreamSynchronize(stream));
+  return build_reverse();
+}
+
+// Reverse indexes for the backward tier: parents through set-adjacency, and the holders of every
+// subject (its row entries sorted by subject, plus a subject -> range hash).  Skipped (tier off)
+// when row positions do not fit u32.
+int Snapshot::build_reverse() {
+  const uint32_t nn = ds.n_nodes;
+  const uint64_t E = n_set_edges, R = h_row_off_last;
+  ds.radj = nullptr;
+  if (R >= 0xFFFFFFFFull || nn == 0) return 0;
+  uint64_t* roff = nullptr;
+  uint32_t* radj = nullptr;
+  if (alloc((void**)&roff, ((size_t)nn + 1) * 8) || alloc((void**)&radj, (E + 1) * 4)) return -1;
+  unsigned long long* deg = nullptr;
+  HIPC(hipMalloc(&deg, ((size_t)nn + 1) * 8));
+  HIPC(hipMemsetAsync(deg, 0, ((size_t)nn + 1) * 8, stream));
+  const uint32_t grid = (nn + 255) / 256;
+  if (E) hipLaunchKernelGGL(k_indeg, dim3(4096), dim3(256), 0, stream, ds.adj, E, deg);
+  HIPC(hipGetLastError());
+  size_t tmp_bytes = 0;
+  HIPC(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, (uint64_t*)deg, roff, (size_t)nn + 1, stream));
+  void* tmp = nullptr;
+  HIPC(hipMalloc(&tmp, tmp_bytes + 16));
+  HIPC(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, (uint64_t*)deg, roff, (size_t)nn + 1, stream));
+  HIPC(hipMemcpyAsync(deg, roff, ((size_t)nn + 1) * 8, hipMemcpyDeviceToDevice, stream));
+  hipLaunchKernelGGL(k_fill_radj, dim3(grid), dim3(256), 0, stream, ds.adj_off, ds.adj, nn, deg, radj);
+  HIPC(hipGetLastError());
+  HIPC(hipStreamSynchronize(stream));
+  HIPC(hipFree(tmp));
+  HIPC(hipFree(deg));
+  // holders: sort (subject, node) by subject
+  uint32_t *k0, *k1, *v0, *v1;
+  HIPC(hipMalloc(&k0, R * 4 + 4));
+  HIPC(hipMalloc(&k1, R * 4 + 4));
+  HIPC(hipMalloc(&v0, R * 4 + 4));
+  HIPC(hipMalloc(&v1, R * 4 + 4));
+  HIPC(hipMemcpyAsync(k0, ds.row_subj, R * 4, hipMemcpyDeviceToDevice, stream));
+  hipLaunchKernelGGL(k_row_nodes, dim3(grid), dim3(256), 0, stream, ds.row_off, nn, v0);
+  HIPC(hipGetLastError());
+  hipcub::DoubleBuffer<uint32_t> kb(k0, k1), vb(v0, v1);
+  tmp_bytes = 0;
+  HIPC(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, kb, vb, (size_t)R, 0, 32, stream));
+  HIPC(hipMalloc(&tmp, tmp_bytes + 16));
+  HIPC(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, kb, vb, (size_t)R, 0, 32, stream));
+  unsigned long long* cnt;
+  HIPC(hipMalloc(&cnt, 8));
+  HIPC(hipMemsetAsync(cnt, 0, 8, stream));
+  if (R) hipLaunchKernelGGL(k_count_runs, dim3(4096), dim3(256), 0, stream, kb.Current(), R, cnt);
+  unsigned long long distinct = 0;
+  HIPC(hipMemcpyAsync(&distinct, cnt, 8, hipMemcpyDeviceToHost, stream));
+  HIPC(hipStreamSynchronize(stream));
+  const uint64_t slots = pow2_at_least(std::max<uint64_t>(16, distinct * 2));
+  uint32_t *hk, *hold;
+  uint2* hv;
+  if (alloc((void**)&hk, slots * 4) || alloc((void**)&hv, slots * 8) || alloc((void**)&hold, R * 4 + 4)) return -1;
+  HIPC(hipMemsetAsync(hk, 0xFF, slots * 4, stream));
+  HIPC(hipMemsetAsync(hv, 0, slots * 8, stream));
+  if (R) {
+    hipLaunchKernelGGL(k_hold_insert, dim3(4096), dim3(256), 0, stream, kb.Current(), R, hk, hv, slots - 1);
+    hipLaunchKernelGGL(k_hold_count, dim3(4096), dim3(256), 0, stream, kb.Current(), R, hk, hv, slots - 1);
+    HIPC(hipGetLastError());
+    HIPC(hipMemcpyAsync(hold, vb.Current(), R * 4, hipMemcpyDeviceToDevice, stream));
+  }
+  HIPC(hipStreamSynchronize(stream));
+  for (void* p : {(void*)k0, (void*)k1, (void*)v0, (void*)v1, tmp, (void*)cnt}) HIPC(hipFree(p));
+  ds.radj_off = roff;
+  ds.radj = radj;
+  ds.hold = hold;
+  ds.hkeys = hk;
+  ds.hvals = hv;
+  ds.hmask = slots - 1;
   return 0;
 }
 

@@ -1,0 +1,17 @@
+# A/B of bench knobs: each argument is one quoted bench arg string; one bench line per variant
+set -u
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+python -c "import __graft_entry__ as g; g.build()" > gpurun_out/build.log 2>&1 || exit 4
+i=0
+for v in "$@"; do
+  i=$((i+1))
+  timeout -k 10 200 python bench.py --cpu-seconds 0 --steps 10 --warmup 3 $v > gpurun_out/ab_$i.log 2>&1; rc=$?
+  echo "[$v] rc=$rc"
+  if [ $rc -ne 0 ]; then tail -5 gpurun_out/ab_$i.log; exit $rc; fi
+  python - gpurun_out/ab_$i.log <<'PY'
+import json,sys
+d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+print(" value=%.3e ms=%.3f k_stream_ms=%.3f tiers=%s" % (d["value"], d["ms_per_step"], d["roofline"]["launch_ms"], d["tiers"]))
+PY
+done

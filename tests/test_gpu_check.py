@@ -76,7 +76,7 @@ def test_random_graphs_vs_oracle(seed):
 
 
 def test_heavy_path_overflow_star():
-    # one query reaching > LDS capacity (512 visited) forces the workgroup (HBM bitmap) tier
+    # one query reaching > LDS capacity (512 visited) leaves the wave tiers (backward / grid tier)
     tuples = [RelationTuple.from_string(f"g:root#m@(g:c{i}#m)") for i in range(3000)]
     tuples += [RelationTuple.from_string(f"g:c{i}#m@(g:d{i % 700}#m)") for i in range(3000)]
     tuples += [RelationTuple.from_string("g:d699#m@target"), RelationTuple.from_string("g:c5#m@near")]
@@ -92,13 +92,15 @@ def test_heavy_path_overflow_star():
         out, _ = e.batch_check_ids(queries_array(q6, 0), with_stats=True)
         exp, _, _ = oracle.check_batch(q6, np.zeros(len(qs), np.int32), gmax)
         assert list(out) == list(exp), (gmax, out, exp)
-    assert e.last_stats["n_medium"] + e.last_stats["n_heavy"] >= 1
+    assert e.last_stats["n_medium"] + e.last_stats["n_heavy"] + e.last_stats["n_back"] >= 1
 
 
-@pytest.mark.parametrize("tiers,wide", [(0, 0), (0, 1), (1, 1), (2, 0)])
-def test_workgroup_tiers_lds_and_hbm(tiers, wide):
-    # > 256 expanded nodes leaves the wave tiers; tiers=0 sends them to the grid tier, 1/2 first to
-    # the LDS workgroup tier (<= 4096 expanded nodes), then to the grid / HBM workgroup tier
+@pytest.mark.parametrize("tiers,wide,back", [(0, 0, 0), (0, 1, 0), (1, 1, 0), (2, 0, 0), (0, 0, 1), (1, 0, 1)])
+def test_workgroup_tiers_lds_and_hbm(tiers, wide, back):
+    # > 256 expanded nodes leaves the wave tiers; with back=1 the backward tier (reverse search
+    # from the subject's holders) answers first and hands on what outgrows it; tiers=0 sends the
+    # rest to the grid tier, 1/2 first to the LDS workgroup tier (<= 4096 expanded nodes), then to
+    # the grid / HBM workgroup tier
     tuples = [RelationTuple.from_string(f"g:root#m@(g:c{i}#m)") for i in range(5000)]
     tuples += [RelationTuple.from_string(f"g:c{i}#m@(g:d{i % 1500}#m)") for i in range(5000)]
     tuples += [RelationTuple.from_string(f"g:d{i}#m@(g:e{i % 400}#m)") for i in range(1500)]
@@ -107,17 +109,21 @@ def test_workgroup_tiers_lds_and_hbm(tiers, wide):
     tuples += [RelationTuple.from_string(f"g:r2#m@(g:f{i}#m)") for i in range(1000)]
     tuples += [RelationTuple.from_string(f"g:f{i}#m@(g:h{i % 100}#m)") for i in range(1000)]
     tuples += [RelationTuple.from_string("g:h99#m@deep")]
+    # a subject held by ~1900 nodes whose parents outgrow the backward tier's LDS (-> forward)
+    tuples += [RelationTuple.from_string(f"g:d{i}#m@pop") for i in range(1500)]
+    tuples += [RelationTuple.from_string(f"g:e{i}#m@pop") for i in range(400)]
     reg = Registry(tuples, [])
     e = reg.permission_engine()
     e.snapshot.tune("tiers", tiers)
     e.snapshot.tune("wide", wide)
+    e.snapshot.tune("back", back)
     it = reg.interner
     qs = [RelationTuple.from_string(s) for s in
           ["g:root#m@target", "g:root#m@mid", "g:root#m@none", "g:c3#m@target", "g:c7#m@mid", "g:d3#m@target",
-           "g:r2#m@deep", "g:r2#m@none"]]
+           "g:r2#m@deep", "g:r2#m@none", "g:root#m@pop", "g:r2#m@pop", "g:root#m@deep"]]
     q6 = np.asarray([it.tuple_ids(t) for t in qs], np.uint32)
     oracle = Oracle(it.tuples_array(tuples), it.wildcard_rel)
-    tiers_mode, tiers = tiers, {"n_medium": 0, "n_heavy": 0}
+    tiers_mode, tiers = tiers, {"n_medium": 0, "n_heavy": 0, "n_back": 0, "n_no_holder": 0}
     for gmax in (2, 3, 4, 5, 6):
         e.config.max_read_depth = gmax
         out, _ = e.batch_check_ids(queries_array(q6, 0), with_stats=True)
@@ -126,6 +132,7 @@ def test_workgroup_tiers_lds_and_hbm(tiers, wide):
         for k in tiers:
             tiers[k] += e.last_stats[k]
     assert tiers["n_heavy"] >= 1 and (tiers["n_medium"] >= 1) == (tiers_mode > 0), tiers
+    assert (tiers["n_back"] >= 1) == bool(back) and (tiers["n_no_holder"] >= 1) == bool(back), tiers
 
 
 def test_empty_and_unknown():
