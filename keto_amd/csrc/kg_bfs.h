@@ -18,17 +18,27 @@ namespace kg {
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
-__device__ __forceinline__ uint32_t nmap_find(const DevSnap& s, uint32_t ns, uint32_t rel, uint32_t obj) {
-  if (ns >= 0xFFFFu || rel >= 0xFFFFu || obj >= 0x7FFFFFFFu) return NONE;
-  uint64_t key = nmap_key(ns, rel, obj);
-  uint64_t i = mix64(key) & s.nmap_mask;
+// Node-map lookup: the slot of (ns, rel, obj), or nullptr.  The first slot is passed in when the
+// caller already issued its load (k_resolve overlaps it with other lookups).
+__device__ __forceinline__ const NSlot* nmap_slot(const DevSnap& s, uint64_t key, uint64_t i) {
   for (uint64_t p = 0; p <= s.nmap_mask; p++) {  // load <= 0.5: ends at an empty slot long before
-    uint64_t k = s.nmap_keys[i];
-    if (k == key) return s.nmap_vals[i];
-    if (k == EMPTY64) return NONE;
+    const uint64_t k = s.nmap[i].key;
+    if (k == key) return &s.nmap[i];
+    if (k == EMPTY64) return nullptr;
     i = (i + 1) & s.nmap_mask;
   }
-  return NONE;
+  return nullptr;
+}
+
+__device__ __forceinline__ bool nmap_key_ok(uint32_t ns, uint32_t rel, uint32_t obj) {
+  return ns < 0xFFFFu && rel < 0xFFFFu && obj < 0x7FFFFFFFu;
+}
+
+__device__ __forceinline__ uint32_t nmap_find(const DevSnap& s, uint32_t ns, uint32_t rel, uint32_t obj) {
+  if (!nmap_key_ok(ns, rel, obj)) return NONE;
+  const uint64_t key = nmap_key(ns, rel, obj);
+  const NSlot* sl = nmap_slot(s, key, mix64(key) & s.nmap_mask);
+  return sl ? sl->node : NONE;
 }
 
 // checkDirect: does the exact tuple (node, subject) exist?  One 64-B bucket per probe.
@@ -53,9 +63,9 @@ __device__ __forceinline__ uint2 holders_find(const DevSnap& s, uint32_t subj) {
   if (subj == NONE) return make_uint2(0, 0);
   uint64_t h = mix64(subj) & s.hmask;
   for (uint64_t p = 0; p <= s.hmask; p++) {  // load <= 0.5
-    const uint32_t k = s.hkeys[h];
-    if (k == subj) return s.hvals[h];
-    if (k == NONE) break;
+    const HSlot sl = s.hslots[h];
+    if (sl.key == subj) return make_uint2(sl.first, sl.count);
+    if (sl.key == NONE) break;
     h = (h + 1) & s.hmask;
   }
   return make_uint2(0, 0);

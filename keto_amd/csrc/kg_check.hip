@@ -105,11 +105,30 @@ __global__ __launch_bounds__(256) void k_resolve(DevSnap s, const kg_query* __re
   bool did_probe = false, no_holder = false;
   if (valid) {
     kg_query x = q[i];
-    uint32_t node = nmap_find(s, x.t.ns, x.t.rel, x.t.obj);
-    uint32_t subj;
-    if (x.t.sns == KG_SUBJECT_ID) {
-      subj = x.t.sobj < 0x7FFFFFFFu ? x.t.sobj : NONE;
-    } else {
+    // node map and (for a subject id) holder hash: the first slots of both are loaded together,
+    // so the common case is one round trip for both lookups
+    const bool key_ok = nmap_key_ok(x.t.ns, x.t.rel, x.t.obj);
+    const uint64_t key = nmap_key(x.t.ns, x.t.rel, x.t.obj);
+    const uint64_t ni = mix64(key) & s.nmap_mask;
+    const bool sid = x.t.sns == KG_SUBJECT_ID;
+    uint32_t subj = sid ? (x.t.sobj < 0x7FFFFFFFu ? x.t.sobj : NONE) : NONE;
+    const bool want_h = no_holder_filter && sid && subj != NONE;
+    const uint64_t hi = mix64(subj) & s.hmask;
+    HSlot h0{};
+    if (want_h) h0 = s.hslots[hi];
+    NSlot n0{};
+    if (key_ok) n0 = s.nmap[ni];
+    uint32_t node = NONE, rb = 0, rl = 0;
+    if (key_ok) {
+      const NSlot* sl = n0.key == key ? &n0 : (n0.key == EMPTY64 ? nullptr : nmap_slot(s, key, (ni + 1) & s.nmap_mask));
+      if (sl) {
+        const NSlot v = *sl;
+        node = v.node;
+        rb = v.beg;
+        rl = v.len;
+      }
+    }
+    if (!sid) {
       uint32_t sn = nmap_find(s, x.t.sns, x.t.srel, x.t.sobj);
       subj = sn == NONE ? NONE : (SET_BIT | sn);
     }
@@ -122,20 +141,22 @@ __global__ __launch_bounds__(256) void k_resolve(DevSnap s, const kg_query* __re
       bool impure = s.nflags && (s.nflags[node] & NF_IMPURE);
       route = impure ? ROUTE_GENERAL : ROUTE_LIGHT;
     }
-    uint32_t rb = 0, rl = 0;
     bool member = false;
     did_probe = route == ROUTE_LIGHT;
     if (route == ROUTE_LIGHT) {
       // the root's checkDirect(D-1) (D >= 1 always) is thread-parallel here: a direct tuple or a
       // depth that cannot reach any child (D < 2) finishes the query before the wave tier
-      rb = (uint32_t)s.adj_off[node];
-      rl = (uint32_t)(s.adj_off[node + 1] - s.adj_off[node]);
       member = dset_probe(s, node, subj);
       if (member || d < 2 || rl == 0) route = ROUTE_DONE;
       // a subject that no row holds cannot be reached from any root (checkDirect never hits)
-      if (route == ROUTE_LIGHT && no_holder_filter && holders_find(s, subj).y == 0) {
-        route = ROUTE_DONE;
-        no_holder = true;
+      if (route == ROUTE_LIGHT && no_holder_filter) {
+        const uint32_t cnt = want_h ? (h0.key == subj ? h0.count
+                                                      : (h0.key == NONE ? 0u : holders_find(s, subj).y))
+                                    : holders_find(s, subj).y;
+        if (cnt == 0) {
+          route = ROUTE_DONE;
+          no_holder = true;
+        }
       }
     }
     rq[i] = RQuery{node, subj, d, route, rb, rl};

@@ -9,7 +9,8 @@
 //                                        (internal/expand/engine.go:57-94) and tuple-to-subject-set.
 //   dset                                  bucketed hash set of (node << 32 | tagged subject):
 //                                        checkDirect's exact-tuple query (engine.go:159-163).
-//   nmap                                  (ns,rel,obj) -> node id, for request mapping on device.
+//   nmap                                  (ns,rel,obj) -> node id + its set row (begin, length), one
+//                                        32-B slot per key, for request mapping on device.
 //   nflags[n_nodes] u8                    bit0 IMPURE: a rewrite / undeclared relation is reachable
 //                                        through set-adjacency (needs the rewrite interpreter).
 //   radj_off[n_nodes+1] u64 / radj[] u32  reverse set-adjacency (parents), for the backward tier.
@@ -74,6 +75,18 @@ __host__ __device__ __forceinline__ bool sig_maybe(uint32_t sig, uint32_t subj_m
   return (sig & subj_mask) == subj_mask;
 }
 
+// Node-map slot: key (ns,rel,obj), node id and the node's set-adjacency row, one 32-B slot so a
+// request mapping is one random line.  key == EMPTY64: free.
+struct NSlot {
+  uint64_t key;
+  uint32_t node, beg, len, pad0;
+  uint64_t pad1;
+};
+// Holder-hash slot: tagged subject -> hold[first, first + count).  key == NONE: free.
+struct HSlot {
+  uint32_t key, first, count, pad;
+};
+
 // Everything a kernel needs, passed by value.
 struct DevSnap {
   uint32_t n_nodes;
@@ -85,8 +98,7 @@ struct DevSnap {
   const uint32_t* row_subj;
   const uint64_t* dset;
   uint64_t dset_mask;  // n_buckets - 1
-  const uint64_t* nmap_keys;
-  const uint32_t* nmap_vals;
+  const NSlot* nmap;
   uint64_t nmap_mask;  // n_slots - 1
   const uint8_t* nflags;  // nullptr: every node pure
   const uint32_t* nd_ns;
@@ -104,8 +116,7 @@ struct DevSnap {
   const uint64_t* radj_off;  // [n_nodes+1] parents of a node through set-adjacency
   const uint32_t* radj;
   const uint32_t* hold;      // holder nodes (rows containing a subject), grouped by subject
-  const uint32_t* hkeys;     // subject hash: tagged subject, NONE = empty slot
-  const uint2* hvals;        // (first index into hold, holder count)
+  const HSlot* hslots;       // subject hash: tagged subject -> (first index into hold, count)
   uint64_t hmask;            // n_slots - 1
 };
 

@@ -45,17 +45,19 @@ __global__ void k_dset_insert_rows(uint64_t* dset, uint64_t mask, const uint64_t
   }
 }
 
-__global__ void k_nmap_insert(uint64_t* keys, uint32_t* vals, uint64_t mask, const uint32_t* nd_ns,
-                              const uint32_t* nd_obj, const uint32_t* nd_rel, uint32_t n_nodes) {
+__global__ void k_nmap_insert(NSlot* nm, uint64_t mask, const uint32_t* nd_ns, const uint32_t* nd_obj,
+                              const uint32_t* nd_rel, const uint64_t* adj_off, uint32_t n_nodes) {
   uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
   if (v >= n_nodes) return;
   uint64_t key = nmap_key(nd_ns[v], nd_rel[v], nd_obj[v]);
   uint64_t i = mix64(key) & mask;
   for (uint64_t n = 0; n <= mask; n++) {  // sized for load <= 0.5: always finds room
     unsigned long long old =
-        atomicCAS((unsigned long long*)&keys[i], (unsigned long long)EMPTY64, (unsigned long long)key);
+        atomicCAS((unsigned long long*)&nm[i].key, (unsigned long long)EMPTY64, (unsigned long long)key);
     if (old == EMPTY64 || old == key) {
-      vals[i] = v;
+      nm[i].node = v;
+      nm[i].beg = (uint32_t)adj_off[v];
+      nm[i].len = (uint32_t)(adj_off[v + 1] - adj_off[v]);
       return;
     }
     i = (i + 1) & mask;
@@ -109,25 +111,25 @@ __global__ void k_count_runs(const uint32_t* key, uint64_t n, unsigned long long
 }
 __device__ __forceinline__ uint64_t hold_slot(uint32_t key, uint64_t mask) { return mix64(key) & mask; }
 // run starts insert (subject -> first index); run ends then add the count
-__global__ void k_hold_insert(const uint32_t* key, uint64_t n, uint32_t* hkeys, uint2* hvals, uint64_t mask) {
+__global__ void k_hold_insert(const uint32_t* key, uint64_t n, HSlot* hs, uint64_t mask) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     if (i != 0 && key[i] == key[i - 1]) continue;
     const uint32_t k = key[i];
     for (uint64_t h = hold_slot(k, mask), p = 0; p <= mask; p++, h = (h + 1) & mask) {  // load <= 0.5
-      if (atomicCAS(&hkeys[h], NONE, k) == NONE) {
-        hvals[h].x = (uint32_t)i;
+      if (atomicCAS(&hs[h].key, NONE, k) == NONE) {
+        hs[h].first = (uint32_t)i;
         break;
       }
     }
   }
 }
-__global__ void k_hold_count(const uint32_t* key, uint64_t n, const uint32_t* hkeys, uint2* hvals, uint64_t mask) {
+__global__ void k_hold_count(const uint32_t* key, uint64_t n, HSlot* hs, uint64_t mask) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     if (i + 1 != n && key[i] == key[i + 1]) continue;
     const uint32_t k = key[i];
     for (uint64_t h = hold_slot(k, mask), p = 0; p <= mask; p++, h = (h + 1) & mask)
-      if (hkeys[h] == k) {
-        hvals[h].y = (uint32_t)(i + 1 - hvals[h].x);
+      if (hs[h].key == k) {
+        hs[h].count = (uint32_t)(i + 1 - hs[h].first);
         break;
       }
   }
@@ -256,23 +258,21 @@ int Snapshot::build_hash_tables() {
   if (alloc((void**)&dset, buckets * DSET_BUCKET * 8)) return -1;
   HIPC(hipMemsetAsync(dset, 0xFF, buckets * DSET_BUCKET * 8, stream));
   uint64_t slots = pow2_at_least(std::max<uint64_t>(16, (uint64_t)ds.n_nodes * 2));
-  uint64_t* nk = nullptr;
-  uint32_t* nv = nullptr;
-  if (alloc((void**)&nk, slots * 8) || alloc((void**)&nv, slots * 4)) return -1;
-  HIPC(hipMemsetAsync(nk, 0xFF, slots * 8, stream));
+  NSlot* nm = nullptr;
+  if (alloc((void**)&nm, slots * sizeof(NSlot))) return -1;
+  HIPC(hipMemsetAsync(nm, 0xFF, slots * sizeof(NSlot), stream));
   uint32_t grid = (ds.n_nodes + 255) / 256;
   if (ds.n_nodes) {
     hipLaunchKernelGGL(k_dset_insert_rows, dim3(grid), dim3(256), 0, stream, dset, buckets - 1, ds.row_off,
                        ds.row_subj, ds.n_nodes);
     HIPC(hipGetLastError());
-    hipLaunchKernelGGL(k_nmap_insert, dim3(grid), dim3(256), 0, stream, nk, nv, slots - 1, ds.nd_ns, ds.nd_obj,
-                       ds.nd_rel, ds.n_nodes);
+    hipLaunchKernelGGL(k_nmap_insert, dim3(grid), dim3(256), 0, stream, nm, slots - 1, ds.nd_ns, ds.nd_obj,
+                       ds.nd_rel, ds.adj_off, ds.n_nodes);
     HIPC(hipGetLastError());
   }
   ds.dset = dset;
   ds.dset_mask = buckets - 1;
-  ds.nmap_keys = nk;
-  ds.nmap_vals = nv;
+  ds.nmap = nm;
   ds.nmap_mask = slots - 1;
   HIPC(hipStreamSynchronize(stream));
   return build_reverse();
@@ -328,14 +328,13 @@ int Snapshot::build_reverse() {
   HIPC(hipMemcpyAsync(&distinct, cnt, 8, hipMemcpyDeviceToHost, stream));
   HIPC(hipStreamSynchronize(stream));
   const uint64_t slots = pow2_at_least(std::max<uint64_t>(16, distinct * 2));
-  uint32_t *hk, *hold;
-  uint2* hv;
-  if (alloc((void**)&hk, slots * 4) || alloc((void**)&hv, slots * 8) || alloc((void**)&hold, R * 4 + 4)) return -1;
-  HIPC(hipMemsetAsync(hk, 0xFF, slots * 4, stream));
-  HIPC(hipMemsetAsync(hv, 0, slots * 8, stream));
+  uint32_t* hold;
+  HSlot* hs;
+  if (alloc((void**)&hs, slots * sizeof(HSlot)) || alloc((void**)&hold, R * 4 + 4)) return -1;
+  HIPC(hipMemsetAsync(hs, 0xFF, slots * sizeof(HSlot), stream));
   if (R) {
-    hipLaunchKernelGGL(k_hold_insert, dim3(4096), dim3(256), 0, stream, kb.Current(), R, hk, hv, slots - 1);
-    hipLaunchKernelGGL(k_hold_count, dim3(4096), dim3(256), 0, stream, kb.Current(), R, hk, hv, slots - 1);
+    hipLaunchKernelGGL(k_hold_insert, dim3(4096), dim3(256), 0, stream, kb.Current(), R, hs, slots - 1);
+    hipLaunchKernelGGL(k_hold_count, dim3(4096), dim3(256), 0, stream, kb.Current(), R, hs, slots - 1);
     HIPC(hipGetLastError());
     HIPC(hipMemcpyAsync(hold, vb.Current(), R * 4, hipMemcpyDeviceToDevice, stream));
   }
@@ -344,8 +343,7 @@ int Snapshot::build_reverse() {
   ds.radj_off = roff;
   ds.radj = radj;
   ds.hold = hold;
-  ds.hkeys = hk;
-  ds.hvals = hv;
+  ds.hslots = hs;
   ds.hmask = slots - 1;
   return 0;
 }
