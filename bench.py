@@ -27,6 +27,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+STREAM_KERNELS = {0: "k_stream<8,7,256,16>", 1: "k_stream<16,6,256,32>", 2: "k_stream<16,7,512,32>"}
 
 
 def parse():
@@ -40,6 +41,7 @@ def parse():
     ap.add_argument("--seed", type=int, default=20250131)
     ap.add_argument("--tiers", type=int, default=0, help="kg_snapshot_tune tiers (0 grid, 1 LDS-WG+grid, 2 WG)")
     ap.add_argument("--wide", type=int, default=0, help="kg_snapshot_tune wide (k_light<64> tier on/off)")
+    ap.add_argument("--stream", type=int, default=1, help="kg_snapshot_tune stream (k_stream variant 0/1/2)")
     ap.add_argument("--back", type=int, default=1, help="kg_snapshot_tune back (backward tier + no-holder filter)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline time budget (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=16)
@@ -136,6 +138,7 @@ def main():
     snap.tune("tiers", a.tiers)
     snap.tune("wide", a.wide)
     snap.tune("back", a.back)
+    snap.tune("stream", a.stream)
     info = snap.info()
     t_build = time.time() - t_build
 
@@ -209,7 +212,7 @@ def main():
                                    "probes": int(stats[-1].direct_probes)},
                            "back": {"rows": int(stats[-1].back_rows), "edges": int(stats[-1].back_edges)}},
         "snapshot_build_s": t_build,
-        "roofline": {"kernel": "k_stream<8,7,256>", "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "roofline": {"kernel": STREAM_KERNELS[a.stream], "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "bytes_model": "8*rows_opened + 4*edges_read + 16*direct_probes (per k_stream launch; R/E/P counted in-kernel)",
                      "launch_ms": float(l_ms.mean()), "bytes_per_launch": float(l_bytes.mean())},

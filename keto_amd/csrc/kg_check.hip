@@ -448,6 +448,7 @@ __global__ __launch_bounds__(256) void k_stream(DevSnap s, const RQuery* __restr
   constexpr int VIS = Lds::VIS;
   constexpr uint32_t INS_CAP = VIS * 5 / 8;  // expanded nodes per query (hash load <= 5/8)
   static_assert(Q <= 16 && Q <= 64, "slot field is 4 bits");
+  static_assert(CHUNK <= 64, "one chunk entry per lane");
   __shared__ Lds lds_all[4];
   Lds& L = lds_all[threadIdx.x >> 6];
   const int lane = lane_id();
@@ -463,7 +464,9 @@ __global__ __launch_bounds__(256) void k_stream(DevSnap s, const RQuery* __restr
   __builtin_amdgcn_wave_barrier();
   uint32_t active = 0;  // wave-uniform: slots holding a query
   bool drained = false;  // the work list is exhausted (the local chunk may still hold entries)
-  uint32_t c_first = 0, c_left = 0;  // wave-local chunk of list positions
+  uint32_t c_left = 0, c_pos = 0;  // wave-local chunk: entries left, next entry
+  uint32_t cq_qi = 0, cq_node = 0, cq_subj = 0, cq_beg = 0, cq_len = 0;  // lane i: chunk entry i
+  int32_t cq_depth = 0;
   uint32_t head = 0, tail = 0, head_off = 0;
   bool pend = false;  // per lane: a child of the previous step awaiting its probe
   uint32_t pend_node = 0, pend_slot = 0, pend_gen = 0;
@@ -473,39 +476,53 @@ __global__ __launch_bounds__(256) void k_stream(DevSnap s, const RQuery* __restr
     const uint32_t freem = ~active & ((1u << Q) - 1);
     const uint32_t want = __popc(freem);
     if (want && !drained && (tail - head) + want <= QC) {
-      // the wave pulls CHUNK consecutive list entries per dequeue and refills from them: a refill
-      // per finished query would put one device-scope atomic per query on the per-XCD heads
+      // the wave pulls CHUNK consecutive list entries per dequeue (one device-scope atomic on the
+      // per-XCD heads per CHUNK queries) and stages their RQuery records in lanes, so a refill
+      // costs shuffles instead of two dependent HBM round trips
       if (c_left == 0) {
-        uint32_t got = 0;
-        if (lane == 0) c_first = dequeue_n(wl, heads, head_sel, head0, CHUNK, got);
-        c_first = __shfl(c_first, 0, 64);
+        uint32_t got = 0, first = 0;
+        if (lane == 0) first = dequeue_n(wl, heads, head_sel, head0, CHUNK, got);
+        first = __shfl(first, 0, 64);
         c_left = __shfl(got, 0, 64);
-        if (c_first == NONE) drained = true;
+        c_pos = 0;
+        if (first == NONE) {
+          drained = true;
+        } else if ((uint32_t)lane < c_left) {  // lane i stages chunk entry i (two dependent loads per chunk)
+          cq_qi = wl.list[first + lane];
+          const RQuery q = rq[cq_qi];
+          cq_node = q.node;
+          cq_subj = q.subj;
+          cq_depth = q.depth;
+          cq_beg = q.beg;
+          cq_len = q.len;
+        }
       }
       const uint32_t got = min(want, c_left);
       if (got) {
-        const uint32_t first = c_first;
-        c_first += got;
+        const int src = (uint32_t)lane < got ? (int)(c_pos + lane) : lane;
+        const uint32_t qi = __shfl(cq_qi, src, 64), qnode = __shfl(cq_node, src, 64),
+                       qsubj = __shfl(cq_subj, src, 64), qbeg = __shfl(cq_beg, src, 64),
+                       qlen = __shfl(cq_len, src, 64);
+        const int32_t qdepth = __shfl(cq_depth, src, 64);
+        c_pos += got;
         c_left -= got;
         uint32_t slot = 0;
         if ((uint32_t)lane < got) {
           uint32_t m = freem;
           for (int k = 0; k < lane; k++) m &= m - 1;
           slot = __ffs(m) - 1;
-          const uint32_t qi = wl.list[first + lane];
-          const RQuery q = rq[qi];
           const uint32_t gen = L.s_gen[slot];
-          const bool over = q.depth > 0xFFFF || q.len > LONG_ROW;
+          const bool over = qdepth > 0xFFFF || qlen > LONG_ROW;
           L.s_qi[slot] = qi;
-          L.s_subj[slot] = q.subj;
+          L.s_subj[slot] = qsubj;
           L.s_flag[slot] = over ? SF_OVER : 0u;
           L.s_cnt[slot] = 1;
           L.s_ins[slot] = 1;
-          lx_insert3<VLOG2>(&L.vis[slot * VIS], q.node);
+          lx_insert3<VLOG2>(&L.vis[slot * VIS], qnode);
           const uint32_t at = (tail + lane) % QC;
-          L.e_beg[at] = q.beg;
-          L.e_len[at] = over ? 0u : q.len;
-          L.e_meta[at] = (slot << 28) | ((gen & 0xFFF) << 16) | (uint32_t)(over ? 2 : q.depth);
+          L.e_beg[at] = qbeg;
+          L.e_len[at] = over ? 0u : qlen;
+          L.e_meta[at] = (slot << 28) | ((gen & 0xFFF) << 16) | (uint32_t)(over ? 2 : qdepth);
         }
         active |= wave_or((uint32_t)lane < got ? 1u << slot : 0u);
         tail += got;
@@ -1097,11 +1114,20 @@ int check_batch_device(Snapshot* s, const kg_query* d_q, size_t n, int32_t globa
                          WorkList{light, ctl->light8, (uint32_t)n, 1u}, ctl->heads, d_out, d_err, ovf_list,
                          ovf_count, ctl);
     } else {
-      // ~30 KiB of LDS per workgroup (8 slots x 512 B visited + 256-entry FIFO per wave): 5 per CU
-      const uint32_t grid = (uint32_t)std::min<uint64_t>((uint64_t)s->n_cu * 5, (n + 31) / 32 + 8);
-      hipLaunchKernelGGL((k_stream<8, 7, 256, 16>), dim3(grid), dim3(256), 0, stream, s->ds, rq,
-                         WorkList{light, ctl->light8, (uint32_t)n, 1u}, ctl->heads, d_out, d_err, ovf_list,
-                         ovf_count, ctl);
+      // ~30 KiB of LDS per workgroup (variant 0: 8 slots x 512 B visited + 256-entry FIFO per wave;
+      // 1: 16 slots x 256 B; 2: 16 slots x 512 B + 512-entry FIFO): 5 (2: 3) workgroups per CU
+      const WorkList wl{light, ctl->light8, (uint32_t)n, 1u};
+      const uint32_t per_cu = s->stream_variant == 2 ? 3 : 5;
+      const uint32_t grid = (uint32_t)std::min<uint64_t>((uint64_t)s->n_cu * per_cu, (n + 31) / 32 + 8);
+      if (s->stream_variant == 1)
+        hipLaunchKernelGGL((k_stream<16, 6, 256, 32>), dim3(grid), dim3(256), 0, stream, s->ds, rq, wl, ctl->heads,
+                           d_out, d_err, ovf_list, ovf_count, ctl);
+      else if (s->stream_variant == 2)
+        hipLaunchKernelGGL((k_stream<16, 7, 512, 32>), dim3(grid), dim3(256), 0, stream, s->ds, rq, wl, ctl->heads,
+                           d_out, d_err, ovf_list, ovf_count, ctl);
+      else
+        hipLaunchKernelGGL((k_stream<8, 7, 256, 16>), dim3(grid), dim3(256), 0, stream, s->ds, rq, wl, ctl->heads,
+                           d_out, d_err, ovf_list, ovf_count, ctl);
     }
     HIPC(hipGetLastError());
     if (stats) HIPC(hipEventRecord(l1, stream));

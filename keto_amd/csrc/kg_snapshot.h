@@ -60,6 +60,7 @@ struct Snapshot {
   void* interp_pool = nullptr;
   size_t interp_pool_bytes = 0;
   uint64_t batch_seq = 0;
+  int stream_variant = 1;  // kg_snapshot_tune("stream"): k_stream slots/LDS variant (0, 1, 2)
   int back_tier = 1;  // kg_snapshot_tune("back"): backward tier + no-holder filter in k_resolve
 
   ~Snapshot();

@@ -58,6 +58,7 @@ def test_random_graphs_vs_oracle(seed):
     it, tuples, nss, rels = random_graph(rng, n_obj=40 + 20 * seed, n_rows=200 + 150 * seed)
     reg = Registry(tuples, [], interner=it)
     reg.snapshot.tune("light", seed % 2)  # first wave tier: k_stream (even seeds) / k_light<16> (odd)
+    reg.snapshot.tune("stream", (seed // 2) % 3)  # k_stream variants 0 / 1 / 2
     qs = random_queries(rng, nss, rels, 3000, n_obj=40 + 20 * seed)
     depths = rng.integers(-1, 9, len(qs))
     q6 = np.asarray([it.tuple_ids(t) for t in qs], np.uint32)
