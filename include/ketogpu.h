@@ -198,6 +198,39 @@ int kg_check_batch_device(kg_snapshot* s, const kg_query* d_q, size_t n, int32_t
  * 50% uniform doc#viewer@user queries, max_depth in {0,1..10}.  d_q is a device buffer. */
 int kg_synth_queries(kg_snapshot* s, uint64_t seed, size_t n, kg_query* d_q);
 
+/* ---- hash-sharded mode --------------------------------------------------------
+ * For graphs larger than one GPU: rank r of N holds the rows of the nodes (ns, obj, rel) with
+ * kg_shard_owner(ns, obj, N) == r (all relations of an object on one rank).  A batch is a
+ * level-synchronous BFS across ranks: every level each rank processes the frontier records it
+ * received (nodes it owns, or hit reports for queries it is home of) and writes the next level's
+ * records into one bucket per destination rank; the caller exchanges the buckets (all-to-all,
+ * RCCL over xGMI) and calls kg_shard_level again until no rank sends anything.  Replaces the
+ * single-GPU kg_check_batch for such snapshots (rewrite-free namespaces only; a snapshot with a
+ * rewrite program returns KG_ERR_NOT_IMPLEMENTED codes).  keto_amd/sharded.py is the driver. */
+typedef struct {
+  uint32_t q;     /* home rank << 26 | index in the home rank's batch                         */
+  uint32_t node;  /* node to check (checkIsAllowed(node, depth)), or KG_FREC_HIT              */
+  uint32_t subj;  /* tagged subject: bit31 set = subject-set node id, else subject id        */
+  int32_t depth;  /* rest depth (>= 1)                                                        */
+} kg_frec;
+#define KG_FREC_HIT 0xFFFFFFFFu /* kg_frec.node of a record reporting IsMember to the query's home */
+#define KG_SHARD_MAX_RANKS 64
+
+uint32_t kg_shard_owner(uint32_t ns, uint32_t obj, uint32_t nranks);
+int kg_snapshot_create_shard(const kg_tuple* rows, size_t n, const kg_dict* dict, const kg_rewrite_prog* prog,
+                             int device, uint32_t rank, uint32_t nranks, kg_snapshot** out);
+int kg_snapshot_synthetic_shard(const kg_synth_params* params, const kg_rewrite_prog* prog, int device,
+                                uint32_t rank, uint32_t nranks, kg_snapshot** out);
+/* Device buffers: d_out = nranks buckets of `cap` records; d_counts[nranks + 1]: records written
+ * per bucket (true counts: > cap means the bucket overflowed and the batch must be rerun with a
+ * larger cap) and, in [nranks], overflow flags (1 bucket, 2 visited table).  kg_shard_seed zeroes
+ * d_res (0 NotMember, 1 IsMember) / d_err and the counters; kg_shard_level zeroes the counters
+ * before writing.  Both only enqueue work on `stream` (NULL = the snapshot's stream). */
+int kg_shard_seed(kg_snapshot* s, const kg_query* d_q, size_t n, int32_t global_max_depth, kg_frec* d_out,
+                  size_t cap, uint32_t* d_counts, uint8_t* d_res, uint32_t* d_err, void* stream);
+int kg_shard_level(kg_snapshot* s, const kg_frec* d_in, size_t n_in, kg_frec* d_out, size_t cap,
+                   uint32_t* d_counts, uint8_t* d_res, void* stream);
+
 /* ---- expand ----------------------------------------------------------------------------- */
 int kg_expand_batch(kg_snapshot* s, const kg_set* roots, size_t n, int32_t global_max_depth, kg_tree_buf* out);
 void kg_tree_free(kg_tree_buf* t);

@@ -10,6 +10,8 @@ LIB_PATH = os.path.join(HERE, "lib", "libketogpu.so")
 
 KG_SUBJECT_ID = 0xFFFFFFFF
 KG_NOT_MEMBER, KG_IS_MEMBER, KG_ERROR = 0, 1, 2
+KG_FREC_HIT = 0xFFFFFFFF
+KG_SHARD_MAX_RANKS = 64
 KG_ERR_NONE, KG_ERR_RELATION_NOT_FOUND, KG_ERR_NOT_IMPLEMENTED, KG_ERR_REWRITE_CYCLE, KG_ERR_RESOURCE = 0, 1, 2, 3, 4
 
 
@@ -71,7 +73,8 @@ class kg_synth_params(C.Structure):
 # every symbol include/ketogpu.h declares
 EXPORTS = ["kg_snapshot_create", "kg_snapshot_synthetic", "kg_snapshot_destroy", "kg_snapshot_info", "kg_snapshot_tune", "kg_synth_ids",
            "kg_snapshot_export", "kg_snapshot_export_csr", "kg_check_batch", "kg_check_batch_device", "kg_synth_queries", "kg_expand_batch",
-           "kg_tree_free", "kg_last_error", "kg_version"]
+           "kg_tree_free", "kg_last_error", "kg_version", "kg_shard_owner", "kg_snapshot_create_shard",
+           "kg_snapshot_synthetic_shard", "kg_shard_seed", "kg_shard_level"]
 
 
 class KetoGPUError(RuntimeError):
@@ -111,8 +114,17 @@ def load(path: str = LIB_PATH):
     L.kg_last_error.argtypes = [C.c_char_p, sz]
     L.kg_last_error.restype = sz
     L.kg_version.restype = C.c_char_p
+    L.kg_shard_owner.argtypes = [u32, u32, u32]
+    L.kg_shard_owner.restype = u32
+    L.kg_snapshot_create_shard.argtypes = [vp, sz, C.POINTER(kg_dict), C.POINTER(kg_rewrite_prog), C.c_int, u32, u32,
+                                           C.POINTER(vp)]
+    L.kg_snapshot_synthetic_shard.argtypes = [C.POINTER(kg_synth_params), C.POINTER(kg_rewrite_prog), C.c_int, u32,
+                                              u32, C.POINTER(vp)]
+    L.kg_shard_seed.argtypes = [vp, vp, sz, i32, vp, sz, vp, vp, vp, vp]
+    L.kg_shard_level.argtypes = [vp, vp, sz, vp, sz, vp, vp, vp]
     for name in ("kg_snapshot_create", "kg_snapshot_synthetic", "kg_snapshot_info", "kg_snapshot_tune", "kg_synth_ids", "kg_check_batch",
-                 "kg_check_batch_device", "kg_synth_queries", "kg_expand_batch"):
+                 "kg_check_batch_device", "kg_synth_queries", "kg_expand_batch", "kg_snapshot_create_shard",
+                 "kg_snapshot_synthetic_shard", "kg_shard_seed", "kg_shard_level"):
         getattr(L, name).restype = C.c_int
     _lib = L
     return L

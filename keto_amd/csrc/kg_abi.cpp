@@ -93,6 +93,71 @@ int kg_snapshot_synthetic(const kg_synth_params* params, const kg_rewrite_prog* 
 
 void kg_snapshot_destroy(kg_snapshot* s) { delete reinterpret_cast<Snapshot*>(s); }
 
+uint32_t kg_shard_owner(uint32_t ns, uint32_t obj, uint32_t nranks) { return kg::shard_owner(ns, obj, nranks); }
+
+int kg_snapshot_create_shard(const kg_tuple* rows, size_t n, const kg_dict* dict, const kg_rewrite_prog* prog,
+                             int device, uint32_t rank, uint32_t nranks, kg_snapshot** out) {
+  KG_GUARD_BEGIN
+  if (!out) return set_error(-2, "out is NULL");
+  *out = nullptr;
+  if (n && !rows) return set_error(-2, "rows is NULL");
+  if (nranks < 1 || nranks > KG_SHARD_MAX_RANKS || rank >= nranks) return set_error(-2, "bad shard %u/%u", rank, nranks);
+  Snapshot* s = new Snapshot();
+  s->shard_rank = rank;
+  s->shard_n = nranks;
+  int rc = s->init_device(device);
+  if (!rc) rc = s->create_from_tuples(rows, n, dict, prog);
+  if (rc) {
+    delete s;
+    return rc;
+  }
+  *out = reinterpret_cast<kg_snapshot*>(s);
+  kg::clear_error();
+  return 0;
+  KG_GUARD_END
+}
+
+int kg_snapshot_synthetic_shard(const kg_synth_params* params, const kg_rewrite_prog* prog, int device, uint32_t rank,
+                                uint32_t nranks, kg_snapshot** out) {
+  KG_GUARD_BEGIN
+  if (!out || !params) return set_error(-2, "NULL argument");
+  *out = nullptr;
+  if (nranks < 1 || nranks > KG_SHARD_MAX_RANKS || rank >= nranks) return set_error(-2, "bad shard %u/%u", rank, nranks);
+  Snapshot* s = new Snapshot();
+  s->shard_rank = rank;
+  s->shard_n = nranks;
+  int rc = s->init_device(device);
+  if (!rc) rc = s->create_synthetic(params, prog);
+  if (rc) {
+    delete s;
+    return rc;
+  }
+  *out = reinterpret_cast<kg_snapshot*>(s);
+  return 0;
+  KG_GUARD_END
+}
+
+int kg_shard_seed(kg_snapshot* sp, const kg_query* d_q, size_t n, int32_t global_max_depth, kg_frec* d_out, size_t cap,
+                  uint32_t* d_counts, uint8_t* d_res, uint32_t* d_err, void* stream) {
+  KG_GUARD_BEGIN
+  if (!sp || !d_counts || !d_res || (n && (!d_q || !d_out))) return set_error(-2, "NULL argument");
+  Snapshot* s = reinterpret_cast<Snapshot*>(sp);
+  std::lock_guard<std::mutex> lk(s->mu);
+  return kg::shard_seed(s, d_q, n, global_max_depth, d_out, cap, d_counts, d_res, d_err, (hipStream_t)stream);
+  KG_GUARD_END
+}
+
+int kg_shard_level(kg_snapshot* sp, const kg_frec* d_in, size_t n_in, kg_frec* d_out, size_t cap, uint32_t* d_counts,
+                   uint8_t* d_res, void* stream) {
+  KG_GUARD_BEGIN
+  if (!sp || !d_counts || !d_res || (n_in && (!d_in || !d_out))) return set_error(-2, "NULL argument");
+  Snapshot* s = reinterpret_cast<Snapshot*>(sp);
+  std::lock_guard<std::mutex> lk(s->mu);
+  if (!s->shard_vis) return set_error(-2, "kg_shard_level before kg_shard_seed");
+  return kg::shard_level(s, d_in, n_in, d_out, cap, d_counts, d_res, (hipStream_t)stream);
+  KG_GUARD_END
+}
+
 int kg_snapshot_info(const kg_snapshot* sp, uint64_t* info4) {
   if (!sp || !info4) return set_error(-2, "NULL argument");
   const Snapshot* s = reinterpret_cast<const Snapshot*>(sp);
@@ -183,6 +248,7 @@ int kg_check_batch_device(kg_snapshot* sp, const kg_query* d_q, size_t n, int32_
   if (!sp) return set_error(-2, "NULL snapshot");
   Snapshot* s = reinterpret_cast<Snapshot*>(sp);
   std::lock_guard<std::mutex> lk(s->mu);
+  if (s->shard_n > 1) return set_error(-2, "sharded snapshot: checks run through kg_shard_seed / kg_shard_level");
   return kg::check_batch_device(s, d_q, n, global_max_depth, d_out, d_err, stats, (hipStream_t)stream);
   KG_GUARD_END
 }
@@ -194,6 +260,7 @@ int kg_check_batch(kg_snapshot* sp, const kg_query* q, size_t n, int32_t global_
   if (n && (!q || !out)) return set_error(-2, "NULL buffer");
   Snapshot* s = reinterpret_cast<Snapshot*>(sp);
   std::lock_guard<std::mutex> lk(s->mu);
+  if (s->shard_n > 1) return set_error(-2, "sharded snapshot: checks run through kg_shard_seed / kg_shard_level");
   HIPC(hipSetDevice(s->device));
   if (n == 0) {
     if (stats) memset(stats, 0, sizeof *stats);

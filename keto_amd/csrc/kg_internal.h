@@ -50,6 +50,12 @@ __host__ __device__ __forceinline__ uint64_t dset_key(uint32_t node, uint32_t su
   return ((uint64_t)node << 32) | subj;
 }
 
+// Shard of a node in the hash-sharded mode: all relations of one object live on
+// one rank, owner = hash(ns, obj) mod nranks.
+__host__ __device__ __forceinline__ uint32_t shard_owner(uint32_t ns, uint32_t obj, uint32_t nranks) {
+  return nranks <= 1 ? 0u : (uint32_t)((mix64(((uint64_t)ns << 32) | obj) >> 20) % nranks);
+}
+
 // Rewrite-program node (kg_rw_node layout).
 struct RwNode {
   int32_t kind, rel, crel, first, count;
@@ -118,6 +124,9 @@ struct DevSnap {
   const uint32_t* hold;      // holder nodes (rows containing a subject), grouped by subject
   const HSlot* hslots;       // subject hash: tagged subject -> (first index into hold, count)
   uint64_t hmask;            // n_slots - 1
+  // hash-sharded mode: this snapshot holds the rows of the nodes with shard_owner == shard_rank
+  uint32_t shard_rank, shard_n;
+  const uint8_t* nowner;  // [n_nodes] owner rank of every node (shard_n > 1)
 };
 
 // astRelationFor (internal/check/engine.go:209-229) as flags: bit0 = has rewrite, bit1 = the

@@ -1,0 +1,210 @@
+// kg_shard.hip -- the hash-sharded check mode: graphs larger than one GPU.
+//
+// Rank r holds the rows of the nodes with shard_owner(ns, obj) == r.  A batch is a level-
+// synchronous BFS across ranks over frontier records kg_frec (query, node, subject, rest depth):
+//   kg_shard_seed   maps the home rank's queries (node map, depth clamp engine.go:68-70) and
+//                   sends one record per query to the owner of its root
+//   kg_shard_level  per received record: a hit report sets the home query's result; otherwise
+//                   the owner deduplicates (query, node) in its visited table (first arrival =
+//                   shallowest level, as in the single-GPU tiers), probes checkDirect
+//                   (engine.go:148-177) on its local dset, reports a hit to the query's home, or
+//                   expands the node's local set row (checkExpandSubject engine.go:87-145) into
+//                   records (query, child, subject, depth - 1) for the children's owners
+// Between levels the driver (keto_amd/sharded.py) exchanges the per-destination buckets with an
+// all-to-all (RCCL over xGMI) and stops when no rank sends anything.  Semantics: bounded
+// reachability over rewrite-free nodes, exactly the single-GPU engine's.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "kg_bfs.h"
+#include "kg_internal.h"
+#include "kg_snapshot.h"
+
+namespace kg {
+
+constexpr uint32_t Q_BITS = 26, Q_MASK = (1u << Q_BITS) - 1;
+constexpr int SV_PROBES = 64;
+
+// (query, node) visited table: open addressing, cleared per batch.  1 fresh, 0 seen, -1 full.
+__device__ __forceinline__ int sv_insert(uint64_t* T, uint64_t mask, uint64_t key) {
+  uint64_t h = mix64(key) & mask;
+  for (int p = 0; p < SV_PROBES; p++) {
+    const uint64_t old = atomicCAS((unsigned long long*)&T[h], (unsigned long long)EMPTY64, (unsigned long long)key);
+    if (old == EMPTY64) return 1;
+    if (old == key) return 0;
+    h = (h + 1) & mask;
+  }
+  return -1;
+}
+
+// Wave-aggregated append of one record per active lane to the bucket of its destination rank:
+// one atomic per (wave, destination) instead of one per record.
+__device__ __forceinline__ void emit(bool act, uint32_t dest, const kg_frec& r, kg_frec* out, uint64_t cap,
+                                     uint32_t* counts, uint32_t nranks) {
+  uint64_t pending = __ballot(act);
+  const int lane = lane_id();
+  while (pending) {
+    const int lead = __ffsll((unsigned long long)pending) - 1;
+    const uint32_t d = __shfl(dest, lead, 64);
+    const uint64_t m = __ballot(act && dest == d);
+    uint32_t base = 0;
+    if (lane == lead) base = atomicAdd(&counts[d], (uint32_t)__popcll(m));
+    base = __shfl(base, lead, 64);
+    if (act && dest == d) {
+      const uint32_t at = base + __popcll(m & ((1ull << lane) - 1));
+      if (at < cap) out[(uint64_t)d * cap + at] = r;
+      else atomicOr(&counts[nranks], 1u);
+    }
+    pending &= ~m;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_shard_seed(DevSnap s, const kg_query* __restrict__ q, uint32_t n,
+                                                    int32_t global, kg_frec* out, uint64_t cap, uint32_t* counts,
+                                                    uint8_t* res, uint32_t* err) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  bool act = false;
+  uint32_t dest = 0;
+  kg_frec r{};
+  if (i < n) {
+    const kg_query x = q[i];
+    const uint32_t node = nmap_find(s, x.t.ns, x.t.rel, x.t.obj);
+    uint32_t subj;
+    if (x.t.sns == KG_SUBJECT_ID) {
+      subj = x.t.sobj < 0x7FFFFFFFu ? x.t.sobj : NONE;
+    } else {
+      const uint32_t sn = nmap_find(s, x.t.sns, x.t.srel, x.t.sobj);
+      subj = sn == NONE ? NONE : (SET_BIT | sn);
+    }
+    int32_t d = x.max_depth;
+    if (d <= 0 || global < d) d = global;  // engine.go:68-70
+    res[i] = KG_NOT_MEMBER;
+    if (err) err[i] = KG_ERR_NONE;
+    if (relflag(s, x.t.ns, x.t.rel)) {  // rewrites are not part of the sharded mode
+      res[i] = KG_ERROR;
+      if (err) err[i] = KG_ERR_NOT_IMPLEMENTED;
+    } else if (node != NONE && subj != NONE) {
+      act = true;
+      dest = s.nowner ? s.nowner[node] : 0u;
+      r = kg_frec{(s.shard_rank << Q_BITS) | i, node, subj, d};
+    }
+  }
+  emit(act, dest, r, out, cap, counts, s.shard_n);
+}
+
+// One workgroup handles 256 received records per iteration; their set rows are expanded
+// edge-parallel (block scan of the row lengths, LDS owner search).
+__global__ __launch_bounds__(256) void k_shard_level(DevSnap s, const kg_frec* __restrict__ in, uint64_t n_in,
+                                                     kg_frec* out, uint64_t cap, uint32_t* counts, uint8_t* res,
+                                                     uint64_t* vis, uint64_t vmask) {
+  __shared__ uint32_t s_pref[256], s_wsum[4];
+  __shared__ uint64_t s_rb[256];
+  __shared__ kg_frec s_rec[256];
+  const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+  const uint32_t me = s.shard_rank;
+  for (uint64_t base = (uint64_t)blockIdx.x * 256; base < n_in; base += (uint64_t)gridDim.x * 256) {
+    const uint64_t i = base + tid;
+    kg_frec r{0, NONE, 0, 0};
+    bool hit_out = false;
+    uint64_t rb = 0, len = 0;
+    if (i < n_in) {
+      r = in[i];
+      if (r.node == KG_FREC_HIT) {
+        if ((r.q >> Q_BITS) == me) res[r.q & Q_MASK] = KG_IS_MEMBER;
+      } else {
+        const int ins = sv_insert(vis, vmask, ((uint64_t)r.q << 32) | r.node);
+        if (ins < 0) atomicOr(&counts[s.shard_n], 2u);
+        if (ins > 0) {
+          if (r.depth >= 1 && dset_probe(s, r.node, r.subj)) {  // checkDirect(depth - 1)
+            if ((r.q >> Q_BITS) == me) res[r.q & Q_MASK] = KG_IS_MEMBER;
+            else hit_out = true;
+          } else if (r.depth >= 2) {  // children at depth - 1 >= 1 can still be probed
+            rb = s.adj_off[r.node];
+            len = s.adj_off[r.node + 1] - rb;
+          }
+        }
+      }
+    }
+    // hit reports go to the query's home
+    kg_frec hr{r.q, KG_FREC_HIT, 0, 0};
+    emit(hit_out, r.q >> Q_BITS, hr, out, cap, counts, s.shard_n);
+    // expansion
+    s_rb[tid] = rb;
+    s_rec[tid] = r;
+    uint32_t total;
+    uint32_t v = (uint32_t)len, x = v;
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t y = __shfl_up(v, off, 64);
+      if (lane >= off) v += y;
+    }
+    if (lane == 63) s_wsum[wave] = v;
+    __syncthreads();
+    uint32_t before = 0;
+    total = 0;
+    for (int w = 0; w < 4; w++) {
+      if (w < wave) before += s_wsum[w];
+      total += s_wsum[w];
+    }
+    s_pref[tid] = before + v - x;
+    __syncthreads();
+    for (uint32_t eb = 0; eb < total; eb += 256) {
+      const uint32_t e = eb + tid;
+      const bool act = e < total;
+      kg_frec c{};
+      uint32_t dest = 0;
+      if (act) {
+        const int own = owner_search(s_pref, 256, e);
+        const kg_frec& pr = s_rec[own];
+        const uint32_t child = s.adj[s_rb[own] + (e - s_pref[own])];
+        c = kg_frec{pr.q, child, pr.subj, pr.depth - 1};
+        dest = s.nowner ? s.nowner[child] : 0u;
+      }
+      emit(act, dest, c, out, cap, counts, s.shard_n);
+    }
+    __syncthreads();
+  }
+}
+
+static int shard_vis_prepare(Snapshot* s, hipStream_t stream) {
+  // per-batch (query, node) table: 2^25 slots (256 MiB); an overflow is reported in the flags
+  const uint64_t slots = 1ull << 25;
+  if (!s->shard_vis) {
+    HIPC(hipMalloc(&s->shard_vis, slots * 8));
+    s->shard_vis_slots = slots;
+  }
+  HIPC(hipMemsetAsync(s->shard_vis, 0xFF, s->shard_vis_slots * 8, stream));
+  return 0;
+}
+
+int shard_seed(Snapshot* s, const kg_query* d_q, size_t n, int32_t gdepth, kg_frec* d_out, size_t cap,
+               uint32_t* d_counts, uint8_t* d_res, uint32_t* d_err, hipStream_t stream) {
+  if (gdepth < 1) gdepth = 5;  // config.schema.json:308-315 default
+  if (n > Q_MASK) return set_error(-2, "sharded batch too large (%zu > %u)", n, Q_MASK);
+  HIPC(hipSetDevice(s->device));
+  if (!stream) stream = s->stream;
+  if (int rc = shard_vis_prepare(s, stream)) return rc;
+  HIPC(hipMemsetAsync(d_counts, 0, (s->shard_n + 1) * 4, stream));
+  if (n) {
+    hipLaunchKernelGGL(k_shard_seed, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, stream, s->ds, d_q, (uint32_t)n,
+                       gdepth, d_out, (uint64_t)cap, d_counts, d_res, d_err);
+    HIPC(hipGetLastError());
+  }
+  return 0;
+}
+
+int shard_level(Snapshot* s, const kg_frec* d_in, size_t n_in, kg_frec* d_out, size_t cap, uint32_t* d_counts,
+                uint8_t* d_res, hipStream_t stream) {
+  HIPC(hipSetDevice(s->device));
+  if (!stream) stream = s->stream;
+  HIPC(hipMemsetAsync(d_counts, 0, (s->shard_n + 1) * 4, stream));
+  if (n_in) {
+    const uint32_t grid = (uint32_t)std::min<uint64_t>((n_in + 255) / 256, (uint64_t)s->n_cu * 8);
+    hipLaunchKernelGGL(k_shard_level, dim3(grid), dim3(256), 0, stream, s->ds, d_in, (uint64_t)n_in, d_out,
+                       (uint64_t)cap, d_counts, d_res, (uint64_t*)s->shard_vis, s->shard_vis_slots - 1);
+    HIPC(hipGetLastError());
+  }
+  return 0;
+}
+
+}  // namespace kg

@@ -60,6 +60,9 @@ struct Snapshot {
   void* interp_pool = nullptr;
   size_t interp_pool_bytes = 0;
   uint64_t batch_seq = 0;
+  uint32_t shard_rank = 0, shard_n = 1;  // hash-sharded mode (set before create)
+  void* shard_vis = nullptr;             // kg_shard.hip: per-batch visited table of (query, node)
+  uint64_t shard_vis_slots = 0;
   int stream_variant = 1;  // kg_snapshot_tune("stream"): k_stream slots/LDS variant (0, 1, 2)
   int back_tier = 1;  // kg_snapshot_tune("back"): backward tier + no-holder filter in k_resolve
 
@@ -79,6 +82,11 @@ struct Snapshot {
 int check_batch_device(Snapshot* s, const kg_query* d_q, size_t n, int32_t global_max_depth, uint8_t* d_out,
                        uint32_t* d_err, kg_stats* stats, hipStream_t stream);
 int synth_queries(Snapshot* s, uint64_t seed, size_t n, kg_query* d_q);
+// kg_shard.hip
+int shard_seed(Snapshot* s, const kg_query* d_q, size_t n, int32_t gdepth, kg_frec* d_out, size_t cap,
+               uint32_t* d_counts, uint8_t* d_res, uint32_t* d_err, hipStream_t stream);
+int shard_level(Snapshot* s, const kg_frec* d_in, size_t n_in, kg_frec* d_out, size_t cap, uint32_t* d_counts,
+                uint8_t* d_res, hipStream_t stream);
 // kg_expand.hip
 int expand_batch(Snapshot* s, const kg_set* roots, size_t n, int32_t global, kg_tree_buf* out);
 

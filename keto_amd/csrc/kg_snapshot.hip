@@ -64,6 +64,12 @@ __global__ void k_nmap_insert(NSlot* nm, uint64_t mask, const uint32_t* nd_ns, c
   }
 }
 
+__global__ void k_node_owner(const uint32_t* nd_ns, const uint32_t* nd_obj, uint32_t n_nodes, uint32_t nranks,
+                             uint8_t* owner) {
+  const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+  if (v < n_nodes) owner[v] = (uint8_t)shard_owner(nd_ns[v], nd_obj[v], nranks);
+}
+
 // Bloom signature of every node's full row (direct subjects, tagged like dset keys).
 __global__ void k_node_sig(const uint64_t* row_off, const uint32_t* row_subj, uint32_t n_nodes, uint32_t* sig) {
   const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
@@ -144,10 +150,14 @@ __device__ __forceinline__ bool synth_is_adj(const SynthLayout& L, uint32_t sub)
   return rel != 0;  // rel 0 == "..."
 }
 
-__global__ void k_synth_degrees(SynthLayout L, uint32_t n_nodes, uint64_t* deg, uint64_t* setdeg) {
+__global__ void k_synth_degrees(SynthLayout L, uint32_t n_nodes, uint32_t rank, uint32_t nranks, uint64_t* deg,
+                                uint64_t* setdeg) {
   uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
   if (v >= n_nodes) return;
-  uint32_t d = synth_degree(L, v);
+  uint32_t ns, obj, rel;
+  synth_node(L, v, ns, obj, rel);
+  // hash-sharded mode: rows of nodes owned by other ranks are empty here
+  uint32_t d = shard_owner(ns, obj, nranks) == rank ? synth_degree(L, v) : 0u;
   uint32_t s = 0;
   for (uint32_t e = 0; e < d; e++) s += synth_is_adj(L, synth_subject(L, v, e)) ? 1u : 0u;
   deg[v] = d;
@@ -204,6 +214,7 @@ Snapshot::~Snapshot() {
   for (auto& e : ev)
     if (e) hipEventDestroy(e);
   if (interp_pool) hipFree(interp_pool);
+  if (shard_vis) hipFree(shard_vis);
   if (stream) hipStreamDestroy(stream);
 }
 
@@ -274,6 +285,16 @@ int Snapshot::build_hash_tables() {
   ds.dset_mask = buckets - 1;
   ds.nmap = nm;
   ds.nmap_mask = slots - 1;
+  ds.shard_rank = shard_rank;
+  ds.shard_n = shard_n;
+  ds.nowner = nullptr;
+  if (shard_n > 1 && ds.n_nodes) {
+    uint8_t* no = nullptr;
+    if (alloc((void**)&no, ds.n_nodes)) return -1;
+    hipLaunchKernelGGL(k_node_owner, dim3(grid), dim3(256), 0, stream, ds.nd_ns, ds.nd_obj, ds.n_nodes, shard_n, no);
+    HIPC(hipGetLastError());
+    ds.nowner = no;
+  }
   HIPC(hipStreamSynchronize(stream));
   return build_reverse();
 }
@@ -482,10 +503,15 @@ int Snapshot::create_from_tuples(const kg_tuple* rows, size_t n, const kg_dict* 
   }
   uint32_t nn = (uint32_t)h_nd_ns.size();
   ds.n_nodes = nn;
-  // 2. rows per node in tuple (shard) order: counting sort
+  // 2. rows per node in tuple (shard) order: counting sort; in the hash-sharded mode only the rows
+  // of nodes this rank owns are kept (node ids stay global)
+  if (shard_n > 1)
+    for (size_t i = 0; i < n; i++)
+      if (shard_owner(h_nd_ns[lhs[i]], h_nd_obj[lhs[i]], shard_n) != shard_rank) lhs[i] = NONE;
   h_row_off.assign((size_t)nn + 1, 0);
   h_adj_off.assign((size_t)nn + 1, 0);
   for (size_t i = 0; i < n; i++) {
+    if (lhs[i] == NONE) continue;
     h_row_off[lhs[i] + 1]++;
     uint32_t s = sub[i];
     if ((s & SET_BIT) && h_nd_rel[s & ~SET_BIT] != wildcard_rel) h_adj_off[lhs[i] + 1]++;
@@ -494,11 +520,12 @@ int Snapshot::create_from_tuples(const kg_tuple* rows, size_t n, const kg_dict* 
     h_row_off[v + 1] += h_row_off[v];
     h_adj_off[v + 1] += h_adj_off[v];
   }
-  h_row_subj.assign(n, 0);
+  h_row_subj.assign(h_row_off[nn], 0);
   std::vector<uint32_t> adj(h_adj_off[nn]);
   {
     std::vector<uint64_t> fr(h_row_off.begin(), h_row_off.end() - 1), fa(h_adj_off.begin(), h_adj_off.end() - 1);
     for (size_t i = 0; i < n; i++) {
+      if (lhs[i] == NONE) continue;
       uint32_t s = sub[i], v = lhs[i];
       h_row_subj[fr[v]++] = s;
       if ((s & SET_BIT) && h_nd_rel[s & ~SET_BIT] != wildcard_rel) adj[fa[v]++] = s & ~SET_BIT;
@@ -546,12 +573,13 @@ int Snapshot::create_from_tuples(const kg_tuple* rows, size_t n, const kg_dict* 
   uint64_t *d_ro, *d_ao;
   uint32_t *d_rs, *d_adj, *d_ns, *d_obj, *d_rel;
   if (alloc((void**)&d_ro, ((size_t)nn + 1) * 8) || alloc((void**)&d_ao, ((size_t)nn + 1) * 8) ||
-      alloc((void**)&d_rs, n * 4) || alloc((void**)&d_adj, adj.size() * 4) || alloc((void**)&d_ns, (size_t)nn * 4) ||
+      alloc((void**)&d_rs, h_row_subj.size() * 4) || alloc((void**)&d_adj, adj.size() * 4) || alloc((void**)&d_ns, (size_t)nn * 4) ||
       alloc((void**)&d_obj, (size_t)nn * 4) || alloc((void**)&d_rel, (size_t)nn * 4))
     return -1;
   HIPC(hipMemcpy(d_ro, h_row_off.data(), ((size_t)nn + 1) * 8, hipMemcpyHostToDevice));
   HIPC(hipMemcpy(d_ao, h_adj_off.data(), ((size_t)nn + 1) * 8, hipMemcpyHostToDevice));
-  if (n) HIPC(hipMemcpy(d_rs, h_row_subj.data(), n * 4, hipMemcpyHostToDevice));
+  if (!h_row_subj.empty())
+    HIPC(hipMemcpy(d_rs, h_row_subj.data(), h_row_subj.size() * 4, hipMemcpyHostToDevice));
   if (!adj.empty()) HIPC(hipMemcpy(d_adj, adj.data(), adj.size() * 4, hipMemcpyHostToDevice));
   if (nn) {
     HIPC(hipMemcpy(d_ns, h_nd_ns.data(), (size_t)nn * 4, hipMemcpyHostToDevice));
@@ -593,7 +621,7 @@ int Snapshot::create_synthetic(const kg_synth_params* p, const kg_rewrite_prog* 
   HIPC(hipMalloc(&deg, ((size_t)nn + 1) * 8));
   HIPC(hipMalloc(&setdeg, ((size_t)nn + 1) * 8));
   const uint32_t grid = (nn + 255) / 256;
-  hipLaunchKernelGGL(k_synth_degrees, dim3(grid), dim3(256), 0, stream, L, nn, deg, setdeg);
+  hipLaunchKernelGGL(k_synth_degrees, dim3(grid), dim3(256), 0, stream, L, nn, shard_rank, shard_n, deg, setdeg);
   HIPC(hipGetLastError());
   HIPC(hipMemsetAsync(deg + nn, 0, 8, stream));
   HIPC(hipMemsetAsync(setdeg + nn, 0, 8, stream));

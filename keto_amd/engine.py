@@ -61,11 +61,14 @@ class Snapshot:
     """An HBM-resident, immutable snapshot of the relation tuples (rows in shard order)."""
 
     def __init__(self, tuples: np.ndarray, interner: Interner, program: Optional[Program] = None, device: int = 0,
-                 _handle=None):
+                 _handle=None, shard: Optional[Tuple[int, int]] = None):
+        """shard = (rank, nranks): keep only the rows of the nodes this rank owns (hash-sharded mode,
+        keto_amd.sharded); every rank passes the same full tuple list."""
         L = _lib.load()
         self.interner = interner
         self.device = device
         self.program = program
+        self.shard = shard
         self._keep = []
         self._h = C.c_void_p()
         if _handle is not None:
@@ -74,8 +77,12 @@ class Snapshot:
         t = np.ascontiguousarray(tuples, dtype=np.uint32).reshape(-1, 6)
         d = _lib.kg_dict(interner.n_namespaces, interner.n_relations, interner.wildcard_rel)
         prog_c = self._prog(program)
-        rc = L.kg_snapshot_create(_ptr(t), t.shape[0], C.byref(d), C.byref(prog_c) if prog_c is not None else None,
-                                  device, C.byref(self._h))
+        pc = C.byref(prog_c) if prog_c is not None else None
+        if shard is None:
+            rc = L.kg_snapshot_create(_ptr(t), t.shape[0], C.byref(d), pc, device, C.byref(self._h))
+        else:
+            rc = L.kg_snapshot_create_shard(_ptr(t), t.shape[0], C.byref(d), pc, device, shard[0], shard[1],
+                                            C.byref(self._h))
         _lib.check(rc, "kg_snapshot_create")
 
     def _prog(self, program: Optional[Program]):
@@ -92,8 +99,9 @@ class Snapshot:
     @classmethod
     def synthetic(cls, n_tuples: int, seed: int = 20250131, device: int = 0, n_layers: int = 8,
                   max_degree: int = 100000, set_fraction: float = 0.25, doc_set_fraction: float = 0.5,
-                  preset: int = 0) -> "Snapshot":
-        """Device-generated Drive-like graph (keto_amd/csrc/kg_synth.h); preset 0 = C2/C4, 1 = C3."""
+                  preset: int = 0, shard: Optional[Tuple[int, int]] = None) -> "Snapshot":
+        """Device-generated Drive-like graph (keto_amd/csrc/kg_synth.h); preset 0 = C2/C4, 1 = C3.
+        shard = (rank, nranks): only this rank's rows (hash-sharded mode)."""
         from . import synth
         L = _lib.load()
         it = synth.interner()
@@ -102,9 +110,14 @@ class Snapshot:
         p = _lib.kg_synth_params(n_tuples, seed, n_layers, max_degree, set_fraction, doc_set_fraction, preset)
         prog_c = snap._prog(prog)
         h = C.c_void_p()
-        _lib.check(L.kg_snapshot_synthetic(C.byref(p), C.byref(prog_c) if prog_c is not None else None, device,
-                                           C.byref(h)), "kg_snapshot_synthetic")
+        pc = C.byref(prog_c) if prog_c is not None else None
+        if shard is None:
+            _lib.check(L.kg_snapshot_synthetic(C.byref(p), pc, device, C.byref(h)), "kg_snapshot_synthetic")
+        else:
+            _lib.check(L.kg_snapshot_synthetic_shard(C.byref(p), pc, device, shard[0], shard[1], C.byref(h)),
+                       "kg_snapshot_synthetic_shard")
         snap._h = h
+        snap.shard = shard
         snap.program = prog
         return snap
 

@@ -1,0 +1,111 @@
+"""Test-only CPU restatement of one rank's local steps of the hash-sharded mode (the contract of
+kg_shard_seed / kg_shard_level in include/ketogpu.h, keto_amd/csrc/kg_shard.hip), used to run
+keto_amd.sharded.ShardedChecker's exchange protocol on CPU ranks under gloo.  Never shipped: the
+product path is keto_amd.sharded.HipShardOps (GPU).  Rewrite-free graphs only.
+
+The checkIsAllowed recursion it restates (internal/check/engine.go:87-207):
+a record (q, v, d) = checkIsAllowed(v, d) -> checkDirect(d-1) on v's row, and children of v's
+subject-set row (no SubjectIDs, no "..." sets, engine.go:118-136) at d-1 when d >= 2.
+"""
+import numpy as np
+import torch
+
+SUBJECT_ID = 0xFFFFFFFF
+SET_BIT = 0x80000000
+Q_BITS = 26
+HIT = -1  # kg_frec.node == KG_FREC_HIT as int32
+M64 = (1 << 64) - 1
+
+
+def mix64(x: int) -> int:  # kg_internal.h mix64
+    x &= M64
+    x ^= x >> 30
+    x = (x * 0xbf58476d1ce4e5b9) & M64
+    x ^= x >> 27
+    x = (x * 0x94d049bb133111eb) & M64
+    x ^= x >> 31
+    return x
+
+
+def shard_owner(ns: int, obj: int, n: int) -> int:  # kg_internal.h shard_owner
+    return 0 if n <= 1 else (mix64((ns << 32) | obj) >> 20) % n
+
+
+class CpuShardOps:
+    def __init__(self, tuples6: np.ndarray, wildcard_rel: int, rank: int, nranks: int):
+        self.rank, self.n = rank, nranks
+        t = np.asarray(tuples6, np.int64).reshape(-1, 6)
+        self.node = {}
+
+        def nid(ns, obj, rel):
+            k = (int(ns), int(obj), int(rel))
+            if k not in self.node:
+                self.node[k] = len(self.node)
+            return self.node[k]
+
+        self.adj, self.direct, self.owner = {}, set(), {}
+        for ns, obj, rel, sns, sobj, srel in t:
+            v = nid(ns, obj, rel)
+            self.owner[v] = shard_owner(int(ns), int(obj), nranks)
+            if sns == SUBJECT_ID:
+                subj = int(sobj)
+            else:
+                c = nid(sns, sobj, srel)
+                self.owner[c] = shard_owner(int(sns), int(sobj), nranks)
+                subj = SET_BIT | c
+                if srel != wildcard_rel and self.owner[v] == rank:
+                    self.adj.setdefault(v, []).append(c)
+            if self.owner[v] == rank:
+                self.direct.add((v, subj))
+        self.vis = set()
+
+    def _emit(self, out, cap, counts, dest, rec):
+        at = int(counts[dest])
+        counts[dest] += 1
+        if at < cap:
+            out[dest * cap + at] = torch.tensor(rec, dtype=torch.int32)
+        else:
+            counts[self.n] |= 1
+
+    def seed(self, dq, n, gdepth, out, cap, counts, res, err):
+        self.vis = set()
+        counts.zero_()
+        res.zero_()
+        err.zero_()
+        qs = dq.numpy().reshape(-1, 7)
+        qu = qs.view(np.uint32).astype(np.int64)
+        for i in range(n):
+            ns, obj, rel, sns, sobj, srel = (int(x) for x in qu[i, :6])
+            md = int(qs[i, 6])
+            v = self.node.get((ns, obj, rel))
+            if sns == SUBJECT_ID:
+                subj = int(sobj)
+            else:
+                c = self.node.get((sns, sobj, srel))
+                subj = None if c is None else SET_BIT | c
+            d = md if 0 < md <= gdepth else gdepth  # engine.go:68-70
+            if v is None or subj is None:
+                continue
+            self._emit(out, cap, counts, self.owner[v],
+                       [(self.rank << Q_BITS) | i, v, np.uint32(subj).view(np.int32), d])
+
+    def level(self, din, n_in, out, cap, counts, res):
+        counts.zero_()
+        for r in din[:n_in].tolist():
+            q, v, subj, d = r[0], r[1], r[2] & 0xFFFFFFFF, r[3]
+            home, qi = q >> Q_BITS, q & ((1 << Q_BITS) - 1)
+            if v == HIT:
+                if home == self.rank:
+                    res[qi] = 1
+                continue
+            if (q, v) in self.vis:
+                continue
+            self.vis.add((q, v))
+            if d >= 1 and (v, subj) in self.direct:
+                if home == self.rank:
+                    res[qi] = 1
+                else:
+                    self._emit(out, cap, counts, home, [q, HIT, 0, 0])
+            elif d >= 2:
+                for c in self.adj.get(v, []):
+                    self._emit(out, cap, counts, self.owner[c], [q, c, np.uint32(subj).view(np.int32), d - 1])

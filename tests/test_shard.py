@@ -1,0 +1,159 @@
+"""Hash-sharded mode: keto_amd.sharded's level/exchange protocol.
+
+CPU (gloo, world_size 2 and 3): ShardedChecker over the test-only restatement of the local steps
+(tests/shard_ref.py) against the C oracle on the full graph -- exercises the all-gather of bucket
+sizes, the all-to-all of records, hit reports to the home rank, termination and the bucket-overflow
+rerun.  GPU: the HIP local steps (kg_shard_seed / kg_shard_level) at world_size 1 and 2 (two
+processes on one GPU, gloo exchange) against the same oracle, bit-exact."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _graph(seed, n_obj=50, n_rows=500):
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from test_gpu_check import random_graph, random_queries  # noqa: E402  (pure-python helpers)
+    from keto_amd.engine import queries_array
+    rng = np.random.default_rng(seed)
+    it, tuples, nss, rels = random_graph(rng, n_obj=n_obj, n_rows=n_rows)
+    qs = random_queries(rng, nss, rels, 400, n_obj=n_obj)
+    q6 = np.asarray([it.tuple_ids(t) for t in qs], np.uint32)
+    depths = rng.integers(-1, 8, len(qs))
+    return it, it.tuples_array(tuples), queries_array(q6, depths)
+
+
+def _expected(t6, wildcard, q, gmax):
+    from oracle.oracle import POLICY_CANONICAL, Oracle
+    o = Oracle(t6, wildcard)
+    exp, err, _ = o.check_batch(q[:, :6], q[:, 6].view(np.int32), gmax, POLICY_CANONICAL)
+    assert (err == 0).all()
+    return exp
+
+
+def _cpu_worker(rank, world, port, seed, cap, outq):
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import torch.distributed as dist
+    from keto_amd.sharded import ShardedChecker
+    from shard_ref import CpuShardOps
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    it, t6, q = _graph(seed)
+    ops = CpuShardOps(t6, it.wildcard_rel, rank, world)
+    mine = np.array_split(np.arange(len(q)), world)[rank]  # this rank's slice of the batch
+    chk = ShardedChecker(ops, rank, world, dist, device="cpu", cap=cap)
+    out = {}
+    for gmax in (2, 5):
+        res, err = chk.check(torch.from_numpy(q[mine].view(np.int32).copy()), gmax)
+        out[gmax] = (mine, res.numpy().copy(), chk.cap)
+    outq.put((rank, out))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,cap", [(2, 1 << 12), (3, 4)])
+def test_sharded_protocol_gloo(world, cap):
+    """cap=4 forces bucket overflows: every rank must rerun the batch with larger buckets."""
+    seed = 3
+    ctx = mp.get_context("spawn")
+    outq = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_cpu_worker, args=(r, world, port, seed, cap, outq)) for r in range(world)]
+    for p in ps:
+        p.start()
+    got = [outq.get(timeout=240) for _ in range(world)]
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    sys.path.insert(0, ROOT)
+    it, t6, q = _graph(seed)
+    for gmax in (2, 5):
+        exp = _expected(t6, it.wildcard_rel, q, gmax)
+        res = np.zeros(len(q), np.uint8)
+        for _, out in got:
+            mine, r, final_cap = out[gmax]
+            res[mine] = r
+            if cap == 4:
+                assert final_cap > 4
+        assert (res == exp).all(), np.nonzero(res != exp)[0][:10]
+        assert 0 < exp.mean() < 1
+
+
+def test_owner_matches_library():
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from keto_amd import _lib
+    from shard_ref import shard_owner
+    L = _lib.load()
+    for ns, obj, n in [(0, 0, 8), (1, 12345, 8), (3, 2 ** 31 - 2, 7), (2, 99, 1), (65534, 5, 64)]:
+        assert L.kg_shard_owner(ns, obj, n) == shard_owner(ns, obj, n)
+
+
+# ------------------------------------------------------------------ GPU (HIP local steps)
+def _gpu_worker(rank, world, port, seed, outq):
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+    from keto_amd.engine import Snapshot
+    from keto_amd.sharded import HipShardOps, ShardedChecker
+    dist_ = None
+    if world > 1:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)  # two ranks on one GPU: host-staged
+        dist_ = dist
+    torch.cuda.set_device(0)
+    it, t6, q = _graph(seed, n_obj=80, n_rows=1500)
+    snap = Snapshot(t6, it, None, 0, shard=(rank, world))
+    mine = np.array_split(np.arange(len(q)), world)[rank]
+    chk = ShardedChecker(HipShardOps(snap), rank, world, dist_, device="cuda", cap=256)
+    out = {}
+    for gmax in (1, 3, 6):
+        dq = torch.from_numpy(q[mine].view(np.int32).copy()).cuda()
+        res, err = chk.check(dq, gmax)
+        out[gmax] = (mine, res.cpu().numpy(), err.cpu().numpy())
+    outq.put((rank, out))
+    if dist_:
+        dist.destroy_process_group()
+
+
+def _run_gpu(world, seed):
+    ctx = mp.get_context("spawn")
+    outq = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_gpu_worker, args=(r, world, port, seed, outq)) for r in range(world)]
+    for p in ps:
+        p.start()
+    got = [outq.get(timeout=100) for _ in range(world)]
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    it, t6, q = _graph(seed, n_obj=80, n_rows=1500)
+    for gmax in (1, 3, 6):
+        exp = _expected(t6, it.wildcard_rel, q, gmax)
+        res = np.zeros(len(q), np.uint8)
+        for _, out in got:
+            mine, r, e = out[gmax]
+            assert (e == 0).all()
+            res[mine] = r
+        assert (res == exp).all(), (gmax, np.nonzero(res != exp)[0][:10])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [1, 2])
+def test_sharded_hip_vs_oracle(world):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    _run_gpu(world, seed=11)
