@@ -47,8 +47,10 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--preset", type=int, default=0,
                     help="0 = C2/C4 rewrite-free (headline); 1 = C3 (OPL view/edit/share via the rewrite interpreter)")
-    ap.add_argument("--mode", choices=["check", "expand"], default="check",
-                    help="expand = config C5: batched BuildTree of hot group#member roots")
+    ap.add_argument("--mode", choices=["check", "expand", "sharded"], default="check",
+                    help="expand = config C5: batched BuildTree of hot group#member roots; sharded = the "
+                         "hash-sharded mode (each rank holds 1/N of the graph, all-to-all frontier exchange)")
+    ap.add_argument("--backend", default="nccl", help="torch.distributed backend for --mode sharded (nccl = RCCL)")
     ap.add_argument("--roots", type=int, default=100_000, help="expand roots per step (C5)")
     return ap.parse_args()
 
@@ -101,6 +103,72 @@ def bench_expand(a):
     print(json.dumps(out), flush=True)
 
 
+def bench_sharded(a):
+    """Config C4's hash-sharded mode: rank r builds only the rows it owns of the same
+    synthetic graph and checks its own batch; every BFS level exchanges frontier records with an
+    all-to-all (RCCL over xGMI under torchrun, backend "nccl").  Weak scaling: B checks per rank."""
+    import torch
+    from keto_amd import _lib
+    from keto_amd.engine import Snapshot
+    from keto_amd.sharded import HipShardOps, ShardedChecker
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    # one rank per GPU; ranks beyond the GPU count share GPUs (a gloo rehearsal on a 1-GPU box)
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
+    dist = None
+    torch.cuda.set_device(local)
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group(a.backend, rank=rank, world_size=world)
+    L = _lib.load()
+    t_build = time.time()
+    snap = Snapshot.synthetic(int(a.tuples), seed=a.seed, device=local, shard=(rank, world))
+    info = snap.info()
+    t_build = time.time() - t_build
+    B = a.batch
+    dq = torch.empty((B, 7), dtype=torch.int32, device=f"cuda:{local}")
+    _lib.check(L.kg_synth_queries(snap.handle, 1000 + rank, B, dq.data_ptr()), "kg_synth_queries")
+    chk = ShardedChecker(HipShardOps(snap), rank, world, dist, device=f"cuda:{local}", cap=1 << 22)
+    for _ in range(a.warmup):
+        chk.check(dq, a.global_depth)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    lat, sent = [], 0
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        s0 = time.perf_counter()
+        res, err = chk.check(dq, a.global_depth)
+        torch.cuda.synchronize()
+        lat.append(time.perf_counter() - s0)
+        sent += chk.records_sent
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    r = res.cpu().numpy()
+    assert (err.cpu().numpy() == 0).all() and (r <= 1).all(), "unexpected errors in the synthetic batch"
+    elapsed, recs = aggregate(dist, elapsed, float(sent), f"cuda:{local}")
+    out = {"metric": "permission checks/sec (batched check, synthetic Drive-like graph, hash-sharded)",
+           "value": world * B * a.steps / elapsed, "unit": "checks/s", "n_gpus": world, "steps": a.steps,
+           "warmup": a.warmup, "ms_per_step": elapsed / a.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+           "vs_baseline": None, "dtype": "u32",
+           "data": "synthetic (device-generated Drive-like tuple graph, seed %d)" % a.seed,
+           "config": {"workload": "C4 generator @ %.3g tuples hash-sharded over %d rank(s), %d checks/step/rank, "
+                                  "max_read_depth %d" % (a.tuples, world, B, a.global_depth),
+                      "rows_on_rank0": info["rows"], "nodes": info["nodes"], "batch_per_gpu": B,
+                      "parallelism": f"shard{world}"},
+           "p99_batch_ms": float(np.percentile(np.array(lat) * 1e3, 99)), "allowed_fraction": float(r.mean()),
+           "levels_per_batch": chk.levels, "records_exchanged_per_batch": recs / a.steps,
+           "snapshot_build_s": t_build}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
 def aggregate(dist, elapsed: float, edges: float, device=None):
     """Whole-job numbers over ranks: elapsed = MAX over ranks (the job ends with its slowest
     rank), edges = SUM.  Replicas exchange nothing else."""
@@ -118,6 +186,8 @@ def main():
     a = parse()
     if a.mode == "expand":
         return bench_expand(a)
+    if a.mode == "sharded":
+        return bench_sharded(a)
     import torch
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))

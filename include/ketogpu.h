@@ -170,7 +170,8 @@ int kg_snapshot_info(const kg_snapshot* s, uint64_t* info4);
  * holders, one workgroup per query) takes the wave tiers' overflow before the grid tier, and
  * k_resolve answers queries whose subject no row holds (default); 0 = off.  key "stream": k_stream
  * variant -- 0 = 8 query slots x 128-entry visited hash per wave, 1 = 16 slots x 64 entries
- * (default), 2 = 16 slots x 128 entries with a 512-entry FIFO. */
+ * (default), 2 = 16 slots x 128 entries with a 512-entry FIFO.  key "shard_vis": log2 of the
+ * hash-sharded mode's per-batch (query, node) visited table (default 25). */
 int kg_snapshot_tune(kg_snapshot* s, const char* key, int64_t value);
 /* Synthetic layout: ids6 = {n_docs, n_groups, n_users, n_folders, user_obj0, folder_obj0}
  * (doc d = object d, group g = object n_docs+g, user u = object user_obj0+u). */

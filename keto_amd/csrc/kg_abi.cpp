@@ -182,6 +182,11 @@ int kg_snapshot_tune(kg_snapshot* sp, const char* key, int64_t value) {
     s->wide_tier = (int)value;
     return 0;
   }
+  if (strcmp(key, "shard_vis") == 0) {
+    if (value < 10 || value > 34) return set_error(-2, "shard_vis must be in [10, 34]");
+    s->shard_vis_log2 = (int)value;
+    return 0;
+  }
   if (strcmp(key, "stream") == 0) {
     if (value < 0 || value > 2) return set_error(-2, "stream must be 0, 1 or 2");
     s->stream_variant = (int)value;

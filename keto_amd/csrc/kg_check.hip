@@ -998,11 +998,13 @@ __global__ void k_synth_queries(SynthLayout L, DevSnap s, uint64_t seed, uint32_
       if (L.b[b].ns == L.ns_doc && L.b[b].rel == wrel) start = L.b[b].node0 + doc;
   }
   if ((i & 1) == 0) {  // positive: walk down random rows until a subject id
+    // rows come from the generator itself (row e of node v == synth_subject(v, e)), so a shard of
+    // the graph (hash-sharded mode) draws exactly the queries the whole graph does
     uint32_t cur = start;
     for (int step = 0; step < 16; step++) {
-      uint64_t b = s.row_off[cur], e = s.row_off[cur + 1];
-      if (e == b) break;
-      uint32_t sub = s.row_subj[b + shash(seed, ((uint64_t)i << 8) | step, 9) % (e - b)];
+      const uint32_t deg = synth_degree(L, cur);
+      if (deg == 0) break;
+      uint32_t sub = synth_subject(L, cur, (uint32_t)(shash(seed, ((uint64_t)i << 8) | step, 9) % deg));
       if (!(sub & SET_BIT)) {
         user = sub;
         break;

@@ -167,8 +167,13 @@ __global__ __launch_bounds__(256) void k_shard_level(DevSnap s, const kg_frec* _
 }
 
 static int shard_vis_prepare(Snapshot* s, hipStream_t stream) {
-  // per-batch (query, node) table: 2^25 slots (256 MiB); an overflow is reported in the flags
-  const uint64_t slots = 1ull << 25;
+  // per-batch (query, node) table of 2^shard_vis_log2 slots (kg_snapshot_tune "shard_vis",
+  // default 2^25 = 256 MiB); an overflow is reported in the flags and the driver grows it
+  const uint64_t slots = 1ull << s->shard_vis_log2;
+  if (s->shard_vis && s->shard_vis_slots != slots) {
+    HIPC(hipFree(s->shard_vis));
+    s->shard_vis = nullptr;
+  }
   if (!s->shard_vis) {
     HIPC(hipMalloc(&s->shard_vis, slots * 8));
     s->shard_vis_slots = slots;

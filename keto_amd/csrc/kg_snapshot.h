@@ -63,6 +63,7 @@ struct Snapshot {
   uint32_t shard_rank = 0, shard_n = 1;  // hash-sharded mode (set before create)
   void* shard_vis = nullptr;             // kg_shard.hip: per-batch visited table of (query, node)
   uint64_t shard_vis_slots = 0;
+  int shard_vis_log2 = 25;
   int stream_variant = 1;  // kg_snapshot_tune("stream"): k_stream slots/LDS variant (0, 1, 2)
   int back_tier = 1;  // kg_snapshot_tune("back"): backward tier + no-holder filter in k_resolve
 

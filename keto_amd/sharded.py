@@ -50,6 +50,10 @@ class HipShardOps:
                                         out.data_ptr(), cap, counts.data_ptr(), res.data_ptr(), err.data_ptr(),
                                         self._s()), "kg_shard_seed")
 
+    def grow_visited(self):
+        self.vis_log2 = getattr(self, "vis_log2", 25) + 1
+        self.snapshot.tune("shard_vis", self.vis_log2)
+
     def level(self, din, n_in, out, cap, counts, res):
         _lib.check(self.L.kg_shard_level(self.snapshot.handle, din.data_ptr() if n_in else None, n_in,
                                          out.data_ptr(), cap, counts.data_ptr(), res.data_ptr(), self._s()),
@@ -57,7 +61,11 @@ class HipShardOps:
 
 
 class ShardOverflow(Exception):
-    pass
+    """Some rank dropped records: 1 = a bucket, 2 = its visited table.  Every rank reruns."""
+
+    def __init__(self, flags: int):
+        super().__init__(flags)
+        self.flags = flags
 
 
 class ShardedChecker:
@@ -121,8 +129,13 @@ class ShardedChecker:
                     res, err = self._check(dq, gdepth)
                 torch.cuda.current_stream().wait_stream(ts)
                 return res, err
-            except ShardOverflow:
-                self.cap *= 2  # every rank saw the same flags: all rerun with larger buckets
+            except ShardOverflow as e:  # every rank saw the same flags: all rerun with more room
+                if e.flags & 1:
+                    self.cap *= 2
+                if e.flags & 2:
+                    if not hasattr(self.ops, "grow_visited"):
+                        raise _lib.KetoGPUError("sharded visited table overflow")
+                    self.ops.grow_visited()
 
     def _check(self, dq, gdepth: int):
         import torch
@@ -140,10 +153,8 @@ class ShardedChecker:
             counts_h = counts.cpu().numpy().view(np.uint32).astype(np.int64)
             counts_h[N] |= int((counts_h[:N] > cap).any())  # a count past cap = dropped records
             m, flags = self._gather_counts(counts_h)
-            if flags & 2:
-                raise _lib.KetoGPUError("sharded visited table overflow (batch too large for one round)")
-            if flags & 1:
-                raise ShardOverflow()
+            if flags & 3:
+                raise ShardOverflow(flags)
             if int(m.sum()) == 0:
                 return res, err
             self.records_sent += int(m[self.rank].sum())
