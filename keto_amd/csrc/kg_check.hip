@@ -43,7 +43,7 @@ struct Ctl {
   uint32_t light_count, gen_count, heavy_count, giant_count;
   uint32_t heavy_head, giant_head, gen_head, pad0;
   uint32_t medium_count, medium_head, light2_count, pad1;
-  uint32_t back_head, fwd_count, pad2[2];  // k_back dequeue head; its overflow (-> grid tier)
+  uint32_t back_head, fwd_count, back2_head, back2_count;  // k_back<64> / k_back<256> lists and heads
   uint32_t heads[8 * 32];   // per-XCD dequeue heads, one 128-B line each (k_light<16>)
   uint32_t heads2[8 * 32];  // (k_light<64>)
   uint32_t light8[8 * 32];  // per-XCD shard sizes of the light list (k_resolve appends)
@@ -859,123 +859,150 @@ __global__ __launch_bounds__(256) void k_heavy(DevSnap s, const RQuery* __restri
 // on to the forward grid tier, which redoes it from scratch (results never depend on the tier).
 // Paths from a LIGHT root only cross rewrite-free nodes (k_resolve's routing), so any backward
 // path that reaches the root is a forward path of the same length.
-constexpr uint32_t BK_VLOG2 = 13, BK_VSLOTS = 1u << BK_VLOG2, BK_CAP = 4096;  // hash load <= 0.5
-
-struct BackShared {
-  uint32_t qi, n, hit, over;
-  uint32_t pref[256];
-  uint64_t rb[256];
-  uint32_t wsum[4];
+// Two widths: k_back<64> runs one query per WAVE (visited hash 2048 / list 1024 in LDS, 12 queries
+// in flight per CU), its overflow goes to k_back<256>, one query per WORKGROUP (8192 / 4096).
+template <int W>
+struct BackCfg;
+template <>
+struct BackCfg<64> {
+  static constexpr uint32_t VLOG2 = 11, CAP = 1024;
+};
+template <>
+struct BackCfg<256> {
+  static constexpr uint32_t VLOG2 = 13, CAP = 4096;
 };
 
-__device__ __forceinline__ int bk_insert(uint32_t* vis, uint32_t key) {
-  uint32_t h = (key * 2654435761u) >> (32 - BK_VLOG2);
-  for (uint32_t p = 0; p < BK_VSLOTS; p++) {
-    const uint32_t old = atomicCAS(&vis[h], NONE, key);
+template <int W>
+struct BackLds {
+  static constexpr uint32_t VSLOTS = 1u << BackCfg<W>::VLOG2, CAP = BackCfg<W>::CAP;  // hash load <= 0.5
+  uint32_t vis[VSLOTS];
+  uint32_t lst[CAP];
+  uint32_t pref[W];
+  uint64_t rb[W];
+  uint32_t wsum[4];
+  uint32_t qi, n, hit, over;
+};
+
+template <int W>
+__device__ __forceinline__ void bk_sync() {
+  if (W == 64) __builtin_amdgcn_wave_barrier();
+  else __syncthreads();
+}
+
+template <int W>
+__device__ __forceinline__ int bk_insert(BackLds<W>& L, uint32_t key) {
+  constexpr uint32_t VSLOTS = BackLds<W>::VSLOTS;
+  uint32_t h = (key * 2654435761u) >> (32 - BackCfg<W>::VLOG2);
+  for (uint32_t p = 0; p < VSLOTS; p++) {
+    const uint32_t old = atomicCAS(&L.vis[h], NONE, key);
     if (old == NONE) return 1;
     if (old == key) return 0;
-    h = (h + 1) & (BK_VSLOTS - 1);
+    h = (h + 1) & (VSLOTS - 1);
   }
   return -1;
 }
 
 // Appends a newly seen node to the level list (capacity first, so the hash never fills).
-__device__ __forceinline__ void bk_add(uint32_t* vis, uint32_t* lst, BackShared& sh, uint32_t v) {
-  if (*(volatile uint32_t*)&sh.n >= BK_CAP) {
-    sh.over = 1;
+template <int W>
+__device__ __forceinline__ void bk_add(BackLds<W>& L, uint32_t v) {
+  if (*(volatile uint32_t*)&L.n >= BackLds<W>::CAP) {
+    L.over = 1;
     return;
   }
-  const int ins = bk_insert(vis, v);
+  const int ins = bk_insert(L, v);
   if (ins < 0) {
-    sh.over = 1;
+    L.over = 1;
   } else if (ins > 0) {
-    const uint32_t pos = atomicAdd(&sh.n, 1u);
-    if (pos < BK_CAP) lst[pos] = v;
-    else sh.over = 1;
+    const uint32_t pos = atomicAdd(&L.n, 1u);
+    if (pos < BackLds<W>::CAP) L.lst[pos] = v;
+    else L.over = 1;
   }
 }
 
+template <int W>
 __global__ __launch_bounds__(256) void k_back(DevSnap s, const RQuery* __restrict__ rq, const uint32_t* qlist,
                                               const uint32_t* qcount_p, uint32_t* qhead, uint8_t* __restrict__ out,
                                               uint32_t* __restrict__ err, uint32_t* next_list, uint32_t* next_count,
                                               Ctl* ctl) {
-  __shared__ uint32_t vis[BK_VSLOTS];
-  __shared__ uint32_t lst[BK_CAP];
-  __shared__ BackShared sh;
-  const int tid = threadIdx.x;
+  constexpr uint32_t VSLOTS = BackLds<W>::VSLOTS, CAP = BackLds<W>::CAP;
+  __shared__ BackLds<W> lds_all[256 / W];
+  BackLds<W>& L = lds_all[threadIdx.x / W];
+  const int t = threadIdx.x % W;  // thread within the query group
   const uint32_t qcount = *qcount_p;
   unsigned long long st_rows = 0, st_edges = 0, st_done = 0;
   for (;;) {
-    if (tid == 0) sh.qi = atomicAdd(qhead, 1u);
-    __syncthreads();
-    const uint32_t hi = sh.qi;
+    if (t == 0) L.qi = atomicAdd(qhead, 1u);
+    bk_sync<W>();
+    const uint32_t hi = L.qi;
     if (hi >= qcount) break;
     const uint32_t qi = qlist[hi];
     const RQuery q = rq[qi];
     const uint2 hr = holders_find(s, q.subj);
-    for (uint32_t i = tid * 4; i < BK_VSLOTS; i += 1024)
-      *reinterpret_cast<uint4*>(&vis[i]) = make_uint4(NONE, NONE, NONE, NONE);
-    if (tid == 0) {
-      sh.n = 0;
-      sh.hit = 0;
-      sh.over = hr.y > BK_CAP ? 1u : 0u;
+    for (uint32_t i = t * 4; i < VSLOTS; i += W * 4)
+      *reinterpret_cast<uint4*>(&L.vis[i]) = make_uint4(NONE, NONE, NONE, NONE);
+    if (t == 0) {
+      L.n = 0;
+      L.hit = 0;
+      L.over = hr.y > CAP ? 1u : 0u;
     }
-    __syncthreads();
-    if (!sh.over) {  // level 0: the holders (the root itself was probed by k_resolve)
-      for (uint32_t i = tid; i < hr.y; i += 256) {
+    bk_sync<W>();
+    if (!L.over) {  // level 0: the holders (the root itself was probed by k_resolve)
+      for (uint32_t i = t; i < hr.y; i += W) {
         const uint32_t v = s.hold[hr.x + i];
-        if (v == q.node) sh.hit = 1;
-        else bk_add(vis, lst, sh, v);
+        if (v == q.node) L.hit = 1;
+        else bk_add(L, v);
       }
     }
-    __syncthreads();
-    uint32_t lvl_b = 0, lvl_e = sh.n;
-    for (int j = 1; j <= q.depth - 1 && lvl_b < lvl_e && !sh.hit && !sh.over; j++) {
+    bk_sync<W>();
+    uint32_t lvl_b = 0, lvl_e = L.n;
+    for (int j = 1; j <= q.depth - 1 && lvl_b < lvl_e && !L.hit && !L.over; j++) {
       const bool keep = j < q.depth - 1;  // parents found here can still be expanded
-      for (uint32_t base = lvl_b; base < lvl_e; base += 256) {
-        const uint32_t i = base + tid;
+      for (uint32_t base = lvl_b; base < lvl_e; base += W) {
+        const uint32_t i = base + t;
         uint64_t rb = 0, re = 0;
         if (i < lvl_e) {
-          const uint32_t v = lst[i];
+          const uint32_t v = L.lst[i];
           rb = s.radj_off[v];
           re = s.radj_off[v + 1];
           st_rows++;
         }
-        sh.rb[tid] = rb;
+        L.rb[t] = rb;
         uint32_t total;
-        const uint32_t excl = block_excl_scan((uint32_t)(re - rb), sh.wsum, &total);
-        sh.pref[tid] = excl;
-        __syncthreads();
-        if (tid == 0) st_edges += total;
-        for (uint32_t eb = 0; eb < total; eb += 256) {
-          if (*(volatile uint32_t*)&sh.over || *(volatile uint32_t*)&sh.hit) break;
-          const uint32_t e = eb + tid;
+        const uint32_t excl = W == 64 ? wave_excl_scan((uint32_t)(re - rb), &total)
+                                      : block_excl_scan((uint32_t)(re - rb), L.wsum, &total);
+        L.pref[t] = excl;
+        bk_sync<W>();
+        if (t == 0) st_edges += total;
+        for (uint32_t eb = 0; eb < total; eb += W) {
+          if (*(volatile uint32_t*)&L.over || *(volatile uint32_t*)&L.hit) break;
+          const uint32_t e = eb + t;
           if (e < total) {
-            const int own = owner_search(sh.pref, 256, e);
-            const uint32_t p = s.radj[sh.rb[own] + (e - sh.pref[own])];
-            if (p == q.node) sh.hit = 1;
-            else if (keep) bk_add(vis, lst, sh, p);
+            const int own = owner_search(L.pref, W, e);
+            const uint32_t p = s.radj[L.rb[own] + (e - L.pref[own])];
+            if (p == q.node) L.hit = 1;
+            else if (keep) bk_add(L, p);
           }
         }
-        __syncthreads();
-        if (sh.hit || sh.over) break;
+        bk_sync<W>();
+        if (L.hit || L.over) break;
       }
-      __syncthreads();
+      bk_sync<W>();
       lvl_b = lvl_e;
-      lvl_e = sh.n;
+      lvl_e = L.n;
     }
-    __syncthreads();
-    if (tid == 0) {
-      if (sh.hit || !sh.over) {
-        out[qi] = sh.hit ? KG_IS_MEMBER : KG_NOT_MEMBER;
+    bk_sync<W>();
+    if (t == 0) {
+      if (L.hit || !L.over) {
+        out[qi] = L.hit ? KG_IS_MEMBER : KG_NOT_MEMBER;
         if (err) err[qi] = KG_ERR_NONE;
         st_done++;
       } else {
         next_list[atomicAdd(next_count, 1u)] = qi;
       }
     }
-    __syncthreads();
+    bk_sync<W>();
   }
+  __syncthreads();  // the groups of a workgroup finish at different times
   const int idx[3] = {ST_BROWS, ST_BEDGES, ST_BACK};
   const unsigned long long v[3] = {st_rows, st_edges, st_done};
   block_stats<3>(ctl, idx, v);
@@ -1044,12 +1071,14 @@ int check_batch_device(Snapshot* s, const kg_query* d_q, size_t n, int32_t globa
   if (n > 0x7FFFFFFFull) return set_error(-2, "batch too large");
   HIPC(hipSetDevice(s->device));
   if (!stream) stream = s->stream;
-  // scratch: rq[n] | light[8n] (8 shards) | light2[n] | gen[n] | medium[n] | heavy[n] | giant[n] | p2[n] | Ctl
+  // scratch: rq[n] | light[8n] (8 shards) | light2[n] | gen[n] | medium[n] | heavy[n] | giant[n] | p2[n] |
+  //          back2[n] | Ctl
   size_t off_rq = 0, off_light = align_up(off_rq + n * sizeof(RQuery)), off_light2 = align_up(off_light + 8 * n * 4),
          off_gen = align_up(off_light2 + n * 4),
          off_med = align_up(off_gen + n * 4), off_heavy = align_up(off_med + n * 4),
          off_giant = align_up(off_heavy + n * 4), off_p2 = align_up(off_giant + n * 4),
-         off_ctl = align_up(off_p2 + n * 4), total = align_up(off_ctl + sizeof(Ctl));
+         off_back2 = align_up(off_p2 + n * 4), off_ctl = align_up(off_back2 + n * 4),
+         total = align_up(off_ctl + sizeof(Ctl));
   if (total > s->scratch_bytes) {
     if (s->scratch) hipFree(s->scratch);
     s->scratch = nullptr;
@@ -1066,6 +1095,7 @@ int check_batch_device(Snapshot* s, const kg_query* d_q, size_t n, int32_t globa
   uint32_t* heavy = (uint32_t*)(base + off_heavy);
   uint32_t* giant = (uint32_t*)(base + off_giant);
   uint32_t* p2 = (uint32_t*)(base + off_p2);
+  uint32_t* back2 = (uint32_t*)(base + off_back2);
   Ctl* ctl = (Ctl*)(base + off_ctl);
   // tiers after k_light<64> (kg_snapshot_tune "tiers"): 0 grid; 1 LDS workgroup tier, then grid;
   // 2 LDS workgroup tier, then HBM workgroup tier (one workgroup per query)
@@ -1157,8 +1187,13 @@ int check_batch_device(Snapshot* s, const kg_query* d_q, size_t n, int32_t globa
       const uint32_t* fwd_list = heavy;
       const uint32_t* fwd_count = &ctl->heavy_count;
       if (use_back) {
-        hipLaunchKernelGGL(k_back, dim3((uint32_t)s->n_cu * 3), dim3(256), 0, stream, s->ds, rq, heavy,
-                           &ctl->heavy_count, &ctl->back_head, d_out, d_err, giant, &ctl->fwd_count, ctl);
+        // wave per query (~48 KiB LDS per workgroup: 3 per CU), its overflow to the workgroup-per-query
+        // width (~52 KiB: 3 per CU), whose overflow goes to the grid tier
+        hipLaunchKernelGGL(k_back<64>, dim3((uint32_t)s->n_cu * 3), dim3(256), 0, stream, s->ds, rq, heavy,
+                           &ctl->heavy_count, &ctl->back_head, d_out, d_err, back2, &ctl->back2_count, ctl);
+        HIPC(hipGetLastError());
+        hipLaunchKernelGGL(k_back<256>, dim3((uint32_t)s->n_cu * 3), dim3(256), 0, stream, s->ds, rq, back2,
+                           &ctl->back2_count, &ctl->back2_head, d_out, d_err, giant, &ctl->fwd_count, ctl);
         HIPC(hipGetLastError());
         fwd_list = giant;
         fwd_count = &ctl->fwd_count;

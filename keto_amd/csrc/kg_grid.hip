@@ -127,13 +127,20 @@ __device__ __forceinline__ void grid_append(GridCtl* ctl, const GridLog& lg, int
   __syncthreads();
 }
 
+// slots of a round: queries [base, base + G) of the list, clamped to its device-side length
+__device__ __forceinline__ uint32_t round_slots(const uint32_t* d_count, uint32_t base, uint32_t G) {
+  const uint32_t c = *d_count;
+  return c > base ? min(G, c - base) : 0u;
+}
+
 // Level 0: the roots (already probed by k_resolve), one per slot.
 __global__ __launch_bounds__(256) void k_grid_init(DevSnap s, const RQuery* __restrict__ rq,
-                                                   const uint32_t* __restrict__ qlist, uint32_t base, uint32_t cnt,
-                                                   GridLog lg, uint32_t* slot_q, uint2* slot_info, uint32_t* slot_hit,
-                                                   uint64_t* H, uint64_t mask, uint64_t epoch, GridCtl* ctl) {
+                                                   const uint32_t* __restrict__ qlist, const uint32_t* d_count,
+                                                   uint32_t base, uint32_t G, GridLog lg, uint32_t* slot_q,
+                                                   uint2* slot_info, uint32_t* slot_hit, uint64_t* H, uint64_t mask,
+                                                   uint64_t epoch, GridCtl* ctl) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  const bool valid = i < cnt;
+  const bool valid = i < round_slots(d_count, base, G);
   uint32_t rb = 0, len = 0;
   if (valid) {
     const uint32_t qi = qlist[base + i];
@@ -254,24 +261,21 @@ __global__ __launch_bounds__(256) void k_grid_level(DevSnap s, GridLog lg, int l
   if (lane == 0 && probes) atomicAdd(&ctl->probes8[blockIdx.x & 7][threadIdx.x >> 6], (unsigned long long)probes);
 }
 
-__global__ void k_grid_finish(const uint32_t* slot_q, const uint32_t* slot_hit, uint32_t cnt, uint8_t* out,
-                              uint32_t* err, const uint32_t* overflow) {
+__global__ void k_grid_finish(const uint32_t* slot_q, const uint32_t* slot_hit, const uint32_t* d_count, uint32_t base,
+                              uint32_t G, uint8_t* out, uint32_t* err, const uint32_t* overflow) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= cnt || *overflow) return;
+  if (i >= round_slots(d_count, base, G) || *overflow) return;
   const uint32_t qi = slot_q[i];
   out[qi] = slot_hit[i] ? KG_IS_MEMBER : KG_NOT_MEMBER;
   if (err) err[qi] = KG_ERR_NONE;
 }
 
-// Host driver: qlist / count live on the device (count is read back once).
+// Host driver: qlist / count live on the device.  A round is launched without knowing the count
+// (the kernels clamp to it); the host reads the counters once per round, after its last kernel.
 int grid_tier(Snapshot* s, const RQuery* rq, const uint32_t* qlist, const uint32_t* d_count, int global_max_depth,
               uint8_t* out, uint32_t* err, hipStream_t stream, GridStats* gs) {
   uint32_t* hb = (uint32_t*)s->host_buf(sizeof(GridCtl) + 64);
   if (!hb) return set_error(-1, "pinned host buffer");
-  HIPC(hipMemcpyAsync(hb, d_count, 4, hipMemcpyDeviceToHost, stream));
-  HIPC(hipStreamSynchronize(stream));
-  const uint32_t count = hb[0];
-  if (count == 0) return 0;
   const uint64_t nn = std::max<uint32_t>(s->ds.n_nodes, 1);
   // log capacity >= n_nodes (one slot alone always fits); hash >= 2x the log (load <= 0.5)
   const uint64_t cap = std::max<uint64_t>(nn + 1024, 64ull << 20);
@@ -310,37 +314,41 @@ int grid_tier(Snapshot* s, const RQuery* rq, const uint32_t* qlist, const uint32
   p += (size_t)G0 * 8;
   GridCtl* ctl = (GridCtl*)(((uintptr_t)p + 255) & ~uintptr_t(255));
   uint32_t G = G0;
-  for (uint32_t done = 0; done < count;) {
-    const uint32_t cnt = std::min(G, count - done);
+  int64_t count = -1;  // unknown until the first readback
+  for (uint32_t done = 0; count < 0 || done < (uint64_t)count;) {
     if (++s->grid_epoch == 0x10000) {  // epoch wrap: the table is zeroed once per 65535 rounds
       HIPC(hipMemsetAsync(H, 0, hcap * 8, stream));
       s->grid_epoch = 1;
     }
     const uint64_t epoch = s->grid_epoch;
+    const uint32_t slot_blocks = (G + 255) / 256;
     HIPC(hipMemsetAsync(ctl, 0, sizeof(GridCtl), stream));
-    hipLaunchKernelGGL(k_grid_init, dim3((cnt + 255) / 256), dim3(256), 0, stream, s->ds, rq, qlist, done, cnt, lg,
+    hipLaunchKernelGGL(k_grid_init, dim3(slot_blocks), dim3(256), 0, stream, s->ds, rq, qlist, d_count, done, G, lg,
                        slot_q, slot_info, slot_hit, H, hcap - 1, epoch, ctl);
     HIPC(hipGetLastError());
     // Levels run back to back on the device (sizes never come back to the host; an empty level
     // costs one near-empty launch).  Level k expands nodes at rest depth D-k >= 2, so at most
-    // global_max_depth-1 levels exist; the host reads the counters once per round.
+    // global_max_depth-1 levels exist.
     const int max_levels = std::max(1, global_max_depth - 1);
     for (int level = 0; level < max_levels; level++) {
       hipLaunchKernelGGL(k_grid_level, dim3((uint32_t)s->n_cu * 16), dim3(256), 0, stream, s->ds, lg, level,
                          slot_info, slot_hit, H, hcap - 1, epoch, ctl);
       HIPC(hipGetLastError());
     }
+    hipLaunchKernelGGL(k_grid_finish, dim3(slot_blocks), dim3(256), 0, stream, slot_q, slot_hit, d_count, done, G, out,
+                       err, &ctl->overflow);
+    HIPC(hipGetLastError());
     GridCtl h{};
     HIPC(hipMemcpyAsync(hb, ctl, sizeof h, hipMemcpyDeviceToHost, stream));
+    HIPC(hipMemcpyAsync(hb + sizeof(GridCtl) / 4, d_count, 4, hipMemcpyDeviceToHost, stream));
     HIPC(hipStreamSynchronize(stream));
     memcpy(&h, hb, sizeof h);
+    count = hb[sizeof(GridCtl) / 4];
+    const uint32_t cnt = count > done ? (uint32_t)std::min<int64_t>(G, count - done) : 0u;
     if (gs) {
       gs->rows += h.logged;
       gs->edges += h.edges;
     }
-    hipLaunchKernelGGL(k_grid_finish, dim3((cnt + 255) / 256), dim3(256), 0, stream, slot_q, slot_hit, cnt, out, err,
-                       &ctl->overflow);
-    HIPC(hipGetLastError());
     if (h.overflow) {  // log or probe bound exceeded: rerun these queries with fewer slots
       if (G == 1) return set_error(KG_ERR_RESOURCE_CODE, "grid tier capacity exceeded");
       G = std::max<uint32_t>(1, std::min(G, cnt) / 4);

@@ -28,3 +28,9 @@ if len(sys.argv) > 2:  # per-call durations of kernels matching argv[2] in that 
     for r in rows[b0:b1]:
         if sys.argv[2] in r["Kernel_Name"]:
             print(short(r["Kernel_Name"]), (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3, "us")
+if len(sys.argv) > 2 and sys.argv[2] == "gaps":
+    prev = t0
+    for r in rows[b0:b1]:
+        s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+        print(f"  +{(s - t0)/1e3:8.1f} gap {(s - prev)/1e3:7.1f}  {short(r['Kernel_Name']):40s} {(e - s)/1e3:7.1f} us")
+        prev = max(prev, e)
