@@ -27,7 +27,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
-STREAM_KERNELS = {0: "k_stream<8,7,256,16>", 1: "k_stream<16,6,256,32>", 2: "k_stream<16,7,512,32>"}
+STREAM_KERNELS = {0: "k_stream<8,7,256,16>", 1: "k_stream<16,6,256,32>", 2: "k_stream<16,7,512,32>",
+                  3: "k_stream<32,5,192,64>", 4: "k_stream<32,6,256,64>"}
 
 
 def parse():
@@ -41,7 +42,9 @@ def parse():
     ap.add_argument("--seed", type=int, default=20250131)
     ap.add_argument("--tiers", type=int, default=0, help="kg_snapshot_tune tiers (0 grid, 1 LDS-WG+grid, 2 WG)")
     ap.add_argument("--wide", type=int, default=0, help="kg_snapshot_tune wide (k_light<64> tier on/off)")
-    ap.add_argument("--stream", type=int, default=1, help="kg_snapshot_tune stream (k_stream variant 0/1/2)")
+    ap.add_argument("--stream", type=int, default=1, help="kg_snapshot_tune stream (k_stream variant 0..4)")
+    ap.add_argument("--stream-ecap", type=int, default=0, help="kg_snapshot_tune stream_ecap (edges per query, 0 = none)")
+    ap.add_argument("--grid-wgs", type=int, default=16, help="kg_snapshot_tune grid_wgs (k_grid_level WGs per CU)")
     ap.add_argument("--back", type=int, default=1, help="kg_snapshot_tune back (backward tier + no-holder filter)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline time budget (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=16)
@@ -209,6 +212,8 @@ def main():
     snap.tune("wide", a.wide)
     snap.tune("back", a.back)
     snap.tune("stream", a.stream)
+    snap.tune("stream_ecap", a.stream_ecap)
+    snap.tune("grid_wgs", a.grid_wgs)
     info = snap.info()
     t_build = time.time() - t_build
 
@@ -281,6 +286,7 @@ def main():
                            "all": {"rows": int(stats[-1].rows_opened), "edges": int(stats[-1].edges_read),
                                    "probes": int(stats[-1].direct_probes)},
                            "back": {"rows": int(stats[-1].back_rows), "edges": int(stats[-1].back_edges)}},
+        "stream_diag": stream_diag(stats[-1]),
         "snapshot_build_s": t_build,
         "roofline": {"kernel": STREAM_KERNELS[a.stream], "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
@@ -293,6 +299,14 @@ def main():
         print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()
+
+
+def stream_diag(s) -> dict:
+    """k_stream occupancy: wave steps (one HBM round trip each), edges per step, mean wave lifetime."""
+    steps, waves = int(s.light_steps), int(s.light_waves)
+    return {"steps": steps, "waves": waves, "edges_per_step": s.light_edges_read / steps if steps else 0.0,
+            "steps_per_wave": steps / waves if waves else 0.0,
+            "mean_wave_us": s.light_wave_ticks / waves / 100.0 if waves else 0.0}
 
 
 def pmc_traffic(tuples: int, batch: int):

@@ -103,6 +103,9 @@ typedef struct {
   uint64_t n_back;                      /* queries resolved by the backward tier         */
   uint64_t n_no_holder;                 /* queries answered NotMember by k_resolve: no row holds the subject */
   uint64_t back_rows, back_edges;       /* backward tier: parent lists opened / parents read */
+  uint64_t light_steps;                 /* k_stream: wave steps (one HBM round trip each) */
+  uint64_t light_waves;                 /* k_stream: waves that ran                      */
+  uint64_t light_wave_ticks;            /* k_stream: sum of wave lifetimes (100 MHz ticks) */
 } kg_stats;
 
 /* Per-query outputs of kg_check_batch. */

@@ -48,7 +48,8 @@ class kg_stats(C.Structure):
                 ("light_probes", C.c_uint64), ("kernel_ms", C.c_double), ("light_ms", C.c_double),
                 ("n_wide", C.c_uint64), ("n_grid", C.c_uint64),
                 ("n_back", C.c_uint64), ("n_no_holder", C.c_uint64), ("back_rows", C.c_uint64),
-                ("back_edges", C.c_uint64)]
+                ("back_edges", C.c_uint64), ("light_steps", C.c_uint64), ("light_waves", C.c_uint64),
+                ("light_wave_ticks", C.c_uint64)]
 
     def as_dict(self) -> dict:
         return {n: getattr(self, n) for n, _ in self._fields_}

@@ -188,8 +188,18 @@ int kg_snapshot_tune(kg_snapshot* sp, const char* key, int64_t value) {
     return 0;
   }
   if (strcmp(key, "stream") == 0) {
-    if (value < 0 || value > 2) return set_error(-2, "stream must be 0, 1 or 2");
+    if (value < 0 || value > 4) return set_error(-2, "stream must be in [0, 4]");
     s->stream_variant = (int)value;
+    return 0;
+  }
+  if (strcmp(key, "stream_ecap") == 0) {
+    if (value < 0 || value > 0xFFFFFFFFll) return set_error(-2, "stream_ecap must be in [0, 2^32)");
+    s->stream_ecap = (uint32_t)value;
+    return 0;
+  }
+  if (strcmp(key, "grid_wgs") == 0) {
+    if (value < 1 || value > 64) return set_error(-2, "grid_wgs must be in [1, 64]");
+    s->grid_wgs = (int)value;
     return 0;
   }
   if (strcmp(key, "back") == 0) {

@@ -35,8 +35,8 @@ namespace kg {
 
 // Counters: [0] rows_opened [1] edges_read [2] probes [3] frontier_hbm [4] light [5] heavy [6] general
 enum { ST_ROWS = 0, ST_EDGES, ST_PROBES, ST_FHBM, ST_LIGHT, ST_HEAVY, ST_GENERAL, ST_LROWS, ST_LEDGES, ST_LPROBES,
-       ST_MEDIUM, ST_BROWS, ST_BEDGES, ST_BACK, ST_NOHOLD, ST_N };
-static_assert(ST_N <= 16, "per-XCD counter shards hold 16 counters");
+       ST_MEDIUM, ST_BROWS, ST_BEDGES, ST_BACK, ST_NOHOLD, ST_LSTEPS, ST_LWAVES, ST_LTICKS, ST_N };
+static_assert(ST_N <= 32, "per-XCD counter shards hold 32 counters");
 
 // Device-side counters/heads (zeroed per batch).
 struct Ctl {
@@ -48,7 +48,7 @@ struct Ctl {
   uint32_t heads2[8 * 32];  // (k_light<64>)
   uint32_t light8[8 * 32];  // per-XCD shard sizes of the light list (k_resolve appends)
   unsigned long long st[ST_N];
-  unsigned long long st8[8][16];  // per-XCD shards of the hot counters (block-reduced adds)
+  unsigned long long st8[8][32];  // per-XCD shards of the hot counters (block-reduced adds)
   InterpCtl ic;
 };
 
@@ -415,9 +415,10 @@ template <int Q, int VLOG2, int QC>
 struct StreamLds {
   static constexpr int VIS = 1 << VLOG2;
   uint32_t vis[Q * VIS];
-  uint32_t e_beg[QC], e_len[QC], e_meta[QC];  // meta = slot (4) | generation (12) | rest depth (16)
+  uint32_t e_beg[QC], e_len[QC], e_meta[QC];  // meta = slot (4 | 5) | generation (12) | rest depth (16 | 15)
   uint32_t pref[64];
   uint32_t s_qi[Q], s_subj[Q], s_gen[Q], s_cnt[Q], s_ins[Q], s_flag[Q];
+  uint32_t s_edg[Q];  // edges scheduled for the slot's query (per-query edge budget)
 };
 
 // 1 inserted, 0 present, -1 table full (bounded)
@@ -443,11 +444,15 @@ template <int Q, int VLOG2, int QC, int CHUNK>
 __global__ __launch_bounds__(256) void k_stream(DevSnap s, const RQuery* __restrict__ rq, WorkList wl,
                                                 uint32_t* heads, uint8_t* __restrict__ out,
                                                 uint32_t* __restrict__ err, uint32_t* next_list,
-                                                uint32_t* next_count, Ctl* ctl) {
+                                                uint32_t* next_count, Ctl* ctl, uint32_t ecap) {
   using Lds = StreamLds<Q, VLOG2, QC>;
   constexpr int VIS = Lds::VIS;
   constexpr uint32_t INS_CAP = VIS * 5 / 8;  // expanded nodes per query (hash load <= 5/8)
-  static_assert(Q <= 16 && Q <= 64, "slot field is 4 bits");
+  // FIFO entry meta = slot (SB bits) | generation (12) | rest depth (DB bits)
+  constexpr int SB = Q <= 16 ? 4 : 5, DB = 32 - SB - 12;
+  constexpr uint32_t DMASK = (1u << DB) - 1, QMASK = Q == 32 ? 0xFFFFFFFFu : (1u << Q) - 1;
+  static_assert(Q <= 32, "slots are the bits of one u32 mask");
+  const uint64_t t_start = wall_clock64();
   static_assert(CHUNK <= 64, "one chunk entry per lane");
   __shared__ Lds lds_all[4];
   Lds& L = lds_all[threadIdx.x >> 6];
@@ -470,10 +475,10 @@ __global__ __launch_bounds__(256) void k_stream(DevSnap s, const RQuery* __restr
   uint32_t head = 0, tail = 0, head_off = 0;
   bool pend = false;  // per lane: a child of the previous step awaiting its probe
   uint32_t pend_node = 0, pend_slot = 0, pend_gen = 0;
-  unsigned long long st_rows = 0, st_edges = 0, st_probes = 0, st_done = 0;
+  unsigned long long st_rows = 0, st_edges = 0, st_probes = 0, st_done = 0, st_steps = 0;
   for (;;) {
     // ---- refill free slots (their root entries need FIFO room)
-    const uint32_t freem = ~active & ((1u << Q) - 1);
+    const uint32_t freem = ~active & QMASK;
     const uint32_t want = __popc(freem);
     if (want && !drained && (tail - head) + want <= QC) {
       // the wave pulls CHUNK consecutive list entries per dequeue (one device-scope atomic on the
@@ -512,17 +517,18 @@ __global__ __launch_bounds__(256) void k_stream(DevSnap s, const RQuery* __restr
           for (int k = 0; k < lane; k++) m &= m - 1;
           slot = __ffs(m) - 1;
           const uint32_t gen = L.s_gen[slot];
-          const bool over = qdepth > 0xFFFF || qlen > LONG_ROW;
+          const bool over = qdepth > (int32_t)DMASK || qlen > LONG_ROW || qlen > ecap;
           L.s_qi[slot] = qi;
           L.s_subj[slot] = qsubj;
           L.s_flag[slot] = over ? SF_OVER : 0u;
           L.s_cnt[slot] = 1;
           L.s_ins[slot] = 1;
+          L.s_edg[slot] = qlen;
           lx_insert3<VLOG2>(&L.vis[slot * VIS], qnode);
           const uint32_t at = (tail + lane) % QC;
           L.e_beg[at] = qbeg;
           L.e_len[at] = over ? 0u : qlen;
-          L.e_meta[at] = (slot << 28) | ((gen & 0xFFF) << 16) | (uint32_t)(over ? 2 : qdepth);
+          L.e_meta[at] = (slot << (32 - SB)) | ((gen & 0xFFF) << DB) | (uint32_t)(over ? 2 : qdepth);
         }
         active |= wave_or((uint32_t)lane < got ? 1u << slot : 0u);
         tail += got;
@@ -540,8 +546,8 @@ __global__ __launch_bounds__(256) void k_stream(DevSnap s, const RQuery* __restr
     if ((uint32_t)lane < avail) {
       const uint32_t at = (head + lane) % QC;
       emeta = L.e_meta[at];
-      const uint32_t sl = emeta >> 28;
-      live = ((active >> sl) & 1) && ((emeta >> 16) & 0xFFF) == (L.s_gen[sl] & 0xFFF) &&
+      const uint32_t sl = emeta >> (32 - SB);
+      live = ((active >> sl) & 1) && ((emeta >> DB) & 0xFFF) == (L.s_gen[sl] & 0xFFF) &&
              (L.s_flag[sl] & (SF_HIT | SF_OVER)) == 0;
       ebeg = L.e_beg[at];
       elen = live ? L.e_len[at] : 0u;
@@ -558,7 +564,7 @@ __global__ __launch_bounds__(256) void k_stream(DevSnap s, const RQuery* __restr
     const bool consumed = (uint32_t)lane < avail && excl + elen <= taken;
     const uint32_t ncons = __popcll(__ballot(consumed));  // a prefix of the window
     if (consumed && live) {
-      atomicSub(&L.s_cnt[emeta >> 28], 1u);
+      atomicSub(&L.s_cnt[emeta >> (32 - SB)], 1u);
       st_rows++;
     }
     {
@@ -579,16 +585,17 @@ __global__ __launch_bounds__(256) void k_stream(DevSnap s, const RQuery* __restr
     if (h) atomicOr(&L.s_flag[pend_slot], SF_HIT);
     head += ncons;
     st_edges += (lane == 0) ? taken : 0u;
+    st_steps += (lane == 0) ? 1u : 0u;
     // ---- children: kept (rest >= 2, non-empty set row) ones are marked + appended; every new
     // child is probed next step
-    const uint32_t slot = om >> 28, d = om & 0xFFFF;
+    const uint32_t slot = om >> (32 - SB), d = om & DMASK;
     const bool keepc = act && d >= 3 && x.len > 0;
     bool fresh = false;
     if (keepc) {
       const int r = x.len > LONG_ROW ? -1 : lx_insert3<VLOG2>(&L.vis[slot * VIS], x.node);
       if (r != 0) {
         const uint32_t k = r > 0 ? atomicAdd(&L.s_ins[slot], 1u) : INS_CAP;
-        if (k >= INS_CAP) atomicOr(&L.s_flag[slot], SF_OVER);
+        if (k >= INS_CAP || atomicAdd(&L.s_edg[slot], x.len) + x.len > ecap) atomicOr(&L.s_flag[slot], SF_OVER);
         else fresh = true;
       }
     }
@@ -601,7 +608,7 @@ __global__ __launch_bounds__(256) void k_stream(DevSnap s, const RQuery* __restr
         const uint32_t at = (tail + pos) % QC;
         L.e_beg[at] = x.begin;
         L.e_len[at] = x.len;
-        L.e_meta[at] = (om & 0xFFFF0000u) | (d - 1);
+        L.e_meta[at] = (om & ~DMASK) | (d - 1);
         atomicAdd(&L.s_cnt[slot], 1u);
         appended = true;
       } else {
@@ -635,7 +642,7 @@ __global__ __launch_bounds__(256) void k_stream(DevSnap s, const RQuery* __restr
       }
       if (done) L.s_gen[lane]++;  // stale: its FIFO entries and pending probes
     }
-    const uint32_t freed = (uint32_t)__ballot(done) & ((1u << Q) - 1);
+    const uint32_t freed = (uint32_t)__ballot(done) & QMASK;
     if (freed) {
       active &= ~freed;
       for (uint32_t m = freed; m; m &= m - 1) {
@@ -646,9 +653,10 @@ __global__ __launch_bounds__(256) void k_stream(DevSnap s, const RQuery* __restr
     }
     __builtin_amdgcn_wave_barrier();
   }
-  const int idx[4] = {ST_LROWS, ST_LEDGES, ST_LPROBES, ST_LIGHT};
-  const unsigned long long v[4] = {st_rows, st_edges, st_probes, st_done};
-  block_stats<4>(ctl, idx, v);
+  const unsigned long long life = lane == 0 ? wall_clock64() - t_start : 0ull;
+  const int idx[7] = {ST_LROWS, ST_LEDGES, ST_LPROBES, ST_LIGHT, ST_LSTEPS, ST_LWAVES, ST_LTICKS};
+  const unsigned long long v[7] = {st_rows, st_edges, st_probes, st_done, st_steps, lane == 0 ? 1ull : 0ull, life};
+  block_stats<7>(ctl, idx, v);
 }
 
 // ------------------------------------------------------------------ workgroup tiers
@@ -1149,17 +1157,20 @@ int check_batch_device(Snapshot* s, const kg_query* d_q, size_t n, int32_t globa
       // ~30 KiB of LDS per workgroup (variant 0: 8 slots x 512 B visited + 256-entry FIFO per wave;
       // 1: 16 slots x 256 B; 2: 16 slots x 512 B + 512-entry FIFO): 5 (2: 3) workgroups per CU
       const WorkList wl{light, ctl->light8, (uint32_t)n, 1u};
-      const uint32_t per_cu = s->stream_variant == 2 ? 3 : 5;
+      // 3: 32 slots x 128 B visited + 192-entry FIFO (~30 KiB, 5 per CU); 4: 32 slots x 256 B (~49 KiB, 3 per CU)
+      const int sv = s->stream_variant;
+      const uint32_t per_cu = (sv == 2 || sv == 4) ? 3 : 5;
+      const uint32_t ecap = s->stream_ecap ? s->stream_ecap : 0xFFFFFFFFu;
       const uint32_t grid = (uint32_t)std::min<uint64_t>((uint64_t)s->n_cu * per_cu, (n + 31) / 32 + 8);
-      if (s->stream_variant == 1)
-        hipLaunchKernelGGL((k_stream<16, 6, 256, 32>), dim3(grid), dim3(256), 0, stream, s->ds, rq, wl, ctl->heads,
-                           d_out, d_err, ovf_list, ovf_count, ctl);
-      else if (s->stream_variant == 2)
-        hipLaunchKernelGGL((k_stream<16, 7, 512, 32>), dim3(grid), dim3(256), 0, stream, s->ds, rq, wl, ctl->heads,
-                           d_out, d_err, ovf_list, ovf_count, ctl);
-      else
-        hipLaunchKernelGGL((k_stream<8, 7, 256, 16>), dim3(grid), dim3(256), 0, stream, s->ds, rq, wl, ctl->heads,
-                           d_out, d_err, ovf_list, ovf_count, ctl);
+#define KG_STREAM(Q, V, QC, CH)                                                                                   \
+  hipLaunchKernelGGL((k_stream<Q, V, QC, CH>), dim3(grid), dim3(256), 0, stream, s->ds, rq, wl, ctl->heads, d_out, \
+                     d_err, ovf_list, ovf_count, ctl, ecap)
+      if (sv == 1) KG_STREAM(16, 6, 256, 32);
+      else if (sv == 2) KG_STREAM(16, 7, 512, 32);
+      else if (sv == 3) KG_STREAM(32, 5, 192, 64);
+      else if (sv == 4) KG_STREAM(32, 6, 256, 64);
+      else KG_STREAM(8, 7, 256, 16);
+#undef KG_STREAM
     }
     HIPC(hipGetLastError());
     if (stats) HIPC(hipEventRecord(l1, stream));
@@ -1249,6 +1260,9 @@ int check_batch_device(Snapshot* s, const kg_query* d_q, size_t n, int32_t globa
     stats->n_no_holder = h.st[ST_NOHOLD];
     stats->back_rows = h.st[ST_BROWS];
     stats->back_edges = h.st[ST_BEDGES];
+    stats->light_steps = h.st[ST_LSTEPS];
+    stats->light_waves = h.st[ST_LWAVES];
+    stats->light_wave_ticks = h.st[ST_LTICKS];
     stats->kernel_ms = ms;
   }
   return 0;

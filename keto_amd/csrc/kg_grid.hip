@@ -331,7 +331,7 @@ int grid_tier(Snapshot* s, const RQuery* rq, const uint32_t* qlist, const uint32
     // global_max_depth-1 levels exist.
     const int max_levels = std::max(1, global_max_depth - 1);
     for (int level = 0; level < max_levels; level++) {
-      hipLaunchKernelGGL(k_grid_level, dim3((uint32_t)s->n_cu * 16), dim3(256), 0, stream, s->ds, lg, level,
+      hipLaunchKernelGGL(k_grid_level, dim3((uint32_t)s->n_cu * s->grid_wgs), dim3(256), 0, stream, s->ds, lg, level,
                          slot_info, slot_hit, H, hcap - 1, epoch, ctl);
       HIPC(hipGetLastError());
     }
