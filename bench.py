@@ -42,9 +42,10 @@ def parse():
     ap.add_argument("--seed", type=int, default=20250131)
     ap.add_argument("--tiers", type=int, default=0, help="kg_snapshot_tune tiers (0 grid, 1 LDS-WG+grid, 2 WG)")
     ap.add_argument("--wide", type=int, default=0, help="kg_snapshot_tune wide (k_light<64> tier on/off)")
-    ap.add_argument("--stream", type=int, default=1, help="kg_snapshot_tune stream (k_stream variant 0..4)")
+    ap.add_argument("--stream", type=int, default=4, help="kg_snapshot_tune stream (k_stream variant 0..4)")
     ap.add_argument("--stream-ecap", type=int, default=0, help="kg_snapshot_tune stream_ecap (edges per query, 0 = none)")
     ap.add_argument("--grid-wgs", type=int, default=16, help="kg_snapshot_tune grid_wgs (k_grid_level WGs per CU)")
+    ap.add_argument("--stream-wgs", type=int, default=0, help="kg_snapshot_tune stream_wgs (k_stream WGs per CU, 0 = auto)")
     ap.add_argument("--back", type=int, default=1, help="kg_snapshot_tune back (backward tier + no-holder filter)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline time budget (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=16)
@@ -214,6 +215,7 @@ def main():
     snap.tune("stream", a.stream)
     snap.tune("stream_ecap", a.stream_ecap)
     snap.tune("grid_wgs", a.grid_wgs)
+    snap.tune("stream_wgs", a.stream_wgs)
     info = snap.info()
     t_build = time.time() - t_build
 

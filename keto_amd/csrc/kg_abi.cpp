@@ -197,6 +197,11 @@ int kg_snapshot_tune(kg_snapshot* sp, const char* key, int64_t value) {
     s->stream_ecap = (uint32_t)value;
     return 0;
   }
+  if (strcmp(key, "stream_wgs") == 0) {
+    if (value < 0 || value > 8) return set_error(-2, "stream_wgs must be in [0, 8]");
+    s->stream_wgs = (int)value;
+    return 0;
+  }
   if (strcmp(key, "grid_wgs") == 0) {
     if (value < 1 || value > 64) return set_error(-2, "grid_wgs must be in [1, 64]");
     s->grid_wgs = (int)value;

@@ -71,15 +71,38 @@ __device__ __forceinline__ uint2 holders_find(const DevSnap& s, uint32_t subj) {
   return make_uint2(0, 0);
 }
 
+// Wave64 scans on DPP (GFX9 data-parallel primitives): every step is one VALU op on registers,
+// no LDS round trip (a __shfl is a ds_bpermute).  row_shr:n = 0x110+n shifts inside rows of 16
+// lanes (lanes without a source read 0), row_bcast:15 / row_bcast:31 (0x142 / 0x143) carry row
+// totals across rows.  Must be called with every lane of the wave active.
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ uint32_t dpp0(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROW_MASK, 0xf, true);
+}
+struct DppAdd {
+  __device__ static uint32_t op(uint32_t a, uint32_t b) { return a + b; }
+};
+struct DppOr {
+  __device__ static uint32_t op(uint32_t a, uint32_t b) { return a | b; }
+};
+struct DppMax {
+  __device__ static uint32_t op(uint32_t a, uint32_t b) { return a > b ? a : b; }
+};
+// inclusive scan over the 64 lanes for an operator whose identity is 0
+template <class Op>
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+  v = Op::op(v, dpp0<0x111, 0xf>(v));
+  v = Op::op(v, dpp0<0x112, 0xf>(v));
+  v = Op::op(v, dpp0<0x114, 0xf>(v));
+  v = Op::op(v, dpp0<0x118, 0xf>(v));
+  v = Op::op(v, dpp0<0x142, 0xa>(v));
+  v = Op::op(v, dpp0<0x143, 0xc>(v));
+  return v;
+}
+
 __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t x, uint32_t* total) {
-  int lane = lane_id();
-  uint32_t v = x;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    uint32_t y = __shfl_up(v, off, 64);
-    if (lane >= off) v += y;
-  }
-  *total = __shfl(v, 63, 64);
+  const uint32_t v = wave_incl_scan<DppAdd>(x);
+  *total = (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
   return v - x;
 }
 

@@ -436,8 +436,7 @@ __device__ __forceinline__ int lx_insert3(uint32_t* vis, uint32_t key) {
 }
 
 __device__ __forceinline__ uint32_t wave_or(uint32_t v) {
-  for (int off = 32; off; off >>= 1) v |= __shfl_xor(v, off, 64);
-  return v;
+  return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan<DppOr>(v), 63);
 }
 
 template <int Q, int VLOG2, int QC, int CHUNK>
@@ -504,18 +503,18 @@ __global__ __launch_bounds__(256) void k_stream(DevSnap s, const RQuery* __restr
       }
       const uint32_t got = min(want, c_left);
       if (got) {
-        const int src = (uint32_t)lane < got ? (int)(c_pos + lane) : lane;
+        // lane = slot: the free slot of rank r (among free slots) takes chunk entry c_pos + r
+        const uint32_t r = __popc(freem & (lane < 32 ? (1u << lane) - 1u : 0xFFFFFFFFu));
+        const bool mine = lane < Q && ((freem >> (lane & 31)) & 1u) && r < got;
+        const int src = mine ? (int)(c_pos + r) : lane;
         const uint32_t qi = __shfl(cq_qi, src, 64), qnode = __shfl(cq_node, src, 64),
                        qsubj = __shfl(cq_subj, src, 64), qbeg = __shfl(cq_beg, src, 64),
                        qlen = __shfl(cq_len, src, 64);
         const int32_t qdepth = __shfl(cq_depth, src, 64);
         c_pos += got;
         c_left -= got;
-        uint32_t slot = 0;
-        if ((uint32_t)lane < got) {
-          uint32_t m = freem;
-          for (int k = 0; k < lane; k++) m &= m - 1;
-          slot = __ffs(m) - 1;
+        if (mine) {
+          const uint32_t slot = lane;
           const uint32_t gen = L.s_gen[slot];
           const bool over = qdepth > (int32_t)DMASK || qlen > LONG_ROW || qlen > ecap;
           L.s_qi[slot] = qi;
@@ -525,12 +524,12 @@ __global__ __launch_bounds__(256) void k_stream(DevSnap s, const RQuery* __restr
           L.s_ins[slot] = 1;
           L.s_edg[slot] = qlen;
           lx_insert3<VLOG2>(&L.vis[slot * VIS], qnode);
-          const uint32_t at = (tail + lane) % QC;
+          const uint32_t at = (tail + r) % QC;
           L.e_beg[at] = qbeg;
           L.e_len[at] = over ? 0u : qlen;
           L.e_meta[at] = (slot << (32 - SB)) | ((gen & 0xFFF) << DB) | (uint32_t)(over ? 2 : qdepth);
         }
-        active |= wave_or((uint32_t)lane < got ? 1u << slot : 0u);
+        active |= (uint32_t)__ballot(mine);
         tail += got;
       }
     }
@@ -558,9 +557,12 @@ __global__ __launch_bounds__(256) void k_stream(DevSnap s, const RQuery* __restr
     }
     uint32_t total;
     const uint32_t excl = wave_excl_scan(elen, &total);
-    L.pref[lane] = excl;
+    // owner of edge e = the non-empty entry starting at or below e: entries mark their start in
+    // L.pref (start position -> entry lane + 1) and a DPP max-scan spreads the marks
+    L.pref[lane] = 0;
     __builtin_amdgcn_wave_barrier();
     const uint32_t taken = min(total, 64u);
+    if (elen > 0 && excl < taken) L.pref[excl] = (uint32_t)lane + 1;
     const bool consumed = (uint32_t)lane < avail && excl + elen <= taken;
     const uint32_t ncons = __popcll(__ballot(consumed));  // a prefix of the window
     if (consumed && live) {
@@ -568,17 +570,19 @@ __global__ __launch_bounds__(256) void k_stream(DevSnap s, const RQuery* __restr
       st_rows++;
     }
     {
-      const uint32_t ex_n = __shfl(excl, ncons & 63, 64);
+      const uint32_t ex_n = (uint32_t)__builtin_amdgcn_readlane((int)excl, ncons & 63);
       if (ncons < avail && ncons < 64 && ex_n < taken) head_off = (ncons == 0 ? head_off : 0u) + (taken - ex_n);
       else if (ncons > 0) head_off = 0;
     }
     // ---- this step's edges; previous step's probes in flight together with them
+    __builtin_amdgcn_wave_barrier();
     const bool act = (uint32_t)lane < taken;
-    const int own = act ? owner_search(L.pref, 64, (uint32_t)lane) : 0;
+    const int own = ((int)wave_incl_scan<DppMax>(L.pref[lane]) - 1) & 63;
     const uint32_t ob = __shfl(ebeg, own, 64);
     const uint32_t om = __shfl(emeta, own, 64);
+    const uint32_t ox = __shfl(excl, own, 64);
     AdjX x{NONE, 0, 0, 0};
-    if (act) x = s.adjx[ob + ((uint32_t)lane - L.pref[own])];
+    if (act) x = s.adjx[ob + ((uint32_t)lane - ox)];
     const bool pvalid = pend && L.s_gen[pend_slot] == pend_gen;
     const bool h = pvalid && dset_probe(s, pend_node, L.s_subj[pend_slot]);
     st_probes += pvalid ? 1 : 0;
@@ -933,6 +937,7 @@ __global__ __launch_bounds__(256) void k_back(DevSnap s, const RQuery* __restric
                                               uint32_t* __restrict__ err, uint32_t* next_list, uint32_t* next_count,
                                               Ctl* ctl) {
   constexpr uint32_t VSLOTS = BackLds<W>::VSLOTS, CAP = BackLds<W>::CAP;
+  constexpr int BU = 4;
   __shared__ BackLds<W> lds_all[256 / W];
   BackLds<W>& L = lds_all[threadIdx.x / W];
   const int t = threadIdx.x % W;  // thread within the query group
@@ -981,14 +986,25 @@ __global__ __launch_bounds__(256) void k_back(DevSnap s, const RQuery* __restric
         L.pref[t] = excl;
         bk_sync<W>();
         if (t == 0) st_edges += total;
-        for (uint32_t eb = 0; eb < total; eb += W) {
+        // BU edges per thread and step: the BU parent loads of a thread are independent, so a long
+        // reverse row costs 1/BU of the dependent round trips
+        for (uint32_t eb = 0; eb < total; eb += W * BU) {
           if (*(volatile uint32_t*)&L.over || *(volatile uint32_t*)&L.hit) break;
-          const uint32_t e = eb + t;
-          if (e < total) {
-            const int own = owner_search(L.pref, W, e);
-            const uint32_t p = s.radj[L.rb[own] + (e - L.pref[own])];
-            if (p == q.node) L.hit = 1;
-            else if (keep) bk_add(L, p);
+          uint32_t p[BU];
+#pragma unroll
+          for (int u = 0; u < BU; u++) {
+            const uint32_t e = eb + u * W + t;
+            p[u] = NONE;
+            if (e < total) {
+              const int own = owner_search(L.pref, W, e);
+              p[u] = s.radj[L.rb[own] + (e - L.pref[own])];
+            }
+          }
+#pragma unroll
+          for (int u = 0; u < BU; u++) {
+            if (p[u] == NONE) continue;
+            if (p[u] == q.node) L.hit = 1;
+            else if (keep) bk_add(L, p[u]);
           }
         }
         bk_sync<W>();
@@ -1159,7 +1175,7 @@ int check_batch_device(Snapshot* s, const kg_query* d_q, size_t n, int32_t globa
       const WorkList wl{light, ctl->light8, (uint32_t)n, 1u};
       // 3: 32 slots x 128 B visited + 192-entry FIFO (~30 KiB, 5 per CU); 4: 32 slots x 256 B (~49 KiB, 3 per CU)
       const int sv = s->stream_variant;
-      const uint32_t per_cu = (sv == 2 || sv == 4) ? 3 : 5;
+      const uint32_t per_cu = s->stream_wgs ? (uint32_t)s->stream_wgs : ((sv == 2 || sv == 4) ? 3u : 5u);
       const uint32_t ecap = s->stream_ecap ? s->stream_ecap : 0xFFFFFFFFu;
       const uint32_t grid = (uint32_t)std::min<uint64_t>((uint64_t)s->n_cu * per_cu, (n + 31) / 32 + 8);
 #define KG_STREAM(Q, V, QC, CH)                                                                                   \
