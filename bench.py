@@ -28,7 +28,8 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 STREAM_KERNELS = {0: "k_stream<8,7,256,16>", 1: "k_stream<16,6,256,32>", 2: "k_stream<16,7,512,32>",
-                  3: "k_stream<32,5,192,64>", 4: "k_stream<32,6,256,64>"}
+                  3: "k_stream<32,5,192,64>", 4: "k_stream<32,6,256,64>", 5: "k_stream<32,wave1024/128,256,64>",
+                  6: "k_stream<32,wave1024/256,320,64>"}
 
 
 def parse():
@@ -42,7 +43,7 @@ def parse():
     ap.add_argument("--seed", type=int, default=20250131)
     ap.add_argument("--tiers", type=int, default=0, help="kg_snapshot_tune tiers (0 grid, 1 LDS-WG+grid, 2 WG)")
     ap.add_argument("--wide", type=int, default=0, help="kg_snapshot_tune wide (k_light<64> tier on/off)")
-    ap.add_argument("--stream", type=int, default=4, help="kg_snapshot_tune stream (k_stream variant 0..4)")
+    ap.add_argument("--stream", type=int, default=5, help="kg_snapshot_tune stream (k_stream variant 0..6)")
     ap.add_argument("--stream-ecap", type=int, default=0, help="kg_snapshot_tune stream_ecap (edges per query, 0 = none)")
     ap.add_argument("--grid-wgs", type=int, default=16, help="kg_snapshot_tune grid_wgs (k_grid_level WGs per CU)")
     ap.add_argument("--stream-wgs", type=int, default=0, help="kg_snapshot_tune stream_wgs (k_stream WGs per CU, 0 = auto)")

@@ -411,16 +411,6 @@ __global__ __launch_bounds__(256) void k_light(DevSnap s, const RQuery* __restri
 constexpr uint32_t LONG_ROW = 2048;  // rows longer than this go to a wider tier
 constexpr uint32_t SF_HIT = 1, SF_OVER = 2;
 
-template <int Q, int VLOG2, int QC>
-struct StreamLds {
-  static constexpr int VIS = 1 << VLOG2;
-  uint32_t vis[Q * VIS];
-  uint32_t e_beg[QC], e_len[QC], e_meta[QC];  // meta = slot (4 | 5) | generation (12) | rest depth (16 | 15)
-  uint32_t pref[64];
-  uint32_t s_qi[Q], s_subj[Q], s_gen[Q], s_cnt[Q], s_ins[Q], s_flag[Q];
-  uint32_t s_edg[Q];  // edges scheduled for the slot's query (per-query edge budget)
-};
-
 // 1 inserted, 0 present, -1 table full (bounded)
 template <int VLOG2>
 __device__ __forceinline__ int lx_insert3(uint32_t* vis, uint32_t key) {
@@ -435,18 +425,89 @@ __device__ __forceinline__ int lx_insert3(uint32_t* vis, uint32_t key) {
   return -1;
 }
 
+// Visited sets of the stream tier's slots (nodes a query has expanded), two layouts:
+//   SlotVis<Q, VLOG2>   one table of 2^VLOG2 u32 keys per slot, cleared when the slot is freed;
+//                       a query may expand 5/8 of its table
+//   WaveVis<VLOG2, CAP> ONE table of 2^VLOG2 64-bit keys valid | generation (26) | slot (5) | node
+//                       shared by the wave's slots: small queries use little, so a single query may
+//                       expand up to CAP nodes as long as the live entries stay <= 5/8 of the table.
+//                       Entries of a finished query (an older generation of their slot) count as
+//                       free and are reclaimed by later inserts; nothing is cleared.  A reclaim can
+//                       let a node be inserted twice (expanded twice: extra work, same answer), but
+//                       a node is never reported present unless this query inserted it.
+template <int Q, int VLOG2>
+struct SlotVis {
+  static constexpr uint32_t VIS = 1u << VLOG2, INS_CAP = VIS * 5 / 8;
+  uint32_t vis[Q * VIS];
+  __device__ void init(int lane) {
+    for (int i = lane; i < Q * (int)VIS; i += 64) vis[i] = NONE;
+  }
+  __device__ int insert(uint32_t slot, uint32_t, uint32_t node, const uint32_t*) {
+    return lx_insert3<VLOG2>(&vis[slot * VIS], node);
+  }
+  __device__ void release(uint32_t slot, uint32_t, int lane) {
+    for (int i = lane; i < (int)VIS; i += 64) vis[slot * VIS + i] = NONE;
+  }
+};
+
+template <int VLOG2, int CAP>
+struct WaveVis {
+  static constexpr uint32_t VT = 1u << VLOG2, INS_CAP = CAP, LIVE_CAP = VT * 5 / 8;
+  unsigned long long vt[VT];
+  uint32_t live;
+  __device__ void init(int lane) {
+    for (int i = lane; i < (int)VT; i += 64) vt[i] = 0ull;
+    if (lane == 0) live = 0;
+  }
+  __device__ int insert(uint32_t slot, uint32_t gen, uint32_t node, const uint32_t* s_gen) {
+    if (*(volatile uint32_t*)&live >= LIVE_CAP) return -1;
+    const unsigned long long key =
+        (1ull << 63) | ((unsigned long long)(gen & 0x3FFFFFFu) << 37) | ((unsigned long long)slot << 32) | node;
+    uint32_t h = ((node ^ (slot * 0x9E3779B9u)) * 2654435761u) >> (32 - VLOG2);
+    for (uint32_t p = 0; p < VT; p++) {
+      unsigned long long cur = vt[h];
+      for (;;) {
+        if (cur == key) return 0;
+        if (cur != 0ull) {  // a live entry of some slot (its generation is current): probe on
+          const uint32_t es = (uint32_t)(cur >> 32) & 31u, eg = (uint32_t)(cur >> 37) & 0x3FFFFFFu;
+          if (eg == (s_gen[es] & 0x3FFFFFFu)) break;
+        }
+        const unsigned long long old = atomicCAS(&vt[h], cur, key);
+        if (old == cur) {
+          atomicAdd(&live, 1u);
+          return 1;
+        }
+        cur = old;
+      }
+      h = (h + 1) & (VT - 1);
+    }
+    return -1;
+  }
+  __device__ void release(uint32_t, uint32_t inserted, int lane) {
+    if (lane == 0) atomicSub(&live, inserted);
+  }
+};
+
+template <int Q, class Vis, int QC>
+struct StreamLds {
+  Vis V;
+  uint32_t e_beg[QC], e_len[QC], e_meta[QC];  // meta = slot (4 | 5) | generation (12) | rest depth (16 | 15)
+  uint32_t pref[64];
+  uint32_t s_qi[Q], s_subj[Q], s_gen[Q], s_cnt[Q], s_ins[Q], s_flag[Q];
+  uint32_t s_edg[Q];  // edges scheduled for the slot's query (per-query edge budget)
+};
+
 __device__ __forceinline__ uint32_t wave_or(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan<DppOr>(v), 63);
 }
 
-template <int Q, int VLOG2, int QC, int CHUNK>
+template <int Q, class Vis, int QC, int CHUNK>
 __global__ __launch_bounds__(256) void k_stream(DevSnap s, const RQuery* __restrict__ rq, WorkList wl,
                                                 uint32_t* heads, uint8_t* __restrict__ out,
                                                 uint32_t* __restrict__ err, uint32_t* next_list,
                                                 uint32_t* next_count, Ctl* ctl, uint32_t ecap) {
-  using Lds = StreamLds<Q, VLOG2, QC>;
-  constexpr int VIS = Lds::VIS;
-  constexpr uint32_t INS_CAP = VIS * 5 / 8;  // expanded nodes per query (hash load <= 5/8)
+  using Lds = StreamLds<Q, Vis, QC>;
+  constexpr uint32_t INS_CAP = Vis::INS_CAP;  // expanded nodes per query
   // FIFO entry meta = slot (SB bits) | generation (12) | rest depth (DB bits)
   constexpr int SB = Q <= 16 ? 4 : 5, DB = 32 - SB - 12;
   constexpr uint32_t DMASK = (1u << DB) - 1, QMASK = Q == 32 ? 0xFFFFFFFFu : (1u << Q) - 1;
@@ -458,7 +519,7 @@ __global__ __launch_bounds__(256) void k_stream(DevSnap s, const RQuery* __restr
   const int lane = lane_id();
   const uint32_t head0 = blockIdx.x & 7;  // XCD label (speed only, never correctness)
   uint32_t head_sel = head0;
-  for (int i = lane; i < Q * VIS; i += 64) L.vis[i] = NONE;
+  L.V.init(lane);
   if (lane < Q) {
     L.s_gen[lane] = 0;
     L.s_flag[lane] = 0;
@@ -521,9 +582,8 @@ __global__ __launch_bounds__(256) void k_stream(DevSnap s, const RQuery* __restr
           L.s_subj[slot] = qsubj;
           L.s_flag[slot] = over ? SF_OVER : 0u;
           L.s_cnt[slot] = 1;
-          L.s_ins[slot] = 1;
           L.s_edg[slot] = qlen;
-          lx_insert3<VLOG2>(&L.vis[slot * VIS], qnode);
+          L.s_ins[slot] = L.V.insert(slot, gen, qnode, L.s_gen) > 0 ? 1u : 0u;
           const uint32_t at = (tail + r) % QC;
           L.e_beg[at] = qbeg;
           L.e_len[at] = over ? 0u : qlen;
@@ -596,7 +656,7 @@ __global__ __launch_bounds__(256) void k_stream(DevSnap s, const RQuery* __restr
     const bool keepc = act && d >= 3 && x.len > 0;
     bool fresh = false;
     if (keepc) {
-      const int r = x.len > LONG_ROW ? -1 : lx_insert3<VLOG2>(&L.vis[slot * VIS], x.node);
+      const int r = x.len > LONG_ROW ? -1 : L.V.insert(slot, L.s_gen[slot], x.node, L.s_gen);
       if (r != 0) {
         const uint32_t k = r > 0 ? atomicAdd(&L.s_ins[slot], 1u) : INS_CAP;
         if (k >= INS_CAP || atomicAdd(&L.s_edg[slot], x.len) + x.len > ecap) atomicOr(&L.s_flag[slot], SF_OVER);
@@ -651,7 +711,7 @@ __global__ __launch_bounds__(256) void k_stream(DevSnap s, const RQuery* __restr
       active &= ~freed;
       for (uint32_t m = freed; m; m &= m - 1) {
         const uint32_t sl = __ffs(m) - 1;
-        for (int i = lane; i < VIS; i += 64) L.vis[sl * VIS + i] = NONE;
+        L.V.release(sl, L.s_ins[sl], lane);
       }
       if (pend && ((freed >> pend_slot) & 1)) pend = false;
     }
@@ -1146,6 +1206,8 @@ int check_batch_device(Snapshot* s, const kg_query* d_q, size_t n, int32_t globa
     gl = gb + words;
   }
   GridStats gs;
+  bool grid_pending = false;
+  const uint32_t *grid_list = nullptr, *grid_count = nullptr;
 
   if (stats && !s->ev[0])
     for (auto& e : s->ev) HIPC(hipEventCreate(&e));
@@ -1173,19 +1235,33 @@ int check_batch_device(Snapshot* s, const kg_query* d_q, size_t n, int32_t globa
       // ~30 KiB of LDS per workgroup (variant 0: 8 slots x 512 B visited + 256-entry FIFO per wave;
       // 1: 16 slots x 256 B; 2: 16 slots x 512 B + 512-entry FIFO): 5 (2: 3) workgroups per CU
       const WorkList wl{light, ctl->light8, (uint32_t)n, 1u};
-      // 3: 32 slots x 128 B visited + 192-entry FIFO (~30 KiB, 5 per CU); 4: 32 slots x 256 B (~49 KiB, 3 per CU)
+      // k_stream variants (slots, visited layout, FIFO, chunk); LDS per workgroup sets the WGs per CU:
+      //   0: 8 x 512 B per slot, 256-entry FIFO (~30 KiB, 5/CU)   1: 16 x 256 B (~31 KiB, 5/CU)
+      //   2: 16 x 512 B, 512 FIFO (~46 KiB, 3/CU)                  3: 32 x 128 B, 192 FIFO (~30 KiB, 5/CU)
+      //   4: 32 x 256 B (~49 KiB, 3/CU)
+      //   5: 32 slots sharing one 1024-key table (8 KiB), <= 128 expanded nodes per query (~49 KiB, 3/CU)
+      //   6: the same with <= 256 per query and a 320-entry FIFO (~53 KiB, 3/CU)
       const int sv = s->stream_variant;
-      const uint32_t per_cu = s->stream_wgs ? (uint32_t)s->stream_wgs : ((sv == 2 || sv == 4) ? 3u : 5u);
+      const uint32_t per_cu = s->stream_wgs ? (uint32_t)s->stream_wgs : ((sv == 0 || sv == 1 || sv == 3) ? 5u : 3u);
       const uint32_t ecap = s->stream_ecap ? s->stream_ecap : 0xFFFFFFFFu;
       const uint32_t grid = (uint32_t)std::min<uint64_t>((uint64_t)s->n_cu * per_cu, (n + 31) / 32 + 8);
+      using V0 = SlotVis<8, 7>;
+      using V1 = SlotVis<16, 6>;
+      using V2 = SlotVis<16, 7>;
+      using V3 = SlotVis<32, 5>;
+      using V4 = SlotVis<32, 6>;
+      using V5 = WaveVis<10, 128>;
+      using V6 = WaveVis<10, 256>;
 #define KG_STREAM(Q, V, QC, CH)                                                                                   \
   hipLaunchKernelGGL((k_stream<Q, V, QC, CH>), dim3(grid), dim3(256), 0, stream, s->ds, rq, wl, ctl->heads, d_out, \
                      d_err, ovf_list, ovf_count, ctl, ecap)
-      if (sv == 1) KG_STREAM(16, 6, 256, 32);
-      else if (sv == 2) KG_STREAM(16, 7, 512, 32);
-      else if (sv == 3) KG_STREAM(32, 5, 192, 64);
-      else if (sv == 4) KG_STREAM(32, 6, 256, 64);
-      else KG_STREAM(8, 7, 256, 16);
+      if (sv == 1) KG_STREAM(16, V1, 256, 32);
+      else if (sv == 2) KG_STREAM(16, V2, 512, 32);
+      else if (sv == 3) KG_STREAM(32, V3, 192, 64);
+      else if (sv == 4) KG_STREAM(32, V4, 256, 64);
+      else if (sv == 5) KG_STREAM(32, V5, 256, 64);
+      else if (sv == 6) KG_STREAM(32, V6, 320, 64);
+      else KG_STREAM(8, V0, 256, 16);
 #undef KG_STREAM
     }
     HIPC(hipGetLastError());
@@ -1225,7 +1301,12 @@ int check_batch_device(Snapshot* s, const kg_query* d_q, size_t n, int32_t globa
         fwd_list = giant;
         fwd_count = &ctl->fwd_count;
       }
-      if (int rc = grid_tier(s, rq, fwd_list, fwd_count, global_max_depth, d_out, d_err, stream, &gs)) return rc;
+      // first grid round enqueued without waiting; its readback is checked after the batch's one sync
+      const int rc = grid_tier(s, rq, fwd_list, fwd_count, global_max_depth, d_out, d_err, stream, &gs, 1);
+      if (rc < 0) return rc;
+      grid_pending = rc == 1;
+      grid_list = fwd_list;
+      grid_count = fwd_count;
     }
     if (s->has_program) {
       InterpCtl ic{};
@@ -1239,17 +1320,22 @@ int check_batch_device(Snapshot* s, const kg_query* d_q, size_t n, int32_t globa
       if (launch_general(s, d_q, rq, gen, &ctl->gen_count, &ctl->ic, d_out, d_err, stream)) return -1;
     }
   }
+  // one synchronisation per batch: the grid round's readback and the counters come back together
+  static_assert(sizeof(Ctl) <= 32768, "Ctl readback fits the lower half of the pinned buffer");
+  void* hbuf = s->host_buf(65536);
+  if (!hbuf) return set_error(-1, "pinned host buffer");
   if (stats) {
     HIPC(hipEventRecord(e1, stream));
-    HIPC(hipEventSynchronize(e1));
+    HIPC(hipMemcpyAsync(hbuf, ctl, sizeof(Ctl), hipMemcpyDeviceToHost, stream));
+  }
+  if (stats || grid_pending) HIPC(hipStreamSynchronize(stream));
+  if (grid_pending) {  // a round that overflowed its log reruns here with fewer slots (synchronously)
+    if (int rc = grid_tier(s, rq, grid_list, grid_count, global_max_depth, d_out, d_err, stream, &gs, 2)) return rc;
+  }
+  if (stats) {
     float ms = 0, lms = 0;
     HIPC(hipEventElapsedTime(&ms, e0, e1));
     if (n) HIPC(hipEventElapsedTime(&lms, l0, l1));
-    static_assert(sizeof(Ctl) <= 65536, "Ctl readback fits the pinned buffer");
-    void* hbuf = s->host_buf(sizeof(Ctl));
-    if (!hbuf) return set_error(-1, "pinned host buffer");
-    HIPC(hipMemcpyAsync(hbuf, ctl, sizeof(Ctl), hipMemcpyDeviceToHost, stream));
-    HIPC(hipStreamSynchronize(stream));
     Ctl h;
     memcpy(&h, hbuf, sizeof(Ctl));
     for (int x = 0; x < 8; x++)

@@ -272,10 +272,15 @@ __global__ void k_grid_finish(const uint32_t* slot_q, const uint32_t* slot_hit, 
 
 // Host driver: qlist / count live on the device.  A round is launched without knowing the count
 // (the kernels clamp to it); the host reads the counters once per round, after its last kernel.
+// phase 0: run every round synchronously.  phase 1: enqueue the first round and its readback, return
+// 1 without waiting (the caller synchronises the stream once for the whole batch).  phase 2: resume
+// after that synchronisation: read the first round's result and run further rounds if needed.
 int grid_tier(Snapshot* s, const RQuery* rq, const uint32_t* qlist, const uint32_t* d_count, int global_max_depth,
-              uint8_t* out, uint32_t* err, hipStream_t stream, GridStats* gs) {
-  uint32_t* hb = (uint32_t*)s->host_buf(sizeof(GridCtl) + 64);
-  if (!hb) return set_error(-1, "pinned host buffer");
+              uint8_t* out, uint32_t* err, hipStream_t stream, GridStats* gs, int phase) {
+  static_assert(sizeof(GridCtl) + 64 <= 32768, "grid readback fits the upper half of the pinned buffer");
+  char* pin = (char*)s->host_buf(65536);
+  if (!pin) return set_error(-1, "pinned host buffer");
+  uint32_t* hb = (uint32_t*)(pin + 32768);  // the lower half holds the batch's Ctl readback
   const uint64_t nn = std::max<uint32_t>(s->ds.n_nodes, 1);
   // log capacity >= n_nodes (one slot alone always fits); hash >= 2x the log (load <= 0.5)
   const uint64_t cap = std::max<uint64_t>(nn + 1024, 64ull << 20);
@@ -315,7 +320,9 @@ int grid_tier(Snapshot* s, const RQuery* rq, const uint32_t* qlist, const uint32
   GridCtl* ctl = (GridCtl*)(((uintptr_t)p + 255) & ~uintptr_t(255));
   uint32_t G = G0;
   int64_t count = -1;  // unknown until the first readback
+  bool resume = phase == 2;
   for (uint32_t done = 0; count < 0 || done < (uint64_t)count;) {
+   if (!resume) {
     if (++s->grid_epoch == 0x10000) {  // epoch wrap: the table is zeroed once per 65535 rounds
       HIPC(hipMemsetAsync(H, 0, hcap * 8, stream));
       s->grid_epoch = 1;
@@ -338,10 +345,13 @@ int grid_tier(Snapshot* s, const RQuery* rq, const uint32_t* qlist, const uint32
     hipLaunchKernelGGL(k_grid_finish, dim3(slot_blocks), dim3(256), 0, stream, slot_q, slot_hit, d_count, done, G, out,
                        err, &ctl->overflow);
     HIPC(hipGetLastError());
-    GridCtl h{};
-    HIPC(hipMemcpyAsync(hb, ctl, sizeof h, hipMemcpyDeviceToHost, stream));
+    HIPC(hipMemcpyAsync(hb, ctl, sizeof(GridCtl), hipMemcpyDeviceToHost, stream));
     HIPC(hipMemcpyAsync(hb + sizeof(GridCtl) / 4, d_count, 4, hipMemcpyDeviceToHost, stream));
+    if (phase == 1) return 1;  // first round enqueued; the caller synchronises and resumes
     HIPC(hipStreamSynchronize(stream));
+   }
+    resume = false;
+    GridCtl h{};
     memcpy(&h, hb, sizeof h);
     count = hb[sizeof(GridCtl) / 4];
     const uint32_t cnt = count > done ? (uint32_t)std::min<int64_t>(G, count - done) : 0u;
