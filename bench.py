@@ -5,7 +5,10 @@ Drive-like tuple graph (SURVEY.md 8d, C2/C4 generator; 8 layered group levels, p
 out-degrees, Zipf-ish popularity, seed 20250131) generated directly in HBM, and per GPU a
 1,000,000-check batch of doc#viewer@user queries (50% positive by random walks, 50% uniform,
 max_depth drawn from {0 (global), 1..10}, global max_read_depth 10).  A "step" is one
-kg_check_batch_device call over the whole batch (queries resident in HBM).
+kg_check_batch_device call over the whole batch (queries resident in HBM).  By default two
+batches are in flight per GPU (--inflight): each on its own HIP stream with its own workspace,
+driven by its own host thread, so the low-occupancy tail tiers of one batch (backward and grid
+tiers) overlap the next batch's k_resolve / k_stream.  p99_batch_ms is per call, submit to done.
 
 Multi-GPU: `torch.distributed.run --nproc-per-node N bench.py --gpus N`: each rank builds the
 same snapshot on its GPU and checks its own batch (weak scaling, no data-path collective;
@@ -19,6 +22,7 @@ import ctypes as C
 import json
 import os
 import sys
+import threading
 import time
 
 import numpy as np
@@ -35,8 +39,8 @@ STREAM_KERNELS = {0: "k_stream<8,7,256,16>", 1: "k_stream<16,6,256,32>", 2: "k_s
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--tuples", type=float, default=1e9, help="synthetic graph size (tuples)")
     ap.add_argument("--batch", type=int, default=1_000_000, help="checks per step per GPU")
     ap.add_argument("--global-depth", type=int, default=10)
@@ -48,6 +52,8 @@ def parse():
     ap.add_argument("--grid-wgs", type=int, default=16, help="kg_snapshot_tune grid_wgs (k_grid_level WGs per CU)")
     ap.add_argument("--stream-wgs", type=int, default=0, help="kg_snapshot_tune stream_wgs (k_stream WGs per CU, 0 = auto)")
     ap.add_argument("--back", type=int, default=1, help="kg_snapshot_tune back (backward tier + no-holder filter)")
+    ap.add_argument("--inflight", type=int, default=2,
+                    help="batches in flight per GPU: one HIP stream (own workspace) and one host thread each")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline time budget (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--preset", type=int, default=0,
@@ -221,37 +227,75 @@ def main():
     t_build = time.time() - t_build
 
     B = a.batch
-    dq = torch.empty((B, 7), dtype=torch.int32, device=f"cuda:{local}")
-    _lib.check(L.kg_synth_queries(snap.handle, 1000 + rank, B, dq.data_ptr()), "kg_synth_queries")
-    dout = torch.empty(B, dtype=torch.uint8, device=f"cuda:{local}")
-    derr = torch.empty(B, dtype=torch.int32, device=f"cuda:{local}")
-    stream = torch.cuda.current_stream(local).cuda_stream
+    P = max(1, a.inflight)
+    dev = f"cuda:{local}"
+    # P batches in flight: batch p lives on stream p with its own query / result buffers (distinct
+    # synthetic batches), and one host thread drives each stream (ctypes releases the GIL)
+    streams = [torch.cuda.current_stream(local)] + [torch.cuda.Stream(local) for _ in range(P - 1)]
+    dqs, douts, derrs = [], [], []
+    for p in range(P):
+        q = torch.empty((B, 7), dtype=torch.int32, device=dev)
+        _lib.check(L.kg_synth_queries(snap.handle, 1000 + rank + 7919 * p, B, q.data_ptr()), "kg_synth_queries")
+        dqs.append(q)
+        douts.append(torch.empty(B, dtype=torch.uint8, device=dev))
+        derrs.append(torch.empty(B, dtype=torch.int32, device=dev))
+    dq = dqs[0]
 
-    def step(st=None):
-        rc = L.kg_check_batch_device(snap.handle, dq.data_ptr(), B, a.global_depth, dout.data_ptr(), derr.data_ptr(),
-                                     C.byref(st) if st is not None else None, C.c_void_p(stream))
+    def step(p, st=None):
+        rc = L.kg_check_batch_device(snap.handle, dqs[p].data_ptr(), B, a.global_depth, douts[p].data_ptr(),
+                                     derrs[p].data_ptr(), C.byref(st) if st is not None else None,
+                                     C.c_void_p(streams[p].cuda_stream))
         _lib.check(rc, "kg_check_batch_device")
 
-    for _ in range(a.warmup):
-        step()
+    def run_steps(K, stats=None, lat=None):
+        """Starts P host threads that run K steps round-robin over the P streams once `go` is set."""
+        go = threading.Event()
+        errors = []
+
+        def worker(p):
+            try:
+                go.wait()
+                for k in range(p, K, P):
+                    s0 = time.perf_counter()
+                    step(p, stats[k] if stats is not None else None)  # stats => waits for its batch
+                    if lat is not None:
+                        lat[k] = time.perf_counter() - s0
+                streams[p].synchronize()
+            except Exception as e:  # noqa: BLE001 -- re-raised on the main thread
+                errors.append(e)
+
+        th = [threading.Thread(target=worker, args=(p,)) for p in range(min(P, max(K, 1)))]
+        for t in th:
+            t.start()
+        return go, th, errors
+
+    def finish(th, errors):
+        for t in th:
+            t.join()
+        if errors:
+            raise errors[0]
+
+    warm = max(a.warmup, P)  # every stream's workspace is allocated before the timed region
+    go, th, errs = run_steps(warm)
+    go.set()
+    finish(th, errs)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     stats = [_lib.kg_stats() for _ in range(a.steps)]
-    lat = []
+    lat = [0.0] * a.steps
+    go, th, errs = run_steps(a.steps, stats, lat)
     t0 = time.perf_counter()
-    for k in range(a.steps):
-        s0 = time.perf_counter()
-        step(stats[k])  # stats => the call waits for its batch: per-batch latency
-        lat.append(time.perf_counter() - s0)
+    go.set()
+    finish(th, errs)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    res = dout.cpu().numpy()
-    errs = derr.cpu().numpy()
+    res = torch.cat(douts).cpu().numpy()
+    errs = torch.cat(derrs).cpu().numpy()
     assert (errs == 0).all() and (res <= 1).all(), "unexpected errors in the synthetic batch"
     elapsed, edges = aggregate(dist, elapsed, float(sum(s.edges_read for s in stats)), f"cuda:{local}")
     l_bytes = np.array([8 * s.light_rows_opened + 4 * s.light_edges_read + 16 * s.light_probes for s in stats], float)
@@ -266,7 +310,7 @@ def main():
         "unit": "checks/s",
         "n_gpus": world,
         "steps": a.steps,
-        "warmup": a.warmup,
+        "warmup": warm,
         "ms_per_step": elapsed / a.steps * 1e3,
         "higher_is_better": True,
         "scaling": "weak",
@@ -277,7 +321,8 @@ def main():
                                % ("C2/C4" if a.preset == 0 else "C3 (OPL view/edit/share)", a.tuples, B,
                                   a.global_depth),
                    "tuples": info["rows"], "nodes": info["nodes"], "set_edges": info["set_edges"],
-                   "batch_per_gpu": B, "global_max_read_depth": a.global_depth, "parallelism": f"replica{world}"},
+                   "batch_per_gpu": B, "global_max_read_depth": a.global_depth, "parallelism": f"replica{world}",
+                   "inflight_per_gpu": P},
         "gteps": edges / elapsed / 1e9,
         "p99_batch_ms": float(np.percentile(np.array(lat) * 1e3, 99)),
         "allowed_fraction": float(res.mean()),

@@ -195,7 +195,10 @@ int kg_check_batch(kg_snapshot* s, const kg_query* q, size_t n, int32_t global_m
 /* Device-resident variant: d_q / d_out / d_err are device pointers (HBM), stream is a
  * hipStream_t (NULL = the snapshot's stream).  Returns once the batch is enqueued; when queries
  * reach the grid tier the call waits for the wave tiers (the grid tier's size is read back), and
- * with stats != NULL it waits for the whole batch. */
+ * with stats != NULL it waits for the whole batch.  Every stream gets its own batch workspace
+ * (scratch lists, tier pools, pinned readback), so calls on different streams -- e.g. one host
+ * thread per stream -- keep several batches in flight on the device at once; calls on the same
+ * stream are serialised.  kg_check_batch uses the snapshot's own stream. */
 int kg_check_batch_device(kg_snapshot* s, const kg_query* d_q, size_t n, int32_t global_max_depth,
                           uint8_t* d_out, uint32_t* d_err, kg_stats* stats, void* stream);
 /* Device-side synthetic check batch for a synthetic snapshot: 50% positive (reverse walks) and

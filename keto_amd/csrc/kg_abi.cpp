@@ -267,9 +267,10 @@ int kg_check_batch_device(kg_snapshot* sp, const kg_query* d_q, size_t n, int32_
   KG_GUARD_BEGIN
   if (!sp) return set_error(-2, "NULL snapshot");
   Snapshot* s = reinterpret_cast<Snapshot*>(sp);
-  std::lock_guard<std::mutex> lk(s->mu);
   if (s->shard_n > 1) return set_error(-2, "sharded snapshot: checks run through kg_shard_seed / kg_shard_level");
-  return kg::check_batch_device(s, d_q, n, global_max_depth, d_out, d_err, stats, (hipStream_t)stream);
+  kg::Workspace* w = s->workspace((hipStream_t)stream);  // one per stream: batches on other streams overlap
+  std::lock_guard<std::mutex> lk(w->mu);
+  return kg::check_batch_device(s, w, d_q, n, global_max_depth, d_out, d_err, stats);
   KG_GUARD_END
 }
 
@@ -279,8 +280,9 @@ int kg_check_batch(kg_snapshot* sp, const kg_query* q, size_t n, int32_t global_
   if (!sp) return set_error(-2, "NULL snapshot");
   if (n && (!q || !out)) return set_error(-2, "NULL buffer");
   Snapshot* s = reinterpret_cast<Snapshot*>(sp);
-  std::lock_guard<std::mutex> lk(s->mu);
   if (s->shard_n > 1) return set_error(-2, "sharded snapshot: checks run through kg_shard_seed / kg_shard_level");
+  kg::Workspace* w = s->workspace(nullptr);
+  std::lock_guard<std::mutex> lk(w->mu);
   HIPC(hipSetDevice(s->device));
   if (n == 0) {
     if (stats) memset(stats, 0, sizeof *stats);
@@ -295,7 +297,7 @@ int kg_check_batch(kg_snapshot* sp, const kg_query* q, size_t n, int32_t global_
   int rc = 0;
   if (hipMemcpyAsync(d_q, q, n * sizeof(kg_query), hipMemcpyHostToDevice, s->stream) != hipSuccess)
     rc = set_error(-1, "H2D copy failed");
-  if (!rc) rc = kg::check_batch_device(s, d_q, n, global_max_depth, d_out, d_err, stats, s->stream);
+  if (!rc) rc = kg::check_batch_device(s, w, d_q, n, global_max_depth, d_out, d_err, stats);
   if (!rc && hipMemcpyAsync(out, d_out, n, hipMemcpyDeviceToHost, s->stream) != hipSuccess)
     rc = set_error(-1, "D2H copy failed");
   if (!rc && err_code && hipMemcpyAsync(err_code, d_err, n * 4, hipMemcpyDeviceToHost, s->stream) != hipSuccess)

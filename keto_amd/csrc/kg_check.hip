@@ -1149,12 +1149,12 @@ int synth_queries(Snapshot* s, uint64_t seed, size_t n, kg_query* d_q) {
 // ------------------------------------------------------------------ batch driver
 static size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 
-int check_batch_device(Snapshot* s, const kg_query* d_q, size_t n, int32_t global_max_depth, uint8_t* d_out,
-                       uint32_t* d_err, kg_stats* stats, hipStream_t stream) {
+int check_batch_device(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n, int32_t global_max_depth,
+                       uint8_t* d_out, uint32_t* d_err, kg_stats* stats) {
   if (global_max_depth < 1) global_max_depth = 5;  // config.schema.json:308-315 default
   if (n > 0x7FFFFFFFull) return set_error(-2, "batch too large");
   HIPC(hipSetDevice(s->device));
-  if (!stream) stream = s->stream;
+  hipStream_t stream = w->stream;
   // scratch: rq[n] | light[8n] (8 shards) | light2[n] | gen[n] | medium[n] | heavy[n] | giant[n] | p2[n] |
   //          back2[n] | Ctl
   size_t off_rq = 0, off_light = align_up(off_rq + n * sizeof(RQuery)), off_light2 = align_up(off_light + 8 * n * 4),
@@ -1163,14 +1163,14 @@ int check_batch_device(Snapshot* s, const kg_query* d_q, size_t n, int32_t globa
          off_giant = align_up(off_heavy + n * 4), off_p2 = align_up(off_giant + n * 4),
          off_back2 = align_up(off_p2 + n * 4), off_ctl = align_up(off_back2 + n * 4),
          total = align_up(off_ctl + sizeof(Ctl));
-  if (total > s->scratch_bytes) {
-    if (s->scratch) hipFree(s->scratch);
-    s->scratch = nullptr;
-    s->scratch_bytes = 0;
-    HIPC(hipMalloc(&s->scratch, total));
-    s->scratch_bytes = total;
+  if (total > w->scratch_bytes) {
+    if (w->scratch) hipFree(w->scratch);
+    w->scratch = nullptr;
+    w->scratch_bytes = 0;
+    HIPC(hipMalloc(&w->scratch, total));
+    w->scratch_bytes = total;
   }
-  char* base = (char*)s->scratch;
+  char* base = (char*)w->scratch;
   RQuery* rq = (RQuery*)(base + off_rq);
   uint32_t* light = (uint32_t*)(base + off_light);
   uint32_t* light2 = (uint32_t*)(base + off_light2);
@@ -1192,15 +1192,15 @@ int check_batch_device(Snapshot* s, const kg_query* d_q, size_t n, int32_t globa
     H = (uint32_t)std::min<uint64_t>(2 * (uint64_t)s->n_cu,
                                      std::max<uint64_t>(1, (8ull << 30) / ((words + cap_h) * 4)));
     const size_t pool = ((size_t)H * (words + cap_h) + (words + nn)) * 4;
-    if (pool > s->heavy_pool_bytes) {
-      if (s->heavy_pool) hipFree(s->heavy_pool);
-      s->heavy_pool = nullptr;
-      s->heavy_pool_bytes = 0;
-      HIPC(hipMalloc(&s->heavy_pool, pool));
-      HIPC(hipMemsetAsync(s->heavy_pool, 0, pool, stream));  // bitmaps start clear and are left clear
-      s->heavy_pool_bytes = pool;
+    if (pool > w->heavy_pool_bytes) {
+      if (w->heavy_pool) hipFree(w->heavy_pool);
+      w->heavy_pool = nullptr;
+      w->heavy_pool_bytes = 0;
+      HIPC(hipMalloc(&w->heavy_pool, pool));
+      HIPC(hipMemsetAsync(w->heavy_pool, 0, pool, stream));  // bitmaps start clear and are left clear
+      w->heavy_pool_bytes = pool;
     }
-    hb = (uint32_t*)s->heavy_pool;
+    hb = (uint32_t*)w->heavy_pool;
     hl = hb + (size_t)H * words;
     gb = hl + (size_t)H * cap_h;
     gl = gb + words;
@@ -1209,9 +1209,9 @@ int check_batch_device(Snapshot* s, const kg_query* d_q, size_t n, int32_t globa
   bool grid_pending = false;
   const uint32_t *grid_list = nullptr, *grid_count = nullptr;
 
-  if (stats && !s->ev[0])
-    for (auto& e : s->ev) HIPC(hipEventCreate(&e));
-  hipEvent_t e0 = s->ev[0], e1 = s->ev[1], l0 = s->ev[2], l1 = s->ev[3];
+  if (stats && !w->ev[0])
+    for (auto& e : w->ev) HIPC(hipEventCreate(&e));
+  hipEvent_t e0 = w->ev[0], e1 = w->ev[1], l0 = w->ev[2], l1 = w->ev[3];
   if (stats) HIPC(hipEventRecord(e0, stream));
   HIPC(hipMemsetAsync(ctl, 0, sizeof(Ctl), stream));
   if (n) {
@@ -1302,7 +1302,7 @@ int check_batch_device(Snapshot* s, const kg_query* d_q, size_t n, int32_t globa
         fwd_count = &ctl->fwd_count;
       }
       // first grid round enqueued without waiting; its readback is checked after the batch's one sync
-      const int rc = grid_tier(s, rq, fwd_list, fwd_count, global_max_depth, d_out, d_err, stream, &gs, 1);
+      const int rc = grid_tier(s, w, rq, fwd_list, fwd_count, global_max_depth, d_out, d_err, stream, &gs, 1);
       if (rc < 0) return rc;
       grid_pending = rc == 1;
       grid_list = fwd_list;
@@ -1317,12 +1317,12 @@ int check_batch_device(Snapshot* s, const kg_query* d_q, size_t n, int32_t globa
       ic.st_edges = &ctl->st[ST_EDGES];
       ic.st_probes = &ctl->st[ST_PROBES];
       HIPC(hipMemcpyAsync(&ctl->ic, &ic, sizeof ic, hipMemcpyHostToDevice, stream));
-      if (launch_general(s, d_q, rq, gen, &ctl->gen_count, &ctl->ic, d_out, d_err, stream)) return -1;
+      if (launch_general(s, w, d_q, rq, gen, &ctl->gen_count, &ctl->ic, d_out, d_err, stream)) return -1;
     }
   }
   // one synchronisation per batch: the grid round's readback and the counters come back together
   static_assert(sizeof(Ctl) <= 32768, "Ctl readback fits the lower half of the pinned buffer");
-  void* hbuf = s->host_buf(65536);
+  void* hbuf = w->host_buf(65536);
   if (!hbuf) return set_error(-1, "pinned host buffer");
   if (stats) {
     HIPC(hipEventRecord(e1, stream));
@@ -1330,7 +1330,7 @@ int check_batch_device(Snapshot* s, const kg_query* d_q, size_t n, int32_t globa
   }
   if (stats || grid_pending) HIPC(hipStreamSynchronize(stream));
   if (grid_pending) {  // a round that overflowed its log reruns here with fewer slots (synchronously)
-    if (int rc = grid_tier(s, rq, grid_list, grid_count, global_max_depth, d_out, d_err, stream, &gs, 2)) return rc;
+    if (int rc = grid_tier(s, w, rq, grid_list, grid_count, global_max_depth, d_out, d_err, stream, &gs, 2)) return rc;
   }
   if (stats) {
     float ms = 0, lms = 0;

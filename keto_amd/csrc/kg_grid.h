@@ -11,7 +11,8 @@ struct GridStats {
 };
 
 struct Snapshot;
-int grid_tier(Snapshot* s, const RQuery* rq, const uint32_t* qlist, const uint32_t* d_count, int global_max_depth,
+struct Workspace;
+int grid_tier(Snapshot* s, Workspace* w, const RQuery* rq, const uint32_t* qlist, const uint32_t* d_count, int global_max_depth,
               uint8_t* out, uint32_t* err, hipStream_t stream, GridStats* gs, int phase = 0);
 
 }  // namespace kg

@@ -275,10 +275,10 @@ __global__ void k_grid_finish(const uint32_t* slot_q, const uint32_t* slot_hit, 
 // phase 0: run every round synchronously.  phase 1: enqueue the first round and its readback, return
 // 1 without waiting (the caller synchronises the stream once for the whole batch).  phase 2: resume
 // after that synchronisation: read the first round's result and run further rounds if needed.
-int grid_tier(Snapshot* s, const RQuery* rq, const uint32_t* qlist, const uint32_t* d_count, int global_max_depth,
+int grid_tier(Snapshot* s, Workspace* w, const RQuery* rq, const uint32_t* qlist, const uint32_t* d_count, int global_max_depth,
               uint8_t* out, uint32_t* err, hipStream_t stream, GridStats* gs, int phase) {
   static_assert(sizeof(GridCtl) + 64 <= 32768, "grid readback fits the upper half of the pinned buffer");
-  char* pin = (char*)s->host_buf(65536);
+  char* pin = (char*)w->host_buf(65536);
   if (!pin) return set_error(-1, "pinned host buffer");
   uint32_t* hb = (uint32_t*)(pin + 32768);  // the lower half holds the batch's Ctl readback
   const uint64_t nn = std::max<uint32_t>(s->ds.n_nodes, 1);
@@ -288,16 +288,16 @@ int grid_tier(Snapshot* s, const RQuery* rq, const uint32_t* qlist, const uint32
   while (hcap < 2 * cap) hcap <<= 1;
   const uint32_t G0 = 0xFFFF;  // slot field is 16 bits
   const size_t need = hcap * 8 + cap * (4 + 4 + 8) + 2 * TILE_CAP * 4 + (size_t)G0 * 16 + sizeof(GridCtl) + 4096;
-  if (need > s->grid_pool_bytes) {
-    if (s->grid_pool) HIPC(hipFree(s->grid_pool));
-    s->grid_pool = nullptr;
-    s->grid_pool_bytes = 0;
-    HIPC(hipMalloc(&s->grid_pool, need));
-    HIPC(hipMemsetAsync(s->grid_pool, 0, hcap * 8, stream));  // epoch 0 = empty
-    s->grid_pool_bytes = need;
-    s->grid_epoch = 0;
+  if (need > w->grid_pool_bytes) {
+    if (w->grid_pool) HIPC(hipFree(w->grid_pool));
+    w->grid_pool = nullptr;
+    w->grid_pool_bytes = 0;
+    HIPC(hipMalloc(&w->grid_pool, need));
+    HIPC(hipMemsetAsync(w->grid_pool, 0, hcap * 8, stream));  // epoch 0 = empty
+    w->grid_pool_bytes = need;
+    w->grid_epoch = 0;
   }
-  char* p = (char*)s->grid_pool;
+  char* p = (char*)w->grid_pool;
   uint64_t* H = (uint64_t*)p;
   p += hcap * 8;
   GridLog lg;
@@ -323,11 +323,11 @@ int grid_tier(Snapshot* s, const RQuery* rq, const uint32_t* qlist, const uint32
   bool resume = phase == 2;
   for (uint32_t done = 0; count < 0 || done < (uint64_t)count;) {
    if (!resume) {
-    if (++s->grid_epoch == 0x10000) {  // epoch wrap: the table is zeroed once per 65535 rounds
+    if (++w->grid_epoch == 0x10000) {  // epoch wrap: the table is zeroed once per 65535 rounds
       HIPC(hipMemsetAsync(H, 0, hcap * 8, stream));
-      s->grid_epoch = 1;
+      w->grid_epoch = 1;
     }
-    const uint64_t epoch = s->grid_epoch;
+    const uint64_t epoch = w->grid_epoch;
     const uint32_t slot_blocks = (G + 255) / 256;
     HIPC(hipMemsetAsync(ctl, 0, sizeof(GridCtl), stream));
     hipLaunchKernelGGL(k_grid_init, dim3(slot_blocks), dim3(256), 0, stream, s->ds, rq, qlist, d_count, done, G, lg,

@@ -30,7 +30,8 @@ struct InterpCtl {
 };
 
 struct Snapshot;
-int launch_general(Snapshot* s, const kg_query* d_q, const RQuery* rq, const uint32_t* gen_list,
+struct Workspace;
+int launch_general(Snapshot* s, Workspace* w, const kg_query* d_q, const RQuery* rq, const uint32_t* gen_list,
                    const uint32_t* gen_count, InterpCtl* ic, uint8_t* out, uint32_t* err, hipStream_t stream);
 
 }  // namespace kg

@@ -541,7 +541,7 @@ __global__ __launch_bounds__(64) void k_interp_hbm(DevSnap s, const kg_query* __
   }
 }
 
-int launch_general(Snapshot* s, const kg_query* d_q, const RQuery* rq, const uint32_t* gen_list,
+int launch_general(Snapshot* s, Workspace* w, const kg_query* d_q, const RQuery* rq, const uint32_t* gen_list,
                    const uint32_t* gen_count, InterpCtl* ic, uint8_t* out, uint32_t* err, hipStream_t stream) {
   if (!s->has_program) return 0;  // without rewrites nothing is ever routed GENERAL
   const uint32_t grid1 = (uint32_t)s->n_cu * 2;
@@ -552,15 +552,15 @@ int launch_general(Snapshot* s, const kg_query* d_q, const RQuery* rq, const uin
       1, std::min<uint64_t>(64, (4ull << 30) / ((words + nn) * 4 + STACK_CAP * sizeof(Frame) + MEMO_CAP * sizeof(MemoEnt))));
   const size_t slot_bytes = STACK_CAP * sizeof(Frame) + MEMO_CAP * sizeof(MemoEnt);
   const size_t need = (size_t)slots1 * slot_bytes + (size_t)slots2 * ((words + nn) * 4 + slot_bytes);
-  if (need > s->interp_pool_bytes) {
-    if (s->interp_pool) hipFree(s->interp_pool);
-    s->interp_pool = nullptr;
-    s->interp_pool_bytes = 0;
-    HIPC(hipMalloc(&s->interp_pool, need));
-    HIPC(hipMemsetAsync(s->interp_pool, 0, need, stream));  // memo tags 0 = empty; bitmaps clear
-    s->interp_pool_bytes = need;
+  if (need > w->interp_pool_bytes) {
+    if (w->interp_pool) hipFree(w->interp_pool);
+    w->interp_pool = nullptr;
+    w->interp_pool_bytes = 0;
+    HIPC(hipMalloc(&w->interp_pool, need));
+    HIPC(hipMemsetAsync(w->interp_pool, 0, need, stream));  // memo tags 0 = empty; bitmaps clear
+    w->interp_pool_bytes = need;
   }
-  char* p = (char*)s->interp_pool;
+  char* p = (char*)w->interp_pool;
   Frame* stacks1 = (Frame*)p;
   MemoEnt* memos1 = (MemoEnt*)(p + (size_t)slots1 * STACK_CAP * sizeof(Frame));
   char* p2 = p + (size_t)slots1 * slot_bytes;

@@ -24,11 +24,34 @@ void clear_error();
                                                  __FILE__, __LINE__);                            \
   } while (0)
 
+// Everything one in-flight check batch mutates: scratch lists, tier pools, the grid tier's epoch,
+// timing events and the pinned readback buffer.  One per HIP stream, so batches on different
+// streams overlap on the device (the tail tiers of one batch run beside the next batch's
+// k_resolve / k_stream); batches on the same stream are serialised by `mu`.
+struct Workspace {
+  int device = -1;
+  hipStream_t stream = nullptr;
+  std::mutex mu;
+  void* scratch = nullptr;
+  size_t scratch_bytes = 0;
+  void* heavy_pool = nullptr;
+  size_t heavy_pool_bytes = 0;
+  void* grid_pool = nullptr;  // grid tier: visited hash | log | slots | ctl | scan sums
+  size_t grid_pool_bytes = 0;
+  uint32_t grid_epoch = 0;
+  void* interp_pool = nullptr;
+  size_t interp_pool_bytes = 0;
+  hipEvent_t ev[4] = {};  // batch timing events (created on first use)
+  void* pinned = nullptr;  // 64 KiB of pinned host memory for small device->host readbacks
+  void* host_buf(size_t bytes);
+  ~Workspace();
+};
+
 struct Snapshot {
   int device = -1;
   int n_cu = 256;
   hipStream_t stream = nullptr;
-  std::mutex mu;  // one batch at a time per snapshot (one stream)
+  std::mutex mu;  // expand / hash-sharded calls and tuning (they run on the snapshot's own stream)
   DevSnap ds{};
   uint32_t wildcard_rel = NONE;
   bool has_program = false;
@@ -43,22 +66,13 @@ struct Snapshot {
   std::vector<int32_t> h_relroot;
   std::vector<RwNode> h_rw;
   std::vector<int32_t> h_rwchild;
-  // per-batch scratch (grown on demand, owned by the snapshot)
-  void* scratch = nullptr;
-  size_t scratch_bytes = 0;
-  void* heavy_pool = nullptr;
-  size_t heavy_pool_bytes = 0;
-  void* grid_pool = nullptr;  // grid tier: visited hash | log | slots | ctl | scan sums
-  size_t grid_pool_bytes = 0;
-  uint32_t grid_epoch = 0;
-  hipEvent_t ev[4] = {};  // batch timing events (created on first use)
-  void* pinned = nullptr;  // 64 KiB of pinned host memory for small device->host readbacks
+  // per-stream batch workspaces (check batches on different streams run concurrently)
+  std::mutex ws_mu;
+  std::vector<Workspace*> wss;
+  Workspace* workspace(hipStream_t st);  // finds or creates the workspace of stream st (NULL = stream)
   int wide_tier = 0;       // kg_snapshot_tune("wide"): 1 = k_light<64> between k_stream and the rest
-  void* host_buf(size_t bytes);
   int tiers = 0;       // kg_snapshot_tune("tiers")
   int light_tier = 0;  // kg_snapshot_tune("light"): 0 k_stream, 1 k_light<16>  // grid tier visited-table epoch (kg_grid.hip)
-  void* interp_pool = nullptr;
-  size_t interp_pool_bytes = 0;
   uint64_t batch_seq = 0;
   uint32_t shard_rank = 0, shard_n = 1;  // hash-sharded mode (set before create)
   void* shard_vis = nullptr;             // kg_shard.hip: per-batch visited table of (query, node)
@@ -83,8 +97,8 @@ struct Snapshot {
 };
 
 // kg_check.hip
-int check_batch_device(Snapshot* s, const kg_query* d_q, size_t n, int32_t global_max_depth, uint8_t* d_out,
-                       uint32_t* d_err, kg_stats* stats, hipStream_t stream);
+int check_batch_device(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n, int32_t global_max_depth,
+                       uint8_t* d_out, uint32_t* d_err, kg_stats* stats);
 int synth_queries(Snapshot* s, uint64_t seed, size_t n, kg_query* d_q);
 // kg_shard.hip
 int shard_seed(Snapshot* s, const kg_query* d_q, size_t n, int32_t gdepth, kg_frec* d_out, size_t cap,

@@ -207,21 +207,38 @@ static uint64_t pow2_at_least(uint64_t x) {
 Snapshot::~Snapshot() {
   if (device >= 0) hipSetDevice(device);
   for (void* p : allocs) hipFree(p);
-  if (scratch) hipFree(scratch);
-  if (heavy_pool) hipFree(heavy_pool);
-  if (grid_pool) hipFree(grid_pool);
-  if (pinned) hipHostFree(pinned);
-  for (auto& e : ev)
-    if (e) hipEventDestroy(e);
-  if (interp_pool) hipFree(interp_pool);
+  for (Workspace* w : wss) delete w;
   if (shard_vis) hipFree(shard_vis);
   if (stream) hipStreamDestroy(stream);
 }
 
-void* Snapshot::host_buf(size_t bytes) {
+Workspace::~Workspace() {
+  if (device >= 0) hipSetDevice(device);
+  if (scratch) hipFree(scratch);
+  if (heavy_pool) hipFree(heavy_pool);
+  if (grid_pool) hipFree(grid_pool);
+  if (interp_pool) hipFree(interp_pool);
+  if (pinned) hipHostFree(pinned);
+  for (auto& e : ev)
+    if (e) hipEventDestroy(e);
+}
+
+void* Workspace::host_buf(size_t bytes) {
   if (bytes > 65536) return nullptr;
   if (!pinned && hipHostMalloc(&pinned, 65536, hipHostMallocDefault) != hipSuccess) pinned = nullptr;
   return pinned;
+}
+
+Workspace* Snapshot::workspace(hipStream_t st) {
+  if (!st) st = stream;
+  std::lock_guard<std::mutex> lk(ws_mu);
+  for (Workspace* w : wss)
+    if (w->stream == st) return w;
+  Workspace* w = new Workspace();
+  w->device = device;
+  w->stream = st;
+  wss.push_back(w);
+  return w;
 }
 
 int Snapshot::alloc(void** p, size_t bytes) {

@@ -180,6 +180,55 @@ def test_synthetic_graph_vs_oracle(n_tuples, gmax):
     assert (dfs == exp).all()
 
 
+def test_concurrent_streams_match_serial():
+    """kg_check_batch_device on several streams at once (one workspace per stream, one host thread
+    per stream, the way bench.py keeps batches in flight) gives exactly the serial answers."""
+    import threading
+    torch = _torch()
+    from keto_amd import _lib
+    import ctypes as C
+    L = _lib.load()
+    snap = Snapshot.synthetic(300_000, seed=20250131)
+    n, P, gmax = 30000, 3, 10
+    streams = [torch.cuda.Stream() for _ in range(P)]
+    dqs = []
+    for p in range(P):
+        q = torch.empty((n, 7), dtype=torch.int32, device="cuda")
+        _lib.check(L.kg_synth_queries(snap.handle, 100 + p, n, q.data_ptr()), "kg_synth_queries")
+        dqs.append(q)
+    e = Engine(snap, Config(gmax))
+    serial = [e.batch_check_ids(q.cpu().numpy().view(np.uint32))[0] for q in dqs]
+    outs = [[torch.full((n,), 7, dtype=torch.uint8, device="cuda") for _ in range(4)] for _ in range(P)]
+    errs = [torch.full((n,), 99, dtype=torch.int32, device="cuda") for _ in range(P)]
+    torch.cuda.synchronize()
+    failures = []
+
+    def worker(p):
+        try:
+            for r in range(4):
+                _lib.check(L.kg_check_batch_device(snap.handle, dqs[p].data_ptr(), n, gmax, outs[p][r].data_ptr(),
+                                                   errs[p].data_ptr(), None, C.c_void_p(streams[p].cuda_stream)),
+                           "kg_check_batch_device")
+            streams[p].synchronize()
+        except Exception as x:  # noqa: BLE001
+            failures.append(x)
+
+    th = [threading.Thread(target=worker, args=(p,)) for p in range(P)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not failures, failures
+    for p in range(P):
+        assert (errs[p].cpu().numpy() == 0).all()
+        for r in range(4):
+            assert (outs[p][r].cpu().numpy() == serial[p]).all(), (p, r)
+    q0 = dqs[0].cpu().numpy().view(np.uint32)
+    exp, _, _ = Oracle(snap.export(), 0).check_batch(q0[:, :6], q0[:, 6].view(np.int32), gmax, POLICY_CANONICAL,
+                                                      nthreads=8)
+    assert (serial[0] == exp).all()
+
+
 # ---------------------------------------------------------------- rewrites (interpreter path)
 from keto_amd.namespace import (ComputedSubjectSet, InvertResult, Namespace, Relation,  # noqa: E402
                                 SubjectSetRewrite, TupleToSubjectSet)
