@@ -5,7 +5,7 @@ Drive-like tuple graph (SURVEY.md 8d, C2/C4 generator; 8 layered group levels, p
 out-degrees, Zipf-ish popularity, seed 20250131) generated directly in HBM, and per GPU a
 1,000,000-check batch of doc#viewer@user queries (50% positive by random walks, 50% uniform,
 max_depth drawn from {0 (global), 1..10}, global max_read_depth 10).  A "step" is one
-kg_check_batch_device call over the whole batch (queries resident in HBM).  By default two
+kg_check_batch_device call over the whole batch (queries resident in HBM).  By default four
 batches are in flight per GPU (--inflight): each on its own HIP stream with its own workspace,
 driven by its own host thread, so the low-occupancy tail tiers of one batch (backward and grid
 tiers) overlap the next batch's k_resolve / k_stream.  p99_batch_ms is per call, submit to done.
@@ -52,7 +52,7 @@ def parse():
     ap.add_argument("--grid-wgs", type=int, default=16, help="kg_snapshot_tune grid_wgs (k_grid_level WGs per CU)")
     ap.add_argument("--stream-wgs", type=int, default=0, help="kg_snapshot_tune stream_wgs (k_stream WGs per CU, 0 = auto)")
     ap.add_argument("--back", type=int, default=1, help="kg_snapshot_tune back (backward tier + no-holder filter)")
-    ap.add_argument("--inflight", type=int, default=2,
+    ap.add_argument("--inflight", type=int, default=4,
                     help="batches in flight per GPU: one HIP stream (own workspace) and one host thread each")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline time budget (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=16)

@@ -15,6 +15,7 @@
 //                                        through set-adjacency (needs the rewrite interpreter).
 //   radj_off[n_nodes+1] u64 / radj[] u32  reverse set-adjacency (parents), for the backward tier.
 //   hold[] u32 + subject hash             holders: the nodes whose row contains a given subject,
+//   hbits[] u32                           holder bitmap over subject ids (k_resolve's no-holder test)
 //                                        grouped by subject (the backward tier's level 0).
 #pragma once
 #include <stdint.h>
@@ -124,6 +125,8 @@ struct DevSnap {
   const uint32_t* hold;      // holder nodes (rows containing a subject), grouped by subject
   const HSlot* hslots;       // subject hash: tagged subject -> (first index into hold, count)
   uint64_t hmask;            // n_slots - 1
+  const uint32_t* hbits;     // holder bitmap over subject ids: bit s set <=> some row holds subject id s
+  uint32_t hbits_n;          // bits in hbits (max held subject id + 1); nullptr / 0: not built
   // hash-sharded mode: this snapshot holds the rows of the nodes with shard_owner == shard_rank
   uint32_t shard_rank, shard_n;
   const uint8_t* nowner;  // [n_nodes] owner rank of every node (shard_n > 1)

@@ -115,6 +115,19 @@ __global__ void k_count_runs(const uint32_t* key, uint64_t n, unsigned long long
   for (int off = 32; off; off >>= 1) c += __shfl_xor(c, off, 64);
   if ((threadIdx.x & 63) == 0 && c) atomicAdd(cnt, (unsigned long long)c);
 }
+// Largest subject id (untagged key) of the sorted holder keys: the one key < SET_BIT whose
+// successor is a tagged key or the end.
+__global__ void k_hold_maxid(const uint32_t* key, uint64_t n, uint32_t* out) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    if (key[i] < SET_BIT && (i + 1 == n || key[i + 1] >= SET_BIT)) *out = key[i] + 1;
+}
+// Holder bitmap: one bit per subject id that some row holds (run starts of the sorted keys).
+__global__ void k_hold_bits(const uint32_t* key, uint64_t n, uint32_t* bits) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t k = key[i];
+    if (k < SET_BIT && (i == 0 || k != key[i - 1])) atomicOr(&bits[k >> 5], 1u << (k & 31));
+  }
+}
 __device__ __forceinline__ uint64_t hold_slot(uint32_t key, uint64_t mask) { return mix64(key) & mask; }
 // run starts insert (subject -> first index); run ends then add the count
 __global__ void k_hold_insert(const uint32_t* key, uint64_t n, HSlot* hs, uint64_t mask) {
@@ -323,6 +336,8 @@ int Snapshot::build_reverse() {
   const uint32_t nn = ds.n_nodes;
   const uint64_t E = n_set_edges, R = h_row_off_last;
   ds.radj = nullptr;
+  ds.hbits = nullptr;
+  ds.hbits_n = 0;
   if (R >= 0xFFFFFFFFull || nn == 0) return 0;
   uint64_t* roff = nullptr;
   uint32_t* radj = nullptr;
@@ -359,12 +374,25 @@ int Snapshot::build_reverse() {
   HIPC(hipMalloc(&tmp, tmp_bytes + 16));
   HIPC(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, kb, vb, (size_t)R, 0, 32, stream));
   unsigned long long* cnt;
-  HIPC(hipMalloc(&cnt, 8));
-  HIPC(hipMemsetAsync(cnt, 0, 8, stream));
-  if (R) hipLaunchKernelGGL(k_count_runs, dim3(4096), dim3(256), 0, stream, kb.Current(), R, cnt);
-  unsigned long long distinct = 0;
-  HIPC(hipMemcpyAsync(&distinct, cnt, 8, hipMemcpyDeviceToHost, stream));
+  HIPC(hipMalloc(&cnt, 16));
+  HIPC(hipMemsetAsync(cnt, 0, 16, stream));
+  if (R) {
+    hipLaunchKernelGGL(k_count_runs, dim3(4096), dim3(256), 0, stream, kb.Current(), R, cnt);
+    hipLaunchKernelGGL(k_hold_maxid, dim3(4096), dim3(256), 0, stream, kb.Current(), R, (uint32_t*)(cnt + 1));
+  }
+  unsigned long long hcnt[2] = {0, 0};
+  HIPC(hipMemcpyAsync(hcnt, cnt, 16, hipMemcpyDeviceToHost, stream));
   HIPC(hipStreamSynchronize(stream));
+  const unsigned long long distinct = hcnt[0];
+  const uint32_t nbits = (uint32_t)hcnt[1];  // max held subject id + 1 (0: no subject ids)
+  uint32_t* hbits = nullptr;
+  if (nbits) {
+    const size_t words = ((size_t)nbits + 31) / 32;
+    if (alloc((void**)&hbits, words * 4)) return -1;
+    HIPC(hipMemsetAsync(hbits, 0, words * 4, stream));
+    hipLaunchKernelGGL(k_hold_bits, dim3(4096), dim3(256), 0, stream, kb.Current(), R, hbits);
+    HIPC(hipGetLastError());
+  }
   const uint64_t slots = pow2_at_least(std::max<uint64_t>(16, distinct * 2));
   uint32_t* hold;
   HSlot* hs;
@@ -383,6 +411,8 @@ int Snapshot::build_reverse() {
   ds.hold = hold;
   ds.hslots = hs;
   ds.hmask = slots - 1;
+  ds.hbits = hbits;
+  ds.hbits_n = nbits;
   return 0;
 }
 
