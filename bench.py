@@ -50,7 +50,8 @@ def parse():
     ap.add_argument("--stream", type=int, default=5, help="kg_snapshot_tune stream (k_stream variant 0..6)")
     ap.add_argument("--stream-ecap", type=int, default=0, help="kg_snapshot_tune stream_ecap (edges per query, 0 = none)")
     ap.add_argument("--grid-wgs", type=int, default=16, help="kg_snapshot_tune grid_wgs (k_grid_level WGs per CU)")
-    ap.add_argument("--stream-wgs", type=int, default=0, help="kg_snapshot_tune stream_wgs (k_stream WGs per CU, 0 = auto)")
+    ap.add_argument("--stream-wgs", type=int, default=2,
+                    help="kg_snapshot_tune stream_wgs (k_stream WGs per CU, 0 = auto; 2 leaves room for the other in-flight batches)")
     ap.add_argument("--back", type=int, default=1, help="kg_snapshot_tune back (backward tier + no-holder filter)")
     ap.add_argument("--inflight", type=int, default=4,
                     help="batches in flight per GPU: one HIP stream (own workspace) and one host thread each")

@@ -123,7 +123,7 @@ __global__ __launch_bounds__(256) void k_resolve(DevSnap s, const kg_query* __re
     else if (want_h) h0 = s.hslots[hi];
     NSlot n0{};
     if (key_ok) n0 = s.nmap[ni];
-    uint32_t node = NONE, rb = 0, rl = 0;
+    uint32_t node = NONE, rb = 0, rl = 0, rsig = 0xFFFFFFFFu;
     if (key_ok) {
       const NSlot* sl = n0.key == key ? &n0 : (n0.key == EMPTY64 ? nullptr : nmap_slot(s, key, (ni + 1) & s.nmap_mask));
       if (sl) {
@@ -131,6 +131,7 @@ __global__ __launch_bounds__(256) void k_resolve(DevSnap s, const kg_query* __re
         node = v.node;
         rb = v.beg;
         rl = v.len;
+        rsig = v.sig;
       }
     }
     if (!sid) {
@@ -147,11 +148,12 @@ __global__ __launch_bounds__(256) void k_resolve(DevSnap s, const kg_query* __re
       route = impure ? ROUTE_GENERAL : ROUTE_LIGHT;
     }
     bool member = false;
-    did_probe = route == ROUTE_LIGHT;
     if (route == ROUTE_LIGHT) {
       // the root's checkDirect(D-1) (D >= 1 always) is thread-parallel here: a direct tuple or a
-      // depth that cannot reach any child (D < 2) finishes the query before the wave tier
-      member = dset_probe(s, node, subj);
+      // depth that cannot reach any child (D < 2) finishes the query before the wave tier.  The
+      // row signature in the node-map slot rules out most misses without touching dset.
+      did_probe = subj != NONE && sig_maybe(rsig, subj_sig(subj));
+      member = did_probe && dset_probe(s, node, subj);
       if (member || d < 2 || rl == 0) route = ROUTE_DONE;
       // a subject that no row holds cannot be reached from any root (checkDirect never hits)
       if (route == ROUTE_LIGHT && no_holder_filter) {

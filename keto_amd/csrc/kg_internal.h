@@ -86,7 +86,8 @@ __host__ __device__ __forceinline__ bool sig_maybe(uint32_t sig, uint32_t subj_m
 // request mapping is one random line.  key == EMPTY64: free.
 struct NSlot {
   uint64_t key;
-  uint32_t node, beg, len, pad0;
+  uint32_t node, beg, len;
+  uint32_t sig;  // Bloom signature of the node's row subjects (as AdjX.sig): k_resolve's root probe filter
   uint64_t pad1;
 };
 // Holder-hash slot: tagged subject -> hold[first, first + count).  key == NONE: free.

@@ -46,7 +46,8 @@ __global__ void k_dset_insert_rows(uint64_t* dset, uint64_t mask, const uint64_t
 }
 
 __global__ void k_nmap_insert(NSlot* nm, uint64_t mask, const uint32_t* nd_ns, const uint32_t* nd_obj,
-                              const uint32_t* nd_rel, const uint64_t* adj_off, uint32_t n_nodes) {
+                              const uint32_t* nd_rel, const uint64_t* adj_off, const uint32_t* sig,
+                              uint32_t n_nodes) {
   uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
   if (v >= n_nodes) return;
   uint64_t key = nmap_key(nd_ns[v], nd_rel[v], nd_obj[v]);
@@ -58,6 +59,7 @@ __global__ void k_nmap_insert(NSlot* nm, uint64_t mask, const uint32_t* nd_ns, c
       nm[i].node = v;
       nm[i].beg = (uint32_t)adj_off[v];
       nm[i].len = (uint32_t)(adj_off[v + 1] - adj_off[v]);
+      nm[i].sig = sig[v];
       return;
     }
     i = (i + 1) & mask;
@@ -281,16 +283,18 @@ int Snapshot::build_hash_tables() {
   if (n_set_edges >= 0xFFFFFFFFull) return set_error(KG_ERR_RESOURCE_CODE, "more than 2^32-1 subject-set edges");
   AdjX* adjx = nullptr;
   if (alloc((void**)&adjx, (n_set_edges + 1) * sizeof(AdjX))) return -1;
-  if (n_set_edges) {
-    uint32_t* sig = nullptr;
-    HIPC(hipMalloc(&sig, (size_t)ds.n_nodes * 4 + 4));
+  // per-node Bloom signature of the row subjects: inlined in adjx (child probes) and in the node map
+  // (k_resolve's root probe)
+  uint32_t* sig = nullptr;
+  HIPC(hipMalloc(&sig, (size_t)ds.n_nodes * 4 + 4));
+  if (ds.n_nodes) {
     hipLaunchKernelGGL(k_node_sig, dim3((ds.n_nodes + 255) / 256), dim3(256), 0, stream, ds.row_off, ds.row_subj,
                        ds.n_nodes, sig);
     HIPC(hipGetLastError());
+  }
+  if (n_set_edges) {
     hipLaunchKernelGGL(k_build_adjx, dim3(2048), dim3(256), 0, stream, ds.adj, ds.adj_off, sig, n_set_edges, adjx);
     HIPC(hipGetLastError());
-    HIPC(hipStreamSynchronize(stream));
-    HIPC(hipFree(sig));
   }
   ds.adjx = adjx;
   uint64_t n_rows = h_row_off_last;
@@ -308,9 +312,11 @@ int Snapshot::build_hash_tables() {
                        ds.row_subj, ds.n_nodes);
     HIPC(hipGetLastError());
     hipLaunchKernelGGL(k_nmap_insert, dim3(grid), dim3(256), 0, stream, nm, slots - 1, ds.nd_ns, ds.nd_obj,
-                       ds.nd_rel, ds.adj_off, ds.n_nodes);
+                       ds.nd_rel, ds.adj_off, sig, ds.n_nodes);
     HIPC(hipGetLastError());
   }
+  HIPC(hipStreamSynchronize(stream));
+  HIPC(hipFree(sig));
   ds.dset = dset;
   ds.dset_mask = buckets - 1;
   ds.nmap = nm;
