@@ -170,10 +170,11 @@ int kg_snapshot_info(const kg_snapshot* s, uint64_t* info4);
  * 16-lane groups per wave).  key "wide": 1 = k_light<64> (one query per wave, 256 expanded
  * nodes) takes the first tier's overflow, 0 = the overflow goes straight on (default).  Results never
  * depend on any of them.  key "back": 1 = the backward tier (reverse search from the subject's
- * holders, one workgroup per query) takes the wave tiers' overflow before the grid tier, and
- * k_resolve answers queries whose subject no row holds (default); 0 = off.  key "stream": k_stream
- * variant -- 0 = 8 query slots x 128-entry visited hash per wave, 1 = 16 slots x 64 entries
- * (default), 2 = 16 slots x 128 entries with a 512-entry FIFO.  key "shard_vis": log2 of the
+ * holders, one wave per query, then one workgroup per query) takes the wave tiers' overflow before the grid tier, and
+ * k_resolve answers queries whose subject no row holds; 2 = the same with the wave width only
+ * (its overflow goes straight to the grid tier; default); 0 = off.  key "stream": k_stream variant
+ * 0..6 (see kg_check.hip; default 5 = 32 query slots per wave sharing one visited table).
+ * key "stream_wgs": k_stream workgroups per CU (0 = by variant).  key "shard_vis": log2 of the
  * hash-sharded mode's per-batch (query, node) visited table (default 25). */
 int kg_snapshot_tune(kg_snapshot* s, const char* key, int64_t value);
 /* Synthetic layout: ids6 = {n_docs, n_groups, n_users, n_folders, user_obj0, folder_obj0}

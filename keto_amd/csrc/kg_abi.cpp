@@ -208,7 +208,7 @@ int kg_snapshot_tune(kg_snapshot* sp, const char* key, int64_t value) {
     return 0;
   }
   if (strcmp(key, "back") == 0) {
-    if (value < 0 || value > 1) return set_error(-2, "back must be 0 or 1");
+    if (value < 0 || value > 2) return set_error(-2, "back must be 0, 1 or 2");
     s->back_tier = (int)value;
     return 0;
   }

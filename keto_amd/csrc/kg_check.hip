@@ -167,7 +167,8 @@ __global__ __launch_bounds__(256) void k_resolve(DevSnap s, const kg_query* __re
         }
       }
     }
-    rq[i] = RQuery{node, subj, d, route, rb, rl};
+    // rq is read only through the tier lists, so finished queries skip it (their 24 B never leave the CU)
+    if (route != ROUTE_DONE) rq[i] = RQuery{node, subj, d, route, rb, rl};
     if (route == ROUTE_DONE) {
       out[i] = member ? KG_IS_MEMBER : KG_NOT_MEMBER;
       if (err) err[i] = KG_ERR_NONE;
@@ -1303,11 +1304,16 @@ int check_batch_device(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n,
         hipLaunchKernelGGL(k_back<64>, dim3((uint32_t)s->n_cu * 3), dim3(256), 0, stream, s->ds, rq, heavy,
                            &ctl->heavy_count, &ctl->back_head, d_out, d_err, back2, &ctl->back2_count, ctl);
         HIPC(hipGetLastError());
-        hipLaunchKernelGGL(k_back<256>, dim3((uint32_t)s->n_cu * 3), dim3(256), 0, stream, s->ds, rq, back2,
-                           &ctl->back2_count, &ctl->back2_head, d_out, d_err, giant, &ctl->fwd_count, ctl);
-        HIPC(hipGetLastError());
-        fwd_list = giant;
-        fwd_count = &ctl->fwd_count;
+        if (s->back_tier == 2) {  // wave width only: its overflow goes straight to the grid tier
+          fwd_list = back2;
+          fwd_count = &ctl->back2_count;
+        } else {
+          hipLaunchKernelGGL(k_back<256>, dim3((uint32_t)s->n_cu * 3), dim3(256), 0, stream, s->ds, rq, back2,
+                             &ctl->back2_count, &ctl->back2_head, d_out, d_err, giant, &ctl->fwd_count, ctl);
+          HIPC(hipGetLastError());
+          fwd_list = giant;
+          fwd_count = &ctl->fwd_count;
+        }
       }
       // first grid round enqueued without waiting; its readback is checked after the batch's one sync
       const int rc = grid_tier(s, w, rq, fwd_list, fwd_count, global_max_depth, d_out, d_err, stream, &gs, 1);

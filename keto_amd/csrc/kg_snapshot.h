@@ -79,7 +79,7 @@ struct Snapshot {
   uint64_t shard_vis_slots = 0;
   int shard_vis_log2 = 25;
   int stream_variant = 5;  // kg_snapshot_tune("stream"): k_stream slots/LDS variant (0..6)
-  int back_tier = 1;  // kg_snapshot_tune("back"): backward tier + no-holder filter in k_resolve
+  int back_tier = 2;  // kg_snapshot_tune("back"): backward tier (1: wave + workgroup widths, 2: wave only) + no-holder filter
   uint32_t stream_ecap = 0;  // kg_snapshot_tune("stream_ecap"): k_stream edge budget per query (0 = none)
   int grid_wgs = 16;         // kg_snapshot_tune("grid_wgs"): k_grid_level workgroups per CU
   int stream_wgs = 0;        // kg_snapshot_tune("stream_wgs"): k_stream workgroups per CU (0 = by LDS)

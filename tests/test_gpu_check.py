@@ -99,7 +99,7 @@ def test_heavy_path_overflow_star():
     assert e.last_stats["n_medium"] + e.last_stats["n_heavy"] + e.last_stats["n_back"] >= 1
 
 
-@pytest.mark.parametrize("tiers,wide,back", [(0, 0, 0), (0, 1, 0), (1, 1, 0), (2, 0, 0), (0, 0, 1), (1, 0, 1)])
+@pytest.mark.parametrize("tiers,wide,back", [(0, 0, 0), (0, 1, 0), (1, 1, 0), (2, 0, 0), (0, 0, 1), (1, 0, 1), (0, 0, 2)])
 def test_workgroup_tiers_lds_and_hbm(tiers, wide, back):
     # > 256 expanded nodes leaves the wave tiers; with back=1 the backward tier (reverse search
     # from the subject's holders) answers first and hands on what outgrows it; tiers=0 sends the
