@@ -49,10 +49,12 @@ def parse():
     ap.add_argument("--wide", type=int, default=0, help="kg_snapshot_tune wide (k_light<64> tier on/off)")
     ap.add_argument("--stream", type=int, default=5, help="kg_snapshot_tune stream (k_stream variant 0..6)")
     ap.add_argument("--stream-ecap", type=int, default=0, help="kg_snapshot_tune stream_ecap (edges per query, 0 = none)")
-    ap.add_argument("--grid-wgs", type=int, default=16, help="kg_snapshot_tune grid_wgs (k_grid_level WGs per CU)")
+    ap.add_argument("--grid-wgs", type=int, default=4, help="kg_snapshot_tune grid_wgs (k_grid_level WGs per CU)")
     ap.add_argument("--stream-wgs", type=int, default=2,
                     help="kg_snapshot_tune stream_wgs (k_stream WGs per CU, 0 = auto; 2 leaves room for the other in-flight batches)")
     ap.add_argument("--back", type=int, default=2, help="kg_snapshot_tune back (1 backward tier wave+WG widths, 2 wave width only, 0 off)")
+    ap.add_argument("--back-wgs", type=int, default=1,
+                    help="kg_snapshot_tune back_wgs (k_back WGs per CU; 1 leaves LDS to the other in-flight batches)")
     ap.add_argument("--inflight", type=int, default=4,
                     help="batches in flight per GPU: one HIP stream (own workspace) and one host thread each")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline time budget (0 = skip)")
@@ -224,6 +226,7 @@ def main():
     snap.tune("stream_ecap", a.stream_ecap)
     snap.tune("grid_wgs", a.grid_wgs)
     snap.tune("stream_wgs", a.stream_wgs)
+    snap.tune("back_wgs", a.back_wgs)
     info = snap.info()
     t_build = time.time() - t_build
 

@@ -1301,14 +1301,14 @@ int check_batch_device(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n,
       if (use_back) {
         // wave per query (~48 KiB LDS per workgroup: 3 per CU), its overflow to the workgroup-per-query
         // width (~52 KiB: 3 per CU), whose overflow goes to the grid tier
-        hipLaunchKernelGGL(k_back<64>, dim3((uint32_t)s->n_cu * 3), dim3(256), 0, stream, s->ds, rq, heavy,
+        hipLaunchKernelGGL(k_back<64>, dim3((uint32_t)s->n_cu * s->back_wgs), dim3(256), 0, stream, s->ds, rq, heavy,
                            &ctl->heavy_count, &ctl->back_head, d_out, d_err, back2, &ctl->back2_count, ctl);
         HIPC(hipGetLastError());
         if (s->back_tier == 2) {  // wave width only: its overflow goes straight to the grid tier
           fwd_list = back2;
           fwd_count = &ctl->back2_count;
         } else {
-          hipLaunchKernelGGL(k_back<256>, dim3((uint32_t)s->n_cu * 3), dim3(256), 0, stream, s->ds, rq, back2,
+          hipLaunchKernelGGL(k_back<256>, dim3((uint32_t)s->n_cu * s->back_wgs), dim3(256), 0, stream, s->ds, rq, back2,
                              &ctl->back2_count, &ctl->back2_head, d_out, d_err, giant, &ctl->fwd_count, ctl);
           HIPC(hipGetLastError());
           fwd_list = giant;

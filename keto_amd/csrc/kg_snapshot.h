@@ -83,6 +83,7 @@ struct Snapshot {
   uint32_t stream_ecap = 0;  // kg_snapshot_tune("stream_ecap"): k_stream edge budget per query (0 = none)
   int grid_wgs = 16;         // kg_snapshot_tune("grid_wgs"): k_grid_level workgroups per CU
   int stream_wgs = 0;        // kg_snapshot_tune("stream_wgs"): k_stream workgroups per CU (0 = by LDS)
+  int back_wgs = 3;          // kg_snapshot_tune("back_wgs"): k_back workgroups per CU (1..3, LDS allows 3)
 
   ~Snapshot();
   int init_device(int dev);
