@@ -940,13 +940,13 @@ __global__ __launch_bounds__(256) void k_heavy(DevSnap s, const RQuery* __restri
 // on to the forward grid tier, which redoes it from scratch (results never depend on the tier).
 // Paths from a LIGHT root only cross rewrite-free nodes (k_resolve's routing), so any backward
 // path that reaches the root is a forward path of the same length.
-// Two widths: k_back<64> runs one query per WAVE (visited hash 2048 / list 1024 in LDS, 12 queries
+// Two widths: k_back<64> runs one query per WAVE (visited hash 512 / list 256 in LDS, 12 queries
 // in flight per CU), its overflow goes to k_back<256>, one query per WORKGROUP (8192 / 4096).
 template <int W>
 struct BackCfg;
 template <>
 struct BackCfg<64> {
-  static constexpr uint32_t VLOG2 = 11, CAP = 1024;
+  static constexpr uint32_t VLOG2 = 9, CAP = 256;  // larger caps only lengthen the tail (1024: -9 % checks/s)
 };
 template <>
 struct BackCfg<256> {
