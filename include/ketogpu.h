@@ -173,8 +173,10 @@ int kg_snapshot_info(const kg_snapshot* s, uint64_t* info4);
  * holders, one wave per query, then one workgroup per query) takes the wave tiers' overflow before the grid tier, and
  * k_resolve answers queries whose subject no row holds; 2 = the same with the wave width only
  * (its overflow goes straight to the grid tier; default); 0 = off.  key "stream": k_stream variant
- * 0..6 (see kg_check.hip; default 5 = 32 query slots per wave sharing one visited table).
- * key "stream_wgs": k_stream workgroups per CU (0 = by variant).  key "shard_vis": log2 of the
+ * 0..8 (see kg_check.hip; default 7 = 32 query slots per wave sharing one visited table, <= 64
+ * expanded nodes per query).
+ * key "stream_wgs": k_stream workgroups per CU (0 = by variant); "back_wgs" (1..3) and "grid_wgs"
+ * (1..64): k_back / k_grid_level workgroups per CU.  key "shard_vis": log2 of the
  * hash-sharded mode's per-batch (query, node) visited table (default 25). */
 int kg_snapshot_tune(kg_snapshot* s, const char* key, int64_t value);
 /* Synthetic layout: ids6 = {n_docs, n_groups, n_users, n_folders, user_obj0, folder_obj0}

@@ -188,7 +188,7 @@ int kg_snapshot_tune(kg_snapshot* sp, const char* key, int64_t value) {
     return 0;
   }
   if (strcmp(key, "stream") == 0) {
-    if (value < 0 || value > 6) return set_error(-2, "stream must be in [0, 6]");
+    if (value < 0 || value > 8) return set_error(-2, "stream must be in [0, 8]");
     s->stream_variant = (int)value;
     return 0;
   }

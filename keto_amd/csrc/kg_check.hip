@@ -1250,6 +1250,7 @@ int check_batch_device(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n,
       //   4: 32 x 256 B (~49 KiB, 3/CU)
       //   5: 32 slots sharing one 1024-key table (8 KiB), <= 128 expanded nodes per query (~49 KiB, 3/CU)
       //   6: the same with <= 256 per query and a 320-entry FIFO (~53 KiB, 3/CU)
+      //   7: as 5 with <= 64 per query   8: as 7 with a 512-key table (~45 KiB)
       const int sv = s->stream_variant;
       const uint32_t per_cu = s->stream_wgs ? (uint32_t)s->stream_wgs : ((sv == 0 || sv == 1 || sv == 3) ? 5u : 3u);
       const uint32_t ecap = s->stream_ecap ? s->stream_ecap : 0xFFFFFFFFu;
@@ -1261,6 +1262,8 @@ int check_batch_device(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n,
       using V4 = SlotVis<32, 6>;
       using V5 = WaveVis<10, 128>;
       using V6 = WaveVis<10, 256>;
+      using V7 = WaveVis<10, 64>;
+      using V8 = WaveVis<9, 64>;
 #define KG_STREAM(Q, V, QC, CH)                                                                                   \
   hipLaunchKernelGGL((k_stream<Q, V, QC, CH>), dim3(grid), dim3(256), 0, stream, s->ds, rq, wl, ctl->heads, d_out, \
                      d_err, ovf_list, ovf_count, ctl, ecap)
@@ -1270,6 +1273,8 @@ int check_batch_device(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n,
       else if (sv == 4) KG_STREAM(32, V4, 256, 64);
       else if (sv == 5) KG_STREAM(32, V5, 256, 64);
       else if (sv == 6) KG_STREAM(32, V6, 320, 64);
+      else if (sv == 7) KG_STREAM(32, V7, 256, 64);
+      else if (sv == 8) KG_STREAM(32, V8, 256, 64);
       else KG_STREAM(8, V0, 256, 16);
 #undef KG_STREAM
     }

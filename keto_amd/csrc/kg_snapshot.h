@@ -78,7 +78,7 @@ struct Snapshot {
   void* shard_vis = nullptr;             // kg_shard.hip: per-batch visited table of (query, node)
   uint64_t shard_vis_slots = 0;
   int shard_vis_log2 = 25;
-  int stream_variant = 5;  // kg_snapshot_tune("stream"): k_stream slots/LDS variant (0..6)
+  int stream_variant = 7;  // kg_snapshot_tune("stream"): k_stream slots/LDS variant (0..8)
   int back_tier = 2;  // kg_snapshot_tune("back"): backward tier (1: wave + workgroup widths, 2: wave only) + no-holder filter
   uint32_t stream_ecap = 0;  // kg_snapshot_tune("stream_ecap"): k_stream edge budget per query (0 = none)
   int grid_wgs = 16;         // kg_snapshot_tune("grid_wgs"): k_grid_level workgroups per CU

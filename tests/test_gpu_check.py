@@ -52,15 +52,15 @@ def random_queries(rng, nss, rels, n, n_obj=60, n_users=40, p_setq=0.15):
     return qs
 
 
-@pytest.mark.parametrize("seed", range(8))
+@pytest.mark.parametrize("seed", range(10))
 def test_random_graphs_vs_oracle(seed):
     rng = np.random.default_rng(seed)
     it, tuples, nss, rels = random_graph(rng, n_obj=40 + 20 * (seed % 6), n_rows=200 + 150 * (seed % 6))
     reg = Registry(tuples, [], interner=it)
-    # first wave tier: k_stream variants 0..6 (seeds 0-6; seed 2 with a tiny per-query edge budget, so
-    # queries overflow into the next tiers mid-search) and k_light<16> (seed 7)
+    # first wave tier: k_stream variants 0..8 (seeds 0-6 and 8-9 -> variants 0-6, 7, 8; seed 2 with a
+    # tiny per-query edge budget, so queries overflow into the next tiers mid-search) and k_light<16> (seed 7)
     reg.snapshot.tune("light", 1 if seed == 7 else 0)
-    reg.snapshot.tune("stream", seed % 7)
+    reg.snapshot.tune("stream", seed % 7 if seed < 7 else seed - 1)
     reg.snapshot.tune("stream_ecap", 6 if seed == 2 else 0)
     qs = random_queries(rng, nss, rels, 3000, n_obj=40 + 20 * (seed % 6))
     depths = rng.integers(-1, 9, len(qs))
