@@ -1,0 +1,124 @@
+"""Request batcher in front of the check engine.
+
+The reference answers every ``Check`` RPC / REST call on its own goroutine
+(``internal/check/handler.go:144-275``, gRPC ``Check`` at :248), one ``CheckIsMember`` each.  The
+GPU engine wants batches, so concurrent callers submit here and a dispatcher thread gathers
+whatever is pending into one ``kg_check_batch`` call: a batch closes when it reaches
+``max_batch`` queries or when its oldest query has waited ``max_wait_us``.  Each caller gets the
+answer of a loop of ``CheckIsMember``: allowed, or the per-query error.
+
+While one batch runs on the GPU the next one fills, so under load the batch size grows to match
+the arrival rate and the GPU stays busy; at low load a query waits at most ``max_wait_us`` plus
+one batch.  ``latency_percentile`` reports the batch latency (submission of the oldest query to
+its answer) that BASELINE.json's p99 metric names.
+"""
+from __future__ import annotations
+
+import threading
+import time
+from concurrent.futures import Future
+from typing import List, Optional, Tuple
+
+import numpy as np
+
+from . import _lib
+from .engine import CheckError, Engine, queries_array
+from .ketoapi import RelationTuple
+
+
+class BatcherClosed(RuntimeError):
+    pass
+
+
+class CheckBatcher:
+    def __init__(self, engine: Engine, max_batch: int = 1 << 16, max_wait_us: int = 200):
+        if max_batch < 1 or max_wait_us < 0:
+            raise ValueError("max_batch >= 1 and max_wait_us >= 0 required")
+        self.engine = engine
+        self.max_batch = max_batch
+        self.max_wait = max_wait_us * 1e-6
+        self._cv = threading.Condition()
+        self._pending: List[Tuple[np.ndarray, Future, float]] = []
+        self._closed = False
+        self.batch_sizes: List[int] = []
+        self.batch_latency_s: List[float] = []
+        self._thread = threading.Thread(target=self._run, name="kg-check-batcher", daemon=True)
+        self._thread.start()
+
+    # ---- submission
+    def submit_ids(self, q7) -> Future:
+        """One kg_query row (ns, obj, rel, sns, sobj, srel, max_depth) -> Future[(result u8, err u32)]."""
+        row = np.ascontiguousarray(q7, np.uint32).reshape(7)
+        f: Future = Future()
+        with self._cv:
+            if self._closed:
+                raise BatcherClosed("batcher is closed")
+            self._pending.append((row, f, time.perf_counter()))
+            if len(self._pending) == 1 or len(self._pending) >= self.max_batch:
+                self._cv.notify()
+        return f
+
+    def submit(self, t: RelationTuple, rest_depth: int) -> Future:
+        it = self.engine.snapshot.interner
+        return self.submit_ids(queries_array(np.asarray(it.tuple_ids(t), np.uint32), rest_depth)[0])
+
+    def check_is_member(self, t: RelationTuple, rest_depth: int, timeout: Optional[float] = None) -> bool:
+        """CheckIsMember through the batcher (internal/check/engine.go:54-60)."""
+        res, err = self.submit(t, rest_depth).result(timeout)
+        if res == _lib.KG_ERROR:
+            raise CheckError(err)
+        return res == _lib.KG_IS_MEMBER
+
+    # ---- dispatcher
+    def _take(self) -> List[Tuple[np.ndarray, Future, float]]:
+        with self._cv:
+            while not self._pending and not self._closed:
+                self._cv.wait()
+            if not self._pending:
+                return []
+            deadline = self._pending[0][2] + self.max_wait
+            while len(self._pending) < self.max_batch and not self._closed:
+                left = deadline - time.perf_counter()
+                if left <= 0:
+                    break
+                self._cv.wait(left)
+            batch, self._pending = self._pending[:self.max_batch], self._pending[self.max_batch:]
+            return batch
+
+    def _run(self) -> None:
+        while True:
+            batch = self._take()
+            if not batch:
+                return
+            q = np.stack([b[0] for b in batch])
+            try:
+                out, err = self.engine.batch_check_ids(q)
+            except BaseException as e:  # the whole batch failed (library status): every caller sees it
+                for _, f, _t in batch:
+                    f.set_exception(e)
+                continue
+            done = time.perf_counter()
+            self.batch_sizes.append(len(batch))
+            self.batch_latency_s.append(done - batch[0][2])
+            for i, (_, f, _t) in enumerate(batch):
+                f.set_result((int(out[i]), int(err[i])))
+
+    # ---- lifecycle / stats
+    def close(self) -> None:
+        """Stop accepting queries; pending ones are still answered."""
+        with self._cv:
+            self._closed = True
+            self._cv.notify_all()
+        self._thread.join()
+
+    def __enter__(self) -> "CheckBatcher":
+        return self
+
+    def __exit__(self, *exc) -> None:
+        self.close()
+
+    def latency_percentile(self, p: float = 99.0) -> float:
+        """Batch latency percentile in ms (oldest submission -> answers delivered)."""
+        if not self.batch_latency_s:
+            return 0.0
+        return float(np.percentile(np.asarray(self.batch_latency_s), p) * 1e3)

@@ -1,0 +1,104 @@
+"""GPU tests: the snapshot persister (writes invalidate the HBM snapshot; checks see every
+committed write) and the request batcher (concurrent callers coalesced into kg_check_batch
+calls), both against the CPU oracle on the persister's rows in shard order.  Bit-exact."""
+import threading
+
+import numpy as np
+import pytest
+
+from keto_amd.batcher import CheckBatcher
+from keto_amd.engine import queries_array
+from keto_amd.ketoapi import RelationTuple, SubjectSet
+from keto_amd.persister import RelationQuery, SnapshotPersister
+from oracle.oracle import POLICY_CANONICAL, Oracle
+from test_gpu_check import random_graph, random_queries
+
+pytestmark = pytest.mark.gpu
+
+
+def shard_rows(m: SnapshotPersister) -> np.ndarray:
+    rows, tok = [], ""
+    while True:
+        page, tok = m.get_relation_tuples(RelationQuery(), page_token=tok, page_size=500)
+        rows += page
+        if not tok:
+            return m.interner.tuples_array(rows)
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_persister_read_your_writes_vs_oracle(seed):
+    rng = np.random.default_rng(100 + seed)
+    it, tuples, nss, rels = random_graph(rng, n_obj=50, n_rows=600)
+    m = SnapshotPersister(interner=it, max_read_depth=6, seed=seed)
+    e = m.permission_engine()
+    qs = random_queries(rng, nss, rels, 1500, n_obj=50)
+    q6 = np.asarray([it.tuple_ids(t) for t in qs], np.uint32)
+    depths = rng.integers(0, 8, len(qs))
+    chunks = np.array_split(np.arange(len(tuples)), 3)
+    for k, idx in enumerate(chunks):
+        ins = [tuples[i] for i in idx]
+        dels = [tuples[i] for i in rng.choice(chunks[k - 1], 40, replace=False)] if k else []
+        m.transact_relation_tuples(ins, dels)
+        out, err = e.batch_check_ids(queries_array(q6, depths))
+        exp, oerr, _ = Oracle(shard_rows(m), it.wildcard_rel).check_batch(q6, depths, 6, POLICY_CANONICAL)
+        assert (err == 0).all() and (oerr == 0).all()
+        assert (out == exp).all(), np.nonzero(out != exp)[0][:10]
+    assert m.rebuilds == 3
+
+
+def test_persister_write_delete_flip():
+    m = SnapshotPersister()
+    e = m.permission_engine()
+    x = m.expand_engine()
+    m.write_relation_tuples(RelationTuple.from_string("group:h#member@bob"))
+    t = RelationTuple.from_string("doc:a#view@(group:g#member)")
+    u = RelationTuple.from_string("group:g#member@alice")
+    q = RelationTuple.from_string("doc:a#view@alice")
+    m.write_relation_tuples(t)
+    assert not e.check_is_member(q, 0)
+    m.write_relation_tuples(u)
+    assert e.check_is_member(q, 0)
+    assert x.build_tree(SubjectSet("doc", "a", "view"), 0) is not None
+    m.delete_relation_tuples(u)
+    assert not e.check_is_member(q, 0)
+    m.delete_all_relation_tuples(RelationQuery("doc"))
+    assert x.build_tree(SubjectSet("doc", "a", "view"), 0) is None
+    assert m.rebuilds == 4
+    assert e.check_is_member(RelationTuple.from_string("group:h#member@bob"), 0)
+
+
+def test_batcher_vs_direct_batch():
+    rng = np.random.default_rng(5)
+    it, tuples, nss, rels = random_graph(rng, n_obj=80, n_rows=900)
+    m = SnapshotPersister(interner=it, max_read_depth=5)
+    m.write_relation_tuples(*tuples)
+    e = m.permission_engine()
+    qs = random_queries(rng, nss, rels, 4000, n_obj=80)
+    q6 = np.asarray([it.tuple_ids(t) for t in qs], np.uint32)
+    depths = rng.integers(0, 7, len(qs))
+    q7 = queries_array(q6, depths)
+    want, _ = e.batch_check_ids(q7)
+    got = np.full(len(qs), 255, np.uint8)
+    with CheckBatcher(e, max_batch=512, max_wait_us=300) as b:
+        def worker(k):
+            fs = [(i, b.submit_ids(q7[i])) for i in range(k, len(qs), 8)]
+            for i, f in fs:
+                got[i] = f.result(60)[0]
+        ts = [threading.Thread(target=worker, args=(k,)) for k in range(8)]
+        [t.start() for t in ts]
+        [t.join() for t in ts]
+        assert b.check_is_member(qs[0], int(depths[0])) == bool(want[0] == 1)
+    assert (got == want).all()
+    assert len(b.batch_sizes) < len(qs) and max(b.batch_sizes) <= 512
+
+
+def test_persister_empty_snapshot():
+    # every row deleted: the snapshot has no nodes; checks answer NotMember, expand a nil tree
+    m = SnapshotPersister()
+    t = RelationTuple.from_string("doc:a#view@alice")
+    m.write_relation_tuples(t)
+    e = m.permission_engine()
+    assert e.check_is_member(t, 0)
+    m.delete_relation_tuples(t)
+    assert not e.check_is_member(t, 0)
+    assert m.expand_engine().build_tree(SubjectSet("doc", "a", "view"), 0) is None
