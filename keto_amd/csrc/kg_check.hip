@@ -1336,7 +1336,7 @@ int check_batch_device(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n,
       ic.st_edges = &ctl->st[ST_EDGES];
       ic.st_probes = &ctl->st[ST_PROBES];
       HIPC(hipMemcpyAsync(&ctl->ic, &ic, sizeof ic, hipMemcpyHostToDevice, stream));
-      if (launch_general(s, w, d_q, rq, gen, &ctl->gen_count, &ctl->ic, d_out, d_err, stream)) return -1;
+      if (launch_general(s, w, d_q, rq, gen, &ctl->gen_count, &ctl->ic, d_out, d_err, (uint32_t)n, stream)) return -1;
     }
   }
   // one synchronisation per batch: the grid round's readback and the counters come back together

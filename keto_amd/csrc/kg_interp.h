@@ -21,7 +21,7 @@ struct MemoEnt {
 struct InterpCtl {
   const uint32_t* gen_count;  // -> Ctl::gen_count
   uint32_t* p2_list;          // pass-2 query list (n entries)
-  uint32_t p2_count, p2_head, pad[2];
+  uint32_t p2_count, p2_head, p3_count, p3_head;  // pass-2 / pass-3 counters (p3 list lives in the pool)
   uint32_t heads[8 * 32];
   unsigned long long* st_general;
   unsigned long long* st_rows;
@@ -32,6 +32,7 @@ struct InterpCtl {
 struct Snapshot;
 struct Workspace;
 int launch_general(Snapshot* s, Workspace* w, const kg_query* d_q, const RQuery* rq, const uint32_t* gen_list,
-                   const uint32_t* gen_count, InterpCtl* ic, uint8_t* out, uint32_t* err, hipStream_t stream);
+                   const uint32_t* gen_count, InterpCtl* ic, uint8_t* out, uint32_t* err, uint32_t n_queries,
+                   hipStream_t stream);
 
 }  // namespace kg

@@ -503,31 +503,50 @@ __global__ __launch_bounds__(256) void k_interp_lds(DevSnap s, const kg_query* _
   }
 }
 
-// Pass 2 (HBM BFS tier): one wave per slot, bitmap + list sized for the whole graph.
+// Pass 2 / pass 3 (HBM BFS tiers): one wave per slot, a visited bitmap over the whole graph.
+// Pass 2 runs many slots with a bounded BFS list (cap entries); a query whose list overflows
+// leaves stray bits in its slot's bitmap, so the wave clears the whole bitmap and hands the
+// query to pass 3, one slot whose list holds every node (cannot overflow).
+__device__ __forceinline__ void clear_bitmap(uint32_t* bm, uint64_t words) {
+  // words is a multiple of 4 and bm 16-B aligned (launch_general)
+  uint4* b4 = reinterpret_cast<uint4*>(bm);
+  for (uint64_t i = lane_id(); i < words / 4; i += 64) b4[i] = make_uint4(0, 0, 0, 0);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
 __global__ __launch_bounds__(64) void k_interp_hbm(DevSnap s, const kg_query* __restrict__ oq,
-                                                   const RQuery* __restrict__ rq, InterpCtl* ic, uint8_t* out,
-                                                   uint32_t* err, Frame* stacks, MemoEnt* memos, uint32_t* bitmaps,
-                                                   uint64_t words, uint32_t* lists, uint64_t cap,
-                                                   uint64_t batch_tag) {
+                                                   const RQuery* __restrict__ rq, InterpCtl* ic, int pass,
+                                                   uint32_t* p3_list, uint8_t* out, uint32_t* err, Frame* stacks,
+                                                   MemoEnt* memos, uint32_t* bitmaps, uint64_t words, uint32_t* lists,
+                                                   uint64_t cap, uint64_t batch_tag) {
   __shared__ uint32_t pref[64];
   const int lane = lane_id();
   const uint32_t slot = blockIdx.x;
-  GlobalStore st{bitmaps + (size_t)slot * words, lists + (size_t)slot * cap, cap, pref};
+  uint32_t* bm = bitmaps + (size_t)slot * words;
+  GlobalStore st{bm, lists + (size_t)slot * cap, cap, pref};
   Frame* stack = stacks + (size_t)slot * STACK_CAP;
   MemoEnt* memo = memos + (size_t)slot * MEMO_CAP;
-  const uint32_t count = ic->p2_count;
+  const uint32_t* qlist = pass == 2 ? ic->p2_list : p3_list;
+  const uint32_t count = pass == 2 ? ic->p2_count : ic->p3_count;
+  uint32_t* head = pass == 2 ? &ic->p2_head : &ic->p3_head;
   BfsStats bs;
   unsigned long long done = 0;
   for (;;) {
     uint32_t li = 0;
-    if (lane == 0) li = atomicAdd(&ic->p2_head, 1u);
+    if (lane == 0) li = atomicAdd(head, 1u);
     li = __shfl(li, 0, 64);
     if (li >= count) break;
-    const uint32_t qi = ic->p2_list[li];
+    const uint32_t qi = qlist[li];
     uint32_t e = 0;
     int r = interp_query(s, st, oq[qi], rq[qi], stack, memo, batch_tag | qi, e, bs);
-    if (r == Q_OVERFLOW) {  // cannot happen with cap = n_nodes; report instead of looping
-      r = R_ERR;
+    if (r == Q_OVERFLOW) {
+      clear_bitmap(bm, words);
+      if (pass == 2) {
+        if (lane == 0) p3_list[atomicAdd(&ic->p3_count, 1u)] = qi;
+        continue;
+      }
+      r = R_ERR;  // pass 3 holds every node: only the frame stack can run out
       e = KG_ERR_RESOURCE;
     }
     finish_query<GlobalStore>(qi, r, e, out, err);
@@ -542,38 +561,74 @@ __global__ __launch_bounds__(64) void k_interp_hbm(DevSnap s, const kg_query* __
 }
 
 int launch_general(Snapshot* s, Workspace* w, const kg_query* d_q, const RQuery* rq, const uint32_t* gen_list,
-                   const uint32_t* gen_count, InterpCtl* ic, uint8_t* out, uint32_t* err, hipStream_t stream) {
+                   const uint32_t* gen_count, InterpCtl* ic, uint8_t* out, uint32_t* err, uint32_t n_queries,
+                   hipStream_t stream) {
   if (!s->has_program) return 0;  // without rewrites nothing is ever routed GENERAL
   const uint32_t grid1 = (uint32_t)s->n_cu * 2;
   const uint32_t slots1 = grid1 * 4;
   const uint64_t nn = std::max<uint32_t>(s->ds.n_nodes, 1);
-  const uint64_t words = (nn + 31) / 32 + 1;
-  const uint32_t slots2 = (uint32_t)std::max<uint64_t>(
-      1, std::min<uint64_t>(64, (4ull << 30) / ((words + nn) * 4 + STACK_CAP * sizeof(Frame) + MEMO_CAP * sizeof(MemoEnt))));
+  const uint64_t words = ((nn + 31) / 32 + 1 + 3) & ~3ull;  // 16-B multiple: clear_bitmap stores uint4
   const size_t slot_bytes = STACK_CAP * sizeof(Frame) + MEMO_CAP * sizeof(MemoEnt);
-  const size_t need = (size_t)slots1 * slot_bytes + (size_t)slots2 * ((words + nn) * 4 + slot_bytes);
+  static_assert((STACK_CAP * sizeof(Frame) + MEMO_CAP * sizeof(MemoEnt)) % 16 == 0, "bitmaps follow the slots 16-B aligned");
+  // pass 2: up to one slot per CU, list cap 4 Mi nodes, within 16 GiB of HBM per workspace
+  const uint64_t cap2 = (std::min<uint64_t>(nn, s->interp_cap2 ? s->interp_cap2 : 1ull << 22) + 3) & ~3ull;  // keeps the pass-3 region 16-B aligned
+  const uint64_t per2 = slot_bytes + (words + cap2) * 4;
+  // pass-2 budget: 16 GiB, or an eighth of the free HBM when less (other streams' workspaces and
+  // the snapshot share the device); a pool that already exists keeps its layout
+  uint64_t budget2 = 16ull << 30;
+  if (w->interp_layout == 0) {
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) budget2 = std::min<uint64_t>(budget2, free_b / 8);
+  } else {
+    budget2 = (w->interp_layout >> 40) * per2;
+  }
+  uint32_t slots2 = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)s->n_cu, budget2 / per2));
+  const size_t bytes1 = (size_t)slots1 * slot_bytes;
+  const size_t bytes3 = nn * 4;  // pass 3 reuses pass-2 slot 0 (clear once pass 2 is done) + a full list
+  const size_t tail = (size_t)std::max<uint32_t>(n_queries, 1) * 4;
+  size_t need = bytes1 + (size_t)slots2 * per2 + bytes3 + tail;
   if (need > w->interp_pool_bytes) {
     if (w->interp_pool) hipFree(w->interp_pool);
     w->interp_pool = nullptr;
     w->interp_pool_bytes = 0;
-    HIPC(hipMalloc(&w->interp_pool, need));
+    // HBM is shared with the snapshot and the other streams' workspaces: fewer pass-2 slots on OOM
+    hipError_t e;
+    while ((e = hipMalloc(&w->interp_pool, need)) == hipErrorOutOfMemory && slots2 > 1) {
+      (void)hipGetLastError();
+      slots2 = slots2 / 2;
+      need = bytes1 + (size_t)slots2 * per2 + bytes3 + tail;
+    }
+    HIPC(e);
     HIPC(hipMemsetAsync(w->interp_pool, 0, need, stream));  // memo tags 0 = empty; bitmaps clear
     w->interp_pool_bytes = need;
+  } else if (w->interp_layout != ((uint64_t)slots2 << 40 | cap2)) {
+    HIPC(hipMemsetAsync(w->interp_pool, 0, need, stream));  // regions moved: bitmaps must start clear
   }
+  const size_t bytes2 = (size_t)slots2 * per2;
+  w->interp_layout = (uint64_t)slots2 << 40 | cap2;
   char* p = (char*)w->interp_pool;
   Frame* stacks1 = (Frame*)p;
   MemoEnt* memos1 = (MemoEnt*)(p + (size_t)slots1 * STACK_CAP * sizeof(Frame));
-  char* p2 = p + (size_t)slots1 * slot_bytes;
+  char* p2 = p + bytes1;
   Frame* stacks2 = (Frame*)p2;
   MemoEnt* memos2 = (MemoEnt*)(p2 + (size_t)slots2 * STACK_CAP * sizeof(Frame));
   uint32_t* bm2 = (uint32_t*)(p2 + (size_t)slots2 * slot_bytes);
   uint32_t* lists2 = bm2 + (size_t)slots2 * words;
+  char* p3 = p2 + bytes2;
+  Frame* stack3 = stacks2;
+  MemoEnt* memo3 = memos2;
+  uint32_t* bm3 = bm2;
+  uint32_t* list3 = (uint32_t*)p3;
+  uint32_t* p3_list = (uint32_t*)(p3 + bytes3);
   const uint64_t tag = (uint64_t)(++s->batch_seq) << 32;
   hipLaunchKernelGGL(k_interp_lds, dim3(grid1), dim3(256), 0, stream, s->ds, d_q, rq, gen_list, ic, out, err, stacks1,
                      memos1, tag);
   HIPC(hipGetLastError());
-  hipLaunchKernelGGL(k_interp_hbm, dim3(slots2), dim3(64), 0, stream, s->ds, d_q, rq, ic, out, err, stacks2, memos2,
-                     bm2, words, lists2, nn, tag);
+  hipLaunchKernelGGL(k_interp_hbm, dim3(slots2), dim3(64), 0, stream, s->ds, d_q, rq, ic, 2, p3_list, out, err,
+                     stacks2, memos2, bm2, words, lists2, cap2, tag);
+  HIPC(hipGetLastError());
+  hipLaunchKernelGGL(k_interp_hbm, dim3(1), dim3(64), 0, stream, s->ds, d_q, rq, ic, 3, p3_list, out, err, stack3,
+                     memo3, bm3, words, list3, nn, tag);
   HIPC(hipGetLastError());
   (void)gen_count;
   return 0;

@@ -310,12 +310,15 @@ def test_relation_not_found_and_cycle():
     assert r.err is not None and r.err.code == 1
 
 
-@pytest.mark.parametrize("n_tuples,gmax", [(150_000, 10), (250_000, 5)])
-def test_synthetic_c3_rewrites_vs_oracle(n_tuples, gmax):
-    """Config C3: the Drive-like graph + folder forest + OPL view/edit/share (interpreter path)."""
+@pytest.mark.parametrize("n_tuples,gmax,cap2", [(150_000, 10, 0), (250_000, 5, 0), (150_000, 10, 32)])
+def test_synthetic_c3_rewrites_vs_oracle(n_tuples, gmax, cap2):
+    """Config C3: the Drive-like graph + folder forest + OPL view/edit/share (interpreter path).
+    cap2 = 32: the many-slot HBM pass holds 32 nodes per BFS, so what reaches it overflows into
+    the single full-size slot (pass 3)."""
     torch = _torch()
     from keto_amd import _lib
     snap = Snapshot.synthetic(n_tuples, seed=20250131, preset=1)
+    snap.tune("interp_cap2", cap2)
     n = 6000
     dq = torch.empty((n, 7), dtype=torch.int32, device="cuda")
     _lib.check(_lib.load().kg_synth_queries(snap.handle, 11, n, dq.data_ptr()), "kg_synth_queries")
