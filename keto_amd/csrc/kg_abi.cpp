@@ -207,6 +207,11 @@ int kg_snapshot_tune(kg_snapshot* sp, const char* key, int64_t value) {
     s->grid_wgs = (int)value;
     return 0;
   }
+  if (strcmp(key, "interp_wgs") == 0) {
+    if (value < 1 || value > 8) return set_error(-2, "interp_wgs must be in [1, 8]");
+    s->interp_wgs = (int)value;
+    return 0;
+  }
   if (strcmp(key, "interp_cap2") == 0) {
     if (value < 0 || value > (1 << 22)) return set_error(-2, "interp_cap2 must be in [0, 4194304]");
     s->interp_cap2 = (uint32_t)value;

@@ -564,7 +564,7 @@ int launch_general(Snapshot* s, Workspace* w, const kg_query* d_q, const RQuery*
                    const uint32_t* gen_count, InterpCtl* ic, uint8_t* out, uint32_t* err, uint32_t n_queries,
                    hipStream_t stream) {
   if (!s->has_program) return 0;  // without rewrites nothing is ever routed GENERAL
-  const uint32_t grid1 = (uint32_t)s->n_cu * 2;
+  const uint32_t grid1 = (uint32_t)s->n_cu * (uint32_t)s->interp_wgs;
   const uint32_t slots1 = grid1 * 4;
   const uint64_t nn = std::max<uint32_t>(s->ds.n_nodes, 1);
   const uint64_t words = ((nn + 31) / 32 + 1 + 3) & ~3ull;  // 16-B multiple: clear_bitmap stores uint4
@@ -601,11 +601,11 @@ int launch_general(Snapshot* s, Workspace* w, const kg_query* d_q, const RQuery*
     HIPC(e);
     HIPC(hipMemsetAsync(w->interp_pool, 0, need, stream));  // memo tags 0 = empty; bitmaps clear
     w->interp_pool_bytes = need;
-  } else if (w->interp_layout != ((uint64_t)slots2 << 40 | cap2)) {
+  } else if (w->interp_layout != (((uint64_t)slots2 << 40 | (uint64_t)slots1 << 24 | cap2))) {
     HIPC(hipMemsetAsync(w->interp_pool, 0, need, stream));  // regions moved: bitmaps must start clear
   }
   const size_t bytes2 = (size_t)slots2 * per2;
-  w->interp_layout = (uint64_t)slots2 << 40 | cap2;
+  w->interp_layout = ((uint64_t)slots2 << 40 | (uint64_t)slots1 << 24 | cap2);
   char* p = (char*)w->interp_pool;
   Frame* stacks1 = (Frame*)p;
   MemoEnt* memos1 = (MemoEnt*)(p + (size_t)slots1 * STACK_CAP * sizeof(Frame));

@@ -41,7 +41,7 @@ struct Workspace {
   uint32_t grid_epoch = 0;
   void* interp_pool = nullptr;
   size_t interp_pool_bytes = 0;
-  uint64_t interp_layout = 0;  // (pass-2 slots, list cap) the pool was last laid out for
+  uint64_t interp_layout = 0;  // (pass-2 slots, pass-1 slots, list cap) the pool was last laid out for
   hipEvent_t ev[4] = {};  // batch timing events (created on first use)
   void* pinned = nullptr;  // 64 KiB of pinned host memory for small device->host readbacks
   void* host_buf(size_t bytes);
@@ -84,6 +84,7 @@ struct Snapshot {
   uint32_t stream_ecap = 0;  // kg_snapshot_tune("stream_ecap"): k_stream edge budget per query (0 = none)
   int grid_wgs = 16;         // kg_snapshot_tune("grid_wgs"): k_grid_level workgroups per CU
   int stream_wgs = 0;        // kg_snapshot_tune("stream_wgs"): k_stream workgroups per CU (0 = by LDS)
+  int interp_wgs = 8;        // kg_snapshot_tune("interp_wgs"): k_interp_lds workgroups (4 waves) per CU (6 resident by LDS)
   uint32_t interp_cap2 = 0;  // kg_snapshot_tune("interp_cap2"): pass-2 BFS list cap of the rewrite path (0 = 4 Mi)
   int back_wgs = 3;          // kg_snapshot_tune("back_wgs"): k_back workgroups per CU (1..3, LDS allows 3)
 
