@@ -56,7 +56,7 @@ def parse():
     ap.add_argument("--back", type=int, default=2, help="kg_snapshot_tune back (1 backward tier wave+WG widths, 2 wave width only, 0 off)")
     ap.add_argument("--back-wgs", type=int, default=1,
                     help="kg_snapshot_tune back_wgs (k_back WGs per CU; 1 leaves LDS to the other in-flight batches)")
-    ap.add_argument("--interp-wgs", type=int, default=8, help="kg_snapshot_tune interp_wgs (rewrite-path LDS pass WGs per CU)")
+    ap.add_argument("--interp-wgs", type=int, default=6, help="kg_snapshot_tune interp_wgs (rewrite-path LDS pass WGs per CU)")
     ap.add_argument("--inflight", type=int, default=4,
                     help="batches in flight per GPU: one HIP stream (own workspace) and one host thread each")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline time budget (0 = skip)")

@@ -178,9 +178,9 @@ int kg_snapshot_info(const kg_snapshot* s, uint64_t* info4);
  * key "stream_wgs": k_stream workgroups per CU (0 = by variant); "back_wgs" (1..3) and "grid_wgs"
  * (1..64): k_back / k_grid_level workgroups per CU.  key "shard_vis": log2 of the
  * hash-sharded mode's per-batch (query, node) visited table (default 25).  key "interp_cap2"
- * (0..4194304): BFS list cap of the rewrite interpreter's many-slot HBM pass (0 = 4 Mi nodes);
+ * (0..4194304): BFS list cap of the rewrite interpreter's many-slot HBM pass (0 = 256 Ki nodes);
  * queries that outgrow it rerun in the single full-size slot.  key "interp_wgs" (1..8): workgroups
- * of 4 query waves per CU in the interpreter's LDS pass (default 8). */
+ * of 4 query waves per CU in the interpreter's LDS pass (default 6). */
 int kg_snapshot_tune(kg_snapshot* s, const char* key, int64_t value);
 /* Synthetic layout: ids6 = {n_docs, n_groups, n_users, n_folders, user_obj0, folder_obj0}
  * (doc d = object d, group g = object n_docs+g, user u = object user_obj0+u). */

@@ -203,6 +203,50 @@ struct GlobalStore {
   }
 };
 
+// HBM tier with a bounded footprint: open-addressing visited hash (tmask+1 >= 2 x cap slots,
+// entries key+1 so the zeroed pool is empty) + BFS list of cap nodes.  The list cap is checked
+// after every 64-wide step, so the table stays below half full and a probe always ends.  finish()
+// removes the listed keys (a lookup of a key known to be present skips zeroed slots, so the
+// removal order does not matter); after an overflow the caller zeroes the whole table.
+struct HashStore {
+  uint32_t* tab;
+  uint32_t tmask;
+  uint32_t* lst;
+  uint64_t capacity;
+  uint32_t* pf;
+  __device__ uint32_t* list() const { return lst; }
+  __device__ uint32_t* pref() const { return pf; }
+  __device__ uint64_t cap() const { return capacity; }
+  __device__ void reset() {}
+  __device__ uint32_t home(uint32_t key) const { return (key * 2654435761u) & tmask; }
+  __device__ bool insert(uint32_t key) {
+    uint32_t h = home(key);
+    for (uint32_t p = 0; p <= tmask; p++) {
+      const uint32_t old = atomicCAS(&tab[h], 0u, key + 1);
+      if (old == 0u) return true;
+      if (old == key + 1) return false;
+      h = (h + 1) & tmask;
+    }
+    return true;
+  }
+  __device__ void sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  }
+  __device__ void finish(uint32_t n) {
+    sync();
+    for (uint32_t i = lane_id(); i < n; i += 64) {
+      const uint32_t key = lst[i];
+      uint32_t h = home(key);
+      for (uint32_t p = 0; p <= tmask; p++) {
+        if (atomicCAS(&tab[h], key + 1, 0u) == key + 1) break;
+        h = (h + 1) & tmask;
+      }
+    }
+    sync();
+  }
+};
+
 struct BfsStats {
   unsigned long long rows = 0, edges = 0, probes = 0;
 };

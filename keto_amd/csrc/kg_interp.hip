@@ -515,18 +515,13 @@ __device__ __forceinline__ void clear_bitmap(uint32_t* bm, uint64_t words) {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
-__global__ __launch_bounds__(64) void k_interp_hbm(DevSnap s, const kg_query* __restrict__ oq,
-                                                   const RQuery* __restrict__ rq, InterpCtl* ic, int pass,
-                                                   uint32_t* p3_list, uint8_t* out, uint32_t* err, Frame* stacks,
-                                                   MemoEnt* memos, uint32_t* bitmaps, uint64_t words, uint32_t* lists,
-                                                   uint64_t cap, uint64_t batch_tag) {
-  __shared__ uint32_t pref[64];
+// One wave per slot: dequeue from qlist, evaluate, hand overflows on (pass 2) or report them.
+template <class Store>
+__device__ void interp_slot_loop(const DevSnap& s, const kg_query* __restrict__ oq, const RQuery* __restrict__ rq,
+                                 InterpCtl* ic, int pass, uint32_t* p3_list, uint8_t* out, uint32_t* err, Store& st,
+                                 uint32_t* clear_base, uint64_t clear_words, Frame* stack, MemoEnt* memo,
+                                 uint64_t batch_tag) {
   const int lane = lane_id();
-  const uint32_t slot = blockIdx.x;
-  uint32_t* bm = bitmaps + (size_t)slot * words;
-  GlobalStore st{bm, lists + (size_t)slot * cap, cap, pref};
-  Frame* stack = stacks + (size_t)slot * STACK_CAP;
-  MemoEnt* memo = memos + (size_t)slot * MEMO_CAP;
   const uint32_t* qlist = pass == 2 ? ic->p2_list : p3_list;
   const uint32_t count = pass == 2 ? ic->p2_count : ic->p3_count;
   uint32_t* head = pass == 2 ? &ic->p2_head : &ic->p3_head;
@@ -541,7 +536,7 @@ __global__ __launch_bounds__(64) void k_interp_hbm(DevSnap s, const kg_query* __
     uint32_t e = 0;
     int r = interp_query(s, st, oq[qi], rq[qi], stack, memo, batch_tag | qi, e, bs);
     if (r == Q_OVERFLOW) {
-      clear_bitmap(bm, words);
+      clear_bitmap(clear_base, clear_words);  // keys inserted but never listed stay behind otherwise
       if (pass == 2) {
         if (lane == 0) p3_list[atomicAdd(&ic->p3_count, 1u)] = qi;
         continue;
@@ -549,7 +544,7 @@ __global__ __launch_bounds__(64) void k_interp_hbm(DevSnap s, const kg_query* __
       r = R_ERR;  // pass 3 holds every node: only the frame stack can run out
       e = KG_ERR_RESOURCE;
     }
-    finish_query<GlobalStore>(qi, r, e, out, err);
+    finish_query<Store>(qi, r, e, out, err);
     done++;
   }
   if (lane == 0) {
@@ -558,6 +553,31 @@ __global__ __launch_bounds__(64) void k_interp_hbm(DevSnap s, const kg_query* __
     atomicAdd(ic->st_edges, bs.edges);
     atomicAdd(ic->st_probes, bs.probes);
   }
+}
+
+// Pass 2: many slots, visited hash of tsize (power of two >= 2 cap) slots + list of cap nodes.
+__global__ __launch_bounds__(64) void k_interp_hash(DevSnap s, const kg_query* __restrict__ oq,
+                                                    const RQuery* __restrict__ rq, InterpCtl* ic, uint32_t* p3_list,
+                                                    uint8_t* out, uint32_t* err, Frame* stacks, MemoEnt* memos,
+                                                    uint32_t* tabs, uint64_t tsize, uint32_t* lists, uint64_t cap,
+                                                    uint64_t batch_tag) {
+  __shared__ uint32_t pref[64];
+  const uint32_t slot = blockIdx.x;
+  uint32_t* tab = tabs + (size_t)slot * tsize;
+  HashStore st{tab, (uint32_t)(tsize - 1), lists + (size_t)slot * cap, cap, pref};
+  interp_slot_loop(s, oq, rq, ic, 2, p3_list, out, err, st, tab, tsize, stacks + (size_t)slot * STACK_CAP,
+                   memos + (size_t)slot * MEMO_CAP, batch_tag);
+}
+
+// Pass 3: one slot, visited bitmap over the whole graph + a list that holds every node.
+__global__ __launch_bounds__(64) void k_interp_hbm(DevSnap s, const kg_query* __restrict__ oq,
+                                                   const RQuery* __restrict__ rq, InterpCtl* ic, uint32_t* p3_list,
+                                                   uint8_t* out, uint32_t* err, Frame* stack, MemoEnt* memo,
+                                                   uint32_t* bm, uint64_t words, uint32_t* list, uint64_t cap,
+                                                   uint64_t batch_tag) {
+  __shared__ uint32_t pref[64];
+  GlobalStore st{bm, list, cap, pref};
+  interp_slot_loop(s, oq, rq, ic, 3, p3_list, out, err, st, bm, words, stack, memo, batch_tag);
 }
 
 int launch_general(Snapshot* s, Workspace* w, const kg_query* d_q, const RQuery* rq, const uint32_t* gen_list,
@@ -569,10 +589,12 @@ int launch_general(Snapshot* s, Workspace* w, const kg_query* d_q, const RQuery*
   const uint64_t nn = std::max<uint32_t>(s->ds.n_nodes, 1);
   const uint64_t words = ((nn + 31) / 32 + 1 + 3) & ~3ull;  // 16-B multiple: clear_bitmap stores uint4
   const size_t slot_bytes = STACK_CAP * sizeof(Frame) + MEMO_CAP * sizeof(MemoEnt);
-  static_assert((STACK_CAP * sizeof(Frame) + MEMO_CAP * sizeof(MemoEnt)) % 16 == 0, "bitmaps follow the slots 16-B aligned");
-  // pass 2: up to one slot per CU, list cap 4 Mi nodes, within 16 GiB of HBM per workspace
-  const uint64_t cap2 = (std::min<uint64_t>(nn, s->interp_cap2 ? s->interp_cap2 : 1ull << 22) + 3) & ~3ull;  // keeps the pass-3 region 16-B aligned
-  const uint64_t per2 = slot_bytes + (words + cap2) * 4;
+  static_assert((STACK_CAP * sizeof(Frame) + MEMO_CAP * sizeof(MemoEnt)) % 16 == 0, "tables follow the slots 16-B aligned");
+  // pass 2: 4 slots per CU, each a visited hash + list of cap2 nodes (default 256 Ki: ~3 MB a slot)
+  const uint64_t cap2 = (std::min<uint64_t>(nn, s->interp_cap2 ? s->interp_cap2 : 1ull << 18) + 3) & ~3ull;
+  uint64_t tsize = 64;
+  while (tsize < 2 * cap2 + 128) tsize <<= 1;
+  const uint64_t per2 = slot_bytes + (tsize + cap2) * 4;
   // pass-2 budget: 16 GiB, or an eighth of the free HBM when less (other streams' workspaces and
   // the snapshot share the device); a pool that already exists keeps its layout
   uint64_t budget2 = 16ull << 30;
@@ -582,9 +604,9 @@ int launch_general(Snapshot* s, Workspace* w, const kg_query* d_q, const RQuery*
   } else {
     budget2 = (w->interp_layout >> 40) * per2;
   }
-  uint32_t slots2 = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)s->n_cu, budget2 / per2));
+  uint32_t slots2 = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)s->n_cu * 4, budget2 / per2));
   const size_t bytes1 = (size_t)slots1 * slot_bytes;
-  const size_t bytes3 = nn * 4;  // pass 3 reuses pass-2 slot 0 (clear once pass 2 is done) + a full list
+  const size_t bytes3 = slot_bytes + (words + nn) * 4;
   const size_t tail = (size_t)std::max<uint32_t>(n_queries, 1) * 4;
   size_t need = bytes1 + (size_t)slots2 * per2 + bytes3 + tail;
   if (need > w->interp_pool_bytes) {
@@ -599,36 +621,36 @@ int launch_general(Snapshot* s, Workspace* w, const kg_query* d_q, const RQuery*
       need = bytes1 + (size_t)slots2 * per2 + bytes3 + tail;
     }
     HIPC(e);
-    HIPC(hipMemsetAsync(w->interp_pool, 0, need, stream));  // memo tags 0 = empty; bitmaps clear
+    HIPC(hipMemsetAsync(w->interp_pool, 0, need, stream));  // memo tags 0 = empty; tables clear
     w->interp_pool_bytes = need;
-  } else if (w->interp_layout != (((uint64_t)slots2 << 40 | (uint64_t)slots1 << 24 | cap2))) {
-    HIPC(hipMemsetAsync(w->interp_pool, 0, need, stream));  // regions moved: bitmaps must start clear
+  } else if (w->interp_layout != ((uint64_t)slots2 << 40 | (uint64_t)slots1 << 24 | cap2)) {
+    HIPC(hipMemsetAsync(w->interp_pool, 0, need, stream));  // regions moved: tables must start clear
   }
+  w->interp_layout = (uint64_t)slots2 << 40 | (uint64_t)slots1 << 24 | cap2;
   const size_t bytes2 = (size_t)slots2 * per2;
-  w->interp_layout = ((uint64_t)slots2 << 40 | (uint64_t)slots1 << 24 | cap2);
   char* p = (char*)w->interp_pool;
   Frame* stacks1 = (Frame*)p;
   MemoEnt* memos1 = (MemoEnt*)(p + (size_t)slots1 * STACK_CAP * sizeof(Frame));
   char* p2 = p + bytes1;
   Frame* stacks2 = (Frame*)p2;
   MemoEnt* memos2 = (MemoEnt*)(p2 + (size_t)slots2 * STACK_CAP * sizeof(Frame));
-  uint32_t* bm2 = (uint32_t*)(p2 + (size_t)slots2 * slot_bytes);
-  uint32_t* lists2 = bm2 + (size_t)slots2 * words;
+  uint32_t* tabs2 = (uint32_t*)(p2 + (size_t)slots2 * slot_bytes);
+  uint32_t* lists2 = tabs2 + (size_t)slots2 * tsize;
   char* p3 = p2 + bytes2;
-  Frame* stack3 = stacks2;
-  MemoEnt* memo3 = memos2;
-  uint32_t* bm3 = bm2;
-  uint32_t* list3 = (uint32_t*)p3;
+  Frame* stack3 = (Frame*)p3;
+  MemoEnt* memo3 = (MemoEnt*)(p3 + STACK_CAP * sizeof(Frame));
+  uint32_t* bm3 = (uint32_t*)(p3 + slot_bytes);
+  uint32_t* list3 = bm3 + words;
   uint32_t* p3_list = (uint32_t*)(p3 + bytes3);
   const uint64_t tag = (uint64_t)(++s->batch_seq) << 32;
   hipLaunchKernelGGL(k_interp_lds, dim3(grid1), dim3(256), 0, stream, s->ds, d_q, rq, gen_list, ic, out, err, stacks1,
                      memos1, tag);
   HIPC(hipGetLastError());
-  hipLaunchKernelGGL(k_interp_hbm, dim3(slots2), dim3(64), 0, stream, s->ds, d_q, rq, ic, 2, p3_list, out, err,
-                     stacks2, memos2, bm2, words, lists2, cap2, tag);
+  hipLaunchKernelGGL(k_interp_hash, dim3(slots2), dim3(64), 0, stream, s->ds, d_q, rq, ic, p3_list, out, err, stacks2,
+                     memos2, tabs2, tsize, lists2, cap2, tag);
   HIPC(hipGetLastError());
-  hipLaunchKernelGGL(k_interp_hbm, dim3(1), dim3(64), 0, stream, s->ds, d_q, rq, ic, 3, p3_list, out, err, stack3,
-                     memo3, bm3, words, list3, nn, tag);
+  hipLaunchKernelGGL(k_interp_hbm, dim3(1), dim3(64), 0, stream, s->ds, d_q, rq, ic, p3_list, out, err, stack3, memo3,
+                     bm3, words, list3, nn, tag);
   HIPC(hipGetLastError());
   (void)gen_count;
   return 0;

@@ -84,8 +84,8 @@ struct Snapshot {
   uint32_t stream_ecap = 0;  // kg_snapshot_tune("stream_ecap"): k_stream edge budget per query (0 = none)
   int grid_wgs = 16;         // kg_snapshot_tune("grid_wgs"): k_grid_level workgroups per CU
   int stream_wgs = 0;        // kg_snapshot_tune("stream_wgs"): k_stream workgroups per CU (0 = by LDS)
-  int interp_wgs = 8;        // kg_snapshot_tune("interp_wgs"): k_interp_lds workgroups (4 waves) per CU (6 resident by LDS)
-  uint32_t interp_cap2 = 0;  // kg_snapshot_tune("interp_cap2"): pass-2 BFS list cap of the rewrite path (0 = 4 Mi)
+  int interp_wgs = 6;        // kg_snapshot_tune("interp_wgs"): k_interp_lds workgroups (4 waves) per CU (6 fit the LDS)
+  uint32_t interp_cap2 = 0;  // kg_snapshot_tune("interp_cap2"): pass-2 BFS list cap of the rewrite path (0 = 256 Ki)
   int back_wgs = 3;          // kg_snapshot_tune("back_wgs"): k_back workgroups per CU (1..3, LDS allows 3)
 
   ~Snapshot();

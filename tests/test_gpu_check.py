@@ -333,3 +333,29 @@ def test_synthetic_c3_rewrites_vs_oracle(n_tuples, gmax, cap2):
     assert 0.05 < (out == 1).mean() < 0.95 and (out == 2).sum() == 0
     dfs, _, _ = oracle.check_batch(q[:, :6], q[:, 6].view(np.int32), gmax, POLICY_DFS, nthreads=8)
     assert (dfs == exp).all()  # rewrites sit outside every visited scope: schedule-invariant
+
+
+@pytest.mark.parametrize("cap2", [0, 32, 700])
+def test_rewrite_bfs_beyond_lds(cap2):
+    # a computed-subject-set rewrite above a rewrite-free subtree of ~3,700 nodes: the
+    # interpreter's BFS run outgrows the LDS pass (512 nodes) and reruns in the many-slot HBM hash
+    # pass; cap2 = 32 / 700 make that pass overflow too, so the query finishes in pass 3
+    nss = [Namespace("g", [Relation("m"), Relation("v", rewrite=SubjectSetRewrite([ComputedSubjectSet("m")]))])]
+    tuples = [RelationTuple.from_string(f"g:root#m@(g:c{i}#m)") for i in range(3000)]
+    tuples += [RelationTuple.from_string(f"g:c{i}#m@(g:d{i % 700}#m)") for i in range(3000)]
+    tuples += [RelationTuple.from_string("g:d699#m@target"), RelationTuple.from_string("g:c5#m@near")]
+    reg = Registry(tuples, nss)
+    reg.snapshot.tune("interp_cap2", cap2)
+    e = reg.permission_engine()
+    it = reg.interner
+    qs = [RelationTuple.from_string(s) for s in
+          ["g:root#v@target", "g:root#v@near", "g:root#v@nobody", "g:c1#v@target", "g:root#m@target",
+           "g:root#v@(g:d3#m)", "g:c9#v@nobody"]]
+    q6 = np.asarray([it.tuple_ids(t) for t in qs], np.uint32)
+    oracle = Oracle(it.tuples_array(tuples), it.wildcard_rel, reg.program)
+    for gmax in (2, 3, 4, 6):
+        e.config.max_read_depth = gmax
+        for rep in range(2):  # the second batch reuses slots whose tables the first one left
+            out, err = e.batch_check_ids(queries_array(q6, 0), with_stats=True)
+            exp, oerr, _ = oracle.check_batch(q6, np.zeros(len(qs), np.int32), gmax, POLICY_CANONICAL)
+            assert list(out) == list(exp) and list(err) == list(oerr), (gmax, rep, out, exp)
