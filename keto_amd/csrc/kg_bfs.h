@@ -145,37 +145,43 @@ constexpr int VIS_LOG2 = 10;  // LDS visited-hash slots per wave
 constexpr int VIS = 1 << VIS_LOG2;
 constexpr int LIST = 512;  // LDS BFS list per wave (visited cap; hash load <= 0.5)
 
-struct WaveLds {
-  uint32_t vis[VIS];
-  uint32_t list[LIST];
+template <int VL2 = VIS_LOG2, int LST = LIST>
+struct WaveLdsT {
+  uint32_t vis[1 << VL2];
+  uint32_t list[LST];
   uint32_t pref[64];
 };
+using WaveLds = WaveLdsT<>;
 
-struct LdsStore {
-  WaveLds* L;
+template <int VL2 = VIS_LOG2, int LST = LIST>
+struct LdsStoreT {
+  static constexpr int NV = 1 << VL2;
+  static_assert(LST + 64 < NV, "the list cap keeps the visited hash below full");
+  WaveLdsT<VL2, LST>* L;
   __device__ uint32_t* list() const { return L->list; }
   __device__ uint32_t* pref() const { return L->pref; }
-  __device__ uint64_t cap() const { return LIST; }
+  __device__ uint64_t cap() const { return LST; }
   __device__ void reset() {
     const int lane = lane_id();
-    for (int i = lane * 4; i < VIS; i += 256) *reinterpret_cast<uint4*>(&L->vis[i]) = make_uint4(NONE, NONE, NONE, NONE);
+    for (int i = lane * 4; i < NV; i += 256) *reinterpret_cast<uint4*>(&L->vis[i]) = make_uint4(NONE, NONE, NONE, NONE);
     __builtin_amdgcn_wave_barrier();
   }
   // Bounded probe: callers check the list cap after every 64-wide step, so the table never holds
-  // more than LIST + 64 < VIS keys; the bound only guarantees termination.
+  // more than LST + 64 < NV keys; the bound only guarantees termination.
   __device__ bool insert(uint32_t key) {
-    uint32_t h = (key * 2654435761u) >> (32 - VIS_LOG2);
-    for (int p = 0; p < VIS; p++) {
+    uint32_t h = (key * 2654435761u) >> (32 - VL2);
+    for (int p = 0; p < NV; p++) {
       uint32_t old = atomicCAS(&L->vis[h], NONE, key);
       if (old == NONE) return true;
       if (old == key) return false;
-      h = (h + 1) & (VIS - 1);
+      h = (h + 1) & (NV - 1);
     }
     return true;
   }
   __device__ void sync() { __builtin_amdgcn_wave_barrier(); }
   __device__ void finish(uint32_t) {}
 };
+using LdsStore = LdsStoreT<>;
 
 // HBM tier: visited bitmap (n_nodes bits, left all-clear between runs) + BFS list; LDS prefix.
 struct GlobalStore {

@@ -453,14 +453,18 @@ __device__ void finish_query(uint32_t qi, int r, uint32_t e, uint8_t* out, uint3
   if (err) err[qi] = r == R_ERR ? e : KG_ERR_NONE;
 }
 
-// Pass 1 (LDS BFS tier): persistent grid, per-XCD dequeue over the GENERAL list.
+// Pass 1 (LDS BFS tier): persistent grid, per-XCD dequeue over the GENERAL list.  1024-slot hash +
+// 512-node list per wave (6.3 KB; a 512 / 256 variant that fits 8 workgroups per CU measured the
+// same on C3: the extra resident waves were offset by more queries reaching pass 2).
+constexpr int ILDS_VL2 = VIS_LOG2, ILDS_LIST = LIST;
+using ILdsStore = LdsStoreT<ILDS_VL2, ILDS_LIST>;
 __global__ __launch_bounds__(256) void k_interp_lds(DevSnap s, const kg_query* __restrict__ oq,
                                                     const RQuery* __restrict__ rq, const uint32_t* gen_list,
                                                     InterpCtl* ic, uint8_t* out, uint32_t* err, Frame* stacks,
                                                     MemoEnt* memos, uint64_t batch_tag) {
-  __shared__ WaveLds lds_all[4];
+  __shared__ WaveLdsT<ILDS_VL2, ILDS_LIST> lds_all[4];
   const int wave = threadIdx.x >> 6, lane = lane_id();
-  LdsStore st{&lds_all[wave]};
+  ILdsStore st{&lds_all[wave]};
   const uint32_t slot = blockIdx.x * 4 + wave;
   Frame* stack = stacks + (size_t)slot * STACK_CAP;
   MemoEnt* memo = memos + (size_t)slot * MEMO_CAP;
@@ -491,7 +495,7 @@ __global__ __launch_bounds__(256) void k_interp_lds(DevSnap s, const kg_query* _
     if (r == Q_OVERFLOW) {
       if (lane == 0) ic->p2_list[atomicAdd(&ic->p2_count, 1u)] = qi;
     } else {
-      finish_query<LdsStore>(qi, r, e, out, err);
+      finish_query<ILdsStore>(qi, r, e, out, err);
       done++;
     }
   }
