@@ -41,7 +41,8 @@ struct ExpCtl {
   uint32_t overflow;     // arena exhausted
   uint32_t p2_count, p2_head;
   uint32_t head;         // pass-1 dequeue
-  uint32_t pad[3];
+  uint32_t p3_count, p3_head;  // pass-3 (full bitmap) queue: pass-2 overflows
+  uint32_t pad;
   unsigned long long records;
 };
 
@@ -269,33 +270,62 @@ __global__ __launch_bounds__(256) void k_expand_lds(DevSnap s, const kg_set* __r
   if (lane == 0) atomicAdd(&ctl->records, recs);
 }
 
-// Pass 2: HBM bitmap visited sets; marks are always recorded in the list so they can be cleared.
-__global__ __launch_bounds__(64) void k_expand_hbm(DevSnap s, const kg_set* __restrict__ roots, int32_t global,
-                                                   ExpCtl* ctl, RootOut* outs, kg_tree_node* arena, uint32_t* next,
-                                                   uint32_t n_chunks, ExpFrame* stacks, uint32_t stack_cap,
-                                                   const uint32_t* p2_list, uint32_t* bitmaps, uint64_t words,
-                                                   uint32_t* lists, uint64_t cap) {
-  __shared__ uint32_t pref[64];
+// Passes 2 and 3: one wave per slot over a queue of roots.  Pass 2 (many slots): bounded HBM
+// visited hash + list (HashStore); a root that overflows it zeroes its table (keys inserted but
+// never listed would stay behind) and moves to pass 3.  Pass 3 (one slot): HBM bitmap over the
+// whole graph + a list that holds every node; marks are always listed so they can be cleared.
+template <class Store>
+__device__ void expand_slot_loop(const DevSnap& s, const kg_set* __restrict__ roots, int32_t global, ExpCtl* ctl,
+                                 RootOut* outs, kg_tree_node* arena, uint32_t* next, uint32_t n_chunks,
+                                 ExpFrame* stack, const uint32_t* qlist, uint32_t count, uint32_t* head, Store& st,
+                                 uint32_t* clear_base, uint64_t clear_words, uint32_t* p3_list) {
   const int lane = lane_id();
-  GlobalStore st{bitmaps + (size_t)blockIdx.x * words, lists + (size_t)blockIdx.x * cap, cap, pref};
-  ExpFrame* stack = stacks + (size_t)blockIdx.x * stack_cap;
   Stream S{arena, next, n_chunks, ctl, 0, 0, 0, true};
   unsigned long long recs = 0;
-  const uint32_t count = ctl->p2_count;
   for (;;) {
     uint32_t k = 0;
-    if (lane == 0) k = atomicAdd(&ctl->p2_head, 1u);
+    if (lane == 0) k = atomicAdd(head, 1u);
     k = __shfl(k, 0, 64);
     if (k >= count) break;
-    const uint32_t ri = p2_list[k];
+    const uint32_t ri = qlist[k];
     uint32_t nr = 0;
     const int r = expand_root(s, st, roots[ri], global, stack, S, nr);
+    if (r == EXP_OVERFLOW && p3_list) {
+      uint4* b4 = reinterpret_cast<uint4*>(clear_base);  // clear_words: multiple of 4, 16-B aligned
+      for (uint64_t i = lane; i < clear_words / 4; i += 64) b4[i] = make_uint4(0, 0, 0, 0);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      if (lane == 0) p3_list[atomicAdd(&ctl->p3_count, 1u)] = ri;
+      continue;
+    }
     if (lane == 0) {
       outs[ri] = r == EXP_OK ? RootOut{S.first, nr} : RootOut{NONE, 0xFFFFFFFFu};
       recs += nr;
     }
   }
   if (lane == 0) atomicAdd(&ctl->records, recs);
+}
+
+__global__ __launch_bounds__(64) void k_expand_hash(DevSnap s, const kg_set* __restrict__ roots, int32_t global,
+                                                    ExpCtl* ctl, RootOut* outs, kg_tree_node* arena, uint32_t* next,
+                                                    uint32_t n_chunks, ExpFrame* stacks, uint32_t stack_cap,
+                                                    const uint32_t* p2_list, uint32_t* tabs, uint64_t tsize,
+                                                    uint32_t* lists, uint64_t cap, uint32_t* p3_list) {
+  __shared__ uint32_t pref[64];
+  uint32_t* tab = tabs + (size_t)blockIdx.x * tsize;
+  HashStore st{tab, (uint32_t)(tsize - 1), lists + (size_t)blockIdx.x * cap, cap, pref};
+  expand_slot_loop(s, roots, global, ctl, outs, arena, next, n_chunks, stacks + (size_t)blockIdx.x * stack_cap, p2_list,
+                   ctl->p2_count, &ctl->p2_head, st, tab, tsize, p3_list);
+}
+
+__global__ __launch_bounds__(64) void k_expand_hbm(DevSnap s, const kg_set* __restrict__ roots, int32_t global,
+                                                   ExpCtl* ctl, RootOut* outs, kg_tree_node* arena, uint32_t* next,
+                                                   uint32_t n_chunks, ExpFrame* stack, const uint32_t* p3_list,
+                                                   uint32_t* bm, uint64_t words, uint32_t* list, uint64_t cap) {
+  __shared__ uint32_t pref[64];
+  GlobalStore st{bm, list, cap, pref};
+  expand_slot_loop(s, roots, global, ctl, outs, arena, next, n_chunks, stack, p3_list, ctl->p3_count, &ctl->p3_head, st,
+                   bm, words, nullptr);
 }
 
 __global__ void k_expand_compact(const RootOut* outs, uint32_t n, const uint64_t* off, const kg_tree_node* arena,
@@ -326,8 +356,13 @@ int expand_batch(Snapshot* s, const kg_set* roots, size_t n, int32_t global, kg_
   // device buffers for this call
   const uint32_t stack_cap = (uint32_t)std::min<int64_t>(0x8000, (int64_t)global + 2);
   const uint32_t grid1 = (uint32_t)s->n_cu * 2, slots1 = grid1 * 4;
-  const uint64_t nn = std::max<uint32_t>(s->ds.n_nodes, 1), words = (nn + 31) / 32 + 1;
-  const uint32_t slots2 = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(32, (2ull << 30) / ((words + nn) * 4)));
+  const uint64_t nn = std::max<uint32_t>(s->ds.n_nodes, 1), words = ((nn + 31) / 32 + 1 + 3) & ~3ull;
+  // pass 2: 2 slots per CU, each a visited hash + list of up to 256 Ki nodes (~5 MB a slot, <= 2 GiB)
+  const uint64_t cap2 = (std::min<uint64_t>(nn, 1ull << 18) + 3) & ~3ull;
+  uint64_t tsize = 64;
+  while (tsize < 2 * cap2 + 128) tsize <<= 1;
+  const uint32_t slots2 =
+      (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)s->n_cu * 2, (2ull << 30) / ((tsize + cap2) * 4)));
   uint32_t n_chunks = (uint32_t)std::min<uint64_t>(1u << 22, std::max<uint64_t>(4096, n * 2 + slots1));
   kg_set* d_roots = nullptr;
   ExpCtl* ctl = nullptr;
@@ -343,12 +378,14 @@ int expand_batch(Snapshot* s, const kg_set* roots, size_t n, int32_t global, kg_
   if ((e = hipMalloc(&d_roots, n * sizeof(kg_set))) != hipSuccess) fail("hipMalloc", e);
   if (!rc && (e = hipMalloc(&ctl, sizeof(ExpCtl))) != hipSuccess) fail("hipMalloc", e);
   if (!rc && (e = hipMalloc(&outs, n * sizeof(RootOut))) != hipSuccess) fail("hipMalloc", e);
-  if (!rc && (e = hipMalloc(&stacks, (size_t)(slots1 + slots2) * stack_cap * sizeof(ExpFrame))) != hipSuccess)
+  if (!rc && (e = hipMalloc(&stacks, (size_t)(slots1 + slots2 + 1) * stack_cap * sizeof(ExpFrame))) != hipSuccess)
     fail("hipMalloc", e);
-  if (!rc && (e = hipMalloc(&p2, n * 4)) != hipSuccess) fail("hipMalloc", e);
-  if (!rc && (e = hipMalloc(&bm, (size_t)slots2 * (words + nn) * 4)) != hipSuccess) fail("hipMalloc", e);
+  if (!rc && (e = hipMalloc(&p2, n * 8)) != hipSuccess) fail("hipMalloc", e);  // pass-2 | pass-3 queues
+  // [pass-2 tables | pass-3 bitmap] (cleared together every attempt) | pass-2 lists | pass-3 list
+  const size_t clear_words = (size_t)slots2 * tsize + words;
+  if (!rc && (e = hipMalloc(&bm, (clear_words + (size_t)slots2 * cap2 + nn) * 4)) != hipSuccess) fail("hipMalloc", e);
   if (!rc) {
-    lists = bm + (size_t)slots2 * words;
+    lists = bm + clear_words;
     if ((e = hipMemcpyAsync(d_roots, roots, n * sizeof(kg_set), hipMemcpyHostToDevice, stream)) != hipSuccess)
       fail("H2D", e);
   }
@@ -368,7 +405,7 @@ int expand_batch(Snapshot* s, const kg_set* roots, size_t n, int32_t global, kg_
       break;
     }
     // every attempt starts from clear visited bitmaps (an arena overflow aborts roots mid-way)
-    if ((e = hipMemsetAsync(bm, 0, (size_t)slots2 * words * 4, stream)) != hipSuccess ||
+    if ((e = hipMemsetAsync(bm, 0, clear_words * 4, stream)) != hipSuccess ||
         (e = hipMemsetAsync(ctl, 0, sizeof(ExpCtl), stream)) != hipSuccess) {
       fail("memset", e);
       break;
@@ -376,8 +413,11 @@ int expand_batch(Snapshot* s, const kg_set* roots, size_t n, int32_t global, kg_
     (void)hipEventRecord(ev[0], stream);
     hipLaunchKernelGGL(k_expand_lds, dim3(grid1), dim3(256), 0, stream, s->ds, d_roots, (uint32_t)n, global, ctl, outs,
                        arena, next, n_chunks, stacks, stack_cap, p2);
-    hipLaunchKernelGGL(k_expand_hbm, dim3(slots2), dim3(64), 0, stream, s->ds, d_roots, global, ctl, outs, arena, next,
-                       n_chunks, stacks + (size_t)slots1 * stack_cap, stack_cap, p2, bm, words, lists, nn);
+    hipLaunchKernelGGL(k_expand_hash, dim3(slots2), dim3(64), 0, stream, s->ds, d_roots, global, ctl, outs, arena,
+                       next, n_chunks, stacks + (size_t)slots1 * stack_cap, stack_cap, p2, bm, tsize, lists, cap2, p2 + n);
+    hipLaunchKernelGGL(k_expand_hbm, dim3(1), dim3(64), 0, stream, s->ds, d_roots, global, ctl, outs, arena, next,
+                       n_chunks, stacks + (size_t)(slots1 + slots2) * stack_cap, p2 + n, bm + (size_t)slots2 * tsize,
+                       words, lists + (size_t)slots2 * cap2, nn);
     (void)hipEventRecord(ev[1], stream);
     if ((e = hipGetLastError()) != hipSuccess) {
       fail("launch", e);
