@@ -357,7 +357,8 @@ int expand_batch(Snapshot* s, const kg_set* roots, size_t n, int32_t global, kg_
   const uint32_t stack_cap = (uint32_t)std::min<int64_t>(0x8000, (int64_t)global + 2);
   const uint32_t grid1 = (uint32_t)s->n_cu * 2, slots1 = grid1 * 4;
   const uint64_t nn = std::max<uint32_t>(s->ds.n_nodes, 1), words = ((nn + 31) / 32 + 1 + 3) & ~3ull;
-  // pass 2: 2 slots per CU, each a visited hash + list of up to 256 Ki nodes (~5 MB a slot, <= 2 GiB)
+  // pass 2: 2 slots per CU, each a visited hash + list of up to 256 Ki nodes (~5 MB a slot, <= 2 GiB;
+  // 4 per CU measured the same on C5)
   const uint64_t cap2 = (std::min<uint64_t>(nn, 1ull << 18) + 3) & ~3ull;
   uint64_t tsize = 64;
   while (tsize < 2 * cap2 + 128) tsize <<= 1;
