@@ -59,7 +59,7 @@ class CheckBatcher:
         return f
 
     def submit(self, t: RelationTuple, rest_depth: int) -> Future:
-        it = self.engine.snapshot.interner
+        it = getattr(self.engine, "interner", None) or self.engine.snapshot.interner  # a live engine: no rebuild
         return self.submit_ids(queries_array(np.asarray(it.tuple_ids(t), np.uint32), rest_depth)[0])
 
     def check_is_member(self, t: RelationTuple, rest_depth: int, timeout: Optional[float] = None) -> bool:

@@ -200,6 +200,10 @@ class _LiveEngine(Engine):
     def snapshot(self, _v) -> None:
         pass
 
+    @property
+    def interner(self) -> Interner:
+        return self._p.interner
+
     def batch_check_ids(self, q, with_stats: bool = False):
         e = Engine(self._p.snapshot(), self.config)
         try:
