@@ -80,17 +80,8 @@ def bench_expand(a):
     L = _lib.load()
     torch.cuda.set_device(0)
     snap = Snapshot.synthetic(int(a.tuples), seed=a.seed, device=0)
-    ids = snap.synth_ids()
-    n_docs, n_groups = ids["n_docs"], ids["n_groups"]
-    gpl = n_groups // 8
-    r = np.arange(a.roots, dtype=np.uint64)
-    layer, rank = r % 8, r // 8
-    node = n_docs + layer * gpl + (rank * 2654435761 + 12345) % gpl  # popularity rank -> group (kg_synth.h)
-    roots = np.zeros((a.roots, 4), np.uint32)
-    roots[:, 0] = 1  # ns group
-    roots[:, 1] = node.astype(np.uint32)  # group object id == node id
-    roots[:, 2] = 2  # rel member
-    roots[:, 3] = 0  # request depth 0 -> global
+    from keto_amd.synth import hot_group_roots
+    roots = hot_group_roots(snap.synth_ids(), a.roots)
     depth = a.global_depth if a.global_depth != 10 else 5
 
     def step():

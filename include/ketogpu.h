@@ -215,18 +215,21 @@ int kg_synth_queries(kg_snapshot* s, uint64_t seed, size_t n, kg_query* d_q);
  * For graphs larger than one GPU: rank r of N holds the rows of the nodes (ns, obj, rel) with
  * kg_shard_owner(ns, obj, N) == r (all relations of an object on one rank).  A batch is a
  * level-synchronous BFS across ranks: every level each rank processes the frontier records it
- * received (nodes it owns, or hit reports for queries it is home of) and writes the next level's
- * records into one bucket per destination rank; the caller exchanges the buckets (all-to-all,
- * RCCL over xGMI) and calls kg_shard_level again until no rank sends anything.  Replaces the
- * single-GPU kg_check_batch for such snapshots (rewrite-free namespaces only; a snapshot with a
- * rewrite program returns KG_ERR_NOT_IMPLEMENTED codes).  keto_amd/sharded.py is the driver. */
+ * received (nodes it owns, or hit / error reports for queries it is home of) and writes the next
+ * level's records into one bucket per destination rank; the caller exchanges the buckets
+ * (all-to-all, RCCL over xGMI) and calls kg_shard_level again until no rank sends anything, then
+ * kg_shard_finish.  Replaces the single-GPU kg_check_batch for such snapshots.  Rewrites are not
+ * evaluated in this mode: a query that reaches a node whose relation has a rewrite or is
+ * undeclared ends as KG_ERROR / KG_ERR_NOT_IMPLEMENTED.  keto_amd/sharded.py is the driver. */
 typedef struct {
   uint32_t q;     /* home rank << 26 | index in the home rank's batch                         */
-  uint32_t node;  /* node to check (checkIsAllowed(node, depth)), or KG_FREC_HIT              */
-  uint32_t subj;  /* tagged subject: bit31 set = subject-set node id, else subject id        */
+  uint32_t node;  /* node to check (checkIsAllowed(node, depth)), KG_FREC_HIT or KG_FREC_ERR  */
+  uint32_t subj;  /* tagged subject: bit31 set = subject-set node id, else subject id;
+                     the err code of a KG_FREC_ERR record                                     */
   int32_t depth;  /* rest depth (>= 1)                                                        */
 } kg_frec;
 #define KG_FREC_HIT 0xFFFFFFFFu /* kg_frec.node of a record reporting IsMember to the query's home */
+#define KG_FREC_ERR 0xFFFFFFFEu /* kg_frec.node of a record reporting an error (code in subj)     */
 #define KG_SHARD_MAX_RANKS 64
 
 uint32_t kg_shard_owner(uint32_t ns, uint32_t obj, uint32_t nranks);
@@ -238,11 +241,15 @@ int kg_snapshot_synthetic_shard(const kg_synth_params* params, const kg_rewrite_
  * per bucket (true counts: > cap means the bucket overflowed and the batch must be rerun with a
  * larger cap) and, in [nranks], overflow flags (1 bucket, 2 visited table).  kg_shard_seed zeroes
  * d_res (0 NotMember, 1 IsMember) / d_err and the counters; kg_shard_level zeroes the counters
- * before writing.  Both only enqueue work on `stream` (NULL = the snapshot's stream). */
+ * before writing.  d_n_in: when non-NULL the level reads its record count from device memory
+ * (n_in is then only an upper bound), so levels can be enqueued without a host round trip.
+ * kg_shard_finish sets d_res[i] = KG_ERROR where d_err[i] != 0.  All of them only enqueue work
+ * on `stream` (NULL = the snapshot's stream). */
 int kg_shard_seed(kg_snapshot* s, const kg_query* d_q, size_t n, int32_t global_max_depth, kg_frec* d_out,
                   size_t cap, uint32_t* d_counts, uint8_t* d_res, uint32_t* d_err, void* stream);
-int kg_shard_level(kg_snapshot* s, const kg_frec* d_in, size_t n_in, kg_frec* d_out, size_t cap,
-                   uint32_t* d_counts, uint8_t* d_res, void* stream);
+int kg_shard_level(kg_snapshot* s, const kg_frec* d_in, size_t n_in, const uint32_t* d_n_in, kg_frec* d_out,
+                   size_t cap, uint32_t* d_counts, uint8_t* d_res, uint32_t* d_err, void* stream);
+int kg_shard_finish(kg_snapshot* s, size_t n, uint8_t* d_res, const uint32_t* d_err, void* stream);
 
 /* ---- expand ----------------------------------------------------------------------------- */
 int kg_expand_batch(kg_snapshot* s, const kg_set* roots, size_t n, int32_t global_max_depth, kg_tree_buf* out);

@@ -11,6 +11,7 @@ LIB_PATH = os.path.join(HERE, "lib", "libketogpu.so")
 KG_SUBJECT_ID = 0xFFFFFFFF
 KG_NOT_MEMBER, KG_IS_MEMBER, KG_ERROR = 0, 1, 2
 KG_FREC_HIT = 0xFFFFFFFF
+KG_FREC_ERR = 0xFFFFFFFE
 KG_SHARD_MAX_RANKS = 64
 KG_ERR_NONE, KG_ERR_RELATION_NOT_FOUND, KG_ERR_NOT_IMPLEMENTED, KG_ERR_REWRITE_CYCLE, KG_ERR_RESOURCE = 0, 1, 2, 3, 4
 
@@ -75,7 +76,7 @@ class kg_synth_params(C.Structure):
 EXPORTS = ["kg_snapshot_create", "kg_snapshot_synthetic", "kg_snapshot_destroy", "kg_snapshot_info", "kg_snapshot_tune", "kg_synth_ids",
            "kg_snapshot_export", "kg_snapshot_export_csr", "kg_check_batch", "kg_check_batch_device", "kg_synth_queries", "kg_expand_batch",
            "kg_tree_free", "kg_last_error", "kg_version", "kg_shard_owner", "kg_snapshot_create_shard",
-           "kg_snapshot_synthetic_shard", "kg_shard_seed", "kg_shard_level"]
+           "kg_snapshot_synthetic_shard", "kg_shard_seed", "kg_shard_level", "kg_shard_finish"]
 
 
 class KetoGPUError(RuntimeError):
@@ -122,10 +123,11 @@ def load(path: str = LIB_PATH):
     L.kg_snapshot_synthetic_shard.argtypes = [C.POINTER(kg_synth_params), C.POINTER(kg_rewrite_prog), C.c_int, u32,
                                               u32, C.POINTER(vp)]
     L.kg_shard_seed.argtypes = [vp, vp, sz, i32, vp, sz, vp, vp, vp, vp]
-    L.kg_shard_level.argtypes = [vp, vp, sz, vp, sz, vp, vp, vp]
+    L.kg_shard_level.argtypes = [vp, vp, sz, vp, vp, sz, vp, vp, vp, vp]
+    L.kg_shard_finish.argtypes = [vp, sz, vp, vp, vp]
     for name in ("kg_snapshot_create", "kg_snapshot_synthetic", "kg_snapshot_info", "kg_snapshot_tune", "kg_synth_ids", "kg_check_batch",
                  "kg_check_batch_device", "kg_synth_queries", "kg_expand_batch", "kg_snapshot_create_shard",
-                 "kg_snapshot_synthetic_shard", "kg_shard_seed", "kg_shard_level"):
+                 "kg_snapshot_synthetic_shard", "kg_shard_seed", "kg_shard_level", "kg_shard_finish"):
         getattr(L, name).restype = C.c_int
     _lib = L
     return L

@@ -14,6 +14,7 @@ its answer) that BASELINE.json's p99 metric names.
 """
 from __future__ import annotations
 
+import collections
 import threading
 import time
 from concurrent.futures import Future
@@ -31,6 +32,8 @@ class BatcherClosed(RuntimeError):
 
 
 class CheckBatcher:
+    STATS_WINDOW = 1 << 16  # latency / size samples kept (the most recent batches)
+
     def __init__(self, engine: Engine, max_batch: int = 1 << 16, max_wait_us: int = 200):
         if max_batch < 1 or max_wait_us < 0:
             raise ValueError("max_batch >= 1 and max_wait_us >= 0 required")
@@ -40,8 +43,9 @@ class CheckBatcher:
         self._cv = threading.Condition()
         self._pending: List[Tuple[np.ndarray, Future, float]] = []
         self._closed = False
-        self.batch_sizes: List[int] = []
-        self.batch_latency_s: List[float] = []
+        self.batch_sizes: "collections.deque[int]" = collections.deque(maxlen=self.STATS_WINDOW)
+        self.batch_latency_s: "collections.deque[float]" = collections.deque(maxlen=self.STATS_WINDOW)
+        self.cancelled = 0
         self._thread = threading.Thread(target=self._run, name="kg-check-batcher", daemon=True)
         self._thread.start()
 
@@ -71,19 +75,36 @@ class CheckBatcher:
 
     # ---- dispatcher
     def _take(self) -> List[Tuple[np.ndarray, Future, float]]:
-        with self._cv:
-            while not self._pending and not self._closed:
-                self._cv.wait()
-            if not self._pending:
-                return []
-            deadline = self._pending[0][2] + self.max_wait
-            while len(self._pending) < self.max_batch and not self._closed:
-                left = deadline - time.perf_counter()
-                if left <= 0:
-                    break
-                self._cv.wait(left)
-            batch, self._pending = self._pending[:self.max_batch], self._pending[self.max_batch:]
-            return batch
+        """The next batch of live (not cancelled) queries; [] once closed and drained."""
+        while True:
+            with self._cv:
+                while not self._pending and not self._closed:
+                    self._cv.wait()
+                if not self._pending:
+                    return []
+                deadline = self._pending[0][2] + self.max_wait
+                while len(self._pending) < self.max_batch and not self._closed:
+                    left = deadline - time.perf_counter()
+                    if left <= 0:
+                        break
+                    self._cv.wait(left)
+                batch, self._pending = self._pending[:self.max_batch], self._pending[self.max_batch:]
+            # a caller may have cancelled its future (directly, or through asyncio.wrap_future when its
+            # RPC was cancelled): drop it here, so result delivery never meets a cancelled future
+            live = [b for b in batch if b[1].set_running_or_notify_cancel()]
+            self.cancelled += len(batch) - len(live)
+            if live:
+                return live
+
+    @staticmethod
+    def _deliver(f: Future, result=None, exc: Optional[BaseException] = None) -> None:
+        try:  # one broken future must never end the dispatcher (every later submit would hang)
+            if exc is not None:
+                f.set_exception(exc)
+            else:
+                f.set_result(result)
+        except Exception:  # noqa: BLE001 -- InvalidStateError and the like
+            pass
 
     def _run(self) -> None:
         while True:
@@ -95,13 +116,13 @@ class CheckBatcher:
                 out, err = self.engine.batch_check_ids(q)
             except BaseException as e:  # the whole batch failed (library status): every caller sees it
                 for _, f, _t in batch:
-                    f.set_exception(e)
+                    self._deliver(f, exc=e)
                 continue
             done = time.perf_counter()
             self.batch_sizes.append(len(batch))
             self.batch_latency_s.append(done - batch[0][2])
             for i, (_, f, _t) in enumerate(batch):
-                f.set_result((int(out[i]), int(err[i])))
+                self._deliver(f, (int(out[i]), int(err[i])))
 
     # ---- lifecycle / stats
     def close(self) -> None:

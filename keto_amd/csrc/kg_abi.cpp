@@ -140,21 +140,30 @@ int kg_snapshot_synthetic_shard(const kg_synth_params* params, const kg_rewrite_
 int kg_shard_seed(kg_snapshot* sp, const kg_query* d_q, size_t n, int32_t global_max_depth, kg_frec* d_out, size_t cap,
                   uint32_t* d_counts, uint8_t* d_res, uint32_t* d_err, void* stream) {
   KG_GUARD_BEGIN
-  if (!sp || !d_counts || !d_res || (n && (!d_q || !d_out))) return set_error(-2, "NULL argument");
+  if (!sp || !d_counts || !d_res || !d_err || (n && (!d_q || !d_out))) return set_error(-2, "NULL argument");
   Snapshot* s = reinterpret_cast<Snapshot*>(sp);
   std::lock_guard<std::mutex> lk(s->mu);
   return kg::shard_seed(s, d_q, n, global_max_depth, d_out, cap, d_counts, d_res, d_err, (hipStream_t)stream);
   KG_GUARD_END
 }
 
-int kg_shard_level(kg_snapshot* sp, const kg_frec* d_in, size_t n_in, kg_frec* d_out, size_t cap, uint32_t* d_counts,
-                   uint8_t* d_res, void* stream) {
+int kg_shard_level(kg_snapshot* sp, const kg_frec* d_in, size_t n_in, const uint32_t* d_n_in, kg_frec* d_out,
+                   size_t cap, uint32_t* d_counts, uint8_t* d_res, uint32_t* d_err, void* stream) {
   KG_GUARD_BEGIN
-  if (!sp || !d_counts || !d_res || (n_in && (!d_in || !d_out))) return set_error(-2, "NULL argument");
+  if (!sp || !d_counts || !d_res || !d_err || (n_in && (!d_in || !d_out))) return set_error(-2, "NULL argument");
   Snapshot* s = reinterpret_cast<Snapshot*>(sp);
   std::lock_guard<std::mutex> lk(s->mu);
   if (!s->shard_vis) return set_error(-2, "kg_shard_level before kg_shard_seed");
-  return kg::shard_level(s, d_in, n_in, d_out, cap, d_counts, d_res, (hipStream_t)stream);
+  return kg::shard_level(s, d_in, n_in, d_n_in, d_out, cap, d_counts, d_res, d_err, (hipStream_t)stream);
+  KG_GUARD_END
+}
+
+int kg_shard_finish(kg_snapshot* sp, size_t n, uint8_t* d_res, const uint32_t* d_err, void* stream) {
+  KG_GUARD_BEGIN
+  if (!sp || (n && (!d_res || !d_err))) return set_error(-2, "NULL argument");
+  Snapshot* s = reinterpret_cast<Snapshot*>(sp);
+  std::lock_guard<std::mutex> lk(s->mu);
+  return kg::shard_finish(s, n, d_res, d_err, (hipStream_t)stream);
   KG_GUARD_END
 }
 

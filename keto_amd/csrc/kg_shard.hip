@@ -12,7 +12,11 @@
 //                   records (query, child, subject, depth - 1) for the children's owners
 // Between levels the driver (keto_amd/sharded.py) exchanges the per-destination buckets with an
 // all-to-all (RCCL over xGMI) and stops when no rank sends anything.  Semantics: bounded
-// reachability over rewrite-free nodes, exactly the single-GPU engine's.
+// reachability over rewrite-free nodes, exactly the single-GPU engine's.  A query
+// that reaches a node whose relation has a rewrite or is undeclared (relflag != 0: the
+// interpreter's territory, rewrites.go:30-260 / engine.go:228) is answered KG_ERROR with
+// KG_ERR_NOT_IMPLEMENTED, whatever else it reaches: the owner reports it to the home rank, which
+// records it in err[] (errors win over hits; kg_shard_finish folds err into res).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -80,11 +84,12 @@ __global__ __launch_bounds__(256) void k_shard_seed(DevSnap s, const kg_query* _
     int32_t d = x.max_depth;
     if (d <= 0 || global < d) d = global;  // engine.go:68-70
     res[i] = KG_NOT_MEMBER;
-    if (err) err[i] = KG_ERR_NONE;
+    err[i] = KG_ERR_NONE;
     if (relflag(s, x.t.ns, x.t.rel)) {  // rewrites are not part of the sharded mode
-      res[i] = KG_ERROR;
-      if (err) err[i] = KG_ERR_NOT_IMPLEMENTED;
-    } else if (node != NONE && subj != NONE) {
+      err[i] = KG_ERR_NOT_IMPLEMENTED;
+    } else if (node != NONE && (subj != NONE || s.relflags)) {
+      // an unknown subject can never be held, but with a namespace program the query can still
+      // reach a rewrite (an error), so it is seeded all the same (its probes are skipped)
       act = true;
       dest = s.nowner ? s.nowner[node] : 0u;
       r = kg_frec{(s.shard_rank << Q_BITS) | i, node, subj, d};
@@ -95,40 +100,51 @@ __global__ __launch_bounds__(256) void k_shard_seed(DevSnap s, const kg_query* _
 
 // One workgroup handles 256 received records per iteration; their set rows are expanded
 // edge-parallel (block scan of the row lengths, LDS owner search).
-__global__ __launch_bounds__(256) void k_shard_level(DevSnap s, const kg_frec* __restrict__ in, uint64_t n_in,
-                                                     kg_frec* out, uint64_t cap, uint32_t* counts, uint8_t* res,
-                                                     uint64_t* vis, uint64_t vmask) {
+__global__ __launch_bounds__(256) void k_shard_level(DevSnap s, const kg_frec* __restrict__ in, uint64_t n_bound,
+                                                     const uint32_t* d_n_in, kg_frec* out, uint64_t cap, uint32_t* counts, uint8_t* res,
+                                                     uint32_t* err, uint64_t* vis, uint64_t vmask) {
   __shared__ uint32_t s_pref[256], s_wsum[4];
   __shared__ uint64_t s_rb[256];
   __shared__ kg_frec s_rec[256];
   const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
   const uint32_t me = s.shard_rank;
+  // record count: from the previous level's counter on the device (clamped to the bucket: a count
+  // past it means dropped records, which the caller's overflow check turns into a rerun)
+  const uint64_t n_in = d_n_in ? min((uint64_t)*d_n_in, n_bound) : n_bound;
   for (uint64_t base = (uint64_t)blockIdx.x * 256; base < n_in; base += (uint64_t)gridDim.x * 256) {
     const uint64_t i = base + tid;
     kg_frec r{0, NONE, 0, 0};
-    bool hit_out = false;
+    bool hit_out = false, err_out = false;
     uint64_t rb = 0, len = 0;
     if (i < n_in) {
       r = in[i];
       if (r.node == KG_FREC_HIT) {
         if ((r.q >> Q_BITS) == me) res[r.q & Q_MASK] = KG_IS_MEMBER;
+      } else if (r.node == KG_FREC_ERR) {
+        if ((r.q >> Q_BITS) == me) atomicMax(&err[r.q & Q_MASK], r.subj);
       } else {
         const int ins = sv_insert(vis, vmask, ((uint64_t)r.q << 32) | r.node);
         if (ins < 0) atomicOr(&counts[s.shard_n], 2u);
-        if (ins > 0) {
-          if (r.depth >= 1 && dset_probe(s, r.node, r.subj)) {  // checkDirect(depth - 1)
+        if (ins > 0 && relflag(s, s.nd_ns[r.node], s.nd_rel[r.node]) != 0) {  // a rewrite / undeclared relation
+          if ((r.q >> Q_BITS) == me) atomicMax(&err[r.q & Q_MASK], (uint32_t)KG_ERR_NOT_IMPLEMENTED);
+          else err_out = true;
+        } else if (ins > 0) {
+          if (r.depth >= 1 && r.subj != NONE && dset_probe(s, r.node, r.subj)) {  // checkDirect(depth - 1)
             if ((r.q >> Q_BITS) == me) res[r.q & Q_MASK] = KG_IS_MEMBER;
             else hit_out = true;
-          } else if (r.depth >= 2) {  // children at depth - 1 >= 1 can still be probed
+          } else if (r.depth >= 2 || (r.depth == 1 && s.relflags)) {
+            // children at depth - 1 >= 1 can still be probed; children at depth 0 cannot, but
+            // checkIsAllowed(child, 0) still evaluates astRelationFor (engine.go:199-206), so with a
+            // namespace program their relation flags are checked (below) for the error report
             rb = s.adj_off[r.node];
             len = s.adj_off[r.node + 1] - rb;
           }
         }
       }
     }
-    // hit reports go to the query's home
-    kg_frec hr{r.q, KG_FREC_HIT, 0, 0};
-    emit(hit_out, r.q >> Q_BITS, hr, out, cap, counts, s.shard_n);
+    // hit and error reports go to the query's home
+    kg_frec hr{r.q, err_out ? KG_FREC_ERR : KG_FREC_HIT, err_out ? (uint32_t)KG_ERR_NOT_IMPLEMENTED : 0u, 0};
+    emit(hit_out || err_out, r.q >> Q_BITS, hr, out, cap, counts, s.shard_n);
     // expansion
     s_rb[tid] = rb;
     s_rec[tid] = r;
@@ -153,17 +169,34 @@ __global__ __launch_bounds__(256) void k_shard_level(DevSnap s, const kg_frec* _
       const bool act = e < total;
       kg_frec c{};
       uint32_t dest = 0;
+      bool send = false;
       if (act) {
         const int own = owner_search(s_pref, 256, e);
         const kg_frec& pr = s_rec[own];
         const uint32_t child = s.adj[s_rb[own] + (e - s_pref[own])];
-        c = kg_frec{pr.q, child, pr.subj, pr.depth - 1};
-        dest = s.nowner ? s.nowner[child] : 0u;
+        if (pr.depth >= 2) {
+          c = kg_frec{pr.q, child, pr.subj, pr.depth - 1};
+          dest = s.nowner ? s.nowner[child] : 0u;
+          send = true;
+        } else if (relflag(s, s.nd_ns[child], s.nd_rel[child]) != 0) {  // a depth-0 child with a rewrite
+          if ((pr.q >> Q_BITS) == me) {
+            atomicMax(&err[pr.q & Q_MASK], (uint32_t)KG_ERR_NOT_IMPLEMENTED);
+          } else {
+            c = kg_frec{pr.q, KG_FREC_ERR, (uint32_t)KG_ERR_NOT_IMPLEMENTED, 0};
+            dest = pr.q >> Q_BITS;
+            send = true;
+          }
+        }
       }
-      emit(act, dest, c, out, cap, counts, s.shard_n);
+      emit(send, dest, c, out, cap, counts, s.shard_n);
     }
     __syncthreads();
   }
+}
+
+__global__ void k_shard_finish(uint32_t n, uint8_t* res, const uint32_t* err) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n && err[i] != KG_ERR_NONE) res[i] = KG_ERROR;
 }
 
 static int shard_vis_prepare(Snapshot* s, hipStream_t stream) {
@@ -198,15 +231,25 @@ int shard_seed(Snapshot* s, const kg_query* d_q, size_t n, int32_t gdepth, kg_fr
   return 0;
 }
 
-int shard_level(Snapshot* s, const kg_frec* d_in, size_t n_in, kg_frec* d_out, size_t cap, uint32_t* d_counts,
-                uint8_t* d_res, hipStream_t stream) {
+int shard_level(Snapshot* s, const kg_frec* d_in, size_t n_in, const uint32_t* d_n_in, kg_frec* d_out, size_t cap,
+                uint32_t* d_counts, uint8_t* d_res, uint32_t* d_err, hipStream_t stream) {
   HIPC(hipSetDevice(s->device));
   if (!stream) stream = s->stream;
   HIPC(hipMemsetAsync(d_counts, 0, (s->shard_n + 1) * 4, stream));
   if (n_in) {
     const uint32_t grid = (uint32_t)std::min<uint64_t>((n_in + 255) / 256, (uint64_t)s->n_cu * 8);
-    hipLaunchKernelGGL(k_shard_level, dim3(grid), dim3(256), 0, stream, s->ds, d_in, (uint64_t)n_in, d_out,
-                       (uint64_t)cap, d_counts, d_res, (uint64_t*)s->shard_vis, s->shard_vis_slots - 1);
+    hipLaunchKernelGGL(k_shard_level, dim3(grid), dim3(256), 0, stream, s->ds, d_in, (uint64_t)n_in, d_n_in, d_out,
+                       (uint64_t)cap, d_counts, d_res, d_err, (uint64_t*)s->shard_vis, s->shard_vis_slots - 1);
+    HIPC(hipGetLastError());
+  }
+  return 0;
+}
+
+int shard_finish(Snapshot* s, size_t n, uint8_t* d_res, const uint32_t* d_err, hipStream_t stream) {
+  HIPC(hipSetDevice(s->device));
+  if (!stream) stream = s->stream;
+  if (n) {
+    hipLaunchKernelGGL(k_shard_finish, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, stream, (uint32_t)n, d_res, d_err);
     HIPC(hipGetLastError());
   }
   return 0;

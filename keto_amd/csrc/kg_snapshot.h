@@ -107,8 +107,9 @@ int synth_queries(Snapshot* s, uint64_t seed, size_t n, kg_query* d_q);
 // kg_shard.hip
 int shard_seed(Snapshot* s, const kg_query* d_q, size_t n, int32_t gdepth, kg_frec* d_out, size_t cap,
                uint32_t* d_counts, uint8_t* d_res, uint32_t* d_err, hipStream_t stream);
-int shard_level(Snapshot* s, const kg_frec* d_in, size_t n_in, kg_frec* d_out, size_t cap, uint32_t* d_counts,
-                uint8_t* d_res, hipStream_t stream);
+int shard_level(Snapshot* s, const kg_frec* d_in, size_t n_in, const uint32_t* d_n_in, kg_frec* d_out, size_t cap,
+                uint32_t* d_counts, uint8_t* d_res, uint32_t* d_err, hipStream_t stream);
+int shard_finish(Snapshot* s, size_t n, uint8_t* d_res, const uint32_t* d_err, hipStream_t stream);
 // kg_expand.hip
 int expand_batch(Snapshot* s, const kg_set* roots, size_t n, int32_t global, kg_tree_buf* out);
 

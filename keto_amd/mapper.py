@@ -9,6 +9,7 @@ strings get a fresh id at query time: a fresh id has no rows, which is what a fr
 """
 from __future__ import annotations
 
+import threading
 import uuid
 from typing import Dict, Iterable, List, Optional, Sequence, Tuple
 
@@ -34,20 +35,27 @@ class Interner:
         self._rel_names: List[str] = []
         self._obj: Dict[str, int] = {}
         self._obj_names: List[str] = []
+        # id creation is check-then-insert on three structures: callers on many threads (the request
+        # batcher's submitters, the persister's snapshot rebuild) intern concurrently, and two new
+        # strings must never share an id -- an unknown subject would then alias a real one
+        self._lock = threading.Lock()
         self.rel_id(WILDCARD_RELATION)  # reserve so the wildcard id is stable
 
     # ---- ids
-    @staticmethod
-    def _get(d: Dict[str, int], names: List[str], s: str, create: bool, limit: int) -> int:
-        v = d.get(s)
-        if v is None:
-            if not create:
-                raise KeyError(s)
-            v = len(names)
-            if v >= limit:
-                raise OverflowError("id space exhausted")
-            d[s] = v
-            names.append(s)
+    def _get(self, d: Dict[str, int], names: List[str], s: str, create: bool, limit: int) -> int:
+        v = d.get(s)  # lock-free fast path: an entry, once published, never changes
+        if v is not None:
+            return v
+        if not create:
+            raise KeyError(s)
+        with self._lock:
+            v = d.get(s)
+            if v is None:
+                v = len(names)
+                if v >= limit:
+                    raise OverflowError("id space exhausted")
+                names.append(s)  # the name first: a reader that sees the id can resolve it
+                d[s] = v
         return v
 
     def ns_id(self, s: str, create: bool = True) -> int:

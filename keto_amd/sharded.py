@@ -10,12 +10,16 @@ Rank r of N holds the rows of the nodes (ns, obj, rel) with kg_shard_owner(ns, o
           a hit to the query's home rank or expands the node's set row into records for the
           children's owners                                             -- kg_shard_level
   exchange the per-destination buckets go through one all-to-all (RCCL over xGMI with the
-          "nccl" backend; staged through host memory with gloo) after an all-gather of the
-          N x N bucket sizes, which also carries termination (nothing sent anywhere) and
-          overflow (every rank reruns the batch with larger buckets)
+          "nccl" backend; staged through host memory with gloo) after an all-to-all of
+          per-destination metadata (bucket size, records sent in total, overflow flags), which
+          gives every rank its receive sizes, termination (nothing sent anywhere) and overflow
+          (every rank reruns the batch with larger buckets) for ONE host round trip per level;
+          a single rank enqueues every level without any (record counts stay on the device)
 
 Results are those of the single-GPU engine (bounded reachability over rewrite-free nodes,
-internal/check/engine.go:87-207 with the SURVEY.md 8a semantics).  The local steps are
+internal/check/engine.go:87-207 with the SURVEY.md 8a semantics); a query that reaches a rewrite
+or an undeclared relation ends as KG_ERROR / KG_ERR_NOT_IMPLEMENTED (rewrites are evaluated by the
+single-GPU engines only).  The local steps are
 `ShardOps` objects: `HipShardOps` runs them on the GPU through the C ABI; the multi-rank CPU
 tests substitute a test-only restatement to exercise this exchange protocol under gloo.
 """
@@ -32,7 +36,9 @@ REC_WORDS = 4  # kg_frec = (q, node, subj, depth) as int32
 
 
 class HipShardOps:
-    """The local steps of one rank on its GPU (kg_shard_seed / kg_shard_level)."""
+    """The local steps of one rank on its GPU (kg_shard_seed / kg_shard_level / kg_shard_finish)."""
+
+    device_counts = True  # kg_shard_level can read its record count from device memory
 
     def __init__(self, snapshot):
         import torch
@@ -54,10 +60,16 @@ class HipShardOps:
         self.vis_log2 = getattr(self, "vis_log2", 25) + 1
         self.snapshot.tune("shard_vis", self.vis_log2)
 
-    def level(self, din, n_in, out, cap, counts, res):
+    def level(self, din, n_in, n_in_dev, out, cap, counts, res, err):
+        """n_in_dev: None, or a device int32 tensor whose element 0 is the record count (n_in bounds it)."""
         _lib.check(self.L.kg_shard_level(self.snapshot.handle, din.data_ptr() if n_in else None, n_in,
-                                         out.data_ptr(), cap, counts.data_ptr(), res.data_ptr(), self._s()),
+                                         n_in_dev.data_ptr() if n_in_dev is not None else None, out.data_ptr(), cap,
+                                         counts.data_ptr(), res.data_ptr(), err.data_ptr(), self._s()),
                    "kg_shard_level")
+
+    def finish(self, n, res, err):
+        _lib.check(self.L.kg_shard_finish(self.snapshot.handle, n, res.data_ptr(), err.data_ptr(), self._s()),
+                   "kg_shard_finish")
 
 
 class ShardOverflow(Exception):
@@ -78,33 +90,45 @@ class ShardedChecker:
         self.ops, self.rank, self.world, self.dist, self.device, self.cap = ops, rank, world, dist, device, cap
         self.levels = 0
         self.records_sent = 0
+        self.host_syncs = 0
 
     # ---- exchange
     def _host_staged(self) -> bool:
         return self.dist is not None and self.dist.get_backend() == "gloo" and str(self.device).startswith("cuda")
 
-    def _gather_counts(self, counts_h: np.ndarray):
-        """All-gather of every rank's (bucket sizes..., flags) -> (N x N matrix, OR of flags)."""
-        import torch
-        if self.dist is None:
-            return counts_h[None, :self.world].astype(np.int64), int(counts_h[self.world])
-        dev = "cpu" if self._host_staged() or not str(self.device).startswith("cuda") else self.device
-        t = torch.as_tensor(counts_h.astype(np.int64), device=dev)
-        parts = [torch.zeros_like(t) for _ in range(self.world)]
-        self.dist.all_gather(parts, t)
-        m = torch.stack(parts).cpu().numpy()
-        flags = 0
-        for f in m[:, self.world]:
-            flags |= int(f)
-        return m[:, :self.world], flags
+    def _meta_exchange(self, counts):
+        """One all-to-all of per-destination metadata, then ONE device->host copy for the level.
 
-    def _exchange(self, out, counts_h: np.ndarray, m: np.ndarray):
+        Rank r sends every destination d the triple (records for d, records r sends in total, r's
+        overflow flags); so each rank learns its receive sizes, the global record total (termination:
+        nothing sent anywhere) and every rank's flags (all ranks rerun together on overflow).
+        Returns (send_splits, recv_splits, global_total, flags) as host ints."""
+        import torch
+        N, cap = self.world, self.cap
+        if self._host_staged():
+            counts = counts.cpu()  # gloo moves host tensors: stage here (the one host copy of the level)
+        c = counts.to(torch.int64)
+        myflags = c[N] | (c[:N] > cap).any().to(torch.int64)  # a count past cap = dropped records
+        meta = torch.stack([c[:N], c[:N].sum().expand(N), myflags.expand(N)], dim=1).contiguous()
+        recv = torch.empty_like(meta)
+        if self.dist is None:
+            recv.copy_(meta)
+        else:
+            self.dist.all_to_all_single(recv, meta)
+        h = torch.cat([c[:N], recv.flatten()]).cpu().numpy()  # the level's host round trip
+        self.host_syncs += 1
+        send = [int(x) for x in h[:N]]
+        rm = h[N:].reshape(N, 3)
+        flags = 0
+        for f in rm[:, 2]:
+            flags |= int(f)
+        return send, [int(x) for x in rm[:, 0]], int(rm[:, 1].sum()), flags
+
+    def _exchange(self, out, send_splits, recv_splits):
         import torch
         cap = self.cap
-        if self.world == 1:
-            return out[:int(counts_h[0])]
-        send_splits = [int(x) for x in m[self.rank]]
-        recv_splits = [int(x) for x in m[:, self.rank]]
+        if self.dist is None:
+            return out[:send_splits[0]]
         send = torch.cat([out[d * cap: d * cap + send_splits[d]] for d in range(self.world)])
         staged = self._host_staged()
         if staged:
@@ -141,24 +165,45 @@ class ShardedChecker:
         import torch
         n = int(dq.shape[0])
         N, cap = self.world, self.cap
+        gdepth = gdepth if gdepth >= 1 else 5  # config.schema.json:308-315 default (as kg_shard_seed)
         bufs = [torch.empty((N * cap, REC_WORDS), dtype=torch.int32, device=self.device) for _ in range(2)]
-        counts = torch.zeros(N + 1, dtype=torch.int32, device=self.device)
+        counts = [torch.zeros(N + 1, dtype=torch.int32, device=self.device) for _ in range(2)]
         res = torch.zeros(n, dtype=torch.uint8, device=self.device)
         err = torch.zeros(n, dtype=torch.int32, device=self.device)
-        self.ops.seed(dq, n, gdepth, bufs[0], cap, counts, res, err)
+        self.ops.seed(dq, n, gdepth, bufs[0], cap, counts[0], res, err)
         cur = 0
         self.levels = 0
         self.records_sent = 0
+        if N == 1 and self.dist is None and getattr(self.ops, "device_counts", False):
+            # one rank: nothing to exchange, so every level is enqueued back to back with its record
+            # count read on the device.  A record's depth falls by one per level and seeds carry
+            # <= gdepth, so gdepth levels drain the batch; overflow is checked once at the end.
+            flags = torch.zeros((), dtype=torch.int64, device=self.device)
+            for _ in range(gdepth):
+                c = counts[cur]
+                flags |= c[1].to(torch.int64) | (c[0].to(torch.int64) > cap).to(torch.int64)
+                self.ops.level(bufs[cur], cap, c, bufs[cur ^ 1], cap, counts[cur ^ 1], res, err)
+                cur ^= 1
+                self.levels += 1
+            c = counts[cur]
+            flags |= c[1].to(torch.int64) | (c[0].to(torch.int64) > cap).to(torch.int64)
+            h = torch.stack([flags, c[0].to(torch.int64)]).cpu().numpy()  # the batch's one host round trip
+            self.host_syncs += 1
+            if int(h[0]) & 3:
+                raise ShardOverflow(int(h[0]))
+            if int(h[1]) != 0:
+                raise _lib.KetoGPUError("sharded batch: records left after %d levels" % gdepth)
+            self.ops.finish(n, res, err)
+            return res, err
         while True:
-            counts_h = counts.cpu().numpy().view(np.uint32).astype(np.int64)
-            counts_h[N] |= int((counts_h[:N] > cap).any())  # a count past cap = dropped records
-            m, flags = self._gather_counts(counts_h)
+            send, recv_splits, total, flags = self._meta_exchange(counts[cur])
             if flags & 3:
                 raise ShardOverflow(flags)
-            if int(m.sum()) == 0:
+            if total == 0:
+                self.ops.finish(n, res, err)
                 return res, err
-            self.records_sent += int(m[self.rank].sum())
-            recv = self._exchange(bufs[cur], counts_h, m)
+            self.records_sent += sum(send)
+            recv = self._exchange(bufs[cur], send, recv_splits)
             cur ^= 1
-            self.ops.level(recv, int(recv.shape[0]), bufs[cur], cap, counts, res)
+            self.ops.level(recv, int(recv.shape[0]), None, bufs[cur], cap, counts[cur], res, err)
             self.levels += 1

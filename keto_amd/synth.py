@@ -11,6 +11,8 @@ from __future__ import annotations
 
 from typing import List
 
+import numpy as np
+
 from .mapper import Interner
 from .namespace import (ComputedSubjectSet, InvertResult, Namespace, Relation, SubjectSetRewrite,
                         TupleToSubjectSet, compile_program)
@@ -56,3 +58,20 @@ def program(preset: int, it: Interner):
     if preset == PRESET_C3:
         return compile_program(c3_namespaces(), it)
     return None
+
+
+def hot_group_roots(ids: dict, n: int, max_depth: int = 0) -> np.ndarray:
+    """Config C5's expand roots: the n most popular group#member sets of the generator (popularity
+    rank r of layer r % 8 -> group by the generator's permutation, keto_amd/csrc/kg_synth.h), as
+    (n, 4) uint32 kg_set rows (ns group, object, rel member, request max depth; 0 = global)."""
+    n_docs, n_groups = ids["n_docs"], ids["n_groups"]
+    gpl = n_groups // 8
+    r = np.arange(n, dtype=np.uint64)
+    layer, rank = r % 8, r // 8
+    node = n_docs + layer * gpl + (rank * 2654435761 + 12345) % gpl
+    roots = np.zeros((n, 4), np.uint32)
+    roots[:, 0] = NAMESPACES.index("group")
+    roots[:, 1] = node.astype(np.uint32)  # group object id == node id
+    roots[:, 2] = 1 + RELATIONS.index("member")
+    roots[:, 3] = np.uint32(max_depth)
+    return roots

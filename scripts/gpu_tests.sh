@@ -1,0 +1,15 @@
+# GPU parity suite + smoke + default bench line (+ optional extra bench args in BENCH_EXTRA).
+# usage: gpurun -- 'bash scripts/gpu_tests.sh'   (env: TESTS="tests -m gpu", TAG=r2a, BENCH=1)
+set -u
+TAG=${TAG:-r2}
+TESTS=${TESTS:-tests -m gpu}
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest $TESTS -q -rs -x --timeout 180 --timeout-method thread --durations 15 > gpurun_out/pytest_${TAG}.log 2>&1; rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/pytest_${TAG}.log
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_${TAG}.log 2>&1; rc=$?; echo "smoke rc=$rc"
+[ $rc -eq 0 ] || exit $rc
+if [ "${BENCH:-1}" = "1" ]; then
+  timeout -k 10 300 python bench.py ${BENCH_EXTRA:-} > gpurun_out/bench_${TAG}.log 2>&1; rc=$?; echo "bench rc=$rc"; tail -1 gpurun_out/bench_${TAG}.log | cut -c1-400
+fi
+exit $rc

@@ -14,6 +14,8 @@ SUBJECT_ID = 0xFFFFFFFF
 SET_BIT = 0x80000000
 Q_BITS = 26
 HIT = -1  # kg_frec.node == KG_FREC_HIT as int32
+ERR = -2  # kg_frec.node == KG_FREC_ERR as int32
+ERR_NOT_IMPLEMENTED = 2
 M64 = (1 << 64) - 1
 
 
@@ -32,15 +34,21 @@ def shard_owner(ns: int, obj: int, n: int) -> int:  # kg_internal.h shard_owner
 
 
 class CpuShardOps:
-    def __init__(self, tuples6: np.ndarray, wildcard_rel: int, rank: int, nranks: int):
+    device_counts = False  # level() takes host record counts only
+
+    def __init__(self, tuples6: np.ndarray, wildcard_rel: int, rank: int, nranks: int, impure=()):
+        """impure: (ns, rel) pairs whose relation has a rewrite or is undeclared (relflag != 0)."""
         self.rank, self.n = rank, nranks
+        self.impure = set((int(a), int(b)) for a, b in impure)
         t = np.asarray(tuples6, np.int64).reshape(-1, 6)
         self.node = {}
+        self.nrel = {}
 
         def nid(ns, obj, rel):
             k = (int(ns), int(obj), int(rel))
             if k not in self.node:
                 self.node[k] = len(self.node)
+                self.nrel[self.node[k]] = (k[0], k[2])
             return self.node[k]
 
         self.adj, self.direct, self.owner = {}, set(), {}
@@ -84,12 +92,18 @@ class CpuShardOps:
                 c = self.node.get((sns, sobj, srel))
                 subj = None if c is None else SET_BIT | c
             d = md if 0 < md <= gdepth else gdepth  # engine.go:68-70
-            if v is None or subj is None:
+            if (ns, rel) in self.impure:
+                err[i] = ERR_NOT_IMPLEMENTED
                 continue
+            if v is None or (subj is None and not self.impure):
+                continue
+            if subj is None:
+                subj = 0xFFFFFFFF  # unknown subject: never held, but the query may still reach a rewrite
             self._emit(out, cap, counts, self.owner[v],
                        [(self.rank << Q_BITS) | i, v, np.uint32(subj).view(np.int32), d])
 
-    def level(self, din, n_in, out, cap, counts, res):
+    def level(self, din, n_in, n_in_dev, out, cap, counts, res, err):
+        assert n_in_dev is None
         counts.zero_()
         for r in din[:n_in].tolist():
             q, v, subj, d = r[0], r[1], r[2] & 0xFFFFFFFF, r[3]
@@ -98,10 +112,19 @@ class CpuShardOps:
                 if home == self.rank:
                     res[qi] = 1
                 continue
+            if v == ERR:
+                if home == self.rank:
+                    err[qi] = max(int(err[qi]), subj)
+                continue
             if (q, v) in self.vis:
                 continue
             self.vis.add((q, v))
-            if d >= 1 and (v, subj) in self.direct:
+            if self.nrel[v] in self.impure:
+                if home == self.rank:
+                    err[qi] = max(int(err[qi]), ERR_NOT_IMPLEMENTED)
+                else:
+                    self._emit(out, cap, counts, home, [q, ERR, ERR_NOT_IMPLEMENTED, 0])
+            elif d >= 1 and (v, subj) in self.direct:
                 if home == self.rank:
                     res[qi] = 1
                 else:
@@ -109,3 +132,13 @@ class CpuShardOps:
             elif d >= 2:
                 for c in self.adj.get(v, []):
                     self._emit(out, cap, counts, self.owner[c], [q, c, np.uint32(subj).view(np.int32), d - 1])
+            elif d == 1:  # checkIsAllowed(child, 0) still evaluates astRelationFor: impure -> error
+                for c in self.adj.get(v, []):
+                    if self.nrel[c] in self.impure:
+                        if home == self.rank:
+                            err[qi] = max(int(err[qi]), ERR_NOT_IMPLEMENTED)
+                        else:
+                            self._emit(out, cap, counts, home, [q, ERR, ERR_NOT_IMPLEMENTED, 0])
+
+    def finish(self, n, res, err):
+        res[:n][err[:n] != 0] = 2

@@ -70,19 +70,7 @@ def test_random_expand_vs_oracle(seed):
         got = ex.build_trees_ids(arr.astype(np.uint32))
         for r, g in zip(roots, got):
             exp = oracle.expand(r[0], r[1], r[2], r[3], gmax)
-            if exp is None:
-                assert g is None, r
-                continue
-            assert g is not None, r
-            # SubjectIDs: oracle records ns=rel=-1, GPU records KG_SUBJECT_ID / 0
-            e2 = np.asarray(exp, np.int64).copy()
-            g2 = np.asarray(g, np.int64).copy()
-            ids = e2[:, 1] == 0
-            e2[ids, 2] = 0
-            e2[ids, 4] = 0
-            g2[g2[:, 1] == 0, 2] = 0
-            g2[g2[:, 1] == 0, 4] = 0
-            assert e2.shape == g2.shape and (e2 == g2).all(), (r, gmax)
+            _cmp_records(exp, g, (r, gmax))
 
 
 def test_expand_overflow_tier_and_wide_rows():
@@ -100,3 +88,39 @@ def test_expand_overflow_tier_and_wide_rows():
         got = ex.build_tree(SubjectSet("g", "root", "m"), 0)
         exp = oracle_tree(oracle.expand(it.ns_id("g"), it.obj_id("root"), it.rel_id("m"), 0, gmax), it)
         assert got == exp, gmax
+
+
+def _cmp_records(exp, g, what):
+    if exp is None:
+        assert g is None, what
+        return
+    assert g is not None, what
+    e2 = np.asarray(exp, np.int64).copy()
+    g2 = np.asarray(g, np.int64).copy()
+    ids = e2[:, 1] == 0  # SubjectIDs: oracle ns=rel=-1, GPU KG_SUBJECT_ID / 0
+    e2[ids, 2] = 0
+    e2[ids, 4] = 0
+    g2[g2[:, 1] == 0, 2] = 0
+    g2[g2[:, 1] == 0, 4] = 0
+    assert e2.shape == g2.shape and (e2 == g2).all(), what
+
+
+@pytest.mark.parametrize("n_tuples,gmax", [(300_000, 5), (1_000_000, 3)])
+def test_c5_hot_group_roots_vs_oracle(n_tuples, gmax):
+    """Config C5's workload at reduced size: the generator's most popular group#member roots (the
+    roots bench.py --mode expand times), expanded at the global depth, against the oracle's
+    BuildTree on the snapshot's own rows -- same pre-order, same child order, every root."""
+    from keto_amd.engine import Snapshot
+    from keto_amd.synth import hot_group_roots
+    snap = Snapshot.synthetic(n_tuples, seed=20250131)
+    roots = hot_group_roots(snap.synth_ids(), 1500)
+    ex = ExpandEngine(snap)
+    ex.config.max_read_depth = gmax
+    got = ex.build_trees_ids(roots)
+    oracle = Oracle(snap.export(), 0)
+    big = 0
+    for r, g in zip(roots, got):
+        exp = oracle.expand(int(r[0]), int(r[1]), int(r[2]), 0, gmax)
+        _cmp_records(exp, g, (r.tolist(), gmax))
+        big += g is not None and len(g) > 512
+    assert big > 0  # some trees outgrow the LDS pass (the hash / bitmap passes are exercised)

@@ -192,3 +192,53 @@ def test_batcher_errors_and_close():
     with CheckBatcher(Broken(), max_wait_us=0) as b2:
         with pytest.raises(_lib.KetoGPUError):
             b2.submit_ids([0, 0, 1, 0xFFFFFFFF, 1, 0, 0]).result(5)
+
+
+def test_batcher_cancelled_future_keeps_dispatcher_alive():
+    """A caller that cancels its future (e.g. a cancelled RPC) must not end the dispatcher."""
+    e = RecordingEngine(delay=0.05)
+    with CheckBatcher(e, max_batch=4, max_wait_us=20000) as b:
+        f0 = b.submit_ids([0, 2, 1, 0xFFFFFFFF, 1, 0, 0])
+        assert f0.cancel()  # still pending: cancellable
+        f1 = b.submit_ids([0, 4, 1, 0xFFFFFFFF, 1, 0, 0])
+        assert f1.result(5) == (_lib.KG_IS_MEMBER, 0)
+        later = [b.submit_ids([0, i, 1, 0xFFFFFFFF, 1, 0, 0]) for i in range(6)]
+        assert [f.result(5)[0] for f in later] == [_lib.KG_IS_MEMBER if i % 2 == 0 else _lib.KG_NOT_MEMBER
+                                                    for i in range(6)]
+    assert b.cancelled >= 1
+    assert all(len(x) >= 1 for x in e.batches) and sum(len(x) for x in e.batches) == 7  # f0 never ran
+
+
+def test_batcher_stats_are_bounded():
+    e = RecordingEngine()
+    with CheckBatcher(e, max_batch=1, max_wait_us=0) as b:
+        b.STATS_WINDOW  # class constant
+        for i in range(20):
+            b.submit_ids([0, i, 1, 0xFFFFFFFF, 1, 0, 0]).result(5)
+    assert b.batch_latency_s.maxlen == CheckBatcher.STATS_WINDOW and len(b.batch_latency_s) == 20
+
+
+def test_interner_concurrent_fresh_strings_get_unique_ids():
+    """Many threads interning fresh strings at once (the batcher's submit path): ids stay unique and
+    resolve back to their own string."""
+    from keto_amd.mapper import Interner
+    it = Interner()
+    n_threads, per = 8, 2000
+    ids = [None] * n_threads
+    start = threading.Barrier(n_threads)
+
+    def worker(k):
+        start.wait()
+        # half the strings are shared between threads, half are private
+        ids[k] = [(s, it.obj_id(s)) for s in
+                  (f"shared{i}" if i % 2 else f"t{k}-{i}" for i in range(per))]
+    ts = [threading.Thread(target=worker, args=(k,)) for k in range(n_threads)]
+    [t.start() for t in ts]
+    [t.join() for t in ts]
+    by_str = {}
+    for lst in ids:
+        for s, v in lst:
+            assert by_str.setdefault(s, v) == v  # one id per string
+            assert it.obj_name(v) == s
+    assert len(set(by_str.values())) == len(by_str)  # one string per id
+    assert len(by_str) == n_threads * per // 2 + per // 2

@@ -157,3 +157,127 @@ def test_sharded_hip_vs_oracle(world):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     _run_gpu(world, seed=11)
+
+
+# ------------------------------------------------------------------ rewrites reached in sharded mode
+def _impure_graph(seed):
+    """A random graph plus a namespace program: relation r2 of n1 has a rewrite and r1 of n2 is
+    declared while r2 is not (undeclared) -> relflag != 0 for (n1, r2), (n2, r0), (n2, r2)."""
+    sys.path.insert(0, ROOT)
+    from keto_amd.namespace import ComputedSubjectSet, Namespace, Relation, SubjectSetRewrite, compile_program
+    it, t6, q = _graph(seed, n_obj=40, n_rows=400)
+    nss = [Namespace("n1", [Relation("r0"), Relation("r1"),
+                            Relation("r2", rewrite=SubjectSetRewrite([ComputedSubjectSet("r0")]))]),
+           Namespace("n2", [Relation("r1")])]
+    prog = compile_program(nss, it)
+    impure = [(it.ns_id("n1"), it.rel_id("r2")), (it.ns_id("n2"), it.rel_id("r0")), (it.ns_id("n2"), it.rel_id("r2")),
+              (it.ns_id("n2"), it.rel_id("..."))]
+    return it, t6, q, prog, impure
+
+
+def _cpu_sharded(t6, wildcard, q, gmax, impure):
+    """Single-rank run of the protocol over the CPU restatement (test reference)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from keto_amd.sharded import ShardedChecker
+    from shard_ref import CpuShardOps
+    chk = ShardedChecker(CpuShardOps(t6, wildcard, 0, 1, impure), 0, 1, None, device="cpu", cap=1 << 12)
+    res, err = chk.check(torch.from_numpy(q.view(np.int32).copy()), gmax)
+    return res.numpy().copy(), err.numpy().copy()
+
+
+def test_sharded_impure_reference_semantics():
+    """CPU restatement: queries that reach a rewrite / undeclared relation end as NOT_IMPLEMENTED
+    errors; every other query agrees with the oracle on the same graph (which evaluates rewrites)."""
+    from oracle.oracle import POLICY_CANONICAL, Oracle
+    it, t6, q, prog, impure = _impure_graph(5)
+    o = Oracle(t6, it.wildcard_rel, prog)
+    n_err = 0
+    for gmax in (2, 5):
+        res, err = _cpu_sharded(t6, it.wildcard_rel, q, gmax, impure)
+        exp, oerr, _ = o.check_batch(q[:, :6], q[:, 6].view(np.int32), gmax, POLICY_CANONICAL)
+        ok = err == 0
+        assert (res[~ok] == 2).all() and (err[~ok] == 2).all()
+        assert (res[ok] == exp[ok]).all() and (oerr[ok] == 0).all()
+        n_err += int((~ok).sum())
+    assert 0 < n_err
+
+
+@pytest.mark.gpu
+def test_sharded_hip_impure_matches_reference():
+    """HIP sharded mode with a rewrite program: the NOT_IMPLEMENTED errors (root or reached through a
+    subject set) and all other answers equal the CPU restatement's, bit for bit."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from keto_amd.engine import Snapshot
+    from keto_amd.sharded import HipShardOps, ShardedChecker
+    it, t6, q, prog, impure = _impure_graph(5)
+    snap = Snapshot(t6, it, prog, 0, shard=(0, 1))
+    chk = ShardedChecker(HipShardOps(snap), 0, 1, None, device="cuda", cap=256)
+    for gmax in (2, 5):
+        res, err = chk.check(torch.from_numpy(q.view(np.int32).copy()).cuda(), gmax)
+        eres, eerr = _cpu_sharded(t6, it.wildcard_rel, q, gmax, impure)
+        assert (res.cpu().numpy() == eres).all() and (err.cpu().numpy() == eerr).all(), gmax
+        assert (eerr != 0).any()
+
+
+# ------------------------------------------------------------------ config C4 generator, sharded
+def _synth_worker(rank, world, port, n_tuples, n_q, gmax, backend, outq):
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+    from keto_amd import _lib
+    from keto_amd.engine import Snapshot
+    from keto_amd.sharded import HipShardOps, ShardedChecker
+    dist_ = None
+    torch.cuda.set_device(0)
+    if backend is not None:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group(backend, rank=rank, world_size=world)
+        dist_ = dist
+    snap = Snapshot.synthetic(n_tuples, seed=20250131, shard=(rank, world))
+    dq = torch.empty((n_q, 7), dtype=torch.int32, device="cuda")
+    _lib.check(_lib.load().kg_synth_queries(snap.handle, 31, n_q, dq.data_ptr()), "kg_synth_queries")
+    mine = np.array_split(np.arange(n_q), world)[rank]
+    chk = ShardedChecker(HipShardOps(snap), rank, world, dist_, device="cuda", cap=1 << 14)
+    res, err = chk.check(dq[mine[0]:mine[-1] + 1].contiguous(), gmax)
+    outq.put((rank, mine, res.cpu().numpy(), err.cpu().numpy(), chk.levels, chk.host_syncs,
+              dq.cpu().numpy() if rank == 0 else None))
+    if dist_:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,backend", [(1, None), (1, "nccl"), (2, "gloo")])
+def test_sharded_c4_generator_vs_oracle(world, backend):
+    """Config C4's generator, hash-sharded: world 1 with every level on the device (no host round
+    trip per level), world 1 through torch.distributed over RCCL ("nccl": the metadata and record
+    all-to-alls run on device tensors), and world 2 (two ranks on one GPU, gloo).  Against the
+    oracle on the whole graph's rows, bit-exact; the synthetic queries only touch rewrite-free nodes."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from keto_amd.engine import Snapshot
+    from oracle.oracle import POLICY_CANONICAL, Oracle
+    n_tuples, n_q, gmax = 300_000, 20_000, 10
+    ctx = mp.get_context("spawn")
+    outq = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_synth_worker, args=(r, world, port, n_tuples, n_q, gmax, backend, outq))
+          for r in range(world)]
+    for p in ps:
+        p.start()
+    got = [outq.get(timeout=110) for _ in range(world)]
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    q = [g[6] for g in got if g[6] is not None][0].view(np.uint32)
+    full = Snapshot.synthetic(n_tuples, seed=20250131)
+    o = Oracle(full.export(), 0)
+    exp, _, _ = o.check_batch(q[:, :6], q[:, 6].view(np.int32), gmax, POLICY_CANONICAL, nthreads=8)
+    res = np.zeros(n_q, np.uint8)
+    for rank, mine, r, e, levels, syncs, _ in got:
+        assert (e == 0).all()
+        res[mine] = r
+        if world == 1 and backend is None:
+            assert syncs == 1 and levels == gmax  # one host round trip for the whole batch
+    assert (res == exp).all(), np.nonzero(res != exp)[0][:10]
+    assert 0.05 < exp.mean() < 0.95
