@@ -153,13 +153,25 @@ typedef struct {
 } kg_synth_params;
 
 /* ---- snapshot --------------------------------------------------------------------------- */
+/* device_mask: bit d set = a replica of the snapshot on device d (0 = device 0 only).  Every
+ * replica holds the whole snapshot (1 B tuples take ~33 GB of a 288 GB MI355X); kg_check_batch and
+ * kg_expand_batch split their host-buffer batches over the replicas inside the call, which is how
+ * one `keto serve` process (one check.Engine, internal/driver/registry_default.go:180-185) uses
+ * every GPU of the node.  Replicas are built concurrently. */
 int kg_snapshot_create(const kg_tuple* rows, size_t n, const kg_dict* dict, const kg_rewrite_prog* prog,
-                       int device, kg_snapshot** out);
+                       int device_mask, kg_snapshot** out);
+/* The same with an explicit device list; entries may repeat (several replicas on one device). */
+int kg_snapshot_create_on(const kg_tuple* rows, size_t n, const kg_dict* dict, const kg_rewrite_prog* prog,
+                          const int* devices, int n_devices, kg_snapshot** out);
 /* prog: the namespace program compiled against the generator's ids (ns doc=0 group=1 user=2
  * folder=3; rel "..."=0 viewer=1 member=2 editor=3 owner=4 parents=5 blocked=6 view=7 edit=8
  * share=9), or NULL for none.  keto_amd/synth.py builds both. */
-int kg_snapshot_synthetic(const kg_synth_params* params, const kg_rewrite_prog* prog, int device,
+int kg_snapshot_synthetic(const kg_synth_params* params, const kg_rewrite_prog* prog, int device_mask,
                           kg_snapshot** out);
+int kg_snapshot_synthetic_on(const kg_synth_params* params, const kg_rewrite_prog* prog, const int* devices,
+                             int n_devices, kg_snapshot** out);
+/* Number of replicas; their devices go to devices[0 .. min(count, cap)) (devices may be NULL). */
+int kg_snapshot_replicas(const kg_snapshot* s, int* devices, int cap);
 void kg_snapshot_destroy(kg_snapshot* s);
 /* sizes: [0]=nodes [1]=rows [2]=set edges [3]=device bytes */
 int kg_snapshot_info(const kg_snapshot* s, uint64_t* info4);
@@ -195,10 +207,13 @@ int kg_snapshot_export_csr(const kg_snapshot* s, uint64_t* row_off, uint32_t* ro
 
 /* ---- check ------------------------------------------------------------------------------ */
 /* Host buffers: q[n] in, out[n] (KG_NOT_MEMBER / KG_IS_MEMBER / KG_ERROR), err_code[n] (may be
- * NULL), stats (may be NULL).  Synchronous. */
+ * NULL), stats (may be NULL; counters summed over replicas, kernel_ms = the slowest replica's).
+ * Synchronous.  Thread-safe: every calling thread gets its own stream and pinned staging per
+ * replica (kept for its later calls), so concurrent callers' batches overlap on the devices.
+ * The batch is split over the replicas in contiguous chunks of >= 16384 queries. */
 int kg_check_batch(kg_snapshot* s, const kg_query* q, size_t n, int32_t global_max_depth, uint8_t* out,
                    uint32_t* err_code, kg_stats* stats);
-/* Device-resident variant: d_q / d_out / d_err are device pointers (HBM), stream is a
+/* Device-resident variant (replica 0 only: the pointers belong to its device): d_q / d_out / d_err are device pointers (HBM), stream is a
  * hipStream_t (NULL = the snapshot's stream).  Returns once the batch is enqueued; when queries
  * reach the grid tier the call waits for the wave tiers (the grid tier's size is read back), and
  * with stats != NULL it waits for the whole batch.  Every stream gets its own batch workspace
@@ -252,6 +267,7 @@ int kg_shard_level(kg_snapshot* s, const kg_frec* d_in, size_t n_in, const uint3
 int kg_shard_finish(kg_snapshot* s, size_t n, uint8_t* d_res, const uint32_t* d_err, void* stream);
 
 /* ---- expand ----------------------------------------------------------------------------- */
+/* Roots are split over the replicas (chunks of >= 1024 roots, one host thread each). */
 int kg_expand_batch(kg_snapshot* s, const kg_set* roots, size_t n, int32_t global_max_depth, kg_tree_buf* out);
 void kg_tree_free(kg_tree_buf* t);
 

@@ -73,7 +73,8 @@ class kg_synth_params(C.Structure):
 
 
 # every symbol include/ketogpu.h declares
-EXPORTS = ["kg_snapshot_create", "kg_snapshot_synthetic", "kg_snapshot_destroy", "kg_snapshot_info", "kg_snapshot_tune", "kg_synth_ids",
+EXPORTS = ["kg_snapshot_create", "kg_snapshot_create_on", "kg_snapshot_synthetic", "kg_snapshot_synthetic_on",
+           "kg_snapshot_replicas", "kg_snapshot_destroy", "kg_snapshot_info", "kg_snapshot_tune", "kg_synth_ids",
            "kg_snapshot_export", "kg_snapshot_export_csr", "kg_check_batch", "kg_check_batch_device", "kg_synth_queries", "kg_expand_batch",
            "kg_tree_free", "kg_last_error", "kg_version", "kg_shard_owner", "kg_snapshot_create_shard",
            "kg_snapshot_synthetic_shard", "kg_shard_seed", "kg_shard_level", "kg_shard_finish"]
@@ -96,8 +97,13 @@ def load(path: str = LIB_PATH):
     L = C.CDLL(path)
     vp, sz, i32, u32, u64 = C.c_void_p, C.c_size_t, C.c_int32, C.c_uint32, C.c_uint64
     L.kg_snapshot_create.argtypes = [vp, sz, C.POINTER(kg_dict), C.POINTER(kg_rewrite_prog), C.c_int, C.POINTER(vp)]
+    L.kg_snapshot_create_on.argtypes = [vp, sz, C.POINTER(kg_dict), C.POINTER(kg_rewrite_prog), vp, C.c_int,
+                                        C.POINTER(vp)]
     L.kg_snapshot_synthetic.argtypes = [C.POINTER(kg_synth_params), C.POINTER(kg_rewrite_prog), C.c_int,
                                         C.POINTER(vp)]
+    L.kg_snapshot_synthetic_on.argtypes = [C.POINTER(kg_synth_params), C.POINTER(kg_rewrite_prog), vp, C.c_int,
+                                           C.POINTER(vp)]
+    L.kg_snapshot_replicas.argtypes = [vp, vp, C.c_int]
     L.kg_snapshot_destroy.argtypes = [vp]
     L.kg_snapshot_destroy.restype = None
     L.kg_snapshot_info.argtypes = [vp, vp]
@@ -125,7 +131,8 @@ def load(path: str = LIB_PATH):
     L.kg_shard_seed.argtypes = [vp, vp, sz, i32, vp, sz, vp, vp, vp, vp]
     L.kg_shard_level.argtypes = [vp, vp, sz, vp, vp, sz, vp, vp, vp, vp]
     L.kg_shard_finish.argtypes = [vp, sz, vp, vp, vp]
-    for name in ("kg_snapshot_create", "kg_snapshot_synthetic", "kg_snapshot_info", "kg_snapshot_tune", "kg_synth_ids", "kg_check_batch",
+    for name in ("kg_snapshot_create", "kg_snapshot_create_on", "kg_snapshot_synthetic", "kg_snapshot_synthetic_on",
+                 "kg_snapshot_replicas", "kg_snapshot_info", "kg_snapshot_tune", "kg_synth_ids", "kg_check_batch",
                  "kg_check_batch_device", "kg_synth_queries", "kg_expand_batch", "kg_snapshot_create_shard",
                  "kg_snapshot_synthetic_shard", "kg_shard_seed", "kg_shard_level", "kg_shard_finish"):
         getattr(L, name).restype = C.c_int

@@ -2,11 +2,15 @@
 // No exception crosses the ABI; every failure returns non-zero and sets kg_last_error().
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <functional>
 #include <new>
 #include <string>
+#include <thread>
+#include <vector>
 
 #include "kg_snapshot.h"
 
@@ -55,40 +59,98 @@ size_t kg_last_error(char* buf, size_t len) {
   return e.size();
 }
 
-int kg_snapshot_create(const kg_tuple* rows, size_t n, const kg_dict* dict, const kg_rewrite_prog* prog, int device,
-                       kg_snapshot** out) {
-  KG_GUARD_BEGIN
+}  // extern "C"
+
+namespace {
+std::vector<int> mask_devices(int device_mask) {
+  std::vector<int> d;
+  for (int b = 0; b < 31; b++)
+    if (device_mask & (1 << b)) d.push_back(b);
+  if (d.empty()) d.push_back(0);
+  return d;
+}
+
+// Builds one replica per entry of devs (entries may repeat: several replicas on one device),
+// concurrently, one host thread per replica; replica 0 owns the others.
+int build_replicas(const int* devs, int n_dev, const std::function<int(Snapshot*)>& build, kg_snapshot** out) {
   if (!out) return set_error(-2, "out is NULL");
   *out = nullptr;
-  if (n && !rows) return set_error(-2, "rows is NULL");
-  Snapshot* s = new Snapshot();
-  int rc = s->init_device(device);
-  if (!rc) rc = s->create_from_tuples(rows, n, dict, prog);
-  if (rc) {
-    delete s;
-    return rc;
+  if (!devs || n_dev < 1 || n_dev > 64) return set_error(-2, "between 1 and 64 devices");
+  std::vector<Snapshot*> reps(n_dev, nullptr);
+  std::vector<int> rcs(n_dev, 0);
+  std::vector<std::string> msgs(n_dev);
+  auto one = [&](int i) {
+    try {
+      Snapshot* s = new Snapshot();
+      reps[i] = s;
+      int rc = s->init_device(devs[i]);
+      if (!rc) rc = build(s);
+      rcs[i] = rc;
+      if (rc) {
+        char buf[1024];
+        kg_last_error(buf, sizeof buf);
+        msgs[i] = buf;
+      }
+    } catch (const std::exception& ex) {
+      rcs[i] = -5;
+      msgs[i] = ex.what();
+    }
+  };
+  std::vector<std::thread> th;
+  for (int i = 1; i < n_dev; i++) th.emplace_back(one, i);
+  one(0);
+  for (auto& t : th) t.join();
+  int bad = -1;
+  for (int i = 0; i < n_dev; i++)
+    if (rcs[i] && bad < 0) bad = i;
+  if (bad >= 0) {
+    for (Snapshot* s : reps) delete s;
+    return set_error(rcs[bad], "replica %d (device %d): %s", bad, devs[bad], msgs[bad].c_str());
   }
-  *out = reinterpret_cast<kg_snapshot*>(s);
+  for (int i = 1; i < n_dev; i++) reps[0]->peers.push_back(reps[i]);
+  *out = reinterpret_cast<kg_snapshot*>(reps[0]);
   kg::clear_error();
   return 0;
+}
+}  // namespace
+
+extern "C" {
+
+int kg_snapshot_create_on(const kg_tuple* rows, size_t n, const kg_dict* dict, const kg_rewrite_prog* prog,
+                          const int* devices, int n_devices, kg_snapshot** out) {
+  KG_GUARD_BEGIN
+  if (n && !rows) return set_error(-2, "rows is NULL");
+  return build_replicas(devices, n_devices, [&](Snapshot* s) { return s->create_from_tuples(rows, n, dict, prog); },
+                        out);
   KG_GUARD_END
 }
 
-int kg_snapshot_synthetic(const kg_synth_params* params, const kg_rewrite_prog* prog, int device,
-                          kg_snapshot** out) {
+int kg_snapshot_create(const kg_tuple* rows, size_t n, const kg_dict* dict, const kg_rewrite_prog* prog, int device_mask,
+                       kg_snapshot** out) {
+  const std::vector<int> d = mask_devices(device_mask);
+  return kg_snapshot_create_on(rows, n, dict, prog, d.data(), (int)d.size(), out);
+}
+
+int kg_snapshot_synthetic_on(const kg_synth_params* params, const kg_rewrite_prog* prog, const int* devices,
+                             int n_devices, kg_snapshot** out) {
   KG_GUARD_BEGIN
-  if (!out || !params) return set_error(-2, "NULL argument");
-  *out = nullptr;
-  Snapshot* s = new Snapshot();
-  int rc = s->init_device(device);
-  if (!rc) rc = s->create_synthetic(params, prog);
-  if (rc) {
-    delete s;
-    return rc;
-  }
-  *out = reinterpret_cast<kg_snapshot*>(s);
-  return 0;
+  if (!params) return set_error(-2, "NULL argument");
+  return build_replicas(devices, n_devices, [&](Snapshot* s) { return s->create_synthetic(params, prog); }, out);
   KG_GUARD_END
+}
+
+int kg_snapshot_synthetic(const kg_synth_params* params, const kg_rewrite_prog* prog, int device_mask,
+                          kg_snapshot** out) {
+  const std::vector<int> d = mask_devices(device_mask);
+  return kg_snapshot_synthetic_on(params, prog, d.data(), (int)d.size(), out);
+}
+
+int kg_snapshot_replicas(const kg_snapshot* sp, int* devices, int cap) {
+  if (!sp) return set_error(-2, "NULL snapshot");
+  Snapshot* s = const_cast<Snapshot*>(reinterpret_cast<const Snapshot*>(sp));
+  const int n = (int)s->n_replicas();
+  for (int i = 0; devices && i < n && i < cap; i++) devices[i] = s->replica(i)->device;
+  return n;
 }
 
 void kg_snapshot_destroy(kg_snapshot* s) { delete reinterpret_cast<Snapshot*>(s); }
@@ -177,9 +239,7 @@ int kg_snapshot_info(const kg_snapshot* sp, uint64_t* info4) {
   return 0;
 }
 
-int kg_snapshot_tune(kg_snapshot* sp, const char* key, int64_t value) {
-  if (!sp || !key) return set_error(-2, "NULL argument");
-  Snapshot* s = reinterpret_cast<Snapshot*>(sp);
+static int tune_one(Snapshot* s, const char* key, int64_t value) {
   std::lock_guard<std::mutex> lk(s->mu);
   if (strcmp(key, "tiers") == 0) {
     if (value < 0 || value > 2) return set_error(-2, "tiers must be 0, 1 or 2");
@@ -244,6 +304,14 @@ int kg_snapshot_tune(kg_snapshot* sp, const char* key, int64_t value) {
   return set_error(-2, "unknown knob '%s'", key);
 }
 
+int kg_snapshot_tune(kg_snapshot* sp, const char* key, int64_t value) {
+  if (!sp || !key) return set_error(-2, "NULL argument");
+  Snapshot* s = reinterpret_cast<Snapshot*>(sp);
+  for (size_t i = 0; i < s->n_replicas(); i++)
+    if (int rc = tune_one(s->replica(i), key, value)) return rc;
+  return 0;
+}
+
 int kg_synth_ids(const kg_snapshot* sp, uint32_t* ids6) {
   if (!sp || !ids6) return set_error(-2, "NULL argument");
   const Snapshot* s = reinterpret_cast<const Snapshot*>(sp);
@@ -298,41 +366,94 @@ int kg_check_batch_device(kg_snapshot* sp, const kg_query* d_q, size_t n, int32_
   KG_GUARD_END
 }
 
+// Host buffers in and out: the batch is split over the snapshot's replicas (one contiguous chunk
+// each, none smaller than MIN_PER_REPLICA queries), every chunk on this thread's lane of its
+// replica.  All chunks are staged and enqueued before the first wait, so the devices run
+// concurrently; queries are staged through pinned memory in slices so the H2D copy of one slice
+// overlaps the staging of the next.
 int kg_check_batch(kg_snapshot* sp, const kg_query* q, size_t n, int32_t global_max_depth, uint8_t* out,
                    uint32_t* err_code, kg_stats* stats) {
   KG_GUARD_BEGIN
+  constexpr size_t MIN_PER_REPLICA = 16384, SLICE = 65536;
   if (!sp) return set_error(-2, "NULL snapshot");
   if (n && (!q || !out)) return set_error(-2, "NULL buffer");
   Snapshot* s = reinterpret_cast<Snapshot*>(sp);
   if (s->shard_n > 1) return set_error(-2, "sharded snapshot: checks run through kg_shard_seed / kg_shard_level");
-  kg::Workspace* w = s->workspace(nullptr);
-  std::lock_guard<std::mutex> lk(w->mu);
-  HIPC(hipSetDevice(s->device));
-  if (n == 0) {
-    if (stats) memset(stats, 0, sizeof *stats);
-    return 0;
-  }
-  kg_query* d_q = nullptr;
-  uint8_t* d_out = nullptr;
-  uint32_t* d_err = nullptr;
-  HIPC(hipMalloc(&d_q, n * sizeof(kg_query)));
-  HIPC(hipMalloc(&d_out, n));
-  HIPC(hipMalloc(&d_err, n * 4));
+  if (stats) memset(stats, 0, sizeof *stats);
+  if (n == 0) return 0;
+  if (n > 0x7FFFFFFFull) return set_error(-2, "batch too large");
+  std::vector<kg::Lane*>* lanes = s->thread_lanes();
+  if (!lanes) return -1;
+  const size_t R = std::max<size_t>(1, std::min(lanes->size(), (n + MIN_PER_REPLICA - 1) / MIN_PER_REPLICA));
+  std::vector<kg::BatchPending> bp(R);
+  std::vector<kg_stats> st(R);
+  std::vector<size_t> b(R + 1);
+  for (size_t i = 0; i <= R; i++) b[i] = n * i / R;
+  size_t begun = 0;
   int rc = 0;
-  if (hipMemcpyAsync(d_q, q, n * sizeof(kg_query), hipMemcpyHostToDevice, s->stream) != hipSuccess)
-    rc = set_error(-1, "H2D copy failed");
-  if (!rc) rc = kg::check_batch_device(s, w, d_q, n, global_max_depth, d_out, d_err, stats);
-  if (!rc && hipMemcpyAsync(out, d_out, n, hipMemcpyDeviceToHost, s->stream) != hipSuccess)
-    rc = set_error(-1, "D2H copy failed");
-  if (!rc && err_code && hipMemcpyAsync(err_code, d_err, n * 4, hipMemcpyDeviceToHost, s->stream) != hipSuccess)
-    rc = set_error(-1, "D2H copy failed");
-  if (!rc) {
-    hipError_t e = hipStreamSynchronize(s->stream);
-    if (e != hipSuccess) rc = set_error(-1, "batch failed: %s", hipGetErrorString(e));
+  for (size_t i = 0; i < R && !rc; i++) {
+    kg::Lane* L = (*lanes)[i];
+    const size_t m = b[i + 1] - b[i];
+    if ((rc = L->reserve(m))) break;
+    HIPC(hipSetDevice(L->device));
+    for (size_t o = 0; o < m; o += SLICE) {
+      const size_t k = std::min(SLICE, m - o);
+      memcpy(L->h_q + o, q + b[i] + o, k * sizeof(kg_query));
+      if (hipMemcpyAsync(L->d_q + o, L->h_q + o, k * sizeof(kg_query), hipMemcpyHostToDevice, L->stream) != hipSuccess) {
+        rc = set_error(-1, "H2D copy failed");
+        break;
+      }
+    }
+    if (rc) break;
+    L->w->mu.lock();
+    rc = kg::check_batch_begin(L->rep, L->w, L->d_q, m, global_max_depth, L->d_out, L->d_err, stats ? &st[i] : nullptr,
+                               &bp[i]);
+    begun++;
+    if (!rc && (hipMemcpyAsync(L->h_out, L->d_out, m, hipMemcpyDeviceToHost, L->stream) != hipSuccess ||
+                hipMemcpyAsync(L->h_err, L->d_err, m * 4, hipMemcpyDeviceToHost, L->stream) != hipSuccess))
+      rc = set_error(-1, "D2H copy failed");
   }
-  hipFree(d_q);
-  hipFree(d_out);
-  hipFree(d_err);
+  for (size_t i = 0; i < begun; i++) {
+    kg::Lane* L = (*lanes)[i];
+    const size_t m = b[i + 1] - b[i];
+    if (!rc) {
+      hipSetDevice(L->device);
+      bool reran = false;
+      int r2 = kg::check_batch_end(L->rep, L->w, &bp[i], &reran);
+      if (!r2 && reran &&  // the grid tier rewrote results after the first copy: copy them again
+          (hipMemcpyAsync(L->h_out, L->d_out, m, hipMemcpyDeviceToHost, L->stream) != hipSuccess ||
+           hipMemcpyAsync(L->h_err, L->d_err, m * 4, hipMemcpyDeviceToHost, L->stream) != hipSuccess))
+        r2 = set_error(-1, "D2H copy failed");
+      if (!r2) {
+        hipError_t e = hipStreamSynchronize(L->stream);
+        if (e != hipSuccess) r2 = set_error(-1, "batch failed: %s", hipGetErrorString(e));
+      }
+      if (!r2) {
+        memcpy(out + b[i], L->h_out, m);
+        if (err_code) memcpy(err_code + b[i], L->h_err, m * 4);
+      }
+      rc = r2;
+    } else {
+      hipSetDevice(L->device);
+      (void)hipStreamSynchronize(L->stream);
+    }
+    L->w->mu.unlock();
+  }
+  if (!rc && stats) {  // counters add up over replicas; device time is the slowest replica's
+    for (size_t i = 0; i < R; i++) {
+      const kg_stats& x = st[i];
+      uint64_t* d = reinterpret_cast<uint64_t*>(stats);
+      const uint64_t* y = reinterpret_cast<const uint64_t*>(&x);
+      for (size_t f = 0; f < sizeof(kg_stats) / 8; f++) d[f] += y[f];
+    }
+    double km = 0, lm = 0;
+    for (size_t i = 0; i < R; i++) {
+      km = std::max(km, st[i].kernel_ms);
+      lm = std::max(lm, st[i].light_ms);
+    }
+    stats->kernel_ms = km;
+    stats->light_ms = lm;
+  }
   return rc;
   KG_GUARD_END
 }
@@ -346,13 +467,72 @@ int kg_synth_queries(kg_snapshot* sp, uint64_t seed, size_t n, kg_query* d_q) {
   KG_GUARD_END
 }
 
+// Roots are split over the replicas (contiguous chunks, one host thread per replica: an expand
+// call waits for its device) and the per-replica trees concatenated in root order.
 int kg_expand_batch(kg_snapshot* sp, const kg_set* roots, size_t n, int32_t global_max_depth, kg_tree_buf* out) {
   KG_GUARD_BEGIN
+  constexpr size_t MIN_PER_REPLICA = 1024;
   if (!sp || !out) return set_error(-2, "NULL argument");
   if (n && !roots) return set_error(-2, "roots is NULL");
   Snapshot* s = reinterpret_cast<Snapshot*>(sp);
-  std::lock_guard<std::mutex> lk(s->mu);
-  return kg::expand_batch(s, roots, n, global_max_depth, out);
+  const size_t R = std::max<size_t>(1, std::min(s->n_replicas(), (n + MIN_PER_REPLICA - 1) / MIN_PER_REPLICA));
+  if (R == 1) {
+    std::lock_guard<std::mutex> lk(s->mu);
+    return kg::expand_batch(s, roots, n, global_max_depth, out);
+  }
+  std::vector<kg_tree_buf> parts(R);
+  std::vector<int> rcs(R, 0);
+  std::vector<std::string> msgs(R);
+  std::vector<size_t> b(R + 1);
+  for (size_t i = 0; i <= R; i++) b[i] = n * i / R;
+  auto one = [&](size_t i) {
+    try {
+      Snapshot* r = s->replica(i);
+      std::lock_guard<std::mutex> lk(r->mu);
+      rcs[i] = kg::expand_batch(r, roots + b[i], b[i + 1] - b[i], global_max_depth, &parts[i]);
+      if (rcs[i]) {
+        char buf[1024];
+        kg_last_error(buf, sizeof buf);
+        msgs[i] = buf;
+      }
+    } catch (const std::exception& ex) {
+      rcs[i] = -5;
+      msgs[i] = ex.what();
+    }
+  };
+  std::vector<std::thread> th;
+  for (size_t i = 1; i < R; i++) th.emplace_back(one, i);
+  one(0);
+  for (auto& t : th) t.join();
+  memset(out, 0, sizeof *out);
+  int rc = 0;
+  for (size_t i = 0; i < R && !rc; i++)
+    if (rcs[i]) rc = set_error(rcs[i], "replica %zu: %s", i, msgs[i].c_str());
+  uint64_t total = 0;
+  for (size_t i = 0; i < R; i++) total += parts[i].n_nodes;
+  if (!rc) {
+    out->root_off = (uint64_t*)calloc(n + 1, 8);
+    out->nodes = (kg_tree_node*)malloc(std::max<uint64_t>(total, 1) * sizeof(kg_tree_node));
+    if (!out->root_off || !out->nodes) rc = set_error(-4, "host allocation failed");
+  }
+  if (!rc) {
+    uint64_t at = 0;
+    for (size_t i = 0; i < R; i++) {
+      const size_t m = b[i + 1] - b[i];
+      for (size_t r = 0; r < m; r++) out->root_off[b[i] + r + 1] = at + parts[i].root_off[r + 1];
+      if (parts[i].n_nodes) memcpy(out->nodes + at, parts[i].nodes, parts[i].n_nodes * sizeof(kg_tree_node));
+      at += parts[i].n_nodes;
+      out->kernel_ms = std::max(out->kernel_ms, parts[i].kernel_ms);
+    }
+    out->n_nodes = total;
+    out->n_roots = n;
+  } else {
+    free(out->root_off);
+    free(out->nodes);
+    memset(out, 0, sizeof *out);
+  }
+  for (auto& p : parts) kg_tree_free(&p);
+  return rc;
   KG_GUARD_END
 }
 

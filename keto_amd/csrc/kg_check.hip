@@ -1158,8 +1158,16 @@ int synth_queries(Snapshot* s, uint64_t seed, size_t n, kg_query* d_q) {
 // ------------------------------------------------------------------ batch driver
 static size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 
-int check_batch_device(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n, int32_t global_max_depth,
-                       uint8_t* d_out, uint32_t* d_err, kg_stats* stats) {
+// A batch in two phases, so one host thread can keep batches in flight on several devices (the
+// multi-replica kg_check_batch): check_batch_begin enqueues every kernel on the workspace's stream
+// and returns without waiting; check_batch_end waits for the stream, finishes the grid tier if its
+// first round overflowed (rare: a rerun with fewer slots) and fills the statistics.
+int check_batch_begin(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n, int32_t global_max_depth,
+                      uint8_t* d_out, uint32_t* d_err, kg_stats* stats, BatchPending* bp) {
+  *bp = BatchPending{};
+  bp->stats = stats;
+  bp->d_out = d_out;
+  bp->d_err = d_err;
   if (global_max_depth < 1) global_max_depth = 5;  // config.schema.json:308-315 default
   if (n > 0x7FFFFFFFull) return set_error(-2, "batch too large");
   HIPC(hipSetDevice(s->device));
@@ -1214,7 +1222,6 @@ int check_batch_device(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n,
     gb = hl + (size_t)H * cap_h;
     gl = gb + words;
   }
-  GridStats gs;
   bool grid_pending = false;
   const uint32_t *grid_list = nullptr, *grid_count = nullptr;
 
@@ -1321,7 +1328,7 @@ int check_batch_device(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n,
         }
       }
       // first grid round enqueued without waiting; its readback is checked after the batch's one sync
-      const int rc = grid_tier(s, w, rq, fwd_list, fwd_count, global_max_depth, d_out, d_err, stream, &gs, 1);
+      const int rc = grid_tier(s, w, rq, fwd_list, fwd_count, global_max_depth, d_out, d_err, stream, &bp->gs, 1);
       if (rc < 0) return rc;
       grid_pending = rc == 1;
       grid_list = fwd_list;
@@ -1347,16 +1354,34 @@ int check_batch_device(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n,
     HIPC(hipEventRecord(e1, stream));
     HIPC(hipMemcpyAsync(hbuf, ctl, sizeof(Ctl), hipMemcpyDeviceToHost, stream));
   }
-  if (stats || grid_pending) HIPC(hipStreamSynchronize(stream));
-  if (grid_pending) {  // a round that overflowed its log reruns here with fewer slots (synchronously)
-    if (int rc = grid_tier(s, w, rq, grid_list, grid_count, global_max_depth, d_out, d_err, stream, &gs, 2)) return rc;
+  bp->grid_pending = grid_pending;
+  bp->grid_list = grid_list;
+  bp->grid_count = grid_count;
+  bp->rq = rq;
+  bp->gdepth = global_max_depth;
+  bp->n = n;
+  bp->wg_heavy = wg_heavy;
+  bp->ctl_host = hbuf;
+  return 0;
+}
+
+int check_batch_end(Snapshot* s, Workspace* w, BatchPending* bp, bool* reran) {
+  if (reran) *reran = false;
+  kg_stats* stats = bp->stats;
+  hipStream_t stream = w->stream;
+  GridStats& gs = bp->gs;
+  if (stats || bp->grid_pending) HIPC(hipStreamSynchronize(stream));
+  if (bp->grid_pending) {  // a round that overflowed its log reruns here with fewer slots (synchronously)
+    if (int rc = grid_tier(s, w, bp->rq, bp->grid_list, bp->grid_count, bp->gdepth, bp->d_out, bp->d_err, stream, &gs, 2))
+      return rc;
+    if (reran) *reran = w->grid_reran;
   }
   if (stats) {
     float ms = 0, lms = 0;
-    HIPC(hipEventElapsedTime(&ms, e0, e1));
-    if (n) HIPC(hipEventElapsedTime(&lms, l0, l1));
+    HIPC(hipEventElapsedTime(&ms, w->ev[0], w->ev[1]));
+    if (bp->n) HIPC(hipEventElapsedTime(&lms, w->ev[2], w->ev[3]));
     Ctl h;
-    memcpy(&h, hbuf, sizeof(Ctl));
+    memcpy(&h, bp->ctl_host, sizeof(Ctl));
     for (int x = 0; x < 8; x++)
       for (int k = 0; k < ST_N; k++) h.st[k] += h.st8[x][k];
     stats->rows_opened = h.st[ST_ROWS] + h.st[ST_LROWS];
@@ -1369,7 +1394,7 @@ int check_batch_device(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n,
     stats->frontier_hbm = h.st[ST_FHBM];
     stats->n_light = h.st[ST_LIGHT];
     stats->n_medium = h.st[ST_MEDIUM];
-    stats->n_heavy = wg_heavy ? h.st[ST_HEAVY] : gs.done;
+    stats->n_heavy = bp->wg_heavy ? h.st[ST_HEAVY] : gs.done;
     stats->n_wide = h.light2_count;
     stats->n_grid = gs.done;
     stats->rows_opened += gs.rows;
@@ -1387,6 +1412,13 @@ int check_batch_device(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n,
     stats->kernel_ms = ms;
   }
   return 0;
+}
+
+int check_batch_device(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n, int32_t global_max_depth,
+                       uint8_t* d_out, uint32_t* d_err, kg_stats* stats) {
+  BatchPending bp;
+  if (int rc = check_batch_begin(s, w, d_q, n, global_max_depth, d_out, d_err, stats, &bp)) return rc;
+  return check_batch_end(s, w, &bp, nullptr);
 }
 
 }  // namespace kg

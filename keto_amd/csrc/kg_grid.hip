@@ -323,6 +323,8 @@ int grid_tier(Snapshot* s, Workspace* w, const RQuery* rq, const uint32_t* qlist
   bool resume = phase == 2;
   for (uint32_t done = 0; count < 0 || done < (uint64_t)count;) {
    if (!resume) {
+    if (phase == 1) w->grid_reran = false;
+    if (phase == 2) w->grid_reran = true;  // rounds past the first: the caller re-reads the results
     if (++w->grid_epoch == 0x10000) {  // epoch wrap: the table is zeroed once per 65535 rounds
       HIPC(hipMemsetAsync(H, 0, hcap * 8, stream));
       w->grid_epoch = 1;

@@ -2,10 +2,13 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <list>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 #include "../../include/ketogpu.h"
+#include "kg_grid.h"
 #include "kg_internal.h"
 #include "kg_synth.h"
 
@@ -39,6 +42,7 @@ struct Workspace {
   void* grid_pool = nullptr;  // grid tier: visited hash | log | slots | ctl | scan sums
   size_t grid_pool_bytes = 0;
   uint32_t grid_epoch = 0;
+  bool grid_reran = false;  // the last batch's grid tier ran rounds after the first (results rewritten)
   void* interp_pool = nullptr;
   size_t interp_pool_bytes = 0;
   uint64_t interp_layout = 0;  // (pass-2 slots, pass-1 slots, list cap) the pool was last laid out for
@@ -46,6 +50,40 @@ struct Workspace {
   void* pinned = nullptr;  // 64 KiB of pinned host memory for small device->host readbacks
   void* host_buf(size_t bytes);
   ~Workspace();
+};
+
+// One in-flight batch between check_batch_begin and check_batch_end (kg_check.hip).
+struct BatchPending {
+  kg_stats* stats = nullptr;
+  uint8_t* d_out = nullptr;
+  uint32_t* d_err = nullptr;
+  bool grid_pending = false, wg_heavy = false;
+  const uint32_t *grid_list = nullptr, *grid_count = nullptr;
+  const RQuery* rq = nullptr;
+  int32_t gdepth = 5;
+  size_t n = 0;
+  void* ctl_host = nullptr;
+  GridStats gs;
+};
+
+struct Snapshot;
+// Host-buffer batches (kg_check_batch): per calling thread, one lane per replica -- its own HIP
+// stream (hence its own batch workspace), pinned staging for queries and results, and device
+// buffers, all grown on demand and reused by every later call of that thread.
+struct Lane {
+  Snapshot* rep = nullptr;
+  int device = -1;
+  hipStream_t stream = nullptr;
+  Workspace* w = nullptr;
+  kg_query* h_q = nullptr;
+  uint8_t* h_out = nullptr;
+  uint32_t* h_err = nullptr;
+  kg_query* d_q = nullptr;
+  uint8_t* d_out = nullptr;
+  uint32_t* d_err = nullptr;
+  size_t cap = 0;
+  int reserve(size_t n);
+  ~Lane();
 };
 
 struct Snapshot {
@@ -87,6 +125,14 @@ struct Snapshot {
   int interp_wgs = 6;        // kg_snapshot_tune("interp_wgs"): k_interp_lds workgroups (4 waves) per CU (6 fit the LDS)
   uint32_t interp_cap2 = 0;  // kg_snapshot_tune("interp_cap2"): pass-2 BFS list cap of the rewrite path (0 = 256 Ki)
   int back_wgs = 3;          // kg_snapshot_tune("back_wgs"): k_back workgroups per CU (1..3, LDS allows 3)
+  // replicas: the same snapshot on more devices (kg_snapshot_create's device mask); this object is
+  // replica 0 and owns the others.  Host-buffer batches and expands are split over all of them.
+  std::vector<Snapshot*> peers;
+  Snapshot* replica(size_t i) { return i == 0 ? this : peers[i - 1]; }
+  size_t n_replicas() const { return 1 + peers.size(); }
+  std::mutex lane_mu;
+  std::list<std::pair<std::thread::id, std::vector<Lane*>>> lanes;  // list: stable addresses
+  std::vector<Lane*>* thread_lanes();  // this thread's lanes (one per replica), created on first use
 
   ~Snapshot();
   int init_device(int dev);
@@ -103,6 +149,9 @@ struct Snapshot {
 // kg_check.hip
 int check_batch_device(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n, int32_t global_max_depth,
                        uint8_t* d_out, uint32_t* d_err, kg_stats* stats);
+int check_batch_begin(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n, int32_t global_max_depth,
+                      uint8_t* d_out, uint32_t* d_err, kg_stats* stats, BatchPending* bp);
+int check_batch_end(Snapshot* s, Workspace* w, BatchPending* bp, bool* reran);
 int synth_queries(Snapshot* s, uint64_t seed, size_t n, kg_query* d_q);
 // kg_shard.hip
 int shard_seed(Snapshot* s, const kg_query* d_q, size_t n, int32_t gdepth, kg_frec* d_out, size_t cap,

@@ -220,6 +220,9 @@ static uint64_t pow2_at_least(uint64_t x) {
 }
 
 Snapshot::~Snapshot() {
+  for (auto& tl : lanes)
+    for (Lane* l : tl.second) delete l;  // before the workspaces: a lane's stream owns one of them
+  for (Snapshot* p : peers) delete p;
   if (device >= 0) hipSetDevice(device);
   for (void* p : allocs) hipFree(p);
   for (Workspace* w : wss) delete w;
@@ -242,6 +245,64 @@ void* Workspace::host_buf(size_t bytes) {
   if (bytes > 65536) return nullptr;
   if (!pinned && hipHostMalloc(&pinned, 65536, hipHostMallocDefault) != hipSuccess) pinned = nullptr;
   return pinned;
+}
+
+Lane::~Lane() {
+  if (device >= 0) hipSetDevice(device);
+  if (h_q) hipHostFree(h_q);
+  if (h_out) hipHostFree(h_out);
+  if (h_err) hipHostFree(h_err);
+  if (d_q) hipFree(d_q);
+  if (d_out) hipFree(d_out);
+  if (d_err) hipFree(d_err);
+  // the stream's workspace belongs to the replica (freed with it); the stream itself is ours
+  if (stream) hipStreamDestroy(stream);
+}
+
+int Lane::reserve(size_t n) {
+  if (n <= cap) return 0;
+  HIPC(hipSetDevice(device));
+  size_t c = std::max<size_t>(n, 4096);
+  c = std::max(c, cap + cap / 2);
+  HIPC(hipStreamSynchronize(stream));
+  for (void* p : {(void*)h_q, (void*)h_out, (void*)h_err})
+    if (p) hipHostFree(p);
+  for (void* p : {(void*)d_q, (void*)d_out, (void*)d_err})
+    if (p) hipFree(p);
+  h_q = nullptr, h_out = nullptr, h_err = nullptr, d_q = nullptr, d_out = nullptr, d_err = nullptr;
+  cap = 0;
+  HIPC(hipHostMalloc(&h_q, c * sizeof(kg_query), hipHostMallocDefault));
+  HIPC(hipHostMalloc(&h_out, c, hipHostMallocDefault));
+  HIPC(hipHostMalloc(&h_err, c * 4, hipHostMallocDefault));
+  HIPC(hipMalloc(&d_q, c * sizeof(kg_query)));
+  HIPC(hipMalloc(&d_out, c));
+  HIPC(hipMalloc(&d_err, c * 4));
+  cap = c;
+  return 0;
+}
+
+std::vector<Lane*>* Snapshot::thread_lanes() {
+  const std::thread::id me = std::this_thread::get_id();
+  std::lock_guard<std::mutex> lk(lane_mu);
+  for (auto& tl : lanes)
+    if (tl.first == me) return &tl.second;
+  std::vector<Lane*> v;
+  for (size_t i = 0; i < n_replicas(); i++) {
+    Snapshot* r = replica(i);
+    Lane* l = new Lane();
+    l->rep = r;
+    l->device = r->device;
+    if (hipSetDevice(r->device) != hipSuccess || hipStreamCreateWithFlags(&l->stream, hipStreamNonBlocking) != hipSuccess) {
+      delete l;
+      for (Lane* x : v) delete x;
+      set_error(-1, "stream for a batch lane on device %d", r->device);
+      return nullptr;
+    }
+    l->w = r->workspace(l->stream);
+    v.push_back(l);
+  }
+  lanes.emplace_back(me, std::move(v));
+  return &lanes.back().second;
 }
 
 Workspace* Snapshot::workspace(hipStream_t st) {

@@ -61,8 +61,10 @@ class Snapshot:
     """An HBM-resident, immutable snapshot of the relation tuples (rows in shard order)."""
 
     def __init__(self, tuples: np.ndarray, interner: Interner, program: Optional[Program] = None, device: int = 0,
-                 _handle=None, shard: Optional[Tuple[int, int]] = None):
-        """shard = (rank, nranks): keep only the rows of the nodes this rank owns (hash-sharded mode,
+                 _handle=None, shard: Optional[Tuple[int, int]] = None, devices: Optional[Sequence[int]] = None):
+        """devices: one replica per entry (entries may repeat); the library splits host-buffer batches
+        over them (kg_snapshot_create_on).  Default: one replica on `device`.
+        shard = (rank, nranks): keep only the rows of the nodes this rank owns (hash-sharded mode,
         keto_amd.sharded); every rank passes the same full tuple list."""
         L = _lib.load()
         self.interner = interner
@@ -79,7 +81,8 @@ class Snapshot:
         prog_c = self._prog(program)
         pc = C.byref(prog_c) if prog_c is not None else None
         if shard is None:
-            rc = L.kg_snapshot_create(_ptr(t), t.shape[0], C.byref(d), pc, device, C.byref(self._h))
+            dv = np.asarray(list(devices) if devices else [device], np.int32)
+            rc = L.kg_snapshot_create_on(_ptr(t), t.shape[0], C.byref(d), pc, _ptr(dv), len(dv), C.byref(self._h))
         else:
             rc = L.kg_snapshot_create_shard(_ptr(t), t.shape[0], C.byref(d), pc, device, shard[0], shard[1],
                                             C.byref(self._h))
@@ -99,7 +102,8 @@ class Snapshot:
     @classmethod
     def synthetic(cls, n_tuples: int, seed: int = 20250131, device: int = 0, n_layers: int = 8,
                   max_degree: int = 100000, set_fraction: float = 0.25, doc_set_fraction: float = 0.5,
-                  preset: int = 0, shard: Optional[Tuple[int, int]] = None) -> "Snapshot":
+                  preset: int = 0, shard: Optional[Tuple[int, int]] = None,
+                  devices: Optional[Sequence[int]] = None) -> "Snapshot":
         """Device-generated Drive-like graph (keto_amd/csrc/kg_synth.h); preset 0 = C2/C4, 1 = C3.
         shard = (rank, nranks): only this rank's rows (hash-sharded mode)."""
         from . import synth
@@ -112,7 +116,9 @@ class Snapshot:
         h = C.c_void_p()
         pc = C.byref(prog_c) if prog_c is not None else None
         if shard is None:
-            _lib.check(L.kg_snapshot_synthetic(C.byref(p), pc, device, C.byref(h)), "kg_snapshot_synthetic")
+            dv = np.asarray(list(devices) if devices else [device], np.int32)
+            _lib.check(L.kg_snapshot_synthetic_on(C.byref(p), pc, _ptr(dv), len(dv), C.byref(h)),
+                       "kg_snapshot_synthetic_on")
         else:
             _lib.check(L.kg_snapshot_synthetic_shard(C.byref(p), pc, device, shard[0], shard[1], C.byref(h)),
                        "kg_snapshot_synthetic_shard")
@@ -124,6 +130,16 @@ class Snapshot:
     @property
     def handle(self):
         return self._h
+
+    def replicas(self) -> List[int]:
+        """Devices of the snapshot's replicas (replica 0 first)."""
+        L = _lib.load()
+        n = L.kg_snapshot_replicas(self._h, None, 0)
+        if n < 0:
+            raise _lib.KetoGPUError(_lib.last_error())
+        a = np.zeros(max(n, 1), np.int32)
+        L.kg_snapshot_replicas(self._h, _ptr(a), n)
+        return [int(x) for x in a[:n]]
 
     def info(self) -> dict:
         a = np.zeros(4, np.uint64)
@@ -289,12 +305,12 @@ class Registry:
     (internal/driver/registry_default.go:180-192): tuples + namespaces -> snapshot + engines."""
 
     def __init__(self, tuples: Sequence[RelationTuple], namespaces: Sequence[Namespace] = (), max_read_depth: int = 5,
-                 device: int = 0, interner: Optional[Interner] = None):
+                 device: int = 0, interner: Optional[Interner] = None, devices: Optional[Sequence[int]] = None):
         self.interner = interner or Interner()
         self.config = Config(max_read_depth, list(namespaces))
         self.program = compile_program(list(namespaces), self.interner)
         arr = self.interner.tuples_array(tuples)
-        self.snapshot = Snapshot(arr, self.interner, self.program, device)
+        self.snapshot = Snapshot(arr, self.interner, self.program, device, devices=devices)
         self.mapper = Mapper(self.interner, list(namespaces) if namespaces else None)
 
     def permission_engine(self) -> Engine:

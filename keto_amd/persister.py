@@ -80,13 +80,14 @@ class SnapshotPersister:
     """relationtuple.Manager whose reads for check / expand come from a GPU snapshot."""
 
     def __init__(self, namespaces: Sequence[Namespace] = (), max_read_depth: int = 5, device: int = 0,
-                 seed: int = 0, interner: Optional[Interner] = None):
+                 seed: int = 0, interner: Optional[Interner] = None, devices: Optional[Sequence[int]] = None):
         self.interner = interner or Interner()
         self.namespaces = list(namespaces)
         self.config = Config(max_read_depth, self.namespaces)
         self.program = compile_program(self.namespaces, self.interner)
         self.mapper = Mapper(self.interner, self.namespaces if self.namespaces else None)
         self.device = device
+        self.devices = list(devices) if devices else None  # replicas (kg_snapshot_create_on)
         self._rng = random.Random(seed)
         self._rows: List[Tuple[uuid.UUID, RelationTuple]] = []  # sorted by shard id
         self._lock = threading.RLock()
@@ -171,7 +172,7 @@ class SnapshotPersister:
         with self._lock:
             if self._snap is None or self._snap_version != self._version:
                 arr = self.interner.tuples_array(t for _, t in self._rows)
-                snap = Snapshot(arr, self.interner, self.program, self.device)
+                snap = Snapshot(arr, self.interner, self.program, self.device, devices=self.devices)
                 self._snap, self._snap_version = snap, self._version
                 self.rebuilds += 1
             return self._snap
