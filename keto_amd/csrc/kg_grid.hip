@@ -282,42 +282,57 @@ int grid_tier(Snapshot* s, Workspace* w, const RQuery* rq, const uint32_t* qlist
   if (!pin) return set_error(-1, "pinned host buffer");
   uint32_t* hb = (uint32_t*)(pin + 32768);  // the lower half holds the batch's Ctl readback
   const uint64_t nn = std::max<uint32_t>(s->ds.n_nodes, 1);
-  // log capacity >= n_nodes (one slot alone always fits); hash >= 2x the log (load <= 0.5)
-  const uint64_t cap = std::max<uint64_t>(nn + 1024, 64ull << 20);
-  uint64_t hcap = 1;
-  while (hcap < 2 * cap) hcap <<= 1;
+  // Log capacity: the queries that reach this tier touch far fewer nodes than the graph holds, so a
+  // workspace starts with a log of min(n_nodes, 16 Mi) entries (~0.6 GB with its hash and tile
+  // maps, instead of ~7 GB at 1 B tuples and ~27 GB at C3's 688 M nodes -- per batch in flight).
+  // Only a single query whose region overflows that log on its own (G == 1) grows it to the size
+  // that always fits (>= n_nodes: one slot logs each node at most once).
+  const uint64_t full_cap = std::max<uint64_t>(nn + 1024, 64ull << 20);
   const uint32_t G0 = 0xFFFF;  // slot field is 16 bits
-  const size_t need = hcap * 8 + cap * (4 + 4 + 8) + 2 * TILE_CAP * 4 + (size_t)G0 * 16 + sizeof(GridCtl) + 4096;
-  if (need > w->grid_pool_bytes) {
-    if (w->grid_pool) HIPC(hipFree(w->grid_pool));
-    w->grid_pool = nullptr;
-    w->grid_pool_bytes = 0;
-    HIPC(hipMalloc(&w->grid_pool, need));
-    HIPC(hipMemsetAsync(w->grid_pool, 0, hcap * 8, stream));  // epoch 0 = empty
-    w->grid_pool_bytes = need;
-    w->grid_epoch = 0;
-  }
-  char* p = (char*)w->grid_pool;
-  uint64_t* H = (uint64_t*)p;
-  p += hcap * 8;
-  GridLog lg;
-  lg.cap = cap;
-  lg.ex = (uint64_t*)p;
-  p += cap * 8;
-  lg.slot = (uint32_t*)p;
-  p += cap * 4;
-  lg.rb = (uint32_t*)p;
-  p += cap * 4;
-  lg.tile_first[0] = (uint32_t*)p;
-  p += TILE_CAP * 4;
-  lg.tile_first[1] = (uint32_t*)p;
-  p += TILE_CAP * 4;
-  uint2* slot_info = (uint2*)p;
-  p += (size_t)G0 * 8;
-  uint32_t* slot_q = (uint32_t*)p;
-  uint32_t* slot_hit = slot_q + G0;
-  p += (size_t)G0 * 8;
-  GridCtl* ctl = (GridCtl*)(((uintptr_t)p + 255) & ~uintptr_t(255));
+  uint64_t cap = 0, hcap = 0;
+  uint64_t* H = nullptr;
+  GridLog lg{};
+  uint2* slot_info = nullptr;
+  uint32_t *slot_q = nullptr, *slot_hit = nullptr;
+  GridCtl* ctl = nullptr;
+  auto layout = [&]() -> int {
+    cap = w->grid_cap ? w->grid_cap : std::min<uint64_t>(full_cap, 16ull << 20);
+    hcap = 1;
+    while (hcap < 2 * cap) hcap <<= 1;  // hash >= 2x the log (load <= 0.5)
+    const size_t need = hcap * 8 + cap * (4 + 4 + 8) + 2 * TILE_CAP * 4 + (size_t)G0 * 16 + sizeof(GridCtl) + 4096;
+    if (need > w->grid_pool_bytes) {
+      if (w->grid_pool) HIPC(hipFree(w->grid_pool));
+      w->grid_pool = nullptr;
+      w->grid_pool_bytes = 0;
+      HIPC(hipMalloc(&w->grid_pool, need));
+      HIPC(hipMemsetAsync(w->grid_pool, 0, hcap * 8, stream));  // epoch 0 = empty
+      w->grid_pool_bytes = need;
+      w->grid_epoch = 0;
+    }
+    w->grid_cap = cap;
+    char* p = (char*)w->grid_pool;
+    H = (uint64_t*)p;
+    p += hcap * 8;
+    lg.cap = cap;
+    lg.ex = (uint64_t*)p;
+    p += cap * 8;
+    lg.slot = (uint32_t*)p;
+    p += cap * 4;
+    lg.rb = (uint32_t*)p;
+    p += cap * 4;
+    lg.tile_first[0] = (uint32_t*)p;
+    p += TILE_CAP * 4;
+    lg.tile_first[1] = (uint32_t*)p;
+    p += TILE_CAP * 4;
+    slot_info = (uint2*)p;
+    p += (size_t)G0 * 8;
+    slot_q = (uint32_t*)p;
+    slot_hit = slot_q + G0;
+    p += (size_t)G0 * 8;
+    ctl = (GridCtl*)(((uintptr_t)p + 255) & ~uintptr_t(255));
+    return 0;
+  };
+  if (int rc = layout()) return rc;
   uint32_t G = G0;
   int64_t count = -1;  // unknown until the first readback
   bool resume = phase == 2;
@@ -362,7 +377,13 @@ int grid_tier(Snapshot* s, Workspace* w, const RQuery* rq, const uint32_t* qlist
       gs->edges += h.edges;
     }
     if (h.overflow) {  // log or probe bound exceeded: rerun these queries with fewer slots
-      if (G == 1) return set_error(KG_ERR_RESOURCE_CODE, "grid tier capacity exceeded");
+      if (G == 1) {
+        if (cap >= full_cap) return set_error(KG_ERR_RESOURCE_CODE, "grid tier capacity exceeded");
+        HIPC(hipStreamSynchronize(stream));  // one query alone overflowed: grow the log to the full size
+        w->grid_cap = full_cap;
+        if (int rc = layout()) return rc;
+        continue;
+      }
       G = std::max<uint32_t>(1, std::min(G, cnt) / 4);
       continue;
     }

@@ -42,6 +42,7 @@ struct Workspace {
   void* grid_pool = nullptr;  // grid tier: visited hash | log | slots | ctl | scan sums
   size_t grid_pool_bytes = 0;
   uint32_t grid_epoch = 0;
+  uint64_t grid_cap = 0;    // grid-tier log entries the pool is laid out for (0: not yet)
   bool grid_reran = false;  // the last batch's grid tier ran rounds after the first (results rewritten)
   void* interp_pool = nullptr;
   size_t interp_pool_bytes = 0;
