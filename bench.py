@@ -18,6 +18,7 @@ over ranks; rank 0 prints ONE JSON line.
 from __future__ import annotations
 
 import argparse
+import collections
 import ctypes as C
 import json
 import os
@@ -63,9 +64,14 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--preset", type=int, default=0,
                     help="0 = C2/C4 rewrite-free (headline); 1 = C3 (OPL view/edit/share via the rewrite interpreter)")
-    ap.add_argument("--mode", choices=["check", "expand", "sharded"], default="check",
+    ap.add_argument("--mode", choices=["check", "expand", "sharded", "host"], default="check",
                     help="expand = config C5: batched BuildTree of hot group#member roots; sharded = the "
-                         "hash-sharded mode (each rank holds 1/N of the graph, all-to-all frontier exchange)")
+                         "hash-sharded mode (each rank holds 1/N of the graph, all-to-all frontier exchange); "
+                         "host = the host-buffer boundary end to end: kg_check_batch over a snapshot replicated "
+                         "on every visible GPU (PCIe included), then the request batcher fed single checks")
+    ap.add_argument("--callers", type=int, default=4, help="--mode host: threads calling kg_check_batch at once")
+    ap.add_argument("--clients", type=int, default=256,
+                    help="--mode host: native caller threads of the request batcher (one blocking call per request)")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for --mode sharded (nccl = RCCL)")
     ap.add_argument("--roots", type=int, default=100_000, help="expand roots per step (C5)")
     return ap.parse_args()
@@ -176,6 +182,135 @@ def bench_sharded(a):
         dist.destroy_process_group()
 
 
+def bench_host(a):
+    """The host-buffer boundary end to end (what the cgo binding in INTEGRATION.md calls): one process,
+    the snapshot replicated on every visible GPU (kg_snapshot_synthetic_on), and
+      (1) `callers` threads each calling kg_check_batch on its own 1M-check host batches -- H2D, the
+          tiers, D2H, split over the replicas inside the library; checks/s and p50/p99 per call;
+      (2) the library's request batcher (kg_batcher_check: one blocking call per request, the shape of
+          one goroutine per Check RPC, internal/check/handler.go:248) driven by `clients` native caller
+          threads (tools/kg_loadgen.cpp, no Python on the request path) for a few seconds, every answer
+          checked against a direct batch; checks/s, per-call and per-batch p50/p99.
+      (3) the same batcher from Python threads (keto_amd.batcher.NativeBatcher.check_ids), for scale."""
+    import torch
+    from keto_amd import _lib
+    from keto_amd.batcher import NativeBatcher
+    from keto_amd.build import TOOLS_LIB
+    from keto_amd.engine import Config, Engine, Snapshot
+    L = _lib.load()
+    n_dev = max(1, torch.cuda.device_count()) if a.gpus <= 1 else a.gpus
+    devices = list(range(n_dev))
+    t_build = time.time()
+    snap = Snapshot.synthetic(int(a.tuples), seed=a.seed, devices=devices, preset=a.preset)
+    snap.tune("stream", a.stream)
+    snap.tune("stream_wgs", a.stream_wgs)
+    snap.tune("back_wgs", a.back_wgs)
+    snap.tune("grid_wgs", a.grid_wgs)
+    t_build = time.time() - t_build
+    B, T = a.batch, max(1, a.callers)
+    torch.cuda.set_device(0)
+    qs = []
+    for t in range(T):  # distinct batches per caller, generated on the device then held on the host
+        d = torch.empty((B, 7), dtype=torch.int32, device="cuda:0")
+        _lib.check(L.kg_synth_queries(snap.handle, 1000 + 7919 * t, B, d.data_ptr()), "kg_synth_queries")
+        qs.append(np.ascontiguousarray(d.cpu().numpy().view(np.uint32)))
+    eng = Engine(snap, Config(a.global_depth))
+    expect = eng.batch_check_ids(qs[0])[0]
+
+    def call(t, out, err):
+        rc = L.kg_check_batch(snap.handle, qs[t].ctypes.data_as(C.c_void_p), B, a.global_depth,
+                              out.ctypes.data_as(C.c_void_p), err.ctypes.data_as(C.c_void_p), None)
+        _lib.check(rc, "kg_check_batch")
+
+    lat, errs = [], []
+    per = max(1, a.steps // T)
+    ready = threading.Barrier(T + 1)
+
+    def worker(t):
+        try:
+            out = np.empty(B, np.uint8)
+            err = np.empty(B, np.uint32)
+            call(t, out, err)  # this thread's lanes (stream, pinned staging, workspace) exist before timing
+            ready.wait()
+            for _ in range(per):
+                s0 = time.perf_counter()
+                call(t, out, err)
+                lat.append(time.perf_counter() - s0)
+            if t == 0:
+                assert (out == expect).all() and (err == 0).all()
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+            ready.abort()
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(T)]
+    [x.start() for x in th]
+    ready.wait()
+    t0 = time.perf_counter()
+    [x.join() for x in th]
+    el = time.perf_counter() - t0
+    if errs:
+        raise errs[0]
+    host_rate = B * per * T / el
+    # (2) native batcher under native callers
+    LG = C.CDLL(TOOLS_LIB)
+    LG.kgl_batcher_load.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_int, C.c_int, C.c_double,
+                                    C.POINTER(C.c_uint64), C.POINTER(C.c_double), C.POINTER(C.c_uint64)]
+    q0 = qs[0]
+    batcher = {}
+    for clients, per_call in ((a.clients, 1), (a.clients, 16)):
+        with NativeBatcher(snap, a.global_depth, max_batch=1 << 16, max_wait_us=200, dispatchers=2) as nb:
+            n_chk, el2, bad = C.c_uint64(), C.c_double(), C.c_uint64()
+            rc = LG.kgl_batcher_load(nb.handle, q0.ctypes.data_as(C.c_void_p), len(q0),
+                                     expect.ctypes.data_as(C.c_void_p), 64, per_call, 0.5, C.byref(n_chk),
+                                     C.byref(el2), C.byref(bad))  # warm-up
+            nb.reset_stats()
+            rc = LG.kgl_batcher_load(nb.handle, q0.ctypes.data_as(C.c_void_p), len(q0),
+                                     expect.ctypes.data_as(C.c_void_p), clients, per_call, 3.0, C.byref(n_chk),
+                                     C.byref(el2), C.byref(bad))
+            assert rc == 0 and bad.value == 0, (rc, bad.value)
+            st = nb.stats()
+            batcher[f"native_{clients}x{per_call}"] = {
+                "callers": clients, "checks_per_call": per_call, "checks_per_s": n_chk.value / el2.value,
+                "p50_call_ms": st["call_p50_ms"], "p99_call_ms": st["call_p99_ms"],
+                "p50_batch_ms": st["batch_p50_ms"], "p99_batch_ms": st["batch_p99_ms"],
+                "mean_batch": st["checks"] / max(1, st["batches"]), "answers_checked": n_chk.value}
+    # (3) the same batcher from Python threads
+    with NativeBatcher(snap, a.global_depth, max_batch=1 << 16, max_wait_us=200, dispatchers=2) as nb:
+        n_py, stop = [0], [False]
+
+        def pyclient(c):
+            i, k = c * 9973 % len(q0), 0
+            while not stop[0]:
+                o, e = nb.check_ids(q0[i:i + 1])
+                assert o[0] == expect[i]
+                i = (i + 1) % len(q0)
+                k += 1
+            n_py[0] += k
+
+        th = [threading.Thread(target=pyclient, args=(c,)) for c in range(16)]
+        t0 = time.perf_counter()
+        [x.start() for x in th]
+        time.sleep(2.0)
+        stop[0] = True
+        [x.join() for x in th]
+        el3 = time.perf_counter() - t0
+        st = nb.stats()
+        batcher["python_16x1"] = {"callers": 16, "checks_per_call": 1, "checks_per_s": n_py[0] / el3,
+                                  "p50_call_ms": st["call_p50_ms"], "p99_call_ms": st["call_p99_ms"],
+                                  "p99_batch_ms": st["batch_p99_ms"], "mean_batch": st["checks"] / max(1, st["batches"])}
+    out = {"metric": "permission checks/sec through the host-buffer boundary (kg_check_batch, PCIe included)",
+           "value": host_rate, "unit": "checks/s", "n_gpus": n_dev, "steps": per * T, "warmup": T,
+           "ms_per_step": el / per * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+           "dtype": "u32", "data": "synthetic (device-generated Drive-like tuple graph, seed %d)" % a.seed,
+           "config": {"workload": "C2/C4 generator @ %.3g tuples, %d-check host batches, %d caller threads, "
+                                  "max_read_depth %d" % (a.tuples, B, T, a.global_depth),
+                      "replicas": devices, "parallelism": "replicas in one process"},
+           "p50_call_ms": float(np.percentile(np.array(lat) * 1e3, 50)),
+           "p99_call_ms": float(np.percentile(np.array(lat) * 1e3, 99)),
+           "batcher": batcher, "snapshot_build_s": t_build}
+    print(json.dumps(out), flush=True)
+
+
 def aggregate(dist, elapsed: float, edges: float, device=None):
     """Whole-job numbers over ranks: elapsed = MAX over ranks (the job ends with its slowest
     rank), edges = SUM.  Replicas exchange nothing else."""
@@ -195,6 +330,8 @@ def main():
         return bench_expand(a)
     if a.mode == "sharded":
         return bench_sharded(a)
+    if a.mode == "host":
+        return bench_host(a)
     import torch
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))

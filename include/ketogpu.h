@@ -226,6 +226,27 @@ int kg_check_batch_device(kg_snapshot* s, const kg_query* d_q, size_t n, int32_t
  * 50% uniform doc#viewer@user queries, max_depth in {0,1..10}.  d_q is a device buffer. */
 int kg_synth_queries(kg_snapshot* s, uint64_t seed, size_t n, kg_query* d_q);
 
+/* ---- request batcher -----------------------------------------------
+ * Replaces one goroutine per Check RPC (internal/check/handler.go:248 -> CheckIsMember,
+ * internal/check/engine.go:54-60) with one BLOCKING call per request: concurrent callers' queries
+ * are coalesced into kg_check_batch batches (closed at max_batch queries or when the oldest has
+ * waited max_wait_us) run by `dispatchers` threads, so consecutive batches overlap on the devices.
+ * Each caller gets exactly its own answers (allowed = a loop of CheckIsMember). */
+typedef struct kg_batcher kg_batcher;
+typedef struct {
+  uint64_t batches, checks;          /* since creation / the last reset                         */
+  double batch_p50_ms, batch_p99_ms; /* oldest submission of a batch -> its answers delivered    */
+  double call_p50_ms, call_p99_ms;   /* one kg_batcher_check call, submit -> return               */
+} kg_batcher_stats_t;
+int kg_batcher_create(kg_snapshot* s, int32_t global_max_depth, size_t max_batch, uint32_t max_wait_us,
+                      int dispatchers, kg_batcher** out);
+/* n queries of one caller (usually 1); out[n] / err_code[n] as in kg_check_batch.  Thread-safe. */
+int kg_batcher_check(kg_batcher* b, const kg_query* q, size_t n, uint8_t* out, uint32_t* err_code);
+int kg_batcher_stats(kg_batcher* b, kg_batcher_stats_t* st);
+void kg_batcher_reset_stats(kg_batcher* b);
+/* Answers what is pending, stops the dispatchers, frees the batcher (the snapshot stays). */
+void kg_batcher_destroy(kg_batcher* b);
+
 /* ---- hash-sharded mode --------------------------------------------------------
  * For graphs larger than one GPU: rank r of N holds the rows of the nodes (ns, obj, rel) with
  * kg_shard_owner(ns, obj, N) == r (all relations of an object on one rank).  A batch is a

@@ -77,7 +77,13 @@ EXPORTS = ["kg_snapshot_create", "kg_snapshot_create_on", "kg_snapshot_synthetic
            "kg_snapshot_replicas", "kg_snapshot_destroy", "kg_snapshot_info", "kg_snapshot_tune", "kg_synth_ids",
            "kg_snapshot_export", "kg_snapshot_export_csr", "kg_check_batch", "kg_check_batch_device", "kg_synth_queries", "kg_expand_batch",
            "kg_tree_free", "kg_last_error", "kg_version", "kg_shard_owner", "kg_snapshot_create_shard",
-           "kg_snapshot_synthetic_shard", "kg_shard_seed", "kg_shard_level", "kg_shard_finish"]
+           "kg_snapshot_synthetic_shard", "kg_shard_seed", "kg_shard_level", "kg_shard_finish",
+           "kg_batcher_create", "kg_batcher_check", "kg_batcher_stats", "kg_batcher_reset_stats", "kg_batcher_destroy"]
+
+
+class kg_batcher_stats_t(C.Structure):
+    _fields_ = [("batches", C.c_uint64), ("checks", C.c_uint64), ("batch_p50_ms", C.c_double),
+                ("batch_p99_ms", C.c_double), ("call_p50_ms", C.c_double), ("call_p99_ms", C.c_double)]
 
 
 class KetoGPUError(RuntimeError):
@@ -131,10 +137,18 @@ def load(path: str = LIB_PATH):
     L.kg_shard_seed.argtypes = [vp, vp, sz, i32, vp, sz, vp, vp, vp, vp]
     L.kg_shard_level.argtypes = [vp, vp, sz, vp, vp, sz, vp, vp, vp, vp]
     L.kg_shard_finish.argtypes = [vp, sz, vp, vp, vp]
+    L.kg_batcher_create.argtypes = [vp, i32, sz, u32, C.c_int, C.POINTER(vp)]
+    L.kg_batcher_check.argtypes = [vp, vp, sz, vp, vp]
+    L.kg_batcher_stats.argtypes = [vp, C.POINTER(kg_batcher_stats_t)]
+    L.kg_batcher_reset_stats.argtypes = [vp]
+    L.kg_batcher_reset_stats.restype = None
+    L.kg_batcher_destroy.argtypes = [vp]
+    L.kg_batcher_destroy.restype = None
     for name in ("kg_snapshot_create", "kg_snapshot_create_on", "kg_snapshot_synthetic", "kg_snapshot_synthetic_on",
                  "kg_snapshot_replicas", "kg_snapshot_info", "kg_snapshot_tune", "kg_synth_ids", "kg_check_batch",
                  "kg_check_batch_device", "kg_synth_queries", "kg_expand_batch", "kg_snapshot_create_shard",
-                 "kg_snapshot_synthetic_shard", "kg_shard_seed", "kg_shard_level", "kg_shard_finish"):
+                 "kg_snapshot_synthetic_shard", "kg_shard_seed", "kg_shard_level", "kg_shard_finish",
+                 "kg_batcher_create", "kg_batcher_check", "kg_batcher_stats"):
         getattr(L, name).restype = C.c_int
     _lib = L
     return L

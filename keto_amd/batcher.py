@@ -15,6 +15,7 @@ its answer) that BASELINE.json's p99 metric names.
 from __future__ import annotations
 
 import collections
+import ctypes as C
 import threading
 import time
 from concurrent.futures import Future
@@ -143,3 +144,64 @@ class CheckBatcher:
         if not self.batch_latency_s:
             return 0.0
         return float(np.percentile(np.asarray(self.batch_latency_s), p) * 1e3)
+
+
+class NativeBatcher:
+    """The library's request batcher (kg_batcher_*, keto_amd/csrc/kg_batcher.cpp): one BLOCKING call
+    per request, the shape a Go handler goroutine binds through cgo.  Calls from
+    many Python threads run concurrently in the library (ctypes releases the GIL for the wait)."""
+
+    def __init__(self, snapshot, max_read_depth: int = 5, max_batch: int = 1 << 16, max_wait_us: int = 200,
+                 dispatchers: int = 2):
+        self.snapshot = snapshot
+        self.L = _lib.load()
+        self._h = C.c_void_p()
+        _lib.check(self.L.kg_batcher_create(snapshot.handle, max_read_depth, max_batch, max_wait_us, dispatchers,
+                                            C.byref(self._h)), "kg_batcher_create")
+
+    @property
+    def handle(self):
+        return self._h
+
+    def check_ids(self, q) -> Tuple[np.ndarray, np.ndarray]:
+        """(n, 7) kg_query rows of ONE caller -> (result u8, err u32); blocks until answered."""
+        q = np.ascontiguousarray(q, np.uint32).reshape(-1, 7)
+        out = np.zeros(q.shape[0], np.uint8)
+        err = np.zeros(q.shape[0], np.uint32)
+        _lib.check(self.L.kg_batcher_check(self._h, q.ctypes.data_as(C.c_void_p), q.shape[0],
+                                           out.ctypes.data_as(C.c_void_p), err.ctypes.data_as(C.c_void_p)),
+                   "kg_batcher_check")
+        return out, err
+
+    def check_is_member(self, t: RelationTuple, rest_depth: int) -> bool:
+        """CheckIsMember through the native batcher (internal/check/engine.go:54-60)."""
+        it = self.snapshot.interner
+        out, err = self.check_ids(queries_array(np.asarray(it.tuple_ids(t), np.uint32), rest_depth))
+        if out[0] == _lib.KG_ERROR:
+            raise CheckError(int(err[0]))
+        return bool(out[0] == _lib.KG_IS_MEMBER)
+
+    def stats(self) -> dict:
+        st = _lib.kg_batcher_stats_t()
+        _lib.check(self.L.kg_batcher_stats(self._h, C.byref(st)), "kg_batcher_stats")
+        return {n: getattr(st, n) for n, _ in st._fields_}
+
+    def reset_stats(self) -> None:
+        self.L.kg_batcher_reset_stats(self._h)
+
+    def close(self) -> None:
+        if self._h:
+            self.L.kg_batcher_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __enter__(self) -> "NativeBatcher":
+        return self
+
+    def __exit__(self, *exc) -> None:
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass

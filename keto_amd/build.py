@@ -10,7 +10,7 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB_DIR = os.path.join(HERE, "lib")
 LIB = os.path.join(LIB_DIR, "libketogpu.so")
-SOURCES = ["kg_abi.cpp", "kg_snapshot.hip", "kg_check.hip", "kg_grid.hip", "kg_interp.hip", "kg_expand.hip", "kg_shard.hip"]
+SOURCES = ["kg_abi.cpp", "kg_batcher.cpp", "kg_snapshot.hip", "kg_check.hip", "kg_grid.hip", "kg_interp.hip", "kg_expand.hip", "kg_shard.hip"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("KG_OFFLOAD_ARCH", "gfx950")
 
@@ -20,7 +20,7 @@ def sources():
 
 
 def stale() -> bool:
-    if not os.path.exists(LIB):
+    if not os.path.exists(LIB) or not os.path.exists(os.path.join(ROOT, "tools", "lib", "libkg_loadgen.so")):
         return True
     t = os.path.getmtime(LIB)
     deps = sources() + [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
@@ -56,7 +56,20 @@ def build(force: bool = False, verbose: bool = False) -> str:
     os.replace(tmp, LIB)
     for o in objs:
         os.remove(o)
+    build_tools()
     return LIB
+
+
+TOOLS_LIB = os.path.join(ROOT, "tools", "lib", "libkg_loadgen.so")
+
+
+def build_tools() -> str:
+    """tools/kg_loadgen.cpp (bench load generator for the batcher; links libketogpu.so)."""
+    src = os.path.join(ROOT, "tools", "kg_loadgen.cpp")
+    os.makedirs(os.path.dirname(TOOLS_LIB), exist_ok=True)
+    subprocess.run(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", src, "-o", TOOLS_LIB, "-L", LIB_DIR, "-lketogpu",
+                    "-Wl,-rpath," + LIB_DIR, "-Wl,-rpath,$ORIGIN/../../keto_amd/lib", "-lpthread"], check=True)
+    return TOOLS_LIB
 
 
 if __name__ == "__main__":

@@ -1,5 +1,7 @@
-# GPU parity suite + smoke + default bench line (+ optional extra bench args in BENCH_EXTRA).
-# usage: gpurun -- 'bash scripts/gpu_tests.sh'   (env: TESTS="tests -m gpu", TAG=r2a, BENCH=1)
+# GPU parity suite + smoke + default bench line, then an optional second bench (BENCH2 args).
+# usage: gpurun -- 'bash scripts/gpu_tests.sh'
+#   env: TESTS="tests -m gpu" (pytest args), TAG=r2a (log suffix), BENCH=1 (0 skips the default
+#        bench), BENCH_EXTRA (args of the default bench), BENCH2 (args of a second bench run)
 set -u
 TAG=${TAG:-r2}
 TESTS=${TESTS:-tests -m gpu}
@@ -11,5 +13,9 @@ timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_ou
 [ $rc -eq 0 ] || exit $rc
 if [ "${BENCH:-1}" = "1" ]; then
   timeout -k 10 300 python bench.py ${BENCH_EXTRA:-} > gpurun_out/bench_${TAG}.log 2>&1; rc=$?; echo "bench rc=$rc"; tail -1 gpurun_out/bench_${TAG}.log | cut -c1-400
+  [ $rc -eq 0 ] || exit $rc
+fi
+if [ -n "${BENCH2:-}" ]; then
+  timeout -k 10 300 python bench.py $BENCH2 > gpurun_out/bench2_${TAG}.log 2>&1; rc=$?; echo "bench2 rc=$rc"; tail -1 gpurun_out/bench2_${TAG}.log | cut -c1-600
 fi
 exit $rc

@@ -1,12 +1,13 @@
 """GPU tests: the snapshot persister (writes invalidate the HBM snapshot; checks see every
 committed write) and the request batcher (concurrent callers coalesced into kg_check_batch
 calls), both against the CPU oracle on the persister's rows in shard order.  Bit-exact."""
+import ctypes as C
 import threading
 
 import numpy as np
 import pytest
 
-from keto_amd.batcher import CheckBatcher
+from keto_amd.batcher import CheckBatcher, NativeBatcher
 from keto_amd.engine import queries_array
 from keto_amd.ketoapi import RelationTuple, SubjectSet
 from keto_amd.persister import RelationQuery, SnapshotPersister
@@ -78,6 +79,8 @@ def test_batcher_vs_direct_batch():
     depths = rng.integers(0, 7, len(qs))
     q7 = queries_array(q6, depths)
     want, _ = e.batch_check_ids(q7)
+    exp, _, _ = Oracle(shard_rows(m), it.wildcard_rel).check_batch(q6, depths, 5, POLICY_CANONICAL)
+    assert (want == exp).all()  # the direct batch is itself pinned to the oracle
     got = np.full(len(qs), 255, np.uint8)
     with CheckBatcher(e, max_batch=512, max_wait_us=300) as b:
         def worker(k):
@@ -102,3 +105,48 @@ def test_persister_empty_snapshot():
     m.delete_relation_tuples(t)
     assert not e.check_is_member(t, 0)
     assert m.expand_engine().build_tree(SubjectSet("doc", "a", "view"), 0) is None
+
+
+def test_native_batcher_many_callers_vs_oracle():
+    """The library's request batcher (kg_batcher_check): 16 threads, each one blocking call per
+    request (single checks and small bursts), against the oracle; rewrite errors come back per
+    query; close answers what is pending and then refuses."""
+    from keto_amd import _lib
+    from keto_amd.engine import Registry
+    from keto_amd.namespace import Namespace, Relation
+    rng = np.random.default_rng(9)
+    it, tuples, nss, rels = random_graph(rng, n_obj=80, n_rows=900)
+    # namespace n0 declares r0, r1 only: queries reaching n0:*#r2 answer "relation not found"
+    namespaces = [Namespace("n0", [Relation("r0"), Relation("r1")])]
+    reg = Registry(tuples, namespaces, max_read_depth=5, interner=it, devices=[0, 0])
+    qs = random_queries(rng, nss, rels, 3000, n_obj=80)
+    q6 = np.asarray([it.tuple_ids(t) for t in qs], np.uint32)
+    depths = rng.integers(0, 7, len(qs))
+    q7 = queries_array(q6, depths)
+    exp, oerr, _ = Oracle(it.tuples_array(tuples), it.wildcard_rel, reg.program).check_batch(
+        q6, depths, 5, POLICY_CANONICAL)
+    assert (oerr != 0).any()
+    got = np.full(len(qs), 255, np.uint8)
+    gerr = np.zeros(len(qs), np.uint32)
+    with NativeBatcher(reg.snapshot, 5, max_batch=256, max_wait_us=500, dispatchers=2) as nb:
+        def worker(k):
+            i = k
+            while i < len(qs):
+                n = 1 if k % 2 else min(5, len(qs) - i)  # odd threads: single checks, even: bursts
+                sl = [i + j * 16 for j in range(n) if i + j * 16 < len(qs)]
+                o, er = nb.check_ids(q7[sl])
+                got[sl], gerr[sl] = o, er
+                i += 16 * len(sl)
+        ts = [threading.Thread(target=worker, args=(k,)) for k in range(16)]
+        [t.start() for t in ts]
+        [t.join() for t in ts]
+        st = nb.stats()
+        assert st["checks"] == len(qs) and st["batches"] < len(qs) and st["call_p99_ms"] > 0
+        assert nb.check_is_member(qs[0], int(depths[0])) == bool(exp[0] == 1) or exp[0] == 2
+    assert (got == exp).all(), np.nonzero(got != exp)[0][:10]
+    assert (gerr.astype(np.int64) == oerr).all()
+    with pytest.raises(_lib.KetoGPUError):
+        nb2 = NativeBatcher(reg.snapshot, 5)
+        nb2.L.kg_batcher_destroy(nb2._h)  # closed under the Python object: the next call must fail cleanly
+        nb2._h = C.c_void_p()
+        nb2.check_ids(q7[:1])
