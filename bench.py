@@ -35,7 +35,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 STREAM_KERNELS = {0: "k_stream<8,7,256,16>", 1: "k_stream<16,6,256,32>", 2: "k_stream<16,7,512,32>",
                   3: "k_stream<32,5,192,64>", 4: "k_stream<32,6,256,64>", 5: "k_stream<32,wave1024/128,256,64>",
                   6: "k_stream<32,wave1024/256,320,64>", 7: "k_stream<32,wave1024/64,256,64>",
-                  8: "k_stream<32,wave512/64,256,64>"}
+                  8: "k_stream<32,wave512/64,256,64>", 9: "k_stream2<9,256,64,64>"}
 
 
 def parse():
@@ -49,11 +49,11 @@ def parse():
     ap.add_argument("--seed", type=int, default=20250131)
     ap.add_argument("--tiers", type=int, default=0, help="kg_snapshot_tune tiers (0 grid, 1 LDS-WG+grid, 2 WG)")
     ap.add_argument("--wide", type=int, default=0, help="kg_snapshot_tune wide (k_light<64> tier on/off)")
-    ap.add_argument("--stream", type=int, default=8, help="kg_snapshot_tune stream (k_stream variant 0..8)")
+    ap.add_argument("--stream", type=int, default=9, help="kg_snapshot_tune stream (k_stream variant 0..8, 9 = k_stream2)")
     ap.add_argument("--stream-ecap", type=int, default=0, help="kg_snapshot_tune stream_ecap (edges per query, 0 = none)")
     ap.add_argument("--grid-wgs", type=int, default=4, help="kg_snapshot_tune grid_wgs (k_grid_level WGs per CU)")
-    ap.add_argument("--stream-wgs", type=int, default=3,
-                    help="kg_snapshot_tune stream_wgs (k_stream WGs per CU, 0 = auto; 3 of the ~45 KiB variant-8 WGs leave room for the other in-flight batches)")
+    ap.add_argument("--stream-wgs", type=int, default=0,
+                    help="kg_snapshot_tune stream_wgs (k_stream WGs per CU, 0 = by variant: 5 for k_stream2's ~29 KiB WGs)")
     ap.add_argument("--back", type=int, default=2, help="kg_snapshot_tune back (1 backward tier wave+WG widths, 2 wave width only, 0 off)")
     ap.add_argument("--back-wgs", type=int, default=1,
                     help="kg_snapshot_tune back_wgs (k_back WGs per CU; 1 leaves LDS to the other in-flight batches)")
@@ -258,7 +258,7 @@ def bench_host(a):
     q0 = qs[0]
     batcher = {}
     for clients, per_call in ((a.clients, 1), (a.clients, 16)):
-        with NativeBatcher(snap, a.global_depth, max_batch=1 << 16, max_wait_us=200, dispatchers=2) as nb:
+        with NativeBatcher(snap, a.global_depth, max_batch=1 << 16, max_wait_us=200, dispatchers=4) as nb:
             n_chk, el2, bad = C.c_uint64(), C.c_double(), C.c_uint64()
             rc = LG.kgl_batcher_load(nb.handle, q0.ctypes.data_as(C.c_void_p), len(q0),
                                      expect.ctypes.data_as(C.c_void_p), 64, per_call, 0.5, C.byref(n_chk),
@@ -275,7 +275,7 @@ def bench_host(a):
                 "p50_batch_ms": st["batch_p50_ms"], "p99_batch_ms": st["batch_p99_ms"],
                 "mean_batch": st["checks"] / max(1, st["batches"]), "answers_checked": n_chk.value}
     # (3) the same batcher from Python threads
-    with NativeBatcher(snap, a.global_depth, max_batch=1 << 16, max_wait_us=200, dispatchers=2) as nb:
+    with NativeBatcher(snap, a.global_depth, max_batch=1 << 16, max_wait_us=200, dispatchers=4) as nb:
         n_py, stop = [0], [False]
 
         def pyclient(c):

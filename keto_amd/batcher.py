@@ -152,7 +152,7 @@ class NativeBatcher:
     many Python threads run concurrently in the library (ctypes releases the GIL for the wait)."""
 
     def __init__(self, snapshot, max_read_depth: int = 5, max_batch: int = 1 << 16, max_wait_us: int = 200,
-                 dispatchers: int = 2):
+                 dispatchers: int = 4):
         self.snapshot = snapshot
         self.L = _lib.load()
         self._h = C.c_void_p()

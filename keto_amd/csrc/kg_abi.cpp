@@ -257,7 +257,7 @@ static int tune_one(Snapshot* s, const char* key, int64_t value) {
     return 0;
   }
   if (strcmp(key, "stream") == 0) {
-    if (value < 0 || value > 8) return set_error(-2, "stream must be in [0, 8]");
+    if (value < 0 || value > 9) return set_error(-2, "stream must be in [0, 9]");
     s->stream_variant = (int)value;
     return 0;
   }
@@ -385,6 +385,10 @@ int kg_check_batch(kg_snapshot* sp, const kg_query* q, size_t n, int32_t global_
   std::vector<kg::Lane*>* lanes = s->thread_lanes();
   if (!lanes) return -1;
   const size_t R = std::max<size_t>(1, std::min(lanes->size(), (n + MIN_PER_REPLICA - 1) / MIN_PER_REPLICA));
+  // batches that use fewer replicas than exist rotate over them (a batcher's small batches spread
+  // over every GPU instead of all landing on replica 0)
+  const size_t r0 = R < lanes->size() ? (size_t)(s->rr_next.fetch_add(1, std::memory_order_relaxed) % lanes->size()) : 0;
+  auto lane = [&](size_t i) { return (*lanes)[(r0 + i) % lanes->size()]; };
   std::vector<kg::BatchPending> bp(R);
   std::vector<kg_stats> st(R);
   std::vector<size_t> b(R + 1);
@@ -392,7 +396,7 @@ int kg_check_batch(kg_snapshot* sp, const kg_query* q, size_t n, int32_t global_
   size_t begun = 0;
   int rc = 0;
   for (size_t i = 0; i < R && !rc; i++) {
-    kg::Lane* L = (*lanes)[i];
+    kg::Lane* L = lane(i);
     const size_t m = b[i + 1] - b[i];
     if ((rc = L->reserve(m))) break;
     HIPC(hipSetDevice(L->device));
@@ -414,7 +418,7 @@ int kg_check_batch(kg_snapshot* sp, const kg_query* q, size_t n, int32_t global_
       rc = set_error(-1, "D2H copy failed");
   }
   for (size_t i = 0; i < begun; i++) {
-    kg::Lane* L = (*lanes)[i];
+    kg::Lane* L = lane(i);
     const size_t m = b[i + 1] - b[i];
     if (!rc) {
       hipSetDevice(L->device);

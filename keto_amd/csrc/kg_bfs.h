@@ -41,17 +41,16 @@ __device__ __forceinline__ uint32_t nmap_find(const DevSnap& s, uint32_t ns, uin
   return sl ? sl->node : NONE;
 }
 
-// checkDirect: does the exact tuple (node, subject) exist?  One 64-B bucket per probe.
+// checkDirect: does the exact tuple (node, subject) exist?  One 16-B bucket (two keys) per probe;
+// at load <= 0.25 the first bucket nearly always decides.
 __device__ __forceinline__ bool dset_probe(const DevSnap& s, uint32_t node, uint32_t subj) {
+  static_assert(DSET_BUCKET == 2, "one ulonglong2 per bucket");
   uint64_t key = dset_key(node, subj);
   uint64_t b = mix64(key) & s.dset_mask;
-  for (uint64_t n = 0; n <= s.dset_mask; n++) {  // load <= 0.5: nearly always the first bucket
-    const ulonglong2* p = reinterpret_cast<const ulonglong2*>(s.dset + b * DSET_BUCKET);
-    ulonglong2 a0 = p[0], a1 = p[1], a2 = p[2], a3 = p[3];
-    if (a0.x == key || a0.y == key || a1.x == key || a1.y == key || a2.x == key || a2.y == key || a3.x == key ||
-        a3.y == key)
-      return true;
-    if (a3.y == EMPTY64) return false;  // buckets fill front to back
+  for (uint64_t n = 0; n <= s.dset_mask; n++) {
+    const ulonglong2 a = *reinterpret_cast<const ulonglong2*>(s.dset + b * DSET_BUCKET);
+    if (a.x == key || a.y == key) return true;
+    if (a.y == EMPTY64) return false;  // buckets fill front to back
     b = (b + 1) & s.dset_mask;
   }
   return false;

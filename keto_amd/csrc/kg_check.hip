@@ -169,10 +169,10 @@ __global__ __launch_bounds__(256) void k_resolve(DevSnap s, const kg_query* __re
     }
     // rq is read only through the tier lists, so finished queries skip it (their 24 B never leave the CU)
     if (route != ROUTE_DONE) rq[i] = RQuery{node, subj, d, route, rb, rl};
-    if (route == ROUTE_DONE) {
-      out[i] = member ? KG_IS_MEMBER : KG_NOT_MEMBER;
-      if (err) err[i] = KG_ERR_NONE;
-    }
+    // every result starts as NotMember / no error (coalesced here): the tiers after this one store
+    // only what differs (k_stream2 writes IsMember bytes only)
+    out[i] = member ? KG_IS_MEMBER : KG_NOT_MEMBER;
+    if (err) err[i] = KG_ERR_NONE;
   }
   {
     const int idx[2] = {ST_PROBES, ST_NOHOLD};
@@ -732,6 +732,255 @@ __global__ __launch_bounds__(256) void k_stream(DevSnap s, const RQuery* __restr
   block_stats<7>(ctl, idx, v);
 }
 
+// ------------------------------------------------------------------ k_stream2 (variant 9, default)
+// The stream tier cut for issue rate.  PMC on k_stream (variant 8) showed a step of 64 edges costing
+// ~1,060 wave instructions, 435 of them SALU exec-mask and loop bookkeeping of divergent code (the
+// CAS-probing visited table, per-lane retry loops, conditional LDS atomics) and the waves parked on
+// memory only 68 % of their life: the kernel was as much issue- as latency-bound.  Same algorithm
+// (one FIFO of row entries shared by 32 query slots, BFS order per query, children probed one step
+// after discovery together with the next edge gathers), but:
+//   * the visited set is a DIRECT-MAPPED cache of keys valid | gen | slot | node with blind writes --
+//     no probing, no CAS, no retry loop.  It may forget a node (a collision evicts it), which can
+//     only make a node be expanded again (extra work, same answer: expanding a node again at a
+//     smaller rest depth explores a subset of what its first expansion did); it never reports a
+//     node present that this query did not insert (the key holds the slot and its generation)
+//   * FIFO entries are 8 bytes (row begin | len 11 | slot 5 | gen 9 | rest depth 7) and the
+//     per-slot state is one word (gen | HIT | OVER): ~7 KiB of LDS per wave, 5 workgroups per CU
+//     (20 waves) instead of 3 (12)
+//   * the step is straight-line, predicated code: no data-dependent loops (a probe chain past the
+//     first dset bucket -- rare at load <= 0.25 -- takes a wave-uniform slow path)
+//   * k_resolve pre-writes every result as NotMember and every err as 0 (coalesced), so this tier
+//     stores only IsMember bytes
+constexpr uint32_t S2_LONG = 2047;  // longest row a FIFO entry can hold (11-bit length)
+constexpr uint32_t S2_GEN = 0x1FF, S2_DMAX = 127;
+constexpr uint32_t S2_HIT = 1u << 30, S2_OVER = 1u << 31;
+
+template <int VLOG2, int QC>
+struct Stream2Lds {
+  unsigned long long vt[1 << VLOG2];  // direct-mapped visited cache (0 = empty)
+  uint32_t e_beg[QC], e_meta[QC];     // FIFO ring
+  uint32_t pref[65];                  // edge-owner marks (+1 dummy)
+  uint32_t s_state[32], s_qi[32], s_subj[32], s_sig[32], s_cnt[32], s_ins[32];
+};
+
+__device__ __forceinline__ uint32_t s2_meta(uint32_t len, uint32_t slot, uint32_t gen, uint32_t depth) {
+  return len | (slot << 11) | ((gen & S2_GEN) << 16) | (depth << 25);
+}
+
+// checkDirect probe, first bucket inline; a chain past a full first bucket (rare at load <= 0.25)
+// is walked by the lanes that need it under a wave-uniform branch.
+__device__ __forceinline__ bool dset_probe_fast(const DevSnap& s, bool want, uint32_t node, uint32_t subj) {
+  const uint64_t key = dset_key(node, subj);
+  uint64_t b = mix64(key) & s.dset_mask;
+  bool hit = false, more = false;
+  if (want) {
+    const ulonglong2 a = *reinterpret_cast<const ulonglong2*>(s.dset + b * DSET_BUCKET);
+    hit = a.x == key || a.y == key;
+    more = !hit && a.y != EMPTY64;
+  }
+  if (__ballot(more)) {
+    if (more) hit = dset_probe(s, node, subj);  // from the first bucket again: exact, rarely run
+  }
+  return hit;
+}
+
+template <int VLOG2, int QC, int CHUNK, int INS_CAP>
+__global__ __launch_bounds__(256) void k_stream2(DevSnap s, const RQuery* __restrict__ rq, WorkList wl, uint32_t* heads,
+                                                 uint8_t* __restrict__ out, uint32_t* next_list, uint32_t* next_count,
+                                                 Ctl* ctl) {
+  using Lds = Stream2Lds<VLOG2, QC>;
+  constexpr uint32_t VT = 1u << VLOG2;
+  static_assert(QC <= 256 && (QC & (QC - 1)) == 0, "FIFO ring of <= 256 entries (9-bit generations stay unique)");
+  static_assert(CHUNK <= 64, "one chunk entry per lane");
+  const uint64_t t_start = wall_clock64();
+  __shared__ Lds lds_all[4];
+  Lds& L = lds_all[threadIdx.x >> 6];
+  const int lane = lane_id();
+  const uint32_t head0 = blockIdx.x & 7;  // XCD label (speed only, never correctness)
+  uint32_t head_sel = head0;
+  for (uint32_t i = lane; i < VT; i += 64) L.vt[i] = 0ull;
+  if (lane < 32) {
+    L.s_state[lane] = 0;
+    L.s_cnt[lane] = 0;
+    L.s_ins[lane] = 0;
+  }
+  if (lane == 0) L.pref[64] = 0;
+  __builtin_amdgcn_wave_barrier();
+  uint32_t active = 0;   // wave-uniform: slots holding a query
+  bool drained = false;  // the work list is exhausted (the local chunk may still hold entries)
+  uint32_t c_left = 0, c_pos = 0;
+  uint32_t cq_qi = 0, cq_node = 0, cq_subj = 0, cq_beg = 0, cq_len = 0;
+  int32_t cq_depth = 0;
+  uint32_t head = 0, tail = 0, head_off = 0;
+  bool pend = false;
+  uint32_t pend_node = 0, pend_slot = 0, pend_gen = 0;
+  unsigned long long st_rows = 0, st_edges = 0, st_probes = 0, st_done = 0, st_steps = 0;
+  for (;;) {
+    // ---- refill free slots (their root entries need FIFO room)
+    const uint32_t freem = ~active;
+    const uint32_t want = __popc(freem);
+    if (want && !drained && (tail - head) + want <= QC) {
+      if (c_left == 0) {
+        uint32_t got = 0, first = 0;
+        if (lane == 0) first = dequeue_n(wl, heads, head_sel, head0, CHUNK, got);
+        first = __shfl(first, 0, 64);
+        c_left = __shfl(got, 0, 64);
+        c_pos = 0;
+        if (first == NONE) {
+          drained = true;
+        } else if ((uint32_t)lane < c_left) {
+          cq_qi = wl.list[first + lane];
+          const RQuery q = rq[cq_qi];
+          cq_node = q.node;
+          cq_subj = q.subj;
+          cq_depth = q.depth;
+          cq_beg = q.beg;
+          cq_len = q.len;
+        }
+      }
+      const uint32_t got = min(want, c_left);
+      if (got) {
+        const uint32_t r = __popc(freem & (lane < 32 ? (1u << lane) - 1u : 0xFFFFFFFFu));
+        const bool mine = lane < 32 && ((freem >> (lane & 31)) & 1u) && r < got;
+        const int src = mine ? (int)(c_pos + r) : lane;
+        const uint32_t qi = __shfl(cq_qi, src, 64), qnode = __shfl(cq_node, src, 64), qsubj = __shfl(cq_subj, src, 64),
+                       qbeg = __shfl(cq_beg, src, 64), qlen = __shfl(cq_len, src, 64);
+        const int32_t qdepth = __shfl(cq_depth, src, 64);
+        c_pos += got;
+        c_left -= got;
+        if (mine) {
+          const uint32_t slot = lane, gen = L.s_state[slot] & S2_GEN;  // freed slots hold a fresh generation
+          const bool over = qdepth > (int32_t)S2_DMAX || qlen > S2_LONG;
+          L.s_qi[slot] = qi;
+          L.s_subj[slot] = qsubj;
+          L.s_sig[slot] = subj_sig(qsubj);
+          L.s_cnt[slot] = 1;
+          L.s_ins[slot] = 0;
+          L.s_state[slot] = over ? (gen | S2_OVER) : gen;
+          // the root counts as visited (a cycle back to it is not expanded again)
+          const unsigned long long key =
+              (1ull << 63) | ((unsigned long long)gen << 37) | ((unsigned long long)slot << 32) | qnode;
+          L.vt[((qnode * 0x9E3779B1u) ^ (slot * 0x85EBCA77u) ^ (gen * 0xC2B2AE3Du)) >> (32 - VLOG2)] = key;
+          const uint32_t at = (tail + r) & (QC - 1);
+          L.e_beg[at] = qbeg;
+          L.e_meta[at] = s2_meta(over ? 0u : qlen, slot, gen, over ? 2u : (uint32_t)qdepth);
+        }
+        active |= (uint32_t)__ballot(mine);
+        tail += got;
+      }
+    }
+    if (active == 0 && ((drained && c_left == 0) || tail == head)) {
+      if (drained && c_left == 0) break;
+      continue;
+    }
+    __builtin_amdgcn_wave_barrier();
+    // ---- window: up to 64 FIFO entries from the head
+    const uint32_t avail = tail - head;
+    uint32_t ebeg = 0, elen = 0, emeta = 0;
+    bool live = false;
+    if ((uint32_t)lane < avail) {
+      const uint32_t at = (head + lane) & (QC - 1);
+      emeta = L.e_meta[at];
+      ebeg = L.e_beg[at];
+      const uint32_t sl = (emeta >> 11) & 31u;
+      const uint32_t st = L.s_state[sl];
+      live = ((active >> sl) & 1u) && (st == ((emeta >> 16) & S2_GEN));  // current generation, no HIT/OVER
+      elen = live ? (emeta & 0x7FFu) : 0u;
+      if (lane == 0) {
+        ebeg += head_off;
+        elen = live ? elen - head_off : 0u;
+      }
+    }
+    uint32_t total;
+    const uint32_t excl = wave_excl_scan(elen, &total);
+    L.pref[lane] = 0;
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t taken = min(total, 64u);
+    L.pref[(elen > 0 && excl < taken) ? excl : 64u] = (uint32_t)lane + 1;
+    const bool consumed = (uint32_t)lane < avail && excl + elen <= taken;
+    const uint32_t ncons = __popcll(__ballot(consumed));  // a prefix of the window
+    if (consumed && live) atomicSub(&L.s_cnt[(emeta >> 11) & 31u], 1u);
+    st_rows += (consumed && live) ? 1u : 0u;
+    {
+      const uint32_t ex_n = (uint32_t)__builtin_amdgcn_readlane((int)excl, ncons & 63);
+      if (ncons < avail && ncons < 64 && ex_n < taken) head_off = (ncons == 0 ? head_off : 0u) + (taken - ex_n);
+      else if (ncons > 0) head_off = 0;
+    }
+    __builtin_amdgcn_wave_barrier();
+    // ---- this step's edge gathers and the previous step's probes, in flight together
+    const bool act = (uint32_t)lane < taken;
+    const int own = ((int)wave_incl_scan<DppMax>(L.pref[lane]) - 1) & 63;
+    const uint32_t ob = __shfl(ebeg, own, 64);
+    const uint32_t om = __shfl(emeta, own, 64);
+    const uint32_t ox = __shfl(excl, own, 64);
+    AdjX x{NONE, 0, 0, 0};
+    if (act) x = s.adjx[ob + ((uint32_t)lane - ox)];
+    const bool pvalid = pend && L.s_state[pend_slot] == pend_gen;
+    const bool h = dset_probe_fast(s, pvalid, pend_node, L.s_subj[pend_slot]);
+    st_probes += pvalid ? 1u : 0u;
+    head += ncons;
+    st_edges += (lane == 0) ? taken : 0u;
+    st_steps += (lane == 0) ? 1u : 0u;
+    // ---- children: kept ones (rest >= 2 after the hop, non-empty set row) are marked + appended;
+    // every child new to the query is probed next step
+    const uint32_t slot = (om >> 11) & 31u, d = om >> 25, g = (om >> 16) & S2_GEN;
+    const bool keepc = act && d >= 3 && x.len > 0;
+    const bool longrow = keepc && x.len > S2_LONG;
+    const unsigned long long key =
+        (1ull << 63) | ((unsigned long long)g << 37) | ((unsigned long long)slot << 32) | x.node;
+    const uint32_t hv = ((x.node * 0x9E3779B1u) ^ (slot * 0x85EBCA77u) ^ (g * 0xC2B2AE3Du)) >> (32 - VLOG2);
+    const unsigned long long old = keepc ? L.vt[hv] : 0ull;
+    const bool fresh = keepc && !longrow && old != key;
+    if (fresh) L.vt[hv] = key;
+    const uint32_t k = fresh ? atomicAdd(&L.s_ins[slot], 1u) : 0u;
+    const bool ok = fresh && k < (uint32_t)INS_CAP;
+    const uint64_t am = __ballot(ok);
+    const uint32_t room = QC - (tail - head);
+    const uint32_t pos = __popcll(am & ((1ull << lane) - 1));
+    const bool appended = ok && pos < room;
+    if (appended) {
+      const uint32_t at = (tail + pos) & (QC - 1);
+      L.e_beg[at] = x.begin;
+      L.e_meta[at] = x.len | (om & 0x01FFF800u) | ((d - 1) << 25);
+      atomicAdd(&L.s_cnt[slot], 1u);
+    }
+    if (longrow || (fresh && !appended)) atomicOr(&L.s_state[slot], S2_OVER);  // visited cap or FIFO full
+    tail += min((uint32_t)__popcll(am), room);
+    if (h) atomicOr(&L.s_state[pend_slot], S2_HIT);
+    pend = act && (keepc ? appended : true) && sig_maybe(x.sig, L.s_sig[slot]);
+    pend_node = x.node;
+    pend_slot = slot;
+    pend_gen = g;
+    // ---- finished queries
+    const uint32_t pslots = wave_or(pend ? 1u << slot : 0u);
+    __builtin_amdgcn_wave_barrier();
+    bool done = false;
+    if (lane < 32 && ((active >> lane) & 1u)) {
+      const uint32_t st = L.s_state[lane];
+      if (st & S2_HIT) {
+        done = true;
+        out[L.s_qi[lane]] = KG_IS_MEMBER;  // NotMember was pre-written by k_resolve
+        st_done++;
+      } else if (st & S2_OVER) {
+        done = true;
+        next_list[atomicAdd(next_count, 1u)] = L.s_qi[lane];
+      } else if (L.s_cnt[lane] == 0 && !((pslots >> lane) & 1u)) {
+        done = true;
+        st_done++;
+      }
+      if (done) L.s_state[lane] = ((st & S2_GEN) + 1u) & S2_GEN;  // stale: its FIFO entries and probes
+    }
+    const uint32_t freed = (uint32_t)__ballot(done);
+    active &= ~freed;
+    if (pend && ((freed >> pend_slot) & 1u)) pend = false;
+    __builtin_amdgcn_wave_barrier();
+  }
+  const unsigned long long life = lane == 0 ? wall_clock64() - t_start : 0ull;
+  const int idx[7] = {ST_LROWS, ST_LEDGES, ST_LPROBES, ST_LIGHT, ST_LSTEPS, ST_LWAVES, ST_LTICKS};
+  const unsigned long long v[7] = {st_rows, st_edges, st_probes, st_done, st_steps, lane == 0 ? 1ull : 0ull, life};
+  block_stats<7>(ctl, idx, v);
+}
+
 // ------------------------------------------------------------------ workgroup tiers
 // Queries whose visited set outgrew one wave's LDS: one 256-lane workgroup per query, same BFS.
 //   k_wg<WgLds>  visited hash (8192 slots) + BFS list (4096) in LDS          ("medium")
@@ -1174,19 +1423,28 @@ int check_batch_begin(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n, 
   hipStream_t stream = w->stream;
   // scratch: rq[n] | light[8n] (8 shards) | light2[n] | gen[n] | medium[n] | heavy[n] | giant[n] | p2[n] |
   //          back2[n] | Ctl
-  size_t off_rq = 0, off_light = align_up(off_rq + n * sizeof(RQuery)), off_light2 = align_up(off_light + 8 * n * 4),
-         off_gen = align_up(off_light2 + n * 4),
-         off_med = align_up(off_gen + n * 4), off_heavy = align_up(off_med + n * 4),
-         off_giant = align_up(off_heavy + n * 4), off_p2 = align_up(off_giant + n * 4),
-         off_back2 = align_up(off_p2 + n * 4), off_ctl = align_up(off_back2 + n * 4),
-         total = align_up(off_ctl + sizeof(Ctl));
-  if (total > w->scratch_bytes) {
+  auto layout = [](size_t m, size_t* off) {  // rq | light[8m] | light2 | gen | medium | heavy | giant | p2 | back2 | Ctl
+    off[0] = 0;
+    off[1] = align_up(off[0] + m * sizeof(RQuery));
+    off[2] = align_up(off[1] + 8 * m * 4);
+    for (int k = 3; k <= 9; k++) off[k] = align_up(off[k - 1] + m * 4);
+    return align_up(off[9] + sizeof(Ctl));
+  };
+  size_t off[10];
+  const size_t total = layout(n, off);
+  if (total > w->scratch_bytes) {  // sized for >= 64 Ki queries, grown geometrically (hipFree stalls the device)
+    const size_t m = std::max<size_t>(65536, std::max<size_t>(2 * w->scratch_n, n));
+    size_t tmp[10];
+    const size_t want = layout(m, tmp);
     if (w->scratch) hipFree(w->scratch);
     w->scratch = nullptr;
     w->scratch_bytes = 0;
-    HIPC(hipMalloc(&w->scratch, total));
-    w->scratch_bytes = total;
+    HIPC(hipMalloc(&w->scratch, want));
+    w->scratch_bytes = want;
+    w->scratch_n = m;
   }
+  const size_t off_rq = off[0], off_light = off[1], off_light2 = off[2], off_gen = off[3], off_med = off[4],
+               off_heavy = off[5], off_giant = off[6], off_p2 = off[7], off_back2 = off[8], off_ctl = off[9];
   char* base = (char*)w->scratch;
   RQuery* rq = (RQuery*)(base + off_rq);
   uint32_t* light = (uint32_t*)(base + off_light);
@@ -1259,7 +1517,8 @@ int check_batch_begin(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n, 
       //   6: the same with <= 256 per query and a 320-entry FIFO (~53 KiB, 3/CU)
       //   7: as 5 with <= 64 per query   8: as 7 with a 512-key table (~45 KiB)
       const int sv = s->stream_variant;
-      const uint32_t per_cu = s->stream_wgs ? (uint32_t)s->stream_wgs : ((sv == 0 || sv == 1 || sv == 3) ? 5u : 3u);
+      const uint32_t per_cu =
+          s->stream_wgs ? (uint32_t)s->stream_wgs : ((sv == 0 || sv == 1 || sv == 3 || sv == 9) ? 5u : 3u);
       const uint32_t ecap = s->stream_ecap ? s->stream_ecap : 0xFFFFFFFFu;
       const uint32_t grid = (uint32_t)std::min<uint64_t>((uint64_t)s->n_cu * per_cu, (n + 31) / 32 + 8);
       using V0 = SlotVis<8, 7>;
@@ -1282,6 +1541,9 @@ int check_batch_begin(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n, 
       else if (sv == 6) KG_STREAM(32, V6, 320, 64);
       else if (sv == 7) KG_STREAM(32, V7, 256, 64);
       else if (sv == 8) KG_STREAM(32, V8, 256, 64);
+      else if (sv == 9)
+        hipLaunchKernelGGL((k_stream2<9, 256, 64, 64>), dim3(grid), dim3(256), 0, stream, s->ds, rq, wl, ctl->heads,
+                           d_out, ovf_list, ovf_count, ctl);
       else KG_STREAM(8, V0, 256, 16);
 #undef KG_STREAM
     }

@@ -31,7 +31,10 @@ namespace kg {
 constexpr uint32_t SET_BIT = 0x80000000u;
 constexpr uint32_t NONE = 0xFFFFFFFFu;
 constexpr uint64_t EMPTY64 = ~0ull;
-constexpr int DSET_BUCKET = 8;  // u64 keys per bucket = one 64-B sector
+// u64 keys per dset bucket: 2 = one 16-B load per probe.  The unit of cost of these kernels is the
+// random lane-request (tools/randprobe: ~41 G/s from HBM-sized tables, whatever their width up to
+// 16 B), so a probe is one request at load <= 0.25 rather than four 16-B loads of a 64-B bucket.
+constexpr int DSET_BUCKET = 2;
 
 enum : uint8_t { NF_IMPURE = 1, NF_REWRITE = 2, NF_ERR = 4 };
 

@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <list>
 #include <mutex>
 #include <thread>
@@ -37,6 +38,7 @@ struct Workspace {
   std::mutex mu;
   void* scratch = nullptr;
   size_t scratch_bytes = 0;
+  size_t scratch_n = 0;  // queries the scratch was last sized for
   void* heavy_pool = nullptr;
   size_t heavy_pool_bytes = 0;
   void* grid_pool = nullptr;  // grid tier: visited hash | log | slots | ctl | scan sums
@@ -118,7 +120,7 @@ struct Snapshot {
   void* shard_vis = nullptr;             // kg_shard.hip: per-batch visited table of (query, node)
   uint64_t shard_vis_slots = 0;
   int shard_vis_log2 = 25;
-  int stream_variant = 7;  // kg_snapshot_tune("stream"): k_stream slots/LDS variant (0..8)
+  int stream_variant = 9;  // kg_snapshot_tune("stream"): k_stream variant (0..8) or 9 = k_stream2
   int back_tier = 2;  // kg_snapshot_tune("back"): backward tier (1: wave + workgroup widths, 2: wave only) + no-holder filter
   uint32_t stream_ecap = 0;  // kg_snapshot_tune("stream_ecap"): k_stream edge budget per query (0 = none)
   int grid_wgs = 16;         // kg_snapshot_tune("grid_wgs"): k_grid_level workgroups per CU
@@ -134,6 +136,7 @@ struct Snapshot {
   std::mutex lane_mu;
   std::list<std::pair<std::thread::id, std::vector<Lane*>>> lanes;  // list: stable addresses
   std::vector<Lane*>* thread_lanes();  // this thread's lanes (one per replica), created on first use
+  std::atomic<uint64_t> rr_next{0};      // replica rotation of batches smaller than one chunk per replica
 
   ~Snapshot();
   int init_device(int dev);

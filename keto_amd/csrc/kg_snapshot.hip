@@ -262,8 +262,10 @@ Lane::~Lane() {
 int Lane::reserve(size_t n) {
   if (n <= cap) return 0;
   HIPC(hipSetDevice(device));
-  size_t c = std::max<size_t>(n, 4096);
-  c = std::max(c, cap + cap / 2);
+  // >= 64 Ki queries (2.3 MB of pinned staging): a request batcher's batches never reallocate
+  // (pinned allocation and hipFree both stall), larger host batches grow it geometrically
+  size_t c = std::max<size_t>(n, 65536);
+  c = std::max(c, 2 * cap);
   HIPC(hipStreamSynchronize(stream));
   for (void* p : {(void*)h_q, (void*)h_out, (void*)h_err})
     if (p) hipHostFree(p);
@@ -338,7 +340,7 @@ int Snapshot::init_device(int dev) {
   return 0;
 }
 
-// Hash tables: dset sized for load <= 0.5 over 8-key buckets; nmap for load <= 0.5.
+// Hash tables: dset sized for load <= 0.25 over 2-key (16-B) buckets; nmap for load <= 0.5.
 int Snapshot::build_hash_tables() {
   // inlined child rows for the BFS (indices are u32: up to 2^32-1 set edges per snapshot)
   if (n_set_edges >= 0xFFFFFFFFull) return set_error(KG_ERR_RESOURCE_CODE, "more than 2^32-1 subject-set edges");
@@ -359,7 +361,8 @@ int Snapshot::build_hash_tables() {
   }
   ds.adjx = adjx;
   uint64_t n_rows = h_row_off_last;
-  uint64_t buckets = pow2_at_least(std::max<uint64_t>(1, (n_rows * 2 + DSET_BUCKET - 1) / DSET_BUCKET));
+  // load <= 0.25 keys per slot: a miss (the common probe) reads one bucket with probability ~0.9
+  uint64_t buckets = pow2_at_least(std::max<uint64_t>(1, (n_rows * 4 + DSET_BUCKET - 1) / DSET_BUCKET));
   uint64_t* dset = nullptr;
   if (alloc((void**)&dset, buckets * DSET_BUCKET * 8)) return -1;
   HIPC(hipMemsetAsync(dset, 0xFF, buckets * DSET_BUCKET * 8, stream));

@@ -24,6 +24,60 @@ NAMESPACES = ["doc", "group", "user", "folder"]
 RELATIONS = ["viewer", "member", "editor", "owner", "parents", "blocked", "view", "edit", "share"]  # after "..."
 
 
+# Config C3's namespaces in OPL (keto_amd.opl parses this into exactly c3_namespaces(); the tests
+# check that both compile to the same rewrite program).
+C3_OPL = """
+class user implements Namespace {}
+
+class doc implements Namespace {
+  related: {
+    viewer: (user | SubjectSet<group, "member">)[]
+    editor: (user | SubjectSet<group, "member">)[]
+    owner: user[]
+    parents: folder[]
+    blocked: user[]
+  }
+  permits = {
+    view: (ctx: Context): boolean =>
+      this.related.viewer.includes(ctx.subject) ||
+      this.related.edit.includes(ctx.subject) ||
+      this.related.parents.traverse(p => p.permits.view(ctx)),
+    edit: (ctx: Context): boolean =>
+      this.related.editor.includes(ctx.subject) ||
+      this.related.owner.includes(ctx.subject) ||
+      this.related.parents.traverse(p => p.permits.edit(ctx)),
+    share: (ctx: Context): boolean =>
+      this.related.view.includes(ctx.subject) && !this.related.blocked.includes(ctx.subject),
+  }
+}
+
+class group implements Namespace {
+  related: {
+    member: (user | SubjectSet<group, "member">)[]
+  }
+}
+
+class folder implements Namespace {
+  related: {
+    viewer: (user | SubjectSet<group, "member">)[]
+    editor: (user | SubjectSet<group, "member">)[]
+    owner: user[]
+    parents: folder[]
+  }
+  permits = {
+    view: (ctx: Context): boolean =>
+      this.related.viewer.includes(ctx.subject) ||
+      this.related.edit.includes(ctx.subject) ||
+      this.related.parents.traverse(p => p.permits.view(ctx)),
+    edit: (ctx: Context): boolean =>
+      this.related.editor.includes(ctx.subject) ||
+      this.related.owner.includes(ctx.subject) ||
+      this.related.parents.traverse(p => p.permits.edit(ctx)),
+  }
+}
+"""
+
+
 def interner() -> Interner:
     it = Interner()  # rel 0 = "..."
     for n in NAMESPACES:
@@ -55,8 +109,10 @@ def c3_namespaces() -> List[Namespace]:
 
 
 def program(preset: int, it: Interner):
+    """The namespace program of a preset: C3's comes from its OPL text (keto_amd.opl)."""
     if preset == PRESET_C3:
-        return compile_program(c3_namespaces(), it)
+        from .opl import parse_strict
+        return compile_program(parse_strict(C3_OPL), it)
     return None
 
 

@@ -52,15 +52,16 @@ def random_queries(rng, nss, rels, n, n_obj=60, n_users=40, p_setq=0.15):
     return qs
 
 
-@pytest.mark.parametrize("seed", range(10))
+@pytest.mark.parametrize("seed", range(13))
 def test_random_graphs_vs_oracle(seed):
     rng = np.random.default_rng(seed)
     it, tuples, nss, rels = random_graph(rng, n_obj=40 + 20 * (seed % 6), n_rows=200 + 150 * (seed % 6))
     reg = Registry(tuples, [], interner=it)
     # first wave tier: k_stream variants 0..8 (seeds 0-6 and 8-9 -> variants 0-6, 7, 8; seed 2 with a
-    # tiny per-query edge budget, so queries overflow into the next tiers mid-search) and k_light<16> (seed 7)
+    # tiny per-query edge budget, so queries overflow into the next tiers mid-search), k_light<16>
+    # (seed 7) and k_stream2 (seeds 10-12, the default; seed 12 on a graph of long rows and cycles)
     reg.snapshot.tune("light", 1 if seed == 7 else 0)
-    reg.snapshot.tune("stream", seed % 7 if seed < 7 else seed - 1)
+    reg.snapshot.tune("stream", seed % 7 if seed < 7 else (seed - 1 if seed < 10 else 9))
     reg.snapshot.tune("stream_ecap", 6 if seed == 2 else 0)
     qs = random_queries(rng, nss, rels, 3000, n_obj=40 + 20 * (seed % 6))
     depths = rng.integers(-1, 9, len(qs))
@@ -77,6 +78,32 @@ def test_random_graphs_vs_oracle(seed):
         dfs, _, _ = oracle.check_batch(q6, depths, gmax, POLICY_DFS)
         inv = dfs == exp
         assert (out[inv] == dfs[inv]).all()
+
+
+@pytest.mark.parametrize("variant", [8, 9])
+def test_stream_tier_long_rows_and_dense_cycles(variant):
+    """Rows longer than a FIFO entry holds (k_stream2: 2047 edges), dense cycles (the direct-mapped
+    visited cache evicts and re-expands), many queries per wave on one hub: exact vs the oracle."""
+    rng = np.random.default_rng(77)
+    tuples = [RelationTuple.from_string(f"g:hub#m@(g:c{i}#m)") for i in range(2500)]  # > 2047-edge row
+    tuples += [RelationTuple.from_string(f"g:c{i}#m@(g:c{(i * 7 + 3) % 2500}#m)") for i in range(2500)]
+    tuples += [RelationTuple.from_string(f"g:c{i}#m@(g:k{i % 40}#m)") for i in range(0, 2500, 3)]
+    tuples += [RelationTuple.from_string(f"g:k{i}#m@(g:k{(i + 1) % 40}#m)") for i in range(40)]  # a 40-cycle
+    tuples += [RelationTuple.from_string(f"g:k{i}#m@u{i}") for i in range(0, 40, 5)]
+    tuples += [RelationTuple.from_string(f"g:c{i}#m@v{i % 97}") for i in range(0, 2500, 11)]
+    reg = Registry(tuples, [])
+    reg.snapshot.tune("stream", variant)
+    it = reg.interner
+    qs = [RelationTuple.from_string(f"g:{r}#m@{u}") for r in ["hub", "k0", "k3", "c5", "c17", "c999"]
+          for u in ["u0", "u35", "v3", "v96", "nobody"]]
+    q6 = np.asarray([it.tuple_ids(t) for t in qs] * 40, np.uint32)
+    depths = rng.integers(0, 12, len(q6))
+    oracle = Oracle(it.tuples_array(tuples), it.wildcard_rel)
+    for gmax in (3, 6, 12):
+        e = Engine(reg.snapshot, Config(gmax))
+        out, err = e.batch_check_ids(queries_array(q6, depths), with_stats=True)
+        exp, _, _ = oracle.check_batch(q6, depths, gmax, POLICY_CANONICAL)
+        assert (out == exp).all() and (err == 0).all(), (gmax, np.nonzero(out != exp)[0][:10])
 
 
 def test_heavy_path_overflow_star():
@@ -359,3 +386,64 @@ def test_rewrite_bfs_beyond_lds(cap2):
             out, err = e.batch_check_ids(queries_array(q6, 0), with_stats=True)
             exp, oerr, _ = oracle.check_batch(q6, np.zeros(len(qs), np.int32), gmax, POLICY_CANONICAL)
             assert list(out) == list(exp) and list(err) == list(oerr), (gmax, rep, out, exp)
+
+
+def test_opl_full_example_rewrites_vs_oracle():
+    """The reference parser's golden AST (internal/schema/.snapshots/TestParser-suite=snapshots-
+    full_example.json, a tests/golden fixture) loaded through namespace_from_json, compiled, and
+    evaluated by the GPU interpreter on a random graph over its namespaces: bit-exact with the
+    oracle, error codes included (the "not" permission and nested and/or/traverse)."""
+    import json
+    import os
+    from keto_amd.namespace import compile_program, namespace_from_json
+    golden = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden",
+                                         "opl_full_example.json")))
+    namespaces = [namespace_from_json({"name": n, "relations": rels}) for n, rels in sorted(golden.items())]
+    it = Interner()
+    prog = compile_program(namespaces, it)
+    rng = np.random.default_rng(2024)
+    files, folders, groups, users = [f"f{i}" for i in range(60)], [f"d{i}" for i in range(20)], \
+        [f"g{i}" for i in range(15)], [f"u{i}" for i in range(30)]
+    tuples = []
+    for _ in range(700):
+        k = rng.integers(9)
+        f = rng.choice(files)
+        if k == 0:
+            tuples.append(f"File:{f}#parents@(File:{rng.choice(files)}#...)")
+        elif k == 1:
+            tuples.append(f"File:{f}#parents@(Folder:{rng.choice(folders)}#...)")
+        elif k == 2:
+            tuples.append(f"File:{f}#viewers@{rng.choice(users)}")
+        elif k == 3:
+            tuples.append(f"File:{f}#viewers@(Group:{rng.choice(groups)}#members)")
+        elif k == 4:
+            tuples.append(f"File:{f}#owners@{rng.choice(users)}")
+        elif k == 5:
+            tuples.append(f"File:{f}#siblings@(File:{rng.choice(files)}#...)")
+        elif k == 6:
+            tuples.append(f"Folder:{rng.choice(folders)}#viewers@(Group:{rng.choice(groups)}#members)")
+        elif k == 7:
+            tuples.append(f"Group:{rng.choice(groups)}#members@{rng.choice(users)}")
+        else:
+            tuples.append(f"Group:{rng.choice(groups)}#members@(Group:{rng.choice(groups)}#members)")
+    tuples = [RelationTuple.from_string(t) for t in tuples]
+    reg = Registry(tuples, namespaces, interner=it)
+    assert reg.snapshot.program is not None
+    qs = []
+    for _ in range(3000):
+        rel = rng.choice(["view", "edit", "not", "rename", "viewers", "owners", "parents"])
+        ns, obj = ("Folder", rng.choice(folders)) if rng.random() < 0.2 else ("File", rng.choice(files))
+        subj = rng.choice(users + ["nobody"]) if rng.random() < 0.9 else f"(Group:{rng.choice(groups)}#members)"
+        qs.append(RelationTuple.from_string(f"{ns}:{obj}#{rel}@{subj}"))
+    q6 = np.asarray([it.tuple_ids(t) for t in qs], np.uint32)
+    depths = rng.integers(-1, 8, len(qs))
+    oracle = Oracle(it.tuples_array(tuples), it.wildcard_rel, prog)
+    for gmax in (2, 5, 8):
+        e = Engine(reg.snapshot, Config(gmax))
+        out, err = e.batch_check_ids(queries_array(q6, depths), with_stats=True)
+        exp, oerr, _ = oracle.check_batch(q6, depths, gmax, POLICY_CANONICAL)
+        bad = np.nonzero((out != exp) | (err.astype(np.int64) != oerr))[0]
+        assert bad.size == 0, [(str(qs[i]), int(depths[i]), int(out[i]), int(exp[i]), int(err[i]), int(oerr[i]))
+                               for i in bad[:8]]
+        assert e.last_stats["n_general"] > 0
+        assert 0 < (exp == 1).sum() and (exp == 0).sum() > 0
