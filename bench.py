@@ -43,7 +43,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--tuples", type=float, default=1e9, help="synthetic graph size (tuples)")
+    ap.add_argument("--tuples", type=float, default=None, help="synthetic graph size (tuples; default 1e9, 1e7 with --heavy-tail)")
+    ap.add_argument("--heavy-tail", action="store_true",
+                    help="out-degree law P(k) ~ k^-1.5 (Pareto tail index 0.5 for docs and groups, SURVEY.md 8d) "
+                         "instead of the default 1.3 / 1.1; ~40x the rows per node")
     ap.add_argument("--batch", type=int, default=1_000_000, help="checks per step per GPU")
     ap.add_argument("--global-depth", type=int, default=10)
     ap.add_argument("--seed", type=int, default=20250131)
@@ -52,8 +55,9 @@ def parse():
     ap.add_argument("--stream", type=int, default=9, help="kg_snapshot_tune stream (k_stream variant 0..8, 9 = k_stream2)")
     ap.add_argument("--stream-ecap", type=int, default=0, help="kg_snapshot_tune stream_ecap (edges per query, 0 = none)")
     ap.add_argument("--grid-wgs", type=int, default=4, help="kg_snapshot_tune grid_wgs (k_grid_level WGs per CU)")
-    ap.add_argument("--stream-wgs", type=int, default=0,
-                    help="kg_snapshot_tune stream_wgs (k_stream WGs per CU, 0 = by variant: 5 for k_stream2's ~29 KiB WGs)")
+    ap.add_argument("--stream-wgs", type=int, default=3,
+                    help="kg_snapshot_tune stream_wgs (k_stream WGs per CU, 0 = by variant: 5 for k_stream2's ~29 KiB "
+                         "WGs; 3 leaves LDS to the other batches in flight, best at --inflight 4: profiles/r2j_sweep.jsonl)")
     ap.add_argument("--back", type=int, default=2, help="kg_snapshot_tune back (1 backward tier wave+WG widths, 2 wave width only, 0 off)")
     ap.add_argument("--back-wgs", type=int, default=1,
                     help="kg_snapshot_tune back_wgs (k_back WGs per CU; 1 leaves LDS to the other in-flight batches)")
@@ -61,7 +65,8 @@ def parse():
     ap.add_argument("--inflight", type=int, default=4,
                     help="batches in flight per GPU: one HIP stream (own workspace) and one host thread each")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline time budget (0 = skip)")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU-baseline threads (0 = os.cpu_count(), also timed at the affinity count, 16 and 1)")
     ap.add_argument("--preset", type=int, default=0,
                     help="0 = C2/C4 rewrite-free (headline); 1 = C3 (OPL view/edit/share via the rewrite interpreter)")
     ap.add_argument("--mode", choices=["check", "expand", "sharded", "host"], default="check",
@@ -326,6 +331,8 @@ def aggregate(dist, elapsed: float, edges: float, device=None):
 
 def main():
     a = parse()
+    if a.tuples is None:
+        a.tuples = 1e7 if a.heavy_tail else 1e9
     if a.mode == "expand":
         return bench_expand(a)
     if a.mode == "sharded":
@@ -348,7 +355,9 @@ def main():
     L = _lib.load()
 
     t_build = time.time()
-    snap = Snapshot.synthetic(int(a.tuples), seed=a.seed, device=local, preset=a.preset)
+    alpha = 0.5 if a.heavy_tail else 0.0
+    snap = Snapshot.synthetic(int(a.tuples), seed=a.seed, device=local, preset=a.preset, doc_alpha=alpha,
+                              group_alpha=alpha)
     snap.tune("tiers", a.tiers)
     snap.tune("wide", a.wide)
     snap.tune("back", a.back)
@@ -365,26 +374,31 @@ def main():
     B = a.batch
     P = max(1, a.inflight)
     dev = f"cuda:{local}"
-    # P batches in flight: batch p lives on stream p with its own query / result buffers (distinct
-    # synthetic batches), and one host thread drives each stream (ctypes releases the GIL)
+    # P batches in flight: P host threads, each driving its own HIP stream (own workspace) with its
+    # own result buffers (ctypes releases the GIL).  Every step checks a DISTINCT synthetic batch
+    # (warm-up and timed steps alike), so no batch re-touches rows and probe lines a previous step
+    # already pulled into L2 / the Infinity Cache.
     streams = [torch.cuda.current_stream(local)] + [torch.cuda.Stream(local) for _ in range(P - 1)]
-    dqs, douts, derrs = [], [], []
-    for p in range(P):
-        q = torch.empty((B, 7), dtype=torch.int32, device=dev)
-        _lib.check(L.kg_synth_queries(snap.handle, 1000 + rank + 7919 * p, B, q.data_ptr()), "kg_synth_queries")
-        dqs.append(q)
-        douts.append(torch.empty(B, dtype=torch.uint8, device=dev))
-        derrs.append(torch.empty(B, dtype=torch.int32, device=dev))
-    dq = dqs[0]
+    warm = max(a.warmup, P)  # every stream's workspace is allocated before the timed region
+    n_batches = warm + a.steps
+    dq_all = torch.empty((n_batches, B, 7), dtype=torch.int32, device=dev)
+    for k in range(n_batches):
+        _lib.check(L.kg_synth_queries(snap.handle, 1000 + rank + 7919 * k, B, dq_all[k].data_ptr()),
+                   "kg_synth_queries")
+    douts = [torch.empty(B, dtype=torch.uint8, device=dev) for _ in range(P)]
+    derrs = [torch.empty(B, dtype=torch.int32, device=dev) for _ in range(P)]
+    dq = dq_all[warm]
+    timed_out = torch.empty((a.steps, B), dtype=torch.uint8, device=dev)
 
-    def step(p, st=None):
-        rc = L.kg_check_batch_device(snap.handle, dqs[p].data_ptr(), B, a.global_depth, douts[p].data_ptr(),
+    def step(p, k, st=None):
+        o = timed_out[k - warm] if k >= warm else douts[p]  # every timed batch keeps its own results
+        rc = L.kg_check_batch_device(snap.handle, dq_all[k].data_ptr(), B, a.global_depth, o.data_ptr(),
                                      derrs[p].data_ptr(), C.byref(st) if st is not None else None,
                                      C.c_void_p(streams[p].cuda_stream))
         _lib.check(rc, "kg_check_batch_device")
 
-    def run_steps(K, stats=None, lat=None):
-        """Starts P host threads that run K steps round-robin over the P streams once `go` is set."""
+    def run_steps(k0, K, stats=None, lat=None):
+        """Starts P host threads that run steps k0 .. k0+K-1 round-robin over the P streams once `go` is set."""
         go = threading.Event()
         errors = []
 
@@ -393,7 +407,7 @@ def main():
                 go.wait()
                 for k in range(p, K, P):
                     s0 = time.perf_counter()
-                    step(p, stats[k] if stats is not None else None)  # stats => waits for its batch
+                    step(p, k0 + k, stats[k] if stats is not None else None)  # stats => waits for its batch
                     if lat is not None:
                         lat[k] = time.perf_counter() - s0
                 streams[p].synchronize()
@@ -411,8 +425,7 @@ def main():
         if errors:
             raise errors[0]
 
-    warm = max(a.warmup, P)  # every stream's workspace is allocated before the timed region
-    go, th, errs = run_steps(warm)
+    go, th, errs = run_steps(0, warm)
     go.set()
     finish(th, errs)
     torch.cuda.synchronize()
@@ -421,7 +434,7 @@ def main():
     torch.cuda.synchronize()
     stats = [_lib.kg_stats() for _ in range(a.steps)]
     lat = [0.0] * a.steps
-    go, th, errs = run_steps(a.steps, stats, lat)
+    go, th, errs = run_steps(warm, a.steps, stats, lat)
     t0 = time.perf_counter()
     go.set()
     finish(th, errs)
@@ -430,7 +443,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    res = torch.cat(douts).cpu().numpy()
+    res = timed_out.cpu().numpy()
     errs = torch.cat(derrs).cpu().numpy()
     assert (errs == 0).all() and (res <= 1).all(), "unexpected errors in the synthetic batch"
     elapsed, edges = aggregate(dist, elapsed, float(sum(s.edges_read for s in stats)), f"cuda:{local}")
@@ -521,8 +534,13 @@ def cpu_baseline(snap, dq, a) -> dict:
     p = lambda x: x.ctypes.data_as(C.c_void_p)
     _lib.check(L.kg_snapshot_export_csr(snap.handle, p(row_off), p(row_subj), p(nd[0]), p(nd[1]), p(nd[2])),
                "kg_snapshot_export_csr")
-    threads = max(1, min(a.cpu_threads, os.cpu_count() or 1))
-    o = Oracle.from_csr(0, nd[0], nd[1], nd[2], row_off, row_subj, nthreads=threads)
+    ncpu = os.cpu_count() or 1
+    try:
+        n_aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n_aff = ncpu
+    threads = a.cpu_threads if a.cpu_threads > 0 else ncpu
+    o = Oracle.from_csr(0, nd[0], nd[1], nd[2], row_off, row_subj, nthreads=min(threads, 64))
     del row_subj
     q = dq.cpu().numpy().view(np.uint32)
     node = q[:, 1].copy()  # synthetic docs: node id == object id
@@ -536,7 +554,12 @@ def cpu_baseline(snap, dq, a) -> dict:
         return time.perf_counter() - t
 
     res = {}
-    for th, budget in ((threads, a.cpu_seconds), (1, a.cpu_seconds / 3)):
+    # T = nproc, the threads this process may run on, 16 and 1 -- each on its own budget
+    plan = [(threads, a.cpu_seconds)]
+    for th in (n_aff, 16, 1):
+        if th not in [p[0] for p in plan]:
+            plan.append((th, a.cpu_seconds / 3))
+    for th, budget in plan:
         n, passes = 256, 1
         t = run(n, th)
         while t < budget / 4 and n < len(node):  # grow the sample of distinct checks first
@@ -550,7 +573,8 @@ def cpu_baseline(snap, dq, a) -> dict:
     return {"value": v, "unit": "checks/s", "cores": threads, "kind": "port",
             "sample": f"{passes} pass(es) over the first {n} checks of the rank-0 batch on the same graph "
                       f"({t:.1f} s), sequential Go-order DFS with visited sets (oracle/keto_oracle.c POLICY_DFS), "
-                      f"{threads} host threads",
+                      f"{threads} host threads (os.cpu_count())",
+            "by_threads": {str(k): v[0] for k, v in res.items()}, "affinity_cpus": n_aff,
             "value_1thread": res[1][0], "host_cpu": host_cpu()}
 
 

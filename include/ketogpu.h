@@ -150,6 +150,9 @@ typedef struct {
   float set_fraction;       /* fraction of group#member subjects that are subject sets */
   float doc_set_fraction;   /* fraction of doc#viewer subjects that are L0 groups  */
   uint32_t preset;          /* 0 = C2/C4 rewrite-free; 1 = C3 (+ folders, OPL view/edit/share) */
+  float doc_alpha;          /* Pareto tail index of doc#viewer out-degrees (0 = 1.3)         */
+  float group_alpha;        /* Pareto tail index of group#member out-degrees (0 = 1.1); 0.5 =
+                               the degree law P(k) ~ k^-1.5 (Zipf 1.5) of SURVEY.md 8d       */
 } kg_synth_params;
 
 /* ---- snapshot --------------------------------------------------------------------------- */

@@ -69,7 +69,7 @@ class kg_tree_buf(C.Structure):
 class kg_synth_params(C.Structure):
     _fields_ = [("n_tuples_target", C.c_uint64), ("seed", C.c_uint64), ("n_layers", C.c_uint32),
                 ("max_degree", C.c_uint32), ("set_fraction", C.c_float), ("doc_set_fraction", C.c_float),
-                ("preset", C.c_uint32)]
+                ("preset", C.c_uint32), ("doc_alpha", C.c_float), ("group_alpha", C.c_float)]
 
 
 # every symbol include/ketogpu.h declares

@@ -725,7 +725,8 @@ int Snapshot::create_synthetic(const kg_synth_params* p, const kg_rewrite_prog* 
   SynthLayout L{};
   const uint64_t T = p->n_tuples_target ? p->n_tuples_target : 10000000ull;
   if (p->preset > 1) return set_error(-2, "unknown synthetic preset %u", p->preset);
-  if (!synth_make_layout(L, T, p->seed, p->n_layers, p->max_degree, p->set_fraction, p->doc_set_fraction, p->preset))
+  if (!synth_make_layout(L, T, p->seed, p->n_layers, p->max_degree, p->set_fraction, p->doc_set_fraction, p->preset,
+                         p->doc_alpha, p->group_alpha))
     return set_error(-2, "synthetic graph too large");
   synth = L;
   is_synth = true;

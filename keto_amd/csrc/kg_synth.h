@@ -110,7 +110,14 @@ __host__ __device__ __forceinline__ void synth_node(const SynthLayout& L, uint32
 
 // Builds the block list for a preset; returns false if ids would overflow.
 inline bool synth_make_layout(SynthLayout& L, uint64_t T, uint64_t seed, uint32_t n_layers, uint32_t max_degree,
-                              float set_frac, float doc_set_frac, uint32_t preset) {
+                              float set_frac, float doc_set_frac, uint32_t preset, float doc_alpha = 0.f,
+                              float group_alpha = 0.f) {
+  // out-degrees: truncated Pareto with tail index alpha (CCDF ~ k^-alpha), default 1.3 (docs) and
+  // 1.1 (groups): mean ~4-10 edges per row at max_degree 1e5, so a "1 B tuples" target holds
+  // ~0.95 B rows.  alpha 0.5 is the degree law P(k) ~ k^-1.5 (Zipf 1.5) SURVEY.md 8d names; its
+  // mean is ~sqrt(max_degree), i.e. ~40x the rows per node (the --heavy-tail bench point)
+  const float inv_doc = 1.f / (doc_alpha > 0.f ? doc_alpha : 1.3f);
+  const float inv_group = 1.f / (group_alpha > 0.f ? group_alpha : 1.1f);
   L = SynthLayout{};
   L.seed = seed;
   L.preset = preset;
@@ -146,11 +153,11 @@ inline bool synth_make_layout(SynthLayout& L, uint64_t T, uint64_t seed, uint32_
     node += count;
   };
   // C2 core (identical ids and hash streams for every preset)
-  add(L.n_docs, L.ns_doc, L.rel_viewer, 0, 1.f / 1.3f, 0, 0.f, doc_set_frac > 0 ? doc_set_frac : 0.5f,
+  add(L.n_docs, L.ns_doc, L.rel_viewer, 0, inv_doc, 0, 0.f, doc_set_frac > 0 ? doc_set_frac : 0.5f,
       SK_GROUP_LAYER, 0);
   L.group_node0 = node;
   for (uint32_t l = 0; l < L.n_layers; l++)
-    add(L.group_per_layer, L.ns_group, L.rel_member, L.n_docs + l * L.group_per_layer, 1.f / 1.1f, 0, 0.f,
+    add(L.group_per_layer, L.ns_group, L.rel_member, L.n_docs + l * L.group_per_layer, inv_group, 0, 0.f,
         l + 1 < L.n_layers ? (set_frac > 0 ? set_frac : 0.25f) : 0.f, l + 1 < L.n_layers ? SK_GROUP_LAYER : SK_NONE,
         l + 1);
   if (preset == 1) {

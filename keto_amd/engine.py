@@ -103,7 +103,8 @@ class Snapshot:
     def synthetic(cls, n_tuples: int, seed: int = 20250131, device: int = 0, n_layers: int = 8,
                   max_degree: int = 100000, set_fraction: float = 0.25, doc_set_fraction: float = 0.5,
                   preset: int = 0, shard: Optional[Tuple[int, int]] = None,
-                  devices: Optional[Sequence[int]] = None) -> "Snapshot":
+                  devices: Optional[Sequence[int]] = None, doc_alpha: float = 0.0,
+                  group_alpha: float = 0.0) -> "Snapshot":
         """Device-generated Drive-like graph (keto_amd/csrc/kg_synth.h); preset 0 = C2/C4, 1 = C3.
         shard = (rank, nranks): only this rank's rows (hash-sharded mode)."""
         from . import synth
@@ -111,7 +112,8 @@ class Snapshot:
         it = synth.interner()
         prog = synth.program(preset, it)
         snap = cls(None, it, device=device, _handle=C.c_void_p())
-        p = _lib.kg_synth_params(n_tuples, seed, n_layers, max_degree, set_fraction, doc_set_fraction, preset)
+        p = _lib.kg_synth_params(n_tuples, seed, n_layers, max_degree, set_fraction, doc_set_fraction, preset, doc_alpha,
+                                 group_alpha)
         prog_c = snap._prog(prog)
         h = C.c_void_p()
         pc = C.byref(prog_c) if prog_c is not None else None

@@ -479,6 +479,7 @@ typedef struct {
 
 static void* batch_worker(void* p) {
   batch_arg* a = (batch_arg*)p;
+  ko_stats mine = {0, 0, 0};  /* per-thread counters, added once: no lock per check */
   for (;;) {
     pthread_mutex_lock(a->mu);
     uint64_t i0 = a->next; a->next += 64;
@@ -497,11 +498,12 @@ static void* batch_worker(void* p) {
       ko_stats st = {0, 0, 0};
       a->out[i] = (uint8_t)check_one(a->ix, &qq, rn, sg, a->depth[i], a->global, a->policy, &e, &st);
       if (a->err) a->err[i] = e;
-      pthread_mutex_lock(a->mu);
-      a->st.rows_opened += st.rows_opened; a->st.edges_read += st.edges_read; a->st.probes += st.probes;
-      pthread_mutex_unlock(a->mu);
+      mine.rows_opened += st.rows_opened; mine.edges_read += st.edges_read; mine.probes += st.probes;
     }
   }
+  pthread_mutex_lock(a->mu);
+  a->st.rows_opened += mine.rows_opened; a->st.edges_read += mine.edges_read; a->st.probes += mine.probes;
+  pthread_mutex_unlock(a->mu);
   return NULL;
 }
 
