@@ -43,7 +43,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--tuples", type=float, default=None, help="synthetic graph size (tuples; default 1e9, 1e7 with --heavy-tail)")
+    ap.add_argument("--tuples", type=float, default=None, help="synthetic graph size (tuples; default 1e9; 2e6 with --heavy-tail, whose ~640 edges per row "
+                         "make that ~240 M rows)")
     ap.add_argument("--heavy-tail", action="store_true",
                     help="out-degree law P(k) ~ k^-1.5 (Pareto tail index 0.5 for docs and groups, SURVEY.md 8d) "
                          "instead of the default 1.3 / 1.1; ~40x the rows per node")
@@ -332,7 +333,7 @@ def aggregate(dist, elapsed: float, edges: float, device=None):
 def main():
     a = parse()
     if a.tuples is None:
-        a.tuples = 1e7 if a.heavy_tail else 1e9
+        a.tuples = 2e6 if a.heavy_tail else 1e9
     if a.mode == "expand":
         return bench_expand(a)
     if a.mode == "sharded":
@@ -366,6 +367,7 @@ def main():
     snap.tune("grid_wgs", a.grid_wgs)
     snap.tune("stream_wgs", a.stream_wgs)
     snap.tune("back_wgs", a.back_wgs)
+    snap.tune("grid_reserve", 1)  # a server pays this once at start-up, not inside some request's batch
     if snap.program is not None and not snap.program.empty:
         snap.tune("interp_wgs", a.interp_wgs)
     info = snap.info()

@@ -195,7 +195,10 @@ int kg_snapshot_info(const kg_snapshot* s, uint64_t* info4);
  * hash-sharded mode's per-batch (query, node) visited table (default 25).  key "interp_cap2"
  * (0..4194304): BFS list cap of the rewrite interpreter's many-slot HBM pass (0 = 256 Ki nodes);
  * queries that outgrow it rerun in the single full-size slot.  key "interp_wgs" (1..8): workgroups
- * of 4 query waves per CU in the interpreter's LDS pass (default 6). */
+ * of 4 query waves per CU in the interpreter's LDS pass (default 6).  key "grid_reserve": allocate
+ * now the grid tier's shared full-size pool (used by a query that overflows a workspace's pool on
+ * its own; otherwise allocated on first need).  key "grid_cap": log entries of a workspace's grid
+ * pool (0 = 16 Mi; small values force the overflow paths in tests). */
 int kg_snapshot_tune(kg_snapshot* s, const char* key, int64_t value);
 /* Synthetic layout: ids6 = {n_docs, n_groups, n_users, n_folders, user_obj0, folder_obj0}
  * (doc d = object d, group g = object n_docs+g, user u = object user_obj0+u). */

@@ -286,6 +286,12 @@ static int tune_one(Snapshot* s, const char* key, int64_t value) {
     s->interp_cap2 = (uint32_t)value;
     return 0;
   }
+  if (strcmp(key, "grid_reserve") == 0) return kg::grid_reserve(s);  // the shared full-size grid pool, now
+  if (strcmp(key, "grid_cap") == 0) {
+    if (value < 0 || value > (1ll << 34)) return set_error(-2, "grid_cap must be in [0, 2^34]");
+    s->grid_small_cap = (uint64_t)value;
+    return 0;
+  }
   if (strcmp(key, "back_wgs") == 0) {
     if (value < 1 || value > 3) return set_error(-2, "back_wgs must be in [1, 3]");
     s->back_wgs = (int)value;

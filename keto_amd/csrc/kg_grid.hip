@@ -275,64 +275,91 @@ __global__ void k_grid_finish(const uint32_t* slot_q, const uint32_t* slot_hit, 
 // phase 0: run every round synchronously.  phase 1: enqueue the first round and its readback, return
 // 1 without waiting (the caller synchronises the stream once for the whole batch).  phase 2: resume
 // after that synchronisation: read the first round's result and run further rounds if needed.
-int grid_tier(Snapshot* s, Workspace* w, const RQuery* rq, const uint32_t* qlist, const uint32_t* d_count, int global_max_depth,
-              uint8_t* out, uint32_t* err, hipStream_t stream, GridStats* gs, int phase) {
-  static_assert(sizeof(GridCtl) + 64 <= 32768, "grid readback fits the upper half of the pinned buffer");
-  char* pin = (char*)w->host_buf(65536);
-  if (!pin) return set_error(-1, "pinned host buffer");
-  uint32_t* hb = (uint32_t*)(pin + 32768);  // the lower half holds the batch's Ctl readback
+static uint64_t grid_full_cap(const Snapshot* s) {
   const uint64_t nn = std::max<uint32_t>(s->ds.n_nodes, 1);
-  // Log capacity: the queries that reach this tier touch far fewer nodes than the graph holds, so a
-  // workspace starts with a log of min(n_nodes, 16 Mi) entries (~0.6 GB with its hash and tile
-  // maps, instead of ~7 GB at 1 B tuples and ~27 GB at C3's 688 M nodes -- per batch in flight).
-  // Only a single query whose region overflows that log on its own (G == 1) grows it to the size
-  // that always fits (>= n_nodes: one slot logs each node at most once).
-  const uint64_t full_cap = std::max<uint64_t>(nn + 1024, 64ull << 20);
-  const uint32_t G0 = 0xFFFF;  // slot field is 16 bits
+  return std::max<uint64_t>(nn + 1024, 64ull << 20);  // one slot logs each node at most once
+}
+constexpr uint32_t G0 = 0xFFFF;  // slot field is 16 bits
+
+struct GridView {  // pointers into a pool laid out for `cap` log entries
   uint64_t cap = 0, hcap = 0;
   uint64_t* H = nullptr;
   GridLog lg{};
   uint2* slot_info = nullptr;
   uint32_t *slot_q = nullptr, *slot_hit = nullptr;
   GridCtl* ctl = nullptr;
-  auto layout = [&]() -> int {
-    cap = w->grid_cap ? w->grid_cap : std::min<uint64_t>(full_cap, 16ull << 20);
-    hcap = 1;
-    while (hcap < 2 * cap) hcap <<= 1;  // hash >= 2x the log (load <= 0.5)
-    const size_t need = hcap * 8 + cap * (4 + 4 + 8) + 2 * TILE_CAP * 4 + (size_t)G0 * 16 + sizeof(GridCtl) + 4096;
-    if (need > w->grid_pool_bytes) {
-      if (w->grid_pool) HIPC(hipFree(w->grid_pool));
-      w->grid_pool = nullptr;
-      w->grid_pool_bytes = 0;
-      HIPC(hipMalloc(&w->grid_pool, need));
-      HIPC(hipMemsetAsync(w->grid_pool, 0, hcap * 8, stream));  // epoch 0 = empty
-      w->grid_pool_bytes = need;
-      w->grid_epoch = 0;
-    }
-    w->grid_cap = cap;
-    char* p = (char*)w->grid_pool;
-    H = (uint64_t*)p;
-    p += hcap * 8;
-    lg.cap = cap;
-    lg.ex = (uint64_t*)p;
-    p += cap * 8;
-    lg.slot = (uint32_t*)p;
-    p += cap * 4;
-    lg.rb = (uint32_t*)p;
-    p += cap * 4;
-    lg.tile_first[0] = (uint32_t*)p;
-    p += TILE_CAP * 4;
-    lg.tile_first[1] = (uint32_t*)p;
-    p += TILE_CAP * 4;
-    slot_info = (uint2*)p;
-    p += (size_t)G0 * 8;
-    slot_q = (uint32_t*)p;
-    slot_hit = slot_q + G0;
-    p += (size_t)G0 * 8;
-    ctl = (GridCtl*)(((uintptr_t)p + 255) & ~uintptr_t(255));
-    return 0;
-  };
-  if (int rc = layout()) return rc;
+};
+
+static int grid_layout(GridPool* P, uint64_t cap, hipStream_t stream, GridView* v) {
+  uint64_t hcap = 1;
+  while (hcap < 2 * cap) hcap <<= 1;  // hash >= 2x the log (load <= 0.5)
+  const size_t need = hcap * 8 + cap * (4 + 4 + 8) + 2 * TILE_CAP * 4 + (size_t)G0 * 16 + sizeof(GridCtl) + 4096;
+  if (need > P->bytes) {
+    P->release();
+    HIPC(hipMalloc(&P->mem, need));
+    HIPC(hipMemsetAsync(P->mem, 0, hcap * 8, stream));  // epoch 0 = empty
+    P->bytes = need;
+  }
+  P->cap = cap;
+  char* p = (char*)P->mem;
+  v->cap = cap;
+  v->hcap = hcap;
+  v->H = (uint64_t*)p;
+  p += hcap * 8;
+  v->lg.cap = cap;
+  v->lg.ex = (uint64_t*)p;
+  p += cap * 8;
+  v->lg.slot = (uint32_t*)p;
+  p += cap * 4;
+  v->lg.rb = (uint32_t*)p;
+  p += cap * 4;
+  v->lg.tile_first[0] = (uint32_t*)p;
+  p += TILE_CAP * 4;
+  v->lg.tile_first[1] = (uint32_t*)p;
+  p += TILE_CAP * 4;
+  v->slot_info = (uint2*)p;
+  p += (size_t)G0 * 8;
+  v->slot_q = (uint32_t*)p;
+  v->slot_hit = v->slot_q + G0;
+  p += (size_t)G0 * 8;
+  v->ctl = (GridCtl*)(((uintptr_t)p + 255) & ~uintptr_t(255));
+  return 0;
+}
+
+int grid_reserve(Snapshot* s) {
+  HIPC(hipSetDevice(s->device));
+  std::lock_guard<std::mutex> lk(s->giant_mu);
+  GridView v;
+  if (int rc = grid_layout(&s->giant, grid_full_cap(s), s->stream, &v)) return rc;
+  HIPC(hipStreamSynchronize(s->stream));
+  return 0;
+}
+
+// Host driver: qlist / count live on the device.  A round is launched without knowing the count
+// (the kernels clamp to it); the host reads the counters once per round, after its last kernel.
+// phase 0: run every round synchronously.  phase 1: enqueue the first round and its readback, return
+// 1 without waiting (the caller synchronises the stream once for the whole batch).  phase 2: resume
+// after that synchronisation: read the first round's result and run further rounds if needed.
+//
+// Memory: the queries that reach this tier touch far fewer nodes than the graph holds, so a
+// workspace's pool has a log of min(n_nodes, 16 Mi) entries (~0.6 GB with its hash and tile maps,
+// instead of ~7 GB at 1 B tuples and ~27 GB at C3's 688 M nodes -- per batch in flight).  A round
+// that overflows reruns with a quarter of the slots; a single query that overflows the workspace
+// pool on its own reruns in the snapshot's shared full-size pool (allocated once, lazily or by
+// kg_snapshot_tune "grid_reserve"; one query at a time), so no workspace ever reallocates.  After
+// a round succeeds the slot count grows back (x4), so one giant query does not serialise the rest.
+int grid_tier(Snapshot* s, Workspace* w, const RQuery* rq, const uint32_t* qlist, const uint32_t* d_count, int global_max_depth,
+              uint8_t* out, uint32_t* err, hipStream_t stream, GridStats* gs, int phase) {
+  static_assert(sizeof(GridCtl) + 64 <= 32768, "grid readback fits the upper half of the pinned buffer");
+  char* pin = (char*)w->host_buf(65536);
+  if (!pin) return set_error(-1, "pinned host buffer");
+  uint32_t* hb = (uint32_t*)(pin + 32768);  // the lower half holds the batch's Ctl readback
+  const uint64_t full_cap = grid_full_cap(s);
+  const uint64_t small_cap = std::min<uint64_t>(full_cap, s->grid_small_cap ? s->grid_small_cap : 16ull << 20);
+  GridPool* gp = &w->grid;
+  std::unique_lock<std::mutex> giant_lk(s->giant_mu, std::defer_lock);
+  GridView v;
+  if (int rc = grid_layout(gp, small_cap, stream, &v)) return rc;
   uint32_t G = G0;
   int64_t count = -1;  // unknown until the first readback
   bool resume = phase == 2;
@@ -340,29 +367,29 @@ int grid_tier(Snapshot* s, Workspace* w, const RQuery* rq, const uint32_t* qlist
    if (!resume) {
     if (phase == 1) w->grid_reran = false;
     if (phase == 2) w->grid_reran = true;  // rounds past the first: the caller re-reads the results
-    if (++w->grid_epoch == 0x10000) {  // epoch wrap: the table is zeroed once per 65535 rounds
-      HIPC(hipMemsetAsync(H, 0, hcap * 8, stream));
-      w->grid_epoch = 1;
+    if (++gp->epoch == 0x10000) {  // epoch wrap: the table is zeroed once per 65535 rounds
+      HIPC(hipMemsetAsync(v.H, 0, v.hcap * 8, stream));
+      gp->epoch = 1;
     }
-    const uint64_t epoch = w->grid_epoch;
+    const uint64_t epoch = gp->epoch;
     const uint32_t slot_blocks = (G + 255) / 256;
-    HIPC(hipMemsetAsync(ctl, 0, sizeof(GridCtl), stream));
-    hipLaunchKernelGGL(k_grid_init, dim3(slot_blocks), dim3(256), 0, stream, s->ds, rq, qlist, d_count, done, G, lg,
-                       slot_q, slot_info, slot_hit, H, hcap - 1, epoch, ctl);
+    HIPC(hipMemsetAsync(v.ctl, 0, sizeof(GridCtl), stream));
+    hipLaunchKernelGGL(k_grid_init, dim3(slot_blocks), dim3(256), 0, stream, s->ds, rq, qlist, d_count, done, G, v.lg,
+                       v.slot_q, v.slot_info, v.slot_hit, v.H, v.hcap - 1, epoch, v.ctl);
     HIPC(hipGetLastError());
     // Levels run back to back on the device (sizes never come back to the host; an empty level
     // costs one near-empty launch).  Level k expands nodes at rest depth D-k >= 2, so at most
     // global_max_depth-1 levels exist.
     const int max_levels = std::max(1, global_max_depth - 1);
     for (int level = 0; level < max_levels; level++) {
-      hipLaunchKernelGGL(k_grid_level, dim3((uint32_t)s->n_cu * s->grid_wgs), dim3(256), 0, stream, s->ds, lg, level,
-                         slot_info, slot_hit, H, hcap - 1, epoch, ctl);
+      hipLaunchKernelGGL(k_grid_level, dim3((uint32_t)s->n_cu * s->grid_wgs), dim3(256), 0, stream, s->ds, v.lg, level,
+                         v.slot_info, v.slot_hit, v.H, v.hcap - 1, epoch, v.ctl);
       HIPC(hipGetLastError());
     }
-    hipLaunchKernelGGL(k_grid_finish, dim3(slot_blocks), dim3(256), 0, stream, slot_q, slot_hit, d_count, done, G, out,
-                       err, &ctl->overflow);
+    hipLaunchKernelGGL(k_grid_finish, dim3(slot_blocks), dim3(256), 0, stream, v.slot_q, v.slot_hit, d_count, done, G,
+                       out, err, &v.ctl->overflow);
     HIPC(hipGetLastError());
-    HIPC(hipMemcpyAsync(hb, ctl, sizeof(GridCtl), hipMemcpyDeviceToHost, stream));
+    HIPC(hipMemcpyAsync(hb, v.ctl, sizeof(GridCtl), hipMemcpyDeviceToHost, stream));
     HIPC(hipMemcpyAsync(hb + sizeof(GridCtl) / 4, d_count, 4, hipMemcpyDeviceToHost, stream));
     if (phase == 1) return 1;  // first round enqueued; the caller synchronises and resumes
     HIPC(hipStreamSynchronize(stream));
@@ -378,10 +405,11 @@ int grid_tier(Snapshot* s, Workspace* w, const RQuery* rq, const uint32_t* qlist
     }
     if (h.overflow) {  // log or probe bound exceeded: rerun these queries with fewer slots
       if (G == 1) {
-        if (cap >= full_cap) return set_error(KG_ERR_RESOURCE_CODE, "grid tier capacity exceeded");
-        HIPC(hipStreamSynchronize(stream));  // one query alone overflowed: grow the log to the full size
-        w->grid_cap = full_cap;
-        if (int rc = layout()) return rc;
+        if (gp == &s->giant) return set_error(KG_ERR_RESOURCE_CODE, "grid tier capacity exceeded");
+        // one query alone overflowed the workspace pool: rerun it in the shared full-size pool
+        giant_lk.lock();
+        gp = &s->giant;
+        if (int rc = grid_layout(gp, full_cap, stream, &v)) return rc;
         continue;
       }
       G = std::max<uint32_t>(1, std::min(G, cnt) / 4);
@@ -394,6 +422,12 @@ int grid_tier(Snapshot* s, Workspace* w, const RQuery* rq, const uint32_t* qlist
       gs->logged += h.logged;
     }
     done += cnt;
+    if (gp == &s->giant) {  // back to the workspace pool for the rest
+      gp = &w->grid;
+      if (int rc = grid_layout(gp, small_cap, stream, &v)) return rc;
+      giant_lk.unlock();
+    }
+    if (G < G0) G = (uint32_t)std::min<uint64_t>(G0, (uint64_t)G * 4);
   }
   return 0;
 }

@@ -28,6 +28,15 @@ void clear_error();
                                                  __FILE__, __LINE__);                            \
   } while (0)
 
+// Grid-tier memory (kg_grid.hip): visited hash | entry log | tile maps | slots | control block.
+struct GridPool {
+  void* mem = nullptr;
+  size_t bytes = 0;
+  uint64_t cap = 0;    // log entries the pool is laid out for (0: not yet)
+  uint32_t epoch = 0;  // visited-table epoch of the last round
+  void release();
+};
+
 // Everything one in-flight check batch mutates: scratch lists, tier pools, the grid tier's epoch,
 // timing events and the pinned readback buffer.  One per HIP stream, so batches on different
 // streams overlap on the device (the tail tiers of one batch run beside the next batch's
@@ -41,10 +50,7 @@ struct Workspace {
   size_t scratch_n = 0;  // queries the scratch was last sized for
   void* heavy_pool = nullptr;
   size_t heavy_pool_bytes = 0;
-  void* grid_pool = nullptr;  // grid tier: visited hash | log | slots | ctl | scan sums
-  size_t grid_pool_bytes = 0;
-  uint32_t grid_epoch = 0;
-  uint64_t grid_cap = 0;    // grid-tier log entries the pool is laid out for (0: not yet)
+  GridPool grid;  // grid tier, sized for the queries that reach it (16 Mi log entries)
   bool grid_reran = false;  // the last batch's grid tier ran rounds after the first (results rewritten)
   void* interp_pool = nullptr;
   size_t interp_pool_bytes = 0;
@@ -128,6 +134,7 @@ struct Snapshot {
   int interp_wgs = 6;        // kg_snapshot_tune("interp_wgs"): k_interp_lds workgroups (4 waves) per CU (6 fit the LDS)
   uint32_t interp_cap2 = 0;  // kg_snapshot_tune("interp_cap2"): pass-2 BFS list cap of the rewrite path (0 = 256 Ki)
   int back_wgs = 3;          // kg_snapshot_tune("back_wgs"): k_back workgroups per CU (1..3, LDS allows 3)
+  uint64_t grid_small_cap = 0;  // kg_snapshot_tune("grid_cap"): workspace grid-log entries (0 = 16 Mi; tests)
   // replicas: the same snapshot on more devices (kg_snapshot_create's device mask); this object is
   // replica 0 and owns the others.  Host-buffer batches and expands are split over all of them.
   std::vector<Snapshot*> peers;
@@ -137,6 +144,10 @@ struct Snapshot {
   std::list<std::pair<std::thread::id, std::vector<Lane*>>> lanes;  // list: stable addresses
   std::vector<Lane*>* thread_lanes();  // this thread's lanes (one per replica), created on first use
   std::atomic<uint64_t> rr_next{0};      // replica rotation of batches smaller than one chunk per replica
+  // The grid tier's full-size pool (a log that holds every node): shared by the workspaces, used
+  // one query at a time by a round whose single query overflowed its workspace's pool.
+  std::mutex giant_mu;
+  GridPool giant;
 
   ~Snapshot();
   int init_device(int dev);
@@ -163,6 +174,8 @@ int shard_seed(Snapshot* s, const kg_query* d_q, size_t n, int32_t gdepth, kg_fr
 int shard_level(Snapshot* s, const kg_frec* d_in, size_t n_in, const uint32_t* d_n_in, kg_frec* d_out, size_t cap,
                 uint32_t* d_counts, uint8_t* d_res, uint32_t* d_err, hipStream_t stream);
 int shard_finish(Snapshot* s, size_t n, uint8_t* d_res, const uint32_t* d_err, hipStream_t stream);
+// kg_grid.hip
+int grid_reserve(Snapshot* s);  // allocates the shared full-size grid pool now (kg_snapshot_tune "grid_reserve")
 // kg_expand.hip
 int expand_batch(Snapshot* s, const kg_set* roots, size_t n, int32_t global, kg_tree_buf* out);
 

@@ -227,14 +227,23 @@ Snapshot::~Snapshot() {
   for (void* p : allocs) hipFree(p);
   for (Workspace* w : wss) delete w;
   if (shard_vis) hipFree(shard_vis);
+  giant.release();
   if (stream) hipStreamDestroy(stream);
+}
+
+void GridPool::release() {
+  if (mem) hipFree(mem);
+  mem = nullptr;
+  bytes = 0;
+  cap = 0;
+  epoch = 0;
 }
 
 Workspace::~Workspace() {
   if (device >= 0) hipSetDevice(device);
   if (scratch) hipFree(scratch);
   if (heavy_pool) hipFree(heavy_pool);
-  if (grid_pool) hipFree(grid_pool);
+  grid.release();
   if (interp_pool) hipFree(interp_pool);
   if (pinned) hipHostFree(pinned);
   for (auto& e : ev)

@@ -126,8 +126,10 @@ def test_heavy_path_overflow_star():
     assert e.last_stats["n_medium"] + e.last_stats["n_heavy"] + e.last_stats["n_back"] >= 1
 
 
-@pytest.mark.parametrize("tiers,wide,back", [(0, 0, 0), (0, 1, 0), (1, 1, 0), (2, 0, 0), (0, 0, 1), (1, 0, 1), (0, 0, 2)])
-def test_workgroup_tiers_lds_and_hbm(tiers, wide, back):
+@pytest.mark.parametrize("tiers,wide,back,grid_cap", [(0, 0, 0, 0), (0, 1, 0, 0), (1, 1, 0, 0), (2, 0, 0, 0),
+                                                     (0, 0, 1, 0), (1, 0, 1, 0), (0, 0, 2, 0), (0, 0, 0, 600),
+                                                     (0, 0, 0, 5000)])
+def test_workgroup_tiers_lds_and_hbm(tiers, wide, back, grid_cap):
     # > 256 expanded nodes leaves the wave tiers; with back=1 the backward tier (reverse search
     # from the subject's holders) answers first and hands on what outgrows it; tiers=0 sends the
     # rest to the grid tier, 1/2 first to the LDS workgroup tier (<= 4096 expanded nodes), then to
@@ -148,6 +150,9 @@ def test_workgroup_tiers_lds_and_hbm(tiers, wide, back):
     e.snapshot.tune("tiers", tiers)
     e.snapshot.tune("wide", wide)
     e.snapshot.tune("back", back)
+    # grid_cap: the workspace's grid log holds 600 / 5000 entries, so rounds overflow, rerun with
+    # fewer slots, and the queries that overflow it alone run in the shared full-size pool
+    e.snapshot.tune("grid_cap", grid_cap)
     it = reg.interner
     qs = [RelationTuple.from_string(s) for s in
           ["g:root#m@target", "g:root#m@mid", "g:root#m@none", "g:c3#m@target", "g:c7#m@mid", "g:d3#m@target",
