@@ -66,6 +66,8 @@ def parse():
     ap.add_argument("--inflight", type=int, default=4,
                     help="batches in flight per GPU: one HIP stream (own workspace) and one host thread each")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline time budget (0 = skip)")
+    ap.add_argument("--replay", type=int, default=0,
+                    help="cycle over this many distinct batches (0 = a distinct batch for every step; diagnostics)")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="CPU-baseline threads (0 = os.cpu_count(), also timed at the affinity count, 16 and 1)")
     ap.add_argument("--preset", type=int, default=0,
@@ -383,18 +385,19 @@ def main():
     streams = [torch.cuda.current_stream(local)] + [torch.cuda.Stream(local) for _ in range(P - 1)]
     warm = max(a.warmup, P)  # every stream's workspace is allocated before the timed region
     n_batches = warm + a.steps
-    dq_all = torch.empty((n_batches, B, 7), dtype=torch.int32, device=dev)
-    for k in range(n_batches):
+    n_distinct = min(n_batches, a.replay) if a.replay > 0 else n_batches
+    dq_all = torch.empty((n_distinct, B, 7), dtype=torch.int32, device=dev)
+    for k in range(n_distinct):
         _lib.check(L.kg_synth_queries(snap.handle, 1000 + rank + 7919 * k, B, dq_all[k].data_ptr()),
                    "kg_synth_queries")
     douts = [torch.empty(B, dtype=torch.uint8, device=dev) for _ in range(P)]
     derrs = [torch.empty(B, dtype=torch.int32, device=dev) for _ in range(P)]
-    dq = dq_all[warm]
+    dq = dq_all[warm % n_distinct]
     timed_out = torch.empty((a.steps, B), dtype=torch.uint8, device=dev)
 
     def step(p, k, st=None):
         o = timed_out[k - warm] if k >= warm else douts[p]  # every timed batch keeps its own results
-        rc = L.kg_check_batch_device(snap.handle, dq_all[k].data_ptr(), B, a.global_depth, o.data_ptr(),
+        rc = L.kg_check_batch_device(snap.handle, dq_all[k % n_distinct].data_ptr(), B, a.global_depth, o.data_ptr(),
                                      derrs[p].data_ptr(), C.byref(st) if st is not None else None,
                                      C.c_void_p(streams[p].cuda_stream))
         _lib.check(rc, "kg_check_batch_device")
@@ -476,6 +479,10 @@ def main():
                    "inflight_per_gpu": P},
         "gteps": edges / elapsed / 1e9,
         "p99_batch_ms": float(np.percentile(np.array(lat) * 1e3, 99)),
+        "batch_ms": {q: float(np.percentile(np.array(lat) * 1e3, v)) for q, v in
+                     (("p50", 50), ("p90", 90), ("p99", 99), ("max", 100))},
+        "edges_per_batch": {q: float(np.percentile([x.edges_read for x in stats], v)) for q, v in
+                            (("p50", 50), ("p90", 90), ("max", 100))},
         "allowed_fraction": float(res.mean()),
         "tiers": {"light": int(stats[-1].n_light), "wide": int(stats[-1].n_wide), "medium": int(stats[-1].n_medium),
                   "back": int(stats[-1].n_back), "grid": int(stats[-1].n_grid), "heavy": int(stats[-1].n_heavy),

@@ -1193,13 +1193,18 @@ __global__ __launch_bounds__(256) void k_heavy(DevSnap s, const RQuery* __restri
 // in flight per CU), its overflow goes to k_back<256>, one query per WORKGROUP (8192 / 4096).
 template <int W>
 struct BackCfg;
+// EDGES: reverse edges one query may read here.  A level that reaches hub groups reads their whole
+// parent lists (up to 1e5 each) on one wave -- 28 ms for one query at 1 B tuples before this bound
+// (profiles/r2o_*): such a query goes to the grid tier, which spreads its edges over the whole GPU.
 template <>
 struct BackCfg<64> {
   static constexpr uint32_t VLOG2 = 9, CAP = 256;  // larger caps only lengthen the tail (1024: -9 % checks/s)
+  static constexpr uint32_t EDGES = 1u << 14;
 };
 template <>
 struct BackCfg<256> {
   static constexpr uint32_t VLOG2 = 13, CAP = 4096;
+  static constexpr uint32_t EDGES = 1u << 17;
 };
 
 template <int W>
@@ -1286,6 +1291,7 @@ __global__ __launch_bounds__(256) void k_back(DevSnap s, const RQuery* __restric
     }
     bk_sync<W>();
     uint32_t lvl_b = 0, lvl_e = L.n;
+    uint32_t budget = BackCfg<W>::EDGES;  // wave-uniform
     for (int j = 1; j <= q.depth - 1 && lvl_b < lvl_e && !L.hit && !L.over; j++) {
       const bool keep = j < q.depth - 1;  // parents found here can still be expanded
       for (uint32_t base = lvl_b; base < lvl_e; base += W) {
@@ -1302,7 +1308,10 @@ __global__ __launch_bounds__(256) void k_back(DevSnap s, const RQuery* __restric
         const uint32_t excl = W == 64 ? wave_excl_scan((uint32_t)(re - rb), &total)
                                       : block_excl_scan((uint32_t)(re - rb), L.wsum, &total);
         L.pref[t] = excl;
+        if (total > budget && t == 0) L.over = 1;  // too much for one wave: the grid tier takes it
         bk_sync<W>();
+        if (L.over) break;
+        budget -= total;
         if (t == 0) st_edges += total;
         // BU edges per thread and step: the BU parent loads of a thread are independent, so a long
         // reverse row costs 1/BU of the dependent round trips
