@@ -178,6 +178,13 @@ int kg_snapshot_replicas(const kg_snapshot* s, int* devices, int cap);
 void kg_snapshot_destroy(kg_snapshot* s);
 /* sizes: [0]=nodes [1]=rows [2]=set edges [3]=device bytes */
 int kg_snapshot_info(const kg_snapshot* s, uint64_t* info4);
+/* Rewrite materialisation at build (no reference counterpart; keto_amd/csrc/kg_augment.hip): every
+ * relation whose rewrite is a union of `this` rows, computed subject sets and tuple-to-subject-sets
+ * (internal/check/rewrites.go:30-260 restricted to `or`) is answered as one plain union node per
+ * object.  out3: [0] union nodes, [1] of them new node ids (objects without a row of the relation
+ * itself), [2] check-row entries (the direct tuples the union nodes hold).  KG_MATERIALIZE=0 in
+ * the environment at snapshot creation turns it off. */
+int kg_snapshot_materialized(const kg_snapshot* s, uint64_t* out3);
 /* Engine knobs (no reference counterpart; tuning and tests).  key "tiers": where queries that
  * overflow the wave tiers go -- 0 = grid tier (default), 1 = LDS workgroup tier then grid tier,
  * 2 = LDS workgroup tier then one-workgroup-per-query HBM tier.  key "light": the first wave

@@ -239,6 +239,15 @@ int kg_snapshot_info(const kg_snapshot* sp, uint64_t* info4) {
   return 0;
 }
 
+int kg_snapshot_materialized(const kg_snapshot* sp, uint64_t* out3) {
+  if (!sp || !out3) return set_error(-2, "NULL argument");
+  const Snapshot* s = reinterpret_cast<const Snapshot*>(sp);
+  out3[0] = s->n_virtual;
+  out3[1] = s->n_virtual_new;
+  out3[2] = s->n_check_rows;
+  return 0;
+}
+
 static int tune_one(Snapshot* s, const char* key, int64_t value) {
   std::lock_guard<std::mutex> lk(s->mu);
   if (strcmp(key, "tiers") == 0) {

@@ -46,12 +46,12 @@ __device__ __forceinline__ uint32_t nmap_find(const DevSnap& s, uint32_t ns, uin
 __device__ __forceinline__ bool dset_probe(const DevSnap& s, uint32_t node, uint32_t subj) {
   static_assert(DSET_BUCKET == 2, "one ulonglong2 per bucket");
   uint64_t key = dset_key(node, subj);
-  uint64_t b = mix64(key) & s.dset_mask;
-  for (uint64_t n = 0; n <= s.dset_mask; n++) {
+  uint64_t b = dset_home(key, s.dset_nb);
+  for (uint64_t n = 0; n < s.dset_nb; n++) {
     const ulonglong2 a = *reinterpret_cast<const ulonglong2*>(s.dset + b * DSET_BUCKET);
     if (a.x == key || a.y == key) return true;
     if (a.y == EMPTY64) return false;  // buckets fill front to back
-    b = (b + 1) & s.dset_mask;
+    b = b + 1 == s.dset_nb ? 0 : b + 1;
   }
   return false;
 }

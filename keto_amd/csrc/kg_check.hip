@@ -771,7 +771,7 @@ __device__ __forceinline__ uint32_t s2_meta(uint32_t len, uint32_t slot, uint32_
 // is walked by the lanes that need it under a wave-uniform branch.
 __device__ __forceinline__ bool dset_probe_fast(const DevSnap& s, bool want, uint32_t node, uint32_t subj) {
   const uint64_t key = dset_key(node, subj);
-  uint64_t b = mix64(key) & s.dset_mask;
+  const uint64_t b = dset_home(key, s.dset_nb);
   bool hit = false, more = false;
   if (want) {
     const ulonglong2 a = *reinterpret_cast<const ulonglong2*>(s.dset + b * DSET_BUCKET);

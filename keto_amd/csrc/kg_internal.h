@@ -7,6 +7,10 @@
 //                                        sets skipped), kept in shard_id order.
 //   row_off[n_nodes+1] u64 / row_subj[]   full rows (every subject, tagged), shard_id order: expand
 //                                        (internal/expand/engine.go:57-94) and tuple-to-subject-set.
+//   crow_off / crow_subj                  check rows (rewrite materialisation, kg_augment.hip): the
+//                                        direct tuples checkDirect sees per node -- a materialised
+//                                        union node holds the rows of every relation it unites;
+//                                        nullptr: the full rows.  dset, signatures and holders use them.
 //   dset                                  bucketed hash set of (node << 32 | tagged subject):
 //                                        checkDirect's exact-tuple query (engine.go:159-163).
 //   nmap                                  (ns,rel,obj) -> node id + its set row (begin, length), one
@@ -52,6 +56,11 @@ __host__ __device__ __forceinline__ uint64_t nmap_key(uint32_t ns, uint32_t rel,
 }
 __host__ __device__ __forceinline__ uint64_t dset_key(uint32_t node, uint32_t subj) {
   return ((uint64_t)node << 32) | subj;
+}
+// Home bucket of a dset key: multiply-shift range reduction over any bucket count, so the table is
+// sized for its load exactly instead of rounding up to a power of two (up to 2x the HBM).
+__host__ __device__ __forceinline__ uint64_t dset_home(uint64_t key, uint64_t nb) {
+  return (uint64_t)(((unsigned __int128)mix64(key) * nb) >> 64);
 }
 
 // Shard of a node in the hash-sharded mode: all relations of one object live on
@@ -107,8 +116,10 @@ struct DevSnap {
   const AdjX* adjx;  // parallel to adj
   const uint64_t* row_off;
   const uint32_t* row_subj;
+  const uint64_t* crow_off;  // check rows (nullptr: row_off / row_subj)
+  const uint32_t* crow_subj;
   const uint64_t* dset;
-  uint64_t dset_mask;  // n_buckets - 1
+  uint64_t dset_nb;  // buckets (DSET_BUCKET keys each); probes wrap at dset_nb
   const NSlot* nmap;
   uint64_t nmap_mask;  // n_slots - 1
   const uint8_t* nflags;  // nullptr: every node pure

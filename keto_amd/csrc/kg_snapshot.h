@@ -106,7 +106,10 @@ struct Snapshot {
   bool is_synth = false;
   SynthLayout synth{};
   uint64_t h_row_off_last = 0, n_set_edges = 0, device_bytes = 0;
-  std::vector<void*> allocs;
+  uint64_t n_check_rows = 0;  // entries of the check rows (crow; == h_row_off_last without materialisation)
+  uint64_t n_virtual = 0, n_virtual_new = 0;  // materialised rewrite nodes (kg_augment.hip), of them new ids
+  int materialize = 1;  // rewrite materialisation at build (KG_MATERIALIZE=0 turns it off)
+  std::vector<std::pair<void*, size_t>> allocs;
   // host mirrors (host-tuple path)
   std::vector<uint32_t> h_nd_ns, h_nd_obj, h_nd_rel, h_row_subj;
   std::vector<uint64_t> h_row_off, h_adj_off;
@@ -152,9 +155,11 @@ struct Snapshot {
   ~Snapshot();
   int init_device(int dev);
   int alloc(void** p, size_t bytes);
+  void free_alloc(const void* p);
   int create_from_tuples(const kg_tuple* rows, size_t n, const kg_dict* dict, const kg_rewrite_prog* prog);
   int create_synthetic(const kg_synth_params* p, const kg_rewrite_prog* prog);
   int upload_program(const kg_dict* dict, const kg_rewrite_prog* prog);
+  int augment_rewrites();  // kg_augment.hip: monotone rewrites -> plain union nodes
   int build_hash_tables();
   int build_reverse();
   uint8_t host_relflag(uint32_t ns, uint32_t rel) const;

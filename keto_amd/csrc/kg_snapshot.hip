@@ -21,14 +21,14 @@
 namespace kg {
 
 // ------------------------------------------------------------------ device hash-table builders
-__global__ void k_dset_insert_rows(uint64_t* dset, uint64_t mask, const uint64_t* row_off, const uint32_t* row_subj,
+__global__ void k_dset_insert_rows(uint64_t* dset, uint64_t nb, const uint64_t* row_off, const uint32_t* row_subj,
                                    uint32_t n_nodes) {
   uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
   if (v >= n_nodes) return;
   for (uint64_t i = row_off[v]; i < row_off[v + 1]; i++) {
     uint64_t key = dset_key(v, row_subj[i]);
-    uint64_t b = mix64(key) & mask;
-    for (uint64_t n = 0; n <= mask; n++) {  // sized for load <= 0.5: always finds room
+    uint64_t b = dset_home(key, nb);
+    for (uint64_t n = 0; n < nb; n++) {  // sized for load <= 0.25: always finds room
       uint64_t* bucket = dset + b * DSET_BUCKET;
       bool done = false;
       for (int s = 0; s < DSET_BUCKET; s++) {
@@ -40,7 +40,7 @@ __global__ void k_dset_insert_rows(uint64_t* dset, uint64_t mask, const uint64_t
         }
       }
       if (done) break;
-      b = (b + 1) & mask;
+      b = b + 1 == nb ? 0 : b + 1;
     }
   }
 }
@@ -224,7 +224,7 @@ Snapshot::~Snapshot() {
     for (Lane* l : tl.second) delete l;  // before the workspaces: a lane's stream owns one of them
   for (Snapshot* p : peers) delete p;
   if (device >= 0) hipSetDevice(device);
-  for (void* p : allocs) hipFree(p);
+  for (auto& a : allocs) hipFree(a.first);
   for (Workspace* w : wss) delete w;
   if (shard_vis) hipFree(shard_vis);
   giant.release();
@@ -332,9 +332,20 @@ int Snapshot::alloc(void** p, size_t bytes) {
   if (bytes == 0) bytes = 16;
   hipError_t e = hipMalloc(p, bytes);
   if (e != hipSuccess) return set_error(KG_ERR_RESOURCE_CODE, "hipMalloc(%zu) failed: %s", bytes, hipGetErrorString(e));
-  allocs.push_back(*p);
+  allocs.emplace_back(*p, bytes);
   device_bytes += bytes;
   return 0;
+}
+
+void Snapshot::free_alloc(const void* p) {
+  for (size_t i = 0; i < allocs.size(); i++)
+    if (allocs[i].first == p) {
+      hipFree(allocs[i].first);
+      device_bytes -= allocs[i].second;
+      allocs[i] = allocs.back();
+      allocs.pop_back();
+      return;
+    }
 }
 
 int Snapshot::init_device(int dev) {
@@ -359,9 +370,11 @@ int Snapshot::build_hash_tables() {
   // (k_resolve's root probe)
   uint32_t* sig = nullptr;
   HIPC(hipMalloc(&sig, (size_t)ds.n_nodes * 4 + 4));
+  // direct tuples as checkDirect sees them: the check rows of a materialised snapshot, else the rows
+  const uint64_t* coff = ds.crow_off ? ds.crow_off : ds.row_off;
+  const uint32_t* csub = ds.crow_off ? ds.crow_subj : ds.row_subj;
   if (ds.n_nodes) {
-    hipLaunchKernelGGL(k_node_sig, dim3((ds.n_nodes + 255) / 256), dim3(256), 0, stream, ds.row_off, ds.row_subj,
-                       ds.n_nodes, sig);
+    hipLaunchKernelGGL(k_node_sig, dim3((ds.n_nodes + 255) / 256), dim3(256), 0, stream, coff, csub, ds.n_nodes, sig);
     HIPC(hipGetLastError());
   }
   if (n_set_edges) {
@@ -369,9 +382,9 @@ int Snapshot::build_hash_tables() {
     HIPC(hipGetLastError());
   }
   ds.adjx = adjx;
-  uint64_t n_rows = h_row_off_last;
+  const uint64_t n_rows = n_check_rows;
   // load <= 0.25 keys per slot: a miss (the common probe) reads one bucket with probability ~0.9
-  uint64_t buckets = pow2_at_least(std::max<uint64_t>(1, (n_rows * 4 + DSET_BUCKET - 1) / DSET_BUCKET));
+  const uint64_t buckets = std::max<uint64_t>(1, (n_rows * 4 + DSET_BUCKET - 1) / DSET_BUCKET);
   uint64_t* dset = nullptr;
   if (alloc((void**)&dset, buckets * DSET_BUCKET * 8)) return -1;
   HIPC(hipMemsetAsync(dset, 0xFF, buckets * DSET_BUCKET * 8, stream));
@@ -381,8 +394,7 @@ int Snapshot::build_hash_tables() {
   HIPC(hipMemsetAsync(nm, 0xFF, slots * sizeof(NSlot), stream));
   uint32_t grid = (ds.n_nodes + 255) / 256;
   if (ds.n_nodes) {
-    hipLaunchKernelGGL(k_dset_insert_rows, dim3(grid), dim3(256), 0, stream, dset, buckets - 1, ds.row_off,
-                       ds.row_subj, ds.n_nodes);
+    hipLaunchKernelGGL(k_dset_insert_rows, dim3(grid), dim3(256), 0, stream, dset, buckets, coff, csub, ds.n_nodes);
     HIPC(hipGetLastError());
     hipLaunchKernelGGL(k_nmap_insert, dim3(grid), dim3(256), 0, stream, nm, slots - 1, ds.nd_ns, ds.nd_obj,
                        ds.nd_rel, ds.adj_off, sig, ds.n_nodes);
@@ -391,7 +403,7 @@ int Snapshot::build_hash_tables() {
   HIPC(hipStreamSynchronize(stream));
   HIPC(hipFree(sig));
   ds.dset = dset;
-  ds.dset_mask = buckets - 1;
+  ds.dset_nb = buckets;
   ds.nmap = nm;
   ds.nmap_mask = slots - 1;
   ds.shard_rank = shard_rank;
@@ -413,7 +425,9 @@ int Snapshot::build_hash_tables() {
 // when row positions do not fit u32.
 int Snapshot::build_reverse() {
   const uint32_t nn = ds.n_nodes;
-  const uint64_t E = n_set_edges, R = h_row_off_last;
+  const uint64_t E = n_set_edges, R = n_check_rows;
+  const uint64_t* coff = ds.crow_off ? ds.crow_off : ds.row_off;
+  const uint32_t* csub = ds.crow_off ? ds.crow_subj : ds.row_subj;
   ds.radj = nullptr;
   ds.hbits = nullptr;
   ds.hbits_n = 0;
@@ -444,8 +458,8 @@ int Snapshot::build_reverse() {
   HIPC(hipMalloc(&k1, R * 4 + 4));
   HIPC(hipMalloc(&v0, R * 4 + 4));
   HIPC(hipMalloc(&v1, R * 4 + 4));
-  HIPC(hipMemcpyAsync(k0, ds.row_subj, R * 4, hipMemcpyDeviceToDevice, stream));
-  hipLaunchKernelGGL(k_row_nodes, dim3(grid), dim3(256), 0, stream, ds.row_off, nn, v0);
+  HIPC(hipMemcpyAsync(k0, csub, R * 4, hipMemcpyDeviceToDevice, stream));
+  hipLaunchKernelGGL(k_row_nodes, dim3(grid), dim3(256), 0, stream, coff, nn, v0);
   HIPC(hipGetLastError());
   hipcub::DoubleBuffer<uint32_t> kb(k0, k1), vb(v0, v1);
   tmp_bytes = 0;
@@ -727,6 +741,8 @@ int Snapshot::create_from_tuples(const kg_tuple* rows, size_t n, const kg_dict* 
     if (nn) HIPC(hipMemcpy(d_f, flags.data(), nn, hipMemcpyHostToDevice));
     ds.nflags = d_f;
   }
+  n_check_rows = h_row_off_last;
+  if (augment_rewrites()) return -1;
   return build_hash_tables();
 }
 
@@ -801,6 +817,8 @@ int Snapshot::create_synthetic(const kg_synth_params* p, const kg_rewrite_prog* 
     HIPC(hipFree(changed));
     ds.nflags = f;
   }
+  n_check_rows = h_row_off_last;
+  if (augment_rewrites()) return -1;
   return build_hash_tables();
 }
 

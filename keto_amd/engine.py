@@ -148,6 +148,13 @@ class Snapshot:
         _lib.check(_lib.load().kg_snapshot_info(self._h, _ptr(a)), "kg_snapshot_info")
         return {"nodes": int(a[0]), "rows": int(a[1]), "set_edges": int(a[2]), "device_bytes": int(a[3])}
 
+    def materialized(self) -> dict:
+        """Rewrite materialisation counts (kg_snapshot_materialized): union nodes, of them new ids,
+        check-row entries."""
+        a = np.zeros(3, np.uint64)
+        _lib.check(_lib.load().kg_snapshot_materialized(self._h, _ptr(a)), "kg_snapshot_materialized")
+        return {"union_nodes": int(a[0]), "new_nodes": int(a[1]), "check_rows": int(a[2])}
+
     def tune(self, key: str, value: int) -> None:
         """Engine knobs (kg_snapshot_tune): "tiers" = 0 grid / 1 LDS workgroup + grid / 2 workgroup tiers."""
         _lib.check(_lib.load().kg_snapshot_tune(self._h, key.encode(), int(value)), "kg_snapshot_tune")

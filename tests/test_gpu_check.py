@@ -266,9 +266,18 @@ from keto_amd.namespace import (ComputedSubjectSet, InvertResult, Namespace, Rel
                                 SubjectSetRewrite, TupleToSubjectSet)
 
 
-def random_program(rng, nss, rels):
-    """Random namespace configs: computed children only point to lower relation indexes (acyclic)."""
+def random_program(rng, nss, rels, unions_only=False):
+    """Random namespace configs: computed children only point to lower relation indexes (acyclic).
+    unions_only: `or` of computed / tuple-to-subject-set children (nested), the shape rewrite
+    materialisation (kg_augment.hip) turns into plain union nodes."""
     def child(level, own):
+        if unions_only:
+            k = rng.integers(3 if level < 2 else 2)
+            if k == 0 and own > 0:
+                return ComputedSubjectSet(rels[rng.integers(own)])
+            if k < 2:
+                return TupleToSubjectSet(rng.choice(rels), rng.choice(rels))
+            return SubjectSetRewrite([child(level + 1, own) for _ in range(rng.integers(1, 3))], "or")
         k = rng.integers(4 if level < 2 else 3)
         if k == 0 and own > 0:
             return ComputedSubjectSet(rels[rng.integers(own)])
@@ -286,20 +295,25 @@ def random_program(rng, nss, rels):
             rw = None
             if rng.random() < 0.5:
                 rw = SubjectSetRewrite([child(0, j) for _ in range(rng.integers(1, 3))],
-                                       "and" if rng.random() < 0.3 else "or")
+                                       "and" if rng.random() < 0.3 and not unions_only else "or")
             relations.append(Relation(r, rewrite=rw))
         out.append(Namespace(ns, relations))
     return out
 
 
+@pytest.mark.parametrize("mat", [1, 0])
+@pytest.mark.parametrize("unions", [False, True])
 @pytest.mark.parametrize("seed", range(8))
-def test_random_rewrites_vs_oracle(seed):
+def test_random_rewrites_vs_oracle(seed, unions, mat, monkeypatch):
+    """Random programs (all rewrite kinds, or unions only) on random graphs with undeclared
+    relations, with rewrite materialisation on (default) and off (KG_MATERIALIZE=0)."""
     from keto_amd.namespace import compile_program
-    rng = np.random.default_rng(100 + seed)
+    monkeypatch.setenv("KG_MATERIALIZE", str(mat))
+    rng = np.random.default_rng(100 + seed + (1000 if unions else 0))
     nss = ["a", "b", "c"]
     rels = ["r0", "r1", "r2", "r3"]
     it = Interner()
-    namespaces = random_program(rng, nss, rels)
+    namespaces = random_program(rng, nss, rels, unions_only=unions)
     prog = compile_program(namespaces, it)
     n_obj, n_users = 30 + 10 * seed, 25
     tuples = []
@@ -324,7 +338,11 @@ def test_random_rewrites_vs_oracle(seed):
         bad = np.nonzero((out != exp) | (err.astype(np.int64) != oerr))[0]
         assert bad.size == 0, [(str(qs[i]), int(depths[i]), int(out[i]), int(err[i]), int(exp[i]), int(oerr[i]))
                                for i in bad[:10]]
-        assert e.last_stats["n_general"] > 0
+    m = reg.snapshot.materialized()
+    if not mat:
+        assert m["union_nodes"] == 0
+    elif unions:
+        assert m["union_nodes"] > 0, m
 
 
 def test_relation_not_found_and_cycle():
@@ -342,14 +360,20 @@ def test_relation_not_found_and_cycle():
     assert r.err is not None and r.err.code == 1
 
 
-@pytest.mark.parametrize("n_tuples,gmax,cap2", [(150_000, 10, 0), (250_000, 5, 0), (150_000, 10, 32)])
-def test_synthetic_c3_rewrites_vs_oracle(n_tuples, gmax, cap2):
-    """Config C3: the Drive-like graph + folder forest + OPL view/edit/share (interpreter path).
-    cap2 = 32: the many-slot HBM pass holds 32 nodes per BFS, so what reaches it overflows into
-    the single full-size slot (pass 3)."""
+@pytest.mark.parametrize("n_tuples,gmax,cap2,mat", [(150_000, 10, 0, 1), (250_000, 5, 0, 1), (150_000, 10, 32, 1),
+                                                  (150_000, 10, 0, 0), (150_000, 10, 32, 0)])
+def test_synthetic_c3_rewrites_vs_oracle(n_tuples, gmax, cap2, mat, monkeypatch):
+    """Config C3: the Drive-like graph + folder forest + OPL view/edit/share.  Materialised
+    (default): view / edit are union nodes answered by the rewrite-free tiers, share = view &
+    !blocked goes through the interpreter, whose computed `view` is one BFS from the union node.
+    mat = 0: every query through the interpreter.  cap2 = 32: the many-slot HBM pass holds 32
+    nodes per BFS, so what reaches it overflows into the single full-size slot (pass 3)."""
     torch = _torch()
     from keto_amd import _lib
+    monkeypatch.setenv("KG_MATERIALIZE", str(mat))
     snap = Snapshot.synthetic(n_tuples, seed=20250131, preset=1)
+    m = snap.materialized()
+    assert (m["union_nodes"] > 0) == bool(mat), m
     snap.tune("interp_cap2", cap2)
     n = 6000
     dq = torch.empty((n, 7), dtype=torch.int32, device="cuda")
@@ -357,7 +381,10 @@ def test_synthetic_c3_rewrites_vs_oracle(n_tuples, gmax, cap2):
     e = Engine(snap, Config(gmax))
     q = dq.cpu().numpy().view(np.uint32)
     out, err = e.batch_check_ids(q, with_stats=True)
-    assert e.last_stats["n_general"] == n
+    if mat:  # share queries only (a third)
+        assert 0 < e.last_stats["n_general"] < n // 2, e.last_stats
+    else:
+        assert e.last_stats["n_general"] == n
     oracle = Oracle(snap.export(), 0, snap.program)
     exp, oerr, _ = oracle.check_batch(q[:, :6], q[:, 6].view(np.int32), gmax, POLICY_CANONICAL, nthreads=8)
     bad = np.nonzero((out != exp) | (err.astype(np.int64) != oerr))[0]
