@@ -374,6 +374,7 @@ def main():
         snap.tune("interp_wgs", a.interp_wgs)
     info = snap.info()
     t_build = time.time() - t_build
+    free_after_build = torch.cuda.mem_get_info(local)[0]
 
     B = a.batch
     P = max(1, a.inflight)
@@ -476,7 +477,9 @@ def main():
                                   a.global_depth),
                    "tuples": info["rows"], "nodes": info["nodes"], "set_edges": info["set_edges"],
                    "batch_per_gpu": B, "global_max_read_depth": a.global_depth, "parallelism": f"replica{world}",
-                   "inflight_per_gpu": P},
+                   "inflight_per_gpu": P, "device_gb": info["device_bytes"] / 1e9,
+                   "hbm_free_gb_after_build": free_after_build / 1e9,
+                   "materialized": snap.materialized()},
         "gteps": edges / elapsed / 1e9,
         "p99_batch_ms": float(np.percentile(np.array(lat) * 1e3, 99)),
         "batch_ms": {q: float(np.percentile(np.array(lat) * 1e3, v)) for q, v in

@@ -123,20 +123,20 @@ __global__ void k_aug_ids(DevSnap s, AugTables A, uint32_t nc, uint32_t n0, cons
 }
 
 // Node map over every node (keys only: the values are filled by build_hash_tables' rebuild).
-__global__ void k_aug_nmap(NSlot* nm, uint64_t mask, const uint32_t* nd_ns, const uint32_t* nd_obj, const uint32_t* nd_rel,
-                           uint32_t n) {
+__global__ void k_aug_nmap(NSlot* nm, uint64_t slots, const uint32_t* nd_ns, const uint32_t* nd_obj,
+                           const uint32_t* nd_rel, uint32_t n) {
   const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
   if (v >= n) return;
   const uint64_t key = nmap_key(nd_ns[v], nd_rel[v], nd_obj[v]);
-  uint64_t i = mix64(key) & mask;
-  for (uint64_t p = 0; p <= mask; p++) {
+  uint64_t i = hash_home(key, slots);
+  for (uint64_t p = 0; p < slots; p++) {
     const unsigned long long old =
         atomicCAS((unsigned long long*)&nm[i].key, (unsigned long long)EMPTY64, (unsigned long long)key);
     if (old == EMPTY64 || old == key) {
       nm[i].node = v;
       return;
     }
-    i = (i + 1) & mask;
+    i = hash_next(i, slots);
   }
 }
 
@@ -350,7 +350,9 @@ int Snapshot::augment_rewrites() {
   std::vector<uint8_t> virt;
   const char* env = getenv("KG_MATERIALIZE");
   if (env && env[0] == '0') materialize = 0;
-  if (!materialize || shard_n > 1 || !aug_build_plans(this, plans, virt) || ds.n_nodes == 0) return 0;
+  if (!materialize || shard_n > 1 || !aug_build_plans(this, plans, virt)) return 0;
+  h_virt = virt;  // the formula splitter's leaves may be union relations (kg_formula.hip)
+  if (ds.n_nodes == 0) return 0;
   const uint32_t n_ns = ds.n_ns, n_rel = ds.n_rel, n0 = ds.n_nodes;
   // contributions: (ns, rel) -> plans whose anchor order lists rel
   std::vector<std::vector<uint32_t>> contrib((size_t)n_ns * n_rel);
@@ -388,16 +390,15 @@ int Snapshot::augment_rewrites() {
   HIPC(hipMemcpy(d_virt, virt.data(), virt.size(), hipMemcpyHostToDevice));
   const AugTables A{d_plans, (uint32_t)plans.size(), d_coff, d_clist, d_virt};
   // the base snapshot needs a node map for the anchor lookups: a keys-only one over the base nodes
-  uint64_t slots0 = 16;
-  while (slots0 < (uint64_t)n0 * 2) slots0 <<= 1;
+  const uint64_t slots0 = std::max<uint64_t>(16, (uint64_t)n0 * 8 / 5);  // load 0.625
   NSlot* nm0;
   if (talloc((void**)&nm0, slots0 * sizeof(NSlot))) return -1;
   HIPC(hipMemsetAsync(nm0, 0xFF, slots0 * sizeof(NSlot), stream));
-  hipLaunchKernelGGL(k_aug_nmap, dim3((n0 + 255) / 256), dim3(256), 0, stream, nm0, slots0 - 1, ds.nd_ns, ds.nd_obj,
+  hipLaunchKernelGGL(k_aug_nmap, dim3((n0 + 255) / 256), dim3(256), 0, stream, nm0, slots0, ds.nd_ns, ds.nd_obj,
                      ds.nd_rel, n0);
   DevSnap b = ds;  // the base graph (its node map: nm0)
   b.nmap = nm0;
-  b.nmap_mask = slots0 - 1;
+  b.nmap_n = slots0;
   // 1. candidates
   HIPC(hipMemsetAsync(d_cnt, 0, 16, stream));
   hipLaunchKernelGGL((k_aug_cands<false>), dim3((n0 + 255) / 256), dim3(256), 0, stream, b, A, n0, d_cnt, nullptr,
@@ -414,6 +415,9 @@ int Snapshot::augment_rewrites() {
   hipLaunchKernelGGL((k_aug_cands<true>), dim3((n0 + 255) / 256), dim3(256), 0, stream, b, A, n0, d_cnt, c_plan, c_obj,
                      c_base);
   HIPC(hipGetLastError());
+  HIPC(hipStreamSynchronize(stream));
+  tmp.erase(std::find(tmp.begin(), tmp.end(), (void*)nm0));  // the base node map is done with
+  HIPC(hipFree(nm0));
   // 2. ids (new nodes after n0) and the node triples of the extended graph
   if ((uint64_t)n0 + nc >= 0x7FFFFFFFull) return set_error(KG_ERR_RESOURCE_CODE, "too many nodes after materialisation");
   const uint32_t nmax = n0 + nc;  // upper bound (replaced candidates take no new id)
@@ -434,17 +438,16 @@ int Snapshot::augment_rewrites() {
   HIPC(hipStreamSynchronize(stream));
   const uint32_t n1 = n0 + n_new;
   // node map over every node of the extended graph (keys + ids) for the successor lookups
-  uint64_t slots1 = 16;
-  while (slots1 < (uint64_t)n1 * 2) slots1 <<= 1;
+  const uint64_t slots1 = std::max<uint64_t>(16, (uint64_t)n1 * 8 / 5);
   NSlot* nm1;
   if (talloc((void**)&nm1, slots1 * sizeof(NSlot))) return -1;
   HIPC(hipMemsetAsync(nm1, 0xFF, slots1 * sizeof(NSlot), stream));
-  hipLaunchKernelGGL(k_aug_nmap, dim3((n1 + 255) / 256), dim3(256), 0, stream, nm1, slots1 - 1, nd_ns, nd_obj, nd_rel,
+  hipLaunchKernelGGL(k_aug_nmap, dim3((n1 + 255) / 256), dim3(256), 0, stream, nm1, slots1, nd_ns, nd_obj, nd_rel,
                      n1);
   DevSnap x = ds;  // the extended graph's ids and node map
   x.n_nodes = n1;
   x.nmap = nm1;
-  x.nmap_mask = slots1 - 1;
+  x.nmap_n = slots1;
   x.nd_ns = nd_ns;
   x.nd_obj = nd_obj;
   x.nd_rel = nd_rel;

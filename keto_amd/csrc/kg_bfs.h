@@ -21,11 +21,11 @@ __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 // Node-map lookup: the slot of (ns, rel, obj), or nullptr.  The first slot is passed in when the
 // caller already issued its load (k_resolve overlaps it with other lookups).
 __device__ __forceinline__ const NSlot* nmap_slot(const DevSnap& s, uint64_t key, uint64_t i) {
-  for (uint64_t p = 0; p <= s.nmap_mask; p++) {  // load <= 0.5: ends at an empty slot long before
+  for (uint64_t p = 0; p < s.nmap_n; p++) {  // load <= 0.625: ends at an empty slot long before
     const uint64_t k = s.nmap[i].key;
     if (k == key) return &s.nmap[i];
     if (k == EMPTY64) return nullptr;
-    i = (i + 1) & s.nmap_mask;
+    i = hash_next(i, s.nmap_n);
   }
   return nullptr;
 }
@@ -37,7 +37,7 @@ __device__ __forceinline__ bool nmap_key_ok(uint32_t ns, uint32_t rel, uint32_t 
 __device__ __forceinline__ uint32_t nmap_find(const DevSnap& s, uint32_t ns, uint32_t rel, uint32_t obj) {
   if (!nmap_key_ok(ns, rel, obj)) return NONE;
   const uint64_t key = nmap_key(ns, rel, obj);
-  const NSlot* sl = nmap_slot(s, key, mix64(key) & s.nmap_mask);
+  const NSlot* sl = nmap_slot(s, key, hash_home(key, s.nmap_n));
   return sl ? sl->node : NONE;
 }
 
@@ -46,12 +46,12 @@ __device__ __forceinline__ uint32_t nmap_find(const DevSnap& s, uint32_t ns, uin
 __device__ __forceinline__ bool dset_probe(const DevSnap& s, uint32_t node, uint32_t subj) {
   static_assert(DSET_BUCKET == 2, "one ulonglong2 per bucket");
   uint64_t key = dset_key(node, subj);
-  uint64_t b = dset_home(key, s.dset_nb);
+  uint64_t b = hash_home(key, s.dset_nb);
   for (uint64_t n = 0; n < s.dset_nb; n++) {
     const ulonglong2 a = *reinterpret_cast<const ulonglong2*>(s.dset + b * DSET_BUCKET);
     if (a.x == key || a.y == key) return true;
     if (a.y == EMPTY64) return false;  // buckets fill front to back
-    b = b + 1 == s.dset_nb ? 0 : b + 1;
+    b = hash_next(b, s.dset_nb);
   }
   return false;
 }

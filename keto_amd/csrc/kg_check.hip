@@ -96,11 +96,13 @@ __device__ void block_append(bool pred, uint32_t val, uint32_t* list, uint32_t* 
 
 // ------------------------------------------------------------------ k_resolve
 __global__ __launch_bounds__(256) void k_resolve(DevSnap s, const kg_query* __restrict__ q, uint32_t n,
+                                                 uint32_t n_base, const uint32_t* __restrict__ n_extra,
                                                  int32_t global, RQuery* __restrict__ rq, uint8_t* __restrict__ out,
                                                  uint32_t* __restrict__ err, uint32_t* light_list,
                                                  uint32_t* gen_list, int no_holder_filter, Ctl* ctl) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  bool valid = i < n;
+  // n: capacity (list strides); with a formula split the live count is n_base + *n_extra
+  bool valid = i < (n_extra ? n_base + *n_extra : n);
   uint32_t route = ROUTE_DONE;
   bool did_probe = false, no_holder = false;
   if (valid) {
@@ -109,7 +111,7 @@ __global__ __launch_bounds__(256) void k_resolve(DevSnap s, const kg_query* __re
     // so the common case is one round trip for both lookups
     const bool key_ok = nmap_key_ok(x.t.ns, x.t.rel, x.t.obj);
     const uint64_t key = nmap_key(x.t.ns, x.t.rel, x.t.obj);
-    const uint64_t ni = mix64(key) & s.nmap_mask;
+    const uint64_t ni = hash_home(key, s.nmap_n);
     const bool sid = x.t.sns == KG_SUBJECT_ID;
     uint32_t subj = sid ? (x.t.sobj < 0x7FFFFFFFu ? x.t.sobj : NONE) : NONE;
     const bool want_h = no_holder_filter && sid && subj != NONE;
@@ -125,7 +127,7 @@ __global__ __launch_bounds__(256) void k_resolve(DevSnap s, const kg_query* __re
     if (key_ok) n0 = s.nmap[ni];
     uint32_t node = NONE, rb = 0, rl = 0, rsig = 0xFFFFFFFFu;
     if (key_ok) {
-      const NSlot* sl = n0.key == key ? &n0 : (n0.key == EMPTY64 ? nullptr : nmap_slot(s, key, (ni + 1) & s.nmap_mask));
+      const NSlot* sl = n0.key == key ? &n0 : (n0.key == EMPTY64 ? nullptr : nmap_slot(s, key, hash_next(ni, s.nmap_n)));
       if (sl) {
         const NSlot v = *sl;
         node = v.node;
@@ -771,7 +773,7 @@ __device__ __forceinline__ uint32_t s2_meta(uint32_t len, uint32_t slot, uint32_
 // is walked by the lanes that need it under a wave-uniform branch.
 __device__ __forceinline__ bool dset_probe_fast(const DevSnap& s, bool want, uint32_t node, uint32_t subj) {
   const uint64_t key = dset_key(node, subj);
-  const uint64_t b = dset_home(key, s.dset_nb);
+  const uint64_t b = hash_home(key, s.dset_nb);
   bool hit = false, more = false;
   if (want) {
     const ulonglong2 a = *reinterpret_cast<const ulonglong2*>(s.dset + b * DSET_BUCKET);
@@ -1430,6 +1432,29 @@ int check_batch_begin(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n, 
   if (n > 0x7FFFFFFFull) return set_error(-2, "batch too large");
   HIPC(hipSetDevice(s->device));
   hipStream_t stream = w->stream;
+  // boolean rewrites over rewrite-free leaves (kg_formula.hip): the batch runs as the originals plus
+  // their leaf sub-checks; check_batch_end combines the leaves into the requested results
+  const uint32_t* n_extra = nullptr;
+  const size_t n_base = n;
+  if (s->n_fplans && n) {
+    const kg_query* q2;
+    size_t n2;
+    uint8_t* out2;
+    uint32_t* err2;
+    const uint2* ref;
+    if (int rc = formula_split(s, w, d_q, n, global_max_depth, &q2, &n2, &n_extra, &out2, &err2, &ref)) return rc;
+    bp->split = true;
+    bp->f_n = n;
+    bp->f_out = d_out;
+    bp->f_err = d_err;
+    bp->f_ref = ref;
+    d_q = q2;
+    n = n2;
+    d_out = out2;
+    d_err = err2;
+    bp->d_out = d_out;
+    bp->d_err = d_err;
+  }
   // scratch: rq[n] | light[8n] (8 shards) | light2[n] | gen[n] | medium[n] | heavy[n] | giant[n] | p2[n] |
   //          back2[n] | Ctl
   auto layout = [](size_t m, size_t* off) {  // rq | light[8m] | light2 | gen | medium | heavy | giant | p2 | back2 | Ctl
@@ -1500,7 +1525,7 @@ int check_batch_begin(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n, 
   if (n) {
     const bool use_back = s->back_tier && s->ds.radj;
     hipLaunchKernelGGL(k_resolve, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, stream, s->ds, d_q, (uint32_t)n,
-                       global_max_depth, rq, d_out, d_err, light, gen, use_back ? 1 : 0, ctl);
+                       (uint32_t)n_base, n_extra, global_max_depth, rq, d_out, d_err, light, gen, use_back ? 1 : 0, ctl);
     HIPC(hipGetLastError());
     uint32_t* const after_list = use_medium ? medium : heavy;
     uint32_t* const after_count = use_medium ? &ctl->medium_count : &ctl->heavy_count;
@@ -1616,6 +1641,8 @@ int check_batch_begin(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n, 
       HIPC(hipMemcpyAsync(&ctl->ic, &ic, sizeof ic, hipMemcpyHostToDevice, stream));
       if (launch_general(s, w, d_q, rq, gen, &ctl->gen_count, &ctl->ic, d_out, d_err, (uint32_t)n, stream)) return -1;
     }
+    // the requested results, stream-ordered before anything the caller enqueues after this call
+    if (bp->split && formula_combine(s, w, bp->f_n, bp->f_ref, d_out, d_err, bp->f_out, bp->f_err)) return -1;
   }
   // one synchronisation per batch: the grid round's readback and the counters come back together
   static_assert(sizeof(Ctl) <= 32768, "Ctl readback fits the lower half of the pinned buffer");
@@ -1646,6 +1673,10 @@ int check_batch_end(Snapshot* s, Workspace* w, BatchPending* bp, bool* reran) {
     if (int rc = grid_tier(s, w, bp->rq, bp->grid_list, bp->grid_count, bp->gdepth, bp->d_out, bp->d_err, stream, &gs, 2))
       return rc;
     if (reran) *reran = w->grid_reran;
+    // the rerun rewrote leaf results after check_batch_begin's combine: combine again
+    if (bp->split && w->grid_reran &&
+        formula_combine(s, w, bp->f_n, bp->f_ref, bp->d_out, bp->d_err, bp->f_out, bp->f_err))
+      return -1;
   }
   if (stats) {
     float ms = 0, lms = 0;

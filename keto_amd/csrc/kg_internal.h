@@ -57,11 +57,13 @@ __host__ __device__ __forceinline__ uint64_t nmap_key(uint32_t ns, uint32_t rel,
 __host__ __device__ __forceinline__ uint64_t dset_key(uint32_t node, uint32_t subj) {
   return ((uint64_t)node << 32) | subj;
 }
-// Home bucket of a dset key: multiply-shift range reduction over any bucket count, so the table is
-// sized for its load exactly instead of rounding up to a power of two (up to 2x the HBM).
-__host__ __device__ __forceinline__ uint64_t dset_home(uint64_t key, uint64_t nb) {
-  return (uint64_t)(((unsigned __int128)mix64(key) * nb) >> 64);
+// Home slot of a key in an open-addressing table of n slots (dset buckets, node map): multiply-shift
+// range reduction over any n, so a table is sized for its load exactly instead of rounding up to a
+// power of two (up to 2x the HBM).  Linear probing wraps with hash_next.
+__host__ __device__ __forceinline__ uint64_t hash_home(uint64_t key, uint64_t n) {
+  return (uint64_t)(((unsigned __int128)mix64(key) * n) >> 64);
 }
+__host__ __device__ __forceinline__ uint64_t hash_next(uint64_t i, uint64_t n) { return i + 1 == n ? 0 : i + 1; }
 
 // Shard of a node in the hash-sharded mode: all relations of one object live on
 // one rank, owner = hash(ns, obj) mod nranks.
@@ -121,7 +123,7 @@ struct DevSnap {
   const uint64_t* dset;
   uint64_t dset_nb;  // buckets (DSET_BUCKET keys each); probes wrap at dset_nb
   const NSlot* nmap;
-  uint64_t nmap_mask;  // n_slots - 1
+  uint64_t nmap_n;  // slots
   const uint8_t* nflags;  // nullptr: every node pure
   const uint32_t* nd_ns;
   const uint32_t* nd_obj;

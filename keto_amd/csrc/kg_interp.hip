@@ -600,9 +600,10 @@ int launch_general(Snapshot* s, Workspace* w, const kg_query* d_q, const RQuery*
   uint64_t tsize = 64;
   while (tsize < 2 * cap2 + 128) tsize <<= 1;
   const uint64_t per2 = slot_bytes + (tsize + cap2) * 4;
-  // pass-2 budget: 16 GiB, or an eighth of the free HBM when less (other streams' workspaces and
-  // the snapshot share the device); a pool that already exists keeps its layout
-  uint64_t budget2 = 16ull << 30;
+  // pass-2 budget: 4 GiB (~800 slots of 256 Ki nodes; what reaches pass 2 is the LDS pass's
+  // overflow, a small fraction of a batch), or an eighth of the free HBM when less (other streams'
+  // workspaces and the snapshot share the device); a pool that already exists keeps its layout
+  uint64_t budget2 = 4ull << 30;
   if (w->interp_layout == 0) {
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) budget2 = std::min<uint64_t>(budget2, free_b / 8);

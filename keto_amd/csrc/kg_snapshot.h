@@ -52,6 +52,8 @@ struct Workspace {
   size_t heavy_pool_bytes = 0;
   GridPool grid;  // grid tier, sized for the queries that reach it (16 Mi log entries)
   bool grid_reran = false;  // the last batch's grid tier ran rounds after the first (results rewritten)
+  void* split = nullptr;  // formula split (kg_formula.hip): leaf queries, their results, per-query plan refs
+  size_t split_bytes = 0;
   void* interp_pool = nullptr;
   size_t interp_pool_bytes = 0;
   uint64_t interp_layout = 0;  // (pass-2 slots, pass-1 slots, list cap) the pool was last laid out for
@@ -71,6 +73,13 @@ struct BatchPending {
   const RQuery* rq = nullptr;
   int32_t gdepth = 5;
   size_t n = 0;
+  // formula split: the batch ran as the originals + leaf sub-checks into split buffers; the
+  // requested results are combined into f_out / f_err at the end
+  bool split = false;
+  size_t f_n = 0;
+  uint8_t* f_out = nullptr;
+  uint32_t* f_err = nullptr;
+  const uint2* f_ref = nullptr;
   void* ctl_host = nullptr;
   GridStats gs;
 };
@@ -109,6 +118,11 @@ struct Snapshot {
   uint64_t n_check_rows = 0;  // entries of the check rows (crow; == h_row_off_last without materialisation)
   uint64_t n_virtual = 0, n_virtual_new = 0;  // materialised rewrite nodes (kg_augment.hip), of them new ids
   int materialize = 1;  // rewrite materialisation at build (KG_MATERIALIZE=0 turns it off)
+  std::vector<uint8_t> h_virt;  // [n_ns * n_rel] materialised union relations (kg_augment.hip)
+  // boolean rewrites over union / plain relations (kg_formula.hip): per (ns, rel) plan index or -1
+  int32_t* d_fidx = nullptr;
+  void* d_fplans = nullptr;
+  uint32_t n_fplans = 0, fp_leaves = 0;  // plans, most leaves of one plan
   std::vector<std::pair<void*, size_t>> allocs;
   // host mirrors (host-tuple path)
   std::vector<uint32_t> h_nd_ns, h_nd_obj, h_nd_rel, h_row_subj;
@@ -160,6 +174,7 @@ struct Snapshot {
   int create_synthetic(const kg_synth_params* p, const kg_rewrite_prog* prog);
   int upload_program(const kg_dict* dict, const kg_rewrite_prog* prog);
   int augment_rewrites();  // kg_augment.hip: monotone rewrites -> plain union nodes
+  int build_formulas();    // kg_formula.hip: boolean rewrites -> leaf sub-checks
   int build_hash_tables();
   int build_reverse();
   uint8_t host_relflag(uint32_t ns, uint32_t rel) const;
@@ -173,6 +188,11 @@ int check_batch_begin(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n, 
                       uint8_t* d_out, uint32_t* d_err, kg_stats* stats, BatchPending* bp);
 int check_batch_end(Snapshot* s, Workspace* w, BatchPending* bp, bool* reran);
 int synth_queries(Snapshot* s, uint64_t seed, size_t n, kg_query* d_q);
+// kg_formula.hip: split a batch's decomposable queries into leaf checks / combine their results
+int formula_split(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n, int32_t gdepth, const kg_query** q2,
+                  size_t* n2, const uint32_t** n_extra, uint8_t** out2, uint32_t** err2, const uint2** ref);
+int formula_combine(Snapshot* s, Workspace* w, size_t n, const uint2* ref, const uint8_t* out2, const uint32_t* err2,
+                    uint8_t* d_out, uint32_t* d_err);
 // kg_shard.hip
 int shard_seed(Snapshot* s, const kg_query* d_q, size_t n, int32_t gdepth, kg_frec* d_out, size_t cap,
                uint32_t* d_counts, uint8_t* d_res, uint32_t* d_err, hipStream_t stream);

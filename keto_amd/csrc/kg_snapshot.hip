@@ -27,7 +27,7 @@ __global__ void k_dset_insert_rows(uint64_t* dset, uint64_t nb, const uint64_t* 
   if (v >= n_nodes) return;
   for (uint64_t i = row_off[v]; i < row_off[v + 1]; i++) {
     uint64_t key = dset_key(v, row_subj[i]);
-    uint64_t b = dset_home(key, nb);
+    uint64_t b = hash_home(key, nb);
     for (uint64_t n = 0; n < nb; n++) {  // sized for load <= 0.25: always finds room
       uint64_t* bucket = dset + b * DSET_BUCKET;
       bool done = false;
@@ -40,19 +40,19 @@ __global__ void k_dset_insert_rows(uint64_t* dset, uint64_t nb, const uint64_t* 
         }
       }
       if (done) break;
-      b = b + 1 == nb ? 0 : b + 1;
+      b = hash_next(b, nb);
     }
   }
 }
 
-__global__ void k_nmap_insert(NSlot* nm, uint64_t mask, const uint32_t* nd_ns, const uint32_t* nd_obj,
+__global__ void k_nmap_insert(NSlot* nm, uint64_t slots, const uint32_t* nd_ns, const uint32_t* nd_obj,
                               const uint32_t* nd_rel, const uint64_t* adj_off, const uint32_t* sig,
                               uint32_t n_nodes) {
   uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
   if (v >= n_nodes) return;
   uint64_t key = nmap_key(nd_ns[v], nd_rel[v], nd_obj[v]);
-  uint64_t i = mix64(key) & mask;
-  for (uint64_t n = 0; n <= mask; n++) {  // sized for load <= 0.5: always finds room
+  uint64_t i = hash_home(key, slots);
+  for (uint64_t n = 0; n < slots; n++) {  // sized for load <= 0.625: always finds room
     unsigned long long old =
         atomicCAS((unsigned long long*)&nm[i].key, (unsigned long long)EMPTY64, (unsigned long long)key);
     if (old == EMPTY64 || old == key) {
@@ -62,7 +62,7 @@ __global__ void k_nmap_insert(NSlot* nm, uint64_t mask, const uint32_t* nd_ns, c
       nm[i].sig = sig[v];
       return;
     }
-    i = (i + 1) & mask;
+    i = hash_next(i, slots);
   }
 }
 
@@ -245,6 +245,7 @@ Workspace::~Workspace() {
   if (heavy_pool) hipFree(heavy_pool);
   grid.release();
   if (interp_pool) hipFree(interp_pool);
+  if (split) hipFree(split);
   if (pinned) hipHostFree(pinned);
   for (auto& e : ev)
     if (e) hipEventDestroy(e);
@@ -383,12 +384,19 @@ int Snapshot::build_hash_tables() {
   }
   ds.adjx = adjx;
   const uint64_t n_rows = n_check_rows;
-  // load <= 0.25 keys per slot: a miss (the common probe) reads one bucket with probability ~0.9
-  const uint64_t buckets = std::max<uint64_t>(1, (n_rows * 4 + DSET_BUCKET - 1) / DSET_BUCKET);
+  // load <= 0.25 keys per slot: a miss (the common probe) reads one bucket with probability ~0.9.
+  // A table that would take more than a fifth of the device's HBM runs at 0.375 instead (and the
+  // node map at 0.625 past an eighth), so the largest graphs leave room for batches in flight.
+  size_t hbm_free = 0, hbm_total = 0;
+  if (hipMemGetInfo(&hbm_free, &hbm_total) != hipSuccess) hbm_total = 288ull << 30;
+  (void)hipGetLastError();
+  uint64_t buckets = std::max<uint64_t>(1, (n_rows * 4 + DSET_BUCKET - 1) / DSET_BUCKET);
+  if (buckets * DSET_BUCKET * 8 > hbm_total / 5) buckets = std::max<uint64_t>(1, (n_rows * 8 + 2) / 3 / DSET_BUCKET);
   uint64_t* dset = nullptr;
   if (alloc((void**)&dset, buckets * DSET_BUCKET * 8)) return -1;
   HIPC(hipMemsetAsync(dset, 0xFF, buckets * DSET_BUCKET * 8, stream));
-  uint64_t slots = pow2_at_least(std::max<uint64_t>(16, (uint64_t)ds.n_nodes * 2));
+  uint64_t slots = std::max<uint64_t>(16, (uint64_t)ds.n_nodes * 2);
+  if (slots * sizeof(NSlot) > hbm_total / 8) slots = std::max<uint64_t>(16, (uint64_t)ds.n_nodes * 8 / 5);
   NSlot* nm = nullptr;
   if (alloc((void**)&nm, slots * sizeof(NSlot))) return -1;
   HIPC(hipMemsetAsync(nm, 0xFF, slots * sizeof(NSlot), stream));
@@ -396,7 +404,7 @@ int Snapshot::build_hash_tables() {
   if (ds.n_nodes) {
     hipLaunchKernelGGL(k_dset_insert_rows, dim3(grid), dim3(256), 0, stream, dset, buckets, coff, csub, ds.n_nodes);
     HIPC(hipGetLastError());
-    hipLaunchKernelGGL(k_nmap_insert, dim3(grid), dim3(256), 0, stream, nm, slots - 1, ds.nd_ns, ds.nd_obj,
+    hipLaunchKernelGGL(k_nmap_insert, dim3(grid), dim3(256), 0, stream, nm, slots, ds.nd_ns, ds.nd_obj,
                        ds.nd_rel, ds.adj_off, sig, ds.n_nodes);
     HIPC(hipGetLastError());
   }
@@ -405,7 +413,7 @@ int Snapshot::build_hash_tables() {
   ds.dset = dset;
   ds.dset_nb = buckets;
   ds.nmap = nm;
-  ds.nmap_mask = slots - 1;
+  ds.nmap_n = slots;
   ds.shard_rank = shard_rank;
   ds.shard_n = shard_n;
   ds.nowner = nullptr;
@@ -742,7 +750,7 @@ int Snapshot::create_from_tuples(const kg_tuple* rows, size_t n, const kg_dict* 
     ds.nflags = d_f;
   }
   n_check_rows = h_row_off_last;
-  if (augment_rewrites()) return -1;
+  if (augment_rewrites() || build_formulas()) return -1;
   return build_hash_tables();
 }
 
@@ -818,7 +826,7 @@ int Snapshot::create_synthetic(const kg_synth_params* p, const kg_rewrite_prog* 
     ds.nflags = f;
   }
   n_check_rows = h_row_off_last;
-  if (augment_rewrites()) return -1;
+  if (augment_rewrites() || build_formulas()) return -1;
   return build_hash_tables();
 }
 

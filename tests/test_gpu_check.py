@@ -381,8 +381,8 @@ def test_synthetic_c3_rewrites_vs_oracle(n_tuples, gmax, cap2, mat, monkeypatch)
     e = Engine(snap, Config(gmax))
     q = dq.cpu().numpy().view(np.uint32)
     out, err = e.batch_check_ids(q, with_stats=True)
-    if mat:  # share queries only (a third)
-        assert 0 < e.last_stats["n_general"] < n // 2, e.last_stats
+    if mat:  # view / edit are union nodes, share = view & !blocked splits into two leaf checks
+        assert e.last_stats["n_general"] < n // 20, e.last_stats
     else:
         assert e.last_stats["n_general"] == n
     oracle = Oracle(snap.export(), 0, snap.program)
@@ -392,6 +392,69 @@ def test_synthetic_c3_rewrites_vs_oracle(n_tuples, gmax, cap2, mat, monkeypatch)
     assert 0.05 < (out == 1).mean() < 0.95 and (out == 2).sum() == 0
     dfs, _, _ = oracle.check_batch(q[:, :6], q[:, 6].view(np.int32), gmax, POLICY_DFS, nthreads=8)
     assert (dfs == exp).all()  # rewrites sit outside every visited scope: schedule-invariant
+
+
+@pytest.mark.parametrize("mat", [1, 0])
+@pytest.mark.parametrize("seed", range(4))
+def test_formula_rewrites_vs_oracle(seed, mat, monkeypatch):
+    """Boolean rewrites over union / plain relations (kg_formula.hip): and / or / not over computed
+    leaves split into leaf checks run by the rewrite-free tiers; formulas with a tuple-to-subject-set
+    leaf, a non-union rewrite leaf or an undeclared leaf, objects whose own node holds rows, and a
+    union that reaches an undeclared relation stay with the interpreter.  Bit-exact with the oracle,
+    materialisation on and off."""
+    from keto_amd.namespace import compile_program
+    monkeypatch.setenv("KG_MATERIALIZE", str(mat))
+    rng = np.random.default_rng(500 + seed)
+    C, T, N, O = ComputedSubjectSet, TupleToSubjectSet, InvertResult, SubjectSetRewrite
+    rels = [Relation("a"), Relation("b"), Relation("blocked"), Relation("parent"),
+            Relation("u1", rewrite=O([C("a"), T("parent", "u1")])),
+            Relation("u2", rewrite=O([C("b"), C("u1")])),
+            Relation("f1", rewrite=O([C("u1"), N(C("blocked"))], "and")),
+            Relation("f2", rewrite=O([O([C("u2"), N(C("a"))], "and"), C("blocked")])),
+            Relation("f3", rewrite=O([N(C("u1"))])),
+            Relation("f4", rewrite=O([C("u1"), T("parent", "f1")], "and")),
+            Relation("f5", rewrite=O([C("a"), C("f1")], "and")),
+            Relation("f6", rewrite=O([C("u2"), C("und")], "and")),
+            Relation("f7", rewrite=O([N(O([C("a"), C("b")], "and")), N(C("u2"))], "and")),
+            Relation("u3", rewrite=O([C("a"), T("parent", "zz")]))]
+    namespaces = [Namespace("d", rels)]
+    it = Interner()
+    prog = compile_program(namespaces, it)
+    n_obj, n_users = 40 + 20 * seed, 20
+    tuples = []
+    for _ in range(400 + 150 * seed):
+        x = f"d:o{rng.integers(n_obj)}"
+        k = rng.integers(10)
+        if k < 3:
+            tuples.append(f"{x}#parent@(d:o{rng.integers(n_obj)}#...)")
+        elif k < 8:
+            r = ["a", "b", "blocked", "a", "b"][k - 3]
+            subj = f"u{rng.integers(n_users)}" if rng.random() < 0.7 else f"(d:o{rng.integers(n_obj)}#u2)"
+            tuples.append(f"{x}#{r}@{subj}")
+        elif k == 8:
+            tuples.append(f"{x}#f1@u{rng.integers(n_users)}")  # own rows: not split
+        else:
+            tuples.append(f"{x}#parent@(d:o{rng.integers(n_obj)}#...)")
+    tuples = [RelationTuple.from_string(t) for t in tuples]
+    reg = Registry(tuples, namespaces, interner=it)
+    qrels = ["a", "u1", "u2", "u3", "f1", "f2", "f3", "f4", "f5", "f6", "f7"]
+    qs = [RelationTuple.from_string(f"d:o{rng.integers(n_obj)}#{rng.choice(qrels)}@u{rng.integers(n_users + 2)}")
+          for _ in range(3000)]
+    q6 = np.asarray([it.tuple_ids(t) for t in qs], np.uint32)
+    depths = rng.integers(-1, 7, len(qs))
+    oracle = Oracle(it.tuples_array(tuples), it.wildcard_rel, prog)
+    general = []
+    for gmax in (1, 2, 3, 5, 7):
+        e = Engine(reg.snapshot, Config(gmax))
+        out, err = e.batch_check_ids(queries_array(q6, depths), with_stats=True)
+        exp, oerr, _ = oracle.check_batch(q6, depths, gmax, POLICY_CANONICAL)
+        bad = np.nonzero((out != exp) | (err.astype(np.int64) != oerr))[0]
+        assert bad.size == 0, [(str(qs[i]), int(depths[i]), int(out[i]), int(err[i]), int(exp[i]), int(oerr[i]))
+                               for i in bad[:10]]
+        general.append(e.last_stats["n_general"])
+        assert 0.05 < (out == 1).mean() < 0.95
+    if mat:  # f1 / f2 / f3 / f7 queries on objects without own rows split (and u1 / u2 are union nodes)
+        assert max(general) < 0.75 * len(qs), general
 
 
 @pytest.mark.parametrize("cap2", [0, 32, 700])
