@@ -456,7 +456,7 @@ def main():
     l_bytes = np.array([8 * s.light_rows_opened + 4 * s.light_edges_read + 16 * s.light_probes for s in stats], float)
     l_ms = np.array([s.light_ms for s in stats], float)
     achieved = float(l_bytes.mean() / (l_ms.mean() * 1e-3) / 1e9)
-    traffic = pmc_traffic(int(a.tuples), B)
+    traffic = pmc_traffic(STREAM_KERNELS[a.stream], int(a.tuples), B, a.preset, P)
 
     value = world * B * a.steps / elapsed
     out = {
@@ -518,14 +518,16 @@ def stream_diag(s) -> dict:
             "mean_wave_us": s.light_wave_ticks / waves / 100.0 if waves else 0.0}
 
 
-def pmc_traffic(tuples: int, batch: int):
-    """HBM bytes per k_stream launch from the committed rocprofv3 --pmc pass (profiles/), if one
-    was taken on this exact workload; else None."""
-    p = os.path.join(ROOT, "profiles", "pmc_k_stream.json")
+def pmc_traffic(kernel: str, tuples: int, batch: int, preset: int, inflight: int):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc passes
+    (profiles/pmc_<kernel>_p<preset>.json, scripts/gpu_profile.sh), if taken on this exact workload;
+    else None."""
+    p = os.path.join(ROOT, "profiles", f"pmc_{kernel.split('<')[0]}_p{preset}.json")
     try:
         with open(p) as f:
             d = json.load(f)
-        if int(d.get("tuples", -1)) == tuples and int(d.get("batch", -1)) == batch:
+        if (int(d.get("tuples", -1)) == tuples and int(d.get("batch", -1)) == batch
+                and int(d.get("inflight", -1)) == inflight):
             return d.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         pass

@@ -38,6 +38,9 @@ struct FPlan {
   uint32_t n_ops, n_leaves;
   uint32_t leaf[FP_LEAVES];  // computed relations (same object)
   uint8_t ops[FP_OPS];
+  // from the snapshot's nodes at build: some (ns, obj, R) node holds rows (its own part must be
+  // looked up per query); bit j: some node of leaf relation j is impure (leaf j looked up per query)
+  uint32_t own_rows, leaf_impure;
 };
 
 // ------------------------------------------------------------------ device
@@ -58,12 +61,15 @@ __global__ __launch_bounds__(256) void k_fsplit(DevSnap s, const int32_t* __rest
       if (p >= 0) {
         const FPlan& P = plans[p];
         bool ok = true;
-        const uint32_t own = nmap_find(s, ns, rel, obj);
-        if (own != NONE) {  // its own rows would join the answer: not split
-          const uint64_t* co = s.crow_off ? s.crow_off : s.row_off;
-          ok = co[own + 1] == co[own] && s.adj_off[own + 1] == s.adj_off[own];
+        if (P.own_rows) {
+          const uint32_t own = nmap_find(s, ns, rel, obj);
+          if (own != NONE) {  // its own rows would join the answer: not split
+            const uint64_t* co = s.crow_off ? s.crow_off : s.row_off;
+            ok = co[own + 1] == co[own] && s.adj_off[own + 1] == s.adj_off[own];
+          }
         }
         for (uint32_t j = 0; j < P.n_leaves && ok; j++) {
+          if (!((P.leaf_impure >> j) & 1)) continue;  // every node of this relation is pure
           ln[j] = nmap_find(s, ns, P.leaf[j], obj);
           if (ln[j] != NONE && s.nflags && (s.nflags[ln[j]] & NF_IMPURE)) ok = false;
         }
@@ -141,6 +147,19 @@ __global__ __launch_bounds__(256) void k_fcombine(const FPlan* __restrict__ plan
   }
   out[i] = (e == KG_ERR_NONE && (st & 1u)) ? KG_IS_MEMBER : KG_NOT_MEMBER;
   if (err) err[i] = e;
+}
+
+// Per (ns, rel): bit0 some node holds rows (check rows or set-adjacency), bit1 some node is impure.
+__global__ void k_relstats(DevSnap s, uint32_t* rs) {
+  const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= s.n_nodes) return;
+  const uint32_t ns = s.nd_ns[v], rel = s.nd_rel[v];
+  if (ns >= s.n_ns || rel >= s.n_rel) return;
+  const uint64_t* co = s.crow_off ? s.crow_off : s.row_off;
+  const uint32_t f = ((co[v + 1] != co[v] || s.adj_off[v + 1] != s.adj_off[v]) ? 1u : 0u) |
+                     ((s.nflags && (s.nflags[v] & NF_IMPURE)) ? 2u : 0u);
+  uint32_t* p = rs + (size_t)ns * s.n_rel + rel;
+  if (f & ~*p) atomicOr(p, f);  // read first: most nodes find their bits already set
 }
 
 // ------------------------------------------------------------------ host
@@ -223,6 +242,27 @@ int Snapshot::build_formulas() {
       fp_leaves = std::max(fp_leaves, P.n_leaves);
     }
   if (plans.empty()) return 0;
+  // which plans need per-query lookups (own rows, impure leaf nodes)
+  std::vector<uint32_t> rs(idx.size(), 0);
+  if (ds.n_nodes) {
+    uint32_t* d_rs = nullptr;
+    HIPC(hipMalloc(&d_rs, rs.size() * 4 + 4));
+    HIPC(hipMemsetAsync(d_rs, 0, rs.size() * 4, stream));
+    hipLaunchKernelGGL(k_relstats, dim3((ds.n_nodes + 255) / 256), dim3(256), 0, stream, ds, d_rs);
+    HIPC(hipGetLastError());
+    HIPC(hipMemcpyAsync(rs.data(), d_rs, rs.size() * 4, hipMemcpyDeviceToHost, stream));
+    HIPC(hipStreamSynchronize(stream));
+    HIPC(hipFree(d_rs));
+  }
+  for (uint32_t ns = 0; ns < n_ns; ns++)
+    for (uint32_t R = 0; R < n_rel; R++) {
+      const int32_t p = idx[(size_t)ns * n_rel + R];
+      if (p < 0) continue;
+      FPlan& P = plans[(size_t)p];
+      P.own_rows = rs[(size_t)ns * n_rel + R] & 1u;
+      for (uint32_t j = 0; j < P.n_leaves; j++)
+        if (rs[(size_t)ns * n_rel + P.leaf[j]] & 2u) P.leaf_impure |= 1u << j;
+    }
   if (alloc((void**)&d_fidx, idx.size() * 4) || alloc(&d_fplans, plans.size() * sizeof(FPlan))) return -1;
   HIPC(hipMemcpy(d_fidx, idx.data(), idx.size() * 4, hipMemcpyHostToDevice));
   HIPC(hipMemcpy(d_fplans, plans.data(), plans.size() * sizeof(FPlan), hipMemcpyHostToDevice));

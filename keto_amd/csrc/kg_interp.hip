@@ -469,6 +469,7 @@ __global__ __launch_bounds__(256) void k_interp_lds(DevSnap s, const kg_query* _
   Frame* stack = stacks + (size_t)slot * STACK_CAP;
   MemoEnt* memo = memos + (size_t)slot * MEMO_CAP;
   const uint32_t count = *ic->gen_count;
+  if (count == 0) return;  // nothing routed here (e.g. every rewrite materialised or split)
   uint32_t head_sel = blockIdx.x & 7;
   const uint32_t head0 = head_sel;
   BfsStats bs;

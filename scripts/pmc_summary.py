@@ -7,8 +7,8 @@ FETCH_SIZE tallies 128-byte memory-side read requests at 64 bytes.  Our reads ar
 gathers, a width the guide leaves uncalibrated; the same correction is applied and the raw values
 are kept next to the corrected figure.
 
-usage: python scripts/pmc_summary.py --kernel k_light --fetch DIR1 --write DIR2 --tuples T --batch B
-       [--out profiles/pmc_k_light.json]
+usage: python scripts/pmc_summary.py --kernel k_stream2 --fetch DIR1 --write DIR2 --tuples T --batch B
+       [--preset P --inflight I] [--out profiles/pmc_k_stream2_p0.json]
 """
 import argparse
 import csv
@@ -37,6 +37,8 @@ def main():
     ap.add_argument("--write", required=True)
     ap.add_argument("--tuples", type=float, required=True)
     ap.add_argument("--batch", type=int, required=True)
+    ap.add_argument("--preset", type=int, default=0)
+    ap.add_argument("--inflight", type=int, default=4)
     ap.add_argument("--skip", type=int, default=1, help="leading (warmup) dispatches to drop")
     ap.add_argument("--out")
     a = ap.parse_args()
@@ -47,14 +49,15 @@ def main():
     f_kib = sum(fetch) / len(fetch)
     w_kib = sum(write) / len(write)
     out = {
-        "kernel": a.kernel, "tuples": int(a.tuples), "batch": a.batch,
+        "kernel": a.kernel, "tuples": int(a.tuples), "batch": a.batch, "preset": a.preset,
+        "inflight": a.inflight,
         "dispatches": {"fetch": len(fetch), "write": len(write)},
         "fetch_size_kib_raw": f_kib, "write_size_kib_raw": w_kib,
         "hbm_bytes_per_launch": (2 * f_kib + w_kib) * 1024.0,
         "correction": "2 x FETCH_SIZE + WRITE_SIZE (MI355X_MICROARCH.md HBM section, gfx950)",
     }
     path = a.out or os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles",
-                                 f"pmc_{a.kernel}.json")
+                                 f"pmc_{a.kernel}_p{a.preset}.json")
     with open(path, "w") as fh:
         json.dump(out, fh, indent=1)
     print(json.dumps(out))
