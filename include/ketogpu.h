@@ -157,7 +157,8 @@ typedef struct {
 
 /* ---- snapshot --------------------------------------------------------------------------- */
 /* device_mask: bit d set = a replica of the snapshot on device d (0 = device 0 only).  Every
- * replica holds the whole snapshot (1 B tuples take ~33 GB of a 288 GB MI355X); kg_check_batch and
+ * replica holds the whole snapshot (1 B synthetic tuples take 69 GB of a 288 GB MI355X rewrite-free,
+ * 194 GB with C3's materialised rewrites); kg_check_batch and
  * kg_expand_batch split their host-buffer batches over the replicas inside the call, which is how
  * one `keto serve` process (one check.Engine, internal/driver/registry_default.go:180-185) uses
  * every GPU of the node.  Replicas are built concurrently. */
@@ -194,9 +195,9 @@ int kg_snapshot_materialized(const kg_snapshot* s, uint64_t* out3);
  * depend on any of them.  key "back": 1 = the backward tier (reverse search from the subject's
  * holders, one wave per query, then one workgroup per query) takes the wave tiers' overflow before the grid tier, and
  * k_resolve answers queries whose subject no row holds; 2 = the same with the wave width only
- * (its overflow goes straight to the grid tier; default); 0 = off.  key "stream": k_stream variant
- * 0..8 (see kg_check.hip; default 7 = 32 query slots per wave sharing one visited table, <= 64
- * expanded nodes per query).
+ * (its overflow goes straight to the grid tier; default); 0 = off.  key "stream": stream-tier
+ * kernel -- 9 = k_stream2 (default: 32 query slots per wave over one FIFO, direct-mapped visited
+ * cache), 0..8 = the round-1 k_stream variants (see kg_check.hip).
  * key "stream_wgs": k_stream workgroups per CU (0 = by variant); "back_wgs" (1..3) and "grid_wgs"
  * (1..64): k_back / k_grid_level workgroups per CU.  key "shard_vis": log2 of the
  * hash-sharded mode's per-batch (query, node) visited table (default 25).  key "interp_cap2"
