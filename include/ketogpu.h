@@ -298,7 +298,20 @@ int kg_snapshot_synthetic_shard(const kg_synth_params* params, const kg_rewrite_
 int kg_shard_seed(kg_snapshot* s, const kg_query* d_q, size_t n, int32_t global_max_depth, kg_frec* d_out,
                   size_t cap, uint32_t* d_counts, uint8_t* d_res, uint32_t* d_err, void* stream);
 int kg_shard_level(kg_snapshot* s, const kg_frec* d_in, size_t n_in, const uint32_t* d_n_in, kg_frec* d_out,
-                   size_t cap, uint32_t* d_counts, uint8_t* d_res, uint32_t* d_err, void* stream);
+                   size_t cap, uint32_t* d_counts, uint8_t* d_res, uint32_t* d_err, const uint32_t* d_done,
+                   uint32_t done_words, void* stream);
+/* Early exit across ranks: d_done (may be NULL) is the done bitmap of the batch, done_words words per
+ * home rank ([rank][word], bit i = query i of that rank answered IsMember by the previous levels);
+ * kg_shard_level drops the records of those queries.  kg_shard_done packs this rank's d_res into its
+ * words (words >= ceil(n / 32)); the driver all-gathers them before each level. */
+int kg_shard_done(kg_snapshot* s, size_t n, const uint8_t* d_res, uint32_t* d_bits, uint32_t words, void* stream);
+/* The no-holder test across ranks (k_resolve's in the single-GPU engine): import 0 copies this
+ * rank's holder bitmap (bit = a subject id some local row holds) into d_bits[words] (words >=
+ * kg_shard_held_words); import 1 installs d_bits -- the OR over all ranks -- so kg_shard_seed
+ * answers NotMember at once for a subject no rank holds (snapshots without a namespace program).
+ * A single-rank snapshot uses its own bitmap without this. */
+int kg_shard_held_words(const kg_snapshot* s, size_t* words);
+int kg_shard_held(kg_snapshot* s, uint32_t* d_bits, size_t words, int import, void* stream);
 int kg_shard_finish(kg_snapshot* s, size_t n, uint8_t* d_res, const uint32_t* d_err, void* stream);
 
 /* ---- expand ----------------------------------------------------------------------------- */

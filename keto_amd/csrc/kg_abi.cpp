@@ -210,14 +210,41 @@ int kg_shard_seed(kg_snapshot* sp, const kg_query* d_q, size_t n, int32_t global
 }
 
 int kg_shard_level(kg_snapshot* sp, const kg_frec* d_in, size_t n_in, const uint32_t* d_n_in, kg_frec* d_out,
-                   size_t cap, uint32_t* d_counts, uint8_t* d_res, uint32_t* d_err, void* stream) {
+                   size_t cap, uint32_t* d_counts, uint8_t* d_res, uint32_t* d_err, const uint32_t* d_done,
+                   uint32_t done_words, void* stream) {
   KG_GUARD_BEGIN
   if (!sp || !d_counts || !d_res || !d_err || (n_in && (!d_in || !d_out))) return set_error(-2, "NULL argument");
   Snapshot* s = reinterpret_cast<Snapshot*>(sp);
   std::lock_guard<std::mutex> lk(s->mu);
   if (!s->shard_vis) return set_error(-2, "kg_shard_level before kg_shard_seed");
-  return kg::shard_level(s, d_in, n_in, d_n_in, d_out, cap, d_counts, d_res, d_err, (hipStream_t)stream);
+  return kg::shard_level(s, d_in, n_in, d_n_in, d_out, cap, d_counts, d_res, d_err, d_done, done_words,
+                         (hipStream_t)stream);
   KG_GUARD_END
+}
+
+int kg_shard_done(kg_snapshot* sp, size_t n, const uint8_t* d_res, uint32_t* d_bits, uint32_t words, void* stream) {
+  KG_GUARD_BEGIN
+  if (!sp || (n && (!d_res || !d_bits))) return set_error(-2, "NULL argument");
+  Snapshot* s = reinterpret_cast<Snapshot*>(sp);
+  std::lock_guard<std::mutex> lk(s->mu);
+  return kg::shard_done(s, n, d_res, d_bits, words, (hipStream_t)stream);
+  KG_GUARD_END
+}
+
+int kg_shard_held(kg_snapshot* sp, uint32_t* d_bits, size_t words, int import, void* stream) {
+  KG_GUARD_BEGIN
+  if (!sp || (words && !d_bits)) return set_error(-2, "NULL argument");
+  Snapshot* s = reinterpret_cast<Snapshot*>(sp);
+  std::lock_guard<std::mutex> lk(s->mu);
+  return kg::shard_held(s, d_bits, words, import, (hipStream_t)stream);
+  KG_GUARD_END
+}
+
+int kg_shard_held_words(const kg_snapshot* sp, size_t* words) {
+  if (!sp || !words) return set_error(-2, "NULL argument");
+  const Snapshot* s = reinterpret_cast<const Snapshot*>(sp);
+  *words = ((size_t)s->ds.hbits_n + 31) / 32;
+  return 0;
 }
 
 int kg_shard_finish(kg_snapshot* sp, size_t n, uint8_t* d_res, const uint32_t* d_err, void* stream) {

@@ -17,6 +17,11 @@
 // interpreter's territory, rewrites.go:30-260 / engine.go:228) is answered KG_ERROR with
 // KG_ERR_NOT_IMPLEMENTED, whatever else it reaches: the owner reports it to the home rank, which
 // records it in err[] (errors win over hits; kg_shard_finish folds err into res).
+// Pruning (the single-GPU tiers' early exits, made rank-independent): a query whose subject id no
+// row of any rank holds is NotMember at seed (no program only: with rewrites it may still reach an
+// error); a query answered IsMember by the end of level k drops its records from level k+1 on --
+// every rank reads the same per-level done bitmap (packed from the home ranks' results, all-gathered
+// by the driver), so the answer does not depend on the number of ranks.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -28,6 +33,9 @@
 namespace kg {
 
 constexpr uint32_t Q_BITS = 26, Q_MASK = (1u << Q_BITS) - 1;
+// kg_frec.depth bit 30: the sender's Bloom signature of the node's row rules the subject out, so the
+// owner skips the checkDirect probe (a certain miss); the rest depth sits in the low bits
+constexpr int32_t D_NOPROBE = 1 << 30, D_MASK = D_NOPROBE - 1;
 constexpr int SV_PROBES = 64;
 
 // (query, node) visited table: open addressing, cleared per batch.  1 fresh, 0 seen, -1 full.
@@ -42,38 +50,58 @@ __device__ __forceinline__ int sv_insert(uint64_t* T, uint64_t mask, uint64_t ke
   return -1;
 }
 
-// Wave-aggregated append of one record per active lane to the bucket of its destination rank:
-// one atomic per (wave, destination) instead of one per record.
+// Workgroup-aggregated append of one record per active thread to the bucket of its destination
+// rank: ballots per wave into LDS counters, then ONE device atomic per (workgroup, destination) --
+// at world 1 every record goes to one counter, so per-wave atomics serialised on it.  Every thread
+// of the workgroup must call it (256 threads).
 __device__ __forceinline__ void emit(bool act, uint32_t dest, const kg_frec& r, kg_frec* out, uint64_t cap,
                                      uint32_t* counts, uint32_t nranks) {
+  __shared__ uint32_t s_cnt[KG_SHARD_MAX_RANKS], s_base[KG_SHARD_MAX_RANKS];
+  const int tid = threadIdx.x, lane = lane_id();
+  if (tid < (int)nranks) s_cnt[tid] = 0;
+  __syncthreads();
   uint64_t pending = __ballot(act);
-  const int lane = lane_id();
+  uint32_t my = 0;
   while (pending) {
     const int lead = __ffsll((unsigned long long)pending) - 1;
     const uint32_t d = __shfl(dest, lead, 64);
     const uint64_t m = __ballot(act && dest == d);
     uint32_t base = 0;
-    if (lane == lead) base = atomicAdd(&counts[d], (uint32_t)__popcll(m));
+    if (lane == lead) base = atomicAdd(&s_cnt[d], (uint32_t)__popcll(m));
     base = __shfl(base, lead, 64);
-    if (act && dest == d) {
-      const uint32_t at = base + __popcll(m & ((1ull << lane) - 1));
-      if (at < cap) out[(uint64_t)d * cap + at] = r;
-      else atomicOr(&counts[nranks], 1u);
-    }
+    if (act && dest == d) my = base + __popcll(m & ((1ull << lane) - 1));
     pending &= ~m;
   }
+  __syncthreads();
+  if (tid < (int)nranks) s_base[tid] = s_cnt[tid] ? atomicAdd(&counts[tid], s_cnt[tid]) : 0u;
+  __syncthreads();
+  if (act) {
+    const uint32_t at = s_base[dest] + my;
+    if (at < cap) out[(uint64_t)dest * cap + at] = r;
+    else atomicOr(&counts[nranks], 1u);
+  }
+  __syncthreads();
 }
 
 __global__ __launch_bounds__(256) void k_shard_seed(DevSnap s, const kg_query* __restrict__ q, uint32_t n,
                                                     int32_t global, kg_frec* out, uint64_t cap, uint32_t* counts,
-                                                    uint8_t* res, uint32_t* err) {
+                                                    uint8_t* res, uint32_t* err, const uint32_t* __restrict__ held,
+                                                    uint32_t held_n) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   bool act = false;
   uint32_t dest = 0;
   kg_frec r{};
   if (i < n) {
     const kg_query x = q[i];
-    const uint32_t node = nmap_find(s, x.t.ns, x.t.rel, x.t.obj);
+    uint32_t node = NONE, rsig = 0xFFFFFFFFu;
+    if (nmap_key_ok(x.t.ns, x.t.rel, x.t.obj)) {
+      const uint64_t key = nmap_key(x.t.ns, x.t.rel, x.t.obj);
+      const NSlot* sl = nmap_slot(s, key, hash_home(key, s.nmap_n));
+      if (sl) {
+        node = sl->node;
+        rsig = sl->sig;
+      }
+    }
     uint32_t subj;
     if (x.t.sns == KG_SUBJECT_ID) {
       subj = x.t.sobj < 0x7FFFFFFFu ? x.t.sobj : NONE;
@@ -87,12 +115,17 @@ __global__ __launch_bounds__(256) void k_shard_seed(DevSnap s, const kg_query* _
     err[i] = KG_ERR_NONE;
     if (relflag(s, x.t.ns, x.t.rel)) {  // rewrites are not part of the sharded mode
       err[i] = KG_ERR_NOT_IMPLEMENTED;
+    } else if (held && !s.relflags && x.t.sns == KG_SUBJECT_ID &&
+               (subj == NONE || subj >= held_n || !((held[subj >> 5] >> (subj & 31)) & 1u))) {
+      // no row of any rank holds the subject: checkDirect can never hit (NotMember)
     } else if (node != NONE && (subj != NONE || s.relflags)) {
       // an unknown subject can never be held, but with a namespace program the query can still
       // reach a rewrite (an error), so it is seeded all the same (its probes are skipped)
       act = true;
       dest = s.nowner ? s.nowner[node] : 0u;
-      r = kg_frec{(s.shard_rank << Q_BITS) | i, node, subj, d};
+      // signatures are built from this rank's rows: only a locally owned node's rules a probe out
+      const bool may = subj == NONE || dest != s.shard_rank || sig_maybe(rsig, subj_sig(subj));
+      r = kg_frec{(s.shard_rank << Q_BITS) | i, node, subj, d | (may ? 0 : D_NOPROBE)};
     }
   }
   emit(act, dest, r, out, cap, counts, s.shard_n);
@@ -102,7 +135,8 @@ __global__ __launch_bounds__(256) void k_shard_seed(DevSnap s, const kg_query* _
 // edge-parallel (block scan of the row lengths, LDS owner search).
 __global__ __launch_bounds__(256) void k_shard_level(DevSnap s, const kg_frec* __restrict__ in, uint64_t n_bound,
                                                      const uint32_t* d_n_in, kg_frec* out, uint64_t cap, uint32_t* counts, uint8_t* res,
-                                                     uint32_t* err, uint64_t* vis, uint64_t vmask) {
+                                                     uint32_t* err, uint64_t* vis, uint64_t vmask,
+                                                     const uint32_t* __restrict__ done, uint32_t done_wpr) {
   __shared__ uint32_t s_pref[256], s_wsum[4];
   __shared__ uint64_t s_rb[256];
   __shared__ kg_frec s_rec[256];
@@ -118,10 +152,15 @@ __global__ __launch_bounds__(256) void k_shard_level(DevSnap s, const kg_frec* _
     uint64_t rb = 0, len = 0;
     if (i < n_in) {
       r = in[i];
+      const bool probe = !(r.depth & D_NOPROBE);
+      r.depth &= D_MASK;
       if (r.node == KG_FREC_HIT) {
         if ((r.q >> Q_BITS) == me) res[r.q & Q_MASK] = KG_IS_MEMBER;
       } else if (r.node == KG_FREC_ERR) {
         if ((r.q >> Q_BITS) == me) atomicMax(&err[r.q & Q_MASK], r.subj);
+      } else if (done && ((r.q & Q_MASK) >> 5) < done_wpr &&
+                 ((done[(size_t)(r.q >> Q_BITS) * done_wpr + ((r.q & Q_MASK) >> 5)] >> (r.q & 31)) & 1u)) {
+        // answered IsMember by an earlier level: nothing more to do for this query
       } else {
         const int ins = sv_insert(vis, vmask, ((uint64_t)r.q << 32) | r.node);
         if (ins < 0) atomicOr(&counts[s.shard_n], 2u);
@@ -129,7 +168,7 @@ __global__ __launch_bounds__(256) void k_shard_level(DevSnap s, const kg_frec* _
           if ((r.q >> Q_BITS) == me) atomicMax(&err[r.q & Q_MASK], (uint32_t)KG_ERR_NOT_IMPLEMENTED);
           else err_out = true;
         } else if (ins > 0) {
-          if (r.depth >= 1 && r.subj != NONE && dset_probe(s, r.node, r.subj)) {  // checkDirect(depth - 1)
+          if (probe && r.depth >= 1 && r.subj != NONE && dset_probe(s, r.node, r.subj)) {  // checkDirect(depth - 1)
             if ((r.q >> Q_BITS) == me) res[r.q & Q_MASK] = KG_IS_MEMBER;
             else hit_out = true;
           } else if (r.depth >= 2 || (r.depth == 1 && s.relflags)) {
@@ -173,10 +212,13 @@ __global__ __launch_bounds__(256) void k_shard_level(DevSnap s, const kg_frec* _
       if (act) {
         const int own = owner_search(s_pref, 256, e);
         const kg_frec& pr = s_rec[own];
-        const uint32_t child = s.adj[s_rb[own] + (e - s_pref[own])];
+        const AdjX ax = s.adjx[s_rb[own] + (e - s_pref[own])];  // child + its row signature
+        const uint32_t child = ax.node;
         if (pr.depth >= 2) {
-          c = kg_frec{pr.q, child, pr.subj, pr.depth - 1};
           dest = s.nowner ? s.nowner[child] : 0u;
+          // signatures are built from this rank's rows: only a locally owned child's rules a probe out
+          const bool may = pr.subj == NONE || dest != me || sig_maybe(ax.sig, subj_sig(pr.subj));
+          c = kg_frec{pr.q, child, pr.subj, (pr.depth - 1) | (may ? 0 : D_NOPROBE)};
           send = true;
         } else if (relflag(s, s.nd_ns[child], s.nd_rel[child]) != 0) {  // a depth-0 child with a rewrite
           if ((pr.q >> Q_BITS) == me) {
@@ -192,6 +234,18 @@ __global__ __launch_bounds__(256) void k_shard_level(DevSnap s, const kg_frec* _
     }
     __syncthreads();
   }
+}
+
+// Done bitmap of this rank's queries (IsMember so far), one word per thread.
+__global__ void k_shard_done(uint32_t n, const uint8_t* __restrict__ res, uint32_t words, uint32_t* __restrict__ bits) {
+  const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= words) return;
+  uint32_t b = 0;
+  for (uint32_t k = 0; k < 32; k++) {
+    const uint32_t i = w * 32 + k;
+    if (i < n && res[i] == KG_IS_MEMBER) b |= 1u << k;
+  }
+  bits[w] = b;
 }
 
 __global__ void k_shard_finish(uint32_t n, uint8_t* res, const uint32_t* err) {
@@ -224,24 +278,61 @@ int shard_seed(Snapshot* s, const kg_query* d_q, size_t n, int32_t gdepth, kg_fr
   if (int rc = shard_vis_prepare(s, stream)) return rc;
   HIPC(hipMemsetAsync(d_counts, 0, (s->shard_n + 1) * 4, stream));
   if (n) {
+    const uint32_t* held = s->shard_held ? s->shard_held : s->ds.hbits;
+    const uint32_t held_n = s->shard_held ? s->shard_held_n : s->ds.hbits_n;
     hipLaunchKernelGGL(k_shard_seed, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, stream, s->ds, d_q, (uint32_t)n,
-                       gdepth, d_out, (uint64_t)cap, d_counts, d_res, d_err);
+                       gdepth, d_out, (uint64_t)cap, d_counts, d_res, d_err,
+                       (s->shard_n == 1 || s->shard_held) ? held : nullptr, held_n);
     HIPC(hipGetLastError());
   }
   return 0;
 }
 
 int shard_level(Snapshot* s, const kg_frec* d_in, size_t n_in, const uint32_t* d_n_in, kg_frec* d_out, size_t cap,
-                uint32_t* d_counts, uint8_t* d_res, uint32_t* d_err, hipStream_t stream) {
+                uint32_t* d_counts, uint8_t* d_res, uint32_t* d_err, const uint32_t* d_done, uint32_t done_words,
+                hipStream_t stream) {
   HIPC(hipSetDevice(s->device));
   if (!stream) stream = s->stream;
   HIPC(hipMemsetAsync(d_counts, 0, (s->shard_n + 1) * 4, stream));
   if (n_in) {
     const uint32_t grid = (uint32_t)std::min<uint64_t>((n_in + 255) / 256, (uint64_t)s->n_cu * 8);
     hipLaunchKernelGGL(k_shard_level, dim3(grid), dim3(256), 0, stream, s->ds, d_in, (uint64_t)n_in, d_n_in, d_out,
-                       (uint64_t)cap, d_counts, d_res, d_err, (uint64_t*)s->shard_vis, s->shard_vis_slots - 1);
+                       (uint64_t)cap, d_counts, d_res, d_err, (uint64_t*)s->shard_vis, s->shard_vis_slots - 1,
+                       d_done, d_done ? done_words : 0u);
     HIPC(hipGetLastError());
   }
+  return 0;
+}
+
+int shard_done(Snapshot* s, size_t n, const uint8_t* d_res, uint32_t* d_bits, uint32_t words, hipStream_t stream) {
+  HIPC(hipSetDevice(s->device));
+  if (!stream) stream = s->stream;
+  if (words < (n + 31) / 32) return set_error(-2, "done bitmap too small (%u words for %zu queries)", words, n);
+  if (words) {
+    hipLaunchKernelGGL(k_shard_done, dim3((words + 255) / 256), dim3(256), 0, stream, (uint32_t)n, d_res, words, d_bits);
+    HIPC(hipGetLastError());
+  }
+  return 0;
+}
+
+// The holder bitmap across ranks: export this rank's (import 0), or install the OR of all ranks'
+// (import 1) so kg_shard_seed's no-holder test sees every rank's rows.
+int shard_held(Snapshot* s, uint32_t* d_bits, size_t words, int import, hipStream_t stream) {
+  HIPC(hipSetDevice(s->device));
+  if (!stream) stream = s->stream;
+  if (!import) {
+    const size_t have = ((size_t)s->ds.hbits_n + 31) / 32;
+    if (words < have) return set_error(-2, "holder bitmap needs %zu words", have);
+    HIPC(hipMemsetAsync(d_bits, 0, words * 4, stream));
+    if (have) HIPC(hipMemcpyAsync(d_bits, s->ds.hbits, have * 4, hipMemcpyDeviceToDevice, stream));
+    return 0;
+  }
+  if (s->shard_held) s->free_alloc(s->shard_held);
+  s->shard_held = nullptr;
+  if (s->alloc((void**)&s->shard_held, words * 4 + 4)) return -1;
+  if (words) HIPC(hipMemcpyAsync(s->shard_held, d_bits, words * 4, hipMemcpyDeviceToDevice, stream));
+  s->shard_held_n = (uint32_t)std::min<size_t>(words * 32, 0xFFFFFFFFull);
+  HIPC(hipStreamSynchronize(stream));
   return 0;
 }
 

@@ -142,6 +142,8 @@ struct Snapshot {
   uint32_t shard_rank = 0, shard_n = 1;  // hash-sharded mode (set before create)
   void* shard_vis = nullptr;             // kg_shard.hip: per-batch visited table of (query, node)
   uint64_t shard_vis_slots = 0;
+  uint32_t* shard_held = nullptr;  // holder bitmap OR-ed over every rank (kg_shard_held), or null
+  uint32_t shard_held_n = 0;
   int shard_vis_log2 = 25;
   int stream_variant = 9;  // kg_snapshot_tune("stream"): k_stream variant (0..8) or 9 = k_stream2
   int back_tier = 2;  // kg_snapshot_tune("back"): backward tier (1: wave + workgroup widths, 2: wave only) + no-holder filter
@@ -197,7 +199,10 @@ int formula_combine(Snapshot* s, Workspace* w, size_t n, const uint2* ref, const
 int shard_seed(Snapshot* s, const kg_query* d_q, size_t n, int32_t gdepth, kg_frec* d_out, size_t cap,
                uint32_t* d_counts, uint8_t* d_res, uint32_t* d_err, hipStream_t stream);
 int shard_level(Snapshot* s, const kg_frec* d_in, size_t n_in, const uint32_t* d_n_in, kg_frec* d_out, size_t cap,
-                uint32_t* d_counts, uint8_t* d_res, uint32_t* d_err, hipStream_t stream);
+                uint32_t* d_counts, uint8_t* d_res, uint32_t* d_err, const uint32_t* d_done, uint32_t done_words,
+                hipStream_t stream);
+int shard_done(Snapshot* s, size_t n, const uint8_t* d_res, uint32_t* d_bits, uint32_t words, hipStream_t stream);
+int shard_held(Snapshot* s, uint32_t* d_bits, size_t words, int import, hipStream_t stream);
 int shard_finish(Snapshot* s, size_t n, uint8_t* d_res, const uint32_t* d_err, hipStream_t stream);
 // kg_grid.hip
 int grid_reserve(Snapshot* s);  // allocates the shared full-size grid pool now (kg_snapshot_tune "grid_reserve")

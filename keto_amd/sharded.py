@@ -60,12 +60,36 @@ class HipShardOps:
         self.vis_log2 = getattr(self, "vis_log2", 25) + 1
         self.snapshot.tune("shard_vis", self.vis_log2)
 
-    def level(self, din, n_in, n_in_dev, out, cap, counts, res, err):
-        """n_in_dev: None, or a device int32 tensor whose element 0 is the record count (n_in bounds it)."""
+    def level(self, din, n_in, n_in_dev, out, cap, counts, res, err, done=None, done_words=0):
+        """n_in_dev: None, or a device int32 tensor whose element 0 is the record count (n_in bounds it).
+        done: None, or the batch's done bitmap (done_words int32 words per rank)."""
         _lib.check(self.L.kg_shard_level(self.snapshot.handle, din.data_ptr() if n_in else None, n_in,
                                          n_in_dev.data_ptr() if n_in_dev is not None else None, out.data_ptr(), cap,
-                                         counts.data_ptr(), res.data_ptr(), err.data_ptr(), self._s()),
+                                         counts.data_ptr(), res.data_ptr(), err.data_ptr(),
+                                         done.data_ptr() if done is not None else None, done_words, self._s()),
                    "kg_shard_level")
+
+    def done_bits(self, res, n, words):
+        import torch
+        bits = torch.empty(max(words, 1), dtype=torch.int32, device=res.device)
+        _lib.check(self.L.kg_shard_done(self.snapshot.handle, n, res.data_ptr(), bits.data_ptr(), words, self._s()),
+                   "kg_shard_done")
+        return bits[:words]
+
+    def held_words(self) -> int:
+        w = C.c_size_t(0)
+        _lib.check(self.L.kg_shard_held_words(self.snapshot.handle, C.byref(w)), "kg_shard_held_words")
+        return int(w.value)
+
+    def held_export(self, words):
+        import torch
+        bits = torch.empty(max(words, 1), dtype=torch.int32, device="cuda")
+        _lib.check(self.L.kg_shard_held(self.snapshot.handle, bits.data_ptr(), words, 0, self._s()), "kg_shard_held")
+        return bits[:words]
+
+    def held_import(self, bits):
+        _lib.check(self.L.kg_shard_held(self.snapshot.handle, bits.data_ptr(), int(bits.shape[0]), 1, self._s()),
+                   "kg_shard_held")
 
     def finish(self, n, res, err):
         _lib.check(self.L.kg_shard_finish(self.snapshot.handle, n, res.data_ptr(), err.data_ptr(), self._s()),
@@ -91,6 +115,40 @@ class ShardedChecker:
         self.levels = 0
         self.records_sent = 0
         self.host_syncs = 0
+        self._held_ready = world == 1 or not hasattr(ops, "held_export")
+
+    def _install_held(self):
+        """Once per snapshot: the OR of every rank's holder bitmap, so kg_shard_seed's no-holder test
+        sees all rows (an all-reduce of the word count, an all-gather of the bitmaps)."""
+        import torch
+        dev = self.device if not self._host_staged() else "cpu"
+        w = torch.tensor([self.ops.held_words()], dtype=torch.int64, device=dev)
+        self.dist.all_reduce(w, op=self.dist.ReduceOp.MAX)
+        words = int(w.item())
+        mine = self.ops.held_export(words)
+        if self._host_staged():
+            mine = mine.cpu()
+        allb = [torch.empty(words, dtype=torch.int32, device=mine.device) for _ in range(self.world)]
+        self.dist.all_gather(allb, mine.contiguous())
+        acc = allb[0].clone()
+        for r in range(1, self.world):
+            acc |= allb[r]
+        self.ops.held_import(acc.to(self.device))
+        self._held_ready = True
+
+    def _done(self, res, n, words):
+        """The batch's done bitmap for the next level: every rank's packed results, all-gathered."""
+        import torch
+        mine = self.ops.done_bits(res, n, words)
+        if self.dist is None or self.world == 1:
+            return mine
+        staged = self._host_staged()
+        if staged:
+            mine = mine.cpu()
+        parts = [torch.empty(words, dtype=torch.int32, device=mine.device) for _ in range(self.world)]
+        self.dist.all_gather(parts, mine.contiguous())
+        allb = torch.cat(parts)
+        return allb.to(self.device) if staged else allb
 
     # ---- exchange
     def _host_staged(self) -> bool:
@@ -109,7 +167,8 @@ class ShardedChecker:
             counts = counts.cpu()  # gloo moves host tensors: stage here (the one host copy of the level)
         c = counts.to(torch.int64)
         myflags = c[N] | (c[:N] > cap).any().to(torch.int64)  # a count past cap = dropped records
-        meta = torch.stack([c[:N], c[:N].sum().expand(N), myflags.expand(N)], dim=1).contiguous()
+        nq = torch.full((N,), self._n, dtype=torch.int64, device=c.device)
+        meta = torch.stack([c[:N], c[:N].sum().expand(N), myflags.expand(N), nq], dim=1).contiguous()
         recv = torch.empty_like(meta)
         if self.dist is None:
             recv.copy_(meta)
@@ -118,10 +177,11 @@ class ShardedChecker:
         h = torch.cat([c[:N], recv.flatten()]).cpu().numpy()  # the level's host round trip
         self.host_syncs += 1
         send = [int(x) for x in h[:N]]
-        rm = h[N:].reshape(N, 3)
+        rm = h[N:].reshape(N, 4)
         flags = 0
         for f in rm[:, 2]:
             flags |= int(f)
+        self._n_max = int(rm[:, 3].max())  # the largest batch of any rank: sizes the done bitmap
         return send, [int(x) for x in rm[:, 0]], int(rm[:, 1].sum()), flags
 
     def _exchange(self, out, send_splits, recv_splits):
@@ -166,6 +226,10 @@ class ShardedChecker:
         n = int(dq.shape[0])
         N, cap = self.world, self.cap
         gdepth = gdepth if gdepth >= 1 else 5  # config.schema.json:308-315 default (as kg_shard_seed)
+        if not self._held_ready:
+            self._install_held()
+        self._n = n
+        prune = hasattr(self.ops, "done_bits")
         bufs = [torch.empty((N * cap, REC_WORDS), dtype=torch.int32, device=self.device) for _ in range(2)]
         counts = [torch.zeros(N + 1, dtype=torch.int32, device=self.device) for _ in range(2)]
         res = torch.zeros(n, dtype=torch.uint8, device=self.device)
@@ -179,10 +243,12 @@ class ShardedChecker:
             # count read on the device.  A record's depth falls by one per level and seeds carry
             # <= gdepth, so gdepth levels drain the batch; overflow is checked once at the end.
             flags = torch.zeros((), dtype=torch.int64, device=self.device)
+            words = (n + 31) // 32
             for _ in range(gdepth):
                 c = counts[cur]
                 flags |= c[1].to(torch.int64) | (c[0].to(torch.int64) > cap).to(torch.int64)
-                self.ops.level(bufs[cur], cap, c, bufs[cur ^ 1], cap, counts[cur ^ 1], res, err)
+                done = self.ops.done_bits(res, n, words) if prune and self.levels > 0 else None
+                self.ops.level(bufs[cur], cap, c, bufs[cur ^ 1], cap, counts[cur ^ 1], res, err, done, words)
                 cur ^= 1
                 self.levels += 1
             c = counts[cur]
@@ -204,6 +270,8 @@ class ShardedChecker:
                 return res, err
             self.records_sent += sum(send)
             recv = self._exchange(bufs[cur], send, recv_splits)
+            words = (self._n_max + 31) // 32
+            done = self._done(res, n, words) if prune and self.levels > 0 else None
             cur ^= 1
-            self.ops.level(recv, int(recv.shape[0]), None, bufs[cur], cap, counts[cur], res, err)
+            self.ops.level(recv, int(recv.shape[0]), None, bufs[cur], cap, counts[cur], res, err, done, words)
             self.levels += 1

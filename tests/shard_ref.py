@@ -51,7 +51,7 @@ class CpuShardOps:
                 self.nrel[self.node[k]] = (k[0], k[2])
             return self.node[k]
 
-        self.adj, self.direct, self.owner = {}, set(), {}
+        self.adj, self.direct, self.owner, self.held = {}, set(), {}, set()
         for ns, obj, rel, sns, sobj, srel in t:
             v = nid(ns, obj, rel)
             self.owner[v] = shard_owner(int(ns), int(obj), nranks)
@@ -65,6 +65,8 @@ class CpuShardOps:
                     self.adj.setdefault(v, []).append(c)
             if self.owner[v] == rank:
                 self.direct.add((v, subj))
+            if sns == SUBJECT_ID:
+                self.held.add(int(sobj))  # every rank's rows: the OR the driver installs (kg_shard_held)
         self.vis = set()
 
     def _emit(self, out, cap, counts, dest, rec):
@@ -97,14 +99,24 @@ class CpuShardOps:
                 continue
             if v is None or (subj is None and not self.impure):
                 continue
+            if not self.impure and sns == SUBJECT_ID and int(sobj) not in self.held:
+                continue  # no row of any rank holds the subject (kg_shard_seed's no-holder test)
             if subj is None:
                 subj = 0xFFFFFFFF  # unknown subject: never held, but the query may still reach a rewrite
             self._emit(out, cap, counts, self.owner[v],
                        [(self.rank << Q_BITS) | i, v, np.uint32(subj).view(np.int32), d])
 
-    def level(self, din, n_in, n_in_dev, out, cap, counts, res, err):
+    def done_bits(self, res, n, words):
+        """kg_shard_done: bit i of this rank's words = query i answered IsMember so far."""
+        bits = np.zeros(words, np.uint32)
+        for i in np.nonzero(res.numpy()[:n] == 1)[0]:
+            bits[i >> 5] |= np.uint32(1 << (int(i) & 31))
+        return torch.from_numpy(bits.view(np.int32).copy())
+
+    def level(self, din, n_in, n_in_dev, out, cap, counts, res, err, done=None, done_words=0):
         assert n_in_dev is None
         counts.zero_()
+        dn = None if done is None else done.numpy().view(np.uint32)
         for r in din[:n_in].tolist():
             q, v, subj, d = r[0], r[1], r[2] & 0xFFFFFFFF, r[3]
             home, qi = q >> Q_BITS, q & ((1 << Q_BITS) - 1)
@@ -116,6 +128,8 @@ class CpuShardOps:
                 if home == self.rank:
                     err[qi] = max(int(err[qi]), subj)
                 continue
+            if dn is not None and (qi >> 5) < done_words and (int(dn[home * done_words + (qi >> 5)]) >> (qi & 31)) & 1:
+                continue  # answered IsMember by an earlier level
             if (q, v) in self.vis:
                 continue
             self.vis.add((q, v))
