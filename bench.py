@@ -63,8 +63,13 @@ def parse():
     ap.add_argument("--back-wgs", type=int, default=1,
                     help="kg_snapshot_tune back_wgs (k_back WGs per CU; 1 leaves LDS to the other in-flight batches)")
     ap.add_argument("--interp-wgs", type=int, default=6, help="kg_snapshot_tune interp_wgs (rewrite-path LDS pass WGs per CU)")
-    ap.add_argument("--inflight", type=int, default=4,
-                    help="batches in flight per GPU: one HIP stream (own workspace) and one host thread each")
+    ap.add_argument("--hw-queues", type=int, default=None,
+                    help="HIP hardware queues for this process (GPU_MAX_HW_QUEUES, 1..32; 0 = HIP's default, 4; "
+                         "default 8 for --mode expand, else 0): batches in flight beyond the queue count share "
+                         "queues and serialise")
+    ap.add_argument("--inflight", type=int, default=None,
+                    help="batches in flight per GPU: one HIP stream (own workspace) and one host thread each "
+                         "(default 4; 6 for --mode expand, whose batches end in one long sequential root)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline time budget (0 = skip)")
     ap.add_argument("--replay", type=int, default=0,
                     help="cycle over this many distinct batches (0 = a distinct batch for every step; diagnostics)")
@@ -102,25 +107,57 @@ def bench_expand(a):
         buf = _lib.kg_tree_buf()
         _lib.check(L.kg_expand_batch(snap.handle, roots.ctypes.data_as(C.c_void_p), a.roots, depth, C.byref(buf)),
                    "kg_expand_batch")
-        res = (buf.n_nodes, buf.kernel_ms)
+        off = np.ctypeslib.as_array(buf.root_off, shape=(a.roots + 1,)).copy() if buf.root_off else None
+        res = (buf.n_nodes, buf.kernel_ms, off)
         L.kg_tree_free(C.byref(buf))
         return res
 
-    for _ in range(a.warmup):
-        step()
+    P = max(1, a.inflight)  # batches in flight: P host threads, each on its own lane (stream + buffers)
+    import threading
+    nw = min(P, a.steps)
+    results = [None] * a.steps
+    errors = []
+    ready = threading.Barrier(nw + 1)
+
+    def worker(p):
+        try:
+            for _ in range(max(1, -(-a.warmup // nw))):  # warm-up: this thread's lane and buffers
+                step()
+        except Exception as e:  # noqa: BLE001 -- re-raised below
+            errors.append(e)
+        ready.wait()
+        try:
+            for k in range(p, a.steps, nw):
+                if not errors:
+                    results[k] = step()
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    th = [threading.Thread(target=worker, args=(p,)) for p in range(nw)]
+    for t in th:
+        t.start()
+    ready.wait()
     t0 = time.perf_counter()
-    nodes, kms = 0, 0.0
-    for _ in range(a.steps):
-        n, k = step()
-        nodes += n
-        kms += k
+    for t in th:
+        t.join()
     el = time.perf_counter() - t0
+    if errors:
+        raise errors[0]
+    nodes = sum(r[0] for r in results)
+    kms = sum(r[1] for r in results)
+    off = results[-1][2]
     out = {"metric": "expand trees/sec (batched BuildTree, hot group#member roots)", "value": a.roots * a.steps / el,
            "unit": "trees/s", "n_gpus": 1, "steps": a.steps, "warmup": a.warmup, "ms_per_step": el / a.steps * 1e3,
            "higher_is_better": True, "dtype": "u32", "data": "synthetic (device-generated, seed %d)" % a.seed,
-           "config": {"workload": "C5: %d hot roots @ %.3g tuples, max_read_depth %d" % (a.roots, a.tuples, depth)},
+           "config": {"workload": "C5: %d hot roots @ %.3g tuples, max_read_depth %d" % (a.roots, a.tuples, depth),
+                      "inflight_per_gpu": P, "hw_queues": a.hw_queues},
            "tree_nodes_per_step": nodes / a.steps, "tree_nodes_per_s": nodes / el,
-           "kernel_ms_per_step": kms / a.steps, "trees_per_s_kernel_only": a.roots * a.steps / (kms * 1e-3)}
+           "kernel_ms_per_step": kms / a.steps}
+    if off is not None:
+        sz = np.diff(off.astype(np.int64))
+        out["records_per_root"] = {"p50": float(np.percentile(sz, 50)), "p99": float(np.percentile(sz, 99)),
+                                   "max": int(sz.max()), "roots_over_512": int((sz > 512).sum()),
+                                   "top10_share": float(np.sort(sz)[-10:].sum() / max(1, sz.sum()))}
     print(json.dumps(out), flush=True)
 
 
@@ -334,6 +371,12 @@ def aggregate(dist, elapsed: float, edges: float, device=None):
 
 def main():
     a = parse()
+    if a.hw_queues is None:
+        a.hw_queues = 8 if a.mode == "expand" else 0
+    if a.inflight is None:
+        a.inflight = 6 if a.mode == "expand" else 4
+    if a.hw_queues > 0:  # before anything initialises HIP (torch and the library load lazily)
+        os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, a.hw_queues))
     if a.tuples is None:
         a.tuples = 2e6 if a.heavy_tail else 1e9
     if a.mode == "expand":

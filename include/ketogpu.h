@@ -136,6 +136,7 @@ typedef struct {
   uint64_t* root_off; /* n_roots + 1 entries */
   uint64_t n_roots;
   double kernel_ms;   /* device time of the expand kernels (HIP events), filled by the library */
+  uint64_t pinned;    /* library use: nodes lives in the library's pinned-host pool (kg_tree_free returns it) */
 } kg_tree_buf;
 
 typedef struct kg_snapshot kg_snapshot;

@@ -63,7 +63,7 @@ class kg_tree_node(C.Structure):
 
 class kg_tree_buf(C.Structure):
     _fields_ = [("nodes", C.POINTER(kg_tree_node)), ("n_nodes", C.c_uint64), ("root_off", C.POINTER(C.c_uint64)),
-                ("n_roots", C.c_uint64), ("kernel_ms", C.c_double)]
+                ("n_roots", C.c_uint64), ("kernel_ms", C.c_double), ("pinned", C.c_uint64)]
 
 
 class kg_synth_params(C.Structure):

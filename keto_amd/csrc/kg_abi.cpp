@@ -521,10 +521,16 @@ int kg_expand_batch(kg_snapshot* sp, const kg_set* roots, size_t n, int32_t glob
   if (!sp || !out) return set_error(-2, "NULL argument");
   if (n && !roots) return set_error(-2, "roots is NULL");
   Snapshot* s = reinterpret_cast<Snapshot*>(sp);
+  if (s->shard_n > 1) return set_error(-2, "sharded snapshot: expand needs every row on one device");
+  // this thread's lanes: one stream + cached buffers per replica, so concurrent callers overlap
+  std::vector<kg::Lane*>* lanes = s->thread_lanes();
+  if (!lanes) return -1;
   const size_t R = std::max<size_t>(1, std::min(s->n_replicas(), (n + MIN_PER_REPLICA - 1) / MIN_PER_REPLICA));
+  const size_t r0 = R < lanes->size() ? (size_t)(s->rr_next.fetch_add(1, std::memory_order_relaxed) % lanes->size()) : 0;
+  auto lane = [&](size_t i) { return (*lanes)[(r0 + i) % lanes->size()]; };
   if (R == 1) {
-    std::lock_guard<std::mutex> lk(s->mu);
-    return kg::expand_batch(s, roots, n, global_max_depth, out);
+    kg::Lane* L = lane(0);
+    return kg::expand_batch(L->rep, L->stream, &L->exp, roots, n, global_max_depth, out);
   }
   std::vector<kg_tree_buf> parts(R);
   std::vector<int> rcs(R, 0);
@@ -533,9 +539,8 @@ int kg_expand_batch(kg_snapshot* sp, const kg_set* roots, size_t n, int32_t glob
   for (size_t i = 0; i <= R; i++) b[i] = n * i / R;
   auto one = [&](size_t i) {
     try {
-      Snapshot* r = s->replica(i);
-      std::lock_guard<std::mutex> lk(r->mu);
-      rcs[i] = kg::expand_batch(r, roots + b[i], b[i + 1] - b[i], global_max_depth, &parts[i]);
+      kg::Lane* L = lane(i);
+      rcs[i] = kg::expand_batch(L->rep, L->stream, &L->exp, roots + b[i], b[i + 1] - b[i], global_max_depth, &parts[i]);
       if (rcs[i]) {
         char buf[1024];
         kg_last_error(buf, sizeof buf);
@@ -584,7 +589,8 @@ int kg_expand_batch(kg_snapshot* sp, const kg_set* roots, size_t n, int32_t glob
 
 void kg_tree_free(kg_tree_buf* t) {
   if (!t) return;
-  free(t->nodes);
+  if (t->pinned) kg::tree_pool_put(t->nodes, t->n_nodes * sizeof(kg_tree_node));
+  else free(t->nodes);
   free(t->root_off);
   memset(t, 0, sizeof *t);
 }

@@ -177,6 +177,17 @@ struct LdsStoreT {
     }
     return true;
   }
+  // lookup only (no insert): the key was inserted earlier by this wave
+  __device__ bool contains(uint32_t key) const {
+    uint32_t h = (key * 2654435761u) >> (32 - VL2);
+    for (int p = 0; p < NV; p++) {
+      const uint32_t k = L->vis[h];
+      if (k == key) return true;
+      if (k == NONE) return false;
+      h = (h + 1) & (NV - 1);
+    }
+    return false;
+  }
   __device__ void sync() { __builtin_amdgcn_wave_barrier(); }
   __device__ void finish(uint32_t) {}
 };
@@ -195,6 +206,9 @@ struct GlobalStore {
   __device__ bool insert(uint32_t key) {
     uint32_t bit = 1u << (key & 31);
     return !(atomicOr(&bm[key >> 5], bit) & bit);
+  }
+  __device__ bool contains(uint32_t key) const {  // coherent load (the marks are device atomics)
+    return (__hip_atomic_load(&bm[key >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> (key & 31)) & 1u;
   }
   __device__ void sync() {
     // list entries written by other lanes of this wave must be visible to its loads
@@ -233,6 +247,16 @@ struct HashStore {
       h = (h + 1) & tmask;
     }
     return true;
+  }
+  __device__ bool contains(uint32_t key) const {  // coherent loads (the entries are device atomics)
+    uint32_t h = home(key);
+    for (uint32_t p = 0; p <= tmask; p++) {
+      const uint32_t k = __hip_atomic_load(&tab[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (k == key + 1) return true;
+      if (k == 0u) return false;
+      h = (h + 1) & tmask;
+    }
+    return false;
   }
   __device__ void sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");

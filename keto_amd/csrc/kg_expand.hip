@@ -19,6 +19,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <vector>
 
 #include "kg_bfs.h"
@@ -176,7 +177,9 @@ __device__ int expand_root(const DevSnap& s, Store& st, const kg_set& root, int3
         const uint32_t c = sub & ~SET_BIT;
         crb = s.row_off[c];
         cre = s.row_off[c + 1];
-        cand = cre > crb;
+        // a set visited before this chunk is a leaf whatever comes first (the visited set only
+        // grows): only unvisited sets with rows are order-dependent candidates, taken one by one
+        cand = cre > crb && !st.contains(c);
       }
       const uint64_t mc = __ballot(cand);
       const uint32_t p = mc ? (uint32_t)(__ffsll((unsigned long long)mc) - 1) : 64u;
@@ -344,7 +347,105 @@ __global__ void k_expand_compact(const RootOut* outs, uint32_t n, const uint64_t
   }
 }
 
-int expand_batch(Snapshot* s, const kg_set* roots, size_t n, int32_t global, kg_tree_buf* out) {
+// Device buffers of one lane's expand calls (kg_expand_batch: one lane per calling thread and
+// replica), grown on demand and kept: hipMalloc / hipFree per call stall the device and would
+// serialise concurrent callers.
+struct ExpandBufs {
+  int device = -1;
+  kg_set* d_roots = nullptr;
+  RootOut* outs = nullptr;
+  uint32_t* p2 = nullptr;  // pass-2 | pass-3 queues
+  size_t n_cap = 0;        // roots the three above hold
+  ExpCtl* ctl = nullptr;
+  ExpFrame* stacks = nullptr;
+  size_t stacks_bytes = 0;
+  uint32_t* bm = nullptr;  // [pass-2 tables | pass-3 bitmap] | pass-2 lists | pass-3 list
+  size_t bm_bytes = 0;
+  kg_tree_node* arena = nullptr;
+  uint32_t* next = nullptr;
+  uint32_t chunks = 0;
+  kg_tree_node* dst = nullptr;
+  size_t dst_cap = 0;
+  uint64_t* d_off = nullptr;
+  size_t off_cap = 0;
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  ~ExpandBufs() {
+    if (device >= 0) hipSetDevice(device);
+    for (void* p : {(void*)d_roots, (void*)outs, (void*)p2, (void*)ctl, (void*)stacks, (void*)bm, (void*)arena,
+                    (void*)next, (void*)dst, (void*)d_off})
+      if (p) hipFree(p);
+    for (auto& e : ev)
+      if (e) hipEventDestroy(e);
+  }
+};
+
+void expand_bufs_free(void* p) { delete static_cast<ExpandBufs*>(p); }
+
+// Tree outputs go to pinned host memory from a process-wide pool: a device->host copy of a C5
+// batch's ~130 MB of records into fresh pageable memory took ~50 ms (page faults + staging), more
+// than the batch's kernels once batches overlap.  Buffers are size-classed (powers of two from
+// 1 MiB) and returned by kg_tree_free; at most POOL_KEEP bytes stay cached.
+namespace {
+constexpr size_t POOL_KEEP = 4ull << 30;
+std::mutex pool_mu;
+std::vector<std::pair<size_t, void*>> pool_free;
+size_t pool_cached = 0;
+size_t pool_class(size_t bytes) {
+  size_t c = 1 << 20;
+  while (c < bytes) c <<= 1;
+  return c;
+}
+}  // namespace
+
+void* tree_pool_get(size_t bytes) {
+  const size_t c = pool_class(bytes);
+  {
+    std::lock_guard<std::mutex> lk(pool_mu);
+    for (size_t i = 0; i < pool_free.size(); i++)
+      if (pool_free[i].first == c) {
+        void* p = pool_free[i].second;
+        pool_free[i] = pool_free.back();
+        pool_free.pop_back();
+        pool_cached -= c;
+        return p;
+      }
+  }
+  void* p = nullptr;
+  if (hipHostMalloc(&p, c, hipHostMallocDefault) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  return p;
+}
+
+void tree_pool_put(void* p, size_t bytes) {
+  if (!p) return;
+  const size_t c = pool_class(bytes);
+  {
+    std::lock_guard<std::mutex> lk(pool_mu);
+    if (pool_cached + c <= POOL_KEEP) {
+      pool_free.emplace_back(c, p);
+      pool_cached += c;
+      return;
+    }
+  }
+  (void)hipHostFree(p);
+}
+
+// Replaces *p with a buffer of at least `need` bytes (contents not kept).
+template <class T>
+static hipError_t grow(T** p, size_t& have, size_t need) {
+  if (need <= have && *p) return hipSuccess;
+  if (*p) hipFree(*p);
+  *p = nullptr;
+  have = 0;
+  const hipError_t e = hipMalloc((void**)p, std::max<size_t>(need, 16));
+  if (e == hipSuccess) have = need;
+  return e;
+}
+
+int expand_batch(Snapshot* s, hipStream_t stream, void** bufs, const kg_set* roots, size_t n, int32_t global,
+                 kg_tree_buf* out) {
   memset(out, 0, sizeof *out);
   if (global < 1) global = 5;
   out->root_off = (uint64_t*)calloc(n + 1, 8);
@@ -352,8 +453,9 @@ int expand_batch(Snapshot* s, const kg_set* roots, size_t n, int32_t global, kg_
   if (!out->root_off) return set_error(-4, "host allocation failed");
   if (n == 0) return 0;
   HIPC(hipSetDevice(s->device));
-  hipStream_t stream = s->stream;
-  // device buffers for this call
+  if (!*bufs) *bufs = new ExpandBufs();
+  ExpandBufs& B = *static_cast<ExpandBufs*>(*bufs);
+  B.device = s->device;
   const uint32_t stack_cap = (uint32_t)std::min<int64_t>(0x8000, (int64_t)global + 2);
   const uint32_t grid1 = (uint32_t)s->n_cu * 2, slots1 = grid1 * 4;
   const uint64_t nn = std::max<uint32_t>(s->ds.n_nodes, 1), words = ((nn + 31) / 32 + 1 + 3) & ~3ull;
@@ -365,66 +467,64 @@ int expand_batch(Snapshot* s, const kg_set* roots, size_t n, int32_t global, kg_
   const uint32_t slots2 =
       (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)s->n_cu * 2, (2ull << 30) / ((tsize + cap2) * 4)));
   uint32_t n_chunks = (uint32_t)std::min<uint64_t>(1u << 22, std::max<uint64_t>(4096, n * 2 + slots1));
-  kg_set* d_roots = nullptr;
-  ExpCtl* ctl = nullptr;
-  RootOut* outs = nullptr;
-  ExpFrame* stacks = nullptr;
-  uint32_t *p2 = nullptr, *bm = nullptr, *lists = nullptr;
-  kg_tree_node *arena = nullptr, *dst = nullptr;
-  uint32_t* next = nullptr;
-  uint64_t* d_off = nullptr;
+  n_chunks = std::max(n_chunks, B.chunks);  // an arena that grew for earlier calls stays grown
+  const size_t clear_words = (size_t)slots2 * tsize + words;
   int rc = 0;
   auto fail = [&](const char* what, hipError_t e) { rc = set_error(-1, "%s: %s", what, hipGetErrorString(e)); };
-  hipError_t e;
-  if ((e = hipMalloc(&d_roots, n * sizeof(kg_set))) != hipSuccess) fail("hipMalloc", e);
-  if (!rc && (e = hipMalloc(&ctl, sizeof(ExpCtl))) != hipSuccess) fail("hipMalloc", e);
-  if (!rc && (e = hipMalloc(&outs, n * sizeof(RootOut))) != hipSuccess) fail("hipMalloc", e);
-  if (!rc && (e = hipMalloc(&stacks, (size_t)(slots1 + slots2 + 1) * stack_cap * sizeof(ExpFrame))) != hipSuccess)
-    fail("hipMalloc", e);
-  if (!rc && (e = hipMalloc(&p2, n * 8)) != hipSuccess) fail("hipMalloc", e);  // pass-2 | pass-3 queues
-  // [pass-2 tables | pass-3 bitmap] (cleared together every attempt) | pass-2 lists | pass-3 list
-  const size_t clear_words = (size_t)slots2 * tsize + words;
-  if (!rc && (e = hipMalloc(&bm, (clear_words + (size_t)slots2 * cap2 + nn) * 4)) != hipSuccess) fail("hipMalloc", e);
-  if (!rc) {
-    lists = bm + clear_words;
-    if ((e = hipMemcpyAsync(d_roots, roots, n * sizeof(kg_set), hipMemcpyHostToDevice, stream)) != hipSuccess)
-      fail("H2D", e);
-  }
-  ExpCtl h{};
-  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
-  for (auto& x : ev)
-    if (!rc && (e = hipEventCreate(&x)) != hipSuccess) fail("hipEventCreate", e);
-  for (int attempt = 0; !rc; attempt++) {
-    if (arena) hipFree(arena), arena = nullptr;
-    if (next) hipFree(next), next = nullptr;
-    if ((e = hipMalloc(&arena, (size_t)n_chunks * CHUNK * sizeof(kg_tree_node))) != hipSuccess) {
-      fail("hipMalloc(arena)", e);
-      break;
-    }
-    if ((e = hipMalloc(&next, (size_t)n_chunks * 4)) != hipSuccess) {
+  hipError_t e = hipSuccess;
+  if (n > B.n_cap) {
+    size_t a = 0, b = 0, c = 0;
+    const size_t cap = std::max(n, 2 * B.n_cap);
+    B.n_cap = 0;
+    if ((e = grow(&B.d_roots, a, cap * sizeof(kg_set))) != hipSuccess || (e = grow(&B.outs, b, cap * sizeof(RootOut))) != hipSuccess ||
+        (e = grow(&B.p2, c, cap * 8)) != hipSuccess)
       fail("hipMalloc", e);
-      break;
+    else
+      B.n_cap = cap;
+  }
+  if (!rc && !B.ctl && (e = hipMalloc(&B.ctl, sizeof(ExpCtl))) != hipSuccess) fail("hipMalloc", e);
+  if (!rc && (e = grow(&B.stacks, B.stacks_bytes, (size_t)(slots1 + slots2 + 1) * stack_cap * sizeof(ExpFrame))) != hipSuccess)
+    fail("hipMalloc", e);
+  if (!rc && (e = grow(&B.bm, B.bm_bytes, (clear_words + (size_t)slots2 * cap2 + nn) * 4)) != hipSuccess)
+    fail("hipMalloc", e);
+  for (auto& x : B.ev)
+    if (!rc && !x && (e = hipEventCreate(&x)) != hipSuccess) fail("hipEventCreate", e);
+  uint32_t* lists = B.bm + clear_words;
+  if (!rc && (e = hipMemcpyAsync(B.d_roots, roots, n * sizeof(kg_set), hipMemcpyHostToDevice, stream)) != hipSuccess)
+    fail("H2D", e);
+  ExpCtl h{};
+  for (int attempt = 0; !rc; attempt++) {
+    if (n_chunks > B.chunks) {
+      size_t a = 0, b = 0;
+      B.chunks = 0;
+      if ((e = grow(&B.arena, a, (size_t)n_chunks * CHUNK * sizeof(kg_tree_node))) != hipSuccess ||
+          (e = grow(&B.next, b, (size_t)n_chunks * 4)) != hipSuccess) {
+        fail("hipMalloc(arena)", e);
+        break;
+      }
+      B.chunks = n_chunks;
     }
     // every attempt starts from clear visited bitmaps (an arena overflow aborts roots mid-way)
-    if ((e = hipMemsetAsync(bm, 0, clear_words * 4, stream)) != hipSuccess ||
-        (e = hipMemsetAsync(ctl, 0, sizeof(ExpCtl), stream)) != hipSuccess) {
+    if ((e = hipMemsetAsync(B.bm, 0, clear_words * 4, stream)) != hipSuccess ||
+        (e = hipMemsetAsync(B.ctl, 0, sizeof(ExpCtl), stream)) != hipSuccess) {
       fail("memset", e);
       break;
     }
-    (void)hipEventRecord(ev[0], stream);
-    hipLaunchKernelGGL(k_expand_lds, dim3(grid1), dim3(256), 0, stream, s->ds, d_roots, (uint32_t)n, global, ctl, outs,
-                       arena, next, n_chunks, stacks, stack_cap, p2);
-    hipLaunchKernelGGL(k_expand_hash, dim3(slots2), dim3(64), 0, stream, s->ds, d_roots, global, ctl, outs, arena,
-                       next, n_chunks, stacks + (size_t)slots1 * stack_cap, stack_cap, p2, bm, tsize, lists, cap2, p2 + n);
-    hipLaunchKernelGGL(k_expand_hbm, dim3(1), dim3(64), 0, stream, s->ds, d_roots, global, ctl, outs, arena, next,
-                       n_chunks, stacks + (size_t)(slots1 + slots2) * stack_cap, p2 + n, bm + (size_t)slots2 * tsize,
-                       words, lists + (size_t)slots2 * cap2, nn);
-    (void)hipEventRecord(ev[1], stream);
+    (void)hipEventRecord(B.ev[0], stream);
+    hipLaunchKernelGGL(k_expand_lds, dim3(grid1), dim3(256), 0, stream, s->ds, B.d_roots, (uint32_t)n, global, B.ctl,
+                       B.outs, B.arena, B.next, n_chunks, B.stacks, stack_cap, B.p2);
+    hipLaunchKernelGGL(k_expand_hash, dim3(slots2), dim3(64), 0, stream, s->ds, B.d_roots, global, B.ctl, B.outs,
+                       B.arena, B.next, n_chunks, B.stacks + (size_t)slots1 * stack_cap, stack_cap, B.p2, B.bm, tsize,
+                       lists, cap2, B.p2 + n);
+    hipLaunchKernelGGL(k_expand_hbm, dim3(1), dim3(64), 0, stream, s->ds, B.d_roots, global, B.ctl, B.outs, B.arena,
+                       B.next, n_chunks, B.stacks + (size_t)(slots1 + slots2) * stack_cap, B.p2 + n,
+                       B.bm + (size_t)slots2 * tsize, words, lists + (size_t)slots2 * cap2, nn);
+    (void)hipEventRecord(B.ev[1], stream);
     if ((e = hipGetLastError()) != hipSuccess) {
       fail("launch", e);
       break;
     }
-    if ((e = hipMemcpyAsync(&h, ctl, sizeof h, hipMemcpyDeviceToHost, stream)) != hipSuccess ||
+    if ((e = hipMemcpyAsync(&h, B.ctl, sizeof h, hipMemcpyDeviceToHost, stream)) != hipSuccess ||
         (e = hipStreamSynchronize(stream)) != hipSuccess) {
       fail("expand", e);
       break;
@@ -437,8 +537,9 @@ int expand_batch(Snapshot* s, const kg_set* roots, size_t n, int32_t global, kg_
     n_chunks *= 4;  // grow the arena and rerun (outputs are rewritten from scratch)
   }
   std::vector<RootOut> ho(n);
-  if (!rc && (e = hipMemcpy(ho.data(), outs, n * sizeof(RootOut), hipMemcpyDeviceToHost)) != hipSuccess)
+  if (!rc && (e = hipMemcpyAsync(ho.data(), B.outs, n * sizeof(RootOut), hipMemcpyDeviceToHost, stream)) != hipSuccess)
     fail("D2H", e);
+  if (!rc && (e = hipStreamSynchronize(stream)) != hipSuccess) fail("D2H", e);
   if (!rc) {
     for (size_t r = 0; r < n; r++) {
       if (ho[r].count == 0xFFFFFFFFu) {
@@ -450,18 +551,21 @@ int expand_batch(Snapshot* s, const kg_set* roots, size_t n, int32_t global, kg_
   }
   const uint64_t total = rc ? 0 : out->root_off[n];
   if (!rc && total) {
-    out->nodes = (kg_tree_node*)malloc(total * sizeof(kg_tree_node));
-    if (!out->nodes) rc = set_error(-4, "host allocation failed");
-    if (!rc && (e = hipMalloc(&dst, total * sizeof(kg_tree_node))) != hipSuccess) fail("hipMalloc", e);
-    if (!rc && (e = hipMalloc(&d_off, (n + 1) * 8)) != hipSuccess) fail("hipMalloc", e);
-    if (!rc && (e = hipMemcpyAsync(d_off, out->root_off, (n + 1) * 8, hipMemcpyHostToDevice, stream)) != hipSuccess)
+    out->nodes = (kg_tree_node*)tree_pool_get(total * sizeof(kg_tree_node));
+    out->pinned = 1;
+    if (!out->nodes) rc = set_error(-4, "pinned host allocation failed");
+    if (!rc && (e = grow(&B.dst, B.dst_cap, std::max<size_t>(total, 2 * B.dst_cap / sizeof(kg_tree_node)) *
+                                                     sizeof(kg_tree_node))) != hipSuccess)
+      fail("hipMalloc", e);
+    if (!rc && (e = grow(&B.d_off, B.off_cap, (n + 1) * 8)) != hipSuccess) fail("hipMalloc", e);
+    if (!rc && (e = hipMemcpyAsync(B.d_off, out->root_off, (n + 1) * 8, hipMemcpyHostToDevice, stream)) != hipSuccess)
       fail("H2D", e);
     if (!rc) {
-      (void)hipEventRecord(ev[2], stream);
-      hipLaunchKernelGGL(k_expand_compact, dim3((uint32_t)((n + 3) / 4)), dim3(256), 0, stream, outs, (uint32_t)n,
-                         d_off, arena, next, dst);
-      (void)hipEventRecord(ev[3], stream);
-      if ((e = hipMemcpyAsync(out->nodes, dst, total * sizeof(kg_tree_node), hipMemcpyDeviceToHost, stream)) !=
+      (void)hipEventRecord(B.ev[2], stream);
+      hipLaunchKernelGGL(k_expand_compact, dim3((uint32_t)((n + 3) / 4)), dim3(256), 0, stream, B.outs, (uint32_t)n,
+                         B.d_off, B.arena, B.next, B.dst);
+      (void)hipEventRecord(B.ev[3], stream);
+      if ((e = hipMemcpyAsync(out->nodes, B.dst, total * sizeof(kg_tree_node), hipMemcpyDeviceToHost, stream)) !=
               hipSuccess ||
           (e = hipStreamSynchronize(stream)) != hipSuccess)
         fail("compact", e);
@@ -470,17 +574,12 @@ int expand_batch(Snapshot* s, const kg_set* roots, size_t n, int32_t global, kg_
   out->n_nodes = total;
   if (!rc) {
     float a = 0, b = 0;
-    (void)hipEventElapsedTime(&a, ev[0], ev[1]);
-    if (total) (void)hipEventElapsedTime(&b, ev[2], ev[3]);
+    (void)hipEventElapsedTime(&a, B.ev[0], B.ev[1]);
+    if (total) (void)hipEventElapsedTime(&b, B.ev[2], B.ev[3]);
     out->kernel_ms = (double)a + (double)b;
   }
-  for (auto& x : ev)
-    if (x) (void)hipEventDestroy(x);
-  for (void* p : {(void*)d_roots, (void*)ctl, (void*)outs, (void*)stacks, (void*)p2, (void*)bm, (void*)arena,
-                  (void*)next, (void*)dst, (void*)d_off})
-    if (p) (void)hipFree(p);
   if (rc) {
-    free(out->nodes);
+    if (out->pinned) tree_pool_put(out->nodes, total * sizeof(kg_tree_node));
     free(out->root_off);
     memset(out, 0, sizeof *out);
   }

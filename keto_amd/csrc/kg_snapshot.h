@@ -100,6 +100,7 @@ struct Lane {
   uint8_t* d_out = nullptr;
   uint32_t* d_err = nullptr;
   size_t cap = 0;
+  void* exp = nullptr;  // expand buffers of this lane (kg_expand.hip)
   int reserve(size_t n);
   ~Lane();
 };
@@ -207,6 +208,11 @@ int shard_finish(Snapshot* s, size_t n, uint8_t* d_res, const uint32_t* d_err, h
 // kg_grid.hip
 int grid_reserve(Snapshot* s);  // allocates the shared full-size grid pool now (kg_snapshot_tune "grid_reserve")
 // kg_expand.hip
-int expand_batch(Snapshot* s, const kg_set* roots, size_t n, int32_t global, kg_tree_buf* out);
+// runs on `stream` with the lane's cached device buffers (*bufs, created on first use)
+int expand_batch(Snapshot* s, hipStream_t stream, void** bufs, const kg_set* roots, size_t n, int32_t global,
+                 kg_tree_buf* out);
+void expand_bufs_free(void* bufs);
+void* tree_pool_get(size_t bytes);  // pinned host memory for tree outputs (kg_tree_free returns it)
+void tree_pool_put(void* p, size_t bytes);
 
 }  // namespace kg

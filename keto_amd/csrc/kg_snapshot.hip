@@ -265,6 +265,7 @@ Lane::~Lane() {
   if (d_q) hipFree(d_q);
   if (d_out) hipFree(d_out);
   if (d_err) hipFree(d_err);
+  if (exp) expand_bufs_free(exp);
   // the stream's workspace belongs to the replica (freed with it); the stream itself is ours
   if (stream) hipStreamDestroy(stream);
 }
