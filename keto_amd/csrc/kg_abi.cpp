@@ -293,7 +293,7 @@ static int tune_one(Snapshot* s, const char* key, int64_t value) {
     return 0;
   }
   if (strcmp(key, "stream") == 0) {
-    if (value < 0 || value > 9) return set_error(-2, "stream must be in [0, 9]");
+    if (value < 0 || value > 10) return set_error(-2, "stream must be in [0, 10]");
     s->stream_variant = (int)value;
     return 0;
   }

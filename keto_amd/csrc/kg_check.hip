@@ -983,6 +983,280 @@ __global__ __launch_bounds__(256) void k_stream2(DevSnap s, const RQuery* __rest
   block_stats<7>(ctl, idx, v);
 }
 
+// ------------------------------------------------------------------ k_stream3 (variant 10)
+// k_stream2 software-pipelined by one step.  k_stream2's step is: take a window of 64 edges at the
+// FIFO head -> gather their adjx records (and probe the previous step's children) -> wait -> process
+// the children; the gather latency and the child processing add up.  Here iteration i takes window
+// i+1 from the FIFO and issues its gathers (with the probes of window i-1's children) BEFORE
+// processing window i, whose records arrived during the previous iteration, so the LDS / DPP work
+// of a step runs under the memory latency of the next.  Window i+1 is cut from the FIFO before
+// window i's children are appended (so it can be shorter than 64 edges when the FIFO runs low);
+// its entries' query counts are released only once their children have been processed, and every
+// child is re-checked against its slot's current generation at processing time, so a query that
+// finished (hit / overflow) or a slot refilled in between never sees stale appends.
+template <int VLOG2, int QC, int CHUNK, int INS_CAP>
+__global__ __launch_bounds__(256) void k_stream3(DevSnap s, const RQuery* __restrict__ rq, WorkList wl, uint32_t* heads,
+                                                 uint8_t* __restrict__ out, uint32_t* next_list, uint32_t* next_count,
+                                                 Ctl* ctl) {
+  using Lds = Stream2Lds<VLOG2, QC>;
+  constexpr uint32_t VT = 1u << VLOG2;
+  static_assert(QC <= 256 && (QC & (QC - 1)) == 0, "FIFO ring of <= 256 entries (9-bit generations stay unique)");
+  static_assert(CHUNK <= 64, "one chunk entry per lane");
+  const uint64_t t_start = wall_clock64();
+  __shared__ Lds lds_all[4];
+  Lds& L = lds_all[threadIdx.x >> 6];
+  const int lane = lane_id();
+  const uint32_t head0 = blockIdx.x & 7;
+  uint32_t head_sel = head0;
+  for (uint32_t i = lane; i < VT; i += 64) L.vt[i] = 0ull;
+  if (lane < 32) {
+    L.s_state[lane] = 0;
+    L.s_cnt[lane] = 0;
+    L.s_ins[lane] = 0;
+  }
+  if (lane == 0) L.pref[64] = 0;
+  __builtin_amdgcn_wave_barrier();
+  uint32_t active = 0;
+  bool drained = false;
+  uint32_t c_left = 0, c_pos = 0;
+  uint32_t cq_qi = 0, cq_node = 0, cq_subj = 0, cq_beg = 0, cq_len = 0;
+  int32_t cq_depth = 0;
+  uint32_t head = 0, tail = 0, head_off = 0;
+  bool pend = false;
+  uint32_t pend_node = 0, pend_slot = 0, pend_gen = 0;
+  // the probes issued last iteration, applied this one (their bucket lands during this step)
+  bool q_valid = false;
+  uint64_t q_key = 0;
+  ulonglong2 q_a = make_ulonglong2(EMPTY64, EMPTY64);
+  uint32_t q_slot = 0, q_gen = 0, q_node = 0, q_subj = 0;
+  // the window gathered last iteration, processed this one: per edge lane its record and owner meta,
+  // per entry lane the slot | generation whose count it releases (NONE = nothing)
+  bool cur_act = false;
+  AdjX cur_x{NONE, 0, 0, 0};
+  uint32_t cur_om = 0, cur_dec = NONE, cur_taken = 0;
+  unsigned long long st_rows = 0, st_edges = 0, st_probes = 0, st_done = 0, st_steps = 0;
+  for (;;) {
+    // ---- refill free slots (their root entries need FIFO room)
+    const uint32_t freem = ~active;
+    const uint32_t want = __popc(freem);
+    if (want && !drained && (tail - head) + want <= QC) {
+      if (c_left == 0) {
+        uint32_t got = 0, first = 0;
+        if (lane == 0) first = dequeue_n(wl, heads, head_sel, head0, CHUNK, got);
+        first = __shfl(first, 0, 64);
+        c_left = __shfl(got, 0, 64);
+        c_pos = 0;
+        if (first == NONE) {
+          drained = true;
+        } else if ((uint32_t)lane < c_left) {
+          cq_qi = wl.list[first + lane];
+          const RQuery q = rq[cq_qi];
+          cq_node = q.node;
+          cq_subj = q.subj;
+          cq_depth = q.depth;
+          cq_beg = q.beg;
+          cq_len = q.len;
+        }
+      }
+      const uint32_t got = min(want, c_left);
+      if (got) {
+        const uint32_t r = __popc(freem & (lane < 32 ? (1u << lane) - 1u : 0xFFFFFFFFu));
+        const bool mine = lane < 32 && ((freem >> (lane & 31)) & 1u) && r < got;
+        const int src = mine ? (int)(c_pos + r) : lane;
+        const uint32_t qi = __shfl(cq_qi, src, 64), qnode = __shfl(cq_node, src, 64), qsubj = __shfl(cq_subj, src, 64),
+                       qbeg = __shfl(cq_beg, src, 64), qlen = __shfl(cq_len, src, 64);
+        const int32_t qdepth = __shfl(cq_depth, src, 64);
+        c_pos += got;
+        c_left -= got;
+        if (mine) {
+          const uint32_t slot = lane, gen = L.s_state[slot] & S2_GEN;
+          const bool over = qdepth > (int32_t)S2_DMAX || qlen > S2_LONG;
+          L.s_qi[slot] = qi;
+          L.s_subj[slot] = qsubj;
+          L.s_sig[slot] = subj_sig(qsubj);
+          L.s_cnt[slot] = 1;
+          L.s_ins[slot] = 0;
+          L.s_state[slot] = over ? (gen | S2_OVER) : gen;
+          const unsigned long long key =
+              (1ull << 63) | ((unsigned long long)gen << 37) | ((unsigned long long)slot << 32) | qnode;
+          L.vt[((qnode * 0x9E3779B1u) ^ (slot * 0x85EBCA77u) ^ (gen * 0xC2B2AE3Du)) >> (32 - VLOG2)] = key;
+          const uint32_t at = (tail + r) & (QC - 1);
+          L.e_beg[at] = qbeg;
+          L.e_meta[at] = s2_meta(over ? 0u : qlen, slot, gen, over ? 2u : (uint32_t)qdepth);
+        }
+        active |= (uint32_t)__ballot(mine);
+        tail += got;
+      }
+    }
+    if (active == 0 && ((drained && c_left == 0) || tail == head)) {
+      if (drained && c_left == 0) break;
+      cur_act = false;  // nothing live: a gathered window and probes in flight can only be stale
+      cur_dec = NONE;
+      cur_taken = 0;
+      q_valid = false;
+      continue;
+    }
+    __builtin_amdgcn_wave_barrier();
+    // ---- next window (up to 64 edges from the FIFO head): consume, then issue its gathers.  Taken
+    // before the current window is processed when the FIFO already holds a full window (the gathers
+    // then fly under this step's processing), else after it, so that the children appended this
+    // step fill the window (k_stream2's order for that step)
+    bool nxt_act = false;
+    AdjX nxt_x{NONE, 0, 0, 0};
+    uint32_t nxt_om = 0, nxt_dec = NONE, taken = 0;
+    auto take_window = [&]() {
+      const uint32_t avail = tail - head;
+      uint32_t ebeg = 0, elen = 0, emeta = 0;
+      bool live = false;
+      if ((uint32_t)lane < avail) {
+        const uint32_t at = (head + lane) & (QC - 1);
+        emeta = L.e_meta[at];
+        ebeg = L.e_beg[at];
+        const uint32_t sl = (emeta >> 11) & 31u;
+        const uint32_t st = L.s_state[sl];
+        live = ((active >> sl) & 1u) && (st == ((emeta >> 16) & S2_GEN));
+        elen = live ? (emeta & 0x7FFu) : 0u;
+        if (lane == 0) {
+          ebeg += head_off;
+          elen = live ? elen - head_off : 0u;
+        }
+      }
+      uint32_t total;
+      const uint32_t excl = wave_excl_scan(elen, &total);
+      L.pref[lane] = 0;
+      __builtin_amdgcn_wave_barrier();
+      taken = min(total, 64u);
+      L.pref[(elen > 0 && excl < taken) ? excl : 64u] = (uint32_t)lane + 1;
+      const bool consumed = (uint32_t)lane < avail && excl + elen <= taken;
+      const uint32_t ncons = __popcll(__ballot(consumed));
+      // released after processing: slot | generation << 5 (NONE = nothing)
+      nxt_dec = (consumed && live) ? (((emeta >> 11) & 31u) | (((emeta >> 16) & S2_GEN) << 5)) : NONE;
+      st_rows += (consumed && live) ? 1u : 0u;
+      {
+        const uint32_t ex_n = (uint32_t)__builtin_amdgcn_readlane((int)excl, ncons & 63);
+        if (ncons < avail && ncons < 64 && ex_n < taken) head_off = (ncons == 0 ? head_off : 0u) + (taken - ex_n);
+        else if (ncons > 0) head_off = 0;
+      }
+      __builtin_amdgcn_wave_barrier();
+      nxt_act = (uint32_t)lane < taken;
+      const int own = ((int)wave_incl_scan<DppMax>(L.pref[lane]) - 1) & 63;
+      const uint32_t ob = __shfl(ebeg, own, 64);
+      nxt_om = __shfl(emeta, own, 64);
+      const uint32_t ox = __shfl(excl, own, 64);
+      if (nxt_act) nxt_x = s.adjx[ob + ((uint32_t)lane - ox)];  // waited on where it is processed
+      head += ncons;
+      st_edges += (lane == 0) ? taken : 0u;
+    };
+    // a full window is waiting in the FIFO (cheap test: at least 64 entries, or the live edge count)
+    bool early = (tail - head) >= 64u || cur_taken == 0;
+    if (!early) {
+      uint32_t el = 0;
+      if ((uint32_t)lane < tail - head) {
+        const uint32_t em = L.e_meta[(head + lane) & (QC - 1)];
+        el = (L.s_state[(em >> 11) & 31u] == ((em >> 16) & S2_GEN)) ? (em & 0x7FFu) : 0u;
+      }
+      uint32_t tot;
+      (void)wave_excl_scan(el, &tot);
+      early = tot >= 64u + head_off;
+    }
+    if (early) take_window();
+    st_steps += (lane == 0) ? 1u : 0u;
+    // ---- the previous window's children: their first probe bucket is loaded now and evaluated next
+    // iteration (in flight with the gathers above and the whole of this step)
+    const bool pvalid = pend && L.s_state[pend_slot] == pend_gen;
+    const uint32_t psubj = L.s_subj[pend_slot];
+    const uint32_t pend_gen_issued = pend_gen, pnode_issued = pend_node, probe_slot = pend_slot;
+    const uint64_t pkey = dset_key(pend_node, psubj);
+    ulonglong2 pa = make_ulonglong2(EMPTY64, EMPTY64);
+    if (pvalid) pa = *reinterpret_cast<const ulonglong2*>(s.dset + hash_home(pkey, s.dset_nb) * DSET_BUCKET);
+    st_probes += pvalid ? 1u : 0u;
+    // ---- process the current window (gathered last iteration)
+    const uint32_t slot = (cur_om >> 11) & 31u, d = cur_om >> 25, g = (cur_om >> 16) & S2_GEN;
+    const bool clive = cur_act && L.s_state[slot] == g;  // the query still runs in this slot
+    const bool keepc = clive && d >= 3 && cur_x.len > 0;
+    const bool longrow = keepc && cur_x.len > S2_LONG;
+    const unsigned long long key =
+        (1ull << 63) | ((unsigned long long)g << 37) | ((unsigned long long)slot << 32) | cur_x.node;
+    const uint32_t hv = ((cur_x.node * 0x9E3779B1u) ^ (slot * 0x85EBCA77u) ^ (g * 0xC2B2AE3Du)) >> (32 - VLOG2);
+    const unsigned long long old = keepc ? L.vt[hv] : 0ull;
+    const bool fresh = keepc && !longrow && old != key;
+    if (fresh) L.vt[hv] = key;
+    const uint32_t k = fresh ? atomicAdd(&L.s_ins[slot], 1u) : 0u;
+    const bool ok = fresh && k < (uint32_t)INS_CAP;
+    const uint64_t am = __ballot(ok);
+    const uint32_t room = QC - (tail - head);
+    const uint32_t pos = __popcll(am & ((1ull << lane) - 1));
+    const bool appended = ok && pos < room;
+    if (appended) {
+      const uint32_t at = (tail + pos) & (QC - 1);
+      L.e_beg[at] = cur_x.begin;
+      L.e_meta[at] = cur_x.len | (cur_om & 0x01FFF800u) | ((d - 1) << 25);
+      atomicAdd(&L.s_cnt[slot], 1u);
+    }
+    if (longrow || (fresh && !appended)) atomicOr(&L.s_state[slot], S2_OVER);
+    tail += min((uint32_t)__popcll(am), room);
+    {  // last iteration's probes: a chain past a full first bucket (rare) is walked here
+      bool h = false, more = false;
+      if (q_valid) {
+        h = q_a.x == q_key || q_a.y == q_key;
+        more = !h && q_a.y != EMPTY64;
+      }
+      if (__ballot(more)) {
+        if (more) h = dset_probe(s, q_node, q_subj);
+      }
+      if (h && L.s_state[q_slot] == q_gen) atomicOr(&L.s_state[q_slot], S2_HIT);  // same query still there
+    }
+    // its consumed entries release their query's count now that their children are accounted for
+    // (a finished / refilled slot's count is not touched: its generation moved on)
+    if (cur_dec != NONE && L.s_state[cur_dec & 31u] == (cur_dec >> 5)) atomicSub(&L.s_cnt[cur_dec & 31u], 1u);
+    pend = clive && (keepc ? appended : true) && sig_maybe(cur_x.sig, L.s_sig[slot]);
+    pend_node = cur_x.node;
+    pend_slot = slot;
+    pend_gen = g;
+    if (!early) take_window();  // deferred: the children appended above join this window
+    // ---- finished queries
+    const uint32_t pslots = wave_or((pend ? 1u << slot : 0u) | (pvalid ? 1u << probe_slot : 0u));
+    __builtin_amdgcn_wave_barrier();
+    bool done = false;
+    if (lane < 32 && ((active >> lane) & 1u)) {
+      const uint32_t st = L.s_state[lane];
+      if (st & S2_HIT) {
+        done = true;
+        out[L.s_qi[lane]] = KG_IS_MEMBER;
+        st_done++;
+      } else if (st & S2_OVER) {
+        done = true;
+        next_list[atomicAdd(next_count, 1u)] = L.s_qi[lane];
+      } else if (L.s_cnt[lane] == 0 && !((pslots >> lane) & 1u)) {
+        done = true;
+        st_done++;
+      }
+      if (done) L.s_state[lane] = ((st & S2_GEN) + 1u) & S2_GEN;
+    }
+    const uint32_t freed = (uint32_t)__ballot(done);
+    active &= ~freed;
+    if (pend && ((freed >> pend_slot) & 1u)) pend = false;
+    // ---- rotate: the next window becomes the current one, this step's probes the ones to apply
+    q_valid = pvalid && !((freed >> probe_slot) & 1u);
+    q_key = pkey;
+    q_a = pa;
+    q_slot = probe_slot;
+    q_gen = pend_gen_issued;
+    q_node = pnode_issued;
+    q_subj = psubj;
+    cur_act = nxt_act;
+    cur_x = nxt_x;
+    cur_om = nxt_om;
+    cur_dec = nxt_dec;
+    cur_taken = taken;
+    __builtin_amdgcn_wave_barrier();
+  }
+  const unsigned long long life = lane == 0 ? wall_clock64() - t_start : 0ull;
+  const int idx[7] = {ST_LROWS, ST_LEDGES, ST_LPROBES, ST_LIGHT, ST_LSTEPS, ST_LWAVES, ST_LTICKS};
+  const unsigned long long v[7] = {st_rows, st_edges, st_probes, st_done, st_steps, lane == 0 ? 1ull : 0ull, life};
+  block_stats<7>(ctl, idx, v);
+}
+
 // ------------------------------------------------------------------ workgroup tiers
 // Queries whose visited set outgrew one wave's LDS: one 256-lane workgroup per query, same BFS.
 //   k_wg<WgLds>  visited hash (8192 slots) + BFS list (4096) in LDS          ("medium")
@@ -1552,7 +1826,7 @@ int check_batch_begin(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n, 
       //   7: as 5 with <= 64 per query   8: as 7 with a 512-key table (~45 KiB)
       const int sv = s->stream_variant;
       const uint32_t per_cu =
-          s->stream_wgs ? (uint32_t)s->stream_wgs : ((sv == 0 || sv == 1 || sv == 3 || sv == 9) ? 5u : 3u);
+          s->stream_wgs ? (uint32_t)s->stream_wgs : ((sv == 0 || sv == 1 || sv == 3 || sv >= 9) ? 5u : 3u);
       const uint32_t ecap = s->stream_ecap ? s->stream_ecap : 0xFFFFFFFFu;
       const uint32_t grid = (uint32_t)std::min<uint64_t>((uint64_t)s->n_cu * per_cu, (n + 31) / 32 + 8);
       using V0 = SlotVis<8, 7>;
@@ -1577,6 +1851,9 @@ int check_batch_begin(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n, 
       else if (sv == 8) KG_STREAM(32, V8, 256, 64);
       else if (sv == 9)
         hipLaunchKernelGGL((k_stream2<9, 256, 64, 64>), dim3(grid), dim3(256), 0, stream, s->ds, rq, wl, ctl->heads,
+                           d_out, ovf_list, ovf_count, ctl);
+      else if (sv == 10)
+        hipLaunchKernelGGL((k_stream3<9, 256, 64, 64>), dim3(grid), dim3(256), 0, stream, s->ds, rq, wl, ctl->heads,
                            d_out, ovf_list, ovf_count, ctl);
       else KG_STREAM(8, V0, 256, 16);
 #undef KG_STREAM

@@ -52,16 +52,17 @@ def random_queries(rng, nss, rels, n, n_obj=60, n_users=40, p_setq=0.15):
     return qs
 
 
-@pytest.mark.parametrize("seed", range(13))
+@pytest.mark.parametrize("seed", range(16))
 def test_random_graphs_vs_oracle(seed):
     rng = np.random.default_rng(seed)
     it, tuples, nss, rels = random_graph(rng, n_obj=40 + 20 * (seed % 6), n_rows=200 + 150 * (seed % 6))
     reg = Registry(tuples, [], interner=it)
     # first wave tier: k_stream variants 0..8 (seeds 0-6 and 8-9 -> variants 0-6, 7, 8; seed 2 with a
     # tiny per-query edge budget, so queries overflow into the next tiers mid-search), k_light<16>
-    # (seed 7) and k_stream2 (seeds 10-12, the default; seed 12 on a graph of long rows and cycles)
+    # (seed 7), k_stream2 (seeds 10-12, the default; seed 12 on a graph of long rows and cycles) and the
+    # software-pipelined k_stream3 (seeds 13-15)
     reg.snapshot.tune("light", 1 if seed == 7 else 0)
-    reg.snapshot.tune("stream", seed % 7 if seed < 7 else (seed - 1 if seed < 10 else 9))
+    reg.snapshot.tune("stream", seed % 7 if seed < 7 else (seed - 1 if seed < 10 else (9 if seed < 13 else 10)))
     reg.snapshot.tune("stream_ecap", 6 if seed == 2 else 0)
     qs = random_queries(rng, nss, rels, 3000, n_obj=40 + 20 * (seed % 6))
     depths = rng.integers(-1, 9, len(qs))
@@ -80,7 +81,7 @@ def test_random_graphs_vs_oracle(seed):
         assert (out[inv] == dfs[inv]).all()
 
 
-@pytest.mark.parametrize("variant", [8, 9])
+@pytest.mark.parametrize("variant", [8, 9, 10])
 def test_stream_tier_long_rows_and_dense_cycles(variant):
     """Rows longer than a FIFO entry holds (k_stream2: 2047 edges), dense cycles (the direct-mapped
     visited cache evicts and re-expands), many queries per wave on one hub: exact vs the oracle."""
@@ -188,12 +189,13 @@ def _torch():
     return torch
 
 
-@pytest.mark.parametrize("n_tuples,gmax", [(200_000, 10), (300_000, 5)])
-def test_synthetic_graph_vs_oracle(n_tuples, gmax):
+@pytest.mark.parametrize("n_tuples,gmax,variant", [(200_000, 10, 9), (300_000, 5, 9), (300_000, 10, 10)])
+def test_synthetic_graph_vs_oracle(n_tuples, gmax, variant):
     torch = _torch()
     from keto_amd import _lib
     snap = Snapshot.synthetic(n_tuples, seed=20250131)
     snap.tune("tiers", 1 if gmax == 5 else 0)
+    snap.tune("stream", variant)
     n = 20000
     dq = torch.empty((n, 7), dtype=torch.int32, device="cuda")
     _lib.check(_lib.load().kg_synth_queries(snap.handle, 7, n, dq.data_ptr()), "kg_synth_queries")
