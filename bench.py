@@ -78,7 +78,7 @@ def parse():
                     help="CPU-baseline threads (0 = os.cpu_count(), also timed at the affinity count, 16 and 1)")
     ap.add_argument("--preset", type=int, default=0,
                     help="0 = C2/C4 rewrite-free (headline); 1 = C3 (OPL view/edit/share via the rewrite interpreter)")
-    ap.add_argument("--mode", choices=["check", "expand", "sharded", "host"], default="check",
+    ap.add_argument("--mode", choices=["check", "expand", "sharded", "host", "refresh"], default="check",
                     help="expand = config C5: batched BuildTree of hot group#member roots; sharded = the "
                          "hash-sharded mode (each rank holds 1/N of the graph, all-to-all frontier exchange); "
                          "host = the host-buffer boundary end to end: kg_check_batch over a snapshot replicated "
@@ -88,6 +88,7 @@ def parse():
                     help="--mode host: native caller threads of the request batcher (one blocking call per request)")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for --mode sharded (nccl = RCCL)")
     ap.add_argument("--roots", type=int, default=100_000, help="expand roots per step (C5)")
+    ap.add_argument("--delta", type=int, default=1000, help="--mode refresh: rows per transaction")
     return ap.parse_args()
 
 
@@ -160,6 +161,69 @@ def bench_expand(a):
                                    "max": int(sz.max()), "roots_over_512": int((sz > 512).sum()),
                                    "top10_share": float(np.sort(sz)[-10:].sum() / max(1, sz.sum()))}
     print(json.dumps(out), flush=True)
+
+
+def bench_refresh(a):
+    """Incremental snapshot refresh (kg_snapshot_apply): on a synthetic graph of
+    --tuples (default 1e7), transactions of --delta rows (half inserts -- new doc#viewer@user and
+    group#member@group#member rows -- half deletes of existing rows), each applied to the latest
+    snapshot, then a 1 M-check batch on the refreshed snapshot.  Reports the commit -> snapshot-ready
+    latency (host delta handling + device rebuild) next to a full rebuild of the same graph."""
+    import torch
+    from keto_amd import _lib
+    from keto_amd.engine import Snapshot
+    L = _lib.load()
+    torch.cuda.set_device(0)
+    t0 = time.perf_counter()
+    base = Snapshot.synthetic(int(a.tuples), seed=a.seed, device=0)
+    t_full = time.perf_counter() - t0
+    ids = base.synth_ids()
+    rows = base.export()  # (n, 6) uint32, shard order
+    rng = np.random.default_rng(a.seed)
+    n_docs, n_groups, n_users = ids["n_docs"], ids["n_groups"], ids["n_users"]
+    half = a.delta // 2
+
+    def delta():
+        ins = np.zeros((half, 6), np.uint32)
+        k = rng.random(half) < 0.5
+        ins[:, 0] = np.where(k, 0, 1)                                   # doc / group
+        ins[:, 1] = np.where(k, rng.integers(0, n_docs, half), n_docs + rng.integers(0, n_groups, half))
+        ins[:, 2] = np.where(k, 1, 2)                                   # viewer / member
+        ins[:, 3] = np.where(k, _lib.KG_SUBJECT_ID, 1)
+        ins[:, 4] = np.where(k, ids["user_obj0"] + rng.integers(0, n_users, half), n_docs + rng.integers(0, n_groups, half))
+        ins[:, 5] = np.where(k, 0, 2)
+        dels = rows[rng.integers(0, len(rows), a.delta - half)]
+        return ins, dels
+
+    cur = base.apply(*delta())  # warm-up: the first apply builds the host node map from the device
+    dq = torch.empty((a.batch, 7), dtype=torch.int32, device="cuda")
+    _lib.check(L.kg_synth_queries(base.handle, 99, a.batch, dq.data_ptr()), "kg_synth_queries")
+    out = torch.empty(a.batch, dtype=torch.uint8, device="cuda")
+    err = torch.empty(a.batch, dtype=torch.int32, device="cuda")
+    lat, chk = [], []
+    for _ in range(a.steps):
+        ins, dels = delta()
+        s0 = time.perf_counter()
+        nxt = cur.apply(ins, dels)
+        s1 = time.perf_counter()
+        _lib.check(L.kg_check_batch_device(nxt.handle, dq.data_ptr(), a.batch, a.global_depth, out.data_ptr(),
+                                           err.data_ptr(), None, None), "kg_check_batch_device")
+        torch.cuda.synchronize()
+        s2 = time.perf_counter()
+        lat.append((s1 - s0) * 1e3)
+        chk.append((s2 - s1) * 1e3)
+        cur = nxt  # the previous snapshot is released here (no batch reads it any more)
+    info = cur.info()
+    res = {"metric": "snapshot refresh latency (commit -> snapshot ready, kg_snapshot_apply)",
+           "value": float(np.percentile(lat, 50)), "unit": "ms", "n_gpus": 1, "steps": a.steps, "warmup": 1,
+           "ms_per_step": float(np.mean(lat)), "higher_is_better": False, "dtype": "u32",
+           "data": "synthetic (device-generated, seed %d) + random deltas" % a.seed,
+           "config": {"workload": "%d-row transactions (%d inserts, %d deletes) on %.3g tuples" %
+                      (a.delta, half, a.delta - half, a.tuples), "rows": info["rows"], "nodes": info["nodes"]},
+           "apply_ms": {"p50": float(np.percentile(lat, 50)), "p99": float(np.percentile(lat, 99)),
+                        "max": float(np.max(lat))},
+           "first_check_batch_ms": float(np.percentile(chk, 50)), "full_build_s": t_full}
+    print(json.dumps(res), flush=True)
 
 
 def bench_sharded(a):
@@ -379,13 +443,15 @@ def main():
     if a.hw_queues > 0:  # before anything initialises HIP (torch and the library load lazily)
         os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, a.hw_queues))
     if a.tuples is None:
-        a.tuples = 2e6 if a.heavy_tail else 1e9
+        a.tuples = 2e6 if a.heavy_tail else (1e7 if a.mode == "refresh" else 1e9)
     if a.mode == "expand":
         return bench_expand(a)
     if a.mode == "sharded":
         return bench_sharded(a)
     if a.mode == "host":
         return bench_host(a)
+    if a.mode == "refresh":
+        return bench_refresh(a)
     import torch
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))

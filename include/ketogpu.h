@@ -165,6 +165,20 @@ typedef struct {
  * every GPU of the node.  Replicas are built concurrently. */
 int kg_snapshot_create(const kg_tuple* rows, size_t n, const kg_dict* dict, const kg_rewrite_prog* prog,
                        int device_mask, kg_snapshot** out);
+/* Rows with an order key each (ascending: the persister's shard ids, relationtuples.go:203-244
+ * ORDER BY shard_id), kept per row so kg_snapshot_apply can place inserted rows in key order. */
+int kg_snapshot_create_ordered(const kg_tuple* rows, const uint64_t* keys, size_t n, const kg_dict* dict,
+                               const kg_rewrite_prog* prog, const int* devices, int n_devices, kg_snapshot** out);
+/* Incremental refresh (TransactRelationTuples, internal/persistence/sql/relationtuples.go:260-270):
+ * *out = base's rows, minus every row equal to a tuple in del (:164-185; deletes apply to base
+ * rows), plus ins (ins_keys: their order keys, or NULL = after the node's existing rows).  Only the
+ * delta is handled on the host; rows and every derived structure are rebuilt on the device, replica
+ * by replica.  The base stays valid (in-flight batches keep reading it) but hands its host node map
+ * on to *out: apply the next delta to *out, not to base (a second apply on the same base rebuilds
+ * the map from the device).  Not concurrently on one base. */
+int kg_snapshot_apply(kg_snapshot* base, const kg_tuple* ins, const uint64_t* ins_keys, size_t n_ins,
+                      const kg_tuple* del, size_t n_del, const kg_dict* dict, const kg_rewrite_prog* prog,
+                      kg_snapshot** out);
 /* The same with an explicit device list; entries may repeat (several replicas on one device). */
 int kg_snapshot_create_on(const kg_tuple* rows, size_t n, const kg_dict* dict, const kg_rewrite_prog* prog,
                           const int* devices, int n_devices, kg_snapshot** out);

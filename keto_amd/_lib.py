@@ -75,6 +75,7 @@ class kg_synth_params(C.Structure):
 # every symbol include/ketogpu.h declares
 EXPORTS = ["kg_snapshot_create", "kg_snapshot_create_on", "kg_snapshot_synthetic", "kg_snapshot_synthetic_on",
            "kg_snapshot_replicas", "kg_snapshot_destroy", "kg_snapshot_info", "kg_snapshot_materialized", "kg_snapshot_tune", "kg_synth_ids",
+           "kg_snapshot_create_ordered", "kg_snapshot_apply",
            "kg_snapshot_export", "kg_snapshot_export_csr", "kg_check_batch", "kg_check_batch_device", "kg_synth_queries", "kg_expand_batch",
            "kg_tree_free", "kg_last_error", "kg_version", "kg_shard_owner", "kg_snapshot_create_shard",
            "kg_snapshot_synthetic_shard", "kg_shard_seed", "kg_shard_level", "kg_shard_finish",
@@ -113,6 +114,8 @@ def load(path: str = LIB_PATH):
     L.kg_snapshot_destroy.argtypes = [vp]
     L.kg_snapshot_destroy.restype = None
     L.kg_snapshot_info.argtypes = [vp, vp]
+    L.kg_snapshot_create_ordered.argtypes = [vp, vp, sz, vp, vp, vp, C.c_int, vp]
+    L.kg_snapshot_apply.argtypes = [vp, vp, vp, sz, vp, sz, vp, vp, vp]
     L.kg_snapshot_materialized.argtypes = [vp, vp]
     L.kg_synth_ids.argtypes = [vp, vp]
     L.kg_snapshot_tune.argtypes = [vp, C.c_char_p, C.c_int64]
@@ -149,7 +152,8 @@ def load(path: str = LIB_PATH):
     L.kg_batcher_destroy.argtypes = [vp]
     L.kg_batcher_destroy.restype = None
     for name in ("kg_snapshot_create", "kg_snapshot_create_on", "kg_snapshot_synthetic", "kg_snapshot_synthetic_on",
-                 "kg_snapshot_replicas", "kg_snapshot_info", "kg_snapshot_materialized", "kg_snapshot_tune", "kg_synth_ids", "kg_check_batch",
+                 "kg_snapshot_replicas", "kg_snapshot_info", "kg_snapshot_materialized", "kg_snapshot_tune",
+                 "kg_snapshot_create_ordered", "kg_snapshot_apply", "kg_synth_ids", "kg_check_batch",
                  "kg_check_batch_device", "kg_synth_queries", "kg_expand_batch", "kg_snapshot_create_shard",
                  "kg_snapshot_synthetic_shard", "kg_shard_seed", "kg_shard_level", "kg_shard_finish",
                  "kg_shard_done", "kg_shard_held_words", "kg_shard_held", "kg_batcher_create", "kg_batcher_check", "kg_batcher_stats"):

@@ -72,7 +72,7 @@ std::vector<int> mask_devices(int device_mask) {
 
 // Builds one replica per entry of devs (entries may repeat: several replicas on one device),
 // concurrently, one host thread per replica; replica 0 owns the others.
-int build_replicas(const int* devs, int n_dev, const std::function<int(Snapshot*)>& build, kg_snapshot** out) {
+int build_replicas(const int* devs, int n_dev, const std::function<int(Snapshot*, int)>& build, kg_snapshot** out) {
   if (!out) return set_error(-2, "out is NULL");
   *out = nullptr;
   if (!devs || n_dev < 1 || n_dev > 64) return set_error(-2, "between 1 and 64 devices");
@@ -84,7 +84,7 @@ int build_replicas(const int* devs, int n_dev, const std::function<int(Snapshot*
       Snapshot* s = new Snapshot();
       reps[i] = s;
       int rc = s->init_device(devs[i]);
-      if (!rc) rc = build(s);
+      if (!rc) rc = build(s, i);
       rcs[i] = rc;
       if (rc) {
         char buf[1024];
@@ -120,8 +120,33 @@ int kg_snapshot_create_on(const kg_tuple* rows, size_t n, const kg_dict* dict, c
                           const int* devices, int n_devices, kg_snapshot** out) {
   KG_GUARD_BEGIN
   if (n && !rows) return set_error(-2, "rows is NULL");
-  return build_replicas(devices, n_devices, [&](Snapshot* s) { return s->create_from_tuples(rows, n, dict, prog); },
+  return build_replicas(devices, n_devices, [&](Snapshot* s, int) { return s->create_from_tuples(rows, n, dict, prog); },
                         out);
+  KG_GUARD_END
+}
+
+int kg_snapshot_create_ordered(const kg_tuple* rows, const uint64_t* keys, size_t n, const kg_dict* dict,
+                               const kg_rewrite_prog* prog, const int* devices, int n_devices, kg_snapshot** out) {
+  KG_GUARD_BEGIN
+  if (n && (!rows || !keys)) return set_error(-2, "rows / keys is NULL");
+  for (size_t i = 1; i < n; i++)
+    if (keys[i] < keys[i - 1]) return set_error(-2, "kg_snapshot_create_ordered: keys not ascending at row %zu", i);
+  return build_replicas(devices, n_devices,
+                        [&](Snapshot* s, int) { return s->create_from_tuples(rows, n, dict, prog, keys); }, out);
+  KG_GUARD_END
+}
+
+int kg_snapshot_apply(kg_snapshot* bp, const kg_tuple* ins, const uint64_t* ins_keys, size_t n_ins, const kg_tuple* del,
+                      size_t n_del, const kg_dict* dict, const kg_rewrite_prog* prog, kg_snapshot** out) {
+  KG_GUARD_BEGIN
+  if (!bp || !out) return set_error(-2, "NULL argument");
+  if ((n_ins && !ins) || (n_del && !del)) return set_error(-2, "ins / del is NULL");
+  Snapshot* base = reinterpret_cast<Snapshot*>(bp);
+  std::vector<int> devs;
+  for (size_t i = 0; i < base->n_replicas(); i++) devs.push_back(base->replica(i)->device);
+  return build_replicas(devs.data(), (int)devs.size(), [&](Snapshot* s, int i) {
+    return s->create_from_delta(base->replica((size_t)i), ins, ins_keys, n_ins, del, n_del, dict, prog);
+  }, out);
   KG_GUARD_END
 }
 
@@ -135,7 +160,7 @@ int kg_snapshot_synthetic_on(const kg_synth_params* params, const kg_rewrite_pro
                              int n_devices, kg_snapshot** out) {
   KG_GUARD_BEGIN
   if (!params) return set_error(-2, "NULL argument");
-  return build_replicas(devices, n_devices, [&](Snapshot* s) { return s->create_synthetic(params, prog); }, out);
+  return build_replicas(devices, n_devices, [&](Snapshot* s, int) { return s->create_synthetic(params, prog); }, out);
   KG_GUARD_END
 }
 

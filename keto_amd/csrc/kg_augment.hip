@@ -517,6 +517,19 @@ int Snapshot::augment_rewrites() {
   ds.nflags = flags;
   n_set_edges = tot[0];
   n_check_rows = tot[1];
+  // a tuple-built snapshot keeps its host node map complete (kg_snapshot_apply interns against it)
+  if (n_new && h_nd_ns.size() == n0 && !hmap.k.empty()) {
+    std::vector<uint32_t> a(n_new), b(n_new), c(n_new);
+    HIPC(hipMemcpy(a.data(), ns2 + n0, (size_t)n_new * 4, hipMemcpyDeviceToHost));
+    HIPC(hipMemcpy(b.data(), obj2 + n0, (size_t)n_new * 4, hipMemcpyDeviceToHost));
+    HIPC(hipMemcpy(c.data(), rel2 + n0, (size_t)n_new * 4, hipMemcpyDeviceToHost));
+    for (uint32_t i = 0; i < n_new; i++) {
+      h_nd_ns.push_back(a[i]);
+      h_nd_obj.push_back(b[i]);
+      h_nd_rel.push_back(c[i]);
+      hmap.put(nmap_key(a[i], c[i], b[i]), n0 + i);
+    }
+  }
   n_virtual = nc;
   n_virtual_new = n_new;
   return 0;

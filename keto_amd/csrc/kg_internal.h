@@ -65,6 +65,30 @@ __host__ __device__ __forceinline__ uint64_t hash_home(uint64_t key, uint64_t n)
 }
 __host__ __device__ __forceinline__ uint64_t hash_next(uint64_t i, uint64_t n) { return i + 1 == n ? 0 : i + 1; }
 
+// Owner of position i in a CSR with offsets off[0..n]: the last node whose row starts at or before i
+// (empty rows share a start; the owner is the one whose range holds i).  Lets the build kernels run
+// one thread per row entry: a thread per node waits for the longest (hub) row.
+__host__ __device__ __forceinline__ uint32_t csr_owner_from(const uint64_t* off, uint32_t lo, uint32_t n, uint64_t i) {
+  uint32_t hi = n;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (off[mid] <= i) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+__host__ __device__ __forceinline__ uint32_t csr_owner(const uint64_t* off, uint32_t n, uint64_t i) {
+  return csr_owner_from(off, 0, n, i);
+}
+// Advances owner v (of some position < i) to the owner of position i: one step covers the common
+// case (the next row), a search the rest (long runs of empty rows: C3 has blocks of 10^8 nodes
+// without set-adjacency, which a step-by-step walk crossed in one thread for seconds).
+__host__ __device__ __forceinline__ uint32_t csr_advance(const uint64_t* off, uint32_t n, uint32_t v, uint64_t i) {
+  if (off[v + 1] > i) return v;
+  if (off[v + 2] > i) return v + 1;
+  return csr_owner_from(off, v + 1, n, i);
+}
+
 // Shard of a node in the hash-sharded mode: all relations of one object live on
 // one rank, owner = hash(ns, obj) mod nranks.
 __host__ __device__ __forceinline__ uint32_t shard_owner(uint32_t ns, uint32_t obj, uint32_t nranks) {

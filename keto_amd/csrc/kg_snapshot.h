@@ -84,6 +84,53 @@ struct BatchPending {
   GridStats gs;
 };
 
+// Host interning map (u64 key (ns, rel, obj) -> node id), open addressing.  Kept by tuple-built
+// snapshots so kg_snapshot_apply can intern a delta's new nodes without rebuilding it.
+struct HostMap {
+  std::vector<uint64_t> k;
+  std::vector<uint32_t> v;
+  uint64_t mask = 0, n = 0;
+  void init(uint64_t cap) {
+    uint64_t c = 16;
+    while (c < cap * 2) c <<= 1;
+    k.assign(c, EMPTY64);
+    v.assign(c, 0);
+    mask = c - 1;
+    n = 0;
+  }
+  void grow() {
+    std::vector<uint64_t> ok;
+    std::vector<uint32_t> ov;
+    ok.swap(k);
+    ov.swap(v);
+    init(ok.size());
+    for (size_t i = 0; i < ok.size(); i++)
+      if (ok[i] != EMPTY64) put(ok[i], ov[i]);
+  }
+  // returns the existing value or inserts val
+  uint32_t put(uint64_t key, uint32_t val) {
+    if ((n + 1) * 2 > k.size()) grow();
+    uint64_t i = mix64(key) & mask;
+    while (k[i] != EMPTY64) {
+      if (k[i] == key) return v[i];
+      i = (i + 1) & mask;
+    }
+    k[i] = key;
+    v[i] = val;
+    n++;
+    return val;
+  }
+  uint32_t get(uint64_t key) const {
+    if (k.empty()) return NONE;
+    uint64_t i = mix64(key) & mask;
+    while (k[i] != EMPTY64) {
+      if (k[i] == key) return v[i];
+      i = (i + 1) & mask;
+    }
+    return NONE;
+  }
+};
+
 struct Snapshot;
 // Host-buffer batches (kg_check_batch): per calling thread, one lane per replica -- its own HIP
 // stream (hence its own batch workspace), pinned staging for queries and results, and device
@@ -125,7 +172,10 @@ struct Snapshot {
   void* d_fplans = nullptr;
   uint32_t n_fplans = 0, fp_leaves = 0;  // plans, most leaves of one plan
   std::vector<std::pair<void*, size_t>> allocs;
-  // host mirrors (host-tuple path)
+  // host mirrors (host-tuple path); hmap + h_nd_* are handed on to a snapshot kg_snapshot_apply
+  // builds from this one
+  HostMap hmap;
+  uint64_t* d_row_key = nullptr;  // per row entry order key (kg_snapshot_create_ordered), or null
   std::vector<uint32_t> h_nd_ns, h_nd_obj, h_nd_rel, h_row_subj;
   std::vector<uint64_t> h_row_off, h_adj_off;
   std::vector<uint8_t> h_relflags;
@@ -173,7 +223,12 @@ struct Snapshot {
   int init_device(int dev);
   int alloc(void** p, size_t bytes);
   void free_alloc(const void* p);
-  int create_from_tuples(const kg_tuple* rows, size_t n, const kg_dict* dict, const kg_rewrite_prog* prog);
+  int create_from_tuples(const kg_tuple* rows, size_t n, const kg_dict* dict, const kg_rewrite_prog* prog,
+                         const uint64_t* keys = nullptr);
+  // kg_delta.hip: this snapshot = base's rows + inserted - deleted, built on the device
+  int create_from_delta(Snapshot* base, const kg_tuple* ins, const uint64_t* ins_keys, size_t n_ins,
+                        const kg_tuple* del, size_t n_del, const kg_dict* dict, const kg_rewrite_prog* prog);
+  int device_flags();  // purity closure on the device (rewrite / undeclared relations reachable)
   int create_synthetic(const kg_synth_params* p, const kg_rewrite_prog* prog);
   int upload_program(const kg_dict* dict, const kg_rewrite_prog* prog);
   int augment_rewrites();  // kg_augment.hip: monotone rewrites -> plain union nodes

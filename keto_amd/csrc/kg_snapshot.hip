@@ -21,26 +21,33 @@
 namespace kg {
 
 // ------------------------------------------------------------------ device hash-table builders
+// Build kernels walk the row entries in chunks of CSR_CHUNK per thread: one owner search per chunk,
+// then the owner advances across row boundaries (a thread per node waited for the longest -- hub --
+// row; a search per entry cost ~28 dependent loads each at 1 B rows).
+constexpr uint32_t CSR_CHUNK = 64;
+
 __global__ void k_dset_insert_rows(uint64_t* dset, uint64_t nb, const uint64_t* row_off, const uint32_t* row_subj,
-                                   uint32_t n_nodes) {
-  uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
-  if (v >= n_nodes) return;
-  for (uint64_t i = row_off[v]; i < row_off[v + 1]; i++) {
-    uint64_t key = dset_key(v, row_subj[i]);
-    uint64_t b = hash_home(key, nb);
-    for (uint64_t n = 0; n < nb; n++) {  // sized for load <= 0.25: always finds room
-      uint64_t* bucket = dset + b * DSET_BUCKET;
-      bool done = false;
-      for (int s = 0; s < DSET_BUCKET; s++) {
-        unsigned long long old = atomicCAS((unsigned long long*)&bucket[s], (unsigned long long)EMPTY64,
-                                           (unsigned long long)key);
-        if (old == EMPTY64 || old == key) {
-          done = true;
-          break;
+                                   uint32_t n_nodes, uint64_t n_rows) {
+  const uint64_t nch = (n_rows + CSR_CHUNK - 1) / CSR_CHUNK;
+  for (uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; c < nch; c += (uint64_t)gridDim.x * blockDim.x) {
+    for (uint64_t i = c * CSR_CHUNK, ie = min(n_rows, i + CSR_CHUNK), v = csr_owner(row_off, n_nodes, i); i < ie; i++) {
+      v = csr_advance(row_off, n_nodes, (uint32_t)v, i);
+      const uint64_t key = dset_key((uint32_t)v, row_subj[i]);
+      uint64_t b = hash_home(key, nb);
+      for (uint64_t n = 0; n < nb; n++) {  // sized for load <= 0.25: always finds room
+        uint64_t* bucket = dset + b * DSET_BUCKET;
+        bool done = false;
+        for (int s = 0; s < DSET_BUCKET; s++) {
+          const unsigned long long old = atomicCAS((unsigned long long*)&bucket[s], (unsigned long long)EMPTY64,
+                                                   (unsigned long long)key);
+          if (old == EMPTY64 || old == key) {
+            done = true;
+            break;
+          }
         }
+        if (done) break;
+        b = hash_next(b, nb);
       }
-      if (done) break;
-      b = hash_next(b, nb);
     }
   }
 }
@@ -98,17 +105,23 @@ __global__ void k_indeg(const uint32_t* adj, uint64_t n_edges, unsigned long lon
   for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < n_edges; e += (uint64_t)gridDim.x * blockDim.x)
     atomicAdd(&deg[adj[e]], 1ull);
 }
-__global__ void k_fill_radj(const uint64_t* adj_off, const uint32_t* adj, uint32_t n_nodes, unsigned long long* cur,
-                            uint32_t* radj) {
-  const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
-  if (v >= n_nodes) return;
-  for (uint64_t i = adj_off[v], e = adj_off[v + 1]; i < e; i++) radj[atomicAdd(&cur[adj[i]], 1ull)] = v;
+// One thread per edge, the edge's source node precomputed (k_row_nodes over adj_off): the parents
+// list slot comes from a returning atomic on the child's cursor, so a thread must not chain them (a
+// chunk of edges per thread took 36 s on C3, whose union rows point at a few hot groups and
+// folders), and a thread per node waits for the longest row.
+__global__ void k_fill_radj(const uint32_t* __restrict__ adj, const uint32_t* __restrict__ src, uint64_t n_edges,
+                            unsigned long long* cur, uint32_t* radj) {
+  for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < n_edges; e += (uint64_t)gridDim.x * blockDim.x)
+    radj[atomicAdd(&cur[adj[e]], 1ull)] = src[e];
 }
 // (subject, node) pairs of every row entry, to be sorted by subject
-__global__ void k_row_nodes(const uint64_t* row_off, uint32_t n_nodes, uint32_t* node_of_row) {
-  const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
-  if (v >= n_nodes) return;
-  for (uint64_t i = row_off[v], e = row_off[v + 1]; i < e; i++) node_of_row[i] = v;
+__global__ void k_row_nodes(const uint64_t* row_off, uint32_t n_nodes, uint64_t n_rows, uint32_t* node_of_row) {
+  const uint64_t nch = (n_rows + CSR_CHUNK - 1) / CSR_CHUNK;
+  for (uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; c < nch; c += (uint64_t)gridDim.x * blockDim.x)
+    for (uint64_t i = c * CSR_CHUNK, ie = min(n_rows, i + CSR_CHUNK), v = csr_owner(row_off, n_nodes, i); i < ie; i++) {
+      v = csr_advance(row_off, n_nodes, (uint32_t)v, i);
+      node_of_row[i] = (uint32_t)v;
+    }
 }
 __global__ void k_count_runs(const uint32_t* key, uint64_t n, unsigned long long* cnt) {
   uint32_t c = 0;
@@ -403,7 +416,9 @@ int Snapshot::build_hash_tables() {
   HIPC(hipMemsetAsync(nm, 0xFF, slots * sizeof(NSlot), stream));
   uint32_t grid = (ds.n_nodes + 255) / 256;
   if (ds.n_nodes) {
-    hipLaunchKernelGGL(k_dset_insert_rows, dim3(grid), dim3(256), 0, stream, dset, buckets, coff, csub, ds.n_nodes);
+    if (n_rows)
+      hipLaunchKernelGGL(k_dset_insert_rows, dim3((uint32_t)std::min<uint64_t>(65536, (n_rows + 64 * 256 - 1) / (64 * 256))), dim3(256), 0,
+                         stream, dset, buckets, coff, csub, ds.n_nodes, n_rows);
     HIPC(hipGetLastError());
     hipLaunchKernelGGL(k_nmap_insert, dim3(grid), dim3(256), 0, stream, nm, slots, ds.nd_ns, ds.nd_obj,
                        ds.nd_rel, ds.adj_off, sig, ds.n_nodes);
@@ -456,7 +471,17 @@ int Snapshot::build_reverse() {
   HIPC(hipMalloc(&tmp, tmp_bytes + 16));
   HIPC(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, (uint64_t*)deg, roff, (size_t)nn + 1, stream));
   HIPC(hipMemcpyAsync(deg, roff, ((size_t)nn + 1) * 8, hipMemcpyDeviceToDevice, stream));
-  hipLaunchKernelGGL(k_fill_radj, dim3(grid), dim3(256), 0, stream, ds.adj_off, ds.adj, nn, deg, radj);
+  if (E) {
+    uint32_t* src = nullptr;
+    HIPC(hipMalloc(&src, E * 4));
+    hipLaunchKernelGGL(k_row_nodes, dim3((uint32_t)std::min<uint64_t>(65536, (E + 64 * 256 - 1) / (64 * 256))), dim3(256),
+                       0, stream, ds.adj_off, nn, E, src);
+    hipLaunchKernelGGL(k_fill_radj, dim3((uint32_t)std::min<uint64_t>(65536, (E + 255) / 256)), dim3(256), 0, stream,
+                       ds.adj, (const uint32_t*)src, E, deg, radj);
+    HIPC(hipGetLastError());
+    HIPC(hipStreamSynchronize(stream));
+    HIPC(hipFree(src));
+  }
   HIPC(hipGetLastError());
   HIPC(hipStreamSynchronize(stream));
   HIPC(hipFree(tmp));
@@ -468,7 +493,9 @@ int Snapshot::build_reverse() {
   HIPC(hipMalloc(&v0, R * 4 + 4));
   HIPC(hipMalloc(&v1, R * 4 + 4));
   HIPC(hipMemcpyAsync(k0, csub, R * 4, hipMemcpyDeviceToDevice, stream));
-  hipLaunchKernelGGL(k_row_nodes, dim3(grid), dim3(256), 0, stream, coff, nn, v0);
+  if (R)
+    hipLaunchKernelGGL(k_row_nodes, dim3((uint32_t)std::min<uint64_t>(65536, (R + 64 * 256 - 1) / (64 * 256))), dim3(256), 0, stream,
+                       coff, nn, R, v0);
   HIPC(hipGetLastError());
   hipcub::DoubleBuffer<uint32_t> kb(k0, k1), vb(v0, v1);
   tmp_bytes = 0;
@@ -581,49 +608,12 @@ uint8_t Snapshot::host_relflag(uint32_t ns, uint32_t rel) const {
   return h_relflags[(size_t)ns * ds.n_rel + rel];
 }
 
-// ------------------------------------------------------------------ host interning map
-namespace {
-struct HostMap {  // (u64 key) -> u32, open addressing
-  std::vector<uint64_t> k;
-  std::vector<uint32_t> v;
-  uint64_t mask = 0, n = 0;
-  void init(uint64_t cap) {
-    uint64_t c = pow2_at_least(std::max<uint64_t>(16, cap * 2));
-    k.assign(c, EMPTY64);
-    v.assign(c, 0);
-    mask = c - 1;
-    n = 0;
-  }
-  void grow() {
-    std::vector<uint64_t> ok;
-    std::vector<uint32_t> ov;
-    ok.swap(k);
-    ov.swap(v);
-    init(ok.size());
-    for (size_t i = 0; i < ok.size(); i++)
-      if (ok[i] != EMPTY64) put(ok[i], ov[i]);
-  }
-  // returns existing value or inserts val
-  uint32_t put(uint64_t key, uint32_t val) {
-    if ((n + 1) * 2 > k.size()) grow();
-    uint64_t i = mix64(key) & mask;
-    while (k[i] != EMPTY64) {
-      if (k[i] == key) return v[i];
-      i = (i + 1) & mask;
-    }
-    k[i] = key;
-    v[i] = val;
-    n++;
-    return val;
-  }
-};
-}  // namespace
-
-int Snapshot::create_from_tuples(const kg_tuple* rows, size_t n, const kg_dict* dict, const kg_rewrite_prog* prog) {
+int Snapshot::create_from_tuples(const kg_tuple* rows, size_t n, const kg_dict* dict, const kg_rewrite_prog* prog,
+                                 const uint64_t* keys) {
   wildcard_rel = dict ? dict->wildcard_rel : NONE;
   ds.wildcard_rel = wildcard_rel;
   // 1. intern nodes (ns, obj, rel) in first-appearance order
-  HostMap m;
+  HostMap& m = hmap;
   m.init(n + 16);
   std::vector<uint32_t> lhs(n), sub(n);
   auto intern = [&](uint32_t ns, uint32_t obj, uint32_t rel) -> uint32_t {
@@ -671,11 +661,13 @@ int Snapshot::create_from_tuples(const kg_tuple* rows, size_t n, const kg_dict* 
   }
   h_row_subj.assign(h_row_off[nn], 0);
   std::vector<uint32_t> adj(h_adj_off[nn]);
+  std::vector<uint64_t> row_key(keys ? h_row_off[nn] : 0);  // rows keep the input (key) order per node
   {
     std::vector<uint64_t> fr(h_row_off.begin(), h_row_off.end() - 1), fa(h_adj_off.begin(), h_adj_off.end() - 1);
     for (size_t i = 0; i < n; i++) {
       if (lhs[i] == NONE) continue;
       uint32_t s = sub[i], v = lhs[i];
+      if (keys) row_key[fr[v]] = keys[i];
       h_row_subj[fr[v]++] = s;
       if ((s & SET_BIT) && h_nd_rel[s & ~SET_BIT] != wildcard_rel) adj[fa[v]++] = s & ~SET_BIT;
     }
@@ -743,6 +735,10 @@ int Snapshot::create_from_tuples(const kg_tuple* rows, size_t n, const kg_dict* 
   ds.nd_obj = d_obj;
   ds.nd_rel = d_rel;
   n_set_edges = adj.size();
+  if (keys) {
+    if (alloc((void**)&d_row_key, row_key.size() * 8 + 8)) return -1;
+    if (!row_key.empty()) HIPC(hipMemcpy(d_row_key, row_key.data(), row_key.size() * 8, hipMemcpyHostToDevice));
+  }
   ds.nflags = nullptr;
   if (has_program) {
     uint8_t* d_f;
@@ -809,13 +805,25 @@ int Snapshot::create_synthetic(const kg_synth_params* p, const kg_rewrite_prog* 
   n_set_edges = tot[1];
   kg_dict dict{4, 10, 0};
   if (upload_program(&dict, prog)) return -1;
-  if (has_program) {
-    uint8_t* f;
-    uint32_t* changed;
-    if (alloc((void**)&f, (size_t)nn + 1)) return -1;
-    HIPC(hipMalloc(&changed, 4));
+  if (has_program && device_flags()) return -1;
+  n_check_rows = h_row_off_last;
+  if (augment_rewrites() || build_formulas()) return -1;
+  return build_hash_tables();
+}
+
+// Purity closure on the device: seed with the relation flags, propagate "impure" backwards over
+// set-adjacency to a fixed point (every round that changes something marks a node).
+int Snapshot::device_flags() {
+  const uint32_t nn = ds.n_nodes;
+  uint8_t* f;
+  uint32_t* changed;
+  if (alloc((void**)&f, (size_t)nn + 1)) return -1;
+  ds.nflags = nullptr;
+  HIPC(hipMalloc(&changed, 4));
+  const uint32_t grid = (nn + 255) / 256;
+  if (nn) {
     hipLaunchKernelGGL(k_flags_init, dim3(grid), dim3(256), 0, stream, ds, f);
-    for (int it = 0; it < 1000; it++) {
+    for (uint64_t it = 0; it <= nn; it++) {
       uint32_t h = 0;
       HIPC(hipMemsetAsync(changed, 0, 4, stream));
       hipLaunchKernelGGL(k_flags_propagate, dim3(grid), dim3(256), 0, stream, ds, f, changed);
@@ -823,12 +831,10 @@ int Snapshot::create_synthetic(const kg_synth_params* p, const kg_rewrite_prog* 
       HIPC(hipStreamSynchronize(stream));
       if (!h) break;
     }
-    HIPC(hipFree(changed));
-    ds.nflags = f;
   }
-  n_check_rows = h_row_off_last;
-  if (augment_rewrites() || build_formulas()) return -1;
-  return build_hash_tables();
+  HIPC(hipFree(changed));
+  ds.nflags = f;
+  return 0;
 }
 
 int64_t Snapshot::export_rows(kg_tuple* out, uint64_t cap) {

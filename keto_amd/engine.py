@@ -61,11 +61,14 @@ class Snapshot:
     """An HBM-resident, immutable snapshot of the relation tuples (rows in shard order)."""
 
     def __init__(self, tuples: np.ndarray, interner: Interner, program: Optional[Program] = None, device: int = 0,
-                 _handle=None, shard: Optional[Tuple[int, int]] = None, devices: Optional[Sequence[int]] = None):
+                 _handle=None, shard: Optional[Tuple[int, int]] = None, devices: Optional[Sequence[int]] = None,
+                 keys: Optional[np.ndarray] = None):
         """devices: one replica per entry (entries may repeat); the library splits host-buffer batches
         over them (kg_snapshot_create_on).  Default: one replica on `device`.
         shard = (rank, nranks): keep only the rows of the nodes this rank owns (hash-sharded mode,
-        keto_amd.sharded); every rank passes the same full tuple list."""
+        keto_amd.sharded); every rank passes the same full tuple list.
+        keys: ascending u64 order key per row (shard ids): kept so `apply` places inserted rows in order
+        (kg_snapshot_create_ordered)."""
         L = _lib.load()
         self.interner = interner
         self.device = device
@@ -80,8 +83,14 @@ class Snapshot:
         d = _lib.kg_dict(interner.n_namespaces, interner.n_relations, interner.wildcard_rel)
         prog_c = self._prog(program)
         pc = C.byref(prog_c) if prog_c is not None else None
-        if shard is None:
-            dv = np.asarray(list(devices) if devices else [device], np.int32)
+        self.devices = list(devices) if devices else [device]
+        if shard is None and keys is not None:
+            dv = np.asarray(self.devices, np.int32)
+            k = np.ascontiguousarray(keys, dtype=np.uint64)
+            rc = L.kg_snapshot_create_ordered(_ptr(t), _ptr(k), t.shape[0], C.byref(d), pc, _ptr(dv), len(dv),
+                                              C.byref(self._h))
+        elif shard is None:
+            dv = np.asarray(self.devices, np.int32)
             rc = L.kg_snapshot_create_on(_ptr(t), t.shape[0], C.byref(d), pc, _ptr(dv), len(dv), C.byref(self._h))
         else:
             rc = L.kg_snapshot_create_shard(_ptr(t), t.shape[0], C.byref(d), pc, device, shard[0], shard[1],
@@ -98,6 +107,27 @@ class Snapshot:
         self._keep = arrs
         return _lib.kg_rewrite_prog(len(arrs[0]), _ptr(arrs[0]), len(arrs[1]), _ptr(arrs[1]), _ptr(arrs[2]),
                                     _ptr(arrs[3]), arrs[4].shape[0], _ptr(arrs[4]), len(arrs[5]), _ptr(arrs[5]))
+
+    def apply(self, ins: np.ndarray, dels: np.ndarray, ins_keys: Optional[np.ndarray] = None) -> "Snapshot":
+        """kg_snapshot_apply: a new snapshot holding this one's rows minus every row equal to a tuple of
+        `dels`, plus `ins` (uint32 (n, 6) tuple ids; ins_keys: their order keys).  This snapshot stays
+        valid for readers; the next delta goes to the returned one."""
+        L = _lib.load()
+        it = self.interner
+        a = np.ascontiguousarray(ins, dtype=np.uint32).reshape(-1, 6)
+        dl = np.ascontiguousarray(dels, dtype=np.uint32).reshape(-1, 6)
+        k = None if ins_keys is None else np.ascontiguousarray(ins_keys, dtype=np.uint64)
+        d = _lib.kg_dict(it.n_namespaces, it.n_relations, it.wildcard_rel)
+        new = Snapshot(None, it, self.program, self.device, _handle=C.c_void_p())
+        prog_c = new._prog(self.program)
+        pc = C.byref(prog_c) if prog_c is not None else None
+        h = C.c_void_p()
+        _lib.check(L.kg_snapshot_apply(self._h, _ptr(a) if len(a) else None, _ptr(k) if k is not None and len(a) else None,
+                                       a.shape[0], _ptr(dl) if len(dl) else None, dl.shape[0], C.byref(d), pc,
+                                       C.byref(h)), "kg_snapshot_apply")
+        new._h = h
+        new.devices = getattr(self, "devices", [self.device])
+        return new
 
     @classmethod
     def synthetic(cls, n_tuples: int, seed: int = 20250131, device: int = 0, n_layers: int = 8,

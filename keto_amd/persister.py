@@ -15,13 +15,17 @@ Reference behaviour mirrored (paths relative to the reference checkout):
   whereSubject: a subject-id query matches only subject-id rows,    relationtuples.go:124-145
     a subject-set query only subject-set rows
 
-The rows live on the host in shard order (the source of truth, like the SQL table); the check /
+The rows live on the host in shard order (the source of truth, like the SQL table: a sorted list
+keyed by shard id plus a tuple -> shard ids index, so a write costs O(delta log n)); the check /
 expand engines read an immutable GPU snapshot built from them.  Every successful write bumps a
-version; the next engine call after a write rebuilds the snapshot (``kg_snapshot_create``) from
-the rows in shard order, so a check always sees every committed write (read-your-writes).  Reads
-of the tuple list (``get_relation_tuples``) are not on the hot path and are answered from the
-host rows.  Shard ids come from a seeded generator so runs are reproducible (the reference draws
-them from crypto/rand; only their order matters, and no reference test pins it).
+version and joins a pending delta; the next engine call after writes refreshes the snapshot
+INCREMENTALLY (``kg_snapshot_apply``: only the delta is interned on the host, rows and every
+derived structure are rebuilt on the device, inserted rows placed by shard id), so a check always
+sees every committed write (read-your-writes).  The first snapshot, and any delta larger than
+``rebuild_fraction`` of the rows, is a full ``kg_snapshot_create_ordered``.  Reads of the tuple
+list (``get_relation_tuples``) are not on the hot path and are answered from the host rows.  Shard
+ids come from a seeded generator so runs are reproducible (the reference draws them from
+crypto/rand; only their order matters, and no reference test pins it).
 """
 from __future__ import annotations
 
@@ -29,7 +33,10 @@ import random
 import threading
 import uuid
 from dataclasses import dataclass
-from typing import Iterable, List, Optional, Sequence, Tuple
+from typing import Dict, Iterable, List, Optional, Sequence, Tuple
+
+import numpy as np
+from sortedcontainers import SortedKeyList
 
 from .engine import Config, Engine, ExpandEngine, Snapshot
 from .ketoapi import RelationTuple, SubjectSet
@@ -80,7 +87,8 @@ class SnapshotPersister:
     """relationtuple.Manager whose reads for check / expand come from a GPU snapshot."""
 
     def __init__(self, namespaces: Sequence[Namespace] = (), max_read_depth: int = 5, device: int = 0,
-                 seed: int = 0, interner: Optional[Interner] = None, devices: Optional[Sequence[int]] = None):
+                 seed: int = 0, interner: Optional[Interner] = None, devices: Optional[Sequence[int]] = None,
+                 rebuild_fraction: float = 0.125):
         self.interner = interner or Interner()
         self.namespaces = list(namespaces)
         self.config = Config(max_read_depth, self.namespaces)
@@ -89,30 +97,41 @@ class SnapshotPersister:
         self.device = device
         self.devices = list(devices) if devices else None  # replicas (kg_snapshot_create_on)
         self._rng = random.Random(seed)
-        self._rows: List[Tuple[uuid.UUID, RelationTuple]] = []  # sorted by shard id
+        self._rows = SortedKeyList(key=lambda r: r[0].int)  # (shard id, tuple), sorted by shard id
+        self._by_tuple: Dict[RelationTuple, List[uuid.UUID]] = {}
         self._lock = threading.RLock()
         self._version = 0
         self._snap: Optional[Snapshot] = None
         self._snap_version = -1
-        self.rebuilds = 0
+        # the delta since the snapshot: inserted rows (shard id -> tuple), deleted tuple values
+        self._p_ins: Dict[int, RelationTuple] = {}
+        self._p_del: set = set()
+        self.rebuild_fraction = rebuild_fraction
+        self.rebuilds = 0  # full builds
+        self.applies = 0   # incremental refreshes
 
     # ---- writes (each one is a transaction: validate everything, then apply)
     def _shard_id(self) -> uuid.UUID:
         return uuid.UUID(int=self._rng.getrandbits(128), version=4)
 
+    def _remove_tuple(self, t: RelationTuple) -> None:
+        for sid in self._by_tuple.pop(t, ()):
+            self._rows.remove((sid, t))
+            self._p_ins.pop(sid.int, None)
+        self._p_del.add(t)  # base rows equal to t go too (relationtuples.go:164-185)
+
     def _apply(self, ins: Sequence[RelationTuple], dels: Sequence[RelationTuple]) -> None:
         for t in list(ins) + list(dels):
-            _check_subject(t)
+            _check_subject(t)  # all-or-nothing: validated before anything changes
         if not ins and not dels:
             return
-        rows = list(self._rows)
-        for t in ins:
-            rows.append((self._shard_id(), t))
-        if dels:
-            gone = set(dels)
-            rows = [r for r in rows if r[1] not in gone]
-        rows.sort(key=lambda r: r[0].int)
-        self._rows = rows
+        for t in ins:  # writes, then deletes (relationtuples.go:260-270)
+            sid = self._shard_id()
+            self._rows.add((sid, t))
+            self._by_tuple.setdefault(t, []).append(sid)
+            self._p_ins[sid.int] = t
+        for t in dels:
+            self._remove_tuple(t)
         self._version += 1
 
     def write_relation_tuples(self, *ts: RelationTuple) -> None:
@@ -129,9 +148,10 @@ class SnapshotPersister:
 
     def delete_all_relation_tuples(self, query: RelationQuery) -> None:
         with self._lock:
-            rows = [r for r in self._rows if not query.matches(r[1])]
-            if len(rows) != len(self._rows):
-                self._rows = rows
+            gone = {t for _, t in self._rows if query.matches(t)}
+            for t in gone:
+                self._remove_tuple(t)
+            if gone:
                 self._version += 1
 
     # ---- reads of the tuple list
@@ -145,14 +165,13 @@ class SnapshotPersister:
                 raise MalformedPageToken(page_token) from e
         else:
             last = 0  # uuid.Nil
-        with self._lock:
-            rows = self._rows
         res: List[Tuple[uuid.UUID, RelationTuple]] = []
-        for sid, t in rows:
-            if sid.int > last and query.matches(t):
-                res.append((sid, t))
-                if len(res) > per_page:
-                    break
+        with self._lock:
+            for sid, t in self._rows.irange_key(min_key=last, inclusive=(False, True)):  # shard_id > lastID
+                if query.matches(t):
+                    res.append((sid, t))
+                    if len(res) > per_page:
+                        break
         token = ""
         if len(res) > per_page:
             res = res[:per_page]
@@ -167,14 +186,30 @@ class SnapshotPersister:
     def version(self) -> int:
         return self._version
 
+    @staticmethod
+    def _key(sid_int: int) -> int:
+        return sid_int >> 64  # order key: the shard id's high 64 bits (uuid order up to a 2^-64 tie)
+
     def snapshot(self) -> Snapshot:
-        """The snapshot of the current rows; rebuilt on the first call after a write."""
+        """The snapshot of the current rows; refreshed on the first call after a write."""
         with self._lock:
-            if self._snap is None or self._snap_version != self._version:
+            if self._snap is not None and self._snap_version == self._version:
+                return self._snap
+            delta = len(self._p_ins) + len(self._p_del)
+            if self._snap is None or delta > max(4096, self.rebuild_fraction * len(self._rows)):
                 arr = self.interner.tuples_array(t for _, t in self._rows)
-                snap = Snapshot(arr, self.interner, self.program, self.device, devices=self.devices)
-                self._snap, self._snap_version = snap, self._version
+                keys = np.fromiter((self._key(sid.int) for sid, _ in self._rows), np.uint64, len(self._rows))
+                snap = Snapshot(arr, self.interner, self.program, self.device, devices=self.devices, keys=keys)
                 self.rebuilds += 1
+            else:
+                ins = sorted(self._p_ins.items())
+                ia = self.interner.tuples_array(t for _, t in ins)
+                ik = np.fromiter((self._key(k) for k, _ in ins), np.uint64, len(ins))
+                da = self.interner.tuples_array(self._p_del)
+                snap = self._snap.apply(ia, da, ik)
+                self.applies += 1
+            self._snap, self._snap_version = snap, self._version
+            self._p_ins, self._p_del = {}, set()
             return self._snap
 
     def permission_engine(self) -> Engine:

@@ -44,7 +44,7 @@ def test_persister_read_your_writes_vs_oracle(seed):
         exp, oerr, _ = Oracle(shard_rows(m), it.wildcard_rel).check_batch(q6, depths, 6, POLICY_CANONICAL)
         assert (err == 0).all() and (oerr == 0).all()
         assert (out == exp).all(), np.nonzero(out != exp)[0][:10]
-    assert m.rebuilds == 3
+    assert m.rebuilds == 1 and m.applies == 2  # the first snapshot is built, then refreshed by deltas
 
 
 def test_persister_write_delete_flip():
@@ -64,7 +64,7 @@ def test_persister_write_delete_flip():
     assert not e.check_is_member(q, 0)
     m.delete_all_relation_tuples(RelationQuery("doc"))
     assert x.build_tree(SubjectSet("doc", "a", "view"), 0) is None
-    assert m.rebuilds == 4
+    assert m.rebuilds + m.applies == 4 and m.applies >= 3
     assert e.check_is_member(RelationTuple.from_string("group:h#member@bob"), 0)
 
 
@@ -150,3 +150,54 @@ def test_native_batcher_many_callers_vs_oracle():
         nb2.L.kg_batcher_destroy(nb2._h)  # closed under the Python object: the next call must fail cleanly
         nb2._h = C.c_void_p()
         nb2.check_ids(q7[:1])
+
+
+@pytest.mark.parametrize("seed,unions", [(0, False), (1, False), (2, True), (3, True)])
+def test_incremental_refresh_matches_full_build(seed, unions):
+    """kg_snapshot_apply after every transaction (inserts incl. new objects and subject sets,
+    deletes of base rows and of rows inserted since the last snapshot, delete-all): checks equal
+    the oracle on the persister's rows in shard order, and both checks and expand trees equal a
+    snapshot built from scratch (kg_snapshot_create_ordered) from the same rows -- same shard order,
+    so the same pre-order.  unions: a namespace program whose union rewrites are materialised."""
+    from keto_amd.engine import Engine, ExpandEngine, Snapshot
+    from keto_amd.mapper import SUBJECT_ID
+    from test_gpu_check import random_program
+    rng = np.random.default_rng(300 + seed)
+    it, tuples, nss, rels = random_graph(rng, n_obj=60, n_rows=700)
+    namespaces = random_program(rng, nss, rels, unions_only=True) if unions else []
+    m = SnapshotPersister(namespaces=namespaces, interner=it, max_read_depth=5, seed=seed)
+    base, rest = tuples[:400], tuples[400:]
+    m.write_relation_tuples(*base)
+    e = m.permission_engine()
+    qs = random_queries(rng, nss, rels, 1200, n_obj=64)
+    q6 = np.asarray([it.tuple_ids(t) for t in qs], np.uint32)
+    depths = rng.integers(0, 7, len(qs))
+    roots = np.asarray([[it.ns_id(rng.choice(nss)), it.obj_id(f"o{rng.integers(64)}"), it.rel_id(rng.choice(rels)), 0]
+                        for _ in range(150)], np.uint32)
+    live = list(base)
+    for step in range(6):
+        ins = [rest.pop() for _ in range(min(len(rest), int(rng.integers(20, 60))))]
+        ins += [RelationTuple.from_string(f"{rng.choice(nss)}:new{step}_{k}#{rng.choice(rels)}@u{k}") for k in range(3)]
+        ins.append(RelationTuple.from_string(f"{nss[0]}:o{step}#{rels[0]}@({nss[1]}:new{step}_0#{rels[1]})"))
+        dels = [live[i] for i in rng.choice(len(live), 15, replace=False)] if live else []
+        m.transact_relation_tuples(ins, dels)
+        live = [t for t in live + ins if t not in set(dels)]
+        if step == 2:  # a row inserted since the last snapshot, deleted before the next one
+            m.delete_relation_tuples(ins[0])
+            live = [t for t in live if t != ins[0]]
+        if step == 4:
+            m.delete_all_relation_tuples(RelationQuery(namespace=nss[2]))
+            live = [t for t in live if t.namespace != nss[2]]
+        out, err = e.batch_check_ids(queries_array(q6, depths))
+        rows = shard_rows(m)
+        keys = np.fromiter((m._key(sid.int) for sid, _ in m._rows), np.uint64, len(m._rows))
+        full = Snapshot(rows, it, m.program, keys=keys)
+        fout, ferr = Engine(full, m.config).batch_check_ids(queries_array(q6, depths))
+        assert (out == fout).all() and (err == ferr).all(), step
+        exp, oerr, _ = Oracle(rows, it.wildcard_rel, m.program).check_batch(q6, depths, 5, POLICY_CANONICAL)
+        assert (out == exp).all() and (err.astype(np.int64) == oerr).all(), (step, np.nonzero(out != exp)[0][:8])
+        ga = ExpandEngine(m.snapshot(), m.config).build_trees_ids(roots)
+        gb = ExpandEngine(full, m.config).build_trees_ids(roots)
+        for a, b in zip(ga, gb):
+            assert (a is None and b is None) or (a is not None and b is not None and np.array_equal(a, b)), step
+    assert m.applies >= 5
