@@ -246,7 +246,7 @@ def bench_sharded(a):
         dist.init_process_group(a.backend, rank=rank, world_size=world)
     L = _lib.load()
     t_build = time.time()
-    snap = Snapshot.synthetic(int(a.tuples), seed=a.seed, device=local, shard=(rank, world))
+    snap = Snapshot.synthetic(int(a.tuples), seed=a.seed, device=local, shard=(rank, world), preset=a.preset)
     info = snap.info()
     t_build = time.time() - t_build
     B = a.batch
@@ -279,8 +279,10 @@ def bench_sharded(a):
            "warmup": a.warmup, "ms_per_step": elapsed / a.steps * 1e3, "higher_is_better": True, "scaling": "weak",
            "vs_baseline": None, "dtype": "u32",
            "data": "synthetic (device-generated Drive-like tuple graph, seed %d)" % a.seed,
-           "config": {"workload": "C4 generator @ %.3g tuples hash-sharded over %d rank(s), %d checks/step/rank, "
-                                  "max_read_depth %d" % (a.tuples, world, B, a.global_depth),
+           "config": {"workload": "%s generator @ %.3g tuples hash-sharded over %d rank(s), %d checks/step/rank, "
+                                  "max_read_depth %d" % ("C3" if a.preset else "C4", a.tuples, world, B,
+                                                         a.global_depth),
+                      "materialized": snap.materialized() if a.preset else None,
                       "rows_on_rank0": info["rows"], "nodes": info["nodes"], "batch_per_gpu": B,
                       "parallelism": f"shard{world}"},
            "p99_batch_ms": float(np.percentile(np.array(lat) * 1e3, 99)), "allowed_fraction": float(r.mean()),

@@ -283,9 +283,11 @@ void kg_batcher_destroy(kg_batcher* b);
  * received (nodes it owns, or hit / error reports for queries it is home of) and writes the next
  * level's records into one bucket per destination rank; the caller exchanges the buckets
  * (all-to-all, RCCL over xGMI) and calls kg_shard_level again until no rank sends anything, then
- * kg_shard_finish.  Replaces the single-GPU kg_check_batch for such snapshots.  Rewrites are not
- * evaluated in this mode: a query that reaches a node whose relation has a rewrite or is
- * undeclared ends as KG_ERROR / KG_ERR_NOT_IMPLEMENTED.  keto_amd/sharded.py is the driver. */
+ * kg_shard_finish.  Replaces the single-GPU kg_check_batch for such snapshots.  Rewrites: union
+ * rewrites are materialised into plain union nodes as in the single-GPU engine and boolean ones
+ * over plain / union leaves are split into parts (kg_shard_result_slots); a query that reaches any
+ * other rewrite (or an undeclared relation) ends as KG_ERROR / KG_ERR_NOT_IMPLEMENTED -- there is no
+ * cross-shard interpreter.  keto_amd/sharded.py is the driver. */
 typedef struct {
   uint32_t q;     /* home rank << 26 | index in the home rank's batch                         */
   uint32_t node;  /* node to check (checkIsAllowed(node, depth)), KG_FREC_HIT or KG_FREC_ERR  */
@@ -327,7 +329,11 @@ int kg_shard_done(kg_snapshot* s, size_t n, const uint8_t* d_res, uint32_t* d_bi
  * A single-rank snapshot uses its own bitmap without this. */
 int kg_shard_held_words(const kg_snapshot* s, size_t* words);
 int kg_shard_held(kg_snapshot* s, uint32_t* d_bits, size_t words, int import, void* stream);
-int kg_shard_finish(kg_snapshot* s, size_t n, uint8_t* d_res, const uint32_t* d_err, void* stream);
+int kg_shard_finish(kg_snapshot* s, size_t n, uint8_t* d_res, uint32_t* d_err, void* stream);
+/* Result slots a batch of n queries needs in d_res / d_err (n, or more when the snapshot splits
+ * boolean rewrites into parts: the parts' answers sit behind the n requested ones and
+ * kg_shard_finish combines them into d_res[0, n) / d_err[0, n)). */
+size_t kg_shard_result_slots(const kg_snapshot* s, size_t n);
 
 /* ---- expand ----------------------------------------------------------------------------- */
 /* Roots are split over the replicas (chunks of >= 1024 roots, one host thread each). */

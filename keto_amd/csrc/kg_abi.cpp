@@ -272,7 +272,11 @@ int kg_shard_held_words(const kg_snapshot* sp, size_t* words) {
   return 0;
 }
 
-int kg_shard_finish(kg_snapshot* sp, size_t n, uint8_t* d_res, const uint32_t* d_err, void* stream) {
+size_t kg_shard_result_slots(const kg_snapshot* sp, size_t n) {
+  return sp ? kg::shard_result_slots(reinterpret_cast<const Snapshot*>(sp), n) : n;
+}
+
+int kg_shard_finish(kg_snapshot* sp, size_t n, uint8_t* d_res, uint32_t* d_err, void* stream) {
   KG_GUARD_BEGIN
   if (!sp || (n && (!d_res || !d_err))) return set_error(-2, "NULL argument");
   Snapshot* s = reinterpret_cast<Snapshot*>(sp);

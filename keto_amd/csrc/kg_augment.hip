@@ -77,14 +77,18 @@ __device__ __forceinline__ bool aug_target_bad(const DevSnap& s, const AugTables
 }
 
 // ---- 1. candidates: one per (plan, object) with any contributing node; emitted by its anchor (the
-// first relation of the plan's order whose node exists), so no dedup table is needed
+// first relation of the plan's order whose node exists), so no dedup table is needed.  Pass 1
+// counts per anchor node, a scan places them: candidate order (hence new node ids) is a function of
+// the node triples alone, the same on every rank of the hash-sharded mode.
 template <bool FILL>
-__global__ void k_aug_cands(DevSnap s, AugTables A, uint32_t n0, uint32_t* count, uint32_t* c_plan, uint32_t* c_obj,
-                            uint32_t* c_base) {
+__global__ void k_aug_cands(DevSnap s, AugTables A, uint32_t n0, uint32_t* count, const uint64_t* cpos,
+                            uint32_t* c_plan, uint32_t* c_obj, uint32_t* c_base) {
   const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
   if (v >= n0) return;
+  uint32_t k = 0;
   const uint32_t ns = s.nd_ns[v], rel = s.nd_rel[v], obj = s.nd_obj[v];
   const uint32_t pr = aug_pair(s, ns, rel);
+  if (!FILL) count[v] = 0;
   if (pr == NONE) return;
   for (uint32_t i = A.c_off[pr]; i < A.c_off[pr + 1]; i++) {
     const uint32_t p = A.c_list[i];
@@ -95,25 +99,32 @@ __global__ void k_aug_cands(DevSnap s, AugTables A, uint32_t n0, uint32_t* count
     for (uint32_t j = 0; j < pos && anchor; j++)
       if (nmap_find(s, ns, P.l[j], obj) != NONE) anchor = false;
     if (!anchor) continue;
-    const uint32_t k = atomicAdd(count, 1u);
     if (FILL) {
-      c_plan[k] = p;
-      c_obj[k] = obj;
-      c_base[k] = rel == P.R ? v : NONE;  // the plain node (ns,obj,R) exists: V replaces it
+      const uint64_t at = cpos[v] + k;
+      c_plan[at] = p;
+      c_obj[at] = obj;
+      c_base[at] = rel == P.R ? v : NONE;  // the plain node (ns,obj,R) exists: V replaces it
     }
+    k++;
   }
+  if (!FILL) count[v] = k;
 }
 
-// ---- 2. ids: replaced candidates keep the plain node id, new ones are appended after n0
+// ---- 2. ids: replaced candidates keep the plain node id, new ones are appended after n0 in
+// candidate order (new_pos: exclusive scan of "is new")
+__global__ void k_aug_isnew(uint32_t nc, const uint32_t* c_base, uint32_t* is_new) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < nc) is_new[k] = c_base[k] == NONE ? 1u : 0u;
+}
 __global__ void k_aug_ids(DevSnap s, AugTables A, uint32_t nc, uint32_t n0, const uint32_t* c_plan,
-                          const uint32_t* c_obj, const uint32_t* c_base, uint32_t* new_count, uint32_t* c_id,
+                          const uint32_t* c_obj, const uint32_t* c_base, const uint64_t* new_pos, uint32_t* c_id,
                           uint32_t* cand_of, uint32_t* nd_ns, uint32_t* nd_obj, uint32_t* nd_rel) {
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= nc) return;
   const AugPlan& P = A.plans[c_plan[k]];
   uint32_t id = c_base[k];
   if (id == NONE) {
-    id = n0 + atomicAdd(new_count, 1u);
+    id = n0 + (uint32_t)new_pos[k];
     nd_ns[id] = P.ns;
     nd_obj[id] = c_obj[k];
     nd_rel[id] = P.R;
@@ -169,12 +180,16 @@ __device__ __forceinline__ bool aug_succ(const DevSnap& s, const DevSnap& base, 
 
 // ---- 3. purity: seeds, then "impure if a successor is impure" to a fixpoint
 __global__ void k_aug_seed(DevSnap s, DevSnap base, AugTables A, uint32_t n1, const uint32_t* cand_of,
-                           const uint32_t* c_plan, const uint32_t* c_obj, uint8_t* imp) {
+                           const uint32_t* c_plan, const uint32_t* c_obj, uint8_t* imp, int sharded) {
   const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
   if (v >= n1) return;
   const uint32_t k = cand_of[v];
   if (k == NONE) {  // a plain node: a rewrite that is not materialised, or an undeclared relation
     imp[v] = relflag(s, s.nd_ns[v], s.nd_rel[v]) != 0 ? 1 : 0;
+    return;
+  }
+  if (sharded) {  // rows are this rank's only: every union node is plain (see augment_rewrites)
+    imp[v] = 0;
     return;
   }
   const AugPlan& P = A.plans[c_plan[k]];
@@ -350,8 +365,10 @@ int Snapshot::augment_rewrites() {
   std::vector<uint8_t> virt;
   const char* env = getenv("KG_MATERIALIZE");
   if (env && env[0] == '0') materialize = 0;
-  if (!materialize || shard_n > 1 || !aug_build_plans(this, plans, virt)) return 0;
+  if (!materialize || !aug_build_plans(this, plans, virt)) return 0;
   h_virt = virt;  // the formula splitter's leaves may be union relations (kg_formula.hip)
+  if (alloc((void**)&d_virt, virt.size() + 1)) return -1;
+  HIPC(hipMemcpy(d_virt, virt.data(), virt.size(), hipMemcpyHostToDevice));
   if (ds.n_nodes == 0) return 0;
   const uint32_t n_ns = ds.n_ns, n_rel = ds.n_rel, n0 = ds.n_nodes;
   // contributions: (ns, rel) -> plans whose anchor order lists rel
@@ -399,21 +416,30 @@ int Snapshot::augment_rewrites() {
   DevSnap b = ds;  // the base graph (its node map: nm0)
   b.nmap = nm0;
   b.nmap_n = slots0;
-  // 1. candidates
-  HIPC(hipMemsetAsync(d_cnt, 0, 16, stream));
-  hipLaunchKernelGGL((k_aug_cands<false>), dim3((n0 + 255) / 256), dim3(256), 0, stream, b, A, n0, d_cnt, nullptr,
-                     nullptr, nullptr);
-  uint32_t nc = 0;
-  HIPC(hipMemcpyAsync(&nc, d_cnt, 4, hipMemcpyDeviceToHost, stream));
+  // 1. candidates: count per anchor node, scan, place
+  uint32_t* ccount;
+  uint64_t* cpos;
+  if (talloc((void**)&ccount, ((size_t)n0 + 1) * 4) || talloc((void**)&cpos, ((size_t)n0 + 1) * 8)) return -1;
+  hipLaunchKernelGGL((k_aug_cands<false>), dim3((n0 + 255) / 256), dim3(256), 0, stream, b, A, n0, ccount, nullptr,
+                     nullptr, nullptr, nullptr);
+  HIPC(hipMemsetAsync(ccount + n0, 0, 4, stream));
+  size_t tb0 = 0;
+  HIPC(hipcub::DeviceScan::ExclusiveSum(nullptr, tb0, ccount, cpos, (size_t)n0 + 1, stream));
+  void* scr0;
+  if (talloc(&scr0, tb0 + 16)) return -1;
+  HIPC(hipcub::DeviceScan::ExclusiveSum(scr0, tb0, ccount, cpos, (size_t)n0 + 1, stream));
+  uint64_t nc64 = 0;
+  HIPC(hipMemcpyAsync(&nc64, cpos + n0, 8, hipMemcpyDeviceToHost, stream));
   HIPC(hipStreamSynchronize(stream));
-  if (nc == 0) return 0;
+  if (nc64 == 0) return 0;
+  if (nc64 >= 0x7FFFFFFFull) return set_error(KG_ERR_RESOURCE_CODE, "too many union nodes");
+  const uint32_t nc = (uint32_t)nc64;
   uint32_t *c_plan, *c_obj, *c_base, *c_id;
   if (talloc((void**)&c_plan, (size_t)nc * 4) || talloc((void**)&c_obj, (size_t)nc * 4) ||
       talloc((void**)&c_base, (size_t)nc * 4) || talloc((void**)&c_id, (size_t)nc * 4))
     return -1;
-  HIPC(hipMemsetAsync(d_cnt, 0, 16, stream));
-  hipLaunchKernelGGL((k_aug_cands<true>), dim3((n0 + 255) / 256), dim3(256), 0, stream, b, A, n0, d_cnt, c_plan, c_obj,
-                     c_base);
+  hipLaunchKernelGGL((k_aug_cands<true>), dim3((n0 + 255) / 256), dim3(256), 0, stream, b, A, n0, nullptr,
+                     (const uint64_t*)cpos, c_plan, c_obj, c_base);
   HIPC(hipGetLastError());
   HIPC(hipStreamSynchronize(stream));
   tmp.erase(std::find(tmp.begin(), tmp.end(), (void*)nm0));  // the base node map is done with
@@ -429,13 +455,23 @@ int Snapshot::augment_rewrites() {
   HIPC(hipMemcpyAsync(nd_obj, ds.nd_obj, (size_t)n0 * 4, hipMemcpyDeviceToDevice, stream));
   HIPC(hipMemcpyAsync(nd_rel, ds.nd_rel, (size_t)n0 * 4, hipMemcpyDeviceToDevice, stream));
   HIPC(hipMemsetAsync(cand_of, 0xFF, (size_t)nmax * 4, stream));
-  HIPC(hipMemsetAsync(d_cnt + 1, 0, 4, stream));
+  uint32_t* is_new;
+  uint64_t* new_pos;
+  if (talloc((void**)&is_new, ((size_t)nc + 1) * 4) || talloc((void**)&new_pos, ((size_t)nc + 1) * 8)) return -1;
+  hipLaunchKernelGGL(k_aug_isnew, dim3((nc + 255) / 256), dim3(256), 0, stream, nc, (const uint32_t*)c_base, is_new);
+  HIPC(hipMemsetAsync(is_new + nc, 0, 4, stream));
+  size_t tb1 = 0;
+  HIPC(hipcub::DeviceScan::ExclusiveSum(nullptr, tb1, is_new, new_pos, (size_t)nc + 1, stream));
+  void* scr1;
+  if (talloc(&scr1, tb1 + 16)) return -1;
+  HIPC(hipcub::DeviceScan::ExclusiveSum(scr1, tb1, is_new, new_pos, (size_t)nc + 1, stream));
   hipLaunchKernelGGL(k_aug_ids, dim3((nc + 255) / 256), dim3(256), 0, stream, b, A, nc, n0, c_plan, c_obj, c_base,
-                     d_cnt + 1, c_id, cand_of, nd_ns, nd_obj, nd_rel);
+                     (const uint64_t*)new_pos, c_id, cand_of, nd_ns, nd_obj, nd_rel);
   HIPC(hipGetLastError());
-  uint32_t n_new = 0;
-  HIPC(hipMemcpyAsync(&n_new, d_cnt + 1, 4, hipMemcpyDeviceToHost, stream));
+  uint64_t n_new64 = 0;
+  HIPC(hipMemcpyAsync(&n_new64, new_pos + nc, 8, hipMemcpyDeviceToHost, stream));
   HIPC(hipStreamSynchronize(stream));
+  const uint32_t n_new = (uint32_t)n_new64;
   const uint32_t n1 = n0 + n_new;
   // node map over every node of the extended graph (keys + ids) for the successor lookups
   const uint64_t slots1 = std::max<uint64_t>(16, (uint64_t)n1 * 8 / 5);
@@ -455,9 +491,12 @@ int Snapshot::augment_rewrites() {
   uint8_t* imp;
   if (talloc((void**)&imp, (size_t)n1 + 16)) return -1;
   const uint32_t g1 = (n1 + 255) / 256;
-  hipLaunchKernelGGL(k_aug_seed, dim3(g1), dim3(256), 0, stream, x, b, A, n1, cand_of, c_plan, c_obj, imp);
+  hipLaunchKernelGGL(k_aug_seed, dim3(g1), dim3(256), 0, stream, x, b, A, n1, cand_of, c_plan, c_obj, imp,
+                     shard_n > 1 ? 1 : 0);
   HIPC(hipGetLastError());
-  for (uint64_t it = 0; it <= n1; it++) {  // every round that changes something marks a node
+  // hash-sharded mode: purity needs every rank's rows, so there is no closure -- union nodes are
+  // plain, and a record that reaches a rewrite / undeclared node ends as an error (kg_shard.hip)
+  for (uint64_t it = 0; shard_n == 1 && it <= n1; it++) {  // every round that changes something marks a node
     uint32_t h = 0;
     HIPC(hipMemsetAsync(d_cnt + 2, 0, 4, stream));
     hipLaunchKernelGGL(k_aug_propagate, dim3(g1), dim3(256), 0, stream, x, b, A, n1, cand_of, c_plan, c_obj, imp,

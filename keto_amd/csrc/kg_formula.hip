@@ -24,24 +24,11 @@
 #include <vector>
 
 #include "kg_bfs.h"
+#include "kg_formula.h"
 #include "kg_internal.h"
 #include "kg_snapshot.h"
 
 namespace kg {
-
-constexpr int FP_OPS = 16, FP_LEAVES = 4;
-// postfix program: LEAF | j pushes leaf j's answer; NOT flips the top; AND | k / OR | k fold the top k
-// (k = 0: NotMember for both, as eval_rw answers an empty operator)
-enum : uint8_t { FOP_LEAF = 0x00, FOP_NOT = 0x40, FOP_AND = 0x80, FOP_OR = 0xC0 };
-
-struct FPlan {
-  uint32_t n_ops, n_leaves;
-  uint32_t leaf[FP_LEAVES];  // computed relations (same object)
-  uint8_t ops[FP_OPS];
-  // from the snapshot's nodes at build: some (ns, obj, R) node holds rows (its own part must be
-  // looked up per query); bit j: some node of leaf relation j is impure (leaf j looked up per query)
-  uint32_t own_rows, leaf_impure;
-};
 
 // ------------------------------------------------------------------ device
 __global__ __launch_bounds__(256) void k_fsplit(DevSnap s, const int32_t* __restrict__ fidx,
@@ -119,32 +106,12 @@ __global__ __launch_bounds__(256) void k_fcombine(const FPlan* __restrict__ plan
     return;
   }
   const FPlan& P = plans[r.y];
-  uint32_t e = KG_ERR_NONE;
-  for (uint32_t j = 0; j < P.n_leaves; j++)
+  uint32_t e = KG_ERR_NONE, bits = 0;
+  for (uint32_t j = 0; j < P.n_leaves; j++) {
     if (e == KG_ERR_NONE) e = err2[r.x + j];  // pure leaves do not fail; a resource error would surface
-  uint32_t st = 0;  // answer stack as bits (top = bit sp-1)
-  int sp = 0;
-  for (uint32_t k = 0; k < P.n_ops; k++) {
-    const uint8_t op = P.ops[k];
-    const uint32_t a = op & 0x3F;
-    switch (op & 0xC0) {
-      case FOP_LEAF:
-        st = (st & ~(1u << sp)) | ((out2[r.x + a] == KG_IS_MEMBER ? 1u : 0u) << sp);
-        sp++;
-        break;
-      case FOP_NOT:
-        st ^= 1u << (sp - 1);
-        break;
-      default: {  // AND / OR over the top a entries
-        const uint32_t m = a ? (((1u << a) - 1u) << (sp - (int)a)) : 0u;
-        const uint32_t v = (op & 0xC0) == FOP_AND ? (a && (st & m) == m) : ((st & m) != 0);
-        sp -= (int)a;
-        st = (st & ~(1u << sp)) | (v << sp);
-        sp++;
-        break;
-      }
-    }
+    bits |= (out2[r.x + j] == KG_IS_MEMBER ? 1u : 0u) << j;
   }
+  const uint32_t st = fplan_eval(P, bits) ? 1u : 0u;
   out[i] = (e == KG_ERR_NONE && (st & 1u)) ? KG_IS_MEMBER : KG_NOT_MEMBER;
   if (err) err[i] = e;
 }
@@ -168,7 +135,7 @@ int Snapshot::build_formulas() {
   fp_leaves = 0;
   d_fidx = nullptr;
   d_fplans = nullptr;
-  if (!materialize || shard_n > 1 || !has_program) return 0;
+  if (!materialize || !has_program) return 0;
   const uint32_t n_ns = ds.n_ns, n_rel = ds.n_rel;
   auto flag = [&](uint32_t ns, uint32_t r) -> uint8_t { return host_relflag(ns, r); };
   auto virt = [&](uint32_t ns, uint32_t r) -> bool {

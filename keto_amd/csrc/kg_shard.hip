@@ -27,6 +27,7 @@
 #include <algorithm>
 
 #include "kg_bfs.h"
+#include "kg_formula.h"
 #include "kg_internal.h"
 #include "kg_snapshot.h"
 
@@ -35,7 +36,30 @@ namespace kg {
 constexpr uint32_t Q_BITS = 26, Q_MASK = (1u << Q_BITS) - 1;
 // kg_frec.depth bit 30: the sender's Bloom signature of the node's row rules the subject out, so the
 // owner skips the checkDirect probe (a certain miss); the rest depth sits in the low bits
-constexpr int32_t D_NOPROBE = 1 << 30, D_MASK = D_NOPROBE - 1;
+constexpr int32_t D_NOPROBE = 1 << 30;
+// bit 29: the record checks the own part of a split formula query's node (its rows as a plain node,
+// the node's rewrite evaluated by the formula instead)
+constexpr int32_t D_OWN = 1 << 29, D_MASK = D_OWN - 1;
+
+// Rewrite materialisation runs in this mode too (union nodes are plain; kg_augment.hip), so a node
+// needs the interpreter -- unavailable across shards: an error -- when its own relation has a
+// rewrite that was not materialised or is undeclared.  The node flags say so for every node on
+// every rank alike (relflag for snapshots without them).
+__device__ __forceinline__ bool node_bad(const DevSnap& s, uint32_t node) {
+  if (s.nflags) return (s.nflags[node] & (NF_REWRITE | NF_ERR)) != 0;
+  return relflag(s, s.nd_ns[node], s.nd_rel[node]) != 0;
+}
+
+// Formula split in this mode: a query whose relation has a formula plan (kg_formula.hip) becomes
+// its own part and its leaves as records of their own, in result slots n + i * (1 + leaves) + k;
+// kg_shard_finish evaluates the formula.
+struct ShardFormula {
+  const int32_t* fidx;   // (ns, rel) -> plan or -1; null: no plans
+  const FPlan* plans;
+  uint32_t k;            // slots per split query: 1 (own part) + most leaves
+  const uint8_t* virt;   // (ns, rel) -> union relation (no node: NotMember)
+  uint32_t* ref;         // [n] plan of query i, or NONE
+};
 constexpr int SV_PROBES = 64;
 
 // (query, node) visited table: open addressing, cleared per batch.  1 fresh, 0 seen, -1 full.
@@ -86,13 +110,17 @@ __device__ __forceinline__ void emit(bool act, uint32_t dest, const kg_frec& r, 
 __global__ __launch_bounds__(256) void k_shard_seed(DevSnap s, const kg_query* __restrict__ q, uint32_t n,
                                                     int32_t global, kg_frec* out, uint64_t cap, uint32_t* counts,
                                                     uint8_t* res, uint32_t* err, const uint32_t* __restrict__ held,
-                                                    uint32_t held_n) {
+                                                    uint32_t held_n, ShardFormula F) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  bool act = false;
+  bool act = false, split = false;
   uint32_t dest = 0;
   kg_frec r{};
+  kg_query x{};
+  int32_t dsplit = 0;
+  uint32_t ssubj = NONE;
   if (i < n) {
-    const kg_query x = q[i];
+    if (F.ref) F.ref[i] = NONE;
+    x = q[i];
     uint32_t node = NONE, rsig = 0xFFFFFFFFu;
     if (nmap_key_ok(x.t.ns, x.t.rel, x.t.obj)) {
       const uint64_t key = nmap_key(x.t.ns, x.t.rel, x.t.obj);
@@ -113,8 +141,27 @@ __global__ __launch_bounds__(256) void k_shard_seed(DevSnap s, const kg_query* _
     if (d <= 0 || global < d) d = global;  // engine.go:68-70
     res[i] = KG_NOT_MEMBER;
     err[i] = KG_ERR_NONE;
-    if (relflag(s, x.t.ns, x.t.rel)) {  // rewrites are not part of the sharded mode
+    const uint8_t rf = relflag(s, x.t.ns, x.t.rel);
+    const uint32_t pr = (x.t.ns < s.n_ns && x.t.rel < s.n_rel) ? x.t.ns * s.n_rel + x.t.rel : NONE;
+    const bool virt = F.virt && pr != NONE && F.virt[pr];
+    bool bad = node != NONE ? node_bad(s, node) : (rf != 0 && !virt);  // a union without a node: NotMember
+    if (bad && F.fidx && pr != NONE && F.fidx[pr] >= 0) {  // a formula over plain / union leaves: split
+      const FPlan& P = F.plans[F.fidx[pr]];
+      bool ok = true;
+      for (uint32_t j = 0; j < P.n_leaves; j++) {
+        const uint32_t ln = nmap_find(s, x.t.ns, P.leaf[j], x.t.obj);
+        if (ln != NONE && node_bad(s, ln)) ok = false;
+      }
+      if (ok) {
+        F.ref[i] = (uint32_t)F.fidx[pr];
+        split = true;
+        bad = false;
+      }
+    }
+    if (bad) {  // the interpreter's territory: not evaluated across shards
       err[i] = KG_ERR_NOT_IMPLEMENTED;
+    } else if (split) {
+      // records below, one per part
     } else if (held && !s.relflags && x.t.sns == KG_SUBJECT_ID &&
                (subj == NONE || subj >= held_n || !((held[subj >> 5] >> (subj & 31)) & 1u))) {
       // no row of any rank holds the subject: checkDirect can never hit (NotMember)
@@ -127,8 +174,30 @@ __global__ __launch_bounds__(256) void k_shard_seed(DevSnap s, const kg_query* _
       const bool may = subj == NONE || dest != s.shard_rank || sig_maybe(rsig, subj_sig(subj));
       r = kg_frec{(s.shard_rank << Q_BITS) | i, node, subj, d | (may ? 0 : D_NOPROBE)};
     }
+    dsplit = d;
+    ssubj = subj;
   }
   emit(act, dest, r, out, cap, counts, s.shard_n);
+  // split queries: the own part (slot 0, the node's rows as a plain node) and every leaf (slot 1 + j),
+  // each the checkIsAllowed of its node at the query's depth; a part without a node is NotMember
+  for (uint32_t k = 0; F.fidx && k < F.k; k++) {  // uniform trip count: emit needs every thread
+    bool pa = false;
+    uint32_t pd = 0;
+    kg_frec pr{};
+    if (split && (ssubj != NONE || s.relflags)) {
+      const FPlan& P = F.plans[F.ref[i]];
+      uint32_t pn = NONE;
+      if (k == 0) pn = nmap_find(s, x.t.ns, x.t.rel, x.t.obj);
+      else if (k - 1 < P.n_leaves) pn = nmap_find(s, x.t.ns, P.leaf[k - 1], x.t.obj);
+      if (pn != NONE) {
+        pa = true;
+        pd = s.nowner ? s.nowner[pn] : 0u;
+        const uint32_t slot = n + i * F.k + k;
+        pr = kg_frec{(s.shard_rank << Q_BITS) | slot, pn, ssubj, dsplit | (k == 0 ? D_OWN : 0)};
+      }
+    }
+    emit(pa, pd, pr, out, cap, counts, s.shard_n);
+  }
 }
 
 // One workgroup handles 256 received records per iteration; their set rows are expanded
@@ -152,7 +221,7 @@ __global__ __launch_bounds__(256) void k_shard_level(DevSnap s, const kg_frec* _
     uint64_t rb = 0, len = 0;
     if (i < n_in) {
       r = in[i];
-      const bool probe = !(r.depth & D_NOPROBE);
+      const bool probe = !(r.depth & D_NOPROBE), own = (r.depth & D_OWN) != 0;
       r.depth &= D_MASK;
       if (r.node == KG_FREC_HIT) {
         if ((r.q >> Q_BITS) == me) res[r.q & Q_MASK] = KG_IS_MEMBER;
@@ -164,7 +233,7 @@ __global__ __launch_bounds__(256) void k_shard_level(DevSnap s, const kg_frec* _
       } else {
         const int ins = sv_insert(vis, vmask, ((uint64_t)r.q << 32) | r.node);
         if (ins < 0) atomicOr(&counts[s.shard_n], 2u);
-        if (ins > 0 && relflag(s, s.nd_ns[r.node], s.nd_rel[r.node]) != 0) {  // a rewrite / undeclared relation
+        if (ins > 0 && !own && node_bad(s, r.node)) {  // a rewrite / undeclared relation
           if ((r.q >> Q_BITS) == me) atomicMax(&err[r.q & Q_MASK], (uint32_t)KG_ERR_NOT_IMPLEMENTED);
           else err_out = true;
         } else if (ins > 0) {
@@ -220,7 +289,7 @@ __global__ __launch_bounds__(256) void k_shard_level(DevSnap s, const kg_frec* _
           const bool may = pr.subj == NONE || dest != me || sig_maybe(ax.sig, subj_sig(pr.subj));
           c = kg_frec{pr.q, child, pr.subj, (pr.depth - 1) | (may ? 0 : D_NOPROBE)};
           send = true;
-        } else if (relflag(s, s.nd_ns[child], s.nd_rel[child]) != 0) {  // a depth-0 child with a rewrite
+        } else if (node_bad(s, child)) {  // a depth-0 child with a rewrite
           if ((pr.q >> Q_BITS) == me) {
             atomicMax(&err[pr.q & Q_MASK], (uint32_t)KG_ERR_NOT_IMPLEMENTED);
           } else {
@@ -248,10 +317,38 @@ __global__ void k_shard_done(uint32_t n, const uint8_t* __restrict__ res, uint32
   bits[w] = b;
 }
 
-__global__ void k_shard_finish(uint32_t n, uint8_t* res, const uint32_t* err) {
+__global__ void k_shard_finish(uint32_t n, uint8_t* res, uint32_t* err, ShardFormula F) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n && err[i] != KG_ERR_NONE) res[i] = KG_ERROR;
+  if (i >= n) return;
+  if (F.ref && F.ref[i] != NONE) {  // own part | formula over the leaves (kg_formula.hip)
+    const FPlan& P = F.plans[F.ref[i]];
+    const uint32_t base = n + i * F.k;
+    uint32_t e = KG_ERR_NONE, bits = 0;
+    for (uint32_t k = 0; k < 1 + P.n_leaves; k++)
+      if (e == KG_ERR_NONE) e = err[base + k];
+    for (uint32_t j = 0; j < P.n_leaves; j++) bits |= (res[base + 1 + j] == KG_IS_MEMBER ? 1u : 0u) << j;
+    err[i] = e;
+    res[i] = (res[base] == KG_IS_MEMBER || fplan_eval(P, bits)) ? KG_IS_MEMBER : KG_NOT_MEMBER;
+  }
+  if (err[i] != KG_ERR_NONE) res[i] = KG_ERROR;
 }
+
+// The formula split's tables for a batch of n queries (plans only when the snapshot has them).
+static int shard_formula(Snapshot* s, size_t n, ShardFormula* F) {
+  *F = ShardFormula{nullptr, nullptr, 0, s->d_virt, nullptr};
+  if (!s->n_fplans) return 0;
+  if (n > s->shard_ref_n) {
+    if (s->shard_ref) s->free_alloc(s->shard_ref);
+    s->shard_ref = nullptr;
+    s->shard_ref_n = 0;
+    if (s->alloc((void**)&s->shard_ref, std::max<size_t>(n, 1024) * 4)) return -1;
+    s->shard_ref_n = std::max<size_t>(n, 1024);
+  }
+  *F = ShardFormula{s->d_fidx, (const FPlan*)s->d_fplans, 1 + s->fp_leaves, s->d_virt, s->shard_ref};
+  return 0;
+}
+
+size_t shard_result_slots(const Snapshot* s, size_t n) { return s->n_fplans ? n * (2 + (size_t)s->fp_leaves) : n; }
 
 static int shard_vis_prepare(Snapshot* s, hipStream_t stream) {
   // per-batch (query, node) table of 2^shard_vis_log2 slots (kg_snapshot_tune "shard_vis",
@@ -272,17 +369,24 @@ static int shard_vis_prepare(Snapshot* s, hipStream_t stream) {
 int shard_seed(Snapshot* s, const kg_query* d_q, size_t n, int32_t gdepth, kg_frec* d_out, size_t cap,
                uint32_t* d_counts, uint8_t* d_res, uint32_t* d_err, hipStream_t stream) {
   if (gdepth < 1) gdepth = 5;  // config.schema.json:308-315 default
-  if (n > Q_MASK) return set_error(-2, "sharded batch too large (%zu > %u)", n, Q_MASK);
+  const size_t slots = shard_result_slots(s, n);
+  if (slots > Q_MASK) return set_error(-2, "sharded batch too large (%zu result slots > %u)", slots, Q_MASK);
   HIPC(hipSetDevice(s->device));
   if (!stream) stream = s->stream;
   if (int rc = shard_vis_prepare(s, stream)) return rc;
   HIPC(hipMemsetAsync(d_counts, 0, (s->shard_n + 1) * 4, stream));
+  ShardFormula F;
+  if (shard_formula(s, n, &F)) return -1;
+  if (slots > n) {  // the split parts' slots start NotMember / no error
+    HIPC(hipMemsetAsync(d_res + n, 0, slots - n, stream));
+    HIPC(hipMemsetAsync(d_err + n, 0, (slots - n) * 4, stream));
+  }
   if (n) {
     const uint32_t* held = s->shard_held ? s->shard_held : s->ds.hbits;
     const uint32_t held_n = s->shard_held ? s->shard_held_n : s->ds.hbits_n;
     hipLaunchKernelGGL(k_shard_seed, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, stream, s->ds, d_q, (uint32_t)n,
                        gdepth, d_out, (uint64_t)cap, d_counts, d_res, d_err,
-                       (s->shard_n == 1 || s->shard_held) ? held : nullptr, held_n);
+                       (s->shard_n == 1 || s->shard_held) ? held : nullptr, held_n, F);
     HIPC(hipGetLastError());
   }
   return 0;
@@ -336,11 +440,14 @@ int shard_held(Snapshot* s, uint32_t* d_bits, size_t words, int import, hipStrea
   return 0;
 }
 
-int shard_finish(Snapshot* s, size_t n, uint8_t* d_res, const uint32_t* d_err, hipStream_t stream) {
+int shard_finish(Snapshot* s, size_t n, uint8_t* d_res, uint32_t* d_err, hipStream_t stream) {
   HIPC(hipSetDevice(s->device));
   if (!stream) stream = s->stream;
   if (n) {
-    hipLaunchKernelGGL(k_shard_finish, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, stream, (uint32_t)n, d_res, d_err);
+    ShardFormula F;
+    if (shard_formula(s, n, &F)) return -1;
+    hipLaunchKernelGGL(k_shard_finish, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, stream, (uint32_t)n, d_res,
+                       d_err, F);
     HIPC(hipGetLastError());
   }
   return 0;

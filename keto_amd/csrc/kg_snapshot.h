@@ -167,6 +167,9 @@ struct Snapshot {
   uint64_t n_virtual = 0, n_virtual_new = 0;  // materialised rewrite nodes (kg_augment.hip), of them new ids
   int materialize = 1;  // rewrite materialisation at build (KG_MATERIALIZE=0 turns it off)
   std::vector<uint8_t> h_virt;  // [n_ns * n_rel] materialised union relations (kg_augment.hip)
+  uint8_t* d_virt = nullptr;    // the same on the device (hash-sharded seed)
+  uint32_t* shard_ref = nullptr;  // hash-sharded formula split: plan of every query of the batch
+  size_t shard_ref_n = 0;
   // boolean rewrites over union / plain relations (kg_formula.hip): per (ns, rel) plan index or -1
   int32_t* d_fidx = nullptr;
   void* d_fplans = nullptr;
@@ -259,7 +262,8 @@ int shard_level(Snapshot* s, const kg_frec* d_in, size_t n_in, const uint32_t* d
                 hipStream_t stream);
 int shard_done(Snapshot* s, size_t n, const uint8_t* d_res, uint32_t* d_bits, uint32_t words, hipStream_t stream);
 int shard_held(Snapshot* s, uint32_t* d_bits, size_t words, int import, hipStream_t stream);
-int shard_finish(Snapshot* s, size_t n, uint8_t* d_res, const uint32_t* d_err, hipStream_t stream);
+int shard_finish(Snapshot* s, size_t n, uint8_t* d_res, uint32_t* d_err, hipStream_t stream);
+size_t shard_result_slots(const Snapshot* s, size_t n);
 // kg_grid.hip
 int grid_reserve(Snapshot* s);  // allocates the shared full-size grid pool now (kg_snapshot_tune "grid_reserve")
 // kg_expand.hip

@@ -16,10 +16,13 @@ Rank r of N holds the rows of the nodes (ns, obj, rel) with kg_shard_owner(ns, o
           (every rank reruns the batch with larger buckets) for ONE host round trip per level;
           a single rank enqueues every level without any (record counts stay on the device)
 
-Results are those of the single-GPU engine (bounded reachability over rewrite-free nodes,
-internal/check/engine.go:87-207 with the SURVEY.md 8a semantics); a query that reaches a rewrite
-or an undeclared relation ends as KG_ERROR / KG_ERR_NOT_IMPLEMENTED (rewrites are evaluated by the
-single-GPU engines only).  The local steps are
+Results are those of the single-GPU engine (bounded reachability, internal/check/engine.go:87-207
+with the SURVEY.md 8a semantics).  Union rewrites (or / computedUserset / tupleToUserset) are
+materialised into plain union nodes on every rank alike; a query whose relation is a boolean formula
+over plain or union relations is split into parts (its own rows and one per leaf relation) that
+travel as queries of their own in extra result slots, and kg_shard_finish evaluates the formula.  A
+query that reaches any other rewrite or an undeclared relation ends as KG_ERROR /
+KG_ERR_NOT_IMPLEMENTED (there is no cross-shard interpreter).  The local steps are
 `ShardOps` objects: `HipShardOps` runs them on the GPU through the C ABI; the multi-rank CPU
 tests substitute a test-only restatement to exercise this exchange protocol under gloo.
 """
@@ -90,6 +93,10 @@ class HipShardOps:
     def held_import(self, bits):
         _lib.check(self.L.kg_shard_held(self.snapshot.handle, bits.data_ptr(), int(bits.shape[0]), 1, self._s()),
                    "kg_shard_held")
+
+    def result_slots(self, n: int) -> int:
+        """Result slots of a batch of n queries: n, plus the parts of formula-split queries."""
+        return int(self.L.kg_shard_result_slots(self.snapshot.handle, n))
 
     def finish(self, n, res, err):
         _lib.check(self.L.kg_shard_finish(self.snapshot.handle, n, res.data_ptr(), err.data_ptr(), self._s()),
@@ -228,12 +235,14 @@ class ShardedChecker:
         gdepth = gdepth if gdepth >= 1 else 5  # config.schema.json:308-315 default (as kg_shard_seed)
         if not self._held_ready:
             self._install_held()
-        self._n = n
+        # result slots: the queries, then the parts of formula-split queries (kg_shard_result_slots)
+        slots = self.ops.result_slots(n) if hasattr(self.ops, "result_slots") else n
+        self._n = slots
         prune = hasattr(self.ops, "done_bits")
         bufs = [torch.empty((N * cap, REC_WORDS), dtype=torch.int32, device=self.device) for _ in range(2)]
         counts = [torch.zeros(N + 1, dtype=torch.int32, device=self.device) for _ in range(2)]
-        res = torch.zeros(n, dtype=torch.uint8, device=self.device)
-        err = torch.zeros(n, dtype=torch.int32, device=self.device)
+        res = torch.zeros(slots, dtype=torch.uint8, device=self.device)
+        err = torch.zeros(slots, dtype=torch.int32, device=self.device)
         self.ops.seed(dq, n, gdepth, bufs[0], cap, counts[0], res, err)
         cur = 0
         self.levels = 0
@@ -243,11 +252,11 @@ class ShardedChecker:
             # count read on the device.  A record's depth falls by one per level and seeds carry
             # <= gdepth, so gdepth levels drain the batch; overflow is checked once at the end.
             flags = torch.zeros((), dtype=torch.int64, device=self.device)
-            words = (n + 31) // 32
+            words = (slots + 31) // 32
             for _ in range(gdepth):
                 c = counts[cur]
                 flags |= c[1].to(torch.int64) | (c[0].to(torch.int64) > cap).to(torch.int64)
-                done = self.ops.done_bits(res, n, words) if prune and self.levels > 0 else None
+                done = self.ops.done_bits(res, slots, words) if prune and self.levels > 0 else None
                 self.ops.level(bufs[cur], cap, c, bufs[cur ^ 1], cap, counts[cur ^ 1], res, err, done, words)
                 cur ^= 1
                 self.levels += 1
@@ -260,18 +269,18 @@ class ShardedChecker:
             if int(h[1]) != 0:
                 raise _lib.KetoGPUError("sharded batch: records left after %d levels" % gdepth)
             self.ops.finish(n, res, err)
-            return res, err
+            return res[:n], err[:n]
         while True:
             send, recv_splits, total, flags = self._meta_exchange(counts[cur])
             if flags & 3:
                 raise ShardOverflow(flags)
             if total == 0:
                 self.ops.finish(n, res, err)
-                return res, err
+                return res[:n], err[:n]
             self.records_sent += sum(send)
             recv = self._exchange(bufs[cur], send, recv_splits)
             words = (self._n_max + 31) // 32
-            done = self._done(res, n, words) if prune and self.levels > 0 else None
+            done = self._done(res, slots, words) if prune and self.levels > 0 else None
             cur ^= 1
             self.ops.level(recv, int(recv.shape[0]), None, bufs[cur], cap, counts[cur], res, err, done, words)
             self.levels += 1
