@@ -229,6 +229,15 @@ int kg_synth_ids(const kg_snapshot* s, uint32_t* ids6);
 /* Copies the snapshot's rows back (shard order) as kg_tuple, for oracle cross-checks.
  * rows may be NULL to query the count. */
 int64_t kg_snapshot_export(const kg_snapshot* s, kg_tuple* rows, uint64_t cap);
+/* GetRelationTuples(namespace, object, relation) for n keys at once (keys[i] = (ns, obj, rel) in
+ * (sns, sobj, srel); max_depth ignored): the rows of each key in shard_id order, concatenated --
+ * key i's rows are out[offsets[i] .. offsets[i+1]).  offsets[n+1] is always filled; out == NULL
+ * returns the total only, cap < total is an error (-3).  Raw tuples (a materialised union node's
+ * merged rows are not returned).  A sharded snapshot returns its own rows only.  Not a hot path:
+ * the CheckRelationTuple tree walk (keto_amd/explain.py) reads rows through it.  Replaces
+ * internal/persistence/sql/relationtuples.go:260-270 for the engines' reads. */
+int64_t kg_snapshot_rows(const kg_snapshot* s, const kg_set* keys, size_t n, uint64_t* offsets, kg_tuple* out,
+                         uint64_t cap);
 /* Copies the row index back: row_off[nodes+1], row_subj[rows] (tagged: bit31 = subject set ->
  * node id, else subject id), node triples nd_ns/nd_obj/nd_rel[nodes].  For the CPU baseline. */
 int kg_snapshot_export_csr(const kg_snapshot* s, uint64_t* row_off, uint32_t* row_subj, uint32_t* nd_ns,

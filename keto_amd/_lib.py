@@ -76,7 +76,7 @@ class kg_synth_params(C.Structure):
 EXPORTS = ["kg_snapshot_create", "kg_snapshot_create_on", "kg_snapshot_synthetic", "kg_snapshot_synthetic_on",
            "kg_snapshot_replicas", "kg_snapshot_destroy", "kg_snapshot_info", "kg_snapshot_materialized", "kg_snapshot_tune", "kg_synth_ids",
            "kg_snapshot_create_ordered", "kg_snapshot_apply",
-           "kg_snapshot_export", "kg_snapshot_export_csr", "kg_check_batch", "kg_check_batch_device", "kg_synth_queries", "kg_expand_batch",
+           "kg_snapshot_export", "kg_snapshot_rows", "kg_snapshot_export_csr", "kg_check_batch", "kg_check_batch_device", "kg_synth_queries", "kg_expand_batch",
            "kg_tree_free", "kg_last_error", "kg_version", "kg_shard_owner", "kg_snapshot_create_shard",
            "kg_snapshot_synthetic_shard", "kg_shard_seed", "kg_shard_level", "kg_shard_finish",
            "kg_shard_done", "kg_shard_held_words", "kg_shard_held", "kg_shard_result_slots", "kg_batcher_create", "kg_batcher_check", "kg_batcher_stats", "kg_batcher_reset_stats", "kg_batcher_destroy"]
@@ -121,6 +121,8 @@ def load(path: str = LIB_PATH):
     L.kg_snapshot_tune.argtypes = [vp, C.c_char_p, C.c_int64]
     L.kg_snapshot_export.argtypes = [vp, vp, u64]
     L.kg_snapshot_export.restype = C.c_int64
+    L.kg_snapshot_rows.argtypes = [vp, vp, sz, vp, vp, u64]
+    L.kg_snapshot_rows.restype = C.c_int64
     L.kg_snapshot_export_csr.argtypes = [vp, vp, vp, vp, vp, vp]
     L.kg_snapshot_export_csr.restype = C.c_int
     L.kg_check_batch.argtypes = [vp, vp, sz, i32, vp, vp, C.POINTER(kg_stats)]

@@ -407,6 +407,16 @@ int64_t kg_snapshot_export(const kg_snapshot* sp, kg_tuple* rows, uint64_t cap) 
   KG_GUARD_END
 }
 
+int64_t kg_snapshot_rows(const kg_snapshot* sp, const kg_set* keys, size_t n, uint64_t* offsets, kg_tuple* out,
+                         uint64_t cap) {
+  KG_GUARD_BEGIN
+  if (!sp || (n && (!keys || !offsets))) return set_error(-2, "NULL argument");
+  Snapshot* s = const_cast<Snapshot*>(reinterpret_cast<const Snapshot*>(sp));
+  std::lock_guard<std::mutex> lk(s->mu);
+  return s->rows_of(keys, n, offsets, out, cap);
+  KG_GUARD_END
+}
+
 int kg_snapshot_export_csr(const kg_snapshot* sp, uint64_t* row_off, uint32_t* row_subj, uint32_t* nd_ns,
                            uint32_t* nd_obj, uint32_t* nd_rel) {
   KG_GUARD_BEGIN

@@ -240,6 +240,7 @@ struct Snapshot {
   int build_reverse();
   uint8_t host_relflag(uint32_t ns, uint32_t rel) const;
   int64_t export_rows(kg_tuple* out, uint64_t cap);
+  int64_t rows_of(const kg_set* keys, size_t n, uint64_t* offsets, kg_tuple* out, uint64_t cap);  // kg_rows.hip
 };
 
 // kg_check.hip

@@ -6,7 +6,8 @@ Reference interfaces mirrored (paths relative to the reference checkout):
   Engine.BatchCheck (new)                         == a loop of CheckIsMember
   expand.Engine.BuildTree                                       internal/expand/engine.go:35-104
   config.Provider.MaxReadDepth (default 5, 1..65535)            internal/driver/config/provider.go:160-162
-  checkgroup.Result{Membership, Err}                            internal/check/checkgroup/definitions.go:46-69
+  checkgroup.Result{Membership, Tree, Err}                      internal/check/checkgroup/definitions.go:46-69
+    (the tree of a member result: keto_amd/explain.py)
 """
 from __future__ import annotations
 
@@ -17,7 +18,7 @@ from typing import List, Optional, Sequence, Tuple
 import numpy as np
 
 from . import _lib
-from .ketoapi import RelationTuple, SubjectSet, Tree, TREE_LEAF, TREE_UNION
+from .ketoapi import CheckTree, RelationTuple, SubjectSet, Tree, TREE_LEAF, TREE_UNION
 from .mapper import Interner, Mapper, SUBJECT_ID
 from .namespace import Namespace, Program, compile_program
 
@@ -41,6 +42,7 @@ class CheckError(RuntimeError):
 class Result:
     membership: int
     err: Optional[CheckError] = None
+    tree: Optional[CheckTree] = None
 
 
 @dataclass
@@ -205,6 +207,25 @@ class Snapshot:
             raise _lib.KetoGPUError(_lib.last_error())
         return out
 
+    def rows(self, keys: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
+        """GetRelationTuples(ns, obj, rel) for a (n,3) array of keys on the device snapshot
+        (kg_snapshot_rows): returns (offsets[n+1], tuples (m,6) uint32), key i's rows in shard order at
+        tuples[offsets[i]:offsets[i+1]]."""
+        L = _lib.load()
+        keys = np.asarray(keys, np.uint32).reshape(-1, 3)
+        ks = np.zeros((keys.shape[0], 4), np.uint32)
+        ks[:, :3] = keys[:, [0, 1, 2]]
+        off = np.zeros(keys.shape[0] + 1, np.uint64)
+        n = L.kg_snapshot_rows(self._h, _ptr(ks), keys.shape[0], _ptr(off), None, 0)
+        if n < 0:
+            raise _lib.KetoGPUError(_lib.last_error())
+        out = np.zeros((max(n, 1), 6), np.uint32)
+        if n:
+            got = L.kg_snapshot_rows(self._h, _ptr(ks), keys.shape[0], _ptr(off), _ptr(out), n)
+            if got != n:
+                raise _lib.KetoGPUError(_lib.last_error())
+        return off.astype(np.int64), out[:n]
+
     def close(self) -> None:
         if self._h:
             _lib.load().kg_snapshot_destroy(self._h)
@@ -258,17 +279,28 @@ class Engine:
         return allowed, errs
 
     # ---- single-query API of the reference
-    def check_relation_tuple(self, t: RelationTuple, rest_depth: int) -> Result:
+    def check_relation_tuple(self, t: RelationTuple, rest_depth: int, with_tree: bool = True) -> Result:
+        """CheckRelationTuple (engine.go:65-80): membership, error, and for a member the tree of the
+        branch that answered it (keto_amd/explain.py)."""
         allowed, errs = self.batch_check([t], [rest_depth])
         if errs[0] is not None:
             return Result(MEMBERSHIP_UNKNOWN, errs[0])
-        return Result(IS_MEMBER if allowed[0] else NOT_MEMBER)
+        if not allowed[0]:
+            return Result(NOT_MEMBER)
+        tree = None
+        if with_tree:
+            from .explain import Explainer
+            g = self.config.max_read_depth
+            d = g if rest_depth <= 0 or g < rest_depth else rest_depth  # engine.go:68-70
+            tree = Explainer(self).tree(tuple(int(x) for x in self.snapshot.interner.tuple_ids(t)), d)
+        return Result(IS_MEMBER, None, tree)
 
     def check_is_member(self, t: RelationTuple, rest_depth: int) -> bool:
-        r = self.check_relation_tuple(t, rest_depth)
-        if r.err is not None:
-            raise r.err
-        return r.membership == IS_MEMBER
+        """CheckIsMember (engine.go:54-60): membership only (no tree)."""
+        allowed, errs = self.batch_check([t], [rest_depth])
+        if errs[0] is not None:
+            raise errs[0]
+        return allowed[0]
 
 
 class ExpandEngine:

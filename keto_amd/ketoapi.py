@@ -4,6 +4,9 @@
   (``ns:obj#rel@subject``; a subject containing ``#`` is a subject set, optional parentheses).
 * ``Tree`` follows ``ketoapi/public_api_definitions.go:136-183`` (``TreeNodeType`` strings and
   the ``{type, tuple, children}`` JSON shape used by the expand API and its golden outputs).
+* ``CheckTree`` is ``Tree[*RelationTuple]`` as a check result carries it
+  (``internal/check/checkgroup/definitions.go:46-50``): nodes labelled by whole tuples, ``Label`` /
+  ``String`` as ``ketoapi/enc_string.go:101-152``.
 """
 from __future__ import annotations
 
@@ -143,3 +146,45 @@ def trees_equal_unordered(a: Optional[Tree], b: Optional[Tree]) -> bool:
         else:
             return False
     return True
+
+
+@dataclass
+class CheckTree:
+    """A check result's tree (checkgroup.Result.Tree): ``tuple`` is None for an ``and`` node
+    (binop.go:47-50 builds it without one)."""
+    type: str
+    tuple: Optional[RelationTuple]
+    children: List["CheckTree"] = field(default_factory=list)
+
+    def label(self) -> str:
+        """Tree.Label (enc_string.go:101-107)."""
+        return "" if self.tuple is None else str(self.tuple)
+
+    def __str__(self) -> str:
+        """Tree.String (enc_string.go:109-152)."""
+        if self.type == TREE_LEAF:
+            return f"\u220b {self.label()}\ufe0f"
+        kids = []
+        for i, c in enumerate(self.children):
+            indent = "   " if i == len(self.children) - 1 else "\u2502  "
+            kids.append(("\n" + indent).join(str(c).split("\n")))
+        op = {TREE_INTERSECTION: "and", TREE_UNION: "or", TREE_EXCLUSION: "\\", TREE_NOT: "not",
+              TREE_TTU: "\u2510 tuple to userset", TREE_COMPUTED: "\u2510 computed userset"}.get(self.type, "")
+        box = "\u2514" if len(kids) == 1 else "\u251c"
+        return f"{op} {self.label()}\n{box}\u2500\u2500" + "\n\u2514\u2500\u2500".join(kids)
+
+    def to_json(self) -> dict:
+        d: dict = {"type": self.type}
+        if self.tuple is not None:
+            d["tuple"] = self.tuple.to_json()
+        if self.children:
+            d["children"] = [c.to_json() for c in self.children]
+        return d
+
+    def has_path(self, path: List[str]) -> bool:
+        """rewrites_test.go:263-288 (hasPath): labels from this node down one branch, "*" matches any."""
+        if not path:
+            return True
+        if path[0] != "*" and path[0] != self.label():
+            return False
+        return len(path) == 1 or any(c.has_path(path[1:]) for c in self.children)

@@ -137,10 +137,19 @@ rewrite_expect = [
     ("acl:document#access@bob", True), ("acl:document#allow@mallory", True),
     ("acl:document#access@mallory", False),
 ]
+# expectedPaths (rewrites_test.go:183-187, :202): labels from the check tree's root down one branch
+# each ("*" = any label; the "and" root has no tuple), asserted with hasPath (:263-288)
+rewrite_paths = {
+    "resource:topsecret#delete@mark": [
+        ["*", "resource:topsecret#delete@mark", "level:superadmin#member@mark"],
+        ["*", "resource:topsecret#delete@mark", "resource:topsecret#owner@mark", "group:editors#member@mark"]],
+    "acl:document#access@alice": [["*", "acl:document#access@alice", "acl:document#allow@alice"]],
+}
 rewrite_cases = [{
     "name": "usersets rewrites", "source": "internal/check/rewrites_test.go:101-257",
     "namespaces": rewrite_namespaces, "tuples": rewrite_tuples,
-    "checks": [{"tuple": q, "max_depth": 100, "global_max_depth": 5, "allowed": a} for q, a in rewrite_expect]}]
+    "checks": [dict({"tuple": q, "max_depth": 100, "global_max_depth": 5, "allowed": a},
+                    **({"paths": rewrite_paths[q]} if q in rewrite_paths else {})) for q, a in rewrite_expect]}]
 
 # --------------------------------------------------------------------------- expand
 # internal/expand/engine_test.go
