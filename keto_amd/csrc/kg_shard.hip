@@ -285,10 +285,29 @@ __global__ __launch_bounds__(256) void k_shard_level(DevSnap s, const kg_frec* _
         const uint32_t child = ax.node;
         if (pr.depth >= 2) {
           dest = s.nowner ? s.nowner[child] : 0u;
-          // signatures are built from this rank's rows: only a locally owned child's rules a probe out
-          const bool may = pr.subj == NONE || dest != me || sig_maybe(ax.sig, subj_sig(pr.subj));
-          c = kg_frec{pr.q, child, pr.subj, (pr.depth - 1) | (may ? 0 : D_NOPROBE)};
-          send = true;
+          if (dest == me && !s.relflags) {
+            // a locally owned child without a namespace program: its checkDirect (depth - 2 >= 0) is
+            // probed here, and a record goes out only if the child can still expand (a set row and
+            // depth - 1 >= 2) -- leaves never travel or touch the visited table.  Results are
+            // unchanged (membership is monotone and nothing can end as an error without a program);
+            // a hit only lands one level earlier.
+            const bool hit = pr.subj != NONE && sig_maybe(ax.sig, subj_sig(pr.subj)) && dset_probe(s, child, pr.subj);
+            if (hit && (pr.q >> Q_BITS) == me) {
+              res[pr.q & Q_MASK] = KG_IS_MEMBER;
+            } else if (hit) {
+              c = kg_frec{pr.q, KG_FREC_HIT, 0u, 0};
+              dest = pr.q >> Q_BITS;
+              send = true;
+            } else if (ax.len && pr.depth >= 3) {
+              c = kg_frec{pr.q, child, pr.subj, (pr.depth - 1) | D_NOPROBE};
+              send = true;
+            }
+          } else {
+            // signatures are built from this rank's rows: only a locally owned child's rules a probe out
+            const bool may = pr.subj == NONE || dest != me || sig_maybe(ax.sig, subj_sig(pr.subj));
+            c = kg_frec{pr.q, child, pr.subj, (pr.depth - 1) | (may ? 0 : D_NOPROBE)};
+            send = true;
+          }
         } else if (node_bad(s, child)) {  // a depth-0 child with a rewrite
           if ((pr.q >> Q_BITS) == me) {
             atomicMax(&err[pr.q & Q_MASK], (uint32_t)KG_ERR_NOT_IMPLEMENTED);
