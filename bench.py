@@ -287,6 +287,7 @@ def bench_sharded(a):
                       "parallelism": f"shard{world}"},
            "p99_batch_ms": float(np.percentile(np.array(lat) * 1e3, 99)), "allowed_fraction": float(r.mean()),
            "levels_per_batch": chk.levels, "records_exchanged_per_batch": recs / a.steps,
+           **({"level_records": chk.level_records} if chk.level_records else {}),
            "snapshot_build_s": t_build}
     if rank == 0:
         print(json.dumps(out), flush=True)

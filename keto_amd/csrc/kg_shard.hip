@@ -61,6 +61,13 @@ struct ShardFormula {
   uint32_t* ref;         // [n] plan of query i, or NONE
 };
 constexpr int SV_PROBES = 64;
+// A received record whose set row is longer than this is expanded by the whole grid (k_shard_heavy).
+constexpr uint32_t SHARD_HEAVY = 4096, SHARD_HEAVY_CAP = 1u << 16;
+struct HeavyRow {
+  kg_frec r;  // depth without flag bits
+  uint64_t rb;
+  uint32_t len, pad;
+};
 
 // (query, node) visited table: open addressing, cleared per batch.  1 fresh, 0 seen, -1 full.
 __device__ __forceinline__ int sv_insert(uint64_t* T, uint64_t mask, uint64_t key) {
@@ -121,13 +128,14 @@ __global__ __launch_bounds__(256) void k_shard_seed(DevSnap s, const kg_query* _
   if (i < n) {
     if (F.ref) F.ref[i] = NONE;
     x = q[i];
-    uint32_t node = NONE, rsig = 0xFFFFFFFFu;
+    uint32_t node = NONE, rsig = 0xFFFFFFFFu, rlen = 0;
     if (nmap_key_ok(x.t.ns, x.t.rel, x.t.obj)) {
       const uint64_t key = nmap_key(x.t.ns, x.t.rel, x.t.obj);
       const NSlot* sl = nmap_slot(s, key, hash_home(key, s.nmap_n));
       if (sl) {
         node = sl->node;
         rsig = sl->sig;
+        rlen = sl->len;
       }
     }
     uint32_t subj;
@@ -173,6 +181,18 @@ __global__ __launch_bounds__(256) void k_shard_seed(DevSnap s, const kg_query* _
       // signatures are built from this rank's rows: only a locally owned node's rules a probe out
       const bool may = subj == NONE || dest != s.shard_rank || sig_maybe(rsig, subj_sig(subj));
       r = kg_frec{(s.shard_rank << Q_BITS) | i, node, subj, d | (may ? 0 : D_NOPROBE)};
+      if (dest == s.shard_rank && !s.relflags) {
+        // a locally owned root without a namespace program (as shard_child): checkDirect here, a
+        // record only if the root can expand
+        if (may && d >= 1 && subj != NONE && dset_probe(s, node, subj)) {
+          res[i] = KG_IS_MEMBER;
+          act = false;
+        } else if (rlen == 0 || d < 2) {
+          act = false;
+        } else {
+          r.depth = d | D_NOPROBE;
+        }
+      }
     }
     dsplit = d;
     ssubj = subj;
@@ -200,12 +220,58 @@ __global__ __launch_bounds__(256) void k_shard_seed(DevSnap s, const kg_query* _
   }
 }
 
+// One set-adjacency edge (parent record pr -> child ax) of an expansion: the child's record for its
+// owner, a hit / error report for the query's home, or nothing.
+__device__ __forceinline__ void shard_child(const DevSnap& s, const kg_frec& pr, const AdjX& ax, uint32_t me,
+                                            uint8_t* res, uint32_t* err, kg_frec& c, uint32_t& dest, bool& send) {
+  const uint32_t child = ax.node;
+  if (pr.depth >= 2) {
+    dest = s.nowner ? s.nowner[child] : 0u;
+    if (dest == me && !s.relflags) {
+      // a locally owned child without a namespace program: its checkDirect (depth - 2 >= 0) is
+      // probed here, and a record goes out only if the child can still expand (a set row and
+      // depth - 1 >= 2) -- leaves never travel or touch the visited table.  Results are
+      // unchanged (membership is monotone and nothing can end as an error without a program);
+      // a hit only lands one level earlier.
+      const bool hit = pr.subj != NONE && sig_maybe(ax.sig, subj_sig(pr.subj)) && dset_probe(s, child, pr.subj);
+      if (hit && (pr.q >> Q_BITS) == me) {
+        res[pr.q & Q_MASK] = KG_IS_MEMBER;
+      } else if (hit) {
+        c = kg_frec{pr.q, KG_FREC_HIT, 0u, 0};
+        dest = pr.q >> Q_BITS;
+        send = true;
+      } else if (ax.len && pr.depth >= 3) {
+        c = kg_frec{pr.q, child, pr.subj, (pr.depth - 1) | D_NOPROBE};
+        send = true;
+      }
+    } else {
+      // signatures are built from this rank's rows: only a locally owned child's rules a probe out
+      const bool may = pr.subj == NONE || dest != me || sig_maybe(ax.sig, subj_sig(pr.subj));
+      c = kg_frec{pr.q, child, pr.subj, (pr.depth - 1) | (may ? 0 : D_NOPROBE)};
+      send = true;
+    }
+  } else if (node_bad(s, child)) {  // a depth-0 child with a rewrite
+    if ((pr.q >> Q_BITS) == me) {
+      atomicMax(&err[pr.q & Q_MASK], (uint32_t)KG_ERR_NOT_IMPLEMENTED);
+    } else {
+      c = kg_frec{pr.q, KG_FREC_ERR, (uint32_t)KG_ERR_NOT_IMPLEMENTED, 0};
+      dest = pr.q >> Q_BITS;
+      send = true;
+    }
+  }
+}
+
 // One workgroup handles 256 received records per iteration; their set rows are expanded
-// edge-parallel (block scan of the row lengths, LDS owner search).
+// edge-parallel (block scan of the row lengths, LDS owner search).  A row longer than SHARD_HEAVY
+// (a hub) is not expanded by its workgroup -- one workgroup would hold the level for the whole row --
+// but queued for k_shard_heavy, which spreads its edges over the grid.  (Expanding every row that
+// way instead -- an expansion list walked edge-parallel by a second kernel -- measured slower: the
+// in-workgroup expansion overlaps other workgroups' record processing, profiles/r2s8_*.)
 __global__ __launch_bounds__(256) void k_shard_level(DevSnap s, const kg_frec* __restrict__ in, uint64_t n_bound,
                                                      const uint32_t* d_n_in, kg_frec* out, uint64_t cap, uint32_t* counts, uint8_t* res,
                                                      uint32_t* err, uint64_t* vis, uint64_t vmask,
-                                                     const uint32_t* __restrict__ done, uint32_t done_wpr) {
+                                                     const uint32_t* __restrict__ done, uint32_t done_wpr,
+                                                     HeavyRow* heavy, uint32_t* heavy_n, uint32_t heavy_cap) {
   __shared__ uint32_t s_pref[256], s_wsum[4];
   __shared__ uint64_t s_rb[256];
   __shared__ kg_frec s_rec[256];
@@ -243,9 +309,16 @@ __global__ __launch_bounds__(256) void k_shard_level(DevSnap s, const kg_frec* _
           } else if (r.depth >= 2 || (r.depth == 1 && s.relflags)) {
             // children at depth - 1 >= 1 can still be probed; children at depth 0 cannot, but
             // checkIsAllowed(child, 0) still evaluates astRelationFor (engine.go:199-206), so with a
-            // namespace program their relation flags are checked (below) for the error report
+            // namespace program their relation flags are checked (shard_child) for the error report
             rb = s.adj_off[r.node];
             len = s.adj_off[r.node + 1] - rb;
+            if (len > SHARD_HEAVY) {
+              const uint32_t at = atomicAdd(heavy_n, 1u);
+              if (at < heavy_cap) {
+                heavy[at] = HeavyRow{r, rb, (uint32_t)len, 0u};
+                len = 0;
+              }
+            }
           }
         }
       }
@@ -274,53 +347,35 @@ __global__ __launch_bounds__(256) void k_shard_level(DevSnap s, const kg_frec* _
     __syncthreads();
     for (uint32_t eb = 0; eb < total; eb += 256) {
       const uint32_t e = eb + tid;
-      const bool act = e < total;
       kg_frec c{};
       uint32_t dest = 0;
       bool send = false;
-      if (act) {
+      if (e < total) {
         const int own = owner_search(s_pref, 256, e);
-        const kg_frec& pr = s_rec[own];
-        const AdjX ax = s.adjx[s_rb[own] + (e - s_pref[own])];  // child + its row signature
-        const uint32_t child = ax.node;
-        if (pr.depth >= 2) {
-          dest = s.nowner ? s.nowner[child] : 0u;
-          if (dest == me && !s.relflags) {
-            // a locally owned child without a namespace program: its checkDirect (depth - 2 >= 0) is
-            // probed here, and a record goes out only if the child can still expand (a set row and
-            // depth - 1 >= 2) -- leaves never travel or touch the visited table.  Results are
-            // unchanged (membership is monotone and nothing can end as an error without a program);
-            // a hit only lands one level earlier.
-            const bool hit = pr.subj != NONE && sig_maybe(ax.sig, subj_sig(pr.subj)) && dset_probe(s, child, pr.subj);
-            if (hit && (pr.q >> Q_BITS) == me) {
-              res[pr.q & Q_MASK] = KG_IS_MEMBER;
-            } else if (hit) {
-              c = kg_frec{pr.q, KG_FREC_HIT, 0u, 0};
-              dest = pr.q >> Q_BITS;
-              send = true;
-            } else if (ax.len && pr.depth >= 3) {
-              c = kg_frec{pr.q, child, pr.subj, (pr.depth - 1) | D_NOPROBE};
-              send = true;
-            }
-          } else {
-            // signatures are built from this rank's rows: only a locally owned child's rules a probe out
-            const bool may = pr.subj == NONE || dest != me || sig_maybe(ax.sig, subj_sig(pr.subj));
-            c = kg_frec{pr.q, child, pr.subj, (pr.depth - 1) | (may ? 0 : D_NOPROBE)};
-            send = true;
-          }
-        } else if (node_bad(s, child)) {  // a depth-0 child with a rewrite
-          if ((pr.q >> Q_BITS) == me) {
-            atomicMax(&err[pr.q & Q_MASK], (uint32_t)KG_ERR_NOT_IMPLEMENTED);
-          } else {
-            c = kg_frec{pr.q, KG_FREC_ERR, (uint32_t)KG_ERR_NOT_IMPLEMENTED, 0};
-            dest = pr.q >> Q_BITS;
-            send = true;
-          }
-        }
+        shard_child(s, s_rec[own], s.adjx[s_rb[own] + (e - s_pref[own])], me, res, err, c, dest, send);
       }
       emit(send, dest, c, out, cap, counts, s.shard_n);
     }
     __syncthreads();
+  }
+}
+
+// The hub rows a level queued: every workgroup takes 256-edge chunks of each row in turn.
+__global__ __launch_bounds__(256) void k_shard_heavy(DevSnap s, const HeavyRow* __restrict__ heavy,
+                                                     const uint32_t* __restrict__ heavy_n, uint32_t heavy_cap,
+                                                     kg_frec* out, uint64_t cap, uint32_t* counts, uint8_t* res,
+                                                     uint32_t* err) {
+  const uint32_t nh = min(*heavy_n, heavy_cap), me = s.shard_rank;
+  for (uint32_t h = 0; h < nh; h++) {
+    const HeavyRow H = heavy[h];
+    for (uint64_t eb = (uint64_t)blockIdx.x * 256; eb < H.len; eb += (uint64_t)gridDim.x * 256) {
+      const uint64_t e = eb + threadIdx.x;
+      kg_frec c{};
+      uint32_t dest = 0;
+      bool send = false;
+      if (e < H.len) shard_child(s, H.r, s.adjx[H.rb + e], me, res, err, c, dest, send);
+      emit(send, dest, c, out, cap, counts, s.shard_n);
+    }
   }
 }
 
@@ -371,7 +426,7 @@ size_t shard_result_slots(const Snapshot* s, size_t n) { return s->n_fplans ? n 
 
 static int shard_vis_prepare(Snapshot* s, hipStream_t stream) {
   // per-batch (query, node) table of 2^shard_vis_log2 slots (kg_snapshot_tune "shard_vis",
-  // default 2^25 = 256 MiB); an overflow is reported in the flags and the driver grows it
+  // default 2^23 = 64 MiB); an overflow is reported in the flags and the driver grows it
   const uint64_t slots = 1ull << s->shard_vis_log2;
   if (s->shard_vis && s->shard_vis_slots != slots) {
     HIPC(hipFree(s->shard_vis));
@@ -382,6 +437,9 @@ static int shard_vis_prepare(Snapshot* s, hipStream_t stream) {
     s->shard_vis_slots = slots;
   }
   HIPC(hipMemsetAsync(s->shard_vis, 0xFF, s->shard_vis_slots * 8, stream));
+  if (!s->shard_heavy) {
+    HIPC(hipMalloc(&s->shard_heavy, (size_t)SHARD_HEAVY_CAP * sizeof(HeavyRow) + 64));
+  }
   return 0;
 }
 
@@ -416,12 +474,20 @@ int shard_level(Snapshot* s, const kg_frec* d_in, size_t n_in, const uint32_t* d
                 hipStream_t stream) {
   HIPC(hipSetDevice(s->device));
   if (!stream) stream = s->stream;
-  HIPC(hipMemsetAsync(d_counts, 0, (s->shard_n + 1) * 4, stream));
+  // the bucket sizes restart; the flags word (counts[shard_n]: dropped records, visited table full)
+  // accumulates over the batch's levels, so the caller reads it once at the end
+  HIPC(hipMemsetAsync(d_counts, 0, s->shard_n * 4, stream));
   if (n_in) {
+    HeavyRow* heavy = (HeavyRow*)s->shard_heavy;
+    uint32_t* heavy_n = (uint32_t*)(heavy + SHARD_HEAVY_CAP);
+    HIPC(hipMemsetAsync(heavy_n, 0, 4, stream));
     const uint32_t grid = (uint32_t)std::min<uint64_t>((n_in + 255) / 256, (uint64_t)s->n_cu * 8);
     hipLaunchKernelGGL(k_shard_level, dim3(grid), dim3(256), 0, stream, s->ds, d_in, (uint64_t)n_in, d_n_in, d_out,
                        (uint64_t)cap, d_counts, d_res, d_err, (uint64_t*)s->shard_vis, s->shard_vis_slots - 1,
-                       d_done, d_done ? done_words : 0u);
+                       d_done, d_done ? done_words : 0u, heavy, heavy_n, SHARD_HEAVY_CAP);
+    HIPC(hipGetLastError());
+    hipLaunchKernelGGL(k_shard_heavy, dim3((uint32_t)s->n_cu * 4), dim3(256), 0, stream, s->ds, heavy, heavy_n,
+                       SHARD_HEAVY_CAP, d_out, (uint64_t)cap, d_counts, d_res, d_err);
     HIPC(hipGetLastError());
   }
   return 0;

@@ -196,9 +196,10 @@ struct Snapshot {
   uint32_t shard_rank = 0, shard_n = 1;  // hash-sharded mode (set before create)
   void* shard_vis = nullptr;             // kg_shard.hip: per-batch visited table of (query, node)
   uint64_t shard_vis_slots = 0;
+  void* shard_heavy = nullptr;           // kg_shard.hip: hub rows a level hands to k_shard_heavy (+ count)
   uint32_t* shard_held = nullptr;  // holder bitmap OR-ed over every rank (kg_shard_held), or null
   uint32_t shard_held_n = 0;
-  int shard_vis_log2 = 25;
+  int shard_vis_log2 = 23;
   int stream_variant = 9;  // kg_snapshot_tune("stream"): k_stream variant (0..8) or 9 = k_stream2
   int back_tier = 2;  // kg_snapshot_tune("back"): backward tier (1: wave + workgroup widths, 2: wave only) + no-holder filter
   uint32_t stream_ecap = 0;  // kg_snapshot_tune("stream_ecap"): k_stream edge budget per query (0 = none)

@@ -240,6 +240,7 @@ Snapshot::~Snapshot() {
   for (auto& a : allocs) hipFree(a.first);
   for (Workspace* w : wss) delete w;
   if (shard_vis) hipFree(shard_vis);
+  if (shard_heavy) hipFree(shard_heavy);
   giant.release();
   if (stream) hipStreamDestroy(stream);
 }

@@ -29,6 +29,7 @@ tests substitute a test-only restatement to exercise this exchange protocol unde
 from __future__ import annotations
 
 import ctypes as C
+import os
 from typing import Optional, Tuple
 
 import numpy as np
@@ -60,7 +61,7 @@ class HipShardOps:
                                         self._s()), "kg_shard_seed")
 
     def grow_visited(self):
-        self.vis_log2 = getattr(self, "vis_log2", 25) + 1
+        self.vis_log2 = getattr(self, "vis_log2", 23) + 1
         self.snapshot.tune("shard_vis", self.vis_log2)
 
     def level(self, din, n_in, n_in_dev, out, cap, counts, res, err, done=None, done_words=0):
@@ -123,6 +124,8 @@ class ShardedChecker:
         self.records_sent = 0
         self.host_syncs = 0
         self._held_ready = world == 1 or not hasattr(ops, "held_export")
+        self.trace = bool(int(os.environ.get("KG_SHARD_TRACE", "0")))  # per-level record counts (diagnostics)
+        self.level_records = None
 
     def _install_held(self):
         """Once per snapshot: the OR of every rank's holder bitmap, so kg_shard_seed's no-holder test
@@ -251,18 +254,21 @@ class ShardedChecker:
             # one rank: nothing to exchange, so every level is enqueued back to back with its record
             # count read on the device.  A record's depth falls by one per level and seeds carry
             # <= gdepth, so gdepth levels drain the batch; overflow is checked once at the end.
-            flags = torch.zeros((), dtype=torch.int64, device=self.device)
             words = (slots + 31) // 32
+            trace = [] if self.trace else None
             for _ in range(gdepth):
                 c = counts[cur]
-                flags |= c[1].to(torch.int64) | (c[0].to(torch.int64) > cap).to(torch.int64)
+                if trace is not None:  # diagnostics: records entering each level (a host sync per level)
+                    trace.append(int(c[0].item()))
                 done = self.ops.done_bits(res, slots, words) if prune and self.levels > 0 else None
                 self.ops.level(bufs[cur], cap, c, bufs[cur ^ 1], cap, counts[cur ^ 1], res, err, done, words)
                 cur ^= 1
                 self.levels += 1
+            self.level_records = trace
+            # kg_shard_level accumulates the flags word (counts[N]: a bucket or the visited table
+            # overflowed) over the levels of each of the two count buffers
             c = counts[cur]
-            flags |= c[1].to(torch.int64) | (c[0].to(torch.int64) > cap).to(torch.int64)
-            h = torch.stack([flags, c[0].to(torch.int64)]).cpu().numpy()  # the batch's one host round trip
+            h = torch.stack([counts[0][1] | counts[1][1], c[0]]).cpu().numpy()  # the batch's one host round trip
             self.host_syncs += 1
             if int(h[0]) & 3:
                 raise ShardOverflow(int(h[0]))

@@ -1,12 +1,14 @@
 """Per-batch kernel timeline from a rocprofv3 kernel trace (gaps included): python scripts/timeline.py run_kernel_trace.csv"""
 import csv
+import os
 import re
 import sys
 
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
 short = lambda n: re.sub(r"\(.*", "", n).replace("kg::", "").replace("void ", "")[:40]
-# batches start at k_resolve; show the last complete one
-starts = [i for i, r in enumerate(rows) if "k_resolve" in r["Kernel_Name"]]
+# batches start at k_resolve (ANCHOR: another kernel, e.g. k_shard_seed); show the last complete one
+anchor = os.environ.get("ANCHOR", "k_resolve")
+starts = [i for i, r in enumerate(rows) if anchor in r["Kernel_Name"]]
 b0, b1 = starts[-2], starts[-1]
 t0 = int(rows[b0]["Start_Timestamp"])
 agg = {}
