@@ -55,7 +55,7 @@ def parse():
     ap.add_argument("--tiers", type=int, default=0, help="kg_snapshot_tune tiers (0 grid, 1 LDS-WG+grid, 2 WG)")
     ap.add_argument("--wide", type=int, default=0, help="kg_snapshot_tune wide (k_light<64> tier on/off)")
     ap.add_argument("--stream", type=int, default=9, help="kg_snapshot_tune stream (k_stream variant 0..8, 9 = k_stream2)")
-    ap.add_argument("--stream-ecap", type=int, default=0, help="kg_snapshot_tune stream_ecap (edges per query, 0 = none)")
+    ap.add_argument("--stream-ecap", type=int, default=512, help="kg_snapshot_tune stream_ecap (stream-tier edges per query, 0 = none)")
     ap.add_argument("--grid-wgs", type=int, default=4, help="kg_snapshot_tune grid_wgs (k_grid_level WGs per CU)")
     ap.add_argument("--stream-wgs", type=int, default=3,
                     help="kg_snapshot_tune stream_wgs (k_stream WGs per CU, 0 = by variant: 5 for k_stream2's ~29 KiB "

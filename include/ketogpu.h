@@ -213,6 +213,8 @@ int kg_snapshot_materialized(const kg_snapshot* s, uint64_t* out3);
  * (its overflow goes straight to the grid tier; default); 0 = off.  key "stream": stream-tier
  * kernel -- 9 = k_stream2 (default: 32 query slots per wave over one FIFO, direct-mapped visited
  * cache), 0..8 = the round-1 k_stream variants (see kg_check.hip).
+ * key "stream_ecap": edges a query may enqueue in the stream tier before it is handed to the
+ * backward / grid tiers (default 512; 0 = no budget) -- cuts the stream kernel's tail of long walks.
  * key "stream_wgs": k_stream workgroups per CU (0 = by variant); "back_wgs" (1..3) and "grid_wgs"
  * (1..64): k_back / k_grid_level workgroups per CU.  key "shard_vis": log2 of the
  * hash-sharded mode's per-batch (query, node) visited table (default 25).  key "interp_cap2"

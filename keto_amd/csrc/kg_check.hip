@@ -762,7 +762,7 @@ struct Stream2Lds {
   unsigned long long vt[1 << VLOG2];  // direct-mapped visited cache (0 = empty)
   uint32_t e_beg[QC], e_meta[QC];     // FIFO ring
   uint32_t pref[65];                  // edge-owner marks (+1 dummy)
-  uint32_t s_state[32], s_qi[32], s_subj[32], s_sig[32], s_cnt[32], s_ins[32];
+  uint32_t s_state[32], s_qi[32], s_subj[32], s_sig[32], s_cnt[32], s_ins[32], s_edg[32];
 };
 
 __device__ __forceinline__ uint32_t s2_meta(uint32_t len, uint32_t slot, uint32_t gen, uint32_t depth) {
@@ -789,7 +789,7 @@ __device__ __forceinline__ bool dset_probe_fast(const DevSnap& s, bool want, uin
 template <int VLOG2, int QC, int CHUNK, int INS_CAP>
 __global__ __launch_bounds__(256) void k_stream2(DevSnap s, const RQuery* __restrict__ rq, WorkList wl, uint32_t* heads,
                                                  uint8_t* __restrict__ out, uint32_t* next_list, uint32_t* next_count,
-                                                 Ctl* ctl) {
+                                                 Ctl* ctl, uint32_t ecap) {
   using Lds = Stream2Lds<VLOG2, QC>;
   constexpr uint32_t VT = 1u << VLOG2;
   static_assert(QC <= 256 && (QC & (QC - 1)) == 0, "FIFO ring of <= 256 entries (9-bit generations stay unique)");
@@ -805,6 +805,7 @@ __global__ __launch_bounds__(256) void k_stream2(DevSnap s, const RQuery* __rest
     L.s_state[lane] = 0;
     L.s_cnt[lane] = 0;
     L.s_ins[lane] = 0;
+    L.s_edg[lane] = 0;
   }
   if (lane == 0) L.pref[64] = 0;
   __builtin_amdgcn_wave_barrier();
@@ -852,8 +853,9 @@ __global__ __launch_bounds__(256) void k_stream2(DevSnap s, const RQuery* __rest
         c_left -= got;
         if (mine) {
           const uint32_t slot = lane, gen = L.s_state[slot] & S2_GEN;  // freed slots hold a fresh generation
-          const bool over = qdepth > (int32_t)S2_DMAX || qlen > S2_LONG;
+          const bool over = qdepth > (int32_t)S2_DMAX || qlen > S2_LONG || qlen > ecap;
           L.s_qi[slot] = qi;
+          L.s_edg[slot] = qlen;
           L.s_subj[slot] = qsubj;
           L.s_sig[slot] = subj_sig(qsubj);
           L.s_cnt[slot] = 1;
@@ -940,13 +942,16 @@ __global__ __launch_bounds__(256) void k_stream2(DevSnap s, const RQuery* __rest
     const uint32_t room = QC - (tail - head);
     const uint32_t pos = __popcll(am & ((1ull << lane) - 1));
     const bool appended = ok && pos < room;
+    // edge budget (kg_snapshot_tune "stream_ecap"): a query whose enqueued rows pass it goes on to
+    // the backward / grid tiers instead of holding its wave's FIFO
+    const bool overbudget = appended && ecap != 0xFFFFFFFFu && atomicAdd(&L.s_edg[slot], x.len) + x.len > ecap;
     if (appended) {
       const uint32_t at = (tail + pos) & (QC - 1);
       L.e_beg[at] = x.begin;
       L.e_meta[at] = x.len | (om & 0x01FFF800u) | ((d - 1) << 25);
       atomicAdd(&L.s_cnt[slot], 1u);
     }
-    if (longrow || (fresh && !appended)) atomicOr(&L.s_state[slot], S2_OVER);  // visited cap or FIFO full
+    if (longrow || (fresh && !appended) || overbudget) atomicOr(&L.s_state[slot], S2_OVER);  // visited cap, FIFO full, budget
     tail += min((uint32_t)__popcll(am), room);
     if (h) atomicOr(&L.s_state[pend_slot], S2_HIT);
     pend = act && (keepc ? appended : true) && sig_maybe(x.sig, L.s_sig[slot]);
@@ -1851,7 +1856,7 @@ int check_batch_begin(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n, 
       else if (sv == 8) KG_STREAM(32, V8, 256, 64);
       else if (sv == 9)
         hipLaunchKernelGGL((k_stream2<9, 256, 64, 64>), dim3(grid), dim3(256), 0, stream, s->ds, rq, wl, ctl->heads,
-                           d_out, ovf_list, ovf_count, ctl);
+                           d_out, ovf_list, ovf_count, ctl, ecap);
       else if (sv == 10)
         hipLaunchKernelGGL((k_stream3<9, 256, 64, 64>), dim3(grid), dim3(256), 0, stream, s->ds, rq, wl, ctl->heads,
                            d_out, ovf_list, ovf_count, ctl);
