@@ -66,11 +66,11 @@ def parse():
     ap.add_argument("--interp-wgs", type=int, default=6, help="kg_snapshot_tune interp_wgs (rewrite-path LDS pass WGs per CU)")
     ap.add_argument("--hw-queues", type=int, default=None,
                     help="HIP hardware queues for this process (GPU_MAX_HW_QUEUES, 1..32; 0 = HIP's default, 4; "
-                         "default 8 for --mode expand, else 0): batches in flight beyond the queue count share "
+                         "default 16 for --mode expand, else 0): batches in flight beyond the queue count share "
                          "queues and serialise")
     ap.add_argument("--inflight", type=int, default=None,
                     help="batches in flight per GPU: one HIP stream (own workspace) and one host thread each "
-                         "(default 4; 6 for --mode expand, whose batches end in one long sequential root)")
+                         "(default 4; 16 for --mode expand, whose batches end in long sequential roots)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline time budget (0 = skip)")
     ap.add_argument("--replay", type=int, default=0,
                     help="cycle over this many distinct batches (0 = a distinct batch for every step; diagnostics)")
@@ -440,9 +440,9 @@ def aggregate(dist, elapsed: float, edges: float, device=None):
 def main():
     a = parse()
     if a.hw_queues is None:
-        a.hw_queues = 8 if a.mode == "expand" else 0
+        a.hw_queues = 16 if a.mode == "expand" else 0
     if a.inflight is None:
-        a.inflight = 6 if a.mode == "expand" else 4
+        a.inflight = 16 if a.mode == "expand" else 4
     if a.hw_queues > 0:  # before anything initialises HIP (torch and the library load lazily)
         os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, a.hw_queues))
     if a.tuples is None:
