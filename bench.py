@@ -72,6 +72,8 @@ def parse():
                     help="batches in flight per GPU: one HIP stream (own workspace) and one host thread each "
                          "(default 4; 16 for --mode expand, whose batches end in long sequential roots)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline time budget (0 = skip)")
+    ap.add_argument("--stats-every", type=int, default=1,
+                    help="collect kernel stats on every k-th timed batch (1 = all; a batch with stats is waited for)")
     ap.add_argument("--replay", type=int, default=0,
                     help="cycle over this many distinct batches (0 = a distinct batch for every step; diagnostics)")
     ap.add_argument("--cpu-threads", type=int, default=0,
@@ -551,7 +553,10 @@ def main():
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
-    stats = [_lib.kg_stats() for _ in range(a.steps)]
+    # kernel stats (tier counts, in-kernel work counters, HIP-event kernel times) of every
+    # `stats_every`-th timed batch; a batch with stats waits for its results before its thread
+    # enqueues the next one
+    stats = [_lib.kg_stats() if k % max(1, a.stats_every) == 0 else None for k in range(a.steps)]
     lat = [0.0] * a.steps
     go, th, errs = run_steps(warm, a.steps, stats, lat)
     t0 = time.perf_counter()
@@ -565,7 +570,10 @@ def main():
     res = timed_out.cpu().numpy()
     errs = torch.cat(derrs).cpu().numpy()
     assert (errs == 0).all() and (res <= 1).all(), "unexpected errors in the synthetic batch"
-    elapsed, edges = aggregate(dist, elapsed, float(sum(s.edges_read for s in stats)), f"cuda:{local}")
+    lat = [x for x, st in zip(lat, stats) if st is not None]  # submit-to-done: batches waited for only
+    stats = [x for x in stats if x is not None]
+    elapsed, edges = aggregate(dist, elapsed, float(sum(s.edges_read for s in stats)) * a.steps / len(stats),
+                               f"cuda:{local}")
     l_bytes = np.array([8 * s.light_rows_opened + 4 * s.light_edges_read + 16 * s.light_probes for s in stats], float)
     l_ms = np.array([s.light_ms for s in stats], float)
     achieved = float(l_bytes.mean() / (l_ms.mean() * 1e-3) / 1e9)
