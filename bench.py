@@ -56,6 +56,10 @@ def parse():
     ap.add_argument("--wide", type=int, default=0, help="kg_snapshot_tune wide (k_light<64> tier on/off)")
     ap.add_argument("--stream", type=int, default=9, help="kg_snapshot_tune stream (k_stream variant 0..8, 9 = k_stream2)")
     ap.add_argument("--stream-ecap", type=int, default=512, help="kg_snapshot_tune stream_ecap (stream-tier edges per query, 0 = none)")
+    ap.add_argument("--resolve-unheld", type=int, default=1,
+                    help="kg_snapshot_tune resolve_unheld (1: k_resolve skips the node map for subjects no row holds)")
+    ap.add_argument("--stream-chunk", type=int, default=64,
+                    help="kg_snapshot_tune stream_chunk (k_stream2 queries per dequeue, 1..64)")
     ap.add_argument("--grid-wgs", type=int, default=4, help="kg_snapshot_tune grid_wgs (k_grid_level WGs per CU)")
     ap.add_argument("--stream-wgs", type=int, default=3,
                     help="kg_snapshot_tune stream_wgs (k_stream WGs per CU, 0 = by variant: 5 for k_stream2's ~29 KiB "
@@ -481,6 +485,10 @@ def main():
     snap.tune("back", a.back)
     snap.tune("stream", a.stream)
     snap.tune("stream_ecap", a.stream_ecap)
+    if a.resolve_unheld != 1:
+        snap.tune("resolve_unheld", a.resolve_unheld)
+    if a.stream_chunk != 64:
+        snap.tune("stream_chunk", a.stream_chunk)
     snap.tune("grid_wgs", a.grid_wgs)
     snap.tune("stream_wgs", a.stream_wgs)
     snap.tune("back_wgs", a.back_wgs)
@@ -636,7 +644,8 @@ def stream_diag(s) -> dict:
     steps, waves = int(s.light_steps), int(s.light_waves)
     return {"steps": steps, "waves": waves, "edges_per_step": s.light_edges_read / steps if steps else 0.0,
             "steps_per_wave": steps / waves if waves else 0.0,
-            "mean_wave_us": s.light_wave_ticks / waves / 100.0 if waves else 0.0}
+            "mean_wave_us": s.light_wave_ticks / waves / 100.0 if waves else 0.0,
+            "max_wave_us": s.light_wave_max_ticks / 100.0, "span_us": s.light_span_ticks / 100.0}
 
 
 def pmc_traffic(kernel: str, tuples: int, batch: int, preset: int, inflight: int):

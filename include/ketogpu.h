@@ -106,6 +106,8 @@ typedef struct {
   uint64_t light_steps;                 /* k_stream: wave steps (one HBM round trip each) */
   uint64_t light_waves;                 /* k_stream: waves that ran                      */
   uint64_t light_wave_ticks;            /* k_stream: sum of wave lifetimes (100 MHz ticks) */
+  uint64_t light_span_ticks;            /* k_stream2: first wave start to last wave end  */
+  uint64_t light_wave_max_ticks;        /* k_stream2: longest wave lifetime              */
 } kg_stats;
 
 /* Per-query outputs of kg_check_batch. */
@@ -215,6 +217,9 @@ int kg_snapshot_materialized(const kg_snapshot* s, uint64_t* out3);
  * cache), 0..8 = the round-1 k_stream variants (see kg_check.hip).
  * key "stream_ecap": edges a query may enqueue in the stream tier before it is handed to the
  * backward / grid tiers (default 512; 0 = no budget) -- cuts the stream kernel's tail of long walks.
+ * key "resolve_unheld" (0/1): without a namespace program, k_resolve reads a subject id's holder
+ * bit before the node map and answers an unheld subject NotMember without the lookup (default 1).
+ * key "stream_chunk" (1..64): queries a k_stream2 wave dequeues at once (default 64).
  * key "stream_wgs": k_stream workgroups per CU (0 = by variant); "back_wgs" (1..3) and "grid_wgs"
  * (1..64): k_back / k_grid_level workgroups per CU.  key "shard_vis": log2 of the
  * hash-sharded mode's per-batch (query, node) visited table (default 25).  key "interp_cap2"

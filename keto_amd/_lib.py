@@ -6,7 +6,8 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libketogpu.so")
+# KG_LIB_PATH: another build of the same library (A/B runs of bench.py on one box)
+LIB_PATH = os.environ.get("KG_LIB_PATH") or os.path.join(HERE, "lib", "libketogpu.so")
 
 KG_SUBJECT_ID = 0xFFFFFFFF
 KG_NOT_MEMBER, KG_IS_MEMBER, KG_ERROR = 0, 1, 2
@@ -50,7 +51,8 @@ class kg_stats(C.Structure):
                 ("n_wide", C.c_uint64), ("n_grid", C.c_uint64),
                 ("n_back", C.c_uint64), ("n_no_holder", C.c_uint64), ("back_rows", C.c_uint64),
                 ("back_edges", C.c_uint64), ("light_steps", C.c_uint64), ("light_waves", C.c_uint64),
-                ("light_wave_ticks", C.c_uint64)]
+                ("light_wave_ticks", C.c_uint64),
+                ("light_span_ticks", C.c_uint64), ("light_wave_max_ticks", C.c_uint64)]
 
     def as_dict(self) -> dict:
         return {n: getattr(self, n) for n, _ in self._fields_}

@@ -331,6 +331,16 @@ static int tune_one(Snapshot* s, const char* key, int64_t value) {
     s->stream_ecap = (uint32_t)value;
     return 0;
   }
+  if (strcmp(key, "resolve_unheld") == 0) {
+    if (value < 0 || value > 1) return set_error(-2, "resolve_unheld must be 0 or 1");
+    s->resolve_unheld = (int)value;
+    return 0;
+  }
+  if (strcmp(key, "stream_chunk") == 0) {
+    if (value < 1 || value > 64) return set_error(-2, "stream_chunk must be in [1, 64]");
+    s->stream_chunk = (uint32_t)value;
+    return 0;
+  }
   if (strcmp(key, "stream_wgs") == 0) {
     if (value < 0 || value > 8) return set_error(-2, "stream_wgs must be in [0, 8]");
     s->stream_wgs = (int)value;

@@ -49,6 +49,9 @@ struct Ctl {
   uint32_t light8[8 * 32];  // per-XCD shard sizes of the light list (k_resolve appends)
   unsigned long long st[ST_N];
   unsigned long long st8[8][32];  // per-XCD shards of the hot counters (block-reduced adds)
+  // k_stream2 wave span on the device clock, per XCD shard (one 128-B line each): max of ~start
+  // (= the earliest start), latest end, longest wave -- workgroup-reduced atomicMax on a zeroed block
+  unsigned long long tmax8[8][16];
   InterpCtl ic;
 };
 
@@ -72,6 +75,25 @@ __device__ void block_stats(Ctl* ctl, const int (&idx)[N], const unsigned long l
   if (threadIdx.x < N) {
     const unsigned long long t = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
     if (t) atomicAdd(&ctl->st8[blockIdx.x & 7][idx[threadIdx.x]], t);
+  }
+  __syncthreads();
+}
+
+// Workgroup max of three values (wave-uniform per wave) into XCD shard (blockIdx & 7) of
+// ctl->tmax8: one device atomic per workgroup and value.  Every thread must call it.
+__device__ void block_max3(Ctl* ctl, unsigned long long a, unsigned long long b, unsigned long long c) {
+  __shared__ unsigned long long red[4][3];
+  const int lane = lane_id(), wave = threadIdx.x >> 6;
+  if (lane == 0) {
+    red[wave][0] = a;
+    red[wave][1] = b;
+    red[wave][2] = c;
+  }
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    unsigned long long m = 0;
+    for (int w = 0; w < 4; w++) m = max(m, red[w][threadIdx.x]);
+    atomicMax(&ctl->tmax8[blockIdx.x & 7][threadIdx.x], m);
   }
   __syncthreads();
 }
@@ -123,10 +145,16 @@ __global__ __launch_bounds__(256) void k_resolve(DevSnap s, const kg_query* __re
     uint32_t hw = 0;
     if (use_bits) hw = subj < s.hbits_n ? s.hbits[subj >> 5] : 0u;
     else if (want_h) h0 = s.hslots[hi];
+    // without a namespace program nothing can end as an error, so a subject that no row holds is
+    // NotMember whatever the root: the bit (an Infinity-Cache hit) is read first and such a query
+    // never touches the node map (~13 % of the C2 batch; one random HBM line each)
+    const bool unheld = no_holder_filter == 2 && use_bits && !s.relflags && !((hw >> (subj & 31)) & 1u);
     NSlot n0{};
-    if (key_ok) n0 = s.nmap[ni];
+    if (key_ok && !unheld) n0 = s.nmap[ni];
     uint32_t node = NONE, rb = 0, rl = 0, rsig = 0xFFFFFFFFu;
-    if (key_ok) {
+    if (unheld) {
+      no_holder = true;
+    } else if (key_ok) {
       const NSlot* sl = n0.key == key ? &n0 : (n0.key == EMPTY64 ? nullptr : nmap_slot(s, key, hash_next(ni, s.nmap_n)));
       if (sl) {
         const NSlot v = *sl;
@@ -154,7 +182,9 @@ __global__ __launch_bounds__(256) void k_resolve(DevSnap s, const kg_query* __re
       // the root's checkDirect(D-1) (D >= 1 always) is thread-parallel here: a direct tuple or a
       // depth that cannot reach any child (D < 2) finishes the query before the wave tier.  The
       // row signature in the node-map slot rules out most misses without touching dset.
-      did_probe = subj != NONE && sig_maybe(rsig, subj_sig(subj));
+      // an unset holder bit rules the probe out as well (the exact tuple would make subj a holder)
+      const bool nobit = use_bits && !((hw >> (subj & 31)) & 1u);
+      did_probe = subj != NONE && !nobit && sig_maybe(rsig, subj_sig(subj));
       member = did_probe && dset_probe(s, node, subj);
       if (member || d < 2 || rl == 0) route = ROUTE_DONE;
       // a subject that no row holds cannot be reached from any root (checkDirect never hits)
@@ -789,7 +819,7 @@ __device__ __forceinline__ bool dset_probe_fast(const DevSnap& s, bool want, uin
 template <int VLOG2, int QC, int CHUNK, int INS_CAP>
 __global__ __launch_bounds__(256) void k_stream2(DevSnap s, const RQuery* __restrict__ rq, WorkList wl, uint32_t* heads,
                                                  uint8_t* __restrict__ out, uint32_t* next_list, uint32_t* next_count,
-                                                 Ctl* ctl, uint32_t ecap) {
+                                                 Ctl* ctl, uint32_t ecap, uint32_t chunk) {
   using Lds = Stream2Lds<VLOG2, QC>;
   constexpr uint32_t VT = 1u << VLOG2;
   static_assert(QC <= 256 && (QC & (QC - 1)) == 0, "FIFO ring of <= 256 entries (9-bit generations stay unique)");
@@ -825,7 +855,10 @@ __global__ __launch_bounds__(256) void k_stream2(DevSnap s, const RQuery* __rest
     if (want && !drained && (tail - head) + want <= QC) {
       if (c_left == 0) {
         uint32_t got = 0, first = 0;
-        if (lane == 0) first = dequeue_n(wl, heads, head_sel, head0, CHUNK, got);
+        // chunk (kg_snapshot_tune "stream_chunk", <= CHUNK): one dequeue costs three dependent
+        // round trips (head atomic, list, rq), so small chunks stall the step loop (guided
+        // self-scheduling toward the free-slot count measured 5.3 -> 3.2 x 10^9 checks/s)
+        if (lane == 0) first = dequeue_n(wl, heads, head_sel, head0, chunk, got);
         first = __shfl(first, 0, 64);
         c_left = __shfl(got, 0, 64);
         c_pos = 0;
@@ -982,7 +1015,8 @@ __global__ __launch_bounds__(256) void k_stream2(DevSnap s, const RQuery* __rest
     if (pend && ((freed >> pend_slot) & 1u)) pend = false;
     __builtin_amdgcn_wave_barrier();
   }
-  const unsigned long long life = lane == 0 ? wall_clock64() - t_start : 0ull;
+  const unsigned long long t_end = wall_clock64(), life = lane == 0 ? t_end - t_start : 0ull;
+  block_max3(ctl, ~(unsigned long long)t_start, t_end, t_end - t_start);
   const int idx[7] = {ST_LROWS, ST_LEDGES, ST_LPROBES, ST_LIGHT, ST_LSTEPS, ST_LWAVES, ST_LTICKS};
   const unsigned long long v[7] = {st_rows, st_edges, st_probes, st_done, st_steps, lane == 0 ? 1ull : 0ull, life};
   block_stats<7>(ctl, idx, v);
@@ -1804,7 +1838,8 @@ int check_batch_begin(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n, 
   if (n) {
     const bool use_back = s->back_tier && s->ds.radj;
     hipLaunchKernelGGL(k_resolve, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, stream, s->ds, d_q, (uint32_t)n,
-                       (uint32_t)n_base, n_extra, global_max_depth, rq, d_out, d_err, light, gen, use_back ? 1 : 0, ctl);
+                       (uint32_t)n_base, n_extra, global_max_depth, rq, d_out, d_err, light, gen,
+                       use_back ? (s->resolve_unheld ? 2 : 1) : 0, ctl);
     HIPC(hipGetLastError());
     uint32_t* const after_list = use_medium ? medium : heavy;
     uint32_t* const after_count = use_medium ? &ctl->medium_count : &ctl->heavy_count;
@@ -1856,7 +1891,7 @@ int check_batch_begin(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n, 
       else if (sv == 8) KG_STREAM(32, V8, 256, 64);
       else if (sv == 9)
         hipLaunchKernelGGL((k_stream2<9, 256, 64, 64>), dim3(grid), dim3(256), 0, stream, s->ds, rq, wl, ctl->heads,
-                           d_out, ovf_list, ovf_count, ctl, ecap);
+                           d_out, ovf_list, ovf_count, ctl, ecap, std::max<uint32_t>(1u, std::min<uint32_t>(s->stream_chunk, 64u)));
       else if (sv == 10)
         hipLaunchKernelGGL((k_stream3<9, 256, 64, 64>), dim3(grid), dim3(256), 0, stream, s->ds, rq, wl, ctl->heads,
                            d_out, ovf_list, ovf_count, ctl);
@@ -1993,6 +2028,14 @@ int check_batch_end(Snapshot* s, Workspace* w, BatchPending* bp, bool* reran) {
     stats->light_steps = h.st[ST_LSTEPS];
     stats->light_waves = h.st[ST_LWAVES];
     stats->light_wave_ticks = h.st[ST_LTICKS];
+    unsigned long long t_ns = 0, t_e = 0, l_m = 0;
+    for (int x = 0; x < 8; x++) {
+      t_ns = std::max(t_ns, h.tmax8[x][0]);
+      t_e = std::max(t_e, h.tmax8[x][1]);
+      l_m = std::max(l_m, h.tmax8[x][2]);
+    }
+    stats->light_span_ticks = t_e ? t_e - ~t_ns : 0;
+    stats->light_wave_max_ticks = l_m;
     stats->kernel_ms = ms;
   }
   return 0;

@@ -203,6 +203,8 @@ struct Snapshot {
   int stream_variant = 9;  // kg_snapshot_tune("stream"): k_stream variant (0..8) or 9 = k_stream2
   int back_tier = 2;  // kg_snapshot_tune("back"): backward tier (1: wave + workgroup widths, 2: wave only) + no-holder filter
   uint32_t stream_ecap = 512;  // kg_snapshot_tune("stream_ecap"): stream-tier edge budget per query (0 = none)
+  int resolve_unheld = 1;  // kg_snapshot_tune("resolve_unheld"): k_resolve reads the holder bit before the node map
+  uint32_t stream_chunk = 64;  // kg_snapshot_tune("stream_chunk"): k_stream2 queries per dequeue (1..64)
   int grid_wgs = 16;         // kg_snapshot_tune("grid_wgs"): k_grid_level workgroups per CU
   int stream_wgs = 0;        // kg_snapshot_tune("stream_wgs"): k_stream workgroups per CU (0 = by LDS)
   int interp_wgs = 6;        // kg_snapshot_tune("interp_wgs"): k_interp_lds workgroups (4 waves) per CU (6 fit the LDS)
