@@ -322,7 +322,7 @@ static int tune_one(Snapshot* s, const char* key, int64_t value) {
     return 0;
   }
   if (strcmp(key, "stream") == 0) {
-    if (value < 0 || value > 10) return set_error(-2, "stream must be in [0, 10]");
+    if (value < 0 || value > 11) return set_error(-2, "stream must be in [0, 11]");
     s->stream_variant = (int)value;
     return 0;
   }

@@ -787,11 +787,11 @@ constexpr uint32_t S2_LONG = 2047;  // longest row a FIFO entry can hold (11-bit
 constexpr uint32_t S2_GEN = 0x1FF, S2_DMAX = 127;
 constexpr uint32_t S2_HIT = 1u << 30, S2_OVER = 1u << 31;
 
-template <int VLOG2, int QC>
+template <int VLOG2, int QC, int EPL>
 struct Stream2Lds {
   unsigned long long vt[1 << VLOG2];  // direct-mapped visited cache (0 = empty)
   uint32_t e_beg[QC], e_meta[QC];     // FIFO ring
-  uint32_t pref[65];                  // edge-owner marks (+1 dummy)
+  uint32_t pref[64 * EPL + 1];        // edge-owner marks (+1 dummy)
   uint32_t s_state[32], s_qi[32], s_subj[32], s_sig[32], s_cnt[32], s_ins[32], s_edg[32];
 };
 
@@ -816,11 +816,12 @@ __device__ __forceinline__ bool dset_probe_fast(const DevSnap& s, bool want, uin
   return hit;
 }
 
-template <int VLOG2, int QC, int CHUNK, int INS_CAP>
+template <int VLOG2, int QC, int CHUNK, int INS_CAP, int EPL>
 __global__ __launch_bounds__(256) void k_stream2(DevSnap s, const RQuery* __restrict__ rq, WorkList wl, uint32_t* heads,
                                                  uint8_t* __restrict__ out, uint32_t* next_list, uint32_t* next_count,
                                                  Ctl* ctl, uint32_t ecap, uint32_t chunk) {
-  using Lds = Stream2Lds<VLOG2, QC>;
+  using Lds = Stream2Lds<VLOG2, QC, EPL>;
+  constexpr uint32_t WIN = 64u * EPL;  // edges per step: EPL per lane
   constexpr uint32_t VT = 1u << VLOG2;
   static_assert(QC <= 256 && (QC & (QC - 1)) == 0, "FIFO ring of <= 256 entries (9-bit generations stay unique)");
   static_assert(CHUNK <= 64, "one chunk entry per lane");
@@ -837,7 +838,7 @@ __global__ __launch_bounds__(256) void k_stream2(DevSnap s, const RQuery* __rest
     L.s_ins[lane] = 0;
     L.s_edg[lane] = 0;
   }
-  if (lane == 0) L.pref[64] = 0;
+  if (lane == 0) L.pref[WIN] = 0;
   __builtin_amdgcn_wave_barrier();
   uint32_t active = 0;   // wave-uniform: slots holding a query
   bool drained = false;  // the work list is exhausted (the local chunk may still hold entries)
@@ -845,8 +846,13 @@ __global__ __launch_bounds__(256) void k_stream2(DevSnap s, const RQuery* __rest
   uint32_t cq_qi = 0, cq_node = 0, cq_subj = 0, cq_beg = 0, cq_len = 0;
   int32_t cq_depth = 0;
   uint32_t head = 0, tail = 0, head_off = 0;
-  bool pend = false;
-  uint32_t pend_node = 0, pend_slot = 0, pend_gen = 0;
+  bool pend[EPL];
+  uint32_t pend_node[EPL], pend_slot[EPL], pend_gen[EPL];
+#pragma unroll
+  for (int hf = 0; hf < EPL; hf++) {
+    pend[hf] = false;
+    pend_node[hf] = pend_slot[hf] = pend_gen[hf] = 0;
+  }
   unsigned long long st_rows = 0, st_edges = 0, st_probes = 0, st_done = 0, st_steps = 0;
   for (;;) {
     // ---- refill free slots (their root entries need FIFO room)
@@ -911,7 +917,7 @@ __global__ __launch_bounds__(256) void k_stream2(DevSnap s, const RQuery* __rest
       continue;
     }
     __builtin_amdgcn_wave_barrier();
-    // ---- window: up to 64 FIFO entries from the head
+    // ---- window: up to 64 FIFO entries from the head, up to WIN edges of them
     const uint32_t avail = tail - head;
     uint32_t ebeg = 0, elen = 0, emeta = 0;
     bool live = false;
@@ -930,10 +936,11 @@ __global__ __launch_bounds__(256) void k_stream2(DevSnap s, const RQuery* __rest
     }
     uint32_t total;
     const uint32_t excl = wave_excl_scan(elen, &total);
-    L.pref[lane] = 0;
+#pragma unroll
+    for (int hf = 0; hf < EPL; hf++) L.pref[lane + 64 * hf] = 0;
     __builtin_amdgcn_wave_barrier();
-    const uint32_t taken = min(total, 64u);
-    L.pref[(elen > 0 && excl < taken) ? excl : 64u] = (uint32_t)lane + 1;
+    const uint32_t taken = min(total, WIN);
+    L.pref[(elen > 0 && excl < taken) ? excl : WIN] = (uint32_t)lane + 1;
     const bool consumed = (uint32_t)lane < avail && excl + elen <= taken;
     const uint32_t ncons = __popcll(__ballot(consumed));  // a prefix of the window
     if (consumed && live) atomicSub(&L.s_cnt[(emeta >> 11) & 31u], 1u);
@@ -944,55 +951,98 @@ __global__ __launch_bounds__(256) void k_stream2(DevSnap s, const RQuery* __rest
       else if (ncons > 0) head_off = 0;
     }
     __builtin_amdgcn_wave_barrier();
-    // ---- this step's edge gathers and the previous step's probes, in flight together
-    const bool act = (uint32_t)lane < taken;
-    const int own = ((int)wave_incl_scan<DppMax>(L.pref[lane]) - 1) & 63;
-    const uint32_t ob = __shfl(ebeg, own, 64);
-    const uint32_t om = __shfl(emeta, own, 64);
-    const uint32_t ox = __shfl(excl, own, 64);
-    AdjX x{NONE, 0, 0, 0};
-    if (act) x = s.adjx[ob + ((uint32_t)lane - ox)];
-    const bool pvalid = pend && L.s_state[pend_slot] == pend_gen;
-    const bool h = dset_probe_fast(s, pvalid, pend_node, L.s_subj[pend_slot]);
-    st_probes += pvalid ? 1u : 0u;
+    // ---- this step's edge gathers (edge lane + 64 hf of the window) and the previous step's probes,
+    // all issued before any of them is waited on
+    AdjX x[EPL];
+    uint32_t om[EPL];
+    uint32_t carry = 0;  // the last edge owner mark of the earlier part of the window
+#pragma unroll
+    for (int hf = 0; hf < EPL; hf++) {
+      const uint32_t m = max(wave_incl_scan<DppMax>(L.pref[lane + 64 * hf]), carry);
+      if (EPL > 1) carry = (uint32_t)__builtin_amdgcn_readlane((int)m, 63);
+      const int own = ((int)m - 1) & 63;
+      const uint32_t ob = __shfl(ebeg, own, 64);
+      om[hf] = __shfl(emeta, own, 64);
+      const uint32_t ox = __shfl(excl, own, 64);
+      const uint32_t e = (uint32_t)lane + 64u * hf;
+      x[hf] = AdjX{NONE, 0, 0, 0};
+      if (e < taken) x[hf] = s.adjx[ob + (e - ox)];
+    }
+    bool pvalid[EPL], hit[EPL];
+    uint64_t pkey[EPL];
+    ulonglong2 pb[EPL];
+#pragma unroll
+    for (int hf = 0; hf < EPL; hf++) {
+      pvalid[hf] = pend[hf] && L.s_state[pend_slot[hf]] == pend_gen[hf];
+      pkey[hf] = dset_key(pend_node[hf], L.s_subj[pend_slot[hf]]);
+      pb[hf] = make_ulonglong2(EMPTY64, EMPTY64);
+      if (pvalid[hf]) pb[hf] = *reinterpret_cast<const ulonglong2*>(s.dset + hash_home(pkey[hf], s.dset_nb) * DSET_BUCKET);
+    }
+#pragma unroll
+    for (int hf = 0; hf < EPL; hf++) {
+      // checkDirect probe, first bucket; a chain past a full first bucket (rare at load <= 0.25) is
+      // walked by the lanes that need it under a wave-uniform branch
+      hit[hf] = pvalid[hf] && (pb[hf].x == pkey[hf] || pb[hf].y == pkey[hf]);
+      const bool more = pvalid[hf] && !hit[hf] && pb[hf].y != EMPTY64;
+      if (__ballot(more)) {
+        if (more) hit[hf] = dset_probe(s, pend_node[hf], L.s_subj[pend_slot[hf]]);
+      }
+      st_probes += pvalid[hf] ? 1u : 0u;
+    }
     head += ncons;
     st_edges += (lane == 0) ? taken : 0u;
     st_steps += (lane == 0) ? 1u : 0u;
     // ---- children: kept ones (rest >= 2 after the hop, non-empty set row) are marked + appended;
-    // every child new to the query is probed next step
-    const uint32_t slot = (om >> 11) & 31u, d = om >> 25, g = (om >> 16) & S2_GEN;
-    const bool keepc = act && d >= 3 && x.len > 0;
-    const bool longrow = keepc && x.len > S2_LONG;
-    const unsigned long long key =
-        (1ull << 63) | ((unsigned long long)g << 37) | ((unsigned long long)slot << 32) | x.node;
-    const uint32_t hv = ((x.node * 0x9E3779B1u) ^ (slot * 0x85EBCA77u) ^ (g * 0xC2B2AE3Du)) >> (32 - VLOG2);
-    const unsigned long long old = keepc ? L.vt[hv] : 0ull;
-    const bool fresh = keepc && !longrow && old != key;
-    if (fresh) L.vt[hv] = key;
-    const uint32_t k = fresh ? atomicAdd(&L.s_ins[slot], 1u) : 0u;
-    const bool ok = fresh && k < (uint32_t)INS_CAP;
-    const uint64_t am = __ballot(ok);
-    const uint32_t room = QC - (tail - head);
-    const uint32_t pos = __popcll(am & ((1ull << lane) - 1));
-    const bool appended = ok && pos < room;
-    // edge budget (kg_snapshot_tune "stream_ecap"): a query whose enqueued rows pass it goes on to
-    // the backward / grid tiers instead of holding its wave's FIFO
-    const bool overbudget = appended && ecap != 0xFFFFFFFFu && atomicAdd(&L.s_edg[slot], x.len) + x.len > ecap;
-    if (appended) {
-      const uint32_t at = (tail + pos) & (QC - 1);
-      L.e_beg[at] = x.begin;
-      L.e_meta[at] = x.len | (om & 0x01FFF800u) | ((d - 1) << 25);
-      atomicAdd(&L.s_cnt[slot], 1u);
+    // every child new to the query is probed next step.  Part hf = 0 first: FIFO order stays BFS order
+    bool npend[EPL];
+    uint32_t nslot[EPL], ngen[EPL];
+#pragma unroll
+    for (int hf = 0; hf < EPL; hf++) {
+      const bool act = (uint32_t)lane + 64u * hf < taken;
+      const AdjX& xc = x[hf];
+      const uint32_t slot = (om[hf] >> 11) & 31u, d = om[hf] >> 25, g = (om[hf] >> 16) & S2_GEN;
+      const bool keepc = act && d >= 3 && xc.len > 0;
+      const bool longrow = keepc && xc.len > S2_LONG;
+      const unsigned long long key =
+          (1ull << 63) | ((unsigned long long)g << 37) | ((unsigned long long)slot << 32) | xc.node;
+      const uint32_t hv = ((xc.node * 0x9E3779B1u) ^ (slot * 0x85EBCA77u) ^ (g * 0xC2B2AE3Du)) >> (32 - VLOG2);
+      const unsigned long long old = keepc ? L.vt[hv] : 0ull;
+      const bool fresh = keepc && !longrow && old != key;
+      if (fresh) L.vt[hv] = key;
+      const uint32_t k = fresh ? atomicAdd(&L.s_ins[slot], 1u) : 0u;
+      const bool ok = fresh && k < (uint32_t)INS_CAP;
+      const uint64_t am = __ballot(ok);
+      const uint32_t room = QC - (tail - head);
+      const uint32_t pos = __popcll(am & ((1ull << lane) - 1));
+      const bool appended = ok && pos < room;
+      // edge budget (kg_snapshot_tune "stream_ecap"): a query whose enqueued rows pass it goes on to
+      // the backward / grid tiers instead of holding its wave's FIFO
+      const bool overbudget = appended && ecap != 0xFFFFFFFFu && atomicAdd(&L.s_edg[slot], xc.len) + xc.len > ecap;
+      if (appended) {
+        const uint32_t at = (tail + pos) & (QC - 1);
+        L.e_beg[at] = xc.begin;
+        L.e_meta[at] = xc.len | (om[hf] & 0x01FFF800u) | ((d - 1) << 25);
+        atomicAdd(&L.s_cnt[slot], 1u);
+      }
+      if (longrow || (fresh && !appended) || overbudget) atomicOr(&L.s_state[slot], S2_OVER);  // visited cap, FIFO full, budget
+      tail += min((uint32_t)__popcll(am), room);
+      npend[hf] = act && (keepc ? appended : true) && sig_maybe(xc.sig, L.s_sig[slot]);
+      nslot[hf] = slot;
+      ngen[hf] = g;
+      __builtin_amdgcn_wave_barrier();
     }
-    if (longrow || (fresh && !appended) || overbudget) atomicOr(&L.s_state[slot], S2_OVER);  // visited cap, FIFO full, budget
-    tail += min((uint32_t)__popcll(am), room);
-    if (h) atomicOr(&L.s_state[pend_slot], S2_HIT);
-    pend = act && (keepc ? appended : true) && sig_maybe(x.sig, L.s_sig[slot]);
-    pend_node = x.node;
-    pend_slot = slot;
-    pend_gen = g;
+    uint32_t pmask = 0;
+#pragma unroll
+    for (int hf = 0; hf < EPL; hf++) {
+      if (hit[hf]) atomicOr(&L.s_state[pend_slot[hf]], S2_HIT);
+      pend[hf] = npend[hf];
+      pend_node[hf] = x[hf].node;
+      pend_slot[hf] = nslot[hf];
+      pend_gen[hf] = ngen[hf];
+      pmask |= pend[hf] ? 1u << nslot[hf] : 0u;
+    }
     // ---- finished queries
-    const uint32_t pslots = wave_or(pend ? 1u << slot : 0u);
+    const uint32_t pslots = wave_or(pmask);
     __builtin_amdgcn_wave_barrier();
     bool done = false;
     if (lane < 32 && ((active >> lane) & 1u)) {
@@ -1012,7 +1062,9 @@ __global__ __launch_bounds__(256) void k_stream2(DevSnap s, const RQuery* __rest
     }
     const uint32_t freed = (uint32_t)__ballot(done);
     active &= ~freed;
-    if (pend && ((freed >> pend_slot) & 1u)) pend = false;
+#pragma unroll
+    for (int hf = 0; hf < EPL; hf++)
+      if (pend[hf] && ((freed >> pend_slot[hf]) & 1u)) pend[hf] = false;
     __builtin_amdgcn_wave_barrier();
   }
   const unsigned long long t_end = wall_clock64(), life = lane == 0 ? t_end - t_start : 0ull;
@@ -1037,7 +1089,7 @@ template <int VLOG2, int QC, int CHUNK, int INS_CAP>
 __global__ __launch_bounds__(256) void k_stream3(DevSnap s, const RQuery* __restrict__ rq, WorkList wl, uint32_t* heads,
                                                  uint8_t* __restrict__ out, uint32_t* next_list, uint32_t* next_count,
                                                  Ctl* ctl) {
-  using Lds = Stream2Lds<VLOG2, QC>;
+  using Lds = Stream2Lds<VLOG2, QC, 1>;
   constexpr uint32_t VT = 1u << VLOG2;
   static_assert(QC <= 256 && (QC & (QC - 1)) == 0, "FIFO ring of <= 256 entries (9-bit generations stay unique)");
   static_assert(CHUNK <= 64, "one chunk entry per lane");
@@ -1890,7 +1942,10 @@ int check_batch_begin(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n, 
       else if (sv == 7) KG_STREAM(32, V7, 256, 64);
       else if (sv == 8) KG_STREAM(32, V8, 256, 64);
       else if (sv == 9)
-        hipLaunchKernelGGL((k_stream2<9, 256, 64, 64>), dim3(grid), dim3(256), 0, stream, s->ds, rq, wl, ctl->heads,
+        hipLaunchKernelGGL((k_stream2<9, 256, 64, 64, 1>), dim3(grid), dim3(256), 0, stream, s->ds, rq, wl, ctl->heads,
+                           d_out, ovf_list, ovf_count, ctl, ecap, std::max<uint32_t>(1u, std::min<uint32_t>(s->stream_chunk, 64u)));
+      else if (sv == 11)  // 128-edge windows (two edges per lane)
+        hipLaunchKernelGGL((k_stream2<9, 256, 64, 64, 2>), dim3(grid), dim3(256), 0, stream, s->ds, rq, wl, ctl->heads,
                            d_out, ovf_list, ovf_count, ctl, ecap, std::max<uint32_t>(1u, std::min<uint32_t>(s->stream_chunk, 64u)));
       else if (sv == 10)
         hipLaunchKernelGGL((k_stream3<9, 256, 64, 64>), dim3(grid), dim3(256), 0, stream, s->ds, rq, wl, ctl->heads,
