@@ -57,6 +57,12 @@ def parse():
     ap.add_argument("--stream", type=int, default=9, help="kg_snapshot_tune stream (k_stream variant 0..8, 9 = k_stream2, "
                     "10 = k_stream3, 11 = k_stream2 with 128-edge windows)")
     ap.add_argument("--stream-ecap", type=int, default=512, help="kg_snapshot_tune stream_ecap (stream-tier edges per query, 0 = none)")
+    ap.add_argument("--shard-budget", type=int, default=0,
+                    help="kg_snapshot_tune shard_budget (sharded mode: forward set edges per query and rank before "
+                         "the query escalates to the backward phase; 0 = off)")
+    ap.add_argument("--shard-back-budget", type=int, default=1 << 14,
+                    help="kg_snapshot_tune shard_back_budget (reverse edges per query and rank before the final "
+                         "forward phase takes it)")
     ap.add_argument("--resolve-unheld", type=int, default=1,
                     help="kg_snapshot_tune resolve_unheld (1: k_resolve skips the node map for subjects no row holds)")
     ap.add_argument("--stream-chunk", type=int, default=64,
@@ -256,6 +262,8 @@ def bench_sharded(a):
     snap = Snapshot.synthetic(int(a.tuples), seed=a.seed, device=local, shard=(rank, world), preset=a.preset)
     info = snap.info()
     t_build = time.time() - t_build
+    snap.tune("shard_budget", a.shard_budget)
+    snap.tune("shard_back_budget", a.shard_back_budget)
     B = a.batch
     dq = torch.empty((B, 7), dtype=torch.int32, device=f"cuda:{local}")
     _lib.check(L.kg_synth_queries(snap.handle, 1000 + rank, B, dq.data_ptr()), "kg_synth_queries")
@@ -293,7 +301,9 @@ def bench_sharded(a):
                       "rows_on_rank0": info["rows"], "nodes": info["nodes"], "batch_per_gpu": B,
                       "parallelism": f"shard{world}"},
            "p99_batch_ms": float(np.percentile(np.array(lat) * 1e3, 99)), "allowed_fraction": float(r.mean()),
-           "levels_per_batch": chk.levels, "records_exchanged_per_batch": recs / a.steps,
+           "levels_per_batch": chk.levels, "backward_levels_per_batch": chk.back_levels,
+           "final_levels_per_batch": chk.final_levels, "shard_budget": a.shard_budget,
+           "shard_back_budget": a.shard_back_budget, "records_exchanged_per_batch": recs / a.steps,
            **({"level_records": chk.level_records} if chk.level_records else {}),
            "snapshot_build_s": t_build}
     if rank == 0:

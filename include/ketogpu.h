@@ -313,6 +313,7 @@ typedef struct {
 } kg_frec;
 #define KG_FREC_HIT 0xFFFFFFFFu /* kg_frec.node of a record reporting IsMember to the query's home */
 #define KG_FREC_ERR 0xFFFFFFFEu /* kg_frec.node of a record reporting an error (code in subj)     */
+#define KG_FREC_ESC 0xFFFFFFFDu /* kg_frec.node of a record handing the query to the backward phase */
 #define KG_SHARD_MAX_RANKS 64
 
 uint32_t kg_shard_owner(uint32_t ns, uint32_t obj, uint32_t nranks);
@@ -336,8 +337,37 @@ int kg_shard_level(kg_snapshot* s, const kg_frec* d_in, size_t n_in, const uint3
 /* Early exit across ranks: d_done (may be NULL) is the done bitmap of the batch, done_words words per
  * home rank ([rank][word], bit i = query i of that rank answered IsMember by the previous levels);
  * kg_shard_level drops the records of those queries.  kg_shard_done packs this rank's d_res into its
- * words (words >= ceil(n / 32)); the driver all-gathers them before each level. */
-int kg_shard_done(kg_snapshot* s, size_t n, const uint8_t* d_res, uint32_t* d_bits, uint32_t words, void* stream);
+ * words (words >= ceil(n / 32)); with_escalated 1: queries escalated out of the forward phase count
+ * as done too, 2: those escalated out of the backward phase; the driver all-gathers the words
+ * before each level. */
+int kg_shard_done(kg_snapshot* s, size_t n, const uint8_t* d_res, const uint32_t* d_err, int with_escalated,
+                  uint32_t* d_bits, uint32_t words, void* stream);
+/* Backward phase (snapshots without a namespace program; kg_snapshot_tune "shard_budget", default
+ * 0 = off).  A query whose forward records expand more than the budget of set edges on one
+ * rank escalates: its forward walk stops (d_err carries a batch-internal marker until
+ * kg_shard_finish) and, once no rank sends forward records, it is answered by a reverse search from
+ * its subject's holders -- the single-GPU backward tier across ranks.  kg_shard_back_list writes
+ * this rank's open escalated queries (q, root, subject, depth) into d_list, count in d_counts[0];
+ * the driver all-gathers every rank's lists.  kg_shard_back_seed turns the global list (m entries,
+ * or the count at d_m) into level-0 records: this rank's holders of each subject.
+ * kg_shard_back_level processes a level's records -- ALL ranks' records, all-gathered: a node's
+ * parents live in the rows of their owners, so every rank expands its own -- into one bucket
+ * (d_counts[0]; d_counts[1] = overflow flags, accumulated), until no rank emits anything.  The done
+ * bitmap of this phase is kg_shard_done without escalated queries. */
+int kg_shard_back_list(kg_snapshot* s, size_t n, const uint8_t* d_res, const uint32_t* d_err, kg_frec* d_list,
+                       size_t cap, uint32_t* d_counts, void* stream);
+int kg_shard_back_seed(kg_snapshot* s, const kg_frec* d_list, size_t m, const uint32_t* d_m, kg_frec* d_out,
+                       size_t cap, uint32_t* d_counts, void* stream);
+int kg_shard_back_level(kg_snapshot* s, const kg_frec* d_in, size_t n_in, const uint32_t* d_n_in, kg_frec* d_out,
+                        size_t cap, uint32_t* d_counts, uint8_t* d_res, uint32_t* d_err, const uint32_t* d_done,
+                        uint32_t done_words, void* stream);
+/* The reverse search has its own budget (kg_snapshot_tune "shard_back_budget", reverse edges per
+ * query and rank, default 2^14); a query past it is handed on once more (d_err marker; done bitmap
+ * mode 2 of kg_shard_done during the backward phase) and kg_shard_refwd_seed re-seeds this rank's
+ * such queries at their roots for a final forward phase: kg_shard_level without any budget until
+ * the next kg_shard_seed (the single-GPU engine's stream -> backward -> grid tier chain). */
+int kg_shard_refwd_seed(kg_snapshot* s, size_t n, const uint8_t* d_res, const uint32_t* d_err, kg_frec* d_out,
+                        size_t cap, uint32_t* d_counts, void* stream);
 /* The no-holder test across ranks (k_resolve's in the single-GPU engine): import 0 copies this
  * rank's holder bitmap (bit = a subject id some local row holds) into d_bits[words] (words >=
  * kg_shard_held_words); import 1 installs d_bits -- the OR over all ranks -- so kg_shard_seed

@@ -81,7 +81,8 @@ EXPORTS = ["kg_snapshot_create", "kg_snapshot_create_on", "kg_snapshot_synthetic
            "kg_snapshot_export", "kg_snapshot_rows", "kg_snapshot_export_csr", "kg_check_batch", "kg_check_batch_device", "kg_synth_queries", "kg_expand_batch",
            "kg_tree_free", "kg_last_error", "kg_version", "kg_shard_owner", "kg_snapshot_create_shard",
            "kg_snapshot_synthetic_shard", "kg_shard_seed", "kg_shard_level", "kg_shard_finish",
-           "kg_shard_done", "kg_shard_held_words", "kg_shard_held", "kg_shard_result_slots", "kg_batcher_create", "kg_batcher_check", "kg_batcher_stats", "kg_batcher_reset_stats", "kg_batcher_destroy"]
+           "kg_shard_done", "kg_shard_back_list", "kg_shard_back_seed", "kg_shard_back_level", "kg_shard_refwd_seed",
+           "kg_shard_held_words", "kg_shard_held", "kg_shard_result_slots", "kg_batcher_create", "kg_batcher_check", "kg_batcher_stats", "kg_batcher_reset_stats", "kg_batcher_destroy"]
 
 
 class kg_batcher_stats_t(C.Structure):
@@ -144,7 +145,11 @@ def load(path: str = LIB_PATH):
                                               u32, C.POINTER(vp)]
     L.kg_shard_seed.argtypes = [vp, vp, sz, i32, vp, sz, vp, vp, vp, vp]
     L.kg_shard_level.argtypes = [vp, vp, sz, vp, vp, sz, vp, vp, vp, vp, C.c_uint32, vp]
-    L.kg_shard_done.argtypes = [vp, sz, vp, vp, C.c_uint32, vp]
+    L.kg_shard_done.argtypes = [vp, sz, vp, vp, C.c_int, vp, C.c_uint32, vp]
+    L.kg_shard_back_list.argtypes = [vp, sz, vp, vp, vp, sz, vp, vp]
+    L.kg_shard_back_seed.argtypes = [vp, vp, sz, vp, vp, sz, vp, vp]
+    L.kg_shard_back_level.argtypes = [vp, vp, sz, vp, vp, sz, vp, vp, vp, vp, C.c_uint32, vp]
+    L.kg_shard_refwd_seed.argtypes = [vp, sz, vp, vp, vp, sz, vp, vp]
     L.kg_shard_held_words.argtypes = [vp, vp]
     L.kg_shard_held.argtypes = [vp, vp, sz, C.c_int, vp]
     L.kg_shard_result_slots.argtypes = [vp, sz]
@@ -162,7 +167,8 @@ def load(path: str = LIB_PATH):
                  "kg_snapshot_create_ordered", "kg_snapshot_apply", "kg_synth_ids", "kg_check_batch",
                  "kg_check_batch_device", "kg_synth_queries", "kg_expand_batch", "kg_snapshot_create_shard",
                  "kg_snapshot_synthetic_shard", "kg_shard_seed", "kg_shard_level", "kg_shard_finish",
-                 "kg_shard_done", "kg_shard_held_words", "kg_shard_held", "kg_batcher_create", "kg_batcher_check", "kg_batcher_stats"):
+                 "kg_shard_done", "kg_shard_back_list", "kg_shard_back_seed", "kg_shard_back_level", "kg_shard_refwd_seed",
+                 "kg_shard_held_words", "kg_shard_held", "kg_batcher_create", "kg_batcher_check", "kg_batcher_stats"):
         getattr(L, name).restype = C.c_int
     _lib = L
     return L

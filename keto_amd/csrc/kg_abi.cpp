@@ -247,12 +247,56 @@ int kg_shard_level(kg_snapshot* sp, const kg_frec* d_in, size_t n_in, const uint
   KG_GUARD_END
 }
 
-int kg_shard_done(kg_snapshot* sp, size_t n, const uint8_t* d_res, uint32_t* d_bits, uint32_t words, void* stream) {
+int kg_shard_done(kg_snapshot* sp, size_t n, const uint8_t* d_res, const uint32_t* d_err, int with_escalated,
+                  uint32_t* d_bits, uint32_t words, void* stream) {
   KG_GUARD_BEGIN
   if (!sp || (n && (!d_res || !d_bits))) return set_error(-2, "NULL argument");
   Snapshot* s = reinterpret_cast<Snapshot*>(sp);
   std::lock_guard<std::mutex> lk(s->mu);
-  return kg::shard_done(s, n, d_res, d_bits, words, (hipStream_t)stream);
+  return kg::shard_done(s, n, d_res, d_err, with_escalated, d_bits, words, (hipStream_t)stream);
+  KG_GUARD_END
+}
+
+int kg_shard_back_list(kg_snapshot* sp, size_t n, const uint8_t* d_res, const uint32_t* d_err, kg_frec* d_list,
+                       size_t cap, uint32_t* d_counts, void* stream) {
+  KG_GUARD_BEGIN
+  if (!sp || !d_counts || (n && (!d_res || !d_err || !d_list))) return set_error(-2, "NULL argument");
+  Snapshot* s = reinterpret_cast<Snapshot*>(sp);
+  std::lock_guard<std::mutex> lk(s->mu);
+  return kg::shard_back_list(s, n, d_res, d_err, d_list, cap, d_counts, (hipStream_t)stream);
+  KG_GUARD_END
+}
+
+int kg_shard_back_seed(kg_snapshot* sp, const kg_frec* d_list, size_t m, const uint32_t* d_m, kg_frec* d_out,
+                       size_t cap, uint32_t* d_counts, void* stream) {
+  KG_GUARD_BEGIN
+  if (!sp || !d_counts || (m && (!d_list || !d_out))) return set_error(-2, "NULL argument");
+  Snapshot* s = reinterpret_cast<Snapshot*>(sp);
+  std::lock_guard<std::mutex> lk(s->mu);
+  return kg::shard_back_seed(s, d_list, m, d_m, d_out, cap, d_counts, (hipStream_t)stream);
+  KG_GUARD_END
+}
+
+int kg_shard_back_level(kg_snapshot* sp, const kg_frec* d_in, size_t n_in, const uint32_t* d_n_in, kg_frec* d_out,
+                        size_t cap, uint32_t* d_counts, uint8_t* d_res, uint32_t* d_err, const uint32_t* d_done,
+                        uint32_t done_words, void* stream) {
+  KG_GUARD_BEGIN
+  if (!sp || !d_counts || !d_res || !d_err || (n_in && (!d_in || !d_out))) return set_error(-2, "NULL argument");
+  Snapshot* s = reinterpret_cast<Snapshot*>(sp);
+  std::lock_guard<std::mutex> lk(s->mu);
+  if (!s->shard_vis) return set_error(-2, "kg_shard_back_level before kg_shard_seed");
+  return kg::shard_back_level(s, d_in, n_in, d_n_in, d_out, cap, d_counts, d_res, d_err, d_done, done_words,
+                              (hipStream_t)stream);
+  KG_GUARD_END
+}
+
+int kg_shard_refwd_seed(kg_snapshot* sp, size_t n, const uint8_t* d_res, const uint32_t* d_err, kg_frec* d_out,
+                        size_t cap, uint32_t* d_counts, void* stream) {
+  KG_GUARD_BEGIN
+  if (!sp || !d_counts || (n && (!d_res || !d_err || !d_out))) return set_error(-2, "NULL argument");
+  Snapshot* s = reinterpret_cast<Snapshot*>(sp);
+  std::lock_guard<std::mutex> lk(s->mu);
+  return kg::shard_refwd_seed(s, n, d_res, d_err, d_out, cap, d_counts, (hipStream_t)stream);
   KG_GUARD_END
 }
 
@@ -329,6 +373,16 @@ static int tune_one(Snapshot* s, const char* key, int64_t value) {
   if (strcmp(key, "stream_ecap") == 0) {
     if (value < 0 || value > 0xFFFFFFFFll) return set_error(-2, "stream_ecap must be in [0, 2^32)");
     s->stream_ecap = (uint32_t)value;
+    return 0;
+  }
+  if (strcmp(key, "shard_budget") == 0) {
+    if (value < 0 || value > 0xFFFFFFFFll) return set_error(-2, "shard_budget must be in [0, 2^32)");
+    s->shard_budget = (uint32_t)value;
+    return 0;
+  }
+  if (strcmp(key, "shard_back_budget") == 0) {
+    if (value < 0 || value > 0xFFFFFFFFll) return set_error(-2, "shard_back_budget must be in [0, 2^32)");
+    s->shard_back_budget = (uint32_t)value;
     return 0;
   }
   if (strcmp(key, "resolve_unheld") == 0) {

@@ -61,6 +61,16 @@ struct ShardFormula {
   uint32_t* ref;         // [n] plan of query i, or NONE
 };
 constexpr int SV_PROBES = 64;
+// Escalation (kg_snapshot_tune "shard_budget", snapshots without a namespace program): a query whose
+// forward records have expanded more set edges than the budget on one rank -- a hub-heavy walk, the
+// stream tier's edge budget in the single-GPU engine -- stops walking forward and is answered by the
+// backward phase (reverse search from its subject's holders, kg_shard_back_*).  The home rank marks
+// it with ESC_BIT in err[] while the batch runs (kg_shard_finish clears it).  The reverse search has
+// a budget of its own (shard_back_budget reverse edges per query and rank, the backward tier's); a
+// query past both (ESC2_BIT) is walked forward once more without any budget (kg_shard_refwd_seed) --
+// the single-GPU engine's stream -> backward -> grid tier chain.
+constexpr uint32_t ESC_BIT = 0x40000000u, ESC2_BIT = 0x20000000u;
+constexpr int QCNT_LOG2 = 22;  // per-rank edge counters, hashed by query (a collision only escalates early)
 // A received record whose set row is longer than this is expanded by the whole grid (k_shard_heavy).
 constexpr uint32_t SHARD_HEAVY = 4096, SHARD_HEAVY_CAP = 1u << 16;
 struct HeavyRow {
@@ -117,7 +127,7 @@ __device__ __forceinline__ void emit(bool act, uint32_t dest, const kg_frec& r, 
 __global__ __launch_bounds__(256) void k_shard_seed(DevSnap s, const kg_query* __restrict__ q, uint32_t n,
                                                     int32_t global, kg_frec* out, uint64_t cap, uint32_t* counts,
                                                     uint8_t* res, uint32_t* err, const uint32_t* __restrict__ held,
-                                                    uint32_t held_n, ShardFormula F) {
+                                                    uint32_t held_n, ShardFormula F, uint4* qinfo) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   bool act = false, split = false;
   uint32_t dest = 0;
@@ -196,6 +206,8 @@ __global__ __launch_bounds__(256) void k_shard_seed(DevSnap s, const kg_query* _
     }
     dsplit = d;
     ssubj = subj;
+    // what the backward phase needs of a query that escalates: root, subject, depth
+    if (qinfo) qinfo[i] = make_uint4(node, subj, (uint32_t)d, act ? 1u : 0u);
   }
   emit(act, dest, r, out, cap, counts, s.shard_n);
   // split queries: the own part (slot 0, the node's rows as a plain node) and every leaf (slot 1 + j),
@@ -261,6 +273,32 @@ __device__ __forceinline__ void shard_child(const DevSnap& s, const kg_frec& pr,
   }
 }
 
+// ---- backward phase (escalated queries, snapshots without a namespace program)
+// The reverse search of the single-GPU backward tier (kg_check.hip k_back) across ranks: a path
+// root -> ... -> N of k <= D - 1 set hops ending in a holder N of the subject (a row of N holds it)
+// exists iff the root is met within D - 1 reverse hops from the holders.  Backward records are
+// (q, node, root, rem): node lies `D - 1 - rem` reverse hops from a holder.  A node's parents sit in
+// the rows of their owners, so every rank keeps the reverse set-adjacency of ITS rows (radj: the
+// local parents of any node) and every rank sees every backward record -- the driver all-gathers a
+// level's records instead of exchanging buckets.  Each (q, node) is emitted by the owner of the
+// parent row only, the root test is a compare at the sender, and the first arrival of (q, node) is
+// at its smallest distance (level order), as in the forward phase.
+
+// One reverse edge (record pr at node N -> parent P of N held in this rank's rows).
+__device__ __forceinline__ void back_child(const DevSnap& s, const kg_frec& pr, uint32_t parent, uint32_t me,
+                                           uint8_t* res, kg_frec& c, bool& send) {
+  if (parent == pr.subj) {  // the root: a path of D - 1 - (rem - 1) <= D - 1 hops
+    if ((pr.q >> Q_BITS) == me) res[pr.q & Q_MASK] = KG_IS_MEMBER;
+    else {
+      c = kg_frec{pr.q, KG_FREC_HIT, 0u, 0};
+      send = true;
+    }
+  } else if (pr.depth >= 2) {  // the parent's own parents are still within D - 1 hops
+    c = kg_frec{pr.q, parent, pr.subj, pr.depth - 1};
+    send = true;
+  }
+}
+
 // One workgroup handles 256 received records per iteration; their set rows are expanded
 // edge-parallel (block scan of the row lengths, LDS owner search).  A row longer than SHARD_HEAVY
 // (a hub) is not expanded by its workgroup -- one workgroup would hold the level for the whole row --
@@ -271,7 +309,8 @@ __global__ __launch_bounds__(256) void k_shard_level(DevSnap s, const kg_frec* _
                                                      const uint32_t* d_n_in, kg_frec* out, uint64_t cap, uint32_t* counts, uint8_t* res,
                                                      uint32_t* err, uint64_t* vis, uint64_t vmask,
                                                      const uint32_t* __restrict__ done, uint32_t done_wpr,
-                                                     HeavyRow* heavy, uint32_t* heavy_n, uint32_t heavy_cap) {
+                                                     HeavyRow* heavy, uint32_t* heavy_n, uint32_t heavy_cap,
+                                                     uint32_t* qcnt, uint32_t budget) {
   __shared__ uint32_t s_pref[256], s_wsum[4];
   __shared__ uint64_t s_rb[256];
   __shared__ kg_frec s_rec[256];
@@ -283,7 +322,7 @@ __global__ __launch_bounds__(256) void k_shard_level(DevSnap s, const kg_frec* _
   for (uint64_t base = (uint64_t)blockIdx.x * 256; base < n_in; base += (uint64_t)gridDim.x * 256) {
     const uint64_t i = base + tid;
     kg_frec r{0, NONE, 0, 0};
-    bool hit_out = false, err_out = false;
+    bool hit_out = false, err_out = false, esc_out = false;
     uint64_t rb = 0, len = 0;
     if (i < n_in) {
       r = in[i];
@@ -291,6 +330,8 @@ __global__ __launch_bounds__(256) void k_shard_level(DevSnap s, const kg_frec* _
       r.depth &= D_MASK;
       if (r.node == KG_FREC_HIT) {
         if ((r.q >> Q_BITS) == me) res[r.q & Q_MASK] = KG_IS_MEMBER;
+      } else if (r.node == KG_FREC_ESC) {
+        if ((r.q >> Q_BITS) == me) atomicOr(&err[r.q & Q_MASK], ESC_BIT);
       } else if (r.node == KG_FREC_ERR) {
         if ((r.q >> Q_BITS) == me) atomicMax(&err[r.q & Q_MASK], r.subj);
       } else if (done && ((r.q & Q_MASK) >> 5) < done_wpr &&
@@ -312,6 +353,15 @@ __global__ __launch_bounds__(256) void k_shard_level(DevSnap s, const kg_frec* _
             // namespace program their relation flags are checked (shard_child) for the error report
             rb = s.adj_off[r.node];
             len = s.adj_off[r.node + 1] - rb;
+            if (len && budget) {  // escalation: this rank's set-edge count of the query passes the budget
+              const uint32_t add = (uint32_t)min(len, (uint64_t)budget);
+              const uint32_t old = atomicAdd(&qcnt[mix64(r.q) & ((1u << QCNT_LOG2) - 1)], add);
+              if (old < budget && old + add >= budget) {
+                if ((r.q >> Q_BITS) == me) atomicOr(&err[r.q & Q_MASK], ESC_BIT);
+                else esc_out = true;
+              }
+              if (old + add >= budget) len = 0;  // escalated: the backward phase answers it
+            }
             if (len > SHARD_HEAVY) {
               const uint32_t at = atomicAdd(heavy_n, 1u);
               if (at < heavy_cap) {
@@ -324,8 +374,9 @@ __global__ __launch_bounds__(256) void k_shard_level(DevSnap s, const kg_frec* _
       }
     }
     // hit and error reports go to the query's home
-    kg_frec hr{r.q, err_out ? KG_FREC_ERR : KG_FREC_HIT, err_out ? (uint32_t)KG_ERR_NOT_IMPLEMENTED : 0u, 0};
-    emit(hit_out || err_out, r.q >> Q_BITS, hr, out, cap, counts, s.shard_n);
+    kg_frec hr{r.q, err_out ? KG_FREC_ERR : (esc_out ? KG_FREC_ESC : KG_FREC_HIT),
+               err_out ? (uint32_t)KG_ERR_NOT_IMPLEMENTED : 0u, 0};
+    emit(hit_out || err_out || esc_out, r.q >> Q_BITS, hr, out, cap, counts, s.shard_n);
     // expansion
     s_rb[tid] = rb;
     s_rec[tid] = r;
@@ -360,11 +411,187 @@ __global__ __launch_bounds__(256) void k_shard_level(DevSnap s, const kg_frec* _
   }
 }
 
+// Escalated queries of this rank still open after the forward phase, as backward list entries
+// (q, root, subject, depth); they go to every rank.  The (query, node) table is cleared for the
+// backward keys.
+__global__ __launch_bounds__(256) void k_shard_back_list(uint32_t n, const uint8_t* __restrict__ res,
+                                                         const uint32_t* __restrict__ err, const uint4* __restrict__ qinfo,
+                                                         uint32_t me, kg_frec* out, uint64_t cap, uint32_t* counts) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  bool act = false;
+  kg_frec r{};
+  if (i < n && (err[i] & ESC_BIT) && res[i] != KG_IS_MEMBER) {
+    const uint4 qi = qinfo[i];
+    // an escalated query was seeded (qi.w), has a root, a subject and depth >= 2 (it expanded)
+    act = qi.w != 0 && qi.y != NONE;
+    r = kg_frec{(me << Q_BITS) | i, qi.x, qi.y, (int32_t)qi.z};
+  }
+  emit(act, 0u, r, out, cap, counts, 1u);
+}
+
+// The final forward phase: this rank's queries that escalated out of both the forward and the
+// backward budget, re-seeded at their roots (their owners probe the root again).
+__global__ __launch_bounds__(256) void k_shard_refwd_seed(DevSnap s, uint32_t n, const uint8_t* __restrict__ res,
+                                                          const uint32_t* __restrict__ err,
+                                                          const uint4* __restrict__ qinfo, kg_frec* out, uint64_t cap,
+                                                          uint32_t* counts) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  bool act = false;
+  kg_frec r{};
+  uint32_t dest = 0;
+  if (i < n && (err[i] & ESC2_BIT) && res[i] != KG_IS_MEMBER) {
+    const uint4 qi = qinfo[i];
+    act = qi.w != 0;
+    r = kg_frec{(s.shard_rank << Q_BITS) | i, qi.x, qi.y, (int32_t)qi.z};
+    dest = act && s.nowner ? s.nowner[qi.x] : 0u;
+  }
+  emit(act, dest, r, out, cap, counts, s.shard_n);
+}
+
+// Level 0 of the backward phase: for every listed query, this rank's holders N of its subject
+// (rows of N hold it) at distance 0, as records (q, N, root, D - 1).  The holder lists are walked
+// edge-parallel like set rows.  A holder that is the root would be a direct tuple, answered by the
+// forward phase's root probe.
+__global__ __launch_bounds__(256) void k_shard_back_seed(DevSnap s, const kg_frec* __restrict__ list, uint64_t m_bound,
+                                                         const uint32_t* d_m, kg_frec* out, uint64_t cap,
+                                                         uint32_t* counts) {
+  __shared__ uint32_t s_pref[256], s_wsum[4], s_first[256];
+  __shared__ kg_frec s_rec[256];
+  const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+  const uint64_t m = d_m ? min((uint64_t)*d_m, m_bound) : m_bound;
+  for (uint64_t base = (uint64_t)blockIdx.x * 256; base < m; base += (uint64_t)gridDim.x * 256) {
+    const uint64_t i = base + tid;
+    uint32_t cnt = 0, first = 0;
+    kg_frec r{0, NONE, NONE, 0};
+    if (i < m) {
+      const kg_frec e = list[i];
+      if (e.depth >= 2) {  // holders at distance 0 lead to the root within D - 1 hops only if D - 1 >= 1
+        const uint2 h = holders_find(s, e.subj);
+        first = h.x;
+        cnt = h.y;
+        r = kg_frec{e.q, NONE, e.node, e.depth - 1};  // subj carries the root from here on
+      }
+    }
+    s_first[tid] = first;
+    s_rec[tid] = r;
+    uint32_t v = cnt, x = v, total = 0, before = 0;
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t y = __shfl_up(v, off, 64);
+      if (lane >= off) v += y;
+    }
+    if (lane == 63) s_wsum[wave] = v;
+    __syncthreads();
+    for (int w = 0; w < 4; w++) {
+      if (w < wave) before += s_wsum[w];
+      total += s_wsum[w];
+    }
+    s_pref[tid] = before + v - x;
+    __syncthreads();
+    for (uint32_t eb = 0; eb < total; eb += 256) {
+      const uint32_t e = eb + tid;
+      kg_frec c{};
+      bool send = false;
+      if (e < total) {
+        const int own = owner_search(s_pref, 256, e);
+        const kg_frec& pr = s_rec[own];
+        c = kg_frec{pr.q, s.hold[s_first[own] + (e - s_pref[own])], pr.subj, pr.depth};
+        send = c.node != pr.subj;
+      }
+      emit(send, 0u, c, out, cap, counts, 1u);
+    }
+    __syncthreads();
+  }
+}
+
+// One backward level over the all-gathered records: hit reports for this rank's queries, else
+// dedup (query, node) and expand this rank's parents of the node (reverse rows longer than
+// SHARD_HEAVY go to k_shard_heavy).  Records go to one bucket (the next level's all-gather).
+__global__ __launch_bounds__(256) void k_shard_back_level(DevSnap s, const kg_frec* __restrict__ in, uint64_t n_bound,
+                                                          const uint32_t* d_n_in, kg_frec* out, uint64_t cap,
+                                                          uint32_t* counts, uint8_t* res, uint32_t* err, uint64_t* vis,
+                                                          uint64_t vmask, const uint32_t* __restrict__ done,
+                                                          uint32_t done_wpr, HeavyRow* heavy, uint32_t* heavy_n,
+                                                          uint32_t heavy_cap, uint32_t* qcnt, uint32_t budget) {
+  __shared__ uint32_t s_pref[256], s_wsum[4];
+  __shared__ uint64_t s_rb[256];
+  __shared__ kg_frec s_rec[256];
+  const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+  const uint32_t me = s.shard_rank;
+  const uint64_t n_in = d_n_in ? min((uint64_t)*d_n_in, n_bound) : n_bound;
+  for (uint64_t base = (uint64_t)blockIdx.x * 256; base < n_in; base += (uint64_t)gridDim.x * 256) {
+    const uint64_t i = base + tid;
+    kg_frec r{0, NONE, 0, 0};
+    uint64_t rb = 0, len = 0;
+    bool esc_out = false;
+    if (i < n_in) {
+      r = in[i];
+      if (r.node == KG_FREC_HIT) {
+        if ((r.q >> Q_BITS) == me) res[r.q & Q_MASK] = KG_IS_MEMBER;
+      } else if (r.node == KG_FREC_ESC) {
+        if ((r.q >> Q_BITS) == me) atomicOr(&err[r.q & Q_MASK], ESC2_BIT);
+      } else if (done && ((r.q & Q_MASK) >> 5) < done_wpr &&
+                 ((done[(size_t)(r.q >> Q_BITS) * done_wpr + ((r.q & Q_MASK) >> 5)] >> (r.q & 31)) & 1u)) {
+        // answered IsMember by an earlier level
+      } else {
+        const int ins = sv_insert(vis, vmask, ((uint64_t)r.q << 32) | r.node);
+        if (ins < 0) atomicOr(&counts[1], 2u);
+        if (ins > 0 && r.depth >= 1) {
+          rb = s.radj_off[r.node];
+          len = s.radj_off[r.node + 1] - rb;
+          if (len && budget) {  // the reverse search's own budget: past it, the final forward phase
+            const uint32_t add = (uint32_t)min(len, (uint64_t)budget);
+            const uint32_t old = atomicAdd(&qcnt[mix64(r.q) & ((1u << QCNT_LOG2) - 1)], add);
+            if (old < budget && old + add >= budget) {
+              if ((r.q >> Q_BITS) == me) atomicOr(&err[r.q & Q_MASK], ESC2_BIT);
+              else esc_out = true;
+            }
+            if (old + add >= budget) len = 0;
+          }
+          if (len > SHARD_HEAVY) {
+            const uint32_t at = atomicAdd(heavy_n, 1u);
+            if (at < heavy_cap) {
+              heavy[at] = HeavyRow{r, rb, (uint32_t)len, 1u};
+              len = 0;
+            }
+          }
+        }
+      }
+    }
+    emit(esc_out, 0u, kg_frec{r.q, KG_FREC_ESC, 0u, 0}, out, cap, counts, 1u);  // to the home, via the all-gather
+    s_rb[tid] = rb;
+    s_rec[tid] = r;
+    uint32_t v = (uint32_t)len, x = v, total = 0, before = 0;
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t y = __shfl_up(v, off, 64);
+      if (lane >= off) v += y;
+    }
+    if (lane == 63) s_wsum[wave] = v;
+    __syncthreads();
+    for (int w = 0; w < 4; w++) {
+      if (w < wave) before += s_wsum[w];
+      total += s_wsum[w];
+    }
+    s_pref[tid] = before + v - x;
+    __syncthreads();
+    for (uint32_t eb = 0; eb < total; eb += 256) {
+      const uint32_t e = eb + tid;
+      kg_frec c{};
+      bool send = false;
+      if (e < total) {
+        const int own = owner_search(s_pref, 256, e);
+        back_child(s, s_rec[own], s.radj[s_rb[own] + (e - s_pref[own])], me, res, c, send);
+      }
+      emit(send, 0u, c, out, cap, counts, 1u);
+    }
+    __syncthreads();
+  }
+}
+
 // The hub rows a level queued: every workgroup takes 256-edge chunks of each row in turn.
 __global__ __launch_bounds__(256) void k_shard_heavy(DevSnap s, const HeavyRow* __restrict__ heavy,
                                                      const uint32_t* __restrict__ heavy_n, uint32_t heavy_cap,
                                                      kg_frec* out, uint64_t cap, uint32_t* counts, uint8_t* res,
-                                                     uint32_t* err) {
+                                                     uint32_t* err, uint32_t nranks) {
   const uint32_t nh = min(*heavy_n, heavy_cap), me = s.shard_rank;
   for (uint32_t h = 0; h < nh; h++) {
     const HeavyRow H = heavy[h];
@@ -373,20 +600,25 @@ __global__ __launch_bounds__(256) void k_shard_heavy(DevSnap s, const HeavyRow* 
       kg_frec c{};
       uint32_t dest = 0;
       bool send = false;
-      if (e < H.len) shard_child(s, H.r, s.adjx[H.rb + e], me, res, err, c, dest, send);
-      emit(send, dest, c, out, cap, counts, s.shard_n);
+      if (e < H.len) {
+        if (H.pad) back_child(s, H.r, s.radj[H.rb + e], me, res, c, send);  // a reverse row (backward phase)
+        else shard_child(s, H.r, s.adjx[H.rb + e], me, res, err, c, dest, send);
+      }
+      emit(send, dest, c, out, cap, counts, nranks);
     }
   }
 }
 
-// Done bitmap of this rank's queries (IsMember so far), one word per thread.
-__global__ void k_shard_done(uint32_t n, const uint8_t* __restrict__ res, uint32_t words, uint32_t* __restrict__ bits) {
+// Done bitmap of this rank's queries (IsMember so far, or an err bit of esc_mask: escalated out of
+// the current phase), one word per thread.
+__global__ void k_shard_done(uint32_t n, const uint8_t* __restrict__ res, const uint32_t* __restrict__ err,
+                             uint32_t esc_mask, uint32_t words, uint32_t* __restrict__ bits) {
   const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
   if (w >= words) return;
   uint32_t b = 0;
   for (uint32_t k = 0; k < 32; k++) {
     const uint32_t i = w * 32 + k;
-    if (i < n && res[i] == KG_IS_MEMBER) b |= 1u << k;
+    if (i < n && (res[i] == KG_IS_MEMBER || (esc_mask && (err[i] & esc_mask)))) b |= 1u << k;
   }
   bits[w] = b;
 }
@@ -394,6 +626,7 @@ __global__ void k_shard_done(uint32_t n, const uint8_t* __restrict__ res, uint32
 __global__ void k_shard_finish(uint32_t n, uint8_t* res, uint32_t* err, ShardFormula F) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
+  err[i] &= ~(ESC_BIT | ESC2_BIT);  // the escalation markers are batch-internal
   if (F.ref && F.ref[i] != NONE) {  // own part | formula over the leaves (kg_formula.hip)
     const FPlan& P = F.plans[F.ref[i]];
     const uint32_t base = n + i * F.k;
@@ -443,6 +676,10 @@ static int shard_vis_prepare(Snapshot* s, hipStream_t stream) {
   return 0;
 }
 
+// Escalation is on for snapshots without a namespace program (errors below the root cannot occur)
+// whose reverse indexes exist, with a non-zero budget.
+static bool shard_escalates(const Snapshot* s) { return s->shard_budget && !s->ds.relflags && s->ds.radj; }
+
 int shard_seed(Snapshot* s, const kg_query* d_q, size_t n, int32_t gdepth, kg_frec* d_out, size_t cap,
                uint32_t* d_counts, uint8_t* d_res, uint32_t* d_err, hipStream_t stream) {
   if (gdepth < 1) gdepth = 5;  // config.schema.json:308-315 default
@@ -452,6 +689,21 @@ int shard_seed(Snapshot* s, const kg_query* d_q, size_t n, int32_t gdepth, kg_fr
   if (!stream) stream = s->stream;
   if (int rc = shard_vis_prepare(s, stream)) return rc;
   HIPC(hipMemsetAsync(d_counts, 0, (s->shard_n + 1) * 4, stream));
+  s->shard_final = false;
+  uint4* qinfo = nullptr;
+  if (shard_escalates(s)) {
+    if (!s->shard_qcnt) HIPC(hipMalloc(&s->shard_qcnt, (4ull << QCNT_LOG2)));
+    HIPC(hipMemsetAsync(s->shard_qcnt, 0, (4ull << QCNT_LOG2), stream));
+    if (slots > s->shard_qinfo_n) {
+      if (s->shard_qinfo) HIPC(hipFree(s->shard_qinfo));
+      s->shard_qinfo = nullptr;
+      s->shard_qinfo_n = 0;
+      HIPC(hipMalloc(&s->shard_qinfo, std::max<size_t>(slots, 1024) * sizeof(uint4)));
+      s->shard_qinfo_n = std::max<size_t>(slots, 1024);
+    }
+    qinfo = (uint4*)s->shard_qinfo;
+    if (slots > n) HIPC(hipMemsetAsync(qinfo + n, 0, (slots - n) * sizeof(uint4), stream));
+  }
   ShardFormula F;
   if (shard_formula(s, n, &F)) return -1;
   if (slots > n) {  // the split parts' slots start NotMember / no error
@@ -463,7 +715,7 @@ int shard_seed(Snapshot* s, const kg_query* d_q, size_t n, int32_t gdepth, kg_fr
     const uint32_t held_n = s->shard_held ? s->shard_held_n : s->ds.hbits_n;
     hipLaunchKernelGGL(k_shard_seed, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, stream, s->ds, d_q, (uint32_t)n,
                        gdepth, d_out, (uint64_t)cap, d_counts, d_res, d_err,
-                       (s->shard_n == 1 || s->shard_held) ? held : nullptr, held_n, F);
+                       (s->shard_n == 1 || s->shard_held) ? held : nullptr, held_n, F, qinfo);
     HIPC(hipGetLastError());
   }
   return 0;
@@ -484,21 +736,96 @@ int shard_level(Snapshot* s, const kg_frec* d_in, size_t n_in, const uint32_t* d
     const uint32_t grid = (uint32_t)std::min<uint64_t>((n_in + 255) / 256, (uint64_t)s->n_cu * 8);
     hipLaunchKernelGGL(k_shard_level, dim3(grid), dim3(256), 0, stream, s->ds, d_in, (uint64_t)n_in, d_n_in, d_out,
                        (uint64_t)cap, d_counts, d_res, d_err, (uint64_t*)s->shard_vis, s->shard_vis_slots - 1,
-                       d_done, d_done ? done_words : 0u, heavy, heavy_n, SHARD_HEAVY_CAP);
+                       d_done, d_done ? done_words : 0u, heavy, heavy_n, SHARD_HEAVY_CAP, (uint32_t*)s->shard_qcnt,
+                       shard_escalates(s) && s->shard_qcnt && !s->shard_final ? s->shard_budget : 0u);
     HIPC(hipGetLastError());
     hipLaunchKernelGGL(k_shard_heavy, dim3((uint32_t)s->n_cu * 4), dim3(256), 0, stream, s->ds, heavy, heavy_n,
-                       SHARD_HEAVY_CAP, d_out, (uint64_t)cap, d_counts, d_res, d_err);
+                       SHARD_HEAVY_CAP, d_out, (uint64_t)cap, d_counts, d_res, d_err, s->shard_n);
     HIPC(hipGetLastError());
   }
   return 0;
 }
 
-int shard_done(Snapshot* s, size_t n, const uint8_t* d_res, uint32_t* d_bits, uint32_t words, hipStream_t stream) {
+int shard_done(Snapshot* s, size_t n, const uint8_t* d_res, const uint32_t* d_err, int with_esc, uint32_t* d_bits,
+               uint32_t words, hipStream_t stream) {
   HIPC(hipSetDevice(s->device));
   if (!stream) stream = s->stream;
   if (words < (n + 31) / 32) return set_error(-2, "done bitmap too small (%u words for %zu queries)", words, n);
+  if (with_esc && !d_err) return set_error(-2, "kg_shard_done: with_escalated needs d_err");
+  if (with_esc < 0 || with_esc > 2) return set_error(-2, "kg_shard_done: with_escalated must be 0, 1 or 2");
   if (words) {
-    hipLaunchKernelGGL(k_shard_done, dim3((words + 255) / 256), dim3(256), 0, stream, (uint32_t)n, d_res, words, d_bits);
+    hipLaunchKernelGGL(k_shard_done, dim3((words + 255) / 256), dim3(256), 0, stream, (uint32_t)n, d_res, d_err,
+                       with_esc == 1 ? ESC_BIT : (with_esc == 2 ? ESC2_BIT : 0u), words, d_bits);
+    HIPC(hipGetLastError());
+  }
+  return 0;
+}
+
+int shard_back_list(Snapshot* s, size_t n, const uint8_t* d_res, const uint32_t* d_err, kg_frec* d_list, size_t cap,
+                    uint32_t* d_counts, hipStream_t stream) {
+  HIPC(hipSetDevice(s->device));
+  if (!stream) stream = s->stream;
+  HIPC(hipMemsetAsync(d_counts, 0, 8, stream));
+  if (!s->shard_vis) return set_error(-2, "kg_shard_back_list before kg_shard_seed");
+  HIPC(hipMemsetAsync(s->shard_vis, 0xFF, s->shard_vis_slots * 8, stream));  // backward keys start clear
+  if (s->shard_qcnt) HIPC(hipMemsetAsync(s->shard_qcnt, 0, (4ull << QCNT_LOG2), stream));  // reverse-edge counts
+  if (n && shard_escalates(s) && s->shard_qinfo && n <= s->shard_qinfo_n) {
+    hipLaunchKernelGGL(k_shard_back_list, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, stream, (uint32_t)n, d_res,
+                       d_err, (const uint4*)s->shard_qinfo, s->shard_rank, d_list, (uint64_t)cap, d_counts);
+    HIPC(hipGetLastError());
+  }
+  return 0;
+}
+
+int shard_refwd_seed(Snapshot* s, size_t n, const uint8_t* d_res, const uint32_t* d_err, kg_frec* d_out, size_t cap,
+                     uint32_t* d_counts, hipStream_t stream) {
+  HIPC(hipSetDevice(s->device));
+  if (!stream) stream = s->stream;
+  HIPC(hipMemsetAsync(d_counts, 0, (s->shard_n + 1) * 4, stream));
+  if (!s->shard_vis) return set_error(-2, "kg_shard_refwd_seed before kg_shard_seed");
+  HIPC(hipMemsetAsync(s->shard_vis, 0xFF, s->shard_vis_slots * 8, stream));  // forward keys start clear again
+  s->shard_final = true;  // kg_shard_level runs without escalation until the next kg_shard_seed
+  if (n && shard_escalates(s) && s->shard_qinfo && n <= s->shard_qinfo_n) {
+    hipLaunchKernelGGL(k_shard_refwd_seed, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, stream, s->ds, (uint32_t)n,
+                       d_res, d_err, (const uint4*)s->shard_qinfo, d_out, (uint64_t)cap, d_counts);
+    HIPC(hipGetLastError());
+  }
+  return 0;
+}
+
+int shard_back_seed(Snapshot* s, const kg_frec* d_list, size_t m, const uint32_t* d_m, kg_frec* d_out, size_t cap,
+                    uint32_t* d_counts, hipStream_t stream) {
+  HIPC(hipSetDevice(s->device));
+  if (!stream) stream = s->stream;
+  HIPC(hipMemsetAsync(d_counts, 0, 8, stream));
+  if (m && s->ds.radj) {
+    const uint32_t grid = (uint32_t)std::min<uint64_t>((m + 255) / 256, (uint64_t)s->n_cu * 8);
+    hipLaunchKernelGGL(k_shard_back_seed, dim3(grid), dim3(256), 0, stream, s->ds, d_list, (uint64_t)m, d_m, d_out,
+                       (uint64_t)cap, d_counts);
+    HIPC(hipGetLastError());
+  }
+  return 0;
+}
+
+int shard_back_level(Snapshot* s, const kg_frec* d_in, size_t n_in, const uint32_t* d_n_in, kg_frec* d_out, size_t cap,
+                     uint32_t* d_counts, uint8_t* d_res, uint32_t* d_err, const uint32_t* d_done, uint32_t done_words,
+                     hipStream_t stream) {
+  HIPC(hipSetDevice(s->device));
+  if (!stream) stream = s->stream;
+  // the bucket size restarts; the flags word (d_counts[1]) accumulates over the phase
+  HIPC(hipMemsetAsync(d_counts, 0, 4, stream));
+  if (n_in && s->ds.radj) {
+    HeavyRow* heavy = (HeavyRow*)s->shard_heavy;
+    uint32_t* heavy_n = (uint32_t*)(heavy + SHARD_HEAVY_CAP);
+    HIPC(hipMemsetAsync(heavy_n, 0, 4, stream));
+    const uint32_t grid = (uint32_t)std::min<uint64_t>((n_in + 255) / 256, (uint64_t)s->n_cu * 8);
+    hipLaunchKernelGGL(k_shard_back_level, dim3(grid), dim3(256), 0, stream, s->ds, d_in, (uint64_t)n_in, d_n_in, d_out,
+                       (uint64_t)cap, d_counts, d_res, d_err, (uint64_t*)s->shard_vis, s->shard_vis_slots - 1, d_done,
+                       d_done ? done_words : 0u, heavy, heavy_n, SHARD_HEAVY_CAP, (uint32_t*)s->shard_qcnt,
+                       s->shard_qcnt ? s->shard_back_budget : 0u);
+    HIPC(hipGetLastError());
+    hipLaunchKernelGGL(k_shard_heavy, dim3((uint32_t)s->n_cu * 4), dim3(256), 0, stream, s->ds, heavy, heavy_n,
+                       SHARD_HEAVY_CAP, d_out, (uint64_t)cap, d_counts, d_res, d_err, 1u);
     HIPC(hipGetLastError());
   }
   return 0;

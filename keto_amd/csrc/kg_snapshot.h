@@ -200,6 +200,12 @@ struct Snapshot {
   uint32_t* shard_held = nullptr;  // holder bitmap OR-ed over every rank (kg_shard_held), or null
   uint32_t shard_held_n = 0;
   int shard_vis_log2 = 23;
+  uint32_t shard_budget = 0;       // kg_snapshot_tune("shard_budget"): forward set edges per query and rank (0 = off)
+  uint32_t shard_back_budget = 1u << 14;  // kg_snapshot_tune("shard_back_budget"): reverse edges per query and rank
+  bool shard_final = false;        // the batch's final forward phase (kg_shard_refwd_seed): no escalation
+  void* shard_qcnt = nullptr;      // kg_shard.hip: per-batch escalation counters (hashed by query)
+  void* shard_qinfo = nullptr;     // kg_shard.hip: per query slot (root, subject, depth, seeded)
+  size_t shard_qinfo_n = 0;
   int stream_variant = 9;  // kg_snapshot_tune("stream"): k_stream variant (0..8) or 9 = k_stream2
   int back_tier = 2;  // kg_snapshot_tune("back"): backward tier (1: wave + workgroup widths, 2: wave only) + no-holder filter
   uint32_t stream_ecap = 512;  // kg_snapshot_tune("stream_ecap"): stream-tier edge budget per query (0 = none)
@@ -264,7 +270,17 @@ int shard_seed(Snapshot* s, const kg_query* d_q, size_t n, int32_t gdepth, kg_fr
 int shard_level(Snapshot* s, const kg_frec* d_in, size_t n_in, const uint32_t* d_n_in, kg_frec* d_out, size_t cap,
                 uint32_t* d_counts, uint8_t* d_res, uint32_t* d_err, const uint32_t* d_done, uint32_t done_words,
                 hipStream_t stream);
-int shard_done(Snapshot* s, size_t n, const uint8_t* d_res, uint32_t* d_bits, uint32_t words, hipStream_t stream);
+int shard_done(Snapshot* s, size_t n, const uint8_t* d_res, const uint32_t* d_err, int with_esc, uint32_t* d_bits,
+               uint32_t words, hipStream_t stream);
+int shard_back_list(Snapshot* s, size_t n, const uint8_t* d_res, const uint32_t* d_err, kg_frec* d_list, size_t cap,
+                    uint32_t* d_counts, hipStream_t stream);
+int shard_back_seed(Snapshot* s, const kg_frec* d_list, size_t m, const uint32_t* d_m, kg_frec* d_out, size_t cap,
+                    uint32_t* d_counts, hipStream_t stream);
+int shard_back_level(Snapshot* s, const kg_frec* d_in, size_t n_in, const uint32_t* d_n_in, kg_frec* d_out, size_t cap,
+                     uint32_t* d_counts, uint8_t* d_res, uint32_t* d_err, const uint32_t* d_done, uint32_t done_words,
+                     hipStream_t stream);
+int shard_refwd_seed(Snapshot* s, size_t n, const uint8_t* d_res, const uint32_t* d_err, kg_frec* d_out, size_t cap,
+                     uint32_t* d_counts, hipStream_t stream);
 int shard_held(Snapshot* s, uint32_t* d_bits, size_t words, int import, hipStream_t stream);
 int shard_finish(Snapshot* s, size_t n, uint8_t* d_res, uint32_t* d_err, hipStream_t stream);
 size_t shard_result_slots(const Snapshot* s, size_t n);

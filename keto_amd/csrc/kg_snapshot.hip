@@ -241,6 +241,8 @@ Snapshot::~Snapshot() {
   for (Workspace* w : wss) delete w;
   if (shard_vis) hipFree(shard_vis);
   if (shard_heavy) hipFree(shard_heavy);
+  if (shard_qcnt) hipFree(shard_qcnt);
+  if (shard_qinfo) hipFree(shard_qinfo);
   giant.release();
   if (stream) hipStreamDestroy(stream);
 }

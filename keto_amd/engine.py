@@ -190,6 +190,7 @@ class Snapshot:
     def tune(self, key: str, value: int) -> None:
         """Engine knobs (kg_snapshot_tune): "tiers" = 0 grid / 1 LDS workgroup + grid / 2 workgroup tiers."""
         _lib.check(_lib.load().kg_snapshot_tune(self._h, key.encode(), int(value)), "kg_snapshot_tune")
+        self.__dict__.setdefault("tuned", {})[key] = int(value)  # what the Python drivers need to know
 
     def synth_ids(self) -> dict:
         a = np.zeros(6, np.uint32)

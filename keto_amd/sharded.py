@@ -44,6 +44,12 @@ class HipShardOps:
 
     device_counts = True  # kg_shard_level can read its record count from device memory
 
+    @property
+    def escalates(self) -> bool:
+        """The backward and final forward phases run only with a forward budget (kg_snapshot_tune
+        "shard_budget", off by default): their levels cost launches even when empty."""
+        return getattr(self.snapshot, "tuned", {}).get("shard_budget", 0) > 0
+
     def __init__(self, snapshot):
         import torch
         self.snapshot = snapshot
@@ -73,12 +79,36 @@ class HipShardOps:
                                          done.data_ptr() if done is not None else None, done_words, self._s()),
                    "kg_shard_level")
 
-    def done_bits(self, res, n, words):
+    def done_bits(self, res, n, words, err=None, mode=1):
+        """err given: queries escalated out of the current phase count as done (mode 1: the forward
+        phase, 2: the backward phase)."""
         import torch
         bits = torch.empty(max(words, 1), dtype=torch.int32, device=res.device)
-        _lib.check(self.L.kg_shard_done(self.snapshot.handle, n, res.data_ptr(), bits.data_ptr(), words, self._s()),
-                   "kg_shard_done")
+        _lib.check(self.L.kg_shard_done(self.snapshot.handle, n, res.data_ptr(),
+                                        err.data_ptr() if err is not None else None, mode if err is not None else 0,
+                                        bits.data_ptr(), words, self._s()), "kg_shard_done")
         return bits[:words]
+
+    # ---- backward phase (escalated queries; kg_shard_back_*)
+    def back_list(self, n, res, err, out, cap, counts):
+        _lib.check(self.L.kg_shard_back_list(self.snapshot.handle, n, res.data_ptr(), err.data_ptr(), out.data_ptr(),
+                                             cap, counts.data_ptr(), self._s()), "kg_shard_back_list")
+
+    def back_seed(self, lst, m, m_dev, out, cap, counts):
+        _lib.check(self.L.kg_shard_back_seed(self.snapshot.handle, lst.data_ptr() if m else None, m,
+                                             m_dev.data_ptr() if m_dev is not None else None, out.data_ptr(), cap,
+                                             counts.data_ptr(), self._s()), "kg_shard_back_seed")
+
+    def back_level(self, din, n_in, n_in_dev, out, cap, counts, res, err, done=None, done_words=0):
+        _lib.check(self.L.kg_shard_back_level(self.snapshot.handle, din.data_ptr() if n_in else None, n_in,
+                                              n_in_dev.data_ptr() if n_in_dev is not None else None, out.data_ptr(),
+                                              cap, counts.data_ptr(), res.data_ptr(), err.data_ptr(),
+                                              done.data_ptr() if done is not None else None, done_words, self._s()),
+                   "kg_shard_back_level")
+
+    def refwd_seed(self, n, res, err, out, cap, counts):
+        _lib.check(self.L.kg_shard_refwd_seed(self.snapshot.handle, n, res.data_ptr(), err.data_ptr(), out.data_ptr(),
+                                              cap, counts.data_ptr(), self._s()), "kg_shard_refwd_seed")
 
     def held_words(self) -> int:
         w = C.c_size_t(0)
@@ -146,10 +176,11 @@ class ShardedChecker:
         self.ops.held_import(acc.to(self.device))
         self._held_ready = True
 
-    def _done(self, res, n, words):
-        """The batch's done bitmap for the next level: every rank's packed results, all-gathered."""
+    def _done(self, res, n, words, err=None, mode=1):
+        """The batch's done bitmap for the next level: every rank's packed results (err given:
+        queries escalated out of the phase too), all-gathered."""
         import torch
-        mine = self.ops.done_bits(res, n, words)
+        mine = self.ops.done_bits(res, n, words, err, mode) if err is not None else self.ops.done_bits(res, n, words)
         if self.dist is None or self.world == 1:
             return mine
         staged = self._host_staged()
@@ -207,6 +238,100 @@ class ShardedChecker:
         self.dist.all_to_all_single(recv, send, recv_splits, send_splits)
         return recv.to(self.device) if staged else recv
 
+    def _all_gather_rows(self, t, n: int, flags: int):
+        """All-gather the first n rows of int32 tensor t from every rank (variable counts, padded to the
+        largest) with every rank's flags; returns (concatenated rows on self.device, OR of the flags)."""
+        import torch
+        if self.dist is None:
+            return t[:0 if flags else n], flags
+        staged = self._host_staged()
+        meta = torch.tensor([n, flags], dtype=torch.int64, device="cpu" if staged else self.device)
+        metas = [torch.empty_like(meta) for _ in range(self.world)]
+        self.dist.all_gather(metas, meta)
+        h = torch.stack(metas).cpu().numpy()
+        self.host_syncs += 1
+        sizes = [int(x) for x in h[:, 0]]
+        fl = 0
+        for f in h[:, 1]:
+            fl |= int(f)
+        mx = max(sizes)
+        if mx == 0 or fl:
+            return t[:0], fl
+        mine = torch.zeros((mx, t.shape[1]), dtype=t.dtype, device=t.device)
+        mine[:n] = t[:n]
+        if staged:
+            mine = mine.cpu()
+        parts = [torch.empty_like(mine) for _ in range(self.world)]
+        self.dist.all_gather(parts, mine)
+        allr = torch.cat([parts[r][:sizes[r]] for r in range(self.world)])
+        return (allr.to(self.device) if staged else allr), 0
+
+    def _backward(self, res, err, slots: int, gdepth: int):
+        """The backward phase of the escalated queries (kg_shard_back_*): level 0 = every rank's holders of
+        their subjects, then reverse hops over all-gathered records until no rank emits any."""
+        import torch
+        cap = self.cap
+        lst = torch.empty((cap, REC_WORDS), dtype=torch.int32, device=self.device)
+        cl = torch.zeros(2, dtype=torch.int32, device=self.device)
+        self.ops.back_list(slots, res, err, lst, cap, cl)
+        bufs = [torch.empty((cap, REC_WORDS), dtype=torch.int32, device=self.device) for _ in range(2)]
+        cb = [torch.zeros(2, dtype=torch.int32, device=self.device) for _ in range(2)]
+        words = (slots + 31) // 32
+        if self.world == 1 and self.dist is None and getattr(self.ops, "device_counts", False):
+            # one rank: no gathers; a level lowers the rest depth by one, so gdepth levels drain it
+            self.ops.back_seed(lst, cap, cl, bufs[0], cap, cb[0])
+            cur = 0
+            for _ in range(gdepth):
+                done = self.ops.done_bits(res, slots, words, err, 2)
+                self.ops.back_level(bufs[cur], cap, cb[cur], bufs[cur ^ 1], cap, cb[cur ^ 1], res, err, done, words)
+                cur ^= 1
+                self.back_levels += 1
+            return torch.stack([cl[1] | cb[0][1] | cb[1][1], cb[cur][0]])  # (flags, records left): read by the caller
+        h = torch.stack([cl[0], cl[1]]).cpu().numpy()
+        self.host_syncs += 1
+        glist, fl = self._all_gather_rows(lst, min(int(h[0]), cap), int(h[1]) | (int(h[0]) > cap))
+        if fl:
+            raise ShardOverflow(fl)
+        if glist.shape[0] == 0:
+            return None
+        self.ops.back_seed(glist, int(glist.shape[0]), None, bufs[0], cap, cb[0])
+        cur = 0
+        while True:
+            h = cb[cur].cpu().numpy()
+            self.host_syncs += 1
+            n_loc = int(h[0])
+            recs, fl = self._all_gather_rows(bufs[cur], min(n_loc, cap), int(h[1]) | (n_loc > cap))
+            if fl:
+                raise ShardOverflow(fl)
+            if recs.shape[0] == 0:
+                return None
+            wmax = (self._n_max + 31) // 32
+            done = self._done(res, slots, wmax, err, 2)
+            cb[cur ^ 1].zero_()
+            self.ops.back_level(recs, int(recs.shape[0]), None, bufs[cur ^ 1], cap, cb[cur ^ 1], res, err, done, wmax)
+            cur ^= 1
+            self.back_levels += 1
+
+    def _device_levels(self, bufs, counts, cur, res, err, slots, gdepth, words, esc_mode, trace, final=False):
+        """One rank: gdepth forward levels enqueued back to back, record counts read on the device
+        (esc_mode 1: escalated queries are done for the done bitmap; final: the batch's final forward
+        phase, counted apart).  Returns the current buffer."""
+        cap = self.cap
+        prune = hasattr(self.ops, "done_bits")
+        for k in range(gdepth):
+            c = counts[cur]
+            if trace is not None:  # diagnostics: records entering each level (a host sync per level)
+                trace.append(int(c[0].item()))
+            done = None
+            if prune and k > 0:
+                done = (self.ops.done_bits(res, slots, words, err, esc_mode) if esc_mode
+                        else self.ops.done_bits(res, slots, words))
+            self.ops.level(bufs[cur], cap, c, bufs[cur ^ 1], cap, counts[cur ^ 1], res, err, done, words)
+            cur ^= 1
+            if not final:
+                self.levels += 1
+        return cur
+
     # ---- one batch
     def check(self, dq, gdepth: int) -> Tuple["object", "object"]:
         """dq: (n, 7) int32 kg_query rows of THIS rank's queries (device tensor).  Returns (res u8, err i32)
@@ -242,6 +367,10 @@ class ShardedChecker:
         slots = self.ops.result_slots(n) if hasattr(self.ops, "result_slots") else n
         self._n = slots
         prune = hasattr(self.ops, "done_bits")
+        # escalation: forward done bits carry escalated queries; backward and final forward phases follow
+        backward = hasattr(self.ops, "back_level") and getattr(self.ops, "escalates", True)
+        self.back_levels = self.final_levels = 0
+        final = False
         bufs = [torch.empty((N * cap, REC_WORDS), dtype=torch.int32, device=self.device) for _ in range(2)]
         counts = [torch.zeros(N + 1, dtype=torch.int32, device=self.device) for _ in range(2)]
         res = torch.zeros(slots, dtype=torch.uint8, device=self.device)
@@ -256,24 +385,28 @@ class ShardedChecker:
             # <= gdepth, so gdepth levels drain the batch; overflow is checked once at the end.
             words = (slots + 31) // 32
             trace = [] if self.trace else None
-            for _ in range(gdepth):
-                c = counts[cur]
-                if trace is not None:  # diagnostics: records entering each level (a host sync per level)
-                    trace.append(int(c[0].item()))
-                done = self.ops.done_bits(res, slots, words) if prune and self.levels > 0 else None
-                self.ops.level(bufs[cur], cap, c, bufs[cur ^ 1], cap, counts[cur ^ 1], res, err, done, words)
-                cur ^= 1
-                self.levels += 1
+            cur = self._device_levels(bufs, counts, cur, res, err, slots, gdepth, words, 1 if backward else 0, trace)
             self.level_records = trace
             # kg_shard_level accumulates the flags word (counts[N]: a bucket or the visited table
             # overflowed) over the levels of each of the two count buffers
-            c = counts[cur]
-            h = torch.stack([counts[0][1] | counts[1][1], c[0]]).cpu().numpy()  # the batch's one host round trip
+            parts = [counts[0][1] | counts[1][1], counts[cur][0]]
+            if backward:
+                parts += list(self._backward(res, err, slots, gdepth))
+                # the final forward phase: queries past both budgets, from their roots, no budget
+                self.ops.refwd_seed(slots, res, err, bufs[0], cap, counts[0])
+                counts[1].zero_()
+                self.final_levels = gdepth
+                cur = self._device_levels(bufs, counts, 0, res, err, slots, gdepth, words, 0, None, final=True)
+                parts += [counts[0][1] | counts[1][1], counts[cur][0]]
+            h = torch.stack(parts).cpu().numpy()  # the batch's one host round trip
             self.host_syncs += 1
-            if int(h[0]) & 3:
-                raise ShardOverflow(int(h[0]))
-            if int(h[1]) != 0:
-                raise _lib.KetoGPUError("sharded batch: records left after %d levels" % gdepth)
+            fl = 0
+            for k in range(0, len(h), 2):
+                fl |= int(h[k])
+                if int(h[k + 1]) != 0:
+                    raise _lib.KetoGPUError("sharded batch: records left after %d levels" % gdepth)
+            if fl & 3:
+                raise ShardOverflow(fl & 3)
             self.ops.finish(n, res, err)
             return res[:n], err[:n]
         while True:
@@ -281,12 +414,23 @@ class ShardedChecker:
             if flags & 3:
                 raise ShardOverflow(flags)
             if total == 0:
+                if backward and not final:
+                    self._backward(res, err, slots, gdepth)
+                    # the final forward phase: queries past both budgets, re-seeded at their roots
+                    self.ops.refwd_seed(slots, res, err, bufs[cur], cap, counts[cur])
+                    final = True
+                    continue
                 self.ops.finish(n, res, err)
                 return res[:n], err[:n]
             self.records_sent += sum(send)
             recv = self._exchange(bufs[cur], send, recv_splits)
             words = (self._n_max + 31) // 32
-            done = self._done(res, slots, words) if prune and self.levels > 0 else None
+            done = None
+            if prune and self.levels > 0:
+                done = self._done(res, slots, words, err if backward and not final else None)
+            if final:
+                self.final_levels += 1
+                self.levels -= 1  # counted apart
             cur ^= 1
             self.ops.level(recv, int(recv.shape[0]), None, bufs[cur], cap, counts[cur], res, err, done, words)
             self.levels += 1

@@ -15,6 +15,9 @@ SET_BIT = 0x80000000
 Q_BITS = 26
 HIT = -1  # kg_frec.node == KG_FREC_HIT as int32
 ERR = -2  # kg_frec.node == KG_FREC_ERR as int32
+ESC = -3  # kg_frec.node == KG_FREC_ESC as int32 (the query escalates to the backward phase)
+ESC_BIT = 0x40000000  # err marker of an escalated query while the batch runs (kg_shard.hip)
+ESC2_BIT = 0x20000000  # ... and of one past the backward budget too (final forward phase)
 ERR_NOT_IMPLEMENTED = 2
 M64 = (1 << 64) - 1
 
@@ -36,9 +39,15 @@ def shard_owner(ns: int, obj: int, n: int) -> int:  # kg_internal.h shard_owner
 class CpuShardOps:
     device_counts = False  # level() takes host record counts only
 
-    def __init__(self, tuples6: np.ndarray, wildcard_rel: int, rank: int, nranks: int, impure=()):
-        """impure: (ns, rel) pairs whose relation has a rewrite or is undeclared (relflag != 0)."""
+    def __init__(self, tuples6: np.ndarray, wildcard_rel: int, rank: int, nranks: int, impure=(), budget=0,
+                 back_budget=1 << 14):
+        """impure: (ns, rel) pairs whose relation has a rewrite or is undeclared (relflag != 0).
+        budget: forward set edges per query on this rank before the query escalates (0 = off; only
+        without impure relations, like kg_snapshot_tune "shard_budget")."""
         self.rank, self.n = rank, nranks
+        self.budget = 0 if impure else int(budget)
+        self.back_budget = int(back_budget)
+        self.final = False
         self.impure = set((int(a), int(b)) for a, b in impure)
         t = np.asarray(tuples6, np.int64).reshape(-1, 6)
         self.node = {}
@@ -51,7 +60,7 @@ class CpuShardOps:
                 self.nrel[self.node[k]] = (k[0], k[2])
             return self.node[k]
 
-        self.adj, self.direct, self.owner, self.held = {}, set(), {}, set()
+        self.adj, self.direct, self.owner, self.held, self.holders = {}, set(), {}, set(), {}
         for ns, obj, rel, sns, sobj, srel in t:
             v = nid(ns, obj, rel)
             self.owner[v] = shard_owner(int(ns), int(obj), nranks)
@@ -65,20 +74,29 @@ class CpuShardOps:
                     self.adj.setdefault(v, []).append(c)
             if self.owner[v] == rank:
                 self.direct.add((v, subj))
+                self.holders.setdefault(subj, []).append(v)  # this rank's rows holding subj
             if sns == SUBJECT_ID:
                 self.held.add(int(sobj))  # every rank's rows: the OR the driver installs (kg_shard_held)
+        self.radj = {}  # local parents: P (owned here) -> N for every set edge P -> N of this rank's rows
+        for p, cs in self.adj.items():
+            for c in cs:
+                self.radj.setdefault(c, []).append(p)
         self.vis = set()
+        self.qcnt, self.qinfo = {}, {}
 
-    def _emit(self, out, cap, counts, dest, rec):
+    def _emit(self, out, cap, counts, dest, rec, nb=None):
+        nb = self.n if nb is None else nb  # buckets (the flags word follows them)
         at = int(counts[dest])
         counts[dest] += 1
         if at < cap:
             out[dest * cap + at] = torch.tensor(rec, dtype=torch.int32)
         else:
-            counts[self.n] |= 1
+            counts[nb] |= 1
 
     def seed(self, dq, n, gdepth, out, cap, counts, res, err):
         self.vis = set()
+        self.qcnt, self.qinfo = {}, {}
+        self.final = False
         counts.zero_()
         res.zero_()
         err.zero_()
@@ -103,13 +121,18 @@ class CpuShardOps:
                 continue  # no row of any rank holds the subject (kg_shard_seed's no-holder test)
             if subj is None:
                 subj = 0xFFFFFFFF  # unknown subject: never held, but the query may still reach a rewrite
+            self.qinfo[i] = (v, subj, d)
             self._emit(out, cap, counts, self.owner[v],
                        [(self.rank << Q_BITS) | i, v, np.uint32(subj).view(np.int32), d])
 
-    def done_bits(self, res, n, words):
-        """kg_shard_done: bit i of this rank's words = query i answered IsMember so far."""
+    def done_bits(self, res, n, words, err=None, mode=1):
+        """kg_shard_done: bit i of this rank's words = query i answered IsMember so far (err given:
+        or escalated out of the phase: mode 1 forward, 2 backward)."""
         bits = np.zeros(words, np.uint32)
-        for i in np.nonzero(res.numpy()[:n] == 1)[0]:
+        d = res.numpy()[:n] == 1
+        if err is not None and mode:
+            d |= (err.numpy()[:n] & (ESC_BIT if mode == 1 else ESC2_BIT)) != 0
+        for i in np.nonzero(d)[0]:
             bits[i >> 5] |= np.uint32(1 << (int(i) & 31))
         return torch.from_numpy(bits.view(np.int32).copy())
 
@@ -128,6 +151,10 @@ class CpuShardOps:
                 if home == self.rank:
                     err[qi] = max(int(err[qi]), subj)
                 continue
+            if v == ESC:
+                if home == self.rank:
+                    err[qi] = int(err[qi]) | ESC_BIT
+                continue
             if dn is not None and (qi >> 5) < done_words and (int(dn[home * done_words + (qi >> 5)]) >> (qi & 31)) & 1:
                 continue  # answered IsMember by an earlier level
             if (q, v) in self.vis:
@@ -144,7 +171,19 @@ class CpuShardOps:
                 else:
                     self._emit(out, cap, counts, home, [q, HIT, 0, 0])
             elif d >= 2:
-                for c in self.adj.get(v, []):
+                kids = self.adj.get(v, [])
+                if self.budget and kids and not self.final:  # escalation: this rank's set-edge count of the query passes the budget
+                    old = self.qcnt.get(q, 0)
+                    add = min(len(kids), self.budget)
+                    self.qcnt[q] = old + add
+                    if old < self.budget <= old + add:
+                        if home == self.rank:
+                            err[qi] = int(err[qi]) | ESC_BIT
+                        else:
+                            self._emit(out, cap, counts, home, [q, ESC, 0, 0])
+                    if old + add >= self.budget:
+                        kids = []
+                for c in kids:
                     self._emit(out, cap, counts, self.owner[c], [q, c, np.uint32(subj).view(np.int32), d - 1])
             elif d == 1:  # checkIsAllowed(child, 0) still evaluates astRelationFor: impure -> error
                 for c in self.adj.get(v, []):
@@ -154,5 +193,73 @@ class CpuShardOps:
                         else:
                             self._emit(out, cap, counts, home, [q, ERR, ERR_NOT_IMPLEMENTED, 0])
 
+    # ---- backward phase (kg_shard_back_list / _seed / _level): reverse search from the holders
+    def back_list(self, n, res, err, out, cap, counts):
+        counts.zero_()
+        self.vis = set()
+        self.qcnt = {}
+        for i, (v, subj, d) in sorted(self.qinfo.items()):
+            if i < n and (int(err[i]) & ESC_BIT) and int(res[i]) != 1 and subj != 0xFFFFFFFF:
+                self._emit(out, cap, counts, 0, [(self.rank << Q_BITS) | i, v, np.uint32(subj).view(np.int32), d], 1)
+
+    def back_seed(self, lst, m, m_dev, out, cap, counts):
+        assert m_dev is None
+        counts.zero_()
+        for q, root, subj, d in lst[:m].tolist():
+            if d >= 2:
+                for h in self.holders.get(subj & 0xFFFFFFFF, []):
+                    if h != root:
+                        self._emit(out, cap, counts, 0, [q, h, root, d - 1], 1)
+
+    def back_level(self, din, n_in, n_in_dev, out, cap, counts, res, err, done=None, done_words=0):
+        assert n_in_dev is None
+        counts[0] = 0
+        dn = None if done is None else done.numpy().view(np.uint32)
+        for q, v, root, d in din[:n_in].tolist():
+            home, qi = q >> Q_BITS, q & ((1 << Q_BITS) - 1)
+            if v == HIT:
+                if home == self.rank:
+                    res[qi] = 1
+                continue
+            if v == ESC:
+                if home == self.rank:
+                    err[qi] = int(err[qi]) | ESC2_BIT
+                continue
+            if dn is not None and (qi >> 5) < done_words and (int(dn[home * done_words + (qi >> 5)]) >> (qi & 31)) & 1:
+                continue
+            if (q, v) in self.vis or d < 1:
+                self.vis.add((q, v))
+                continue
+            self.vis.add((q, v))
+            parents = self.radj.get(v, [])
+            if self.back_budget and parents:  # the reverse search's budget: past it, the final forward phase
+                old = self.qcnt.get(q, 0)
+                add = min(len(parents), self.back_budget)
+                self.qcnt[q] = old + add
+                if old < self.back_budget <= old + add:
+                    if home == self.rank:
+                        err[qi] = int(err[qi]) | ESC2_BIT
+                    else:
+                        self._emit(out, cap, counts, 0, [q, ESC, 0, 0], 1)
+                if old + add >= self.back_budget:
+                    parents = []
+            for p in parents:
+                if p == root:
+                    if home == self.rank:
+                        res[qi] = 1
+                    else:
+                        self._emit(out, cap, counts, 0, [q, HIT, 0, 0], 1)
+                elif d >= 2:
+                    self._emit(out, cap, counts, 0, [q, p, root, d - 1], 1)
+
+    def refwd_seed(self, n, res, err, out, cap, counts):
+        counts.zero_()
+        self.vis = set()
+        self.final = True
+        for i, (v, subj, d) in sorted(self.qinfo.items()):
+            if i < n and (int(err[i]) & ESC2_BIT) and int(res[i]) != 1:
+                self._emit(out, cap, counts, self.owner[v], [(self.rank << Q_BITS) | i, v, np.uint32(subj).view(np.int32), d])
+
     def finish(self, n, res, err):
+        err[:n] = err[:n] & ~(ESC_BIT | ESC2_BIT)
         res[:n][err[:n] != 0] = 2

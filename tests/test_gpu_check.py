@@ -192,14 +192,15 @@ def _torch():
     return torch
 
 
-@pytest.mark.parametrize("n_tuples,gmax,variant", [(200_000, 10, 9), (300_000, 5, 9), (300_000, 10, 10),
-                                                    (300_000, 10, 11)])
-def test_synthetic_graph_vs_oracle(n_tuples, gmax, variant):
+@pytest.mark.parametrize("n_tuples,gmax,variant,unheld", [(200_000, 10, 9, 1), (300_000, 5, 9, 1), (300_000, 10, 10, 1),
+                                                           (300_000, 10, 11, 1), (300_000, 10, 9, 0)])
+def test_synthetic_graph_vs_oracle(n_tuples, gmax, variant, unheld):
     torch = _torch()
     from keto_amd import _lib
     snap = Snapshot.synthetic(n_tuples, seed=20250131)
     snap.tune("tiers", 1 if gmax == 5 else 0)
     snap.tune("stream", variant)
+    snap.tune("resolve_unheld", unheld)  # 0: the node map is read for every query (round-1 order)
     n = 20000
     dq = torch.empty((n, 7), dtype=torch.int32, device="cuda")
     _lib.check(_lib.load().kg_synth_queries(snap.handle, 7, n, dq.data_ptr()), "kg_synth_queries")

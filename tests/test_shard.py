@@ -44,7 +44,7 @@ def _expected(t6, wildcard, q, gmax):
     return exp
 
 
-def _cpu_worker(rank, world, port, seed, cap, outq):
+def _cpu_worker(rank, world, port, seed, cap, outq, budget=0, back_budget=1 << 14):
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import torch.distributed as dist
@@ -54,25 +54,30 @@ def _cpu_worker(rank, world, port, seed, cap, outq):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     it, t6, q = _graph(seed)
-    ops = CpuShardOps(t6, it.wildcard_rel, rank, world)
+    ops = CpuShardOps(t6, it.wildcard_rel, rank, world, budget=budget, back_budget=back_budget)
     mine = np.array_split(np.arange(len(q)), world)[rank]  # this rank's slice of the batch
     chk = ShardedChecker(ops, rank, world, dist, device="cpu", cap=cap)
     out = {}
     for gmax in (2, 5):
         res, err = chk.check(torch.from_numpy(q[mine].view(np.int32).copy()), gmax)
-        out[gmax] = (mine, res.numpy().copy(), chk.cap)
+        out[gmax] = (mine, res.numpy().copy(), chk.cap, chk.back_levels, chk.final_levels)
     outq.put((rank, out))
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,cap", [(2, 1 << 12), (3, 4)])
-def test_sharded_protocol_gloo(world, cap):
-    """cap=4 forces bucket overflows: every rank must rerun the batch with larger buckets."""
+@pytest.mark.parametrize("world,cap,budget,back_budget", [(2, 1 << 12, 0, 0), (3, 4, 0, 0), (2, 1 << 12, 2, 1 << 14),
+                                                          (3, 8, 1, 1 << 14), (2, 1 << 12, 1, 2)])
+def test_sharded_protocol_gloo(world, cap, budget, back_budget):
+    """cap=4 / 8 force bucket overflows: every rank must rerun the batch with larger buckets.  budget
+    1 / 2: nearly every expanding query escalates, so the backward phase (all-gathered reverse hops
+    from the subject's holders) decides it; back_budget 2: most of those go on to the final forward
+    phase."""
     seed = 3
     ctx = mp.get_context("spawn")
     outq = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_cpu_worker, args=(r, world, port, seed, cap, outq)) for r in range(world)]
+    ps = [ctx.Process(target=_cpu_worker, args=(r, world, port, seed, cap, outq, budget, back_budget))
+          for r in range(world)]
     for p in ps:
         p.start()
     got = [outq.get(timeout=240) for _ in range(world)]
@@ -85,10 +90,14 @@ def test_sharded_protocol_gloo(world, cap):
         exp = _expected(t6, it.wildcard_rel, q, gmax)
         res = np.zeros(len(q), np.uint8)
         for _, out in got:
-            mine, r, final_cap = out[gmax]
+            mine, r, final_cap, back_levels, final_levels = out[gmax]
             res[mine] = r
-            if cap == 4:
-                assert final_cap > 4
+            if cap <= 8:
+                assert final_cap > cap
+            if budget and gmax == 5:
+                assert back_levels > 0
+            if back_budget == 2 and gmax == 5:
+                assert final_levels > 0
         assert (res == exp).all(), np.nonzero(res != exp)[0][:10]
         assert 0 < exp.mean() < 1
 
@@ -103,7 +112,7 @@ def test_owner_matches_library():
 
 
 # ------------------------------------------------------------------ GPU (HIP local steps)
-def _gpu_worker(rank, world, port, seed, outq):
+def _gpu_worker(rank, world, port, seed, outq, budget=None, back_budget=None):
     sys.path.insert(0, ROOT)
     import torch.distributed as dist
     from keto_amd.engine import Snapshot
@@ -117,6 +126,10 @@ def _gpu_worker(rank, world, port, seed, outq):
     torch.cuda.set_device(0)
     it, t6, q = _graph(seed, n_obj=80, n_rows=1500)
     snap = Snapshot(t6, it, None, 0, shard=(rank, world))
+    if budget is not None:
+        snap.tune("shard_budget", budget)
+    if back_budget is not None:
+        snap.tune("shard_back_budget", back_budget)
     mine = np.array_split(np.arange(len(q)), world)[rank]
     chk = ShardedChecker(HipShardOps(snap), rank, world, dist_, device="cuda", cap=256)
     out = {}
@@ -129,11 +142,12 @@ def _gpu_worker(rank, world, port, seed, outq):
         dist.destroy_process_group()
 
 
-def _run_gpu(world, seed):
+def _run_gpu(world, seed, budget=None, back_budget=None):
     ctx = mp.get_context("spawn")
     outq = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_gpu_worker, args=(r, world, port, seed, outq)) for r in range(world)]
+    ps = [ctx.Process(target=_gpu_worker, args=(r, world, port, seed, outq, budget, back_budget))
+          for r in range(world)]
     for p in ps:
         p.start()
     got = [outq.get(timeout=100) for _ in range(world)]
@@ -152,11 +166,16 @@ def _run_gpu(world, seed):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world", [1, 2])
-def test_sharded_hip_vs_oracle(world):
+@pytest.mark.parametrize("world,budget,back_budget", [(1, None, None), (2, None, None), (1, 1, None), (2, 2, None),
+                                                     (1, 0, None), (1, 1, 2), (2, 1, 2)])
+def test_sharded_hip_vs_oracle(world, budget, back_budget):
+    """Random graphs (cycles, subject sets as subjects), against the oracle.  Budgets 1 / 2 escalate
+    nearly every query that expands to the backward phase (reverse search from the subject's holders
+    over all-gathered records); 0 turns escalation off; back_budget 2 sends most of them on to the
+    final forward phase."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    _run_gpu(world, seed=11)
+    _run_gpu(world, seed=11, budget=budget, back_budget=back_budget)
 
 
 # ------------------------------------------------------------------ rewrites reached in sharded mode
@@ -238,7 +257,7 @@ def test_sharded_hip_impure_matches_reference(mat, monkeypatch):
 
 
 # ------------------------------------------------------------------ config C4 generator, sharded
-def _synth_worker(rank, world, port, n_tuples, n_q, gmax, backend, outq, preset=0):
+def _synth_worker(rank, world, port, n_tuples, n_q, gmax, backend, outq, preset=0, budget=None, back_budget=None):
     sys.path.insert(0, ROOT)
     import torch.distributed as dist
     from keto_amd import _lib
@@ -252,6 +271,10 @@ def _synth_worker(rank, world, port, n_tuples, n_q, gmax, backend, outq, preset=
         dist.init_process_group(backend, rank=rank, world_size=world)
         dist_ = dist
     snap = Snapshot.synthetic(n_tuples, seed=20250131, shard=(rank, world), preset=preset)
+    if budget is not None:
+        snap.tune("shard_budget", budget)
+    if back_budget is not None:
+        snap.tune("shard_back_budget", back_budget)
     dq = torch.empty((n_q, 7), dtype=torch.int32, device="cuda")
     _lib.check(_lib.load().kg_synth_queries(snap.handle, 31, n_q, dq.data_ptr()), "kg_synth_queries")
     mine = np.array_split(np.arange(n_q), world)[rank]
@@ -261,21 +284,25 @@ def _synth_worker(rank, world, port, n_tuples, n_q, gmax, backend, outq, preset=
     s0 = chk.host_syncs
     res, err = chk.check(mq, gmax)
     outq.put((rank, mine, res.cpu().numpy(), err.cpu().numpy(), chk.levels, chk.host_syncs - s0,
-              dq.cpu().numpy() if rank == 0 else None, snap.materialized()))
+              dq.cpu().numpy() if rank == 0 else None, snap.materialized(), chk.back_levels))
     if dist_:
         dist.destroy_process_group()
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,backend", [(1, None), (1, "nccl"), (2, "gloo")])
-def test_sharded_c4_generator_vs_oracle(world, backend):
+@pytest.mark.parametrize("world,backend,budget,back_budget", [(1, None, None, None), (1, "nccl", None, None),
+                                                              (2, "gloo", None, None), (1, None, 8, None),
+                                                              (1, "nccl", 8, 64), (2, "gloo", 8, 64)])
+def test_sharded_c4_generator_vs_oracle(world, backend, budget, back_budget):
     """Config C4's generator, hash-sharded: world 1 with every level on the device (no host round
     trip per level), world 1 through torch.distributed over RCCL ("nccl": the metadata and record
     all-to-alls run on device tensors), and world 2 (two ranks on one GPU, gloo).  Against the
-    oracle on the whole graph's rows, bit-exact; the synthetic queries only touch rewrite-free nodes."""
+    oracle on the whole graph's rows, bit-exact; the synthetic queries only touch rewrite-free nodes.
+    Budget 8: most walks escalate to the backward phase (the default budget escalates the hub-heavy
+    ones only)."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    _run_synth(world, backend, 300_000, 20_000, 10, preset=0)
+    _run_synth(world, backend, 300_000, 20_000, 10, preset=0, budget=budget, back_budget=back_budget)
 
 
 @pytest.mark.gpu
@@ -291,14 +318,14 @@ def test_sharded_c3_rewrites_vs_oracle(world, backend):
     _run_synth(world, backend, 150_000, 6000, 10, preset=1)
 
 
-def _run_synth(world, backend, n_tuples, n_q, gmax, preset):
+def _run_synth(world, backend, n_tuples, n_q, gmax, preset, budget=None, back_budget=None):
     from keto_amd.engine import Snapshot
     from oracle.oracle import POLICY_CANONICAL, Oracle
     ctx = mp.get_context("spawn")
     outq = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_synth_worker, args=(r, world, port, n_tuples, n_q, gmax, backend, outq, preset))
-          for r in range(world)]
+    ps = [ctx.Process(target=_synth_worker, args=(r, world, port, n_tuples, n_q, gmax, backend, outq, preset, budget,
+                                                  back_budget)) for r in range(world)]
     for p in ps:
         p.start()
     got = [outq.get(timeout=110) for _ in range(world)]
@@ -311,11 +338,13 @@ def _run_synth(world, backend, n_tuples, n_q, gmax, preset):
     exp, oerr, _ = o.check_batch(q[:, :6], q[:, 6].view(np.int32), gmax, POLICY_CANONICAL, nthreads=8)
     assert (oerr == 0).all()
     res = np.zeros(n_q, np.uint8)
-    for rank, mine, r, e, levels, syncs, _, mat in got:
+    for rank, mine, r, e, levels, syncs, _, mat, back_levels in got:
         assert (e == 0).all(), (rank, np.nonzero(e)[0][:10])
         res[mine] = r
         if world == 1 and backend is None:
             assert syncs == 1 and levels == gmax  # one host round trip for the whole batch
+        if budget is not None and budget <= 8 and not preset:
+            assert back_levels > 0  # the backward phase ran
         if preset:
             assert mat["union_nodes"] > 0, mat
     bad = np.nonzero(res != exp)[0]
