@@ -30,11 +30,14 @@ namespace kg {
 
 constexpr uint32_t CHUNK = 256;  // records per arena chunk
 
+// A DFS frame carries its node's row range, so neither a push (the candidate's range is known from
+// the parent's chunk scan) nor a pop re-reads row_off on the walk's dependent chain.
 struct ExpFrame {
+  uint64_t rb;
   uint32_t node;
   uint32_t cursor;
+  uint32_t len;
   int32_t d;
-  uint32_t pad;
 };
 
 struct ExpCtl {
@@ -161,10 +164,10 @@ __device__ int expand_root(const DevSnap& s, Store& st, const kg_set& root, int3
   emit(S, lane == 0, rec_set(s, 1, rn, (uint32_t)(re0 - rb0)));
   uint32_t count = 1;
   int sp = 0;
-  ExpFrame F{rn, 0, d, 0};
+  ExpFrame F{rb0, rn, 0, (uint32_t)(re0 - rb0), d};
   int status = EXP_OK;
   for (;;) {
-    const uint64_t rb = s.row_off[F.node], re = s.row_off[F.node + 1];
+    const uint64_t rb = F.rb, re = F.rb + F.len;
     const bool can_expand = F.d - 1 >= 2;
     bool pushed = false;
     while (rb + F.cursor < re) {
@@ -178,8 +181,10 @@ __device__ int expand_root(const DevSnap& s, Store& st, const kg_set& root, int3
         crb = s.row_off[c];
         cre = s.row_off[c + 1];
         // a set visited before this chunk is a leaf whatever comes first (the visited set only
-        // grows): only unvisited sets with rows are order-dependent candidates, taken one by one
-        cand = cre > crb && !st.contains(c);
+        // grows): only unvisited sets with rows are order-dependent candidates, taken one by one.
+        // The visited lookup does not wait for the row range (both depend on the subject only).
+        const bool seen = st.contains(c);
+        cand = cre > crb && !seen;
       }
       const uint64_t mc = __ballot(cand);
       const uint32_t p = mc ? (uint32_t)(__ffsll((unsigned long long)mc) - 1) : 64u;
@@ -203,6 +208,8 @@ __device__ int expand_root(const DevSnap& s, Store& st, const kg_set& root, int3
       const uint32_t csub = __shfl(sub, (int)p, 64);
       const uint32_t cnode = csub & ~SET_BIT;
       const uint32_t clen = (uint32_t)(__shfl((uint32_t)(cre - crb), (int)p, 64));
+      const uint64_t cbeg = ((uint64_t)(uint32_t)__shfl((uint32_t)(crb >> 32), (int)p, 64) << 32) |
+                            (uint32_t)__shfl((uint32_t)crb, (int)p, 64);
       F.cursor += p + 1;
       const uint32_t before = n_vis;
       if (!wave_add_roots(st, lane == 0, cnode, n_vis)) {
@@ -224,7 +231,7 @@ __device__ int expand_root(const DevSnap& s, Store& st, const kg_set& root, int3
       }
       if (lane == 0) stack[sp] = F;
       sp++;
-      F = ExpFrame{cnode, 0, F.d - 1, 0};
+      F = ExpFrame{cbeg, cnode, 0, clen, F.d - 1};
       pushed = true;
       break;
     }
