@@ -63,6 +63,8 @@ def parse():
     ap.add_argument("--shard-back-budget", type=int, default=1 << 14,
                     help="kg_snapshot_tune shard_back_budget (reverse edges per query and rank before the final "
                          "forward phase takes it)")
+    ap.add_argument("--host-sync", type=int, default=1,
+                    help="kg_snapshot_tune host_sync (--mode host: 1 = kg_check_batch waits asleep, 0 = spins)")
     ap.add_argument("--resolve-unheld", type=int, default=1,
                     help="kg_snapshot_tune resolve_unheld (1: k_resolve skips the node map for subjects no row holds)")
     ap.add_argument("--stream-chunk", type=int, default=64,
@@ -332,6 +334,7 @@ def bench_host(a):
     devices = list(range(n_dev))
     t_build = time.time()
     snap = Snapshot.synthetic(int(a.tuples), seed=a.seed, devices=devices, preset=a.preset)
+    snap.tune("host_sync", a.host_sync)
     snap.tune("stream", a.stream)
     snap.tune("stream_wgs", a.stream_wgs)
     snap.tune("back_wgs", a.back_wgs)
@@ -434,7 +437,7 @@ def bench_host(a):
            "dtype": "u32", "data": "synthetic (device-generated Drive-like tuple graph, seed %d)" % a.seed,
            "config": {"workload": "C2/C4 generator @ %.3g tuples, %d-check host batches, %d caller threads, "
                                   "max_read_depth %d" % (a.tuples, B, T, a.global_depth),
-                      "replicas": devices, "parallelism": "replicas in one process"},
+                      "replicas": devices, "parallelism": "replicas in one process", "host_sync": a.host_sync},
            "p50_call_ms": float(np.percentile(np.array(lat) * 1e3, 50)),
            "p99_call_ms": float(np.percentile(np.array(lat) * 1e3, 99)),
            "batcher": batcher, "snapshot_build_s": t_build}

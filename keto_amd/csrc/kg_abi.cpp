@@ -380,6 +380,11 @@ static int tune_one(Snapshot* s, const char* key, int64_t value) {
     s->shard_budget = (uint32_t)value;
     return 0;
   }
+  if (strcmp(key, "host_sync") == 0) {
+    if (value < 0 || value > 1) return set_error(-2, "host_sync must be 0 or 1");
+    s->host_sync = (int)value;
+    return 0;
+  }
   if (strcmp(key, "shard_back_budget") == 0) {
     if (value < 0 || value > 0xFFFFFFFFll) return set_error(-2, "shard_back_budget must be in [0, 2^32)");
     s->shard_back_budget = (uint32_t)value;
@@ -568,15 +573,13 @@ int kg_check_batch(kg_snapshot* sp, const kg_query* q, size_t n, int32_t global_
     if (!rc) {
       hipSetDevice(L->device);
       bool reran = false;
-      int r2 = kg::check_batch_end(L->rep, L->w, &bp[i], &reran);
+      const bool blocking = s->host_sync != 0;
+      int r2 = kg::check_batch_end(L->rep, L->w, &bp[i], &reran, blocking);
       if (!r2 && reran &&  // the grid tier rewrote results after the first copy: copy them again
           (hipMemcpyAsync(L->h_out, L->d_out, m, hipMemcpyDeviceToHost, L->stream) != hipSuccess ||
            hipMemcpyAsync(L->h_err, L->d_err, m * 4, hipMemcpyDeviceToHost, L->stream) != hipSuccess))
         r2 = set_error(-1, "D2H copy failed");
-      if (!r2) {
-        hipError_t e = hipStreamSynchronize(L->stream);
-        if (e != hipSuccess) r2 = set_error(-1, "batch failed: %s", hipGetErrorString(e));
-      }
+      if (!r2) r2 = L->w->wait(L->stream, blocking);  // the error text is set by wait()
       if (!r2) {
         memcpy(out + b[i], L->h_out, m);
         if (err_code) memcpy(err_code + b[i], L->h_err, m * 4);

@@ -2035,12 +2035,13 @@ int check_batch_begin(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n, 
   return 0;
 }
 
-int check_batch_end(Snapshot* s, Workspace* w, BatchPending* bp, bool* reran) {
+int check_batch_end(Snapshot* s, Workspace* w, BatchPending* bp, bool* reran, bool blocking) {
   if (reran) *reran = false;
   kg_stats* stats = bp->stats;
   hipStream_t stream = w->stream;
   GridStats& gs = bp->gs;
-  if (stats || bp->grid_pending) HIPC(hipStreamSynchronize(stream));
+  if (stats || bp->grid_pending)
+    if (int rc = w->wait(stream, blocking)) return rc;
   if (bp->grid_pending) {  // a round that overflowed its log reruns here with fewer slots (synchronously)
     if (int rc = grid_tier(s, w, bp->rq, bp->grid_list, bp->grid_count, bp->gdepth, bp->d_out, bp->d_err, stream, &gs, 2))
       return rc;

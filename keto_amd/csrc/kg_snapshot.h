@@ -58,6 +58,8 @@ struct Workspace {
   size_t interp_pool_bytes = 0;
   uint64_t interp_layout = 0;  // (pass-2 slots, pass-1 slots, list cap) the pool was last laid out for
   hipEvent_t ev[4] = {};  // batch timing events (created on first use)
+  hipEvent_t sync_ev = nullptr;  // blocking-sync event (host-buffer batches wait on it asleep)
+  int wait(hipStream_t st, bool blocking);  // waits for st: spin (hipStreamSynchronize) or asleep
   void* pinned = nullptr;  // 64 KiB of pinned host memory for small device->host readbacks
   void* host_buf(size_t bytes);
   ~Workspace();
@@ -212,6 +214,7 @@ struct Snapshot {
   int resolve_unheld = 1;  // kg_snapshot_tune("resolve_unheld"): k_resolve reads the holder bit before the node map
   uint32_t stream_chunk = 64;  // kg_snapshot_tune("stream_chunk"): k_stream2 queries per dequeue (1..64)
   int grid_wgs = 16;         // kg_snapshot_tune("grid_wgs"): k_grid_level workgroups per CU
+  int host_sync = 1;        // kg_snapshot_tune("host_sync"): kg_check_batch waits asleep (1) or spinning (0)
   int stream_wgs = 0;        // kg_snapshot_tune("stream_wgs"): k_stream workgroups per CU (0 = by LDS)
   int interp_wgs = 6;        // kg_snapshot_tune("interp_wgs"): k_interp_lds workgroups (4 waves) per CU (6 fit the LDS)
   uint32_t interp_cap2 = 0;  // kg_snapshot_tune("interp_cap2"): pass-2 BFS list cap of the rewrite path (0 = 256 Ki)
@@ -257,7 +260,7 @@ int check_batch_device(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n,
                        uint8_t* d_out, uint32_t* d_err, kg_stats* stats);
 int check_batch_begin(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n, int32_t global_max_depth,
                       uint8_t* d_out, uint32_t* d_err, kg_stats* stats, BatchPending* bp);
-int check_batch_end(Snapshot* s, Workspace* w, BatchPending* bp, bool* reran);
+int check_batch_end(Snapshot* s, Workspace* w, BatchPending* bp, bool* reran, bool blocking = false);
 int synth_queries(Snapshot* s, uint64_t seed, size_t n, kg_query* d_q);
 // kg_formula.hip: split a batch's decomposable queries into leaf checks / combine their results
 int formula_split(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n, int32_t gdepth, const kg_query** q2,

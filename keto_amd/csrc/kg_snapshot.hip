@@ -255,8 +255,24 @@ void GridPool::release() {
   epoch = 0;
 }
 
+// Host-buffer batches (kg_check_batch, the batcher's dispatchers) wait asleep on a blocking-sync
+// event: a spinning hipStreamSynchronize per in-flight batch burns a core each, and a server whose
+// cgroup CPU quota runs out is throttled for the rest of the period -- the native batcher's p99 of
+// ~70 ms at 256 callers.
+int Workspace::wait(hipStream_t st, bool blocking) {
+  if (!blocking) {
+    HIPC(hipStreamSynchronize(st));
+    return 0;
+  }
+  if (!sync_ev) HIPC(hipEventCreateWithFlags(&sync_ev, hipEventBlockingSync | hipEventDisableTiming));
+  HIPC(hipEventRecord(sync_ev, st));
+  HIPC(hipEventSynchronize(sync_ev));
+  return 0;
+}
+
 Workspace::~Workspace() {
   if (device >= 0) hipSetDevice(device);
+  if (sync_ev) hipEventDestroy(sync_ev);
   if (scratch) hipFree(scratch);
   if (heavy_pool) hipFree(heavy_pool);
   grid.release();
