@@ -390,7 +390,7 @@ def bench_host(a):
                                     C.POINTER(C.c_uint64), C.POINTER(C.c_double), C.POINTER(C.c_uint64)]
     q0 = qs[0]
     batcher = {}
-    for clients, per_call in ((a.clients, 1), (a.clients, 16)):
+    for clients, per_call in ((a.clients, 1), (a.clients, 16), (64, 1)):
         with NativeBatcher(snap, a.global_depth, max_batch=1 << 16, max_wait_us=200, dispatchers=4) as nb:
             n_chk, el2, bad = C.c_uint64(), C.c_double(), C.c_uint64()
             rc = LG.kgl_batcher_load(nb.handle, q0.ctypes.data_as(C.c_void_p), len(q0),
