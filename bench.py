@@ -63,6 +63,8 @@ def parse():
     ap.add_argument("--shard-back-budget", type=int, default=1 << 14,
                     help="kg_snapshot_tune shard_back_budget (reverse edges per query and rank before the final "
                          "forward phase takes it)")
+    ap.add_argument("--shard-vis-mode", type=int, default=0,
+                    help="kg_snapshot_tune shard_vis_mode (sharded (query, node) dedup: 0 exact CAS table, 1 lossy cache)")
     ap.add_argument("--host-sync", type=int, default=1,
                     help="kg_snapshot_tune host_sync (--mode host: 1 = kg_check_batch waits asleep, 0 = spins)")
     ap.add_argument("--resolve-unheld", type=int, default=1,
@@ -266,6 +268,7 @@ def bench_sharded(a):
     t_build = time.time() - t_build
     snap.tune("shard_budget", a.shard_budget)
     snap.tune("shard_back_budget", a.shard_back_budget)
+    snap.tune("shard_vis_mode", a.shard_vis_mode)
     B = a.batch
     dq = torch.empty((B, 7), dtype=torch.int32, device=f"cuda:{local}")
     _lib.check(L.kg_synth_queries(snap.handle, 1000 + rank, B, dq.data_ptr()), "kg_synth_queries")
@@ -305,7 +308,7 @@ def bench_sharded(a):
            "p99_batch_ms": float(np.percentile(np.array(lat) * 1e3, 99)), "allowed_fraction": float(r.mean()),
            "levels_per_batch": chk.levels, "backward_levels_per_batch": chk.back_levels,
            "final_levels_per_batch": chk.final_levels, "shard_budget": a.shard_budget,
-           "shard_back_budget": a.shard_back_budget, "records_exchanged_per_batch": recs / a.steps,
+           "shard_back_budget": a.shard_back_budget, "shard_vis_mode": a.shard_vis_mode, "records_exchanged_per_batch": recs / a.steps,
            **({"level_records": chk.level_records} if chk.level_records else {}),
            "snapshot_build_s": t_build}
     if rank == 0:

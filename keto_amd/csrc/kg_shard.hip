@@ -91,6 +91,19 @@ __device__ __forceinline__ int sv_insert(uint64_t* T, uint64_t mask, uint64_t ke
   return -1;
 }
 
+// Lossy variant (kg_snapshot_tune "shard_vis_mode" 1): a direct-mapped cache of keys with blind
+// writes -- one load and one store instead of a device-scope CAS probe chain.  A collision or a
+// race only lets a (query, node) record be processed again, at the same or a later level, i.e. with
+// the same or a smaller rest depth: it explores a subset of what the first arrival did (extra work,
+// the same answers), and rest depths still fall every level, so batches still terminate.  It never
+// reports a key this batch did not insert (the table starts empty).  1 fresh, 0 seen.
+__device__ __forceinline__ int sv_insert_lossy(uint64_t* T, uint64_t mask, uint64_t key) {
+  uint64_t* slot = &T[mix64(key) & mask];
+  if (*slot == key) return 0;
+  *slot = key;
+  return 1;
+}
+
 // Workgroup-aggregated append of one record per active thread to the bucket of its destination
 // rank: ballots per wave into LDS counters, then ONE device atomic per (workgroup, destination) --
 // at world 1 every record goes to one counter, so per-wave atomics serialised on it.  Every thread
@@ -310,7 +323,7 @@ __global__ __launch_bounds__(256) void k_shard_level(DevSnap s, const kg_frec* _
                                                      uint32_t* err, uint64_t* vis, uint64_t vmask,
                                                      const uint32_t* __restrict__ done, uint32_t done_wpr,
                                                      HeavyRow* heavy, uint32_t* heavy_n, uint32_t heavy_cap,
-                                                     uint32_t* qcnt, uint32_t budget) {
+                                                     uint32_t* qcnt, uint32_t budget, uint32_t lossy) {
   __shared__ uint32_t s_pref[256], s_wsum[4];
   __shared__ uint64_t s_rb[256];
   __shared__ kg_frec s_rec[256];
@@ -338,7 +351,8 @@ __global__ __launch_bounds__(256) void k_shard_level(DevSnap s, const kg_frec* _
                  ((done[(size_t)(r.q >> Q_BITS) * done_wpr + ((r.q & Q_MASK) >> 5)] >> (r.q & 31)) & 1u)) {
         // answered IsMember by an earlier level: nothing more to do for this query
       } else {
-        const int ins = sv_insert(vis, vmask, ((uint64_t)r.q << 32) | r.node);
+        const uint64_t vkey = ((uint64_t)r.q << 32) | r.node;
+        const int ins = lossy ? sv_insert_lossy(vis, vmask, vkey) : sv_insert(vis, vmask, vkey);
         if (ins < 0) atomicOr(&counts[s.shard_n], 2u);
         if (ins > 0 && !own && node_bad(s, r.node)) {  // a rewrite / undeclared relation
           if ((r.q >> Q_BITS) == me) atomicMax(&err[r.q & Q_MASK], (uint32_t)KG_ERR_NOT_IMPLEMENTED);
@@ -511,7 +525,8 @@ __global__ __launch_bounds__(256) void k_shard_back_level(DevSnap s, const kg_fr
                                                           uint32_t* counts, uint8_t* res, uint32_t* err, uint64_t* vis,
                                                           uint64_t vmask, const uint32_t* __restrict__ done,
                                                           uint32_t done_wpr, HeavyRow* heavy, uint32_t* heavy_n,
-                                                          uint32_t heavy_cap, uint32_t* qcnt, uint32_t budget) {
+                                                          uint32_t heavy_cap, uint32_t* qcnt, uint32_t budget,
+                                                          uint32_t lossy) {
   __shared__ uint32_t s_pref[256], s_wsum[4];
   __shared__ uint64_t s_rb[256];
   __shared__ kg_frec s_rec[256];
@@ -533,7 +548,8 @@ __global__ __launch_bounds__(256) void k_shard_back_level(DevSnap s, const kg_fr
                  ((done[(size_t)(r.q >> Q_BITS) * done_wpr + ((r.q & Q_MASK) >> 5)] >> (r.q & 31)) & 1u)) {
         // answered IsMember by an earlier level
       } else {
-        const int ins = sv_insert(vis, vmask, ((uint64_t)r.q << 32) | r.node);
+        const uint64_t vkey = ((uint64_t)r.q << 32) | r.node;
+        const int ins = lossy ? sv_insert_lossy(vis, vmask, vkey) : sv_insert(vis, vmask, vkey);
         if (ins < 0) atomicOr(&counts[1], 2u);
         if (ins > 0 && r.depth >= 1) {
           rb = s.radj_off[r.node];
@@ -737,7 +753,8 @@ int shard_level(Snapshot* s, const kg_frec* d_in, size_t n_in, const uint32_t* d
     hipLaunchKernelGGL(k_shard_level, dim3(grid), dim3(256), 0, stream, s->ds, d_in, (uint64_t)n_in, d_n_in, d_out,
                        (uint64_t)cap, d_counts, d_res, d_err, (uint64_t*)s->shard_vis, s->shard_vis_slots - 1,
                        d_done, d_done ? done_words : 0u, heavy, heavy_n, SHARD_HEAVY_CAP, (uint32_t*)s->shard_qcnt,
-                       shard_escalates(s) && s->shard_qcnt && !s->shard_final ? s->shard_budget : 0u);
+                       shard_escalates(s) && s->shard_qcnt && !s->shard_final ? s->shard_budget : 0u,
+                       s->shard_vis_mode ? 1u : 0u);
     HIPC(hipGetLastError());
     hipLaunchKernelGGL(k_shard_heavy, dim3((uint32_t)s->n_cu * 4), dim3(256), 0, stream, s->ds, heavy, heavy_n,
                        SHARD_HEAVY_CAP, d_out, (uint64_t)cap, d_counts, d_res, d_err, s->shard_n);
@@ -822,7 +839,7 @@ int shard_back_level(Snapshot* s, const kg_frec* d_in, size_t n_in, const uint32
     hipLaunchKernelGGL(k_shard_back_level, dim3(grid), dim3(256), 0, stream, s->ds, d_in, (uint64_t)n_in, d_n_in, d_out,
                        (uint64_t)cap, d_counts, d_res, d_err, (uint64_t*)s->shard_vis, s->shard_vis_slots - 1, d_done,
                        d_done ? done_words : 0u, heavy, heavy_n, SHARD_HEAVY_CAP, (uint32_t*)s->shard_qcnt,
-                       s->shard_qcnt ? s->shard_back_budget : 0u);
+                       s->shard_qcnt ? s->shard_back_budget : 0u, s->shard_vis_mode ? 1u : 0u);
     HIPC(hipGetLastError());
     hipLaunchKernelGGL(k_shard_heavy, dim3((uint32_t)s->n_cu * 4), dim3(256), 0, stream, s->ds, heavy, heavy_n,
                        SHARD_HEAVY_CAP, d_out, (uint64_t)cap, d_counts, d_res, d_err, 1u);

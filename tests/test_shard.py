@@ -112,7 +112,7 @@ def test_owner_matches_library():
 
 
 # ------------------------------------------------------------------ GPU (HIP local steps)
-def _gpu_worker(rank, world, port, seed, outq, budget=None, back_budget=None):
+def _gpu_worker(rank, world, port, seed, outq, budget=None, back_budget=None, vis_mode=0):
     sys.path.insert(0, ROOT)
     import torch.distributed as dist
     from keto_amd.engine import Snapshot
@@ -130,6 +130,7 @@ def _gpu_worker(rank, world, port, seed, outq, budget=None, back_budget=None):
         snap.tune("shard_budget", budget)
     if back_budget is not None:
         snap.tune("shard_back_budget", back_budget)
+    snap.tune("shard_vis_mode", vis_mode)
     mine = np.array_split(np.arange(len(q)), world)[rank]
     chk = ShardedChecker(HipShardOps(snap), rank, world, dist_, device="cuda", cap=256)
     out = {}
@@ -142,11 +143,11 @@ def _gpu_worker(rank, world, port, seed, outq, budget=None, back_budget=None):
         dist.destroy_process_group()
 
 
-def _run_gpu(world, seed, budget=None, back_budget=None):
+def _run_gpu(world, seed, budget=None, back_budget=None, vis_mode=0):
     ctx = mp.get_context("spawn")
     outq = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_gpu_worker, args=(r, world, port, seed, outq, budget, back_budget))
+    ps = [ctx.Process(target=_gpu_worker, args=(r, world, port, seed, outq, budget, back_budget, vis_mode))
           for r in range(world)]
     for p in ps:
         p.start()
@@ -166,16 +167,18 @@ def _run_gpu(world, seed, budget=None, back_budget=None):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,budget,back_budget", [(1, None, None), (2, None, None), (1, 1, None), (2, 2, None),
-                                                     (1, 0, None), (1, 1, 2), (2, 1, 2)])
-def test_sharded_hip_vs_oracle(world, budget, back_budget):
+@pytest.mark.parametrize("world,budget,back_budget,vis_mode", [(1, None, None, 0), (2, None, None, 0), (1, 1, None, 0),
+                                                              (2, 2, None, 0), (1, 0, None, 0), (1, 1, 2, 0),
+                                                              (2, 1, 2, 0), (1, None, None, 1), (2, None, None, 1),
+                                                              (2, 1, 2, 1)])
+def test_sharded_hip_vs_oracle(world, budget, back_budget, vis_mode):
     """Random graphs (cycles, subject sets as subjects), against the oracle.  Budgets 1 / 2 escalate
     nearly every query that expands to the backward phase (reverse search from the subject's holders
     over all-gathered records); 0 turns escalation off; back_budget 2 sends most of them on to the
     final forward phase."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    _run_gpu(world, seed=11, budget=budget, back_budget=back_budget)
+    _run_gpu(world, seed=11, budget=budget, back_budget=back_budget, vis_mode=vis_mode)
 
 
 # ------------------------------------------------------------------ rewrites reached in sharded mode
@@ -257,7 +260,8 @@ def test_sharded_hip_impure_matches_reference(mat, monkeypatch):
 
 
 # ------------------------------------------------------------------ config C4 generator, sharded
-def _synth_worker(rank, world, port, n_tuples, n_q, gmax, backend, outq, preset=0, budget=None, back_budget=None):
+def _synth_worker(rank, world, port, n_tuples, n_q, gmax, backend, outq, preset=0, budget=None, back_budget=None,
+                  vis_mode=0):
     sys.path.insert(0, ROOT)
     import torch.distributed as dist
     from keto_amd import _lib
@@ -275,6 +279,7 @@ def _synth_worker(rank, world, port, n_tuples, n_q, gmax, backend, outq, preset=
         snap.tune("shard_budget", budget)
     if back_budget is not None:
         snap.tune("shard_back_budget", back_budget)
+    snap.tune("shard_vis_mode", vis_mode)
     dq = torch.empty((n_q, 7), dtype=torch.int32, device="cuda")
     _lib.check(_lib.load().kg_synth_queries(snap.handle, 31, n_q, dq.data_ptr()), "kg_synth_queries")
     mine = np.array_split(np.arange(n_q), world)[rank]
@@ -290,10 +295,11 @@ def _synth_worker(rank, world, port, n_tuples, n_q, gmax, backend, outq, preset=
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,backend,budget,back_budget", [(1, None, None, None), (1, "nccl", None, None),
-                                                              (2, "gloo", None, None), (1, None, 8, None),
-                                                              (1, "nccl", 8, 64), (2, "gloo", 8, 64)])
-def test_sharded_c4_generator_vs_oracle(world, backend, budget, back_budget):
+@pytest.mark.parametrize("world,backend,budget,back_budget,vis_mode", [(1, None, None, None, 0), (1, "nccl", None, None, 0),
+                                                                       (2, "gloo", None, None, 0), (1, None, 8, None, 0),
+                                                                       (1, "nccl", 8, 64, 0), (2, "gloo", 8, 64, 0),
+                                                                       (1, None, None, None, 1), (2, "gloo", None, None, 1)])
+def test_sharded_c4_generator_vs_oracle(world, backend, budget, back_budget, vis_mode):
     """Config C4's generator, hash-sharded: world 1 with every level on the device (no host round
     trip per level), world 1 through torch.distributed over RCCL ("nccl": the metadata and record
     all-to-alls run on device tensors), and world 2 (two ranks on one GPU, gloo).  Against the
@@ -302,7 +308,7 @@ def test_sharded_c4_generator_vs_oracle(world, backend, budget, back_budget):
     ones only)."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    _run_synth(world, backend, 300_000, 20_000, 10, preset=0, budget=budget, back_budget=back_budget)
+    _run_synth(world, backend, 300_000, 20_000, 10, preset=0, budget=budget, back_budget=back_budget, vis_mode=vis_mode)
 
 
 @pytest.mark.gpu
@@ -318,14 +324,14 @@ def test_sharded_c3_rewrites_vs_oracle(world, backend):
     _run_synth(world, backend, 150_000, 6000, 10, preset=1)
 
 
-def _run_synth(world, backend, n_tuples, n_q, gmax, preset, budget=None, back_budget=None):
+def _run_synth(world, backend, n_tuples, n_q, gmax, preset, budget=None, back_budget=None, vis_mode=0):
     from keto_amd.engine import Snapshot
     from oracle.oracle import POLICY_CANONICAL, Oracle
     ctx = mp.get_context("spawn")
     outq = ctx.Queue()
     port = _free_port()
     ps = [ctx.Process(target=_synth_worker, args=(r, world, port, n_tuples, n_q, gmax, backend, outq, preset, budget,
-                                                  back_budget)) for r in range(world)]
+                                                  back_budget, vis_mode)) for r in range(world)]
     for p in ps:
         p.start()
     got = [outq.get(timeout=110) for _ in range(world)]
