@@ -36,7 +36,7 @@ STREAM_KERNELS = {0: "k_stream<8,7,256,16>", 1: "k_stream<16,6,256,32>", 2: "k_s
                   3: "k_stream<32,5,192,64>", 4: "k_stream<32,6,256,64>", 5: "k_stream<32,wave1024/128,256,64>",
                   6: "k_stream<32,wave1024/256,320,64>", 7: "k_stream<32,wave1024/64,256,64>",
                   8: "k_stream<32,wave512/64,256,64>", 9: "k_stream2<9,256,64,64,1>",
-                  10: "k_stream3<9,256,64,64>", 11: "k_stream2<9,256,64,64,2>"}
+                  10: "k_stream3<9,256,64,64>", 11: "k_stream2<9,256,64,64,2>", 12: "k_stream2<9,256,64,0,1>"}
 
 
 def parse():
@@ -54,8 +54,9 @@ def parse():
     ap.add_argument("--seed", type=int, default=20250131)
     ap.add_argument("--tiers", type=int, default=0, help="kg_snapshot_tune tiers (0 grid, 1 LDS-WG+grid, 2 WG)")
     ap.add_argument("--wide", type=int, default=0, help="kg_snapshot_tune wide (k_light<64> tier on/off)")
-    ap.add_argument("--stream", type=int, default=9, help="kg_snapshot_tune stream (k_stream variant 0..8, 9 = k_stream2, "
-                    "10 = k_stream3, 11 = k_stream2 with 128-edge windows)")
+    ap.add_argument("--stream", type=int, default=12, help="kg_snapshot_tune stream (k_stream variant 0..8, 9 = k_stream2, "
+                    "10 = k_stream3, 11 = k_stream2 with 128-edge windows, 12 = k_stream2 without the per-query "
+                    "expanded-node cap: default)")
     ap.add_argument("--stream-ecap", type=int, default=512, help="kg_snapshot_tune stream_ecap (stream-tier edges per query, 0 = none)")
     ap.add_argument("--shard-budget", type=int, default=0,
                     help="kg_snapshot_tune shard_budget (sharded mode: forward set edges per query and rank before "

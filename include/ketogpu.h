@@ -213,8 +213,9 @@ int kg_snapshot_materialized(const kg_snapshot* s, uint64_t* out3);
  * holders, one wave per query, then one workgroup per query) takes the wave tiers' overflow before the grid tier, and
  * k_resolve answers queries whose subject no row holds; 2 = the same with the wave width only
  * (its overflow goes straight to the grid tier; default); 0 = off.  key "stream": stream-tier
- * kernel -- 9 = k_stream2 (default: 32 query slots per wave over one FIFO, direct-mapped visited
- * cache), 0..8 = the round-1 k_stream variants (see kg_check.hip).
+ * kernel -- 12 = k_stream2 (default: 32 query slots per wave over one FIFO, direct-mapped visited
+ * cache, a query bounded by its edge budget), 9 = the same with a cap of 64 expanded nodes per query,
+ * 11 = 128-edge windows, 10 = k_stream3 (software-pipelined), 0..8 = the round-1 k_stream variants.
  * key "stream_ecap": edges a query may enqueue in the stream tier before it is handed to the
  * backward / grid tiers (default 512; 0 = no budget) -- cuts the stream kernel's tail of long walks.
  * key "resolve_unheld" (0/1): without a namespace program, k_resolve reads a subject id's holder

@@ -1009,8 +1009,10 @@ __global__ __launch_bounds__(256) void k_stream2(DevSnap s, const RQuery* __rest
       const unsigned long long old = keepc ? L.vt[hv] : 0ull;
       const bool fresh = keepc && !longrow && old != key;
       if (fresh) L.vt[hv] = key;
-      const uint32_t k = fresh ? atomicAdd(&L.s_ins[slot], 1u) : 0u;
-      const bool ok = fresh && k < (uint32_t)INS_CAP;
+      // INS_CAP 0: no per-query cap on expanded nodes (the edge budget ecap still bounds a query),
+      // which saves a returning LDS atomic on the step's dependent chain
+      const uint32_t k = (INS_CAP && fresh) ? atomicAdd(&L.s_ins[slot], 1u) : 0u;
+      const bool ok = fresh && (INS_CAP == 0 || k < (uint32_t)INS_CAP);
       const uint64_t am = __ballot(ok);
       const uint32_t room = QC - (tail - head);
       const uint32_t pos = __popcll(am & ((1ull << lane) - 1));
@@ -1946,6 +1948,9 @@ int check_batch_begin(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n, 
                            d_out, ovf_list, ovf_count, ctl, ecap, std::max<uint32_t>(1u, std::min<uint32_t>(s->stream_chunk, 64u)));
       else if (sv == 11)  // 128-edge windows (two edges per lane)
         hipLaunchKernelGGL((k_stream2<9, 256, 64, 64, 2>), dim3(grid), dim3(256), 0, stream, s->ds, rq, wl, ctl->heads,
+                           d_out, ovf_list, ovf_count, ctl, ecap, std::max<uint32_t>(1u, std::min<uint32_t>(s->stream_chunk, 64u)));
+      else if (sv == 12)  // no expanded-node cap per query (edge budget only)
+        hipLaunchKernelGGL((k_stream2<9, 256, 64, 0, 1>), dim3(grid), dim3(256), 0, stream, s->ds, rq, wl, ctl->heads,
                            d_out, ovf_list, ovf_count, ctl, ecap, std::max<uint32_t>(1u, std::min<uint32_t>(s->stream_chunk, 64u)));
       else if (sv == 10)
         hipLaunchKernelGGL((k_stream3<9, 256, 64, 64>), dim3(grid), dim3(256), 0, stream, s->ds, rq, wl, ctl->heads,

@@ -209,7 +209,7 @@ struct Snapshot {
   void* shard_qcnt = nullptr;      // kg_shard.hip: per-batch escalation counters (hashed by query)
   void* shard_qinfo = nullptr;     // kg_shard.hip: per query slot (root, subject, depth, seeded)
   size_t shard_qinfo_n = 0;
-  int stream_variant = 9;  // kg_snapshot_tune("stream"): k_stream variant (0..8) or 9 = k_stream2
+  int stream_variant = 12;  // kg_snapshot_tune("stream"): k_stream variant (0..8), 9 / 11 / 12 = k_stream2, 10 = k_stream3
   int back_tier = 2;  // kg_snapshot_tune("back"): backward tier (1: wave + workgroup widths, 2: wave only) + no-holder filter
   uint32_t stream_ecap = 512;  // kg_snapshot_tune("stream_ecap"): stream-tier edge budget per query (0 = none)
   int resolve_unheld = 1;  // kg_snapshot_tune("resolve_unheld"): k_resolve reads the holder bit before the node map
