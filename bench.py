@@ -66,6 +66,8 @@ def parse():
                          "forward phase takes it)")
     ap.add_argument("--shard-vis-mode", type=int, default=0,
                     help="kg_snapshot_tune shard_vis_mode (sharded (query, node) dedup: 0 exact CAS table, 1 lossy cache)")
+    ap.add_argument("--device-sync", type=int, default=1,
+                    help="kg_snapshot_tune device_sync (1: kg_check_batch_device waits asleep instead of spinning)")
     ap.add_argument("--host-sync", type=int, default=1,
                     help="kg_snapshot_tune host_sync (--mode host: 1 = kg_check_batch waits asleep, 0 = spins)")
     ap.add_argument("--resolve-unheld", type=int, default=1,
@@ -505,6 +507,7 @@ def main():
     snap.tune("stream_ecap", a.stream_ecap)
     if a.resolve_unheld != 1:
         snap.tune("resolve_unheld", a.resolve_unheld)
+    snap.tune("device_sync", a.device_sync)
     if a.stream_chunk != 64:
         snap.tune("stream_chunk", a.stream_chunk)
     snap.tune("grid_wgs", a.grid_wgs)

@@ -220,7 +220,8 @@ int kg_snapshot_materialized(const kg_snapshot* s, uint64_t* out3);
  * backward / grid tiers (default 512; 0 = no budget) -- cuts the stream kernel's tail of long walks.
  * key "resolve_unheld" (0/1): without a namespace program, k_resolve reads a subject id's holder
  * bit before the node map and answers an unheld subject NotMember without the lookup (default 1).
- * key "host_sync" (0/1): kg_check_batch waits for its device work asleep on a blocking-sync event
+ * key "device_sync" (0/1): the same for kg_check_batch_device when it waits (stats or a grid-tier
+ * readback; default 1: asleep -- 5.6 -> 5.8 x 10^9 checks/s with 4 batches in flight).  key "host_sync" (0/1): kg_check_batch waits for its device work asleep on a blocking-sync event
  * (1, default: no core spins per in-flight batch) or spinning in hipStreamSynchronize (0).
  * key "stream_chunk" (1..64): queries a k_stream2 wave dequeues at once (default 64).
  * key "stream_wgs": k_stream workgroups per CU (0 = by variant); "back_wgs" (1..3) and "grid_wgs"

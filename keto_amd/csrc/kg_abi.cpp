@@ -385,6 +385,11 @@ static int tune_one(Snapshot* s, const char* key, int64_t value) {
     s->shard_vis_mode = (int)value;
     return 0;
   }
+  if (strcmp(key, "device_sync") == 0) {
+    if (value < 0 || value > 1) return set_error(-2, "device_sync must be 0 or 1");
+    s->device_sync = (int)value;
+    return 0;
+  }
   if (strcmp(key, "host_sync") == 0) {
     if (value < 0 || value > 1) return set_error(-2, "host_sync must be 0 or 1");
     s->host_sync = (int)value;

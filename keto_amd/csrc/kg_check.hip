@@ -2106,7 +2106,7 @@ int check_batch_device(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n,
                        uint8_t* d_out, uint32_t* d_err, kg_stats* stats) {
   BatchPending bp;
   if (int rc = check_batch_begin(s, w, d_q, n, global_max_depth, d_out, d_err, stats, &bp)) return rc;
-  return check_batch_end(s, w, &bp, nullptr);
+  return check_batch_end(s, w, &bp, nullptr, s->device_sync != 0);
 }
 
 }  // namespace kg

@@ -215,6 +215,7 @@ struct Snapshot {
   int resolve_unheld = 1;  // kg_snapshot_tune("resolve_unheld"): k_resolve reads the holder bit before the node map
   uint32_t stream_chunk = 64;  // kg_snapshot_tune("stream_chunk"): k_stream2 queries per dequeue (1..64)
   int grid_wgs = 16;         // kg_snapshot_tune("grid_wgs"): k_grid_level workgroups per CU
+  int device_sync = 1;      // kg_snapshot_tune("device_sync"): kg_check_batch_device waits asleep (1) or spinning (0)
   int host_sync = 1;        // kg_snapshot_tune("host_sync"): kg_check_batch waits asleep (1) or spinning (0)
   int stream_wgs = 0;        // kg_snapshot_tune("stream_wgs"): k_stream workgroups per CU (0 = by LDS)
   int interp_wgs = 6;        // kg_snapshot_tune("interp_wgs"): k_interp_lds workgroups (4 waves) per CU (6 fit the LDS)
