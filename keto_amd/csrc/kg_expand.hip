@@ -376,6 +376,15 @@ struct ExpandBufs {
   uint64_t* d_off = nullptr;
   size_t off_cap = 0;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  hipEvent_t sync_ev = nullptr;  // blocking-sync: a caller waits asleep (16 batches in flight, 16 CPUs)
+  // Waits for everything enqueued on st so far without spinning a core.
+  hipError_t wait(hipStream_t st) {
+    hipError_t e = hipSuccess;
+    if (!sync_ev && (e = hipEventCreateWithFlags(&sync_ev, hipEventBlockingSync | hipEventDisableTiming)) != hipSuccess)
+      return e;
+    if ((e = hipEventRecord(sync_ev, st)) != hipSuccess) return e;
+    return hipEventSynchronize(sync_ev);
+  }
   ~ExpandBufs() {
     if (device >= 0) hipSetDevice(device);
     for (void* p : {(void*)d_roots, (void*)outs, (void*)p2, (void*)ctl, (void*)stacks, (void*)bm, (void*)arena,
@@ -383,6 +392,7 @@ struct ExpandBufs {
       if (p) hipFree(p);
     for (auto& e : ev)
       if (e) hipEventDestroy(e);
+    if (sync_ev) hipEventDestroy(sync_ev);
   }
 };
 
@@ -532,7 +542,7 @@ int expand_batch(Snapshot* s, hipStream_t stream, void** bufs, const kg_set* roo
       break;
     }
     if ((e = hipMemcpyAsync(&h, B.ctl, sizeof h, hipMemcpyDeviceToHost, stream)) != hipSuccess ||
-        (e = hipStreamSynchronize(stream)) != hipSuccess) {
+        (e = B.wait(stream)) != hipSuccess) {
       fail("expand", e);
       break;
     }
@@ -546,7 +556,7 @@ int expand_batch(Snapshot* s, hipStream_t stream, void** bufs, const kg_set* roo
   std::vector<RootOut> ho(n);
   if (!rc && (e = hipMemcpyAsync(ho.data(), B.outs, n * sizeof(RootOut), hipMemcpyDeviceToHost, stream)) != hipSuccess)
     fail("D2H", e);
-  if (!rc && (e = hipStreamSynchronize(stream)) != hipSuccess) fail("D2H", e);
+  if (!rc && (e = B.wait(stream)) != hipSuccess) fail("D2H", e);
   if (!rc) {
     for (size_t r = 0; r < n; r++) {
       if (ho[r].count == 0xFFFFFFFFu) {
@@ -574,7 +584,7 @@ int expand_batch(Snapshot* s, hipStream_t stream, void** bufs, const kg_set* roo
       (void)hipEventRecord(B.ev[3], stream);
       if ((e = hipMemcpyAsync(out->nodes, B.dst, total * sizeof(kg_tree_node), hipMemcpyDeviceToHost, stream)) !=
               hipSuccess ||
-          (e = hipStreamSynchronize(stream)) != hipSuccess)
+          (e = B.wait(stream)) != hipSuccess)
         fail("compact", e);
     }
   }
