@@ -1090,7 +1090,7 @@ __global__ __launch_bounds__(256) void k_stream2(DevSnap s, const RQuery* __rest
 template <int VLOG2, int QC, int CHUNK, int INS_CAP>
 __global__ __launch_bounds__(256) void k_stream3(DevSnap s, const RQuery* __restrict__ rq, WorkList wl, uint32_t* heads,
                                                  uint8_t* __restrict__ out, uint32_t* next_list, uint32_t* next_count,
-                                                 Ctl* ctl) {
+                                                 Ctl* ctl, uint32_t ecap) {
   using Lds = Stream2Lds<VLOG2, QC, 1>;
   constexpr uint32_t VT = 1u << VLOG2;
   static_assert(QC <= 256 && (QC & (QC - 1)) == 0, "FIFO ring of <= 256 entries (9-bit generations stay unique)");
@@ -1163,12 +1163,13 @@ __global__ __launch_bounds__(256) void k_stream3(DevSnap s, const RQuery* __rest
         c_left -= got;
         if (mine) {
           const uint32_t slot = lane, gen = L.s_state[slot] & S2_GEN;
-          const bool over = qdepth > (int32_t)S2_DMAX || qlen > S2_LONG;
+          const bool over = qdepth > (int32_t)S2_DMAX || qlen > S2_LONG || qlen > ecap;
           L.s_qi[slot] = qi;
           L.s_subj[slot] = qsubj;
           L.s_sig[slot] = subj_sig(qsubj);
           L.s_cnt[slot] = 1;
           L.s_ins[slot] = 0;
+          L.s_edg[slot] = qlen;
           L.s_state[slot] = over ? (gen | S2_OVER) : gen;
           const unsigned long long key =
               (1ull << 63) | ((unsigned long long)gen << 37) | ((unsigned long long)slot << 32) | qnode;
@@ -1274,19 +1275,22 @@ __global__ __launch_bounds__(256) void k_stream3(DevSnap s, const RQuery* __rest
     const unsigned long long old = keepc ? L.vt[hv] : 0ull;
     const bool fresh = keepc && !longrow && old != key;
     if (fresh) L.vt[hv] = key;
-    const uint32_t k = fresh ? atomicAdd(&L.s_ins[slot], 1u) : 0u;
-    const bool ok = fresh && k < (uint32_t)INS_CAP;
+    // INS_CAP 0: the edge budget ecap bounds a query instead (as k_stream2 variant 12)
+    const uint32_t k = (INS_CAP && fresh) ? atomicAdd(&L.s_ins[slot], 1u) : 0u;
+    const bool ok = fresh && (INS_CAP == 0 || k < (uint32_t)INS_CAP);
     const uint64_t am = __ballot(ok);
     const uint32_t room = QC - (tail - head);
     const uint32_t pos = __popcll(am & ((1ull << lane) - 1));
     const bool appended = ok && pos < room;
+    const bool overbudget =
+        appended && ecap != 0xFFFFFFFFu && atomicAdd(&L.s_edg[slot], cur_x.len) + cur_x.len > ecap;
     if (appended) {
       const uint32_t at = (tail + pos) & (QC - 1);
       L.e_beg[at] = cur_x.begin;
       L.e_meta[at] = cur_x.len | (cur_om & 0x01FFF800u) | ((d - 1) << 25);
       atomicAdd(&L.s_cnt[slot], 1u);
     }
-    if (longrow || (fresh && !appended)) atomicOr(&L.s_state[slot], S2_OVER);
+    if (longrow || (fresh && !appended) || overbudget) atomicOr(&L.s_state[slot], S2_OVER);
     tail += min((uint32_t)__popcll(am), room);
     {  // last iteration's probes: a chain past a full first bucket (rare) is walked here
       bool h = false, more = false;
@@ -1954,7 +1958,10 @@ int check_batch_begin(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n, 
                            d_out, ovf_list, ovf_count, ctl, ecap, std::max<uint32_t>(1u, std::min<uint32_t>(s->stream_chunk, 64u)));
       else if (sv == 10)
         hipLaunchKernelGGL((k_stream3<9, 256, 64, 64>), dim3(grid), dim3(256), 0, stream, s->ds, rq, wl, ctl->heads,
-                           d_out, ovf_list, ovf_count, ctl);
+                           d_out, ovf_list, ovf_count, ctl, 0xFFFFFFFFu);
+      else if (sv == 13)  // k_stream3 without the node cap, bounded by the edge budget
+        hipLaunchKernelGGL((k_stream3<9, 256, 64, 0>), dim3(grid), dim3(256), 0, stream, s->ds, rq, wl, ctl->heads,
+                           d_out, ovf_list, ovf_count, ctl, ecap);
       else KG_STREAM(8, V0, 256, 16);
 #undef KG_STREAM
     }
