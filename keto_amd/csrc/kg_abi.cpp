@@ -366,7 +366,7 @@ static int tune_one(Snapshot* s, const char* key, int64_t value) {
     return 0;
   }
   if (strcmp(key, "stream") == 0) {
-    if (value < 0 || value > 13) return set_error(-2, "stream must be in [0, 13]");
+    if (value < 0 || value > 14) return set_error(-2, "stream must be in [0, 14]");
     s->stream_variant = (int)value;
     return 0;
   }

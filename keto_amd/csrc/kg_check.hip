@@ -1956,6 +1956,9 @@ int check_batch_begin(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n, 
       else if (sv == 12)  // no expanded-node cap per query (edge budget only)
         hipLaunchKernelGGL((k_stream2<9, 256, 64, 0, 1>), dim3(grid), dim3(256), 0, stream, s->ds, rq, wl, ctl->heads,
                            d_out, ovf_list, ovf_count, ctl, ecap, std::max<uint32_t>(1u, std::min<uint32_t>(s->stream_chunk, 64u)));
+      else if (sv == 14)  // 128-edge windows, no node cap
+        hipLaunchKernelGGL((k_stream2<9, 256, 64, 0, 2>), dim3(grid), dim3(256), 0, stream, s->ds, rq, wl, ctl->heads,
+                           d_out, ovf_list, ovf_count, ctl, ecap, std::max<uint32_t>(1u, std::min<uint32_t>(s->stream_chunk, 64u)));
       else if (sv == 10)
         hipLaunchKernelGGL((k_stream3<9, 256, 64, 64>), dim3(grid), dim3(256), 0, stream, s->ds, rq, wl, ctl->heads,
                            d_out, ovf_list, ovf_count, ctl, 0xFFFFFFFFu);

@@ -86,7 +86,7 @@ def test_random_graphs_vs_oracle(seed):
         assert (out[inv] == dfs[inv]).all()
 
 
-@pytest.mark.parametrize("variant", [8, 9, 10, 11, 12, 13])
+@pytest.mark.parametrize("variant", [8, 9, 10, 11, 12, 13, 14])
 def test_stream_tier_long_rows_and_dense_cycles(variant):
     """Rows longer than a FIFO entry holds (k_stream2: 2047 edges), dense cycles (the direct-mapped
     visited cache evicts and re-expands), many queries per wave on one hub: exact vs the oracle."""
@@ -196,7 +196,8 @@ def _torch():
 
 @pytest.mark.parametrize("n_tuples,gmax,variant,unheld", [(200_000, 10, 9, 1), (300_000, 5, 9, 1), (300_000, 10, 10, 1),
                                                            (300_000, 10, 11, 1), (300_000, 10, 9, 0),
-                                                           (300_000, 10, 12, 1), (300_000, 10, 13, 1)])
+                                                           (300_000, 10, 12, 1), (300_000, 10, 13, 1),
+                                                           (300_000, 10, 14, 1)])
 def test_synthetic_graph_vs_oracle(n_tuples, gmax, variant, unheld):
     torch = _torch()
     from keto_amd import _lib
