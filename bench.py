@@ -118,9 +118,19 @@ def bench_expand(a):
     import torch
     from keto_amd import _lib
     from keto_amd.engine import Snapshot
+    # one process per GPU under torchrun (each rank its own replica and batches, max-over-ranks time:
+    # weak scaling); ranks beyond the GPU count share GPUs (a gloo rehearsal on a 1-GPU box)
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
+    dist = None
+    torch.cuda.set_device(local)
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group(a.backend, rank=rank, world_size=world)
     L = _lib.load()
-    torch.cuda.set_device(0)
-    snap = Snapshot.synthetic(int(a.tuples), seed=a.seed, device=0)
+    snap = Snapshot.synthetic(int(a.tuples), seed=a.seed, device=local)
     from keto_amd.synth import hot_group_roots
     roots = hot_group_roots(snap.synth_ids(), a.roots)
     depth = a.global_depth if a.global_depth != 10 else 5
@@ -139,7 +149,8 @@ def bench_expand(a):
     nw = min(P, a.steps)
     results = [None] * a.steps
     errors = []
-    ready = threading.Barrier(nw + 1)
+    warm = threading.Barrier(nw + 1)  # every lane warmed up
+    go = threading.Barrier(nw + 1)    # timed region starts (after the ranks' barrier)
 
     def worker(p):
         try:
@@ -147,7 +158,8 @@ def bench_expand(a):
                 step()
         except Exception as e:  # noqa: BLE001 -- re-raised below
             errors.append(e)
-        ready.wait()
+        warm.wait()
+        go.wait()
         try:
             for k in range(p, a.steps, nw):
                 if not errors:
@@ -158,21 +170,26 @@ def bench_expand(a):
     th = [threading.Thread(target=worker, args=(p,)) for p in range(nw)]
     for t in th:
         t.start()
-    ready.wait()
+    warm.wait()
+    if dist:
+        dist.barrier()
     t0 = time.perf_counter()
+    go.wait()
     for t in th:
         t.join()
     el = time.perf_counter() - t0
     if errors:
         raise errors[0]
+    el, _ = aggregate(dist, el, 0.0, f"cuda:{local}" if a.backend == "nccl" else None)
     nodes = sum(r[0] for r in results)
     kms = sum(r[1] for r in results)
     off = results[-1][2]
-    out = {"metric": "expand trees/sec (batched BuildTree, hot group#member roots)", "value": a.roots * a.steps / el,
-           "unit": "trees/s", "n_gpus": 1, "steps": a.steps, "warmup": a.warmup, "ms_per_step": el / a.steps * 1e3,
+    out = {"metric": "expand trees/sec (batched BuildTree, hot group#member roots)",
+           "value": world * a.roots * a.steps / el, "unit": "trees/s", "n_gpus": world, "scaling": "weak",
+           "steps": a.steps, "warmup": a.warmup, "ms_per_step": el / a.steps * 1e3,
            "higher_is_better": True, "dtype": "u32", "data": "synthetic (device-generated, seed %d)" % a.seed,
            "config": {"workload": "C5: %d hot roots @ %.3g tuples, max_read_depth %d" % (a.roots, a.tuples, depth),
-                      "inflight_per_gpu": P, "hw_queues": a.hw_queues},
+                      "inflight_per_gpu": P, "hw_queues": a.hw_queues, "parallelism": f"replica{world}"},
            "tree_nodes_per_step": nodes / a.steps, "tree_nodes_per_s": nodes / el,
            "kernel_ms_per_step": kms / a.steps}
     if off is not None:
@@ -180,7 +197,10 @@ def bench_expand(a):
         out["records_per_root"] = {"p50": float(np.percentile(sz, 50)), "p99": float(np.percentile(sz, 99)),
                                    "max": int(sz.max()), "roots_over_512": int((sz > 512).sum()),
                                    "top10_share": float(np.sort(sz)[-10:].sum() / max(1, sz.sum()))}
-    print(json.dumps(out), flush=True)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
 
 
 def bench_refresh(a):
