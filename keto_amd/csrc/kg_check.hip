@@ -151,7 +151,7 @@ __global__ __launch_bounds__(256) void k_resolve(DevSnap s, const kg_query* __re
     const bool unheld = no_holder_filter == 2 && use_bits && !s.relflags && !((hw >> (subj & 31)) & 1u);
     NSlot n0{};
     if (key_ok && !unheld) n0 = s.nmap[ni];
-    uint32_t node = NONE, rb = 0, rl = 0, rsig = 0xFFFFFFFFu;
+    uint32_t node = NONE, rb = 0, rl = 0, rsig = 0xFFFFFFFFu, nfl = 0;
     if (unheld) {
       no_holder = true;
     } else if (key_ok) {
@@ -162,6 +162,7 @@ __global__ __launch_bounds__(256) void k_resolve(DevSnap s, const kg_query* __re
         rb = v.beg;
         rl = v.len;
         rsig = v.sig;
+        nfl = (uint32_t)(v.pad1 & 0xFFu);
       }
     }
     if (!sid) {
@@ -174,7 +175,8 @@ __global__ __launch_bounds__(256) void k_resolve(DevSnap s, const kg_query* __re
     if (node == NONE) {
       route = rf ? ROUTE_GENERAL : ROUTE_DONE;
     } else {
-      bool impure = s.nflags && (s.nflags[node] & NF_IMPURE);
+      // the node's flags ride in its node-map slot (a random nflags read per query otherwise)
+      bool impure = s.nflags && (nfl & NF_IMPURE);
       route = impure ? ROUTE_GENERAL : ROUTE_LIGHT;
     }
     bool member = false;

@@ -126,7 +126,7 @@ struct NSlot {
   uint64_t key;
   uint32_t node, beg, len;
   uint32_t sig;  // Bloom signature of the node's row subjects (as AdjX.sig): k_resolve's root probe filter
-  uint64_t pad1;
+  uint64_t pad1;  // low byte: the node's flags (nflags; 0 without a namespace program)
 };
 // Holder-hash slot: tagged subject -> hold[first, first + count).  key == NONE: free.
 struct HSlot {

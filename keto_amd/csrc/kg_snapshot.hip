@@ -54,7 +54,7 @@ __global__ void k_dset_insert_rows(uint64_t* dset, uint64_t nb, const uint64_t* 
 
 __global__ void k_nmap_insert(NSlot* nm, uint64_t slots, const uint32_t* nd_ns, const uint32_t* nd_obj,
                               const uint32_t* nd_rel, const uint64_t* adj_off, const uint32_t* sig,
-                              uint32_t n_nodes) {
+                              const uint8_t* flags, uint32_t n_nodes) {
   uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
   if (v >= n_nodes) return;
   uint64_t key = nmap_key(nd_ns[v], nd_rel[v], nd_obj[v]);
@@ -67,6 +67,7 @@ __global__ void k_nmap_insert(NSlot* nm, uint64_t slots, const uint32_t* nd_ns, 
       nm[i].beg = (uint32_t)adj_off[v];
       nm[i].len = (uint32_t)(adj_off[v + 1] - adj_off[v]);
       nm[i].sig = sig[v];
+      nm[i].pad1 = flags ? flags[v] : 0u;  // node flags: k_resolve's impurity test without a random nflags read
       return;
     }
     i = hash_next(i, slots);
@@ -440,7 +441,7 @@ int Snapshot::build_hash_tables() {
                          stream, dset, buckets, coff, csub, ds.n_nodes, n_rows);
     HIPC(hipGetLastError());
     hipLaunchKernelGGL(k_nmap_insert, dim3(grid), dim3(256), 0, stream, nm, slots, ds.nd_ns, ds.nd_obj,
-                       ds.nd_rel, ds.adj_off, sig, ds.n_nodes);
+                       ds.nd_rel, ds.adj_off, sig, ds.nflags, ds.n_nodes);
     HIPC(hipGetLastError());
   }
   HIPC(hipStreamSynchronize(stream));
