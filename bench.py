@@ -72,6 +72,8 @@ def parse():
                     help="kg_snapshot_tune host_sync (--mode host: 1 = kg_check_batch waits asleep, 0 = spins)")
     ap.add_argument("--resolve-unheld", type=int, default=1,
                     help="kg_snapshot_tune resolve_unheld (1: k_resolve skips the node map for subjects no row holds)")
+    ap.add_argument("--stream-steal", type=int, default=4,
+                    help="kg_snapshot_tune stream_steal (XCD ranges a k_stream2 wave dequeues from, 1..8)")
     ap.add_argument("--stream-chunk", type=int, default=64,
                     help="kg_snapshot_tune stream_chunk (k_stream2 queries per dequeue, 1..64)")
     ap.add_argument("--grid-wgs", type=int, default=4, help="kg_snapshot_tune grid_wgs (k_grid_level WGs per CU)")
@@ -528,6 +530,7 @@ def main():
     if a.resolve_unheld != 1:
         snap.tune("resolve_unheld", a.resolve_unheld)
     snap.tune("device_sync", a.device_sync)
+    snap.tune("stream_steal", a.stream_steal)
     if a.stream_chunk != 64:
         snap.tune("stream_chunk", a.stream_chunk)
     snap.tune("grid_wgs", a.grid_wgs)

@@ -223,6 +223,8 @@ int kg_snapshot_materialized(const kg_snapshot* s, uint64_t* out3);
  * key "device_sync" (0/1): the same for kg_check_batch_device when it waits (stats or a grid-tier
  * readback; default 1: asleep -- 5.6 -> 5.8 x 10^9 checks/s with 4 batches in flight).  key "host_sync" (0/1): kg_check_batch waits for its device work asleep on a blocking-sync event
  * (1, default: no core spins per in-flight batch) or spinning in hipStreamSynchronize (0).
+ * key "stream_steal" (1..8): XCD ranges of the work list a k_stream2 wave dequeues from (default 4:
+ * when the list drains every wave walks them, one atomic each on a few hot words).
  * key "stream_chunk" (1..64): queries a k_stream2 wave dequeues at once (default 64).
  * key "stream_wgs": k_stream workgroups per CU (0 = by variant); "back_wgs" (1..3) and "grid_wgs"
  * (1..64): k_back / k_grid_level workgroups per CU.  key "shard_vis": log2 of the

@@ -405,6 +405,11 @@ static int tune_one(Snapshot* s, const char* key, int64_t value) {
     s->resolve_unheld = (int)value;
     return 0;
   }
+  if (strcmp(key, "stream_steal") == 0) {
+    if (value < 1 || value > 8) return set_error(-2, "stream_steal must be in [1, 8]");
+    s->stream_steal = (uint32_t)value;
+    return 0;
+  }
   if (strcmp(key, "stream_chunk") == 0) {
     if (value < 1 || value > 64) return set_error(-2, "stream_chunk must be in [1, 64]");
     s->stream_chunk = (uint32_t)value;

@@ -373,8 +373,8 @@ struct WorkList {
 // Dequeue up to `want` consecutive work items for a wave from per-XCD heads.  Returns the first
 // list position (NONE when every range is drained) and the number taken.
 __device__ __forceinline__ uint32_t dequeue_n(const WorkList& wl, uint32_t* heads, uint32_t& head_sel, uint32_t head0,
-                                              uint32_t want, uint32_t& got) {
-  while (head_sel < head0 + 8) {
+                                              uint32_t want, uint32_t& got, uint32_t ranges = 8) {
+  while (head_sel < head0 + ranges) {
     const uint32_t h = head_sel & 7;
     uint32_t lo, hi;
     wl.range(h, lo, hi);
@@ -821,7 +821,7 @@ __device__ __forceinline__ bool dset_probe_fast(const DevSnap& s, bool want, uin
 template <int VLOG2, int QC, int CHUNK, int INS_CAP, int EPL>
 __global__ __launch_bounds__(256) void k_stream2(DevSnap s, const RQuery* __restrict__ rq, WorkList wl, uint32_t* heads,
                                                  uint8_t* __restrict__ out, uint32_t* next_list, uint32_t* next_count,
-                                                 Ctl* ctl, uint32_t ecap, uint32_t chunk) {
+                                                 Ctl* ctl, uint32_t ecap, uint32_t chunk, uint32_t ranges) {
   using Lds = Stream2Lds<VLOG2, QC, EPL>;
   constexpr uint32_t WIN = 64u * EPL;  // edges per step: EPL per lane
   constexpr uint32_t VT = 1u << VLOG2;
@@ -866,7 +866,9 @@ __global__ __launch_bounds__(256) void k_stream2(DevSnap s, const RQuery* __rest
         // chunk (kg_snapshot_tune "stream_chunk", <= CHUNK): one dequeue costs three dependent
         // round trips (head atomic, list, rq), so small chunks stall the step loop (guided
         // self-scheduling toward the free-slot count measured 5.3 -> 3.2 x 10^9 checks/s)
-        if (lane == 0) first = dequeue_n(wl, heads, head_sel, head0, chunk, got);
+        // ranges (kg_snapshot_tune "stream_steal"): how many XCD ranges a wave dequeues from; once
+        // the list drains every wave walks them, one atomic each on 8 hot words
+        if (lane == 0) first = dequeue_n(wl, heads, head_sel, head0, chunk, got, ranges);
         first = __shfl(first, 0, 64);
         c_left = __shfl(got, 0, 64);
         c_pos = 0;
@@ -1951,16 +1953,16 @@ int check_batch_begin(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n, 
       else if (sv == 8) KG_STREAM(32, V8, 256, 64);
       else if (sv == 9)
         hipLaunchKernelGGL((k_stream2<9, 256, 64, 64, 1>), dim3(grid), dim3(256), 0, stream, s->ds, rq, wl, ctl->heads,
-                           d_out, ovf_list, ovf_count, ctl, ecap, std::max<uint32_t>(1u, std::min<uint32_t>(s->stream_chunk, 64u)));
+                           d_out, ovf_list, ovf_count, ctl, ecap, std::max<uint32_t>(1u, std::min<uint32_t>(s->stream_chunk, 64u)), s->stream_steal);
       else if (sv == 11)  // 128-edge windows (two edges per lane)
         hipLaunchKernelGGL((k_stream2<9, 256, 64, 64, 2>), dim3(grid), dim3(256), 0, stream, s->ds, rq, wl, ctl->heads,
-                           d_out, ovf_list, ovf_count, ctl, ecap, std::max<uint32_t>(1u, std::min<uint32_t>(s->stream_chunk, 64u)));
+                           d_out, ovf_list, ovf_count, ctl, ecap, std::max<uint32_t>(1u, std::min<uint32_t>(s->stream_chunk, 64u)), s->stream_steal);
       else if (sv == 12)  // no expanded-node cap per query (edge budget only)
         hipLaunchKernelGGL((k_stream2<9, 256, 64, 0, 1>), dim3(grid), dim3(256), 0, stream, s->ds, rq, wl, ctl->heads,
-                           d_out, ovf_list, ovf_count, ctl, ecap, std::max<uint32_t>(1u, std::min<uint32_t>(s->stream_chunk, 64u)));
+                           d_out, ovf_list, ovf_count, ctl, ecap, std::max<uint32_t>(1u, std::min<uint32_t>(s->stream_chunk, 64u)), s->stream_steal);
       else if (sv == 14)  // 128-edge windows, no node cap
         hipLaunchKernelGGL((k_stream2<9, 256, 64, 0, 2>), dim3(grid), dim3(256), 0, stream, s->ds, rq, wl, ctl->heads,
-                           d_out, ovf_list, ovf_count, ctl, ecap, std::max<uint32_t>(1u, std::min<uint32_t>(s->stream_chunk, 64u)));
+                           d_out, ovf_list, ovf_count, ctl, ecap, std::max<uint32_t>(1u, std::min<uint32_t>(s->stream_chunk, 64u)), s->stream_steal);
       else if (sv == 10)
         hipLaunchKernelGGL((k_stream3<9, 256, 64, 64>), dim3(grid), dim3(256), 0, stream, s->ds, rq, wl, ctl->heads,
                            d_out, ovf_list, ovf_count, ctl, 0xFFFFFFFFu);

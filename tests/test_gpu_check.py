@@ -69,6 +69,7 @@ def test_random_graphs_vs_oracle(seed):
                                                                                        (11 if seed < 19 else 13)))))
     reg.snapshot.tune("stream_ecap", 6 if seed in (2, 17, 20) else 0)
     reg.snapshot.tune("stream_chunk", 1 if seed == 18 else 64)
+    reg.snapshot.tune("stream_steal", 1 if seed in (11, 18) else (8 if seed == 12 else 4))
     qs = random_queries(rng, nss, rels, 3000, n_obj=40 + 20 * (seed % 6))
     depths = rng.integers(-1, 9, len(qs))
     q6 = np.asarray([it.tuple_ids(t) for t in qs], np.uint32)
