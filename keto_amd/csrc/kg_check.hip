@@ -1643,8 +1643,16 @@ __global__ __launch_bounds__(256) void k_back(DevSnap s, const RQuery* __restric
   const int t = threadIdx.x % W;  // thread within the query group
   const uint32_t qcount = *qcount_p;
   unsigned long long st_rows = 0, st_edges = 0, st_done = 0;
-  for (;;) {
-    if (t == 0) L.qi = atomicAdd(qhead, 1u);
+  // the first query of every group is static (group g takes g); later ones are dequeued past the
+  // groups' count, so groups beyond the list and the list's end cost no atomic on the one hot word
+  const uint32_t n_groups = gridDim.x * (256 / W), g0 = blockIdx.x * (256 / W) + threadIdx.x / W;
+  for (bool first = true;; first = false) {
+    if (first) {
+      if (t == 0) L.qi = g0;
+    } else {
+      if (n_groups >= qcount) break;  // the static round took every query
+      if (t == 0) L.qi = n_groups + atomicAdd(qhead, 1u);
+    }
     bk_sync<W>();
     const uint32_t hi = L.qi;
     if (hi >= qcount) break;
