@@ -32,6 +32,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+# independent random 16-B loads/s from HBM-sized tables (16-160 GiB) on one MI355X: tools/randprobe.hip,
+# profiles/r2_randprobe_sizes.jsonl (~37 G/s; the line, not the byte, is the unit of a random gather)
+RAND_REQ_PEAK = 37.0e9
 STREAM_KERNELS = {0: "k_stream<8,7,256,16>", 1: "k_stream<16,6,256,32>", 2: "k_stream<16,7,512,32>",
                   3: "k_stream<32,5,192,64>", 4: "k_stream<32,6,256,64>", 5: "k_stream<32,wave1024/128,256,64>",
                   6: "k_stream<32,wave1024/256,320,64>", 7: "k_stream<32,wave1024/64,256,64>",
@@ -39,13 +42,15 @@ STREAM_KERNELS = {0: "k_stream<8,7,256,16>", 1: "k_stream<16,6,256,32>", 2: "k_s
                   10: "k_stream3<9,256,64,64>", 11: "k_stream2<9,256,64,64,2>", 12: "k_stream2<9,256,64,0,1>", 13: "k_stream3<9,256,64,0>", 14: "k_stream2<9,256,64,0,2>"}
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--tuples", type=float, default=None, help="synthetic graph size (tuples; default 1e9; 2e6 with --heavy-tail, whose ~640 edges per row "
-                         "make that ~240 M rows)")
+    ap.add_argument("--tuples", type=float, default=None,
+                    help="synthetic graph size in tuples (rows actually generated; default 1e9, 1e7 for --mode refresh, "
+                         "1.2e8 with --heavy-tail).  The generator's size parameter is calibrated so the snapshot "
+                         "holds at least this many rows")
     ap.add_argument("--heavy-tail", action="store_true",
                     help="out-degree law P(k) ~ k^-1.5 (Pareto tail index 0.5 for docs and groups, SURVEY.md 8d) "
                          "instead of the default 1.3 / 1.1; ~40x the rows per node")
@@ -93,6 +98,18 @@ def parse():
                     help="batches in flight per GPU: one HIP stream (own workspace) and one host thread each "
                          "(default 4; 16 for --mode expand, whose batches end in long sequential roots)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline time budget (0 = skip)")
+    ap.add_argument("--parity", type=int, default=1_000_000,
+                    help="checks of the first timed batch compared with the oracle (Go-order DFS; 0 = skip).  Any "
+                         "mismatch makes bench.py exit 1 after printing its line")
+    ap.add_argument("--parity-canonical", type=int, default=100_000,
+                    help="of those, checks also compared under the oracle's schedule-free (canonical) policy")
+    ap.add_argument("--parity-roots", type=int, default=300, help="--mode expand: roots compared with oracle.expand")
+    ap.add_argument("--latency-batches", type=int, default=240,
+                    help="batches of the separate latency phase (after the timed region, same batches in flight): "
+                         "p50 / p99 batch latency, submit to done")
+    ap.add_argument("--host-calls", type=int, default=6,
+                    help="kg_check_batch calls per in-flight thread in the host-path leg (1 M-check host batches, "
+                         "PCIe both ways; 0 = skip)")
     ap.add_argument("--stats-every", type=int, default=1,
                     help="collect kernel stats on every k-th timed batch (1 = all; a batch with stats is waited for)")
     ap.add_argument("--replay", type=int, default=0,
@@ -112,7 +129,38 @@ def parse():
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for --mode sharded (nccl = RCCL)")
     ap.add_argument("--roots", type=int, default=100_000, help="expand roots per step (C5)")
     ap.add_argument("--delta", type=int, default=1000, help="--mode refresh: rows per transaction")
-    return ap.parse_args()
+    a = ap.parse_args(argv)
+    if a.hw_queues is None:
+        a.hw_queues = 16 if a.mode == "expand" else 0
+    if a.inflight is None:
+        a.inflight = 16 if a.mode == "expand" else 4
+    if a.back_wgs is None:
+        a.back_wgs = 1 if a.preset else 2
+    if a.tuples is None:
+        a.tuples = 1.2e8 if a.heavy_tail else (1e7 if a.mode == "refresh" else 1e9)
+    return a
+
+
+def apply_tune(snap, a) -> None:
+    """The engine knobs of the check bench (tests/test_gpu_check.py::test_bench_tune_set_vs_oracle runs
+    the parity test with exactly this set)."""
+    snap.tune("tiers", a.tiers)
+    snap.tune("wide", a.wide)
+    snap.tune("back", a.back)
+    snap.tune("stream", a.stream)
+    snap.tune("stream_ecap", a.stream_ecap)
+    if a.resolve_unheld != 1:
+        snap.tune("resolve_unheld", a.resolve_unheld)
+    snap.tune("device_sync", a.device_sync)
+    snap.tune("stream_steal", a.stream_steal)
+    if a.stream_chunk != 64:
+        snap.tune("stream_chunk", a.stream_chunk)
+    snap.tune("grid_wgs", a.grid_wgs)
+    snap.tune("stream_wgs", a.stream_wgs)
+    snap.tune("back_wgs", a.back_wgs)
+    snap.tune("grid_reserve", 1)  # a server pays this once at start-up, not inside some request's batch
+    if snap.program is not None and not snap.program.empty:
+        snap.tune("interp_wgs", a.interp_wgs)
 
 
 def bench_expand(a):
@@ -133,7 +181,7 @@ def bench_expand(a):
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group(a.backend, rank=rank, world_size=world)
     L = _lib.load()
-    snap = Snapshot.synthetic(int(a.tuples), seed=a.seed, device=local)
+    snap, _ = build_synthetic(a, a.tuples, device=local)
     from keto_amd.synth import hot_group_roots
     roots = hot_group_roots(snap.synth_ids(), a.roots)
     depth = a.global_depth if a.global_depth != 10 else 5
@@ -200,10 +248,65 @@ def bench_expand(a):
         out["records_per_root"] = {"p50": float(np.percentile(sz, 50)), "p99": float(np.percentile(sz, 99)),
                                    "max": int(sz.max()), "roots_over_512": int((sz > 512).sum()),
                                    "top10_share": float(np.sort(sz)[-10:].sum() / max(1, sz.sum()))}
+    if rank == 0 and a.parity_roots > 0 and off is not None:
+        out["parity"] = expand_parity(snap, roots, np.diff(off.astype(np.int64)), depth, a)
     if rank == 0:
         print(json.dumps(out), flush=True)
+        if out.get("parity") and out["parity"]["mismatches"]:
+            sys.stderr.write("PARITY FAILURE: GPU expand trees differ from the oracle\n")
+            if dist:
+                dist.destroy_process_group()
+            sys.exit(1)
     if dist:
         dist.destroy_process_group()
+
+
+def expand_parity(snap, roots: np.ndarray, sizes: np.ndarray, depth: int, a) -> dict:
+    """C5 trees vs the oracle's BuildTree (oracle/keto_oracle.c, expand/engine.go:35-104) on the snapshot's
+    own rows: the 10 largest roots of the timed batch plus a seeded sample of the rest, same pre-order and
+    same child order (rows are in shard order on both sides)."""
+    from keto_amd import _lib
+    from keto_amd.engine import ExpandEngine, Config
+    from oracle.oracle import Oracle
+    L = _lib.load()
+    t0 = time.perf_counter()
+    info = snap.info()
+    nn, nr = info["nodes"], info["rows"]
+    row_off = np.zeros(nn + 1, np.uint64)
+    row_subj = np.zeros(nr, np.uint32)
+    nd = [np.zeros(nn, np.uint32) for _ in range(3)]
+    p = lambda x: x.ctypes.data_as(C.c_void_p)
+    _lib.check(L.kg_snapshot_export_csr(snap.handle, p(row_off), p(row_subj), p(nd[0]), p(nd[1]), p(nd[2])),
+               "kg_snapshot_export_csr")
+    orc = Oracle.from_csr(0, nd[0], nd[1], nd[2], row_off, row_subj, nthreads=16)
+    del row_subj
+    rng = np.random.default_rng(a.seed)
+    top = np.argsort(sizes)[-10:]
+    rest = rng.choice(len(roots), size=min(len(roots), max(0, a.parity_roots - 10)), replace=False)
+    pick = np.unique(np.concatenate([top, rest]))
+    ex = ExpandEngine(snap, Config(depth))
+    got = ex.build_trees_ids(roots[pick])
+    bad, recs = [], 0
+    for i, g in zip(pick, got):
+        r = roots[i]
+        node = int(r[1])  # synthetic group#member: node id == object id (kg_synth.h block layout)
+        assert nd[0][node] == r[0] and nd[1][node] == r[1] and nd[2][node] == r[2], "root is not its node"
+        exp = orc.expand_node(node, int(np.int32(np.uint32(r[3]))), depth)
+        recs += 0 if exp is None else len(exp)
+        if (exp is None) != (g is None):
+            bad.append(int(i))
+            continue
+        if exp is None:
+            continue
+        e2, g2 = np.asarray(exp, np.int64).copy(), np.asarray(g, np.int64).copy()
+        for x in (e2, g2):  # subject ids: oracle ns = rel = -1, GPU KG_SUBJECT_ID / 0
+            x[x[:, 1] == 0, 2] = 0
+            x[x[:, 1] == 0, 4] = 0
+        if e2.shape != g2.shape or not (e2 == g2).all():
+            bad.append(int(i))
+    return {"roots": int(len(pick)), "records": int(recs), "mismatches": len(bad), "first_mismatches": bad[:8],
+            "largest_roots_included": 10, "compare": "exact pre-order records, same child order",
+            "oracle": "oracle/keto_oracle.c ko_expand_node", "seconds": time.perf_counter() - t0}
 
 
 def bench_refresh(a):
@@ -218,7 +321,7 @@ def bench_refresh(a):
     L = _lib.load()
     torch.cuda.set_device(0)
     t0 = time.perf_counter()
-    base = Snapshot.synthetic(int(a.tuples), seed=a.seed, device=0)
+    base, _ = build_synthetic(a, a.tuples, device=0)
     t_full = time.perf_counter() - t0
     ids = base.synth_ids()
     rows = base.export()  # (n, 6) uint32, shard order
@@ -289,7 +392,7 @@ def bench_sharded(a):
         dist.init_process_group(a.backend, rank=rank, world_size=world)
     L = _lib.load()
     t_build = time.time()
-    snap = Snapshot.synthetic(int(a.tuples), seed=a.seed, device=local, shard=(rank, world), preset=a.preset)
+    snap, _ = build_synthetic(a, a.tuples, device=local, shard=(rank, world))
     info = snap.info()
     t_build = time.time() - t_build
     snap.tune("shard_budget", a.shard_budget)
@@ -362,7 +465,7 @@ def bench_host(a):
     n_dev = max(1, torch.cuda.device_count()) if a.gpus <= 1 else a.gpus
     devices = list(range(n_dev))
     t_build = time.time()
-    snap = Snapshot.synthetic(int(a.tuples), seed=a.seed, devices=devices, preset=a.preset)
+    snap, _ = build_synthetic(a, a.tuples, devices=devices)
     snap.tune("host_sync", a.host_sync)
     snap.tune("stream", a.stream)
     snap.tune("stream_wgs", a.stream_wgs)
@@ -473,6 +576,54 @@ def bench_host(a):
     print(json.dumps(out), flush=True)
 
 
+# rows per unit of the generator's size parameter (kg_synth.h: out-degree laws truncated at 1e5), measured at
+# 1e9 (preset 0: 945,129,335 rows; preset 1: ~1.34e9) and 2e6 (--heavy-tail: 239,847,864)
+ROWS_PER_T = {(0, False): 0.94513, (1, False): 1.3400, (0, True): 119.92, (1, True): 119.92}
+
+
+def build_synthetic(a, target_rows: float, **kw):
+    """Snapshot.synthetic sized so that it holds at least `target_rows` rows: the generator's size
+    parameter is the row target over the measured rows-per-parameter ratio (+0.2 %), and a build that
+    still falls short is rebuilt once with the ratio it measured (a build is ~1.4 s at 1e9)."""
+    from keto_amd.engine import Snapshot
+    ratio = ROWS_PER_T[(a.preset, bool(a.heavy_tail))]
+    shard = kw.get("shard")
+    for _ in range(2):
+        T = int(target_rows / ratio * 1.002) + 1
+        snap = Snapshot.synthetic(T, seed=a.seed, preset=a.preset, **kw)
+        rows = snap.info()["rows"]
+        if shard is not None or rows >= target_rows:
+            return snap, T
+        ratio = rows / T
+        snap.close()
+    raise RuntimeError(f"synthetic graph holds {rows} rows, below the {target_rows:.3g} target")
+
+
+def effective_cpus() -> dict:
+    """CPUs this process can actually use: the affinity mask, capped by the cgroup CPU quota
+    (cgroup v2 cpu.max or v1 cfs_quota_us / cfs_period_us) -- the GPU box's cgroup allows 16 of 256."""
+    ncpu = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = ncpu
+    quota = None
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(p)
+    except (OSError, ValueError):
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            p = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = q / p
+        except (OSError, ValueError):
+            pass
+    eff = aff if quota is None else max(1, min(aff, int(quota + 0.999)))
+    return {"nproc": ncpu, "affinity": aff, "cgroup_quota": quota, "effective": eff}
+
+
 def aggregate(dist, elapsed: float, edges: float, device=None):
     """Whole-job numbers over ranks: elapsed = MAX over ranks (the job ends with its slowest
     rank), edges = SUM.  Replicas exchange nothing else."""
@@ -488,16 +639,8 @@ def aggregate(dist, elapsed: float, edges: float, device=None):
 
 def main():
     a = parse()
-    if a.hw_queues is None:
-        a.hw_queues = 16 if a.mode == "expand" else 0
-    if a.inflight is None:
-        a.inflight = 16 if a.mode == "expand" else 4
-    if a.back_wgs is None:
-        a.back_wgs = 1 if a.preset else 2
     if a.hw_queues > 0:  # before anything initialises HIP (torch and the library load lazily)
         os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, a.hw_queues))
-    if a.tuples is None:
-        a.tuples = 2e6 if a.heavy_tail else (1e7 if a.mode == "refresh" else 1e9)
     if a.mode == "expand":
         return bench_expand(a)
     if a.mode == "sharded":
@@ -523,25 +666,8 @@ def main():
 
     t_build = time.time()
     alpha = 0.5 if a.heavy_tail else 0.0
-    snap = Snapshot.synthetic(int(a.tuples), seed=a.seed, device=local, preset=a.preset, doc_alpha=alpha,
-                              group_alpha=alpha)
-    snap.tune("tiers", a.tiers)
-    snap.tune("wide", a.wide)
-    snap.tune("back", a.back)
-    snap.tune("stream", a.stream)
-    snap.tune("stream_ecap", a.stream_ecap)
-    if a.resolve_unheld != 1:
-        snap.tune("resolve_unheld", a.resolve_unheld)
-    snap.tune("device_sync", a.device_sync)
-    snap.tune("stream_steal", a.stream_steal)
-    if a.stream_chunk != 64:
-        snap.tune("stream_chunk", a.stream_chunk)
-    snap.tune("grid_wgs", a.grid_wgs)
-    snap.tune("stream_wgs", a.stream_wgs)
-    snap.tune("back_wgs", a.back_wgs)
-    snap.tune("grid_reserve", 1)  # a server pays this once at start-up, not inside some request's batch
-    if snap.program is not None and not snap.program.empty:
-        snap.tune("interp_wgs", a.interp_wgs)
+    snap, size_param = build_synthetic(a, a.tuples, device=local, doc_alpha=alpha, group_alpha=alpha)
+    apply_tune(snap, a)
     info = snap.info()
     t_build = time.time() - t_build
     free_after_build = torch.cuda.mem_get_info(local)[0]
@@ -625,14 +751,50 @@ def main():
     res = timed_out.cpu().numpy()
     errs = torch.cat(derrs).cpu().numpy()
     assert (errs == 0).all() and (res <= 1).all(), "unexpected errors in the synthetic batch"
-    lat = [x for x, st in zip(lat, stats) if st is not None]  # submit-to-done: batches waited for only
     stats = [x for x in stats if x is not None]
     elapsed, edges = aggregate(dist, elapsed, float(sum(s.edges_read for s in stats)) * a.steps / len(stats),
                                f"cuda:{local}")
     l_bytes = np.array([8 * s.light_rows_opened + 4 * s.light_edges_read + 16 * s.light_probes for s in stats], float)
+    l_reqs = np.array([s.light_rows_opened + s.light_probes for s in stats], float)
     l_ms = np.array([s.light_ms for s in stats], float)
     achieved = float(l_bytes.mean() / (l_ms.mean() * 1e-3) / 1e9)
+    req_rate = float(l_reqs.mean() / (l_ms.mean() * 1e-3))
     traffic = pmc_traffic(STREAM_KERNELS[a.stream], int(a.tuples), B, a.preset, P)
+
+    # ---- latency phase (outside the timed region): the same P batches in flight, every batch waited for
+    # (submit -> results on the host side of the stream), distinct query batches
+    lat_n = max(0, a.latency_batches)
+    lat_ms = []
+    if lat_n:
+        n_ld = min(lat_n, 64)
+        dq_lat = torch.empty((n_ld, B, 7), dtype=torch.int32, device=dev)
+        for k in range(n_ld):
+            _lib.check(L.kg_synth_queries(snap.handle, 500000 + rank + 7919 * k, B, dq_lat[k].data_ptr()),
+                       "kg_synth_queries")
+        lat = [0.0] * lat_n
+        errors = []
+
+        def lat_worker(p):
+            try:
+                st = _lib.kg_stats()
+                for k in range(p, lat_n, P):
+                    s0 = time.perf_counter()
+                    _lib.check(L.kg_check_batch_device(snap.handle, dq_lat[k % n_ld].data_ptr(), B, a.global_depth,
+                                                       douts[p].data_ptr(), derrs[p].data_ptr(), C.byref(st),
+                                                       C.c_void_p(streams[p].cuda_stream)), "kg_check_batch_device")
+                    lat[k] = time.perf_counter() - s0  # a batch with stats returns once its results are in
+            except Exception as e:  # noqa: BLE001
+                errors.append(e)
+
+        th = [threading.Thread(target=lat_worker, args=(p,)) for p in range(P)]
+        [t.start() for t in th]
+        [t.join() for t in th]
+        if errors:
+            raise errors[0]
+        lat_ms = np.array(lat) * 1e3
+        del dq_lat
+    # ---- host path: the same engine through kg_check_batch (host buffers, H2D + tiers + D2H)
+    host = host_path(L, snap, dq_all, n_distinct, a, P) if a.host_calls > 0 else None
 
     value = world * B * a.steps / elapsed
     out = {
@@ -648,18 +810,19 @@ def main():
         "vs_baseline": None,
         "dtype": "u32",
         "data": "synthetic (device-generated Drive-like tuple graph, seed %d)" % a.seed,
-        "config": {"workload": "%s generator @ %.3g tuples, %d checks/step/GPU, max_read_depth %d"
-                               % ("C2/C4" if a.preset == 0 else "C3 (OPL view/edit/share)", a.tuples, B,
-                                  a.global_depth),
-                   "tuples": info["rows"], "nodes": info["nodes"], "set_edges": info["set_edges"],
+        "config": {"workload": "%s generator @ %.4g tuples (rows), %d checks/step/GPU, max_read_depth %d"
+                               % ("C2/C4" if a.preset == 0 else "C3 (OPL view/edit/share)", info["rows"], B,
+                                  a.global_depth) + (", out-degree law P(k)~k^-1.5" if a.heavy_tail else ""),
+                   "tuples": info["rows"], "tuples_target": a.tuples, "generator_size_param": size_param,
+                   "nodes": info["nodes"], "set_edges": info["set_edges"],
                    "batch_per_gpu": B, "global_max_read_depth": a.global_depth, "parallelism": f"replica{world}",
                    "inflight_per_gpu": P, "device_gb": info["device_bytes"] / 1e9,
                    "hbm_free_gb_after_build": free_after_build / 1e9,
-                   "materialized": snap.materialized()},
+                   "materialized": snap.materialized(), "tune": dict(snap.__dict__.get("tuned", {}))},
         "gteps": edges / elapsed / 1e9,
-        "p99_batch_ms": float(np.percentile(np.array(lat) * 1e3, 99)),
-        "batch_ms": {q: float(np.percentile(np.array(lat) * 1e3, v)) for q, v in
-                     (("p50", 50), ("p90", 90), ("p99", 99), ("max", 100))},
+        "p99_batch_ms": float(np.percentile(lat_ms, 99)) if lat_n else None,
+        "batch_ms": ({"batches": lat_n, "inflight": P, **{q: float(np.percentile(lat_ms, v)) for q, v in
+                     (("p50", 50), ("p90", 90), ("p99", 99), ("max", 100))}} if lat_n else None),
         "edges_per_batch": {q: float(np.percentile([x.edges_read for x in stats], v)) for q, v in
                             (("p50", 50), ("p90", 90), ("max", 100))},
         "allowed_fraction": float(res.mean()),
@@ -676,14 +839,129 @@ def main():
         "roofline": {"kernel": STREAM_KERNELS[a.stream], "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "bytes_model": "8*rows_opened + 4*edges_read + 16*direct_probes (per k_stream launch; R/E/P counted in-kernel)",
-                     "launch_ms": float(l_ms.mean()), "bytes_per_launch": float(l_bytes.mean())},
+                     "launch_ms": float(l_ms.mean()), "bytes_per_launch": float(l_bytes.mean()),
+                     # the random-request view: one row open and one dset probe are one random line each;
+                     # ceiling = independent random 16-B loads/s measured by tools/randprobe.hip on MI355X
+                     "requests_per_launch": float(l_reqs.mean()), "request_rate": req_rate,
+                     "request_peak": RAND_REQ_PEAK, "request_frac": req_rate / RAND_REQ_PEAK},
+        "host_path": host,
     }
-    if rank == 0 and world == 1 and a.cpu_seconds > 0:
-        out["cpu_baseline"] = cpu_baseline(snap, dq, a)
     if rank == 0:
+        orc = None
+        if a.parity > 0 or (world == 1 and a.cpu_seconds > 0):
+            cpus = effective_cpus()
+            orc = CheckOracle(snap, a, cpus["effective"])
+            q0 = dq.cpu().numpy().view(np.uint32)
+        if a.parity > 0:
+            out["parity"] = orc.parity(q0, res[0], a.parity, a.parity_canonical)
+        if world == 1 and a.cpu_seconds > 0:
+            out["cpu_baseline"] = cpu_baseline(orc, q0, a, cpus)
         print(json.dumps(out), flush=True)
+        if a.parity > 0 and out["parity"]["mismatches"] + out["parity"]["canonical_mismatches"]:
+            sys.stderr.write("PARITY FAILURE: GPU answers differ from the oracle\n")
+            if dist:
+                dist.destroy_process_group()
+            sys.exit(1)
     if dist:
         dist.destroy_process_group()
+
+
+def host_path(L, snap, dq_all, n_distinct, a, P) -> dict:
+    """kg_check_batch (what the cgo binding calls) over 1 M-check HOST batches from P
+    threads: H2D of the queries, the tier chain, D2H of results and error codes, all inside the call."""
+    from keto_amd import _lib
+    B = a.batch
+    qs = [np.ascontiguousarray(dq_all[p % n_distinct].cpu().numpy().view(np.uint32)) for p in range(P)]
+    lat, errors = [], []
+    ready = threading.Barrier(P + 1)
+
+    def worker(p):
+        try:
+            o = np.empty(B, np.uint8)
+            e = np.empty(B, np.uint32)
+
+            def call():
+                _lib.check(L.kg_check_batch(snap.handle, qs[p].ctypes.data_as(C.c_void_p), B, a.global_depth,
+                                            o.ctypes.data_as(C.c_void_p), e.ctypes.data_as(C.c_void_p), None),
+                           "kg_check_batch")
+            call()  # this thread's lane (stream, pinned staging, workspace) exists before timing
+            ready.wait()
+            for _ in range(a.host_calls):
+                s0 = time.perf_counter()
+                call()
+                lat.append(time.perf_counter() - s0)
+        except Exception as x:  # noqa: BLE001
+            errors.append(x)
+            ready.abort()
+
+    th = [threading.Thread(target=worker, args=(p,)) for p in range(P)]
+    [t.start() for t in th]
+    ready.wait()
+    t0 = time.perf_counter()
+    [t.join() for t in th]
+    el = time.perf_counter() - t0
+    if errors:
+        raise errors[0]
+    ms = np.array(lat) * 1e3
+    return {"value": B * a.host_calls * P / el, "unit": "checks/s", "callers": P, "calls": len(lat),
+            "checks_per_call": B, "p50_call_ms": float(np.percentile(ms, 50)),
+            "p99_call_ms": float(np.percentile(ms, 99)),
+            "what": "kg_check_batch on 1 M-check host batches: PCIe both ways included (not the headline value)"}
+
+
+class CheckOracle:
+    """The C restatement of the reference engine (oracle/keto_oracle.c) over the snapshot's own rows
+    (kg_snapshot_export_csr, shard order), as the parity checker and the CPU baseline.  Preset 0 queries
+    doc#viewer roots by node id (synthetic docs: node id == object id); preset 1 resolves (ns, obj, rel)
+    through the oracle's own node map and evaluates the OPL program."""
+
+    def __init__(self, snap, a, nthreads: int):
+        from keto_amd import _lib
+        from oracle.oracle import Oracle
+        L = _lib.load()
+        info = snap.info()
+        nn, nr = info["nodes"], info["rows"]
+        row_off = np.zeros(nn + 1, np.uint64)
+        row_subj = np.zeros(nr, np.uint32)
+        nd = [np.zeros(nn, np.uint32) for _ in range(3)]
+        p = lambda x: x.ctypes.data_as(C.c_void_p)
+        _lib.check(L.kg_snapshot_export_csr(snap.handle, p(row_off), p(row_subj), p(nd[0]), p(nd[1]), p(nd[2])),
+                   "kg_snapshot_export_csr")
+        self.by_node = a.preset == 0
+        t = time.perf_counter()
+        self.o = Oracle.from_csr(0, nd[0], nd[1], nd[2], row_off, row_subj, with_node_map=not self.by_node,
+                                 nthreads=min(nthreads, 64))
+        if not self.by_node:
+            self.o.set_program(snap.program)
+        self.build_s = time.perf_counter() - t
+        self.a = a
+        self.nthreads = nthreads
+        self.ids = snap.synth_ids()
+
+    def run(self, q: np.ndarray, policy: int, nthreads: int) -> np.ndarray:
+        dep = q[:, 6].view(np.int32)
+        if self.by_node:
+            assert (q[:, 3] == 0xFFFFFFFF).all() and (q[:, 1] < self.ids["n_docs"]).all(), "preset-0 batch shape"
+            return self.o.check_nodes_batch(q[:, 1].copy(), q[:, 4].copy(), dep.copy(), self.a.global_depth, policy,
+                                            nthreads)[0]
+        return self.o.check_batch(q[:, :6], dep, self.a.global_depth, policy, nthreads)[0]
+
+    def parity(self, q: np.ndarray, gpu: np.ndarray, n: int, n_canon: int) -> dict:
+        """GPU answers of one timed batch vs the oracle: the Go-order DFS schedule on the first n checks
+        and the schedule-free canonical policy on the first n_canon of them."""
+        from oracle.oracle import POLICY_CANONICAL, POLICY_DFS
+        n = min(n, len(q))
+        t = time.perf_counter()
+        dfs = self.run(q[:n], POLICY_DFS, self.nthreads)
+        nc = min(n_canon, n)
+        can = self.run(q[:nc], POLICY_CANONICAL, self.nthreads) if nc else np.zeros(0, np.uint8)
+        bad = np.nonzero(dfs != gpu[:n])[0]
+        return {"checks": int(n), "mismatches": int(bad.size), "canonical_checks": int(nc),
+                "canonical_mismatches": int((can != gpu[:nc]).sum()),
+                "schedule_variant": int((dfs[:nc] != can).sum()), "allowed": int((dfs == 1).sum()),
+                "errors": int((dfs == 2).sum()), "first_mismatches": [int(i) for i in bad[:8]],
+                "batch": "first timed batch (timed_out[0])", "oracle": "oracle/keto_oracle.c",
+                "oracle_build_s": self.build_s, "seconds": time.perf_counter() - t}
 
 
 def stream_diag(s) -> dict:
@@ -711,62 +989,44 @@ def pmc_traffic(kernel: str, tuples: int, batch: int, preset: int, inflight: int
     return None
 
 
-def cpu_baseline(snap, dq, a) -> dict:
-    """The C restatement of the reference engine (oracle, sequential Go DFS schedule with visited
-    sets) over the same row index, on a bounded sample of the same batch."""
-    from keto_amd import _lib
-    from oracle.oracle import POLICY_DFS, Oracle
-    L = _lib.load()
-    info = snap.info()
-    nn, nr = info["nodes"], info["rows"]
-    row_off = np.zeros(nn + 1, np.uint64)
-    row_subj = np.zeros(nr, np.uint32)
-    nd = [np.zeros(nn, np.uint32) for _ in range(3)]
-    p = lambda x: x.ctypes.data_as(C.c_void_p)
-    _lib.check(L.kg_snapshot_export_csr(snap.handle, p(row_off), p(row_subj), p(nd[0]), p(nd[1]), p(nd[2])),
-               "kg_snapshot_export_csr")
-    ncpu = os.cpu_count() or 1
-    try:
-        n_aff = len(os.sched_getaffinity(0))
-    except (AttributeError, OSError):
-        n_aff = ncpu
-    threads = a.cpu_threads if a.cpu_threads > 0 else ncpu
-    o = Oracle.from_csr(0, nd[0], nd[1], nd[2], row_off, row_subj, nthreads=min(threads, 64))
-    del row_subj
-    q = dq.cpu().numpy().view(np.uint32)
-    node = q[:, 1].copy()  # synthetic docs: node id == object id
-    subj = q[:, 4].copy()
-    dep = q[:, 6].view(np.int32).copy()
+def cpu_baseline(orc: "CheckOracle", q: np.ndarray, a, cpus: dict) -> dict:
+    """The C restatement of the reference engine (oracle, sequential Go-order DFS with visited sets)
+    over the same rows, on a bounded sample of the same batch, timed at the CPUs this process can
+    actually use (affinity mask capped by the cgroup quota), at 1 thread and at nproc; `value` is the
+    best of them, every count is kept in `by_threads`."""
+    from oracle.oracle import POLICY_DFS
+    eff = cpus["effective"]
 
     def run(n, th, passes=1):
         t = time.perf_counter()
         for _ in range(passes):
-            o.check_nodes_batch(node[:n], subj[:n], dep[:n], a.global_depth, POLICY_DFS, th)
+            orc.run(q[:n], POLICY_DFS, th)
         return time.perf_counter() - t
 
     res = {}
-    # T = nproc (SURVEY.md 8d), the threads this process may run on, 16 and 1 -- each on its own budget
-    plan = [(threads, a.cpu_seconds)]
-    for th in (n_aff, 16, 1):
+    plan = [(eff, a.cpu_seconds / 2)]
+    for th in (1, cpus["nproc"]):
         if th not in [p[0] for p in plan]:
-            plan.append((th, a.cpu_seconds / 3))
+            plan.append((th, a.cpu_seconds / 4))
     for th, budget in plan:
         n, passes = 256, 1
         t = run(n, th)
-        while t < budget / 4 and n < len(node):  # grow the sample of distinct checks first
-            n = min(len(node), n * 4)
+        while t < budget / 4 and n < len(q):  # grow the sample of distinct checks first
+            n = min(len(q), n * 4)
             t = run(n, th)
         if t < budget / 2:  # then repeat it to reach ~budget seconds of CPU work
             passes = max(1, int(budget / max(t, 1e-6)))
             t = run(n, th, passes)
         res[th] = (n * passes / t, n, passes, t)
-    v, n, passes, t = res[threads]
-    return {"value": v, "unit": "checks/s", "cores": threads, "kind": "port",
+    best = max(res, key=lambda k: res[k][0])
+    v, n, passes, t = res[best]
+    return {"value": v, "unit": "checks/s", "cores": best, "kind": "port",
             "sample": f"{passes} pass(es) over the first {n} checks of the rank-0 batch on the same graph "
                       f"({t:.1f} s), sequential Go-order DFS with visited sets (oracle/keto_oracle.c POLICY_DFS), "
-                      f"{threads} host threads (os.cpu_count())",
-            "by_threads": {str(k): v[0] for k, v in res.items()}, "affinity_cpus": n_aff,
-            "value_1thread": res[1][0], "host_cpu": host_cpu()}
+                      f"{best} host threads (best of {sorted(res)}; {eff} CPUs usable: affinity "
+                      f"{cpus['affinity']}, cgroup quota {cpus['cgroup_quota']})",
+            "by_threads": {str(k): r[0] for k, r in sorted(res.items())}, "effective_cpus": eff,
+            "cpus": cpus, "value_1thread": res[1][0], "host_cpu": host_cpu()}
 
 
 def host_cpu() -> str:

@@ -226,15 +226,17 @@ int kg_snapshot_materialized(const kg_snapshot* s, uint64_t* out3);
  * key "stream_steal" (1..8): XCD ranges of the work list a k_stream2 wave dequeues from (default 4:
  * when the list drains every wave walks them, one atomic each on a few hot words).
  * key "stream_chunk" (1..64): queries a k_stream2 wave dequeues at once (default 64).
- * key "stream_wgs": k_stream workgroups per CU (0 = by variant); "back_wgs" (1..3) and "grid_wgs"
- * (1..64): k_back / k_grid_level workgroups per CU.  key "shard_vis": log2 of the
+ * key "stream_wgs": k_stream workgroups per CU (0 = by variant; default 3); "back_wgs" (1..3, default 2)
+ * and "grid_wgs" (1..64, default 4): k_back / k_grid_level workgroups per CU (defaults = bench.py's C2 set).  key "shard_vis": log2 of the
  * hash-sharded mode's per-batch (query, node) visited table (default 25).  key "interp_cap2"
  * (0..4194304): BFS list cap of the rewrite interpreter's many-slot HBM pass (0 = 256 Ki nodes);
  * queries that outgrow it rerun in the single full-size slot.  key "interp_wgs" (1..8): workgroups
  * of 4 query waves per CU in the interpreter's LDS pass (default 6).  key "grid_reserve": allocate
  * now the grid tier's shared full-size pool (used by a query that overflows a workspace's pool on
  * its own; otherwise allocated on first need).  key "grid_cap": log entries of a workspace's grid
- * pool (0 = 16 Mi; small values force the overflow paths in tests). */
+ * pool (0 = 16 Mi; small values force the overflow paths in tests).  key "max_lanes" (1..1024, default
+ * 32): lane sets (a stream, staging and workspace per replica) that concurrent kg_check_batch /
+ * kg_expand_batch calls check out of the snapshot's pool; at the cap a call waits for one to return. */
 int kg_snapshot_tune(kg_snapshot* s, const char* key, int64_t value);
 /* Synthetic layout: ids6 = {n_docs, n_groups, n_users, n_folders, user_obj0, folder_obj0}
  * (doc d = object d, group g = object n_docs+g, user u = object user_obj0+u). */

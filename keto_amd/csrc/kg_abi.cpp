@@ -441,6 +441,15 @@ static int tune_one(Snapshot* s, const char* key, int64_t value) {
     s->grid_small_cap = (uint64_t)value;
     return 0;
   }
+  if (strcmp(key, "max_lanes") == 0) {
+    if (value < 1 || value > 1024) return set_error(-2, "max_lanes in [1, 1024]");
+    {
+      std::lock_guard<std::mutex> lk(s->lane_mu);
+      s->lane_cap = (size_t)value;  // sets already created stay in the pool
+    }
+    s->lane_cv.notify_all();
+    return 0;
+  }
   if (strcmp(key, "back_wgs") == 0) {
     if (value < 1 || value > 3) return set_error(-2, "back_wgs must be in [1, 3]");
     s->back_wgs = (int)value;
@@ -531,6 +540,13 @@ int kg_check_batch_device(kg_snapshot* sp, const kg_query* d_q, size_t n, int32_
   KG_GUARD_END
 }
 
+// A checked-out lane set goes back to the snapshot's pool when the call returns (any path).
+struct LaneLease {
+  Snapshot* s;
+  std::vector<kg::Lane*>* v;
+  ~LaneLease() { s->lanes_release(v); }
+};
+
 // Host buffers in and out: the batch is split over the snapshot's replicas (one contiguous chunk
 // each, none smaller than MIN_PER_REPLICA queries), every chunk on this thread's lane of its
 // replica.  All chunks are staged and enqueued before the first wait, so the devices run
@@ -547,8 +563,9 @@ int kg_check_batch(kg_snapshot* sp, const kg_query* q, size_t n, int32_t global_
   if (stats) memset(stats, 0, sizeof *stats);
   if (n == 0) return 0;
   if (n > 0x7FFFFFFFull) return set_error(-2, "batch too large");
-  std::vector<kg::Lane*>* lanes = s->thread_lanes();
+  std::vector<kg::Lane*>* lanes = s->lanes_acquire();
   if (!lanes) return -1;
+  LaneLease lease{s, lanes};
   const size_t R = std::max<size_t>(1, std::min(lanes->size(), (n + MIN_PER_REPLICA - 1) / MIN_PER_REPLICA));
   // batches that use fewer replicas than exist rotate over them (a batcher's small batches spread
   // over every GPU instead of all landing on replica 0)
@@ -643,9 +660,10 @@ int kg_expand_batch(kg_snapshot* sp, const kg_set* roots, size_t n, int32_t glob
   if (n && !roots) return set_error(-2, "roots is NULL");
   Snapshot* s = reinterpret_cast<Snapshot*>(sp);
   if (s->shard_n > 1) return set_error(-2, "sharded snapshot: expand needs every row on one device");
-  // this thread's lanes: one stream + cached buffers per replica, so concurrent callers overlap
-  std::vector<kg::Lane*>* lanes = s->thread_lanes();
+  // a lane set from the pool: one stream + cached buffers per replica, so concurrent callers overlap
+  std::vector<kg::Lane*>* lanes = s->lanes_acquire();
   if (!lanes) return -1;
+  LaneLease lease{s, lanes};
   const size_t R = std::max<size_t>(1, std::min(s->n_replicas(), (n + MIN_PER_REPLICA - 1) / MIN_PER_REPLICA));
   const size_t r0 = R < lanes->size() ? (size_t)(s->rr_next.fetch_add(1, std::memory_order_relaxed) % lanes->size()) : 0;
   auto lane = [&](size_t i) { return (*lanes)[(r0 + i) % lanes->size()]; };

@@ -92,8 +92,17 @@ struct Batcher {
   std::mutex st_mu;
   LatRing batch_lat, call_lat;
   uint64_t batches = 0, checks = 0;
+  // callers inside kg_batcher_check: kg_batcher_destroy frees the batcher only once every caller it
+  // woke has left (a woken caller still records its latency and may loop for its next chunk)
+  std::atomic<int> callers{0};
 
   void run();
+};
+
+struct CallerGuard {
+  std::atomic<int>& c;
+  explicit CallerGuard(std::atomic<int>& x) : c(x) { c.fetch_add(1, std::memory_order_acq_rel); }
+  ~CallerGuard() { c.fetch_sub(1, std::memory_order_acq_rel); }
 };
 
 void Batcher::run() {
@@ -166,6 +175,7 @@ int kg_batcher_create(kg_snapshot* sp, int32_t global_max_depth, size_t max_batc
 int kg_batcher_check(kg_batcher* bp, const kg_query* q, size_t n, uint8_t* out, uint32_t* err_code) {
   if (!bp || (n && (!q || !out))) return set_error(-2, "NULL argument");
   Batcher* b = reinterpret_cast<Batcher*>(bp);
+  kg::CallerGuard guard(b->callers);  // destroy waits for it (the last thing this call touches is `b`)
   const auto t0 = kg::Clock::now();
   size_t done = 0;
   int rc = 0;
@@ -228,7 +238,10 @@ void kg_batcher_reset_stats(kg_batcher* bp) {
   b->batches = b->checks = 0;
 }
 
-// Stops accepting queries, answers what is pending, joins the dispatchers and frees the batcher.
+// Stops accepting queries, answers what is pending, joins the dispatchers, waits for every caller
+// still inside kg_batcher_check to leave (callers blocked at the time get their answers, or an error
+// for chunks not yet queued), then frees the batcher.  A call that STARTS after destroy returned is
+// a use of a freed handle (as with any destroy).
 void kg_batcher_destroy(kg_batcher* bp) {
   if (!bp) return;
   Batcher* b = reinterpret_cast<Batcher*>(bp);
@@ -238,6 +251,7 @@ void kg_batcher_destroy(kg_batcher* bp) {
   }
   b->cv.notify_all();
   for (auto& t : b->th) t.join();
+  while (b->callers.load(std::memory_order_acquire) != 0) std::this_thread::sleep_for(std::chrono::microseconds(50));
   delete b;
 }
 

@@ -831,7 +831,9 @@ __global__ __launch_bounds__(256) void k_stream2(DevSnap s, const RQuery* __rest
   __shared__ Lds lds_all[4];
   Lds& L = lds_all[threadIdx.x >> 6];
   const int lane = lane_id();
-  const uint32_t head0 = blockIdx.x & 7;  // XCD label (speed only, never correctness)
+  // XCD label: the first range this wave drains.  With ranges < 8 (stream_steal) correctness needs
+  // every label in the grid (the launch keeps grid >= 8), else some range is never drained.
+  const uint32_t head0 = blockIdx.x & 7;
   uint32_t head_sel = head0;
   for (uint32_t i = lane; i < VT; i += 64) L.vt[i] = 0ull;
   if (lane < 32) {
@@ -1938,7 +1940,10 @@ int check_batch_begin(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n, 
       const uint32_t per_cu =
           s->stream_wgs ? (uint32_t)s->stream_wgs : ((sv == 0 || sv == 1 || sv == 3 || sv >= 9) ? 5u : 3u);
       const uint32_t ecap = s->stream_ecap ? s->stream_ecap : 0xFFFFFFFFu;
-      const uint32_t grid = (uint32_t)std::min<uint64_t>((uint64_t)s->n_cu * per_cu, (n + 31) / 32 + 8);
+      // >= 8 workgroups: with stream_steal < 8 a wave drains only `ranges` of the 8 per-XCD ranges
+      // starting at its label blockIdx & 7, so every label must occur for every range to be drained
+      const uint32_t grid =
+          std::max<uint32_t>(8u, (uint32_t)std::min<uint64_t>((uint64_t)s->n_cu * per_cu, (n + 31) / 32 + 8));
       using V0 = SlotVis<8, 7>;
       using V1 = SlotVis<16, 6>;
       using V2 = SlotVis<16, 7>;

@@ -47,10 +47,16 @@ __device__ __forceinline__ uint32_t lower_node(const uint32_t* a, uint32_t n, ui
   return lo;
 }
 
+// A node's deletes del_subj[db, de) are sorted by subject: binary search (a delete_all of a hub's
+// rows can leave thousands on one node, and every old entry of its row asks)
 __device__ __forceinline__ bool is_deleted(const DeltaDev& D, uint32_t db, uint32_t de, uint32_t subj) {
-  for (uint32_t k = db; k < de; k++)  // a node's deletes: a handful
-    if (D.del_subj[k] == subj) return true;
-  return false;
+  uint32_t lo = db, hi = de;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (D.del_subj[mid] < subj) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo < de && D.del_subj[lo] == subj;
 }
 
 // Everything below is edge-parallel: a node-per-thread loop over its row leaves the whole kernel
@@ -204,6 +210,9 @@ int Snapshot::create_from_delta(Snapshot* base, const kg_tuple* ins, const uint6
   ds.wildcard_rel = wildcard_rel;
   // 1. the node map: taken over from the base (built once by kg_snapshot_create), or rebuilt from
   // the base's node triples when the base has none (synthetic, or already handed on)
+  // base->mu guards the hand-over: two applies on one base (or an apply racing another host-side user
+  // of these fields) take turns; the loser rebuilds the map from the device triples below
+  std::unique_lock<std::mutex> base_lk(base->mu);
   if (!base->hmap.k.empty() && base->h_nd_ns.size() == n0) {
     hmap = std::move(base->hmap);
     h_nd_ns = std::move(base->h_nd_ns);
@@ -222,6 +231,7 @@ int Snapshot::create_from_delta(Snapshot* base, const kg_tuple* ins, const uint6
     hmap.init((uint64_t)n0 + n_ins + 16);
     for (uint32_t v = 0; v < n0; v++) hmap.put(nmap_key(h_nd_ns[v], h_nd_rel[v], h_nd_obj[v]), v);
   }
+  base_lk.unlock();  // everything else read from the base is immutable device data
   auto intern = [&](uint32_t ns, uint32_t obj, uint32_t rel) -> uint32_t {
     const uint32_t id = (uint32_t)h_nd_ns.size();
     const uint32_t got = hmap.put(nmap_key(ns, rel, obj), id);

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <condition_variable>
 #include <list>
 #include <mutex>
 #include <thread>
@@ -134,9 +135,11 @@ struct HostMap {
 };
 
 struct Snapshot;
-// Host-buffer batches (kg_check_batch): per calling thread, one lane per replica -- its own HIP
-// stream (hence its own batch workspace), pinned staging for queries and results, and device
-// buffers, all grown on demand and reused by every later call of that thread.
+// Host-buffer batches (kg_check_batch, kg_expand_batch): a call checks out one lane set (one lane per
+// replica -- its own HIP stream, hence its own batch workspace, pinned staging for queries and
+// results, and device buffers, all grown on demand) from the snapshot's bounded pool and returns it
+// when done, so thread churn (a Go server's cgo calls each pin an OS thread) never grows streams or
+// HBM past the pool's cap; at the cap a call waits for a set to come back.
 struct Lane {
   Snapshot* rep = nullptr;
   int device = -1;
@@ -215,13 +218,13 @@ struct Snapshot {
   int resolve_unheld = 1;  // kg_snapshot_tune("resolve_unheld"): k_resolve reads the holder bit before the node map
   uint32_t stream_steal = 4;   // kg_snapshot_tune("stream_steal"): XCD ranges a k_stream2 wave dequeues from (1..8)
   uint32_t stream_chunk = 64;  // kg_snapshot_tune("stream_chunk"): k_stream2 queries per dequeue (1..64)
-  int grid_wgs = 16;         // kg_snapshot_tune("grid_wgs"): k_grid_level workgroups per CU
+  int grid_wgs = 4;          // kg_snapshot_tune("grid_wgs"): k_grid_level workgroups per CU (bench default)
   int device_sync = 1;      // kg_snapshot_tune("device_sync"): kg_check_batch_device waits asleep (1) or spinning (0)
   int host_sync = 1;        // kg_snapshot_tune("host_sync"): kg_check_batch waits asleep (1) or spinning (0)
-  int stream_wgs = 0;        // kg_snapshot_tune("stream_wgs"): k_stream workgroups per CU (0 = by LDS)
+  int stream_wgs = 3;        // kg_snapshot_tune("stream_wgs"): k_stream workgroups per CU (0 = by LDS; 3 = bench default)
   int interp_wgs = 6;        // kg_snapshot_tune("interp_wgs"): k_interp_lds workgroups (4 waves) per CU (6 fit the LDS)
   uint32_t interp_cap2 = 0;  // kg_snapshot_tune("interp_cap2"): pass-2 BFS list cap of the rewrite path (0 = 256 Ki)
-  int back_wgs = 3;          // kg_snapshot_tune("back_wgs"): k_back workgroups per CU (1..3, LDS allows 3)
+  int back_wgs = 2;          // kg_snapshot_tune("back_wgs"): k_back workgroups per CU (1..3, LDS allows 3; 2 = bench C2 default)
   uint64_t grid_small_cap = 0;  // kg_snapshot_tune("grid_cap"): workspace grid-log entries (0 = 16 Mi; tests)
   // replicas: the same snapshot on more devices (kg_snapshot_create's device mask); this object is
   // replica 0 and owns the others.  Host-buffer batches and expands are split over all of them.
@@ -229,8 +232,12 @@ struct Snapshot {
   Snapshot* replica(size_t i) { return i == 0 ? this : peers[i - 1]; }
   size_t n_replicas() const { return 1 + peers.size(); }
   std::mutex lane_mu;
-  std::list<std::pair<std::thread::id, std::vector<Lane*>>> lanes;  // list: stable addresses
-  std::vector<Lane*>* thread_lanes();  // this thread's lanes (one per replica), created on first use
+  std::condition_variable lane_cv;
+  std::list<std::vector<Lane*>> lane_sets;     // every set created (list: stable addresses)
+  std::vector<std::vector<Lane*>*> lane_free;  // sets not checked out (LIFO: the warmest first)
+  size_t lane_cap = 32;                        // kg_snapshot_tune("max_lanes"): concurrent host-buffer calls
+  std::vector<Lane*>* lanes_acquire();         // a free lane set (created up to lane_cap; waits at the cap)
+  void lanes_release(std::vector<Lane*>* v);
   std::atomic<uint64_t> rr_next{0};      // replica rotation of batches smaller than one chunk per replica
   // The grid tier's full-size pool (a log that holds every node): shared by the workspaces, used
   // one query at a time by a round whose single query overflowed its workspace's pool.

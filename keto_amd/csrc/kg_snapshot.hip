@@ -234,8 +234,8 @@ static uint64_t pow2_at_least(uint64_t x) {
 }
 
 Snapshot::~Snapshot() {
-  for (auto& tl : lanes)
-    for (Lane* l : tl.second) delete l;  // before the workspaces: a lane's stream owns one of them
+  for (auto& set : lane_sets)
+    for (Lane* l : set) delete l;  // before the workspaces: a lane's stream owns one of them
   for (Snapshot* p : peers) delete p;
   if (device >= 0) hipSetDevice(device);
   for (auto& a : allocs) hipFree(a.first);
@@ -327,11 +327,14 @@ int Lane::reserve(size_t n) {
   return 0;
 }
 
-std::vector<Lane*>* Snapshot::thread_lanes() {
-  const std::thread::id me = std::this_thread::get_id();
-  std::lock_guard<std::mutex> lk(lane_mu);
-  for (auto& tl : lanes)
-    if (tl.first == me) return &tl.second;
+std::vector<Lane*>* Snapshot::lanes_acquire() {
+  std::unique_lock<std::mutex> lk(lane_mu);
+  lane_cv.wait(lk, [&] { return !lane_free.empty() || lane_sets.size() < lane_cap; });
+  if (!lane_free.empty()) {
+    std::vector<Lane*>* v = lane_free.back();
+    lane_free.pop_back();
+    return v;
+  }
   std::vector<Lane*> v;
   for (size_t i = 0; i < n_replicas(); i++) {
     Snapshot* r = replica(i);
@@ -347,8 +350,16 @@ std::vector<Lane*>* Snapshot::thread_lanes() {
     l->w = r->workspace(l->stream);
     v.push_back(l);
   }
-  lanes.emplace_back(me, std::move(v));
-  return &lanes.back().second;
+  lane_sets.emplace_back(std::move(v));
+  return &lane_sets.back();
+}
+
+void Snapshot::lanes_release(std::vector<Lane*>* v) {
+  {
+    std::lock_guard<std::mutex> lk(lane_mu);
+    lane_free.push_back(v);
+  }
+  lane_cv.notify_one();
 }
 
 Workspace* Snapshot::workspace(hipStream_t st) {

@@ -595,3 +595,16 @@ int64_t ko_expand(const ko_index* ix, uint32_t sns, uint32_t sobj, uint32_t srel
   if (!ok) return 0;
   return t.overflow ? -t.n : t.n;
 }
+
+/* ko_expand with the root given as a node id (an index built without a node map, e.g. the synthetic
+ * graphs' group#member roots, whose node id equals their object id). */
+int64_t ko_expand_node(const ko_index* ix, uint32_t node, int rest_depth, int global, int32_t* buf,
+                       int64_t cap_records) {
+  if (!ix->finalized || node >= ix->n_nodes) return -1;
+  tbuf t = {buf, cap_records * 6, 0, 0};
+  tmap visited; tmap_init(&visited, 64);
+  int ok = build_tree(ix, SET_BIT | node, rest_depth, global, &visited, &t);
+  tmap_free(&visited);
+  if (!ok) return 0;
+  return t.overflow ? -t.n : t.n;
+}

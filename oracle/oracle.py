@@ -54,6 +54,8 @@ def lib():
         L.ko_check_nodes_batch.argtypes = [vp, vp, vp, vp, u64, C.c_int, C.c_int, C.c_int, vp, vp]
         L.ko_expand.restype = i64
         L.ko_expand.argtypes = [vp, u32, u32, u32, C.c_int, C.c_int, vp, i64]
+        L.ko_expand_node.restype = i64
+        L.ko_expand_node.argtypes = [vp, u32, C.c_int, C.c_int, vp, i64]
         _lib = L
     return _lib
 
@@ -148,6 +150,18 @@ class Oracle:
         while True:
             buf = np.zeros((cap, 6), np.int32)
             n = lib().ko_expand(self.h, sns, sobj, srel, int(max_depth), int(global_max), _p(buf), cap)
+            if n >= 0:
+                return buf[:n] if n > 0 else None
+            cap = -n + 16
+
+    def expand_node(self, node: int, max_depth: int, global_max: int) -> Optional[np.ndarray]:
+        """expand of the subject set whose node id is `node` (no node map needed)."""
+        if not 0 <= int(node) < self.n_nodes:
+            raise ValueError(f"node {node} out of range")
+        cap = 1024
+        while True:
+            buf = np.zeros((cap, 6), np.int32)
+            n = lib().ko_expand_node(self.h, int(node), int(max_depth), int(global_max), _p(buf), cap)
             if n >= 0:
                 return buf[:n] if n > 0 else None
             cap = -n + 16

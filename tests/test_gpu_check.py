@@ -554,3 +554,59 @@ def test_opl_full_example_rewrites_vs_oracle():
                                for i in bad[:8]]
         assert e.last_stats["n_general"] > 0
         assert 0 < (exp == 1).sum() and (exp == 0).sum() > 0
+
+
+@pytest.mark.parametrize("preset,n_tuples", [(0, 2_000_000), (1, 600_000)])
+def test_bench_tune_set_vs_oracle(preset, n_tuples):
+    """The exact engine configuration bench.py times (bench.apply_tune with bench.py's default
+    arguments: stream variant, edge budget, stream_steal, back_wgs, stream_wgs, grid_wgs, grid_reserve,
+    device_sync), with the bench's batches in flight on their own streams through
+    kg_check_batch_device: every answer of every batch equals the oracle (Go-order DFS and canonical)."""
+    import ctypes as C
+    import threading
+    import bench
+    torch = _torch()
+    from keto_amd import _lib
+    L = _lib.load()
+    a = bench.parse(["--preset", str(preset)])
+    snap = Snapshot.synthetic(n_tuples, seed=20250131, preset=preset)
+    bench.apply_tune(snap, a)
+    assert snap.tuned["back_wgs"] == (1 if preset else 2) and snap.tuned["stream_steal"] == 4
+    P, n, gmax = a.inflight, 50_000, a.global_depth
+    streams = [torch.cuda.Stream() for _ in range(P)]
+    dqs = []
+    for p in range(2 * P):
+        q = torch.empty((n, 7), dtype=torch.int32, device="cuda")
+        _lib.check(L.kg_synth_queries(snap.handle, 300 + p, n, q.data_ptr()), "kg_synth_queries")
+        dqs.append(q)
+    outs = [torch.full((n,), 7, dtype=torch.uint8, device="cuda") for _ in range(2 * P)]
+    errs = [torch.full((n,), 99, dtype=torch.int32, device="cuda") for _ in range(2 * P)]
+    torch.cuda.synchronize()
+    failures = []
+
+    def worker(p):
+        try:
+            for k in (p, p + P):
+                st = _lib.kg_stats()
+                _lib.check(L.kg_check_batch_device(snap.handle, dqs[k].data_ptr(), n, gmax, outs[k].data_ptr(),
+                                                   errs[k].data_ptr(), C.byref(st) if k == p else None,
+                                                   C.c_void_p(streams[p].cuda_stream)), "kg_check_batch_device")
+            streams[p].synchronize()
+        except Exception as x:  # noqa: BLE001
+            failures.append(x)
+
+    th = [threading.Thread(target=worker, args=(p,)) for p in range(P)]
+    [t.start() for t in th]
+    [t.join() for t in th]
+    assert not failures, failures
+    oracle = Oracle(snap.export(), 0, snap.program if preset else None)
+    for k in range(2 * P):
+        q = dqs[k].cpu().numpy().view(np.uint32)
+        out, err = outs[k].cpu().numpy(), errs[k].cpu().numpy()
+        exp, oerr, _ = oracle.check_batch(q[:, :6], q[:, 6].view(np.int32), gmax, POLICY_CANONICAL, nthreads=8)
+        bad = np.nonzero((out != exp) | (err.astype(np.int64) != oerr))[0]
+        assert bad.size == 0, (k, bad[:10])
+        if k < 2:
+            dfs, _, _ = oracle.check_batch(q[:, :6], q[:, 6].view(np.int32), gmax, POLICY_DFS, nthreads=8)
+            assert (dfs == exp).all()
+        assert 0.05 < (out == 1).mean() < 0.95

@@ -3,6 +3,7 @@ committed write) and the request batcher (concurrent callers coalesced into kg_c
 calls), both against the CPU oracle on the persister's rows in shard order.  Bit-exact."""
 import ctypes as C
 import threading
+import time
 
 import numpy as np
 import pytest
@@ -150,6 +151,77 @@ def test_native_batcher_many_callers_vs_oracle():
         nb2.L.kg_batcher_destroy(nb2._h)  # closed under the Python object: the next call must fail cleanly
         nb2._h = C.c_void_p()
         nb2.check_ids(q7[:1])
+
+
+def _batcher_graph(seed=19):
+    from keto_amd.engine import Registry
+    rng = np.random.default_rng(seed)
+    it, tuples, nss, rels = random_graph(rng, n_obj=80, n_rows=900)
+    reg = Registry(tuples, [], max_read_depth=5, interner=it)
+    qs = random_queries(rng, nss, rels, 2000, n_obj=80)
+    q6 = np.asarray([it.tuple_ids(t) for t in qs], np.uint32)
+    depths = rng.integers(0, 7, len(qs))
+    exp, _, _ = Oracle(it.tuples_array(tuples), it.wildcard_rel).check_batch(q6, depths, 5, POLICY_CANONICAL)
+    return reg, queries_array(q6, depths), exp
+
+
+def test_native_batcher_destroy_with_blocked_callers():
+    """kg_batcher_destroy while 16 callers are blocked in kg_batcher_check (a batch that would only
+    close after 5 s): destroy answers the pending batch, waits until every woken caller has left the
+    call, and only then frees the batcher (the callers used to touch it after the free)."""
+    reg, q7, exp = _batcher_graph()
+    nb = NativeBatcher(reg.snapshot, 5, max_batch=1 << 20, max_wait_us=5_000_000, dispatchers=2)
+    got = np.full(16 * 4, 255, np.uint8)
+    errs = []
+    entered = threading.Barrier(17)
+
+    def worker(k):
+        entered.wait()
+        try:
+            sl = list(range(4 * k, 4 * k + 4))
+            o, _ = nb.check_ids(q7[sl])
+            got[sl] = o
+        except Exception as x:  # noqa: BLE001
+            errs.append(x)
+
+    ts = [threading.Thread(target=worker, args=(k,)) for k in range(16)]
+    [t.start() for t in ts]
+    entered.wait()
+    time.sleep(0.3)  # every caller is inside kg_batcher_check, waiting on the open batch
+    t0 = time.perf_counter()
+    nb.close()
+    assert time.perf_counter() - t0 < 4.0  # the batch closed on destroy, not on its 5 s deadline
+    for t in ts:
+        t.join(timeout=10)
+        assert not t.is_alive()
+    assert not errs, errs
+    assert (got == exp[:64]).all()
+
+
+@pytest.mark.parametrize("callers", [1, 16, 64])
+def test_native_batcher_single_checks_vs_oracle(callers):
+    """The drop-in CheckIsMember path of INTEGRATION.md: every request is ONE blocking
+    kg_batcher_check of one query (handler.go:248-275 -> engine.go:54-60), from 1 / 16 / 64 caller
+    threads; every answer equals the oracle; call and batch latency percentiles are reported."""
+    reg, q7, exp = _batcher_graph(23)
+    got = np.full(len(q7), 255, np.uint8)
+    with NativeBatcher(reg.snapshot, 5, max_batch=4096, max_wait_us=200, dispatchers=4) as nb:
+        def worker(k):
+            for i in range(k, len(q7), callers):
+                got[i] = nb.check_ids(q7[i:i + 1])[0][0]
+        ts = [threading.Thread(target=worker, args=(k,)) for k in range(callers)]
+        t0 = time.perf_counter()
+        [t.start() for t in ts]
+        [t.join() for t in ts]
+        el = time.perf_counter() - t0
+        st = nb.stats()
+    assert (got == exp).all(), np.nonzero(got != exp)[0][:10]
+    assert st["checks"] == len(q7)
+    if callers > 1:
+        assert st["batches"] < len(q7)  # concurrent callers share batches
+    print(f"batcher callers={callers}: {len(q7) / el:.0f} checks/s, call p50 {st['call_p50_ms']:.3f} ms "
+          f"p99 {st['call_p99_ms']:.3f} ms, batch p99 {st['batch_p99_ms']:.3f} ms, "
+          f"mean batch {st['checks'] / max(1, st['batches']):.1f}")
 
 
 @pytest.mark.parametrize("seed,unions", [(0, False), (1, False), (2, True), (3, True)])
