@@ -342,6 +342,13 @@ int kg_shard_seed(kg_snapshot* s, const kg_query* d_q, size_t n, int32_t global_
 int kg_shard_level(kg_snapshot* s, const kg_frec* d_in, size_t n_in, const uint32_t* d_n_in, kg_frec* d_out,
                    size_t cap, uint32_t* d_counts, uint8_t* d_res, uint32_t* d_err, const uint32_t* d_done,
                    uint32_t done_words, void* stream);
+/* kg_shard_level over the receive buffer of a fixed-split all-to-all: segment k (k < n_seg) holds
+ * d_seg_counts[k] records (device memory, clamped to seg_cap) at d_in + k * seg_cap.  With it a
+ * multi-rank driver exchanges fixed-size buckets and never reads a count on the host inside a batch
+ * (keto_amd/sharded.py: the level loop runs a fixed number of levels, overflow is checked once). */
+int kg_shard_level_seg(kg_snapshot* s, const kg_frec* d_in, uint32_t n_seg, size_t seg_cap,
+                       const uint32_t* d_seg_counts, kg_frec* d_out, size_t cap, uint32_t* d_counts, uint8_t* d_res,
+                       uint32_t* d_err, const uint32_t* d_done, uint32_t done_words, void* stream);
 /* Early exit across ranks: d_done (may be NULL) is the done bitmap of the batch, done_words words per
  * home rank ([rank][word], bit i = query i of that rank answered IsMember by the previous levels);
  * kg_shard_level drops the records of those queries.  kg_shard_done packs this rank's d_res into its

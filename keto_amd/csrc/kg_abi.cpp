@@ -247,6 +247,21 @@ int kg_shard_level(kg_snapshot* sp, const kg_frec* d_in, size_t n_in, const uint
   KG_GUARD_END
 }
 
+int kg_shard_level_seg(kg_snapshot* sp, const kg_frec* d_in, uint32_t n_seg, size_t seg_cap,
+                       const uint32_t* d_seg_counts, kg_frec* d_out, size_t cap, uint32_t* d_counts, uint8_t* d_res,
+                       uint32_t* d_err, const uint32_t* d_done, uint32_t done_words, void* stream) {
+  KG_GUARD_BEGIN
+  if (!sp || !d_counts || !d_res || !d_err || !d_seg_counts || (n_seg && (!d_in || !d_out)))
+    return set_error(-2, "NULL argument");
+  if (n_seg < 1 || n_seg > KG_SHARD_MAX_RANKS || seg_cap == 0) return set_error(-2, "n_seg in [1, %d], seg_cap > 0", KG_SHARD_MAX_RANKS);
+  Snapshot* s = reinterpret_cast<Snapshot*>(sp);
+  std::lock_guard<std::mutex> lk(s->mu);
+  if (!s->shard_vis) return set_error(-2, "kg_shard_level_seg before kg_shard_seed");
+  return kg::shard_level(s, d_in, (size_t)n_seg * seg_cap, d_seg_counts, d_out, cap, d_counts, d_res, d_err, d_done,
+                         done_words, (hipStream_t)stream, n_seg, seg_cap);
+  KG_GUARD_END
+}
+
 int kg_shard_done(kg_snapshot* sp, size_t n, const uint8_t* d_res, const uint32_t* d_err, int with_escalated,
                   uint32_t* d_bits, uint32_t words, void* stream) {
   KG_GUARD_BEGIN
@@ -366,7 +381,7 @@ static int tune_one(Snapshot* s, const char* key, int64_t value) {
     return 0;
   }
   if (strcmp(key, "stream") == 0) {
-    if (value < 0 || value > 14) return set_error(-2, "stream must be in [0, 14]");
+    if (value < 0 || value > 15) return set_error(-2, "stream must be in [0, 15]");
     s->stream_variant = (int)value;
     return 0;
   }

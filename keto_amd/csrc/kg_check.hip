@@ -116,17 +116,41 @@ __device__ void block_append(bool pred, uint32_t val, uint32_t* list, uint32_t* 
   __syncthreads();
 }
 
+// Workgroup-aggregated append of LQuery records (one atomic per workgroup, contiguous 24-B stores).
+// Every thread must call it.
+__device__ void block_append_lq(bool pred, const LQuery& v, LQuery* list, uint32_t* count) {
+  __shared__ uint32_t wcnt[4], bbase;
+  const int lane = lane_id(), wave = threadIdx.x >> 6;
+  const uint64_t m = __ballot(pred);
+  if (lane == 0) wcnt[wave] = __popcll(m);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t t = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+    bbase = t ? atomicAdd(count, t) : 0u;
+  }
+  __syncthreads();
+  uint32_t off = bbase;
+  for (int w = 0; w < wave; w++) off += wcnt[w];
+  if (pred) list[off + lanes_below(m)] = v;
+  __syncthreads();
+}
+
 // ------------------------------------------------------------------ k_resolve
+// lq_list != nullptr (stream variant 15, k_stream4): light-routed queries go to the stream tier as
+// LQuery records in 8 shards of lq_cap entries (shard blockIdx & 7) and skip rq[i]; only queries
+// that later tiers read by index (GENERAL) are written to rq.
 __global__ __launch_bounds__(256) void k_resolve(DevSnap s, const kg_query* __restrict__ q, uint32_t n,
                                                  uint32_t n_base, const uint32_t* __restrict__ n_extra,
                                                  int32_t global, RQuery* __restrict__ rq, uint8_t* __restrict__ out,
                                                  uint32_t* __restrict__ err, uint32_t* light_list,
-                                                 uint32_t* gen_list, int no_holder_filter, Ctl* ctl) {
+                                                 uint32_t* gen_list, int no_holder_filter, Ctl* ctl,
+                                                 LQuery* lq_list, uint32_t lq_cap) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   // n: capacity (list strides); with a formula split the live count is n_base + *n_extra
   bool valid = i < (n_extra ? n_base + *n_extra : n);
   uint32_t route = ROUTE_DONE;
   bool did_probe = false, no_holder = false;
+  LQuery lq{};
   if (valid) {
     kg_query x = q[i];
     // node map and (for a subject id) holder hash: the first slots of both are loaded together,
@@ -202,7 +226,8 @@ __global__ __launch_bounds__(256) void k_resolve(DevSnap s, const kg_query* __re
       }
     }
     // rq is read only through the tier lists, so finished queries skip it (their 24 B never leave the CU)
-    if (route != ROUTE_DONE) rq[i] = RQuery{node, subj, d, route, rb, rl};
+    if (route == ROUTE_GENERAL || (route == ROUTE_LIGHT && !lq_list)) rq[i] = RQuery{node, subj, d, route, rb, rl};
+    lq = LQuery{i, node, subj, d, rb, rl};
     // every result starts as NotMember / no error (coalesced here): the tiers after this one store
     // only what differs (k_stream2 writes IsMember bytes only)
     out[i] = member ? KG_IS_MEMBER : KG_NOT_MEMBER;
@@ -215,7 +240,8 @@ __global__ __launch_bounds__(256) void k_resolve(DevSnap s, const kg_query* __re
   }
   // light list: 8 shards of capacity n (shard = blockIdx & 7), dequeued by k_light per XCD
   const uint32_t h = blockIdx.x & 7;
-  block_append(valid && route == ROUTE_LIGHT, i, light_list + (size_t)h * n, &ctl->light8[h * 32]);
+  if (lq_list) block_append_lq(valid && route == ROUTE_LIGHT, lq, lq_list + (size_t)h * lq_cap, &ctl->light8[h * 32]);
+  else block_append(valid && route == ROUTE_LIGHT, i, light_list + (size_t)h * n, &ctl->light8[h * 32]);
   block_append(valid && route == ROUTE_GENERAL, i, gen_list, &ctl->gen_count);
 }
 
@@ -1082,6 +1108,270 @@ __global__ __launch_bounds__(256) void k_stream2(DevSnap s, const RQuery* __rest
   block_stats<7>(ctl, idx, v);
 }
 
+// ------------------------------------------------------------------ k_stream4 (variant 15)
+// k_stream2's algorithm (one FIFO of row entries shared by 32 query slots, BFS order per query, a
+// direct-mapped visited cache with blind writes, children probed one step after discovery) with the
+// step's dependent chain and the work distribution reworked:
+//   * work comes as LQuery records (k_resolve writes the resolved query into the list itself), and a
+//     dequeue is PIPELINED over steps: step t issues the head atomic, step t+1 issues the coalesced
+//     record load, the records are used from step t+2 on -- both round trips hide under the steps'
+//     gathers, so chunks can be small (kg_snapshot_tune "stream_chunk") and the waves finish
+//     together instead of the last few running one 64-query chunk each (k_stream2's tail)
+//   * per-slot bookkeeping without returning LDS atomics: a query is finished when the FIFO position
+//     of its last appended entry (s_last, an atomicMax) lies behind the head -- no decrement per
+//     consumed entry and no increment per append; the edge budget is an atomicAdd read once, at the
+//     step's finish check (a query past it is retired in the same step)
+//   * the range bounds of the 8 per-XCD list shards are read once, into lanes 0..7
+//   * queries handed on write their RQuery for the next tiers (k_resolve no longer does)
+constexpr uint32_t S4_CHUNK = 64;
+
+template <int VLOG2, int QC>
+struct Stream4Lds {
+  unsigned long long vt[1 << VLOG2];  // direct-mapped visited cache (0 = empty)
+  uint32_t e_beg[QC], e_meta[QC];     // FIFO ring
+  uint32_t pref[65];                  // edge-owner marks (+1 dummy)
+  uint32_t s_state[32], s_qi[32], s_subj[32], s_sig[32], s_last[32], s_edg[32];
+  uint32_t s_node[32], s_depth[32], s_beg[32], s_len[32];
+};
+
+struct LqList {
+  const LQuery* list;
+  const uint32_t* counts;  // shard h holds counts[32 h] records from list[h * cap]
+  uint32_t cap;
+};
+
+template <int VLOG2, int QC>
+__global__ __launch_bounds__(256) void k_stream4(DevSnap s, LqList wl, uint32_t* heads, uint8_t* __restrict__ out,
+                                                 RQuery* __restrict__ rq, uint32_t* next_list, uint32_t* next_count,
+                                                 Ctl* ctl, uint32_t ecap, uint32_t chunk, uint32_t ranges) {
+  using Lds = Stream4Lds<VLOG2, QC>;
+  constexpr uint32_t WIN = 64u;
+  constexpr uint32_t VT = 1u << VLOG2;
+  static_assert(QC <= 256 && (QC & (QC - 1)) == 0, "FIFO ring of <= 256 entries (9-bit generations stay unique)");
+  const uint64_t t_start = wall_clock64();
+  __shared__ Lds lds_all[4];
+  Lds& L = lds_all[threadIdx.x >> 6];
+  const int lane = lane_id();
+  // XCD label: the first range this wave drains (the launch keeps grid >= 8 so every range is drained)
+  const uint32_t head0 = blockIdx.x & 7;
+  uint32_t head_sel = head0;
+  for (uint32_t i = lane; i < VT; i += 64) L.vt[i] = 0ull;
+  if (lane < 32) {
+    L.s_state[lane] = 0;
+    L.s_last[lane] = 0;
+    L.s_edg[lane] = 0;
+  }
+  if (lane == 0) L.pref[WIN] = 0;
+  // shard sizes, final before this kernel starts: lanes 0..7
+  const uint32_t shard_n = lane < 8 ? wl.counts[lane * 32] : 0u;
+  __builtin_amdgcn_wave_barrier();
+  uint32_t active = 0;  // wave-uniform: slots holding a query
+  // dequeue pipeline (wave-uniform state): 0 idle, 1 head atomic in flight (tk, lane 0), 2 records staged
+  uint32_t pf = 0, tk = 0, st_got = 0;
+  bool exhausted = false;  // every range this wave drains is empty
+  LQuery sq{};             // staged chunk (lane k: record k)
+  uint32_t c_left = 0, c_pos = 0;
+  LQuery cq{};             // current chunk
+  uint32_t head = 0, tail = 0, head_off = 0;
+  bool pend = false;
+  uint32_t pend_node = 0, pend_slot = 0, pend_gen = 0;
+  unsigned long long st_rows = 0, st_edges = 0, st_probes = 0, st_done = 0, st_steps = 0;
+  for (;;) {
+    // ---- the staged chunk (loaded at least one step ago) becomes the current one
+    if (c_left == 0 && pf == 2) {
+      cq = sq;
+      c_left = st_got;
+      c_pos = 0;
+      pf = 0;
+    }
+    // ---- refill free slots (their root entries need FIFO room)
+    const uint32_t freem = ~active;
+    const uint32_t want = __popc(freem);
+    const uint32_t got = min(want, c_left);
+    if (got && (tail - head) + got <= QC) {
+      const uint32_t r = __popc(freem & (lane < 32 ? (1u << lane) - 1u : 0xFFFFFFFFu));
+      const bool mine = lane < 32 && ((freem >> (lane & 31)) & 1u) && r < got;
+      const int src = mine ? (int)(c_pos + r) : lane;
+      const uint32_t qi = __shfl(cq.qi, src, 64), qnode = __shfl(cq.node, src, 64), qsubj = __shfl(cq.subj, src, 64),
+                     qbeg = __shfl(cq.beg, src, 64), qlen = __shfl(cq.len, src, 64);
+      const int32_t qdepth = __shfl(cq.depth, src, 64);
+      c_pos += got;
+      c_left -= got;
+      if (mine) {
+        const uint32_t slot = lane, gen = L.s_state[slot] & S2_GEN;  // freed slots hold a fresh generation
+        const bool over = qdepth > (int32_t)S2_DMAX || qlen > S2_LONG || qlen > ecap;
+        const uint32_t at = tail + r;
+        L.s_qi[slot] = qi;
+        L.s_subj[slot] = qsubj;
+        L.s_sig[slot] = subj_sig(qsubj);
+        L.s_node[slot] = qnode;
+        L.s_depth[slot] = (uint32_t)qdepth;
+        L.s_beg[slot] = qbeg;
+        L.s_len[slot] = qlen;
+        L.s_edg[slot] = qlen;
+        L.s_last[slot] = at;
+        L.s_state[slot] = over ? (gen | S2_OVER) : gen;
+        // the root counts as visited (a cycle back to it is not expanded again)
+        const unsigned long long key =
+            (1ull << 63) | ((unsigned long long)gen << 37) | ((unsigned long long)slot << 32) | qnode;
+        L.vt[((qnode * 0x9E3779B1u) ^ (slot * 0x85EBCA77u) ^ (gen * 0xC2B2AE3Du)) >> (32 - VLOG2)] = key;
+        L.e_beg[at & (QC - 1)] = qbeg;
+        L.e_meta[at & (QC - 1)] = s2_meta(over ? 0u : qlen, slot, gen, over ? 2u : (uint32_t)qdepth);
+      }
+      active |= (uint32_t)__ballot(mine);
+      tail += got;
+    }
+    // ---- advance the dequeue pipeline (nothing here is waited for in this step)
+    if (pf == 1) {
+      const uint32_t k = (uint32_t)__builtin_amdgcn_readfirstlane((int)tk);  // issued a step ago
+      const uint32_t h = head_sel & 7;
+      const uint32_t lo = h * wl.cap, hi = lo + (uint32_t)__builtin_amdgcn_readlane((int)shard_n, (int)h);
+      if (lo + k < hi) {
+        st_got = min(chunk, hi - (lo + k));
+        if ((uint32_t)lane < st_got) sq = wl.list[lo + k + lane];
+        pf = 2;
+      } else {
+        pf = 0;
+        if (++head_sel >= head0 + ranges) exhausted = true;
+      }
+    }
+    if (pf == 0 && !exhausted) {
+      if (lane == 0) tk = atomicAdd(&heads[(head_sel & 7) * 32], chunk);
+      pf = 1;
+    }
+    if (active == 0) {
+      if (exhausted && pf == 0 && c_left == 0) break;
+      head = tail;  // no query holds the FIFO: whatever is left in it is stale
+      head_off = 0;
+      continue;
+    }
+    __builtin_amdgcn_wave_barrier();
+    // ---- window: up to 64 FIFO entries from the head, up to WIN edges of them
+    // Every load of the step below is unconditional (lanes without work read a valid dummy slot) and
+    // predicated afterwards: a load inside a branch whose value is merged after the branch makes the
+    // compiler wait for it inside the branch -- k_stream2's gather was waited for before its probe
+    // load was even issued, two serial memory round trips per step.
+    const uint32_t avail = tail - head;
+    const uint32_t at0 = (head + lane) & (QC - 1);
+    uint32_t emeta = L.e_meta[at0], ebeg = L.e_beg[at0];
+    const uint32_t sl0 = (emeta >> 11) & 31u;
+    const uint32_t st0 = L.s_state[sl0];
+    // the previous step's children: probe validity and keys (LDS reads independent of the gathers)
+    const uint32_t pst = L.s_state[pend_slot], psubj = L.s_subj[pend_slot];
+    const bool inwin = (uint32_t)lane < avail;
+    const bool live = inwin && ((active >> sl0) & 1u) && (st0 == ((emeta >> 16) & S2_GEN));  // no HIT/OVER
+    uint32_t elen = live ? (emeta & 0x7FFu) : 0u;
+    if (lane == 0) {
+      ebeg += head_off;
+      elen = live ? elen - head_off : 0u;
+    }
+    if (!inwin) emeta = 0;
+    const bool pvalid = pend && pst == pend_gen;
+    const uint64_t pkey = dset_key(pend_node, psubj);
+    uint32_t total;
+    const uint32_t excl = wave_excl_scan(elen, &total);
+    L.pref[lane] = 0;
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t taken = min(total, WIN);
+    L.pref[(elen > 0 && excl < taken) ? excl : WIN] = (uint32_t)lane + 1;
+    const bool consumed = (uint32_t)lane < avail && excl + elen <= taken;
+    const uint32_t ncons = __popcll(__ballot(consumed));  // a prefix of the window
+    st_rows += (consumed && live) ? 1u : 0u;
+    {
+      const uint32_t ex_n = (uint32_t)__builtin_amdgcn_readlane((int)excl, ncons & 63);
+      if (ncons < avail && ncons < 64 && ex_n < taken) head_off = (ncons == 0 ? head_off : 0u) + (taken - ex_n);
+      else if (ncons > 0) head_off = 0;
+    }
+    __builtin_amdgcn_wave_barrier();
+    // ---- this step's edge gathers and the previous step's probes, all issued before any wait
+    const uint32_t m = wave_incl_scan<DppMax>(L.pref[lane]);
+    const int own = ((int)m - 1) & 63;
+    const uint32_t ob = __shfl(ebeg, own, 64);
+    const uint32_t om = __shfl(emeta, own, 64);
+    const uint32_t ox = __shfl(excl, own, 64);
+    const bool act = (uint32_t)lane < taken;
+    const AdjX x = s.adjx[act ? ob + ((uint32_t)lane - ox) : 0u];  // adjx[0] exists (n_set_edges + 1)
+    const ulonglong2 pb =
+        *reinterpret_cast<const ulonglong2*>(s.dset + (pvalid ? hash_home(pkey, s.dset_nb) : 0ull) * DSET_BUCKET);
+    const uint32_t slot = (om >> 11) & 31u, d = om >> 25, g = (om >> 16) & S2_GEN;
+    const uint32_t ssig = L.s_sig[slot];  // LDS, under the gathers' latency
+    head += ncons;
+    st_edges += (lane == 0) ? taken : 0u;
+    st_steps += (lane == 0) ? 1u : 0u;
+    // checkDirect probe, first bucket; a chain past a full first bucket (rare at load <= 0.25) is
+    // walked by the lanes that need it under a wave-uniform branch
+    bool hit = pvalid && (pb.x == pkey || pb.y == pkey);
+    {
+      const bool more = pvalid && !hit && pb.y != EMPTY64;
+      if (__ballot(more)) {
+        if (more) hit = dset_probe(s, pend_node, (uint32_t)pkey);
+      }
+    }
+    st_probes += pvalid ? 1u : 0u;
+    // ---- children: kept ones (rest >= 2 after the hop, non-empty set row) are marked + appended;
+    // every child new to the query is probed next step
+    const bool keepc = act && d >= 3 && x.len > 0;  // x of an inactive lane is adjx[0]: never used
+    const bool longrow = keepc && x.len > S2_LONG;
+    const unsigned long long key =
+        (1ull << 63) | ((unsigned long long)g << 37) | ((unsigned long long)slot << 32) | x.node;
+    const uint32_t hv = ((x.node * 0x9E3779B1u) ^ (slot * 0x85EBCA77u) ^ (g * 0xC2B2AE3Du)) >> (32 - VLOG2);
+    const unsigned long long old = keepc ? L.vt[hv] : 0ull;
+    const bool fresh = keepc && !longrow && old != key;
+    if (fresh) L.vt[hv] = key;
+    const uint64_t am = __ballot(fresh);
+    const uint32_t room = QC - (tail - head);
+    const uint32_t pos = __popcll(am & ((1ull << lane) - 1));
+    const bool appended = fresh && pos < room;
+    if (appended) {
+      const uint32_t at = tail + pos;
+      L.e_beg[at & (QC - 1)] = x.begin;
+      L.e_meta[at & (QC - 1)] = x.len | (om & 0x01FFF800u) | ((d - 1) << 25);
+      atomicMax(&L.s_last[slot], at);   // no return: read at the finish check
+      atomicAdd(&L.s_edg[slot], x.len);  // edge budget, likewise
+    }
+    if (longrow || (fresh && !appended)) atomicOr(&L.s_state[slot], S2_OVER);  // row too long / FIFO full
+    tail += min((uint32_t)__popcll(am), room);
+    if (hit) atomicOr(&L.s_state[pend_slot], S2_HIT);
+    pend = act && (keepc ? appended : true) && sig_maybe(x.sig, ssig);
+    pend_node = x.node;
+    pend_slot = slot;
+    pend_gen = g;
+    const uint32_t pslots = wave_or(pend ? 1u << slot : 0u);
+    __builtin_amdgcn_wave_barrier();
+    // ---- finished queries
+    bool done = false;
+    if (lane < 32 && ((active >> lane) & 1u)) {
+      const uint32_t st = L.s_state[lane];
+      const uint32_t last = L.s_last[lane], edg = L.s_edg[lane];
+      const uint32_t qi = L.s_qi[lane];
+      if (st & S2_HIT) {
+        done = true;
+        out[qi] = KG_IS_MEMBER;  // NotMember was pre-written by k_resolve
+        st_done++;
+      } else if ((st & S2_OVER) || (ecap != 0xFFFFFFFFu && edg > ecap)) {
+        done = true;
+        // the next tiers read the query by index
+        rq[qi] = RQuery{L.s_node[lane], L.s_subj[lane], (int32_t)L.s_depth[lane], ROUTE_LIGHT, L.s_beg[lane],
+                        L.s_len[lane]};
+        next_list[atomicAdd(next_count, 1u)] = qi;
+      } else if ((int32_t)(last - head) < 0 && !((pslots >> lane) & 1u)) {
+        done = true;  // every entry consumed, no probe pending: NotMember (pre-written)
+        st_done++;
+      }
+      if (done) L.s_state[lane] = ((st & S2_GEN) + 1u) & S2_GEN;  // stale: its FIFO entries and probes
+    }
+    const uint32_t freed = (uint32_t)__ballot(done);
+    active &= ~freed;
+    if (pend && ((freed >> pend_slot) & 1u)) pend = false;
+    __builtin_amdgcn_wave_barrier();
+  }
+  const unsigned long long t_end = wall_clock64(), life = lane == 0 ? t_end - t_start : 0ull;
+  block_max3(ctl, ~(unsigned long long)t_start, t_end, t_end - t_start);
+  const int idx[7] = {ST_LROWS, ST_LEDGES, ST_LPROBES, ST_LIGHT, ST_LSTEPS, ST_LWAVES, ST_LTICKS};
+  const unsigned long long v[7] = {st_rows, st_edges, st_probes, st_done, st_steps, lane == 0 ? 1ull : 0ull, life};
+  block_stats<7>(ctl, idx, v);
+}
+
 // ------------------------------------------------------------------ k_stream3 (variant 10)
 // k_stream2 software-pipelined by one step.  k_stream2's step is: take a window of 64 edges at the
 // FIFO head -> gather their adjx records (and probe the previous step's children) -> wait -> process
@@ -1909,9 +2199,18 @@ int check_batch_begin(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n, 
   HIPC(hipMemsetAsync(ctl, 0, sizeof(Ctl), stream));
   if (n) {
     const bool use_back = s->back_tier && s->ds.radj;
-    hipLaunchKernelGGL(k_resolve, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, stream, s->ds, d_q, (uint32_t)n,
+    // k_stream4 (variant 15) takes its work as LQuery records in 8 shards; shard h receives the
+    // appends of k_resolve's blocks h, h + 8, ... (<= 256 each).  They live in the light list's
+    // space (8 n u32 >= (n + 2048) LQuery for the >= 64 Ki queries the scratch is sized for).
+    const uint32_t nblk = (uint32_t)((n + 255) / 256);
+    const bool compact = s->light_tier != 1 && s->stream_variant == 15;
+    const uint32_t lq_cap = (nblk + 7) / 8 * 256;
+    LQuery* lq = compact ? reinterpret_cast<LQuery*>(light) : nullptr;
+    if (compact && (size_t)8 * lq_cap * sizeof(LQuery) > (size_t)8 * w->scratch_n * 4)
+      return set_error(-5, "stream work list does not fit the scratch");
+    hipLaunchKernelGGL(k_resolve, dim3(nblk), dim3(256), 0, stream, s->ds, d_q, (uint32_t)n,
                        (uint32_t)n_base, n_extra, global_max_depth, rq, d_out, d_err, light, gen,
-                       use_back ? (s->resolve_unheld ? 2 : 1) : 0, ctl);
+                       use_back ? (s->resolve_unheld ? 2 : 1) : 0, ctl, lq, lq_cap);
     HIPC(hipGetLastError());
     uint32_t* const after_list = use_medium ? medium : heavy;
     uint32_t* const after_count = use_medium ? &ctl->medium_count : &ctl->heavy_count;
@@ -1976,6 +2275,10 @@ int check_batch_begin(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n, 
       else if (sv == 14)  // 128-edge windows, no node cap
         hipLaunchKernelGGL((k_stream2<9, 256, 64, 0, 2>), dim3(grid), dim3(256), 0, stream, s->ds, rq, wl, ctl->heads,
                            d_out, ovf_list, ovf_count, ctl, ecap, std::max<uint32_t>(1u, std::min<uint32_t>(s->stream_chunk, 64u)), s->stream_steal);
+      else if (sv == 15)  // pipelined dequeue of LQuery records, no returning LDS atomics
+        hipLaunchKernelGGL((k_stream4<9, 256>), dim3(grid), dim3(256), 0, stream, s->ds, LqList{lq, ctl->light8, lq_cap},
+                           ctl->heads, d_out, rq, ovf_list, ovf_count, ctl, ecap,
+                           std::max<uint32_t>(1u, std::min<uint32_t>(s->stream_chunk, S4_CHUNK)), s->stream_steal);
       else if (sv == 10)
         hipLaunchKernelGGL((k_stream3<9, 256, 64, 64>), dim3(grid), dim3(256), 0, stream, s->ds, rq, wl, ctl->heads,
                            d_out, ovf_list, ovf_count, ctl, 0xFFFFFFFFu);

@@ -192,4 +192,15 @@ struct RQuery {
 };
 enum : uint32_t { ROUTE_DONE = 0, ROUTE_LIGHT = 1, ROUTE_GENERAL = 2 };
 
+// A light-routed query as k_resolve appends it to the stream tier's work list (k_stream4): the
+// resolved query travels with its list entry, so k_resolve writes it once, contiguously (no
+// scattered 24-B rq[i] store), and a stream-tier dequeue is one coalesced read (no list -> rq hop).
+struct LQuery {
+  uint32_t qi;     // query index in the batch
+  uint32_t node;   // root node
+  uint32_t subj;   // tagged subject
+  int32_t depth;   // clamped rest depth
+  uint32_t beg, len;  // root's set-adjacency row
+};
+
 }  // namespace kg

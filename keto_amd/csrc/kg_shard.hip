@@ -318,27 +318,51 @@ __device__ __forceinline__ void back_child(const DevSnap& s, const kg_frec& pr, 
 // but queued for k_shard_heavy, which spreads its edges over the grid.  (Expanding every row that
 // way instead -- an expansion list walked edge-parallel by a second kernel -- measured slower: the
 // in-workgroup expansion overlaps other workgroups' record processing, profiles/r2s8_*.)
+// Segmented input (n_seg > 1): the receive buffer of a fixed-split all-to-all -- segment k holds
+// d_n_in[k] records (clamped to seg_cap) from in[k * seg_cap]; the level walks their concatenation.
 __global__ __launch_bounds__(256) void k_shard_level(DevSnap s, const kg_frec* __restrict__ in, uint64_t n_bound,
                                                      const uint32_t* d_n_in, kg_frec* out, uint64_t cap, uint32_t* counts, uint8_t* res,
                                                      uint32_t* err, uint64_t* vis, uint64_t vmask,
                                                      const uint32_t* __restrict__ done, uint32_t done_wpr,
                                                      HeavyRow* heavy, uint32_t* heavy_n, uint32_t heavy_cap,
-                                                     uint32_t* qcnt, uint32_t budget, uint32_t lossy) {
+                                                     uint32_t* qcnt, uint32_t budget, uint32_t lossy, uint32_t n_seg,
+                                                     uint64_t seg_cap) {
   __shared__ uint32_t s_pref[256], s_wsum[4];
   __shared__ uint64_t s_rb[256];
   __shared__ kg_frec s_rec[256];
+  __shared__ uint64_t s_segpre[KG_SHARD_MAX_RANKS + 1];
   const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
   const uint32_t me = s.shard_rank;
   // record count: from the previous level's counter on the device (clamped to the bucket: a count
   // past it means dropped records, which the caller's overflow check turns into a rerun)
-  const uint64_t n_in = d_n_in ? min((uint64_t)*d_n_in, n_bound) : n_bound;
+  uint64_t n_in;
+  if (n_seg > 1) {
+    if (tid == 0) {
+      uint64_t a = 0;
+      for (uint32_t k = 0; k < n_seg; k++) {
+        s_segpre[k] = a;
+        a += min((uint64_t)d_n_in[k], seg_cap);
+      }
+      s_segpre[n_seg] = a;
+    }
+    __syncthreads();
+    n_in = s_segpre[n_seg];
+  } else {
+    n_in = d_n_in ? min((uint64_t)*d_n_in, n_bound) : n_bound;
+  }
   for (uint64_t base = (uint64_t)blockIdx.x * 256; base < n_in; base += (uint64_t)gridDim.x * 256) {
     const uint64_t i = base + tid;
     kg_frec r{0, NONE, 0, 0};
     bool hit_out = false, err_out = false, esc_out = false;
     uint64_t rb = 0, len = 0;
     if (i < n_in) {
-      r = in[i];
+      uint64_t src = i;
+      if (n_seg > 1) {
+        uint32_t k = 0;
+        while (k + 1 < n_seg && s_segpre[k + 1] <= i) k++;
+        src = (uint64_t)k * seg_cap + (i - s_segpre[k]);
+      }
+      r = in[src];
       const bool probe = !(r.depth & D_NOPROBE), own = (r.depth & D_OWN) != 0;
       r.depth &= D_MASK;
       if (r.node == KG_FREC_HIT) {
@@ -739,7 +763,7 @@ int shard_seed(Snapshot* s, const kg_query* d_q, size_t n, int32_t gdepth, kg_fr
 
 int shard_level(Snapshot* s, const kg_frec* d_in, size_t n_in, const uint32_t* d_n_in, kg_frec* d_out, size_t cap,
                 uint32_t* d_counts, uint8_t* d_res, uint32_t* d_err, const uint32_t* d_done, uint32_t done_words,
-                hipStream_t stream) {
+                hipStream_t stream, uint32_t n_seg, size_t seg_cap) {
   HIPC(hipSetDevice(s->device));
   if (!stream) stream = s->stream;
   // the bucket sizes restart; the flags word (counts[shard_n]: dropped records, visited table full)
@@ -754,7 +778,7 @@ int shard_level(Snapshot* s, const kg_frec* d_in, size_t n_in, const uint32_t* d
                        (uint64_t)cap, d_counts, d_res, d_err, (uint64_t*)s->shard_vis, s->shard_vis_slots - 1,
                        d_done, d_done ? done_words : 0u, heavy, heavy_n, SHARD_HEAVY_CAP, (uint32_t*)s->shard_qcnt,
                        shard_escalates(s) && s->shard_qcnt && !s->shard_final ? s->shard_budget : 0u,
-                       s->shard_vis_mode ? 1u : 0u);
+                       s->shard_vis_mode ? 1u : 0u, n_seg, (uint64_t)seg_cap);
     HIPC(hipGetLastError());
     hipLaunchKernelGGL(k_shard_heavy, dim3((uint32_t)s->n_cu * 4), dim3(256), 0, stream, s->ds, heavy, heavy_n,
                        SHARD_HEAVY_CAP, d_out, (uint64_t)cap, d_counts, d_res, d_err, s->shard_n);

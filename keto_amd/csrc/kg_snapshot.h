@@ -282,7 +282,7 @@ int shard_seed(Snapshot* s, const kg_query* d_q, size_t n, int32_t gdepth, kg_fr
                uint32_t* d_counts, uint8_t* d_res, uint32_t* d_err, hipStream_t stream);
 int shard_level(Snapshot* s, const kg_frec* d_in, size_t n_in, const uint32_t* d_n_in, kg_frec* d_out, size_t cap,
                 uint32_t* d_counts, uint8_t* d_res, uint32_t* d_err, const uint32_t* d_done, uint32_t done_words,
-                hipStream_t stream);
+                hipStream_t stream, uint32_t n_seg = 1, size_t seg_cap = 0);
 int shard_done(Snapshot* s, size_t n, const uint8_t* d_res, const uint32_t* d_err, int with_esc, uint32_t* d_bits,
                uint32_t words, hipStream_t stream);
 int shard_back_list(Snapshot* s, size_t n, const uint8_t* d_res, const uint32_t* d_err, kg_frec* d_list, size_t cap,

@@ -79,6 +79,15 @@ class HipShardOps:
                                          done.data_ptr() if done is not None else None, done_words, self._s()),
                    "kg_shard_level")
 
+    def level_seg(self, din, n_seg, seg_cap, seg_counts, out, cap, counts, res, err, done=None, done_words=0):
+        """kg_shard_level over a fixed-split receive buffer: segment k = din[k * seg_cap:], seg_counts[k]
+        records (a device int32 tensor, clamped to seg_cap)."""
+        _lib.check(self.L.kg_shard_level_seg(self.snapshot.handle, din.data_ptr(), n_seg, seg_cap,
+                                             seg_counts.data_ptr(), out.data_ptr(), cap, counts.data_ptr(),
+                                             res.data_ptr(), err.data_ptr(),
+                                             done.data_ptr() if done is not None else None, done_words, self._s()),
+                   "kg_shard_level_seg")
+
     def done_bits(self, res, n, words, err=None, mode=1):
         """err given: queries escalated out of the current phase count as done (mode 1: the forward
         phase, 2: the backward phase)."""
@@ -146,10 +155,18 @@ class ShardedChecker:
     """Drives one rank's side of a sharded batch.  dist = torch.distributed (initialised) or None
     for a single rank; device = the torch device the records live on."""
 
-    def __init__(self, ops, rank: int = 0, world: int = 1, dist=None, device="cuda", cap: int = 1 << 20):
+    def __init__(self, ops, rank: int = 0, world: int = 1, dist=None, device="cuda", cap: int = 1 << 20,
+                 protocol: str = "auto"):
+        """protocol (world > 1): "fixed" = every level exchanges fixed-size buckets (records per destination
+        <= bucket) and the batch runs gdepth + 1 levels with no host round trip inside it (counts, flags and
+        termination stay on the device; one readback at the end); "dynamic" = one metadata exchange and
+        host round trip per level, buckets sized by the real counts, early termination; "auto" = fixed
+        when the ops support it and no backward escalation phase is enabled."""
         if world > _lib.KG_SHARD_MAX_RANKS:
             raise ValueError("at most %d ranks" % _lib.KG_SHARD_MAX_RANKS)
         self.ops, self.rank, self.world, self.dist, self.device, self.cap = ops, rank, world, dist, device, cap
+        self.protocol = protocol
+        self.bucket = None  # fixed protocol: records per destination per level (learned per batch)
         self.levels = 0
         self.records_sent = 0
         self.host_syncs = 0
@@ -409,6 +426,11 @@ class ShardedChecker:
                 raise ShardOverflow(fl & 3)
             self.ops.finish(n, res, err)
             return res[:n], err[:n]
+        fixed = (self.protocol == "fixed" or (self.protocol == "auto" and not backward)) and hasattr(self.ops, "level_seg")
+        if fixed:
+            if backward:
+                raise ValueError("the fixed-bucket protocol has no backward escalation phase")
+            return self._check_fixed(dq, n, slots, gdepth, res, err)
         while True:
             send, recv_splits, total, flags = self._meta_exchange(counts[cur])
             if flags & 3:
@@ -434,3 +456,86 @@ class ShardedChecker:
             cur ^= 1
             self.ops.level(recv, int(recv.shape[0]), None, bufs[cur], cap, counts[cur], res, err, done, words)
             self.levels += 1
+
+    # ---- fixed-bucket protocol (world > 1): no host round trip inside a batch
+    def _max_slots(self, slots: int) -> int:
+        """The largest result-slot count of any rank (it sizes the done bitmap and the first bucket, which
+        every rank must agree on), cached per slot count: one all-reduce the first time a rank sees a
+        batch of this size."""
+        import torch
+        cache = self.__dict__.setdefault("_slots_cache", {})
+        if slots not in cache:
+            t = torch.tensor([slots], dtype=torch.int64, device="cpu" if self._host_staged() else self.device)
+            self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+            self.host_syncs += 1
+            cache[slots] = int(t.item())
+        return cache[slots]
+
+    def _check_fixed(self, dq, n: int, slots: int, gdepth: int, res, err):
+        """gdepth + 1 levels (a record's rest depth falls by one per level and seeds carry <= gdepth; the
+        last level only delivers hit / error reports to their home ranks), each: an all-to-all of the
+        per-destination counts, an all-to-all of fixed-size buckets (B records per destination), an
+        all-gather of the done bitmap, and kg_shard_level_seg over the received segments.  Counts,
+        overflow flags and the records-left check stay on the device; the batch reads them back once
+        (all-reduced over ranks), and a bucket or visited-table overflow anywhere reruns the batch on
+        every rank with room to spare (ShardOverflow)."""
+        import torch
+        N = self.world
+        smax = self._max_slots(slots)
+        words = (smax + 31) // 32
+        B = self.bucket or min(self.cap, (2 * smax) // N + 1024)  # the same on every rank
+        self.bucket = B
+        staged = self._host_staged()
+        xdev = "cpu" if staged else self.device
+        bufs = [torch.empty((N * B, REC_WORDS), dtype=torch.int32, device=self.device) for _ in range(2)]
+        counts = [torch.zeros(N + 1, dtype=torch.int32, device=self.device) for _ in range(2)]
+        recv = torch.empty((N * B, REC_WORDS), dtype=torch.int32, device=xdev)
+        rc = torch.empty(N, dtype=torch.int32, device=xdev)
+        acc = torch.zeros(3, dtype=torch.int64, device=self.device)  # flags, largest bucket, records sent
+        self.ops.seed(dq, n, gdepth, bufs[0], B, counts[0], res, err)
+        cur = 0
+        self.levels = 0
+        prune = hasattr(self.ops, "done_bits")
+        for k in range(gdepth + 1):
+            c = counts[cur]
+            c64 = c[:N].to(torch.int64)
+            acc[0] |= c[N].to(torch.int64) | (c64 > B).any().to(torch.int64)
+            acc[1] = torch.maximum(acc[1], c64.max())
+            acc[2] += c64.sum()
+            sc = c[:N].contiguous()
+            self.dist.all_to_all_single(rc, sc.cpu() if staged else sc)
+            snd = bufs[cur].cpu() if staged else bufs[cur]
+            self.dist.all_to_all_single(recv, snd)
+            done = None
+            if prune and k > 0:
+                mine = self.ops.done_bits(res, slots, words)
+                parts = torch.empty(N * words, dtype=torch.int32, device=xdev)
+                self.dist.all_gather_into_tensor(parts, mine.cpu() if staged else mine)
+                done = parts.to(self.device) if staged else parts
+            nxt = cur ^ 1
+            self.ops.level_seg(recv.to(self.device) if staged else recv, N, B, rc.to(self.device) if staged else rc,
+                               bufs[nxt], B, counts[nxt], res, err, done, words)
+            cur = nxt
+            self.levels += 1
+        c = counts[cur]
+        acc[0] |= c[N].to(torch.int64) | (c[:N].to(torch.int64) > B).any().to(torch.int64)
+        left = c[:N].to(torch.int64).sum()
+        # over ranks: each flag bit (bucket / visited-table overflow), the largest bucket, records left
+        tot = torch.stack([acc[0] & 1, (acc[0] >> 1) & 1, acc[1], left]).to(xdev)
+        self.dist.all_reduce(tot, op=self.dist.ReduceOp.MAX)
+        h = torch.cat([tot, acc[2:3].to(xdev)]).cpu().numpy()  # the batch's one host round trip
+        self.host_syncs += 1
+        flags = int(h[0]) | (int(h[1]) << 1)
+        self.records_sent = int(h[4])
+        big = int(h[2])
+        if flags & 3:
+            if flags & 1:
+                self.bucket = max(2 * B, int(big * 1.25) + 1024)
+                self.cap = max(self.cap, self.bucket)
+            raise ShardOverflow(flags & 2)  # a bucket overflow is handled here (bigger buckets); 2 = visited
+        if int(h[3]) != 0:
+            raise _lib.KetoGPUError("sharded batch: records left after %d levels" % (gdepth + 1))
+        # next batch: buckets 25 % above the largest one this batch needed (shrinking slowly)
+        self.bucket = max(1024, min(B, int(big * 1.25) + 1024)) if big * 2 < B else B
+        self.ops.finish(n, res, err)
+        return res[:n], err[:n]

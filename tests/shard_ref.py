@@ -39,6 +39,10 @@ def shard_owner(ns: int, obj: int, n: int) -> int:  # kg_internal.h shard_owner
 class CpuShardOps:
     device_counts = False  # level() takes host record counts only
 
+    @property
+    def escalates(self) -> bool:  # the backward / final forward phases run only with a forward budget
+        return self.budget > 0
+
     def __init__(self, tuples6: np.ndarray, wildcard_rel: int, rank: int, nranks: int, impure=(), budget=0,
                  back_budget=1 << 14):
         """impure: (ns, rel) pairs whose relation has a rewrite or is undeclared (relflag != 0).
@@ -135,6 +139,12 @@ class CpuShardOps:
         for i in np.nonzero(d)[0]:
             bits[i >> 5] |= np.uint32(1 << (int(i) & 31))
         return torch.from_numpy(bits.view(np.int32).copy())
+
+    def level_seg(self, din, n_seg, seg_cap, seg_counts, out, cap, counts, res, err, done=None, done_words=0):
+        """kg_shard_level_seg: segment k = din[k * seg_cap:], min(seg_counts[k], seg_cap) records."""
+        cnt = [min(int(x), seg_cap) for x in seg_counts.tolist()]
+        recs = torch.cat([din[k * seg_cap: k * seg_cap + cnt[k]] for k in range(n_seg)])
+        self.level(recs, int(recs.shape[0]), None, out, cap, counts, res, err, done, done_words)
 
     def level(self, din, n_in, n_in_dev, out, cap, counts, res, err, done=None, done_words=0):
         assert n_in_dev is None

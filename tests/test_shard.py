@@ -44,7 +44,7 @@ def _expected(t6, wildcard, q, gmax):
     return exp
 
 
-def _cpu_worker(rank, world, port, seed, cap, outq, budget=0, back_budget=1 << 14):
+def _cpu_worker(rank, world, port, seed, cap, outq, budget=0, back_budget=1 << 14, protocol="auto"):
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import torch.distributed as dist
@@ -56,27 +56,33 @@ def _cpu_worker(rank, world, port, seed, cap, outq, budget=0, back_budget=1 << 1
     it, t6, q = _graph(seed)
     ops = CpuShardOps(t6, it.wildcard_rel, rank, world, budget=budget, back_budget=back_budget)
     mine = np.array_split(np.arange(len(q)), world)[rank]  # this rank's slice of the batch
-    chk = ShardedChecker(ops, rank, world, dist, device="cpu", cap=cap)
+    chk = ShardedChecker(ops, rank, world, dist, device="cpu", cap=cap, protocol=protocol)
     out = {}
     for gmax in (2, 5):
+        syncs = chk.host_syncs
         res, err = chk.check(torch.from_numpy(q[mine].view(np.int32).copy()), gmax)
-        out[gmax] = (mine, res.numpy().copy(), chk.cap, chk.back_levels, chk.final_levels)
+        out[gmax] = (mine, res.numpy().copy(), chk.cap, chk.back_levels, chk.final_levels, chk.host_syncs - syncs,
+                     chk.levels)
     outq.put((rank, out))
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,cap,budget,back_budget", [(2, 1 << 12, 0, 0), (3, 4, 0, 0), (2, 1 << 12, 2, 1 << 14),
-                                                          (3, 8, 1, 1 << 14), (2, 1 << 12, 1, 2)])
-def test_sharded_protocol_gloo(world, cap, budget, back_budget):
+@pytest.mark.parametrize("world,cap,budget,back_budget,protocol",
+                         [(2, 1 << 12, 0, 0, "dynamic"), (3, 4, 0, 0, "dynamic"), (2, 1 << 12, 0, 0, "fixed"),
+                          (3, 4, 0, 0, "fixed"), (3, 1 << 12, 0, 0, "auto"), (2, 1 << 12, 2, 1 << 14, "auto"),
+                          (3, 8, 1, 1 << 14, "auto"), (2, 1 << 12, 1, 2, "auto")])
+def test_sharded_protocol_gloo(world, cap, budget, back_budget, protocol):
     """cap=4 / 8 force bucket overflows: every rank must rerun the batch with larger buckets.  budget
     1 / 2: nearly every expanding query escalates, so the backward phase (all-gathered reverse hops
     from the subject's holders) decides it; back_budget 2: most of those go on to the final forward
-    phase."""
+    phase.  protocol "fixed" (the default without escalation): fixed-size buckets, gdepth + 1 levels,
+    no host round trip inside a batch (at most 2 per batch: the first batch of a size reads the
+    done-bitmap width, and the end-of-batch readback; a rerun after an overflow adds one)."""
     seed = 3
     ctx = mp.get_context("spawn")
     outq = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_cpu_worker, args=(r, world, port, seed, cap, outq, budget, back_budget))
+    ps = [ctx.Process(target=_cpu_worker, args=(r, world, port, seed, cap, outq, budget, back_budget, protocol))
           for r in range(world)]
     for p in ps:
         p.start()
@@ -90,10 +96,14 @@ def test_sharded_protocol_gloo(world, cap, budget, back_budget):
         exp = _expected(t6, it.wildcard_rel, q, gmax)
         res = np.zeros(len(q), np.uint8)
         for _, out in got:
-            mine, r, final_cap, back_levels, final_levels = out[gmax]
+            mine, r, final_cap, back_levels, final_levels, syncs, levels = out[gmax]
             res[mine] = r
             if cap <= 8:
                 assert final_cap > cap
+            if protocol == "fixed" or (protocol == "auto" and not budget):
+                assert levels == gmax + 1
+                if cap > 8:
+                    assert syncs <= 2, syncs
             if budget and gmax == 5:
                 assert back_levels > 0
             if back_budget == 2 and gmax == 5:
