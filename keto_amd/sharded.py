@@ -426,7 +426,8 @@ class ShardedChecker:
                 raise ShardOverflow(fl & 3)
             self.ops.finish(n, res, err)
             return res[:n], err[:n]
-        fixed = (self.protocol == "fixed" or (self.protocol == "auto" and not backward)) and hasattr(self.ops, "level_seg")
+        fixed = (self.dist is not None and hasattr(self.ops, "level_seg")
+                 and (self.protocol == "fixed" or (self.protocol == "auto" and not backward)))
         if fixed:
             if backward:
                 raise ValueError("the fixed-bucket protocol has no backward escalation phase")
