@@ -83,6 +83,8 @@ def parse(argv=None):
     ap.add_argument("--stream-chunk", type=int, default=64,
                     help="kg_snapshot_tune stream_chunk (k_stream2 queries per dequeue, 1..64)")
     ap.add_argument("--grid-wgs", type=int, default=4, help="kg_snapshot_tune grid_wgs (k_grid_level WGs per CU)")
+    ap.add_argument("--grid-bidir", type=int, default=1,
+                    help="kg_snapshot_tune grid_bidir (1: the grid tier alternates forward and backward turns)")
     ap.add_argument("--stream-wgs", type=int, default=3,
                     help="kg_snapshot_tune stream_wgs (k_stream WGs per CU, 0 = by variant: 5 for k_stream2's ~29 KiB "
                          "WGs; 3 leaves LDS to the other batches in flight, best at --inflight 4: profiles/r2j_sweep.jsonl)")
@@ -157,6 +159,7 @@ def apply_tune(snap, a) -> None:
     if a.stream_chunk != 64:
         snap.tune("stream_chunk", a.stream_chunk)
     snap.tune("grid_wgs", a.grid_wgs)
+    snap.tune("grid_bidir", a.grid_bidir)
     snap.tune("stream_wgs", a.stream_wgs)
     snap.tune("back_wgs", a.back_wgs)
     snap.tune("grid_reserve", 1)  # a server pays this once at start-up, not inside some request's batch

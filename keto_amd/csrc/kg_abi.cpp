@@ -456,6 +456,11 @@ static int tune_one(Snapshot* s, const char* key, int64_t value) {
     s->grid_small_cap = (uint64_t)value;
     return 0;
   }
+  if (strcmp(key, "grid_bidir") == 0) {
+    if (value < 0 || value > 1) return set_error(-2, "grid_bidir must be 0 or 1");
+    s->grid_bidir = (int)value;
+    return 0;
+  }
   if (strcmp(key, "max_lanes") == 0) {
     if (value < 1 || value > 1024) return set_error(-2, "max_lanes in [1, 1024]");
     {

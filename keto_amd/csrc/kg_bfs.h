@@ -210,6 +210,14 @@ struct GlobalStore {
   __device__ bool contains(uint32_t key) const {  // coherent load (the marks are device atomics)
     return (__hip_atomic_load(&bm[key >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> (key & 31)) & 1u;
   }
+  // contains() that also returns where an absent key goes (expand's known-new insert)
+  __device__ bool find(uint32_t key, uint32_t& at) const {
+    at = key;
+    return contains(key);
+  }
+  // inserts a key known to be absent (find() said so and nothing was inserted since): no return
+  // value is needed, so nothing is waited for
+  __device__ void put_new(uint32_t key, uint32_t) { atomicOr(&bm[key >> 5], 1u << (key & 31)); }
   __device__ void sync() {
     // list entries written by other lanes of this wave must be visible to its loads
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -257,6 +265,26 @@ struct HashStore {
       h = (h + 1) & tmask;
     }
     return false;
+  }
+  // contains() that also returns the empty slot an absent key would take
+  __device__ bool find(uint32_t key, uint32_t& at) const {
+    uint32_t h = home(key);
+    at = h;
+    for (uint32_t p = 0; p <= tmask; p++) {
+      const uint32_t k = __hip_atomic_load(&tab[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (k == key + 1) return true;
+      if (k == 0u) {
+        at = h;
+        return false;
+      }
+      h = (h + 1) & tmask;
+    }
+    return false;
+  }
+  // a key known to be absent goes to the slot find() returned: the table belongs to one wave and
+  // nothing was inserted since, so a plain (coherent) store takes it -- no CAS round trip
+  __device__ void put_new(uint32_t key, uint32_t at) {
+    __hip_atomic_store(&tab[at], key + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __device__ void sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");

@@ -250,6 +250,203 @@ __device__ int expand_root(const DevSnap& s, Store& st, const kg_set& root, int3
 
 
 
+// Passes 2 and 3 hold the batch's largest roots, whose walks are the batch's tail: one wave doing
+// hundreds of thousands of dependent round trips (C5's largest tree: 335 k records, ~135 ms).  This
+// variant of expand_root cuts the trips per expanded set:
+//   * a chunk scan issues the child's row range, its node triple (for the record) and the visited
+//     lookup in ONE round trip after the row_subj load, so leaves are emitted from registers;
+//   * the frame stack and each frame's scanned chunk live in LDS (XF frames: C5's depth-5 walk needs
+//     7), so a pop resumes the parent's chunk without re-reading row_subj / row_off / nd_* -- only the
+//     visited lookups are redone (the set grew during the subtree);
+//   * the candidate's insert is a plain store into the empty slot its lookup found (the table belongs
+//     to this wave and nothing was inserted in between): no CAS round trip before the push.
+// Output is identical to expand_root (same candidates in the same order).
+constexpr int XF = 16;
+struct ExpLds {
+  ExpFrame fr[XF];
+  uint64_t cbase[XF];  // row position of lane 0 of the frame's cached chunk
+  uint32_t cn[XF];     // cached lanes (0: none)
+  uint32_t sub[XF][64], clen[XF][64], ns[XF][64], obj[XF][64], rel[XF][64];
+  uint64_t crb[XF][64];
+};
+
+template <class Store>
+__device__ int expand_root_x(const DevSnap& s, Store& st, const kg_set& root, int32_t global, ExpFrame* gstack,
+                             Stream& S, uint32_t& n_records, ExpLds& X) {
+  const int lane = lane_id();
+  S.ok = true;
+  S.pos = 0;
+  S.first = S.cur = alloc_chunk(S);
+  n_records = 0;
+  if (!S.ok) return EXP_ARENA;
+  int32_t d = root.max_depth;
+  if (d <= 0 || global < d) d = global;  // engine.go:37-39
+  if (root.sns == KG_SUBJECT_ID) {       // SubjectID -> Leaf
+    emit(S, lane == 0, rec_subject(s, root.sobj < 0x7FFFFFFFu ? root.sobj : 0x7FFFFFFFu));
+    n_records = 1;
+    return S.ok ? EXP_OK : EXP_ARENA;
+  }
+  const uint32_t rn = nmap_find(s, root.sns, root.srel, root.sobj);
+  if (rn == NONE) return EXP_OK;  // no rows anywhere: nil
+  st.reset();
+  uint32_t n_vis = 0;
+  wave_add_roots(st, lane == 0, rn, n_vis);  // marks the root visited
+  const uint64_t rb0 = s.row_off[rn], re0 = s.row_off[rn + 1];
+  if (rb0 == re0) {
+    st.finish(n_vis);
+    return EXP_OK;
+  }
+  if (d <= 1) {
+    emit(S, lane == 0, rec_set(s, 2, rn, 0));
+    st.finish(n_vis);
+    n_records = 1;
+    return S.ok ? EXP_OK : EXP_ARENA;
+  }
+  emit(S, lane == 0, rec_set(s, 1, rn, (uint32_t)(re0 - rb0)));
+  uint32_t count = 1;
+  int sp = 0;
+  if (lane < XF) X.cn[lane] = 0;
+  __builtin_amdgcn_wave_barrier();
+  ExpFrame F{rb0, rn, 0, (uint32_t)(re0 - rb0), d};
+  int status = EXP_OK;
+  for (;;) {
+    const uint64_t rb = F.rb, re = F.rb + F.len;
+    const bool can_expand = F.d - 1 >= 2;
+    bool pushed = false;
+    while (rb + F.cursor < re) {
+      const uint64_t at0 = rb + F.cursor;
+      // the chunk: the rest of this frame's cached chunk if the cursor is inside it, else a fresh one
+      const bool cached = sp < XF && X.cn[sp] && at0 >= X.cbase[sp] && at0 < X.cbase[sp] + X.cn[sp];
+      uint32_t sub = 0, clen = 0, nns = 0, nobj = 0, nrel = 0;
+      uint64_t crb = 0;
+      bool valid;
+      uint32_t width;
+      if (cached) {
+        const uint32_t k0 = (uint32_t)(at0 - X.cbase[sp]);
+        width = X.cn[sp] - k0;
+        valid = (uint32_t)lane < width;
+        const uint32_t k = valid ? k0 + lane : 0u;
+        sub = X.sub[sp][k];
+        clen = X.clen[sp][k];
+        crb = X.crb[sp][k];
+        nns = X.ns[sp][k];
+        nobj = X.obj[sp][k];
+        nrel = X.rel[sp][k];
+      } else {
+        width = (uint32_t)min<uint64_t>(64, re - at0);
+        valid = (uint32_t)lane < width;
+        sub = s.row_subj[valid ? at0 + lane : at0];
+        const bool set = valid && (sub & SET_BIT);
+        const uint32_t c = set ? sub & ~SET_BIT : 0u;  // node 0 exists: unconditional loads, no waits in branches
+        const uint64_t r0 = s.row_off[c], r1 = s.row_off[c + 1];
+        nns = s.nd_ns[c];
+        nobj = s.nd_obj[c];
+        nrel = s.nd_rel[c];
+        crb = set ? r0 : 0;
+        clen = set ? (uint32_t)(r1 - r0) : 0u;
+        if (sp < XF) {
+          X.sub[sp][lane] = sub;
+          X.clen[sp][lane] = clen;
+          X.crb[sp][lane] = crb;
+          X.ns[sp][lane] = nns;
+          X.obj[sp][lane] = nobj;
+          X.rel[sp][lane] = nrel;
+          if (lane == 0) {
+            X.cbase[sp] = at0;
+            X.cn[sp] = width;
+          }
+        }
+      }
+      const bool is_set = valid && (sub & SET_BIT);
+      const uint32_t c = sub & ~SET_BIT;
+      bool cand = false;
+      uint32_t vat = 0;
+      if (is_set && can_expand) {
+        // a set visited before this chunk is a leaf whatever comes first (the visited set only
+        // grows): only unvisited sets with rows are order-dependent candidates, taken one by one
+        const bool seen = st.find(c, vat);
+        cand = clen > 0 && !seen;
+      }
+      const uint64_t mc = __ballot(cand);
+      const uint32_t p = mc ? (uint32_t)(__ffsll((unsigned long long)mc) - 1) : 64u;
+      // everything before the first candidate: leaves (and marks, order-free for non-candidates)
+      const bool leaf = valid && (uint32_t)lane < p;
+      // d-1 <= 1: child sets become leaves but BuildTree still marks them visited, which a later
+      // (shallower) encounter elsewhere in the tree observes.  SubjectIDs are never marked.
+      if (!can_expand && !wave_add_roots(st, leaf && is_set, c, n_vis)) {
+        status = EXP_OVERFLOW;
+        break;
+      }
+      kg_tree_node r;
+      r.type = 2;
+      r.pad = 0;
+      r.n_children = 0;
+      r.is_set = is_set ? 1 : 0;
+      r.ns = is_set ? nns : KG_SUBJECT_ID;
+      r.obj = is_set ? nobj : sub;
+      r.rel = is_set ? nrel : 0u;
+      emit(S, leaf, r);
+      count += __popcll(__ballot(leaf));
+      if (!S.ok) return EXP_ARENA;
+      if (p == 64u) {
+        F.cursor += width;
+        continue;
+      }
+      // candidate at lane p, in order: unvisited when its lookup ran, and nothing was inserted since
+      const uint32_t cnode = __shfl(c, (int)p, 64);
+      const uint32_t cl = __shfl(clen, (int)p, 64);
+      const uint32_t cat = __shfl(vat, (int)p, 64);
+      const uint64_t cbeg = ((uint64_t)(uint32_t)__shfl((uint32_t)(crb >> 32), (int)p, 64) << 32) |
+                            (uint32_t)__shfl((uint32_t)crb, (int)p, 64);
+      kg_tree_node u;
+      u.type = 1;
+      u.is_set = 1;
+      u.pad = 0;
+      u.ns = __shfl(nns, (int)p, 64);
+      u.obj = __shfl(nobj, (int)p, 64);
+      u.rel = __shfl(nrel, (int)p, 64);
+      u.n_children = cl;
+      F.cursor += p + 1;
+      if (n_vis + 1 > st.cap()) {
+        status = EXP_OVERFLOW;
+        break;
+      }
+      if (lane == 0) {
+        st.put_new(cnode, cat);
+        st.list()[n_vis] = cnode;
+      }
+      n_vis++;
+      emit(S, lane == 0, u);
+      count++;
+      if (!S.ok) return EXP_ARENA;
+      if (sp >= 0x7FFF) {
+        status = EXP_OVERFLOW;
+        break;
+      }
+      if (lane == 0) {
+        if (sp < XF) X.fr[sp] = F;
+        else gstack[sp] = F;
+      }
+      sp++;
+      if (lane == 0 && sp < XF) X.cn[sp] = 0;  // the child frame starts without a cached chunk
+      __builtin_amdgcn_wave_barrier();
+      F = ExpFrame{cbeg, cnode, 0, cl, F.d - 1};
+      pushed = true;
+      break;
+    }
+    if (status != EXP_OK) break;
+    if (pushed) continue;
+    if (sp == 0) break;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    sp--;
+    F = sp < XF ? X.fr[sp] : gstack[sp];
+  }
+  st.finish((uint32_t)min<uint64_t>(n_vis, st.cap()));
+  n_records = count;
+  return status;
+}
+
 __global__ __launch_bounds__(256) void k_expand_lds(DevSnap s, const kg_set* __restrict__ roots, uint32_t n,
                                                     int32_t global, ExpCtl* ctl, RootOut* outs, kg_tree_node* arena,
                                                     uint32_t* next, uint32_t n_chunks, ExpFrame* stacks,
@@ -289,6 +486,7 @@ __device__ void expand_slot_loop(const DevSnap& s, const kg_set* __restrict__ ro
                                  RootOut* outs, kg_tree_node* arena, uint32_t* next, uint32_t n_chunks,
                                  ExpFrame* stack, const uint32_t* qlist, uint32_t count, uint32_t* head, Store& st,
                                  uint32_t* clear_base, uint64_t clear_words, uint32_t* p3_list) {
+  __shared__ ExpLds X;
   const int lane = lane_id();
   Stream S{arena, next, n_chunks, ctl, 0, 0, 0, true};
   unsigned long long recs = 0;
@@ -299,7 +497,7 @@ __device__ void expand_slot_loop(const DevSnap& s, const kg_set* __restrict__ ro
     if (k >= count) break;
     const uint32_t ri = qlist[k];
     uint32_t nr = 0;
-    const int r = expand_root(s, st, roots[ri], global, stack, S, nr);
+    const int r = expand_root_x(s, st, roots[ri], global, stack, S, nr, X);
     if (r == EXP_OVERFLOW && p3_list) {
       uint4* b4 = reinterpret_cast<uint4*>(clear_base);  // clear_words: multiple of 4, 16-B aligned
       for (uint64_t i = lane; i < clear_words / 4; i += 64) b4[i] = make_uint4(0, 0, 0, 0);

@@ -15,6 +15,21 @@
 // level's edge prefix sums and tile_first come out of the appends themselves (no scan pass).
 // Semantics are those of k_stream / k_medium (kg_check.hip): bounded reachability with every node
 // probed once at its shallowest depth.  A round that overflows the log is rerun with fewer slots.
+//
+// Bidirectional mode (default, kg_snapshot_tune "grid_bidir"): the queries that reach this tier are the
+// ones whose forward search is huge -- on a heavy-tailed graph every root reaches whole layers within
+// two hops (SURVEY.md 8d's degree law: ~1.2 M edge visits per query).  Each round alternates a forward
+// turn (the log above) with a BACKWARD turn over a second log: backward turn 0 reads the subject's
+// holders (hold[], engine.go:159-163's exact tuples seen from the subject), turn j their parents
+// through the reverse set-adjacency.  Forward turn t runs while 2t <= D-1 and backward turn t while
+// 2t+1 <= D-1, so every node either side has recorded can close a path of <= D-1 hops with every node
+// the other side has recorded: a forward child found in the backward set, or a backward parent that is
+// the root or in the forward set, is a hit (checkExpandSubject's "first IsMember wins").  A side whose
+// frontier runs dry while its turns are still active has its whole closure: nothing the other side
+// finds later can be new to it, so the query is NotMember at once (a root that reaches no holder, or a
+// subject no ancestor chain leads up from to the root).  Both sides share the visited table (a
+// direction bit in the key).  Typical heavy-tail negatives -- subjects held only by rows nothing points
+// at -- end after one backward turn instead of a forward walk over whole layers.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -41,27 +56,49 @@ struct GridLv {
 };
 
 struct GridCtl {
-  GridLv lv[3];
+  GridLv lv[3];   // forward log
+  GridLv blv[3];  // backward log (bidirectional mode)
   uint32_t overflow, pad;
   unsigned long long logged;  // entries over all levels (stats: rows opened)
   unsigned long long edges;   // edges over all levels (stats)
   unsigned long long probes8[8][16];  // per-XCD shards (one 128-B line each)
 };
 
+// Per-slot state of a round.  hit: 0 live, 1 IsMember, 2 NotMember decided early (a side's closure
+// ran dry).  lastf / lastb: the last turn that appended to the side's next level.
+struct GridSlots {
+  uint32_t* q;     // query index
+  uint2* info;     // (tagged subject, rest depth of the root)
+  uint32_t* hit;
+  uint32_t* root;  // root node (a backward parent equal to it closes a path)
+  uint32_t* lastf;
+  uint32_t* lastb;
+};
+
+// Turn activity for a slot of rest depth D (bidir = 0: forward only, the classic schedule).
+__device__ __forceinline__ bool fwd_active(int bidir, int t, int D) { return bidir ? 2 * t <= D - 1 : t + 1 <= D - 1; }
+__device__ __forceinline__ bool back_active(int bidir, int t, int D) { return bidir && 2 * t + 1 <= D - 1; }
+
 // Visited sets of all slots in ONE open-addressing table of 64-bit keys
-//   epoch (16) | slot (16) | node (32)
+//   epoch (15) | direction (1: backward) | slot (16) | node (32)
 // Entries of older epochs (earlier rounds / batches) count as empty, so the table is never
-// cleared between rounds; it is zeroed once per 65535 rounds.  Within a round an entry never
+// cleared between rounds; it is zeroed once per 32767 rounds.  Within a round an entry never
 // changes once written, so a (possibly stale) plain load that shows this round's epoch is final.
 constexpr int GH_PROBES = 128;
+constexpr int GH_EPOCH_SHIFT = 49;
+constexpr uint64_t GH_BACK = 1ull << 48;
+constexpr uint32_t GH_EPOCH_WRAP = 0x8000;
+__device__ __forceinline__ uint64_t gh_key(uint64_t epoch, bool back, uint32_t slot, uint32_t node) {
+  return (epoch << GH_EPOCH_SHIFT) | (back ? GH_BACK : 0ull) | ((uint64_t)slot << 32) | node;
+}
 __device__ __forceinline__ int gh_insert(uint64_t* H, uint64_t mask, uint64_t key) {
-  const uint64_t ep = key >> 48;
-  uint64_t h = mix64(key & 0xFFFFFFFFFFFFull) & mask;
+  const uint64_t ep = key >> GH_EPOCH_SHIFT;
+  uint64_t h = mix64(key & ((1ull << GH_EPOCH_SHIFT) - 1)) & mask;
   for (int p = 0; p < GH_PROBES; p++) {
     uint64_t cur = H[h];
     for (;;) {
-      if (cur == key) return 0;      // already visited
-      if ((cur >> 48) == ep) break;  // another key of this round: next slot
+      if (cur == key) return 0;                   // already visited
+      if ((cur >> GH_EPOCH_SHIFT) == ep) break;   // another key of this round: next slot
       const uint64_t old = atomicCAS((unsigned long long*)&H[h], (unsigned long long)cur, (unsigned long long)key);
       if (old == cur) return 1;      // inserted
       cur = old;
@@ -69,6 +106,18 @@ __device__ __forceinline__ int gh_insert(uint64_t* H, uint64_t mask, uint64_t ke
     h = (h + 1) & mask;
   }
   return -1;  // probe bound: the round is rerun with fewer slots
+}
+// Membership only (the other direction's set): 1 present, 0 absent, -1 probe bound (rerun).
+__device__ __forceinline__ int gh_contains(const uint64_t* H, uint64_t mask, uint64_t key) {
+  const uint64_t ep = key >> GH_EPOCH_SHIFT;
+  uint64_t h = mix64(key & ((1ull << GH_EPOCH_SHIFT) - 1)) & mask;
+  for (int p = 0; p < GH_PROBES; p++) {
+    const uint64_t cur = H[h];
+    if (cur == key) return 1;
+    if ((cur >> GH_EPOCH_SHIFT) != ep) return 0;  // an empty slot of this round ends the probe
+    h = (h + 1) & mask;
+  }
+  return -1;
 }
 
 struct GridLog {
@@ -81,8 +130,8 @@ struct GridLog {
 
 // Workgroup-aggregated append of the lanes with `app` set (entry slot / row start rb / row length
 // len) to level counters lv[nl] (tile map tile_first[np]); every thread of the workgroup must call it.
-__device__ __forceinline__ void grid_append(GridCtl* ctl, const GridLog& lg, int nl, int np, uint64_t next_base,
-                                            bool app, uint32_t slot, uint32_t rb, uint32_t len) {
+__device__ __forceinline__ void grid_append(GridCtl* ctl, GridLv* lvs, const GridLog& lg, int nl, int np,
+                                            uint64_t next_base, bool app, uint32_t slot, uint32_t rb, uint32_t len) {
   __shared__ uint32_t s_wcnt[4];
   __shared__ uint64_t s_wedge[4];
   __shared__ unsigned long long s_old;
@@ -102,7 +151,7 @@ __device__ __forceinline__ void grid_append(GridCtl* ctl, const GridLog& lg, int
   if (threadIdx.x == 0) {
     const uint64_t tc = s_wcnt[0] + s_wcnt[1] + s_wcnt[2] + s_wcnt[3];
     const uint64_t te = s_wedge[0] + s_wedge[1] + s_wedge[2] + s_wedge[3];
-    s_old = tc ? atomicAdd(&ctl->lv[nl].packed, (unsigned long long)((tc << EDGE_BITS) | te)) : 0ull;
+    s_old = tc ? atomicAdd(&lvs[nl].packed, (unsigned long long)((tc << EDGE_BITS) | te)) : 0ull;
   }
   __syncthreads();
   if (app) {
@@ -133,26 +182,49 @@ __device__ __forceinline__ uint32_t round_slots(const uint32_t* d_count, uint32_
   return c > base ? min(G, c - base) : 0u;
 }
 
-// Level 0: the roots (already probed by k_resolve), one per slot.
+// Level 0: the roots (already probed by k_resolve), one per slot; in bidirectional mode also the
+// backward log's level 0: one pseudo-entry per slot whose "edges" are the subject's holders.
 __global__ __launch_bounds__(256) void k_grid_init(DevSnap s, const RQuery* __restrict__ rq,
                                                    const uint32_t* __restrict__ qlist, const uint32_t* d_count,
-                                                   uint32_t base, uint32_t G, GridLog lg, uint32_t* slot_q,
-                                                   uint2* slot_info, uint32_t* slot_hit, uint64_t* H, uint64_t mask,
-                                                   uint64_t epoch, GridCtl* ctl) {
+                                                   uint32_t base, uint32_t G, GridLog lg, GridLog blg, GridSlots sl,
+                                                   uint64_t* H, uint64_t mask, uint64_t epoch, GridCtl* ctl,
+                                                   int bidir) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   const bool valid = i < round_slots(d_count, base, G);
-  uint32_t rb = 0, len = 0;
+  uint32_t rb = 0, len = 0, hb = 0, hn = 0;
   if (valid) {
     const uint32_t qi = qlist[base + i];
     const RQuery q = rq[qi];
-    slot_q[i] = qi;
-    slot_info[i] = make_uint2(q.subj, (uint32_t)q.depth);
-    slot_hit[i] = 0;  // the root was already probed (k_resolve)
-    if (gh_insert(H, mask, (epoch << 48) | ((uint64_t)i << 32) | q.node) < 0) ctl->overflow = 1;
+    sl.q[i] = qi;
+    sl.info[i] = make_uint2(q.subj, (uint32_t)q.depth);
+    sl.hit[i] = 0;  // the root was already probed (k_resolve)
+    sl.root[i] = q.node;
+    sl.lastf[i] = 0;
+    sl.lastb[i] = NONE;
+    if (gh_insert(H, mask, gh_key(epoch, false, i, q.node)) < 0) ctl->overflow = 1;
     rb = q.beg;
     len = q.len;
+    if (bidir) {
+      const uint2 hr = holders_find(s, q.subj);
+      hb = hr.x;
+      hn = hr.y;
+      if (hn) sl.lastb[i] = 0;
+    }
   }
-  grid_append(ctl, lg, 0, 0, 0, valid, i, rb, len);
+  grid_append(ctl, ctl->lv, lg, 0, 0, 0, valid, i, rb, len);
+  if (bidir) grid_append(ctl, ctl->blv, blg, 0, 0, 0, valid && hn > 0, i, hb, hn);
+}
+
+// Before a turn: a live slot whose side `back` has an active turn t but appended nothing at turn t-1
+// has that side's whole closure (BFS stopped by itself, not by depth) -- NotMember (see the header).
+__global__ void k_grid_settle(GridSlots sl, const uint32_t* d_count, uint32_t base, uint32_t G, int t, int back,
+                              int bidir) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= round_slots(d_count, base, G) || sl.hit[i]) return;
+  const int D = (int)sl.info[i].y;
+  if (back ? (back_active(bidir, t, D) && sl.lastb[i] != (uint32_t)t)
+           : (fwd_active(bidir, t, D) && sl.lastf[i] != (uint32_t)t))
+    sl.hit[i] = 2;
 }
 
 // Largest j in [lo, hi) with ex[base + j] <= e: the entry holding edge e (search in the log).
@@ -165,22 +237,25 @@ __device__ __forceinline__ uint64_t entry_of(const uint64_t* ex, uint64_t base, 
   return lo;
 }
 
-// One level: one thread per edge, one GT-edge tile per workgroup iteration.
-__global__ __launch_bounds__(256) void k_grid_level(DevSnap s, GridLog lg, int level,
-                                                    const uint2* __restrict__ slot_info, uint32_t* slot_hit,
-                                                    uint64_t* H, uint64_t mask, uint64_t epoch, GridCtl* ctl) {
+// One level: one thread per edge, one GT-edge tile per workgroup iteration.  back = 0: a forward
+// turn over the forward log (edges = adjx records: children); back = 1: a backward turn over the
+// backward log (edges = reverse-adjacency parents, or at turn 0 the subject's holders).
+template <int BACK>
+__global__ __launch_bounds__(256) void k_grid_level(DevSnap s, GridLog lg, int level, GridSlots sl, uint64_t* H,
+                                                    uint64_t mask, uint64_t epoch, GridCtl* ctl, int bidir) {
   __shared__ uint64_t s_beg[GT + 2];
   __shared__ uint32_t s_slot[GT + 2], s_rb[GT + 2];
   __shared__ uint64_t s_j0, s_cnt;
   if (ctl->overflow) return;  // the round is void (entries past the log were dropped)
+  GridLv* lvs = BACK ? ctl->blv : ctl->lv;
   const int cl3 = level % 3, nl = (level + 1) % 3, zl = (level + 2) % 3;
-  const uint64_t lb = ctl->lv[cl3].base, packed = ctl->lv[cl3].packed;
+  const uint64_t lb = lvs[cl3].base, packed = lvs[cl3].packed;
   const uint64_t n = packed >> EDGE_BITS, total = packed & EDGE_MASK;
   const uint64_t next_base = lb + n;
   const uint32_t* tf = lg.tile_first[level & 1];
   if (blockIdx.x == 0 && threadIdx.x == 0) {
-    ctl->lv[nl].base = next_base;
-    ctl->lv[zl].packed = 0;
+    lvs[nl].base = next_base;
+    lvs[zl].packed = 0;
     ctl->edges += total;
     ctl->logged += n;
   }
@@ -212,8 +287,8 @@ __global__ __launch_bounds__(256) void k_grid_level(DevSnap s, GridLog lg, int l
       }
     __syncthreads();
     const uint64_t e = t0 + threadIdx.x;
-    bool act = e < t1, keep = false;
-    uint32_t slot = 0, child = 0, cb = 0, clen = 0;
+    bool act = e < t1, app = false;
+    uint32_t slot = 0, cb = 0, clen = 0, child = 0;
     if (act) {
       uint64_t beg;
       uint32_t rb;
@@ -234,39 +309,87 @@ __global__ __launch_bounds__(256) void k_grid_level(DevSnap s, GridLog lg, int l
         rb = lg.rb[lb + j];
       }
       // the slot's state and the edge load are independent: one round trip for both
-      const uint32_t hit = slot_hit[slot];
-      const uint2 si = slot_info[slot];  // (tagged subject, rest depth of the root)
-      const AdjX x = s.adjx[rb + (e - beg)];
-      if (hit) {
-        act = false;
-      } else {
-        child = x.node;
-        cb = x.begin;
-        clen = x.len;
-        keep = clen > 0 && (int)si.y - level - 1 >= 2;  // child will itself be expanded
-        if (keep) {
-          const int ins = gh_insert(H, mask, (epoch << 48) | ((uint64_t)slot << 32) | child);
-          if (ins < 0) ctl->overflow = 1;
-          if (ins == 0) act = false;
+      const uint32_t hit = sl.hit[slot];
+      const uint2 si = sl.info[slot];  // (tagged subject, rest depth of the root)
+      const int D = (int)si.y;
+      if (!BACK) {
+        const AdjX x = s.adjx[rb + (e - beg)];
+        if (hit) {
+          act = false;
+        } else {
+          child = x.node;
+          cb = x.begin;
+          clen = x.len;
+          // forward turn `level` finds hop level+1: it is expanded at forward turn level+1 and may be met
+          // by backward turn `level` (both need a set row)
+          const bool next_f = fwd_active(bidir, level + 1, D), meet_b = back_active(bidir, level, D);
+          const bool keep = clen > 0 && (next_f || meet_b);
+          bool fresh = true;
+          if (keep) {
+            const int ins = gh_insert(H, mask, gh_key(epoch, false, slot, child));
+            if (ins < 0) ctl->overflow = 1;
+            fresh = ins > 0;
+          }
+          if (fresh) {
+            if (sig_maybe(x.sig, subj_sig(si.x))) {  // the signature rules out most misses
+              probes++;
+              if (dset_probe(s, child, si.x)) atomicExch(&sl.hit[slot], 1u);
+            }
+            // the backward set of hops 1..level-1 (backward turns 0..level-1 ran; hop 0 = the
+            // holders, which the probe above covers)
+            if (bidir && level >= 2) {
+              const int c = gh_contains(H, mask, gh_key(epoch, true, slot, child));
+              if (c < 0) ctl->overflow = 1;
+              if (c > 0) atomicExch(&sl.hit[slot], 1u);
+            }
+            app = keep && next_f;
+          }
         }
-        if (act && sig_maybe(x.sig, subj_sig(si.x))) {  // the signature rules out most misses
-          probes++;
-          if (dset_probe(s, child, si.x)) atomicExch(&slot_hit[slot], 1u);
+      } else {
+        // backward turn `level`: hop `level` parents (turn 0: the holders themselves)
+        const uint32_t p = level == 0 ? s.hold[rb + (e - beg)] : s.radj[rb + (e - beg)];
+        if (hit) {
+          act = false;
+        } else {
+          child = p;
+          if (p == sl.root[slot]) {
+            atomicExch(&sl.hit[slot], 1u);
+          } else {
+            const int ins = gh_insert(H, mask, gh_key(epoch, true, slot, p));
+            if (ins < 0) ctl->overflow = 1;
+            if (ins > 0) {
+              // the forward set (hops 0..level+1, nodes with a set row): a parent in it closes a path
+              const int c = gh_contains(H, mask, gh_key(epoch, false, slot, p));
+              if (c < 0) ctl->overflow = 1;
+              if (c > 0) atomicExch(&sl.hit[slot], 1u);
+              if (back_active(bidir, level + 1, D)) {
+                const uint64_t r0 = s.radj_off[p], r1 = s.radj_off[p + 1];
+                cb = (uint32_t)r0;
+                clen = (uint32_t)(r1 - r0);
+                app = clen > 0;
+              }
+            }
+          }
         }
       }
     }
-    grid_append(ctl, lg, nl, (level + 1) & 1, next_base, act && keep, slot, cb, clen);
+    const bool do_app = act && app;
+    if (do_app) {
+      if (BACK) sl.lastb[slot] = (uint32_t)level + 1;
+      else sl.lastf[slot] = (uint32_t)level + 1;
+    }
+    grid_append(ctl, lvs, lg, nl, (level + 1) & 1, next_base, do_app, slot, cb, clen);
   }
   for (int off = 32; off; off >>= 1) probes += __shfl_xor(probes, off, 64);
   if (lane == 0 && probes) atomicAdd(&ctl->probes8[blockIdx.x & 7][threadIdx.x >> 6], (unsigned long long)probes);
 }
 
-__global__ void k_grid_finish(const uint32_t* slot_q, const uint32_t* slot_hit, const uint32_t* d_count, uint32_t base,
-                              uint32_t G, uint8_t* out, uint32_t* err, const uint32_t* overflow) {
+__global__ void k_grid_finish(GridSlots sl, const uint32_t* d_count, uint32_t base, uint32_t G, uint8_t* out,
+                              uint32_t* err, const uint32_t* overflow) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= round_slots(d_count, base, G) || *overflow) return;
-  const uint32_t qi = slot_q[i];
-  out[qi] = slot_hit[i] ? KG_IS_MEMBER : KG_NOT_MEMBER;
+  const uint32_t qi = sl.q[i];
+  out[qi] = sl.hit[i] == 1 ? KG_IS_MEMBER : KG_NOT_MEMBER;
   if (err) err[qi] = KG_ERR_NONE;
 }
 
@@ -281,19 +404,23 @@ static uint64_t grid_full_cap(const Snapshot* s) {
 }
 constexpr uint32_t G0 = 0xFFFF;  // slot field is 16 bits
 
-struct GridView {  // pointers into a pool laid out for `cap` log entries
+struct GridView {  // pointers into a pool laid out for `cap` log entries (per direction)
   uint64_t cap = 0, hcap = 0;
   uint64_t* H = nullptr;
-  GridLog lg{};
-  uint2* slot_info = nullptr;
-  uint32_t *slot_q = nullptr, *slot_hit = nullptr;
+  GridLog lg{}, blg{};
+  GridSlots sl{};
   GridCtl* ctl = nullptr;
 };
 
-static int grid_layout(GridPool* P, uint64_t cap, hipStream_t stream, GridView* v) {
+// two: a backward log too (bidirectional rounds), and a visited table for both directions' nodes;
+// the table is sized for twice the logged entries (load <= 0.5).  The snapshot's full-size pool (one
+// query that overflowed a workspace's pool) runs forward only: two node-sized logs at C3's ~10^9 nodes
+// would take ~60 GB.
+static int grid_layout(GridPool* P, uint64_t cap, hipStream_t stream, GridView* v, bool two = true) {
   uint64_t hcap = 1;
-  while (hcap < 2 * cap) hcap <<= 1;  // hash >= 2x the log (load <= 0.5)
-  const size_t need = hcap * 8 + cap * (4 + 4 + 8) + 2 * TILE_CAP * 4 + (size_t)G0 * 16 + sizeof(GridCtl) + 4096;
+  while (hcap < (two ? 4 : 2) * cap) hcap <<= 1;
+  const size_t log_bytes = cap * (4 + 4 + 8) + 2 * TILE_CAP * 4;
+  const size_t need = hcap * 8 + (two ? 2 : 1) * log_bytes + (size_t)G0 * 28 + sizeof(GridCtl) + 4096;
   if (need > P->bytes) {
     P->release();
     HIPC(hipMalloc(&P->mem, need));
@@ -306,22 +433,29 @@ static int grid_layout(GridPool* P, uint64_t cap, hipStream_t stream, GridView* 
   v->hcap = hcap;
   v->H = (uint64_t*)p;
   p += hcap * 8;
-  v->lg.cap = cap;
-  v->lg.ex = (uint64_t*)p;
-  p += cap * 8;
-  v->lg.slot = (uint32_t*)p;
-  p += cap * 4;
-  v->lg.rb = (uint32_t*)p;
-  p += cap * 4;
-  v->lg.tile_first[0] = (uint32_t*)p;
-  p += TILE_CAP * 4;
-  v->lg.tile_first[1] = (uint32_t*)p;
-  p += TILE_CAP * 4;
-  v->slot_info = (uint2*)p;
+  v->blg = GridLog{};
+  for (GridLog* lg : {&v->lg, &v->blg}) {
+    if (lg == &v->blg && !two) break;
+    lg->cap = cap;
+    lg->ex = (uint64_t*)p;
+    p += cap * 8;
+    lg->slot = (uint32_t*)p;
+    p += cap * 4;
+    lg->rb = (uint32_t*)p;
+    p += cap * 4;
+    lg->tile_first[0] = (uint32_t*)p;
+    p += TILE_CAP * 4;
+    lg->tile_first[1] = (uint32_t*)p;
+    p += TILE_CAP * 4;
+  }
+  v->sl.info = (uint2*)p;
   p += (size_t)G0 * 8;
-  v->slot_q = (uint32_t*)p;
-  v->slot_hit = v->slot_q + G0;
-  p += (size_t)G0 * 8;
+  v->sl.q = (uint32_t*)p;
+  v->sl.hit = v->sl.q + G0;
+  v->sl.root = v->sl.hit + G0;
+  v->sl.lastf = v->sl.root + G0;
+  v->sl.lastb = v->sl.lastf + G0;
+  p += (size_t)G0 * 20;
   v->ctl = (GridCtl*)(((uintptr_t)p + 255) & ~uintptr_t(255));
   return 0;
 }
@@ -330,7 +464,7 @@ int grid_reserve(Snapshot* s) {
   HIPC(hipSetDevice(s->device));
   std::lock_guard<std::mutex> lk(s->giant_mu);
   GridView v;
-  if (int rc = grid_layout(&s->giant, grid_full_cap(s), s->stream, &v)) return rc;
+  if (int rc = grid_layout(&s->giant, grid_full_cap(s), s->stream, &v, false)) return rc;
   HIPC(hipStreamSynchronize(s->stream));
   return 0;
 }
@@ -357,6 +491,8 @@ int grid_tier(Snapshot* s, Workspace* w, const RQuery* rq, const uint32_t* qlist
   const uint64_t full_cap = grid_full_cap(s);
   const uint64_t small_cap = std::min<uint64_t>(full_cap, s->grid_small_cap ? s->grid_small_cap : 16ull << 20);
   GridPool* gp = &w->grid;
+  // bidirectional turns need the reverse indexes (holders, reverse set-adjacency)
+  const int bidir_ok = s->grid_bidir && s->ds.radj && s->ds.hold && s->ds.hslots ? 1 : 0;
   std::unique_lock<std::mutex> giant_lk(s->giant_mu, std::defer_lock);
   GridView v;
   if (int rc = grid_layout(gp, small_cap, stream, &v)) return rc;
@@ -367,27 +503,42 @@ int grid_tier(Snapshot* s, Workspace* w, const RQuery* rq, const uint32_t* qlist
    if (!resume) {
     if (phase == 1) w->grid_reran = false;
     if (phase == 2) w->grid_reran = true;  // rounds past the first: the caller re-reads the results
-    if (++gp->epoch == 0x10000) {  // epoch wrap: the table is zeroed once per 65535 rounds
+    if (++gp->epoch == GH_EPOCH_WRAP) {  // epoch wrap: the table is zeroed once per 32767 rounds
       HIPC(hipMemsetAsync(v.H, 0, v.hcap * 8, stream));
       gp->epoch = 1;
     }
     const uint64_t epoch = gp->epoch;
+    const int bidir = bidir_ok && gp != &s->giant ? 1 : 0;  // the full-size pool has no backward log
     const uint32_t slot_blocks = (G + 255) / 256;
+    const uint32_t lgrid = (uint32_t)s->n_cu * s->grid_wgs;
     HIPC(hipMemsetAsync(v.ctl, 0, sizeof(GridCtl), stream));
     hipLaunchKernelGGL(k_grid_init, dim3(slot_blocks), dim3(256), 0, stream, s->ds, rq, qlist, d_count, done, G, v.lg,
-                       v.slot_q, v.slot_info, v.slot_hit, v.H, v.hcap - 1, epoch, v.ctl);
+                       v.blg, v.sl, v.H, v.hcap - 1, epoch, v.ctl, bidir);
     HIPC(hipGetLastError());
     // Levels run back to back on the device (sizes never come back to the host; an empty level
-    // costs one near-empty launch).  Level k expands nodes at rest depth D-k >= 2, so at most
-    // global_max_depth-1 levels exist.
+    // costs one near-empty launch).  Forward only: level k expands nodes at rest depth D-k >= 2, so
+    // at most global_max_depth-1 levels exist.  Bidirectional: forward turn t while 2t <= D-1,
+    // backward turn t while 2t+1 <= D-1, alternating, each side's dry closure settled before its turn.
     const int max_levels = std::max(1, global_max_depth - 1);
-    for (int level = 0; level < max_levels; level++) {
-      hipLaunchKernelGGL(k_grid_level, dim3((uint32_t)s->n_cu * s->grid_wgs), dim3(256), 0, stream, s->ds, v.lg, level,
-                         v.slot_info, v.slot_hit, v.H, v.hcap - 1, epoch, v.ctl);
+    const int turns = bidir ? (global_max_depth - 1) / 2 + 1 : max_levels;
+    for (int t = 0; t < turns; t++) {
+      if (bidir && t > 0) {
+        hipLaunchKernelGGL(k_grid_settle, dim3(slot_blocks), dim3(256), 0, stream, v.sl, d_count, done, G, t, 0, bidir);
+        HIPC(hipGetLastError());
+      }
+      hipLaunchKernelGGL(k_grid_level<0>, dim3(lgrid), dim3(256), 0, stream, s->ds, v.lg, t, v.sl, v.H, v.hcap - 1,
+                         epoch, v.ctl, bidir);
       HIPC(hipGetLastError());
+      if (bidir && 2 * t + 1 <= global_max_depth - 1) {
+        hipLaunchKernelGGL(k_grid_settle, dim3(slot_blocks), dim3(256), 0, stream, v.sl, d_count, done, G, t, 1, bidir);
+        HIPC(hipGetLastError());
+        hipLaunchKernelGGL(k_grid_level<1>, dim3(lgrid), dim3(256), 0, stream, s->ds, v.blg, t, v.sl, v.H,
+                           v.hcap - 1, epoch, v.ctl, bidir);
+        HIPC(hipGetLastError());
+      }
     }
-    hipLaunchKernelGGL(k_grid_finish, dim3(slot_blocks), dim3(256), 0, stream, v.slot_q, v.slot_hit, d_count, done, G,
-                       out, err, &v.ctl->overflow);
+    hipLaunchKernelGGL(k_grid_finish, dim3(slot_blocks), dim3(256), 0, stream, v.sl, d_count, done, G, out, err,
+                       &v.ctl->overflow);
     HIPC(hipGetLastError());
     HIPC(hipMemcpyAsync(hb, v.ctl, sizeof(GridCtl), hipMemcpyDeviceToHost, stream));
     HIPC(hipMemcpyAsync(hb + sizeof(GridCtl) / 4, d_count, 4, hipMemcpyDeviceToHost, stream));
@@ -409,7 +560,7 @@ int grid_tier(Snapshot* s, Workspace* w, const RQuery* rq, const uint32_t* qlist
         // one query alone overflowed the workspace pool: rerun it in the shared full-size pool
         giant_lk.lock();
         gp = &s->giant;
-        if (int rc = grid_layout(gp, full_cap, stream, &v)) return rc;
+        if (int rc = grid_layout(gp, full_cap, stream, &v, false)) return rc;
         continue;
       }
       G = std::max<uint32_t>(1, std::min(G, cnt) / 4);

@@ -613,3 +613,52 @@ def test_bench_tune_set_vs_oracle(preset, n_tuples):
             dfs, _, _ = oracle.check_batch(q[:, :6], q[:, 6].view(np.int32), gmax, POLICY_DFS, nthreads=8)
             assert (dfs == exp).all()
         assert 0.05 < (out == 1).mean() < 0.95
+
+
+@pytest.mark.parametrize("bidir,grid_cap,seed", [(1, 0, 0), (1, 0, 1), (0, 0, 0), (1, 700, 2), (1, 0, 3)])
+def test_grid_bidirectional_dense_vs_oracle(bidir, grid_cap, seed):
+    """The grid tier's bidirectional rounds (kg_grid.hip) on dense graphs with cycles, hubs and
+    subjects held only by rows nothing points at: a tiny stream-tier edge budget and the backward
+    tier off send nearly every query there; every depth 2..9 is bit-exact with the oracle, with
+    grid_bidir on and off, and with a log small enough that rounds overflow and rerun (grid_cap)."""
+    rng = np.random.default_rng(900 + seed)
+    n_obj, n_users = 120, 60
+    tuples = []
+    for i in range(n_obj):
+        for _ in range(int(rng.integers(1, 14))):  # dense set edges, cycles included
+            tuples.append(f"g:o{i}#m@(g:o{int(rng.integers(n_obj))}#m)")
+        if rng.random() < 0.3:
+            tuples.append(f"g:o{i}#m@u{int(rng.integers(n_users))}")
+    for i in range(40):  # docs: roots that nothing points at, holding users directly too
+        for _ in range(int(rng.integers(1, 8))):
+            tuples.append(f"d:x{i}#v@(g:o{int(rng.integers(n_obj))}#m)")
+        tuples.append(f"d:x{i}#v@w{int(rng.integers(20))}")  # w*: held only by docs
+    tuples = [RelationTuple.from_string(t) for t in tuples]
+    reg = Registry(tuples, [])
+    snap = reg.snapshot
+    snap.tune("stream_ecap", 3)
+    snap.tune("back", 0)
+    snap.tune("grid_bidir", bidir)
+    snap.tune("grid_cap", grid_cap)
+    it = reg.interner
+    qs = []
+    for _ in range(2500):
+        root = f"d:x{int(rng.integers(40))}#v" if rng.random() < 0.6 else f"g:o{int(rng.integers(n_obj))}#m"
+        r = rng.random()
+        subj = f"u{int(rng.integers(n_users))}" if r < 0.7 else (f"w{int(rng.integers(20))}" if r < 0.9
+                                                                  else f"(g:o{int(rng.integers(n_obj))}#m)")
+        qs.append(RelationTuple.from_string(f"{root}@{subj}"))
+    q6 = np.asarray([it.tuple_ids(t) for t in qs], np.uint32)
+    depths = rng.integers(0, 10, len(qs))
+    oracle = Oracle(it.tuples_array(tuples), it.wildcard_rel)
+    grid = 0
+    for gmax in (2, 3, 4, 5, 6, 9):
+        e = Engine(snap, Config(gmax))
+        out, err = e.batch_check_ids(queries_array(q6, depths), with_stats=True)
+        exp, _, _ = oracle.check_batch(q6, depths, gmax, POLICY_CANONICAL)
+        bad = np.nonzero(out != exp)[0]
+        assert bad.size == 0 and (err == 0).all(), (gmax, [(str(qs[i]), int(depths[i]), int(out[i]), int(exp[i]))
+                                                            for i in bad[:8]])
+        grid += e.last_stats["n_grid"]
+        assert 0.05 < out.mean() < 0.95
+    assert grid > 1000
