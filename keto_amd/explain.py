@@ -28,7 +28,7 @@ from . import _lib
 from .ketoapi import (CheckTree, RelationTuple, SubjectSet, TREE_COMPUTED, TREE_INTERSECTION, TREE_LEAF, TREE_NOT,
                       TREE_TTU, TREE_UNION)
 from .mapper import SUBJECT_ID
-from .namespace import RW_AND, RW_COMPUTED, RW_NOT, RW_OR, RW_TTU
+from .namespace import HIDDEN_TTU_PREFIX, RW_AND, RW_COMPUTED, RW_NOT, RW_OR, RW_TTU
 
 M, N, E, U = "member", "not_member", "error", "unknown"
 Q = Tuple[int, int, int, int, int, int]  # (ns, obj, rel, sns, sobj, srel) ids
@@ -186,6 +186,13 @@ class Explainer:
     def _edge(self, idx: int, q: Q, d: int) -> Tuple[str, int, Optional[CheckTree]]:
         """One rewrite child behind WithEdge(request tuple, child type)."""
         kind, rel, crel, first, _count = (int(x) for x in self.prog.rw[idx])
+        if kind == RW_COMPUTED and self.it.rel_name(rel).startswith(HIDDEN_TTU_PREFIX):
+            # a lowered tuple-to-subject-set leaf (namespace.lower_ttu_leaves): the hidden relation holds
+            # no tuples, so its only member branch is its TTU -- the reference's tree has that TTU edge
+            # right here, without a computed edge in between
+            _k, root = self.relation(q[0], rel)
+            _kind, _r, _c, f2, _n = (int(x) for x in self.prog.rw[root])
+            return self._edge(int(self.prog.child[f2]), q, d)
         if kind == RW_COMPUTED:
             etype = TREE_COMPUTED
             m, e, t = self._computed(rel, q, d)

@@ -144,9 +144,57 @@ class Program:
         return not bool(self.ns_has_rel.any())
 
 
-def compile_program(namespaces: List[Namespace], interner) -> Program:
+HIDDEN_TTU_PREFIX = "\x1fttu/"  # hidden relations of lowered tuple-to-subject-set leaves (no tuple can name one)
+
+
+def _pure_union(c: Child) -> bool:
+    if isinstance(c, SubjectSetRewrite):
+        return c.operation == OP_OR and all(_pure_union(x) for x in c.children)
+    return isinstance(c, (ComputedSubjectSet, TupleToSubjectSet))
+
+
+def lower_ttu_leaves(namespaces: List[Namespace]) -> List[Namespace]:
+    """Boolean rewrites (and / not, rewrites.go:30-159) whose leaves include tuple-to-subject-sets:
+    every such TTU(rel, crel) leaf becomes computed(H) with H a hidden relation of the same namespace
+    whose rewrite is ``or(TTU(rel, crel))``.  For any depth d, checkIsAllowed((ns,obj,H), d) =
+    checkDirect(H) | checkExpandSubject(H) | TTU at d, and H holds no tuples, so it equals the TTU leaf
+    evaluated at d (rewrites.go:167-193 keeps the depth, :205-260 lowers it for the targets) -- but H is
+    a union, which kg_augment.hip materialises into plain union nodes, so the formula's leaves are all
+    computed and kg_formula.hip splits it into rewrite-free sub-checks (single GPU and hash-sharded)
+    instead of the interpreter.  Pure unions are left alone (materialised as they are)."""
+    out = []
+    for n in namespaces:
+        hidden: Dict[str, Relation] = {}
+
+        def lower(c: Child) -> Child:
+            if isinstance(c, SubjectSetRewrite):
+                return SubjectSetRewrite([lower(x) for x in c.children], c.operation)
+            if isinstance(c, InvertResult):
+                return InvertResult(lower(c.child))
+            if isinstance(c, TupleToSubjectSet):
+                name = f"{HIDDEN_TTU_PREFIX}{c.relation}/{c.computed_subject_set_relation}"
+                if name not in hidden:
+                    hidden[name] = Relation(name, [], SubjectSetRewrite([TupleToSubjectSet(c.relation, c.computed_subject_set_relation)]))
+                return ComputedSubjectSet(name)
+            return c
+
+        rels = []
+        for r in n.relations:
+            if r.rewrite is None or _pure_union(r.rewrite):
+                rels.append(r)
+            else:
+                rels.append(Relation(r.name, r.types, lower(r.rewrite)))
+        out.append(Namespace(n.name, rels + list(hidden.values()), n.id))
+    return out
+
+
+def compile_program(namespaces: List[Namespace], interner, lower_ttu: bool = True) -> Program:
     """Compile namespace configs into the flat rewrite program.  ``interner`` provides
-    ``ns_id(name)`` and ``rel_id(name)`` (see keto_amd.mapper.Interner)."""
+    ``ns_id(name)`` and ``rel_id(name)`` (see keto_amd.mapper.Interner).  lower_ttu: TTU leaves of
+    boolean rewrites become hidden union relations (lower_ttu_leaves; the oracle compiles without it,
+    so the parity tests check the lowering's semantics)."""
+    if lower_ttu:
+        namespaces = lower_ttu_leaves(namespaces)
     rw: List[List[int]] = []
     child: List[int] = []
     rel_ns: List[int] = []

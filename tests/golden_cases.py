@@ -28,7 +28,7 @@ class Case:
         self.case = case
         self.it = Interner()
         self.namespaces = [namespace_from_json(n) for n in case["namespaces"]]
-        self.prog = compile_program(self.namespaces, self.it)
+        self.prog = compile_program(self.namespaces, self.it, lower_ttu=False)  # the oracle: as written
         self.tuples = [RelationTuple.from_string(s) for s in case["tuples"]]
         self.arr = self.it.tuples_array(self.tuples)
 

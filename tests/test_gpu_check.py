@@ -329,7 +329,7 @@ def test_random_rewrites_vs_oracle(seed, unions, mat, monkeypatch):
     rels = ["r0", "r1", "r2", "r3"]
     it = Interner()
     namespaces = random_program(rng, nss, rels, unions_only=unions)
-    prog = compile_program(namespaces, it)
+    prog = compile_program(namespaces, it, lower_ttu=False)  # the oracle: TTU leaves as written
     n_obj, n_users = 30 + 10 * seed, 25
     tuples = []
     for _ in range(150 + 60 * seed):
@@ -434,7 +434,7 @@ def test_formula_rewrites_vs_oracle(seed, mat, monkeypatch):
             Relation("u3", rewrite=O([C("a"), T("parent", "zz")]))]
     namespaces = [Namespace("d", rels)]
     it = Interner()
-    prog = compile_program(namespaces, it)
+    prog = compile_program(namespaces, it, lower_ttu=False)  # the oracle: TTU leaves as written
     n_obj, n_users = 40 + 20 * seed, 20
     tuples = []
     for _ in range(400 + 150 * seed):
@@ -510,7 +510,7 @@ def test_opl_full_example_rewrites_vs_oracle():
                                          "opl_full_example.json")))
     namespaces = [namespace_from_json({"name": n, "relations": rels}) for n, rels in sorted(golden.items())]
     it = Interner()
-    prog = compile_program(namespaces, it)
+    prog = compile_program(namespaces, it, lower_ttu=False)  # the oracle: TTU leaves as written
     rng = np.random.default_rng(2024)
     files, folders, groups, users = [f"f{i}" for i in range(60)], [f"d{i}" for i in range(20)], \
         [f"g{i}" for i in range(15)], [f"u{i}" for i in range(30)]
@@ -651,7 +651,7 @@ def test_grid_bidirectional_dense_vs_oracle(bidir, grid_cap, seed):
     q6 = np.asarray([it.tuple_ids(t) for t in qs], np.uint32)
     depths = rng.integers(0, 10, len(qs))
     oracle = Oracle(it.tuples_array(tuples), it.wildcard_rel)
-    grid = 0
+    grid, allowed = 0, []
     for gmax in (2, 3, 4, 5, 6, 9):
         e = Engine(snap, Config(gmax))
         out, err = e.batch_check_ids(queries_array(q6, depths), with_stats=True)
@@ -660,5 +660,6 @@ def test_grid_bidirectional_dense_vs_oracle(bidir, grid_cap, seed):
         assert bad.size == 0 and (err == 0).all(), (gmax, [(str(qs[i]), int(depths[i]), int(out[i]), int(exp[i]))
                                                             for i in bad[:8]])
         grid += e.last_stats["n_grid"]
-        assert 0.05 < out.mean() < 0.95
+        allowed.append(out.mean())
     assert grid > 1000
+    assert min(allowed) < 0.5 < max(allowed) and 0.01 < min(allowed) and max(allowed) < 0.99, allowed

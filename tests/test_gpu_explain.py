@@ -125,7 +125,7 @@ def test_random_check_trees(seed, mat, monkeypatch):
     nss, rels = ["a", "b", "c"], ["r0", "r1", "r2", "r3"]
     it = Interner()
     namespaces = random_program(rng, nss, rels, unions_only=bool(seed % 2))
-    prog = compile_program(namespaces, it)
+    prog = compile_program(namespaces, it, lower_ttu=False)  # the oracle: TTU leaves as written
     n_obj, n_users = 20 + 5 * seed, 15
     tuples = []
     for _ in range(120 + 40 * seed):

@@ -59,11 +59,17 @@ def test_namespace_json_roundtrip_and_compile():
     assert isinstance(ns.relations[2].rewrite.children[1], InvertResult)
     assert namespace_from_json(namespace_to_json(ns)) == ns
     it = Interner()
-    p = compile_program([ns], it)
+    p = compile_program([ns], it, lower_ttu=False)
     assert p.ns_has_rel[it.ns_id("acl")] == 1
     assert list(p.rel_root) == [-1, -1, 0]
     kinds = list(p.rw[:, 0])
     assert kinds == [1, 2, 4, 2, 3]  # and, computed, not, computed(deny), ttu
+    # lowered (the engine's program): the TTU leaf of the `and` becomes computed(hidden), a hidden relation
+    # of the same namespace whose rewrite is or(ttu) -- a union the engine materialises
+    pl = compile_program([ns], it)
+    assert list(pl.rw[:, 0]) == [1, 2, 4, 2, 2, 0, 3]
+    hidden = it.rel_id("\x1fttu/parent/access")
+    assert int(pl.rw[4, 1]) == hidden and list(pl.rel_rel)[-1] == hidden and list(pl.rel_root)[-1] == 5
     # single child without operator is wrapped into an "or" (ast_definitions.go:59-68)
     ns2 = namespace_from_json({"name": "d", "relations": [{"name": "v", "rewrite": {"relation": "o"}}]})
     assert ns2.relations[0].rewrite.operation == "or"
