@@ -241,7 +241,10 @@ int kg_shard_level(kg_snapshot* sp, const kg_frec* d_in, size_t n_in, const uint
   if (!sp || !d_counts || !d_res || !d_err || (n_in && (!d_in || !d_out))) return set_error(-2, "NULL argument");
   Snapshot* s = reinterpret_cast<Snapshot*>(sp);
   std::lock_guard<std::mutex> lk(s->mu);
-  if (!s->shard_vis) return set_error(-2, "kg_shard_level before kg_shard_seed");
+  {
+    kg::ShardCtx* c = s->shard_ctx((hipStream_t)stream, false);
+    if (!c || !c->vis) return set_error(-2, "kg_shard_level before kg_shard_seed (on this stream)");
+  }
   return kg::shard_level(s, d_in, n_in, d_n_in, d_out, cap, d_counts, d_res, d_err, d_done, done_words,
                          (hipStream_t)stream);
   KG_GUARD_END
@@ -256,7 +259,10 @@ int kg_shard_level_seg(kg_snapshot* sp, const kg_frec* d_in, uint32_t n_seg, siz
   if (n_seg < 1 || n_seg > KG_SHARD_MAX_RANKS || seg_cap == 0) return set_error(-2, "n_seg in [1, %d], seg_cap > 0", KG_SHARD_MAX_RANKS);
   Snapshot* s = reinterpret_cast<Snapshot*>(sp);
   std::lock_guard<std::mutex> lk(s->mu);
-  if (!s->shard_vis) return set_error(-2, "kg_shard_level_seg before kg_shard_seed");
+  {
+    kg::ShardCtx* c = s->shard_ctx((hipStream_t)stream, false);
+    if (!c || !c->vis) return set_error(-2, "kg_shard_level_seg before kg_shard_seed (on this stream)");
+  }
   return kg::shard_level(s, d_in, (size_t)n_seg * seg_cap, d_seg_counts, d_out, cap, d_counts, d_res, d_err, d_done,
                          done_words, (hipStream_t)stream, n_seg, seg_cap);
   KG_GUARD_END
@@ -299,7 +305,10 @@ int kg_shard_back_level(kg_snapshot* sp, const kg_frec* d_in, size_t n_in, const
   if (!sp || !d_counts || !d_res || !d_err || (n_in && (!d_in || !d_out))) return set_error(-2, "NULL argument");
   Snapshot* s = reinterpret_cast<Snapshot*>(sp);
   std::lock_guard<std::mutex> lk(s->mu);
-  if (!s->shard_vis) return set_error(-2, "kg_shard_back_level before kg_shard_seed");
+  {
+    kg::ShardCtx* c = s->shard_ctx((hipStream_t)stream, false);
+    if (!c || !c->vis) return set_error(-2, "kg_shard_back_level before kg_shard_seed (on this stream)");
+  }
   return kg::shard_back_level(s, d_in, n_in, d_n_in, d_out, cap, d_counts, d_res, d_err, d_done, done_words,
                               (hipStream_t)stream);
   KG_GUARD_END

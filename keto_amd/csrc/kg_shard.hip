@@ -681,37 +681,37 @@ __global__ void k_shard_finish(uint32_t n, uint8_t* res, uint32_t* err, ShardFor
 }
 
 // The formula split's tables for a batch of n queries (plans only when the snapshot has them).
-static int shard_formula(Snapshot* s, size_t n, ShardFormula* F) {
+static int shard_formula(Snapshot* s, ShardCtx* c, size_t n, ShardFormula* F) {
   *F = ShardFormula{nullptr, nullptr, 0, s->d_virt, nullptr};
   if (!s->n_fplans) return 0;
-  if (n > s->shard_ref_n) {
-    if (s->shard_ref) s->free_alloc(s->shard_ref);
-    s->shard_ref = nullptr;
-    s->shard_ref_n = 0;
-    if (s->alloc((void**)&s->shard_ref, std::max<size_t>(n, 1024) * 4)) return -1;
-    s->shard_ref_n = std::max<size_t>(n, 1024);
+  if (n > c->ref_n) {
+    if (c->ref) HIPC(hipFree(c->ref));
+    c->ref = nullptr;
+    c->ref_n = 0;
+    HIPC(hipMalloc((void**)&c->ref, std::max<size_t>(n, 1024) * 4));
+    c->ref_n = std::max<size_t>(n, 1024);
   }
-  *F = ShardFormula{s->d_fidx, (const FPlan*)s->d_fplans, 1 + s->fp_leaves, s->d_virt, s->shard_ref};
+  *F = ShardFormula{s->d_fidx, (const FPlan*)s->d_fplans, 1 + s->fp_leaves, s->d_virt, c->ref};
   return 0;
 }
 
 size_t shard_result_slots(const Snapshot* s, size_t n) { return s->n_fplans ? n * (2 + (size_t)s->fp_leaves) : n; }
 
-static int shard_vis_prepare(Snapshot* s, hipStream_t stream) {
+static int shard_vis_prepare(Snapshot* s, ShardCtx* c, hipStream_t stream) {
   // per-batch (query, node) table of 2^shard_vis_log2 slots (kg_snapshot_tune "shard_vis",
   // default 2^23 = 64 MiB); an overflow is reported in the flags and the driver grows it
   const uint64_t slots = 1ull << s->shard_vis_log2;
-  if (s->shard_vis && s->shard_vis_slots != slots) {
-    HIPC(hipFree(s->shard_vis));
-    s->shard_vis = nullptr;
+  if (c->vis && c->vis_slots != slots) {
+    HIPC(hipFree(c->vis));
+    c->vis = nullptr;
   }
-  if (!s->shard_vis) {
-    HIPC(hipMalloc(&s->shard_vis, slots * 8));
-    s->shard_vis_slots = slots;
+  if (!c->vis) {
+    HIPC(hipMalloc(&c->vis, slots * 8));
+    c->vis_slots = slots;
   }
-  HIPC(hipMemsetAsync(s->shard_vis, 0xFF, s->shard_vis_slots * 8, stream));
-  if (!s->shard_heavy) {
-    HIPC(hipMalloc(&s->shard_heavy, (size_t)SHARD_HEAVY_CAP * sizeof(HeavyRow) + 64));
+  HIPC(hipMemsetAsync(c->vis, 0xFF, c->vis_slots * 8, stream));
+  if (!c->heavy) {
+    HIPC(hipMalloc(&c->heavy, (size_t)SHARD_HEAVY_CAP * sizeof(HeavyRow) + 64));
   }
   return 0;
 }
@@ -727,25 +727,27 @@ int shard_seed(Snapshot* s, const kg_query* d_q, size_t n, int32_t gdepth, kg_fr
   if (slots > Q_MASK) return set_error(-2, "sharded batch too large (%zu result slots > %u)", slots, Q_MASK);
   HIPC(hipSetDevice(s->device));
   if (!stream) stream = s->stream;
-  if (int rc = shard_vis_prepare(s, stream)) return rc;
+  ShardCtx* c = s->shard_ctx(stream);  // this stream's batch state (batches in flight on other streams)
+  if (!c) return set_error(-4, "sharded batch state");
+  if (int rc = shard_vis_prepare(s, c, stream)) return rc;
   HIPC(hipMemsetAsync(d_counts, 0, (s->shard_n + 1) * 4, stream));
-  s->shard_final = false;
+  c->final = false;
   uint4* qinfo = nullptr;
   if (shard_escalates(s)) {
-    if (!s->shard_qcnt) HIPC(hipMalloc(&s->shard_qcnt, (4ull << QCNT_LOG2)));
-    HIPC(hipMemsetAsync(s->shard_qcnt, 0, (4ull << QCNT_LOG2), stream));
-    if (slots > s->shard_qinfo_n) {
-      if (s->shard_qinfo) HIPC(hipFree(s->shard_qinfo));
-      s->shard_qinfo = nullptr;
-      s->shard_qinfo_n = 0;
-      HIPC(hipMalloc(&s->shard_qinfo, std::max<size_t>(slots, 1024) * sizeof(uint4)));
-      s->shard_qinfo_n = std::max<size_t>(slots, 1024);
+    if (!c->qcnt) HIPC(hipMalloc(&c->qcnt, (4ull << QCNT_LOG2)));
+    HIPC(hipMemsetAsync(c->qcnt, 0, (4ull << QCNT_LOG2), stream));
+    if (slots > c->qinfo_n) {
+      if (c->qinfo) HIPC(hipFree(c->qinfo));
+      c->qinfo = nullptr;
+      c->qinfo_n = 0;
+      HIPC(hipMalloc(&c->qinfo, std::max<size_t>(slots, 1024) * sizeof(uint4)));
+      c->qinfo_n = std::max<size_t>(slots, 1024);
     }
-    qinfo = (uint4*)s->shard_qinfo;
+    qinfo = (uint4*)c->qinfo;
     if (slots > n) HIPC(hipMemsetAsync(qinfo + n, 0, (slots - n) * sizeof(uint4), stream));
   }
   ShardFormula F;
-  if (shard_formula(s, n, &F)) return -1;
+  if (shard_formula(s, c, n, &F)) return -1;
   if (slots > n) {  // the split parts' slots start NotMember / no error
     HIPC(hipMemsetAsync(d_res + n, 0, slots - n, stream));
     HIPC(hipMemsetAsync(d_err + n, 0, (slots - n) * 4, stream));
@@ -766,18 +768,20 @@ int shard_level(Snapshot* s, const kg_frec* d_in, size_t n_in, const uint32_t* d
                 hipStream_t stream, uint32_t n_seg, size_t seg_cap) {
   HIPC(hipSetDevice(s->device));
   if (!stream) stream = s->stream;
+  ShardCtx* c = s->shard_ctx(stream);  // this stream's batch state (batches in flight on other streams)
+  if (!c) return set_error(-4, "sharded batch state");
   // the bucket sizes restart; the flags word (counts[shard_n]: dropped records, visited table full)
   // accumulates over the batch's levels, so the caller reads it once at the end
   HIPC(hipMemsetAsync(d_counts, 0, s->shard_n * 4, stream));
   if (n_in) {
-    HeavyRow* heavy = (HeavyRow*)s->shard_heavy;
+    HeavyRow* heavy = (HeavyRow*)c->heavy;
     uint32_t* heavy_n = (uint32_t*)(heavy + SHARD_HEAVY_CAP);
     HIPC(hipMemsetAsync(heavy_n, 0, 4, stream));
     const uint32_t grid = (uint32_t)std::min<uint64_t>((n_in + 255) / 256, (uint64_t)s->n_cu * 8);
     hipLaunchKernelGGL(k_shard_level, dim3(grid), dim3(256), 0, stream, s->ds, d_in, (uint64_t)n_in, d_n_in, d_out,
-                       (uint64_t)cap, d_counts, d_res, d_err, (uint64_t*)s->shard_vis, s->shard_vis_slots - 1,
-                       d_done, d_done ? done_words : 0u, heavy, heavy_n, SHARD_HEAVY_CAP, (uint32_t*)s->shard_qcnt,
-                       shard_escalates(s) && s->shard_qcnt && !s->shard_final ? s->shard_budget : 0u,
+                       (uint64_t)cap, d_counts, d_res, d_err, (uint64_t*)c->vis, c->vis_slots - 1,
+                       d_done, d_done ? done_words : 0u, heavy, heavy_n, SHARD_HEAVY_CAP, (uint32_t*)c->qcnt,
+                       shard_escalates(s) && c->qcnt && !c->final ? s->shard_budget : 0u,
                        s->shard_vis_mode ? 1u : 0u, n_seg, (uint64_t)seg_cap);
     HIPC(hipGetLastError());
     hipLaunchKernelGGL(k_shard_heavy, dim3((uint32_t)s->n_cu * 4), dim3(256), 0, stream, s->ds, heavy, heavy_n,
@@ -806,13 +810,15 @@ int shard_back_list(Snapshot* s, size_t n, const uint8_t* d_res, const uint32_t*
                     uint32_t* d_counts, hipStream_t stream) {
   HIPC(hipSetDevice(s->device));
   if (!stream) stream = s->stream;
+  ShardCtx* c = s->shard_ctx(stream);  // this stream's batch state (batches in flight on other streams)
+  if (!c) return set_error(-4, "sharded batch state");
   HIPC(hipMemsetAsync(d_counts, 0, 8, stream));
-  if (!s->shard_vis) return set_error(-2, "kg_shard_back_list before kg_shard_seed");
-  HIPC(hipMemsetAsync(s->shard_vis, 0xFF, s->shard_vis_slots * 8, stream));  // backward keys start clear
-  if (s->shard_qcnt) HIPC(hipMemsetAsync(s->shard_qcnt, 0, (4ull << QCNT_LOG2), stream));  // reverse-edge counts
-  if (n && shard_escalates(s) && s->shard_qinfo && n <= s->shard_qinfo_n) {
+  if (!c->vis) return set_error(-2, "kg_shard_back_list before kg_shard_seed");
+  HIPC(hipMemsetAsync(c->vis, 0xFF, c->vis_slots * 8, stream));  // backward keys start clear
+  if (c->qcnt) HIPC(hipMemsetAsync(c->qcnt, 0, (4ull << QCNT_LOG2), stream));  // reverse-edge counts
+  if (n && shard_escalates(s) && c->qinfo && n <= c->qinfo_n) {
     hipLaunchKernelGGL(k_shard_back_list, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, stream, (uint32_t)n, d_res,
-                       d_err, (const uint4*)s->shard_qinfo, s->shard_rank, d_list, (uint64_t)cap, d_counts);
+                       d_err, (const uint4*)c->qinfo, s->shard_rank, d_list, (uint64_t)cap, d_counts);
     HIPC(hipGetLastError());
   }
   return 0;
@@ -822,13 +828,15 @@ int shard_refwd_seed(Snapshot* s, size_t n, const uint8_t* d_res, const uint32_t
                      uint32_t* d_counts, hipStream_t stream) {
   HIPC(hipSetDevice(s->device));
   if (!stream) stream = s->stream;
+  ShardCtx* c = s->shard_ctx(stream);  // this stream's batch state (batches in flight on other streams)
+  if (!c) return set_error(-4, "sharded batch state");
   HIPC(hipMemsetAsync(d_counts, 0, (s->shard_n + 1) * 4, stream));
-  if (!s->shard_vis) return set_error(-2, "kg_shard_refwd_seed before kg_shard_seed");
-  HIPC(hipMemsetAsync(s->shard_vis, 0xFF, s->shard_vis_slots * 8, stream));  // forward keys start clear again
-  s->shard_final = true;  // kg_shard_level runs without escalation until the next kg_shard_seed
-  if (n && shard_escalates(s) && s->shard_qinfo && n <= s->shard_qinfo_n) {
+  if (!c->vis) return set_error(-2, "kg_shard_refwd_seed before kg_shard_seed");
+  HIPC(hipMemsetAsync(c->vis, 0xFF, c->vis_slots * 8, stream));  // forward keys start clear again
+  c->final = true;  // kg_shard_level runs without escalation until the next kg_shard_seed
+  if (n && shard_escalates(s) && c->qinfo && n <= c->qinfo_n) {
     hipLaunchKernelGGL(k_shard_refwd_seed, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, stream, s->ds, (uint32_t)n,
-                       d_res, d_err, (const uint4*)s->shard_qinfo, d_out, (uint64_t)cap, d_counts);
+                       d_res, d_err, (const uint4*)c->qinfo, d_out, (uint64_t)cap, d_counts);
     HIPC(hipGetLastError());
   }
   return 0;
@@ -853,17 +861,19 @@ int shard_back_level(Snapshot* s, const kg_frec* d_in, size_t n_in, const uint32
                      hipStream_t stream) {
   HIPC(hipSetDevice(s->device));
   if (!stream) stream = s->stream;
+  ShardCtx* c = s->shard_ctx(stream);  // this stream's batch state (batches in flight on other streams)
+  if (!c) return set_error(-4, "sharded batch state");
   // the bucket size restarts; the flags word (d_counts[1]) accumulates over the phase
   HIPC(hipMemsetAsync(d_counts, 0, 4, stream));
   if (n_in && s->ds.radj) {
-    HeavyRow* heavy = (HeavyRow*)s->shard_heavy;
+    HeavyRow* heavy = (HeavyRow*)c->heavy;
     uint32_t* heavy_n = (uint32_t*)(heavy + SHARD_HEAVY_CAP);
     HIPC(hipMemsetAsync(heavy_n, 0, 4, stream));
     const uint32_t grid = (uint32_t)std::min<uint64_t>((n_in + 255) / 256, (uint64_t)s->n_cu * 8);
     hipLaunchKernelGGL(k_shard_back_level, dim3(grid), dim3(256), 0, stream, s->ds, d_in, (uint64_t)n_in, d_n_in, d_out,
-                       (uint64_t)cap, d_counts, d_res, d_err, (uint64_t*)s->shard_vis, s->shard_vis_slots - 1, d_done,
-                       d_done ? done_words : 0u, heavy, heavy_n, SHARD_HEAVY_CAP, (uint32_t*)s->shard_qcnt,
-                       s->shard_qcnt ? s->shard_back_budget : 0u, s->shard_vis_mode ? 1u : 0u);
+                       (uint64_t)cap, d_counts, d_res, d_err, (uint64_t*)c->vis, c->vis_slots - 1, d_done,
+                       d_done ? done_words : 0u, heavy, heavy_n, SHARD_HEAVY_CAP, (uint32_t*)c->qcnt,
+                       c->qcnt ? s->shard_back_budget : 0u, s->shard_vis_mode ? 1u : 0u);
     HIPC(hipGetLastError());
     hipLaunchKernelGGL(k_shard_heavy, dim3((uint32_t)s->n_cu * 4), dim3(256), 0, stream, s->ds, heavy, heavy_n,
                        SHARD_HEAVY_CAP, d_out, (uint64_t)cap, d_counts, d_res, d_err, 1u);
@@ -896,9 +906,11 @@ int shard_held(Snapshot* s, uint32_t* d_bits, size_t words, int import, hipStrea
 int shard_finish(Snapshot* s, size_t n, uint8_t* d_res, uint32_t* d_err, hipStream_t stream) {
   HIPC(hipSetDevice(s->device));
   if (!stream) stream = s->stream;
+  ShardCtx* c = s->shard_ctx(stream);  // this stream's batch state (batches in flight on other streams)
+  if (!c) return set_error(-4, "sharded batch state");
   if (n) {
     ShardFormula F;
-    if (shard_formula(s, n, &F)) return -1;
+    if (shard_formula(s, c, n, &F)) return -1;
     hipLaunchKernelGGL(k_shard_finish, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, stream, (uint32_t)n, d_res,
                        d_err, F);
     HIPC(hipGetLastError());

@@ -134,6 +134,22 @@ struct HostMap {
   }
 };
 
+// One stream's hash-sharded batch state (kg_shard.hip).
+struct ShardCtx {
+  hipStream_t stream = nullptr;
+  int device = -1;
+  void* vis = nullptr;  // per-batch visited table of (query, node)
+  uint64_t vis_slots = 0;
+  void* heavy = nullptr;  // hub rows a level hands to k_shard_heavy (+ count)
+  void* qcnt = nullptr;   // per-batch escalation counters (hashed by query)
+  void* qinfo = nullptr;  // per query slot (root, subject, depth, seeded)
+  size_t qinfo_n = 0;
+  bool final = false;      // the batch's final forward phase (kg_shard_refwd_seed): no escalation
+  uint32_t* ref = nullptr;  // formula split: plan of every query of the batch
+  size_t ref_n = 0;
+  ~ShardCtx();
+};
+
 struct Snapshot;
 // Host-buffer batches (kg_check_batch, kg_expand_batch): a call checks out one lane set (one lane per
 // replica -- its own HIP stream, hence its own batch workspace, pinned staging for queries and
@@ -173,8 +189,6 @@ struct Snapshot {
   int materialize = 1;  // rewrite materialisation at build (KG_MATERIALIZE=0 turns it off)
   std::vector<uint8_t> h_virt;  // [n_ns * n_rel] materialised union relations (kg_augment.hip)
   uint8_t* d_virt = nullptr;    // the same on the device (hash-sharded seed)
-  uint32_t* shard_ref = nullptr;  // hash-sharded formula split: plan of every query of the batch
-  size_t shard_ref_n = 0;
   // boolean rewrites over union / plain relations (kg_formula.hip): per (ns, rel) plan index or -1
   int32_t* d_fidx = nullptr;
   void* d_fplans = nullptr;
@@ -199,19 +213,16 @@ struct Snapshot {
   int light_tier = 0;  // kg_snapshot_tune("light"): 0 k_stream, 1 k_light<16>  // grid tier visited-table epoch (kg_grid.hip)
   uint64_t batch_seq = 0;
   uint32_t shard_rank = 0, shard_n = 1;  // hash-sharded mode (set before create)
-  void* shard_vis = nullptr;             // kg_shard.hip: per-batch visited table of (query, node)
-  uint64_t shard_vis_slots = 0;
-  void* shard_heavy = nullptr;           // kg_shard.hip: hub rows a level hands to k_shard_heavy (+ count)
+  // per-stream batch state of the hash-sharded mode (kg_shard.hip), so batches on different streams
+  // can be in flight at once; created by the first kg_shard_seed on a stream
+  std::vector<ShardCtx*> shard_ctxs;
+  ShardCtx* shard_ctx(hipStream_t st, bool create = true);  // st == NULL: the snapshot's stream
   uint32_t* shard_held = nullptr;  // holder bitmap OR-ed over every rank (kg_shard_held), or null
   uint32_t shard_held_n = 0;
   int shard_vis_log2 = 23;
   int shard_vis_mode = 0;  // kg_snapshot_tune("shard_vis_mode"): (query, node) dedup 0 = exact CAS table, 1 = lossy cache
   uint32_t shard_budget = 0;       // kg_snapshot_tune("shard_budget"): forward set edges per query and rank (0 = off)
   uint32_t shard_back_budget = 1u << 14;  // kg_snapshot_tune("shard_back_budget"): reverse edges per query and rank
-  bool shard_final = false;        // the batch's final forward phase (kg_shard_refwd_seed): no escalation
-  void* shard_qcnt = nullptr;      // kg_shard.hip: per-batch escalation counters (hashed by query)
-  void* shard_qinfo = nullptr;     // kg_shard.hip: per query slot (root, subject, depth, seeded)
-  size_t shard_qinfo_n = 0;
   int stream_variant = 12;  // kg_snapshot_tune("stream"): k_stream variant (0..8), 9 / 11 / 12 = k_stream2, 10 = k_stream3
   int back_tier = 2;  // kg_snapshot_tune("back"): backward tier (1: wave + workgroup widths, 2: wave only) + no-holder filter
   uint32_t stream_ecap = 512;  // kg_snapshot_tune("stream_ecap"): stream-tier edge budget per query (0 = none)

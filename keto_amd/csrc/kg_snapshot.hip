@@ -12,6 +12,7 @@
 #include <algorithm>
 #include <cstring>
 #include <memory>
+#include <new>
 #include <vector>
 
 #include "kg_internal.h"
@@ -240,10 +241,7 @@ Snapshot::~Snapshot() {
   if (device >= 0) hipSetDevice(device);
   for (auto& a : allocs) hipFree(a.first);
   for (Workspace* w : wss) delete w;
-  if (shard_vis) hipFree(shard_vis);
-  if (shard_heavy) hipFree(shard_heavy);
-  if (shard_qcnt) hipFree(shard_qcnt);
-  if (shard_qinfo) hipFree(shard_qinfo);
+  for (ShardCtx* c : shard_ctxs) delete c;
   giant.release();
   if (stream) hipStreamDestroy(stream);
 }
@@ -360,6 +358,26 @@ void Snapshot::lanes_release(std::vector<Lane*>* v) {
     lane_free.push_back(v);
   }
   lane_cv.notify_one();
+}
+
+ShardCtx::~ShardCtx() {
+  if (device >= 0) hipSetDevice(device);
+  for (void* p : {vis, heavy, qcnt, qinfo, (void*)ref})
+    if (p) hipFree(p);
+}
+
+ShardCtx* Snapshot::shard_ctx(hipStream_t st, bool create) {
+  if (!st) st = stream;
+  std::lock_guard<std::mutex> lk(ws_mu);
+  for (ShardCtx* c : shard_ctxs)
+    if (c->stream == st) return c;
+  if (!create) return nullptr;
+  ShardCtx* c = new (std::nothrow) ShardCtx();
+  if (!c) return nullptr;
+  c->stream = st;
+  c->device = device;
+  shard_ctxs.push_back(c);
+  return c;
 }
 
 Workspace* Snapshot::workspace(hipStream_t st) {
