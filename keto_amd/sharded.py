@@ -156,7 +156,7 @@ class ShardedChecker:
     for a single rank; device = the torch device the records live on."""
 
     def __init__(self, ops, rank: int = 0, world: int = 1, dist=None, device="cuda", cap: int = 1 << 20,
-                 protocol: str = "auto"):
+                 protocol: str = "auto", group=None):
         """protocol (world > 1): "fixed" = every level exchanges fixed-size buckets (records per destination
         <= bucket) and the batch runs gdepth + 1 levels with no host round trip inside it (counts, flags and
         termination stay on the device; one readback at the end); "dynamic" = one metadata exchange and
@@ -166,6 +166,10 @@ class ShardedChecker:
             raise ValueError("at most %d ranks" % _lib.KG_SHARD_MAX_RANKS)
         self.ops, self.rank, self.world, self.dist, self.device, self.cap = ops, rank, world, dist, device, cap
         self.protocol = protocol
+        # process group of this checker's collectives (None: the default group).  Batches in flight at
+        # once on one rank each need their own group (and ops on their own stream): collectives of
+        # one group are matched across ranks in issue order
+        self.group = group
         self.bucket = None  # fixed protocol: records per destination per level (learned per batch)
         self.levels = 0
         self.records_sent = 0
@@ -180,13 +184,13 @@ class ShardedChecker:
         import torch
         dev = self.device if not self._host_staged() else "cpu"
         w = torch.tensor([self.ops.held_words()], dtype=torch.int64, device=dev)
-        self.dist.all_reduce(w, op=self.dist.ReduceOp.MAX)
+        self.dist.all_reduce(w, op=self.dist.ReduceOp.MAX, group=self.group)
         words = int(w.item())
         mine = self.ops.held_export(words)
         if self._host_staged():
             mine = mine.cpu()
         allb = [torch.empty(words, dtype=torch.int32, device=mine.device) for _ in range(self.world)]
-        self.dist.all_gather(allb, mine.contiguous())
+        self.dist.all_gather(allb, mine.contiguous(), group=self.group)
         acc = allb[0].clone()
         for r in range(1, self.world):
             acc |= allb[r]
@@ -204,7 +208,7 @@ class ShardedChecker:
         if staged:
             mine = mine.cpu()
         parts = [torch.empty(words, dtype=torch.int32, device=mine.device) for _ in range(self.world)]
-        self.dist.all_gather(parts, mine.contiguous())
+        self.dist.all_gather(parts, mine.contiguous(), group=self.group)
         allb = torch.cat(parts)
         return allb.to(self.device) if staged else allb
 
@@ -231,7 +235,7 @@ class ShardedChecker:
         if self.dist is None:
             recv.copy_(meta)
         else:
-            self.dist.all_to_all_single(recv, meta)
+            self.dist.all_to_all_single(recv, meta, group=self.group)
         h = torch.cat([c[:N], recv.flatten()]).cpu().numpy()  # the level's host round trip
         self.host_syncs += 1
         send = [int(x) for x in h[:N]]
@@ -252,7 +256,7 @@ class ShardedChecker:
         if staged:
             send = send.cpu()
         recv = torch.empty((sum(recv_splits), REC_WORDS), dtype=torch.int32, device=send.device)
-        self.dist.all_to_all_single(recv, send, recv_splits, send_splits)
+        self.dist.all_to_all_single(recv, send, recv_splits, send_splits, group=self.group)
         return recv.to(self.device) if staged else recv
 
     def _all_gather_rows(self, t, n: int, flags: int):
@@ -264,7 +268,7 @@ class ShardedChecker:
         staged = self._host_staged()
         meta = torch.tensor([n, flags], dtype=torch.int64, device="cpu" if staged else self.device)
         metas = [torch.empty_like(meta) for _ in range(self.world)]
-        self.dist.all_gather(metas, meta)
+        self.dist.all_gather(metas, meta, group=self.group)
         h = torch.stack(metas).cpu().numpy()
         self.host_syncs += 1
         sizes = [int(x) for x in h[:, 0]]
@@ -279,7 +283,7 @@ class ShardedChecker:
         if staged:
             mine = mine.cpu()
         parts = [torch.empty_like(mine) for _ in range(self.world)]
-        self.dist.all_gather(parts, mine)
+        self.dist.all_gather(parts, mine, group=self.group)
         allr = torch.cat([parts[r][:sizes[r]] for r in range(self.world)])
         return (allr.to(self.device) if staged else allr), 0
 
@@ -467,7 +471,7 @@ class ShardedChecker:
         cache = self.__dict__.setdefault("_slots_cache", {})
         if slots not in cache:
             t = torch.tensor([slots], dtype=torch.int64, device="cpu" if self._host_staged() else self.device)
-            self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+            self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX, group=self.group)
             self.host_syncs += 1
             cache[slots] = int(t.item())
         return cache[slots]
@@ -504,14 +508,14 @@ class ShardedChecker:
             acc[1] = torch.maximum(acc[1], c64.max())
             acc[2] += c64.sum()
             sc = c[:N].contiguous()
-            self.dist.all_to_all_single(rc, sc.cpu() if staged else sc)
+            self.dist.all_to_all_single(rc, sc.cpu() if staged else sc, group=self.group)
             snd = bufs[cur].cpu() if staged else bufs[cur]
-            self.dist.all_to_all_single(recv, snd)
+            self.dist.all_to_all_single(recv, snd, group=self.group)
             done = None
             if prune and k > 0:
                 mine = self.ops.done_bits(res, slots, words)
                 parts = torch.empty(N * words, dtype=torch.int32, device=xdev)
-                self.dist.all_gather_into_tensor(parts, mine.cpu() if staged else mine)
+                self.dist.all_gather_into_tensor(parts, mine.cpu() if staged else mine, group=self.group)
                 done = parts.to(self.device) if staged else parts
             nxt = cur ^ 1
             self.ops.level_seg(recv.to(self.device) if staged else recv, N, B, rc.to(self.device) if staged else rc,
@@ -523,7 +527,7 @@ class ShardedChecker:
         left = c[:N].to(torch.int64).sum()
         # over ranks: each flag bit (bucket / visited-table overflow), the largest bucket, records left
         tot = torch.stack([acc[0] & 1, (acc[0] >> 1) & 1, acc[1], left]).to(xdev)
-        self.dist.all_reduce(tot, op=self.dist.ReduceOp.MAX)
+        self.dist.all_reduce(tot, op=self.dist.ReduceOp.MAX, group=self.group)
         h = torch.cat([tot, acc[2:3].to(xdev)]).cpu().numpy()  # the batch's one host round trip
         self.host_syncs += 1
         flags = int(h[0]) | (int(h[1]) << 1)
