@@ -662,4 +662,4 @@ def test_grid_bidirectional_dense_vs_oracle(bidir, grid_cap, seed):
         grid += e.last_stats["n_grid"]
         allowed.append(out.mean())
     assert grid > 1000
-    assert min(allowed) < 0.5 < max(allowed) and 0.01 < min(allowed) and max(allowed) < 0.99, allowed
+    assert 0.01 < min(allowed) and 0.2 < max(allowed) < 0.99, allowed
