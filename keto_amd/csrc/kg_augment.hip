@@ -369,6 +369,7 @@ int Snapshot::augment_rewrites() {
   h_virt = virt;  // the formula splitter's leaves may be union relations (kg_formula.hip)
   if (alloc((void**)&d_virt, virt.size() + 1)) return -1;
   HIPC(hipMemcpy(d_virt, virt.data(), virt.size(), hipMemcpyHostToDevice));
+  ds.virt = d_virt;
   if (ds.n_nodes == 0) return 0;
   const uint32_t n_ns = ds.n_ns, n_rel = ds.n_rel, n0 = ds.n_nodes;
   // contributions: (ns, rel) -> plans whose anchor order lists rel

@@ -197,7 +197,10 @@ __global__ __launch_bounds__(256) void k_resolve(DevSnap s, const kg_query* __re
     if (d <= 0 || global < d) d = global;  // engine.go:68-70
     const uint8_t rf = relflag(s, x.t.ns, x.t.rel);
     if (node == NONE) {
-      route = rf ? ROUTE_GENERAL : ROUTE_DONE;
+      // a materialised union relation without a node for this object: none of its components has a
+      // node either (the node exists as soon as one does), so every branch is NotMember
+      const bool virt = s.virt && x.t.ns < s.n_ns && x.t.rel < s.n_rel && s.virt[(size_t)x.t.ns * s.n_rel + x.t.rel];
+      route = rf && !virt ? ROUTE_GENERAL : ROUTE_DONE;
     } else {
       // the node's flags ride in its node-map slot (a random nflags read per query otherwise)
       bool impure = s.nflags && (nfl & NF_IMPURE);

@@ -160,6 +160,7 @@ struct DevSnap {
   const RwNode* rw;
   const int32_t* rwchild;
   uint32_t n_rw;
+  const uint8_t* virt;  // [n_ns * n_rel]: 1 = a materialised union relation (kg_augment.hip), or nullptr
   // reverse indexes (backward tier, kg_check.hip k_back); radj == nullptr: not built
   const uint64_t* radj_off;  // [n_nodes+1] parents of a node through set-adjacency
   const uint32_t* radj;
