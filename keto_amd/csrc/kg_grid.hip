@@ -73,11 +73,12 @@ struct GridSlots {
   uint32_t* root;  // root node (a backward parent equal to it closes a path)
   uint32_t* lastf;
   uint32_t* lastb;
+  uint32_t* bd;    // 1: this slot runs bidirectional turns, 0: forward only
 };
 
-// Turn activity for a slot of rest depth D (bidir = 0: forward only, the classic schedule).
-__device__ __forceinline__ bool fwd_active(int bidir, int t, int D) { return bidir ? 2 * t <= D - 1 : t + 1 <= D - 1; }
-__device__ __forceinline__ bool back_active(int bidir, int t, int D) { return bidir && 2 * t + 1 <= D - 1; }
+// Turn activity for a slot of rest depth D (bd = 0: forward only, the classic schedule).
+__device__ __forceinline__ bool fwd_active(uint32_t bd, int t, int D) { return bd ? 2 * t <= D - 1 : t + 1 <= D - 1; }
+__device__ __forceinline__ bool back_active(uint32_t bd, int t, int D) { return bd && 2 * t + 1 <= D - 1; }
 
 // Visited sets of all slots in ONE open-addressing table of 64-bit keys
 //   epoch (15) | direction (1: backward) | slot (16) | node (32)
@@ -188,10 +189,10 @@ __global__ __launch_bounds__(256) void k_grid_init(DevSnap s, const RQuery* __re
                                                    const uint32_t* __restrict__ qlist, const uint32_t* d_count,
                                                    uint32_t base, uint32_t G, GridLog lg, GridLog blg, GridSlots sl,
                                                    uint64_t* H, uint64_t mask, uint64_t epoch, GridCtl* ctl,
-                                                   int bidir) {
+                                                   uint32_t hb) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   const bool valid = i < round_slots(d_count, base, G);
-  uint32_t rb = 0, len = 0, hb = 0, hn = 0;
+  uint32_t rb = 0, len = 0, hb0 = 0, hn = 0;
   if (valid) {
     const uint32_t qi = qlist[base + i];
     const RQuery q = rq[qi];
@@ -201,29 +202,34 @@ __global__ __launch_bounds__(256) void k_grid_init(DevSnap s, const RQuery* __re
     sl.root[i] = q.node;
     sl.lastf[i] = 0;
     sl.lastb[i] = NONE;
+    sl.bd[i] = 0;
     if (gh_insert(H, mask, gh_key(epoch, false, i, q.node)) < 0) ctl->overflow = 1;
     rb = q.beg;
     len = q.len;
-    if (bidir) {
+    if (hb) {
+      // bidirectional only for subjects with at most hb holders: backward turn 0 reads every holder
+      // and turn 1 their parents, which for a popular subject is most of the reverse graph, while its
+      // forward search usually hits within a hop or two
       const uint2 hr = holders_find(s, q.subj);
-      hb = hr.x;
-      hn = hr.y;
-      if (hn) sl.lastb[i] = 0;
+      if (hr.y > 0 && hr.y <= hb) {
+        hb0 = hr.x;
+        hn = hr.y;
+        sl.bd[i] = 1;
+        sl.lastb[i] = 0;
+      }
     }
   }
   grid_append(ctl, ctl->lv, lg, 0, 0, 0, valid, i, rb, len);
-  if (bidir) grid_append(ctl, ctl->blv, blg, 0, 0, 0, valid && hn > 0, i, hb, hn);
+  if (hb) grid_append(ctl, ctl->blv, blg, 0, 0, 0, valid && hn > 0, i, hb0, hn);
 }
 
 // Before a turn: a live slot whose side `back` has an active turn t but appended nothing at turn t-1
 // has that side's whole closure (BFS stopped by itself, not by depth) -- NotMember (see the header).
-__global__ void k_grid_settle(GridSlots sl, const uint32_t* d_count, uint32_t base, uint32_t G, int t, int back,
-                              int bidir) {
+__global__ void k_grid_settle(GridSlots sl, const uint32_t* d_count, uint32_t base, uint32_t G, int t, int back) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= round_slots(d_count, base, G) || sl.hit[i]) return;
+  if (i >= round_slots(d_count, base, G) || sl.hit[i] || !sl.bd[i]) return;
   const int D = (int)sl.info[i].y;
-  if (back ? (back_active(bidir, t, D) && sl.lastb[i] != (uint32_t)t)
-           : (fwd_active(bidir, t, D) && sl.lastf[i] != (uint32_t)t))
+  if (back ? (back_active(1, t, D) && sl.lastb[i] != (uint32_t)t) : (fwd_active(1, t, D) && sl.lastf[i] != (uint32_t)t))
     sl.hit[i] = 2;
 }
 
@@ -242,7 +248,7 @@ __device__ __forceinline__ uint64_t entry_of(const uint64_t* ex, uint64_t base, 
 // backward log (edges = reverse-adjacency parents, or at turn 0 the subject's holders).
 template <int BACK>
 __global__ __launch_bounds__(256) void k_grid_level(DevSnap s, GridLog lg, int level, GridSlots sl, uint64_t* H,
-                                                    uint64_t mask, uint64_t epoch, GridCtl* ctl, int bidir) {
+                                                    uint64_t mask, uint64_t epoch, GridCtl* ctl) {
   __shared__ uint64_t s_beg[GT + 2];
   __shared__ uint32_t s_slot[GT + 2], s_rb[GT + 2];
   __shared__ uint64_t s_j0, s_cnt;
@@ -311,6 +317,7 @@ __global__ __launch_bounds__(256) void k_grid_level(DevSnap s, GridLog lg, int l
       // the slot's state and the edge load are independent: one round trip for both
       const uint32_t hit = sl.hit[slot];
       const uint2 si = sl.info[slot];  // (tagged subject, rest depth of the root)
+      const uint32_t bidir = sl.bd[slot];
       const int D = (int)si.y;
       if (!BACK) {
         const AdjX x = s.adjx[rb + (e - beg)];
@@ -420,7 +427,7 @@ static int grid_layout(GridPool* P, uint64_t cap, hipStream_t stream, GridView* 
   uint64_t hcap = 1;
   while (hcap < (two ? 4 : 2) * cap) hcap <<= 1;
   const size_t log_bytes = cap * (4 + 4 + 8) + 2 * TILE_CAP * 4;
-  const size_t need = hcap * 8 + (two ? 2 : 1) * log_bytes + (size_t)G0 * 28 + sizeof(GridCtl) + 4096;
+  const size_t need = hcap * 8 + (two ? 2 : 1) * log_bytes + (size_t)G0 * 32 + sizeof(GridCtl) + 4096;
   if (need > P->bytes) {
     P->release();
     HIPC(hipMalloc(&P->mem, need));
@@ -455,7 +462,8 @@ static int grid_layout(GridPool* P, uint64_t cap, hipStream_t stream, GridView* 
   v->sl.root = v->sl.hit + G0;
   v->sl.lastf = v->sl.root + G0;
   v->sl.lastb = v->sl.lastf + G0;
-  p += (size_t)G0 * 20;
+  v->sl.bd = v->sl.lastb + G0;
+  p += (size_t)G0 * 24;
   v->ctl = (GridCtl*)(((uintptr_t)p + 255) & ~uintptr_t(255));
   return 0;
 }
@@ -493,6 +501,7 @@ int grid_tier(Snapshot* s, Workspace* w, const RQuery* rq, const uint32_t* qlist
   GridPool* gp = &w->grid;
   // bidirectional turns need the reverse indexes (holders, reverse set-adjacency)
   const int bidir_ok = s->grid_bidir && s->ds.radj && s->ds.hold && s->ds.hslots ? 1 : 0;
+  const uint32_t hold_cap = s->grid_bidir > 1 ? (uint32_t)s->grid_bidir : 1024u;  // holders a bidirectional slot may have
   std::unique_lock<std::mutex> giant_lk(s->giant_mu, std::defer_lock);
   GridView v;
   if (int rc = grid_layout(gp, small_cap, stream, &v)) return rc;
@@ -513,27 +522,27 @@ int grid_tier(Snapshot* s, Workspace* w, const RQuery* rq, const uint32_t* qlist
     const uint32_t lgrid = (uint32_t)s->n_cu * s->grid_wgs;
     HIPC(hipMemsetAsync(v.ctl, 0, sizeof(GridCtl), stream));
     hipLaunchKernelGGL(k_grid_init, dim3(slot_blocks), dim3(256), 0, stream, s->ds, rq, qlist, d_count, done, G, v.lg,
-                       v.blg, v.sl, v.H, v.hcap - 1, epoch, v.ctl, bidir);
+                       v.blg, v.sl, v.H, v.hcap - 1, epoch, v.ctl, bidir ? hold_cap : 0u);
     HIPC(hipGetLastError());
     // Levels run back to back on the device (sizes never come back to the host; an empty level
     // costs one near-empty launch).  Forward only: level k expands nodes at rest depth D-k >= 2, so
     // at most global_max_depth-1 levels exist.  Bidirectional: forward turn t while 2t <= D-1,
     // backward turn t while 2t+1 <= D-1, alternating, each side's dry closure settled before its turn.
+    // forward-only slots take up to D-1 forward turns; bidirectional ones alternate while 2t(+1) <= D-1
     const int max_levels = std::max(1, global_max_depth - 1);
-    const int turns = bidir ? (global_max_depth - 1) / 2 + 1 : max_levels;
-    for (int t = 0; t < turns; t++) {
-      if (bidir && t > 0) {
-        hipLaunchKernelGGL(k_grid_settle, dim3(slot_blocks), dim3(256), 0, stream, v.sl, d_count, done, G, t, 0, bidir);
+    for (int t = 0; t < max_levels; t++) {
+      if (bidir && t > 0 && 2 * t <= global_max_depth - 1) {
+        hipLaunchKernelGGL(k_grid_settle, dim3(slot_blocks), dim3(256), 0, stream, v.sl, d_count, done, G, t, 0);
         HIPC(hipGetLastError());
       }
       hipLaunchKernelGGL(k_grid_level<0>, dim3(lgrid), dim3(256), 0, stream, s->ds, v.lg, t, v.sl, v.H, v.hcap - 1,
-                         epoch, v.ctl, bidir);
+                         epoch, v.ctl);
       HIPC(hipGetLastError());
       if (bidir && 2 * t + 1 <= global_max_depth - 1) {
-        hipLaunchKernelGGL(k_grid_settle, dim3(slot_blocks), dim3(256), 0, stream, v.sl, d_count, done, G, t, 1, bidir);
+        hipLaunchKernelGGL(k_grid_settle, dim3(slot_blocks), dim3(256), 0, stream, v.sl, d_count, done, G, t, 1);
         HIPC(hipGetLastError());
         hipLaunchKernelGGL(k_grid_level<1>, dim3(lgrid), dim3(256), 0, stream, s->ds, v.blg, t, v.sl, v.H,
-                           v.hcap - 1, epoch, v.ctl, bidir);
+                           v.hcap - 1, epoch, v.ctl);
         HIPC(hipGetLastError());
       }
     }
