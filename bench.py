@@ -133,6 +133,8 @@ def parse(argv=None):
     ap.add_argument("--shard-protocol", default="auto", choices=["auto", "fixed", "dynamic"],
                     help="--mode sharded exchange protocol (keto_amd.sharded.ShardedChecker)")
     ap.add_argument("--roots", type=int, default=100_000, help="expand roots per step (C5)")
+    ap.add_argument("--expand-tail", type=int, default=1,
+                    help="kg_snapshot_tune expand_tail (1: passes 2/3 walk with LDS-cached frames; 0: round 2's walk)")
     ap.add_argument("--delta", type=int, default=1000, help="--mode refresh: rows per transaction")
     a = ap.parse_args(argv)
     if a.hw_queues is None:
@@ -188,6 +190,7 @@ def bench_expand(a):
         dist.init_process_group(a.backend, rank=rank, world_size=world)
     L = _lib.load()
     snap, _ = build_synthetic(a, a.tuples, device=local)
+    snap.tune("expand_tail", a.expand_tail)
     from keto_amd.synth import hot_group_roots
     roots = hot_group_roots(snap.synth_ids(), a.roots)
     depth = a.global_depth if a.global_depth != 10 else 5
@@ -245,8 +248,10 @@ def bench_expand(a):
            "value": world * a.roots * a.steps / el, "unit": "trees/s", "n_gpus": world, "scaling": "weak",
            "steps": a.steps, "warmup": a.warmup, "ms_per_step": el / a.steps * 1e3,
            "higher_is_better": True, "dtype": "u32", "data": "synthetic (device-generated, seed %d)" % a.seed,
-           "config": {"workload": "C5: %d hot roots @ %.3g tuples, max_read_depth %d" % (a.roots, a.tuples, depth),
-                      "inflight_per_gpu": P, "hw_queues": a.hw_queues, "parallelism": f"replica{world}"},
+           "config": {"workload": "C5: %d hot roots @ %.4g tuples (rows), max_read_depth %d" % (a.roots, snap.info()["rows"],
+                                                                                            depth),
+                      "inflight_per_gpu": P, "hw_queues": a.hw_queues, "parallelism": f"replica{world}",
+                      "expand_tail": a.expand_tail},
            "tree_nodes_per_step": nodes / a.steps, "tree_nodes_per_s": nodes / el,
            "kernel_ms_per_step": kms / a.steps}
     if off is not None:

@@ -465,6 +465,11 @@ static int tune_one(Snapshot* s, const char* key, int64_t value) {
     s->grid_small_cap = (uint64_t)value;
     return 0;
   }
+  if (strcmp(key, "expand_tail") == 0) {
+    if (value < 0 || value > 1) return set_error(-2, "expand_tail must be 0 or 1");
+    s->expand_tail = (int)value;
+    return 0;
+  }
   if (strcmp(key, "grid_bidir") == 0) {
     // 0 off, 1 on (a slot is bidirectional when its subject has <= 1024 holders), > 1: that holder cap
     if (value < 0 || value > 0x7FFFFFFF) return set_error(-2, "grid_bidir must be in [0, 2^31)");

@@ -485,7 +485,7 @@ template <class Store>
 __device__ void expand_slot_loop(const DevSnap& s, const kg_set* __restrict__ roots, int32_t global, ExpCtl* ctl,
                                  RootOut* outs, kg_tree_node* arena, uint32_t* next, uint32_t n_chunks,
                                  ExpFrame* stack, const uint32_t* qlist, uint32_t count, uint32_t* head, Store& st,
-                                 uint32_t* clear_base, uint64_t clear_words, uint32_t* p3_list) {
+                                 uint32_t* clear_base, uint64_t clear_words, uint32_t* p3_list, int cached) {
   __shared__ ExpLds X;
   const int lane = lane_id();
   Stream S{arena, next, n_chunks, ctl, 0, 0, 0, true};
@@ -497,7 +497,8 @@ __device__ void expand_slot_loop(const DevSnap& s, const kg_set* __restrict__ ro
     if (k >= count) break;
     const uint32_t ri = qlist[k];
     uint32_t nr = 0;
-    const int r = expand_root_x(s, st, roots[ri], global, stack, S, nr, X);
+    const int r = cached ? expand_root_x(s, st, roots[ri], global, stack, S, nr, X)
+                         : expand_root(s, st, roots[ri], global, stack, S, nr);
     if (r == EXP_OVERFLOW && p3_list) {
       uint4* b4 = reinterpret_cast<uint4*>(clear_base);  // clear_words: multiple of 4, 16-B aligned
       for (uint64_t i = lane; i < clear_words / 4; i += 64) b4[i] = make_uint4(0, 0, 0, 0);
@@ -518,22 +519,23 @@ __global__ __launch_bounds__(64) void k_expand_hash(DevSnap s, const kg_set* __r
                                                     ExpCtl* ctl, RootOut* outs, kg_tree_node* arena, uint32_t* next,
                                                     uint32_t n_chunks, ExpFrame* stacks, uint32_t stack_cap,
                                                     const uint32_t* p2_list, uint32_t* tabs, uint64_t tsize,
-                                                    uint32_t* lists, uint64_t cap, uint32_t* p3_list) {
+                                                    uint32_t* lists, uint64_t cap, uint32_t* p3_list, int cached) {
   __shared__ uint32_t pref[64];
   uint32_t* tab = tabs + (size_t)blockIdx.x * tsize;
   HashStore st{tab, (uint32_t)(tsize - 1), lists + (size_t)blockIdx.x * cap, cap, pref};
   expand_slot_loop(s, roots, global, ctl, outs, arena, next, n_chunks, stacks + (size_t)blockIdx.x * stack_cap, p2_list,
-                   ctl->p2_count, &ctl->p2_head, st, tab, tsize, p3_list);
+                   ctl->p2_count, &ctl->p2_head, st, tab, tsize, p3_list, cached);
 }
 
 __global__ __launch_bounds__(64) void k_expand_hbm(DevSnap s, const kg_set* __restrict__ roots, int32_t global,
                                                    ExpCtl* ctl, RootOut* outs, kg_tree_node* arena, uint32_t* next,
                                                    uint32_t n_chunks, ExpFrame* stack, const uint32_t* p3_list,
-                                                   uint32_t* bm, uint64_t words, uint32_t* list, uint64_t cap) {
+                                                   uint32_t* bm, uint64_t words, uint32_t* list, uint64_t cap,
+                                                   int cached) {
   __shared__ uint32_t pref[64];
   GlobalStore st{bm, list, cap, pref};
   expand_slot_loop(s, roots, global, ctl, outs, arena, next, n_chunks, stack, p3_list, ctl->p3_count, &ctl->p3_head, st,
-                   bm, words, nullptr);
+                   bm, words, nullptr, cached);
 }
 
 __global__ void k_expand_compact(const RootOut* outs, uint32_t n, const uint64_t* off, const kg_tree_node* arena,
@@ -730,10 +732,10 @@ int expand_batch(Snapshot* s, hipStream_t stream, void** bufs, const kg_set* roo
                        B.outs, B.arena, B.next, n_chunks, B.stacks, stack_cap, B.p2);
     hipLaunchKernelGGL(k_expand_hash, dim3(slots2), dim3(64), 0, stream, s->ds, B.d_roots, global, B.ctl, B.outs,
                        B.arena, B.next, n_chunks, B.stacks + (size_t)slots1 * stack_cap, stack_cap, B.p2, B.bm, tsize,
-                       lists, cap2, B.p2 + n);
+                       lists, cap2, B.p2 + n, s->expand_tail);
     hipLaunchKernelGGL(k_expand_hbm, dim3(1), dim3(64), 0, stream, s->ds, B.d_roots, global, B.ctl, B.outs, B.arena,
                        B.next, n_chunks, B.stacks + (size_t)(slots1 + slots2) * stack_cap, B.p2 + n,
-                       B.bm + (size_t)slots2 * tsize, words, lists + (size_t)slots2 * cap2, nn);
+                       B.bm + (size_t)slots2 * tsize, words, lists + (size_t)slots2 * cap2, nn, s->expand_tail);
     (void)hipEventRecord(B.ev[1], stream);
     if ((e = hipGetLastError()) != hipSuccess) {
       fail("launch", e);

@@ -237,6 +237,7 @@ struct Snapshot {
   uint32_t interp_cap2 = 0;  // kg_snapshot_tune("interp_cap2"): pass-2 BFS list cap of the rewrite path (0 = 256 Ki)
   int back_wgs = 2;          // kg_snapshot_tune("back_wgs"): k_back workgroups per CU (1..3, LDS allows 3; 2 = bench C2 default)
   uint64_t grid_small_cap = 0;  // kg_snapshot_tune("grid_cap"): workspace grid-log entries (0 = 16 Mi; tests)
+  int expand_tail = 1;  // kg_snapshot_tune("expand_tail"): expand passes 2/3 walk with LDS-cached frames (0: round 2)
   int grid_bidir = 1;  // kg_snapshot_tune("grid_bidir"): grid slots whose subject has <= 1024 holders (> 1: this many)
                        // alternate forward and backward turns (0: forward only)
   // replicas: the same snapshot on more devices (kg_snapshot_create's device mask); this object is
