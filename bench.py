@@ -259,6 +259,20 @@ def bench_expand(a):
         out["records_per_root"] = {"p50": float(np.percentile(sz, 50)), "p99": float(np.percentile(sz, 99)),
                                    "max": int(sz.max()), "roots_over_512": int((sz > 512).sum()),
                                    "top10_share": float(np.sort(sz)[-10:].sum() / max(1, sz.sum()))}
+    if off is not None:
+        # the batch's tail: the largest root's walk alone (one sequential pre-order DFS on one wave)
+        big = int(np.argmax(np.diff(off.astype(np.int64))))
+        one = np.ascontiguousarray(roots[big:big + 1])
+        walk = []
+        for _ in range(3):
+            buf = _lib.kg_tree_buf()
+            _lib.check(L.kg_expand_batch(snap.handle, one.ctypes.data_as(C.c_void_p), 1, depth, C.byref(buf)),
+                       "kg_expand_batch")
+            walk.append(buf.kernel_ms)
+            n_big = int(buf.n_nodes)
+            L.kg_tree_free(C.byref(buf))
+        out["largest_root"] = {"records": n_big, "walk_kernel_ms": float(min(walk)),
+                               "expand_tail": a.expand_tail}
     if rank == 0 and a.parity_roots > 0 and off is not None:
         out["parity"] = expand_parity(snap, roots, np.diff(off.astype(np.int64)), depth, a)
     if rank == 0:
