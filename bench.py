@@ -60,9 +60,9 @@ def parse(argv=None):
     ap.add_argument("--seed", type=int, default=20250131)
     ap.add_argument("--tiers", type=int, default=0, help="kg_snapshot_tune tiers (0 grid, 1 LDS-WG+grid, 2 WG)")
     ap.add_argument("--wide", type=int, default=0, help="kg_snapshot_tune wide (k_light<64> tier on/off)")
-    ap.add_argument("--stream", type=int, default=12, help="kg_snapshot_tune stream (k_stream variant 0..8, 9 = k_stream2, "
+    ap.add_argument("--stream", type=int, default=15, help="kg_snapshot_tune stream (k_stream variant 0..8, 9 = k_stream2, "
                     "10 = k_stream3, 11 = k_stream2 with 128-edge windows, 12 = k_stream2 without the per-query "
-                    "expanded-node cap: default)")
+                    "expanded-node cap, 15 = k_stream4 over k_resolve's compact work list: default)")
     ap.add_argument("--stream-ecap", type=int, default=512, help="kg_snapshot_tune stream_ecap (stream-tier edges per query, 0 = none)")
     ap.add_argument("--shard-budget", type=int, default=0,
                     help="kg_snapshot_tune shard_budget (sharded mode: forward set edges per query and rank before "
@@ -83,8 +83,9 @@ def parse(argv=None):
     ap.add_argument("--stream-chunk", type=int, default=64,
                     help="kg_snapshot_tune stream_chunk (k_stream2 queries per dequeue, 1..64)")
     ap.add_argument("--grid-wgs", type=int, default=4, help="kg_snapshot_tune grid_wgs (k_grid_level WGs per CU)")
-    ap.add_argument("--grid-bidir", type=int, default=1,
-                    help="kg_snapshot_tune grid_bidir (1: the grid tier alternates forward and backward turns)")
+    ap.add_argument("--grid-bidir", type=int, default=64,
+                    help="kg_snapshot_tune grid_bidir: grid slots whose subject has <= this many holders "
+                         "alternate forward and backward turns (0: forward only)")
     ap.add_argument("--stream-wgs", type=int, default=3,
                     help="kg_snapshot_tune stream_wgs (k_stream WGs per CU, 0 = by variant: 5 for k_stream2's ~29 KiB "
                          "WGs; 3 leaves LDS to the other batches in flight, best at --inflight 4: profiles/r2j_sweep.jsonl)")

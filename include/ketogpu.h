@@ -213,8 +213,10 @@ int kg_snapshot_materialized(const kg_snapshot* s, uint64_t* out3);
  * holders, one wave per query, then one workgroup per query) takes the wave tiers' overflow before the grid tier, and
  * k_resolve answers queries whose subject no row holds; 2 = the same with the wave width only
  * (its overflow goes straight to the grid tier; default); 0 = off.  key "stream": stream-tier
- * kernel -- 12 = k_stream2 (default: 32 query slots per wave over one FIFO, direct-mapped visited
- * cache, a query bounded by its edge budget), 9 = the same with a cap of 64 expanded nodes per query,
+ * kernel -- 15 = k_stream4 (default: k_resolve writes the stream tier's queries as compact records
+ * into 8 per-XCD shards, and a wave dequeues the next chunk while it walks the current one), 12 =
+ * k_stream2 (32 query slots per wave over one FIFO, direct-mapped visited cache, a query bounded by
+ * its edge budget), 9 = the same with a cap of 64 expanded nodes per query,
  * 11 = 128-edge windows, 10 = k_stream3 (software-pipelined), 0..8 = the round-1 k_stream variants.
  * key "stream_ecap": edges a query may enqueue in the stream tier before it is handed to the
  * backward / grid tiers (default 512; 0 = no budget) -- cuts the stream kernel's tail of long walks.
@@ -236,7 +238,10 @@ int kg_snapshot_materialized(const kg_snapshot* s, uint64_t* out3);
  * its own; otherwise allocated on first need).  key "grid_cap": log entries of a workspace's grid
  * pool (0 = 16 Mi; small values force the overflow paths in tests).  key "max_lanes" (1..1024, default
  * 32): lane sets (a stream, staging and workspace per replica) that concurrent kg_check_batch /
- * kg_expand_batch calls check out of the snapshot's pool; at the cap a call waits for one to return. */
+ * kg_expand_batch calls check out of the snapshot's pool; at the cap a call waits for one to return.
+ * key "grid_bidir" (0..2^31-1, default 64): grid-tier slots whose subject has at most this many
+ * holders alternate forward and backward turns (0: forward only).  key "expand_tail" (0/1, default
+ * 1): the expand walk caches a root's last frontier in LDS. */
 int kg_snapshot_tune(kg_snapshot* s, const char* key, int64_t value);
 /* Synthetic layout: ids6 = {n_docs, n_groups, n_users, n_folders, user_obj0, folder_obj0}
  * (doc d = object d, group g = object n_docs+g, user u = object user_obj0+u). */
@@ -355,6 +360,15 @@ int kg_shard_level_seg(kg_snapshot* s, const kg_frec* d_in, uint32_t n_seg, size
  * words (words >= ceil(n / 32)); with_escalated 1: queries escalated out of the forward phase count
  * as done too, 2: those escalated out of the backward phase; the driver all-gathers the words
  * before each level. */
+/* One-rank snapshots (nranks 1): `levels` kg_shard_level calls enqueued back to back in ONE call,
+ * ping-ponging between (d_buf0, d_counts0) and (d_buf1, d_counts1) from buffer `start` (0 / 1;
+ * each buffer holds cap records, its record count in counts[0] on the device), with the done bitmap
+ * of kg_shard_done (with_escalated as there) rebuilt before every level after the first.  *end
+ * receives the buffer the last level wrote.  Replaces the driver's per-level loop when no exchange
+ * happens between levels (keto_amd/sharded.py at world 1). */
+int kg_shard_levels(kg_snapshot* s, int32_t levels, kg_frec* d_buf0, kg_frec* d_buf1, size_t cap, uint32_t* d_counts0,
+                    uint32_t* d_counts1, int32_t start, uint8_t* d_res, uint32_t* d_err, size_t n_slots,
+                    int32_t with_escalated, int32_t* end, void* stream);
 int kg_shard_done(kg_snapshot* s, size_t n, const uint8_t* d_res, const uint32_t* d_err, int with_escalated,
                   uint32_t* d_bits, uint32_t words, void* stream);
 /* Backward phase (snapshots without a namespace program; kg_snapshot_tune "shard_budget", default

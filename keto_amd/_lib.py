@@ -81,7 +81,7 @@ EXPORTS = ["kg_snapshot_create", "kg_snapshot_create_on", "kg_snapshot_synthetic
            "kg_snapshot_export", "kg_snapshot_rows", "kg_snapshot_export_csr", "kg_check_batch", "kg_check_batch_device", "kg_synth_queries", "kg_expand_batch",
            "kg_tree_free", "kg_last_error", "kg_version", "kg_shard_owner", "kg_snapshot_create_shard",
            "kg_snapshot_synthetic_shard", "kg_shard_seed", "kg_shard_level", "kg_shard_level_seg", "kg_shard_finish",
-           "kg_shard_done", "kg_shard_back_list", "kg_shard_back_seed", "kg_shard_back_level", "kg_shard_refwd_seed",
+           "kg_shard_done", "kg_shard_levels", "kg_shard_back_list", "kg_shard_back_seed", "kg_shard_back_level", "kg_shard_refwd_seed",
            "kg_shard_held_words", "kg_shard_held", "kg_shard_result_slots", "kg_batcher_create", "kg_batcher_check", "kg_batcher_stats", "kg_batcher_reset_stats", "kg_batcher_destroy"]
 
 
@@ -148,6 +148,8 @@ def load(path: str = LIB_PATH):
     L.kg_shard_level_seg.argtypes = [vp, vp, C.c_uint32, sz, vp, vp, sz, vp, vp, vp, vp, C.c_uint32, vp]
     L.kg_shard_level_seg.restype = C.c_int
     L.kg_shard_done.argtypes = [vp, sz, vp, vp, C.c_int, vp, C.c_uint32, vp]
+    L.kg_shard_levels.argtypes = [vp, i32, vp, vp, sz, vp, vp, i32, vp, vp, sz, i32, C.POINTER(i32), vp]
+    L.kg_shard_levels.restype = C.c_int
     L.kg_shard_back_list.argtypes = [vp, sz, vp, vp, vp, sz, vp, vp]
     L.kg_shard_back_seed.argtypes = [vp, vp, sz, vp, vp, sz, vp, vp]
     L.kg_shard_back_level.argtypes = [vp, vp, sz, vp, vp, sz, vp, vp, vp, vp, C.c_uint32, vp]
@@ -169,7 +171,7 @@ def load(path: str = LIB_PATH):
                  "kg_snapshot_create_ordered", "kg_snapshot_apply", "kg_synth_ids", "kg_check_batch",
                  "kg_check_batch_device", "kg_synth_queries", "kg_expand_batch", "kg_snapshot_create_shard",
                  "kg_snapshot_synthetic_shard", "kg_shard_seed", "kg_shard_level", "kg_shard_level_seg", "kg_shard_finish",
-                 "kg_shard_done", "kg_shard_back_list", "kg_shard_back_seed", "kg_shard_back_level", "kg_shard_refwd_seed",
+                 "kg_shard_done", "kg_shard_levels", "kg_shard_back_list", "kg_shard_back_seed", "kg_shard_back_level", "kg_shard_refwd_seed",
                  "kg_shard_held_words", "kg_shard_held", "kg_batcher_create", "kg_batcher_check", "kg_batcher_stats"):
         getattr(L, name).restype = C.c_int
     _lib = L

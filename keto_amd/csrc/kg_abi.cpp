@@ -268,6 +268,25 @@ int kg_shard_level_seg(kg_snapshot* sp, const kg_frec* d_in, uint32_t n_seg, siz
   KG_GUARD_END
 }
 
+int kg_shard_levels(kg_snapshot* sp, int32_t levels, kg_frec* d_buf0, kg_frec* d_buf1, size_t cap, uint32_t* d_counts0,
+                    uint32_t* d_counts1, int32_t start, uint8_t* d_res, uint32_t* d_err, size_t n_slots,
+                    int32_t with_escalated, int32_t* end, void* stream) {
+  KG_GUARD_BEGIN
+  if (!sp || !d_buf0 || !d_buf1 || !d_counts0 || !d_counts1 || !d_res || !d_err) return set_error(-2, "NULL argument");
+  if (levels < 0 || levels > 1024 || (start != 0 && start != 1) || with_escalated < 0 || with_escalated > 2 || cap == 0)
+    return set_error(-2, "kg_shard_levels: levels in [0, 1024], start 0 / 1, with_escalated 0..2, cap > 0");
+  Snapshot* s = reinterpret_cast<Snapshot*>(sp);
+  std::lock_guard<std::mutex> lk(s->mu);
+  kg_frec* bufs[2] = {d_buf0, d_buf1};
+  uint32_t* counts[2] = {d_counts0, d_counts1};
+  int e = start;
+  const int rc = kg::shard_levels(s, levels, bufs, cap, counts, start, d_res, d_err, n_slots, with_escalated, &e,
+                                  (hipStream_t)stream);
+  if (end) *end = e;
+  return rc;
+  KG_GUARD_END
+}
+
 int kg_shard_done(kg_snapshot* sp, size_t n, const uint8_t* d_res, const uint32_t* d_err, int with_escalated,
                   uint32_t* d_bits, uint32_t words, void* stream) {
   KG_GUARD_BEGIN

@@ -16,7 +16,7 @@
 // Semantics are those of k_stream / k_medium (kg_check.hip): bounded reachability with every node
 // probed once at its shallowest depth.  A round that overflows the log is rerun with fewer slots.
 //
-// Bidirectional mode (default, kg_snapshot_tune "grid_bidir"): the queries that reach this tier are the
+// Bidirectional mode (kg_snapshot_tune "grid_bidir" = holder cap, default 64): the queries that reach this tier are the
 // ones whose forward search is huge -- on a heavy-tailed graph every root reaches whole layers within
 // two hops (SURVEY.md 8d's degree law: ~1.2 M edge visits per query).  Each round alternates a forward
 // turn (the log above) with a BACKWARD turn over a second log: backward turn 0 reads the subject's
@@ -501,7 +501,7 @@ int grid_tier(Snapshot* s, Workspace* w, const RQuery* rq, const uint32_t* qlist
   GridPool* gp = &w->grid;
   // bidirectional turns need the reverse indexes (holders, reverse set-adjacency)
   const int bidir_ok = s->grid_bidir && s->ds.radj && s->ds.hold && s->ds.hslots ? 1 : 0;
-  const uint32_t hold_cap = s->grid_bidir > 1 ? (uint32_t)s->grid_bidir : 1024u;  // holders a bidirectional slot may have
+  const uint32_t hold_cap = (uint32_t)s->grid_bidir;  // holders a bidirectional slot's subject may have
   std::unique_lock<std::mutex> giant_lk(s->giant_mu, std::defer_lock);
   GridView v;
   if (int rc = grid_layout(gp, small_cap, stream, &v)) return rc;

@@ -663,6 +663,26 @@ __global__ void k_shard_done(uint32_t n, const uint8_t* __restrict__ res, const 
   bits[w] = b;
 }
 
+// One launch before each level of kg_shard_levels: the done bitmap from the results so far
+// (k_shard_done's packing; words = 0 at the first level) and the level's zeroed bucket counter and
+// hub-row count -- what the per-level driver did with a kernel and two fills.
+__global__ void k_shard_prep(uint32_t n, const uint8_t* __restrict__ res, const uint32_t* __restrict__ err,
+                             uint32_t esc_mask, uint32_t words, uint32_t* __restrict__ bits, uint32_t* counts,
+                             uint32_t* heavy_n) {
+  const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
+  if (w == 0) {
+    counts[0] = 0;  // one rank: one bucket (the flags word counts[1] accumulates over the batch)
+    *heavy_n = 0;
+  }
+  if (w >= words) return;
+  uint32_t b = 0;
+  for (uint32_t k = 0; k < 32; k++) {
+    const uint32_t i = w * 32 + k;
+    if (i < n && (res[i] == KG_IS_MEMBER || (esc_mask && (err[i] & esc_mask)))) b |= 1u << k;
+  }
+  bits[w] = b;
+}
+
 __global__ void k_shard_finish(uint32_t n, uint8_t* res, uint32_t* err, ShardFormula F) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -788,6 +808,52 @@ int shard_level(Snapshot* s, const kg_frec* d_in, size_t n_in, const uint32_t* d
                        SHARD_HEAVY_CAP, d_out, (uint64_t)cap, d_counts, d_res, d_err, s->shard_n);
     HIPC(hipGetLastError());
   }
+  return 0;
+}
+
+// One rank: `levels` forward levels enqueued back to back in ONE call (the Python driver's per-level
+// loop cost ~6 host calls and launches per level; with several batches in flight on one process the
+// enqueue thread, not the device, set the step time).  Level k reads buffer cur (its record count
+// from d_counts[cur][0] on the device) and writes buffer cur ^ 1; from the second level on, queries
+// answered IsMember (esc_mode 1: or escalated) drop their records through the done bitmap.
+int shard_levels(Snapshot* s, int levels, kg_frec* d_buf[2], size_t cap, uint32_t* d_counts[2], int start,
+                 uint8_t* d_res, uint32_t* d_err, size_t slots, int esc_mode, int* end, hipStream_t stream) {
+  HIPC(hipSetDevice(s->device));
+  if (!stream) stream = s->stream;
+  if (s->shard_n != 1) return set_error(-2, "kg_shard_levels runs one-rank batches (shard_n = %u)", s->shard_n);
+  ShardCtx* c = s->shard_ctx(stream);
+  if (!c || !c->vis) return set_error(-2, "kg_shard_levels before kg_shard_seed (on this stream)");
+  const uint32_t words = (uint32_t)((slots + 31) / 32);
+  if ((size_t)words + 1 > c->bits_n) {
+    if (c->bits) HIPC(hipFree(c->bits));
+    c->bits = nullptr;
+    c->bits_n = 0;
+    HIPC(hipMalloc((void**)&c->bits, ((size_t)words + 1) * 4));
+    c->bits_n = (size_t)words + 1;
+  }
+  HeavyRow* heavy = (HeavyRow*)c->heavy;
+  uint32_t* heavy_n = (uint32_t*)(heavy + SHARD_HEAVY_CAP);
+  const uint32_t esc = esc_mode == 1 ? ESC_BIT : (esc_mode == 2 ? ESC2_BIT : 0u);
+  const uint32_t budget = shard_escalates(s) && c->qcnt && !c->final ? s->shard_budget : 0u;
+  const uint32_t grid = (uint32_t)std::min<uint64_t>((cap + 255) / 256, (uint64_t)s->n_cu * 8);
+  int cur = start & 1;
+  for (int k = 0; k < levels; k++) {
+    const int nx = cur ^ 1;
+    const uint32_t w = k > 0 ? words : 0u;
+    hipLaunchKernelGGL(k_shard_prep, dim3(std::max<uint32_t>(1, (w + 255) / 256)), dim3(256), 0, stream, (uint32_t)slots,
+                       d_res, d_err, esc, w, c->bits, d_counts[nx], heavy_n);
+    HIPC(hipGetLastError());
+    hipLaunchKernelGGL(k_shard_level, dim3(grid), dim3(256), 0, stream, s->ds, d_buf[cur], (uint64_t)cap, d_counts[cur],
+                       d_buf[nx], (uint64_t)cap, d_counts[nx], d_res, d_err, (uint64_t*)c->vis, c->vis_slots - 1,
+                       k > 0 ? (const uint32_t*)c->bits : nullptr, w, heavy, heavy_n, SHARD_HEAVY_CAP, (uint32_t*)c->qcnt,
+                       budget, s->shard_vis_mode ? 1u : 0u, 1u, (uint64_t)0);
+    HIPC(hipGetLastError());
+    hipLaunchKernelGGL(k_shard_heavy, dim3((uint32_t)s->n_cu * 4), dim3(256), 0, stream, s->ds, heavy, heavy_n,
+                       SHARD_HEAVY_CAP, d_buf[nx], (uint64_t)cap, d_counts[nx], d_res, d_err, s->shard_n);
+    HIPC(hipGetLastError());
+    cur = nx;
+  }
+  if (end) *end = cur;
   return 0;
 }
 

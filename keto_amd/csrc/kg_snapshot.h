@@ -147,6 +147,8 @@ struct ShardCtx {
   bool final = false;      // the batch's final forward phase (kg_shard_refwd_seed): no escalation
   uint32_t* ref = nullptr;  // formula split: plan of every query of the batch
   size_t ref_n = 0;
+  uint32_t* bits = nullptr;  // kg_shard_levels: the batch's done bitmap
+  size_t bits_n = 0;
   ~ShardCtx();
 };
 
@@ -223,7 +225,7 @@ struct Snapshot {
   int shard_vis_mode = 0;  // kg_snapshot_tune("shard_vis_mode"): (query, node) dedup 0 = exact CAS table, 1 = lossy cache
   uint32_t shard_budget = 0;       // kg_snapshot_tune("shard_budget"): forward set edges per query and rank (0 = off)
   uint32_t shard_back_budget = 1u << 14;  // kg_snapshot_tune("shard_back_budget"): reverse edges per query and rank
-  int stream_variant = 12;  // kg_snapshot_tune("stream"): k_stream variant (0..8), 9 / 11 / 12 = k_stream2, 10 = k_stream3
+  int stream_variant = 15;  // kg_snapshot_tune("stream"): k_stream variant (0..8), 9 / 11 / 12 = k_stream2, 10 = k_stream3, 15 = k_stream4
   int back_tier = 2;  // kg_snapshot_tune("back"): backward tier (1: wave + workgroup widths, 2: wave only) + no-holder filter
   uint32_t stream_ecap = 512;  // kg_snapshot_tune("stream_ecap"): stream-tier edge budget per query (0 = none)
   int resolve_unheld = 1;  // kg_snapshot_tune("resolve_unheld"): k_resolve reads the holder bit before the node map
@@ -238,7 +240,7 @@ struct Snapshot {
   int back_wgs = 2;          // kg_snapshot_tune("back_wgs"): k_back workgroups per CU (1..3, LDS allows 3; 2 = bench C2 default)
   uint64_t grid_small_cap = 0;  // kg_snapshot_tune("grid_cap"): workspace grid-log entries (0 = 16 Mi; tests)
   int expand_tail = 1;  // kg_snapshot_tune("expand_tail"): expand passes 2/3 walk with LDS-cached frames (0: round 2)
-  int grid_bidir = 1;  // kg_snapshot_tune("grid_bidir"): grid slots whose subject has <= 1024 holders (> 1: this many)
+  int grid_bidir = 64;  // kg_snapshot_tune("grid_bidir"): grid slots whose subject has <= this many holders go bidirectional (0: none)
                        // alternate forward and backward turns (0: forward only)
   // replicas: the same snapshot on more devices (kg_snapshot_create's device mask); this object is
   // replica 0 and owns the others.  Host-buffer batches and expands are split over all of them.
@@ -299,6 +301,8 @@ int shard_level(Snapshot* s, const kg_frec* d_in, size_t n_in, const uint32_t* d
                 hipStream_t stream, uint32_t n_seg = 1, size_t seg_cap = 0);
 int shard_done(Snapshot* s, size_t n, const uint8_t* d_res, const uint32_t* d_err, int with_esc, uint32_t* d_bits,
                uint32_t words, hipStream_t stream);
+int shard_levels(Snapshot* s, int levels, kg_frec* d_buf[2], size_t cap, uint32_t* d_counts[2], int start,
+                 uint8_t* d_res, uint32_t* d_err, size_t slots, int esc_mode, int* end, hipStream_t stream);
 int shard_back_list(Snapshot* s, size_t n, const uint8_t* d_res, const uint32_t* d_err, kg_frec* d_list, size_t cap,
                     uint32_t* d_counts, hipStream_t stream);
 int shard_back_seed(Snapshot* s, const kg_frec* d_list, size_t m, const uint32_t* d_m, kg_frec* d_out, size_t cap,

@@ -362,7 +362,7 @@ void Snapshot::lanes_release(std::vector<Lane*>* v) {
 
 ShardCtx::~ShardCtx() {
   if (device >= 0) hipSetDevice(device);
-  for (void* p : {vis, heavy, qcnt, qinfo, (void*)ref})
+  for (void* p : {vis, heavy, qcnt, qinfo, (void*)ref, (void*)bits})
     if (p) hipFree(p);
 }
 

@@ -79,6 +79,15 @@ class HipShardOps:
                                          done.data_ptr() if done is not None else None, done_words, self._s()),
                    "kg_shard_level")
 
+    def levels(self, k, bufs, cap, counts, cur, res, err, slots, esc_mode=0):
+        """One rank: k levels back to back in one library call (kg_shard_levels); returns the buffer the
+        last level wrote."""
+        end = C.c_int32(cur)
+        _lib.check(self.L.kg_shard_levels(self.snapshot.handle, k, bufs[0].data_ptr(), bufs[1].data_ptr(), cap,
+                                          counts[0].data_ptr(), counts[1].data_ptr(), cur, res.data_ptr(),
+                                          err.data_ptr(), slots, esc_mode, C.byref(end), self._s()), "kg_shard_levels")
+        return int(end.value)
+
     def level_seg(self, din, n_seg, seg_cap, seg_counts, out, cap, counts, res, err, done=None, done_words=0):
         """kg_shard_level over a fixed-split receive buffer: segment k = din[k * seg_cap:], seg_counts[k]
         records (a device int32 tensor, clamped to seg_cap)."""
@@ -339,6 +348,10 @@ class ShardedChecker:
         phase, counted apart).  Returns the current buffer."""
         cap = self.cap
         prune = hasattr(self.ops, "done_bits")
+        if trace is None and prune and hasattr(self.ops, "levels"):  # the whole loop in one library call
+            if not final:
+                self.levels += gdepth
+            return self.ops.levels(gdepth, bufs, cap, counts, cur, res, err, slots, esc_mode)
         for k in range(gdepth):
             c = counts[cur]
             if trace is not None:  # diagnostics: records entering each level (a host sync per level)

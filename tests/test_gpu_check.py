@@ -615,7 +615,7 @@ def test_bench_tune_set_vs_oracle(preset, n_tuples):
         assert 0.05 < (out == 1).mean() < 0.95
 
 
-@pytest.mark.parametrize("bidir,grid_cap,seed", [(1, 0, 0), (1, 0, 1), (0, 0, 0), (1, 700, 2), (1, 0, 3)])
+@pytest.mark.parametrize("bidir,grid_cap,seed", [(1024, 0, 0), (1024, 0, 1), (0, 0, 0), (1024, 700, 2), (2, 0, 3), (64, 0, 4)])
 def test_grid_bidirectional_dense_vs_oracle(bidir, grid_cap, seed):
     """The grid tier's bidirectional rounds (kg_grid.hip) on dense graphs with cycles, hubs and
     subjects held only by rows nothing points at: a tiny stream-tier edge budget and the backward
