@@ -83,7 +83,7 @@ def parse(argv=None):
     ap.add_argument("--stream-chunk", type=int, default=64,
                     help="kg_snapshot_tune stream_chunk (k_stream2 queries per dequeue, 1..64)")
     ap.add_argument("--grid-wgs", type=int, default=4, help="kg_snapshot_tune grid_wgs (k_grid_level WGs per CU)")
-    ap.add_argument("--grid-bidir", type=int, default=64,
+    ap.add_argument("--grid-bidir", type=int, default=0,
                     help="kg_snapshot_tune grid_bidir: grid slots whose subject has <= this many holders "
                          "alternate forward and backward turns (0: forward only)")
     ap.add_argument("--stream-wgs", type=int, default=3,

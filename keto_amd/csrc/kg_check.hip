@@ -116,22 +116,27 @@ __device__ void block_append(bool pred, uint32_t val, uint32_t* list, uint32_t* 
   __syncthreads();
 }
 
-// Workgroup-aggregated append of LQuery records (one atomic per workgroup, contiguous 24-B stores).
-// Every thread must call it.
+// Workgroup-aggregated append of LQuery records (one atomic per workgroup).  The workgroup's records
+// are packed in LDS first and leave as one contiguous run of 8-B words: a lane storing its own 24-B
+// record would make each store instruction span 24 B x 64 lanes in three partial passes.
+// Every thread must call it (256 threads).
 __device__ void block_append_lq(bool pred, const LQuery& v, LQuery* list, uint32_t* count) {
+  static_assert(sizeof(LQuery) == 24, "LQuery is three 8-B words");
   __shared__ uint32_t wcnt[4], bbase;
+  __shared__ LQuery s_lq[256];
   const int lane = lane_id(), wave = threadIdx.x >> 6;
   const uint64_t m = __ballot(pred);
   if (lane == 0) wcnt[wave] = __popcll(m);
   __syncthreads();
-  if (threadIdx.x == 0) {
-    const uint32_t t = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
-    bbase = t ? atomicAdd(count, t) : 0u;
-  }
+  const uint32_t t = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+  if (threadIdx.x == 0) bbase = t ? atomicAdd(count, t) : 0u;
+  uint32_t li = 0;
+  for (int w = 0; w < wave; w++) li += wcnt[w];
+  if (pred) s_lq[li + lanes_below(m)] = v;
   __syncthreads();
-  uint32_t off = bbase;
-  for (int w = 0; w < wave; w++) off += wcnt[w];
-  if (pred) list[off + lanes_below(m)] = v;
+  const uint2* src = reinterpret_cast<const uint2*>(s_lq);
+  uint2* dst = reinterpret_cast<uint2*>(list + bbase);
+  for (uint32_t k = threadIdx.x; k < 3 * t; k += 256) dst[k] = src[k];
   __syncthreads();
 }
 

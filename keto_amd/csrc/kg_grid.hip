@@ -16,7 +16,7 @@
 // Semantics are those of k_stream / k_medium (kg_check.hip): bounded reachability with every node
 // probed once at its shallowest depth.  A round that overflows the log is rerun with fewer slots.
 //
-// Bidirectional mode (kg_snapshot_tune "grid_bidir" = holder cap, default 64): the queries that reach this tier are the
+// Bidirectional mode (kg_snapshot_tune "grid_bidir" = holder cap; default 0 = off): the queries that reach this tier are the
 // ones whose forward search is huge -- on a heavy-tailed graph every root reaches whole layers within
 // two hops (SURVEY.md 8d's degree law: ~1.2 M edge visits per query).  Each round alternates a forward
 // turn (the log above) with a BACKWARD turn over a second log: backward turn 0 reads the subject's
@@ -251,6 +251,10 @@ __global__ __launch_bounds__(256) void k_grid_level(DevSnap s, GridLog lg, int l
                                                     uint64_t mask, uint64_t epoch, GridCtl* ctl) {
   __shared__ uint64_t s_beg[GT + 2];
   __shared__ uint32_t s_slot[GT + 2], s_rb[GT + 2];
+  // per entry: its slot's state at tile start (subject, rest depth, hit | bidir << 8, root) -- one
+  // load per entry instead of four per edge, and a slot already answered skips its edges' loads
+  __shared__ uint2 s_info[GT + 2];
+  __shared__ uint32_t s_hb[GT + 2], s_root[GT + 2];
   __shared__ uint64_t s_j0, s_cnt;
   if (ctl->overflow) return;  // the round is void (entries past the log were dropped)
   GridLv* lvs = BACK ? ctl->blv : ctl->lv;
@@ -288,8 +292,12 @@ __global__ __launch_bounds__(256) void k_grid_level(DevSnap s, GridLog lg, int l
     if (use_lds)
       for (uint32_t i = threadIdx.x; i < cnt; i += 256) {
         s_beg[i] = lg.ex[lb + j0 + i];
-        s_slot[i] = lg.slot[lb + j0 + i];
+        const uint32_t sl_i = lg.slot[lb + j0 + i];
+        s_slot[i] = sl_i;
         s_rb[i] = lg.rb[lb + j0 + i];
+        s_info[i] = sl.info[sl_i];
+        s_hb[i] = sl.hit[sl_i] | (sl.bd[sl_i] << 8);
+        if (BACK) s_root[i] = sl.root[sl_i];
       }
     __syncthreads();
     const uint64_t e = t0 + threadIdx.x;
@@ -297,7 +305,8 @@ __global__ __launch_bounds__(256) void k_grid_level(DevSnap s, GridLog lg, int l
     uint32_t slot = 0, cb = 0, clen = 0, child = 0;
     if (act) {
       uint64_t beg;
-      uint32_t rb;
+      uint32_t rb, hit, bidir, root;
+      uint2 si;  // (tagged subject, rest depth of the root)
       if (use_lds) {
         uint32_t lo = 0, hi = (uint32_t)cnt;  // largest i < cnt with s_beg[i] <= e
         while (hi - lo > 1) {
@@ -308,22 +317,26 @@ __global__ __launch_bounds__(256) void k_grid_level(DevSnap s, GridLog lg, int l
         beg = s_beg[lo];
         slot = s_slot[lo];
         rb = s_rb[lo];
+        si = s_info[lo];
+        hit = s_hb[lo] & 0xFF;
+        bidir = s_hb[lo] >> 8;
+        root = BACK ? s_root[lo] : 0u;
       } else {
         const uint64_t j = entry_of(lg.ex, lb, j0, j0 + cnt, e);
         beg = lg.ex[lb + j];
         slot = lg.slot[lb + j];
         rb = lg.rb[lb + j];
+        hit = sl.hit[slot];
+        si = sl.info[slot];
+        bidir = sl.bd[slot];
+        root = BACK ? sl.root[slot] : 0u;
       }
-      // the slot's state and the edge load are independent: one round trip for both
-      const uint32_t hit = sl.hit[slot];
-      const uint2 si = sl.info[slot];  // (tagged subject, rest depth of the root)
-      const uint32_t bidir = sl.bd[slot];
       const int D = (int)si.y;
       if (!BACK) {
-        const AdjX x = s.adjx[rb + (e - beg)];
         if (hit) {
-          act = false;
+          act = false;  // answered at tile start: the edge is not even loaded
         } else {
+          const AdjX x = s.adjx[rb + (e - beg)];
           child = x.node;
           cb = x.begin;
           clen = x.len;
@@ -354,12 +367,12 @@ __global__ __launch_bounds__(256) void k_grid_level(DevSnap s, GridLog lg, int l
         }
       } else {
         // backward turn `level`: hop `level` parents (turn 0: the holders themselves)
-        const uint32_t p = level == 0 ? s.hold[rb + (e - beg)] : s.radj[rb + (e - beg)];
         if (hit) {
           act = false;
         } else {
+          const uint32_t p = level == 0 ? s.hold[rb + (e - beg)] : s.radj[rb + (e - beg)];
           child = p;
-          if (p == sl.root[slot]) {
+          if (p == root) {
             atomicExch(&sl.hit[slot], 1u);
           } else {
             const int ins = gh_insert(H, mask, gh_key(epoch, true, slot, p));

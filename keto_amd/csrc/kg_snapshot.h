@@ -240,7 +240,7 @@ struct Snapshot {
   int back_wgs = 2;          // kg_snapshot_tune("back_wgs"): k_back workgroups per CU (1..3, LDS allows 3; 2 = bench C2 default)
   uint64_t grid_small_cap = 0;  // kg_snapshot_tune("grid_cap"): workspace grid-log entries (0 = 16 Mi; tests)
   int expand_tail = 1;  // kg_snapshot_tune("expand_tail"): expand passes 2/3 walk with LDS-cached frames (0: round 2)
-  int grid_bidir = 64;  // kg_snapshot_tune("grid_bidir"): grid slots whose subject has <= this many holders go bidirectional (0: none)
+  int grid_bidir = 0;  // kg_snapshot_tune("grid_bidir"): grid slots whose subject has <= this many holders go bidirectional (0: none)
                        // alternate forward and backward turns (0: forward only)
   // replicas: the same snapshot on more devices (kg_snapshot_create's device mask); this object is
   // replica 0 and owns the others.  Host-buffer batches and expands are split over all of them.
