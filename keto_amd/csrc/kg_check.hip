@@ -184,9 +184,18 @@ __global__ __launch_bounds__(256) void k_resolve(DevSnap s, const kg_query* __re
     if (unheld) {
       no_holder = true;
     } else if (key_ok) {
-      const NSlot* sl = n0.key == key ? &n0 : (n0.key == EMPTY64 ? nullptr : nmap_slot(s, key, hash_next(ni, s.nmap_n)));
-      if (sl) {
-        const NSlot v = *sl;
+      // (no pointer to the register copy n0: a pointer that may address private memory puts n0 in
+      // scratch -- 40 B stored and reloaded per query, ~40 % of this kernel's HBM writes)
+      NSlot v = n0;
+      bool found = n0.key == key;
+      if (!found && n0.key != EMPTY64) {
+        const NSlot* sl = nmap_slot(s, key, hash_next(ni, s.nmap_n));
+        if (sl) {
+          v = *sl;
+          found = true;
+        }
+      }
+      if (found) {
         node = v.node;
         rb = v.beg;
         rl = v.len;
