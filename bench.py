@@ -83,6 +83,9 @@ def parse(argv=None):
     ap.add_argument("--stream-chunk", type=int, default=64,
                     help="kg_snapshot_tune stream_chunk (k_stream2 queries per dequeue, 1..64)")
     ap.add_argument("--grid-wgs", type=int, default=4, help="kg_snapshot_tune grid_wgs (k_grid_level WGs per CU)")
+    ap.add_argument("--grid-ms", type=int, default=1,
+                    help="kg_snapshot_tune grid_ms: the grid tier's queries as a multi-source bit-parallel BFS "
+                         "(64 queries per group) when dense per-node masks fit (graphs up to ~4 M nodes)")
     ap.add_argument("--grid-bidir", type=int, default=0,
                     help="kg_snapshot_tune grid_bidir: grid slots whose subject has <= this many holders "
                          "alternate forward and backward turns (0: forward only)")
@@ -165,6 +168,7 @@ def apply_tune(snap, a) -> None:
         snap.tune("stream_chunk", a.stream_chunk)
     snap.tune("grid_wgs", a.grid_wgs)
     snap.tune("grid_bidir", a.grid_bidir)
+    snap.tune("grid_ms", a.grid_ms)
     snap.tune("stream_wgs", a.stream_wgs)
     snap.tune("back_wgs", a.back_wgs)
     snap.tune("grid_reserve", 1)  # a server pays this once at start-up, not inside some request's batch

@@ -489,6 +489,21 @@ static int tune_one(Snapshot* s, const char* key, int64_t value) {
     s->expand_tail = (int)value;
     return 0;
   }
+  if (strcmp(key, "grid_ms") == 0) {
+    if (value < 0 || value > 1) return set_error(-2, "grid_ms must be 0 or 1");
+    s->grid_ms = (int)value;
+    return 0;
+  }
+  if (strcmp(key, "grid_ms_bytes") == 0) {
+    if (value < (1 << 20) || value > (1ll << 40)) return set_error(-2, "grid_ms_bytes must be in [2^20, 2^40]");
+    s->grid_ms_bytes = (size_t)value;
+    return 0;
+  }
+  if (strcmp(key, "grid_ms_cap") == 0) {
+    if (value < 0 || value > (1ll << 28)) return set_error(-2, "grid_ms_cap must be in [0, 2^28]");
+    s->grid_ms_cap = (uint64_t)value;
+    return 0;
+  }
   if (strcmp(key, "grid_bidir") == 0) {
     // 0 off, 1 on (a slot is bidirectional when its subject has <= 1024 holders), > 1: that holder cap
     if (value < 0 || value > 0x7FFFFFFF) return set_error(-2, "grid_bidir must be in [0, 2^31)");

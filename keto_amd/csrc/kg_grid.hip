@@ -506,6 +506,9 @@ int grid_reserve(Snapshot* s) {
 int grid_tier(Snapshot* s, Workspace* w, const RQuery* rq, const uint32_t* qlist, const uint32_t* d_count, int global_max_depth,
               uint8_t* out, uint32_t* err, hipStream_t stream, GridStats* gs, int phase) {
   static_assert(sizeof(GridCtl) + 64 <= 32768, "grid readback fits the upper half of the pinned buffer");
+  // graphs small enough for dense per-node masks: 64 queries share each walk (kg_msbfs.hip)
+  if (ms_usable(s, global_max_depth))
+    return ms_tier(s, w, rq, qlist, d_count, global_max_depth, out, err, stream, gs, phase);
   char* pin = (char*)w->host_buf(65536);
   if (!pin) return set_error(-1, "pinned host buffer");
   uint32_t* hb = (uint32_t*)(pin + 32768);  // the lower half holds the batch's Ctl readback

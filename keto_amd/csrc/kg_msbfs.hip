@@ -1,0 +1,448 @@
+// kg_msbfs.hip -- the grid tier's queries as a multi-source bit-parallel BFS (MS-BFS), for graphs
+// whose node count is small enough for dense per-node masks (the heavy-tail point: ~2 x 10^5 nodes,
+// ~250 set edges per node).
+//
+// Why: on such a graph every root reaches the same hub groups within two hops, so the per-query
+// forward searches of the grid tier (kg_grid.hip) walk the SAME edges again and again -- ~1 M edge
+// visits per query, 30-70 G per 250 k-check batch, at the HBM rate of the adjacency stream.  Here 64
+// queries share one walk: every node holds a 64-bit mask per group of 64 queries (bit j = query j of
+// the group), a level expands each frontier node's set row ONCE for all the group's queries that
+// reached it at that hop, and the work per level is the union of the 64 frontiers instead of their
+// sum.  Per query the semantics are exactly the grid tier's / k_stream's (bounded reachability,
+// engine.go:87-145 checkExpandSubject over checkDirect engine.go:148-177, every node expanded once at
+// its shallowest hop): a bit of a node's frontier mask is set only at the hop where that query first
+// reaches the node, and it is expanded only while the query's rest depth allows.
+//
+//   VIS[g][node]  queries of group g that reached the node (and may expand it)
+//   FR[2][g][node] frontier masks of the current / next level
+//   TG[g][node]   queries of group g whose subject the node holds (its check row has the exact tuple:
+//                 the holder index hold[], i.e. checkDirect's answer for every query at once)
+//   HIT[g]        queries of group g answered IsMember; their bits stop propagating at the next tile
+//   PM / EM[g][h] queries whose rest depth lets a node at hop h be probed (D-1 >= h) / expanded (D-2 >= h)
+// Levels are edge-balanced over the whole GPU like the grid tier's: entries (group, node, row) of a
+// level are appended with one packed 64-bit atomic per workgroup (entries << 36 | edges), which
+// yields each entry's edge offset, and tile_first maps every 256-edge tile to its first entry.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+
+#include "kg_bfs.h"
+#include "kg_grid.h"
+#include "kg_internal.h"
+#include "kg_snapshot.h"
+
+namespace kg {
+
+namespace {
+
+constexpr uint32_t MT = 256;                // edges per tile = threads per workgroup
+constexpr uint64_t MS_TILE_CAP = 1ull << 22;  // tiles per level with a tile_first entry (beyond: search)
+constexpr int MS_EDGE_BITS = 36;
+constexpr uint64_t MS_EDGE_MASK = (1ull << MS_EDGE_BITS) - 1;
+constexpr uint64_t MS_ENTRY_MAX = (1ull << (64 - MS_EDGE_BITS)) - 1;
+constexpr int MS_HOPS = 32;  // depth masks per group (global max depth <= 32 here)
+
+struct MsCtl {
+  unsigned long long packed[2];  // per level buffer: entries << 36 | edges
+  unsigned long long edges, logged;
+  uint32_t overflow, pad;
+};
+
+struct MsView {
+  uint32_t n;      // nodes
+  uint32_t G;      // groups of this layout
+  uint64_t cap;    // entries per level buffer
+  uint64_t* vis;   // [G][n]
+  uint64_t* fr[2];  // [G][n] each
+  uint64_t* tg;    // [G][n]
+  uint64_t* hit;   // [G]
+  uint64_t* pm;    // [G][MS_HOPS]
+  uint64_t* em;    // [G][MS_HOPS]
+  uint32_t* qi;    // [G][64] query index (NONE: empty bit)
+  uint32_t* qd;    // [G][64] rest depth
+  uint32_t* eg[2];  // entry group
+  uint32_t* en[2];  // entry node
+  uint32_t* erb[2];  // entry row start (adjx)
+  uint64_t* ex[2];  // entry edge offset within its level
+  uint32_t* tf[2];  // tile -> first entry
+  MsCtl* ctl;
+};
+
+__device__ __forceinline__ uint32_t ms_round_slots(const uint32_t* d_count, uint32_t base, uint32_t cap) {
+  const uint32_t c = *d_count;
+  return c > base ? min(cap, c - base) : 0u;
+}
+
+// Workgroup-aggregated append to level buffer b (every thread of the workgroup calls it).
+__device__ __forceinline__ void ms_append(const MsView& v, int b, bool app, uint32_t g, uint32_t node, uint32_t rb,
+                                          uint32_t len) {
+  __shared__ uint32_t s_wcnt[4];
+  __shared__ uint64_t s_wedge[4];
+  __shared__ unsigned long long s_old;
+  const int lane = lane_id(), wave = threadIdx.x >> 6;
+  const uint64_t m = __ballot(app);
+  uint64_t x = app ? len : 0;
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint64_t y = shfl_up64(x, off);
+    if (lane >= off) x += y;
+  }
+  if (lane == 63) {
+    s_wcnt[wave] = __popcll(m);
+    s_wedge[wave] = x;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint64_t tc = s_wcnt[0] + s_wcnt[1] + s_wcnt[2] + s_wcnt[3];
+    const uint64_t te = s_wedge[0] + s_wedge[1] + s_wedge[2] + s_wedge[3];
+    s_old = tc ? atomicAdd(&v.ctl->packed[b], (unsigned long long)((tc << MS_EDGE_BITS) | te)) : 0ull;
+  }
+  __syncthreads();
+  if (app) {
+    uint64_t at = s_old >> MS_EDGE_BITS, e0 = s_old & MS_EDGE_MASK;
+    for (int w = 0; w < wave; w++) {
+      at += s_wcnt[w];
+      e0 += s_wedge[w];
+    }
+    at += lanes_below(m);
+    e0 += x - len;
+    if (at < v.cap && at < MS_ENTRY_MAX && e0 + len <= MS_EDGE_MASK) {
+      v.eg[b][at] = g;
+      v.en[b][at] = node;
+      v.erb[b][at] = rb;
+      v.ex[b][at] = e0;
+      for (uint64_t t = (e0 + MT - 1) / MT; t * MT < e0 + len && t < MS_TILE_CAP; t++) v.tf[b][t] = (uint32_t)at;
+    } else {
+      v.ctl->overflow = 1;
+    }
+  }
+  __syncthreads();
+}
+
+// The round's queries: bit j of group g = query base + 64 g + j.  Roots are hop 0 (k_resolve probed
+// them); each (group, root) pair becomes one level-0 entry.
+__global__ __launch_bounds__(256) void k_ms_init(const RQuery* __restrict__ rq, const uint32_t* __restrict__ qlist,
+                                                 const uint32_t* d_count, uint32_t base, MsView v) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t nq = ms_round_slots(d_count, base, v.G * 64u);
+  const bool inside = i < v.G * 64u;
+  const bool valid = i < nq;
+  const uint32_t g = i >> 6, j = i & 63;
+  bool app = false;
+  uint32_t node = 0, rb = 0, len = 0;
+  if (inside) {
+    uint32_t qidx = NONE, d = 0;
+    if (valid) {
+      qidx = qlist[base + i];
+      const RQuery q = rq[qidx];
+      d = (uint32_t)max(q.depth, 0);
+      node = q.node;
+      rb = q.beg;
+      len = q.len;
+      const uint64_t bit = 1ull << j;
+      const size_t at = (size_t)g * v.n + node;
+      atomicOr((unsigned long long*)&v.vis[at], (unsigned long long)bit);
+      const uint64_t old = atomicOr((unsigned long long*)&v.fr[0][at], (unsigned long long)bit);
+      app = old == 0 && len > 0;
+    }
+    v.qi[i] = qidx;
+    v.qd[i] = d;
+  }
+  ms_append(v, 0, app, g, node, rb, len);
+}
+
+// One thread per (group, hop): the group's depth masks at that hop (and, at hop 0, a clear hit word).
+__global__ void k_ms_masks(MsView v) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= v.G * (uint32_t)MS_HOPS) return;
+  const uint32_t g = i / MS_HOPS;
+  const int h = (int)(i % MS_HOPS);
+  uint64_t pm = 0, em = 0;
+  for (int j = 0; j < 64; j++) {
+    const int d = (int)v.qd[g * 64 + j];
+    if (d - 1 >= h) pm |= 1ull << j;
+    if (d - 2 >= h) em |= 1ull << j;
+  }
+  v.pm[i] = pm;
+  v.em[i] = em;
+  if (h == 0) v.hit[g] = 0;
+}
+
+// One wave per query: its subject's holders get the query's bit in TG (checkDirect for every node).
+__global__ __launch_bounds__(256) void k_ms_holders(DevSnap s, const RQuery* __restrict__ rq, MsView v) {
+  const uint32_t i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= v.G * 64u) return;
+  const uint32_t qidx = v.qi[i];
+  if (qidx == NONE) return;
+  const uint2 hr = holders_find(s, rq[qidx].subj);
+  const uint64_t bit = 1ull << (i & 63);
+  uint64_t* tg = v.tg + (size_t)(i >> 6) * v.n;
+  for (uint32_t k = lane_id(); k < hr.y; k += 64) atomicOr((unsigned long long*)&tg[s.hold[hr.x + k]], (unsigned long long)bit);
+}
+
+__device__ __forceinline__ uint64_t ms_entry_of(const uint64_t* ex, uint64_t lo, uint64_t hi, uint64_t e) {
+  while (hi - lo > 1) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (ex[mid] <= e) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// Level L: the frontier (hop L) in buffer cur is expanded into hop L+1, appended to buffer cur ^ 1.
+// One thread per edge.  A tile's entries are staged in LDS with their group's masks at tile start,
+// so an edge whose frontier mask is empty (every query of the entry answered or out of depth) is not
+// even loaded.
+__global__ __launch_bounds__(256) void k_ms_level(DevSnap s, MsView v, int L, int cur) {
+  __shared__ uint64_t s_beg[MT + 2], s_f[MT + 2], s_pm[MT + 2], s_em[MT + 2];
+  __shared__ uint32_t s_g[MT + 2], s_rb[MT + 2];
+  __shared__ uint64_t s_j0, s_cnt;
+  if (v.ctl->overflow) return;
+  const int nx = cur ^ 1;
+  const uint64_t packed = v.ctl->packed[cur];
+  const uint64_t n_e = packed >> MS_EDGE_BITS, total = packed & MS_EDGE_MASK;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    v.ctl->edges += total;
+    v.ctl->logged += n_e;
+  }
+  const uint32_t n = v.n;
+  const int h1 = min(L + 1, MS_HOPS - 1);
+  for (uint64_t t0 = (uint64_t)blockIdx.x * MT; t0 < total; t0 += (uint64_t)gridDim.x * MT) {
+    const uint64_t t1 = t0 + MT < total ? t0 + MT : total;
+    if (threadIdx.x == 0) {
+      const uint64_t t = t0 / MT;
+      uint64_t j0, jl;
+      if (t + 1 < MS_TILE_CAP) {
+        j0 = v.tf[cur][t];
+        jl = t1 < total ? v.tf[cur][t + 1] : n_e - 1;
+      } else {
+        j0 = ms_entry_of(v.ex[cur], 0, n_e, t0);
+        jl = ms_entry_of(v.ex[cur], j0, n_e, t1 - 1);
+      }
+      s_j0 = j0;
+      s_cnt = jl - j0 + 1;
+    }
+    __syncthreads();
+    const uint64_t j0 = s_j0, cnt = s_cnt;
+    const bool use_lds = cnt <= MT + 2;  // entries are non-empty: a tile spans <= MT + 1 of them
+    if (use_lds)
+      for (uint32_t i = threadIdx.x; i < cnt; i += MT) {
+        const uint64_t k = j0 + i;
+        const uint32_t g = v.eg[cur][k];
+        s_beg[i] = v.ex[cur][k];
+        s_rb[i] = v.erb[cur][k];
+        s_g[i] = g;
+        s_f[i] = v.fr[cur][(size_t)g * n + v.en[cur][k]] & v.em[(size_t)g * MS_HOPS + min(L, MS_HOPS - 1)] & ~v.hit[g];
+        s_pm[i] = v.pm[(size_t)g * MS_HOPS + h1];
+        s_em[i] = v.em[(size_t)g * MS_HOPS + h1];
+      }
+    __syncthreads();
+    const uint64_t e = t0 + threadIdx.x;
+    bool app = false;
+    uint32_t g = 0, child = 0, cb = 0, clen = 0;
+    if (e < t1) {
+      uint64_t beg, f, pm, em;
+      uint32_t rb;
+      if (use_lds) {
+        uint32_t lo = 0, hi = (uint32_t)cnt;
+        while (hi - lo > 1) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (s_beg[mid] <= e) lo = mid;
+          else hi = mid;
+        }
+        beg = s_beg[lo];
+        rb = s_rb[lo];
+        g = s_g[lo];
+        f = s_f[lo];
+        pm = s_pm[lo];
+        em = s_em[lo];
+      } else {
+        const uint64_t k = j0 + ms_entry_of(v.ex[cur] + j0, 0, cnt, e);
+        g = v.eg[cur][k];
+        beg = v.ex[cur][k];
+        rb = v.erb[cur][k];
+        f = v.fr[cur][(size_t)g * n + v.en[cur][k]] & v.em[(size_t)g * MS_HOPS + min(L, MS_HOPS - 1)] & ~v.hit[g];
+        pm = v.pm[(size_t)g * MS_HOPS + h1];
+        em = v.em[(size_t)g * MS_HOPS + h1];
+      }
+      if (f) {
+        const AdjX x = s.adjx[rb + (e - beg)];
+        child = x.node;
+        const size_t at = (size_t)g * n + child;
+        // checkDirect at hop L+1 for every query of the frontier mask that may still probe there
+        const uint64_t probe = f & pm;
+        const uint64_t tgm = probe ? v.tg[at] : 0ull;
+        if (probe & tgm) atomicOr((unsigned long long*)&v.hit[g], (unsigned long long)(probe & tgm));
+        // expansion: the queries that reach the child first at this hop and may expand it
+        const uint64_t want = x.len ? (f & em) : 0ull;
+        if (want) {
+          uint64_t nw = want & ~v.vis[at];
+          if (nw) {
+            nw &= ~(uint64_t)atomicOr((unsigned long long*)&v.vis[at], (unsigned long long)nw);
+            if (nw) {
+              const uint64_t o2 = atomicOr((unsigned long long*)&v.fr[nx][at], (unsigned long long)nw);
+              app = o2 == 0;
+              cb = x.begin;
+              clen = x.len;
+            }
+          }
+        }
+      }
+    }
+    ms_append(v, nx, app, g, child, cb, clen);
+  }
+}
+
+// After level L: the level's frontier masks are cleared (the buffer is the level after next's).
+__global__ __launch_bounds__(256) void k_ms_clear(MsView v, int cur) {
+  const uint64_t n_e = v.ctl->packed[cur] >> MS_EDGE_BITS;
+  const uint64_t lim = n_e < v.cap ? n_e : v.cap;
+  for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < lim; k += (uint64_t)gridDim.x * blockDim.x)
+    v.fr[cur][(size_t)v.eg[cur][k] * v.n + v.en[cur][k]] = 0;
+}
+
+__global__ void k_ms_finish(MsView v, const uint32_t* d_count, uint32_t base, uint8_t* out, uint32_t* err) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= ms_round_slots(d_count, base, v.G * 64u) || v.ctl->overflow) return;
+  const uint32_t qidx = v.qi[i];
+  out[qidx] = ((v.hit[i >> 6] >> (i & 63)) & 1ull) ? KG_IS_MEMBER : KG_NOT_MEMBER;
+  if (err) err[qidx] = KG_ERR_NONE;
+}
+
+size_t ms_group_bytes(uint32_t n) { return (size_t)n * 8 * 4 + 8 + 2 * MS_HOPS * 8 + 64 * 8; }
+
+// Pool layout for G groups and level buffers of `cap` entries.
+int ms_layout(GridPool* P, uint32_t n, uint32_t G, uint64_t cap, MsView* v) {
+  const size_t gn = (size_t)G * n * 8;
+  const size_t need = 4 * gn + (size_t)G * (8 + 2 * MS_HOPS * 8 + 64 * 8) + 2 * (cap * (4 + 4 + 4 + 8) + MS_TILE_CAP * 4) +
+                      sizeof(MsCtl) + 8192;
+  if (need > P->bytes) {
+    P->release();
+    HIPC(hipMalloc(&P->mem, need));
+    P->bytes = need;
+  }
+  char* p = (char*)P->mem;
+  v->n = n;
+  v->G = G;
+  v->cap = cap;
+  v->vis = (uint64_t*)p;
+  p += gn;
+  v->fr[0] = (uint64_t*)p;
+  p += gn;
+  v->fr[1] = (uint64_t*)p;
+  p += gn;
+  v->tg = (uint64_t*)p;
+  p += gn;
+  v->hit = (uint64_t*)p;
+  p += (size_t)G * 8;
+  v->pm = (uint64_t*)p;
+  p += (size_t)G * MS_HOPS * 8;
+  v->em = (uint64_t*)p;
+  p += (size_t)G * MS_HOPS * 8;
+  v->qi = (uint32_t*)p;
+  p += (size_t)G * 64 * 4;
+  v->qd = (uint32_t*)p;
+  p += (size_t)G * 64 * 4;
+  for (int b = 0; b < 2; b++) {
+    v->ex[b] = (uint64_t*)p;
+    p += cap * 8;
+    v->eg[b] = (uint32_t*)p;
+    p += cap * 4;
+    v->en[b] = (uint32_t*)p;
+    p += cap * 4;
+    v->erb[b] = (uint32_t*)p;
+    p += cap * 4;
+    v->tf[b] = (uint32_t*)p;
+    p += MS_TILE_CAP * 4;
+  }
+  v->ctl = (MsCtl*)(((uintptr_t)p + 255) & ~uintptr_t(255));
+  return 0;
+}
+
+}  // namespace
+
+// Whether the MS-BFS path serves this snapshot's grid tier (kg_snapshot_tune "grid_ms"): the dense
+// masks of one group must fit an eighth of the pool budget, and the holder index must exist.
+bool ms_usable(const Snapshot* s, int global_max_depth) {
+  if (!s->grid_ms || !s->ds.hold || !s->ds.hslots || s->ds.n_nodes == 0 || global_max_depth > MS_HOPS) return false;
+  return ms_group_bytes(s->ds.n_nodes) * 8 <= s->grid_ms_bytes;
+}
+
+// Same protocol as grid_tier (kg_grid.hip): phase 1 enqueues the first round and returns 1, phase 2
+// resumes after the batch's synchronisation; a round that overflows a level buffer reruns with a
+// quarter of the groups.
+int ms_tier(Snapshot* s, Workspace* w, const RQuery* rq, const uint32_t* qlist, const uint32_t* d_count,
+            int global_max_depth, uint8_t* out, uint32_t* err, hipStream_t stream, GridStats* gs, int phase) {
+  char* pin = (char*)w->host_buf(65536);
+  if (!pin) return set_error(-1, "pinned host buffer");
+  uint32_t* hb = (uint32_t*)(pin + 32768);
+  const uint32_t n = s->ds.n_nodes;
+  const uint32_t g_max = (uint32_t)std::max<size_t>(1, std::min<size_t>(1u << 14, s->grid_ms_bytes / ms_group_bytes(n)));
+  const uint64_t cap = s->grid_ms_cap ? s->grid_ms_cap : 16ull << 20;  // entries per level buffer
+  GridPool* gp = &w->ms;
+  MsView v{};
+  uint32_t G = g_max;
+  if (int rc = ms_layout(gp, n, G, std::min<uint64_t>(cap, (uint64_t)G * n + 1024), &v)) return rc;
+  const int levels = std::max(0, global_max_depth - 1);  // level L expands hop L (D - 2 >= L)
+  const uint32_t lgrid = (uint32_t)s->n_cu * s->grid_wgs;
+  int64_t count = -1;
+  bool resume = phase == 2;
+  for (uint32_t done = 0; count < 0 || done < (uint64_t)count;) {
+    if (!resume) {
+      if (phase == 1) w->grid_reran = false;
+      if (phase == 2) w->grid_reran = true;
+      v.G = G;
+      const size_t gn = (size_t)G * n * 8;
+      // the round's masks start clear (frontier buffers are cleared level by level, but an
+      // overflowed round may leave them dirty)
+      HIPC(hipMemsetAsync(v.vis, 0, gn, stream));
+      HIPC(hipMemsetAsync(v.fr[0], 0, gn, stream));
+      HIPC(hipMemsetAsync(v.fr[1], 0, gn, stream));
+      HIPC(hipMemsetAsync(v.tg, 0, gn, stream));
+      HIPC(hipMemsetAsync(v.ctl, 0, sizeof(MsCtl), stream));
+      const uint32_t qblocks = (G * 64 + 255) / 256;
+      hipLaunchKernelGGL(k_ms_init, dim3(qblocks), dim3(256), 0, stream, rq, qlist, d_count, done, v);
+      HIPC(hipGetLastError());
+      hipLaunchKernelGGL(k_ms_masks, dim3((G * MS_HOPS + 255) / 256), dim3(256), 0, stream, v);
+      HIPC(hipGetLastError());
+      hipLaunchKernelGGL(k_ms_holders, dim3((G * 64 + 3) / 4), dim3(256), 0, stream, s->ds, rq, v);
+      HIPC(hipGetLastError());
+      for (int L = 0; L < levels; L++) {
+        const int cur = L & 1;
+        hipLaunchKernelGGL(k_ms_level, dim3(lgrid), dim3(256), 0, stream, s->ds, v, L, cur);
+        HIPC(hipGetLastError());
+        hipLaunchKernelGGL(k_ms_clear, dim3((uint32_t)s->n_cu * 4), dim3(256), 0, stream, v, cur);
+        HIPC(hipGetLastError());
+        HIPC(hipMemsetAsync(&v.ctl->packed[cur], 0, 8, stream));
+      }
+      hipLaunchKernelGGL(k_ms_finish, dim3(qblocks), dim3(256), 0, stream, v, d_count, done, out, err);
+      HIPC(hipGetLastError());
+      HIPC(hipMemcpyAsync(hb, v.ctl, sizeof(MsCtl), hipMemcpyDeviceToHost, stream));
+      HIPC(hipMemcpyAsync(hb + sizeof(MsCtl) / 4, d_count, 4, hipMemcpyDeviceToHost, stream));
+      if (phase == 1) return 1;
+      HIPC(hipStreamSynchronize(stream));
+    }
+    resume = false;
+    MsCtl h{};
+    memcpy(&h, hb, sizeof h);
+    count = hb[sizeof(MsCtl) / 4];
+    const uint32_t cnt = count > done ? (uint32_t)std::min<int64_t>((int64_t)G * 64, count - done) : 0u;
+    if (gs) {
+      gs->rows += h.logged;
+      gs->edges += h.edges;
+    }
+    if (h.overflow) {
+      if (G == 1) return set_error(KG_ERR_RESOURCE_CODE, "MS-BFS level buffer exceeded with one group");
+      G = std::max<uint32_t>(1, std::min(G, (cnt + 63) / 64) / 4);
+      continue;
+    }
+    if (gs) {
+      gs->done += cnt;
+      gs->logged += h.logged;
+    }
+    done += cnt;
+  }
+  return 0;
+}
+
+}  // namespace kg

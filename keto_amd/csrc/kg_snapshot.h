@@ -52,6 +52,7 @@ struct Workspace {
   void* heavy_pool = nullptr;
   size_t heavy_pool_bytes = 0;
   GridPool grid;  // grid tier, sized for the queries that reach it (16 Mi log entries)
+  GridPool ms;    // the grid tier's MS-BFS path (kg_msbfs.hip): dense masks of its query groups
   bool grid_reran = false;  // the last batch's grid tier ran rounds after the first (results rewritten)
   void* split = nullptr;  // formula split (kg_formula.hip): leaf queries, their results, per-query plan refs
   size_t split_bytes = 0;
@@ -240,6 +241,9 @@ struct Snapshot {
   int back_wgs = 2;          // kg_snapshot_tune("back_wgs"): k_back workgroups per CU (1..3, LDS allows 3; 2 = bench C2 default)
   uint64_t grid_small_cap = 0;  // kg_snapshot_tune("grid_cap"): workspace grid-log entries (0 = 16 Mi; tests)
   int expand_tail = 1;  // kg_snapshot_tune("expand_tail"): expand passes 2/3 walk with LDS-cached frames (0: round 2)
+  int grid_ms = 1;  // kg_snapshot_tune("grid_ms"): grid-tier queries as MS-BFS when the dense masks fit (0: off)
+  size_t grid_ms_bytes = 1ull << 30;  // kg_snapshot_tune("grid_ms_bytes"): MS-BFS mask budget per workspace
+  uint64_t grid_ms_cap = 0;  // kg_snapshot_tune("grid_ms_cap"): MS-BFS entries per level buffer (0 = 16 Mi; tests)
   int grid_bidir = 0;  // kg_snapshot_tune("grid_bidir"): grid slots whose subject has <= this many holders go bidirectional (0: none)
                        // alternate forward and backward turns (0: forward only)
   // replicas: the same snapshot on more devices (kg_snapshot_create's device mask); this object is

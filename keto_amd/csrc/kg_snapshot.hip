@@ -275,6 +275,7 @@ Workspace::~Workspace() {
   if (scratch) hipFree(scratch);
   if (heavy_pool) hipFree(heavy_pool);
   grid.release();
+  ms.release();
   if (interp_pool) hipFree(interp_pool);
   if (split) hipFree(split);
   if (pinned) hipHostFree(pinned);

@@ -160,8 +160,10 @@ def test_workgroup_tiers_lds_and_hbm(tiers, wide, back, grid_cap):
     e.snapshot.tune("wide", wide)
     e.snapshot.tune("back", back)
     # grid_cap: the workspace's grid log holds 600 / 5000 entries, so rounds overflow, rerun with
-    # fewer slots, and the queries that overflow it alone run in the shared full-size pool
+    # fewer slots, and the queries that overflow it alone run in the shared full-size pool (the
+    # per-query rounds: MS-BFS off); grid_cap 0 runs the grid tier's queries as MS-BFS (kg_msbfs.hip)
     e.snapshot.tune("grid_cap", grid_cap)
+    e.snapshot.tune("grid_ms", 0 if grid_cap else 1)
     it = reg.interner
     qs = [RelationTuple.from_string(s) for s in
           ["g:root#m@target", "g:root#m@mid", "g:root#m@none", "g:c3#m@target", "g:c7#m@mid", "g:d3#m@target",
@@ -615,12 +617,17 @@ def test_bench_tune_set_vs_oracle(preset, n_tuples):
         assert 0.05 < (out == 1).mean() < 0.95
 
 
-@pytest.mark.parametrize("bidir,grid_cap,seed", [(1024, 0, 0), (1024, 0, 1), (0, 0, 0), (1024, 700, 2), (2, 0, 3), (64, 0, 4)])
-def test_grid_bidirectional_dense_vs_oracle(bidir, grid_cap, seed):
-    """The grid tier's bidirectional rounds (kg_grid.hip) on dense graphs with cycles, hubs and
-    subjects held only by rows nothing points at: a tiny stream-tier edge budget and the backward
-    tier off send nearly every query there; every depth 2..9 is bit-exact with the oracle, with
-    grid_bidir on and off, and with a log small enough that rounds overflow and rerun (grid_cap)."""
+@pytest.mark.parametrize("ms,bidir,grid_cap,seed", [(0, 1024, 0, 0), (0, 1024, 0, 1), (0, 0, 0, 0), (0, 1024, 700, 2),
+                                                     (0, 2, 0, 3), (0, 64, 0, 4), (1, 0, 0, 0), (1, 0, 0, 1),
+                                                     (1, 0, 40, 2), (1, 0, 300, 3), (1, 1024, 0, 5)])
+def test_grid_bidirectional_dense_vs_oracle(ms, bidir, grid_cap, seed):
+    """The grid tier on dense graphs with cycles, hubs and subjects held only by rows nothing points
+    at: a tiny stream-tier edge budget and the backward tier off send nearly every query there; every
+    depth 2..9 is bit-exact with the oracle.  ms 0: the per-query rounds (kg_grid.hip), bidirectional
+    or forward only, with a log small enough that rounds overflow and rerun (grid_cap); ms 1: the
+    multi-source bit-parallel BFS (kg_msbfs.hip, 64 queries per group, ~40 groups per batch), with
+    level buffers small enough that rounds overflow and rerun with fewer groups (grid_cap as
+    grid_ms_cap)."""
     rng = np.random.default_rng(900 + seed)
     n_obj, n_users = 120, 60
     tuples = []
@@ -639,7 +646,8 @@ def test_grid_bidirectional_dense_vs_oracle(bidir, grid_cap, seed):
     snap.tune("stream_ecap", 3)
     snap.tune("back", 0)
     snap.tune("grid_bidir", bidir)
-    snap.tune("grid_cap", grid_cap)
+    snap.tune("grid_ms", ms)
+    snap.tune("grid_ms_cap" if ms else "grid_cap", grid_cap)
     it = reg.interner
     qs = []
     for _ in range(2500):
