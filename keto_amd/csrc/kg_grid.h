@@ -13,7 +13,7 @@ struct GridStats {
 struct Snapshot;
 struct Workspace;
 int grid_tier(Snapshot* s, Workspace* w, const RQuery* rq, const uint32_t* qlist, const uint32_t* d_count, int global_max_depth,
-              uint8_t* out, uint32_t* err, hipStream_t stream, GridStats* gs, int phase = 0);
+              uint8_t* out, uint32_t* err, hipStream_t stream, GridStats* gs, int phase = 0, bool allow_ms = true);
 // kg_msbfs.hip: the grid tier's queries as a multi-source bit-parallel BFS (64 queries per group)
 bool ms_usable(const Snapshot* s, int global_max_depth);
 int ms_tier(Snapshot* s, Workspace* w, const RQuery* rq, const uint32_t* qlist, const uint32_t* d_count,

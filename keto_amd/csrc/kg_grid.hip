@@ -504,11 +504,18 @@ int grid_reserve(Snapshot* s) {
 // kg_snapshot_tune "grid_reserve"; one query at a time), so no workspace ever reallocates.  After
 // a round succeeds the slot count grows back (x4), so one giant query does not serialise the rest.
 int grid_tier(Snapshot* s, Workspace* w, const RQuery* rq, const uint32_t* qlist, const uint32_t* d_count, int global_max_depth,
-              uint8_t* out, uint32_t* err, hipStream_t stream, GridStats* gs, int phase) {
+              uint8_t* out, uint32_t* err, hipStream_t stream, GridStats* gs, int phase, bool allow_ms) {
   static_assert(sizeof(GridCtl) + 64 <= 32768, "grid readback fits the upper half of the pinned buffer");
   // graphs small enough for dense per-node masks: 64 queries share each walk (kg_msbfs.hip)
-  if (ms_usable(s, global_max_depth))
-    return ms_tier(s, w, rq, qlist, d_count, global_max_depth, out, err, stream, gs, phase);
+  if (allow_ms && ms_usable(s, global_max_depth)) {
+    const int rc = ms_tier(s, w, rq, qlist, d_count, global_max_depth, out, err, stream, gs, phase);
+    if (rc != 2) return rc;
+    // a single group overflowed the MS-BFS level buffers: every query of the list runs the per-query
+    // rounds (answers already written are rewritten with the same values)
+    if (int rc2 = grid_tier(s, w, rq, qlist, d_count, global_max_depth, out, err, stream, gs, 0, false)) return rc2;
+    w->grid_reran = true;
+    return 0;
+  }
   char* pin = (char*)w->host_buf(65536);
   if (!pin) return set_error(-1, "pinned host buffer");
   uint32_t* hb = (uint32_t*)(pin + 32768);  // the lower half holds the batch's Ctl readback

@@ -370,7 +370,8 @@ bool ms_usable(const Snapshot* s, int global_max_depth) {
 
 // Same protocol as grid_tier (kg_grid.hip): phase 1 enqueues the first round and returns 1, phase 2
 // resumes after the batch's synchronisation; a round that overflows a level buffer reruns with a
-// quarter of the groups.
+// quarter of the groups.  Returns 2 when a single group overflows them: the caller runs the rest of
+// the list (from the first query not yet answered) through the per-query rounds.
 int ms_tier(Snapshot* s, Workspace* w, const RQuery* rq, const uint32_t* qlist, const uint32_t* d_count,
             int global_max_depth, uint8_t* out, uint32_t* err, hipStream_t stream, GridStats* gs, int phase) {
   char* pin = (char*)w->host_buf(65536);
@@ -432,7 +433,10 @@ int ms_tier(Snapshot* s, Workspace* w, const RQuery* rq, const uint32_t* qlist, 
       gs->edges += h.edges;
     }
     if (h.overflow) {
-      if (G == 1) return set_error(KG_ERR_RESOURCE_CODE, "MS-BFS level buffer exceeded with one group");
+      if (G == 1) {  // one group alone overflows the level buffers: the per-query rounds take the list
+        if (gs) gs->done -= done;
+        return 2;
+      }
       G = std::max<uint32_t>(1, std::min(G, (cnt + 63) / 64) / 4);
       continue;
     }
