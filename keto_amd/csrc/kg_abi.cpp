@@ -499,6 +499,12 @@ static int tune_one(Snapshot* s, const char* key, int64_t value) {
     s->grid_ms_bytes = (size_t)value;
     return 0;
   }
+  if (strcmp(key, "grid_ms_words") == 0) {
+    if (value != 1 && value != 2 && value != 4 && value != 8 && value != 16)
+      return set_error(-2, "grid_ms_words must be 1, 2, 4, 8 or 16");
+    s->grid_ms_words = (int)value;
+    return 0;
+  }
   if (strcmp(key, "grid_ms_cap") == 0) {
     if (value < 0 || value > (1ll << 28)) return set_error(-2, "grid_ms_cap must be in [0, 2^28]");
     s->grid_ms_cap = (uint64_t)value;

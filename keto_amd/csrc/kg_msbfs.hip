@@ -36,8 +36,7 @@ namespace kg {
 
 namespace {
 
-constexpr uint32_t MT = 256;                // edges per tile = threads per workgroup
-constexpr uint64_t MS_TILE_CAP = 1ull << 22;  // tiles per level with a tile_first entry (beyond: search)
+constexpr uint64_t MS_TILE_CAP = 1ull << 24;  // tiles per level with a tile_first entry (beyond: search)
 constexpr int MS_EDGE_BITS = 36;
 constexpr uint64_t MS_EDGE_MASK = (1ull << MS_EDGE_BITS) - 1;
 constexpr uint64_t MS_ENTRY_MAX = (1ull << (64 - MS_EDGE_BITS)) - 1;
@@ -49,18 +48,21 @@ struct MsCtl {
   uint32_t overflow, pad;
 };
 
+// A group is 64 * K queries; every per-node mask is K consecutive 64-bit words (node-major), so the
+// K lanes that handle one edge touch one contiguous 8K-byte run of each mask array.
 struct MsView {
   uint32_t n;      // nodes
-  uint32_t G;      // groups of this layout
+  uint32_t G;      // groups of this round
   uint64_t cap;    // entries per level buffer
-  uint64_t* vis;   // [G][n]
-  uint64_t* fr[2];  // [G][n] each
-  uint64_t* tg;    // [G][n]
-  uint64_t* hit;   // [G]
-  uint64_t* pm;    // [G][MS_HOPS]
-  uint64_t* em;    // [G][MS_HOPS]
-  uint32_t* qi;    // [G][64] query index (NONE: empty bit)
-  uint32_t* qd;    // [G][64] rest depth
+  uint64_t* vis;   // [G][n][K]
+  uint64_t* fr[2];  // [G][n][K] each
+  uint64_t* tg;    // [G][n][K]
+  uint32_t* stamp;  // [G][n]: 1 + the last hop the node was appended at (one entry per hop)
+  uint64_t* hit;   // [G][K]
+  uint64_t* pm;    // [G][MS_HOPS][K]
+  uint64_t* em;    // [G][MS_HOPS][K]
+  uint32_t* qi;    // [G][64K] query index (NONE: empty bit)
+  uint32_t* qd;    // [G][64K] rest depth
   uint32_t* eg[2];  // entry group
   uint32_t* en[2];  // entry node
   uint32_t* erb[2];  // entry row start (adjx)
@@ -74,7 +76,9 @@ __device__ __forceinline__ uint32_t ms_round_slots(const uint32_t* d_count, uint
   return c > base ? min(cap, c - base) : 0u;
 }
 
-// Workgroup-aggregated append to level buffer b (every thread of the workgroup calls it).
+// Workgroup-aggregated append to level buffer b (every thread of the workgroup calls it); TE edges
+// per tile of the level kernel that will read the buffer.
+template <uint32_t TE>
 __device__ __forceinline__ void ms_append(const MsView& v, int b, bool app, uint32_t g, uint32_t node, uint32_t rb,
                                           uint32_t len) {
   __shared__ uint32_t s_wcnt[4];
@@ -111,7 +115,7 @@ __device__ __forceinline__ void ms_append(const MsView& v, int b, bool app, uint
       v.en[b][at] = node;
       v.erb[b][at] = rb;
       v.ex[b][at] = e0;
-      for (uint64_t t = (e0 + MT - 1) / MT; t * MT < e0 + len && t < MS_TILE_CAP; t++) v.tf[b][t] = (uint32_t)at;
+      for (uint64_t t = (e0 + TE - 1) / TE; t * TE < e0 + len && t < MS_TILE_CAP; t++) v.tf[b][t] = (uint32_t)at;
     } else {
       v.ctl->overflow = 1;
     }
@@ -119,65 +123,70 @@ __device__ __forceinline__ void ms_append(const MsView& v, int b, bool app, uint
   __syncthreads();
 }
 
-// The round's queries: bit j of group g = query base + 64 g + j.  Roots are hop 0 (k_resolve probed
-// them); each (group, root) pair becomes one level-0 entry.
+// The round's queries: bit b of group g = query base + 64K g + b (word b / 64).  Roots are hop 0
+// (k_resolve probed them); each (group, root) pair becomes one level-0 entry.
+template <int K>
 __global__ __launch_bounds__(256) void k_ms_init(const RQuery* __restrict__ rq, const uint32_t* __restrict__ qlist,
                                                  const uint32_t* d_count, uint32_t base, MsView v) {
+  constexpr uint32_t Q = 64u * K;
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t nq = ms_round_slots(d_count, base, v.G * 64u);
-  const bool inside = i < v.G * 64u;
-  const bool valid = i < nq;
-  const uint32_t g = i >> 6, j = i & 63;
+  const uint32_t nq = ms_round_slots(d_count, base, v.G * Q);
+  const bool inside = i < v.G * Q;
+  const uint32_t g = i / Q, b = i % Q;
   bool app = false;
   uint32_t node = 0, rb = 0, len = 0;
   if (inside) {
     uint32_t qidx = NONE, d = 0;
-    if (valid) {
+    if (i < nq) {
       qidx = qlist[base + i];
       const RQuery q = rq[qidx];
       d = (uint32_t)max(q.depth, 0);
       node = q.node;
       rb = q.beg;
       len = q.len;
-      const uint64_t bit = 1ull << j;
-      const size_t at = (size_t)g * v.n + node;
+      const uint64_t bit = 1ull << (b & 63);
+      const size_t at = ((size_t)g * v.n + node) * K + (b >> 6);
       atomicOr((unsigned long long*)&v.vis[at], (unsigned long long)bit);
-      const uint64_t old = atomicOr((unsigned long long*)&v.fr[0][at], (unsigned long long)bit);
-      app = old == 0 && len > 0;
+      atomicOr((unsigned long long*)&v.fr[0][at], (unsigned long long)bit);
+      app = len > 0 && atomicMax(&v.stamp[(size_t)g * v.n + node], 1u) < 1u;
     }
     v.qi[i] = qidx;
     v.qd[i] = d;
   }
-  ms_append(v, 0, app, g, node, rb, len);
+  ms_append<256u / K>(v, 0, app, g, node, rb, len);
 }
 
-// One thread per (group, hop): the group's depth masks at that hop (and, at hop 0, a clear hit word).
+// One thread per (group, hop, word): the depth masks (and, at hop 0, a clear hit word).
+template <int K>
 __global__ void k_ms_masks(MsView v) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= v.G * (uint32_t)MS_HOPS) return;
-  const uint32_t g = i / MS_HOPS;
-  const int h = (int)(i % MS_HOPS);
+  if (i >= v.G * (uint32_t)MS_HOPS * K) return;
+  const uint32_t g = i / (MS_HOPS * K), r = i % (MS_HOPS * K);
+  const int h = (int)(r / K), k = (int)(r % K);
   uint64_t pm = 0, em = 0;
   for (int j = 0; j < 64; j++) {
-    const int d = (int)v.qd[g * 64 + j];
+    const int d = (int)v.qd[(size_t)g * 64 * K + k * 64 + j];
     if (d - 1 >= h) pm |= 1ull << j;
     if (d - 2 >= h) em |= 1ull << j;
   }
   v.pm[i] = pm;
   v.em[i] = em;
-  if (h == 0) v.hit[g] = 0;
+  if (h == 0) v.hit[(size_t)g * K + k] = 0;
 }
 
 // One wave per query: its subject's holders get the query's bit in TG (checkDirect for every node).
+template <int K>
 __global__ __launch_bounds__(256) void k_ms_holders(DevSnap s, const RQuery* __restrict__ rq, MsView v) {
+  constexpr uint32_t Q = 64u * K;
   const uint32_t i = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (i >= v.G * 64u) return;
+  if (i >= v.G * Q) return;
   const uint32_t qidx = v.qi[i];
   if (qidx == NONE) return;
   const uint2 hr = holders_find(s, rq[qidx].subj);
-  const uint64_t bit = 1ull << (i & 63);
-  uint64_t* tg = v.tg + (size_t)(i >> 6) * v.n;
-  for (uint32_t k = lane_id(); k < hr.y; k += 64) atomicOr((unsigned long long*)&tg[s.hold[hr.x + k]], (unsigned long long)bit);
+  const uint32_t g = i / Q, b = i % Q;
+  const uint64_t bit = 1ull << (b & 63);
+  for (uint32_t k = lane_id(); k < hr.y; k += 64)
+    atomicOr((unsigned long long*)&v.tg[((size_t)g * v.n + s.hold[hr.x + k]) * K + (b >> 6)], (unsigned long long)bit);
 }
 
 __device__ __forceinline__ uint64_t ms_entry_of(const uint64_t* ex, uint64_t lo, uint64_t hi, uint64_t e) {
@@ -190,12 +199,15 @@ __device__ __forceinline__ uint64_t ms_entry_of(const uint64_t* ex, uint64_t lo,
 }
 
 // Level L: the frontier (hop L) in buffer cur is expanded into hop L+1, appended to buffer cur ^ 1.
-// One thread per edge.  A tile's entries are staged in LDS with their group's masks at tile start,
-// so an edge whose frontier mask is empty (every query of the entry answered or out of depth) is not
-// even loaded.
+// K lanes per edge (lane k owns mask word k), TE = 256 / K edges per tile.  A tile's entries are
+// staged in LDS with their frontier masks (already filtered by depth and answered queries at tile
+// start), so a word with nothing to propagate costs no memory access, and an edge whose K words are
+// all empty is not even loaded.
+template <int K>
 __global__ __launch_bounds__(256) void k_ms_level(DevSnap s, MsView v, int L, int cur) {
-  __shared__ uint64_t s_beg[MT + 2], s_f[MT + 2], s_pm[MT + 2], s_em[MT + 2];
-  __shared__ uint32_t s_g[MT + 2], s_rb[MT + 2];
+  constexpr uint32_t TE = 256u / K;
+  __shared__ uint64_t s_beg[TE + 2], s_f[TE + 2][K], s_pm[TE + 2][K], s_em[TE + 2][K];
+  __shared__ uint32_t s_g[TE + 2], s_rb[TE + 2];
   __shared__ uint64_t s_j0, s_cnt;
   if (v.ctl->overflow) return;
   const int nx = cur ^ 1;
@@ -206,11 +218,12 @@ __global__ __launch_bounds__(256) void k_ms_level(DevSnap s, MsView v, int L, in
     v.ctl->logged += n_e;
   }
   const uint32_t n = v.n;
-  const int h1 = min(L + 1, MS_HOPS - 1);
-  for (uint64_t t0 = (uint64_t)blockIdx.x * MT; t0 < total; t0 += (uint64_t)gridDim.x * MT) {
-    const uint64_t t1 = t0 + MT < total ? t0 + MT : total;
+  const int h0 = min(L, MS_HOPS - 1), h1 = min(L + 1, MS_HOPS - 1);
+  const uint32_t my_e = threadIdx.x / K, k = threadIdx.x % K;
+  for (uint64_t t0 = (uint64_t)blockIdx.x * TE; t0 < total; t0 += (uint64_t)gridDim.x * TE) {
+    const uint64_t t1 = t0 + TE < total ? t0 + TE : total;
     if (threadIdx.x == 0) {
-      const uint64_t t = t0 / MT;
+      const uint64_t t = t0 / TE;
       uint64_t j0, jl;
       if (t + 1 < MS_TILE_CAP) {
         j0 = v.tf[cur][t];
@@ -223,65 +236,52 @@ __global__ __launch_bounds__(256) void k_ms_level(DevSnap s, MsView v, int L, in
       s_cnt = jl - j0 + 1;
     }
     __syncthreads();
-    const uint64_t j0 = s_j0, cnt = s_cnt;
-    const bool use_lds = cnt <= MT + 2;  // entries are non-empty: a tile spans <= MT + 1 of them
-    if (use_lds)
-      for (uint32_t i = threadIdx.x; i < cnt; i += MT) {
-        const uint64_t k = j0 + i;
-        const uint32_t g = v.eg[cur][k];
-        s_beg[i] = v.ex[cur][k];
-        s_rb[i] = v.erb[cur][k];
+    const uint64_t j0 = s_j0, cnt = s_cnt;  // entries are non-empty: a tile spans <= TE + 1 of them
+    for (uint32_t w = threadIdx.x; w < cnt * K; w += 256) {
+      const uint32_t i = w / K, kk = w % K;
+      const uint64_t q = j0 + i;
+      const uint32_t g = v.eg[cur][q];
+      if (kk == 0) {
+        s_beg[i] = v.ex[cur][q];
+        s_rb[i] = v.erb[cur][q];
         s_g[i] = g;
-        s_f[i] = v.fr[cur][(size_t)g * n + v.en[cur][k]] & v.em[(size_t)g * MS_HOPS + min(L, MS_HOPS - 1)] & ~v.hit[g];
-        s_pm[i] = v.pm[(size_t)g * MS_HOPS + h1];
-        s_em[i] = v.em[(size_t)g * MS_HOPS + h1];
       }
+      s_f[i][kk] = v.fr[cur][((size_t)g * n + v.en[cur][q]) * K + kk] & v.em[((size_t)g * MS_HOPS + h0) * K + kk] &
+                   ~v.hit[(size_t)g * K + kk];
+      s_pm[i][kk] = v.pm[((size_t)g * MS_HOPS + h1) * K + kk];
+      s_em[i][kk] = v.em[((size_t)g * MS_HOPS + h1) * K + kk];
+    }
     __syncthreads();
-    const uint64_t e = t0 + threadIdx.x;
+    const uint64_t e = t0 + my_e;
     bool app = false;
     uint32_t g = 0, child = 0, cb = 0, clen = 0;
     if (e < t1) {
-      uint64_t beg, f, pm, em;
-      uint32_t rb;
-      if (use_lds) {
-        uint32_t lo = 0, hi = (uint32_t)cnt;
-        while (hi - lo > 1) {
-          const uint32_t mid = (lo + hi) >> 1;
-          if (s_beg[mid] <= e) lo = mid;
-          else hi = mid;
-        }
-        beg = s_beg[lo];
-        rb = s_rb[lo];
-        g = s_g[lo];
-        f = s_f[lo];
-        pm = s_pm[lo];
-        em = s_em[lo];
-      } else {
-        const uint64_t k = j0 + ms_entry_of(v.ex[cur] + j0, 0, cnt, e);
-        g = v.eg[cur][k];
-        beg = v.ex[cur][k];
-        rb = v.erb[cur][k];
-        f = v.fr[cur][(size_t)g * n + v.en[cur][k]] & v.em[(size_t)g * MS_HOPS + min(L, MS_HOPS - 1)] & ~v.hit[g];
-        pm = v.pm[(size_t)g * MS_HOPS + h1];
-        em = v.em[(size_t)g * MS_HOPS + h1];
+      uint32_t lo = 0, hi = (uint32_t)cnt;
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (s_beg[mid] <= e) lo = mid;
+        else hi = mid;
       }
+      const uint64_t f = s_f[lo][k];
+      g = s_g[lo];
       if (f) {
-        const AdjX x = s.adjx[rb + (e - beg)];
+        const AdjX x = s.adjx[s_rb[lo] + (e - s_beg[lo])];
         child = x.node;
-        const size_t at = (size_t)g * n + child;
-        // checkDirect at hop L+1 for every query of the frontier mask that may still probe there
-        const uint64_t probe = f & pm;
+        const size_t at = ((size_t)g * n + child) * K + k;
+        // checkDirect at hop L+1 for every query of the word that may still probe there
+        const uint64_t probe = f & s_pm[lo][k];
         const uint64_t tgm = probe ? v.tg[at] : 0ull;
-        if (probe & tgm) atomicOr((unsigned long long*)&v.hit[g], (unsigned long long)(probe & tgm));
+        if (probe & tgm) atomicOr((unsigned long long*)&v.hit[(size_t)g * K + k], (unsigned long long)(probe & tgm));
         // expansion: the queries that reach the child first at this hop and may expand it
-        const uint64_t want = x.len ? (f & em) : 0ull;
+        const uint64_t want = x.len ? (f & s_em[lo][k]) : 0ull;
         if (want) {
           uint64_t nw = want & ~v.vis[at];
           if (nw) {
             nw &= ~(uint64_t)atomicOr((unsigned long long*)&v.vis[at], (unsigned long long)nw);
             if (nw) {
-              const uint64_t o2 = atomicOr((unsigned long long*)&v.fr[nx][at], (unsigned long long)nw);
-              app = o2 == 0;
+              atomicOr((unsigned long long*)&v.fr[nx][at], (unsigned long long)nw);
+              // one entry per (group, node, hop) whatever word set it first
+              app = atomicMax(&v.stamp[(size_t)g * n + child], (uint32_t)L + 2) < (uint32_t)L + 2;
               cb = x.begin;
               clen = x.len;
             }
@@ -289,33 +289,40 @@ __global__ __launch_bounds__(256) void k_ms_level(DevSnap s, MsView v, int L, in
         }
       }
     }
-    ms_append(v, nx, app, g, child, cb, clen);
+    ms_append<TE>(v, nx, app, g, child, cb, clen);
   }
 }
 
 // After level L: the level's frontier masks are cleared (the buffer is the level after next's).
+template <int K>
 __global__ __launch_bounds__(256) void k_ms_clear(MsView v, int cur) {
   const uint64_t n_e = v.ctl->packed[cur] >> MS_EDGE_BITS;
-  const uint64_t lim = n_e < v.cap ? n_e : v.cap;
-  for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < lim; k += (uint64_t)gridDim.x * blockDim.x)
-    v.fr[cur][(size_t)v.eg[cur][k] * v.n + v.en[cur][k]] = 0;
+  const uint64_t lim = (n_e < v.cap ? n_e : v.cap) * K;
+  for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < lim; w += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t q = w / K;
+    v.fr[cur][((size_t)v.eg[cur][q] * v.n + v.en[cur][q]) * K + w % K] = 0;
+  }
 }
 
+template <int K>
 __global__ void k_ms_finish(MsView v, const uint32_t* d_count, uint32_t base, uint8_t* out, uint32_t* err) {
+  constexpr uint32_t Q = 64u * K;
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= ms_round_slots(d_count, base, v.G * 64u) || v.ctl->overflow) return;
-  const uint32_t qidx = v.qi[i];
-  out[qidx] = ((v.hit[i >> 6] >> (i & 63)) & 1ull) ? KG_IS_MEMBER : KG_NOT_MEMBER;
+  if (i >= ms_round_slots(d_count, base, v.G * Q) || v.ctl->overflow) return;
+  const uint32_t qidx = v.qi[i], g = i / Q, b = i % Q;
+  out[qidx] = ((v.hit[(size_t)g * K + (b >> 6)] >> (b & 63)) & 1ull) ? KG_IS_MEMBER : KG_NOT_MEMBER;
   if (err) err[qidx] = KG_ERR_NONE;
 }
 
-size_t ms_group_bytes(uint32_t n) { return (size_t)n * 8 * 4 + 8 + 2 * MS_HOPS * 8 + 64 * 8; }
+size_t ms_group_bytes(uint32_t n, int K) {
+  return (size_t)n * (8 * 4 * K + 4) + (size_t)K * (8 + 2 * MS_HOPS * 8 + 64 * 8);
+}
 
-// Pool layout for G groups and level buffers of `cap` entries.
-int ms_layout(GridPool* P, uint32_t n, uint32_t G, uint64_t cap, MsView* v) {
-  const size_t gn = (size_t)G * n * 8;
-  const size_t need = 4 * gn + (size_t)G * (8 + 2 * MS_HOPS * 8 + 64 * 8) + 2 * (cap * (4 + 4 + 4 + 8) + MS_TILE_CAP * 4) +
-                      sizeof(MsCtl) + 8192;
+// Pool layout for G groups of K words and level buffers of `cap` entries.
+int ms_layout(GridPool* P, uint32_t n, int K, uint32_t G, uint64_t cap, MsView* v) {
+  const size_t gn = (size_t)G * n * K * 8;
+  const size_t need = 4 * gn + (size_t)G * n * 4 + (size_t)G * K * (8 + 2 * MS_HOPS * 8 + 64 * 8) +
+                      2 * (cap * (4 + 4 + 4 + 8) + MS_TILE_CAP * 4) + sizeof(MsCtl) + 8192;
   if (need > P->bytes) {
     P->release();
     HIPC(hipMalloc(&P->mem, need));
@@ -334,15 +341,18 @@ int ms_layout(GridPool* P, uint32_t n, uint32_t G, uint64_t cap, MsView* v) {
   v->tg = (uint64_t*)p;
   p += gn;
   v->hit = (uint64_t*)p;
-  p += (size_t)G * 8;
+  p += (size_t)G * K * 8;
   v->pm = (uint64_t*)p;
-  p += (size_t)G * MS_HOPS * 8;
+  p += (size_t)G * MS_HOPS * K * 8;
   v->em = (uint64_t*)p;
-  p += (size_t)G * MS_HOPS * 8;
+  p += (size_t)G * MS_HOPS * K * 8;
   v->qi = (uint32_t*)p;
-  p += (size_t)G * 64 * 4;
+  p += (size_t)G * 64 * K * 4;
   v->qd = (uint32_t*)p;
-  p += (size_t)G * 64 * 4;
+  p += (size_t)G * 64 * K * 4;
+  v->stamp = (uint32_t*)p;
+  p += (size_t)G * n * 4;
+  p = (char*)(((uintptr_t)p + 255) & ~uintptr_t(255));
   for (int b = 0; b < 2; b++) {
     v->ex[b] = (uint64_t*)p;
     p += cap * 8;
@@ -359,31 +369,29 @@ int ms_layout(GridPool* P, uint32_t n, uint32_t G, uint64_t cap, MsView* v) {
   return 0;
 }
 
-}  // namespace
-
-// Whether the MS-BFS path serves this snapshot's grid tier (kg_snapshot_tune "grid_ms"): the dense
-// masks of one group must fit an eighth of the pool budget, and the holder index must exist.
-bool ms_usable(const Snapshot* s, int global_max_depth) {
-  if (!s->grid_ms || !s->ds.hold || !s->ds.hslots || s->ds.n_nodes == 0 || global_max_depth > MS_HOPS) return false;
-  return ms_group_bytes(s->ds.n_nodes) * 8 <= s->grid_ms_bytes;
+// Words per mask for this snapshot: the configured width, halved until one group's masks fit an
+// eighth of the budget (0: none fits).
+int ms_words(const Snapshot* s) {
+  for (int K = s->grid_ms_words; K >= 1; K >>= 1)
+    if (ms_group_bytes(s->ds.n_nodes, K) * 8 <= s->grid_ms_bytes) return K;
+  return 0;
 }
 
-// Same protocol as grid_tier (kg_grid.hip): phase 1 enqueues the first round and returns 1, phase 2
-// resumes after the batch's synchronisation; a round that overflows a level buffer reruns with a
-// quarter of the groups.  Returns 2 when a single group overflows them: the caller runs the rest of
-// the list (from the first query not yet answered) through the per-query rounds.
-int ms_tier(Snapshot* s, Workspace* w, const RQuery* rq, const uint32_t* qlist, const uint32_t* d_count,
-            int global_max_depth, uint8_t* out, uint32_t* err, hipStream_t stream, GridStats* gs, int phase) {
+template <int K>
+int ms_rounds(Snapshot* s, Workspace* w, const RQuery* rq, const uint32_t* qlist, const uint32_t* d_count,
+              int global_max_depth, uint8_t* out, uint32_t* err, hipStream_t stream, GridStats* gs, int phase) {
+  constexpr uint32_t Q = 64u * K;
   char* pin = (char*)w->host_buf(65536);
   if (!pin) return set_error(-1, "pinned host buffer");
   uint32_t* hb = (uint32_t*)(pin + 32768);
   const uint32_t n = s->ds.n_nodes;
-  const uint32_t g_max = (uint32_t)std::max<size_t>(1, std::min<size_t>(1u << 14, s->grid_ms_bytes / ms_group_bytes(n)));
+  const uint32_t g_max =
+      (uint32_t)std::max<size_t>(1, std::min<size_t>((1u << 20) / Q, s->grid_ms_bytes / ms_group_bytes(n, K)));
   const uint64_t cap = s->grid_ms_cap ? s->grid_ms_cap : 16ull << 20;  // entries per level buffer
   GridPool* gp = &w->ms;
   MsView v{};
   uint32_t G = g_max;
-  if (int rc = ms_layout(gp, n, G, std::min<uint64_t>(cap, (uint64_t)G * n + 1024), &v)) return rc;
+  if (int rc = ms_layout(gp, n, K, G, std::min<uint64_t>(cap, (uint64_t)G * n + 1024), &v)) return rc;
   const int levels = std::max(0, global_max_depth - 1);  // level L expands hop L (D - 2 >= L)
   const uint32_t lgrid = (uint32_t)s->n_cu * s->grid_wgs;
   int64_t count = -1;
@@ -393,30 +401,31 @@ int ms_tier(Snapshot* s, Workspace* w, const RQuery* rq, const uint32_t* qlist, 
       if (phase == 1) w->grid_reran = false;
       if (phase == 2) w->grid_reran = true;
       v.G = G;
-      const size_t gn = (size_t)G * n * 8;
+      const size_t gn = (size_t)G * n * K * 8;
       // the round's masks start clear (frontier buffers are cleared level by level, but an
       // overflowed round may leave them dirty)
       HIPC(hipMemsetAsync(v.vis, 0, gn, stream));
       HIPC(hipMemsetAsync(v.fr[0], 0, gn, stream));
       HIPC(hipMemsetAsync(v.fr[1], 0, gn, stream));
       HIPC(hipMemsetAsync(v.tg, 0, gn, stream));
+      HIPC(hipMemsetAsync(v.stamp, 0, (size_t)G * n * 4, stream));
       HIPC(hipMemsetAsync(v.ctl, 0, sizeof(MsCtl), stream));
-      const uint32_t qblocks = (G * 64 + 255) / 256;
-      hipLaunchKernelGGL(k_ms_init, dim3(qblocks), dim3(256), 0, stream, rq, qlist, d_count, done, v);
+      const uint32_t qblocks = (G * Q + 255) / 256;
+      hipLaunchKernelGGL(k_ms_init<K>, dim3(qblocks), dim3(256), 0, stream, rq, qlist, d_count, done, v);
       HIPC(hipGetLastError());
-      hipLaunchKernelGGL(k_ms_masks, dim3((G * MS_HOPS + 255) / 256), dim3(256), 0, stream, v);
+      hipLaunchKernelGGL(k_ms_masks<K>, dim3((G * MS_HOPS * K + 255) / 256), dim3(256), 0, stream, v);
       HIPC(hipGetLastError());
-      hipLaunchKernelGGL(k_ms_holders, dim3((G * 64 + 3) / 4), dim3(256), 0, stream, s->ds, rq, v);
+      hipLaunchKernelGGL(k_ms_holders<K>, dim3((G * Q + 3) / 4), dim3(256), 0, stream, s->ds, rq, v);
       HIPC(hipGetLastError());
       for (int L = 0; L < levels; L++) {
         const int cur = L & 1;
-        hipLaunchKernelGGL(k_ms_level, dim3(lgrid), dim3(256), 0, stream, s->ds, v, L, cur);
+        hipLaunchKernelGGL(k_ms_level<K>, dim3(lgrid), dim3(256), 0, stream, s->ds, v, L, cur);
         HIPC(hipGetLastError());
-        hipLaunchKernelGGL(k_ms_clear, dim3((uint32_t)s->n_cu * 4), dim3(256), 0, stream, v, cur);
+        hipLaunchKernelGGL(k_ms_clear<K>, dim3((uint32_t)s->n_cu * 4), dim3(256), 0, stream, v, cur);
         HIPC(hipGetLastError());
         HIPC(hipMemsetAsync(&v.ctl->packed[cur], 0, 8, stream));
       }
-      hipLaunchKernelGGL(k_ms_finish, dim3(qblocks), dim3(256), 0, stream, v, d_count, done, out, err);
+      hipLaunchKernelGGL(k_ms_finish<K>, dim3(qblocks), dim3(256), 0, stream, v, d_count, done, out, err);
       HIPC(hipGetLastError());
       HIPC(hipMemcpyAsync(hb, v.ctl, sizeof(MsCtl), hipMemcpyDeviceToHost, stream));
       HIPC(hipMemcpyAsync(hb + sizeof(MsCtl) / 4, d_count, 4, hipMemcpyDeviceToHost, stream));
@@ -427,7 +436,7 @@ int ms_tier(Snapshot* s, Workspace* w, const RQuery* rq, const uint32_t* qlist, 
     MsCtl h{};
     memcpy(&h, hb, sizeof h);
     count = hb[sizeof(MsCtl) / 4];
-    const uint32_t cnt = count > done ? (uint32_t)std::min<int64_t>((int64_t)G * 64, count - done) : 0u;
+    const uint32_t cnt = count > done ? (uint32_t)std::min<int64_t>((int64_t)G * Q, count - done) : 0u;
     if (gs) {
       gs->rows += h.logged;
       gs->edges += h.edges;
@@ -437,7 +446,7 @@ int ms_tier(Snapshot* s, Workspace* w, const RQuery* rq, const uint32_t* qlist, 
         if (gs) gs->done -= done;
         return 2;
       }
-      G = std::max<uint32_t>(1, std::min(G, (cnt + 63) / 64) / 4);
+      G = std::max<uint32_t>(1, std::min(G, (cnt + Q - 1) / Q) / 4);
       continue;
     }
     if (gs) {
@@ -447,6 +456,31 @@ int ms_tier(Snapshot* s, Workspace* w, const RQuery* rq, const uint32_t* qlist, 
     done += cnt;
   }
   return 0;
+}
+
+}  // namespace
+
+// Whether the MS-BFS path serves this snapshot's grid tier (kg_snapshot_tune "grid_ms"): one group's
+// dense masks must fit an eighth of the pool budget, and the holder index must exist.
+bool ms_usable(const Snapshot* s, int global_max_depth) {
+  if (!s->grid_ms || !s->ds.hold || !s->ds.hslots || s->ds.n_nodes == 0 || global_max_depth > MS_HOPS) return false;
+  return ms_words(s) > 0;
+}
+
+// Same protocol as grid_tier (kg_grid.hip): phase 1 enqueues the first round and returns 1, phase 2
+// resumes after the batch's synchronisation; a round that overflows a level buffer reruns with a
+// quarter of the groups.  Returns 2 when a single group overflows them: the caller runs the rest of
+// the list (from the first query not yet answered) through the per-query rounds.
+int ms_tier(Snapshot* s, Workspace* w, const RQuery* rq, const uint32_t* qlist, const uint32_t* d_count,
+            int global_max_depth, uint8_t* out, uint32_t* err, hipStream_t stream, GridStats* gs, int phase) {
+  switch (ms_words(s)) {
+    case 16: return ms_rounds<16>(s, w, rq, qlist, d_count, global_max_depth, out, err, stream, gs, phase);
+    case 8: return ms_rounds<8>(s, w, rq, qlist, d_count, global_max_depth, out, err, stream, gs, phase);
+    case 4: return ms_rounds<4>(s, w, rq, qlist, d_count, global_max_depth, out, err, stream, gs, phase);
+    case 2: return ms_rounds<2>(s, w, rq, qlist, d_count, global_max_depth, out, err, stream, gs, phase);
+    case 1: return ms_rounds<1>(s, w, rq, qlist, d_count, global_max_depth, out, err, stream, gs, phase);
+    default: return set_error(-2, "MS-BFS masks do not fit");
+  }
 }
 
 }  // namespace kg

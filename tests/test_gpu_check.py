@@ -618,16 +618,19 @@ def test_bench_tune_set_vs_oracle(preset, n_tuples):
 
 
 @pytest.mark.parametrize("ms,bidir,grid_cap,seed", [(0, 1024, 0, 0), (0, 1024, 0, 1), (0, 0, 0, 0), (0, 1024, 700, 2),
-                                                     (0, 2, 0, 3), (0, 64, 0, 4), (1, 0, 0, 0), (1, 0, 0, 1),
-                                                     (1, 0, 40, 2), (1, 0, 300, 3), (1, 1024, 0, 5)])
+                                                     (0, 2, 0, 3), (0, 64, 0, 4), (8, 0, 0, 0), (1, 0, 0, 1),
+                                                     (1, 0, 40, 2), (2, 0, 300, 3), (8, 1024, 0, 5), (16, 0, 0, 6),
+                                                     (4, 0, 120, 7)])
 def test_grid_bidirectional_dense_vs_oracle(ms, bidir, grid_cap, seed):
     """The grid tier on dense graphs with cycles, hubs and subjects held only by rows nothing points
     at: a tiny stream-tier edge budget and the backward tier off send nearly every query there; every
     depth 2..9 is bit-exact with the oracle.  ms 0: the per-query rounds (kg_grid.hip), bidirectional
     or forward only, with a log small enough that rounds overflow and rerun (grid_cap); ms 1: the
-    multi-source bit-parallel BFS (kg_msbfs.hip, 64 queries per group, ~40 groups per batch), with
-    level buffers small enough that rounds overflow and rerun with fewer groups (grid_cap as
-    grid_ms_cap)."""
+    multi-source bit-parallel BFS (kg_msbfs.hip, 64 x ms queries per group), with
+    level buffers small enough that rounds overflow and rerun with fewer groups, or that one group
+    overflows them alone and the list falls back to the per-query rounds (grid_cap as grid_ms_cap);
+    ms = 64-bit words per node mask (64 queries each: 1 word = ~40 groups of the batch's grid
+    queries, 16 words = one group)."""
     rng = np.random.default_rng(900 + seed)
     n_obj, n_users = 120, 60
     tuples = []
@@ -646,7 +649,9 @@ def test_grid_bidirectional_dense_vs_oracle(ms, bidir, grid_cap, seed):
     snap.tune("stream_ecap", 3)
     snap.tune("back", 0)
     snap.tune("grid_bidir", bidir)
-    snap.tune("grid_ms", ms)
+    snap.tune("grid_ms", 1 if ms else 0)
+    if ms:
+        snap.tune("grid_ms_words", ms)
     snap.tune("grid_ms_cap" if ms else "grid_cap", grid_cap)
     it = reg.interner
     qs = []
