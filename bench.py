@@ -88,6 +88,8 @@ def parse(argv=None):
                          "(64 queries per group) when dense per-node masks fit (graphs up to ~4 M nodes)")
     ap.add_argument("--grid-ms-words", type=int, default=8,
                     help="kg_snapshot_tune grid_ms_words: 64-bit words per MS-BFS node mask (64 queries each)")
+    ap.add_argument("--grid-ms-tg-cap", type=int, default=256,
+                    help="kg_snapshot_tune grid_ms_tg_cap: holders above which MS-BFS probes a query's subject in dset")
     ap.add_argument("--grid-bidir", type=int, default=0,
                     help="kg_snapshot_tune grid_bidir: grid slots whose subject has <= this many holders "
                          "alternate forward and backward turns (0: forward only)")
@@ -172,6 +174,7 @@ def apply_tune(snap, a) -> None:
     snap.tune("grid_bidir", a.grid_bidir)
     snap.tune("grid_ms", a.grid_ms)
     snap.tune("grid_ms_words", a.grid_ms_words)
+    snap.tune("grid_ms_tg_cap", a.grid_ms_tg_cap)
     snap.tune("stream_wgs", a.stream_wgs)
     snap.tune("back_wgs", a.back_wgs)
     snap.tune("grid_reserve", 1)  # a server pays this once at start-up, not inside some request's batch

@@ -242,7 +242,9 @@ int kg_snapshot_materialized(const kg_snapshot* s, uint64_t* out3);
  * key "grid_ms" (0/1, default 1): the grid tier's queries run as a multi-source bit-parallel BFS,
  * 64 x "grid_ms_words" (1..16, default 8) queries per group sharing each level's walk, when one
  * group's dense per-node masks (32 B per word per node) fit an eighth of "grid_ms_bytes" (default
- * 2^30 per in-flight batch; the width halves until they do) -- graphs of up to ~4 M nodes.  key "grid_ms_cap": entries per MS-BFS level buffer (0 = 16 Mi; small values force the
+ * 2^30 per in-flight batch; the width halves until they do) -- graphs of up to ~4 M nodes.  key
+ * "grid_ms_tg_cap" (default 256): a query whose subject has more holders is probed in dset per
+ * newly reached node instead of marking its holders in the group's target masks.  key "grid_ms_cap": entries per MS-BFS level buffer (0 = 16 Mi; small values force the
  * overflow reruns in tests).
  * key "grid_bidir" (0..2^31-1, default 0): grid-tier slots whose subject has at most this many
  * holders alternate forward and backward turns (0: forward only).  key "expand_tail" (0/1, default

@@ -505,6 +505,11 @@ static int tune_one(Snapshot* s, const char* key, int64_t value) {
     s->grid_ms_words = (int)value;
     return 0;
   }
+  if (strcmp(key, "grid_ms_tg_cap") == 0) {
+    if (value < 0 || value > 0x7FFFFFFF) return set_error(-2, "grid_ms_tg_cap must be in [0, 2^31)");
+    s->grid_ms_tg_cap = (uint32_t)value;
+    return 0;
+  }
   if (strcmp(key, "grid_ms_cap") == 0) {
     if (value < 0 || value > (1ll << 28)) return set_error(-2, "grid_ms_cap must be in [0, 2^28]");
     s->grid_ms_cap = (uint64_t)value;

@@ -16,7 +16,10 @@
 //   VIS[g][node]  queries of group g that reached the node (and may expand it)
 //   FR[2][g][node] frontier masks of the current / next level
 //   TG[g][node]   queries of group g whose subject the node holds (its check row has the exact tuple:
-//                 the holder index hold[], i.e. checkDirect's answer for every query at once)
+//                 the holder index hold[], i.e. checkDirect's answer for every query at once) -- for
+//                 subjects with at most tg_cap holders; a popular subject's queries are probed in
+//                 dset per newly reached node instead (marking 10^4..10^5 holders per query cost
+//                 more than the whole walk)
 //   HIT[g]        queries of group g answered IsMember; their bits stop propagating at the next tile
 //   PM / EM[g][h] queries whose rest depth lets a node at hop h be probed (D-1 >= h) / expanded (D-2 >= h)
 // Levels are edge-balanced over the whole GPU like the grid tier's: entries (group, node, row) of a
@@ -59,6 +62,9 @@ struct MsView {
   uint64_t* tg;    // [G][n][K]
   uint32_t* stamp;  // [G][n]: 1 + the last hop the node was appended at (one entry per hop)
   uint64_t* hit;   // [G][K]
+  uint64_t* many;  // [G][K]: queries whose subject has more than tg_cap holders (probed, no TG bits)
+  uint32_t* qs;    // [G][64K] tagged subject
+  uint32_t tg_cap;
   uint64_t* pm;    // [G][MS_HOPS][K]
   uint64_t* em;    // [G][MS_HOPS][K]
   uint32_t* qi;    // [G][64K] query index (NONE: empty bit)
@@ -136,11 +142,12 @@ __global__ __launch_bounds__(256) void k_ms_init(const RQuery* __restrict__ rq, 
   bool app = false;
   uint32_t node = 0, rb = 0, len = 0;
   if (inside) {
-    uint32_t qidx = NONE, d = 0;
+    uint32_t qidx = NONE, d = 0, subj = NONE;
     if (i < nq) {
       qidx = qlist[base + i];
       const RQuery q = rq[qidx];
       d = (uint32_t)max(q.depth, 0);
+      subj = q.subj;
       node = q.node;
       rb = q.beg;
       len = q.len;
@@ -152,6 +159,7 @@ __global__ __launch_bounds__(256) void k_ms_init(const RQuery* __restrict__ rq, 
     }
     v.qi[i] = qidx;
     v.qd[i] = d;
+    v.qs[i] = subj;
   }
   ms_append<256u / K>(v, 0, app, g, node, rb, len);
 }
@@ -171,7 +179,10 @@ __global__ void k_ms_masks(MsView v) {
   }
   v.pm[i] = pm;
   v.em[i] = em;
-  if (h == 0) v.hit[(size_t)g * K + k] = 0;
+  if (h == 0) {
+    v.hit[(size_t)g * K + k] = 0;
+    v.many[(size_t)g * K + k] = 0;
+  }
 }
 
 // One wave per query: its subject's holders get the query's bit in TG (checkDirect for every node).
@@ -182,9 +193,13 @@ __global__ __launch_bounds__(256) void k_ms_holders(DevSnap s, const RQuery* __r
   if (i >= v.G * Q) return;
   const uint32_t qidx = v.qi[i];
   if (qidx == NONE) return;
-  const uint2 hr = holders_find(s, rq[qidx].subj);
+  const uint2 hr = holders_find(s, v.qs[i]);
   const uint32_t g = i / Q, b = i % Q;
   const uint64_t bit = 1ull << (b & 63);
+  if (hr.y > v.tg_cap) {
+    if (lane_id() == 0) atomicOr((unsigned long long*)&v.many[(size_t)g * K + (b >> 6)], (unsigned long long)bit);
+    return;
+  }
   for (uint32_t k = lane_id(); k < hr.y; k += 64)
     atomicOr((unsigned long long*)&v.tg[((size_t)g * v.n + s.hold[hr.x + k]) * K + (b >> 6)], (unsigned long long)bit);
 }
@@ -264,27 +279,32 @@ __global__ __launch_bounds__(256) void k_ms_level(DevSnap s, MsView v, int L, in
       }
       const uint64_t f = s_f[lo][k];
       g = s_g[lo];
-      if (f) {
+      // the queries of the word that reach the child first at hop L+1 and may still probe there (a
+      // later arrival has less rest depth: its probe and expansion are subsets of the first one's)
+      const uint64_t want = f & s_pm[lo][k];
+      if (want) {
         const AdjX x = s.adjx[s_rb[lo] + (e - s_beg[lo])];
         child = x.node;
         const size_t at = ((size_t)g * n + child) * K + k;
-        // checkDirect at hop L+1 for every query of the word that may still probe there
-        const uint64_t probe = f & s_pm[lo][k];
-        const uint64_t tgm = probe ? v.tg[at] : 0ull;
-        if (probe & tgm) atomicOr((unsigned long long*)&v.hit[(size_t)g * K + k], (unsigned long long)(probe & tgm));
-        // expansion: the queries that reach the child first at this hop and may expand it
-        const uint64_t want = x.len ? (f & s_em[lo][k]) : 0ull;
-        if (want) {
-          uint64_t nw = want & ~v.vis[at];
-          if (nw) {
-            nw &= ~(uint64_t)atomicOr((unsigned long long*)&v.vis[at], (unsigned long long)nw);
-            if (nw) {
-              atomicOr((unsigned long long*)&v.fr[nx][at], (unsigned long long)nw);
-              // one entry per (group, node, hop) whatever word set it first
-              app = atomicMax(&v.stamp[(size_t)g * n + child], (uint32_t)L + 2) < (uint32_t)L + 2;
-              cb = x.begin;
-              clen = x.len;
-            }
+        uint64_t nw = want & ~v.vis[at];
+        if (nw) nw &= ~(uint64_t)atomicOr((unsigned long long*)&v.vis[at], (unsigned long long)nw);
+        if (nw) {
+          // checkDirect: TG bits for subjects with few holders, dset probes for popular ones
+          const uint64_t many = v.many[(size_t)g * K + k];
+          uint64_t hits = (nw & ~many) ? (nw & ~many & v.tg[at]) : 0ull;
+          for (uint64_t m = nw & many; m; m &= m - 1) {
+            const uint32_t subj = v.qs[(size_t)g * 64 * K + k * 64 + __builtin_ctzll(m)];
+            if (sig_maybe(x.sig, subj_sig(subj)) && dset_probe(s, child, subj)) hits |= m & (~m + 1);
+          }
+          if (hits) atomicOr((unsigned long long*)&v.hit[(size_t)g * K + k], (unsigned long long)hits);
+          // expansion: those that may expand it
+          const uint64_t ex = x.len ? (nw & s_em[lo][k]) : 0ull;
+          if (ex) {
+            atomicOr((unsigned long long*)&v.fr[nx][at], (unsigned long long)ex);
+            // one entry per (group, node, hop) whatever word set it first
+            app = atomicMax(&v.stamp[(size_t)g * n + child], (uint32_t)L + 2) < (uint32_t)L + 2;
+            cb = x.begin;
+            clen = x.len;
           }
         }
       }
@@ -315,13 +335,13 @@ __global__ void k_ms_finish(MsView v, const uint32_t* d_count, uint32_t base, ui
 }
 
 size_t ms_group_bytes(uint32_t n, int K) {
-  return (size_t)n * (8 * 4 * K + 4) + (size_t)K * (8 + 2 * MS_HOPS * 8 + 64 * 8);
+  return (size_t)n * (8 * 4 * K + 4) + (size_t)K * (16 + 2 * MS_HOPS * 8 + 64 * 12);
 }
 
 // Pool layout for G groups of K words and level buffers of `cap` entries.
 int ms_layout(GridPool* P, uint32_t n, int K, uint32_t G, uint64_t cap, MsView* v) {
   const size_t gn = (size_t)G * n * K * 8;
-  const size_t need = 4 * gn + (size_t)G * n * 4 + (size_t)G * K * (8 + 2 * MS_HOPS * 8 + 64 * 8) +
+  const size_t need = 4 * gn + (size_t)G * n * 4 + (size_t)G * K * (16 + 2 * MS_HOPS * 8 + 64 * 12) +
                       2 * (cap * (4 + 4 + 4 + 8) + MS_TILE_CAP * 4) + sizeof(MsCtl) + 8192;
   if (need > P->bytes) {
     P->release();
@@ -342,6 +362,8 @@ int ms_layout(GridPool* P, uint32_t n, int K, uint32_t G, uint64_t cap, MsView* 
   p += gn;
   v->hit = (uint64_t*)p;
   p += (size_t)G * K * 8;
+  v->many = (uint64_t*)p;
+  p += (size_t)G * K * 8;
   v->pm = (uint64_t*)p;
   p += (size_t)G * MS_HOPS * K * 8;
   v->em = (uint64_t*)p;
@@ -349,6 +371,8 @@ int ms_layout(GridPool* P, uint32_t n, int K, uint32_t G, uint64_t cap, MsView* 
   v->qi = (uint32_t*)p;
   p += (size_t)G * 64 * K * 4;
   v->qd = (uint32_t*)p;
+  p += (size_t)G * 64 * K * 4;
+  v->qs = (uint32_t*)p;
   p += (size_t)G * 64 * K * 4;
   v->stamp = (uint32_t*)p;
   p += (size_t)G * n * 4;
@@ -391,6 +415,7 @@ int ms_rounds(Snapshot* s, Workspace* w, const RQuery* rq, const uint32_t* qlist
   GridPool* gp = &w->ms;
   MsView v{};
   uint32_t G = g_max;
+  v.tg_cap = s->grid_ms_tg_cap;
   if (int rc = ms_layout(gp, n, K, G, std::min<uint64_t>(cap, (uint64_t)G * n + 1024), &v)) return rc;
   const int levels = std::max(0, global_max_depth - 1);  // level L expands hop L (D - 2 >= L)
   const uint32_t lgrid = (uint32_t)s->n_cu * s->grid_wgs;

@@ -243,7 +243,8 @@ struct Snapshot {
   int expand_tail = 1;  // kg_snapshot_tune("expand_tail"): expand passes 2/3 walk with LDS-cached frames (0: round 2)
   int grid_ms = 1;  // kg_snapshot_tune("grid_ms"): grid-tier queries as MS-BFS when the dense masks fit (0: off)
   size_t grid_ms_bytes = 1ull << 30;  // kg_snapshot_tune("grid_ms_bytes"): MS-BFS mask budget per workspace
-  int grid_ms_words = 8;  // kg_snapshot_tune("grid_ms_words"): 64-bit words per MS-BFS mask (64 queries each)
+  int grid_ms_words = 8;
+  uint32_t grid_ms_tg_cap = 256;  // kg_snapshot_tune("grid_ms_tg_cap"): holders above which MS-BFS probes dset instead  // kg_snapshot_tune("grid_ms_words"): 64-bit words per MS-BFS mask (64 queries each)
   uint64_t grid_ms_cap = 0;  // kg_snapshot_tune("grid_ms_cap"): MS-BFS entries per level buffer (0 = 16 Mi; tests)
   int grid_bidir = 0;  // kg_snapshot_tune("grid_bidir"): grid slots whose subject has <= this many holders go bidirectional (0: none)
                        // alternate forward and backward turns (0: forward only)

@@ -617,11 +617,11 @@ def test_bench_tune_set_vs_oracle(preset, n_tuples):
         assert 0.05 < (out == 1).mean() < 0.95
 
 
-@pytest.mark.parametrize("ms,bidir,grid_cap,seed", [(0, 1024, 0, 0), (0, 1024, 0, 1), (0, 0, 0, 0), (0, 1024, 700, 2),
-                                                     (0, 2, 0, 3), (0, 64, 0, 4), (8, 0, 0, 0), (1, 0, 0, 1),
-                                                     (1, 0, 40, 2), (2, 0, 300, 3), (8, 1024, 0, 5), (16, 0, 0, 6),
-                                                     (4, 0, 120, 7)])
-def test_grid_bidirectional_dense_vs_oracle(ms, bidir, grid_cap, seed):
+@pytest.mark.parametrize("ms,bidir,grid_cap,seed,tg_cap", [
+    (0, 1024, 0, 0, 256), (0, 1024, 0, 1, 256), (0, 0, 0, 0, 256), (0, 1024, 700, 2, 256), (0, 2, 0, 3, 256),
+    (0, 64, 0, 4, 256), (8, 0, 0, 0, 256), (1, 0, 0, 1, 256), (1, 0, 40, 2, 256), (2, 0, 300, 3, 256),
+    (8, 1024, 0, 5, 256), (16, 0, 0, 6, 256), (4, 0, 120, 7, 256), (8, 0, 0, 8, 0), (1, 0, 0, 9, 3)])
+def test_grid_bidirectional_dense_vs_oracle(ms, bidir, grid_cap, seed, tg_cap):
     """The grid tier on dense graphs with cycles, hubs and subjects held only by rows nothing points
     at: a tiny stream-tier edge budget and the backward tier off send nearly every query there; every
     depth 2..9 is bit-exact with the oracle.  ms 0: the per-query rounds (kg_grid.hip), bidirectional
@@ -630,7 +630,8 @@ def test_grid_bidirectional_dense_vs_oracle(ms, bidir, grid_cap, seed):
     level buffers small enough that rounds overflow and rerun with fewer groups, or that one group
     overflows them alone and the list falls back to the per-query rounds (grid_cap as grid_ms_cap);
     ms = 64-bit words per node mask (64 queries each: 1 word = ~40 groups of the batch's grid
-    queries, 16 words = one group)."""
+    queries, 16 words = one group); tg_cap = holders above which a query's subject is probed in
+    dset per newly reached node instead of marked in the target masks (0: every query probed)."""
     rng = np.random.default_rng(900 + seed)
     n_obj, n_users = 120, 60
     tuples = []
@@ -652,6 +653,7 @@ def test_grid_bidirectional_dense_vs_oracle(ms, bidir, grid_cap, seed):
     snap.tune("grid_ms", 1 if ms else 0)
     if ms:
         snap.tune("grid_ms_words", ms)
+        snap.tune("grid_ms_tg_cap", tg_cap)
     snap.tune("grid_ms_cap" if ms else "grid_cap", grid_cap)
     it = reg.interner
     qs = []
