@@ -88,6 +88,8 @@ def parse(argv=None):
                          "(64 queries per group) when dense per-node masks fit (graphs up to ~4 M nodes)")
     ap.add_argument("--grid-ms-words", type=int, default=8,
                     help="kg_snapshot_tune grid_ms_words: 64-bit words per MS-BFS node mask (64 queries each)")
+    ap.add_argument("--grid-ms-bytes", type=float, default=0,
+                    help="kg_snapshot_tune grid_ms_bytes: MS-BFS mask budget per workspace in bytes (0: library default)")
     ap.add_argument("--grid-ms-tg-cap", type=int, default=256,
                     help="kg_snapshot_tune grid_ms_tg_cap: holders above which MS-BFS probes a query's subject in dset")
     ap.add_argument("--grid-bidir", type=int, default=0,
@@ -175,6 +177,8 @@ def apply_tune(snap, a) -> None:
     snap.tune("grid_ms", a.grid_ms)
     snap.tune("grid_ms_words", a.grid_ms_words)
     snap.tune("grid_ms_tg_cap", a.grid_ms_tg_cap)
+    if a.grid_ms_bytes:
+        snap.tune("grid_ms_bytes", int(a.grid_ms_bytes))
     snap.tune("stream_wgs", a.stream_wgs)
     snap.tune("back_wgs", a.back_wgs)
     snap.tune("grid_reserve", 1)  # a server pays this once at start-up, not inside some request's batch
