@@ -322,8 +322,11 @@ void kg_batcher_destroy(kg_batcher* b);
  * kg_shard_finish.  Replaces the single-GPU kg_check_batch for such snapshots.  Rewrites: union
  * rewrites are materialised into plain union nodes as in the single-GPU engine and boolean ones
  * over plain / union leaves are split into parts (kg_shard_result_slots); a query that reaches any
- * other rewrite (or an undeclared relation) ends as KG_ERROR / KG_ERR_NOT_IMPLEMENTED -- there is no
- * cross-shard interpreter.  keto_amd/sharded.py is the driver. */
+ * other rewrite (or an undeclared relation) ends here as KG_ERROR / KG_ERR_NOT_IMPLEMENTED, and the
+ * driver's general phase answers it: the rows of every object within gdepth + 1 subject-set hops of
+ * its root are gathered to its home rank (kg_snapshot_rows at each owner, all-to-all) and a
+ * single-GPU snapshot of them (kg_snapshot_create + kg_check_batch: the rewrite interpreter) gives
+ * the reference's answer and error.  keto_amd/sharded.py is the driver. */
 typedef struct {
   uint32_t q;     /* home rank << 26 | index in the home rank's batch                         */
   uint32_t node;  /* node to check (checkIsAllowed(node, depth)), KG_FREC_HIT or KG_FREC_ERR  */

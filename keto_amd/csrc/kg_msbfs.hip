@@ -44,6 +44,8 @@ constexpr int MS_EDGE_BITS = 36;
 constexpr uint64_t MS_EDGE_MASK = (1ull << MS_EDGE_BITS) - 1;
 constexpr uint64_t MS_ENTRY_MAX = (1ull << (64 - MS_EDGE_BITS)) - 1;
 constexpr int MS_HOPS = 32;  // depth masks per group (global max depth <= 32 here)
+// edges per tile of k_ms_level: K lanes per edge, two edges per lane group
+constexpr uint32_t ms_tile_edges(int K) { return 2u * 256u / (uint32_t)K; }
 
 struct MsCtl {
   unsigned long long packed[2];  // per level buffer: entries << 36 | edges
@@ -161,7 +163,7 @@ __global__ __launch_bounds__(256) void k_ms_init(const RQuery* __restrict__ rq, 
     v.qd[i] = d;
     v.qs[i] = subj;
   }
-  ms_append<256u / K>(v, 0, app, g, node, rb, len);
+  ms_append<ms_tile_edges(K)>(v, 0, app, g, node, rb, len);
 }
 
 // One thread per (group, hop, word): the depth masks (and, at hop 0, a clear hit word).
@@ -214,14 +216,51 @@ __device__ __forceinline__ uint64_t ms_entry_of(const uint64_t* ex, uint64_t lo,
 }
 
 // Level L: the frontier (hop L) in buffer cur is expanded into hop L+1, appended to buffer cur ^ 1.
-// K lanes per edge (lane k owns mask word k), TE = 256 / K edges per tile.  A tile's entries are
-// staged in LDS with their frontier masks (already filtered by depth and answered queries at tile
-// start), so a word with nothing to propagate costs no memory access, and an edge whose K words are
-// all empty is not even loaded.
+// K lanes per edge (lane k owns mask word k), TE = 2 * 256 / K edges per tile (two per lane group:
+// both edges' loads are issued before either is used).  A tile's entries are staged in LDS with
+// their frontier masks (already filtered by depth and answered queries at tile start), so a word
+// with nothing to propagate costs no memory access, and an edge whose K words are all empty is not
+// even loaded.
+//
+// Per edge the updates are blind ORs on the masks loaded once (no returning atomic on the chain): the
+// bits new to the child are `want & ~vis` as loaded.  Two edges of one level that reach the same
+// child can both see a bit as new; both then OR the same bits into vis / the next frontier / hit
+// (idempotent) and probe the same subjects -- duplicated work, the same answer, since a bit absent
+// from vis when this level started can only have been set by this level, i.e. at the same hop.  The
+// one returning atomic is the node's hop stamp (one level entry per (group, node, hop)), skipped when
+// the loaded stamp already says so.
+template <int K>
+__device__ __forceinline__ void ms_edge(const DevSnap& s, const MsView& v, uint32_t n, int L, int nx, uint64_t want,
+                                        uint64_t many, uint64_t em, uint32_t g, uint32_t k, const AdjX& x, bool& app,
+                                        uint32_t& child, uint32_t& cb, uint32_t& clen, uint64_t vis0, uint64_t tg0,
+                                        uint32_t st0) {
+  const uint64_t nw = want & ~vis0;
+  if (!nw) return;
+  const size_t at = ((size_t)g * n + x.node) * K + k;
+  atomicOr((unsigned long long*)&v.vis[at], (unsigned long long)nw);
+  // checkDirect: TG bits for subjects with few holders, dset probes for popular ones
+  uint64_t hits = nw & ~many & tg0;
+  for (uint64_t m = nw & many; m; m &= m - 1) {
+    const uint32_t subj = v.qs[(size_t)g * 64 * K + k * 64 + __builtin_ctzll(m)];
+    if (sig_maybe(x.sig, subj_sig(subj)) && dset_probe(s, x.node, subj)) hits |= m & (~m + 1);
+  }
+  if (hits) atomicOr((unsigned long long*)&v.hit[(size_t)g * K + k], (unsigned long long)hits);
+  // expansion: those that may expand it
+  const uint64_t ex = x.len ? (nw & em) : 0ull;
+  if (ex) {
+    atomicOr((unsigned long long*)&v.fr[nx][at], (unsigned long long)ex);
+    const uint32_t want_st = (uint32_t)L + 2;
+    app = st0 < want_st && atomicMax(&v.stamp[(size_t)g * n + x.node], want_st) < want_st;
+    child = x.node;
+    cb = x.begin;
+    clen = x.len;
+  }
+}
+
 template <int K>
 __global__ __launch_bounds__(256) void k_ms_level(DevSnap s, MsView v, int L, int cur) {
-  constexpr uint32_t TE = 256u / K;
-  __shared__ uint64_t s_beg[TE + 2], s_f[TE + 2][K], s_pm[TE + 2][K], s_em[TE + 2][K];
+  constexpr uint32_t TE = ms_tile_edges(K);
+  __shared__ uint64_t s_beg[TE + 2], s_f[TE + 2][K], s_pm[TE + 2][K], s_em[TE + 2][K], s_many[TE + 2][K];
   __shared__ uint32_t s_g[TE + 2], s_rb[TE + 2];
   __shared__ uint64_t s_j0, s_cnt;
   if (v.ctl->overflow) return;
@@ -265,51 +304,52 @@ __global__ __launch_bounds__(256) void k_ms_level(DevSnap s, MsView v, int L, in
                    ~v.hit[(size_t)g * K + kk];
       s_pm[i][kk] = v.pm[((size_t)g * MS_HOPS + h1) * K + kk];
       s_em[i][kk] = v.em[((size_t)g * MS_HOPS + h1) * K + kk];
+      s_many[i][kk] = v.many[(size_t)g * K + kk];
     }
     __syncthreads();
-    const uint64_t e = t0 + my_e;
-    bool app = false;
-    uint32_t g = 0, child = 0, cb = 0, clen = 0;
-    if (e < t1) {
-      uint32_t lo = 0, hi = (uint32_t)cnt;
-      while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (s_beg[mid] <= e) lo = mid;
-        else hi = mid;
-      }
-      const uint64_t f = s_f[lo][k];
-      g = s_g[lo];
-      // the queries of the word that reach the child first at hop L+1 and may still probe there (a
-      // later arrival has less rest depth: its probe and expansion are subsets of the first one's)
-      const uint64_t want = f & s_pm[lo][k];
-      if (want) {
-        const AdjX x = s.adjx[s_rb[lo] + (e - s_beg[lo])];
-        child = x.node;
-        const size_t at = ((size_t)g * n + child) * K + k;
-        uint64_t nw = want & ~v.vis[at];
-        if (nw) nw &= ~(uint64_t)atomicOr((unsigned long long*)&v.vis[at], (unsigned long long)nw);
-        if (nw) {
-          // checkDirect: TG bits for subjects with few holders, dset probes for popular ones
-          const uint64_t many = v.many[(size_t)g * K + k];
-          uint64_t hits = (nw & ~many) ? (nw & ~many & v.tg[at]) : 0ull;
-          for (uint64_t m = nw & many; m; m &= m - 1) {
-            const uint32_t subj = v.qs[(size_t)g * 64 * K + k * 64 + __builtin_ctzll(m)];
-            if (sig_maybe(x.sig, subj_sig(subj)) && dset_probe(s, child, subj)) hits |= m & (~m + 1);
-          }
-          if (hits) atomicOr((unsigned long long*)&v.hit[(size_t)g * K + k], (unsigned long long)hits);
-          // expansion: those that may expand it
-          const uint64_t ex = x.len ? (nw & s_em[lo][k]) : 0ull;
-          if (ex) {
-            atomicOr((unsigned long long*)&v.fr[nx][at], (unsigned long long)ex);
-            // one entry per (group, node, hop) whatever word set it first
-            app = atomicMax(&v.stamp[(size_t)g * n + child], (uint32_t)L + 2) < (uint32_t)L + 2;
-            cb = x.begin;
-            clen = x.len;
-          }
+    // two edges per lane group: e and e + TE / 2
+    uint64_t want[2] = {0ull, 0ull};
+    uint32_t ent[2] = {0u, 0u};
+    AdjX x[2];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const uint64_t e = t0 + my_e + (uint64_t)h * (TE / 2);
+      if (e < t1) {
+        uint32_t lo = 0, hi = (uint32_t)cnt;
+        while (hi - lo > 1) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (s_beg[mid] <= e) lo = mid;
+          else hi = mid;
         }
+        ent[h] = lo;
+        // the queries of the word that reach the child first at hop L+1 and may still probe there (a
+        // later arrival has less rest depth: its probe and expansion are subsets of the first one's)
+        want[h] = s_f[lo][k] & s_pm[lo][k];
       }
+      // unconditional load (adjx[0] exists), predicated afterwards: both edges' gathers in flight at once
+      x[h] = s.adjx[want[h] ? s_rb[ent[h]] + (uint32_t)(e - s_beg[ent[h]]) : 0u];
     }
-    ms_append<TE>(v, nx, app, g, child, cb, clen);
+    // the child's masks and hop stamp, both edges' loads issued before either is used
+    uint64_t vis0[2], tg0[2];
+    uint32_t st0[2];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const uint32_t g = s_g[ent[h]], c = want[h] ? x[h].node : 0u;
+      const size_t at = ((size_t)g * n + c) * K + k;
+      vis0[h] = v.vis[at];
+      tg0[h] = v.tg[at];
+      st0[h] = v.stamp[(size_t)g * n + c];
+    }
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      bool app = false;
+      uint32_t child = 0, cb = 0, clen = 0;
+      const uint32_t g = s_g[ent[h]];
+      if (want[h])
+        ms_edge<K>(s, v, n, L, nx, want[h], s_many[ent[h]][k], s_em[ent[h]][k], g, k, x[h], app, child, cb, clen,
+                   vis0[h], tg0[h], st0[h]);
+      ms_append<TE>(v, nx, app, g, child, cb, clen);
+    }
   }
 }
 

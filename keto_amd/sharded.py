@@ -21,8 +21,11 @@ with the SURVEY.md 8a semantics).  Union rewrites (or / computedUserset / tupleT
 materialised into plain union nodes on every rank alike; a query whose relation is a boolean formula
 over plain or union relations is split into parts (its own rows and one per leaf relation) that
 travel as queries of their own in extra result slots, and kg_shard_finish evaluates the formula.  A
-query that reaches any other rewrite or an undeclared relation ends as KG_ERROR /
-KG_ERR_NOT_IMPLEMENTED (there is no cross-shard interpreter).  The local steps are
+query that reaches any other rewrite or an undeclared relation (an impure union, a formula recursive
+through tuple-to-subject-set such as the reference parser's full example's `view`) ends the level
+protocol as KG_ERR_NOT_IMPLEMENTED and goes to the general phase: the rows of every object within
+gdepth + 1 subject-set hops of its root are gathered to its home rank and the single-GPU engine
+(rewrite interpreter included) answers it on a snapshot of them.  The local steps are
 `ShardOps` objects: `HipShardOps` runs them on the GPU through the C ABI; the multi-rank CPU
 tests substitute a test-only restatement to exercise this exchange protocol under gloo.
 """
@@ -151,6 +154,52 @@ class HipShardOps:
         _lib.check(self.L.kg_shard_finish(self.snapshot.handle, n, res.data_ptr(), err.data_ptr(), self._s()),
                    "kg_shard_finish")
 
+    # ---- general rewrites (queries the level protocol ends as KG_ERR_NOT_IMPLEMENTED)
+    def region_rows(self, objs: np.ndarray):
+        """GetRelationTuples (kg_snapshot_rows) of every relation of each (ns, obj) row of `objs` that this
+        rank holds, rows of each relation in shard order.  Returns (offs[m + 1], tuples (t, 6) uint32):
+        object j's rows at tuples[offs[j]:offs[j + 1]]."""
+        nrel = self.snapshot.interner.n_relations
+        m = int(objs.shape[0])
+        if m == 0:
+            return np.zeros(1, np.int64), np.zeros((0, 6), np.uint32)
+        keys = np.empty((m * nrel, 3), np.uint32)
+        keys[:, 0] = np.repeat(objs[:, 0], nrel)
+        keys[:, 1] = np.repeat(objs[:, 1], nrel)
+        keys[:, 2] = np.tile(np.arange(nrel, dtype=np.uint32), m)
+        off, tup = self.snapshot.rows(keys)
+        return off[::nrel].copy(), tup
+
+    def general_check(self, region: np.ndarray, q7: np.ndarray, gdepth: int):
+        """The single-GPU engine (tiers + rewrite interpreter) on a snapshot of `region` -- every row the
+        queries can read -- with this snapshot's namespace program.  Returns (res u8, err u32) host arrays."""
+        from .engine import Config, Engine, Snapshot
+        snap = Snapshot(region, self.snapshot.interner, self.snapshot.program, self.snapshot.device)
+        try:
+            return Engine(snap, Config(gdepth)).batch_check_ids(q7)
+        finally:
+            snap.close()
+
+
+KG_SUBJECT_ID = 0xFFFFFFFF
+ERR_NOT_IMPLEMENTED = 2
+
+
+def shard_owners(ns: np.ndarray, obj: np.ndarray, nranks: int) -> np.ndarray:
+    """kg_shard_owner (kg_internal.h shard_owner) over arrays: hash(ns, obj) mod nranks."""
+    ns = np.asarray(ns, np.uint64)
+    obj = np.asarray(obj, np.uint64)
+    if nranks <= 1:
+        return np.zeros(ns.shape, np.int64)
+    with np.errstate(over="ignore"):
+        x = (ns << np.uint64(32)) | obj
+        x ^= x >> np.uint64(30)
+        x *= np.uint64(0xbf58476d1ce4e5b9)
+        x ^= x >> np.uint64(27)
+        x *= np.uint64(0x94d049bb133111eb)
+        x ^= x >> np.uint64(31)
+    return ((x >> np.uint64(20)) % np.uint64(nranks)).astype(np.int64)
+
 
 class ShardOverflow(Exception):
     """Some rank dropped records: 1 = a bucket, 2 = its visited table.  Every rank reruns."""
@@ -165,7 +214,7 @@ class ShardedChecker:
     for a single rank; device = the torch device the records live on."""
 
     def __init__(self, ops, rank: int = 0, world: int = 1, dist=None, device="cuda", cap: int = 1 << 20,
-                 protocol: str = "auto", group=None):
+                 protocol: str = "auto", group=None, general: bool = True):
         """protocol (world > 1): "fixed" = every level exchanges fixed-size buckets (records per destination
         <= bucket) and the batch runs gdepth + 1 levels with no host round trip inside it (counts, flags and
         termination stay on the device; one readback at the end); "dynamic" = one metadata exchange and
@@ -186,6 +235,12 @@ class ShardedChecker:
         self._held_ready = world == 1 or not hasattr(ops, "held_export")
         self.trace = bool(int(os.environ.get("KG_SHARD_TRACE", "0")))  # per-level record counts (diagnostics)
         self.level_records = None
+        # general rewrites: queries the level protocol ends as NOT_IMPLEMENTED are answered by the
+        # single-GPU engine on a snapshot of the rows they can read, gathered to their home rank
+        self.general = bool(general) and hasattr(ops, "general_check")
+        self._gen_any = False
+        self.general_queries = 0
+        self.general_rows = 0
 
     def _install_held(self):
         """Once per snapshot: the OR of every rank's holder bitmap, so kg_shard_seed's no-holder test
@@ -366,6 +421,96 @@ class ShardedChecker:
                 self.levels += 1
         return cur
 
+    # ---- general rewrites across shards
+    def _open_general(self, res, err, n):
+        """Device flag: some query of this rank ended KG_ERROR / NOT_IMPLEMENTED (after kg_shard_finish)."""
+        import torch
+        return ((res[:n] == 2) & (err[:n] == ERR_NOT_IMPLEMENTED)).any().to(torch.int64)
+
+    def _xdev(self):
+        return "cpu" if self.dist is None or self.dist.get_backend() == "gloo" else self.device
+
+    def _any_rank(self, flag: bool) -> bool:
+        import torch
+        if self.dist is None or self.world == 1:
+            return bool(flag)
+        t = torch.tensor([1 if flag else 0], dtype=torch.int64, device=self._xdev())
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX, group=self.group)
+        self.host_syncs += 1
+        return bool(int(t.item()))
+
+    def _a2a_rows(self, rows: np.ndarray, dest: np.ndarray) -> np.ndarray:
+        """All-to-all of int64 host rows: row i goes to rank dest[i]; returns the rows this rank received."""
+        import torch
+        if self.dist is None or self.world == 1:
+            return rows
+        N = self.world
+        order = np.argsort(dest, kind="stable")
+        rows = np.ascontiguousarray(rows[order])
+        send = np.bincount(dest, minlength=N).astype(np.int64)
+        dev = self._xdev()
+        rc = torch.empty(N, dtype=torch.int64, device=dev)
+        self.dist.all_to_all_single(rc, torch.from_numpy(send).to(dev), group=self.group)
+        recv_n = [int(x) for x in rc.cpu().numpy()]
+        w = rows.shape[1]
+        out = torch.empty((sum(recv_n), w), dtype=torch.int64, device=dev)
+        self.dist.all_to_all_single(out, torch.from_numpy(rows).to(dev), recv_n, [int(x) for x in send],
+                                    group=self.group)
+        self.host_syncs += 1
+        return out.cpu().numpy()
+
+    def _gather_region(self, q: np.ndarray, gdepth: int) -> np.ndarray:
+        """Every row of every object within gdepth + 1 subject-set hops of this rank's queries' root objects,
+        gathered at this rank (collective: every rank takes part, with or without queries).  Hop h+1 =
+        the objects of the subject sets in hop h's rows: the objects an expand row or a tuple-to-subject-set
+        row leads to (rewrites.go:205-260); computed subject sets stay on the object, and the owner ships
+        all of an object's relations (every relation of an object lives on one rank).  Owners ship an
+        object once per home; rows keep their shard order per (ns, obj, rel)."""
+        N = self.world
+        req = np.unique(np.stack([np.full(q.shape[0], self.rank, np.int64), q[:, 0].astype(np.int64),
+                                  q[:, 1].astype(np.int64)], 1), axis=0) if q.shape[0] else np.zeros((0, 3), np.int64)
+        seen = set()
+        got_rows = []
+        for hop in range(gdepth + 2):
+            recv = self._a2a_rows(req, shard_owners(req[:, 1], req[:, 2], N))
+            keep = []
+            for i, (h, ns, obj) in enumerate(recv.tolist()):
+                if (h, ns, obj) not in seen:
+                    seen.add((h, ns, obj))
+                    keep.append(i)
+            new = recv[keep] if keep else np.zeros((0, 3), np.int64)
+            off, tup = self.ops.region_rows(new[:, 1:3].astype(np.uint32))
+            homes = np.repeat(new[:, 0], np.diff(off).astype(np.int64))
+            payload = np.concatenate([homes[:, None], tup.astype(np.int64)], 1)
+            got_rows.append(self._a2a_rows(payload, homes))
+            sets = tup[:, 3] != KG_SUBJECT_ID
+            if hop <= gdepth and sets.any():
+                req = np.unique(np.stack([homes[sets], tup[sets, 3].astype(np.int64), tup[sets, 4].astype(np.int64)],
+                                         1), axis=0)
+            else:
+                req = np.zeros((0, 3), np.int64)
+            if not self._any_rank(req.shape[0] > 0):
+                break
+        allr = np.concatenate(got_rows) if got_rows else np.zeros((0, 7), np.int64)
+        return np.ascontiguousarray(allr[:, 1:7].astype(np.uint32))
+
+    def _general_phase(self, dq, res, err, gdepth: int):
+        """Queries that reached a rewrite the level protocol cannot evaluate across ranks (an impure union,
+        a recursive formula through tuple-to-subject-set, an undeclared relation): their rows are gathered
+        to their home rank and the single-GPU engine answers them there (rewrite interpreter included),
+        so the sharded mode returns the reference's answers and errors for every program."""
+        import torch
+        n = int(dq.shape[0])
+        sel = ((res[:n] == 2) & (err[:n] == ERR_NOT_IMPLEMENTED)).nonzero().flatten()
+        q = dq[sel].cpu().numpy().view(np.uint32).reshape(-1, 7) if sel.numel() else np.zeros((0, 7), np.uint32)
+        region = self._gather_region(q, gdepth)
+        self.general_queries += int(q.shape[0])
+        self.general_rows += int(region.shape[0])
+        if q.shape[0]:
+            r, e = self.ops.general_check(region, q, gdepth)
+            res[sel] = torch.from_numpy(np.asarray(r, np.uint8)).to(res.device)
+            err[sel] = torch.from_numpy(np.asarray(e, np.uint32).view(np.int32)).to(err.device)
+
     # ---- one batch
     def check(self, dq, gdepth: int) -> Tuple["object", "object"]:
         """dq: (n, 7) int32 kg_query rows of THIS rank's queries (device tensor).  Returns (res u8, err i32)
@@ -374,12 +519,19 @@ class ShardedChecker:
         ts = getattr(self.ops, "torch_stream", None)
         if ts is not None:  # the local steps and every torch op of the batch run on the ops' stream
             ts.wait_stream(torch.cuda.current_stream())
+        gd = gdepth if gdepth >= 1 else 5
         while True:
             try:
+                self._gen_any = False
                 if ts is None:
-                    return self._check(dq, gdepth)
+                    res, err = self._check(dq, gdepth)
+                    if self._gen_any:
+                        self._general_phase(dq, res, err, gd)
+                    return res, err
                 with torch.cuda.stream(ts):
                     res, err = self._check(dq, gdepth)
+                    if self._gen_any:
+                        self._general_phase(dq, res, err, gd)
                 torch.cuda.current_stream().wait_stream(ts)
                 return res, err
             except ShardOverflow as e:  # every rank saw the same flags: all rerun with more room
@@ -432,8 +584,14 @@ class ShardedChecker:
                 self.final_levels = gdepth
                 cur = self._device_levels(bufs, counts, 0, res, err, slots, gdepth, words, 0, None, final=True)
                 parts += [counts[0][1] | counts[1][1], counts[cur][0]]
+            if self.general:  # results final before the readback, so it also says whether any query is open
+                self.ops.finish(n, res, err)
+                parts.append(self._open_general(res, err, n).to(parts[0].dtype))
             h = torch.stack(parts).cpu().numpy()  # the batch's one host round trip
             self.host_syncs += 1
+            if self.general:
+                self._gen_any = bool(h[-1])
+                h = h[:-1]
             fl = 0
             for k in range(0, len(h), 2):
                 fl |= int(h[k])
@@ -441,7 +599,8 @@ class ShardedChecker:
                     raise _lib.KetoGPUError("sharded batch: records left after %d levels" % gdepth)
             if fl & 3:
                 raise ShardOverflow(fl & 3)
-            self.ops.finish(n, res, err)
+            if not self.general:
+                self.ops.finish(n, res, err)
             return res[:n], err[:n]
         fixed = (self.dist is not None and hasattr(self.ops, "level_seg")
                  and (self.protocol == "fixed" or (self.protocol == "auto" and not backward)))
@@ -461,6 +620,8 @@ class ShardedChecker:
                     final = True
                     continue
                 self.ops.finish(n, res, err)
+                if self.general:
+                    self._gen_any = self._any_rank(bool(self._open_general(res, err, n).item()))
                 return res[:n], err[:n]
             self.records_sent += sum(send)
             recv = self._exchange(bufs[cur], send, recv_splits)
@@ -538,13 +699,18 @@ class ShardedChecker:
         c = counts[cur]
         acc[0] |= c[N].to(torch.int64) | (c[:N].to(torch.int64) > B).any().to(torch.int64)
         left = c[:N].to(torch.int64).sum()
-        # over ranks: each flag bit (bucket / visited-table overflow), the largest bucket, records left
-        tot = torch.stack([acc[0] & 1, (acc[0] >> 1) & 1, acc[1], left]).to(xdev)
+        if self.general:  # results final before the all-reduce, which then also carries "a query is open"
+            self.ops.finish(n, res, err)
+        gen = self._open_general(res, err, n) if self.general else torch.zeros((), dtype=torch.int64,
+                                                                                   device=self.device)
+        # over ranks: each flag bit (bucket / visited-table overflow), the largest bucket, records left, open
+        tot = torch.stack([acc[0] & 1, (acc[0] >> 1) & 1, acc[1], left, gen]).to(xdev)
         self.dist.all_reduce(tot, op=self.dist.ReduceOp.MAX, group=self.group)
         h = torch.cat([tot, acc[2:3].to(xdev)]).cpu().numpy()  # the batch's one host round trip
         self.host_syncs += 1
         flags = int(h[0]) | (int(h[1]) << 1)
-        self.records_sent = int(h[4])
+        self._gen_any = bool(h[4])
+        self.records_sent = int(h[5])
         big = int(h[2])
         if flags & 3:
             if flags & 1:
@@ -555,5 +721,6 @@ class ShardedChecker:
             raise _lib.KetoGPUError("sharded batch: records left after %d levels" % (gdepth + 1))
         # next batch: buckets 25 % above the largest one this batch needed (shrinking slowly)
         self.bucket = max(1024, min(B, int(big * 1.25) + 1024)) if big * 2 < B else B
-        self.ops.finish(n, res, err)
+        if not self.general:
+            self.ops.finish(n, res, err)
         return res[:n], err[:n]

@@ -44,7 +44,7 @@ class CpuShardOps:
         return self.budget > 0
 
     def __init__(self, tuples6: np.ndarray, wildcard_rel: int, rank: int, nranks: int, impure=(), budget=0,
-                 back_budget=1 << 14):
+                 back_budget=1 << 14, program=None):
         """impure: (ns, rel) pairs whose relation has a rewrite or is undeclared (relflag != 0).
         budget: forward set edges per query on this rank before the query escalates (0 = off; only
         without impure relations, like kg_snapshot_tune "shard_budget")."""
@@ -54,6 +54,14 @@ class CpuShardOps:
         self.final = False
         self.impure = set((int(a), int(b)) for a, b in impure)
         t = np.asarray(tuples6, np.int64).reshape(-1, 6)
+        self.wildcard_rel, self.program = wildcard_rel, program
+        # rows of this rank's objects in tuple (shard) order, per (ns, obj): GetRelationTuples of the
+        # general-rewrite region gather (HipShardOps.region_rows, kg_snapshot_rows)
+        self.obj_rows = {}
+        for k, row in enumerate(t):
+            if shard_owner(int(row[0]), int(row[1]), nranks) == rank:
+                self.obj_rows.setdefault((int(row[0]), int(row[1])), []).append(k)
+        self.t6 = np.asarray(tuples6, np.uint32).reshape(-1, 6)
         self.node = {}
         self.nrel = {}
 
@@ -273,3 +281,24 @@ class CpuShardOps:
     def finish(self, n, res, err):
         err[:n] = err[:n] & ~(ESC_BIT | ESC2_BIT)
         res[:n][err[:n] != 0] = 2
+
+    # ---- general rewrites: the region gather's local steps (HipShardOps.region_rows / general_check)
+    def region_rows(self, objs):
+        """Rows of every relation of each held (ns, obj), grouped by relation in shard order."""
+        offs, parts = [0], []
+        for ns, obj in np.asarray(objs, np.int64).reshape(-1, 2).tolist():
+            idx = self.obj_rows.get((ns, obj), [])
+            rows = self.t6[idx] if idx else np.zeros((0, 6), np.uint32)
+            rows = rows[np.argsort(rows[:, 2], kind="stable")]  # relation by relation, each in shard order
+            parts.append(rows)
+            offs.append(offs[-1] + rows.shape[0])
+        tup = np.concatenate(parts) if parts else np.zeros((0, 6), np.uint32)
+        return np.asarray(offs, np.int64), tup
+
+    def general_check(self, region, q7, gdepth):
+        """The oracle (test-only, in the role of the single-GPU engine) on the gathered region's rows."""
+        from oracle.oracle import POLICY_CANONICAL, Oracle
+        q7 = np.asarray(q7, np.uint32).reshape(-1, 7)
+        o = Oracle(np.asarray(region, np.uint32).reshape(-1, 6), self.wildcard_rel, self.program)
+        res, err, _ = o.check_batch(q7[:, :6], q7[:, 6].view(np.int32), gdepth, POLICY_CANONICAL)
+        return np.asarray(res, np.uint8), np.asarray(err, np.uint32)

@@ -212,9 +212,77 @@ def _cpu_sharded(t6, wildcard, q, gmax, impure):
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from keto_amd.sharded import ShardedChecker
     from shard_ref import CpuShardOps
-    chk = ShardedChecker(CpuShardOps(t6, wildcard, 0, 1, impure), 0, 1, None, device="cpu", cap=1 << 12)
+    chk = ShardedChecker(CpuShardOps(t6, wildcard, 0, 1, impure), 0, 1, None, device="cpu", cap=1 << 12,
+                         general=False)
     res, err = chk.check(torch.from_numpy(q.view(np.int32).copy()), gmax)
     return res.numpy().copy(), err.numpy().copy()
+
+
+def _cpu_general_worker(rank, world, port, seed, outq, protocol):
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import torch.distributed as dist
+    from keto_amd.sharded import ShardedChecker
+    from shard_ref import CpuShardOps
+    dist_ = None
+    if world > 1:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dist_ = dist
+    if seed == "opl":  # every query to the general phase: the gather must cover TTU targets and recursion
+        it, t6, q, _, prog = _opl_full_example_graph(7, n_q=600)
+        impure = [(a, b) for a in range(it.n_namespaces) for b in range(it.n_relations)]
+    else:
+        it, t6, q, prog, impure = _impure_graph(seed)
+    ops = CpuShardOps(t6, it.wildcard_rel, rank, world, impure, program=prog)
+    mine = np.array_split(np.arange(len(q)), world)[rank]
+    chk = ShardedChecker(ops, rank, world, dist_, device="cpu", cap=1 << 12, protocol=protocol)
+    out = {}
+    for gmax in (2, 5):
+        res, err = chk.check(torch.from_numpy(q[mine].view(np.int32).copy()), gmax)
+        out[gmax] = (mine, res.numpy().copy(), err.numpy().copy())
+    outq.put((rank, out, chk.general_queries, chk.general_rows))
+    if dist_:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,protocol,seed", [(1, "auto", 5), (2, "dynamic", 5), (2, "fixed", 5), (3, "fixed", 5),
+                                                (2, "fixed", "opl"), (3, "dynamic", "opl")])
+def test_sharded_general_rewrites_gloo(world, protocol, seed):
+    """Queries that reach a rewrite the level protocol cannot evaluate across ranks (here a computed
+    rewrite and undeclared relations) are not left as NOT_IMPLEMENTED: every rank gathers the rows of
+    the objects its open queries can reach (keto_amd.sharded._gather_region: all-to-all of object
+    requests to their owners, rows back to the home rank, gdepth + 1 subject-set hops) and evaluates
+    them on that region.  Answers AND error codes equal the oracle's on the whole graph, with the
+    oracle program (rewrites, RELATION_NOT_FOUND for undeclared relations)."""
+    from oracle.oracle import POLICY_CANONICAL, Oracle
+    ctx = mp.get_context("spawn")
+    outq = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_cpu_general_worker, args=(r, world, port, seed, outq, protocol)) for r in range(world)]
+    for p in ps:
+        p.start()
+    got = [outq.get(timeout=240) for _ in range(world)]
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    if seed == "opl":
+        it, t6, q, _, prog = _opl_full_example_graph(7, n_q=600)
+    else:
+        it, t6, q, prog, impure = _impure_graph(seed)
+    o = Oracle(t6, it.wildcard_rel, prog)
+    assert sum(g[2] for g in got) > 0 and sum(g[3] for g in got) > 0  # the general phase ran, rows moved
+    for gmax in (2, 5):
+        exp, oerr, _ = o.check_batch(q[:, :6], q[:, 6].view(np.int32), gmax, POLICY_CANONICAL)
+        res = np.zeros(len(q), np.uint8)
+        err = np.zeros(len(q), np.int64)
+        for _, out, _, _ in got:
+            mine, r, e = out[gmax]
+            res[mine], err[mine] = r, e
+        bad = np.nonzero((res != exp) | (err != oerr))[0]
+        assert bad.size == 0, [(q[i].tolist(), int(res[i]), int(exp[i]), int(err[i]), int(oerr[i])) for i in bad[:8]]
+        assert (exp == 1).any() and (exp == 0).any()
 
 
 def test_sharded_impure_reference_semantics():
@@ -249,7 +317,7 @@ def test_sharded_hip_impure_matches_reference(mat, monkeypatch):
     monkeypatch.setenv("KG_MATERIALIZE", str(mat))
     it, t6, q, prog, impure = _impure_graph(5)
     snap = Snapshot(t6, it, prog, 0, shard=(0, 1))
-    chk = ShardedChecker(HipShardOps(snap), 0, 1, None, device="cuda", cap=256)
+    chk = ShardedChecker(HipShardOps(snap), 0, 1, None, device="cuda", cap=256, general=False)
     o = Oracle(t6, it.wildcard_rel, prog)
     r2 = (q[:, 0] == it.ns_id("n1")) & (q[:, 2] == it.rel_id("r2"))
     assert r2.any()
@@ -267,6 +335,111 @@ def test_sharded_hip_impure_matches_reference(mat, monkeypatch):
         bad = np.nonzero(ok & ((res != exp) | (oerr != 0)))[0]
         assert bad.size == 0, [(q[i].tolist(), int(res[i]), int(exp[i]), int(oerr[i])) for i in bad[:8]]
         assert (err <= eerr).all() and (err[r2 & (eerr != 0)] == 0).any()  # the union now answers
+
+
+def _opl_full_example_graph(seed, n_q=2000):
+    """The reference parser's full example (tests/golden/opl_full_example.json: view = (parents.traverse(
+    viewers) & parents.traverse(view)) | viewers | owners -- a formula recursive through tuple-to-subject-
+    set --, not = !owners, rename = siblings.traverse(edit)) on a random graph over its namespaces."""
+    import json
+    sys.path.insert(0, ROOT)
+    from keto_amd.engine import queries_array
+    from keto_amd.ketoapi import RelationTuple
+    from keto_amd.mapper import Interner
+    from keto_amd.namespace import compile_program, namespace_from_json
+    golden = json.load(open(os.path.join(ROOT, "tests", "golden", "opl_full_example.json")))
+    nss = [namespace_from_json({"name": n, "relations": rels}) for n, rels in sorted(golden.items())]
+    it = Interner()
+    prog_ref = compile_program(nss, it, lower_ttu=False)
+    prog = compile_program(nss, it)
+    rng = np.random.default_rng(seed)
+    files, folders, groups, users = ([f"f{i}" for i in range(60)], [f"d{i}" for i in range(20)],
+                                     [f"g{i}" for i in range(15)], [f"u{i}" for i in range(30)])
+    kinds = [lambda: f"File:{rng.choice(files)}#parents@(File:{rng.choice(files)}#...)",
+             lambda: f"File:{rng.choice(files)}#parents@(Folder:{rng.choice(folders)}#...)",
+             lambda: f"File:{rng.choice(files)}#viewers@{rng.choice(users)}",
+             lambda: f"File:{rng.choice(files)}#viewers@(Group:{rng.choice(groups)}#members)",
+             lambda: f"File:{rng.choice(files)}#owners@{rng.choice(users)}",
+             lambda: f"File:{rng.choice(files)}#siblings@(File:{rng.choice(files)}#...)",
+             lambda: f"Folder:{rng.choice(folders)}#viewers@(Group:{rng.choice(groups)}#members)",
+             lambda: f"Group:{rng.choice(groups)}#members@{rng.choice(users)}",
+             lambda: f"Group:{rng.choice(groups)}#members@(Group:{rng.choice(groups)}#members)"]
+    tuples = [RelationTuple.from_string(kinds[rng.integers(len(kinds))]()) for _ in range(700)]
+    qs = []
+    for _ in range(n_q):
+        rel = rng.choice(["view", "edit", "not", "rename", "viewers", "owners", "parents"])
+        ns, obj = ("Folder", rng.choice(folders)) if rng.random() < 0.2 else ("File", rng.choice(files))
+        subj = rng.choice(users + ["nobody"]) if rng.random() < 0.9 else f"(Group:{rng.choice(groups)}#members)"
+        qs.append(RelationTuple.from_string(f"{ns}:{obj}#{rel}@{subj}"))
+    q6 = np.asarray([it.tuple_ids(t) for t in qs], np.uint32)
+    return it, it.tuples_array(tuples), queries_array(q6, rng.integers(-1, 8, len(qs))), prog, prog_ref
+
+
+def _general_gpu_worker(rank, world, port, outq, kind):
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+    from keto_amd.engine import Snapshot
+    from keto_amd.sharded import HipShardOps, ShardedChecker
+    dist_ = None
+    if world > 1:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)  # two ranks on one GPU: host-staged
+        dist_ = dist
+    torch.cuda.set_device(0)
+    if kind == "opl":
+        it, t6, q, prog, _ = _opl_full_example_graph(7)
+    else:
+        it, t6, q, prog, _ = _impure_graph(5)
+    snap = Snapshot(t6, it, prog, 0, shard=(rank, world))
+    mine = np.array_split(np.arange(len(q)), world)[rank]
+    chk = ShardedChecker(HipShardOps(snap), rank, world, dist_, device="cuda", cap=256)
+    out = {}
+    for gmax in (2, 5, 8):
+        res, err = chk.check(torch.from_numpy(q[mine].view(np.int32).copy()).cuda(), gmax)
+        out[gmax] = (mine, res.cpu().numpy(), err.cpu().numpy())
+    outq.put((rank, out, chk.general_queries))
+    if dist_:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,world", [("impure", 1), ("opl", 1), ("opl", 2)])
+def test_sharded_general_rewrites_vs_oracle(kind, world):
+    """Every rewrite in the hash-sharded mode: the reference parser's full example (a `view` formula
+    recursive through tuple-to-subject-set, `not`, nested traverse) and a program with a computed
+    rewrite and undeclared relations.  Queries the level protocol ends as NOT_IMPLEMENTED go to the
+    general phase (their rows gathered to the home rank, the single-GPU engine's interpreter on them):
+    answers and error codes bit-exact with the oracle evaluating the program as written."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from oracle.oracle import POLICY_CANONICAL, Oracle
+    ctx = mp.get_context("spawn")
+    outq = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_general_gpu_worker, args=(r, world, port, outq, kind)) for r in range(world)]
+    for p in ps:
+        p.start()
+    got = [outq.get(timeout=150) for _ in range(world)]
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    if kind == "opl":
+        it, t6, q, _, prog_ref = _opl_full_example_graph(7)
+    else:
+        it, t6, q, prog_ref, _ = _impure_graph(5)
+    o = Oracle(t6, it.wildcard_rel, prog_ref)
+    assert sum(g[2] for g in got) > 0
+    for gmax in (2, 5, 8):
+        exp, oerr, _ = o.check_batch(q[:, :6], q[:, 6].view(np.int32), gmax, POLICY_CANONICAL)
+        res = np.zeros(len(q), np.uint8)
+        err = np.zeros(len(q), np.int64)
+        for _, out, _ in got:
+            mine, r, e = out[gmax]
+            res[mine], err[mine] = r, e
+        bad = np.nonzero((res != exp) | (err != oerr))[0]
+        assert bad.size == 0, [(q[i].tolist(), int(res[i]), int(exp[i]), int(err[i]), int(oerr[i])) for i in bad[:8]]
+        assert (exp == 1).any() and (exp == 0).any()
 
 
 # ------------------------------------------------------------------ config C4 generator, sharded
