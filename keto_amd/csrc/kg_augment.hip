@@ -180,7 +180,8 @@ __device__ __forceinline__ bool aug_succ(const DevSnap& s, const DevSnap& base, 
 
 // ---- 3. purity: seeds, then "impure if a successor is impure" to a fixpoint
 __global__ void k_aug_seed(DevSnap s, DevSnap base, AugTables A, uint32_t n1, const uint32_t* cand_of,
-                           const uint32_t* c_plan, const uint32_t* c_obj, uint8_t* imp, int sharded) {
+                           const uint32_t* c_plan, const uint32_t* c_obj, uint8_t* imp, uint32_t rank,
+                           uint32_t nranks) {
   const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
   if (v >= n1) return;
   const uint32_t k = cand_of[v];
@@ -188,11 +189,13 @@ __global__ void k_aug_seed(DevSnap s, DevSnap base, AugTables A, uint32_t n1, co
     imp[v] = relflag(s, s.nd_ns[v], s.nd_rel[v]) != 0 ? 1 : 0;
     return;
   }
-  if (sharded) {  // rows are this rank's only: every union node is plain (see augment_rewrites)
+  const AugPlan& P = A.plans[c_plan[k]];
+  if (nranks > 1 && shard_owner(P.ns, c_obj[k], nranks) != rank) {
+    // hash-sharded mode: the object's rows (its TTU tuple rows among them) live on its owner, which
+    // decides; records reach a node only at its owner, so no other rank reads this flag for a check
     imp[v] = 0;
     return;
   }
-  const AugPlan& P = A.plans[c_plan[k]];
   imp[v] = aug_succ(s, base, A, P, c_obj[k], [](uint32_t) {}) ? 0 : 1;
 }
 
@@ -493,10 +496,13 @@ int Snapshot::augment_rewrites() {
   if (talloc((void**)&imp, (size_t)n1 + 16)) return -1;
   const uint32_t g1 = (n1 + 255) / 256;
   hipLaunchKernelGGL(k_aug_seed, dim3(g1), dim3(256), 0, stream, x, b, A, n1, cand_of, c_plan, c_obj, imp,
-                     shard_n > 1 ? 1 : 0);
+                     shard_rank, shard_n);
   HIPC(hipGetLastError());
-  // hash-sharded mode: purity needs every rank's rows, so there is no closure -- union nodes are
-  // plain, and a record that reaches a rewrite / undeclared node ends as an error (kg_shard.hip)
+  // hash-sharded mode: the closure needs every rank's rows, so only the seeds are marked -- by the
+  // owner of each union node, from its own TTU rows (a target relation that is undeclared or an
+  // unmaterialised rewrite, e.g. a formula reached through tuple-to-subject-set); a record reaches a
+  // node at its owner, so the impure node (or one it leads to) ends the query as NOT_IMPLEMENTED and
+  // the driver's general phase answers it (keto_amd/sharded.py)
   for (uint64_t it = 0; shard_n == 1 && it <= n1; it++) {  // every round that changes something marks a node
     uint32_t h = 0;
     HIPC(hipMemsetAsync(d_cnt + 2, 0, 4, stream));
