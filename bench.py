@@ -70,6 +70,9 @@ def parse(argv=None):
     ap.add_argument("--shard-back-budget", type=int, default=1 << 14,
                     help="kg_snapshot_tune shard_back_budget (reverse edges per query and rank before the final "
                          "forward phase takes it)")
+    ap.add_argument("--shard-heavy", type=int, default=-1,
+                    help="kg_snapshot_tune shard_heavy: set rows longer than this are expanded grid-wide (k_shard_heavy; "
+                         "0: every expansion; -1: the library default)")
     ap.add_argument("--shard-vis-mode", type=int, default=0,
                     help="kg_snapshot_tune shard_vis_mode (sharded (query, node) dedup: 0 exact CAS table, 1 lossy cache)")
     ap.add_argument("--device-sync", type=int, default=1,
@@ -440,6 +443,8 @@ def bench_sharded(a):
     snap.tune("shard_budget", a.shard_budget)
     snap.tune("shard_back_budget", a.shard_back_budget)
     snap.tune("shard_vis_mode", a.shard_vis_mode)
+    if a.shard_heavy >= 0:
+        snap.tune("shard_heavy", a.shard_heavy)
     B = a.batch
     P = max(1, a.inflight)
     n_distinct = max(P, 2)
@@ -517,7 +522,7 @@ def bench_sharded(a):
            "final_levels_per_batch": chk.final_levels, "shard_budget": a.shard_budget,
            "host_syncs_per_batch": (sum(c.host_syncs for c in chks) - sum(syncs0)) / max(1, a.steps),
            "bucket": chk.bucket, "shard_back_budget": a.shard_back_budget, "shard_vis_mode": a.shard_vis_mode,
-           "records_exchanged_per_batch": recs / a.steps,
+           "shard_heavy": a.shard_heavy, "records_exchanged_per_batch": recs / a.steps,
            **({"level_records": chk.level_records} if chk.level_records else {}),
            "snapshot_build_s": t_build}
     if rank == 0:

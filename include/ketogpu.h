@@ -375,7 +375,9 @@ int kg_shard_level_seg(kg_snapshot* s, const kg_frec* d_in, uint32_t n_seg, size
  * each buffer holds cap records, its record count in counts[0] on the device), with the done bitmap
  * of kg_shard_done (with_escalated as there) rebuilt before every level after the first.  *end
  * receives the buffer the last level wrote.  Replaces the driver's per-level loop when no exchange
- * happens between levels (keto_amd/sharded.py at world 1). */
+ * happens between levels (keto_amd/sharded.py at world 1).  n_slots 0: no done bitmap (no query's
+ * records are dropped once it is a member -- what a graph that can end a check in an error needs,
+ * kg_shard_bad_nodes). */
 int kg_shard_levels(kg_snapshot* s, int32_t levels, kg_frec* d_buf0, kg_frec* d_buf1, size_t cap, uint32_t* d_counts0,
                     uint32_t* d_counts1, int32_t start, uint8_t* d_res, uint32_t* d_err, size_t n_slots,
                     int32_t with_escalated, int32_t* end, void* stream);
@@ -419,6 +421,13 @@ int kg_shard_finish(kg_snapshot* s, size_t n, uint8_t* d_res, uint32_t* d_err, v
  * boolean rewrites into parts: the parts' answers sit behind the n requested ones and
  * kg_shard_finish combines them into d_res[0, n) / d_err[0, n)). */
 size_t kg_shard_result_slots(const kg_snapshot* s, size_t n);
+/* Nodes this rank owns that a record can reach and the level protocol cannot evaluate (a relation
+ * with a rewrite that is not materialised, or undeclared): when no rank has any, no check can end in
+ * an error below its root, and the driver may drop a member query's records (the done bitmap).
+ * Otherwise it must not: the reference's order can make an error in an earlier branch win over a
+ * member found at a shallower level in a later one (internal/check/checkgroup's first-decisive
+ * rule); the walk then goes on, the error reaches the query's home and the general phase decides. */
+int kg_shard_bad_nodes(const kg_snapshot* s, uint64_t* count);
 
 /* ---- expand ----------------------------------------------------------------------------- */
 /* Roots are split over the replicas (chunks of >= 1024 roots, one host thread each). */

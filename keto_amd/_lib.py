@@ -82,7 +82,7 @@ EXPORTS = ["kg_snapshot_create", "kg_snapshot_create_on", "kg_snapshot_synthetic
            "kg_tree_free", "kg_last_error", "kg_version", "kg_shard_owner", "kg_snapshot_create_shard",
            "kg_snapshot_synthetic_shard", "kg_shard_seed", "kg_shard_level", "kg_shard_level_seg", "kg_shard_finish",
            "kg_shard_done", "kg_shard_levels", "kg_shard_back_list", "kg_shard_back_seed", "kg_shard_back_level", "kg_shard_refwd_seed",
-           "kg_shard_held_words", "kg_shard_held", "kg_shard_result_slots", "kg_batcher_create", "kg_batcher_check", "kg_batcher_stats", "kg_batcher_reset_stats", "kg_batcher_destroy"]
+           "kg_shard_held_words", "kg_shard_held", "kg_shard_result_slots", "kg_shard_bad_nodes", "kg_batcher_create", "kg_batcher_check", "kg_batcher_stats", "kg_batcher_reset_stats", "kg_batcher_destroy"]
 
 
 class kg_batcher_stats_t(C.Structure):
@@ -156,6 +156,7 @@ def load(path: str = LIB_PATH):
     L.kg_shard_refwd_seed.argtypes = [vp, sz, vp, vp, vp, sz, vp, vp]
     L.kg_shard_held_words.argtypes = [vp, vp]
     L.kg_shard_held.argtypes = [vp, vp, sz, C.c_int, vp]
+    L.kg_shard_bad_nodes.argtypes = [vp, vp]
     L.kg_shard_result_slots.argtypes = [vp, sz]
     L.kg_shard_result_slots.restype = sz
     L.kg_shard_finish.argtypes = [vp, sz, vp, vp, vp]

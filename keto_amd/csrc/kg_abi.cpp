@@ -359,6 +359,15 @@ int kg_shard_held_words(const kg_snapshot* sp, size_t* words) {
   return 0;
 }
 
+int kg_shard_bad_nodes(const kg_snapshot* sp, uint64_t* count) {
+  KG_GUARD_BEGIN
+  if (!sp || !count) return set_error(-2, "NULL argument");
+  Snapshot* s = const_cast<Snapshot*>(reinterpret_cast<const Snapshot*>(sp));
+  std::lock_guard<std::mutex> lk(s->mu);
+  return kg::shard_bad_nodes(s, count);
+  KG_GUARD_END
+}
+
 size_t kg_shard_result_slots(const kg_snapshot* sp, size_t n) {
   return sp ? kg::shard_result_slots(reinterpret_cast<const Snapshot*>(sp), n) : n;
 }
@@ -421,6 +430,11 @@ static int tune_one(Snapshot* s, const char* key, int64_t value) {
   if (strcmp(key, "shard_budget") == 0) {
     if (value < 0 || value > 0xFFFFFFFFll) return set_error(-2, "shard_budget must be in [0, 2^32)");
     s->shard_budget = (uint32_t)value;
+    return 0;
+  }
+  if (strcmp(key, "shard_heavy") == 0) {
+    if (value < 0 || value > 0xFFFFFFFFll) return set_error(-2, "shard_heavy must be in [0, 2^32)");
+    s->shard_heavy = (uint32_t)value;
     return 0;
   }
   if (strcmp(key, "shard_vis_mode") == 0) {

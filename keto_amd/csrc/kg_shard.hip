@@ -72,12 +72,72 @@ constexpr int SV_PROBES = 64;
 constexpr uint32_t ESC_BIT = 0x40000000u, ESC2_BIT = 0x20000000u;
 constexpr int QCNT_LOG2 = 22;  // per-rank edge counters, hashed by query (a collision only escalates early)
 // A received record whose set row is longer than this is expanded by the whole grid (k_shard_heavy).
-constexpr uint32_t SHARD_HEAVY = 4096, SHARD_HEAVY_CAP = 1u << 16;
+constexpr uint32_t SHARD_HEAVY = 4096, SHARD_HEAVY_CAP = 1u << 20;
+constexpr uint32_t HEAVY_TILE = 256;              // edges per k_shard_heavy tile
+constexpr uint64_t HEAVY_TF_CAP = 1ull << 22;     // tiles with a first-row entry (beyond: binary search)
+constexpr int HEAVY_EDGE_BITS = 40;               // packed counter: rows << 40 | edges
 struct HeavyRow {
   kg_frec r;  // depth without flag bits
   uint64_t rb;
+  uint64_t e0;  // first edge of the row in the level's heavy-edge space
   uint32_t len, pad;
 };
+// The hub rows a level queues for k_shard_heavy: one packed 64-bit atomic per row gives its slot
+// and its edge offset together (rows in slot order = edge order, no gaps but past `cap`), and every
+// HEAVY_TILE-edge tile that starts inside a row records the row (tile -> first row), so the heavy
+// kernel walks the level's hub edges flat, edge-parallel over the whole grid.
+struct HeavyList {
+  HeavyRow* rows;
+  unsigned long long* pk;
+  uint32_t* tf;
+  uint32_t cap;
+};
+// Workgroup-aggregated append (every thread of the 256-thread workgroup calls it): one packed atomic
+// per workgroup gives the workgroup's first slot and edge offset.  Returns whether this thread's row
+// was queued (false past the cap: the caller expands it itself).
+__device__ __forceinline__ bool heavy_append(const HeavyList& H, bool app, const HeavyRow& row) {
+  __shared__ uint32_t s_hc[4];
+  __shared__ uint64_t s_he[4];
+  __shared__ unsigned long long s_hold;
+  const int lane = lane_id(), wave = threadIdx.x >> 6;
+  const uint64_t m = __ballot(app);
+  const uint64_t len = app ? row.len : 0ull;
+  uint64_t x = len;  // inclusive scan of the lengths within the wave
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint64_t y = shfl_up64(x, off);
+    if (lane >= off) x += y;
+  }
+  if (lane == 63) {
+    s_hc[wave] = (uint32_t)__popcll(m);
+    s_he[wave] = x;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint64_t tc = s_hc[0] + s_hc[1] + s_hc[2] + s_hc[3], te = s_he[0] + s_he[1] + s_he[2] + s_he[3];
+    s_hold = tc ? atomicAdd(H.pk, (unsigned long long)((tc << HEAVY_EDGE_BITS) | te)) : 0ull;
+  }
+  __syncthreads();
+  bool ok = false;
+  if (app) {
+    uint64_t at = s_hold >> HEAVY_EDGE_BITS, e0 = s_hold & ((1ull << HEAVY_EDGE_BITS) - 1);
+    for (int w = 0; w < wave; w++) {
+      at += s_hc[w];
+      e0 += s_he[w];
+    }
+    at += (uint64_t)__popcll(m & ((1ull << lane) - 1));
+    e0 += x - len;
+    if (at < H.cap) {
+      HeavyRow y = row;
+      y.e0 = e0;
+      H.rows[at] = y;
+      for (uint64_t t = (e0 + HEAVY_TILE - 1) / HEAVY_TILE; t * HEAVY_TILE < e0 + len && t < HEAVY_TF_CAP; t++)
+        H.tf[t] = (uint32_t)at;
+      ok = true;
+    }
+  }
+  __syncthreads();
+  return ok;
+}
 
 // (query, node) visited table: open addressing, cleared per batch.  1 fresh, 0 seen, -1 full.
 __device__ __forceinline__ int sv_insert(uint64_t* T, uint64_t mask, uint64_t key) {
@@ -108,10 +168,18 @@ __device__ __forceinline__ int sv_insert_lossy(uint64_t* T, uint64_t mask, uint6
 // rank: ballots per wave into LDS counters, then ONE device atomic per (workgroup, destination) --
 // at world 1 every record goes to one counter, so per-wave atomics serialised on it.  Every thread
 // of the workgroup must call it (256 threads).
+// sub > 1 (one rank, kg_shard_levels): the single bucket is `sub` segments of `cap` records with a
+// counter each, picked by the workgroup's XCD label (blockIdx & (sub - 1)), flags word counts[sub]:
+// a level's thousands of workgroup appends no longer queue on one counter word (~11 ns each at the
+// memory side, ~90 M/s per word: MI355X_MICROARCH.md); the next level reads the segments.
 __device__ __forceinline__ void emit(bool act, uint32_t dest, const kg_frec& r, kg_frec* out, uint64_t cap,
-                                     uint32_t* counts, uint32_t nranks) {
+                                     uint32_t* counts, uint32_t nranks, uint32_t sub = 1) {
   __shared__ uint32_t s_cnt[KG_SHARD_MAX_RANKS], s_base[KG_SHARD_MAX_RANKS];
   const int tid = threadIdx.x, lane = lane_id();
+  if (sub > 1) {
+    dest = blockIdx.x & (sub - 1);
+    nranks = sub;
+  }
   if (tid < (int)nranks) s_cnt[tid] = 0;
   __syncthreads();
   uint64_t pending = __ballot(act);
@@ -324,9 +392,9 @@ __global__ __launch_bounds__(256) void k_shard_level(DevSnap s, const kg_frec* _
                                                      const uint32_t* d_n_in, kg_frec* out, uint64_t cap, uint32_t* counts, uint8_t* res,
                                                      uint32_t* err, uint64_t* vis, uint64_t vmask,
                                                      const uint32_t* __restrict__ done, uint32_t done_wpr,
-                                                     HeavyRow* heavy, uint32_t* heavy_n, uint32_t heavy_cap,
+                                                     HeavyList heavy,
                                                      uint32_t* qcnt, uint32_t budget, uint32_t lossy, uint32_t n_seg,
-                                                     uint64_t seg_cap) {
+                                                     uint64_t seg_cap, uint32_t heavy_min, uint32_t out_sub) {
   __shared__ uint32_t s_pref[256], s_wsum[4];
   __shared__ uint64_t s_rb[256];
   __shared__ kg_frec s_rec[256];
@@ -375,6 +443,13 @@ __global__ __launch_bounds__(256) void k_shard_level(DevSnap s, const kg_frec* _
                  ((done[(size_t)(r.q >> Q_BITS) * done_wpr + ((r.q & Q_MASK) >> 5)] >> (r.q & 31)) & 1u)) {
         // answered IsMember by an earlier level: nothing more to do for this query
       } else {
+        // the probe's first dset bucket and the node's set-row bounds are loaded before the visited
+        // insert returns (all three in one round trip; a node already visited just ignores them)
+        const bool want_p = probe && r.depth >= 1 && r.subj != NONE;
+        const uint64_t dkey = dset_key(r.node, r.subj);
+        const ulonglong2 pb = *reinterpret_cast<const ulonglong2*>(
+            s.dset + (want_p ? hash_home(dkey, s.dset_nb) : 0ull) * DSET_BUCKET);
+        const uint64_t a0 = s.adj_off[r.node], a1 = s.adj_off[r.node + 1];
         const uint64_t vkey = ((uint64_t)r.q << 32) | r.node;
         const int ins = lossy ? sv_insert_lossy(vis, vmask, vkey) : sv_insert(vis, vmask, vkey);
         if (ins < 0) atomicOr(&counts[s.shard_n], 2u);
@@ -382,15 +457,18 @@ __global__ __launch_bounds__(256) void k_shard_level(DevSnap s, const kg_frec* _
           if ((r.q >> Q_BITS) == me) atomicMax(&err[r.q & Q_MASK], (uint32_t)KG_ERR_NOT_IMPLEMENTED);
           else err_out = true;
         } else if (ins > 0) {
-          if (probe && r.depth >= 1 && r.subj != NONE && dset_probe(s, r.node, r.subj)) {  // checkDirect(depth - 1)
+          // checkDirect(depth - 1): the first bucket, then (rarely, load <= 0.25) the rest of the chain
+          bool direct = want_p && (pb.x == dkey || pb.y == dkey);
+          if (want_p && !direct && pb.y != EMPTY64) direct = dset_probe(s, r.node, r.subj);
+          if (direct) {
             if ((r.q >> Q_BITS) == me) res[r.q & Q_MASK] = KG_IS_MEMBER;
             else hit_out = true;
           } else if (r.depth >= 2 || (r.depth == 1 && s.relflags)) {
             // children at depth - 1 >= 1 can still be probed; children at depth 0 cannot, but
             // checkIsAllowed(child, 0) still evaluates astRelationFor (engine.go:199-206), so with a
             // namespace program their relation flags are checked (shard_child) for the error report
-            rb = s.adj_off[r.node];
-            len = s.adj_off[r.node + 1] - rb;
+            rb = a0;
+            len = a1 - a0;
             if (len && budget) {  // escalation: this rank's set-edge count of the query passes the budget
               const uint32_t add = (uint32_t)min(len, (uint64_t)budget);
               const uint32_t old = atomicAdd(&qcnt[mix64(r.q) & ((1u << QCNT_LOG2) - 1)], add);
@@ -400,21 +478,17 @@ __global__ __launch_bounds__(256) void k_shard_level(DevSnap s, const kg_frec* _
               }
               if (old + add >= budget) len = 0;  // escalated: the backward phase answers it
             }
-            if (len > SHARD_HEAVY) {
-              const uint32_t at = atomicAdd(heavy_n, 1u);
-              if (at < heavy_cap) {
-                heavy[at] = HeavyRow{r, rb, (uint32_t)len, 0u};
-                len = 0;
-              }
-            }
           }
         }
       }
     }
+    // set rows longer than heavy_min go to the level's hub list (k_shard_heavy walks them flat over the
+    // grid); with heavy_min 0 every expansion does, and this workgroup only handles its records
+    if (heavy_append(heavy, len > heavy_min, HeavyRow{r, rb, 0ull, (uint32_t)len, 0u})) len = 0;
     // hit and error reports go to the query's home
     kg_frec hr{r.q, err_out ? KG_FREC_ERR : (esc_out ? KG_FREC_ESC : KG_FREC_HIT),
                err_out ? (uint32_t)KG_ERR_NOT_IMPLEMENTED : 0u, 0};
-    emit(hit_out || err_out || esc_out, r.q >> Q_BITS, hr, out, cap, counts, s.shard_n);
+    emit(hit_out || err_out || esc_out, r.q >> Q_BITS, hr, out, cap, counts, s.shard_n, out_sub);
     // expansion
     s_rb[tid] = rb;
     s_rec[tid] = r;
@@ -443,7 +517,7 @@ __global__ __launch_bounds__(256) void k_shard_level(DevSnap s, const kg_frec* _
         const int own = owner_search(s_pref, 256, e);
         shard_child(s, s_rec[own], s.adjx[s_rb[own] + (e - s_pref[own])], me, res, err, c, dest, send);
       }
-      emit(send, dest, c, out, cap, counts, s.shard_n);
+      emit(send, dest, c, out, cap, counts, s.shard_n, out_sub);
     }
     __syncthreads();
   }
@@ -548,8 +622,8 @@ __global__ __launch_bounds__(256) void k_shard_back_level(DevSnap s, const kg_fr
                                                           const uint32_t* d_n_in, kg_frec* out, uint64_t cap,
                                                           uint32_t* counts, uint8_t* res, uint32_t* err, uint64_t* vis,
                                                           uint64_t vmask, const uint32_t* __restrict__ done,
-                                                          uint32_t done_wpr, HeavyRow* heavy, uint32_t* heavy_n,
-                                                          uint32_t heavy_cap, uint32_t* qcnt, uint32_t budget,
+                                                          uint32_t done_wpr, HeavyList heavy, uint32_t* qcnt,
+                                                          uint32_t budget,
                                                           uint32_t lossy) {
   __shared__ uint32_t s_pref[256], s_wsum[4];
   __shared__ uint64_t s_rb[256];
@@ -587,16 +661,10 @@ __global__ __launch_bounds__(256) void k_shard_back_level(DevSnap s, const kg_fr
             }
             if (old + add >= budget) len = 0;
           }
-          if (len > SHARD_HEAVY) {
-            const uint32_t at = atomicAdd(heavy_n, 1u);
-            if (at < heavy_cap) {
-              heavy[at] = HeavyRow{r, rb, (uint32_t)len, 1u};
-              len = 0;
-            }
-          }
         }
       }
     }
+    if (heavy_append(heavy, len > SHARD_HEAVY, HeavyRow{r, rb, 0ull, (uint32_t)len, 1u})) len = 0;
     emit(esc_out, 0u, kg_frec{r.q, KG_FREC_ESC, 0u, 0}, out, cap, counts, 1u);  // to the home, via the all-gather
     s_rb[tid] = rb;
     s_rec[tid] = r;
@@ -627,25 +695,59 @@ __global__ __launch_bounds__(256) void k_shard_back_level(DevSnap s, const kg_fr
   }
 }
 
-// The hub rows a level queued: every workgroup takes 256-edge chunks of each row in turn.
-__global__ __launch_bounds__(256) void k_shard_heavy(DevSnap s, const HeavyRow* __restrict__ heavy,
-                                                     const uint32_t* __restrict__ heavy_n, uint32_t heavy_cap,
-                                                     kg_frec* out, uint64_t cap, uint32_t* counts, uint8_t* res,
-                                                     uint32_t* err, uint32_t nranks) {
-  const uint32_t nh = min(*heavy_n, heavy_cap), me = s.shard_rank;
-  for (uint32_t h = 0; h < nh; h++) {
-    const HeavyRow H = heavy[h];
-    for (uint64_t eb = (uint64_t)blockIdx.x * 256; eb < H.len; eb += (uint64_t)gridDim.x * 256) {
-      const uint64_t e = eb + threadIdx.x;
-      kg_frec c{};
-      uint32_t dest = 0;
-      bool send = false;
-      if (e < H.len) {
-        if (H.pad) back_child(s, H.r, s.radj[H.rb + e], me, res, c, send);  // a reverse row (backward phase)
-        else shard_child(s, H.r, s.adjx[H.rb + e], me, res, err, c, dest, send);
+// The hub rows a level queued, walked flat: HEAVY_TILE-edge tiles of the level's hub-edge space over
+// the whole grid, each tile's first row from the tile map, the row of each edge by a search over the
+// tile's rows staged in LDS.
+__global__ __launch_bounds__(256) void k_shard_heavy(DevSnap s, HeavyList heavy, kg_frec* out, uint64_t cap,
+                                                     uint32_t* counts, uint8_t* res, uint32_t* err, uint32_t nranks,
+                                                     uint32_t out_sub) {
+  static_assert(HEAVY_TILE == 256, "one edge per thread");
+  __shared__ uint32_t s_r0;
+  __shared__ uint64_t s_e0[HEAVY_TILE + 1];
+  const uint32_t nh = (uint32_t)min((unsigned long long)heavy.cap, *heavy.pk >> HEAVY_EDGE_BITS), me = s.shard_rank;
+  if (nh == 0) return;
+  const HeavyRow last = heavy.rows[nh - 1];
+  const uint64_t total = last.e0 + last.len;  // rows past the cap were expanded by their workgroup
+  for (uint64_t t0 = (uint64_t)blockIdx.x * HEAVY_TILE; t0 < total; t0 += (uint64_t)gridDim.x * HEAVY_TILE) {
+    if (threadIdx.x == 0) {
+      const uint64_t t = t0 / HEAVY_TILE;
+      uint32_t r0 = 0;
+      if (t < HEAVY_TF_CAP) {
+        r0 = heavy.tf[t];
+      } else {  // past the tile map: the last row starting at or before t0
+        uint32_t lo = 0, hi = nh;
+        while (hi - lo > 1) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (heavy.rows[mid].e0 <= t0) lo = mid;
+          else hi = mid;
+        }
+        r0 = lo;
       }
-      emit(send, dest, c, out, cap, counts, nranks);
+      s_r0 = r0;
     }
+    __syncthreads();
+    // the tile's rows (every queued row has >= 1 edge, so at most HEAVY_TILE + 1 of them): their first
+    // edges staged in LDS, each thread's row by binary search there
+    const uint32_t r0 = s_r0, nr = min(nh - r0, HEAVY_TILE + 1u);
+    for (uint32_t k = threadIdx.x; k < nr; k += HEAVY_TILE) s_e0[k] = heavy.rows[r0 + k].e0;
+    __syncthreads();
+    const uint64_t e = t0 + threadIdx.x;
+    kg_frec c{};
+    uint32_t dest = 0;
+    bool send = false;
+    if (e < total) {
+      uint32_t lo = 0, hi = nr;
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (s_e0[mid] <= e) lo = mid;
+        else hi = mid;
+      }
+      const HeavyRow H = heavy.rows[r0 + lo];
+      const uint64_t k = e - H.e0;
+      if (H.pad) back_child(s, H.r, s.radj[H.rb + k], me, res, c, send);  // a reverse row (backward phase)
+      else shard_child(s, H.r, s.adjx[H.rb + k], me, res, err, c, dest, send);
+    }
+    emit(send, dest, c, out, cap, counts, nranks, out_sub);  // ends with a barrier: s_r0 is free again
   }
 }
 
@@ -668,12 +770,10 @@ __global__ void k_shard_done(uint32_t n, const uint8_t* __restrict__ res, const 
 // hub-row count -- what the per-level driver did with a kernel and two fills.
 __global__ void k_shard_prep(uint32_t n, const uint8_t* __restrict__ res, const uint32_t* __restrict__ err,
                              uint32_t esc_mask, uint32_t words, uint32_t* __restrict__ bits, uint32_t* counts,
-                             uint32_t* heavy_n) {
+                             uint32_t n_sub, unsigned long long* heavy_pk) {
   const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
-  if (w == 0) {
-    counts[0] = 0;  // one rank: one bucket (the flags word counts[1] accumulates over the batch)
-    *heavy_n = 0;
-  }
+  if (w < n_sub) counts[w] = 0;  // the level's (sub-)bucket counters; the flags word after them accumulates
+  if (w == 0) *heavy_pk = 0;
   if (w >= words) return;
   uint32_t b = 0;
   for (uint32_t k = 0; k < 32; k++) {
@@ -681,6 +781,17 @@ __global__ void k_shard_prep(uint32_t n, const uint8_t* __restrict__ res, const 
     if (i < n && (res[i] == KG_IS_MEMBER || (esc_mask && (err[i] & esc_mask)))) b |= 1u << k;
   }
   bits[w] = b;
+}
+
+// After kg_shard_levels: the caller's view of the two level buffers -- records left in the last one
+// (the sum of its sub-bucket counters) and the flags accumulated in both.
+__global__ void k_shard_fold(const uint32_t* __restrict__ sub_end, const uint32_t* __restrict__ sub_other,
+                             uint32_t n_sub, uint32_t* counts_end, uint32_t* counts0) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  uint32_t left = 0;
+  for (uint32_t k = 0; k < n_sub; k++) left += sub_end[k];
+  counts_end[0] = left;
+  counts0[1] |= sub_end[n_sub] | sub_other[n_sub];
 }
 
 __global__ void k_shard_finish(uint32_t n, uint8_t* res, uint32_t* err, ShardFormula F) {
@@ -715,6 +826,30 @@ static int shard_formula(Snapshot* s, ShardCtx* c, size_t n, ShardFormula* F) {
   return 0;
 }
 
+__global__ void k_shard_bad_nodes(DevSnap s, unsigned long long* count) {
+  const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool bad = v < s.n_nodes && (!s.nowner || s.nowner[v] == s.shard_rank) && node_bad(s, v);
+  const uint64_t m = __ballot(bad);
+  if (lane_id() == 0 && m) atomicAdd(count, (unsigned long long)__popcll(m));
+}
+
+int shard_bad_nodes(Snapshot* s, uint64_t* count) {
+  HIPC(hipSetDevice(s->device));
+  *count = 0;
+  if (!s->ds.n_nodes) return 0;
+  unsigned long long* d = nullptr;
+  HIPC(hipMalloc((void**)&d, 8));
+  HIPC(hipMemsetAsync(d, 0, 8, s->stream));
+  hipLaunchKernelGGL(k_shard_bad_nodes, dim3((s->ds.n_nodes + 255) / 256), dim3(256), 0, s->stream, s->ds, d);
+  HIPC(hipGetLastError());
+  unsigned long long h = 0;
+  HIPC(hipMemcpyAsync(&h, d, 8, hipMemcpyDeviceToHost, s->stream));
+  HIPC(hipStreamSynchronize(s->stream));
+  HIPC(hipFree(d));
+  *count = h;
+  return 0;
+}
+
 size_t shard_result_slots(const Snapshot* s, size_t n) { return s->n_fplans ? n * (2 + (size_t)s->fp_leaves) : n; }
 
 static int shard_vis_prepare(Snapshot* s, ShardCtx* c, hipStream_t stream) {
@@ -731,9 +866,17 @@ static int shard_vis_prepare(Snapshot* s, ShardCtx* c, hipStream_t stream) {
   }
   HIPC(hipMemsetAsync(c->vis, 0xFF, c->vis_slots * 8, stream));
   if (!c->heavy) {
-    HIPC(hipMalloc(&c->heavy, (size_t)SHARD_HEAVY_CAP * sizeof(HeavyRow) + 64));
+    HIPC(hipMalloc(&c->heavy, (size_t)SHARD_HEAVY_CAP * sizeof(HeavyRow) + 256 + HEAVY_TF_CAP * 4));
   }
   return 0;
+}
+
+// The stream's hub-row list: rows, then the packed counter, then the tile map.
+static HeavyList heavy_list(ShardCtx* c) {
+  HeavyRow* rows = (HeavyRow*)c->heavy;
+  unsigned long long* pk = (unsigned long long*)(rows + SHARD_HEAVY_CAP);
+  uint32_t* tf = (uint32_t*)((char*)pk + 256);
+  return HeavyList{rows, pk, tf, SHARD_HEAVY_CAP};
 }
 
 // Escalation is on for snapshots without a namespace program (errors below the root cannot occur)
@@ -794,18 +937,17 @@ int shard_level(Snapshot* s, const kg_frec* d_in, size_t n_in, const uint32_t* d
   // accumulates over the batch's levels, so the caller reads it once at the end
   HIPC(hipMemsetAsync(d_counts, 0, s->shard_n * 4, stream));
   if (n_in) {
-    HeavyRow* heavy = (HeavyRow*)c->heavy;
-    uint32_t* heavy_n = (uint32_t*)(heavy + SHARD_HEAVY_CAP);
-    HIPC(hipMemsetAsync(heavy_n, 0, 4, stream));
+    const HeavyList heavy = heavy_list(c);
+    HIPC(hipMemsetAsync(heavy.pk, 0, 8, stream));
     const uint32_t grid = (uint32_t)std::min<uint64_t>((n_in + 255) / 256, (uint64_t)s->n_cu * 8);
     hipLaunchKernelGGL(k_shard_level, dim3(grid), dim3(256), 0, stream, s->ds, d_in, (uint64_t)n_in, d_n_in, d_out,
                        (uint64_t)cap, d_counts, d_res, d_err, (uint64_t*)c->vis, c->vis_slots - 1,
-                       d_done, d_done ? done_words : 0u, heavy, heavy_n, SHARD_HEAVY_CAP, (uint32_t*)c->qcnt,
+                       d_done, d_done ? done_words : 0u, heavy, (uint32_t*)c->qcnt,
                        shard_escalates(s) && c->qcnt && !c->final ? s->shard_budget : 0u,
-                       s->shard_vis_mode ? 1u : 0u, n_seg, (uint64_t)seg_cap);
+                       s->shard_vis_mode ? 1u : 0u, n_seg, (uint64_t)seg_cap, s->shard_heavy, 1u);
     HIPC(hipGetLastError());
-    hipLaunchKernelGGL(k_shard_heavy, dim3((uint32_t)s->n_cu * 4), dim3(256), 0, stream, s->ds, heavy, heavy_n,
-                       SHARD_HEAVY_CAP, d_out, (uint64_t)cap, d_counts, d_res, d_err, s->shard_n);
+    hipLaunchKernelGGL(k_shard_heavy, dim3((uint32_t)s->n_cu * 4), dim3(256), 0, stream, s->ds, heavy, d_out,
+                       (uint64_t)cap, d_counts, d_res, d_err, s->shard_n, 1u);
     HIPC(hipGetLastError());
   }
   return 0;
@@ -831,27 +973,40 @@ int shard_levels(Snapshot* s, int levels, kg_frec* d_buf[2], size_t cap, uint32_
     HIPC(hipMalloc((void**)&c->bits, ((size_t)words + 1) * 4));
     c->bits_n = (size_t)words + 1;
   }
-  HeavyRow* heavy = (HeavyRow*)c->heavy;
-  uint32_t* heavy_n = (uint32_t*)(heavy + SHARD_HEAVY_CAP);
+  const HeavyList heavy = heavy_list(c);
   const uint32_t esc = esc_mode == 1 ? ESC_BIT : (esc_mode == 2 ? ESC2_BIT : 0u);
   const uint32_t budget = shard_escalates(s) && c->qcnt && !c->final ? s->shard_budget : 0u;
   const uint32_t grid = (uint32_t)std::min<uint64_t>((cap + 255) / 256, (uint64_t)s->n_cu * 8);
+  // the levels' records go to SUB per-XCD segments of one buffer, each with its own counter (emit's
+  // sub mode): level 0 reads the seed's bucket, every later level the SUB segments of the one before
+  const uint32_t SUB = cap >= 8 * 256 ? 8u : 1u;
+  const uint64_t seg = cap / SUB;
+  if (!c->cnt8) HIPC(hipMalloc((void**)&c->cnt8, 32 * 4));
+  HIPC(hipMemsetAsync(c->cnt8, 0, 32 * 4, stream));
+  uint32_t* sub[2] = {c->cnt8, c->cnt8 + 16};
   int cur = start & 1;
   for (int k = 0; k < levels; k++) {
     const int nx = cur ^ 1;
     const uint32_t w = k > 0 ? words : 0u;
     hipLaunchKernelGGL(k_shard_prep, dim3(std::max<uint32_t>(1, (w + 255) / 256)), dim3(256), 0, stream, (uint32_t)slots,
-                       d_res, d_err, esc, w, c->bits, d_counts[nx], heavy_n);
+                       d_res, d_err, esc, w, c->bits, sub[nx], SUB, heavy.pk);
     HIPC(hipGetLastError());
-    hipLaunchKernelGGL(k_shard_level, dim3(grid), dim3(256), 0, stream, s->ds, d_buf[cur], (uint64_t)cap, d_counts[cur],
-                       d_buf[nx], (uint64_t)cap, d_counts[nx], d_res, d_err, (uint64_t*)c->vis, c->vis_slots - 1,
-                       k > 0 ? (const uint32_t*)c->bits : nullptr, w, heavy, heavy_n, SHARD_HEAVY_CAP, (uint32_t*)c->qcnt,
-                       budget, s->shard_vis_mode ? 1u : 0u, 1u, (uint64_t)0);
+    const bool seg_in = k > 0;
+    hipLaunchKernelGGL(k_shard_level, dim3(grid), dim3(256), 0, stream, s->ds, d_buf[cur], (uint64_t)cap,
+                       seg_in ? sub[cur] : d_counts[cur], d_buf[nx], seg, sub[nx], d_res, d_err, (uint64_t*)c->vis,
+                       c->vis_slots - 1, k > 0 ? (const uint32_t*)c->bits : nullptr, w, heavy, (uint32_t*)c->qcnt,
+                       budget, s->shard_vis_mode ? 1u : 0u, seg_in ? SUB : 1u, seg_in ? seg : (uint64_t)0,
+                       s->shard_heavy, SUB);
     HIPC(hipGetLastError());
-    hipLaunchKernelGGL(k_shard_heavy, dim3((uint32_t)s->n_cu * 4), dim3(256), 0, stream, s->ds, heavy, heavy_n,
-                       SHARD_HEAVY_CAP, d_buf[nx], (uint64_t)cap, d_counts[nx], d_res, d_err, s->shard_n);
+    hipLaunchKernelGGL(k_shard_heavy, dim3((uint32_t)s->n_cu * 4), dim3(256), 0, stream, s->ds, heavy, d_buf[nx], seg,
+                       sub[nx], d_res, d_err, s->shard_n, SUB);
     HIPC(hipGetLastError());
     cur = nx;
+  }
+  if (levels > 0) {  // the caller's counters: records left in the last buffer, flags of both
+    hipLaunchKernelGGL(k_shard_fold, dim3(1), dim3(64), 0, stream, sub[cur], sub[cur ^ 1], SUB, d_counts[cur],
+                       d_counts[0]);
+    HIPC(hipGetLastError());
   }
   if (end) *end = cur;
   return 0;
@@ -932,17 +1087,16 @@ int shard_back_level(Snapshot* s, const kg_frec* d_in, size_t n_in, const uint32
   // the bucket size restarts; the flags word (d_counts[1]) accumulates over the phase
   HIPC(hipMemsetAsync(d_counts, 0, 4, stream));
   if (n_in && s->ds.radj) {
-    HeavyRow* heavy = (HeavyRow*)c->heavy;
-    uint32_t* heavy_n = (uint32_t*)(heavy + SHARD_HEAVY_CAP);
-    HIPC(hipMemsetAsync(heavy_n, 0, 4, stream));
+    const HeavyList heavy = heavy_list(c);
+    HIPC(hipMemsetAsync(heavy.pk, 0, 8, stream));
     const uint32_t grid = (uint32_t)std::min<uint64_t>((n_in + 255) / 256, (uint64_t)s->n_cu * 8);
     hipLaunchKernelGGL(k_shard_back_level, dim3(grid), dim3(256), 0, stream, s->ds, d_in, (uint64_t)n_in, d_n_in, d_out,
                        (uint64_t)cap, d_counts, d_res, d_err, (uint64_t*)c->vis, c->vis_slots - 1, d_done,
-                       d_done ? done_words : 0u, heavy, heavy_n, SHARD_HEAVY_CAP, (uint32_t*)c->qcnt,
+                       d_done ? done_words : 0u, heavy, (uint32_t*)c->qcnt,
                        c->qcnt ? s->shard_back_budget : 0u, s->shard_vis_mode ? 1u : 0u);
     HIPC(hipGetLastError());
-    hipLaunchKernelGGL(k_shard_heavy, dim3((uint32_t)s->n_cu * 4), dim3(256), 0, stream, s->ds, heavy, heavy_n,
-                       SHARD_HEAVY_CAP, d_out, (uint64_t)cap, d_counts, d_res, d_err, 1u);
+    hipLaunchKernelGGL(k_shard_heavy, dim3((uint32_t)s->n_cu * 4), dim3(256), 0, stream, s->ds, heavy, d_out,
+                       (uint64_t)cap, d_counts, d_res, d_err, 1u, 1u);
     HIPC(hipGetLastError());
   }
   return 0;

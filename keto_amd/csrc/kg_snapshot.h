@@ -150,6 +150,7 @@ struct ShardCtx {
   size_t ref_n = 0;
   uint32_t* bits = nullptr;  // kg_shard_levels: the batch's done bitmap
   size_t bits_n = 0;
+  uint32_t* cnt8 = nullptr;  // kg_shard_levels: per-XCD sub-bucket counters of the two level buffers (+ flags)
   ~ShardCtx();
 };
 
@@ -223,6 +224,7 @@ struct Snapshot {
   uint32_t* shard_held = nullptr;  // holder bitmap OR-ed over every rank (kg_shard_held), or null
   uint32_t shard_held_n = 0;
   int shard_vis_log2 = 23;
+  uint32_t shard_heavy = 64;  // kg_snapshot_tune("shard_heavy"): set rows longer than this go to k_shard_heavy (r3p A/B)
   int shard_vis_mode = 0;  // kg_snapshot_tune("shard_vis_mode"): (query, node) dedup 0 = exact CAS table, 1 = lossy cache
   uint32_t shard_budget = 0;       // kg_snapshot_tune("shard_budget"): forward set edges per query and rank (0 = off)
   uint32_t shard_back_budget = 1u << 14;  // kg_snapshot_tune("shard_back_budget"): reverse edges per query and rank
@@ -321,6 +323,7 @@ int shard_refwd_seed(Snapshot* s, size_t n, const uint8_t* d_res, const uint32_t
 int shard_held(Snapshot* s, uint32_t* d_bits, size_t words, int import, hipStream_t stream);
 int shard_finish(Snapshot* s, size_t n, uint8_t* d_res, uint32_t* d_err, hipStream_t stream);
 size_t shard_result_slots(const Snapshot* s, size_t n);
+int shard_bad_nodes(Snapshot* s, uint64_t* count);
 // kg_grid.hip
 int grid_reserve(Snapshot* s);  // allocates the shared full-size grid pool now (kg_snapshot_tune "grid_reserve")
 // kg_expand.hip

@@ -363,7 +363,7 @@ void Snapshot::lanes_release(std::vector<Lane*>* v) {
 
 ShardCtx::~ShardCtx() {
   if (device >= 0) hipSetDevice(device);
-  for (void* p : {vis, heavy, qcnt, qinfo, (void*)ref, (void*)bits})
+  for (void* p : {vis, heavy, qcnt, qinfo, (void*)ref, (void*)bits, (void*)cnt8})
     if (p) hipFree(p);
 }
 

@@ -146,6 +146,12 @@ class HipShardOps:
         _lib.check(self.L.kg_shard_held(self.snapshot.handle, bits.data_ptr(), int(bits.shape[0]), 1, self._s()),
                    "kg_shard_held")
 
+    def errors_possible(self) -> bool:
+        """Some node this rank owns can end a check in an error (kg_shard_bad_nodes)."""
+        c = C.c_uint64(0)
+        _lib.check(self.L.kg_shard_bad_nodes(self.snapshot.handle, C.byref(c)), "kg_shard_bad_nodes")
+        return c.value > 0
+
     def result_slots(self, n: int) -> int:
         """Result slots of a batch of n queries: n, plus the parts of formula-split queries."""
         return int(self.L.kg_shard_result_slots(self.snapshot.handle, n))
@@ -239,6 +245,10 @@ class ShardedChecker:
         # single-GPU engine on a snapshot of the rows they can read, gathered to their home rank
         self.general = bool(general) and hasattr(ops, "general_check")
         self._gen_any = False
+        # the done bitmap drops a member query's records; with errors possible anywhere it must not
+        # (an error in an earlier branch wins over a member found at a shallower level in a later one:
+        # the reference's first-decisive order), so it is on only when no rank has a node that errors
+        self._prune = None
         self.general_queries = 0
         self.general_rows = 0
 
@@ -397,16 +407,27 @@ class ShardedChecker:
             cur ^= 1
             self.back_levels += 1
 
+    def _pruning(self) -> bool:
+        """Whether the done bitmap may drop member queries' records: no rank can end a check in an error
+        below its root (kg_shard_bad_nodes; asked once, all-reduced)."""
+        if self._prune is None:
+            if self.dist is not None and self.world > 1:
+                self._max_slots(self._n)  # its one-time all-reduce carries the flag
+            else:
+                mine = bool(self.ops.errors_possible()) if hasattr(self.ops, "errors_possible") else False
+                self._prune = hasattr(self.ops, "done_bits") and not mine
+        return self._prune
+
     def _device_levels(self, bufs, counts, cur, res, err, slots, gdepth, words, esc_mode, trace, final=False):
         """One rank: gdepth forward levels enqueued back to back, record counts read on the device
         (esc_mode 1: escalated queries are done for the done bitmap; final: the batch's final forward
         phase, counted apart).  Returns the current buffer."""
         cap = self.cap
-        prune = hasattr(self.ops, "done_bits")
-        if trace is None and prune and hasattr(self.ops, "levels"):  # the whole loop in one library call
+        prune = self._pruning()
+        if trace is None and hasattr(self.ops, "done_bits") and hasattr(self.ops, "levels"):  # one library call
             if not final:
                 self.levels += gdepth
-            return self.ops.levels(gdepth, bufs, cap, counts, cur, res, err, slots, esc_mode)
+            return self.ops.levels(gdepth, bufs, cap, counts, cur, res, err, slots if prune else 0, esc_mode)
         for k in range(gdepth):
             c = counts[cur]
             if trace is not None:  # diagnostics: records entering each level (a host sync per level)
@@ -552,7 +573,7 @@ class ShardedChecker:
         # result slots: the queries, then the parts of formula-split queries (kg_shard_result_slots)
         slots = self.ops.result_slots(n) if hasattr(self.ops, "result_slots") else n
         self._n = slots
-        prune = hasattr(self.ops, "done_bits")
+        prune = self._pruning()
         # escalation: forward done bits carry escalated queries; backward and final forward phases follow
         backward = hasattr(self.ops, "back_level") and getattr(self.ops, "escalates", True)
         self.back_levels = self.final_levels = 0
@@ -644,10 +665,15 @@ class ShardedChecker:
         import torch
         cache = self.__dict__.setdefault("_slots_cache", {})
         if slots not in cache:
-            t = torch.tensor([slots], dtype=torch.int64, device="cpu" if self._host_staged() else self.device)
+            # the same all-reduce carries "some rank can end a check in an error" the first time (_pruning)
+            mine = bool(self.ops.errors_possible()) if self._prune is None and hasattr(self.ops, "errors_possible") else False
+            t = torch.tensor([slots, int(mine)], dtype=torch.int64, device="cpu" if self._host_staged() else self.device)
             self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX, group=self.group)
             self.host_syncs += 1
-            cache[slots] = int(t.item())
+            h = t.cpu().numpy()
+            cache[slots] = int(h[0])
+            if self._prune is None:
+                self._prune = hasattr(self.ops, "done_bits") and not bool(h[1])
         return cache[slots]
 
     def _check_fixed(self, dq, n: int, slots: int, gdepth: int, res, err):
@@ -674,7 +700,7 @@ class ShardedChecker:
         self.ops.seed(dq, n, gdepth, bufs[0], B, counts[0], res, err)
         cur = 0
         self.levels = 0
-        prune = hasattr(self.ops, "done_bits")
+        prune = self._pruning()
         for k in range(gdepth + 1):
             c = counts[cur]
             c64 = c[:N].to(torch.int64)

@@ -96,6 +96,9 @@ class CpuShardOps:
         self.vis = set()
         self.qcnt, self.qinfo = {}, {}
 
+    def errors_possible(self) -> bool:  # kg_shard_bad_nodes: a relation the protocol cannot evaluate
+        return bool(self.impure)
+
     def _emit(self, out, cap, counts, dest, rec, nb=None):
         nb = self.n if nb is None else nb  # buckets (the flags word follows them)
         at = int(counts[dest])

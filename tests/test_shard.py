@@ -444,7 +444,7 @@ def test_sharded_general_rewrites_vs_oracle(kind, world):
 
 # ------------------------------------------------------------------ config C4 generator, sharded
 def _synth_worker(rank, world, port, n_tuples, n_q, gmax, backend, outq, preset=0, budget=None, back_budget=None,
-                  vis_mode=0):
+                  vis_mode=0, heavy=None):
     sys.path.insert(0, ROOT)
     import torch.distributed as dist
     from keto_amd import _lib
@@ -463,6 +463,8 @@ def _synth_worker(rank, world, port, n_tuples, n_q, gmax, backend, outq, preset=
     if back_budget is not None:
         snap.tune("shard_back_budget", back_budget)
     snap.tune("shard_vis_mode", vis_mode)
+    if heavy is not None:
+        snap.tune("shard_heavy", heavy)
     dq = torch.empty((n_q, 7), dtype=torch.int32, device="cuda")
     _lib.check(_lib.load().kg_synth_queries(snap.handle, 31, n_q, dq.data_ptr()), "kg_synth_queries")
     mine = np.array_split(np.arange(n_q), world)[rank]
@@ -478,20 +480,25 @@ def _synth_worker(rank, world, port, n_tuples, n_q, gmax, backend, outq, preset=
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,backend,budget,back_budget,vis_mode", [(1, None, None, None, 0), (1, "nccl", None, None, 0),
-                                                                       (2, "gloo", None, None, 0), (1, None, 8, None, 0),
-                                                                       (1, "nccl", 8, 64, 0), (2, "gloo", 8, 64, 0),
-                                                                       (1, None, None, None, 1), (2, "gloo", None, None, 1)])
-def test_sharded_c4_generator_vs_oracle(world, backend, budget, back_budget, vis_mode):
+@pytest.mark.parametrize("world,backend,budget,back_budget,vis_mode,heavy",
+                         [(1, None, None, None, 0, None), (1, "nccl", None, None, 0, None),
+                          (2, "gloo", None, None, 0, None), (1, None, 8, None, 0, None),
+                          (1, "nccl", 8, 64, 0, None), (2, "gloo", 8, 64, 0, None),
+                          (1, None, None, None, 1, None), (2, "gloo", None, None, 1, None),
+                          (1, None, None, None, 0, 256), (2, "gloo", None, None, 0, 256), (1, None, 8, 64, 0, 256),
+                          (1, None, None, None, 0, 0), (2, "gloo", None, None, 0, 0), (1, "nccl", None, None, 0, 0)])
+def test_sharded_c4_generator_vs_oracle(world, backend, budget, back_budget, vis_mode, heavy):
     """Config C4's generator, hash-sharded: world 1 with every level on the device (no host round
     trip per level), world 1 through torch.distributed over RCCL ("nccl": the metadata and record
     all-to-alls run on device tensors), and world 2 (two ranks on one GPU, gloo).  Against the
     oracle on the whole graph's rows, bit-exact; the synthetic queries only touch rewrite-free nodes.
     Budget 8: most walks escalate to the backward phase (the default budget escalates the hub-heavy
-    ones only)."""
+    ones only).  heavy 256 / 0: every set row over 256 edges / every set row goes to the flat
+    grid-wide hub kernel (k_shard_heavy's tile map), in the forward and the backward phase."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    _run_synth(world, backend, 300_000, 20_000, 10, preset=0, budget=budget, back_budget=back_budget, vis_mode=vis_mode)
+    _run_synth(world, backend, 300_000, 20_000, 10, preset=0, budget=budget, back_budget=back_budget, vis_mode=vis_mode,
+               heavy=heavy)
 
 
 @pytest.mark.gpu
@@ -507,14 +514,14 @@ def test_sharded_c3_rewrites_vs_oracle(world, backend):
     _run_synth(world, backend, 150_000, 6000, 10, preset=1)
 
 
-def _run_synth(world, backend, n_tuples, n_q, gmax, preset, budget=None, back_budget=None, vis_mode=0):
+def _run_synth(world, backend, n_tuples, n_q, gmax, preset, budget=None, back_budget=None, vis_mode=0, heavy=None):
     from keto_amd.engine import Snapshot
     from oracle.oracle import POLICY_CANONICAL, Oracle
     ctx = mp.get_context("spawn")
     outq = ctx.Queue()
     port = _free_port()
     ps = [ctx.Process(target=_synth_worker, args=(r, world, port, n_tuples, n_q, gmax, backend, outq, preset, budget,
-                                                  back_budget, vis_mode)) for r in range(world)]
+                                                  back_budget, vis_mode, heavy)) for r in range(world)]
     for p in ps:
         p.start()
     got = [outq.get(timeout=110) for _ in range(world)]
@@ -606,3 +613,50 @@ def test_formula_ttu_leaves_vs_oracle(sharded):
         bad = np.nonzero((out != exp) | (err.astype(np.int64) != oerr))[0]
         assert bad.size == 0, [(str(qs[i]), int(depths[i]), int(out[i]), int(exp[i]), int(err[i])) for i in bad[:8]]
         assert 0.05 < (out == 1).mean() < 0.95 and (oerr == 0).all()
+
+
+def _order_graph():
+    """A member found at a shallow level in a LATER branch, an error deeper in an EARLIER one:
+    d:x#a has rows (d:y#a), (d:z#a) in that order; d:y#a -> (d:w#nope) where nope is undeclared
+    (checkIsAllowed on it fails with RELATION_NOT_FOUND, engine.go:228); d:z#a holds u directly.
+    The canonical recursion visits y's subtree first, so x#a@u is an error at depths >= 3 and a
+    member at depth 2 (w is then at rest depth -1, never looked up)."""
+    sys.path.insert(0, ROOT)
+    from keto_amd.engine import queries_array
+    from keto_amd.ketoapi import RelationTuple
+    from keto_amd.mapper import Interner
+    from keto_amd.namespace import Namespace, Relation, compile_program
+    it = Interner()
+    rows = ["d:x#a@(d:y#a)", "d:x#a@(d:z#a)", "d:y#a@(d:w#nope)", "d:z#a@u", "d:w#nope@v", "d:p#a@(d:x#a)"]
+    t6 = it.tuples_array([RelationTuple.from_string(r) for r in rows])
+    prog = compile_program([Namespace("d", [Relation("a")])], it)
+    qs = ["d:x#a@u", "d:p#a@u", "d:z#a@u", "d:y#a@u", "d:x#a@v"]
+    q6 = np.asarray([it.tuple_ids(RelationTuple.from_string(x)) for x in qs], np.uint32)
+    q = np.concatenate([queries_array(q6, d) for d in (2, 3, 4, 5)])
+    impure = [(it.ns_id("d"), it.rel_id("nope"))]
+    return it, t6, q, prog, impure
+
+
+@pytest.mark.parametrize("general", [True, False])
+def test_sharded_member_does_not_hide_an_earlier_error(general):
+    """The level protocol finds z's direct tuple one level before it reaches w's undeclared relation;
+    pruning the query's records once it is a member would hide the error the canonical order
+    reports first.  With errors possible in the graph the protocol does not prune, so the query ends
+    NOT_IMPLEMENTED and the general phase gives the oracle's answer (general off: the error stays)."""
+    from oracle.oracle import POLICY_CANONICAL, Oracle
+    from keto_amd.sharded import ShardedChecker
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from shard_ref import CpuShardOps
+    it, t6, q, prog, impure = _order_graph()
+    o = Oracle(t6, it.wildcard_rel, prog)
+    for gmax in (2, 5):
+        exp, oerr, _ = o.check_batch(q[:, :6], q[:, 6].view(np.int32), gmax, POLICY_CANONICAL)
+        chk = ShardedChecker(CpuShardOps(t6, it.wildcard_rel, 0, 1, impure, program=prog), 0, 1, None, device="cpu",
+                             cap=1 << 10, general=general)
+        res, err = chk.check(torch.from_numpy(q.view(np.int32).copy()), gmax)
+        res, err = res.numpy(), err.numpy()
+        if general:
+            assert (res == exp).all() and (err == oerr).all(), (gmax, res, exp, err, oerr)
+        else:  # every query the oracle answers with an error is an error here too (never a member)
+            assert (res[oerr != 0] == 2).all(), (gmax, res, exp, err, oerr)
+    assert (oerr != 0).any() and (exp == 1).any()
