@@ -70,6 +70,8 @@ def parse(argv=None):
     ap.add_argument("--shard-back-budget", type=int, default=1 << 14,
                     help="kg_snapshot_tune shard_back_budget (reverse edges per query and rank before the final "
                          "forward phase takes it)")
+    ap.add_argument("--shard-wgs", type=int, default=0,
+                    help="kg_snapshot_tune shard_wgs: sharded level kernel workgroups per CU (0: library default)")
     ap.add_argument("--shard-heavy", type=int, default=-1,
                     help="kg_snapshot_tune shard_heavy: set rows longer than this are expanded grid-wide (k_shard_heavy; "
                          "0: every expansion; -1: the library default)")
@@ -445,6 +447,8 @@ def bench_sharded(a):
     snap.tune("shard_vis_mode", a.shard_vis_mode)
     if a.shard_heavy >= 0:
         snap.tune("shard_heavy", a.shard_heavy)
+    if a.shard_wgs:
+        snap.tune("shard_wgs", a.shard_wgs)
     B = a.batch
     P = max(1, a.inflight)
     n_distinct = max(P, 2)

@@ -432,6 +432,11 @@ static int tune_one(Snapshot* s, const char* key, int64_t value) {
     s->shard_budget = (uint32_t)value;
     return 0;
   }
+  if (strcmp(key, "shard_wgs") == 0) {
+    if (value < 1 || value > 64) return set_error(-2, "shard_wgs must be in [1, 64]");
+    s->shard_wgs = (uint32_t)value;
+    return 0;
+  }
   if (strcmp(key, "shard_heavy") == 0) {
     if (value < 0 || value > 0xFFFFFFFFll) return set_error(-2, "shard_heavy must be in [0, 2^32)");
     s->shard_heavy = (uint32_t)value;

@@ -205,111 +205,186 @@ __device__ __forceinline__ void emit(bool act, uint32_t dest, const kg_frec& r, 
   __syncthreads();
 }
 
+// emit() for Q records per thread (one ballot pass per record slot, still ONE device atomic per
+// (workgroup, destination)): the seed handles Q queries per thread, so a batch takes Q times fewer
+// workgroup appends on the bucket counters.  Every thread of the workgroup must call it.
+template <int Q>
+__device__ __forceinline__ void emit_q(const bool (&act)[Q], const uint32_t (&dest)[Q], const kg_frec (&r)[Q],
+                                       kg_frec* out, uint64_t cap, uint32_t* counts, uint32_t nranks) {
+  __shared__ uint32_t s_cnt[KG_SHARD_MAX_RANKS], s_base[KG_SHARD_MAX_RANKS];
+  const int tid = threadIdx.x, lane = lane_id();
+  if (tid < (int)nranks) s_cnt[tid] = 0;
+  __syncthreads();
+  uint32_t my[Q];
+#pragma unroll
+  for (int j = 0; j < Q; j++) {
+    my[j] = 0;
+    uint64_t pending = __ballot(act[j]);
+    while (pending) {
+      const int lead = __ffsll((unsigned long long)pending) - 1;
+      const uint32_t d = __shfl(dest[j], lead, 64);
+      const uint64_t m = __ballot(act[j] && dest[j] == d);
+      uint32_t base = 0;
+      if (lane == lead) base = atomicAdd(&s_cnt[d], (uint32_t)__popcll(m));
+      base = __shfl(base, lead, 64);
+      if (act[j] && dest[j] == d) my[j] = base + __popcll(m & ((1ull << lane) - 1));
+      pending &= ~m;
+    }
+  }
+  __syncthreads();
+  if (tid < (int)nranks) s_base[tid] = s_cnt[tid] ? atomicAdd(&counts[tid], s_cnt[tid]) : 0u;
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < Q; j++) {
+    if (act[j]) {
+      const uint32_t at = s_base[dest[j]] + my[j];
+      if (at < cap) out[(uint64_t)dest[j] * cap + at] = r[j];
+      else atomicOr(&counts[nranks], 1u);
+    }
+  }
+  __syncthreads();
+}
+
+// One query of the seed: mapping, depth clamp, the root's record (or an answer at once), and what the
+// formula split's parts need.
+struct SeedQ {
+  bool act, split;
+  uint32_t dest, ssubj;
+  int32_t dsplit;
+  kg_frec r;
+  kg_query x;
+};
+
+__device__ __forceinline__ SeedQ seed_query(const DevSnap& s, const kg_query* __restrict__ q, uint32_t i, uint32_t n,
+                                           int32_t global, uint8_t* res, uint32_t* err,
+                                           const uint32_t* __restrict__ held, uint32_t held_n, const ShardFormula& F,
+                                           uint4* qinfo) {
+  SeedQ o{};
+  o.ssubj = NONE;
+  if (i >= n) return o;
+  if (F.ref) F.ref[i] = NONE;
+  const kg_query x = q[i];
+  o.x = x;
+  uint32_t subj = NONE;
+  const bool sid = x.t.sns == KG_SUBJECT_ID;
+  if (sid) subj = x.t.sobj < 0x7FFFFFFFu ? x.t.sobj : NONE;
+  // without a namespace program a subject id that no rank's row holds is NotMember whatever the root:
+  // the holder bit (a small, cache-resident bitmap) is read first and such a query never touches the
+  // node map (k_resolve's resolve_unheld order)
+  const bool unheld = held && !s.relflags && sid &&
+                      (subj == NONE || subj >= held_n || !((held[subj >> 5] >> (subj & 31)) & 1u));
+  uint32_t node = NONE, rsig = 0xFFFFFFFFu, rlen = 0;
+  if (!unheld && nmap_key_ok(x.t.ns, x.t.rel, x.t.obj)) {
+    const uint64_t key = nmap_key(x.t.ns, x.t.rel, x.t.obj);
+    const NSlot* sl = nmap_slot(s, key, hash_home(key, s.nmap_n));
+    if (sl) {
+      node = sl->node;
+      rsig = sl->sig;
+      rlen = sl->len;
+    }
+  }
+  if (!sid) {
+    const uint32_t sn = nmap_find(s, x.t.sns, x.t.srel, x.t.sobj);
+    subj = sn == NONE ? NONE : (SET_BIT | sn);
+  }
+  int32_t d = x.max_depth;
+  if (d <= 0 || global < d) d = global;  // engine.go:68-70
+  res[i] = KG_NOT_MEMBER;
+  err[i] = KG_ERR_NONE;
+  const uint8_t rf = relflag(s, x.t.ns, x.t.rel);
+  const uint32_t pr = (x.t.ns < s.n_ns && x.t.rel < s.n_rel) ? x.t.ns * s.n_rel + x.t.rel : NONE;
+  const bool virt = F.virt && pr != NONE && F.virt[pr];
+  bool bad = node != NONE ? node_bad(s, node) : (rf != 0 && !virt);  // a union without a node: NotMember
+  if (bad && F.fidx && pr != NONE && F.fidx[pr] >= 0) {  // a formula over plain / union leaves: split
+    const FPlan& P = F.plans[F.fidx[pr]];
+    bool ok = true;
+    for (uint32_t j = 0; j < P.n_leaves; j++) {
+      const uint32_t ln = nmap_find(s, x.t.ns, P.leaf[j], x.t.obj);
+      if (ln != NONE && node_bad(s, ln)) ok = false;
+    }
+    if (ok) {
+      F.ref[i] = (uint32_t)F.fidx[pr];
+      o.split = true;
+      bad = false;
+    }
+  }
+  if (bad) {  // the interpreter's territory: the driver's general phase (keto_amd/sharded.py)
+    err[i] = KG_ERR_NOT_IMPLEMENTED;
+  } else if (o.split) {
+    // records by the caller, one per part
+  } else if (unheld) {
+    // no row of any rank holds the subject: checkDirect can never hit (NotMember)
+  } else if (node != NONE && (subj != NONE || s.relflags)) {
+    // an unknown subject can never be held, but with a namespace program the query can still
+    // reach a rewrite (an error), so it is seeded all the same (its probes are skipped)
+    o.act = true;
+    o.dest = s.nowner ? s.nowner[node] : 0u;
+    // signatures are built from this rank's rows: only a locally owned node's rules a probe out
+    const bool may = subj == NONE || o.dest != s.shard_rank || sig_maybe(rsig, subj_sig(subj));
+    o.r = kg_frec{(s.shard_rank << Q_BITS) | i, node, subj, d | (may ? 0 : D_NOPROBE)};
+    if (o.dest == s.shard_rank && !s.relflags) {
+      // a locally owned root without a namespace program (as shard_child): checkDirect here, a
+      // record only if the root can expand
+      if (may && d >= 1 && subj != NONE && dset_probe(s, node, subj)) {
+        res[i] = KG_IS_MEMBER;
+        o.act = false;
+      } else if (rlen == 0 || d < 2) {
+        o.act = false;
+      } else {
+        o.r.depth = d | D_NOPROBE;
+      }
+    }
+  }
+  o.dsplit = d;
+  o.ssubj = subj;
+  // what the backward phase needs of a query that escalates: root, subject, depth
+  if (qinfo) qinfo[i] = make_uint4(node, subj, (uint32_t)d, o.act ? 1u : 0u);
+  return o;
+}
+
+// SEED_Q queries per thread: query (blockIdx * SEED_Q + j) * 256 + threadIdx (coalesced per j).
+constexpr int SEED_Q = 4;
 __global__ __launch_bounds__(256) void k_shard_seed(DevSnap s, const kg_query* __restrict__ q, uint32_t n,
                                                     int32_t global, kg_frec* out, uint64_t cap, uint32_t* counts,
                                                     uint8_t* res, uint32_t* err, const uint32_t* __restrict__ held,
                                                     uint32_t held_n, ShardFormula F, uint4* qinfo) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  bool act = false, split = false;
-  uint32_t dest = 0;
-  kg_frec r{};
-  kg_query x{};
-  int32_t dsplit = 0;
-  uint32_t ssubj = NONE;
-  if (i < n) {
-    if (F.ref) F.ref[i] = NONE;
-    x = q[i];
-    uint32_t node = NONE, rsig = 0xFFFFFFFFu, rlen = 0;
-    if (nmap_key_ok(x.t.ns, x.t.rel, x.t.obj)) {
-      const uint64_t key = nmap_key(x.t.ns, x.t.rel, x.t.obj);
-      const NSlot* sl = nmap_slot(s, key, hash_home(key, s.nmap_n));
-      if (sl) {
-        node = sl->node;
-        rsig = sl->sig;
-        rlen = sl->len;
-      }
-    }
-    uint32_t subj;
-    if (x.t.sns == KG_SUBJECT_ID) {
-      subj = x.t.sobj < 0x7FFFFFFFu ? x.t.sobj : NONE;
-    } else {
-      const uint32_t sn = nmap_find(s, x.t.sns, x.t.srel, x.t.sobj);
-      subj = sn == NONE ? NONE : (SET_BIT | sn);
-    }
-    int32_t d = x.max_depth;
-    if (d <= 0 || global < d) d = global;  // engine.go:68-70
-    res[i] = KG_NOT_MEMBER;
-    err[i] = KG_ERR_NONE;
-    const uint8_t rf = relflag(s, x.t.ns, x.t.rel);
-    const uint32_t pr = (x.t.ns < s.n_ns && x.t.rel < s.n_rel) ? x.t.ns * s.n_rel + x.t.rel : NONE;
-    const bool virt = F.virt && pr != NONE && F.virt[pr];
-    bool bad = node != NONE ? node_bad(s, node) : (rf != 0 && !virt);  // a union without a node: NotMember
-    if (bad && F.fidx && pr != NONE && F.fidx[pr] >= 0) {  // a formula over plain / union leaves: split
-      const FPlan& P = F.plans[F.fidx[pr]];
-      bool ok = true;
-      for (uint32_t j = 0; j < P.n_leaves; j++) {
-        const uint32_t ln = nmap_find(s, x.t.ns, P.leaf[j], x.t.obj);
-        if (ln != NONE && node_bad(s, ln)) ok = false;
-      }
-      if (ok) {
-        F.ref[i] = (uint32_t)F.fidx[pr];
-        split = true;
-        bad = false;
-      }
-    }
-    if (bad) {  // the interpreter's territory: not evaluated across shards
-      err[i] = KG_ERR_NOT_IMPLEMENTED;
-    } else if (split) {
-      // records below, one per part
-    } else if (held && !s.relflags && x.t.sns == KG_SUBJECT_ID &&
-               (subj == NONE || subj >= held_n || !((held[subj >> 5] >> (subj & 31)) & 1u))) {
-      // no row of any rank holds the subject: checkDirect can never hit (NotMember)
-    } else if (node != NONE && (subj != NONE || s.relflags)) {
-      // an unknown subject can never be held, but with a namespace program the query can still
-      // reach a rewrite (an error), so it is seeded all the same (its probes are skipped)
-      act = true;
-      dest = s.nowner ? s.nowner[node] : 0u;
-      // signatures are built from this rank's rows: only a locally owned node's rules a probe out
-      const bool may = subj == NONE || dest != s.shard_rank || sig_maybe(rsig, subj_sig(subj));
-      r = kg_frec{(s.shard_rank << Q_BITS) | i, node, subj, d | (may ? 0 : D_NOPROBE)};
-      if (dest == s.shard_rank && !s.relflags) {
-        // a locally owned root without a namespace program (as shard_child): checkDirect here, a
-        // record only if the root can expand
-        if (may && d >= 1 && subj != NONE && dset_probe(s, node, subj)) {
-          res[i] = KG_IS_MEMBER;
-          act = false;
-        } else if (rlen == 0 || d < 2) {
-          act = false;
-        } else {
-          r.depth = d | D_NOPROBE;
-        }
-      }
-    }
-    dsplit = d;
-    ssubj = subj;
-    // what the backward phase needs of a query that escalates: root, subject, depth
-    if (qinfo) qinfo[i] = make_uint4(node, subj, (uint32_t)d, act ? 1u : 0u);
+  bool act[SEED_Q];
+  uint32_t dest[SEED_Q];
+  kg_frec rec[SEED_Q];
+  SeedQ sq[SEED_Q];
+#pragma unroll
+  for (int j = 0; j < SEED_Q; j++) {
+    const uint32_t i = (blockIdx.x * SEED_Q + j) * blockDim.x + threadIdx.x;
+    sq[j] = seed_query(s, q, i, n, global, res, err, held, held_n, F, qinfo);
+    act[j] = sq[j].act;
+    dest[j] = sq[j].dest;
+    rec[j] = sq[j].r;
   }
-  emit(act, dest, r, out, cap, counts, s.shard_n);
+  emit_q<SEED_Q>(act, dest, rec, out, cap, counts, s.shard_n);
   // split queries: the own part (slot 0, the node's rows as a plain node) and every leaf (slot 1 + j),
   // each the checkIsAllowed of its node at the query's depth; a part without a node is NotMember
-  for (uint32_t k = 0; F.fidx && k < F.k; k++) {  // uniform trip count: emit needs every thread
-    bool pa = false;
-    uint32_t pd = 0;
-    kg_frec pr{};
-    if (split && (ssubj != NONE || s.relflags)) {
-      const FPlan& P = F.plans[F.ref[i]];
-      uint32_t pn = NONE;
-      if (k == 0) pn = nmap_find(s, x.t.ns, x.t.rel, x.t.obj);
-      else if (k - 1 < P.n_leaves) pn = nmap_find(s, x.t.ns, P.leaf[k - 1], x.t.obj);
-      if (pn != NONE) {
-        pa = true;
-        pd = s.nowner ? s.nowner[pn] : 0u;
-        const uint32_t slot = n + i * F.k + k;
-        pr = kg_frec{(s.shard_rank << Q_BITS) | slot, pn, ssubj, dsplit | (k == 0 ? D_OWN : 0)};
+  if (!F.fidx) return;  // uniform over the grid
+  for (int j = 0; j < SEED_Q; j++) {
+    const uint32_t i = (blockIdx.x * SEED_Q + j) * blockDim.x + threadIdx.x;
+    const SeedQ& o = sq[j];
+    for (uint32_t k = 0; k < F.k; k++) {  // uniform trip count: emit needs every thread
+      bool pa = false;
+      uint32_t pd = 0;
+      kg_frec pr{};
+      if (o.split && (o.ssubj != NONE || s.relflags)) {
+        const FPlan& P = F.plans[F.ref[i]];
+        uint32_t pn = NONE;
+        if (k == 0) pn = nmap_find(s, o.x.t.ns, o.x.t.rel, o.x.t.obj);
+        else if (k - 1 < P.n_leaves) pn = nmap_find(s, o.x.t.ns, P.leaf[k - 1], o.x.t.obj);
+        if (pn != NONE) {
+          pa = true;
+          pd = s.nowner ? s.nowner[pn] : 0u;
+          const uint32_t slot = n + i * F.k + k;
+          pr = kg_frec{(s.shard_rank << Q_BITS) | slot, pn, o.ssubj, o.dsplit | (k == 0 ? D_OWN : 0)};
+        }
       }
+      emit(pa, pd, pr, out, cap, counts, s.shard_n);
     }
-    emit(pa, pd, pr, out, cap, counts, s.shard_n);
   }
 }
 
@@ -918,7 +993,8 @@ int shard_seed(Snapshot* s, const kg_query* d_q, size_t n, int32_t gdepth, kg_fr
   if (n) {
     const uint32_t* held = s->shard_held ? s->shard_held : s->ds.hbits;
     const uint32_t held_n = s->shard_held ? s->shard_held_n : s->ds.hbits_n;
-    hipLaunchKernelGGL(k_shard_seed, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, stream, s->ds, d_q, (uint32_t)n,
+    hipLaunchKernelGGL(k_shard_seed, dim3((uint32_t)((n + 256 * SEED_Q - 1) / (256 * SEED_Q))), dim3(256), 0, stream,
+                       s->ds, d_q, (uint32_t)n,
                        gdepth, d_out, (uint64_t)cap, d_counts, d_res, d_err,
                        (s->shard_n == 1 || s->shard_held) ? held : nullptr, held_n, F, qinfo);
     HIPC(hipGetLastError());
@@ -939,7 +1015,7 @@ int shard_level(Snapshot* s, const kg_frec* d_in, size_t n_in, const uint32_t* d
   if (n_in) {
     const HeavyList heavy = heavy_list(c);
     HIPC(hipMemsetAsync(heavy.pk, 0, 8, stream));
-    const uint32_t grid = (uint32_t)std::min<uint64_t>((n_in + 255) / 256, (uint64_t)s->n_cu * 8);
+    const uint32_t grid = (uint32_t)std::min<uint64_t>((n_in + 255) / 256, (uint64_t)s->n_cu * s->shard_wgs);
     hipLaunchKernelGGL(k_shard_level, dim3(grid), dim3(256), 0, stream, s->ds, d_in, (uint64_t)n_in, d_n_in, d_out,
                        (uint64_t)cap, d_counts, d_res, d_err, (uint64_t*)c->vis, c->vis_slots - 1,
                        d_done, d_done ? done_words : 0u, heavy, (uint32_t*)c->qcnt,
@@ -976,7 +1052,7 @@ int shard_levels(Snapshot* s, int levels, kg_frec* d_buf[2], size_t cap, uint32_
   const HeavyList heavy = heavy_list(c);
   const uint32_t esc = esc_mode == 1 ? ESC_BIT : (esc_mode == 2 ? ESC2_BIT : 0u);
   const uint32_t budget = shard_escalates(s) && c->qcnt && !c->final ? s->shard_budget : 0u;
-  const uint32_t grid = (uint32_t)std::min<uint64_t>((cap + 255) / 256, (uint64_t)s->n_cu * 8);
+  const uint32_t grid = (uint32_t)std::min<uint64_t>((cap + 255) / 256, (uint64_t)s->n_cu * s->shard_wgs);
   // the levels' records go to SUB per-XCD segments of one buffer, each with its own counter (emit's
   // sub mode): level 0 reads the seed's bucket, every later level the SUB segments of the one before
   const uint32_t SUB = cap >= 8 * 256 ? 8u : 1u;
@@ -1069,7 +1145,7 @@ int shard_back_seed(Snapshot* s, const kg_frec* d_list, size_t m, const uint32_t
   if (!stream) stream = s->stream;
   HIPC(hipMemsetAsync(d_counts, 0, 8, stream));
   if (m && s->ds.radj) {
-    const uint32_t grid = (uint32_t)std::min<uint64_t>((m + 255) / 256, (uint64_t)s->n_cu * 8);
+    const uint32_t grid = (uint32_t)std::min<uint64_t>((m + 255) / 256, (uint64_t)s->n_cu * s->shard_wgs);
     hipLaunchKernelGGL(k_shard_back_seed, dim3(grid), dim3(256), 0, stream, s->ds, d_list, (uint64_t)m, d_m, d_out,
                        (uint64_t)cap, d_counts);
     HIPC(hipGetLastError());
@@ -1089,7 +1165,7 @@ int shard_back_level(Snapshot* s, const kg_frec* d_in, size_t n_in, const uint32
   if (n_in && s->ds.radj) {
     const HeavyList heavy = heavy_list(c);
     HIPC(hipMemsetAsync(heavy.pk, 0, 8, stream));
-    const uint32_t grid = (uint32_t)std::min<uint64_t>((n_in + 255) / 256, (uint64_t)s->n_cu * 8);
+    const uint32_t grid = (uint32_t)std::min<uint64_t>((n_in + 255) / 256, (uint64_t)s->n_cu * s->shard_wgs);
     hipLaunchKernelGGL(k_shard_back_level, dim3(grid), dim3(256), 0, stream, s->ds, d_in, (uint64_t)n_in, d_n_in, d_out,
                        (uint64_t)cap, d_counts, d_res, d_err, (uint64_t*)c->vis, c->vis_slots - 1, d_done,
                        d_done ? done_words : 0u, heavy, (uint32_t*)c->qcnt,

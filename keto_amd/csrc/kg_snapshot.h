@@ -224,6 +224,7 @@ struct Snapshot {
   uint32_t* shard_held = nullptr;  // holder bitmap OR-ed over every rank (kg_shard_held), or null
   uint32_t shard_held_n = 0;
   int shard_vis_log2 = 23;
+  uint32_t shard_wgs = 8;  // kg_snapshot_tune("shard_wgs"): k_shard_level workgroups per CU
   uint32_t shard_heavy = 64;  // kg_snapshot_tune("shard_heavy"): set rows longer than this go to k_shard_heavy (r3p A/B)
   int shard_vis_mode = 0;  // kg_snapshot_tune("shard_vis_mode"): (query, node) dedup 0 = exact CAS table, 1 = lossy cache
   uint32_t shard_budget = 0;       // kg_snapshot_tune("shard_budget"): forward set edges per query and rank (0 = off)
