@@ -40,7 +40,7 @@ STREAM_KERNELS = {0: "k_stream<8,7,256,16>", 1: "k_stream<16,6,256,32>", 2: "k_s
                   6: "k_stream<32,wave1024/256,320,64>", 7: "k_stream<32,wave1024/64,256,64>",
                   8: "k_stream<32,wave512/64,256,64>", 9: "k_stream2<9,256,64,64,1>",
                   10: "k_stream3<9,256,64,64>", 11: "k_stream2<9,256,64,64,2>", 12: "k_stream2<9,256,64,0,1>", 13: "k_stream3<9,256,64,0>", 14: "k_stream2<9,256,64,0,2>",
-                  15: "k_stream4<9,256>"}
+                  15: "k_stream4<9,256>", 16: "k_stream5<9,128>"}
 
 
 def parse(argv=None):

@@ -418,7 +418,7 @@ static int tune_one(Snapshot* s, const char* key, int64_t value) {
     return 0;
   }
   if (strcmp(key, "stream") == 0) {
-    if (value < 0 || value > 15) return set_error(-2, "stream must be in [0, 15]");
+    if (value < 0 || value > 16) return set_error(-2, "stream must be in [0, 16]");
     s->stream_variant = (int)value;
     return 0;
   }

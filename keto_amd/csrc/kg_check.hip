@@ -1389,6 +1389,278 @@ __global__ __launch_bounds__(256) void k_stream4(DevSnap s, LqList wl, uint32_t*
   block_stats<7>(ctl, idx, v);
 }
 
+// ------------------------------------------------------------------ k_stream5 (variant 16)
+// k_stream4 with two independent FIFO engines per wave, interleaved: engine e owns slots
+// [16e, 16e + 16) and its own ring of QE entries.  Each half-iteration refills and windows one
+// engine and issues its gathers and probes, then processes the OTHER engine's step, whose loads were
+// issued a half-iteration earlier -- so one engine's LDS / VALU bookkeeping runs under the other's
+// memory round trip, and a wave has up to two steps' loads in flight instead of one.  Per engine the
+// step is k_stream4's exactly (window of up to 64 edges from the ring head, children appended in
+// order, probes one step after discovery, blind-write visited cache keyed by slot + generation --
+// shared by both engines, slot ids are distinct), so per query the FIFO is BFS order.
+template <int VLOG2, int QE>
+struct Stream5Lds {
+  unsigned long long vt[1 << VLOG2];
+  uint32_t e_beg[2][QE], e_meta[2][QE];
+  uint32_t pref[65];
+  uint32_t s_state[32], s_qi[32], s_subj[32], s_sig[32], s_last[32], s_edg[32];
+  uint32_t s_node[32], s_depth[32], s_beg[32], s_len[32];
+};
+
+template <int VLOG2, int QE>
+__global__ __launch_bounds__(256) void k_stream5(DevSnap s, LqList wl, uint32_t* heads, uint8_t* __restrict__ out,
+                                                 RQuery* __restrict__ rq, uint32_t* next_list, uint32_t* next_count,
+                                                 Ctl* ctl, uint32_t ecap, uint32_t chunk, uint32_t ranges) {
+  using Lds = Stream5Lds<VLOG2, QE>;
+  constexpr uint32_t WIN = 64u;
+  constexpr uint32_t VT = 1u << VLOG2;
+  static_assert(QE <= 256 && (QE & (QE - 1)) == 0, "ring of <= 256 entries (9-bit generations stay unique)");
+  const uint64_t t_start = wall_clock64();
+  __shared__ Lds lds_all[4];
+  Lds& L = lds_all[threadIdx.x >> 6];
+  const int lane = lane_id();
+  const uint32_t head0 = blockIdx.x & 7;  // XCD label (the launch keeps grid >= 8)
+  uint32_t head_sel = head0;
+  for (uint32_t i = lane; i < VT; i += 64) L.vt[i] = 0ull;
+  if (lane < 32) {
+    L.s_state[lane] = 0;
+    L.s_last[lane] = 0;
+    L.s_edg[lane] = 0;
+  }
+  if (lane == 0) L.pref[WIN] = 0;
+  const uint32_t shard_n = lane < 8 ? wl.counts[lane * 32] : 0u;
+  __builtin_amdgcn_wave_barrier();
+  uint32_t active = 0;  // wave-uniform: slots holding a query (engine e: bits [16e, 16e + 16))
+  uint32_t pf = 0, tk = 0, st_got = 0;
+  bool exhausted = false;
+  LQuery sq{};
+  uint32_t c_left = 0, c_pos = 0;
+  LQuery cq{};
+  // per engine (index a compile-time constant after unrolling: registers)
+  uint32_t head[2] = {0, 0}, tail[2] = {0, 0}, head_off[2] = {0, 0};
+  bool pend[2] = {false, false};
+  uint32_t pend_node[2] = {0, 0}, pend_slot[2] = {0, 0}, pend_gen[2] = {0, 0};
+  // a step's issued loads and what processing them needs
+  AdjX xs[2];
+  ulonglong2 pbs[2];
+  bool act_s[2] = {false, false}, pvalid_s[2] = {false, false};
+  uint32_t om_s[2] = {0, 0}, ssig_s[2] = {0, 0}, pnode_s[2] = {0, 0}, pslot_s[2] = {0, 0};
+  uint64_t pkey_s[2] = {0, 0};
+  unsigned long long st_rows = 0, st_edges = 0, st_probes = 0, st_done = 0, st_steps = 0;
+  for (;;) {
+    // ---- the staged chunk becomes the current one; the dequeue pipeline advances (as k_stream4)
+    if (c_left == 0 && pf == 2) {
+      cq = sq;
+      c_left = st_got;
+      c_pos = 0;
+      pf = 0;
+    }
+    if (pf == 1) {
+      const uint32_t k = (uint32_t)__builtin_amdgcn_readfirstlane((int)tk);
+      const uint32_t h = head_sel & 7;
+      const uint32_t lo = h * wl.cap, hi = lo + (uint32_t)__builtin_amdgcn_readlane((int)shard_n, (int)h);
+      if (lo + k < hi) {
+        st_got = min(chunk, hi - (lo + k));
+        if ((uint32_t)lane < st_got) sq = wl.list[lo + k + lane];
+        pf = 2;
+      } else {
+        pf = 0;
+        if (++head_sel >= head0 + ranges) exhausted = true;
+      }
+    }
+    if (pf == 0 && !exhausted) {
+      if (lane == 0) tk = atomicAdd(&heads[(head_sel & 7) * 32], chunk);
+      pf = 1;
+    }
+    if (active == 0 && exhausted && pf == 0 && c_left == 0 &&
+        !__ballot(act_s[0] || act_s[1] || pvalid_s[0] || pvalid_s[1] || pend[0] || pend[1]))
+      break;  // every wave reaches this: no slot, no step in flight, nothing left to dequeue
+#pragma unroll
+    for (int e = 0; e < 2; e++) {
+      const uint32_t emask = 0xFFFFu << (16 * e);
+      // ---- refill engine e's free slots (their root entries need ring room)
+      {
+        const uint32_t freem = ~active & emask;
+        const uint32_t got = min((uint32_t)__popc(freem), c_left);
+        if (got && (tail[e] - head[e]) + got <= QE) {
+          const uint32_t r = __popc(freem & (lane < 32 ? (1u << lane) - 1u : 0xFFFFFFFFu));
+          const bool mine = lane < 32 && ((freem >> (lane & 31)) & 1u) && r < got;
+          const int src = mine ? (int)(c_pos + r) : lane;
+          const uint32_t qi = __shfl(cq.qi, src, 64), qnode = __shfl(cq.node, src, 64),
+                         qsubj = __shfl(cq.subj, src, 64), qbeg = __shfl(cq.beg, src, 64),
+                         qlen = __shfl(cq.len, src, 64);
+          const int32_t qdepth = __shfl(cq.depth, src, 64);
+          c_pos += got;
+          c_left -= got;
+          if (mine) {
+            const uint32_t slot = lane, gen = L.s_state[slot] & S2_GEN;
+            const bool over = qdepth > (int32_t)S2_DMAX || qlen > S2_LONG || qlen > ecap;
+            const uint32_t at = tail[e] + r;
+            L.s_qi[slot] = qi;
+            L.s_subj[slot] = qsubj;
+            L.s_sig[slot] = subj_sig(qsubj);
+            L.s_node[slot] = qnode;
+            L.s_depth[slot] = (uint32_t)qdepth;
+            L.s_beg[slot] = qbeg;
+            L.s_len[slot] = qlen;
+            L.s_edg[slot] = qlen;
+            L.s_last[slot] = at;
+            L.s_state[slot] = over ? (gen | S2_OVER) : gen;
+            const unsigned long long key =
+                (1ull << 63) | ((unsigned long long)gen << 37) | ((unsigned long long)slot << 32) | qnode;
+            L.vt[((qnode * 0x9E3779B1u) ^ (slot * 0x85EBCA77u) ^ (gen * 0xC2B2AE3Du)) >> (32 - VLOG2)] = key;
+            L.e_beg[e][at & (QE - 1)] = qbeg;
+            L.e_meta[e][at & (QE - 1)] = s2_meta(over ? 0u : qlen, slot, gen, over ? 2u : (uint32_t)qdepth);
+          }
+          active |= (uint32_t)__ballot(mine);
+          tail[e] += got;
+        }
+      }
+      if ((active & emask) == 0) {  // nothing holds engine e's ring: whatever is left in it is stale
+        head[e] = tail[e];
+        head_off[e] = 0;
+      }
+      __builtin_amdgcn_wave_barrier();
+      // ---- engine e: window from its ring head, then this step's gathers and the previous step's
+      // probes, issued (not waited for: engine e^1's processing below runs under them)
+      {
+        const uint32_t avail = tail[e] - head[e];
+        const uint32_t at0 = (head[e] + lane) & (QE - 1);
+        uint32_t emeta = L.e_meta[e][at0], ebeg = L.e_beg[e][at0];
+        const uint32_t sl0 = (emeta >> 11) & 31u;
+        const uint32_t st0 = L.s_state[sl0];
+        const uint32_t pst = L.s_state[pend_slot[e]], psubj = L.s_subj[pend_slot[e]];
+        const bool inwin = (uint32_t)lane < avail;
+        const bool live = inwin && ((active >> sl0) & 1u) && (st0 == ((emeta >> 16) & S2_GEN));
+        uint32_t elen = live ? (emeta & 0x7FFu) : 0u;
+        if (lane == 0) {
+          ebeg += head_off[e];
+          elen = live ? elen - head_off[e] : 0u;
+        }
+        if (!inwin) emeta = 0;
+        const bool pvalid = pend[e] && pst == pend_gen[e];
+        const uint64_t pkey = dset_key(pend_node[e], psubj);
+        uint32_t total;
+        const uint32_t excl = wave_excl_scan(elen, &total);
+        L.pref[lane] = 0;
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t taken = min(total, WIN);
+        L.pref[(elen > 0 && excl < taken) ? excl : WIN] = (uint32_t)lane + 1;
+        const bool consumed = (uint32_t)lane < avail && excl + elen <= taken;
+        const uint32_t ncons = __popcll(__ballot(consumed));
+        st_rows += (consumed && live) ? 1u : 0u;
+        {
+          const uint32_t ex_n = (uint32_t)__builtin_amdgcn_readlane((int)excl, ncons & 63);
+          if (ncons < avail && ncons < 64 && ex_n < taken) head_off[e] = (ncons == 0 ? head_off[e] : 0u) + (taken - ex_n);
+          else if (ncons > 0) head_off[e] = 0;
+        }
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t m = wave_incl_scan<DppMax>(L.pref[lane]);
+        const int own = ((int)m - 1) & 63;
+        const uint32_t ob = __shfl(ebeg, own, 64);
+        const uint32_t om = __shfl(emeta, own, 64);
+        const uint32_t ox = __shfl(excl, own, 64);
+        const bool act = (uint32_t)lane < taken;
+        xs[e] = s.adjx[act ? ob + ((uint32_t)lane - ox) : 0u];  // adjx[0] exists
+        pbs[e] = *reinterpret_cast<const ulonglong2*>(s.dset + (pvalid ? hash_home(pkey, s.dset_nb) : 0ull) * DSET_BUCKET);
+        act_s[e] = act;
+        pvalid_s[e] = pvalid;
+        om_s[e] = om;
+        ssig_s[e] = L.s_sig[(om >> 11) & 31u];
+        pkey_s[e] = pkey;
+        pnode_s[e] = pend_node[e];
+        pslot_s[e] = pend_slot[e];
+        pend[e] = false;  // the probes now in flight are this step's; processing sets the next ones
+        head[e] += ncons;
+        st_edges += (lane == 0) ? taken : 0u;
+        st_steps += (lane == 0 && total) ? 1u : 0u;
+      }
+      __builtin_amdgcn_wave_barrier();
+      // ---- engine f = e^1: its step's loads (issued a half-iteration ago) are processed
+      {
+        const int f = 1 - e;
+        const AdjX x = xs[f];
+        const ulonglong2 pb = pbs[f];
+        const bool act = act_s[f], pvalid = pvalid_s[f];
+        const uint32_t om = om_s[f], ssig = ssig_s[f];
+        const uint64_t pkey = pkey_s[f];
+        const uint32_t slot = (om >> 11) & 31u, d = om >> 25, g = (om >> 16) & S2_GEN;
+        bool hit = pvalid && (pb.x == pkey || pb.y == pkey);
+        {
+          const bool more = pvalid && !hit && pb.y != EMPTY64;
+          if (__ballot(more)) {
+            if (more) hit = dset_probe(s, pnode_s[f], (uint32_t)pkey);
+          }
+        }
+        st_probes += pvalid ? 1u : 0u;
+        const bool keepc = act && d >= 3 && x.len > 0;
+        const bool longrow = keepc && x.len > S2_LONG;
+        const unsigned long long key =
+            (1ull << 63) | ((unsigned long long)g << 37) | ((unsigned long long)slot << 32) | x.node;
+        const uint32_t hv = ((x.node * 0x9E3779B1u) ^ (slot * 0x85EBCA77u) ^ (g * 0xC2B2AE3Du)) >> (32 - VLOG2);
+        // (engine f's slots cannot change between its issue and this processing: the other engine's
+        // half touches only its own slots, and a refill only free ones)
+        const unsigned long long old = keepc ? L.vt[hv] : 0ull;
+        const bool fresh = keepc && !longrow && old != key;
+        if (fresh) L.vt[hv] = key;
+        const uint64_t am = __ballot(fresh);
+        const uint32_t room = QE - (tail[f] - head[f]);
+        const uint32_t pos = __popcll(am & ((1ull << lane) - 1));
+        const bool appended = fresh && pos < room;
+        if (appended) {
+          const uint32_t at = tail[f] + pos;
+          L.e_beg[f][at & (QE - 1)] = x.begin;
+          L.e_meta[f][at & (QE - 1)] = x.len | (om & 0x01FFF800u) | ((d - 1) << 25);
+          atomicMax(&L.s_last[slot], at);
+          atomicAdd(&L.s_edg[slot], x.len);
+        }
+        if (longrow || (fresh && !appended)) atomicOr(&L.s_state[slot], S2_OVER);
+        tail[f] += min((uint32_t)__popcll(am), room);
+        if (hit) atomicOr(&L.s_state[pslot_s[f]], S2_HIT);
+        pend[f] = act && (keepc ? appended : true) && sig_maybe(x.sig, ssig);
+        pend_node[f] = x.node;
+        pend_slot[f] = slot;
+        pend_gen[f] = g;
+        act_s[f] = false;
+        pvalid_s[f] = false;
+        const uint32_t pslots = wave_or(pend[f] ? 1u << slot : 0u);
+        __builtin_amdgcn_wave_barrier();
+        // finished queries of engine f
+        bool done = false;
+        const uint32_t fmask = 0xFFFFu << (16 * f);
+        if (lane < 32 && ((fmask >> lane) & 1u) && ((active >> lane) & 1u)) {
+          const uint32_t st = L.s_state[lane];
+          const uint32_t last = L.s_last[lane], edg = L.s_edg[lane];
+          const uint32_t qi = L.s_qi[lane];
+          if (st & S2_HIT) {
+            done = true;
+            out[qi] = KG_IS_MEMBER;  // NotMember was pre-written by k_resolve
+            st_done++;
+          } else if ((st & S2_OVER) || (ecap != 0xFFFFFFFFu && edg > ecap)) {
+            done = true;
+            rq[qi] = RQuery{L.s_node[lane], L.s_subj[lane], (int32_t)L.s_depth[lane], ROUTE_LIGHT, L.s_beg[lane],
+                            L.s_len[lane]};
+            next_list[atomicAdd(next_count, 1u)] = qi;
+          } else if ((int32_t)(last - head[f]) < 0 && !((pslots >> lane) & 1u)) {
+            done = true;  // every entry consumed, no probe pending: NotMember (pre-written)
+            st_done++;
+          }
+          if (done) L.s_state[lane] = ((st & S2_GEN) + 1u) & S2_GEN;
+        }
+        const uint32_t freed = (uint32_t)__ballot(done);
+        active &= ~freed;
+        if (pend[f] && ((freed >> pend_slot[f]) & 1u)) pend[f] = false;
+        __builtin_amdgcn_wave_barrier();
+      }
+    }
+  }
+  const unsigned long long t_end = wall_clock64(), life = lane == 0 ? t_end - t_start : 0ull;
+  block_max3(ctl, ~(unsigned long long)t_start, t_end, t_end - t_start);
+  const int idx[7] = {ST_LROWS, ST_LEDGES, ST_LPROBES, ST_LIGHT, ST_LSTEPS, ST_LWAVES, ST_LTICKS};
+  const unsigned long long v[7] = {st_rows, st_edges, st_probes, st_done, st_steps, lane == 0 ? 1ull : 0ull, life};
+  block_stats<7>(ctl, idx, v);
+}
+
 // ------------------------------------------------------------------ k_stream3 (variant 10)
 // k_stream2 software-pipelined by one step.  k_stream2's step is: take a window of 64 edges at the
 // FIFO head -> gather their adjx records (and probe the previous step's children) -> wait -> process
@@ -2220,7 +2492,7 @@ int check_batch_begin(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n, 
     // appends of k_resolve's blocks h, h + 8, ... (<= 256 each).  They live in the light list's
     // space (8 n u32 >= (n + 2048) LQuery for the >= 64 Ki queries the scratch is sized for).
     const uint32_t nblk = (uint32_t)((n + 255) / 256);
-    const bool compact = s->light_tier != 1 && s->stream_variant == 15;
+    const bool compact = s->light_tier != 1 && (s->stream_variant == 15 || s->stream_variant == 16);
     const uint32_t lq_cap = (nblk + 7) / 8 * 256;
     LQuery* lq = compact ? reinterpret_cast<LQuery*>(light) : nullptr;
     if (compact && (size_t)8 * lq_cap * sizeof(LQuery) > (size_t)8 * w->scratch_n * 4)
@@ -2294,6 +2566,10 @@ int check_batch_begin(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n, 
                            d_out, ovf_list, ovf_count, ctl, ecap, std::max<uint32_t>(1u, std::min<uint32_t>(s->stream_chunk, 64u)), s->stream_steal);
       else if (sv == 15)  // pipelined dequeue of LQuery records, no returning LDS atomics
         hipLaunchKernelGGL((k_stream4<9, 256>), dim3(grid), dim3(256), 0, stream, s->ds, LqList{lq, ctl->light8, lq_cap},
+                           ctl->heads, d_out, rq, ovf_list, ovf_count, ctl, ecap,
+                           std::max<uint32_t>(1u, std::min<uint32_t>(s->stream_chunk, S4_CHUNK)), s->stream_steal);
+      else if (sv == 16)  // two interleaved FIFO engines per wave
+        hipLaunchKernelGGL((k_stream5<9, 128>), dim3(grid), dim3(256), 0, stream, s->ds, LqList{lq, ctl->light8, lq_cap},
                            ctl->heads, d_out, rq, ovf_list, ovf_count, ctl, ecap,
                            std::max<uint32_t>(1u, std::min<uint32_t>(s->stream_chunk, S4_CHUNK)), s->stream_steal);
       else if (sv == 10)

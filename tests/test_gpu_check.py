@@ -52,7 +52,7 @@ def random_queries(rng, nss, rels, n, n_obj=60, n_users=40, p_setq=0.15):
     return qs
 
 
-@pytest.mark.parametrize("seed", range(25))
+@pytest.mark.parametrize("seed", range(30))
 def test_random_graphs_vs_oracle(seed):
     rng = np.random.default_rng(seed)
     it, tuples, nss, rels = random_graph(rng, n_obj=40 + 20 * (seed % 6), n_rows=200 + 150 * (seed % 6))
@@ -64,14 +64,16 @@ def test_random_graphs_vs_oracle(seed):
     # seed 17 with a tiny edge budget, seed 18 dequeuing one query at a time)
     reg.snapshot.tune("light", 1 if seed == 7 else 0)
     # k_stream3 without the node cap (seeds 19-20, seed 20 with a tiny edge budget)
-    # k_stream4 (seeds 21-24: chunks of 16 / 1 / 64, a tiny edge budget, one or eight steal ranges)
+    # k_stream4 (seeds 21-24: chunks of 16 / 1 / 64, a tiny edge budget, one or eight steal ranges),
+    # k_stream5 (seeds 25-29: the same knobs over two interleaved engines per wave)
     reg.snapshot.tune("stream", seed % 7 if seed < 7 else (seed - 1 if seed < 10 else (9 if seed < 13 else
                                                                                       (10 if seed < 16 else
                                                                                        (11 if seed < 19 else
-                                                                                        (13 if seed < 21 else 15))))))
-    reg.snapshot.tune("stream_ecap", 6 if seed in (2, 17, 20, 22) else 0)
-    reg.snapshot.tune("stream_chunk", 1 if seed in (18, 22) else (16 if seed in (21, 24) else 64))
-    reg.snapshot.tune("stream_steal", 1 if seed in (11, 18, 23) else (8 if seed in (12, 24) else 4))
+                                                                                        (13 if seed < 21 else
+                                                                                         (15 if seed < 25 else 16)))))))
+    reg.snapshot.tune("stream_ecap", 6 if seed in (2, 17, 20, 22, 27) else 0)
+    reg.snapshot.tune("stream_chunk", 1 if seed in (18, 22, 26) else (16 if seed in (21, 24, 29) else 64))
+    reg.snapshot.tune("stream_steal", 1 if seed in (11, 18, 23, 28) else (8 if seed in (12, 24, 29) else 4))
     qs = random_queries(rng, nss, rels, 3000, n_obj=40 + 20 * (seed % 6))
     depths = rng.integers(-1, 9, len(qs))
     q6 = np.asarray([it.tuple_ids(t) for t in qs], np.uint32)
@@ -89,7 +91,7 @@ def test_random_graphs_vs_oracle(seed):
         assert (out[inv] == dfs[inv]).all()
 
 
-@pytest.mark.parametrize("variant", [8, 9, 10, 11, 12, 13, 14, 15])
+@pytest.mark.parametrize("variant", [8, 9, 10, 11, 12, 13, 14, 15, 16])
 def test_stream_tier_long_rows_and_dense_cycles(variant):
     """Rows longer than a FIFO entry holds (k_stream2: 2047 edges), dense cycles (the direct-mapped
     visited cache evicts and re-expands), many queries per wave on one hub: exact vs the oracle."""
@@ -203,7 +205,8 @@ def _torch():
                                                            (300_000, 10, 11, 1), (300_000, 10, 9, 0),
                                                            (300_000, 10, 12, 1), (300_000, 10, 13, 1),
                                                            (300_000, 10, 14, 1), (300_000, 10, 15, 1),
-                                                           (300_000, 5, 15, 0)])
+                                                           (300_000, 5, 15, 0), (300_000, 10, 16, 1),
+                                                           (200_000, 5, 16, 0)])
 def test_synthetic_graph_vs_oracle(n_tuples, gmax, variant, unheld):
     torch = _torch()
     from keto_amd import _lib
