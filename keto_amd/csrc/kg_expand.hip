@@ -771,8 +771,12 @@ int expand_batch(Snapshot* s, hipStream_t stream, void** bufs, const kg_set* roo
     out->nodes = (kg_tree_node*)tree_pool_get(total * sizeof(kg_tree_node));
     out->pinned = 1;
     if (!out->nodes) rc = set_error(-4, "pinned host allocation failed");
-    if (!rc && (e = grow(&B.dst, B.dst_cap, std::max<size_t>(total, 2 * B.dst_cap / sizeof(kg_tree_node)) *
-                                                     sizeof(kg_tree_node))) != hipSuccess)
+    // grown only when this call's records do not fit, then to twice the old size at least (a request
+    // of "twice the capacity" on every call doubled the buffer per call: a long-lived lane ran the
+    // device out of memory)
+    const size_t dst_need = total * sizeof(kg_tree_node);
+    if (!rc && dst_need > B.dst_cap &&
+        (e = grow(&B.dst, B.dst_cap, std::max<size_t>(dst_need, 2 * B.dst_cap))) != hipSuccess)
       fail("hipMalloc", e);
     if (!rc && (e = grow(&B.d_off, B.off_cap, (n + 1) * 8)) != hipSuccess) fail("hipMalloc", e);
     if (!rc && (e = hipMemcpyAsync(B.d_off, out->root_off, (n + 1) * 8, hipMemcpyHostToDevice, stream)) != hipSuccess)

@@ -124,3 +124,26 @@ def test_c5_hot_group_roots_vs_oracle(n_tuples, gmax):
         _cmp_records(exp, g, (r.tolist(), gmax))
         big += g is not None and len(g) > 512
     assert big > 0  # some trees outgrow the LDS pass (the hash / bitmap passes are exercised)
+
+
+def test_expand_lane_memory_stays_flat():
+    """A long-lived caller's lane keeps its device buffers, grown only when a call's output does not
+    fit: 16 calls of the same batch on one thread allocate nothing after the first (the compacted-
+    output buffer used to double on every call until hipMalloc failed, seen at C5 scale)."""
+    import torch
+    from keto_amd.engine import Snapshot
+    from keto_amd.synth import hot_group_roots
+    snap = Snapshot.synthetic(300_000, seed=20250131)
+    roots = hot_group_roots(snap.synth_ids(), 2000)
+    ex = ExpandEngine(snap)
+    ex.config.max_read_depth = 5
+    first = ex.build_trees_ids(roots)
+    ex.build_trees_ids(roots)
+    torch.cuda.synchronize()
+    free0 = torch.cuda.mem_get_info(0)[0]
+    for _ in range(14):
+        again = ex.build_trees_ids(roots)
+    torch.cuda.synchronize()
+    free1 = torch.cuda.mem_get_info(0)[0]
+    assert free0 - free1 < (64 << 20), (free0, free1)
+    assert all((a is None and b is None) or (a == b).all() for a, b in zip(first, again))
