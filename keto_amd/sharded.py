@@ -616,10 +616,11 @@ class ShardedChecker:
             fl = 0
             for k in range(0, len(h), 2):
                 fl |= int(h[k])
-                if int(h[k + 1]) != 0:
-                    raise _lib.KetoGPUError("sharded batch: records left after %d levels" % gdepth)
-            if fl & 3:
+            if fl & 3:  # dropped records (a bucket or the visited table): rerun before judging what is left
                 raise ShardOverflow(fl & 3)
+            left = [int(h[k + 1]) for k in range(0, len(h), 2)]
+            if any(left):
+                raise _lib.KetoGPUError("sharded batch: records left after %d levels (%s)" % (gdepth, left))
             if not self.general:
                 self.ops.finish(n, res, err)
             return res[:n], err[:n]
