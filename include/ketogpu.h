@@ -421,8 +421,9 @@ int kg_shard_finish(kg_snapshot* s, size_t n, uint8_t* d_res, uint32_t* d_err, v
  * boolean rewrites into parts: the parts' answers sit behind the n requested ones and
  * kg_shard_finish combines them into d_res[0, n) / d_err[0, n)). */
 size_t kg_shard_result_slots(const kg_snapshot* s, size_t n);
-/* Nodes this rank owns that a record can reach and the level protocol cannot evaluate (a relation
- * with a rewrite that is not materialised, or undeclared): when no rank has any, no check can end in
+/* Nodes a record can reach (a set edge of this rank's rows leads to them; an impure union counted by
+ * its owner) that the level protocol cannot evaluate (a relation with a rewrite that is not
+ * materialised, or undeclared): when no rank has any, no check can end in
  * an error below its root, and the driver may drop a member query's records (the done bitmap).
  * Otherwise it must not: the reference's order can make an error in an earlier branch win over a
  * member found at a shallower level in a later one (internal/check/checkgroup's first-decisive

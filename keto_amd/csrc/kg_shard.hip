@@ -527,7 +527,8 @@ __global__ __launch_bounds__(256) void k_shard_level(DevSnap s, const kg_frec* _
         const uint64_t a0 = s.adj_off[r.node], a1 = s.adj_off[r.node + 1];
         const uint64_t vkey = ((uint64_t)r.q << 32) | r.node;
         const int ins = lossy ? sv_insert_lossy(vis, vmask, vkey) : sv_insert(vis, vmask, vkey);
-        if (ins < 0) atomicOr(&counts[s.shard_n], 2u);
+        // the flags word follows the (sub-)bucket counters: counts[out_sub] in the one-rank sub mode
+        if (ins < 0) atomicOr(&counts[out_sub > 1 ? out_sub : s.shard_n], 2u);
         if (ins > 0 && !own && node_bad(s, r.node)) {  // a rewrite / undeclared relation
           if ((r.q >> Q_BITS) == me) atomicMax(&err[r.q & Q_MASK], (uint32_t)KG_ERR_NOT_IMPLEMENTED);
           else err_out = true;
@@ -901,9 +902,20 @@ static int shard_formula(Snapshot* s, ShardCtx* c, size_t n, ShardFormula* F) {
   return 0;
 }
 
+// A node that can end a check in an error, counted where a record could reach it: a set edge leads
+// to it from this rank's rows (its local parents; roots are judged by the seed itself), or -- a union
+// the owner found impure from its own TTU rows, a flag only the owner holds -- at its owner.  Without
+// the reverse index every bad node counts.
 __global__ void k_shard_bad_nodes(DevSnap s, unsigned long long* count) {
   const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
-  const bool bad = v < s.n_nodes && (!s.nowner || s.nowner[v] == s.shard_rank) && node_bad(s, v);
+  bool bad = v < s.n_nodes && node_bad(s, v);
+  if (bad && s.radj_off) {
+    const bool reached = s.radj_off[v + 1] > s.radj_off[v];
+    const uint32_t ns = s.nd_ns[v], rel = s.nd_rel[v];
+    const bool vunion = s.virt && ns < s.n_ns && rel < s.n_rel && s.virt[(size_t)ns * s.n_rel + rel];
+    const bool owned = !s.nowner || s.nowner[v] == s.shard_rank;
+    bad = reached || (vunion && owned && s.shard_n > 1);
+  }
   const uint64_t m = __ballot(bad);
   if (lane_id() == 0 && m) atomicAdd(count, (unsigned long long)__popcll(m));
 }
