@@ -88,6 +88,9 @@ def parse(argv=None):
     ap.add_argument("--stream-chunk", type=int, default=64,
                     help="kg_snapshot_tune stream_chunk (k_stream2 queries per dequeue, 1..64)")
     ap.add_argument("--grid-wgs", type=int, default=4, help="kg_snapshot_tune grid_wgs (k_grid_level WGs per CU)")
+    ap.add_argument("--stream-tail-ecap", type=int, default=-1,
+                    help="kg_snapshot_tune stream_tail_ecap: k_stream4's edge budget once its work list is drained "
+                         "(queries past it go to the next tier; 0 off, -1 library default)")
     ap.add_argument("--grid-ms", type=int, default=1,
                     help="kg_snapshot_tune grid_ms: the grid tier's queries as a multi-source bit-parallel BFS "
                          "(64 queries per group) when dense per-node masks fit (graphs up to ~4 M nodes)")
@@ -179,6 +182,8 @@ def apply_tune(snap, a) -> None:
         snap.tune("stream_chunk", a.stream_chunk)
     snap.tune("grid_wgs", a.grid_wgs)
     snap.tune("grid_bidir", a.grid_bidir)
+    if a.stream_tail_ecap >= 0:
+        snap.tune("stream_tail_ecap", a.stream_tail_ecap)
     snap.tune("grid_ms", a.grid_ms)
     snap.tune("grid_ms_words", a.grid_ms_words)
     snap.tune("grid_ms_tg_cap", a.grid_ms_tg_cap)

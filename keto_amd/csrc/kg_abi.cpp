@@ -422,6 +422,11 @@ static int tune_one(Snapshot* s, const char* key, int64_t value) {
     s->stream_variant = (int)value;
     return 0;
   }
+  if (strcmp(key, "stream_tail_ecap") == 0) {
+    if (value < 0 || value > 0xFFFFFFFFll) return set_error(-2, "stream_tail_ecap must be in [0, 2^32)");
+    s->stream_tail_ecap = (uint32_t)value;
+    return 0;
+  }
   if (strcmp(key, "stream_ecap") == 0) {
     if (value < 0 || value > 0xFFFFFFFFll) return set_error(-2, "stream_ecap must be in [0, 2^32)");
     s->stream_ecap = (uint32_t)value;

@@ -1160,7 +1160,8 @@ struct LqList {
 template <int VLOG2, int QC>
 __global__ __launch_bounds__(256) void k_stream4(DevSnap s, LqList wl, uint32_t* heads, uint8_t* __restrict__ out,
                                                  RQuery* __restrict__ rq, uint32_t* next_list, uint32_t* next_count,
-                                                 Ctl* ctl, uint32_t ecap, uint32_t chunk, uint32_t ranges) {
+                                                 Ctl* ctl, uint32_t ecap, uint32_t chunk, uint32_t ranges,
+                                                 uint32_t tail_ecap) {
   using Lds = Stream4Lds<VLOG2, QC>;
   constexpr uint32_t WIN = 64u;
   constexpr uint32_t VT = 1u << VLOG2;
@@ -1365,7 +1366,11 @@ __global__ __launch_bounds__(256) void k_stream4(DevSnap s, LqList wl, uint32_t*
         done = true;
         out[qi] = KG_IS_MEMBER;  // NotMember was pre-written by k_resolve
         st_done++;
-      } else if ((st & S2_OVER) || (ecap != 0xFFFFFFFFu && edg > ecap)) {
+      } else if ((st & S2_OVER) || (ecap != 0xFFFFFFFFu && edg > ecap) ||
+                   (tail_ecap && exhausted && pf == 0 && c_left == 0 && edg > tail_ecap)) {
+        // (the list is drained and this wave holds only its last queries: one past the tail budget
+        // goes to the next tier now instead of keeping the launch open -- the tail waves set the
+        // launch's length, kg_snapshot_tune "stream_tail_ecap")
         done = true;
         // the next tiers read the query by index
         rq[qi] = RQuery{L.s_node[lane], L.s_subj[lane], (int32_t)L.s_depth[lane], ROUTE_LIGHT, L.s_beg[lane],
@@ -2567,7 +2572,8 @@ int check_batch_begin(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n, 
       else if (sv == 15)  // pipelined dequeue of LQuery records, no returning LDS atomics
         hipLaunchKernelGGL((k_stream4<9, 256>), dim3(grid), dim3(256), 0, stream, s->ds, LqList{lq, ctl->light8, lq_cap},
                            ctl->heads, d_out, rq, ovf_list, ovf_count, ctl, ecap,
-                           std::max<uint32_t>(1u, std::min<uint32_t>(s->stream_chunk, S4_CHUNK)), s->stream_steal);
+                           std::max<uint32_t>(1u, std::min<uint32_t>(s->stream_chunk, S4_CHUNK)), s->stream_steal,
+                           s->stream_tail_ecap);
       else if (sv == 16)  // two interleaved FIFO engines per wave
         hipLaunchKernelGGL((k_stream5<9, 128>), dim3(grid), dim3(256), 0, stream, s->ds, LqList{lq, ctl->light8, lq_cap},
                            ctl->heads, d_out, rq, ovf_list, ovf_count, ctl, ecap,

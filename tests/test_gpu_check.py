@@ -206,13 +206,18 @@ def _torch():
                                                            (300_000, 10, 12, 1), (300_000, 10, 13, 1),
                                                            (300_000, 10, 14, 1), (300_000, 10, 15, 1),
                                                            (300_000, 5, 15, 0), (300_000, 10, 16, 1),
-                                                           (200_000, 5, 16, 0)])
+                                                           (200_000, 5, 16, 0), (300_000, 10, -32, 1),
+                                                           (300_000, 5, -4, 1)])
 def test_synthetic_graph_vs_oracle(n_tuples, gmax, variant, unheld):
+    """variant < 0: k_stream4 with a tail edge budget of -variant (stream_tail_ecap: once its work list
+    is drained, a wave hands queries past that many edges to the backward / grid tiers)."""
     torch = _torch()
     from keto_amd import _lib
     snap = Snapshot.synthetic(n_tuples, seed=20250131)
     snap.tune("tiers", 1 if gmax == 5 else 0)
-    snap.tune("stream", variant)
+    snap.tune("stream", variant if variant >= 0 else 15)
+    if variant < 0:
+        snap.tune("stream_tail_ecap", -variant)
     snap.tune("resolve_unheld", unheld)  # 0: the node map is read for every query (round-1 order)
     n = 20000
     dq = torch.empty((n, 7), dtype=torch.int32, device="cuda")
