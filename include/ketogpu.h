@@ -217,7 +217,11 @@ int kg_snapshot_materialized(const kg_snapshot* s, uint64_t* out3);
  * into 8 per-XCD shards, and a wave dequeues the next chunk while it walks the current one), 12 =
  * k_stream2 (32 query slots per wave over one FIFO, direct-mapped visited cache, a query bounded by
  * its edge budget), 9 = the same with a cap of 64 expanded nodes per query,
- * 11 = 128-edge windows, 10 = k_stream3 (software-pipelined), 0..8 = the round-1 k_stream variants.
+ * 11 = 128-edge windows, 10 = k_stream3 (software-pipelined), 0..8 = the round-1 k_stream variants,
+ * 16 = k_stream5 (two interleaved FIFO engines per wave; measured flat against 15).
+ * key "stream_tail_ecap" (default 0 = off): a k_stream4 wave whose work list is drained hands each
+ * query past this many edges to the backward / grid tiers (shortens the launch's tail; measured slower
+ * overall).
  * key "stream_ecap": edges a query may enqueue in the stream tier before it is handed to the
  * backward / grid tiers (default 512; 0 = no budget) -- cuts the stream kernel's tail of long walks.
  * key "resolve_unheld" (0/1): without a namespace program, k_resolve reads a subject id's holder
@@ -248,7 +252,11 @@ int kg_snapshot_materialized(const kg_snapshot* s, uint64_t* out3);
  * overflow reruns in tests).
  * key "grid_bidir" (0..2^31-1, default 0): grid-tier slots whose subject has at most this many
  * holders alternate forward and backward turns (0: forward only).  key "expand_tail" (0/1, default
- * 1): the expand walk caches a root's last frontier in LDS. */
+ * 1): the expand walk caches a root's last frontier in LDS.  Hash-sharded mode: key "shard_wgs"
+ * (1..64, default 8) k_shard_level workgroups per CU; "shard_heavy" (default 64) set rows longer than
+ * this go to k_shard_heavy, which spreads their edges over the grid (0: every row); "shard_vis_mode"
+ * 0 = exact (query, node) CAS table (default), 1 = lossy direct-mapped cache; "shard_budget" /
+ * "shard_back_budget": see kg_shard_back_* below. */
 int kg_snapshot_tune(kg_snapshot* s, const char* key, int64_t value);
 /* Synthetic layout: ids6 = {n_docs, n_groups, n_users, n_folders, user_obj0, folder_obj0}
  * (doc d = object d, group g = object n_docs+g, user u = object user_obj0+u). */
