@@ -47,6 +47,8 @@ constexpr int32_t D_OWN = 1 << 29, D_MASK = D_OWN - 1;
 // every rank alike (relflag for snapshots without them).
 __device__ __forceinline__ bool node_bad(const DevSnap& s, uint32_t node) {
   if (s.nflags) return (s.nflags[node] & (NF_REWRITE | NF_ERR)) != 0;
+  // no namespace program: nothing is bad, and the node's (ns, rel) -- two random loads -- is not read
+  if (!s.relflags) return false;
   return relflag(s, s.nd_ns[node], s.nd_rel[node]) != 0;
 }
 
