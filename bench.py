@@ -91,6 +91,12 @@ def parse(argv=None):
     ap.add_argument("--stream-tail-ecap", type=int, default=-1,
                     help="kg_snapshot_tune stream_tail_ecap: k_stream4's edge budget once its work list is drained "
                          "(queries past it go to the next tier; 0 off, -1 library default)")
+    ap.add_argument("--stream-order", type=str, default="",
+                    help="kg_snapshot_tune stream_order as LEN[:DEPTH]: k_resolve puts stream-tier queries whose "
+                         "root row has >= LEN set edges (and rest depth >= DEPTH) first in the work list (0 off)")
+    ap.add_argument("--stream-big-chunk", type=int, default=0,
+                    help="kg_snapshot_tune stream_big_chunk: k_stream4 claim size inside the stream_order front run "
+                         "(0 library default)")
     ap.add_argument("--grid-ms", type=int, default=1,
                     help="kg_snapshot_tune grid_ms: the grid tier's queries as a multi-source bit-parallel BFS "
                          "(64 queries per group) when dense per-node masks fit (graphs up to ~4 M nodes)")
@@ -184,6 +190,11 @@ def apply_tune(snap, a) -> None:
     snap.tune("grid_bidir", a.grid_bidir)
     if a.stream_tail_ecap >= 0:
         snap.tune("stream_tail_ecap", a.stream_tail_ecap)
+    if a.stream_big_chunk:
+        snap.tune("stream_big_chunk", a.stream_big_chunk)
+    if a.stream_order:
+        ln, _, dp = a.stream_order.partition(":")
+        snap.tune("stream_order", int(ln) | (int(dp or 0) << 16))
     snap.tune("grid_ms", a.grid_ms)
     snap.tune("grid_ms_words", a.grid_ms_words)
     snap.tune("grid_ms_tg_cap", a.grid_ms_tg_cap)

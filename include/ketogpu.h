@@ -221,7 +221,10 @@ int kg_snapshot_materialized(const kg_snapshot* s, uint64_t* out3);
  * 16 = k_stream5 (two interleaved FIFO engines per wave; measured flat against 15).
  * key "stream_tail_ecap" (default 0 = off): a k_stream4 wave whose work list is drained hands each
  * query past this many edges to the backward / grid tiers (shortens the launch's tail; measured slower
- * overall).
+ * overall).  key "stream_order" (LEN | DEPTH << 16, default 0 = off): k_resolve puts
+ * stream-tier queries whose root row has >= LEN set edges and rest depth >= DEPTH first in the work
+ * list, and k_stream4 claims them "stream_big_chunk" (1..64, default 4) at a time (measured level or
+ * slower).
  * key "stream_ecap": edges a query may enqueue in the stream tier before it is handed to the
  * backward / grid tiers (default 512; 0 = no budget) -- cuts the stream kernel's tail of long walks.
  * key "resolve_unheld" (0/1): without a namespace program, k_resolve reads a subject id's holder

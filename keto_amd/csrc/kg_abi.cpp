@@ -422,6 +422,17 @@ static int tune_one(Snapshot* s, const char* key, int64_t value) {
     s->stream_variant = (int)value;
     return 0;
   }
+  if (strcmp(key, "stream_order") == 0) {  // low 16 bits: root row length, bits 16..23: rest depth
+    if (value < 0 || value >= (1ll << 24)) return set_error(-2, "stream_order must be in [0, 2^24)");
+    s->stream_big_len = (uint32_t)(value & 0xFFFF);
+    s->stream_big_depth = (int32_t)(value >> 16);
+    return 0;
+  }
+  if (strcmp(key, "stream_big_chunk") == 0) {
+    if (value < 1 || value > 64) return set_error(-2, "stream_big_chunk must be in [1, 64]");
+    s->stream_big_chunk = (uint32_t)value;
+    return 0;
+  }
   if (strcmp(key, "stream_tail_ecap") == 0) {
     if (value < 0 || value > 0xFFFFFFFFll) return set_error(-2, "stream_tail_ecap must be in [0, 2^32)");
     s->stream_tail_ecap = (uint32_t)value;

@@ -119,8 +119,10 @@ __device__ void block_append(bool pred, uint32_t val, uint32_t* list, uint32_t* 
 // Workgroup-aggregated append of LQuery records (one atomic per workgroup).  The workgroup's records
 // are packed in LDS first and leave as one contiguous run of 8-B words: a lane storing its own 24-B
 // record would make each store instruction span 24 B x 64 lanes in three partial passes.
+// back_cap != 0: the run fills the shard from its end instead -- entries [back_cap - c - t, back_cap - c)
+// for the c records appended that way before it (the stream tier's work order, k_resolve).
 // Every thread must call it (256 threads).
-__device__ void block_append_lq(bool pred, const LQuery& v, LQuery* list, uint32_t* count) {
+__device__ void block_append_lq(bool pred, const LQuery& v, LQuery* list, uint32_t* count, uint32_t back_cap = 0) {
   static_assert(sizeof(LQuery) == 24, "LQuery is three 8-B words");
   __shared__ uint32_t wcnt[4], bbase;
   __shared__ LQuery s_lq[256];
@@ -135,7 +137,7 @@ __device__ void block_append_lq(bool pred, const LQuery& v, LQuery* list, uint32
   if (pred) s_lq[li + lanes_below(m)] = v;
   __syncthreads();
   const uint2* src = reinterpret_cast<const uint2*>(s_lq);
-  uint2* dst = reinterpret_cast<uint2*>(list + bbase);
+  uint2* dst = reinterpret_cast<uint2*>(list + (back_cap ? back_cap - bbase - t : bbase));
   for (uint32_t k = threadIdx.x; k < 3 * t; k += 256) dst[k] = src[k];
   __syncthreads();
 }
@@ -149,7 +151,7 @@ __global__ __launch_bounds__(256) void k_resolve(DevSnap s, const kg_query* __re
                                                  int32_t global, RQuery* __restrict__ rq, uint8_t* __restrict__ out,
                                                  uint32_t* __restrict__ err, uint32_t* light_list,
                                                  uint32_t* gen_list, int no_holder_filter, Ctl* ctl,
-                                                 LQuery* lq_list, uint32_t lq_cap) {
+                                                 LQuery* lq_list, uint32_t lq_cap, uint32_t big_len, int32_t big_depth) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   // n: capacity (list strides); with a formula split the live count is n_base + *n_extra
   bool valid = i < (n_extra ? n_base + *n_extra : n);
@@ -257,7 +259,17 @@ __global__ __launch_bounds__(256) void k_resolve(DevSnap s, const kg_query* __re
   }
   // light list: 8 shards of capacity n (shard = blockIdx & 7), dequeued by k_light per XCD
   const uint32_t h = blockIdx.x & 7;
-  if (lq_list) block_append_lq(valid && route == ROUTE_LIGHT, lq, lq_list + (size_t)h * lq_cap, &ctl->light8[h * 32]);
+  if (lq_list && big_len) {
+    // work order for the stream tier (kg_snapshot_tune "stream_order"): queries whose root row has >=
+    // big_len set edges and depth >= big_depth fill each shard from the front, the rest from the back,
+    // and waves dequeue front-first -- the likely-long walks start early instead of holding the
+    // launch's tail
+    const bool big = lq.len >= big_len && lq.depth >= big_depth;
+    LQuery* const sh = lq_list + (size_t)h * lq_cap;
+    block_append_lq(valid && route == ROUTE_LIGHT && big, lq, sh, &ctl->light8[h * 32]);
+    block_append_lq(valid && route == ROUTE_LIGHT && !big, lq, sh, &ctl->light8[h * 32 + 16], lq_cap);
+  } else if (lq_list)
+    block_append_lq(valid && route == ROUTE_LIGHT, lq, lq_list + (size_t)h * lq_cap, &ctl->light8[h * 32]);
   else block_append(valid && route == ROUTE_LIGHT, i, light_list + (size_t)h * n, &ctl->light8[h * 32]);
   block_append(valid && route == ROUTE_GENERAL, i, gen_list, &ctl->gen_count);
 }
@@ -1153,7 +1165,8 @@ struct Stream4Lds {
 
 struct LqList {
   const LQuery* list;
-  const uint32_t* counts;  // shard h holds counts[32 h] records from list[h * cap]
+  const uint32_t* counts;  // shard h: counts[32 h] records from list[h * cap] (the front run) and
+                           // counts[32 h + 16] ending at list[(h + 1) * cap] (the back run, k_resolve)
   uint32_t cap;
 };
 
@@ -1161,7 +1174,7 @@ template <int VLOG2, int QC>
 __global__ __launch_bounds__(256) void k_stream4(DevSnap s, LqList wl, uint32_t* heads, uint8_t* __restrict__ out,
                                                  RQuery* __restrict__ rq, uint32_t* next_list, uint32_t* next_count,
                                                  Ctl* ctl, uint32_t ecap, uint32_t chunk, uint32_t ranges,
-                                                 uint32_t tail_ecap) {
+                                                 uint32_t tail_ecap, uint32_t big_chunk) {
   using Lds = Stream4Lds<VLOG2, QC>;
   constexpr uint32_t WIN = 64u;
   constexpr uint32_t VT = 1u << VLOG2;
@@ -1181,11 +1194,13 @@ __global__ __launch_bounds__(256) void k_stream4(DevSnap s, LqList wl, uint32_t*
   }
   if (lane == 0) L.pref[WIN] = 0;
   // shard sizes, final before this kernel starts: lanes 0..7
-  const uint32_t shard_n = lane < 8 ? wl.counts[lane * 32] : 0u;
+  const uint32_t shard_b = lane < 8 ? wl.counts[lane * 32] : 0u;  // front run (all of it without an order)
+  const uint32_t shard_n = lane < 8 ? shard_b + wl.counts[lane * 32 + 16] : 0u;
   __builtin_amdgcn_wave_barrier();
   uint32_t active = 0;  // wave-uniform: slots holding a query
   // dequeue pipeline (wave-uniform state): 0 idle, 1 head atomic in flight (tk, lane 0), 2 records staged
   uint32_t pf = 0, tk = 0, st_got = 0;
+  uint32_t claim = chunk, last_k = 0;  // size of the claim in flight; end of this wave's last claim in the shard
   bool exhausted = false;  // every range this wave drains is empty
   LQuery sq{};             // staged chunk (lane k: record k)
   uint32_t c_left = 0, c_pos = 0;
@@ -1245,16 +1260,24 @@ __global__ __launch_bounds__(256) void k_stream4(DevSnap s, LqList wl, uint32_t*
       const uint32_t h = head_sel & 7;
       const uint32_t lo = h * wl.cap, hi = lo + (uint32_t)__builtin_amdgcn_readlane((int)shard_n, (int)h);
       if (lo + k < hi) {
-        st_got = min(chunk, hi - (lo + k));
-        if ((uint32_t)lane < st_got) sq = wl.list[lo + k + lane];
+        st_got = min(claim, hi - (lo + k));
+        last_k = k + claim;
+        // position p of the shard's order: the front run, then the back run at the shard's end
+        const uint32_t nb = (uint32_t)__builtin_amdgcn_readlane((int)shard_b, (int)h), p = k + (uint32_t)lane;
+        if ((uint32_t)lane < st_got) sq = wl.list[lo + (p < nb ? p : p + (wl.cap - (hi - lo)))];
         pf = 2;
       } else {
         pf = 0;
+        last_k = 0;
         if (++head_sel >= head0 + ranges) exhausted = true;
       }
     }
     if (pf == 0 && !exhausted) {
-      if (lane == 0) tk = atomicAdd(&heads[(head_sel & 7) * 32], chunk);
+      // the front run of a shard (stream_order) is dequeued in small claims: a 64-query chunk of it
+      // would put 64 long walks on one wave
+      const uint32_t nbh = (uint32_t)__builtin_amdgcn_readlane((int)shard_b, (int)(head_sel & 7));
+      claim = (big_chunk && last_k < nbh) ? big_chunk : chunk;
+      if (lane == 0) tk = atomicAdd(&heads[(head_sel & 7) * 32], claim);
       pf = 1;
     }
     if (active == 0) {
@@ -1433,7 +1456,8 @@ __global__ __launch_bounds__(256) void k_stream5(DevSnap s, LqList wl, uint32_t*
     L.s_edg[lane] = 0;
   }
   if (lane == 0) L.pref[WIN] = 0;
-  const uint32_t shard_n = lane < 8 ? wl.counts[lane * 32] : 0u;
+  const uint32_t shard_b = lane < 8 ? wl.counts[lane * 32] : 0u;  // front run (all of it without an order)
+  const uint32_t shard_n = lane < 8 ? shard_b + wl.counts[lane * 32 + 16] : 0u;
   __builtin_amdgcn_wave_barrier();
   uint32_t active = 0;  // wave-uniform: slots holding a query (engine e: bits [16e, 16e + 16))
   uint32_t pf = 0, tk = 0, st_got = 0;
@@ -1466,7 +1490,9 @@ __global__ __launch_bounds__(256) void k_stream5(DevSnap s, LqList wl, uint32_t*
       const uint32_t lo = h * wl.cap, hi = lo + (uint32_t)__builtin_amdgcn_readlane((int)shard_n, (int)h);
       if (lo + k < hi) {
         st_got = min(chunk, hi - (lo + k));
-        if ((uint32_t)lane < st_got) sq = wl.list[lo + k + lane];
+        // position p of the shard's order: the front run, then the back run at the shard's end
+        const uint32_t nb = (uint32_t)__builtin_amdgcn_readlane((int)shard_b, (int)h), p = k + (uint32_t)lane;
+        if ((uint32_t)lane < st_got) sq = wl.list[lo + (p < nb ? p : p + (wl.cap - (hi - lo)))];
         pf = 2;
       } else {
         pf = 0;
@@ -2504,7 +2530,8 @@ int check_batch_begin(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n, 
       return set_error(-5, "stream work list does not fit the scratch");
     hipLaunchKernelGGL(k_resolve, dim3(nblk), dim3(256), 0, stream, s->ds, d_q, (uint32_t)n,
                        (uint32_t)n_base, n_extra, global_max_depth, rq, d_out, d_err, light, gen,
-                       use_back ? (s->resolve_unheld ? 2 : 1) : 0, ctl, lq, lq_cap);
+                       use_back ? (s->resolve_unheld ? 2 : 1) : 0, ctl, lq, lq_cap, compact ? s->stream_big_len : 0u,
+                       s->stream_big_depth);
     HIPC(hipGetLastError());
     uint32_t* const after_list = use_medium ? medium : heavy;
     uint32_t* const after_count = use_medium ? &ctl->medium_count : &ctl->heavy_count;
@@ -2573,7 +2600,7 @@ int check_batch_begin(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n, 
         hipLaunchKernelGGL((k_stream4<9, 256>), dim3(grid), dim3(256), 0, stream, s->ds, LqList{lq, ctl->light8, lq_cap},
                            ctl->heads, d_out, rq, ovf_list, ovf_count, ctl, ecap,
                            std::max<uint32_t>(1u, std::min<uint32_t>(s->stream_chunk, S4_CHUNK)), s->stream_steal,
-                           s->stream_tail_ecap);
+                           s->stream_tail_ecap, s->stream_big_len ? std::min<uint32_t>(s->stream_big_chunk, S4_CHUNK) : 0u);
       else if (sv == 16)  // two interleaved FIFO engines per wave
         hipLaunchKernelGGL((k_stream5<9, 128>), dim3(grid), dim3(256), 0, stream, s->ds, LqList{lq, ctl->light8, lq_cap},
                            ctl->heads, d_out, rq, ovf_list, ovf_count, ctl, ecap,

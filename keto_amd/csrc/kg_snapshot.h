@@ -234,6 +234,9 @@ struct Snapshot {
   uint32_t stream_ecap = 512;  // kg_snapshot_tune("stream_ecap"): stream-tier edge budget per query (0 = none)
   int resolve_unheld = 1;  // kg_snapshot_tune("resolve_unheld"): k_resolve reads the holder bit before the node map
   uint32_t stream_steal = 4;   // kg_snapshot_tune("stream_steal"): XCD ranges a k_stream2 wave dequeues from (1..8)
+  uint32_t stream_big_len = 0;    // kg_snapshot_tune("stream_order"): root rows of >= this many set edges go first (0 = off)
+  int32_t stream_big_depth = 0;   // ... together with a rest depth >= this (the tune's value >> 16)
+  uint32_t stream_big_chunk = 4;  // kg_snapshot_tune("stream_big_chunk"): k_stream4 claim size inside the front run
   uint32_t stream_tail_ecap = 0;  // kg_snapshot_tune("stream_tail_ecap"): k_stream4's edge budget once the list is drained (0 = off)
   uint32_t stream_chunk = 64;  // kg_snapshot_tune("stream_chunk"): k_stream2 queries per dequeue (1..64)
   int grid_wgs = 4;          // kg_snapshot_tune("grid_wgs"): k_grid_level workgroups per CU (bench default)

@@ -237,6 +237,32 @@ def test_synthetic_graph_vs_oracle(n_tuples, gmax, variant, unheld):
     assert (dfs == exp).all()
 
 
+@pytest.mark.parametrize("variant,order,big_chunk", [(15, 1, 4), (15, 3 | (2 << 16), 1), (15, 60000, 4),
+                                                     (15, 8, 64), (15, 2 | (3 << 16), 7), (16, 2 | (3 << 16), 4),
+                                                     (16, 1, 4)])
+def test_stream_order_vs_oracle(variant, order, big_chunk):
+    """kg_snapshot_tune("stream_order"): k_resolve writes each stream-tier shard as a front run (root row
+    >= LEN set edges, rest depth >= DEPTH) and a back run at the shard's end; the stream kernels dequeue
+    the front run first.  Every query is still answered once: all-front (LEN 1), all-back (LEN 60000)
+    and mixed splits match the oracle, over a batch whose last resolve block is partial."""
+    torch = _torch()
+    from keto_amd import _lib
+    snap = Snapshot.synthetic(300_000, seed=20250131)
+    snap.tune("stream", variant)
+    snap.tune("stream_order", order)
+    snap.tune("stream_big_chunk", big_chunk)  # k_stream4's claim size inside the front run
+    n, gmax = 20000 + 77, 10
+    dq = torch.empty((n, 7), dtype=torch.int32, device="cuda")
+    _lib.check(_lib.load().kg_synth_queries(snap.handle, 7, n, dq.data_ptr()), "kg_synth_queries")
+    q = dq.cpu().numpy().view(np.uint32)
+    out, err = Engine(snap, Config(gmax)).batch_check_ids(q, with_stats=True)
+    assert (err == 0).all()
+    exp, _, _ = Oracle(snap.export(), 0).check_batch(q[:, :6], q[:, 6].view(np.int32), gmax, POLICY_CANONICAL,
+                                                     nthreads=8)
+    assert (out == exp).all(), np.nonzero(out != exp)[0][:10]
+    assert 0.05 < out.mean() < 0.95
+
+
 def test_concurrent_streams_match_serial():
     """kg_check_batch_device on several streams at once (one workspace per stream, one host thread
     per stream, the way bench.py keeps batches in flight) gives exactly the serial answers."""
