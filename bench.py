@@ -72,6 +72,8 @@ def parse(argv=None):
                          "forward phase takes it)")
     ap.add_argument("--shard-wgs", type=int, default=0,
                     help="kg_snapshot_tune shard_wgs: sharded level kernel workgroups per CU (0: library default)")
+    ap.add_argument("--shard-pack", type=int, default=-1,
+                    help="kg_snapshot_tune shard_pack: packed local records in the one-rank level loop (-1 library default)")
     ap.add_argument("--shard-heavy", type=int, default=-1,
                     help="kg_snapshot_tune shard_heavy: set rows longer than this are expanded grid-wide (k_shard_heavy; "
                          "0: every expansion; -1: the library default)")
@@ -463,6 +465,8 @@ def bench_sharded(a):
     snap.tune("shard_vis_mode", a.shard_vis_mode)
     if a.shard_heavy >= 0:
         snap.tune("shard_heavy", a.shard_heavy)
+    if a.shard_pack >= 0:
+        snap.tune("shard_pack", a.shard_pack)
     if a.shard_wgs:
         snap.tune("shard_wgs", a.shard_wgs)
     B = a.batch
@@ -542,13 +546,24 @@ def bench_sharded(a):
            "final_levels_per_batch": chk.final_levels, "shard_budget": a.shard_budget,
            "host_syncs_per_batch": (sum(c.host_syncs for c in chks) - sum(syncs0)) / max(1, a.steps),
            "bucket": chk.bucket, "shard_back_budget": a.shard_back_budget, "shard_vis_mode": a.shard_vis_mode,
-           "shard_heavy": a.shard_heavy, "records_exchanged_per_batch": recs / a.steps,
+           "shard_heavy": a.shard_heavy, "shard_pack": a.shard_pack, "records_exchanged_per_batch": recs / a.steps,
            **({"level_records": chk.level_records} if chk.level_records else {}),
            "snapshot_build_s": t_build}
+    bad = 0
+    if rank == 0 and world == 1 and a.parity > 0:
+        # untimed: batch 0 once more through the sharded path, against the oracle over the same rows
+        res0, _ = chks[0].check(dqs[0], a.global_depth)
+        orc = CheckOracle(snap, a, effective_cpus()["effective"])
+        out["parity"] = orc.parity(dqs[0].cpu().numpy().view(np.uint32), res0.cpu().numpy(), a.parity,
+                                   a.parity_canonical)
+        bad = out["parity"]["mismatches"] + out["parity"]["canonical_mismatches"]
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()
+    if bad:
+        sys.stderr.write("PARITY FAILURE: sharded answers differ from the oracle\n")
+        sys.exit(1)
 
 
 def bench_host(a):

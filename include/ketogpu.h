@@ -258,7 +258,9 @@ int kg_snapshot_materialized(const kg_snapshot* s, uint64_t* out3);
  * 1): the expand walk caches a root's last frontier in LDS.  Hash-sharded mode: key "shard_wgs"
  * (1..64, default 8) k_shard_level workgroups per CU; "shard_heavy" (default 64) set rows longer than
  * this go to k_shard_heavy, which spreads their edges over the grid (0: every row); "shard_vis_mode"
- * 0 = exact (query, node) CAS table (default), 1 = lossy direct-mapped cache; "shard_budget" /
+ * 0 = exact (query, node) CAS table (default), 1 = lossy direct-mapped cache; "shard_pack" (0/1,
+ * default 0): kg_shard_levels sends a locally owned child as its set-row begin and length (no
+ * adj_off read at the next level; no namespace program, depths < 256); "shard_budget" /
  * "shard_back_budget": see kg_shard_back_* below. */
 int kg_snapshot_tune(kg_snapshot* s, const char* key, int64_t value);
 /* Synthetic layout: ids6 = {n_docs, n_groups, n_users, n_folders, user_obj0, folder_obj0}

@@ -428,6 +428,11 @@ static int tune_one(Snapshot* s, const char* key, int64_t value) {
     s->stream_big_depth = (int32_t)(value >> 16);
     return 0;
   }
+  if (strcmp(key, "shard_pack") == 0) {
+    if (value < 0 || value > 1) return set_error(-2, "shard_pack must be 0 or 1");
+    s->shard_pack = (int)value;
+    return 0;
+  }
   if (strcmp(key, "stream_big_chunk") == 0) {
     if (value < 1 || value > 64) return set_error(-2, "stream_big_chunk must be in [1, 64]");
     s->stream_big_chunk = (uint32_t)value;

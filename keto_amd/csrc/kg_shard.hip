@@ -40,6 +40,12 @@ constexpr int32_t D_NOPROBE = 1 << 30;
 // bit 29: the record checks the own part of a split formula query's node (its rows as a plain node,
 // the node's rewrite evaluated by the formula instead)
 constexpr int32_t D_OWN = 1 << 29, D_MASK = D_OWN - 1;
+// A packed local record (one-rank levels, no namespace program, kg_snapshot_tune "shard_pack"): node
+// holds the child's set-row begin (< 2^31) and depth holds D_ROW | len << 8 | rest depth (< 256), so
+// the receiving level reads no adj_off pair; its visited key is (q, 2^31 | begin) -- a row begin
+// identifies its node (rows are disjoint), and plain keys keep node ids < 2^31.
+constexpr int32_t D_ROW = 1 << 28;
+constexpr uint32_t PK_LEN_BITS = 20;
 
 // Rewrite materialisation runs in this mode too (union nodes are plain; kg_augment.hip), so a node
 // needs the interpreter -- unavailable across shards: an error -- when its own relation has a
@@ -393,7 +399,8 @@ __global__ __launch_bounds__(256) void k_shard_seed(DevSnap s, const kg_query* _
 // One set-adjacency edge (parent record pr -> child ax) of an expansion: the child's record for its
 // owner, a hit / error report for the query's home, or nothing.
 __device__ __forceinline__ void shard_child(const DevSnap& s, const kg_frec& pr, const AdjX& ax, uint32_t me,
-                                            uint8_t* res, uint32_t* err, kg_frec& c, uint32_t& dest, bool& send) {
+                                            uint8_t* res, uint32_t* err, kg_frec& c, uint32_t& dest, bool& send,
+                                            bool pack = false) {
   const uint32_t child = ax.node;
   if (pr.depth >= 2) {
     dest = s.nowner ? s.nowner[child] : 0u;
@@ -411,7 +418,10 @@ __device__ __forceinline__ void shard_child(const DevSnap& s, const kg_frec& pr,
         dest = pr.q >> Q_BITS;
         send = true;
       } else if (ax.len && pr.depth >= 3) {
-        c = kg_frec{pr.q, child, pr.subj, (pr.depth - 1) | D_NOPROBE};
+        if (pack && ax.begin < 0x80000000u && ax.len < (1u << PK_LEN_BITS) && pr.depth - 1 < 256)
+          c = kg_frec{pr.q, ax.begin, pr.subj, (int32_t)((ax.len << 8) | (uint32_t)(pr.depth - 1)) | D_ROW | D_NOPROBE};
+        else
+          c = kg_frec{pr.q, child, pr.subj, (pr.depth - 1) | D_NOPROBE};
         send = true;
       }
     } else {
@@ -471,7 +481,8 @@ __global__ __launch_bounds__(256) void k_shard_level(DevSnap s, const kg_frec* _
                                                      const uint32_t* __restrict__ done, uint32_t done_wpr,
                                                      HeavyList heavy,
                                                      uint32_t* qcnt, uint32_t budget, uint32_t lossy, uint32_t n_seg,
-                                                     uint64_t seg_cap, uint32_t heavy_min, uint32_t out_sub) {
+                                                     uint64_t seg_cap, uint32_t heavy_min, uint32_t out_sub,
+                                                     uint32_t pack) {
   __shared__ uint32_t s_pref[256], s_wsum[4];
   __shared__ uint64_t s_rb[256];
   __shared__ kg_frec s_rec[256];
@@ -509,7 +520,13 @@ __global__ __launch_bounds__(256) void k_shard_level(DevSnap s, const kg_frec* _
       }
       r = in[src];
       const bool probe = !(r.depth & D_NOPROBE), own = (r.depth & D_OWN) != 0;
+      const bool packed = pack && (r.depth & D_ROW) != 0;  // r.node = the row's begin, the length in the depth word
       r.depth &= D_MASK;
+      uint32_t pk_len = 0;
+      if (packed) {
+        pk_len = ((uint32_t)r.depth >> 8) & ((1u << PK_LEN_BITS) - 1);
+        r.depth &= 0xFF;
+      }
       if (r.node == KG_FREC_HIT) {
         if ((r.q >> Q_BITS) == me) res[r.q & Q_MASK] = KG_IS_MEMBER;
       } else if (r.node == KG_FREC_ESC) {
@@ -526,12 +543,13 @@ __global__ __launch_bounds__(256) void k_shard_level(DevSnap s, const kg_frec* _
         const uint64_t dkey = dset_key(r.node, r.subj);
         const ulonglong2 pb = *reinterpret_cast<const ulonglong2*>(
             s.dset + (want_p ? hash_home(dkey, s.dset_nb) : 0ull) * DSET_BUCKET);
-        const uint64_t a0 = s.adj_off[r.node], a1 = s.adj_off[r.node + 1];
-        const uint64_t vkey = ((uint64_t)r.q << 32) | r.node;
+        const uint32_t an = packed ? 0u : r.node;
+        const uint64_t a0 = s.adj_off[an], a1 = s.adj_off[an + 1];
+        const uint64_t vkey = ((uint64_t)r.q << 32) | (packed ? (0x80000000u | r.node) : r.node);
         const int ins = lossy ? sv_insert_lossy(vis, vmask, vkey) : sv_insert(vis, vmask, vkey);
         // the flags word follows the (sub-)bucket counters: counts[out_sub] in the one-rank sub mode
         if (ins < 0) atomicOr(&counts[out_sub > 1 ? out_sub : s.shard_n], 2u);
-        if (ins > 0 && !own && node_bad(s, r.node)) {  // a rewrite / undeclared relation
+        if (ins > 0 && !own && !packed && node_bad(s, r.node)) {  // a rewrite / undeclared relation
           if ((r.q >> Q_BITS) == me) atomicMax(&err[r.q & Q_MASK], (uint32_t)KG_ERR_NOT_IMPLEMENTED);
           else err_out = true;
         } else if (ins > 0) {
@@ -545,8 +563,8 @@ __global__ __launch_bounds__(256) void k_shard_level(DevSnap s, const kg_frec* _
             // children at depth - 1 >= 1 can still be probed; children at depth 0 cannot, but
             // checkIsAllowed(child, 0) still evaluates astRelationFor (engine.go:199-206), so with a
             // namespace program their relation flags are checked (shard_child) for the error report
-            rb = a0;
-            len = a1 - a0;
+            rb = packed ? (uint64_t)r.node : a0;
+            len = packed ? (uint64_t)pk_len : a1 - a0;
             if (len && budget) {  // escalation: this rank's set-edge count of the query passes the budget
               const uint32_t add = (uint32_t)min(len, (uint64_t)budget);
               const uint32_t old = atomicAdd(&qcnt[mix64(r.q) & ((1u << QCNT_LOG2) - 1)], add);
@@ -593,7 +611,7 @@ __global__ __launch_bounds__(256) void k_shard_level(DevSnap s, const kg_frec* _
       bool send = false;
       if (e < total) {
         const int own = owner_search(s_pref, 256, e);
-        shard_child(s, s_rec[own], s.adjx[s_rb[own] + (e - s_pref[own])], me, res, err, c, dest, send);
+        shard_child(s, s_rec[own], s.adjx[s_rb[own] + (e - s_pref[own])], me, res, err, c, dest, send, pack != 0);
       }
       emit(send, dest, c, out, cap, counts, s.shard_n, out_sub);
     }
@@ -778,7 +796,7 @@ __global__ __launch_bounds__(256) void k_shard_back_level(DevSnap s, const kg_fr
 // tile's rows staged in LDS.
 __global__ __launch_bounds__(256) void k_shard_heavy(DevSnap s, HeavyList heavy, kg_frec* out, uint64_t cap,
                                                      uint32_t* counts, uint8_t* res, uint32_t* err, uint32_t nranks,
-                                                     uint32_t out_sub) {
+                                                     uint32_t out_sub, uint32_t pack) {
   static_assert(HEAVY_TILE == 256, "one edge per thread");
   __shared__ uint32_t s_r0;
   __shared__ uint64_t s_e0[HEAVY_TILE + 1];
@@ -823,7 +841,7 @@ __global__ __launch_bounds__(256) void k_shard_heavy(DevSnap s, HeavyList heavy,
       const HeavyRow H = heavy.rows[r0 + lo];
       const uint64_t k = e - H.e0;
       if (H.pad) back_child(s, H.r, s.radj[H.rb + k], me, res, c, send);  // a reverse row (backward phase)
-      else shard_child(s, H.r, s.adjx[H.rb + k], me, res, err, c, dest, send);
+      else shard_child(s, H.r, s.adjx[H.rb + k], me, res, err, c, dest, send, pack != 0);
     }
     emit(send, dest, c, out, cap, counts, nranks, out_sub);  // ends with a barrier: s_r0 is free again
   }
@@ -984,6 +1002,7 @@ int shard_seed(Snapshot* s, const kg_query* d_q, size_t n, int32_t gdepth, kg_fr
   if (int rc = shard_vis_prepare(s, c, stream)) return rc;
   HIPC(hipMemsetAsync(d_counts, 0, (s->shard_n + 1) * 4, stream));
   c->final = false;
+  c->gdepth = gdepth;
   uint4* qinfo = nullptr;
   if (shard_escalates(s)) {
     if (!c->qcnt) HIPC(hipMalloc(&c->qcnt, (4ull << QCNT_LOG2)));
@@ -1034,10 +1053,10 @@ int shard_level(Snapshot* s, const kg_frec* d_in, size_t n_in, const uint32_t* d
                        (uint64_t)cap, d_counts, d_res, d_err, (uint64_t*)c->vis, c->vis_slots - 1,
                        d_done, d_done ? done_words : 0u, heavy, (uint32_t*)c->qcnt,
                        shard_escalates(s) && c->qcnt && !c->final ? s->shard_budget : 0u,
-                       s->shard_vis_mode ? 1u : 0u, n_seg, (uint64_t)seg_cap, s->shard_heavy, 1u);
+                       s->shard_vis_mode ? 1u : 0u, n_seg, (uint64_t)seg_cap, s->shard_heavy, 1u, 0u);
     HIPC(hipGetLastError());
     hipLaunchKernelGGL(k_shard_heavy, dim3((uint32_t)s->n_cu * 4), dim3(256), 0, stream, s->ds, heavy, d_out,
-                       (uint64_t)cap, d_counts, d_res, d_err, s->shard_n, 1u);
+                       (uint64_t)cap, d_counts, d_res, d_err, s->shard_n, 1u, 0u);
     HIPC(hipGetLastError());
   }
   return 0;
@@ -1071,6 +1090,10 @@ int shard_levels(Snapshot* s, int levels, kg_frec* d_buf[2], size_t cap, uint32_
   // sub mode): level 0 reads the seed's bucket, every later level the SUB segments of the one before
   const uint32_t SUB = cap >= 8 * 256 ? 8u : 1u;
   const uint64_t seg = cap / SUB;
+  // packed local records (D_ROW): only here, where every record stays on this rank and is read by the
+  // next level of this loop; not with a namespace program (node flags) or an escalation budget
+  const uint32_t pack = (s->shard_pack && !s->ds.relflags && !s->ds.nflags && budget == 0 &&
+                         s->ds.n_nodes < 0x80000000u && c->gdepth > 0 && c->gdepth < 256) ? 1u : 0u;
   if (!c->cnt8) HIPC(hipMalloc((void**)&c->cnt8, 32 * 4));
   HIPC(hipMemsetAsync(c->cnt8, 0, 32 * 4, stream));
   uint32_t* sub[2] = {c->cnt8, c->cnt8 + 16};
@@ -1086,10 +1109,10 @@ int shard_levels(Snapshot* s, int levels, kg_frec* d_buf[2], size_t cap, uint32_
                        seg_in ? sub[cur] : d_counts[cur], d_buf[nx], seg, sub[nx], d_res, d_err, (uint64_t*)c->vis,
                        c->vis_slots - 1, k > 0 ? (const uint32_t*)c->bits : nullptr, w, heavy, (uint32_t*)c->qcnt,
                        budget, s->shard_vis_mode ? 1u : 0u, seg_in ? SUB : 1u, seg_in ? seg : (uint64_t)0,
-                       s->shard_heavy, SUB);
+                       s->shard_heavy, SUB, pack);
     HIPC(hipGetLastError());
     hipLaunchKernelGGL(k_shard_heavy, dim3((uint32_t)s->n_cu * 4), dim3(256), 0, stream, s->ds, heavy, d_buf[nx], seg,
-                       sub[nx], d_res, d_err, s->shard_n, SUB);
+                       sub[nx], d_res, d_err, s->shard_n, SUB, pack);
     HIPC(hipGetLastError());
     cur = nx;
   }
@@ -1186,7 +1209,7 @@ int shard_back_level(Snapshot* s, const kg_frec* d_in, size_t n_in, const uint32
                        c->qcnt ? s->shard_back_budget : 0u, s->shard_vis_mode ? 1u : 0u);
     HIPC(hipGetLastError());
     hipLaunchKernelGGL(k_shard_heavy, dim3((uint32_t)s->n_cu * 4), dim3(256), 0, stream, s->ds, heavy, d_out,
-                       (uint64_t)cap, d_counts, d_res, d_err, 1u, 1u);
+                       (uint64_t)cap, d_counts, d_res, d_err, 1u, 1u, 0u);
     HIPC(hipGetLastError());
   }
   return 0;

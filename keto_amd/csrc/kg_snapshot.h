@@ -151,6 +151,7 @@ struct ShardCtx {
   uint32_t* bits = nullptr;  // kg_shard_levels: the batch's done bitmap
   size_t bits_n = 0;
   uint32_t* cnt8 = nullptr;  // kg_shard_levels: per-XCD sub-bucket counters of the two level buffers (+ flags)
+  int32_t gdepth = 0;        // the batch's global depth (kg_shard_seed): packed records need depths < 256
   ~ShardCtx();
 };
 
@@ -225,6 +226,7 @@ struct Snapshot {
   uint32_t shard_held_n = 0;
   int shard_vis_log2 = 23;
   uint32_t shard_wgs = 8;  // kg_snapshot_tune("shard_wgs"): k_shard_level workgroups per CU
+  int shard_pack = 0;  // kg_snapshot_tune("shard_pack"): packed local records in kg_shard_levels (D_ROW; measured neutral)
   uint32_t shard_heavy = 64;  // kg_snapshot_tune("shard_heavy"): set rows longer than this go to k_shard_heavy (r3p A/B)
   int shard_vis_mode = 0;  // kg_snapshot_tune("shard_vis_mode"): (query, node) dedup 0 = exact CAS table, 1 = lossy cache
   uint32_t shard_budget = 0;       // kg_snapshot_tune("shard_budget"): forward set edges per query and rank (0 = off)

@@ -448,7 +448,7 @@ def test_sharded_general_rewrites_vs_oracle(kind, world):
 
 # ------------------------------------------------------------------ config C4 generator, sharded
 def _synth_worker(rank, world, port, n_tuples, n_q, gmax, backend, outq, preset=0, budget=None, back_budget=None,
-                  vis_mode=0, heavy=None):
+                  vis_mode=0, heavy=None, pack=None):
     sys.path.insert(0, ROOT)
     import torch.distributed as dist
     from keto_amd import _lib
@@ -469,6 +469,8 @@ def _synth_worker(rank, world, port, n_tuples, n_q, gmax, backend, outq, preset=
     snap.tune("shard_vis_mode", vis_mode)
     if heavy is not None:
         snap.tune("shard_heavy", heavy)
+    if pack is not None:
+        snap.tune("shard_pack", pack)
     dq = torch.empty((n_q, 7), dtype=torch.int32, device="cuda")
     _lib.check(_lib.load().kg_synth_queries(snap.handle, 31, n_q, dq.data_ptr()), "kg_synth_queries")
     mine = np.array_split(np.arange(n_q), world)[rank]
@@ -506,6 +508,18 @@ def test_sharded_c4_generator_vs_oracle(world, backend, budget, back_budget, vis
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("pack,heavy,gmax", [(0, None, 10), (1, None, 10), (1, 0, 10), (1, 256, 5), (0, 0, 5)])
+def test_sharded_packed_records_vs_oracle(pack, heavy, gmax):
+    """kg_snapshot_tune("shard_pack"): in the one-rank device level loop a locally owned child travels as
+    a packed record (its set-row begin and length instead of its node id: the next level reads no
+    adj_off pair; its visited key lives in a separate half of the key space).  On and off, with every
+    row / rows over 256 edges through the hub kernel, bit-exact with the oracle."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    _run_synth(1, None, 300_000, 20_000, gmax, preset=0, heavy=heavy, pack=pack)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("world,backend", [(1, None), (2, "gloo")])
 def test_sharded_c3_rewrites_vs_oracle(world, backend):
     """Config C3 (Drive-like graph + folder forest + OPL view / edit / share), hash-sharded: view and
@@ -518,14 +532,15 @@ def test_sharded_c3_rewrites_vs_oracle(world, backend):
     _run_synth(world, backend, 150_000, 6000, 10, preset=1)
 
 
-def _run_synth(world, backend, n_tuples, n_q, gmax, preset, budget=None, back_budget=None, vis_mode=0, heavy=None):
+def _run_synth(world, backend, n_tuples, n_q, gmax, preset, budget=None, back_budget=None, vis_mode=0, heavy=None,
+               pack=None):
     from keto_amd.engine import Snapshot
     from oracle.oracle import POLICY_CANONICAL, Oracle
     ctx = mp.get_context("spawn")
     outq = ctx.Queue()
     port = _free_port()
     ps = [ctx.Process(target=_synth_worker, args=(r, world, port, n_tuples, n_q, gmax, backend, outq, preset, budget,
-                                                  back_budget, vis_mode, heavy)) for r in range(world)]
+                                                  back_budget, vis_mode, heavy, pack)) for r in range(world)]
     for p in ps:
         p.start()
     got = [outq.get(timeout=110) for _ in range(world)]
