@@ -35,12 +35,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 # independent random 16-B loads/s from HBM-sized tables (16-160 GiB) on one MI355X: tools/randprobe.hip,
 # profiles/r2_randprobe_sizes.jsonl (~37 G/s; the line, not the byte, is the unit of a random gather)
 RAND_REQ_PEAK = 37.0e9
-STREAM_KERNELS = {0: "k_stream<8,7,256,16>", 1: "k_stream<16,6,256,32>", 2: "k_stream<16,7,512,32>",
-                  3: "k_stream<32,5,192,64>", 4: "k_stream<32,6,256,64>", 5: "k_stream<32,wave1024/128,256,64>",
-                  6: "k_stream<32,wave1024/256,320,64>", 7: "k_stream<32,wave1024/64,256,64>",
-                  8: "k_stream<32,wave512/64,256,64>", 9: "k_stream2<9,256,64,64,1>",
-                  10: "k_stream3<9,256,64,64>", 11: "k_stream2<9,256,64,64,2>", 12: "k_stream2<9,256,64,0,1>", 13: "k_stream3<9,256,64,0>", 14: "k_stream2<9,256,64,0,2>",
-                  15: "k_stream4<9,256>", 16: "k_stream5<9,128>"}
+STREAM_KERNEL = "k_stream4<9,256>"
 
 
 def parse(argv=None):
@@ -58,11 +53,6 @@ def parse(argv=None):
     ap.add_argument("--batch", type=int, default=1_000_000, help="checks per step per GPU")
     ap.add_argument("--global-depth", type=int, default=10)
     ap.add_argument("--seed", type=int, default=20250131)
-    ap.add_argument("--tiers", type=int, default=0, help="kg_snapshot_tune tiers (0 grid, 1 LDS-WG+grid, 2 WG)")
-    ap.add_argument("--wide", type=int, default=0, help="kg_snapshot_tune wide (k_light<64> tier on/off)")
-    ap.add_argument("--stream", type=int, default=15, help="kg_snapshot_tune stream (k_stream variant 0..8, 9 = k_stream2, "
-                    "10 = k_stream3, 11 = k_stream2 with 128-edge windows, 12 = k_stream2 without the per-query "
-                    "expanded-node cap, 15 = k_stream4 over k_resolve's compact work list: default)")
     ap.add_argument("--stream-ecap", type=int, default=512, help="kg_snapshot_tune stream_ecap (stream-tier edges per query, 0 = none)")
     ap.add_argument("--shard-budget", type=int, default=0,
                     help="kg_snapshot_tune shard_budget (sharded mode: forward set edges per query and rank before "
@@ -86,19 +76,10 @@ def parse(argv=None):
     ap.add_argument("--resolve-unheld", type=int, default=1,
                     help="kg_snapshot_tune resolve_unheld (1: k_resolve skips the node map for subjects no row holds)")
     ap.add_argument("--stream-steal", type=int, default=4,
-                    help="kg_snapshot_tune stream_steal (XCD ranges a k_stream2 wave dequeues from, 1..8)")
+                    help="kg_snapshot_tune stream_steal (XCD ranges a k_stream4 wave dequeues from, 1..8)")
     ap.add_argument("--stream-chunk", type=int, default=64,
-                    help="kg_snapshot_tune stream_chunk (k_stream2 queries per dequeue, 1..64)")
+                    help="kg_snapshot_tune stream_chunk (k_stream4 queries per dequeue, 1..64)")
     ap.add_argument("--grid-wgs", type=int, default=4, help="kg_snapshot_tune grid_wgs (k_grid_level WGs per CU)")
-    ap.add_argument("--stream-tail-ecap", type=int, default=-1,
-                    help="kg_snapshot_tune stream_tail_ecap: k_stream4's edge budget once its work list is drained "
-                         "(queries past it go to the next tier; 0 off, -1 library default)")
-    ap.add_argument("--stream-order", type=str, default="",
-                    help="kg_snapshot_tune stream_order as LEN[:DEPTH]: k_resolve puts stream-tier queries whose "
-                         "root row has >= LEN set edges (and rest depth >= DEPTH) first in the work list (0 off)")
-    ap.add_argument("--stream-big-chunk", type=int, default=0,
-                    help="kg_snapshot_tune stream_big_chunk: k_stream4 claim size inside the stream_order front run "
-                         "(0 library default)")
     ap.add_argument("--grid-ms", type=int, default=1,
                     help="kg_snapshot_tune grid_ms: the grid tier's queries as a multi-source bit-parallel BFS "
                          "(64 queries per group) when dense per-node masks fit (graphs up to ~4 M nodes)")
@@ -112,8 +93,8 @@ def parse(argv=None):
                     help="kg_snapshot_tune grid_bidir: grid slots whose subject has <= this many holders "
                          "alternate forward and backward turns (0: forward only)")
     ap.add_argument("--stream-wgs", type=int, default=3,
-                    help="kg_snapshot_tune stream_wgs (k_stream WGs per CU, 0 = by variant: 5 for k_stream2's ~29 KiB "
-                         "WGs; 3 leaves LDS to the other batches in flight, best at --inflight 4: profiles/r2j_sweep.jsonl)")
+                    help="kg_snapshot_tune stream_wgs (k_stream4 WGs per CU; 3 leaves LDS to the other batches in "
+                         "flight, best at --inflight 4: profiles/r2j_sweep.jsonl)")
     ap.add_argument("--back", type=int, default=2, help="kg_snapshot_tune back (1 backward tier wave+WG widths, 2 wave width only, 0 off)")
     ap.add_argument("--back-wgs", type=int, default=None,
                     help="kg_snapshot_tune back_wgs (k_back WGs per CU; default 2 for C2/C4 with 4 batches in "
@@ -147,11 +128,12 @@ def parse(argv=None):
                     help="CPU-baseline threads (0 = os.cpu_count(), also timed at the affinity count, 16 and 1)")
     ap.add_argument("--preset", type=int, default=0,
                     help="0 = C2/C4 rewrite-free (headline); 1 = C3 (OPL view/edit/share via the rewrite interpreter)")
-    ap.add_argument("--mode", choices=["check", "expand", "sharded", "host", "refresh"], default="check",
+    ap.add_argument("--mode", choices=["check", "expand", "sharded", "host", "refresh", "rehearse"], default="check",
                     help="expand = config C5: batched BuildTree of hot group#member roots; sharded = the "
                          "hash-sharded mode (each rank holds 1/N of the graph, all-to-all frontier exchange); "
                          "host = the host-buffer boundary end to end: kg_check_batch over a snapshot replicated "
-                         "on every visible GPU (PCIe included), then the request batcher fed single checks")
+                         "on every visible GPU (PCIe included), then the request batcher fed single checks; "
+                         "rehearse = the multi-rank launch and aggregation alone on CPU ranks (gloo; tests)")
     ap.add_argument("--callers", type=int, default=4, help="--mode host: threads calling kg_check_batch at once")
     ap.add_argument("--clients", type=int, default=256,
                     help="--mode host: native caller threads of the request batcher (one blocking call per request)")
@@ -177,10 +159,7 @@ def parse(argv=None):
 def apply_tune(snap, a) -> None:
     """The engine knobs of the check bench (tests/test_gpu_check.py::test_bench_tune_set_vs_oracle runs
     the parity test with exactly this set)."""
-    snap.tune("tiers", a.tiers)
-    snap.tune("wide", a.wide)
     snap.tune("back", a.back)
-    snap.tune("stream", a.stream)
     snap.tune("stream_ecap", a.stream_ecap)
     if a.resolve_unheld != 1:
         snap.tune("resolve_unheld", a.resolve_unheld)
@@ -190,13 +169,6 @@ def apply_tune(snap, a) -> None:
         snap.tune("stream_chunk", a.stream_chunk)
     snap.tune("grid_wgs", a.grid_wgs)
     snap.tune("grid_bidir", a.grid_bidir)
-    if a.stream_tail_ecap >= 0:
-        snap.tune("stream_tail_ecap", a.stream_tail_ecap)
-    if a.stream_big_chunk:
-        snap.tune("stream_big_chunk", a.stream_big_chunk)
-    if a.stream_order:
-        ln, _, dp = a.stream_order.partition(":")
-        snap.tune("stream_order", int(ln) | (int(dp or 0) << 16))
     snap.tune("grid_ms", a.grid_ms)
     snap.tune("grid_ms_words", a.grid_ms_words)
     snap.tune("grid_ms_tg_cap", a.grid_ms_tg_cap)
@@ -587,7 +559,6 @@ def bench_host(a):
     t_build = time.time()
     snap, _ = build_synthetic(a, a.tuples, devices=devices)
     snap.tune("host_sync", a.host_sync)
-    snap.tune("stream", a.stream)
     snap.tune("stream_wgs", a.stream_wgs)
     snap.tune("back_wgs", a.back_wgs)
     snap.tune("grid_wgs", a.grid_wgs)
@@ -757,8 +728,76 @@ def aggregate(dist, elapsed: float, edges: float, device=None):
     return float(t[0].item()), float(e[0].item())
 
 
+def spawn_ranks(a, argv) -> int:
+    """`bench.py --gpus N` (N > 1) started without a launcher: this process becomes a launcher that never
+    touches the GPU.  It starts N children -- this script with the same arguments and RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_ADDR / MASTER_PORT set, one per GPU, the environment torch.distributed.run
+    gives its workers -- forwards rank 0's stdout (its one JSON line), and exits non-zero if any rank
+    fails (the other ranks are then killed: they would wait in a collective forever)."""
+    import signal
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    procs = []
+    for r in range(a.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(a.gpus), LOCAL_WORLD_SIZE=str(a.gpus),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env,
+                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
+    chunks = []  # rank 0's stdout, read beside the wait loop (a failed rank must not block the launcher)
+    reader = threading.Thread(target=lambda: chunks.append(procs[0].stdout.read()), daemon=True)
+    reader.start()
+    rc = 0
+    pending = list(procs)
+    while pending:
+        for p in list(pending):
+            c = p.poll()
+            if c is None:
+                continue
+            pending.remove(p)
+            if c != 0 and rc == 0:
+                rc = c if c > 0 else 128 - c
+                for q in pending:  # exact children of this launcher
+                    q.send_signal(signal.SIGTERM)
+        time.sleep(0.05)
+    reader.join(30)
+    out = b"".join(chunks).decode(errors="replace")
+    sys.stdout.write(out)
+    sys.stdout.flush()
+    return rc
+
+
+def bench_rehearse(a):
+    """--mode rehearse: the multi-rank contract without a GPU -- every rank joins a gloo group, times K
+    empty steps between barriers and reports fixed per-rank work; rank 0 prints the JSON line of the
+    whole job (max elapsed over ranks, work summed), as the GPU modes do."""
+    import torch.distributed as dist
+    rank, world = int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dist.barrier()
+    t = time.perf_counter()
+    units = float(a.batch * a.steps)
+    if world > 1:
+        dist.barrier()
+    elapsed, total = aggregate(dist if world > 1 else None, time.perf_counter() - t, units)
+    if rank == 0:
+        print(json.dumps({"metric": "rehearsal (no GPU)", "value": total / max(elapsed, 1e-9), "unit": "units/s",
+                          "n_gpus": world, "steps": a.steps, "warmup": a.warmup, "units": total,
+                          "config": {"parallelism": f"replica{world}"}}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     a = parse()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ and a.mode != "host":
+        # no launcher around us: become one (one process per GPU; host mode spans the GPUs in-library)
+        sys.exit(spawn_ranks(a, sys.argv[1:]))
+    if a.mode == "rehearse":
+        return bench_rehearse(a)
     if a.hw_queues > 0:  # before anything initialises HIP (torch and the library load lazily)
         os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, a.hw_queues))
     if a.mode == "expand":
@@ -879,7 +918,7 @@ def main():
     l_ms = np.array([s.light_ms for s in stats], float)
     achieved = float(l_bytes.mean() / (l_ms.mean() * 1e-3) / 1e9)
     req_rate = float(l_reqs.mean() / (l_ms.mean() * 1e-3))
-    traffic = pmc_traffic(STREAM_KERNELS[a.stream], int(a.tuples), B, a.preset, P)
+    traffic = pmc_traffic(STREAM_KERNEL, int(a.tuples), B, a.preset, P)
 
     # ---- latency phase (outside the timed region): the same P batches in flight, every batch waited for
     # (submit -> results on the host side of the stream), distinct query batches
@@ -946,7 +985,7 @@ def main():
         "edges_per_batch": {q: float(np.percentile([x.edges_read for x in stats], v)) for q, v in
                             (("p50", 50), ("p90", 90), ("max", 100))},
         "allowed_fraction": float(res.mean()),
-        "tiers": {"light": int(stats[-1].n_light), "wide": int(stats[-1].n_wide), "medium": int(stats[-1].n_medium),
+        "tiers": {"light": int(stats[-1].n_light),
                   "back": int(stats[-1].n_back), "grid": int(stats[-1].n_grid), "heavy": int(stats[-1].n_heavy),
                   "general": int(stats[-1].n_general), "no_holder": int(stats[-1].n_no_holder)},
         "work_per_batch": {"light": {"rows": int(stats[-1].light_rows_opened), "edges": int(stats[-1].light_edges_read),
@@ -956,7 +995,7 @@ def main():
                            "back": {"rows": int(stats[-1].back_rows), "edges": int(stats[-1].back_edges)}},
         "stream_diag": stream_diag(stats[-1]),
         "snapshot_build_s": t_build,
-        "roofline": {"kernel": STREAM_KERNELS[a.stream], "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "roofline": {"kernel": STREAM_KERNEL, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "bytes_model": "8*rows_opened + 4*edges_read + 16*direct_probes (per k_stream launch; R/E/P counted in-kernel)",
                      "launch_ms": float(l_ms.mean()), "bytes_per_launch": float(l_bytes.mean()),

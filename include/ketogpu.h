@@ -93,21 +93,21 @@ typedef struct {
   uint64_t edges_read;
   uint64_t direct_probes;
   uint64_t frontier_hbm;
-  uint64_t n_light, n_heavy, n_general; /* queries finished per engine tier */
-  uint64_t n_medium;
-  uint64_t light_rows_opened, light_edges_read, light_probes; /* k_light's share of the counters */
+  uint64_t n_light, n_heavy, n_general; /* queries finished by the stream tier / reaching the grid tier / the interpreter */
+  uint64_t n_medium;                    /* reserved (0) */
+  uint64_t light_rows_opened, light_edges_read, light_probes; /* the stream tier's (k_stream4's) share of the counters */
   double kernel_ms;                     /* device time of the whole batch (HIP events)  */
-  double light_ms;                      /* device time of the k_light<16> launch         */
-  uint64_t n_wide;                      /* queries handed from k_light<16> to k_light<64> */
+  double light_ms;                      /* device time of the k_stream4 launch           */
+  uint64_t n_wide;                      /* reserved (0) */
   uint64_t n_grid;                      /* queries resolved by the grid tier             */
   uint64_t n_back;                      /* queries resolved by the backward tier         */
   uint64_t n_no_holder;                 /* queries answered NotMember by k_resolve: no row holds the subject */
   uint64_t back_rows, back_edges;       /* backward tier: parent lists opened / parents read */
-  uint64_t light_steps;                 /* k_stream: wave steps (one HBM round trip each) */
-  uint64_t light_waves;                 /* k_stream: waves that ran                      */
-  uint64_t light_wave_ticks;            /* k_stream: sum of wave lifetimes (100 MHz ticks) */
-  uint64_t light_span_ticks;            /* k_stream2: first wave start to last wave end  */
-  uint64_t light_wave_max_ticks;        /* k_stream2: longest wave lifetime              */
+  uint64_t light_steps;                 /* k_stream4: wave steps (one HBM round trip each) */
+  uint64_t light_waves;                 /* k_stream4: waves that ran                     */
+  uint64_t light_wave_ticks;            /* k_stream4: sum of wave lifetimes (100 MHz ticks) */
+  uint64_t light_span_ticks;            /* k_stream4: first wave start to last wave end  */
+  uint64_t light_wave_max_ticks;        /* k_stream4: longest wave lifetime              */
 } kg_stats;
 
 /* Per-query outputs of kg_check_batch. */
@@ -203,28 +203,11 @@ int kg_snapshot_info(const kg_snapshot* s, uint64_t* info4);
  * itself), [2] check-row entries (the direct tuples the union nodes hold).  KG_MATERIALIZE=0 in
  * the environment at snapshot creation turns it off. */
 int kg_snapshot_materialized(const kg_snapshot* s, uint64_t* out3);
-/* Engine knobs (no reference counterpart; tuning and tests).  key "tiers": where queries that
- * overflow the wave tiers go -- 0 = grid tier (default), 1 = LDS workgroup tier then grid tier,
- * 2 = LDS workgroup tier then one-workgroup-per-query HBM tier.  key "light": the first wave
- * tier -- 0 = k_stream (many queries per wave over one FIFO, default), 1 = k_light<16> (four
- * 16-lane groups per wave).  key "wide": 1 = k_light<64> (one query per wave, 256 expanded
- * nodes) takes the first tier's overflow, 0 = the overflow goes straight on (default).  Results never
- * depend on any of them.  key "back": 1 = the backward tier (reverse search from the subject's
- * holders, one wave per query, then one workgroup per query) takes the wave tiers' overflow before the grid tier, and
- * k_resolve answers queries whose subject no row holds; 2 = the same with the wave width only
- * (its overflow goes straight to the grid tier; default); 0 = off.  key "stream": stream-tier
- * kernel -- 15 = k_stream4 (default: k_resolve writes the stream tier's queries as compact records
- * into 8 per-XCD shards, and a wave dequeues the next chunk while it walks the current one), 12 =
- * k_stream2 (32 query slots per wave over one FIFO, direct-mapped visited cache, a query bounded by
- * its edge budget), 9 = the same with a cap of 64 expanded nodes per query,
- * 11 = 128-edge windows, 10 = k_stream3 (software-pipelined), 0..8 = the round-1 k_stream variants,
- * 16 = k_stream5 (two interleaved FIFO engines per wave; measured flat against 15).
- * key "stream_tail_ecap" (default 0 = off): a k_stream4 wave whose work list is drained hands each
- * query past this many edges to the backward / grid tiers (shortens the launch's tail; measured slower
- * overall).  key "stream_order" (LEN | DEPTH << 16, default 0 = off): k_resolve puts
- * stream-tier queries whose root row has >= LEN set edges and rest depth >= DEPTH first in the work
- * list, and k_stream4 claims them "stream_big_chunk" (1..64, default 4) at a time (measured level or
- * slower).
+/* Engine knobs (no reference counterpart; tuning and tests).  Results never depend on any of them.
+ * key "back": 1 = the backward tier (reverse search from the subject's holders, one wave per query,
+ * then one workgroup per query) takes the stream tier's overflow before the grid tier, and k_resolve
+ * answers queries whose subject no row holds; 2 = the same with the wave width only (its overflow
+ * goes straight to the grid tier; default); 0 = off.
  * key "stream_ecap": edges a query may enqueue in the stream tier before it is handed to the
  * backward / grid tiers (default 512; 0 = no budget) -- cuts the stream kernel's tail of long walks.
  * key "resolve_unheld" (0/1): without a namespace program, k_resolve reads a subject id's holder
@@ -232,10 +215,10 @@ int kg_snapshot_materialized(const kg_snapshot* s, uint64_t* out3);
  * key "device_sync" (0/1): the same for kg_check_batch_device when it waits (stats or a grid-tier
  * readback; default 1: asleep -- 5.6 -> 5.8 x 10^9 checks/s with 4 batches in flight).  key "host_sync" (0/1): kg_check_batch waits for its device work asleep on a blocking-sync event
  * (1, default: no core spins per in-flight batch) or spinning in hipStreamSynchronize (0).
- * key "stream_steal" (1..8): XCD ranges of the work list a k_stream2 wave dequeues from (default 4:
+ * key "stream_steal" (1..8): XCD ranges of the work list a k_stream4 wave dequeues from (default 4:
  * when the list drains every wave walks them, one atomic each on a few hot words).
- * key "stream_chunk" (1..64): queries a k_stream2 wave dequeues at once (default 64).
- * key "stream_wgs": k_stream workgroups per CU (0 = by variant; default 3); "back_wgs" (1..3, default 2)
+ * key "stream_chunk" (1..64): queries a k_stream4 wave dequeues at once (default 64).
+ * key "stream_wgs": k_stream4 workgroups per CU (0 = 3; default 3); "back_wgs" (1..3, default 2)
  * and "grid_wgs" (1..64, default 4): k_back / k_grid_level workgroups per CU (defaults = bench.py's C2 set).  key "shard_vis": log2 of the
  * hash-sharded mode's per-batch (query, node) visited table (default 25).  key "interp_cap2"
  * (0..4194304): BFS list cap of the rewrite interpreter's many-slot HBM pass (0 = 256 Ki nodes);

@@ -402,45 +402,14 @@ int kg_snapshot_materialized(const kg_snapshot* sp, uint64_t* out3) {
 
 static int tune_one(Snapshot* s, const char* key, int64_t value) {
   std::lock_guard<std::mutex> lk(s->mu);
-  if (strcmp(key, "tiers") == 0) {
-    if (value < 0 || value > 2) return set_error(-2, "tiers must be 0, 1 or 2");
-    s->tiers = (int)value;
-    return 0;
-  }
-  if (strcmp(key, "wide") == 0) {
-    if (value < 0 || value > 1) return set_error(-2, "wide must be 0 or 1");
-    s->wide_tier = (int)value;
-    return 0;
-  }
   if (strcmp(key, "shard_vis") == 0) {
     if (value < 10 || value > 34) return set_error(-2, "shard_vis must be in [10, 34]");
     s->shard_vis_log2 = (int)value;
     return 0;
   }
-  if (strcmp(key, "stream") == 0) {
-    if (value < 0 || value > 16) return set_error(-2, "stream must be in [0, 16]");
-    s->stream_variant = (int)value;
-    return 0;
-  }
-  if (strcmp(key, "stream_order") == 0) {  // low 16 bits: root row length, bits 16..23: rest depth
-    if (value < 0 || value >= (1ll << 24)) return set_error(-2, "stream_order must be in [0, 2^24)");
-    s->stream_big_len = (uint32_t)(value & 0xFFFF);
-    s->stream_big_depth = (int32_t)(value >> 16);
-    return 0;
-  }
   if (strcmp(key, "shard_pack") == 0) {
     if (value < 0 || value > 1) return set_error(-2, "shard_pack must be 0 or 1");
     s->shard_pack = (int)value;
-    return 0;
-  }
-  if (strcmp(key, "stream_big_chunk") == 0) {
-    if (value < 1 || value > 64) return set_error(-2, "stream_big_chunk must be in [1, 64]");
-    s->stream_big_chunk = (uint32_t)value;
-    return 0;
-  }
-  if (strcmp(key, "stream_tail_ecap") == 0) {
-    if (value < 0 || value > 0xFFFFFFFFll) return set_error(-2, "stream_tail_ecap must be in [0, 2^32)");
-    s->stream_tail_ecap = (uint32_t)value;
     return 0;
   }
   if (strcmp(key, "stream_ecap") == 0) {
@@ -578,11 +547,6 @@ static int tune_one(Snapshot* s, const char* key, int64_t value) {
   if (strcmp(key, "back") == 0) {
     if (value < 0 || value > 2) return set_error(-2, "back must be 0, 1 or 2");
     s->back_tier = (int)value;
-    return 0;
-  }
-  if (strcmp(key, "light") == 0) {
-    if (value < 0 || value > 1) return set_error(-2, "light must be 0 or 1");
-    s->light_tier = (int)value;
     return 0;
   }
   return set_error(-2, "unknown knob '%s'", key);

@@ -49,8 +49,6 @@ struct Workspace {
   void* scratch = nullptr;
   size_t scratch_bytes = 0;
   size_t scratch_n = 0;  // queries the scratch was last sized for
-  void* heavy_pool = nullptr;
-  size_t heavy_pool_bytes = 0;
   GridPool grid;  // grid tier, sized for the queries that reach it (16 Mi log entries)
   GridPool ms;    // the grid tier's MS-BFS path (kg_msbfs.hip): dense masks of its query groups
   bool grid_reran = false;  // the last batch's grid tier ran rounds after the first (results rewritten)
@@ -72,7 +70,7 @@ struct BatchPending {
   kg_stats* stats = nullptr;
   uint8_t* d_out = nullptr;
   uint32_t* d_err = nullptr;
-  bool grid_pending = false, wg_heavy = false;
+  bool grid_pending = false;
   const uint32_t *grid_list = nullptr, *grid_count = nullptr;
   const RQuery* rq = nullptr;
   int32_t gdepth = 5;
@@ -213,9 +211,6 @@ struct Snapshot {
   std::mutex ws_mu;
   std::vector<Workspace*> wss;
   Workspace* workspace(hipStream_t st);  // finds or creates the workspace of stream st (NULL = stream)
-  int wide_tier = 0;       // kg_snapshot_tune("wide"): 1 = k_light<64> between k_stream and the rest
-  int tiers = 0;       // kg_snapshot_tune("tiers")
-  int light_tier = 0;  // kg_snapshot_tune("light"): 0 k_stream, 1 k_light<16>  // grid tier visited-table epoch (kg_grid.hip)
   uint64_t batch_seq = 0;
   uint32_t shard_rank = 0, shard_n = 1;  // hash-sharded mode (set before create)
   // per-stream batch state of the hash-sharded mode (kg_shard.hip), so batches on different streams
@@ -231,32 +226,30 @@ struct Snapshot {
   int shard_vis_mode = 0;  // kg_snapshot_tune("shard_vis_mode"): (query, node) dedup 0 = exact CAS table, 1 = lossy cache
   uint32_t shard_budget = 0;       // kg_snapshot_tune("shard_budget"): forward set edges per query and rank (0 = off)
   uint32_t shard_back_budget = 1u << 14;  // kg_snapshot_tune("shard_back_budget"): reverse edges per query and rank
-  int stream_variant = 15;  // kg_snapshot_tune("stream"): k_stream variant (0..8), 9 / 11 / 12 = k_stream2, 10 = k_stream3, 15 = k_stream4
   int back_tier = 2;  // kg_snapshot_tune("back"): backward tier (1: wave + workgroup widths, 2: wave only) + no-holder filter
   uint32_t stream_ecap = 512;  // kg_snapshot_tune("stream_ecap"): stream-tier edge budget per query (0 = none)
   int resolve_unheld = 1;  // kg_snapshot_tune("resolve_unheld"): k_resolve reads the holder bit before the node map
-  uint32_t stream_steal = 4;   // kg_snapshot_tune("stream_steal"): XCD ranges a k_stream2 wave dequeues from (1..8)
-  uint32_t stream_big_len = 0;    // kg_snapshot_tune("stream_order"): root rows of >= this many set edges go first (0 = off)
-  int32_t stream_big_depth = 0;   // ... together with a rest depth >= this (the tune's value >> 16)
-  uint32_t stream_big_chunk = 4;  // kg_snapshot_tune("stream_big_chunk"): k_stream4 claim size inside the front run
-  uint32_t stream_tail_ecap = 0;  // kg_snapshot_tune("stream_tail_ecap"): k_stream4's edge budget once the list is drained (0 = off)
-  uint32_t stream_chunk = 64;  // kg_snapshot_tune("stream_chunk"): k_stream2 queries per dequeue (1..64)
-  int grid_wgs = 4;          // kg_snapshot_tune("grid_wgs"): k_grid_level workgroups per CU (bench default)
+  uint32_t stream_steal = 4;   // kg_snapshot_tune("stream_steal"): XCD ranges a k_stream4 wave dequeues from (1..8)
+  uint32_t stream_chunk = 64;  // kg_snapshot_tune("stream_chunk"): k_stream4 queries per dequeue (1..64)
+  // Occupancy defaults (library-wide, measured with several batches in flight, the way a server keeps
+  // them: C2 and C3 A/Bs in profiles/r2gw_tier_wgs_sweep.jsonl, r2v_occupancy_sweep.jsonl,
+  // r2bw_back_wgs_ab.jsonl; a one-batch-at-a-time caller loses < 5 % with them)
+  int grid_wgs = 4;          // kg_snapshot_tune("grid_wgs"): k_grid_level workgroups per CU
   int device_sync = 1;      // kg_snapshot_tune("device_sync"): kg_check_batch_device waits asleep (1) or spinning (0)
   int host_sync = 1;        // kg_snapshot_tune("host_sync"): kg_check_batch waits asleep (1) or spinning (0)
-  int stream_wgs = 3;        // kg_snapshot_tune("stream_wgs"): k_stream workgroups per CU (0 = by LDS; 3 = bench default)
+  int stream_wgs = 3;        // kg_snapshot_tune("stream_wgs"): k_stream4 workgroups per CU (3 leaves LDS to other batches)
   int interp_wgs = 6;        // kg_snapshot_tune("interp_wgs"): k_interp_lds workgroups (4 waves) per CU (6 fit the LDS)
   uint32_t interp_cap2 = 0;  // kg_snapshot_tune("interp_cap2"): pass-2 BFS list cap of the rewrite path (0 = 256 Ki)
-  int back_wgs = 2;          // kg_snapshot_tune("back_wgs"): k_back workgroups per CU (1..3, LDS allows 3; 2 = bench C2 default)
+  int back_wgs = 2;          // kg_snapshot_tune("back_wgs"): k_back workgroups per CU (1..3, LDS allows 3; C3 prefers 1)
   uint64_t grid_small_cap = 0;  // kg_snapshot_tune("grid_cap"): workspace grid-log entries (0 = 16 Mi; tests)
   int expand_tail = 1;  // kg_snapshot_tune("expand_tail"): expand passes 2/3 walk with LDS-cached frames (0: round 2)
   int grid_ms = 1;  // kg_snapshot_tune("grid_ms"): grid-tier queries as MS-BFS when the dense masks fit (0: off)
   size_t grid_ms_bytes = 1ull << 30;  // kg_snapshot_tune("grid_ms_bytes"): MS-BFS mask budget per workspace
-  int grid_ms_words = 8;
-  uint32_t grid_ms_tg_cap = 256;  // kg_snapshot_tune("grid_ms_tg_cap"): holders above which MS-BFS probes dset instead  // kg_snapshot_tune("grid_ms_words"): 64-bit words per MS-BFS mask (64 queries each)
+  int grid_ms_words = 8;     // kg_snapshot_tune("grid_ms_words"): 64-bit words per MS-BFS mask (64 queries each)
+  uint32_t grid_ms_tg_cap = 256;  // kg_snapshot_tune("grid_ms_tg_cap"): holders above which MS-BFS probes dset instead
   uint64_t grid_ms_cap = 0;  // kg_snapshot_tune("grid_ms_cap"): MS-BFS entries per level buffer (0 = 16 Mi; tests)
-  int grid_bidir = 0;  // kg_snapshot_tune("grid_bidir"): grid slots whose subject has <= this many holders go bidirectional (0: none)
-                       // alternate forward and backward turns (0: forward only)
+  int grid_bidir = 0;  // kg_snapshot_tune("grid_bidir"): grid slots whose subject has <= this many holders alternate
+                       // forward and backward turns (0: none, forward only)
   // replicas: the same snapshot on more devices (kg_snapshot_create's device mask); this object is
   // replica 0 and owns the others.  Host-buffer batches and expands are split over all of them.
   std::vector<Snapshot*> peers;

@@ -273,7 +273,6 @@ Workspace::~Workspace() {
   if (device >= 0) hipSetDevice(device);
   if (sync_ev) hipEventDestroy(sync_ev);
   if (scratch) hipFree(scratch);
-  if (heavy_pool) hipFree(heavy_pool);
   grid.release();
   ms.release();
   if (interp_pool) hipFree(interp_pool);

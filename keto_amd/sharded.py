@@ -251,6 +251,7 @@ class ShardedChecker:
         self._prune = None
         self.general_queries = 0
         self.general_rows = 0
+        self.reruns = {1: 0, 2: 0}  # batches rerun after a bucket (1) / visited-table (2) overflow
 
     def _install_held(self):
         """Once per snapshot: the OR of every rank's holder bitmap, so kg_shard_seed's no-holder test
@@ -556,6 +557,8 @@ class ShardedChecker:
                 torch.cuda.current_stream().wait_stream(ts)
                 return res, err
             except ShardOverflow as e:  # every rank saw the same flags: all rerun with more room
+                for f in (1, 2):
+                    self.reruns[f] += 1 if e.flags & f else 0
                 if e.flags & 1:
                     self.cap *= 2
                 if e.flags & 2:
@@ -573,10 +576,18 @@ class ShardedChecker:
         # result slots: the queries, then the parts of formula-split queries (kg_shard_result_slots)
         slots = self.ops.result_slots(n) if hasattr(self.ops, "result_slots") else n
         self._n = slots
-        prune = self._pruning()
         # escalation: forward done bits carry escalated queries; backward and final forward phases follow
         backward = hasattr(self.ops, "back_level") and getattr(self.ops, "escalates", True)
         self.back_levels = self.final_levels = 0
+        fixed = self.dist is not None and hasattr(self.ops, "level_seg") and \
+            (self.protocol == "fixed" or (self.protocol == "auto" and not backward))
+        if fixed:  # decided before any buffer or seed of the other protocols
+            if backward:
+                raise ValueError("the fixed-bucket protocol has no backward escalation phase")
+            res = torch.zeros(slots, dtype=torch.uint8, device=self.device)
+            err = torch.zeros(slots, dtype=torch.int32, device=self.device)
+            return self._check_fixed(dq, n, slots, gdepth, res, err)
+        prune = self._pruning()
         final = False
         bufs = [torch.empty((N * cap, REC_WORDS), dtype=torch.int32, device=self.device) for _ in range(2)]
         counts = [torch.zeros(N + 1, dtype=torch.int32, device=self.device) for _ in range(2)]
@@ -624,12 +635,6 @@ class ShardedChecker:
             if not self.general:
                 self.ops.finish(n, res, err)
             return res[:n], err[:n]
-        fixed = (self.dist is not None and hasattr(self.ops, "level_seg")
-                 and (self.protocol == "fixed" or (self.protocol == "auto" and not backward)))
-        if fixed:
-            if backward:
-                raise ValueError("the fixed-bucket protocol has no backward escalation phase")
-            return self._check_fixed(dq, n, slots, gdepth, res, err)
         while True:
             send, recv_splits, total, flags = self._meta_exchange(counts[cur])
             if flags & 3:
@@ -661,21 +666,21 @@ class ShardedChecker:
     # ---- fixed-bucket protocol (world > 1): no host round trip inside a batch
     def _max_slots(self, slots: int) -> int:
         """The largest result-slot count of any rank (it sizes the done bitmap and the first bucket, which
-        every rank must agree on), cached per slot count: one all-reduce the first time a rank sees a
-        batch of this size."""
+        every rank must agree on): one small all-reduce on EVERY batch.  Ranks' slot counts differ and
+        change from batch to batch, so a per-rank cache would let one rank skip the collective another
+        rank issues (a mismatched collective).  The same all-reduce carries "some rank can
+        end a check in an error" (_pruning), this rank's part of which is asked once."""
         import torch
-        cache = self.__dict__.setdefault("_slots_cache", {})
-        if slots not in cache:
-            # the same all-reduce carries "some rank can end a check in an error" the first time (_pruning)
-            mine = bool(self.ops.errors_possible()) if self._prune is None and hasattr(self.ops, "errors_possible") else False
-            t = torch.tensor([slots, int(mine)], dtype=torch.int64, device="cpu" if self._host_staged() else self.device)
-            self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX, group=self.group)
-            self.host_syncs += 1
-            h = t.cpu().numpy()
-            cache[slots] = int(h[0])
-            if self._prune is None:
-                self._prune = hasattr(self.ops, "done_bits") and not bool(h[1])
-        return cache[slots]
+        if not hasattr(self, "_errors_mine"):
+            self._errors_mine = bool(self.ops.errors_possible()) if hasattr(self.ops, "errors_possible") else False
+        t = torch.tensor([slots, int(self._errors_mine)], dtype=torch.int64,
+                         device="cpu" if self._host_staged() else self.device)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX, group=self.group)
+        self.host_syncs += 1
+        h = t.cpu().numpy()
+        if self._prune is None:
+            self._prune = hasattr(self.ops, "done_bits") and not bool(h[1])
+        return int(h[0])
 
     def _check_fixed(self, dq, n: int, slots: int, gdepth: int, res, err):
         """gdepth + 1 levels (a record's rest depth falls by one per level and seeds carry <= gdepth; the
@@ -741,6 +746,7 @@ class ShardedChecker:
         big = int(h[2])
         if flags & 3:
             if flags & 1:
+                self.reruns[1] += 1
                 self.bucket = max(2 * B, int(big * 1.25) + 1024)
                 self.cap = max(self.cap, self.bucket)
             raise ShardOverflow(flags & 2)  # a bucket overflow is handled here (bigger buckets); 2 = visited

@@ -19,7 +19,7 @@ def test_defaults_and_tune_set():
     assert a.parity >= 1_000_000 and a.latency_batches >= 200
     s = _FakeSnap()
     bench.apply_tune(s, a)
-    for k in ("stream", "stream_ecap", "stream_steal", "back_wgs", "stream_wgs", "grid_wgs", "grid_reserve",
+    for k in ("stream_ecap", "stream_steal", "back_wgs", "stream_wgs", "grid_wgs", "grid_reserve",
               "device_sync"):
         assert k in s.tuned, k
     c3 = bench.parse(["--preset", "1"])

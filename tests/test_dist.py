@@ -46,3 +46,17 @@ def test_single_rank_passthrough():
     sys.path.insert(0, ROOT)
     import bench
     assert bench.aggregate(None, 3.5, 7.0) == (3.5, 7.0)
+
+
+def test_bench_spawns_ranks_without_launcher():
+    """`bench.py --gpus 3` with no WORLD_SIZE in the environment starts 3 ranks itself (the parent never
+    touches a GPU) and forwards rank 0's whole-job line: n_gpus 3, work summed over the 3 ranks."""
+    import json
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "3", "--mode", "rehearse",
+                        "--steps", "5", "--batch", "100"], env=env, capture_output=True, timeout=180)
+    assert r.returncode == 0, r.stderr.decode()[-2000:]
+    line = json.loads(r.stdout.decode().strip().splitlines()[-1])
+    assert line["n_gpus"] == 3 and line["config"]["parallelism"] == "replica3"
+    assert line["units"] == 3 * 5 * 100

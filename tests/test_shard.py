@@ -112,6 +112,54 @@ def test_sharded_protocol_gloo(world, cap, budget, back_budget, protocol):
         assert 0 < exp.mean() < 1
 
 
+ASYM_SIZES = [(10, 250), (10, 5), (300, 5), (0, 200), (150, 0), (150, 37), (37, 37)]  # per call: (rank 0, rank 1)
+
+
+def _cpu_asym_worker(rank, world, port, seed, outq, protocol):
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import torch.distributed as dist
+    from keto_amd.sharded import ShardedChecker
+    from shard_ref import CpuShardOps
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    it, t6, q = _graph(seed)
+    chk = ShardedChecker(CpuShardOps(t6, it.wildcard_rel, rank, world), rank, world, dist, device="cpu", cap=1 << 12,
+                         protocol=protocol)
+    out = []
+    for sizes in ASYM_SIZES:
+        lo = sum(sizes[:rank])
+        mine = np.arange(lo, lo + sizes[rank])
+        res, err = chk.check(torch.from_numpy(q[mine].view(np.int32).copy().reshape(-1, 7)), 4)
+        out.append((mine, res.numpy().copy(), err.numpy().copy()))
+    outq.put((rank, out))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("protocol", ["fixed", "dynamic"])
+def test_sharded_asymmetric_batches_gloo(protocol):
+    """Per-rank batch sizes that differ and change asymmetrically from call to call (a rank with no
+    query at all included): every rank must issue the same collectives in the same order on every
+    batch (a per-rank cache of the slot count let one rank skip an all-reduce another rank
+    issued), and the answers equal the oracle's."""
+    ctx = mp.get_context("spawn")
+    outq = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_cpu_asym_worker, args=(r, 2, port, 4, outq, protocol)) for r in range(2)]
+    for p in ps:
+        p.start()
+    got = [outq.get(timeout=240) for _ in range(2)]
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    it, t6, q = _graph(4)
+    exp = _expected(t6, it.wildcard_rel, q, 4)
+    for _, out in got:
+        for mine, r, e in out:
+            assert (e == 0).all() and (r == exp[mine]).all(), mine[:5]
+
+
 def test_owner_matches_library():
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from keto_amd import _lib
@@ -448,7 +496,7 @@ def test_sharded_general_rewrites_vs_oracle(kind, world):
 
 # ------------------------------------------------------------------ config C4 generator, sharded
 def _synth_worker(rank, world, port, n_tuples, n_q, gmax, backend, outq, preset=0, budget=None, back_budget=None,
-                  vis_mode=0, heavy=None, pack=None):
+                  vis_mode=0, heavy=None, pack=None, vis=None, bucket=None):
     sys.path.insert(0, ROOT)
     import torch.distributed as dist
     from keto_amd import _lib
@@ -471,16 +519,22 @@ def _synth_worker(rank, world, port, n_tuples, n_q, gmax, backend, outq, preset=
         snap.tune("shard_heavy", heavy)
     if pack is not None:
         snap.tune("shard_pack", pack)
+    if vis is not None:  # a per-batch visited table of 2^vis (query, node) keys: overflows, reruns larger
+        snap.tune("shard_vis", vis)
     dq = torch.empty((n_q, 7), dtype=torch.int32, device="cuda")
     _lib.check(_lib.load().kg_synth_queries(snap.handle, 31, n_q, dq.data_ptr()), "kg_synth_queries")
     mine = np.array_split(np.arange(n_q), world)[rank]
     chk = ShardedChecker(HipShardOps(snap), rank, world, dist_, device="cuda", cap=1 << 14)
+    if bucket is not None:  # fixed-bucket protocol: B records per destination, far too few
+        chk.bucket = bucket
     mq = dq[mine[0]:mine[-1] + 1].contiguous()
-    chk.check(mq, gmax)  # the first batch grows the buckets to fit (overflow reruns)
+    res0, err0 = chk.check(mq, gmax)  # the first batch grows the buckets to fit (overflow reruns)
+    res0, err0 = res0.cpu().numpy(), err0.cpu().numpy()
     s0 = chk.host_syncs
     res, err = chk.check(mq, gmax)
+    assert (res.cpu().numpy() == res0).all() and (err.cpu().numpy() == err0).all()  # the rerun batch = a clean one
     outq.put((rank, mine, res.cpu().numpy(), err.cpu().numpy(), chk.levels, chk.host_syncs - s0,
-              dq.cpu().numpy() if rank == 0 else None, snap.materialized(), chk.back_levels))
+              dq.cpu().numpy() if rank == 0 else None, snap.materialized(), chk.back_levels, dict(chk.reruns)))
     if dist_:
         dist.destroy_process_group()
 
@@ -533,14 +587,15 @@ def test_sharded_c3_rewrites_vs_oracle(world, backend):
 
 
 def _run_synth(world, backend, n_tuples, n_q, gmax, preset, budget=None, back_budget=None, vis_mode=0, heavy=None,
-               pack=None):
+               pack=None, vis=None, bucket=None):
     from keto_amd.engine import Snapshot
     from oracle.oracle import POLICY_CANONICAL, Oracle
     ctx = mp.get_context("spawn")
     outq = ctx.Queue()
     port = _free_port()
     ps = [ctx.Process(target=_synth_worker, args=(r, world, port, n_tuples, n_q, gmax, backend, outq, preset, budget,
-                                                  back_budget, vis_mode, heavy, pack)) for r in range(world)]
+                                                  back_budget, vis_mode, heavy, pack, vis, bucket))
+          for r in range(world)]
     for p in ps:
         p.start()
     got = [outq.get(timeout=110) for _ in range(world)]
@@ -553,7 +608,7 @@ def _run_synth(world, backend, n_tuples, n_q, gmax, preset, budget=None, back_bu
     exp, oerr, _ = o.check_batch(q[:, :6], q[:, 6].view(np.int32), gmax, POLICY_CANONICAL, nthreads=8)
     assert (oerr == 0).all()
     res = np.zeros(n_q, np.uint8)
-    for rank, mine, r, e, levels, syncs, _, mat, back_levels in got:
+    for rank, mine, r, e, levels, syncs, _, mat, back_levels, reruns in got:
         assert (e == 0).all(), (rank, np.nonzero(e)[0][:10])
         res[mine] = r
         if world == 1 and backend is None:
@@ -562,9 +617,28 @@ def _run_synth(world, backend, n_tuples, n_q, gmax, preset, budget=None, back_bu
             assert back_levels > 0  # the backward phase ran
         if preset:
             assert mat["union_nodes"] > 0, mat
+        if vis is not None:
+            assert reruns[2] >= 1, reruns  # the visited table overflowed and the batch reran
+        if bucket is not None:
+            assert reruns[1] >= 1, reruns  # a bucket overflowed and the batch reran with bigger ones
     bad = np.nonzero(res != exp)[0]
     assert bad.size == 0, [(q[i].tolist(), int(res[i]), int(exp[i])) for i in bad[:8]]
     assert 0.05 < exp.mean() < 0.95
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,backend,vis,bucket", [(1, None, 10, None), (2, "gloo", 10, None),
+                                                      (2, "gloo", None, 64), (1, "nccl", 11, None)])
+def test_sharded_visited_overflow_reruns(world, backend, vis, bucket):
+    """Regression (round 3: "records left after 10 levels" on C3 sharded, an overflow flag OR-ed into a
+    sub-bucket count in kg_shard.hip): a C3-shaped graph with a per-batch (query, node) visited table
+    of 2^10 / 2^11 keys overflows it, the batch reruns with a larger table (ShardOverflow), and the
+    answers and error codes equal the oracle's -- world 1 in the one-rank device loop and over RCCL,
+    world 2 over gloo; and the fixed-bucket protocol with 64-record buckets overflows them and reruns
+    with bigger ones (reference semantics: internal/check/engine.go:87-145)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    _run_synth(world, backend, 150_000, 6000, 10, preset=1, vis=vis, bucket=bucket)
 
 
 @pytest.mark.gpu
