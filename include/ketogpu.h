@@ -244,7 +244,8 @@ int kg_snapshot_materialized(const kg_snapshot* s, uint64_t* out3);
  * 0 = exact (query, node) CAS table (default), 1 = lossy direct-mapped cache; "shard_pack" (0/1,
  * default 0): kg_shard_levels sends a locally owned child as its set-row begin and length (no
  * adj_off read at the next level; no namespace program, depths < 256); "shard_budget" /
- * "shard_back_budget": see kg_shard_back_* below. */
+ * "shard_back_budget": see kg_shard_back_* below; "shard_bucket" (0..2^26, default 0 = sized from the
+ * batch): the first bucket size (records per destination) of in-library bindings made after it. */
 int kg_snapshot_tune(kg_snapshot* s, const char* key, int64_t value);
 /* Synthetic layout: ids6 = {n_docs, n_groups, n_users, n_folders, user_obj0, folder_obj0}
  * (doc d = object d, group g = object n_docs+g, user u = object user_obj0+u). */
@@ -425,6 +426,56 @@ size_t kg_shard_result_slots(const kg_snapshot* s, size_t n);
  * member found at a shallower level in a later one (internal/check/checkgroup's first-decisive
  * rule); the walk then goes on, the error reaches the query's home and the general phase decides. */
 int kg_shard_bad_nodes(const kg_snapshot* s, uint64_t* count);
+
+/* ---- hash-sharded batches inside the library (round 4) --------------------------------------
+ * The whole sharded batch -- seed, gdepth + 1 levels with their all-to-all exchanges, the done
+ * bitmap, finish and the general phase -- runs inside kg_check_batch / kg_check_batch_device once a
+ * transport is bound to the snapshot, so a host drives a sharded engine exactly like a replicated
+ * one (internal/driver/registry_default.go:180-185 builds ONE check.Engine, engine.go:65-80): every
+ * rank calls kg_check_batch(_device) with its own queries (any count, 0 included) in the same order
+ * on the same stream, and gets its own answers back.  Per level: ONE grouped exchange of the
+ * per-destination record counts and fixed-size buckets (B records each, the same B on every rank,
+ * learned from the previous batch), one all-gather of the done bitmap, the level kernels; per
+ * batch: one all-reduce that agrees on the slot count (the done bitmap's width) and one at the end
+ * (overflow flags, largest bucket, records left, "a query needs the general phase") -- two host
+ * round trips per batch, none per level.  A bucket or visited-table overflow on any rank reruns the
+ * batch on every rank with room to spare.  Escalation (kg_snapshot_tune "shard_budget") is not
+ * available here (keto_amd/sharded.py drives it through the kg_shard_* steps above).
+ *
+ * kg_shard_comm_init binds an RCCL communicator (over xGMI on one node) to the batches the
+ * snapshot runs on `stream` (NULL: the snapshot's own stream, which kg_check_batch uses); several
+ * streams with a communicator each keep several batches in flight per rank.  All ranks call it
+ * collectively with the id rank 0 got from kg_shard_unique_id (the host broadcasts the 128 bytes);
+ * the snapshot must have been created for (rank, world) (kg_snapshot_create_shard / _synthetic_shard).
+ * It also installs the OR of every rank's holder bitmap (kg_shard_held) and agrees whether any rank
+ * can end a check in an error (kg_shard_bad_nodes). */
+#define KG_SHARD_UNIQUE_ID_BYTES 128
+int kg_shard_unique_id(void* id);
+int kg_shard_comm_init(kg_snapshot* s, const void* id, int rank, int world, void* stream);
+/* Any other transport (MPI, a test harness) as callbacks, bound the same way.  Every call is
+ * collective over the `world` ranks, in the same order on every rank.  host_memory 1: the library
+ * hands the callbacks host buffers (it stages through pinned memory and completes its stream
+ * first); 0: device buffers, the work enqueued on `stream`.
+ *   alltoall2  fixed-size all-to-all of two buffers at once: block p (bytes0 / bytes1 bytes) of
+ *              send0 / send1 goes to rank p, block q of recv0 / recv1 comes from rank q
+ *   allgather  block r of recv (bytes each) = rank r's send
+ *   allreduce_max_u64  element-wise max over ranks, in place
+ * Each returns 0 on success. */
+typedef struct {
+  void* ctx;
+  int32_t rank, world, host_memory;
+  int (*alltoall2)(void* ctx, const void* send0, void* recv0, size_t bytes0, const void* send1, void* recv1,
+                   size_t bytes1, void* stream);
+  int (*allgather)(void* ctx, const void* send, void* recv, size_t bytes, void* stream);
+  int (*allreduce_max_u64)(void* ctx, uint64_t* buf, size_t count, void* stream);
+} kg_shard_transport;
+int kg_shard_transport_attach(kg_snapshot* s, const kg_shard_transport* t, void* stream);
+/* Unbinds (and for RCCL destroys) the communicator of `stream`; kg_snapshot_destroy does it for all. */
+int kg_shard_comm_release(kg_snapshot* s, void* stream);
+/* Counters of the last batch on `stream`: [0] levels, [1] records sent, [2] host round trips,
+ * [3] reruns after a bucket overflow, [4] after a visited-table overflow, [5] queries answered by
+ * the general phase, [6] rows it gathered, [7] bucket size B. */
+int kg_shard_comm_stats(const kg_snapshot* s, void* stream, uint64_t out8[8]);
 
 /* ---- expand ----------------------------------------------------------------------------- */
 /* Roots are split over the replicas (chunks of >= 1024 roots, one host thread each). */

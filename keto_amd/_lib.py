@@ -82,7 +82,21 @@ EXPORTS = ["kg_snapshot_create", "kg_snapshot_create_on", "kg_snapshot_synthetic
            "kg_tree_free", "kg_last_error", "kg_version", "kg_shard_owner", "kg_snapshot_create_shard",
            "kg_snapshot_synthetic_shard", "kg_shard_seed", "kg_shard_level", "kg_shard_level_seg", "kg_shard_finish",
            "kg_shard_done", "kg_shard_levels", "kg_shard_back_list", "kg_shard_back_seed", "kg_shard_back_level", "kg_shard_refwd_seed",
-           "kg_shard_held_words", "kg_shard_held", "kg_shard_result_slots", "kg_shard_bad_nodes", "kg_batcher_create", "kg_batcher_check", "kg_batcher_stats", "kg_batcher_reset_stats", "kg_batcher_destroy"]
+           "kg_shard_held_words", "kg_shard_held", "kg_shard_result_slots", "kg_shard_bad_nodes", "kg_batcher_create", "kg_batcher_check", "kg_batcher_stats", "kg_batcher_reset_stats", "kg_batcher_destroy",
+           "kg_shard_unique_id", "kg_shard_comm_init", "kg_shard_transport_attach", "kg_shard_comm_release",
+           "kg_shard_comm_stats"]
+
+KG_SHARD_UNIQUE_ID_BYTES = 128
+# kg_shard_transport callbacks (include/ketogpu.h): collective over the ranks, 0 = success
+ALLTOALL2_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p, C.c_size_t,
+                           C.c_void_p)
+ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p)
+ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_uint64), C.c_size_t, C.c_void_p)
+
+
+class kg_shard_transport(C.Structure):
+    _fields_ = [("ctx", C.c_void_p), ("rank", C.c_int32), ("world", C.c_int32), ("host_memory", C.c_int32),
+                ("alltoall2", ALLTOALL2_FN), ("allgather", ALLGATHER_FN), ("allreduce_max_u64", ALLREDUCE_FN)]
 
 
 class kg_batcher_stats_t(C.Structure):
@@ -160,6 +174,11 @@ def load(path: str = LIB_PATH):
     L.kg_shard_result_slots.argtypes = [vp, sz]
     L.kg_shard_result_slots.restype = sz
     L.kg_shard_finish.argtypes = [vp, sz, vp, vp, vp]
+    L.kg_shard_unique_id.argtypes = [vp]
+    L.kg_shard_comm_init.argtypes = [vp, vp, C.c_int, C.c_int, vp]
+    L.kg_shard_transport_attach.argtypes = [vp, C.POINTER(kg_shard_transport), vp]
+    L.kg_shard_comm_release.argtypes = [vp, vp]
+    L.kg_shard_comm_stats.argtypes = [vp, vp, vp]
     L.kg_batcher_create.argtypes = [vp, i32, sz, u32, C.c_int, C.POINTER(vp)]
     L.kg_batcher_check.argtypes = [vp, vp, sz, vp, vp]
     L.kg_batcher_stats.argtypes = [vp, C.POINTER(kg_batcher_stats_t)]
@@ -173,7 +192,9 @@ def load(path: str = LIB_PATH):
                  "kg_check_batch_device", "kg_synth_queries", "kg_expand_batch", "kg_snapshot_create_shard",
                  "kg_snapshot_synthetic_shard", "kg_shard_seed", "kg_shard_level", "kg_shard_level_seg", "kg_shard_finish",
                  "kg_shard_done", "kg_shard_levels", "kg_shard_back_list", "kg_shard_back_seed", "kg_shard_back_level", "kg_shard_refwd_seed",
-                 "kg_shard_held_words", "kg_shard_held", "kg_batcher_create", "kg_batcher_check", "kg_batcher_stats"):
+                 "kg_shard_held_words", "kg_shard_held", "kg_batcher_create", "kg_batcher_check", "kg_batcher_stats",
+                 "kg_shard_unique_id", "kg_shard_comm_init", "kg_shard_transport_attach", "kg_shard_comm_release",
+                 "kg_shard_comm_stats"):
         getattr(L, name).restype = C.c_int
     _lib = L
     return L

@@ -407,6 +407,11 @@ static int tune_one(Snapshot* s, const char* key, int64_t value) {
     s->shard_vis_log2 = (int)value;
     return 0;
   }
+  if (strcmp(key, "shard_bucket") == 0) {
+    if (value < 0 || value > (1ll << 26)) return set_error(-2, "shard_bucket must be in [0, 2^26]");
+    s->shard_bucket0 = (uint32_t)value;
+    return 0;
+  }
   if (strcmp(key, "shard_pack") == 0) {
     if (value < 0 || value > 1) return set_error(-2, "shard_pack must be 0 or 1");
     s->shard_pack = (int)value;
@@ -617,7 +622,12 @@ int kg_check_batch_device(kg_snapshot* sp, const kg_query* d_q, size_t n, int32_
   KG_GUARD_BEGIN
   if (!sp) return set_error(-2, "NULL snapshot");
   Snapshot* s = reinterpret_cast<Snapshot*>(sp);
-  if (s->shard_n > 1) return set_error(-2, "sharded snapshot: checks run through kg_shard_seed / kg_shard_level");
+  // a transport bound to this stream: the whole hash-sharded batch inside the library (kg_shard_comm.hip)
+  if (kg::ShardComm* c = kg::shard_comm_of(s, (hipStream_t)stream))
+    return kg::shard_check(s, c, d_q, n, global_max_depth, d_out, d_err, stats);
+  if (s->shard_n > 1)
+    return set_error(-2, "sharded snapshot: bind a transport to this stream (kg_shard_comm_init) or drive "
+                         "kg_shard_seed / kg_shard_level");
   kg::Workspace* w = s->workspace((hipStream_t)stream);  // one per stream: batches on other streams overlap
   std::lock_guard<std::mutex> lk(w->mu);
   return kg::check_batch_device(s, w, d_q, n, global_max_depth, d_out, d_err, stats);
@@ -643,7 +653,8 @@ int kg_check_batch(kg_snapshot* sp, const kg_query* q, size_t n, int32_t global_
   if (!sp) return set_error(-2, "NULL snapshot");
   if (n && (!q || !out)) return set_error(-2, "NULL buffer");
   Snapshot* s = reinterpret_cast<Snapshot*>(sp);
-  if (s->shard_n > 1) return set_error(-2, "sharded snapshot: checks run through kg_shard_seed / kg_shard_level");
+  if (s->shard_n > 1 || kg::shard_comm_of(s, nullptr))  // hash-sharded: the whole batch in kg_shard_comm.hip
+    return kg::shard_check_host_entry(s, q, n, global_max_depth, out, err_code, stats);
   if (stats) memset(stats, 0, sizeof *stats);
   if (n == 0) return 0;
   if (n > 0x7FFFFFFFull) return set_error(-2, "batch too large");

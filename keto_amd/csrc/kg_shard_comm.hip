@@ -1,0 +1,752 @@
+// kg_shard_comm.hip -- hash-sharded batches inside the library.
+//
+// kg_check_batch / kg_check_batch_device on a snapshot with a transport bound to the call's stream
+// run the whole sharded batch here, so a host drives the sharded engine through the same entry
+// point as the replicated one (the reference wires ONE check.Engine into the registry,
+// internal/driver/registry_default.go:180-185, internal/check/engine.go:65-80):
+//
+//   agree    all-reduce of this rank's result-slot count (the done bitmap's width)  host round trip 1
+//   seed     kg_shard_seed: this rank's queries -> one record each at its root's owner
+//   level k  (k = 0 .. gdepth; a record's rest depth falls by one per level, the last level only
+//            delivers hit / error reports) ONE grouped exchange of the per-destination counts and
+//            the fixed-size buckets (B records per destination, the same B on every rank), the
+//            done bitmap all-gathered when pruning is on, kg_shard_level over the N received
+//            segments (their counts read on the device)
+//   end      kg_shard_finish, then one all-reduce of (bucket overflow, visited overflow, largest
+//            bucket, records left, a query needs the general phase)           host round trip 2
+//   rerun    on an overflow anywhere: every rank reruns with bigger buckets / a bigger table
+//   general  queries that reached a rewrite the level protocol cannot evaluate across ranks: the rows
+//            of every object within gdepth + 1 subject-set hops of their roots are gathered to their
+//            home rank (each owner ships an object's rows once per home) and a single-GPU snapshot of
+//            them answers them with the rewrite interpreter -- the reference's answers and errors
+//
+// This is keto_amd/sharded.py's fixed-bucket protocol (ShardedChecker._check_fixed, _general_phase,
+// still the CPU-tested restatement) moved below the C ABI.  The transport is RCCL over xGMI
+// (kg_shard_comm_init) or any host callbacks (kg_shard_transport_attach).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <array>
+#include <cstring>
+#include <set>
+#include <vector>
+
+#include "kg_internal.h"
+#include "kg_snapshot.h"
+
+namespace kg {
+
+struct ShardComm {
+  hipStream_t bound = nullptr;  // as bound by the caller (NULL: the snapshot's stream)
+  hipStream_t run = nullptr;    // the stream the batches run on
+  int device = -1;
+  int rank = 0, world = 1;
+  kg_shard_transport t{};
+  ncclComm_t nccl = nullptr;
+  std::mutex mu;
+  bool prune = false;
+  // device buffers, grown on demand
+  kg_frec* buf[2] = {nullptr, nullptr};
+  kg_frec* recv = nullptr;
+  size_t recs = 0;                  // records each of buf[0], buf[1], recv holds (N * B)
+  uint32_t* cnt = nullptr;          // counts[2][N + 1] | rc[N]
+  unsigned long long* acc = nullptr;  // acc[4] | tot[8] | scratch[8]
+  uint32_t* bits = nullptr;
+  uint32_t* bits_all = nullptr;
+  size_t words_cap = 0, all_cap = 0;
+  uint8_t* res = nullptr;
+  uint32_t* err = nullptr;
+  size_t slots_cap = 0;
+  kg_query* dq = nullptr;  // kg_check_batch (host buffers): staged queries and results
+  uint8_t* dout = nullptr;
+  uint32_t* derr = nullptr;
+  size_t dq_cap = 0;
+  void* pinned = nullptr;  // host staging: host-memory transports and readbacks
+  size_t pinned_bytes = 0;
+  size_t bucket = 0;     // B, learned from the previous batch
+  uint64_t st[8] = {};   // kg_shard_comm_stats
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  ~ShardComm();
+};
+
+ShardComm::~ShardComm() {
+  if (device >= 0) hipSetDevice(device);
+  if (run) hipStreamSynchronize(run);
+  if (nccl) ncclCommDestroy(nccl);
+  hipFree(buf[0]);
+  hipFree(buf[1]);
+  hipFree(recv);
+  hipFree(cnt);
+  hipFree(acc);
+  hipFree(bits);
+  hipFree(bits_all);
+  hipFree(res);
+  hipFree(err);
+  hipFree(dq);
+  hipFree(dout);
+  hipFree(derr);
+  if (pinned) hipHostFree(pinned);
+  for (auto e : ev)
+    if (e) hipEventDestroy(e);
+}
+
+void shard_comms_free(Snapshot* s) {
+  std::lock_guard<std::mutex> lk(s->comm_mu);
+  for (ShardComm* c : s->comms) delete c;
+  s->comms.clear();
+}
+
+ShardComm* shard_comm_of(Snapshot* s, hipStream_t st) {
+  std::lock_guard<std::mutex> lk(s->comm_mu);
+  for (ShardComm* c : s->comms)
+    if (c->bound == st) return c;
+  return nullptr;
+}
+
+// ------------------------------------------------------------------ RCCL transport
+#define NCCLC(expr)                                                                                            \
+  do {                                                                                                         \
+    ncclResult_t _r = (expr);                                                                                  \
+    if (_r != ncclSuccess) return set_error(-1, "%s: %s", #expr, ncclGetErrorString(_r));                    \
+  } while (0)
+
+static int rccl_alltoall2(void* ctx, const void* s0, void* r0, size_t b0, const void* s1, void* r1, size_t b1,
+                          void* stream) {
+  ShardComm* c = static_cast<ShardComm*>(ctx);
+  hipStream_t st = (hipStream_t)stream;
+  NCCLC(ncclGroupStart());
+  for (int p = 0; p < c->world; p++) {
+    if (b0) {
+      NCCLC(ncclSend((const char*)s0 + p * b0, b0 / 4, ncclUint32, p, c->nccl, st));
+      NCCLC(ncclRecv((char*)r0 + p * b0, b0 / 4, ncclUint32, p, c->nccl, st));
+    }
+    if (b1) {
+      NCCLC(ncclSend((const char*)s1 + p * b1, b1 / 4, ncclUint32, p, c->nccl, st));
+      NCCLC(ncclRecv((char*)r1 + p * b1, b1 / 4, ncclUint32, p, c->nccl, st));
+    }
+  }
+  NCCLC(ncclGroupEnd());
+  return 0;
+}
+
+static int rccl_allgather(void* ctx, const void* s, void* r, size_t bytes, void* stream) {
+  ShardComm* c = static_cast<ShardComm*>(ctx);
+  NCCLC(ncclAllGather(s, r, bytes / 4, ncclUint32, c->nccl, (hipStream_t)stream));
+  return 0;
+}
+
+static int rccl_allreduce_max(void* ctx, uint64_t* buf, size_t count, void* stream) {
+  ShardComm* c = static_cast<ShardComm*>(ctx);
+  NCCLC(ncclAllReduce(buf, buf, count, ncclUint64, ncclMax, c->nccl, (hipStream_t)stream));
+  return 0;
+}
+
+// ------------------------------------------------------------------ transport calls, staged as needed
+static void* pinned_at_least(ShardComm* c, size_t bytes) {
+  if (bytes > c->pinned_bytes) {
+    if (c->pinned) hipHostFree(c->pinned);
+    c->pinned = nullptr;
+    c->pinned_bytes = 0;
+    const size_t b = std::max<size_t>(bytes, 1 << 16);
+    if (hipHostMalloc(&c->pinned, b) != hipSuccess) return nullptr;
+    c->pinned_bytes = b;
+  }
+  return c->pinned;
+}
+
+static int tcall(int rc, const char* what) {
+  return rc ? set_error(-1, "sharded transport: %s failed (%d)", what, rc) : 0;
+}
+
+// device buffers in, device buffers out (enqueued on c->run, or staged and completed)
+static int x_alltoall2(ShardComm* c, const void* s0, void* r0, size_t b0, const void* s1, void* r1, size_t b1) {
+  if (!c->t.host_memory) return tcall(c->t.alltoall2(c->t.ctx, s0, r0, b0, s1, r1, b1, c->run), "alltoall2");
+  const size_t N = (size_t)c->world, a = N * b0, b = N * b1;
+  char* h = (char*)pinned_at_least(c, 2 * (a + b));
+  if (!h) return set_error(-1, "pinned staging");
+  HIPC(hipStreamSynchronize(c->run));  // earlier H2D copies out of the staging area are done
+  if (a) HIPC(hipMemcpyAsync(h, s0, a, hipMemcpyDeviceToHost, c->run));
+  if (b) HIPC(hipMemcpyAsync(h + a, s1, b, hipMemcpyDeviceToHost, c->run));
+  HIPC(hipStreamSynchronize(c->run));
+  if (int rc = tcall(c->t.alltoall2(c->t.ctx, h, h + a + b, b0, h + a, h + 2 * a + b, b1, nullptr), "alltoall2"))
+    return rc;
+  if (a) HIPC(hipMemcpyAsync(r0, h + a + b, a, hipMemcpyHostToDevice, c->run));
+  if (b) HIPC(hipMemcpyAsync(r1, h + 2 * a + b, b, hipMemcpyHostToDevice, c->run));
+  return 0;
+}
+
+static int x_allgather(ShardComm* c, const void* s, void* r, size_t bytes) {
+  if (!c->t.host_memory) return tcall(c->t.allgather(c->t.ctx, s, r, bytes, c->run), "allgather");
+  const size_t N = (size_t)c->world;
+  char* h = (char*)pinned_at_least(c, (N + 1) * bytes);
+  if (!h) return set_error(-1, "pinned staging");
+  HIPC(hipStreamSynchronize(c->run));
+  HIPC(hipMemcpyAsync(h, s, bytes, hipMemcpyDeviceToHost, c->run));
+  HIPC(hipStreamSynchronize(c->run));
+  if (int rc = tcall(c->t.allgather(c->t.ctx, h, h + bytes, bytes, nullptr), "allgather")) return rc;
+  HIPC(hipMemcpyAsync(r, h + bytes, N * bytes, hipMemcpyHostToDevice, c->run));
+  return 0;
+}
+
+static int x_allreduce_max(ShardComm* c, unsigned long long* d, size_t count) {
+  if (!c->t.host_memory) return tcall(c->t.allreduce_max_u64(c->t.ctx, (uint64_t*)d, count, c->run), "allreduce");
+  uint64_t* h = (uint64_t*)pinned_at_least(c, count * 8);
+  if (!h) return set_error(-1, "pinned staging");
+  HIPC(hipStreamSynchronize(c->run));
+  HIPC(hipMemcpyAsync(h, d, count * 8, hipMemcpyDeviceToHost, c->run));
+  HIPC(hipStreamSynchronize(c->run));
+  if (int rc = tcall(c->t.allreduce_max_u64(c->t.ctx, h, count, nullptr), "allreduce")) return rc;
+  HIPC(hipMemcpyAsync(d, h, count * 8, hipMemcpyHostToDevice, c->run));
+  return 0;
+}
+
+// host buffers in and out, completed on return (agreement, the general phase)
+static int h_allreduce_max(ShardComm* c, uint64_t* v, size_t count) {
+  if (count > 8) return set_error(-2, "h_allreduce_max: at most 8 values");
+  unsigned long long* d = c->acc + 12;
+  HIPC(hipMemcpyAsync(d, v, count * 8, hipMemcpyHostToDevice, c->run));
+  if (int rc = x_allreduce_max(c, d, count)) return rc;
+  HIPC(hipMemcpyAsync(v, d, count * 8, hipMemcpyDeviceToHost, c->run));
+  HIPC(hipStreamSynchronize(c->run));
+  return 0;
+}
+
+static int h_alltoall2(ShardComm* c, const void* s0, void* r0, size_t b0, const void* s1, void* r1, size_t b1) {
+  if (c->t.host_memory) {
+    HIPC(hipStreamSynchronize(c->run));
+    return tcall(c->t.alltoall2(c->t.ctx, s0, r0, b0, s1, r1, b1, nullptr), "alltoall2");
+  }
+  const size_t N = (size_t)c->world, a = N * b0, b = N * b1;
+  char* d = nullptr;
+  HIPC(hipMalloc(&d, 2 * (a + b) + 16));
+  int rc = 0;
+  if (a) rc |= hipMemcpyAsync(d, s0, a, hipMemcpyHostToDevice, c->run) != hipSuccess;
+  if (b) rc |= hipMemcpyAsync(d + a, s1, b, hipMemcpyHostToDevice, c->run) != hipSuccess;
+  if (!rc) rc = x_alltoall2(c, d, d + a + b, b0, d + a, d + 2 * a + b, b1);
+  else rc = set_error(-1, "H2D staging");
+  if (!rc && a && hipMemcpyAsync(r0, d + a + b, a, hipMemcpyDeviceToHost, c->run) != hipSuccess) rc = -1;
+  if (!rc && b && hipMemcpyAsync(r1, d + 2 * a + b, b, hipMemcpyDeviceToHost, c->run) != hipSuccess) rc = -1;
+  if (hipStreamSynchronize(c->run) != hipSuccess && !rc) rc = set_error(-1, "D2H staging");
+  hipFree(d);
+  return rc;
+}
+
+// ------------------------------------------------------------------ small kernels
+// Per level before the exchange (keto_amd/sharded.py _check_fixed's device accumulators): acc[0] |=
+// overflow flags (c[N], or a bucket past B), acc[1] = largest bucket, acc[2] += records sent.
+__global__ void k_sc_acc(const uint32_t* __restrict__ c, uint32_t N, uint32_t B, unsigned long long* acc) {
+  const uint32_t i = threadIdx.x;
+  const uint32_t v = i < N ? c[i] : 0u;
+  unsigned long long fl = (i < N && v > B) ? 1ull : 0ull, mx = v, sum = v;
+  for (int off = 32; off; off >>= 1) {
+    fl |= __shfl_xor(fl, off, 64);
+    mx = max(mx, __shfl_xor(mx, off, 64));
+    sum += __shfl_xor(sum, off, 64);
+  }
+  if (i == 0) {
+    acc[0] |= fl | c[N];
+    acc[1] = max(acc[1], mx);
+    acc[2] += sum;
+  }
+}
+
+// After the last level: tot = (bucket overflow, visited overflow, largest bucket, records left, 0).
+__global__ void k_sc_final(const uint32_t* __restrict__ c, uint32_t N, uint32_t B, unsigned long long* acc,
+                           unsigned long long* tot) {
+  const uint32_t i = threadIdx.x;
+  const uint32_t v = i < N ? c[i] : 0u;
+  unsigned long long fl = (i < N && v > B) ? 1ull : 0ull, sum = v;
+  for (int off = 32; off; off >>= 1) {
+    fl |= __shfl_xor(fl, off, 64);
+    sum += __shfl_xor(sum, off, 64);
+  }
+  if (i == 0) {
+    const unsigned long long f = acc[0] | fl | c[N];
+    tot[0] = f & 1ull;
+    tot[1] = (f >> 1) & 1ull;
+    tot[2] = acc[1];
+    tot[3] = sum;
+    tot[4] = 0;
+  }
+}
+
+// tot[4] = 1 when some query of [0, n) ended KG_ERROR / KG_ERR_NOT_IMPLEMENTED (general phase).
+__global__ void k_sc_open(uint32_t n, const uint8_t* __restrict__ res, const uint32_t* __restrict__ err,
+                          unsigned long long* tot) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool open = i < n && res[i] == KG_ERROR && err[i] == KG_ERR_NOT_IMPLEMENTED;
+  if (__ballot(open) && (threadIdx.x & 63) == 0) tot[4] = 1ull;
+}
+
+// out[w] = OR over ranks of parts[r * words + w] (the holder bitmaps of every rank).
+__global__ void k_sc_or(const uint32_t* __restrict__ parts, uint32_t N, uint64_t words, uint32_t* out) {
+  const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= words) return;
+  uint32_t v = 0;
+  for (uint32_t r = 0; r < N; r++) v |= parts[r * words + w];
+  out[w] = v;
+}
+
+// ------------------------------------------------------------------ binding
+static int grow(void** p, size_t* have, size_t want, size_t unit) {
+  if (want <= *have && *p) return 0;
+  if (*p) hipFree(*p);
+  *p = nullptr;
+  *have = 0;
+  const size_t n = std::max<size_t>(want, 1024);
+  HIPC(hipMalloc(p, n * unit));
+  *have = n;
+  return 0;
+}
+
+// Collective, once per binding: the OR of every rank's holder bitmap (kg_shard_seed's no-holder test
+// across ranks) and whether any rank can end a check in an error (pruning through the done bitmap).
+static int comm_setup(Snapshot* s, ShardComm* c) {
+  HIPC(hipMalloc((void**)&c->acc, 32 * 8));
+  HIPC(hipMemsetAsync(c->acc, 0, 32 * 8, c->run));
+  HIPC(hipMalloc((void**)&c->cnt, (3 * (size_t)KG_SHARD_MAX_RANKS + 2) * 4));
+  uint64_t bad = 0;
+  if (int rc = shard_bad_nodes(s, &bad)) return rc;
+  size_t words = 0;
+  if (c->world > 1) words = ((size_t)s->ds.hbits_n + 31) / 32;
+  uint64_t v[2] = {bad, words};
+  if (int rc = h_allreduce_max(c, v, 2)) return rc;
+  c->prune = v[0] == 0;
+  words = (size_t)v[1];
+  if (c->world > 1 && words) {
+    uint32_t *mine = nullptr, *all = nullptr;
+    HIPC(hipMalloc((void**)&mine, words * 4));
+    HIPC(hipMalloc((void**)&all, (size_t)c->world * words * 4));
+    int rc = shard_held(s, mine, words, 0, c->run);
+    if (!rc) rc = x_allgather(c, mine, all, words * 4);
+    if (!rc) {
+      hipLaunchKernelGGL(k_sc_or, dim3((uint32_t)((words + 255) / 256)), dim3(256), 0, c->run, all, (uint32_t)c->world,
+                         (uint64_t)words, mine);
+      rc = shard_held(s, mine, words, 1, c->run);  // synchronises
+    }
+    hipFree(mine);
+    hipFree(all);
+    if (rc) return rc;
+  }
+  return 0;
+}
+
+static int bind(Snapshot* s, ShardComm* c, hipStream_t st) {
+  if ((uint32_t)c->world != s->shard_n || (uint32_t)c->rank != s->shard_rank)
+    return set_error(-2, "transport is rank %d of %d, the snapshot was built as shard %u of %u", c->rank, c->world,
+                     s->shard_rank, s->shard_n);
+  c->bound = st;
+  c->run = st ? st : s->stream;
+  c->bucket = s->shard_bucket0;
+  c->device = s->device;
+  if (int rc = comm_setup(s, c)) return rc;
+  std::lock_guard<std::mutex> lk(s->comm_mu);
+  for (auto it = s->comms.begin(); it != s->comms.end(); ++it)
+    if ((*it)->bound == st) {
+      delete *it;
+      s->comms.erase(it);
+      break;
+    }
+  s->comms.push_back(c);
+  return 0;
+}
+
+// ------------------------------------------------------------------ the general phase
+template <int W>
+using Row = std::array<uint64_t, W>;
+
+// All-to-all of host rows: rows[i] goes to rank dest[i]; returns what this rank received (collective).
+template <int W>
+static int a2a_rows(ShardComm* c, const std::vector<Row<W>>& rows, const std::vector<int>& dest,
+                    std::vector<Row<W>>* out) {
+  const size_t N = (size_t)c->world;
+  out->clear();
+  std::vector<uint64_t> cnt(N, 0);
+  for (int d : dest) cnt[(size_t)d]++;
+  uint64_t m = 0;
+  for (uint64_t x : cnt) m = std::max(m, x);
+  if (int rc = h_allreduce_max(c, &m, 1)) return rc;
+  if (m == 0) return 0;
+  std::vector<uint64_t> send(N * m * W, 0), recv(N * m * W, 0), rcnt(N, 0);
+  std::vector<uint64_t> fill(N, 0);
+  for (size_t i = 0; i < rows.size(); i++) {
+    const size_t d = (size_t)dest[i];
+    std::memcpy(&send[(d * m + fill[d]++) * W], rows[i].data(), W * 8);
+  }
+  if (int rc = h_alltoall2(c, cnt.data(), rcnt.data(), 8, send.data(), recv.data(), m * W * 8)) return rc;
+  for (size_t q = 0; q < N; q++)
+    for (uint64_t j = 0; j < rcnt[q] && j < m; j++) {
+      Row<W> r;
+      std::memcpy(r.data(), &recv[(q * m + j) * W], W * 8);
+      out->push_back(r);
+    }
+  return 0;
+}
+
+// Every row of every object within gdepth + 1 subject-set hops of the open queries' root objects,
+// gathered at their home rank (keto_amd/sharded.py _gather_region: expand rows and tuple-to-subject-set
+// rows both lead through subject sets; computed subject sets stay on the object, all of whose
+// relations live on its owner).  Collective: every rank takes part, with or without open queries.
+static int gather_region(Snapshot* s, ShardComm* c, const std::vector<kg_query>& open_q, int32_t gdepth,
+                         std::vector<kg_tuple>* region) {
+  const uint32_t N = (uint32_t)c->world;
+  std::set<Row<3>> reqset;
+  for (const kg_query& q : open_q) reqset.insert(Row<3>{(uint64_t)c->rank, q.t.ns, q.t.obj});
+  std::vector<Row<3>> req(reqset.begin(), reqset.end());
+  std::set<Row<3>> seen;  // (home, ns, obj) this owner has shipped
+  const uint32_t nrel = std::max<uint32_t>(s->ds.n_rel, 1);
+  for (int hop = 0; hop < gdepth + 2; hop++) {
+    std::vector<int> dest(req.size());
+    for (size_t i = 0; i < req.size(); i++) dest[i] = (int)shard_owner((uint32_t)req[i][1], (uint32_t)req[i][2], N);
+    std::vector<Row<3>> got;
+    if (int rc = a2a_rows<3>(c, req, dest, &got)) return rc;
+    std::vector<Row<3>> fresh;
+    for (const Row<3>& r : got)
+      if (seen.insert(r).second) fresh.push_back(r);
+    std::vector<kg_set> keys(fresh.size() * nrel);
+    for (size_t i = 0; i < fresh.size(); i++)
+      for (uint32_t r = 0; r < nrel; r++) keys[i * nrel + r] = kg_set{(uint32_t)fresh[i][1], (uint32_t)fresh[i][2], r, 0};
+    std::vector<uint64_t> off(keys.size() + 1, 0);
+    std::vector<kg_tuple> tup;
+    if (!keys.empty()) {
+      const int64_t total = s->rows_of(keys.data(), keys.size(), off.data(), nullptr, 0);
+      if (total < 0) return (int)total;
+      tup.resize((size_t)total);
+      if (total && s->rows_of(keys.data(), keys.size(), off.data(), tup.data(), (uint64_t)total) < 0) return -1;
+    }
+    std::vector<Row<7>> pay;
+    std::vector<int> pdest;
+    for (size_t i = 0; i < fresh.size(); i++)
+      for (uint64_t j = off[i * nrel]; j < off[(i + 1) * nrel]; j++) {
+        const kg_tuple& t = tup[j];
+        pay.push_back(Row<7>{fresh[i][0], t.ns, t.obj, t.rel, t.sns, t.sobj, t.srel});
+        pdest.push_back((int)fresh[i][0]);
+      }
+    std::vector<Row<7>> mine;
+    if (int rc = a2a_rows<7>(c, pay, pdest, &mine)) return rc;
+    std::set<Row<3>> next;
+    for (const Row<7>& r : mine) {
+      region->push_back(kg_tuple{(uint32_t)r[1], (uint32_t)r[2], (uint32_t)r[3], (uint32_t)r[4], (uint32_t)r[5],
+                                 (uint32_t)r[6]});
+      if (hop <= gdepth && (uint32_t)r[4] != KG_SUBJECT_ID) next.insert(Row<3>{(uint64_t)c->rank, r[4], r[5]});
+    }
+    req.assign(next.begin(), next.end());
+    uint64_t any = req.empty() ? 0 : 1;
+    if (int rc = h_allreduce_max(c, &any, 1)) return rc;
+    if (!any) break;
+  }
+  return 0;
+}
+
+static int general_phase(Snapshot* s, ShardComm* c, const kg_query* d_q, size_t n, int32_t gdepth) {
+  std::vector<uint8_t> hres(n);
+  std::vector<uint32_t> herr(n);
+  std::vector<kg_query> hq(n);
+  if (n) {
+    HIPC(hipMemcpyAsync(hres.data(), c->res, n, hipMemcpyDeviceToHost, c->run));
+    HIPC(hipMemcpyAsync(herr.data(), c->err, n * 4, hipMemcpyDeviceToHost, c->run));
+    HIPC(hipMemcpyAsync(hq.data(), d_q, n * sizeof(kg_query), hipMemcpyDeviceToHost, c->run));
+  }
+  HIPC(hipStreamSynchronize(c->run));
+  std::vector<uint32_t> open;
+  std::vector<kg_query> oq;
+  for (size_t i = 0; i < n; i++)
+    if (hres[i] == KG_ERROR && herr[i] == KG_ERR_NOT_IMPLEMENTED) {
+      open.push_back((uint32_t)i);
+      oq.push_back(hq[i]);
+    }
+  std::vector<kg_tuple> region;
+  if (int rc = gather_region(s, c, oq, gdepth, &region)) return rc;
+  c->st[5] = open.size();
+  c->st[6] = region.size();
+  if (open.empty()) return 0;
+  // the single-GPU engine (rewrite interpreter included) on a snapshot of the gathered rows
+  Snapshot* g = new (std::nothrow) Snapshot();
+  if (!g) return set_error(KG_ERR_RESOURCE_CODE, "general phase snapshot");
+  kg_rewrite_prog p = s->prog_copy.view();
+  const bool prog = s->prog_copy.have && !s->prog_copy.ns_has_rel.empty();
+  int rc = g->init_device(s->device);
+  if (!rc) rc = g->create_from_tuples(region.data(), region.size(), &s->prog_copy.dict, prog ? &p : nullptr);
+  const size_t m = open.size();
+  kg_query* dq = nullptr;
+  uint8_t* dout = nullptr;
+  uint32_t* derr = nullptr;
+  std::vector<uint8_t> r(m);
+  std::vector<uint32_t> e(m);
+  if (!rc && (hipMalloc(&dq, m * sizeof(kg_query)) != hipSuccess || hipMalloc(&dout, m) != hipSuccess ||
+              hipMalloc(&derr, m * 4) != hipSuccess))
+    rc = set_error(-1, "general phase buffers");
+  if (!rc && hipMemcpy(dq, oq.data(), m * sizeof(kg_query), hipMemcpyHostToDevice) != hipSuccess)
+    rc = set_error(-1, "general phase H2D");
+  if (!rc) rc = check_batch_device(g, g->workspace(nullptr), dq, m, gdepth, dout, derr, nullptr);
+  if (!rc && (hipMemcpy(r.data(), dout, m, hipMemcpyDeviceToHost) != hipSuccess ||
+              hipMemcpy(e.data(), derr, m * 4, hipMemcpyDeviceToHost) != hipSuccess))
+    rc = set_error(-1, "general phase D2H");
+  hipFree(dq);
+  hipFree(dout);
+  hipFree(derr);
+  delete g;
+  hipSetDevice(s->device);
+  if (rc) return rc;
+  for (size_t k = 0; k < m; k++) {
+    hres[open[k]] = r[k];
+    herr[open[k]] = e[k];
+  }
+  HIPC(hipMemcpyAsync(c->res, hres.data(), n, hipMemcpyHostToDevice, c->run));
+  HIPC(hipMemcpyAsync(c->err, herr.data(), n * 4, hipMemcpyHostToDevice, c->run));
+  HIPC(hipStreamSynchronize(c->run));
+  return 0;
+}
+
+// ------------------------------------------------------------------ one batch
+int shard_check(Snapshot* s, ShardComm* c, const kg_query* d_q, size_t n, int32_t gdepth, uint8_t* d_out,
+                uint32_t* d_err, kg_stats* stats) {
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIPC(hipSetDevice(s->device));
+  if (gdepth < 1) gdepth = 5;  // config.schema.json:308-315 default (as kg_shard_seed)
+  if (n > 0x7FFFFFFFull) return set_error(-2, "batch too large");
+  hipStream_t st = c->run;
+  const uint32_t N = (uint32_t)c->world;
+  memset(c->st, 0, sizeof c->st);
+  if (stats) {
+    memset(stats, 0, sizeof *stats);
+    for (auto& e : c->ev)
+      if (!e) HIPC(hipEventCreate(&e));
+    HIPC(hipEventRecord(c->ev[0], st));
+  }
+  // the largest result-slot count of any rank: the done bitmap's width (host round trip 1)
+  const size_t slots = shard_result_slots(s, n);
+  uint64_t smax = slots;
+  if (int rc = h_allreduce_max(c, &smax, 1)) return rc;
+  c->st[2]++;
+  const uint32_t words = (uint32_t)((smax + 31) / 32);
+  if (grow((void**)&c->bits, &c->words_cap, (size_t)words + 1, 4)) return -1;
+  if (grow((void**)&c->bits_all, &c->all_cap, (size_t)N * words + 1, 4)) return -1;
+  size_t have = c->slots_cap;
+  if (slots > have || !c->res) {
+    hipFree(c->res);
+    hipFree(c->err);
+    c->res = nullptr;
+    c->err = nullptr;
+    c->slots_cap = 0;
+    const size_t m = std::max<size_t>(slots, 1024);
+    HIPC(hipMalloc((void**)&c->res, m));
+    HIPC(hipMalloc((void**)&c->err, m * 4));
+    c->slots_cap = m;
+  }
+  uint32_t* counts[2] = {c->cnt, c->cnt + (N + 1)};
+  uint32_t* rcv = c->cnt + 2 * (N + 1);
+  unsigned long long* acc = c->acc;
+  unsigned long long* tot = c->acc + 4;
+  for (;;) {
+    const size_t B = c->bucket ? c->bucket : std::min<size_t>(2 * smax / N + 1024, 1ull << 26);
+    c->bucket = B;
+    if ((size_t)N * B > c->recs) {
+      for (kg_frec** p : {&c->buf[0], &c->buf[1], &c->recv}) {
+        hipFree(*p);
+        *p = nullptr;
+      }
+      c->recs = 0;
+      for (kg_frec** p : {&c->buf[0], &c->buf[1], &c->recv}) HIPC(hipMalloc((void**)p, (size_t)N * B * sizeof(kg_frec)));
+      c->recs = (size_t)N * B;
+    }
+    HIPC(hipMemsetAsync(acc, 0, 12 * 8, st));
+    if (int rc = shard_seed(s, d_q, n, gdepth, c->buf[0], B, counts[0], c->res, c->err, st)) return rc;
+    int cur = 0;
+    for (int k = 0; k <= gdepth; k++) {
+      hipLaunchKernelGGL(k_sc_acc, dim3(1), dim3(64), 0, st, counts[cur], N, (uint32_t)B, acc);
+      HIPC(hipGetLastError());
+      if (int rc = x_alltoall2(c, counts[cur], rcv, 4, c->buf[cur], c->recv, B * sizeof(kg_frec))) return rc;
+      const uint32_t* done = nullptr;
+      if (c->prune && k > 0) {
+        if (int rc = shard_done(s, slots, c->res, c->err, 0, c->bits, words, st)) return rc;
+        if (int rc = x_allgather(c, c->bits, c->bits_all, (size_t)words * 4)) return rc;
+        done = c->bits_all;
+      }
+      const int nx = cur ^ 1;
+      if (int rc = shard_level(s, c->recv, (size_t)N * B, rcv, c->buf[nx], B, counts[nx], c->res, c->err, done, words,
+                               st, N, B))
+        return rc;
+      cur = nx;
+      c->st[0]++;
+    }
+    hipLaunchKernelGGL(k_sc_final, dim3(1), dim3(64), 0, st, counts[cur], N, (uint32_t)B, acc, tot);
+    HIPC(hipGetLastError());
+    // results final before the all-reduce, which then also carries "a query needs the general phase"
+    if (int rc = shard_finish(s, n, c->res, c->err, st)) return rc;
+    if (n) {
+      hipLaunchKernelGGL(k_sc_open, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, (uint32_t)n, c->res, c->err,
+                         tot);
+      HIPC(hipGetLastError());
+    }
+    if (int rc = x_allreduce_max(c, tot, 5)) return rc;
+    uint64_t h[8];
+    HIPC(hipMemcpyAsync(h, tot, 5 * 8, hipMemcpyDeviceToHost, st));
+    HIPC(hipMemcpyAsync(h + 5, acc + 2, 8, hipMemcpyDeviceToHost, st));
+    HIPC(hipStreamSynchronize(st));  // host round trip 2
+    c->st[2]++;
+    const uint64_t big = h[2];
+    if (h[0] || h[1]) {  // dropped records somewhere: every rank reruns with more room
+      if (h[0]) {
+        c->st[3]++;
+        c->bucket = std::max<size_t>(2 * B, (size_t)(big * 1.25) + 1024);
+      }
+      if (h[1]) {
+        c->st[4]++;
+        if (s->shard_vis_log2 >= 34) return set_error(KG_ERR_RESOURCE_CODE, "sharded visited table overflow");
+        s->shard_vis_log2 = std::min(34, s->shard_vis_log2 + 2);
+      }
+      continue;
+    }
+    if (h[3]) return set_error(-1, "sharded batch: records left after %d levels", gdepth + 1);
+    // next batch: buckets 25 % above the largest one this batch needed (shrinking slowly)
+    if (big * 2 < B) c->bucket = std::max<size_t>(1024, std::min<size_t>(B, (size_t)(big * 1.25) + 1024));
+    c->st[1] = h[5];
+    if (h[4])
+      if (int rc = general_phase(s, c, d_q, n, gdepth)) return rc;
+    break;
+  }
+  c->st[7] = c->bucket;
+  if (n) {
+    HIPC(hipMemcpyAsync(d_out, c->res, n, hipMemcpyDeviceToDevice, st));
+    if (d_err) HIPC(hipMemcpyAsync(d_err, c->err, n * 4, hipMemcpyDeviceToDevice, st));
+  }
+  if (stats) {
+    HIPC(hipEventRecord(c->ev[1], st));
+    HIPC(hipEventSynchronize(c->ev[1]));
+    float ms = 0;
+    HIPC(hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
+    stats->kernel_ms = ms;
+  }
+  return 0;
+}
+
+// Host buffers: staged through the binding's device buffers, on the bound stream.
+static int shard_check_host(Snapshot* s, ShardComm* c, const kg_query* q, size_t n, int32_t gdepth, uint8_t* out,
+                            uint32_t* err, kg_stats* stats) {
+  {
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIPC(hipSetDevice(s->device));
+    if (n > c->dq_cap || !c->dq) {
+      hipFree(c->dq);
+      hipFree(c->dout);
+      hipFree(c->derr);
+      c->dq = nullptr;
+      c->dout = nullptr;
+      c->derr = nullptr;
+      c->dq_cap = 0;
+      const size_t m = std::max<size_t>(n, 1024);
+      HIPC(hipMalloc((void**)&c->dq, m * sizeof(kg_query)));
+      HIPC(hipMalloc((void**)&c->dout, m));
+      HIPC(hipMalloc((void**)&c->derr, m * 4));
+      c->dq_cap = m;
+    }
+    if (n) HIPC(hipMemcpyAsync(c->dq, q, n * sizeof(kg_query), hipMemcpyHostToDevice, c->run));
+  }
+  if (int rc = shard_check(s, c, c->dq, n, gdepth, c->dout, c->derr, stats)) return rc;
+  std::lock_guard<std::mutex> lk(c->mu);
+  if (n) {
+    HIPC(hipMemcpyAsync(out, c->dout, n, hipMemcpyDeviceToHost, c->run));
+    if (err) HIPC(hipMemcpyAsync(err, c->derr, n * 4, hipMemcpyDeviceToHost, c->run));
+  }
+  HIPC(hipStreamSynchronize(c->run));
+  return 0;
+}
+
+int shard_check_host_entry(Snapshot* s, const kg_query* q, size_t n, int32_t gdepth, uint8_t* out, uint32_t* err,
+                           kg_stats* stats) {
+  ShardComm* c = shard_comm_of(s, nullptr);
+  if (!c) return set_error(-2, "sharded snapshot: bind a transport to its own stream first (kg_shard_comm_init)");
+  return shard_check_host(s, c, q, n, gdepth, out, err, stats);
+}
+
+}  // namespace kg
+
+using kg::set_error;
+
+extern "C" {
+
+int kg_shard_unique_id(void* id) {
+  if (!id) return set_error(-2, "NULL argument");
+  ncclUniqueId u;
+  ncclResult_t r = ncclGetUniqueId(&u);
+  if (r != ncclSuccess) return set_error(-1, "ncclGetUniqueId: %s", ncclGetErrorString(r));
+  static_assert(sizeof(u) == KG_SHARD_UNIQUE_ID_BYTES, "ncclUniqueId size");
+  memcpy(id, &u, sizeof u);
+  return 0;
+}
+
+int kg_shard_comm_init(kg_snapshot* sp, const void* id, int rank, int world, void* stream) {
+  try {
+    if (!sp || !id) return set_error(-2, "NULL argument");
+    if (world < 1 || world > KG_SHARD_MAX_RANKS || rank < 0 || rank >= world)
+      return set_error(-2, "bad rank %d of %d", rank, world);
+    kg::Snapshot* s = reinterpret_cast<kg::Snapshot*>(sp);
+    HIPC(hipSetDevice(s->device));
+    kg::ShardComm* c = new kg::ShardComm();
+    c->rank = rank;
+    c->world = world;
+    ncclUniqueId u;
+    memcpy(&u, id, sizeof u);
+    ncclResult_t r = ncclCommInitRank(&c->nccl, world, u, rank);
+    if (r != ncclSuccess) {
+      c->nccl = nullptr;
+      delete c;
+      return set_error(-1, "ncclCommInitRank: %s", ncclGetErrorString(r));
+    }
+    c->t = kg_shard_transport{c, rank, world, 0, kg::rccl_alltoall2, kg::rccl_allgather, kg::rccl_allreduce_max};
+    if (int rc = kg::bind(s, c, (hipStream_t)stream)) {
+      delete c;
+      return rc;
+    }
+    return 0;
+  } catch (...) {
+    return set_error(-4, "kg_shard_comm_init: exception");
+  }
+}
+
+int kg_shard_transport_attach(kg_snapshot* sp, const kg_shard_transport* t, void* stream) {
+  try {
+    if (!sp || !t || !t->alltoall2 || !t->allgather || !t->allreduce_max_u64) return set_error(-2, "NULL argument");
+    if (t->world < 1 || t->world > KG_SHARD_MAX_RANKS || t->rank < 0 || t->rank >= t->world)
+      return set_error(-2, "bad rank %d of %d", t->rank, t->world);
+    kg::Snapshot* s = reinterpret_cast<kg::Snapshot*>(sp);
+    HIPC(hipSetDevice(s->device));
+    kg::ShardComm* c = new kg::ShardComm();
+    c->rank = t->rank;
+    c->world = t->world;
+    c->t = *t;
+    if (int rc = kg::bind(s, c, (hipStream_t)stream)) {
+      delete c;
+      return rc;
+    }
+    return 0;
+  } catch (...) {
+    return set_error(-4, "kg_shard_transport_attach: exception");
+  }
+}
+
+int kg_shard_comm_release(kg_snapshot* sp, void* stream) {
+  if (!sp) return set_error(-2, "NULL snapshot");
+  kg::Snapshot* s = reinterpret_cast<kg::Snapshot*>(sp);
+  std::lock_guard<std::mutex> lk(s->comm_mu);
+  for (auto it = s->comms.begin(); it != s->comms.end(); ++it)
+    if ((*it)->bound == (hipStream_t)stream) {
+      delete *it;
+      s->comms.erase(it);
+      return 0;
+    }
+  return set_error(-2, "no transport bound to this stream");
+}
+
+int kg_shard_comm_stats(const kg_snapshot* sp, void* stream, uint64_t out8[8]) {
+  if (!sp || !out8) return set_error(-2, "NULL argument");
+  kg::Snapshot* s = const_cast<kg::Snapshot*>(reinterpret_cast<const kg::Snapshot*>(sp));
+  kg::ShardComm* c = kg::shard_comm_of(s, (hipStream_t)stream);
+  if (!c) return set_error(-2, "no transport bound to this stream");
+  memcpy(out8, c->st, sizeof c->st);
+  return 0;
+}
+
+}  // extern "C"

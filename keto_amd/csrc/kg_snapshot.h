@@ -154,6 +154,34 @@ struct ShardCtx {
 };
 
 struct Snapshot;
+struct ShardComm;  // kg_shard_comm.hip: a transport bound to one stream's sharded batches
+
+// A deep copy of the kg_dict + kg_rewrite_prog a snapshot was built with (the sharded general phase
+// builds a snapshot of gathered rows with the same program).
+struct ProgCopy {
+  bool have = false;
+  kg_dict dict{};
+  std::vector<uint8_t> ns_has_rel;
+  std::vector<uint32_t> rel_ns, rel_rel;
+  std::vector<int32_t> rel_root;
+  std::vector<kg_rw_node> rw;
+  std::vector<int32_t> child;
+  kg_rewrite_prog view() const {
+    kg_rewrite_prog p{};
+    p.n_ns = (uint32_t)ns_has_rel.size();
+    p.ns_has_rel = ns_has_rel.data();
+    p.n_rel = (uint32_t)rel_ns.size();
+    p.rel_ns = rel_ns.data();
+    p.rel_rel = rel_rel.data();
+    p.rel_root = rel_root.data();
+    p.n_rw = (uint32_t)rw.size();
+    p.rw = rw.data();
+    p.n_child = (uint32_t)child.size();
+    p.child = child.data();
+    return p;
+  }
+};
+
 // Host-buffer batches (kg_check_batch, kg_expand_batch): a call checks out one lane set (one lane per
 // replica -- its own HIP stream, hence its own batch workspace, pinned staging for queries and
 // results, and device buffers, all grown on demand) from the snapshot's bounded pool and returns it
@@ -217,9 +245,14 @@ struct Snapshot {
   // can be in flight at once; created by the first kg_shard_seed on a stream
   std::vector<ShardCtx*> shard_ctxs;
   ShardCtx* shard_ctx(hipStream_t st, bool create = true);  // st == NULL: the snapshot's stream
+  // sharded batches inside the library (kg_shard_comm.hip): a transport per stream
+  std::mutex comm_mu;
+  std::vector<ShardComm*> comms;
+  ProgCopy prog_copy;  // the program the snapshot was built with (the general phase's region snapshots)
   uint32_t* shard_held = nullptr;  // holder bitmap OR-ed over every rank (kg_shard_held), or null
   uint32_t shard_held_n = 0;
   int shard_vis_log2 = 23;
+  uint32_t shard_bucket0 = 0;  // kg_snapshot_tune("shard_bucket"): first bucket size of new in-library bindings (0: by batch)
   uint32_t shard_wgs = 8;  // kg_snapshot_tune("shard_wgs"): k_shard_level workgroups per CU
   int shard_pack = 0;  // kg_snapshot_tune("shard_pack"): packed local records in kg_shard_levels (D_ROW; measured neutral)
   uint32_t shard_heavy = 64;  // kg_snapshot_tune("shard_heavy"): set rows longer than this go to k_shard_heavy (r3p A/B)
@@ -324,6 +357,13 @@ int shard_held(Snapshot* s, uint32_t* d_bits, size_t words, int import, hipStrea
 int shard_finish(Snapshot* s, size_t n, uint8_t* d_res, uint32_t* d_err, hipStream_t stream);
 size_t shard_result_slots(const Snapshot* s, size_t n);
 int shard_bad_nodes(Snapshot* s, uint64_t* count);
+// kg_shard_comm.hip: sharded batches inside the library
+void shard_comms_free(Snapshot* s);
+ShardComm* shard_comm_of(Snapshot* s, hipStream_t st);  // the transport bound to st, or null
+int shard_check(Snapshot* s, ShardComm* c, const kg_query* d_q, size_t n, int32_t gdepth, uint8_t* d_out,
+                uint32_t* d_err, kg_stats* stats);
+int shard_check_host_entry(Snapshot* s, const kg_query* q, size_t n, int32_t gdepth, uint8_t* out, uint32_t* err,
+                           kg_stats* stats);  // kg_check_batch on a sharded snapshot (its own stream's binding)
 // kg_grid.hip
 int grid_reserve(Snapshot* s);  // allocates the shared full-size grid pool now (kg_snapshot_tune "grid_reserve")
 // kg_expand.hip

@@ -235,6 +235,7 @@ static uint64_t pow2_at_least(uint64_t x) {
 }
 
 Snapshot::~Snapshot() {
+  shard_comms_free(this);  // before the streams and buffers they use
   for (auto& set : lane_sets)
     for (Lane* l : set) delete l;  // before the workspaces: a lane's stream owns one of them
   for (Snapshot* p : peers) delete p;
@@ -596,6 +597,18 @@ int Snapshot::build_reverse() {
 
 // Upload the rewrite program and the (ns,rel) flag table (dense n_ns x n_rel).
 int Snapshot::upload_program(const kg_dict* dict, const kg_rewrite_prog* prog) {
+  prog_copy = ProgCopy{};
+  prog_copy.have = true;
+  if (dict) prog_copy.dict = *dict;
+  else prog_copy.dict = kg_dict{0, 0, 0xFFFFFFFFu};
+  if (prog) {
+    prog_copy.ns_has_rel.assign(prog->ns_has_rel, prog->ns_has_rel + prog->n_ns);
+    prog_copy.rel_ns.assign(prog->rel_ns, prog->rel_ns + prog->n_rel);
+    prog_copy.rel_rel.assign(prog->rel_rel, prog->rel_rel + prog->n_rel);
+    prog_copy.rel_root.assign(prog->rel_root, prog->rel_root + prog->n_rel);
+    prog_copy.rw.assign(prog->rw, prog->rw + prog->n_rw);
+    prog_copy.child.assign(prog->child, prog->child + prog->n_child);
+  }
   ds.n_ns = std::max<uint32_t>(dict ? dict->n_namespaces : 0, prog ? prog->n_ns : 0);
   ds.n_rel = dict ? dict->n_relations : 0;
   if (prog)

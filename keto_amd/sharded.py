@@ -28,6 +28,11 @@ gdepth + 1 subject-set hops of its root are gathered to its home rank and the si
 (rewrite interpreter included) answers it on a snapshot of them.  The local steps are
 `ShardOps` objects: `HipShardOps` runs them on the GPU through the C ABI; the multi-rank CPU
 tests substitute a test-only restatement to exercise this exchange protocol under gloo.
+
+Round 4: the product path is `LibShardedChecker` -- the same fixed-bucket protocol and general phase
+inside libketogpu.so (kg_shard_comm.hip), one kg_check_batch_device call per batch over RCCL, as a
+Go host calls it.  `ShardedChecker` stays as the CPU-tested restatement of the protocol and the
+driver of the opt-in escalation phases (kg_snapshot_tune "shard_budget").
 """
 from __future__ import annotations
 
@@ -185,6 +190,128 @@ class HipShardOps:
             return Engine(snap, Config(gdepth)).batch_check_ids(q7)
         finally:
             snap.close()
+
+
+class GlooTransport:
+    """kg_shard_transport over torch.distributed on host buffers (host_memory 1): any backend that moves
+    CPU tensors (gloo).  The library's hash-sharded batch calls these from kg_check_batch(_device)
+    on the calling thread; the product transport is RCCL (kg_shard_comm_init)."""
+
+    def __init__(self, dist, rank: int, world: int, group=None):
+        import torch
+        self.dist, self.rank, self.world, self.group, self.torch = dist, rank, world, group, torch
+        self.error = None
+        L = _lib.load()
+        self._fns = (_lib.ALLTOALL2_FN(self._alltoall2), _lib.ALLGATHER_FN(self._allgather),
+                     _lib.ALLREDUCE_FN(self._allreduce))  # kept alive as long as the binding
+        self.struct = _lib.kg_shard_transport(None, rank, world, 1, *self._fns)
+        self.L = L
+
+    def _i32(self, ptr, nbytes):
+        return np.ctypeslib.as_array((C.c_int32 * (nbytes // 4)).from_address(ptr)) if nbytes else np.zeros(0, np.int32)
+
+    def _alltoall2(self, ctx, s0, r0, b0, s1, r1, b1, stream):
+        try:
+            N = self.world
+            for s, r, b in ((s0, r0, b0), (s1, r1, b1)):
+                if not b:
+                    continue
+                src = self.torch.from_numpy(self._i32(s, N * b).copy())
+                dst = self.torch.empty(N * b // 4, dtype=self.torch.int32)
+                self.dist.all_to_all_single(dst, src, group=self.group)
+                self._i32(r, N * b)[:] = dst.numpy()
+            return 0
+        except Exception as x:  # noqa: BLE001 -- a C callback must not raise
+            self.error = x
+            return 1
+
+    def _allgather(self, ctx, s, r, nbytes, stream):
+        try:
+            src = self.torch.from_numpy(self._i32(s, nbytes).copy())
+            dst = self.torch.empty(self.world * (nbytes // 4), dtype=self.torch.int32)
+            self.dist.all_gather_into_tensor(dst, src, group=self.group)
+            self._i32(r, self.world * nbytes)[:] = dst.numpy()
+            return 0
+        except Exception as x:  # noqa: BLE001
+            self.error = x
+            return 1
+
+    def _allreduce(self, ctx, buf, count, stream):
+        try:
+            a = np.ctypeslib.as_array(buf, shape=(count,))
+            t = self.torch.from_numpy(a.astype(np.int64))  # counts and flags < 2^63
+            self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX, group=self.group)
+            a[:] = t.numpy().astype(np.uint64)
+            return 0
+        except Exception as x:  # noqa: BLE001
+            self.error = x
+            return 1
+
+
+class LibShardedChecker:
+    """One rank's side of hash-sharded batches run INSIDE libketogpu.so (kg_shard_comm.hip): seed, the
+    gdepth + 1 levels with their exchanges, finish and the general phase are all one
+    kg_check_batch_device call, as a Go host makes it.  transport "rccl" (default):
+    an RCCL communicator bound to this checker's stream, its unique id broadcast over `dist` (or made
+    locally at world 1); "host": GlooTransport callbacks over `dist` (CPU tensors; two ranks may share
+    one GPU, which RCCL does not allow)."""
+
+    def __init__(self, snapshot, rank: int = 0, world: int = 1, dist=None, group=None, transport: str = "rccl",
+                 stream=None):
+        import torch
+        self.snapshot, self.rank, self.world = snapshot, rank, world
+        self.L = _lib.load()
+        self.stream = stream if stream is not None else torch.cuda.Stream()
+        self._sp = C.c_void_p(self.stream.cuda_stream)
+        self.transport = transport
+        if transport == "rccl":
+            uid = (C.c_uint8 * _lib.KG_SHARD_UNIQUE_ID_BYTES)()
+            if rank == 0:
+                _lib.check(self.L.kg_shard_unique_id(uid), "kg_shard_unique_id")
+            if world > 1:
+                t = torch.tensor(bytearray(uid), dtype=torch.uint8)
+                if dist.get_backend(group) == "nccl":
+                    t = t.cuda()
+                dist.broadcast(t, 0, group=group)
+                C.memmove(uid, bytes(t.cpu().numpy().tobytes()), _lib.KG_SHARD_UNIQUE_ID_BYTES)
+            _lib.check(self.L.kg_shard_comm_init(snapshot.handle, uid, rank, world, self._sp), "kg_shard_comm_init")
+            self._t = None
+        elif transport == "host":
+            self._t = GlooTransport(dist, rank, world, group)
+            self._check_t(self.L.kg_shard_transport_attach(snapshot.handle, C.byref(self._t.struct), self._sp),
+                          "kg_shard_transport_attach")
+        else:
+            raise ValueError("transport must be 'rccl' or 'host'")
+
+    def _check_t(self, rc, what):
+        if rc != 0 and self._t is not None and self._t.error is not None:
+            raise _lib.KetoGPUError(f"{what}: transport callback failed: {self._t.error!r}")
+        _lib.check(rc, what)
+
+    def check(self, dq, gdepth: int):
+        """dq: (n, 7) int32 kg_query rows of THIS rank's queries (device tensor).  Returns (res u8, err i32)
+        device tensors, ordered after the caller's current stream's work."""
+        import torch
+        n = int(dq.shape[0])
+        res = torch.empty(max(n, 1), dtype=torch.uint8, device=dq.device)
+        err = torch.empty(max(n, 1), dtype=torch.int32, device=dq.device)
+        self.stream.wait_stream(torch.cuda.current_stream())
+        self._check_t(self.L.kg_check_batch_device(self.snapshot.handle, dq.data_ptr() if n else None, n, gdepth,
+                                                   res.data_ptr(), err.data_ptr(), None, self._sp),
+                      "kg_check_batch_device (sharded)")
+        torch.cuda.current_stream().wait_stream(self.stream)
+        return res[:n], err[:n]
+
+    def stats(self) -> dict:
+        out = (C.c_uint64 * 8)()
+        _lib.check(self.L.kg_shard_comm_stats(self.snapshot.handle, self._sp, out), "kg_shard_comm_stats")
+        keys = ("levels", "records_sent", "host_syncs", "reruns_bucket", "reruns_visited", "general_queries",
+                "general_rows", "bucket")
+        return dict(zip(keys, (int(x) for x in out)))
+
+    def close(self):
+        if self.snapshot.handle:
+            self.L.kg_shard_comm_release(self.snapshot.handle, self._sp)
 
 
 KG_SUBJECT_ID = 0xFFFFFFFF

@@ -169,6 +169,38 @@ def test_owner_matches_library():
         assert L.kg_shard_owner(ns, obj, n) == shard_owner(ns, obj, n)
 
 
+class _LibAdapter:
+    """keto_amd.sharded.LibShardedChecker (the whole batch inside libketogpu.so) with ShardedChecker's
+    counters, so the same workers and assertions run both drivers."""
+
+    def __init__(self, snap, rank, world, dist_, transport):
+        from keto_amd.sharded import LibShardedChecker
+        self.chk = LibShardedChecker(snap, rank, world, dist_, transport=transport)
+        self.levels = self.host_syncs = self.back_levels = self.general_queries = 0
+        self.reruns = {1: 0, 2: 0}
+
+    def check(self, dq, gmax):
+        r = self.chk.check(dq, gmax)
+        st = self.chk.stats()
+        self.levels = st["levels"]
+        self.host_syncs += st["host_syncs"]
+        self.reruns[1] += st["reruns_bucket"]
+        self.reruns[2] += st["reruns_visited"]
+        self.general_queries += st["general_queries"]
+        return r
+
+
+def _checker(driver, snap, rank, world, dist_, cap=256):
+    """driver "py": keto_amd.sharded.ShardedChecker over the kg_shard_* steps; "lib": the in-library batch
+    over RCCL (world 1) or the gloo host transport (world > 1: ranks share the one GPU, which RCCL does
+    not allow); "lib-rccl" / "lib-host": that transport explicitly."""
+    from keto_amd.sharded import HipShardOps, ShardedChecker
+    if driver == "py":
+        return ShardedChecker(HipShardOps(snap), rank, world, dist_, device="cuda", cap=cap)
+    transport = driver.split("-")[1] if "-" in driver else ("rccl" if world == 1 else "host")
+    return _LibAdapter(snap, rank, world, dist_, transport)
+
+
 # ------------------------------------------------------------------ GPU (HIP local steps)
 def _gpu_worker(rank, world, port, seed, outq, budget=None, back_budget=None, vis_mode=0):
     sys.path.insert(0, ROOT)
@@ -423,7 +455,7 @@ def _opl_full_example_graph(seed, n_q=2000):
     return it, it.tuples_array(tuples), queries_array(q6, rng.integers(-1, 8, len(qs))), prog, prog_ref
 
 
-def _general_gpu_worker(rank, world, port, outq, kind):
+def _general_gpu_worker(rank, world, port, outq, kind, driver="py"):
     sys.path.insert(0, ROOT)
     import torch.distributed as dist
     from keto_amd.engine import Snapshot
@@ -443,7 +475,7 @@ def _general_gpu_worker(rank, world, port, outq, kind):
         it, t6, q, prog, _ = _impure_graph(5)
     snap = Snapshot(t6, it, prog, 0, shard=(rank, world))
     mine = np.array_split(np.arange(len(q)), world)[rank]
-    chk = ShardedChecker(HipShardOps(snap), rank, world, dist_, device="cuda", cap=256)
+    chk = _checker(driver, snap, rank, world, dist_)
     out = {}
     for gmax in (2, 5, 8):
         res, err = chk.check(torch.from_numpy(q[mine].view(np.int32).copy()).cuda(), gmax)
@@ -454,8 +486,11 @@ def _general_gpu_worker(rank, world, port, outq, kind):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("kind,world", [("impure", 1), ("opl", 1), ("opl", 2), ("order", 1), ("order", 2)])
-def test_sharded_general_rewrites_vs_oracle(kind, world):
+@pytest.mark.parametrize("kind,world,driver", [("impure", 1, "py"), ("opl", 1, "py"), ("opl", 2, "py"),
+                                               ("order", 1, "py"), ("order", 2, "py"), ("impure", 1, "lib"),
+                                               ("opl", 1, "lib"), ("opl", 2, "lib"), ("order", 1, "lib"),
+                                               ("order", 2, "lib"), ("impure", 2, "lib")])
+def test_sharded_general_rewrites_vs_oracle(kind, world, driver):
     """Every rewrite in the hash-sharded mode: the reference parser's full example (a `view` formula
     recursive through tuple-to-subject-set, `not`, nested traverse) and a program with a computed
     rewrite and undeclared relations.  Queries the level protocol ends as NOT_IMPLEMENTED go to the
@@ -467,7 +502,7 @@ def test_sharded_general_rewrites_vs_oracle(kind, world):
     ctx = mp.get_context("spawn")
     outq = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_general_gpu_worker, args=(r, world, port, outq, kind)) for r in range(world)]
+    ps = [ctx.Process(target=_general_gpu_worker, args=(r, world, port, outq, kind, driver)) for r in range(world)]
     for p in ps:
         p.start()
     got = [outq.get(timeout=150) for _ in range(world)]
@@ -496,7 +531,7 @@ def test_sharded_general_rewrites_vs_oracle(kind, world):
 
 # ------------------------------------------------------------------ config C4 generator, sharded
 def _synth_worker(rank, world, port, n_tuples, n_q, gmax, backend, outq, preset=0, budget=None, back_budget=None,
-                  vis_mode=0, heavy=None, pack=None, vis=None, bucket=None):
+                  vis_mode=0, heavy=None, pack=None, vis=None, bucket=None, driver="py"):
     sys.path.insert(0, ROOT)
     import torch.distributed as dist
     from keto_amd import _lib
@@ -524,8 +559,10 @@ def _synth_worker(rank, world, port, n_tuples, n_q, gmax, backend, outq, preset=
     dq = torch.empty((n_q, 7), dtype=torch.int32, device="cuda")
     _lib.check(_lib.load().kg_synth_queries(snap.handle, 31, n_q, dq.data_ptr()), "kg_synth_queries")
     mine = np.array_split(np.arange(n_q), world)[rank]
-    chk = ShardedChecker(HipShardOps(snap), rank, world, dist_, device="cuda", cap=1 << 14)
-    if bucket is not None:  # fixed-bucket protocol: B records per destination, far too few
+    if bucket is not None and driver != "py":  # in-library: the first bucket size of the binding
+        snap.tune("shard_bucket", bucket)
+    chk = _checker(driver, snap, rank, world, dist_, cap=1 << 14)
+    if bucket is not None and driver == "py":  # fixed-bucket protocol: B records per destination, far too few
         chk.bucket = bucket
     mq = dq[mine[0]:mine[-1] + 1].contiguous()
     res0, err0 = chk.check(mq, gmax)  # the first batch grows the buckets to fit (overflow reruns)
@@ -587,14 +624,14 @@ def test_sharded_c3_rewrites_vs_oracle(world, backend):
 
 
 def _run_synth(world, backend, n_tuples, n_q, gmax, preset, budget=None, back_budget=None, vis_mode=0, heavy=None,
-               pack=None, vis=None, bucket=None):
+               pack=None, vis=None, bucket=None, driver="py"):
     from keto_amd.engine import Snapshot
     from oracle.oracle import POLICY_CANONICAL, Oracle
     ctx = mp.get_context("spawn")
     outq = ctx.Queue()
     port = _free_port()
     ps = [ctx.Process(target=_synth_worker, args=(r, world, port, n_tuples, n_q, gmax, backend, outq, preset, budget,
-                                                  back_budget, vis_mode, heavy, pack, vis, bucket))
+                                                  back_budget, vis_mode, heavy, pack, vis, bucket, driver))
           for r in range(world)]
     for p in ps:
         p.start()
@@ -611,8 +648,10 @@ def _run_synth(world, backend, n_tuples, n_q, gmax, preset, budget=None, back_bu
     for rank, mine, r, e, levels, syncs, _, mat, back_levels, reruns in got:
         assert (e == 0).all(), (rank, np.nonzero(e)[0][:10])
         res[mine] = r
-        if world == 1 and backend is None:
+        if world == 1 and backend is None and driver == "py":
             assert syncs == 1 and levels == gmax  # one host round trip for the whole batch
+        if driver != "py":  # in-library: the agreement all-reduce and the end-of-batch one, no rerun
+            assert syncs == 2 and levels == gmax + 1, (syncs, levels)
         if budget is not None and budget <= 8 and not preset:
             assert back_levels > 0  # the backward phase ran
         if preset:
@@ -627,8 +666,25 @@ def _run_synth(world, backend, n_tuples, n_q, gmax, preset, budget=None, back_bu
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("world,backend,preset,driver", [(1, None, 0, "lib"), (1, None, 1, "lib"),
+                                                         (2, "gloo", 0, "lib"), (2, "gloo", 1, "lib"),
+                                                         (1, "gloo", 0, "lib-host")])
+def test_sharded_in_library_vs_oracle(world, backend, preset, driver):
+    """The hash-sharded batch inside libketogpu.so (kg_shard_comm.hip: one kg_check_batch_device call per
+    batch, as a Go host makes it): C4's generator (preset 0) and C3's (preset 1: union nodes across ranks,
+    split formulas) at world 1 over RCCL and at world 2 over the gloo host transport (two ranks on one
+    GPU), bit-exact with the oracle on the whole graph; two host round trips per batch, gdepth + 1 levels."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    _run_synth(world, backend, 300_000 if preset == 0 else 150_000, 20_000 if preset == 0 else 6000, 10, preset=preset,
+               driver=driver)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("world,backend,vis,bucket", [(1, None, 10, None), (2, "gloo", 10, None),
-                                                      (2, "gloo", None, 64), (1, "nccl", 11, None)])
+                                                      (2, "gloo", None, 64), (1, "nccl", 11, None),
+                                                      ("lib", None, 10, None), ("lib", None, None, 64),
+                                                      ("lib2", "gloo", 10, 64)])
 def test_sharded_visited_overflow_reruns(world, backend, vis, bucket):
     """Regression (round 3: "records left after 10 levels" on C3 sharded, an overflow flag OR-ed into a
     sub-bucket count in kg_shard.hip): a C3-shaped graph with a per-batch (query, node) visited table
@@ -638,7 +694,10 @@ def test_sharded_visited_overflow_reruns(world, backend, vis, bucket):
     with bigger ones (reference semantics: internal/check/engine.go:87-145)."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    _run_synth(world, backend, 150_000, 6000, 10, preset=1, vis=vis, bucket=bucket)
+    driver = "py"
+    if world in ("lib", "lib2"):  # the same through the in-library batch (kg_shard_comm.hip)
+        driver, world = "lib", (1 if world == "lib" else 2)
+    _run_synth(world, backend, 150_000, 6000, 10, preset=1, vis=vis, bucket=bucket, driver=driver)
 
 
 @pytest.mark.gpu
