@@ -552,6 +552,9 @@ int shard_check(Snapshot* s, ShardComm* c, const kg_query* d_q, size_t n, int32_
       c->recs = (size_t)N * B;
     }
     HIPC(hipMemsetAsync(acc, 0, 12 * 8, st));
+    // both count buffers start clear: the flags word counts[k][N] accumulates over the levels that
+    // write buffer k, and shard_seed / shard_level clear only what they write
+    HIPC(hipMemsetAsync(c->cnt, 0, (3 * (size_t)N + 2) * 4, st));
     if (int rc = shard_seed(s, d_q, n, gdepth, c->buf[0], B, counts[0], c->res, c->err, st)) return rc;
     int cur = 0;
     for (int k = 0; k <= gdepth; k++) {
