@@ -139,7 +139,12 @@ def parse(argv=None):
                     help="--mode host: native caller threads of the request batcher (one blocking call per request)")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for --mode sharded (nccl = RCCL)")
     ap.add_argument("--shard-protocol", default="auto", choices=["auto", "fixed", "dynamic"],
-                    help="--mode sharded exchange protocol (keto_amd.sharded.ShardedChecker)")
+                    help="--mode sharded --shard-driver py: exchange protocol (keto_amd.sharded.ShardedChecker)")
+    ap.add_argument("--shard-driver", default="lib", choices=["lib", "py"],
+                    help="--mode sharded: lib = the whole batch inside libketogpu.so over RCCL (kg_shard_comm_init; "
+                         "the gloo host transport with --backend gloo), one kg_check_batch_device call per batch as "
+                         "a Go host makes it; py = keto_amd.sharded.ShardedChecker driving the kg_shard_* steps "
+                         "(needed for --shard-budget)")
     ap.add_argument("--roots", type=int, default=100_000, help="expand roots per step (C5)")
     ap.add_argument("--expand-tail", type=int, default=1,
                     help="kg_snapshot_tune expand_tail (1: passes 2/3 walk with LDS-cached frames; 0: round 2's walk)")
@@ -416,9 +421,12 @@ def bench_sharded(a):
     process group.  Weak scaling: B checks per rank per step."""
     import torch
     from keto_amd import _lib
-    from keto_amd.sharded import HipShardOps, ShardedChecker
+    from keto_amd.sharded import HipShardOps, LibShardedChecker, ShardedChecker
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    lib = a.shard_driver == "lib"
+    if lib and a.shard_budget:
+        raise SystemExit("--shard-budget (escalation) runs with --shard-driver py")
     # one rank per GPU; ranks beyond the GPU count share GPUs (a gloo rehearsal on a 1-GPU box)
     local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
     dist = None
@@ -452,8 +460,22 @@ def bench_sharded(a):
     groups = [None] * P
     if dist is not None and P > 1:
         groups = [dist.new_group(list(range(world))) for _ in range(P)]
-    chks = [ShardedChecker(HipShardOps(snap), rank, world, dist, device=f"cuda:{local}", cap=1 << 22,
-                           protocol=a.shard_protocol, group=groups[p]) for p in range(P)]
+    if lib:  # one communicator per in-flight stream (RCCL ids broadcast over the default group, in order)
+        transport = "rccl" if a.backend == "nccl" else "host"
+        chks = [LibShardedChecker(snap, rank, world, dist, group=groups[p], transport=transport) for p in range(P)]
+    else:
+        chks = [ShardedChecker(HipShardOps(snap), rank, world, dist, device=f"cuda:{local}", cap=1 << 22,
+                               protocol=a.shard_protocol, group=groups[p]) for p in range(P)]
+
+    def cstats(c):  # the counters both drivers report
+        if lib:
+            st = c.stats()
+            return {"levels": st["levels"], "back_levels": 0, "final_levels": 0, "records_sent": st["records_sent"],
+                    "host_syncs": st["host_syncs"], "bucket": st["bucket"], "level_records": None,
+                    "general_queries": st["general_queries"]}
+        return {"levels": c.levels, "back_levels": c.back_levels, "final_levels": c.final_levels,
+                "records_sent": c.records_sent, "host_syncs": c.host_syncs, "bucket": c.bucket,
+                "level_records": c.level_records, "general_queries": c.general_queries}
     for p in range(P):  # warm-up: each checker sizes its buckets / per-stream state
         for _ in range(max(1, a.warmup // P)):
             chks[p].check(dqs[p % n_distinct], a.global_depth)
@@ -463,20 +485,23 @@ def bench_sharded(a):
     torch.cuda.synchronize()
     lat, outs, errors = [], [None] * P, []
     sent = [0] * P
-    syncs0 = [c.host_syncs for c in chks]
+    syncs = [0] * P
     go = threading.Barrier(P + 1)
 
     def worker(p):
         try:
             go.wait()
             # this thread's current stream is its checker's own: no ordering through a shared stream
-            with torch.cuda.stream(chks[p].ops.torch_stream):
+            with torch.cuda.stream(chks[p].stream if lib else chks[p].ops.torch_stream):
                 for k in range(p, a.steps, P):
                     s0 = time.perf_counter()
+                    h0 = chks[p].host_syncs if not lib else 0
                     res, err = chks[p].check(dqs[k % n_distinct], a.global_depth)
                     torch.cuda.current_stream().synchronize()
                     lat.append(time.perf_counter() - s0)
-                    sent[p] += chks[p].records_sent
+                    st = cstats(chks[p])
+                    sent[p] += st["records_sent"]
+                    syncs[p] += st["host_syncs"] - h0
                     outs[p] = (res, err)
         except Exception as e:  # noqa: BLE001
             errors.append(e)
@@ -499,7 +524,7 @@ def bench_sharded(a):
         r = o[0].cpu().numpy()
         assert (o[1].cpu().numpy() == 0).all() and (r <= 1).all(), "unexpected errors in the synthetic batch"
     elapsed, recs = aggregate(dist, elapsed, float(sum(sent)), f"cuda:{local}" if a.backend == "nccl" else None)
-    chk = chks[0]
+    cs = cstats(chks[0])
     out = {"metric": "permission checks/sec (batched check, synthetic Drive-like graph, hash-sharded)",
            "value": world * B * a.steps / elapsed, "unit": "checks/s", "n_gpus": world, "steps": a.steps,
            "warmup": a.warmup, "ms_per_step": elapsed / a.steps * 1e3, "higher_is_better": True, "scaling": "weak",
@@ -510,16 +535,19 @@ def bench_sharded(a):
                                                          a.global_depth),
                       "materialized": snap.materialized() if a.preset else None,
                       "rows_on_rank": info["rows"], "nodes": info["nodes"], "batch_per_gpu": B,
-                      "inflight_per_gpu": P, "protocol": a.shard_protocol, "parallelism": f"shard{world}"},
+                      "inflight_per_gpu": P, "driver": ("in-library kg_check_batch_device (kg_shard_comm.hip, %s)"
+                                                        % ("RCCL" if a.backend == "nccl" else "host transport")
+                                                        if lib else "keto_amd.sharded.ShardedChecker"),
+                      "protocol": "fixed" if lib else a.shard_protocol, "parallelism": f"shard{world}"},
            "p99_batch_ms": float(np.percentile(np.array(lat) * 1e3, 99)),
            "batch_ms_p50": float(np.percentile(np.array(lat) * 1e3, 50)),
            "allowed_fraction": float(outs[0][0].float().mean().item()) if outs[0] is not None else None,
-           "levels_per_batch": chk.levels, "backward_levels_per_batch": chk.back_levels,
-           "final_levels_per_batch": chk.final_levels, "shard_budget": a.shard_budget,
-           "host_syncs_per_batch": (sum(c.host_syncs for c in chks) - sum(syncs0)) / max(1, a.steps),
-           "bucket": chk.bucket, "shard_back_budget": a.shard_back_budget, "shard_vis_mode": a.shard_vis_mode,
+           "levels_per_batch": cs["levels"], "backward_levels_per_batch": cs["back_levels"],
+           "final_levels_per_batch": cs["final_levels"], "shard_budget": a.shard_budget,
+           "host_syncs_per_batch": sum(syncs) / max(1, a.steps),
+           "bucket": cs["bucket"], "shard_back_budget": a.shard_back_budget, "shard_vis_mode": a.shard_vis_mode,
            "shard_heavy": a.shard_heavy, "shard_pack": a.shard_pack, "records_exchanged_per_batch": recs / a.steps,
-           **({"level_records": chk.level_records} if chk.level_records else {}),
+           **({"level_records": cs["level_records"]} if cs["level_records"] else {}),
            "snapshot_build_s": t_build}
     bad = 0
     if rank == 0 and world == 1 and a.parity > 0:

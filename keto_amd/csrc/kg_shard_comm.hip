@@ -271,6 +271,20 @@ __global__ void k_sc_final(const uint32_t* __restrict__ c, uint32_t N, uint32_t 
   }
 }
 
+// One rank (kg_shard_levels' device loop): tot = (bucket overflow, visited overflow, 0, records left, 0)
+// from the flags words of both buffers and the count of the last one.
+__global__ void k_sc_final1(const uint32_t* __restrict__ c0, const uint32_t* __restrict__ c1, int end,
+                            unsigned long long* tot) {
+  if (threadIdx.x == 0) {
+    const uint32_t f = c0[1] | c1[1];
+    tot[0] = f & 1u;
+    tot[1] = (f >> 1) & 1u;
+    tot[2] = 0;
+    tot[3] = end ? c1[0] : c0[0];
+    tot[4] = 0;
+  }
+}
+
 // tot[4] = 1 when some query of [0, n) ended KG_ERROR / KG_ERR_NOT_IMPLEMENTED (general phase).
 __global__ void k_sc_open(uint32_t n, const uint8_t* __restrict__ res, const uint32_t* __restrict__ err,
                           unsigned long long* tot) {
@@ -515,11 +529,14 @@ int shard_check(Snapshot* s, ShardComm* c, const kg_query* d_q, size_t n, int32_
       if (!e) HIPC(hipEventCreate(&e));
     HIPC(hipEventRecord(c->ev[0], st));
   }
-  // the largest result-slot count of any rank: the done bitmap's width (host round trip 1)
+  // the largest result-slot count of any rank: the done bitmap's width (host round trip 1; one rank
+  // needs none)
   const size_t slots = shard_result_slots(s, n);
   uint64_t smax = slots;
-  if (int rc = h_allreduce_max(c, &smax, 1)) return rc;
-  c->st[2]++;
+  if (N > 1) {
+    if (int rc = h_allreduce_max(c, &smax, 1)) return rc;
+    c->st[2]++;
+  }
   const uint32_t words = (uint32_t)((smax + 31) / 32);
   if (grow((void**)&c->bits, &c->words_cap, (size_t)words + 1, 4)) return -1;
   if (grow((void**)&c->bits_all, &c->all_cap, (size_t)N * words + 1, 4)) return -1;
@@ -557,7 +574,17 @@ int shard_check(Snapshot* s, ShardComm* c, const kg_query* d_q, size_t n, int32_
     HIPC(hipMemsetAsync(c->cnt, 0, (3 * (size_t)N + 2) * 4, st));
     if (int rc = shard_seed(s, d_q, n, gdepth, c->buf[0], B, counts[0], c->res, c->err, st)) return rc;
     int cur = 0;
-    for (int k = 0; k <= gdepth; k++) {
+    if (N == 1) {
+      // one rank: nothing to exchange -- gdepth levels back to back in the device loop (per-XCD
+      // sub-buckets, hub rows grid-wide; kg_shard_levels), hit reports stay local
+      kg_frec* bufs[2] = {c->buf[0], c->buf[1]};
+      if (int rc = shard_levels(s, gdepth, bufs, B, counts, 0, c->res, c->err, c->prune ? slots : 0, 0, &cur, st))
+        return rc;
+      c->st[0] += (uint64_t)gdepth;
+      hipLaunchKernelGGL(k_sc_final1, dim3(1), dim3(64), 0, st, counts[0], counts[1], cur, tot);
+      HIPC(hipGetLastError());
+    }
+    for (int k = 0; N > 1 && k <= gdepth; k++) {
       hipLaunchKernelGGL(k_sc_acc, dim3(1), dim3(64), 0, st, counts[cur], N, (uint32_t)B, acc);
       HIPC(hipGetLastError());
       if (int rc = x_alltoall2(c, counts[cur], rcv, 4, c->buf[cur], c->recv, B * sizeof(kg_frec))) return rc;
@@ -574,8 +601,10 @@ int shard_check(Snapshot* s, ShardComm* c, const kg_query* d_q, size_t n, int32_
       cur = nx;
       c->st[0]++;
     }
-    hipLaunchKernelGGL(k_sc_final, dim3(1), dim3(64), 0, st, counts[cur], N, (uint32_t)B, acc, tot);
-    HIPC(hipGetLastError());
+    if (N > 1) {
+      hipLaunchKernelGGL(k_sc_final, dim3(1), dim3(64), 0, st, counts[cur], N, (uint32_t)B, acc, tot);
+      HIPC(hipGetLastError());
+    }
     // results final before the all-reduce, which then also carries "a query needs the general phase"
     if (int rc = shard_finish(s, n, c->res, c->err, st)) return rc;
     if (n) {
@@ -583,7 +612,8 @@ int shard_check(Snapshot* s, ShardComm* c, const kg_query* d_q, size_t n, int32_
                          tot);
       HIPC(hipGetLastError());
     }
-    if (int rc = x_allreduce_max(c, tot, 5)) return rc;
+    if (N > 1)
+      if (int rc = x_allreduce_max(c, tot, 5)) return rc;
     uint64_t h[8];
     HIPC(hipMemcpyAsync(h, tot, 5 * 8, hipMemcpyDeviceToHost, st));
     HIPC(hipMemcpyAsync(h + 5, acc + 2, 8, hipMemcpyDeviceToHost, st));
@@ -591,7 +621,7 @@ int shard_check(Snapshot* s, ShardComm* c, const kg_query* d_q, size_t n, int32_
     c->st[2]++;
     const uint64_t big = h[2];
     if (h[0] || h[1]) {  // dropped records somewhere: every rank reruns with more room
-      if (h[0]) {
+      if (h[0]) {  // (one rank: the device loop does not report its largest bucket)
         c->st[3]++;
         c->bucket = std::max<size_t>(2 * B, (size_t)(big * 1.25) + 1024);
       }
@@ -602,9 +632,9 @@ int shard_check(Snapshot* s, ShardComm* c, const kg_query* d_q, size_t n, int32_
       }
       continue;
     }
-    if (h[3]) return set_error(-1, "sharded batch: records left after %d levels", gdepth + 1);
+    if (h[3]) return set_error(-1, "sharded batch: records left after %d levels", N > 1 ? gdepth + 1 : gdepth);
     // next batch: buckets 25 % above the largest one this batch needed (shrinking slowly)
-    if (big * 2 < B) c->bucket = std::max<size_t>(1024, std::min<size_t>(B, (size_t)(big * 1.25) + 1024));
+    if (N > 1 && big * 2 < B) c->bucket = std::max<size_t>(1024, std::min<size_t>(B, (size_t)(big * 1.25) + 1024));
     c->st[1] = h[5];
     if (h[4])
       if (int rc = general_phase(s, c, d_q, n, gdepth)) return rc;
