@@ -974,8 +974,12 @@ def main():
                 errors.append(e)
 
         th = [threading.Thread(target=lat_worker, args=(p,)) for p in range(P)]
+        torch.cuda.synchronize()
+        t_lat = time.perf_counter()
         [t.start() for t in th]
         [t.join() for t in th]
+        torch.cuda.synchronize()
+        lat_wall = time.perf_counter() - t_lat
         if errors:
             raise errors[0]
         lat_ms = np.array(lat) * 1e3
@@ -1008,6 +1012,10 @@ def main():
                    "materialized": snap.materialized(), "tune": dict(snap.__dict__.get("tuned", {}))},
         "gteps": edges / elapsed / 1e9,
         "p99_batch_ms": float(np.percentile(lat_ms, 99)) if lat_n else None,
+        # the latency phase is a second, longer throughput sample of the same workload (distinct batches,
+        # same batches in flight, every batch waited for): the timed region alone is only a few ms long
+        "steady": ({"value": lat_n * B / lat_wall, "unit": "checks/s", "batches": lat_n, "seconds": lat_wall,
+                    "what": "rank-0 checks/s over the latency phase (outside the timed region)"} if lat_n else None),
         "batch_ms": ({"batches": lat_n, "inflight": P, **{q: float(np.percentile(lat_ms, v)) for q, v in
                      (("p50", 50), ("p90", 90), ("p99", 99), ("max", 100))}} if lat_n else None),
         "edges_per_batch": {q: float(np.percentile([x.edges_read for x in stats], v)) for q, v in
