@@ -109,13 +109,21 @@ struct AdjX {
   uint32_t node, begin, len, sig;
 };
 
+// 31-bit Bloom (bit 31 of a node's signature is SIG_DREC, never set by a subject's mask).
 __host__ __device__ __forceinline__ uint32_t subj_sig(uint32_t subj) {
   uint32_t h = subj * 0x9E3779B1u;
   h ^= h >> 15;
   h *= 0x85EBCA77u;
   h ^= h >> 13;
-  return (1u << (h & 31)) | (1u << ((h >> 5) & 31));
+  return (1u << (h % 31u)) | (1u << ((h >> 5) % 31u));
 }
+// A node's direct subjects (its check row) inline in its 64-B direct record drec[node]: word 0 the
+// count (<= DREC_CAP), words 1.. the tagged subjects.  checkDirect for such a node reads that record
+// -- one line per NODE, shared by every query that probes it (a hot group's record stays in L2 / the
+// Infinity Cache) -- instead of a dset bucket keyed by (node, subject), which is a cold line per query.
+constexpr uint32_t SIG_DREC = 1u << 31;
+constexpr uint32_t DREC_CAP = 15, DREC_WORDS = 16;
+constexpr uint32_t SIG_FULL = 0x7FFFFFFFu;  // every Bloom bit set
 __host__ __device__ __forceinline__ bool sig_maybe(uint32_t sig, uint32_t subj_mask) {
   return (sig & subj_mask) == subj_mask;
 }
@@ -140,6 +148,7 @@ struct DevSnap {
   const uint64_t* adj_off;
   const uint32_t* adj;
   const AdjX* adjx;  // parallel to adj
+  const uint32_t* drec;  // [n_nodes * DREC_WORDS] direct records (nodes whose sig has SIG_DREC), or null
   const uint64_t* row_off;
   const uint32_t* row_subj;
   const uint64_t* crow_off;  // check rows (nullptr: row_off / row_subj)

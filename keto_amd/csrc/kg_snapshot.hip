@@ -10,6 +10,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <new>
@@ -82,11 +83,21 @@ __global__ void k_node_owner(const uint32_t* nd_ns, const uint32_t* nd_obj, uint
 }
 
 // Bloom signature of every node's full row (direct subjects, tagged like dset keys).
-__global__ void k_node_sig(const uint64_t* row_off, const uint32_t* row_subj, uint32_t n_nodes, uint32_t* sig) {
+// Bloom signature of every node's direct subjects; with drec, a node of <= DREC_CAP direct subjects also
+// gets its direct record (count + subjects) and SIG_DREC in its signature.
+__global__ void k_node_sig(const uint64_t* row_off, const uint32_t* row_subj, uint32_t n_nodes, uint32_t* sig,
+                           uint32_t* drec) {
   const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
   if (v >= n_nodes) return;
+  const uint64_t b = row_off[v], e = row_off[v + 1];
   uint32_t m = 0;
-  for (uint64_t i = row_off[v], e = row_off[v + 1]; i < e && m != 0xFFFFFFFFu; i++) m |= subj_sig(row_subj[i]);
+  for (uint64_t i = b; i < e && m != SIG_FULL; i++) m |= subj_sig(row_subj[i]);
+  if (drec && e - b <= DREC_CAP) {
+    uint32_t* r = drec + (uint64_t)v * DREC_WORDS;
+    r[0] = (uint32_t)(e - b);
+    for (uint32_t k = 0; k < DREC_CAP; k++) r[1 + k] = k < e - b ? row_subj[b + k] : NONE;
+    m |= SIG_DREC;
+  }
   sig[v] = m;
 }
 
@@ -438,8 +449,21 @@ int Snapshot::build_hash_tables() {
   // direct tuples as checkDirect sees them: the check rows of a materialised snapshot, else the rows
   const uint64_t* coff = ds.crow_off ? ds.crow_off : ds.row_off;
   const uint32_t* csub = ds.crow_off ? ds.crow_subj : ds.row_subj;
+  // direct records (64 B per node) when they take at most 1/16 of HBM (KG_DREC=0 at build: off)
+  size_t hbm_free0 = 0, hbm_total0 = 0;
+  if (hipMemGetInfo(&hbm_free0, &hbm_total0) != hipSuccess) hbm_total0 = 288ull << 30;
+  (void)hipGetLastError();
+  const char* dr_env = getenv("KG_DREC");
+  uint32_t* drec = nullptr;
+  const uint64_t drec_bytes = (uint64_t)ds.n_nodes * DREC_WORDS * 4;
+  const bool use_drec = ds.n_nodes && !(dr_env && dr_env[0] == '0') && drec_bytes <= hbm_total0 / 16;
+  // (always at least one zeroed record: kernels load record 0 for lanes without a probe)
+  if (alloc((void**)&drec, use_drec ? drec_bytes : DREC_WORDS * 4)) return -1;
+  if (!use_drec) HIPC(hipMemsetAsync(drec, 0, DREC_WORDS * 4, stream));
+  ds.drec = drec;
   if (ds.n_nodes) {
-    hipLaunchKernelGGL(k_node_sig, dim3((ds.n_nodes + 255) / 256), dim3(256), 0, stream, coff, csub, ds.n_nodes, sig);
+    hipLaunchKernelGGL(k_node_sig, dim3((ds.n_nodes + 255) / 256), dim3(256), 0, stream, coff, csub, ds.n_nodes, sig,
+                       use_drec ? drec : nullptr);
     HIPC(hipGetLastError());
   }
   if (n_set_edges) {
