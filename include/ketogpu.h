@@ -477,6 +477,34 @@ int kg_shard_comm_release(kg_snapshot* s, void* stream);
  * the general phase, [6] rows it gathered, [7] bucket size B. */
 int kg_shard_comm_stats(const kg_snapshot* s, void* stream, uint64_t out8[8]);
 
+/* ---- check trees ----------------------------------------------------------------------------
+ * CheckRelationTuple's Result.Tree (internal/check/engine.go:65-80, checkgroup/definitions.go:46-50,
+ * 101-124): for a member, the tree of the branch that answered -- direct tuples, then subject-set rows
+ * in row order, then the rewrite (the reference runs them concurrently; its asserted paths are
+ * rewrites_test.go:186-205).  Every membership the walk relies on comes from kg_check_batch on this
+ * snapshot (batched per row of candidates) and every row from the snapshot's row reads.  *result /
+ * *err_code: the check's answer; the tree (pre-order kg_check_node records, n_children each) only for
+ * KG_IS_MEMBER.  hidden_rels: relations a compiler introduced for tuple-to-subject-set leaves of
+ * boolean rewrites (keto_amd/namespace.py lower_ttu_leaves) -- their computed edge is inlined, as the
+ * reference's tree has the TTU edge there.  cap too small: returns -3 with *n_nodes = records needed.
+ * Not on hash-sharded snapshots.  Not a hot path. */
+#define KG_CTREE_LEAF 1
+#define KG_CTREE_UNION 2
+#define KG_CTREE_INTERSECTION 3 /* an `and`: has_tuple 0 (binop.go:47-50 builds it without one) */
+#define KG_CTREE_COMPUTED 4
+#define KG_CTREE_TTU 5
+#define KG_CTREE_NOT 6
+typedef struct {
+  uint8_t type;      /* KG_CTREE_* */
+  uint8_t has_tuple; /* 0: no tuple (an `and` node) */
+  uint16_t pad;
+  uint32_t n_children;
+  kg_tuple t;        /* the node's tuple (its request tuple) */
+} kg_check_node;
+int kg_check_tree(kg_snapshot* s, const kg_query* q, int32_t global_max_depth, const uint32_t* hidden_rels,
+                  size_t n_hidden, kg_check_node* out, size_t cap, size_t* n_nodes, uint8_t* result,
+                  uint32_t* err_code);
+
 /* ---- expand ----------------------------------------------------------------------------- */
 /* Roots are split over the replicas (chunks of >= 1024 roots, one host thread each). */
 int kg_expand_batch(kg_snapshot* s, const kg_set* roots, size_t n, int32_t global_max_depth, kg_tree_buf* out);

@@ -84,7 +84,7 @@ EXPORTS = ["kg_snapshot_create", "kg_snapshot_create_on", "kg_snapshot_synthetic
            "kg_shard_done", "kg_shard_levels", "kg_shard_back_list", "kg_shard_back_seed", "kg_shard_back_level", "kg_shard_refwd_seed",
            "kg_shard_held_words", "kg_shard_held", "kg_shard_result_slots", "kg_shard_bad_nodes", "kg_batcher_create", "kg_batcher_check", "kg_batcher_stats", "kg_batcher_reset_stats", "kg_batcher_destroy",
            "kg_shard_unique_id", "kg_shard_comm_init", "kg_shard_transport_attach", "kg_shard_comm_release",
-           "kg_shard_comm_stats"]
+           "kg_shard_comm_stats", "kg_check_tree"]
 
 KG_SHARD_UNIQUE_ID_BYTES = 128
 # kg_shard_transport callbacks (include/ketogpu.h): collective over the ranks, 0 = success
@@ -92,6 +92,18 @@ ALLTOALL2_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size
                            C.c_void_p)
 ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p)
 ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_uint64), C.c_size_t, C.c_void_p)
+
+
+class kg_tuple(C.Structure):
+    _fields_ = [(k, C.c_uint32) for k in ("ns", "obj", "rel", "sns", "sobj", "srel")]
+
+
+class kg_check_node(C.Structure):
+    _fields_ = [("type", C.c_uint8), ("has_tuple", C.c_uint8), ("pad", C.c_uint16), ("n_children", C.c_uint32),
+                ("t", kg_tuple)]
+
+
+KG_CTREE = {1: "leaf", 2: "union", 3: "intersection", 4: "computed_subject_set", 5: "tuple_to_subject_set", 6: "not"}
 
 
 class kg_shard_transport(C.Structure):
@@ -179,6 +191,7 @@ def load(path: str = LIB_PATH):
     L.kg_shard_transport_attach.argtypes = [vp, C.POINTER(kg_shard_transport), vp]
     L.kg_shard_comm_release.argtypes = [vp, vp]
     L.kg_shard_comm_stats.argtypes = [vp, vp, vp]
+    L.kg_check_tree.argtypes = [vp, vp, i32, vp, sz, vp, sz, C.POINTER(sz), C.POINTER(C.c_uint8), C.POINTER(u32)]
     L.kg_batcher_create.argtypes = [vp, i32, sz, u32, C.c_int, C.POINTER(vp)]
     L.kg_batcher_check.argtypes = [vp, vp, sz, vp, vp]
     L.kg_batcher_stats.argtypes = [vp, C.POINTER(kg_batcher_stats_t)]
@@ -194,7 +207,7 @@ def load(path: str = LIB_PATH):
                  "kg_shard_done", "kg_shard_levels", "kg_shard_back_list", "kg_shard_back_seed", "kg_shard_back_level", "kg_shard_refwd_seed",
                  "kg_shard_held_words", "kg_shard_held", "kg_batcher_create", "kg_batcher_check", "kg_batcher_stats",
                  "kg_shard_unique_id", "kg_shard_comm_init", "kg_shard_transport_attach", "kg_shard_comm_release",
-                 "kg_shard_comm_stats"):
+                 "kg_shard_comm_stats", "kg_check_tree"):
         getattr(L, name).restype = C.c_int
     _lib = L
     return L

@@ -10,7 +10,7 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB_DIR = os.path.join(HERE, "lib")
 LIB = os.path.join(LIB_DIR, "libketogpu.so")
-SOURCES = ["kg_abi.cpp", "kg_batcher.cpp", "kg_snapshot.hip", "kg_check.hip", "kg_grid.hip", "kg_msbfs.hip", "kg_interp.hip", "kg_expand.hip", "kg_shard.hip", "kg_shard_comm.hip", "kg_augment.hip", "kg_formula.hip", "kg_delta.hip", "kg_rows.hip"]
+SOURCES = ["kg_abi.cpp", "kg_batcher.cpp", "kg_snapshot.hip", "kg_check.hip", "kg_grid.hip", "kg_msbfs.hip", "kg_interp.hip", "kg_expand.hip", "kg_shard.hip", "kg_shard_comm.hip", "kg_augment.hip", "kg_formula.hip", "kg_delta.hip", "kg_rows.hip", "kg_tree.cpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("KG_OFFLOAD_ARCH", "gfx950")
 

@@ -290,11 +290,47 @@ class Engine:
             return Result(NOT_MEMBER)
         tree = None
         if with_tree:
-            from .explain import Explainer
-            g = self.config.max_read_depth
-            d = g if rest_depth <= 0 or g < rest_depth else rest_depth  # engine.go:68-70
-            tree = Explainer(self).tree(tuple(int(x) for x in self.snapshot.interner.tuple_ids(t)), d)
+            tree = self.check_tree(t, rest_depth)
         return Result(IS_MEMBER, None, tree)
+
+    def check_tree(self, t: RelationTuple, rest_depth: int):
+        """The tree of a member check, built inside the library (kg_check_tree: the walk over GPU
+        sub-check answers and row reads; keto_amd/explain.py is its CPU-tested restatement)."""
+        import ctypes as C
+        from .ketoapi import CheckTree, TREE_INTERSECTION
+        from .namespace import HIDDEN_TTU_PREFIX
+        it = self.snapshot.interner
+        L = _lib.load()
+        ids = [int(x) for x in it.tuple_ids(t)]
+        q = (C.c_uint32 * 7)(*ids, rest_depth & 0xFFFFFFFF)
+        hidden = [r for r in range(it.n_relations) if it.rel_name(r).startswith(HIDDEN_TTU_PREFIX)]
+        hid = (C.c_uint32 * max(1, len(hidden)))(*hidden)
+        n = C.c_size_t(0)
+        res, err = C.c_uint8(0), C.c_uint32(0)
+        cap = 64
+        while True:
+            buf = (_lib.kg_check_node * cap)()
+            rc = L.kg_check_tree(self.snapshot.handle, q, self.config.max_read_depth, hid, len(hidden), buf, cap,
+                                 C.byref(n), C.byref(res), C.byref(err))
+            if rc == -3 and n.value > cap:
+                cap = n.value
+                continue
+            _lib.check(rc, "kg_check_tree")
+            break
+        if res.value != _lib.KG_IS_MEMBER:
+            return None
+        pos = 0
+
+        def build():
+            nonlocal pos
+            r = buf[pos]
+            pos += 1
+            kids = [build() for _ in range(r.n_children)]
+            tup = it.relation_tuple((r.t.ns, r.t.obj, r.t.rel, r.t.sns, r.t.sobj, r.t.srel)) if r.has_tuple else None
+            typ = _lib.KG_CTREE[r.type]
+            return CheckTree(TREE_INTERSECTION if typ == "intersection" else typ, tup, kids)
+
+        return build()
 
     def check_is_member(self, t: RelationTuple, rest_depth: int) -> bool:
         """CheckIsMember (engine.go:54-60): membership only (no tree)."""

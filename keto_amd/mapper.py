@@ -106,6 +106,14 @@ class Interner:
         rows = [self.tuple_ids(t) for t in ts]
         return np.asarray(rows, dtype=np.uint32).reshape(-1, 6)
 
+    def relation_tuple(self, ids) -> RelationTuple:
+        """The RelationTuple of (ns, obj, rel, sns, sobj, srel) ids (sns == SUBJECT_ID: a subject id)."""
+        ns, obj, rel, sns, sobj, srel = (int(x) for x in ids)
+        if sns == SUBJECT_ID:
+            return RelationTuple(self.ns_name(ns), self.obj_name(obj), self.rel_name(rel), subject_id=self.obj_name(sobj))
+        return RelationTuple(self.ns_name(ns), self.obj_name(obj), self.rel_name(rel),
+                             subject_set=SubjectSet(self.ns_name(sns), self.obj_name(sobj), self.rel_name(srel)))
+
     def subject_set_ids(self, s: SubjectSet) -> Tuple[int, int, int]:
         return self.ns_id(s.namespace), self.obj_id(s.object), self.rel_id(s.relation)
 

@@ -1,4 +1,5 @@
-"""Check trees (CheckRelationTuple's Result.Tree, keto_amd/explain.py) on the GPU engine.
+"""Check trees (CheckRelationTuple's Result.Tree: kg_check_tree in the library, keto_amd/explain.py its
+restatement) on the GPU engine.
 
 * the reference's expected paths (rewrites_test.go:183-205, hasPath :263-288) on its fixture;
 * every member answer's tree is a proof: a test-side checker walks it against the tuples and the
@@ -15,6 +16,7 @@ import pytest
 
 from golden_cases import Case, all_cases
 from keto_amd.engine import IS_MEMBER, NOT_MEMBER, Config, Engine, Registry
+from keto_amd.explain import Explainer
 from keto_amd.ketoapi import (RelationTuple, SubjectSet, TREE_COMPUTED, TREE_INTERSECTION, TREE_LEAF, TREE_NOT,
                               TREE_TTU, TREE_UNION)
 from keto_amd.namespace import ComputedSubjectSet, InvertResult, SubjectSetRewrite, TupleToSubjectSet
@@ -157,6 +159,10 @@ def test_random_check_trees(seed, mat, monkeypatch):
         if r.membership == IS_MEMBER:
             n_member += 1
             assert proof.member(r.tree, q, _clamp(d, gmax)), (str(q), d, str(r.tree))
+            # the library's walk (kg_check_tree, C++) builds exactly the tree of keto_amd/explain.py's
+            # restatement over the same GPU answers
+            py = Explainer(e).tree(tuple(int(x) for x in it.tuple_ids(q)), _clamp(d, gmax))
+            assert r.tree.to_json() == py.to_json(), (str(q), d, str(r.tree), str(py))
         else:
             assert r.tree is None
     assert n_member >= 5, n_member
