@@ -506,7 +506,11 @@ int kg_check_tree(kg_snapshot* s, const kg_query* q, int32_t global_max_depth, c
                   uint32_t* err_code);
 
 /* ---- expand ----------------------------------------------------------------------------- */
-/* Roots are split over the replicas (chunks of >= 1024 roots, one host thread each). */
+/* Roots are split over the replicas (chunks of >= 1024 roots, one host thread each).  On a
+ * hash-sharded snapshot with a transport bound to its own stream (kg_shard_comm_init(.., NULL)) the
+ * call is collective like kg_check_batch: every rank passes its own roots (any count) and the rows
+ * those roots can reach are gathered to it first (the general phase's region gather), then expanded
+ * there -- the same trees as an unsharded snapshot. */
 int kg_expand_batch(kg_snapshot* s, const kg_set* roots, size_t n, int32_t global_max_depth, kg_tree_buf* out);
 void kg_tree_free(kg_tree_buf* t);
 

@@ -754,7 +754,8 @@ int kg_expand_batch(kg_snapshot* sp, const kg_set* roots, size_t n, int32_t glob
   if (!sp || !out) return set_error(-2, "NULL argument");
   if (n && !roots) return set_error(-2, "roots is NULL");
   Snapshot* s = reinterpret_cast<Snapshot*>(sp);
-  if (s->shard_n > 1) return set_error(-2, "sharded snapshot: expand needs every row on one device");
+  // hash-sharded: the rows the roots can reach are gathered to this rank first (collective)
+  if (s->shard_n > 1 || kg::shard_comm_of(s, nullptr)) return kg::shard_expand(s, roots, n, global_max_depth, out);
   // a lane set from the pool: one stream + cached buffers per replica, so concurrent callers overlap
   std::vector<kg::Lane*>* lanes = s->lanes_acquire();
   if (!lanes) return -1;

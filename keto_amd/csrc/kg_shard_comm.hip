@@ -402,11 +402,11 @@ static int a2a_rows(ShardComm* c, const std::vector<Row<W>>& rows, const std::ve
 // gathered at their home rank (keto_amd/sharded.py _gather_region: expand rows and tuple-to-subject-set
 // rows both lead through subject sets; computed subject sets stay on the object, all of whose
 // relations live on its owner).  Collective: every rank takes part, with or without open queries.
-static int gather_region(Snapshot* s, ShardComm* c, const std::vector<kg_query>& open_q, int32_t gdepth,
-                         std::vector<kg_tuple>* region) {
+static int gather_region(Snapshot* s, ShardComm* c, const std::vector<std::pair<uint32_t, uint32_t>>& starts,
+                         int32_t gdepth, std::vector<kg_tuple>* region) {
   const uint32_t N = (uint32_t)c->world;
   std::set<Row<3>> reqset;
-  for (const kg_query& q : open_q) reqset.insert(Row<3>{(uint64_t)c->rank, q.t.ns, q.t.obj});
+  for (const auto& o : starts) reqset.insert(Row<3>{(uint64_t)c->rank, o.first, o.second});
   std::vector<Row<3>> req(reqset.begin(), reqset.end());
   std::set<Row<3>> seen;  // (home, ns, obj) this owner has shipped
   const uint32_t nrel = std::max<uint32_t>(s->ds.n_rel, 1);
@@ -471,7 +471,9 @@ static int general_phase(Snapshot* s, ShardComm* c, const kg_query* d_q, size_t 
       oq.push_back(hq[i]);
     }
   std::vector<kg_tuple> region;
-  if (int rc = gather_region(s, c, oq, gdepth, &region)) return rc;
+  std::vector<std::pair<uint32_t, uint32_t>> starts;
+  for (const kg_query& q : oq) starts.emplace_back(q.t.ns, q.t.obj);
+  if (int rc = gather_region(s, c, starts, gdepth, &region)) return rc;
   c->st[5] = open.size();
   c->st[6] = region.size();
   if (open.empty()) return 0;
@@ -511,6 +513,36 @@ static int general_phase(Snapshot* s, ShardComm* c, const kg_query* d_q, size_t 
   HIPC(hipMemcpyAsync(c->err, herr.data(), n * 4, hipMemcpyHostToDevice, c->run));
   HIPC(hipStreamSynchronize(c->run));
   return 0;
+}
+
+// BuildTree on a hash-sharded snapshot (internal/expand/engine.go:35-104): the rows of every object
+// within gdepth + 1 subject-set hops of the roots are gathered to this rank (collective, as the general
+// phase) and the single-GPU expand runs on a snapshot of them -- the same rows in the same shard order
+// per (ns, obj, rel), so the same trees.
+int shard_expand(Snapshot* s, const kg_set* roots, size_t n, int32_t gdepth, kg_tree_buf* out) {
+  ShardComm* c = shard_comm_of(s, nullptr);
+  if (!c) return set_error(-2, "sharded snapshot: bind a transport to its own stream first (kg_shard_comm_init)");
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIPC(hipSetDevice(s->device));
+  if (gdepth < 1) gdepth = 5;  // config.schema.json:308-315 default
+  std::vector<std::pair<uint32_t, uint32_t>> starts;
+  for (size_t i = 0; i < n; i++)
+    if (roots[i].sns != KG_SUBJECT_ID) starts.emplace_back(roots[i].sns, roots[i].sobj);
+  std::vector<kg_tuple> region;
+  if (int rc = gather_region(s, c, starts, gdepth, &region)) return rc;
+  c->st[6] = region.size();
+  Snapshot* g = new (std::nothrow) Snapshot();
+  if (!g) return set_error(KG_ERR_RESOURCE_CODE, "expand region snapshot");
+  kg_rewrite_prog p = s->prog_copy.view();
+  const bool prog = s->prog_copy.have && !s->prog_copy.ns_has_rel.empty();
+  int rc = g->init_device(s->device);
+  if (!rc) rc = g->create_from_tuples(region.data(), region.size(), &s->prog_copy.dict, prog ? &p : nullptr);
+  void* bufs = nullptr;
+  if (!rc) rc = expand_batch(g, g->stream, &bufs, roots, n, gdepth, out);
+  if (bufs) expand_bufs_free(bufs);
+  delete g;
+  hipSetDevice(s->device);
+  return rc;
 }
 
 // ------------------------------------------------------------------ one batch

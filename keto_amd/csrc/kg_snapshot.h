@@ -362,6 +362,7 @@ void shard_comms_free(Snapshot* s);
 ShardComm* shard_comm_of(Snapshot* s, hipStream_t st);  // the transport bound to st, or null
 int shard_check(Snapshot* s, ShardComm* c, const kg_query* d_q, size_t n, int32_t gdepth, uint8_t* d_out,
                 uint32_t* d_err, kg_stats* stats);
+int shard_expand(Snapshot* s, const kg_set* roots, size_t n, int32_t gdepth, kg_tree_buf* out);  // collective
 int shard_check_host_entry(Snapshot* s, const kg_query* q, size_t n, int32_t gdepth, uint8_t* out, uint32_t* err,
                            kg_stats* stats);  // kg_check_batch on a sharded snapshot (its own stream's binding)
 // kg_grid.hip

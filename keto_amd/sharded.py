@@ -257,12 +257,15 @@ class LibShardedChecker:
     one GPU, which RCCL does not allow)."""
 
     def __init__(self, snapshot, rank: int = 0, world: int = 1, dist=None, group=None, transport: str = "rccl",
-                 stream=None):
+                 stream=None, snapshot_stream: bool = False):
+        """snapshot_stream: bind the snapshot's own stream (what kg_check_batch with host buffers and
+        kg_expand_batch use -- sharded expand goes through it) instead of a torch stream of this checker."""
         import torch
         self.snapshot, self.rank, self.world = snapshot, rank, world
         self.L = _lib.load()
-        self.stream = stream if stream is not None else torch.cuda.Stream()
-        self._sp = C.c_void_p(self.stream.cuda_stream)
+        self.snapshot_stream = snapshot_stream
+        self.stream = None if snapshot_stream else (stream if stream is not None else torch.cuda.Stream())
+        self._sp = C.c_void_p(None if snapshot_stream else self.stream.cuda_stream)
         self.transport = transport
         if transport == "rccl":
             uid = (C.c_uint8 * _lib.KG_SHARD_UNIQUE_ID_BYTES)()
@@ -295,12 +298,27 @@ class LibShardedChecker:
         n = int(dq.shape[0])
         res = torch.empty(max(n, 1), dtype=torch.uint8, device=dq.device)
         err = torch.empty(max(n, 1), dtype=torch.int32, device=dq.device)
-        self.stream.wait_stream(torch.cuda.current_stream())
+        if self.snapshot_stream:  # the library's own stream: order through the device
+            torch.cuda.synchronize()
+        else:
+            self.stream.wait_stream(torch.cuda.current_stream())
         self._check_t(self.L.kg_check_batch_device(self.snapshot.handle, dq.data_ptr() if n else None, n, gdepth,
                                                    res.data_ptr(), err.data_ptr(), None, self._sp),
                       "kg_check_batch_device (sharded)")
-        torch.cuda.current_stream().wait_stream(self.stream)
+        if self.snapshot_stream:
+            torch.cuda.synchronize()
+        else:
+            torch.cuda.current_stream().wait_stream(self.stream)
         return res[:n], err[:n]
+
+    def expand(self, roots: np.ndarray, gdepth: int):
+        """BuildTree for this rank's roots ((n, 4) uint32 kg_set rows) on the sharded snapshot
+        (collective: every rank calls it; needs snapshot_stream=True).  Per root the pre-order records or
+        None, as ExpandEngine.build_trees_ids."""
+        from .engine import Config, ExpandEngine
+        if not self.snapshot_stream:
+            raise ValueError("sharded expand runs on the snapshot's own stream (snapshot_stream=True)")
+        return ExpandEngine(self.snapshot, Config(gdepth)).build_trees_ids(roots)
 
     def stats(self) -> dict:
         out = (C.c_uint64 * 8)()

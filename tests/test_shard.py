@@ -815,3 +815,89 @@ def test_sharded_member_does_not_hide_an_earlier_error(general):
         else:  # every query the oracle answers with an error is an error here too (never a member)
             assert (res[oerr != 0] == 2).all(), (gmax, res, exp, err, oerr)
     assert (oerr != 0).any() and (exp == 1).any()
+
+
+# ------------------------------------------------------------------ expand on a hash-sharded snapshot
+def _expand_graph(seed):
+    sys.path.insert(0, ROOT)
+    from keto_amd.ketoapi import RelationTuple
+    from keto_amd.mapper import SUBJECT_ID, Interner
+    rng = np.random.default_rng(seed)
+    n_obj = 70
+    tuples = []
+    for _ in range(900):
+        ns, obj, rel = rng.choice(["a", "b"]), f"o{rng.integers(n_obj)}", rng.choice(["r0", "r1", "r2"])
+        if rng.random() < 0.55:
+            s = f"({rng.choice(['a', 'b'])}:o{rng.integers(n_obj)}#{rng.choice(['r0', 'r1', 'r2', '...'])})"
+        else:
+            s = f"u{rng.integers(30)}"
+        tuples.append(RelationTuple.from_string(f"{ns}:{obj}#{rel}@{s}"))
+    it = Interner()
+    t6 = it.tuples_array(tuples)
+    roots = []
+    for _ in range(300):
+        if rng.random() < 0.05:
+            roots.append([SUBJECT_ID, it.obj_id(f"u{rng.integers(30)}"), 0, 0])
+        else:
+            roots.append([it.ns_id(rng.choice(["a", "b"])), it.obj_id(f"o{rng.integers(n_obj + 2)}"),
+                          it.rel_id(rng.choice(["r0", "r1", "r2"])), int(rng.integers(-1, 7)) & 0xFFFFFFFF])
+    return it, t6, np.asarray(roots, np.uint32)
+
+
+def _expand_worker(rank, world, port, transport, outq):
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+    from keto_amd.engine import Snapshot
+    from keto_amd.sharded import LibShardedChecker
+    dist_ = None
+    if transport == "host":
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dist_ = dist
+    torch.cuda.set_device(0)
+    it, t6, roots = _expand_graph(5)
+    snap = Snapshot(t6, it, None, 0, shard=(rank, world))
+    chk = LibShardedChecker(snap, rank, world, dist_, transport=transport, snapshot_stream=True)
+    mine = np.array_split(np.arange(len(roots)), world)[rank]
+    out = {}
+    for gmax in (1, 3, 6):
+        out[gmax] = (mine, chk.expand(roots[mine], gmax))
+    outq.put((rank, out))
+    if dist_:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,transport", [(1, "rccl"), (2, "host"), (3, "host")])
+def test_sharded_expand_vs_oracle(world, transport):
+    """kg_expand_batch on a hash-sharded snapshot (collective; the rows the roots can reach gathered to
+    their rank, then the single-GPU BuildTree, internal/expand/engine.go:35-104): every tree equals the
+    oracle's on the whole graph record for record (same pre-order, same child order) -- world 1 over RCCL,
+    worlds 2 and 3 over the gloo host transport."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from oracle.oracle import Oracle
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from test_gpu_expand import _cmp_records
+    ctx = mp.get_context("spawn")
+    outq = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_expand_worker, args=(r, world, port, transport, outq)) for r in range(world)]
+    for p in ps:
+        p.start()
+    got = [outq.get(timeout=150) for _ in range(world)]
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    it, t6, roots = _expand_graph(5)
+    oracle = Oracle(t6, it.wildcard_rel)
+    n_trees = 0
+    for _, out in got:
+        for gmax, (mine, trees) in out.items():
+            for i, g in zip(mine, trees):
+                r = roots[i]
+                exp = oracle.expand(int(r[0]), int(r[1]), int(r[2]), int(np.uint32(r[3]).view(np.int32)), gmax)
+                _cmp_records(exp, g, (r.tolist(), gmax))
+                n_trees += g is not None
+    assert n_trees > 100
