@@ -176,8 +176,16 @@ __global__ __launch_bounds__(256) void k_resolve(DevSnap s, const kg_query* __re
     // never touches the node map (~13 % of the C2 batch; one random HBM line each)
     const bool unheld = no_holder_filter == 2 && use_bits && !s.relflags && !((hw >> (subj & 31)) & 1u);
     NSlot n0{};
-    if (key_ok && !unheld) n0 = s.nmap[ni];
+    uint4 dlo = make_uint4(0, 0, 0, 0), dhi = dlo;  // the slot's inline direct subjects (64-B slots)
+    if (key_ok && !unheld) {
+      const NSlot* sl0 = nmap_at(s, ni);
+      n0 = *sl0;
+      const uint4* dp = reinterpret_cast<const uint4*>(sl0 + s.nmap_x2);  // (32-B slots: the slot again)
+      dlo = dp[0];
+      dhi = dp[1];
+    }
     uint32_t node = NONE, rb = 0, rl = 0, rsig = 0xFFFFFFFFu, nfl = 0;
+    bool inl = false;  // the root's direct subjects are inline in its (home) slot
     if (unheld) {
       no_holder = true;
     } else if (key_ok) {
@@ -185,6 +193,7 @@ __global__ __launch_bounds__(256) void k_resolve(DevSnap s, const kg_query* __re
       // scratch -- 40 B stored and reloaded per query, ~40 % of this kernel's HBM writes)
       NSlot v = n0;
       bool found = n0.key == key;
+      inl = found && s.nmap_x2 && dlo.x != NONE;
       if (!found && n0.key != EMPTY64) {
         const NSlot* sl = nmap_slot(s, key, hash_next(ni, s.nmap_n));
         if (sl) {
@@ -225,7 +234,15 @@ __global__ __launch_bounds__(256) void k_resolve(DevSnap s, const kg_query* __re
       // an unset holder bit rules the probe out as well (the exact tuple would make subj a holder)
       const bool nobit = use_bits && !((hw >> (subj & 31)) & 1u);
       did_probe = subj != NONE && !nobit && sig_maybe(rsig, subj_sig(subj));
-      member = did_probe && dset_probe(s, node, subj);
+      if (inl) {  // checkDirect from the slot: dlo.x subjects in dlo.y .. dhi.w
+        const uint32_t dn = dlo.x;
+        member = did_probe && ((dn > 0 && dlo.y == subj) || (dn > 1 && dlo.z == subj) || (dn > 2 && dlo.w == subj) ||
+                               (dn > 3 && dhi.x == subj) || (dn > 4 && dhi.y == subj) || (dn > 5 && dhi.z == subj) ||
+                               (dn > 6 && dhi.w == subj));
+        did_probe = false;  // no dset request
+      } else {
+        member = did_probe && dset_probe(s, node, subj);
+      }
       if (member || d < 2 || rl == 0) route = ROUTE_DONE;
       // a subject that no row holds cannot be reached from any root (checkDirect never hits)
       if (route == ROUTE_LIGHT && no_holder_filter) {

@@ -136,6 +136,15 @@ struct NSlot {
   uint32_t sig;  // Bloom signature of the node's row subjects (as AdjX.sig): k_resolve's root probe filter
   uint64_t pad1;  // low byte: the node's flags (nflags; 0 without a namespace program)
 };
+// Second half of a 64-B node-map slot (DevSnap::nmap_x2): the node's direct subjects (its check
+// row) when it has at most NSLOT_DIR of them (dn = count; NONE: more), so k_resolve answers the
+// root's checkDirect from the slot it already read -- one line per query instead of two (the
+// slot, then a dset bucket keyed by (node, subject)).
+constexpr uint32_t NSLOT_DIR = 7;
+struct NSlotDir {
+  uint32_t dn;
+  uint32_t d[NSLOT_DIR];
+};
 // Holder-hash slot: tagged subject -> hold[first, first + count).  key == NONE: free.
 struct HSlot {
   uint32_t key, first, count, pad;
@@ -157,6 +166,7 @@ struct DevSnap {
   uint64_t dset_nb;  // buckets (DSET_BUCKET keys each); probes wrap at dset_nb
   const NSlot* nmap;
   uint64_t nmap_n;  // slots
+  uint32_t nmap_x2;  // 1: 64-B slots (NSlot, then its NSlotDir), slot i at nmap + 2 i; 0: 32-B slots
   const uint8_t* nflags;  // nullptr: every node pure
   const uint32_t* nd_ns;
   const uint32_t* nd_obj;

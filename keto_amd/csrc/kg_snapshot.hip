@@ -54,22 +54,32 @@ __global__ void k_dset_insert_rows(uint64_t* dset, uint64_t nb, const uint64_t* 
   }
 }
 
+// x2: 64-B slots -- the second half holds the node's direct subjects (coff / csub: its check row)
+// when it has at most NSLOT_DIR of them.
 __global__ void k_nmap_insert(NSlot* nm, uint64_t slots, const uint32_t* nd_ns, const uint32_t* nd_obj,
                               const uint32_t* nd_rel, const uint64_t* adj_off, const uint32_t* sig,
-                              const uint8_t* flags, uint32_t n_nodes) {
+                              const uint8_t* flags, uint32_t n_nodes, uint32_t x2, const uint64_t* coff,
+                              const uint32_t* csub) {
   uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
   if (v >= n_nodes) return;
   uint64_t key = nmap_key(nd_ns[v], nd_rel[v], nd_obj[v]);
   uint64_t i = hash_home(key, slots);
   for (uint64_t n = 0; n < slots; n++) {  // sized for load <= 0.625: always finds room
+    NSlot* sl = nm + (i << x2);
     unsigned long long old =
-        atomicCAS((unsigned long long*)&nm[i].key, (unsigned long long)EMPTY64, (unsigned long long)key);
+        atomicCAS((unsigned long long*)&sl->key, (unsigned long long)EMPTY64, (unsigned long long)key);
     if (old == EMPTY64 || old == key) {
-      nm[i].node = v;
-      nm[i].beg = (uint32_t)adj_off[v];
-      nm[i].len = (uint32_t)(adj_off[v + 1] - adj_off[v]);
-      nm[i].sig = sig[v];
-      nm[i].pad1 = flags ? flags[v] : 0u;  // node flags: k_resolve's impurity test without a random nflags read
+      sl->node = v;
+      sl->beg = (uint32_t)adj_off[v];
+      sl->len = (uint32_t)(adj_off[v + 1] - adj_off[v]);
+      sl->sig = sig[v];
+      sl->pad1 = flags ? flags[v] : 0u;  // node flags: k_resolve's impurity test without a random nflags read
+      if (x2) {
+        NSlotDir* d = reinterpret_cast<NSlotDir*>(sl + 1);
+        const uint64_t b = coff[v], e = coff[v + 1];
+        d->dn = e - b <= NSLOT_DIR ? (uint32_t)(e - b) : NONE;
+        for (uint32_t k = 0; k < NSLOT_DIR; k++) d->d[k] = b + k < e ? csub[b + k] : NONE;
+      }
       return;
     }
     i = hash_next(i, slots);
@@ -485,9 +495,13 @@ int Snapshot::build_hash_tables() {
   HIPC(hipMemsetAsync(dset, 0xFF, buckets * DSET_BUCKET * 8, stream));
   uint64_t slots = std::max<uint64_t>(16, (uint64_t)ds.n_nodes * 2);
   if (slots * sizeof(NSlot) > hbm_total / 8) slots = std::max<uint64_t>(16, (uint64_t)ds.n_nodes * 8 / 5);
+  // 64-B slots with the node's direct subjects inline (k_resolve's root checkDirect from the slot)
+  // when they take at most 1/8 of HBM (C2: 25 GB; not C3's ~10^9 nodes) -- KG_NMAP64=0 at build: off
+  const char* nm_env = getenv("KG_NMAP64");
+  const uint32_t x2 = (!(nm_env && nm_env[0] == '0') && slots * 2 * sizeof(NSlot) <= hbm_total / 8) ? 1u : 0u;
   NSlot* nm = nullptr;
-  if (alloc((void**)&nm, slots * sizeof(NSlot))) return -1;
-  HIPC(hipMemsetAsync(nm, 0xFF, slots * sizeof(NSlot), stream));
+  if (alloc((void**)&nm, (slots << x2) * sizeof(NSlot))) return -1;
+  HIPC(hipMemsetAsync(nm, 0xFF, (slots << x2) * sizeof(NSlot), stream));
   uint32_t grid = (ds.n_nodes + 255) / 256;
   if (ds.n_nodes) {
     if (n_rows)
@@ -495,7 +509,7 @@ int Snapshot::build_hash_tables() {
                          stream, dset, buckets, coff, csub, ds.n_nodes, n_rows);
     HIPC(hipGetLastError());
     hipLaunchKernelGGL(k_nmap_insert, dim3(grid), dim3(256), 0, stream, nm, slots, ds.nd_ns, ds.nd_obj,
-                       ds.nd_rel, ds.adj_off, sig, ds.nflags, ds.n_nodes);
+                       ds.nd_rel, ds.adj_off, sig, ds.nflags, ds.n_nodes, x2, coff, csub);
     HIPC(hipGetLastError());
   }
   HIPC(hipStreamSynchronize(stream));
@@ -504,6 +518,7 @@ int Snapshot::build_hash_tables() {
   ds.dset_nb = buckets;
   ds.nmap = nm;
   ds.nmap_n = slots;
+  ds.nmap_x2 = x2;
   ds.shard_rank = shard_rank;
   ds.shard_n = shard_n;
   ds.nowner = nullptr;
