@@ -418,7 +418,6 @@ int Snapshot::augment_rewrites() {
   hipLaunchKernelGGL(k_aug_nmap, dim3((n0 + 255) / 256), dim3(256), 0, stream, nm0, slots0, ds.nd_ns, ds.nd_obj,
                      ds.nd_rel, n0);
   DevSnap b = ds;  // the base graph (its node map: nm0)
-  b.nmap_x2 = 0;
   b.nmap = nm0;
   b.nmap_n = slots0;
   // 1. candidates: count per anchor node, scan, place
@@ -486,7 +485,6 @@ int Snapshot::augment_rewrites() {
   hipLaunchKernelGGL(k_aug_nmap, dim3((n1 + 255) / 256), dim3(256), 0, stream, nm1, slots1, nd_ns, nd_obj, nd_rel,
                      n1);
   DevSnap x = ds;  // the extended graph's ids and node map
-  x.nmap_x2 = 0;
   x.n_nodes = n1;
   x.nmap = nm1;
   x.nmap_n = slots1;

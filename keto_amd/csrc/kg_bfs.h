@@ -18,16 +18,12 @@ namespace kg {
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
-// Slot i of the node map (32- or 64-B slots, DevSnap::nmap_x2).
-__device__ __forceinline__ const NSlot* nmap_at(const DevSnap& s, uint64_t i) { return s.nmap + (i << s.nmap_x2); }
-
 // Node-map lookup: the slot of (ns, rel, obj), or nullptr.  The first slot is passed in when the
 // caller already issued its load (k_resolve overlaps it with other lookups).
 __device__ __forceinline__ const NSlot* nmap_slot(const DevSnap& s, uint64_t key, uint64_t i) {
   for (uint64_t p = 0; p < s.nmap_n; p++) {  // load <= 0.625: ends at an empty slot long before
-    const NSlot* sl = nmap_at(s, i);
-    const uint64_t k = sl->key;
-    if (k == key) return sl;
+    const uint64_t k = s.nmap[i].key;
+    if (k == key) return &s.nmap[i];
     if (k == EMPTY64) return nullptr;
     i = hash_next(i, s.nmap_n);
   }

@@ -176,16 +176,8 @@ __global__ __launch_bounds__(256) void k_resolve(DevSnap s, const kg_query* __re
     // never touches the node map (~13 % of the C2 batch; one random HBM line each)
     const bool unheld = no_holder_filter == 2 && use_bits && !s.relflags && !((hw >> (subj & 31)) & 1u);
     NSlot n0{};
-    uint4 dlo = make_uint4(0, 0, 0, 0), dhi = dlo;  // the slot's inline direct subjects (64-B slots)
-    if (key_ok && !unheld) {
-      const NSlot* sl0 = nmap_at(s, ni);
-      n0 = *sl0;
-      const uint4* dp = reinterpret_cast<const uint4*>(sl0 + s.nmap_x2);  // (32-B slots: the slot again)
-      dlo = dp[0];
-      dhi = dp[1];
-    }
+    if (key_ok && !unheld) n0 = s.nmap[ni];
     uint32_t node = NONE, rb = 0, rl = 0, rsig = 0xFFFFFFFFu, nfl = 0;
-    bool inl = false;  // the root's direct subjects are inline in its (home) slot
     if (unheld) {
       no_holder = true;
     } else if (key_ok) {
@@ -193,7 +185,6 @@ __global__ __launch_bounds__(256) void k_resolve(DevSnap s, const kg_query* __re
       // scratch -- 40 B stored and reloaded per query, ~40 % of this kernel's HBM writes)
       NSlot v = n0;
       bool found = n0.key == key;
-      inl = found && s.nmap_x2 && dlo.x != NONE;
       if (!found && n0.key != EMPTY64) {
         const NSlot* sl = nmap_slot(s, key, hash_next(ni, s.nmap_n));
         if (sl) {
@@ -234,15 +225,7 @@ __global__ __launch_bounds__(256) void k_resolve(DevSnap s, const kg_query* __re
       // an unset holder bit rules the probe out as well (the exact tuple would make subj a holder)
       const bool nobit = use_bits && !((hw >> (subj & 31)) & 1u);
       did_probe = subj != NONE && !nobit && sig_maybe(rsig, subj_sig(subj));
-      if (inl) {  // checkDirect from the slot: dlo.x subjects in dlo.y .. dhi.w
-        const uint32_t dn = dlo.x;
-        member = did_probe && ((dn > 0 && dlo.y == subj) || (dn > 1 && dlo.z == subj) || (dn > 2 && dlo.w == subj) ||
-                               (dn > 3 && dhi.x == subj) || (dn > 4 && dhi.y == subj) || (dn > 5 && dhi.z == subj) ||
-                               (dn > 6 && dhi.w == subj));
-        did_probe = false;  // no dset request
-      } else {
-        member = did_probe && dset_probe(s, node, subj);
-      }
+      member = did_probe && dset_probe(s, node, subj);
       if (member || d < 2 || rl == 0) route = ROUTE_DONE;
       // a subject that no row holds cannot be reached from any root (checkDirect never hits)
       if (route == ROUTE_LIGHT && no_holder_filter) {
@@ -367,7 +350,7 @@ __global__ __launch_bounds__(256) void k_stream4(DevSnap s, LqList wl, uint32_t*
   uint32_t c_left = 0, c_pos = 0;
   LQuery cq{};             // current chunk
   uint32_t head = 0, tail = 0, head_off = 0;
-  bool pend = false, pend_dr = false;
+  bool pend = false;
   uint32_t pend_node = 0, pend_slot = 0, pend_gen = 0;
   unsigned long long st_rows = 0, st_edges = 0, st_probes = 0, st_done = 0, st_steps = 0;
   for (;;) {
@@ -485,13 +468,8 @@ __global__ __launch_bounds__(256) void k_stream4(DevSnap s, LqList wl, uint32_t*
     const uint32_t ox = __shfl(excl, own, 64);
     const bool act = (uint32_t)lane < taken;
     const AdjX x = s.adjx[act ? ob + ((uint32_t)lane - ox) : 0u];  // adjx[0] exists (n_set_edges + 1)
-    // checkDirect: a node with its direct subjects inline reads its 64-B direct record (one line per
-    // node, hot for popular groups), any other node a dset bucket keyed by (node, subject)
-    const bool pdr = pvalid && pend_dr, pds = pvalid && !pend_dr;
     const ulonglong2 pb =
-        *reinterpret_cast<const ulonglong2*>(s.dset + (pds ? hash_home(pkey, s.dset_nb) : 0ull) * DSET_BUCKET);
-    const uint4* drp = reinterpret_cast<const uint4*>(s.drec + (pdr ? (uint64_t)pend_node * DREC_WORDS : 0ull));
-    const uint4 d0 = drp[0], d1 = drp[1], d2 = drp[2], d3 = drp[3];  // record 0 always exists
+        *reinterpret_cast<const ulonglong2*>(s.dset + (pvalid ? hash_home(pkey, s.dset_nb) : 0ull) * DSET_BUCKET);
     const uint32_t slot = (om >> 11) & 31u, d = om >> 25, g = (om >> 16) & S2_GEN;
     const uint32_t ssig = L.s_sig[slot];  // LDS, under the gathers' latency
     head += ncons;
@@ -499,17 +477,9 @@ __global__ __launch_bounds__(256) void k_stream4(DevSnap s, LqList wl, uint32_t*
     st_steps += (lane == 0) ? 1u : 0u;
     // checkDirect probe, first bucket; a chain past a full first bucket (rare at load <= 0.25) is
     // walked by the lanes that need it under a wave-uniform branch
-    bool hit = pds && (pb.x == pkey || pb.y == pkey);
-    if (pdr) {
-      const uint32_t dn = d0.x;  // subjects in words 1 .. dn
-      hit = (dn > 0 && d0.y == psubj) || (dn > 1 && d0.z == psubj) || (dn > 2 && d0.w == psubj) ||
-            (dn > 3 && d1.x == psubj) || (dn > 4 && d1.y == psubj) || (dn > 5 && d1.z == psubj) ||
-            (dn > 6 && d1.w == psubj) || (dn > 7 && d2.x == psubj) || (dn > 8 && d2.y == psubj) ||
-            (dn > 9 && d2.z == psubj) || (dn > 10 && d2.w == psubj) || (dn > 11 && d3.x == psubj) ||
-            (dn > 12 && d3.y == psubj) || (dn > 13 && d3.z == psubj) || (dn > 14 && d3.w == psubj);
-    }
+    bool hit = pvalid && (pb.x == pkey || pb.y == pkey);
     {
-      const bool more = pds && !hit && pb.y != EMPTY64;
+      const bool more = pvalid && !hit && pb.y != EMPTY64;
       if (__ballot(more)) {
         if (more) hit = dset_probe(s, pend_node, (uint32_t)pkey);
       }
@@ -540,7 +510,6 @@ __global__ __launch_bounds__(256) void k_stream4(DevSnap s, LqList wl, uint32_t*
     tail += min((uint32_t)__popcll(am), room);
     if (hit) atomicOr(&L.s_state[pend_slot], S2_HIT);
     pend = act && (keepc ? appended : true) && sig_maybe(x.sig, ssig);
-    pend_dr = (x.sig & SIG_DREC) != 0;
     pend_node = x.node;
     pend_slot = slot;
     pend_gen = g;

@@ -109,21 +109,13 @@ struct AdjX {
   uint32_t node, begin, len, sig;
 };
 
-// 31-bit Bloom (bit 31 of a node's signature is SIG_DREC, never set by a subject's mask).
 __host__ __device__ __forceinline__ uint32_t subj_sig(uint32_t subj) {
   uint32_t h = subj * 0x9E3779B1u;
   h ^= h >> 15;
   h *= 0x85EBCA77u;
   h ^= h >> 13;
-  return (1u << (h % 31u)) | (1u << ((h >> 5) % 31u));
+  return (1u << (h & 31)) | (1u << ((h >> 5) & 31));
 }
-// A node's direct subjects (its check row) inline in its 64-B direct record drec[node]: word 0 the
-// count (<= DREC_CAP), words 1.. the tagged subjects.  checkDirect for such a node reads that record
-// -- one line per NODE, shared by every query that probes it (a hot group's record stays in L2 / the
-// Infinity Cache) -- instead of a dset bucket keyed by (node, subject), which is a cold line per query.
-constexpr uint32_t SIG_DREC = 1u << 31;
-constexpr uint32_t DREC_CAP = 15, DREC_WORDS = 16;
-constexpr uint32_t SIG_FULL = 0x7FFFFFFFu;  // every Bloom bit set
 __host__ __device__ __forceinline__ bool sig_maybe(uint32_t sig, uint32_t subj_mask) {
   return (sig & subj_mask) == subj_mask;
 }
@@ -135,15 +127,6 @@ struct NSlot {
   uint32_t node, beg, len;
   uint32_t sig;  // Bloom signature of the node's row subjects (as AdjX.sig): k_resolve's root probe filter
   uint64_t pad1;  // low byte: the node's flags (nflags; 0 without a namespace program)
-};
-// Second half of a 64-B node-map slot (DevSnap::nmap_x2): the node's direct subjects (its check
-// row) when it has at most NSLOT_DIR of them (dn = count; NONE: more), so k_resolve answers the
-// root's checkDirect from the slot it already read -- one line per query instead of two (the
-// slot, then a dset bucket keyed by (node, subject)).
-constexpr uint32_t NSLOT_DIR = 7;
-struct NSlotDir {
-  uint32_t dn;
-  uint32_t d[NSLOT_DIR];
 };
 // Holder-hash slot: tagged subject -> hold[first, first + count).  key == NONE: free.
 struct HSlot {
@@ -157,7 +140,6 @@ struct DevSnap {
   const uint64_t* adj_off;
   const uint32_t* adj;
   const AdjX* adjx;  // parallel to adj
-  const uint32_t* drec;  // [n_nodes * DREC_WORDS] direct records (nodes whose sig has SIG_DREC), or null
   const uint64_t* row_off;
   const uint32_t* row_subj;
   const uint64_t* crow_off;  // check rows (nullptr: row_off / row_subj)
@@ -166,7 +148,6 @@ struct DevSnap {
   uint64_t dset_nb;  // buckets (DSET_BUCKET keys each); probes wrap at dset_nb
   const NSlot* nmap;
   uint64_t nmap_n;  // slots
-  uint32_t nmap_x2;  // 1: 64-B slots (NSlot, then its NSlotDir), slot i at nmap + 2 i; 0: 32-B slots
   const uint8_t* nflags;  // nullptr: every node pure
   const uint32_t* nd_ns;
   const uint32_t* nd_obj;

@@ -10,7 +10,6 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
-#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <new>
@@ -54,32 +53,22 @@ __global__ void k_dset_insert_rows(uint64_t* dset, uint64_t nb, const uint64_t* 
   }
 }
 
-// x2: 64-B slots -- the second half holds the node's direct subjects (coff / csub: its check row)
-// when it has at most NSLOT_DIR of them.
 __global__ void k_nmap_insert(NSlot* nm, uint64_t slots, const uint32_t* nd_ns, const uint32_t* nd_obj,
                               const uint32_t* nd_rel, const uint64_t* adj_off, const uint32_t* sig,
-                              const uint8_t* flags, uint32_t n_nodes, uint32_t x2, const uint64_t* coff,
-                              const uint32_t* csub) {
+                              const uint8_t* flags, uint32_t n_nodes) {
   uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
   if (v >= n_nodes) return;
   uint64_t key = nmap_key(nd_ns[v], nd_rel[v], nd_obj[v]);
   uint64_t i = hash_home(key, slots);
   for (uint64_t n = 0; n < slots; n++) {  // sized for load <= 0.625: always finds room
-    NSlot* sl = nm + (i << x2);
     unsigned long long old =
-        atomicCAS((unsigned long long*)&sl->key, (unsigned long long)EMPTY64, (unsigned long long)key);
+        atomicCAS((unsigned long long*)&nm[i].key, (unsigned long long)EMPTY64, (unsigned long long)key);
     if (old == EMPTY64 || old == key) {
-      sl->node = v;
-      sl->beg = (uint32_t)adj_off[v];
-      sl->len = (uint32_t)(adj_off[v + 1] - adj_off[v]);
-      sl->sig = sig[v];
-      sl->pad1 = flags ? flags[v] : 0u;  // node flags: k_resolve's impurity test without a random nflags read
-      if (x2) {
-        NSlotDir* d = reinterpret_cast<NSlotDir*>(sl + 1);
-        const uint64_t b = coff[v], e = coff[v + 1];
-        d->dn = e - b <= NSLOT_DIR ? (uint32_t)(e - b) : NONE;
-        for (uint32_t k = 0; k < NSLOT_DIR; k++) d->d[k] = b + k < e ? csub[b + k] : NONE;
-      }
+      nm[i].node = v;
+      nm[i].beg = (uint32_t)adj_off[v];
+      nm[i].len = (uint32_t)(adj_off[v + 1] - adj_off[v]);
+      nm[i].sig = sig[v];
+      nm[i].pad1 = flags ? flags[v] : 0u;  // node flags: k_resolve's impurity test without a random nflags read
       return;
     }
     i = hash_next(i, slots);
@@ -93,21 +82,11 @@ __global__ void k_node_owner(const uint32_t* nd_ns, const uint32_t* nd_obj, uint
 }
 
 // Bloom signature of every node's full row (direct subjects, tagged like dset keys).
-// Bloom signature of every node's direct subjects; with drec, a node of <= DREC_CAP direct subjects also
-// gets its direct record (count + subjects) and SIG_DREC in its signature.
-__global__ void k_node_sig(const uint64_t* row_off, const uint32_t* row_subj, uint32_t n_nodes, uint32_t* sig,
-                           uint32_t* drec) {
+__global__ void k_node_sig(const uint64_t* row_off, const uint32_t* row_subj, uint32_t n_nodes, uint32_t* sig) {
   const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
   if (v >= n_nodes) return;
-  const uint64_t b = row_off[v], e = row_off[v + 1];
   uint32_t m = 0;
-  for (uint64_t i = b; i < e && m != SIG_FULL; i++) m |= subj_sig(row_subj[i]);
-  if (drec && e - b <= DREC_CAP) {
-    uint32_t* r = drec + (uint64_t)v * DREC_WORDS;
-    r[0] = (uint32_t)(e - b);
-    for (uint32_t k = 0; k < DREC_CAP; k++) r[1 + k] = k < e - b ? row_subj[b + k] : NONE;
-    m |= SIG_DREC;
-  }
+  for (uint64_t i = row_off[v], e = row_off[v + 1]; i < e && m != 0xFFFFFFFFu; i++) m |= subj_sig(row_subj[i]);
   sig[v] = m;
 }
 
@@ -459,21 +438,8 @@ int Snapshot::build_hash_tables() {
   // direct tuples as checkDirect sees them: the check rows of a materialised snapshot, else the rows
   const uint64_t* coff = ds.crow_off ? ds.crow_off : ds.row_off;
   const uint32_t* csub = ds.crow_off ? ds.crow_subj : ds.row_subj;
-  // direct records (64 B per node) when they take at most 1/16 of HBM (KG_DREC=0 at build: off)
-  size_t hbm_free0 = 0, hbm_total0 = 0;
-  if (hipMemGetInfo(&hbm_free0, &hbm_total0) != hipSuccess) hbm_total0 = 288ull << 30;
-  (void)hipGetLastError();
-  const char* dr_env = getenv("KG_DREC");
-  uint32_t* drec = nullptr;
-  const uint64_t drec_bytes = (uint64_t)ds.n_nodes * DREC_WORDS * 4;
-  const bool use_drec = ds.n_nodes && !(dr_env && dr_env[0] == '0') && drec_bytes <= hbm_total0 / 16;
-  // (always at least one zeroed record: kernels load record 0 for lanes without a probe)
-  if (alloc((void**)&drec, use_drec ? drec_bytes : DREC_WORDS * 4)) return -1;
-  if (!use_drec) HIPC(hipMemsetAsync(drec, 0, DREC_WORDS * 4, stream));
-  ds.drec = drec;
   if (ds.n_nodes) {
-    hipLaunchKernelGGL(k_node_sig, dim3((ds.n_nodes + 255) / 256), dim3(256), 0, stream, coff, csub, ds.n_nodes, sig,
-                       use_drec ? drec : nullptr);
+    hipLaunchKernelGGL(k_node_sig, dim3((ds.n_nodes + 255) / 256), dim3(256), 0, stream, coff, csub, ds.n_nodes, sig);
     HIPC(hipGetLastError());
   }
   if (n_set_edges) {
@@ -495,13 +461,9 @@ int Snapshot::build_hash_tables() {
   HIPC(hipMemsetAsync(dset, 0xFF, buckets * DSET_BUCKET * 8, stream));
   uint64_t slots = std::max<uint64_t>(16, (uint64_t)ds.n_nodes * 2);
   if (slots * sizeof(NSlot) > hbm_total / 8) slots = std::max<uint64_t>(16, (uint64_t)ds.n_nodes * 8 / 5);
-  // 64-B slots with the node's direct subjects inline (k_resolve's root checkDirect from the slot)
-  // when they take at most 1/8 of HBM (C2: 25 GB; not C3's ~10^9 nodes) -- KG_NMAP64=0 at build: off
-  const char* nm_env = getenv("KG_NMAP64");
-  const uint32_t x2 = (!(nm_env && nm_env[0] == '0') && slots * 2 * sizeof(NSlot) <= hbm_total / 8) ? 1u : 0u;
   NSlot* nm = nullptr;
-  if (alloc((void**)&nm, (slots << x2) * sizeof(NSlot))) return -1;
-  HIPC(hipMemsetAsync(nm, 0xFF, (slots << x2) * sizeof(NSlot), stream));
+  if (alloc((void**)&nm, slots * sizeof(NSlot))) return -1;
+  HIPC(hipMemsetAsync(nm, 0xFF, slots * sizeof(NSlot), stream));
   uint32_t grid = (ds.n_nodes + 255) / 256;
   if (ds.n_nodes) {
     if (n_rows)
@@ -509,7 +471,7 @@ int Snapshot::build_hash_tables() {
                          stream, dset, buckets, coff, csub, ds.n_nodes, n_rows);
     HIPC(hipGetLastError());
     hipLaunchKernelGGL(k_nmap_insert, dim3(grid), dim3(256), 0, stream, nm, slots, ds.nd_ns, ds.nd_obj,
-                       ds.nd_rel, ds.adj_off, sig, ds.nflags, ds.n_nodes, x2, coff, csub);
+                       ds.nd_rel, ds.adj_off, sig, ds.nflags, ds.n_nodes);
     HIPC(hipGetLastError());
   }
   HIPC(hipStreamSynchronize(stream));
@@ -518,7 +480,6 @@ int Snapshot::build_hash_tables() {
   ds.dset_nb = buckets;
   ds.nmap = nm;
   ds.nmap_n = slots;
-  ds.nmap_x2 = x2;
   ds.shard_rank = shard_rank;
   ds.shard_n = shard_n;
   ds.nowner = nullptr;

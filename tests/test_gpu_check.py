@@ -186,18 +186,13 @@ def _torch():
     return torch
 
 
-@pytest.mark.parametrize("n_tuples,gmax,ecap,unheld,drec", [(200_000, 10, 512, 1, 1), (300_000, 5, 512, 1, 1),
-                                                             (300_000, 10, 512, 0, 1), (300_000, 10, 32, 1, 1),
-                                                             (300_000, 5, 0, 0, 1), (300_000, 10, 512, 1, 0)])
-def test_synthetic_graph_vs_oracle(n_tuples, gmax, ecap, unheld, drec, monkeypatch):
+@pytest.mark.parametrize("n_tuples,gmax,ecap,unheld", [(200_000, 10, 512, 1), (300_000, 5, 512, 1), (300_000, 10, 512, 0),
+                                                        (300_000, 10, 32, 1), (300_000, 5, 0, 0)])
+def test_synthetic_graph_vs_oracle(n_tuples, gmax, ecap, unheld):
     """ecap: the stream tier's per-query edge budget (32: most long walks go on to the backward and
-    grid tiers; 0: no budget, every walk finishes in the stream tier).  drec 0 (KG_DREC=0 and KG_NMAP64=0
-    at build): every checkDirect probe through dset, none through the nodes' direct records or the
-    node-map slots' inline subjects (the round-3 layout)."""
+    grid tiers; 0: no budget, every walk finishes in the stream tier)."""
     torch = _torch()
     from keto_amd import _lib
-    monkeypatch.setenv("KG_DREC", str(drec))
-    monkeypatch.setenv("KG_NMAP64", str(drec))
     snap = Snapshot.synthetic(n_tuples, seed=20250131)
     snap.tune("stream_ecap", ecap)
     snap.tune("resolve_unheld", unheld)  # 0: the node map is read for every query (round-1 order)
