@@ -3,13 +3,10 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
-#include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
-#include <deque>
 #include <functional>
-#include <mutex>
 #include <new>
 #include <string>
 #include <thread>
@@ -30,80 +27,6 @@ int set_error(int code, const char* fmt, ...) {
   return code;
 }
 void clear_error() { g_err.clear(); }
-
-// Host-side copies of host-buffer batches (caller's queries -> pinned staging, pinned results ->
-// caller) split over a small pool of library threads: one core's memcpy (~10 GB/s) bounded a
-// 1 M-check kg_check_batch call (28 MB of kg_query in) at ~3 ms, more than its device time.
-class CopyPool {
- public:
-  CopyPool() {
-    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-    const unsigned n = std::min(7u, std::max(1u, hw / 4));  // the caller copies too
-    for (unsigned i = 0; i < n; i++) th_.emplace_back([this] { loop(); });
-  }
-  ~CopyPool() {
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      stop_ = true;
-    }
-    cv_.notify_all();
-    for (auto& t : th_) t.join();
-  }
-  size_t workers() const { return th_.size(); }
-  // memcpy(dst, src, bytes) in pieces over the pool and the calling thread; returns when done
-  void copy(void* dst, const void* src, size_t bytes) {
-    constexpr size_t MIN_PIECE = 2u << 20;
-    const size_t k = std::min<size_t>(th_.size() + 1, bytes / MIN_PIECE);
-    if (k <= 1) {
-      memcpy(dst, src, bytes);
-      return;
-    }
-    const size_t piece = (bytes + k - 1) / k;
-    std::mutex m;
-    std::condition_variable cv;
-    size_t left = k - 1;
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      for (size_t i = 1; i < k; i++) {
-        const size_t o = i * piece, b = std::min(piece, bytes - std::min(bytes, o));
-        q_.push_back([=, &m, &cv, &left] {
-          if (b) memcpy((char*)dst + o, (const char*)src + o, b);
-          std::lock_guard<std::mutex> l2(m);
-          if (--left == 0) cv.notify_one();
-        });
-      }
-    }
-    cv_.notify_all();
-    memcpy(dst, src, std::min(piece, bytes));
-    std::unique_lock<std::mutex> lk(m);
-    cv.wait(lk, [&] { return left == 0; });
-  }
-
- private:
-  void loop() {
-    for (;;) {
-      std::function<void()> f;
-      {
-        std::unique_lock<std::mutex> lk(mu_);
-        cv_.wait(lk, [this] { return stop_ || !q_.empty(); });
-        if (stop_ && q_.empty()) return;
-        f = std::move(q_.front());
-        q_.pop_front();
-      }
-      f();
-    }
-  }
-  std::vector<std::thread> th_;
-  std::mutex mu_;
-  std::condition_variable cv_;
-  std::deque<std::function<void()>> q_;
-  bool stop_ = false;
-};
-
-static CopyPool& copy_pool() {
-  static CopyPool* p = new CopyPool();  // never destroyed: callers may copy during process exit
-  return *p;
-}
 }  // namespace kg
 
 using kg::Snapshot;
@@ -726,7 +649,7 @@ struct LaneLease {
 int kg_check_batch(kg_snapshot* sp, const kg_query* q, size_t n, int32_t global_max_depth, uint8_t* out,
                    uint32_t* err_code, kg_stats* stats) {
   KG_GUARD_BEGIN
-  constexpr size_t MIN_PER_REPLICA = 16384, SLICE = 262144;
+  constexpr size_t MIN_PER_REPLICA = 16384, SLICE = 65536;
   if (!sp) return set_error(-2, "NULL snapshot");
   if (n && (!q || !out)) return set_error(-2, "NULL buffer");
   Snapshot* s = reinterpret_cast<Snapshot*>(sp);
@@ -756,7 +679,7 @@ int kg_check_batch(kg_snapshot* sp, const kg_query* q, size_t n, int32_t global_
     HIPC(hipSetDevice(L->device));
     for (size_t o = 0; o < m; o += SLICE) {
       const size_t k = std::min(SLICE, m - o);
-      kg::copy_pool().copy(L->h_q + o, q + b[i] + o, k * sizeof(kg_query));
+      memcpy(L->h_q + o, q + b[i] + o, k * sizeof(kg_query));
       if (hipMemcpyAsync(L->d_q + o, L->h_q + o, k * sizeof(kg_query), hipMemcpyHostToDevice, L->stream) != hipSuccess) {
         rc = set_error(-1, "H2D copy failed");
         break;
@@ -785,8 +708,8 @@ int kg_check_batch(kg_snapshot* sp, const kg_query* q, size_t n, int32_t global_
         r2 = set_error(-1, "D2H copy failed");
       if (!r2) r2 = L->w->wait(L->stream, blocking);  // the error text is set by wait()
       if (!r2) {
-        kg::copy_pool().copy(out + b[i], L->h_out, m);
-        if (err_code) kg::copy_pool().copy(err_code + b[i], L->h_err, m * 4);
+        memcpy(out + b[i], L->h_out, m);
+        if (err_code) memcpy(err_code + b[i], L->h_err, m * 4);
       }
       rc = r2;
     } else {
