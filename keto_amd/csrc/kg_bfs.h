@@ -46,7 +46,7 @@ __device__ __forceinline__ uint32_t nmap_find(const DevSnap& s, uint32_t ns, uin
 __device__ __forceinline__ bool dset_probe(const DevSnap& s, uint32_t node, uint32_t subj) {
   static_assert(DSET_BUCKET == 2, "one ulonglong2 per bucket");
   uint64_t key = dset_key(node, subj);
-  uint64_t b = hash_home(key, s.dset_nb);
+  uint64_t b = dset_home(key, s.dset_nb);
   for (uint64_t n = 0; n < s.dset_nb; n++) {
     const ulonglong2 a = *reinterpret_cast<const ulonglong2*>(s.dset + b * DSET_BUCKET);
     if (a.x == key || a.y == key) return true;

@@ -307,8 +307,9 @@ struct Stream4Lds {
   unsigned long long vt[1 << VLOG2];  // direct-mapped visited cache (0 = empty)
   uint32_t e_beg[QC], e_meta[QC];     // FIFO ring
   uint32_t pref[65];                  // edge-owner marks (+1 dummy)
-  uint32_t s_state[32], s_qi[32], s_subj[32], s_sig[32], s_last[32], s_edg[32];
+  uint32_t s_state[32], s_qi[32], s_subj[32], s_last[32], s_edg[32];
   uint32_t s_node[32], s_depth[32], s_beg[32], s_len[32];
+  uint2 s_ss[32];  // per slot: the subject's Bloom mask, the visited-cache salt of (slot, generation)
 };
 
 struct LqList {
@@ -352,7 +353,8 @@ __global__ __launch_bounds__(256) void k_stream4(DevSnap s, LqList wl, uint32_t*
   uint32_t head = 0, tail = 0, head_off = 0;
   bool pend = false;
   uint32_t pend_node = 0, pend_slot = 0, pend_gen = 0;
-  unsigned long long st_rows = 0, st_edges = 0, st_probes = 0, st_done = 0, st_steps = 0;
+  // per-lane counters: each grows by at most one per step, and a wave's steps stay far below 2^32
+  uint32_t st_rows = 0, st_edges = 0, st_probes = 0, st_done = 0, st_steps = 0;
   for (;;) {
     // ---- the staged chunk (loaded at least one step ago) becomes the current one
     if (c_left == 0 && pf == 2) {
@@ -378,9 +380,11 @@ __global__ __launch_bounds__(256) void k_stream4(DevSnap s, LqList wl, uint32_t*
         const uint32_t slot = lane, gen = L.s_state[slot] & S2_GEN;  // freed slots hold a fresh generation
         const bool over = qdepth > (int32_t)S2_DMAX || qlen > S2_LONG || qlen > ecap;
         const uint32_t at = tail + r;
+        // visited-cache salt of (slot, generation): one LDS read per step instead of two multiplies
+        const uint32_t salt = (slot * 0x85EBCA77u) ^ (gen * 0xC2B2AE3Du);
         L.s_qi[slot] = qi;
         L.s_subj[slot] = qsubj;
-        L.s_sig[slot] = subj_sig(qsubj);
+        L.s_ss[slot] = make_uint2(subj_sig(qsubj), salt);
         L.s_node[slot] = qnode;
         L.s_depth[slot] = (uint32_t)qdepth;
         L.s_beg[slot] = qbeg;
@@ -391,7 +395,7 @@ __global__ __launch_bounds__(256) void k_stream4(DevSnap s, LqList wl, uint32_t*
         // the root counts as visited (a cycle back to it is not expanded again)
         const unsigned long long key =
             (1ull << 63) | ((unsigned long long)gen << 37) | ((unsigned long long)slot << 32) | qnode;
-        L.vt[((qnode * 0x9E3779B1u) ^ (slot * 0x85EBCA77u) ^ (gen * 0xC2B2AE3Du)) >> (32 - VLOG2)] = key;
+        L.vt[((qnode * 0x9E3779B1u) ^ salt) >> (32 - VLOG2)] = key;
         L.e_beg[at & (QC - 1)] = qbeg;
         L.e_meta[at & (QC - 1)] = s2_meta(over ? 0u : qlen, slot, gen, over ? 2u : (uint32_t)qdepth);
       }
@@ -469,9 +473,10 @@ __global__ __launch_bounds__(256) void k_stream4(DevSnap s, LqList wl, uint32_t*
     const bool act = (uint32_t)lane < taken;
     const AdjX x = s.adjx[act ? ob + ((uint32_t)lane - ox) : 0u];  // adjx[0] exists (n_set_edges + 1)
     const ulonglong2 pb =
-        *reinterpret_cast<const ulonglong2*>(s.dset + (pvalid ? hash_home(pkey, s.dset_nb) : 0ull) * DSET_BUCKET);
+        *reinterpret_cast<const ulonglong2*>(s.dset + (pvalid ? dset_home(pkey, s.dset_nb) : 0ull) * DSET_BUCKET);
     const uint32_t slot = (om >> 11) & 31u, d = om >> 25, g = (om >> 16) & S2_GEN;
-    const uint32_t ssig = L.s_sig[slot];  // LDS, under the gathers' latency
+    const uint2 ss = L.s_ss[slot];  // LDS, under the gathers' latency: Bloom mask, visited-cache salt
+    const uint32_t ssig = ss.x;
     head += ncons;
     st_edges += (lane == 0) ? taken : 0u;
     st_steps += (lane == 0) ? 1u : 0u;
@@ -491,7 +496,7 @@ __global__ __launch_bounds__(256) void k_stream4(DevSnap s, LqList wl, uint32_t*
     const bool longrow = keepc && x.len > S2_LONG;
     const unsigned long long key =
         (1ull << 63) | ((unsigned long long)g << 37) | ((unsigned long long)slot << 32) | x.node;
-    const uint32_t hv = ((x.node * 0x9E3779B1u) ^ (slot * 0x85EBCA77u) ^ (g * 0xC2B2AE3Du)) >> (32 - VLOG2);
+    const uint32_t hv = ((x.node * 0x9E3779B1u) ^ ss.y) >> (32 - VLOG2);
     const unsigned long long old = keepc ? L.vt[hv] : 0ull;
     const bool fresh = keepc && !longrow && old != key;
     if (fresh) L.vt[hv] = key;

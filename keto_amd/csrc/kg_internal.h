@@ -64,6 +64,15 @@ __host__ __device__ __forceinline__ uint64_t hash_home(uint64_t key, uint64_t n)
   return (uint64_t)(((unsigned __int128)mix64(key) * n) >> 64);
 }
 __host__ __device__ __forceinline__ uint64_t hash_next(uint64_t i, uint64_t n) { return i + 1 == n ? 0 : i + 1; }
+// dset home bucket of a (node << 32 | subject) key: multiply-shift (Fibonacci) hashing -- the key times
+// an odd 64-bit constant, whose high bits mix every key bit, scaled to the bucket count by a 64 x 32 high
+// product (n < 2^32: the table is capped below a fifth of HBM).  5 integer multiplies where mix64 plus a
+// 128-bit product took 10: the stream tier spends most of its time issuing VALU (profiles/r4g_*), and
+// this hash ran for every lane of every step.
+__host__ __device__ __forceinline__ uint64_t dset_home(uint64_t key, uint64_t n) {
+  const uint64_t x = key * 0x9E3779B97F4A7C15ull;
+  return ((x >> 32) * n + (((x & 0xFFFFFFFFull) * n) >> 32)) >> 32;
+}
 
 // Owner of position i in a CSR with offsets off[0..n]: the last node whose row starts at or before i
 // (empty rows share a start; the owner is the one whose range holds i).  Lets the build kernels run

@@ -542,7 +542,7 @@ __global__ __launch_bounds__(256) void k_shard_level(DevSnap s, const kg_frec* _
         const bool want_p = probe && r.depth >= 1 && r.subj != NONE;
         const uint64_t dkey = dset_key(r.node, r.subj);
         const ulonglong2 pb = *reinterpret_cast<const ulonglong2*>(
-            s.dset + (want_p ? hash_home(dkey, s.dset_nb) : 0ull) * DSET_BUCKET);
+            s.dset + (want_p ? dset_home(dkey, s.dset_nb) : 0ull) * DSET_BUCKET);
         const uint32_t an = packed ? 0u : r.node;
         const uint64_t a0 = s.adj_off[an], a1 = s.adj_off[an + 1];
         const uint64_t vkey = ((uint64_t)r.q << 32) | (packed ? (0x80000000u | r.node) : r.node);

@@ -34,7 +34,7 @@ __global__ void k_dset_insert_rows(uint64_t* dset, uint64_t nb, const uint64_t* 
     for (uint64_t i = c * CSR_CHUNK, ie = min(n_rows, i + CSR_CHUNK), v = csr_owner(row_off, n_nodes, i); i < ie; i++) {
       v = csr_advance(row_off, n_nodes, (uint32_t)v, i);
       const uint64_t key = dset_key((uint32_t)v, row_subj[i]);
-      uint64_t b = hash_home(key, nb);
+      uint64_t b = dset_home(key, nb);
       for (uint64_t n = 0; n < nb; n++) {  // sized for load <= 0.25: always finds room
         uint64_t* bucket = dset + b * DSET_BUCKET;
         bool done = false;
@@ -456,6 +456,10 @@ int Snapshot::build_hash_tables() {
   (void)hipGetLastError();
   uint64_t buckets = std::max<uint64_t>(1, (n_rows * 4 + DSET_BUCKET - 1) / DSET_BUCKET);
   if (buckets * DSET_BUCKET * 8 > hbm_total / 5) buckets = std::max<uint64_t>(1, (n_rows * 8 + 2) / 3 / DSET_BUCKET);
+  if (buckets >= (1ull << 32)) {  // dset_home scales by a 32-bit bucket count
+    if (n_rows * 2 >= (0xFFFFFFFFull - 1) * DSET_BUCKET) return set_error(KG_ERR_RESOURCE_CODE, "check rows exceed dset");
+    buckets = 0xFFFFFFFFull;
+  }
   uint64_t* dset = nullptr;
   if (alloc((void**)&dset, buckets * DSET_BUCKET * 8)) return -1;
   HIPC(hipMemsetAsync(dset, 0xFF, buckets * DSET_BUCKET * 8, stream));
