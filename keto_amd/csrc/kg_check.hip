@@ -482,9 +482,11 @@ __global__ __launch_bounds__(256) void k_stream4(DevSnap s, LqList wl, uint32_t*
     st_steps += (lane == 0) ? 1u : 0u;
     // checkDirect probe, first bucket; a chain past a full first bucket (rare at load <= 0.25) is
     // walked by the lanes that need it under a wave-uniform branch
-    bool hit = pvalid && (pb.x == pkey || pb.y == pkey);
+    // bitwise, not short-circuit: a branch on pvalid split the bucket's 16-B load in two, one half
+    // issued and waited for inside the branch
+    bool hit = pvalid & ((pb.x == pkey) | (pb.y == pkey));
     {
-      const bool more = pvalid && !hit && pb.y != EMPTY64;
+      const bool more = pvalid & !hit & (pb.y != EMPTY64);
       if (__ballot(more)) {
         if (more) hit = dset_probe(s, pend_node, (uint32_t)pkey);
       }
