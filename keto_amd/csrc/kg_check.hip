@@ -177,7 +177,7 @@ __global__ __launch_bounds__(256) void k_resolve(DevSnap s, const kg_query* __re
     const bool unheld = no_holder_filter == 2 && use_bits && !s.relflags && !((hw >> (subj & 31)) & 1u);
     NSlot n0{};
     if (key_ok && !unheld) n0 = s.nmap[ni];
-    uint32_t node = NONE, rb = 0, rl = 0, rsig = 0xFFFFFFFFu, nfl = 0;
+    uint32_t node = NONE, rb = 0, rl = 0, rsig_lo = 0xFFFFFFFFu, rsig = 0xFFFFFFFFu, nfl = 0;
     if (unheld) {
       no_holder = true;
     } else if (key_ok) {
@@ -197,6 +197,7 @@ __global__ __launch_bounds__(256) void k_resolve(DevSnap s, const kg_query* __re
         rb = v.beg;
         rl = v.len;
         rsig = v.sig;
+        rsig_lo = (uint32_t)v.pad1;  // signature bits 0-15 in bits 16-31
         nfl = (uint32_t)(v.pad1 & 0xFFu);
       }
     }
@@ -224,7 +225,7 @@ __global__ __launch_bounds__(256) void k_resolve(DevSnap s, const kg_query* __re
       // row signature in the node-map slot rules out most misses without touching dset.
       // an unset holder bit rules the probe out as well (the exact tuple would make subj a holder)
       const bool nobit = use_bits && !((hw >> (subj & 31)) & 1u);
-      did_probe = subj != NONE && !nobit && sig_maybe(rsig, subj_sig(subj));
+      did_probe = subj != NONE && !nobit && sig_maybe(rsig_lo, rsig, subj_sig(subj));
       member = did_probe && dset_probe(s, node, subj);
       if (member || d < 2 || rl == 0) route = ROUTE_DONE;
       // a subject that no row holds cannot be reached from any root (checkDirect never hits)
@@ -309,7 +310,7 @@ struct Stream4Lds {
   uint32_t pref[65];                  // edge-owner marks (+1 dummy)
   uint32_t s_state[32], s_qi[32], s_subj[32], s_last[32], s_edg[32];
   uint32_t s_node[32], s_depth[32], s_beg[32], s_len[32];
-  uint2 s_ss[32];  // per slot: the subject's Bloom mask, the visited-cache salt of (slot, generation)
+  uint4 s_ss[32];  // per slot: the subject's Bloom mask (2 words), the visited-cache salt of (slot, generation)
 };
 
 struct LqList {
@@ -384,7 +385,8 @@ __global__ __launch_bounds__(256) void k_stream4(DevSnap s, LqList wl, uint32_t*
         const uint32_t salt = (slot * 0x85EBCA77u) ^ (gen * 0xC2B2AE3Du);
         L.s_qi[slot] = qi;
         L.s_subj[slot] = qsubj;
-        L.s_ss[slot] = make_uint2(subj_sig(qsubj), salt);
+        const uint2 qm = subj_sig(qsubj);
+        L.s_ss[slot] = make_uint4(qm.x, qm.y, salt, 0u);
         L.s_node[slot] = qnode;
         L.s_depth[slot] = (uint32_t)qdepth;
         L.s_beg[slot] = qbeg;
@@ -475,8 +477,8 @@ __global__ __launch_bounds__(256) void k_stream4(DevSnap s, LqList wl, uint32_t*
     const ulonglong2 pb =
         *reinterpret_cast<const ulonglong2*>(s.dset + (pvalid ? dset_home(pkey, s.dset_nb) : 0ull) * DSET_BUCKET);
     const uint32_t slot = (om >> 11) & 31u, d = om >> 25, g = (om >> 16) & S2_GEN;
-    const uint2 ss = L.s_ss[slot];  // LDS, under the gathers' latency: Bloom mask, visited-cache salt
-    const uint32_t ssig = ss.x;
+    const uint4 ss = L.s_ss[slot];  // LDS, under the gathers' latency: Bloom mask, visited-cache salt
+    const uint2 ssig = make_uint2(ss.x, ss.y);
     head += ncons;
     st_edges += (lane == 0) ? taken : 0u;
     st_steps += (lane == 0) ? 1u : 0u;
@@ -494,11 +496,12 @@ __global__ __launch_bounds__(256) void k_stream4(DevSnap s, LqList wl, uint32_t*
     st_probes += pvalid ? 1u : 0u;
     // ---- children: kept ones (rest >= 2 after the hop, non-empty set row) are marked + appended;
     // every child new to the query is probed next step
-    const bool keepc = act && d >= 3 && x.len > 0;  // x of an inactive lane is adjx[0]: never used
-    const bool longrow = keepc && x.len > S2_LONG;
+    const uint32_t xlen = adjx_len16(x);  // saturated at ADJX_LEN_SAT: any such row is long here
+    const bool keepc = act && d >= 3 && xlen > 0;  // x of an inactive lane is adjx[0]: never used
+    const bool longrow = keepc && xlen > S2_LONG;
     const unsigned long long key =
         (1ull << 63) | ((unsigned long long)g << 37) | ((unsigned long long)slot << 32) | x.node;
-    const uint32_t hv = ((x.node * 0x9E3779B1u) ^ ss.y) >> (32 - VLOG2);
+    const uint32_t hv = ((x.node * 0x9E3779B1u) ^ ss.z) >> (32 - VLOG2);
     const unsigned long long old = keepc ? L.vt[hv] : 0ull;
     const bool fresh = keepc && !longrow && old != key;
     if (fresh) L.vt[hv] = key;
@@ -509,14 +512,14 @@ __global__ __launch_bounds__(256) void k_stream4(DevSnap s, LqList wl, uint32_t*
     if (appended) {
       const uint32_t at = tail + pos;
       L.e_beg[at & (QC - 1)] = x.begin;
-      L.e_meta[at & (QC - 1)] = x.len | (om & 0x01FFF800u) | ((d - 1) << 25);
+      L.e_meta[at & (QC - 1)] = xlen | (om & 0x01FFF800u) | ((d - 1) << 25);
       atomicMax(&L.s_last[slot], at);   // no return: read at the finish check
-      atomicAdd(&L.s_edg[slot], x.len);  // edge budget, likewise
+      atomicAdd(&L.s_edg[slot], xlen);  // edge budget, likewise
     }
     if (longrow || (fresh && !appended)) atomicOr(&L.s_state[slot], S2_OVER);  // row too long / FIFO full
     tail += min((uint32_t)__popcll(am), room);
     if (hit) atomicOr(&L.s_state[pend_slot], S2_HIT);
-    pend = act && (keepc ? appended : true) && sig_maybe(x.sig, ssig);
+    pend = act && (keepc ? appended : true) && sig_maybe(x.lsig, x.sig, ssig);
     pend_node = x.node;
     pend_slot = slot;
     pend_gen = g;

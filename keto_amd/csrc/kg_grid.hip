@@ -339,7 +339,7 @@ __global__ __launch_bounds__(256) void k_grid_level(DevSnap s, GridLog lg, int l
           const AdjX x = s.adjx[rb + (e - beg)];
           child = x.node;
           cb = x.begin;
-          clen = x.len;
+          clen = adjx_len(s, x);
           // forward turn `level` finds hop level+1: it is expanded at forward turn level+1 and may be met
           // by backward turn `level` (both need a set row)
           const bool next_f = fwd_active(bidir, level + 1, D), meet_b = back_active(bidir, level, D);
@@ -351,7 +351,7 @@ __global__ __launch_bounds__(256) void k_grid_level(DevSnap s, GridLog lg, int l
             fresh = ins > 0;
           }
           if (fresh) {
-            if (sig_maybe(x.sig, subj_sig(si.x))) {  // the signature rules out most misses
+            if (sig_maybe(x.lsig, x.sig, subj_sig(si.x))) {  // the signature rules out most misses
               probes++;
               if (dset_probe(s, child, si.x)) atomicExch(&sl.hit[slot], 1u);
             }

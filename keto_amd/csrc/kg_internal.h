@@ -110,32 +110,47 @@ struct RwNode {
 };
 enum { RW_OR = 0, RW_AND = 1, RW_COMPUTED = 2, RW_TTU = 3, RW_NOT = 4 };
 
-// One set-adjacency edge with the child's own set row inlined (begin/len) and a 2-bit Bloom
-// signature of the child's direct subjects (its full row): a checkDirect probe whose subject bits
-// are not all present in the signature is a certain miss and is skipped.  A BFS level needs one
-// dependent HBM round trip instead of two (no adj_off lookup per discovered node).
-struct AdjX {
-  uint32_t node, begin, len, sig;
-};
-
-__host__ __device__ __forceinline__ uint32_t subj_sig(uint32_t subj) {
+// Bloom signature of a node's direct subjects (its full row): 48 bits, 2 per subject.  A
+// checkDirect probe whose subject bits are not all present is a certain miss and is skipped.  The
+// bits sit in two words as they are stored: x = signature bits 0-15 in bits 16-31 (bits 0-15 hold
+// the carrier's own low field: AdjX's row length, NSlot's flags), y = signature bits 16-47.
+// (Round 3 had 32 bits: a row of 20 subjects passed 52 % of absent subjects, now 32 %.)
+constexpr uint32_t SIG_LO = 0xFFFF0000u;
+__host__ __device__ __forceinline__ uint2 subj_sig(uint32_t subj) {
   uint32_t h = subj * 0x9E3779B1u;
   h ^= h >> 15;
   h *= 0x85EBCA77u;
   h ^= h >> 13;
-  return (1u << (h & 31)) | (1u << ((h >> 5) & 31));
+  const uint32_t p0 = ((h & 0xFFFFu) * 48u) >> 16, p1 = ((h >> 16) * 48u) >> 16;  // two positions in [0, 48)
+  uint2 m = make_uint2(0u, 0u);
+  if (p0 < 16) m.x |= 1u << (16 + p0);
+  else m.y |= 1u << (p0 - 16);
+  if (p1 < 16) m.x |= 1u << (16 + p1);
+  else m.y |= 1u << (p1 - 16);
+  return m;
 }
-__host__ __device__ __forceinline__ bool sig_maybe(uint32_t sig, uint32_t subj_mask) {
-  return (sig & subj_mask) == subj_mask;
+// sig_lo: a word whose bits 16-31 are signature bits 0-15 (its low half is ignored), sig_hi: bits 16-47
+__host__ __device__ __forceinline__ bool sig_maybe(uint32_t sig_lo, uint32_t sig_hi, uint2 m) {
+  return ((sig_lo & m.x) == m.x) & ((sig_hi & m.y) == m.y);
 }
+
+// One set-adjacency edge with the child's own set row inlined (begin / length) and the child's
+// signature: a BFS level needs one dependent HBM round trip instead of two (no adj_off lookup per
+// discovered node).  lsig: the row length in bits 0-15 (ADJX_LEN_SAT = 65535 or longer: read
+// adj_off, adjx_len) and signature bits 0-15 in bits 16-31; sig: signature bits 16-47.
+constexpr uint32_t ADJX_LEN_SAT = 0xFFFFu;
+struct AdjX {
+  uint32_t node, begin, lsig, sig;
+};
+__host__ __device__ __forceinline__ uint32_t adjx_len16(const AdjX& x) { return x.lsig & ADJX_LEN_SAT; }
 
 // Node-map slot: key (ns,rel,obj), node id and the node's set-adjacency row, one 32-B slot so a
 // request mapping is one random line.  key == EMPTY64: free.
 struct NSlot {
   uint64_t key;
   uint32_t node, beg, len;
-  uint32_t sig;  // Bloom signature of the node's row subjects (as AdjX.sig): k_resolve's root probe filter
-  uint64_t pad1;  // low byte: the node's flags (nflags; 0 without a namespace program)
+  uint32_t sig;  // signature bits 16-47 of the node's row subjects (as AdjX.sig): k_resolve's root probe filter
+  uint64_t pad1;  // low byte: the node's flags (nflags; 0 without a namespace program); bits 16-31: signature bits 0-15
 };
 // Holder-hash slot: tagged subject -> hold[first, first + count).  key == NONE: free.
 struct HSlot {
@@ -182,6 +197,12 @@ struct DevSnap {
   uint32_t shard_rank, shard_n;
   const uint8_t* nowner;  // [n_nodes] owner rank of every node (shard_n > 1)
 };
+
+// The child's exact set-row length (one adj_off read for rows of ADJX_LEN_SAT edges or more).
+__device__ __forceinline__ uint32_t adjx_len(const DevSnap& s, const AdjX& x) {
+  const uint32_t l = adjx_len16(x);
+  return l < ADJX_LEN_SAT ? l : (uint32_t)(s.adj_off[x.node + 1] - s.adj_off[x.node]);
+}
 
 // astRelationFor (internal/check/engine.go:209-229) as flags: bit0 = has rewrite, bit1 = the
 // namespace is configured with relations and this one is not declared ("relation %q not found").

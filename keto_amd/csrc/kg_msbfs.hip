@@ -242,18 +242,18 @@ __device__ __forceinline__ void ms_edge(const DevSnap& s, const MsView& v, uint3
   uint64_t hits = nw & ~many & tg0;
   for (uint64_t m = nw & many; m; m &= m - 1) {
     const uint32_t subj = v.qs[(size_t)g * 64 * K + k * 64 + __builtin_ctzll(m)];
-    if (sig_maybe(x.sig, subj_sig(subj)) && dset_probe(s, x.node, subj)) hits |= m & (~m + 1);
+    if (sig_maybe(x.lsig, x.sig, subj_sig(subj)) && dset_probe(s, x.node, subj)) hits |= m & (~m + 1);
   }
   if (hits) atomicOr((unsigned long long*)&v.hit[(size_t)g * K + k], (unsigned long long)hits);
   // expansion: those that may expand it
-  const uint64_t ex = x.len ? (nw & em) : 0ull;
+  const uint64_t ex = adjx_len16(x) ? (nw & em) : 0ull;
   if (ex) {
     atomicOr((unsigned long long*)&v.fr[nx][at], (unsigned long long)ex);
     const uint32_t want_st = (uint32_t)L + 2;
     app = st0 < want_st && atomicMax(&v.stamp[(size_t)g * n + x.node], want_st) < want_st;
     child = x.node;
     cb = x.begin;
-    clen = x.len;
+    clen = adjx_len(s, x);
   }
 }
 

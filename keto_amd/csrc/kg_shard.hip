@@ -281,13 +281,14 @@ __device__ __forceinline__ SeedQ seed_query(const DevSnap& s, const kg_query* __
   // node map (k_resolve's resolve_unheld order)
   const bool unheld = held && !s.relflags && sid &&
                       (subj == NONE || subj >= held_n || !((held[subj >> 5] >> (subj & 31)) & 1u));
-  uint32_t node = NONE, rsig = 0xFFFFFFFFu, rlen = 0;
+  uint32_t node = NONE, rsig_lo = 0xFFFFFFFFu, rsig = 0xFFFFFFFFu, rlen = 0;
   if (!unheld && nmap_key_ok(x.t.ns, x.t.rel, x.t.obj)) {
     const uint64_t key = nmap_key(x.t.ns, x.t.rel, x.t.obj);
     const NSlot* sl = nmap_slot(s, key, hash_home(key, s.nmap_n));
     if (sl) {
       node = sl->node;
       rsig = sl->sig;
+      rsig_lo = (uint32_t)sl->pad1;  // signature bits 0-15 in bits 16-31
       rlen = sl->len;
     }
   }
@@ -328,7 +329,7 @@ __device__ __forceinline__ SeedQ seed_query(const DevSnap& s, const kg_query* __
     o.act = true;
     o.dest = s.nowner ? s.nowner[node] : 0u;
     // signatures are built from this rank's rows: only a locally owned node's rules a probe out
-    const bool may = subj == NONE || o.dest != s.shard_rank || sig_maybe(rsig, subj_sig(subj));
+    const bool may = subj == NONE || o.dest != s.shard_rank || sig_maybe(rsig_lo, rsig, subj_sig(subj));
     o.r = kg_frec{(s.shard_rank << Q_BITS) | i, node, subj, d | (may ? 0 : D_NOPROBE)};
     if (o.dest == s.shard_rank && !s.relflags) {
       // a locally owned root without a namespace program (as shard_child): checkDirect here, a
@@ -410,23 +411,25 @@ __device__ __forceinline__ void shard_child(const DevSnap& s, const kg_frec& pr,
       // depth - 1 >= 2) -- leaves never travel or touch the visited table.  Results are
       // unchanged (membership is monotone and nothing can end as an error without a program);
       // a hit only lands one level earlier.
-      const bool hit = pr.subj != NONE && sig_maybe(ax.sig, subj_sig(pr.subj)) && dset_probe(s, child, pr.subj);
+      const bool hit =
+          pr.subj != NONE && sig_maybe(ax.lsig, ax.sig, subj_sig(pr.subj)) && dset_probe(s, child, pr.subj);
+      const uint32_t alen = adjx_len16(ax);  // exact below ADJX_LEN_SAT
       if (hit && (pr.q >> Q_BITS) == me) {
         res[pr.q & Q_MASK] = KG_IS_MEMBER;
       } else if (hit) {
         c = kg_frec{pr.q, KG_FREC_HIT, 0u, 0};
         dest = pr.q >> Q_BITS;
         send = true;
-      } else if (ax.len && pr.depth >= 3) {
-        if (pack && ax.begin < 0x80000000u && ax.len < (1u << PK_LEN_BITS) && pr.depth - 1 < 256)
-          c = kg_frec{pr.q, ax.begin, pr.subj, (int32_t)((ax.len << 8) | (uint32_t)(pr.depth - 1)) | D_ROW | D_NOPROBE};
+      } else if (alen && pr.depth >= 3) {
+        if (pack && ax.begin < 0x80000000u && alen < ADJX_LEN_SAT && alen < (1u << PK_LEN_BITS) && pr.depth - 1 < 256)
+          c = kg_frec{pr.q, ax.begin, pr.subj, (int32_t)((alen << 8) | (uint32_t)(pr.depth - 1)) | D_ROW | D_NOPROBE};
         else
           c = kg_frec{pr.q, child, pr.subj, (pr.depth - 1) | D_NOPROBE};
         send = true;
       }
     } else {
       // signatures are built from this rank's rows: only a locally owned child's rules a probe out
-      const bool may = pr.subj == NONE || dest != me || sig_maybe(ax.sig, subj_sig(pr.subj));
+      const bool may = pr.subj == NONE || dest != me || sig_maybe(ax.lsig, ax.sig, subj_sig(pr.subj));
       c = kg_frec{pr.q, child, pr.subj, (pr.depth - 1) | (may ? 0 : D_NOPROBE)};
       send = true;
     }

@@ -54,7 +54,7 @@ __global__ void k_dset_insert_rows(uint64_t* dset, uint64_t nb, const uint64_t* 
 }
 
 __global__ void k_nmap_insert(NSlot* nm, uint64_t slots, const uint32_t* nd_ns, const uint32_t* nd_obj,
-                              const uint32_t* nd_rel, const uint64_t* adj_off, const uint32_t* sig,
+                              const uint32_t* nd_rel, const uint64_t* adj_off, const uint2* sig,
                               const uint8_t* flags, uint32_t n_nodes) {
   uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
   if (v >= n_nodes) return;
@@ -67,8 +67,10 @@ __global__ void k_nmap_insert(NSlot* nm, uint64_t slots, const uint32_t* nd_ns, 
       nm[i].node = v;
       nm[i].beg = (uint32_t)adj_off[v];
       nm[i].len = (uint32_t)(adj_off[v + 1] - adj_off[v]);
-      nm[i].sig = sig[v];
-      nm[i].pad1 = flags ? flags[v] : 0u;  // node flags: k_resolve's impurity test without a random nflags read
+      const uint2 g = sig[v];
+      nm[i].sig = g.y;
+      // node flags (k_resolve's impurity test without a random nflags read) + signature bits 0-15
+      nm[i].pad1 = (flags ? flags[v] : 0u) | (g.x & SIG_LO);
       return;
     }
     i = hash_next(i, slots);
@@ -82,21 +84,26 @@ __global__ void k_node_owner(const uint32_t* nd_ns, const uint32_t* nd_obj, uint
 }
 
 // Bloom signature of every node's full row (direct subjects, tagged like dset keys).
-__global__ void k_node_sig(const uint64_t* row_off, const uint32_t* row_subj, uint32_t n_nodes, uint32_t* sig) {
+__global__ void k_node_sig(const uint64_t* row_off, const uint32_t* row_subj, uint32_t n_nodes, uint2* sig) {
   const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
   if (v >= n_nodes) return;
-  uint32_t m = 0;
-  for (uint64_t i = row_off[v], e = row_off[v + 1]; i < e && m != 0xFFFFFFFFu; i++) m |= subj_sig(row_subj[i]);
+  uint2 m = make_uint2(0u, 0u);
+  for (uint64_t i = row_off[v], e = row_off[v + 1]; i < e && (m.x != SIG_LO || m.y != 0xFFFFFFFFu); i++) {
+    const uint2 b = subj_sig(row_subj[i]);
+    m.x |= b.x;
+    m.y |= b.y;
+  }
   sig[v] = m;
 }
 
-__global__ void k_build_adjx(const uint32_t* adj, const uint64_t* adj_off, const uint32_t* sig, uint64_t n_edges,
+__global__ void k_build_adjx(const uint32_t* adj, const uint64_t* adj_off, const uint2* sig, uint64_t n_edges,
                              AdjX* adjx) {
   for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < n_edges;
        e += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t c = adj[e];
     const uint64_t b = adj_off[c], x = adj_off[c + 1];
-    adjx[e] = AdjX{c, (uint32_t)b, (uint32_t)(x - b), sig[c]};
+    const uint2 g = sig[c];
+    adjx[e] = AdjX{c, (uint32_t)b, (uint32_t)std::min<uint64_t>(x - b, ADJX_LEN_SAT) | (g.x & SIG_LO), g.y};
   }
 }
 
@@ -433,8 +440,8 @@ int Snapshot::build_hash_tables() {
   if (alloc((void**)&adjx, (n_set_edges + 1) * sizeof(AdjX))) return -1;
   // per-node Bloom signature of the row subjects: inlined in adjx (child probes) and in the node map
   // (k_resolve's root probe)
-  uint32_t* sig = nullptr;
-  HIPC(hipMalloc(&sig, (size_t)ds.n_nodes * 4 + 4));
+  uint2* sig = nullptr;
+  HIPC(hipMalloc(&sig, (size_t)ds.n_nodes * 8 + 8));
   // direct tuples as checkDirect sees them: the check rows of a materialised snapshot, else the rows
   const uint64_t* coff = ds.crow_off ? ds.crow_off : ds.row_off;
   const uint32_t* csub = ds.crow_off ? ds.crow_subj : ds.row_subj;
