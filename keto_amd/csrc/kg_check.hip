@@ -51,6 +51,7 @@ struct Ctl {
   // (= the earliest start), latest end, longest wave -- workgroup-reduced atomicMax on a zeroed block
   unsigned long long tmax8[8][16];
   InterpCtl ic;
+  uint64_t grid_sum[GRID_SUM_WORDS];  // the grid tier's first-round summary (k_grid_finish), read back with Ctl
 };
 
 // One device-scope atomic on a single word costs ~11 ns at the memory side and one word saturates
@@ -947,7 +948,8 @@ int check_batch_begin(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n, 
         }
       }
       // first grid round enqueued without waiting; its readback is checked after the batch's one sync
-      const int rc = grid_tier(s, w, rq, fwd_list, fwd_count, global_max_depth, d_out, d_err, stream, &bp->gs, 1);
+      const int rc = grid_tier(s, w, rq, fwd_list, fwd_count, global_max_depth, d_out, d_err, stream, &bp->gs, 1, true,
+                               ctl->grid_sum);
       if (rc < 0) return rc;
       grid_pending = rc == 1;
       grid_list = fwd_list;
@@ -971,10 +973,9 @@ int check_batch_begin(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n, 
   static_assert(sizeof(Ctl) <= 32768, "Ctl readback fits the lower half of the pinned buffer");
   void* hbuf = w->host_buf(65536);
   if (!hbuf) return set_error(-1, "pinned host buffer");
-  if (stats) {
-    HIPC(hipEventRecord(e1, stream));
-    HIPC(hipMemcpyAsync(hbuf, ctl, sizeof(Ctl), hipMemcpyDeviceToHost, stream));
-  }
+  if (stats) HIPC(hipEventRecord(e1, stream));
+  // one readback: the counters and, when the grid tier ran a round, its summary (Ctl::grid_sum)
+  if (stats || grid_pending) HIPC(hipMemcpyAsync(hbuf, ctl, sizeof(Ctl), hipMemcpyDeviceToHost, stream));
   bp->grid_pending = grid_pending;
   bp->grid_list = grid_list;
   bp->grid_count = grid_count;
@@ -993,7 +994,9 @@ int check_batch_end(Snapshot* s, Workspace* w, BatchPending* bp, bool* reran, bo
   if (stats || bp->grid_pending)
     if (int rc = w->wait(stream, blocking)) return rc;
   if (bp->grid_pending) {  // a round that overflowed its log reruns here with fewer slots (synchronously)
-    if (int rc = grid_tier(s, w, bp->rq, bp->grid_list, bp->grid_count, bp->gdepth, bp->d_out, bp->d_err, stream, &gs, 2))
+    const Ctl* hc = reinterpret_cast<const Ctl*>(bp->ctl_host);
+    if (int rc = grid_tier(s, w, bp->rq, bp->grid_list, bp->grid_count, bp->gdepth, bp->d_out, bp->d_err, stream, &gs, 2,
+                           true, nullptr, hc->grid_sum))
       return rc;
     if (reran) *reran = w->grid_reran;
     // the rerun rewrote leaf results after check_batch_begin's combine: combine again

@@ -10,10 +10,15 @@ struct GridStats {
   unsigned long long rows = 0, edges = 0, probes = 0, done = 0, logged = 0;
 };
 
+// The first round's counters and the list length, as k_grid_finish leaves them for the batch's one
+// readback (phase 1 with dsum: no readback of their own; phase 2 reads them from hsum, the host copy).
+constexpr uint32_t GRID_SUM_WORDS = 160;
+
 struct Snapshot;
 struct Workspace;
 int grid_tier(Snapshot* s, Workspace* w, const RQuery* rq, const uint32_t* qlist, const uint32_t* d_count, int global_max_depth,
-              uint8_t* out, uint32_t* err, hipStream_t stream, GridStats* gs, int phase = 0, bool allow_ms = true);
+              uint8_t* out, uint32_t* err, hipStream_t stream, GridStats* gs, int phase = 0, bool allow_ms = true,
+              uint64_t* dsum = nullptr, const uint64_t* hsum = nullptr);
 // kg_msbfs.hip: the grid tier's queries as a multi-source bit-parallel BFS (64 queries per group)
 bool ms_usable(const Snapshot* s, int global_max_depth);
 int ms_tier(Snapshot* s, Workspace* w, const RQuery* rq, const uint32_t* qlist, const uint32_t* d_count,

@@ -404,10 +404,18 @@ __global__ __launch_bounds__(256) void k_grid_level(DevSnap s, GridLog lg, int l
   if (lane == 0 && probes) atomicAdd(&ctl->probes8[blockIdx.x & 7][threadIdx.x >> 6], (unsigned long long)probes);
 }
 
+static_assert(sizeof(GridCtl) % 8 == 0 && sizeof(GridCtl) / 8 + 1 <= GRID_SUM_WORDS && sizeof(GridCtl) / 8 < 256,
+              "the round summary fits GRID_SUM_WORDS and one workgroup copies it");
 __global__ void k_grid_finish(GridSlots sl, const uint32_t* d_count, uint32_t base, uint32_t G, uint8_t* out,
-                              uint32_t* err, const uint32_t* overflow) {
+                              uint32_t* err, const GridCtl* ctl, uint64_t* sum) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= round_slots(d_count, base, G) || *overflow) return;
+  // the round's counters and the list length for the batch's single readback (see kg_grid.h)
+  if (sum && blockIdx.x == 0) {
+    constexpr uint32_t W = sizeof(GridCtl) / 8;
+    if (threadIdx.x < W) sum[threadIdx.x] = reinterpret_cast<const uint64_t*>(ctl)[threadIdx.x];
+    else if (threadIdx.x == W) sum[W] = *d_count;
+  }
+  if (i >= round_slots(d_count, base, G) || ctl->overflow) return;
   const uint32_t qi = sl.q[i];
   out[qi] = sl.hit[i] == 1 ? KG_IS_MEMBER : KG_NOT_MEMBER;
   if (err) err[qi] = KG_ERR_NONE;
@@ -504,7 +512,8 @@ int grid_reserve(Snapshot* s) {
 // kg_snapshot_tune "grid_reserve"; one query at a time), so no workspace ever reallocates.  After
 // a round succeeds the slot count grows back (x4), so one giant query does not serialise the rest.
 int grid_tier(Snapshot* s, Workspace* w, const RQuery* rq, const uint32_t* qlist, const uint32_t* d_count, int global_max_depth,
-              uint8_t* out, uint32_t* err, hipStream_t stream, GridStats* gs, int phase, bool allow_ms) {
+              uint8_t* out, uint32_t* err, hipStream_t stream, GridStats* gs, int phase, bool allow_ms, uint64_t* dsum,
+              const uint64_t* hsum) {
   static_assert(sizeof(GridCtl) + 64 <= 32768, "grid readback fits the upper half of the pinned buffer");
   // graphs small enough for dense per-node masks: 64 queries share each walk (kg_msbfs.hip)
   if (allow_ms && ms_usable(s, global_max_depth)) {
@@ -569,18 +578,26 @@ int grid_tier(Snapshot* s, Workspace* w, const RQuery* rq, const uint32_t* qlist
         HIPC(hipGetLastError());
       }
     }
-    hipLaunchKernelGGL(k_grid_finish, dim3(slot_blocks), dim3(256), 0, stream, v.sl, d_count, done, G, out, err,
-                       &v.ctl->overflow);
+    const bool fold = phase == 1 && dsum;  // the summary rides in the caller's readback
+    hipLaunchKernelGGL(k_grid_finish, dim3(slot_blocks), dim3(256), 0, stream, v.sl, d_count, done, G, out, err, v.ctl,
+                       fold ? dsum : nullptr);
     HIPC(hipGetLastError());
-    HIPC(hipMemcpyAsync(hb, v.ctl, sizeof(GridCtl), hipMemcpyDeviceToHost, stream));
-    HIPC(hipMemcpyAsync(hb + sizeof(GridCtl) / 4, d_count, 4, hipMemcpyDeviceToHost, stream));
+    if (!fold) {
+      HIPC(hipMemcpyAsync(hb, v.ctl, sizeof(GridCtl), hipMemcpyDeviceToHost, stream));
+      HIPC(hipMemcpyAsync(hb + sizeof(GridCtl) / 4, d_count, 4, hipMemcpyDeviceToHost, stream));
+    }
     if (phase == 1) return 1;  // first round enqueued; the caller synchronises and resumes
     HIPC(hipStreamSynchronize(stream));
    }
-    resume = false;
     GridCtl h{};
-    memcpy(&h, hb, sizeof h);
-    count = hb[sizeof(GridCtl) / 4];
+    if (resume && hsum) {  // the first round's summary came back with the caller's readback
+      memcpy(&h, hsum, sizeof h);
+      count = (int64_t)(uint32_t)hsum[sizeof(GridCtl) / 8];
+    } else {
+      memcpy(&h, hb, sizeof h);
+      count = hb[sizeof(GridCtl) / 4];
+    }
+    resume = false;
     const uint32_t cnt = count > done ? (uint32_t)std::min<int64_t>(G, count - done) : 0u;
     if (gs) {
       gs->rows += h.logged;
