@@ -51,7 +51,7 @@ struct Ctl {
   // (= the earliest start), latest end, longest wave -- workgroup-reduced atomicMax on a zeroed block
   unsigned long long tmax8[8][16];
   InterpCtl ic;
-  uint64_t grid_sum[GRID_SUM_WORDS];  // the grid tier's first-round summary (k_grid_finish), read back with Ctl
+  alignas(256) uint64_t grid_sum[GRID_SUM_WORDS];  // the grid tier's first-round counters + list length (kg_grid.h)
 };
 
 // One device-scope atomic on a single word costs ~11 ns at the memory side and one word saturates

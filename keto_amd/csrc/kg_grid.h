@@ -10,8 +10,9 @@ struct GridStats {
   unsigned long long rows = 0, edges = 0, probes = 0, done = 0, logged = 0;
 };
 
-// The first round's counters and the list length, as k_grid_finish leaves them for the batch's one
-// readback (phase 1 with dsum: no readback of their own; phase 2 reads them from hsum, the host copy).
+// phase 1 with dsum (zeroed, 256-B aligned, GRID_SUM_WORDS): the first round keeps its counters there
+// and k_grid_finish adds the list length, so they come back with the caller's one readback and need
+// no memset or copy of their own; phase 2 reads them from hsum, the host copy.
 constexpr uint32_t GRID_SUM_WORDS = 160;
 
 struct Snapshot;

@@ -404,17 +404,13 @@ __global__ __launch_bounds__(256) void k_grid_level(DevSnap s, GridLog lg, int l
   if (lane == 0 && probes) atomicAdd(&ctl->probes8[blockIdx.x & 7][threadIdx.x >> 6], (unsigned long long)probes);
 }
 
-static_assert(sizeof(GridCtl) % 8 == 0 && sizeof(GridCtl) / 8 + 1 <= GRID_SUM_WORDS && sizeof(GridCtl) / 8 < 256,
-              "the round summary fits GRID_SUM_WORDS and one workgroup copies it");
+static_assert(sizeof(GridCtl) % 8 == 0 && sizeof(GridCtl) / 8 + 1 <= GRID_SUM_WORDS,
+              "a round's counters and the list length fit GRID_SUM_WORDS");
 __global__ void k_grid_finish(GridSlots sl, const uint32_t* d_count, uint32_t base, uint32_t G, uint8_t* out,
                               uint32_t* err, const GridCtl* ctl, uint64_t* sum) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  // the round's counters and the list length for the batch's single readback (see kg_grid.h)
-  if (sum && blockIdx.x == 0) {
-    constexpr uint32_t W = sizeof(GridCtl) / 8;
-    if (threadIdx.x < W) sum[threadIdx.x] = reinterpret_cast<const uint64_t*>(ctl)[threadIdx.x];
-    else if (threadIdx.x == W) sum[W] = *d_count;
-  }
+  // the list length next to the round's counters (which live in sum) for the batch's single readback
+  if (sum && i == 0) sum[sizeof(GridCtl) / 8] = *d_count;
   if (i >= round_slots(d_count, base, G) || ctl->overflow) return;
   const uint32_t qi = sl.q[i];
   out[qi] = sl.hit[i] == 1 ? KG_IS_MEMBER : KG_NOT_MEMBER;
@@ -437,7 +433,8 @@ struct GridView {  // pointers into a pool laid out for `cap` log entries (per d
   uint64_t* H = nullptr;
   GridLog lg{}, blg{};
   GridSlots sl{};
-  GridCtl* ctl = nullptr;
+  GridCtl* ctl = nullptr;       // the running round's counters
+  GridCtl* ctl_pool = nullptr;  // the pool's own block
 };
 
 // two: a backward log too (bidirectional rounds), and a visited table for both directions' nodes;
@@ -485,7 +482,7 @@ static int grid_layout(GridPool* P, uint64_t cap, hipStream_t stream, GridView* 
   v->sl.lastb = v->sl.lastf + G0;
   v->sl.bd = v->sl.lastb + G0;
   p += (size_t)G0 * 24;
-  v->ctl = (GridCtl*)(((uintptr_t)p + 255) & ~uintptr_t(255));
+  v->ctl = v->ctl_pool = (GridCtl*)(((uintptr_t)p + 255) & ~uintptr_t(255));
   return 0;
 }
 
@@ -552,7 +549,11 @@ int grid_tier(Snapshot* s, Workspace* w, const RQuery* rq, const uint32_t* qlist
     const int bidir = bidir_ok && gp != &s->giant ? 1 : 0;  // the full-size pool has no backward log
     const uint32_t slot_blocks = (G + 255) / 256;
     const uint32_t lgrid = (uint32_t)s->n_cu * s->grid_wgs;
-    HIPC(hipMemsetAsync(v.ctl, 0, sizeof(GridCtl), stream));
+    // the first round of a batch keeps its counters in the caller's zeroed Ctl (kg_grid.h), later
+    // rounds in the pool's own block
+    const bool fold = phase == 1 && dsum;
+    v.ctl = fold ? reinterpret_cast<GridCtl*>(dsum) : v.ctl_pool;
+    if (!fold) HIPC(hipMemsetAsync(v.ctl, 0, sizeof(GridCtl), stream));
     hipLaunchKernelGGL(k_grid_init, dim3(slot_blocks), dim3(256), 0, stream, s->ds, rq, qlist, d_count, done, G, v.lg,
                        v.blg, v.sl, v.H, v.hcap - 1, epoch, v.ctl, bidir ? hold_cap : 0u);
     HIPC(hipGetLastError());
@@ -578,7 +579,6 @@ int grid_tier(Snapshot* s, Workspace* w, const RQuery* rq, const uint32_t* qlist
         HIPC(hipGetLastError());
       }
     }
-    const bool fold = phase == 1 && dsum;  // the summary rides in the caller's readback
     hipLaunchKernelGGL(k_grid_finish, dim3(slot_blocks), dim3(256), 0, stream, v.sl, d_count, done, G, out, err, v.ctl,
                        fold ? dsum : nullptr);
     HIPC(hipGetLastError());
