@@ -97,8 +97,8 @@ def parse(argv=None):
                          "flight, best at --inflight 4: profiles/r2j_sweep.jsonl)")
     ap.add_argument("--back", type=int, default=2, help="kg_snapshot_tune back (1 backward tier wave+WG widths, 2 wave width only, 0 off)")
     ap.add_argument("--back-wgs", type=int, default=None,
-                    help="kg_snapshot_tune back_wgs (k_back WGs per CU; default 2 for C2/C4 with 4 batches in "
-                         "flight, 1 for C3 with 6: profiles/r2bw_back_wgs_ab.jsonl, r2bwc3_back_wgs_c3_ab.jsonl)")
+                    help="kg_snapshot_tune back_wgs (k_back WGs per CU; default 3 for C2/C4 with 4 batches in "
+                         "flight, 1 for C3 with 6: profiles/r4s_back_wgs_ab.jsonl, r2bwc3_back_wgs_c3_ab.jsonl)")
     ap.add_argument("--interp-wgs", type=int, default=6, help="kg_snapshot_tune interp_wgs (rewrite-path LDS pass WGs per CU)")
     ap.add_argument("--hw-queues", type=int, default=None,
                     help="HIP hardware queues for this process (GPU_MAX_HW_QUEUES, 1..32; 0 = HIP's default, 4; "
@@ -155,7 +155,7 @@ def parse(argv=None):
     if a.inflight is None:
         a.inflight = 16 if a.mode == "expand" else 4
     if a.back_wgs is None:
-        a.back_wgs = 1 if a.preset else 2
+        a.back_wgs = 1 if a.preset else 3
     if a.tuples is None:
         a.tuples = 1.2e8 if a.heavy_tail else (1e7 if a.mode == "refresh" else 1e9)
     return a

@@ -273,7 +273,10 @@ struct Snapshot {
   int stream_wgs = 3;        // kg_snapshot_tune("stream_wgs"): k_stream4 workgroups per CU (3 leaves LDS to other batches)
   int interp_wgs = 6;        // kg_snapshot_tune("interp_wgs"): k_interp_lds workgroups (4 waves) per CU (6 fit the LDS)
   uint32_t interp_cap2 = 0;  // kg_snapshot_tune("interp_cap2"): pass-2 BFS list cap of the rewrite path (0 = 256 Ki)
-  int back_wgs = 2;          // kg_snapshot_tune("back_wgs"): k_back workgroups per CU (1..3, LDS allows 3; C3 prefers 1)
+  // k_back workgroups per CU (1..3, LDS allows 3; C3 prefers 1).  3: one wave per query for up to 3 Ki
+  // hand-ons (C2 hands on ~2.2 k per 1 M batch: at 2, ~170 of them waited for a second pass on a
+  // freed wave; 6.3 -> 6.8 x 10^9 checks/s, profiles/r4s_back_wgs_ab.jsonl)
+  int back_wgs = 3;          // kg_snapshot_tune("back_wgs")
   uint64_t grid_small_cap = 0;  // kg_snapshot_tune("grid_cap"): workspace grid-log entries (0 = 16 Mi; tests)
   int expand_tail = 1;  // kg_snapshot_tune("expand_tail"): expand passes 2/3 walk with LDS-cached frames (0: round 2)
   int grid_ms = 1;  // kg_snapshot_tune("grid_ms"): grid-tier queries as MS-BFS when the dense masks fit (0: off)

@@ -15,7 +15,7 @@ class _FakeSnap:
 
 def test_defaults_and_tune_set():
     a = bench.parse([])
-    assert a.gpus == 1 and a.inflight == 4 and a.back_wgs == 2 and a.tuples == 1e9
+    assert a.gpus == 1 and a.inflight == 4 and a.back_wgs == 3 and a.tuples == 1e9
     assert a.parity >= 1_000_000 and a.latency_batches >= 200
     s = _FakeSnap()
     bench.apply_tune(s, a)

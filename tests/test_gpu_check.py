@@ -593,7 +593,7 @@ def test_bench_tune_set_vs_oracle(preset, n_tuples):
     a = bench.parse(["--preset", str(preset)])
     snap = Snapshot.synthetic(n_tuples, seed=20250131, preset=preset)
     bench.apply_tune(snap, a)
-    assert snap.tuned["back_wgs"] == (1 if preset else 2) and snap.tuned["stream_steal"] == 4
+    assert snap.tuned["back_wgs"] == (1 if preset else 3) and snap.tuned["stream_steal"] == 4
     P, n, gmax = a.inflight, 50_000, a.global_depth
     streams = [torch.cuda.Stream() for _ in range(P)]
     dqs = []
