@@ -99,6 +99,8 @@ def parse(argv=None):
     ap.add_argument("--back-wgs", type=int, default=None,
                     help="kg_snapshot_tune back_wgs (k_back WGs per CU; default 3 for C2/C4 with 4 batches in "
                          "flight, 1 for C3 with 6: profiles/r4s_back_wgs_ab.jsonl, r2bwc3_back_wgs_c3_ab.jsonl)")
+    ap.add_argument("--back-edges", type=int, default=0,
+                    help="kg_snapshot_tune back_edges (k_back reverse-edge budget per query, 0 = library default 2^12)")
     ap.add_argument("--interp-wgs", type=int, default=6, help="kg_snapshot_tune interp_wgs (rewrite-path LDS pass WGs per CU)")
     ap.add_argument("--hw-queues", type=int, default=None,
                     help="HIP hardware queues for this process (GPU_MAX_HW_QUEUES, 1..32; 0 = HIP's default, 4; "
@@ -181,6 +183,8 @@ def apply_tune(snap, a) -> None:
         snap.tune("grid_ms_bytes", int(a.grid_ms_bytes))
     snap.tune("stream_wgs", a.stream_wgs)
     snap.tune("back_wgs", a.back_wgs)
+    if a.back_edges:
+        snap.tune("back_edges", a.back_edges)
     snap.tune("grid_reserve", 1)  # a server pays this once at start-up, not inside some request's batch
     if snap.program is not None and not snap.program.empty:
         snap.tune("interp_wgs", a.interp_wgs)

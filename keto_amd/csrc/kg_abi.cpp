@@ -544,6 +544,11 @@ static int tune_one(Snapshot* s, const char* key, int64_t value) {
     s->lane_cv.notify_all();
     return 0;
   }
+  if (strcmp(key, "back_edges") == 0) {
+    if (value < 0 || value > (1 << 20)) return set_error(-2, "back_edges must be in [0, 2^20]");
+    s->back_edges = (uint32_t)value;
+    return 0;
+  }
   if (strcmp(key, "back_wgs") == 0) {
     if (value < 1 || value > 3) return set_error(-2, "back_wgs must be in [1, 3]");
     s->back_wgs = (int)value;

@@ -596,10 +596,13 @@ struct BackCfg;
 // EDGES: reverse edges one query may read here.  A level that reaches hub groups reads their whole
 // parent lists (up to 1e5 each) on one wave -- 28 ms for one query at 1 B tuples before this bound
 // (profiles/r2o_*): such a query goes to the grid tier, which spreads its edges over the whole GPU.
+// The launch lasts as long as its longest query and the grid tier runs for the hand-ons anyway, so
+// the bound is low: 2^14 -> 2^12 took C2 from 6.8 to 7.0-7.2 x 10^9 checks/s
+// (profiles/r4t_back_edges_ecap_sweep.jsonl, r4u_back_edges_sweep.jsonl; 2^10-2^11 and 2^15 slower).
 template <>
 struct BackCfg<64> {
   static constexpr uint32_t VLOG2 = 9, CAP = 256;  // larger caps only lengthen the tail (1024: -9 % checks/s)
-  static constexpr uint32_t EDGES = 1u << 14;
+  static constexpr uint32_t EDGES = 1u << 12;
 };
 template <>
 struct BackCfg<256> {
@@ -658,7 +661,7 @@ template <int W>
 __global__ __launch_bounds__(256) void k_back(DevSnap s, const RQuery* __restrict__ rq, const uint32_t* qlist,
                                               const uint32_t* qcount_p, uint32_t* qhead, uint8_t* __restrict__ out,
                                               uint32_t* __restrict__ err, uint32_t* next_list, uint32_t* next_count,
-                                              Ctl* ctl) {
+                                              Ctl* ctl, uint32_t edges) {
   constexpr uint32_t VSLOTS = BackLds<W>::VSLOTS, CAP = BackLds<W>::CAP;
   constexpr int BU = 4;
   __shared__ BackLds<W> lds_all[256 / W];
@@ -699,7 +702,7 @@ __global__ __launch_bounds__(256) void k_back(DevSnap s, const RQuery* __restric
     }
     bk_sync<W>();
     uint32_t lvl_b = 0, lvl_e = L.n;
-    uint32_t budget = BackCfg<W>::EDGES;  // wave-uniform
+    uint32_t budget = edges ? edges : BackCfg<W>::EDGES;  // wave-uniform
     for (int j = 1; j <= q.depth - 1 && lvl_b < lvl_e && !L.hit && !L.over; j++) {
       const bool keep = j < q.depth - 1;  // parents found here can still be expanded
       for (uint32_t base = lvl_b; base < lvl_e; base += W) {
@@ -934,14 +937,15 @@ int check_batch_begin(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n, 
         // wave per query (~48 KiB LDS per workgroup: 3 per CU), its overflow to the workgroup-per-query
         // width (~52 KiB: 3 per CU), whose overflow goes to the grid tier
         hipLaunchKernelGGL(k_back<64>, dim3((uint32_t)s->n_cu * s->back_wgs), dim3(256), 0, stream, s->ds, rq, heavy,
-                           &ctl->heavy_count, &ctl->back_head, d_out, d_err, back2, &ctl->back2_count, ctl);
+                           &ctl->heavy_count, &ctl->back_head, d_out, d_err, back2, &ctl->back2_count, ctl,
+                           (uint32_t)s->back_edges);
         HIPC(hipGetLastError());
         if (s->back_tier == 2) {  // wave width only: its overflow goes straight to the grid tier
           fwd_list = back2;
           fwd_count = &ctl->back2_count;
         } else {
           hipLaunchKernelGGL(k_back<256>, dim3((uint32_t)s->n_cu * s->back_wgs), dim3(256), 0, stream, s->ds, rq, back2,
-                             &ctl->back2_count, &ctl->back2_head, d_out, d_err, giant, &ctl->fwd_count, ctl);
+                             &ctl->back2_count, &ctl->back2_head, d_out, d_err, giant, &ctl->fwd_count, ctl, 0u);
           HIPC(hipGetLastError());
           fwd_list = giant;
           fwd_count = &ctl->fwd_count;

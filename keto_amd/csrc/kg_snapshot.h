@@ -277,6 +277,7 @@ struct Snapshot {
   // hand-ons (C2 hands on ~2.2 k per 1 M batch: at 2, ~170 of them waited for a second pass on a
   // freed wave; 6.3 -> 6.8 x 10^9 checks/s, profiles/r4s_back_wgs_ab.jsonl)
   int back_wgs = 3;          // kg_snapshot_tune("back_wgs")
+  uint32_t back_edges = 0;   // kg_snapshot_tune("back_edges"): k_back<64>'s reverse-edge budget per query (0 = 2^12)
   uint64_t grid_small_cap = 0;  // kg_snapshot_tune("grid_cap"): workspace grid-log entries (0 = 16 Mi; tests)
   int expand_tail = 1;  // kg_snapshot_tune("expand_tail"): expand passes 2/3 walk with LDS-cached frames (0: round 2)
   int grid_ms = 1;  // kg_snapshot_tune("grid_ms"): grid-tier queries as MS-BFS when the dense masks fit (0: off)
