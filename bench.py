@@ -79,7 +79,9 @@ def parse(argv=None):
                     help="kg_snapshot_tune stream_steal (XCD ranges a k_stream4 wave dequeues from, 1..8)")
     ap.add_argument("--stream-chunk", type=int, default=64,
                     help="kg_snapshot_tune stream_chunk (k_stream4 queries per dequeue, 1..64)")
-    ap.add_argument("--grid-wgs", type=int, default=4, help="kg_snapshot_tune grid_wgs (k_grid_level WGs per CU)")
+    ap.add_argument("--grid-wgs", type=int, default=None,
+                    help="kg_snapshot_tune grid_wgs (k_grid_level WGs per CU; default 2 for C2/C4, 4 for C3: "
+                         "profiles/r4w_grid_stream_wgs_ab.jsonl)")
     ap.add_argument("--grid-ms", type=int, default=1,
                     help="kg_snapshot_tune grid_ms: the grid tier's queries as a multi-source bit-parallel BFS "
                          "(64 queries per group) when dense per-node masks fit (graphs up to ~4 M nodes)")
@@ -92,9 +94,9 @@ def parse(argv=None):
     ap.add_argument("--grid-bidir", type=int, default=0,
                     help="kg_snapshot_tune grid_bidir: grid slots whose subject has <= this many holders "
                          "alternate forward and backward turns (0: forward only)")
-    ap.add_argument("--stream-wgs", type=int, default=3,
-                    help="kg_snapshot_tune stream_wgs (k_stream4 WGs per CU; 3 leaves LDS to the other batches in "
-                         "flight, best at --inflight 4: profiles/r2j_sweep.jsonl)")
+    ap.add_argument("--stream-wgs", type=int, default=None,
+                    help="kg_snapshot_tune stream_wgs (k_stream4 WGs per CU; default 2 for C2/C4 -- LDS left to the "
+                         "other batches' tail tiers, profiles/r4w_grid_stream_wgs_ab.jsonl -- and 3 for C3)")
     ap.add_argument("--back", type=int, default=2, help="kg_snapshot_tune back (1 backward tier wave+WG widths, 2 wave width only, 0 off)")
     ap.add_argument("--back-wgs", type=int, default=None,
                     help="kg_snapshot_tune back_wgs (k_back WGs per CU; default 3 for C2/C4 with 4 batches in "
@@ -158,6 +160,10 @@ def parse(argv=None):
         a.inflight = 16 if a.mode == "expand" else 4
     if a.back_wgs is None:
         a.back_wgs = 1 if a.preset else 3
+    if a.grid_wgs is None:
+        a.grid_wgs = 4 if a.preset else 2
+    if a.stream_wgs is None:
+        a.stream_wgs = 3 if a.preset else 2
     if a.tuples is None:
         a.tuples = 1.2e8 if a.heavy_tail else (1e7 if a.mode == "refresh" else 1e9)
     return a

@@ -218,8 +218,8 @@ int kg_snapshot_materialized(const kg_snapshot* s, uint64_t* out3);
  * key "stream_steal" (1..8): XCD ranges of the work list a k_stream4 wave dequeues from (default 4:
  * when the list drains every wave walks them, one atomic each on a few hot words).
  * key "stream_chunk" (1..64): queries a k_stream4 wave dequeues at once (default 64).
- * key "stream_wgs": k_stream4 workgroups per CU (0 = 3; default 3); "back_wgs" (1..3, default 3), "back_edges" (reverse edges one backward-tier query may read, 0 = 2^12)
- * and "grid_wgs" (1..64, default 4): k_back / k_grid_level workgroups per CU (defaults = bench.py's C2 set).  key "shard_vis": log2 of the
+ * key "stream_wgs": k_stream4 workgroups per CU (0 = 2; default 2); "back_wgs" (1..3, default 3), "back_edges" (reverse edges one backward-tier query may read, 0 = 2^12)
+ * and "grid_wgs" (1..64, default 2): k_back / k_grid_level workgroups per CU (defaults = bench.py's C2 set).  key "shard_vis": log2 of the
  * hash-sharded mode's per-batch (query, node) visited table (default 25).  key "interp_cap2"
  * (0..4194304): BFS list cap of the rewrite interpreter's many-slot HBM pass (0 = 256 Ki nodes);
  * queries that outgrow it rerun in the single full-size slot.  key "interp_wgs" (1..8): workgroups

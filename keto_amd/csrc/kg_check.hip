@@ -916,8 +916,8 @@ int check_batch_begin(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n, 
     if (stats) HIPC(hipEventRecord(l0, stream));
     {
       // ~32 KiB of LDS per workgroup (4 waves: a 512-key visited cache and a 256-entry FIFO each);
-      // stream_wgs per CU (3 leaves LDS to the other batches in flight)
-      const uint32_t per_cu = s->stream_wgs ? (uint32_t)s->stream_wgs : 3u;
+      // stream_wgs per CU (default 2: the rest of the LDS serves the other batches in flight)
+      const uint32_t per_cu = s->stream_wgs ? (uint32_t)s->stream_wgs : 2u;
       const uint32_t ecap = s->stream_ecap ? s->stream_ecap : 0xFFFFFFFFu;
       // >= 8 workgroups: with stream_steal < 8 a wave drains only `ranges` of the 8 per-XCD ranges
       // starting at its label blockIdx & 7, so every label must occur for every range to be drained

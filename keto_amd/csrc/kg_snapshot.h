@@ -267,10 +267,13 @@ struct Snapshot {
   // Occupancy defaults (library-wide, measured with several batches in flight, the way a server keeps
   // them: C2 and C3 A/Bs in profiles/r2gw_tier_wgs_sweep.jsonl, r2v_occupancy_sweep.jsonl,
   // r2bw_back_wgs_ab.jsonl; a one-batch-at-a-time caller loses < 5 % with them)
-  int grid_wgs = 4;          // kg_snapshot_tune("grid_wgs"): k_grid_level workgroups per CU
+  // C2 (round 4, profiles/r4w_grid_stream_wgs_ab.jsonl): k_grid_level 2 and k_stream4 2 workgroups per CU
+  // (the LDS a third stream workgroup held now serves the other batches' tail tiers): 7.00 -> 7.20 x 10^9;
+  // C3 keeps 4 / 3 through bench.py
+  int grid_wgs = 2;          // kg_snapshot_tune("grid_wgs"): k_grid_level workgroups per CU
   int device_sync = 1;      // kg_snapshot_tune("device_sync"): kg_check_batch_device waits asleep (1) or spinning (0)
   int host_sync = 1;        // kg_snapshot_tune("host_sync"): kg_check_batch waits asleep (1) or spinning (0)
-  int stream_wgs = 3;        // kg_snapshot_tune("stream_wgs"): k_stream4 workgroups per CU (3 leaves LDS to other batches)
+  int stream_wgs = 2;        // kg_snapshot_tune("stream_wgs"): k_stream4 workgroups per CU (LDS left to other batches)
   int interp_wgs = 6;        // kg_snapshot_tune("interp_wgs"): k_interp_lds workgroups (4 waves) per CU (6 fit the LDS)
   uint32_t interp_cap2 = 0;  // kg_snapshot_tune("interp_cap2"): pass-2 BFS list cap of the rewrite path (0 = 256 Ki)
   // k_back workgroups per CU (1..3, LDS allows 3; C3 prefers 1).  3: one wave per query for up to 3 Ki

@@ -23,7 +23,8 @@ def test_defaults_and_tune_set():
               "device_sync"):
         assert k in s.tuned, k
     c3 = bench.parse(["--preset", "1"])
-    assert c3.back_wgs == 1
+    assert c3.back_wgs == 1 and c3.grid_wgs == 4 and c3.stream_wgs == 3
+    assert a.grid_wgs == 2 and a.stream_wgs == 2
     assert bench.parse(["--heavy-tail"]).tuples >= 1e8
 
 
