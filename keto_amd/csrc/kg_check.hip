@@ -198,7 +198,7 @@ __global__ __launch_bounds__(256) void k_resolve(DevSnap s, const kg_query* __re
         rb = v.beg;
         rl = v.len;
         rsig = v.sig;
-        rsig_lo = (uint32_t)v.pad1;  // signature bits 0-15 in bits 16-31
+        rsig_lo = (uint32_t)v.pad1;  // signature bits 0-11 in bits 20-31
         nfl = (uint32_t)(v.pad1 & 0xFFu);
       }
     }

@@ -110,35 +110,38 @@ struct RwNode {
 };
 enum { RW_OR = 0, RW_AND = 1, RW_COMPUTED = 2, RW_TTU = 3, RW_NOT = 4 };
 
-// Bloom signature of a node's direct subjects (its full row): 48 bits, 2 per subject.  A
+// Bloom signature of a node's direct subjects (its full row): 44 bits, 2 per subject.  A
 // checkDirect probe whose subject bits are not all present is a certain miss and is skipped.  The
-// bits sit in two words as they are stored: x = signature bits 0-15 in bits 16-31 (bits 0-15 hold
-// the carrier's own low field: AdjX's row length, NSlot's flags), y = signature bits 16-47.
-// (Round 3 had 32 bits: a row of 20 subjects passed 52 % of absent subjects, now 32 %.)
-constexpr uint32_t SIG_LO = 0xFFFF0000u;
+// bits sit in two words as they are stored: x = signature bits 0-11 in bits 20-31 (bits 0-19 hold
+// the carrier's own low field: AdjX's row length, NSlot's flags), y = signature bits 12-43.
+// (Round 3 had 32 bits: a row of 20 subjects passed 52 % of absent subjects, now 36 %.)
+constexpr uint32_t SIG_LO = 0xFFF00000u;
 __host__ __device__ __forceinline__ uint2 subj_sig(uint32_t subj) {
   uint32_t h = subj * 0x9E3779B1u;
   h ^= h >> 15;
   h *= 0x85EBCA77u;
   h ^= h >> 13;
-  const uint32_t p0 = ((h & 0xFFFFu) * 48u) >> 16, p1 = ((h >> 16) * 48u) >> 16;  // two positions in [0, 48)
+  const uint32_t p0 = ((h & 0xFFFFu) * 44u) >> 16, p1 = ((h >> 16) * 44u) >> 16;  // two positions in [0, 44)
   uint2 m = make_uint2(0u, 0u);
-  if (p0 < 16) m.x |= 1u << (16 + p0);
-  else m.y |= 1u << (p0 - 16);
-  if (p1 < 16) m.x |= 1u << (16 + p1);
-  else m.y |= 1u << (p1 - 16);
+  if (p0 < 12) m.x |= 1u << (20 + p0);
+  else m.y |= 1u << (p0 - 12);
+  if (p1 < 12) m.x |= 1u << (20 + p1);
+  else m.y |= 1u << (p1 - 12);
   return m;
 }
-// sig_lo: a word whose bits 16-31 are signature bits 0-15 (its low half is ignored), sig_hi: bits 16-47
+// sig_lo: a word whose bits 20-31 are signature bits 0-11 (bits 0-19 are ignored), sig_hi: bits 12-43
 __host__ __device__ __forceinline__ bool sig_maybe(uint32_t sig_lo, uint32_t sig_hi, uint2 m) {
   return ((sig_lo & m.x) == m.x) & ((sig_hi & m.y) == m.y);
 }
 
 // One set-adjacency edge with the child's own set row inlined (begin / length) and the child's
 // signature: a BFS level needs one dependent HBM round trip instead of two (no adj_off lookup per
-// discovered node).  lsig: the row length in bits 0-15 (ADJX_LEN_SAT = 65535 or longer: read
-// adj_off, adjx_len) and signature bits 0-15 in bits 16-31; sig: signature bits 16-47.
-constexpr uint32_t ADJX_LEN_SAT = 0xFFFFu;
+// discovered node).  lsig: the row length in bits 0-19 (ADJX_LEN_SAT = 2^20 - 1 or longer: read
+// adj_off, adjx_len) and signature bits 0-11 in bits 20-31; sig: signature bits 12-43.  20 bits keep
+// hub rows exact (the heavy-tail point's 10^5-edge rows: a 16-bit length sent every edge into a hub
+// through an extra dependent adj_off read in the grid tiers, -12 % checks/s there,
+// profiles/r4bis_heavy_tail_bisect.jsonl).
+constexpr uint32_t ADJX_LEN_SAT = 0xFFFFFu;
 struct AdjX {
   uint32_t node, begin, lsig, sig;
 };
@@ -150,7 +153,7 @@ struct NSlot {
   uint64_t key;
   uint32_t node, beg, len;
   uint32_t sig;  // signature bits 16-47 of the node's row subjects (as AdjX.sig): k_resolve's root probe filter
-  uint64_t pad1;  // low byte: the node's flags (nflags; 0 without a namespace program); bits 16-31: signature bits 0-15
+  uint64_t pad1;  // low byte: the node's flags (nflags; 0 without a namespace program); bits 20-31: signature bits 0-11
 };
 // Holder-hash slot: tagged subject -> hold[first, first + count).  key == NONE: free.
 struct HSlot {

@@ -257,8 +257,10 @@ __device__ __forceinline__ void ms_edge(const DevSnap& s, const MsView& v, uint3
   }
 }
 
+// (256, 5): at least 5 waves per SIMD -- at 97 VGPRs the level ran 4 and the heavy-tail point lost 12 %
+// (profiles/r4bis_heavy_tail_bisect.jsonl)
 template <int K>
-__global__ __launch_bounds__(256) void k_ms_level(DevSnap s, MsView v, int L, int cur) {
+__global__ __launch_bounds__(256, 5) void k_ms_level(DevSnap s, MsView v, int L, int cur) {
   constexpr uint32_t TE = ms_tile_edges(K);
   __shared__ uint64_t s_beg[TE + 2], s_f[TE + 2][K], s_pm[TE + 2][K], s_em[TE + 2][K], s_many[TE + 2][K];
   __shared__ uint32_t s_g[TE + 2], s_rb[TE + 2];
@@ -458,7 +460,9 @@ int ms_rounds(Snapshot* s, Workspace* w, const RQuery* rq, const uint32_t* qlist
   v.tg_cap = s->grid_ms_tg_cap;
   if (int rc = ms_layout(gp, n, K, G, std::min<uint64_t>(cap, (uint64_t)G * n + 1024), &v)) return rc;
   const int levels = std::max(0, global_max_depth - 1);  // level L expands hop L (D - 2 >= L)
-  const uint32_t lgrid = (uint32_t)s->n_cu * s->grid_wgs;
+  // at least 4 workgroups per CU: an MS-BFS level walks whole hub layers (the per-query grid tier's few
+  // edges per level prefer grid_wgs = 2; the heavy-tail point lost 12 % at 2, profiles/r4h2_heavy_knobs_ab.jsonl)
+  const uint32_t lgrid = (uint32_t)s->n_cu * (uint32_t)std::max(4, s->grid_wgs);
   int64_t count = -1;
   bool resume = phase == 2;
   for (uint32_t done = 0; count < 0 || done < (uint64_t)count;) {

@@ -288,7 +288,7 @@ __device__ __forceinline__ SeedQ seed_query(const DevSnap& s, const kg_query* __
     if (sl) {
       node = sl->node;
       rsig = sl->sig;
-      rsig_lo = (uint32_t)sl->pad1;  // signature bits 0-15 in bits 16-31
+      rsig_lo = (uint32_t)sl->pad1;  // signature bits 0-11 in bits 20-31
       rlen = sl->len;
     }
   }
