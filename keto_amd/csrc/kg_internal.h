@@ -138,9 +138,8 @@ __host__ __device__ __forceinline__ bool sig_maybe(uint32_t sig_lo, uint32_t sig
 // signature: a BFS level needs one dependent HBM round trip instead of two (no adj_off lookup per
 // discovered node).  lsig: the row length in bits 0-19 (ADJX_LEN_SAT = 2^20 - 1 or longer: read
 // adj_off, adjx_len) and signature bits 0-11 in bits 20-31; sig: signature bits 12-43.  20 bits keep
-// hub rows exact (the heavy-tail point's 10^5-edge rows: a 16-bit length sent every edge into a hub
-// through an extra dependent adj_off read in the grid tiers, -12 % checks/s there,
-// profiles/r4bis_heavy_tail_bisect.jsonl).
+// hub rows exact (the heavy-tail point's 10^5-edge rows would otherwise cost every edge into a hub
+// a dependent adj_off read in the grid tiers).
 constexpr uint32_t ADJX_LEN_SAT = 0xFFFFFu;
 struct AdjX {
   uint32_t node, begin, lsig, sig;
