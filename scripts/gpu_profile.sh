@@ -16,12 +16,12 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG} -o 
 [ $rc -eq 0 ] || exit $rc
 python3 scripts/timeline.py gpurun_out/prof_${TAG}/run_kernel_trace.csv > gpurun_out/timeline_${TAG}.txt || true
 B="python3 bench.py --steps 4 --warmup 2 --cpu-seconds 0 --parity 0 --latency-batches 0 --host-calls 0 $EXTRA"
-RX="k_stream2|k_stream4|k_resolve|k_back|k_grid_level|k_fsplit"
+RX="k_stream4|k_resolve|k_back|k_grid_level|k_fsplit"
 timeout -s KILL 150 rocprofv3 --kernel-include-regex "$RX" --pmc FETCH_SIZE -d gpurun_out/pmc_${TAG}_fetch -o run --output-format csv -- $B > gpurun_out/pmc_${TAG}_fetch.log 2>&1; rc=$?; echo "fetch rc=$rc"
 [ $rc -eq 0 ] || exit $rc
 timeout -s KILL 150 rocprofv3 --kernel-include-regex "$RX" --pmc WRITE_SIZE -d gpurun_out/pmc_${TAG}_write -o run --output-format csv -- $B > gpurun_out/pmc_${TAG}_write.log 2>&1; rc=$?; echo "write rc=$rc"
 [ $rc -eq 0 ] || exit $rc
-for K in k_stream2 k_stream4 k_resolve k_back; do
+for K in k_stream4 k_resolve k_back; do
   python3 scripts/pmc_summary.py --kernel $K --fetch gpurun_out/pmc_${TAG}_fetch --write gpurun_out/pmc_${TAG}_write --tuples $TUPLES --batch 1000000 --preset $PRESET --inflight $INFLIGHT --out profiles/pmc_${K}_p${PRESET}.json > /dev/null || true
 done
 cp profiles/pmc_k_*_p${PRESET}.json gpurun_out/ 2>/dev/null || true  # the bench below reads them; copied back for committing

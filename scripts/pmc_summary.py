@@ -7,8 +7,8 @@ FETCH_SIZE tallies 128-byte memory-side read requests at 64 bytes.  Our reads ar
 gathers, a width the guide leaves uncalibrated; the same correction is applied and the raw values
 are kept next to the corrected figure.
 
-usage: python scripts/pmc_summary.py --kernel k_stream2 --fetch DIR1 --write DIR2 --tuples T --batch B
-       [--preset P --inflight I] [--out profiles/pmc_k_stream2_p0.json]
+usage: python scripts/pmc_summary.py --kernel k_stream4 --fetch DIR1 --write DIR2 --tuples T --batch B
+       [--preset P --inflight I] [--out profiles/pmc_k_stream4_p0.json]
 """
 import argparse
 import csv
