@@ -849,12 +849,17 @@ def main():
     import torch
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    n_dev = max(1, torch.cuda.device_count())
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one rank per GPU over RCCL; more ranks than GPUs (a rehearsal of the N-rank launch on a smaller
+    # box) share GPUs and aggregate over gloo -- RCCL takes one rank per GPU
+    backend = "nccl" if world <= n_dev else "gloo"
+    local %= n_dev
     dist = None
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", rank=rank, world_size=world)
+        dist.init_process_group(backend, rank=rank, world_size=world)
     torch.cuda.set_device(local)
 
     from keto_amd import _lib
@@ -950,7 +955,7 @@ def main():
     assert (errs == 0).all() and (res <= 1).all(), "unexpected errors in the synthetic batch"
     stats = [x for x in stats if x is not None]
     elapsed, edges = aggregate(dist, elapsed, float(sum(s.edges_read for s in stats)) * a.steps / len(stats),
-                               f"cuda:{local}")
+                               f"cuda:{local}" if backend == "nccl" else None)
     l_bytes = np.array([8 * s.light_rows_opened + 4 * s.light_edges_read + 16 * s.light_probes for s in stats], float)
     l_reqs = np.array([s.light_rows_opened + s.light_probes for s in stats], float)
     l_ms = np.array([s.light_ms for s in stats], float)
