@@ -214,6 +214,32 @@ def test_synthetic_graph_vs_oracle(n_tuples, gmax, ecap, unheld):
     assert (dfs == exp).all()
 
 
+@pytest.mark.parametrize("back_edges,back_wgs", [(32, 3), (4096, 1), (1 << 16, 2)])
+def test_backward_budget_vs_oracle(back_edges, back_wgs):
+    """The backward tier's reverse-edge budget (kg_snapshot_tune back_edges; default 2^12) and its
+    workgroup count: a tiny budget hands most backward walks on to the grid tier, a large one keeps
+    hub-heavy ones in the wave; one workgroup per CU makes waves take a second query.  Answers equal
+    the oracle's whatever tier finishes a query."""
+    torch = _torch()
+    from keto_amd import _lib
+    snap = Snapshot.synthetic(300_000, seed=20250131)
+    snap.tune("stream_ecap", 32)  # most long walks leave the stream tier
+    snap.tune("back_edges", back_edges)
+    snap.tune("back_wgs", back_wgs)
+    n = 20000
+    dq = torch.empty((n, 7), dtype=torch.int32, device="cuda")
+    _lib.check(_lib.load().kg_synth_queries(snap.handle, 11, n, dq.data_ptr()), "kg_synth_queries")
+    q = dq.cpu().numpy().view(np.uint32)
+    e = Engine(snap, Config(10))
+    out, err = e.batch_check_ids(q, with_stats=True)
+    assert (err == 0).all()
+    exp, _, _ = Oracle(snap.export(), 0).check_batch(q[:, :6], q[:, 6].view(np.int32), 10, POLICY_CANONICAL,
+                                                     nthreads=8)
+    assert (out == exp).all(), np.nonzero(out != exp)[0][:10]
+    st = e.last_stats
+    assert st["n_back"] > 0 and st["n_heavy"] + st["n_back"] > 0, st
+
+
 @pytest.mark.parametrize("n,mat", [(2049, 0), (2304, 1), (4352, 0), (6100, 1), (2305, 0)])
 def test_small_batches_mixed_routes_vs_oracle(n, mat, monkeypatch):
     """Batches just past a multiple of 2048 queries: the stream tier's work list has 8 shards of
