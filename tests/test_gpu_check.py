@@ -214,6 +214,29 @@ def test_synthetic_graph_vs_oracle(n_tuples, gmax, ecap, unheld):
     assert (dfs == exp).all()
 
 
+@pytest.mark.parametrize("stream_wgs,grid_wgs", [(1, 1), (3, 8)])
+def test_occupancy_knobs_vs_oracle(stream_wgs, grid_wgs):
+    """k_stream4 / k_grid_level workgroups per CU (defaults 2 / 2): fewer or more waves draining the
+    stream tier's per-XCD work lists and spreading a grid level, the same answers."""
+    torch = _torch()
+    from keto_amd import _lib
+    snap = Snapshot.synthetic(300_000, seed=20250131)
+    snap.tune("stream_wgs", stream_wgs)
+    snap.tune("grid_wgs", grid_wgs)
+    snap.tune("stream_ecap", 64)
+    snap.tune("grid_ms", 0)  # the per-query grid rounds (the MS-BFS tier takes >= 4 workgroups per CU)
+    n = 20000
+    dq = torch.empty((n, 7), dtype=torch.int32, device="cuda")
+    _lib.check(_lib.load().kg_synth_queries(snap.handle, 23, n, dq.data_ptr()), "kg_synth_queries")
+    q = dq.cpu().numpy().view(np.uint32)
+    e = Engine(snap, Config(10))
+    out, err = e.batch_check_ids(q, with_stats=True)
+    assert (err == 0).all()
+    exp, _, _ = Oracle(snap.export(), 0).check_batch(q[:, :6], q[:, 6].view(np.int32), 10, POLICY_CANONICAL,
+                                                     nthreads=8)
+    assert (out == exp).all(), np.nonzero(out != exp)[0][:10]
+
+
 @pytest.mark.parametrize("back_edges,back_wgs", [(32, 3), (4096, 1), (1 << 16, 2)])
 def test_backward_budget_vs_oracle(back_edges, back_wgs):
     """The backward tier's reverse-edge budget (kg_snapshot_tune back_edges; default 2^12) and its
