@@ -485,7 +485,7 @@ __global__ __launch_bounds__(256) void k_shard_level(DevSnap s, const kg_frec* _
                                                      HeavyList heavy,
                                                      uint32_t* qcnt, uint32_t budget, uint32_t lossy, uint32_t n_seg,
                                                      uint64_t seg_cap, uint32_t heavy_min, uint32_t out_sub,
-                                                     uint32_t pack) {
+                                                     uint32_t pack, uint32_t res_done) {
   __shared__ uint32_t s_pref[256], s_wsum[4];
   __shared__ uint64_t s_rb[256];
   __shared__ kg_frec s_rec[256];
@@ -539,6 +539,9 @@ __global__ __launch_bounds__(256) void k_shard_level(DevSnap s, const kg_frec* _
       } else if (done && ((r.q & Q_MASK) >> 5) < done_wpr &&
                  ((done[(size_t)(r.q >> Q_BITS) * done_wpr + ((r.q & Q_MASK) >> 5)] >> (r.q & 31)) & 1u)) {
         // answered IsMember by an earlier level: nothing more to do for this query
+      } else if (res_done && (r.q >> Q_BITS) == me && res[r.q & Q_MASK] == KG_IS_MEMBER) {
+        // the same read from the results themselves (one rank: every query is this rank's; a result
+        // set by this very level only prunes earlier)
       } else {
         // the probe's first dset bucket and the node's set-row bounds are loaded before the visited
         // insert returns (all three in one round trip; a node already visited just ignores them)
@@ -799,10 +802,17 @@ __global__ __launch_bounds__(256) void k_shard_back_level(DevSnap s, const kg_fr
 // tile's rows staged in LDS.
 __global__ __launch_bounds__(256) void k_shard_heavy(DevSnap s, HeavyList heavy, kg_frec* out, uint64_t cap,
                                                      uint32_t* counts, uint8_t* res, uint32_t* err, uint32_t nranks,
-                                                     uint32_t out_sub, uint32_t pack) {
+                                                     uint32_t out_sub, uint32_t pack, uint32_t* zero_counts,
+                                                     uint32_t zero_n, unsigned long long* zero_pk) {
   static_assert(HEAVY_TILE == 256, "one edge per thread");
   __shared__ uint32_t s_r0;
   __shared__ uint64_t s_e0[HEAVY_TILE + 1];
+  // kg_shard_levels: the next level's bucket counters and hub-list counter, free since the level
+  // before this one read them (what a separate k_shard_prep launch per level did)
+  if (blockIdx.x == 0) {
+    if (zero_counts && threadIdx.x < zero_n) zero_counts[threadIdx.x] = 0;
+    if (zero_pk && threadIdx.x == 0) *zero_pk = 0;
+  }
   const uint32_t nh = (uint32_t)min((unsigned long long)heavy.cap, *heavy.pk >> HEAVY_EDGE_BITS), me = s.shard_rank;
   if (nh == 0) return;
   const HeavyRow last = heavy.rows[nh - 1];
@@ -1056,10 +1066,10 @@ int shard_level(Snapshot* s, const kg_frec* d_in, size_t n_in, const uint32_t* d
                        (uint64_t)cap, d_counts, d_res, d_err, (uint64_t*)c->vis, c->vis_slots - 1,
                        d_done, d_done ? done_words : 0u, heavy, (uint32_t*)c->qcnt,
                        shard_escalates(s) && c->qcnt && !c->final ? s->shard_budget : 0u,
-                       s->shard_vis_mode ? 1u : 0u, n_seg, (uint64_t)seg_cap, s->shard_heavy, 1u, 0u);
+                       s->shard_vis_mode ? 1u : 0u, n_seg, (uint64_t)seg_cap, s->shard_heavy, 1u, 0u, 0u);
     HIPC(hipGetLastError());
     hipLaunchKernelGGL(k_shard_heavy, dim3((uint32_t)s->n_cu * 4), dim3(256), 0, stream, s->ds, heavy, d_out,
-                       (uint64_t)cap, d_counts, d_res, d_err, s->shard_n, 1u, 0u);
+                       (uint64_t)cap, d_counts, d_res, d_err, s->shard_n, 1u, 0u, nullptr, 0u, nullptr);
     HIPC(hipGetLastError());
   }
   return 0;
@@ -1100,22 +1110,37 @@ int shard_levels(Snapshot* s, int levels, kg_frec* d_buf[2], size_t cap, uint32_
   if (!c->cnt8) HIPC(hipMalloc((void**)&c->cnt8, 32 * 4));
   HIPC(hipMemsetAsync(c->cnt8, 0, 32 * 4, stream));
   uint32_t* sub[2] = {c->cnt8, c->cnt8 + 16};
+  // Without escalation the levels need no done bitmap -- every query is this rank's, so a level
+  // reads its results directly when pruning is on (slots > 0; off when a query can still end in an
+  // error an IsMember must not hide) -- and no k_shard_prep launch per level: each level's k_shard_heavy
+  // zeroes the next level's bucket counters (read by the level before it) and hub-list counter (two
+  // alternating words, 128 B apart).  Two launches per level instead of three.
+  const bool direct = esc == 0 && budget == 0;
+  unsigned long long* pk2[2] = {heavy.pk, heavy.pk + 16};  // inside the 256-B gap before the tile map
+  if (direct) HIPC(hipMemsetAsync(heavy.pk, 0, 256, stream));
   int cur = start & 1;
   for (int k = 0; k < levels; k++) {
     const int nx = cur ^ 1;
     const uint32_t w = k > 0 ? words : 0u;
-    hipLaunchKernelGGL(k_shard_prep, dim3(std::max<uint32_t>(1, (w + 255) / 256)), dim3(256), 0, stream, (uint32_t)slots,
-                       d_res, d_err, esc, w, c->bits, sub[nx], SUB, heavy.pk);
-    HIPC(hipGetLastError());
+    HeavyList hk = heavy;
+    if (direct) {
+      hk.pk = pk2[k & 1];
+    } else {
+      hipLaunchKernelGGL(k_shard_prep, dim3(std::max<uint32_t>(1, (w + 255) / 256)), dim3(256), 0, stream,
+                         (uint32_t)slots, d_res, d_err, esc, w, c->bits, sub[nx], SUB, heavy.pk);
+      HIPC(hipGetLastError());
+    }
     const bool seg_in = k > 0;
     hipLaunchKernelGGL(k_shard_level, dim3(grid), dim3(256), 0, stream, s->ds, d_buf[cur], (uint64_t)cap,
                        seg_in ? sub[cur] : d_counts[cur], d_buf[nx], seg, sub[nx], d_res, d_err, (uint64_t*)c->vis,
-                       c->vis_slots - 1, k > 0 ? (const uint32_t*)c->bits : nullptr, w, heavy, (uint32_t*)c->qcnt,
-                       budget, s->shard_vis_mode ? 1u : 0u, seg_in ? SUB : 1u, seg_in ? seg : (uint64_t)0,
-                       s->shard_heavy, SUB, pack);
+                       c->vis_slots - 1, k > 0 && !direct ? (const uint32_t*)c->bits : nullptr, direct ? 0u : w, hk,
+                       (uint32_t*)c->qcnt, budget, s->shard_vis_mode ? 1u : 0u, seg_in ? SUB : 1u,
+                       seg_in ? seg : (uint64_t)0, s->shard_heavy, SUB, pack, direct && k > 0 && slots ? 1u : 0u);
     HIPC(hipGetLastError());
-    hipLaunchKernelGGL(k_shard_heavy, dim3((uint32_t)s->n_cu * 4), dim3(256), 0, stream, s->ds, heavy, d_buf[nx], seg,
-                       sub[nx], d_res, d_err, s->shard_n, SUB, pack);
+    // direct: the level after this one writes sub[cur] (this level's input counters) and pk2[(k+1) & 1]
+    hipLaunchKernelGGL(k_shard_heavy, dim3((uint32_t)s->n_cu * 4), dim3(256), 0, stream, s->ds, hk, d_buf[nx], seg,
+                       sub[nx], d_res, d_err, s->shard_n, SUB, pack, direct && seg_in ? sub[cur] : nullptr,
+                       direct && seg_in ? SUB : 0u, direct ? pk2[(k + 1) & 1] : nullptr);
     HIPC(hipGetLastError());
     cur = nx;
   }
@@ -1212,7 +1237,7 @@ int shard_back_level(Snapshot* s, const kg_frec* d_in, size_t n_in, const uint32
                        c->qcnt ? s->shard_back_budget : 0u, s->shard_vis_mode ? 1u : 0u);
     HIPC(hipGetLastError());
     hipLaunchKernelGGL(k_shard_heavy, dim3((uint32_t)s->n_cu * 4), dim3(256), 0, stream, s->ds, heavy, d_out,
-                       (uint64_t)cap, d_counts, d_res, d_err, 1u, 1u, 0u);
+                       (uint64_t)cap, d_counts, d_res, d_err, 1u, 1u, 0u, nullptr, 0u, nullptr);
     HIPC(hipGetLastError());
   }
   return 0;
