@@ -67,6 +67,8 @@ def parse(argv=None):
     ap.add_argument("--shard-heavy", type=int, default=-1,
                     help="kg_snapshot_tune shard_heavy: set rows longer than this are expanded grid-wide (k_shard_heavy; "
                          "0: every expansion; -1: the library default)")
+    ap.add_argument("--shard-vis", type=int, default=0,
+                    help="kg_snapshot_tune shard_vis: log2 of the sharded mode's (query, node) visited table (0: library default)")
     ap.add_argument("--shard-vis-mode", type=int, default=0,
                     help="kg_snapshot_tune shard_vis_mode (sharded (query, node) dedup: 0 exact CAS table, 1 lossy cache)")
     ap.add_argument("--device-sync", type=int, default=1,
@@ -453,6 +455,8 @@ def bench_sharded(a):
     snap.tune("shard_budget", a.shard_budget)
     snap.tune("shard_back_budget", a.shard_back_budget)
     snap.tune("shard_vis_mode", a.shard_vis_mode)
+    if a.shard_vis:
+        snap.tune("shard_vis", a.shard_vis)
     if a.shard_heavy >= 0:
         snap.tune("shard_heavy", a.shard_heavy)
     if a.shard_pack >= 0:
