@@ -54,6 +54,13 @@ def parse(argv=None):
     ap.add_argument("--global-depth", type=int, default=10)
     ap.add_argument("--seed", type=int, default=20250131)
     ap.add_argument("--stream-ecap", type=int, default=512, help="kg_snapshot_tune stream_ecap (stream-tier edges per query, 0 = none)")
+    ap.add_argument("--sharded-steps", type=int, default=20,
+                    help="check mode: timed batches of the hash-sharded sub-line (the C4 engine through "
+                         "kg_check_batch_device over RCCL, one shard per rank; 0 = off)")
+    ap.add_argument("--sharded-warmup", type=int, default=4)
+    ap.add_argument("--sharded-inflight", type=int, default=4, help="sharded batches in flight per rank")
+    ap.add_argument("--sharded-timeout", type=float, default=300.0,
+                    help="watchdog of the sharded sub-line: past it rank 0 prints the line without it")
     ap.add_argument("--shard-budget", type=int, default=0,
                     help="kg_snapshot_tune shard_budget (sharded mode: forward set edges per query and rank before "
                          "the query escalates to the backward phase; 0 = off)")
@@ -1060,8 +1067,8 @@ def main():
                      "request_peak": RAND_REQ_PEAK, "request_frac": req_rate / RAND_REQ_PEAK},
         "host_path": host,
     }
+    orc = None
     if rank == 0:
-        orc = None
         if a.parity > 0 or (world == 1 and a.cpu_seconds > 0):
             cpus = effective_cpus()
             orc = CheckOracle(snap, a, cpus["effective"])
@@ -1070,14 +1077,151 @@ def main():
             out["parity"] = orc.parity(q0, res[0], a.parity, a.parity_canonical)
         if world == 1 and a.cpu_seconds > 0:
             out["cpu_baseline"] = cpu_baseline(orc, q0, a, cpus)
+    bad = a.parity > 0 and rank == 0 and out["parity"]["mismatches"] + out["parity"]["canonical_mismatches"]
+    if a.sharded_steps > 0 and a.preset == 0 and not a.heavy_tail:
+        # the hash-sharded C4 engine beside the replica headline; a watchdog keeps a
+        # hung collective from costing the whole line: rank 0 then prints it without the sub-line
+        def on_timeout():
+            if rank == 0:
+                out["sharded"] = {"error": "sharded sub-line did not finish within %.0f s" % a.sharded_timeout}
+                print(json.dumps(out), flush=True)
+            os._exit(1 if bad else 0)
+        wd = threading.Timer(a.sharded_timeout, on_timeout)
+        wd.daemon = True
+        wd.start()
+        try:
+            out["sharded"] = sharded_leg(a, snap, size_param, dist, rank, world, local, backend, orc)
+        except Exception as e:  # noqa: BLE001 -- reported in the line; the replica headline stands
+            out["sharded"] = {"error": f"{type(e).__name__}: {e}"}
+        wd.cancel()
+        sp = [x.get("parity") for x in (out["sharded"], out["sharded"].get("exchange") or {}) if x.get("parity")]
+        bad = bad or any(x["mismatches"] + x["canonical_mismatches"] for x in sp)
+    if rank == 0:
         print(json.dumps(out), flush=True)
-        if a.parity > 0 and out["parity"]["mismatches"] + out["parity"]["canonical_mismatches"]:
+        if bad:
             sys.stderr.write("PARITY FAILURE: GPU answers differ from the oracle\n")
             if dist:
                 dist.destroy_process_group()
             sys.exit(1)
     if dist:
         dist.destroy_process_group()
+
+
+def sharded_leg(a, snap, size_param, dist, rank, world, local, backend, orc) -> dict:
+    """Config C4 hash-sharded (BASELINE.json configs[3]) beside the replica headline: rank r
+    holds only the rows of the objects hash(ns, obj) mod N == r of the same generator graph, and every
+    batch runs inside kg_check_batch_device over the rank's RCCL communicator (kg_shard_comm.hip: seed,
+    gdepth + 1 exchanges of per-destination buckets, done-bitmap all-gathers, two host round trips) --
+    the path a Go host drives.  Queries are the headline's kind (drawn from the full
+    graph), B per rank per step, --sharded-inflight batches in flight per rank (one stream +
+    communicator each).  One rank holds every row: its shard IS the replica snapshot, the batch runs
+    local-first (the replica tier chain, `path`), and `exchange` times the same batches through the N > 1
+    exchange protocol over RCCL anyway (kg_snapshot_tune shard_force_exchange: self send / recv), the
+    baseline of the N-rank curve.  Weak scaling; value = all ranks' checks / max-over-ranks time."""
+    import torch
+    from keto_amd import _lib
+    from keto_amd.engine import Snapshot
+    from keto_amd.sharded import LibShardedChecker
+    L = _lib.load()
+    dev = f"cuda:{local}"
+    t0 = time.time()
+    if world == 1:
+        ssnap = snap  # one rank: its shard is the whole graph, i.e. the replica snapshot itself
+    else:
+        alpha = 0.5 if a.heavy_tail else 0.0
+        ssnap = Snapshot.synthetic(size_param, seed=a.seed, device=local, shard=(rank, world), preset=a.preset,
+                                   doc_alpha=alpha, group_alpha=alpha)
+    t_build = time.time() - t0
+    transport = "rccl" if backend == "nccl" else "host"
+    P = max(1, a.sharded_inflight)
+    groups = [None] * P
+    if dist is not None and P > 1:
+        groups = [dist.new_group(list(range(world))) for _ in range(P)]
+    chks = [LibShardedChecker(ssnap, rank, world, dist, group=groups[p], transport=transport) for p in range(P)]
+    B, K, W = a.batch, a.sharded_steps, max(a.sharded_warmup, P)
+    dqs = []
+    for k in range(W + K):  # distinct batches, drawn from the full graph (the replica snapshot)
+        d = torch.empty((B, 7), dtype=torch.int32, device=dev)
+        _lib.check(L.kg_synth_queries(snap.handle, 900000 + rank + 7919 * k, B, d.data_ptr()), "kg_synth_queries")
+        dqs.append(d)
+
+    def run_phase(k0, n, lat=None, keep=None):
+        errors = []
+
+        def worker(p):
+            try:
+                with torch.cuda.stream(chks[p].stream):
+                    for k in range(p, n, P):
+                        s0 = time.perf_counter()
+                        r, e = chks[p].check(dqs[k0 + k], a.global_depth)
+                        torch.cuda.current_stream().synchronize()
+                        if lat is not None:
+                            lat[k] = time.perf_counter() - s0
+                        if keep is not None and k == 0:
+                            keep.append((r.cpu().numpy(), e.cpu().numpy()))
+            except Exception as x:  # noqa: BLE001 -- re-raised below
+                errors.append(x)
+
+        th = [threading.Thread(target=worker, args=(p,)) for p in range(min(P, max(n, 1)))]
+        [t.start() for t in th]
+        [t.join() for t in th]
+        if errors:
+            raise errors[0]
+
+    def measure(tag):
+        run_phase(0, W)
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        lat, keep = [0.0] * K, []
+        t1 = time.perf_counter()
+        run_phase(W, K, lat, keep)
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        el, _ = aggregate(dist, time.perf_counter() - t1, 0.0, dev if backend == "nccl" else None)
+        st = chks[0].stats()
+        lv = chks[0].levels()
+        r0, e0 = keep[0]
+        assert (e0 == 0).all() and (r0 <= 1).all(), "unexpected errors in the synthetic batch"
+        res = {"value": world * B * K / el, "unit": "checks/s", "steps": K, "warmup": W, "inflight": P,
+               "ms_per_step": el / K * 1e3, "p99_batch_ms": float(np.percentile(np.array(lat) * 1e3, 99)),
+               "p50_batch_ms": float(np.percentile(np.array(lat) * 1e3, 50)),
+               "path": LibShardedChecker.PATHS.get(st["path"], st["path"]),
+               "levels_per_batch": st["levels"], "host_syncs_per_batch": st["host_syncs"],
+               "records_sent_per_batch": st["records_sent"], "records_to_peers_per_batch": st["records_to_peers"],
+               "wire_bytes_per_batch": st["wire_bytes"], "reruns_last_batch": st["reruns_bucket"] + st["reruns_visited"],
+               "allowed_fraction": float(r0.mean())}
+        if lv:  # per exchange: B_k (records per destination on the wire) and the largest bucket it needed
+            res["exchanges"] = [{"bucket": b, "largest": m, "wire_bytes": (world - 1) * (4 + 16 * b)} for b, m in lv]
+            res["padding_fraction"] = 1.0 - sum(m for _, m in lv) / max(1, sum(b for b, _ in lv))
+        if rank == 0 and orc is not None and a.parity > 0:
+            res["parity"] = orc.parity(dqs[W].cpu().numpy().view(np.uint32), r0, a.parity, a.parity_canonical)
+            res["parity"]["batch"] = "rank 0's first timed sharded batch"
+        return res
+
+    out = {"metric": "permission checks/sec, hash-sharded (kg_check_batch_device, one shard per rank)",
+           "n_gpus": world, "transport": "RCCL over xGMI" if transport == "rccl" else "host (gloo)",
+           "config": {"workload": "C4: the headline's generator graph hash-sharded by object over %d rank(s), "
+                                  "%d checks/step/rank, max_read_depth %d" % (world, B, a.global_depth),
+                      "rows_on_rank": ssnap.info()["rows"], "parallelism": f"shard{world}"},
+           "snapshot_build_s": t_build, "scaling": "weak"}
+    out.update(measure("default"))
+    if world == 1:
+        ssnap.tune("shard_force_exchange", 1)
+        try:
+            out["exchange"] = measure("exchange")
+        finally:
+            ssnap.tune("shard_force_exchange", 0)
+        out["exchange"]["what"] = ("the same batches through the N > 1 exchange protocol over a one-rank RCCL "
+                                   "communicator (the N-rank curve's baseline)")
+    for c in chks:
+        c.close()
+    if ssnap is not snap:
+        ssnap.close()
+    return out
 
 
 def host_path(L, snap, dq_all, n_distinct, a, P) -> dict:

@@ -472,10 +472,31 @@ typedef struct {
 int kg_shard_transport_attach(kg_snapshot* s, const kg_shard_transport* t, void* stream);
 /* Unbinds (and for RCCL destroys) the communicator of `stream`; kg_snapshot_destroy does it for all. */
 int kg_shard_comm_release(kg_snapshot* s, void* stream);
+/* Round 5.  Local-first: a one-rank binding (world 1) runs a batch through the replica engine's tier
+ * chain -- every row is that rank's, so no record would leave it (kg_snapshot_tune "shard_local" 0:
+ * the one-rank device level loop instead).  kg_snapshot_tune "shard_force_exchange" 1 makes a
+ * one-rank binding run the N > 1 exchange protocol over its transport (RCCL: self send / recv,
+ * all-gather and all-reduce over one rank), so the transport code an N-GPU run uses can run, and be
+ * tested, on one GPU.  The exchange protocol sizes the buckets of each exchange k (k = 0 .. gdepth)
+ * separately, from what exchange k needed in the previous batch.  Overflow reruns are bounded
+ * ("shard_max_reruns", default 4) and so are the bucket buffers ("shard_max_bytes", default a quarter
+ * of the free HBM): past either, every rank returns KG_ERR_RESOURCE (-4) together, with the reason in
+ * kg_last_error.  A rank that cannot run its batch (too large, out of memory) says so in the batch's
+ * first all-reduce and every rank returns an error; any other failure inside the protocol (a transport
+ * error, a failed kernel launch) leaves the binding unusable: release it (kg_shard_comm_release) and
+ * bind a new one on every rank. */
 /* Counters of the last batch on `stream`: [0] levels, [1] records sent, [2] host round trips,
  * [3] reruns after a bucket overflow, [4] after a visited-table overflow, [5] queries answered by
- * the general phase, [6] rows it gathered, [7] bucket size B. */
+ * the general phase, [6] rows it gathered, [7] bucket size B (the largest B_k).
+ * kg_shard_comm_stats_ex gives up to 16: [8] records this rank sent to OTHER ranks (what crosses
+ * xGMI), [9] bytes it put on the wire (every other rank gets B_k records per exchange, plus counts
+ * and done bitmaps), [10] path (0 local-first tier chain, 1 one-rank device loop, 2 exchange
+ * protocol), [11] exchanges. */
 int kg_shard_comm_stats(const kg_snapshot* s, void* stream, uint64_t out8[8]);
+int kg_shard_comm_stats_ex(const kg_snapshot* s, void* stream, uint64_t* out, size_t n);
+/* Per exchange k of the last batch: out[2k] = B_k (records per destination it was sent with),
+ * out[2k + 1] = its largest bucket (records).  Returns the number of exchanges (0 without one). */
+int64_t kg_shard_comm_levels(const kg_snapshot* s, void* stream, uint64_t* out, size_t cap);
 
 /* ---- check trees ----------------------------------------------------------------------------
  * CheckRelationTuple's Result.Tree (internal/check/engine.go:65-80, checkgroup/definitions.go:46-50,

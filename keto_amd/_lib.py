@@ -84,7 +84,7 @@ EXPORTS = ["kg_snapshot_create", "kg_snapshot_create_on", "kg_snapshot_synthetic
            "kg_shard_done", "kg_shard_levels", "kg_shard_back_list", "kg_shard_back_seed", "kg_shard_back_level", "kg_shard_refwd_seed",
            "kg_shard_held_words", "kg_shard_held", "kg_shard_result_slots", "kg_shard_bad_nodes", "kg_batcher_create", "kg_batcher_check", "kg_batcher_stats", "kg_batcher_reset_stats", "kg_batcher_destroy",
            "kg_shard_unique_id", "kg_shard_comm_init", "kg_shard_transport_attach", "kg_shard_comm_release",
-           "kg_shard_comm_stats", "kg_check_tree"]
+           "kg_shard_comm_stats", "kg_shard_comm_stats_ex", "kg_shard_comm_levels", "kg_check_tree"]
 
 KG_SHARD_UNIQUE_ID_BYTES = 128
 # kg_shard_transport callbacks (include/ketogpu.h): collective over the ranks, 0 = success
@@ -191,6 +191,9 @@ def load(path: str = LIB_PATH):
     L.kg_shard_transport_attach.argtypes = [vp, C.POINTER(kg_shard_transport), vp]
     L.kg_shard_comm_release.argtypes = [vp, vp]
     L.kg_shard_comm_stats.argtypes = [vp, vp, vp]
+    L.kg_shard_comm_stats_ex.argtypes = [vp, vp, vp, sz]
+    L.kg_shard_comm_levels.argtypes = [vp, vp, vp, sz]
+    L.kg_shard_comm_levels.restype = C.c_int64
     L.kg_check_tree.argtypes = [vp, vp, i32, vp, sz, vp, sz, C.POINTER(sz), C.POINTER(C.c_uint8), C.POINTER(u32)]
     L.kg_batcher_create.argtypes = [vp, i32, sz, u32, C.c_int, C.POINTER(vp)]
     L.kg_batcher_check.argtypes = [vp, vp, sz, vp, vp]
@@ -207,7 +210,7 @@ def load(path: str = LIB_PATH):
                  "kg_shard_done", "kg_shard_levels", "kg_shard_back_list", "kg_shard_back_seed", "kg_shard_back_level", "kg_shard_refwd_seed",
                  "kg_shard_held_words", "kg_shard_held", "kg_batcher_create", "kg_batcher_check", "kg_batcher_stats",
                  "kg_shard_unique_id", "kg_shard_comm_init", "kg_shard_transport_attach", "kg_shard_comm_release",
-                 "kg_shard_comm_stats", "kg_check_tree"):
+                 "kg_shard_comm_stats", "kg_shard_comm_stats_ex", "kg_check_tree"):
         getattr(L, name).restype = C.c_int
     _lib = L
     return L

@@ -412,6 +412,31 @@ static int tune_one(Snapshot* s, const char* key, int64_t value) {
     s->shard_bucket0 = (uint32_t)value;
     return 0;
   }
+  if (strcmp(key, "shard_force_exchange") == 0) {
+    if (value < 0 || value > 1) return set_error(-2, "shard_force_exchange must be 0 or 1");
+    s->shard_force_exchange = (int)value;
+    return 0;
+  }
+  if (strcmp(key, "shard_local") == 0) {
+    if (value < 0 || value > 1) return set_error(-2, "shard_local must be 0 or 1");
+    s->shard_local = (int)value;
+    return 0;
+  }
+  if (strcmp(key, "shard_max_reruns") == 0) {
+    if (value < 0 || value > 64) return set_error(-2, "shard_max_reruns must be in [0, 64]");
+    s->shard_max_reruns = (uint32_t)value;
+    return 0;
+  }
+  if (strcmp(key, "shard_max_bytes") == 0) {
+    if (value < 0) return set_error(-2, "shard_max_bytes must be >= 0 (0: a quarter of the free HBM)");
+    s->shard_max_bytes = (uint64_t)value;
+    return 0;
+  }
+  if (strcmp(key, "shard_force_overflow") == 0) {
+    if (value < 0 || value > 1) return set_error(-2, "shard_force_overflow must be 0 or 1");
+    s->shard_force_overflow = (int)value;
+    return 0;
+  }
   if (strcmp(key, "shard_pack") == 0) {
     if (value < 0 || value > 1) return set_error(-2, "shard_pack must be 0 or 1");
     s->shard_pack = (int)value;
@@ -628,8 +653,9 @@ int kg_check_batch_device(kg_snapshot* sp, const kg_query* d_q, size_t n, int32_
   if (!sp) return set_error(-2, "NULL snapshot");
   Snapshot* s = reinterpret_cast<Snapshot*>(sp);
   // a transport bound to this stream: the whole hash-sharded batch inside the library (kg_shard_comm.hip)
-  if (kg::ShardComm* c = kg::shard_comm_of(s, (hipStream_t)stream))
-    return kg::shard_check(s, c, d_q, n, global_max_depth, d_out, d_err, stats);
+  bool sharded = false;
+  const int src = kg::shard_check_entry(s, (hipStream_t)stream, d_q, n, global_max_depth, d_out, d_err, stats, &sharded);
+  if (sharded) return src;
   if (s->shard_n > 1)
     return set_error(-2, "sharded snapshot: bind a transport to this stream (kg_shard_comm_init) or drive "
                          "kg_shard_seed / kg_shard_level");

@@ -151,7 +151,7 @@ __host__ __device__ __forceinline__ uint32_t adjx_len16(const AdjX& x) { return 
 struct NSlot {
   uint64_t key;
   uint32_t node, beg, len;
-  uint32_t sig;  // signature bits 16-47 of the node's row subjects (as AdjX.sig): k_resolve's root probe filter
+  uint32_t sig;  // signature bits 12-43 of the node's row subjects (as AdjX.sig): k_resolve's root probe filter
   uint64_t pad1;  // low byte: the node's flags (nflags; 0 without a namespace program); bits 20-31: signature bits 0-11
 };
 // Holder-hash slot: tagged subject -> hold[first, first + count).  key == NONE: free.

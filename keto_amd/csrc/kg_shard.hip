@@ -803,14 +803,19 @@ __global__ __launch_bounds__(256) void k_shard_back_level(DevSnap s, const kg_fr
 __global__ __launch_bounds__(256) void k_shard_heavy(DevSnap s, HeavyList heavy, kg_frec* out, uint64_t cap,
                                                      uint32_t* counts, uint8_t* res, uint32_t* err, uint32_t nranks,
                                                      uint32_t out_sub, uint32_t pack, uint32_t* zero_counts,
-                                                     uint32_t zero_n, unsigned long long* zero_pk) {
+                                                     uint32_t zero_n, unsigned long long* zero_pk,
+                                                     uint32_t* maxacc) {
   static_assert(HEAVY_TILE == 256, "one edge per thread");
   __shared__ uint32_t s_r0;
   __shared__ uint64_t s_e0[HEAVY_TILE + 1];
   // kg_shard_levels: the next level's bucket counters and hub-list counter, free since the level
-  // before this one read them (what a separate k_shard_prep launch per level did)
+  // before this one read them (what a separate k_shard_prep launch per level did); the largest
+  // sub-bucket count goes to *maxacc first (the counters count past the cap: what a rerun needs)
   if (blockIdx.x == 0) {
-    if (zero_counts && threadIdx.x < zero_n) zero_counts[threadIdx.x] = 0;
+    if (zero_counts && threadIdx.x < zero_n) {
+      if (maxacc) atomicMax(maxacc, zero_counts[threadIdx.x]);
+      zero_counts[threadIdx.x] = 0;
+    }
     if (zero_pk && threadIdx.x == 0) *zero_pk = 0;
   }
   const uint32_t nh = (uint32_t)min((unsigned long long)heavy.cap, *heavy.pk >> HEAVY_EDGE_BITS), me = s.shard_rank;
@@ -879,9 +884,12 @@ __global__ void k_shard_done(uint32_t n, const uint8_t* __restrict__ res, const 
 // hub-row count -- what the per-level driver did with a kernel and two fills.
 __global__ void k_shard_prep(uint32_t n, const uint8_t* __restrict__ res, const uint32_t* __restrict__ err,
                              uint32_t esc_mask, uint32_t words, uint32_t* __restrict__ bits, uint32_t* counts,
-                             uint32_t n_sub, unsigned long long* heavy_pk) {
+                             uint32_t n_sub, unsigned long long* heavy_pk, uint32_t* maxacc) {
   const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
-  if (w < n_sub) counts[w] = 0;  // the level's (sub-)bucket counters; the flags word after them accumulates
+  if (w < n_sub) {  // the level's (sub-)bucket counters; the flags word after them accumulates
+    atomicMax(maxacc, counts[w]);
+    counts[w] = 0;
+  }
   if (w == 0) *heavy_pk = 0;
   if (w >= words) return;
   uint32_t b = 0;
@@ -894,13 +902,22 @@ __global__ void k_shard_prep(uint32_t n, const uint8_t* __restrict__ res, const 
 
 // After kg_shard_levels: the caller's view of the two level buffers -- records left in the last one
 // (the sum of its sub-bucket counters) and the flags accumulated in both.
+// *need (if given) = the bucket size every level's sub-buckets would have fit in: n_sub x the largest
+// sub-bucket count of the loop (the counters keep counting past a full segment), and at least the
+// seed's record count (*seed, the loop's first input; read before counts_end is written).
 __global__ void k_shard_fold(const uint32_t* __restrict__ sub_end, const uint32_t* __restrict__ sub_other,
-                             uint32_t n_sub, uint32_t* counts_end, uint32_t* counts0) {
+                             uint32_t n_sub, uint32_t* counts_end, uint32_t* counts0, const uint32_t* maxacc,
+                             const uint32_t* seed, unsigned long long* need) {
   if (blockIdx.x != 0 || threadIdx.x != 0) return;
-  uint32_t left = 0;
-  for (uint32_t k = 0; k < n_sub; k++) left += sub_end[k];
+  const unsigned long long seeded = *seed;
+  uint32_t left = 0, mx = *maxacc;
+  for (uint32_t k = 0; k < n_sub; k++) {
+    left += sub_end[k];
+    mx = max(mx, max(sub_end[k], sub_other[k]));
+  }
   counts_end[0] = left;
   counts0[1] |= sub_end[n_sub] | sub_other[n_sub];
+  if (need) *need = max((unsigned long long)mx * n_sub, seeded);
 }
 
 __global__ void k_shard_finish(uint32_t n, uint8_t* res, uint32_t* err, ShardFormula F) {
@@ -969,6 +986,8 @@ int shard_bad_nodes(Snapshot* s, uint64_t* count) {
   *count = h;
   return 0;
 }
+
+size_t shard_slot_limit() { return Q_MASK; }
 
 size_t shard_result_slots(const Snapshot* s, size_t n) { return s->n_fplans ? n * (2 + (size_t)s->fp_leaves) : n; }
 
@@ -1069,7 +1088,7 @@ int shard_level(Snapshot* s, const kg_frec* d_in, size_t n_in, const uint32_t* d
                        s->shard_vis_mode ? 1u : 0u, n_seg, (uint64_t)seg_cap, s->shard_heavy, 1u, 0u, 0u);
     HIPC(hipGetLastError());
     hipLaunchKernelGGL(k_shard_heavy, dim3((uint32_t)s->n_cu * 4), dim3(256), 0, stream, s->ds, heavy, d_out,
-                       (uint64_t)cap, d_counts, d_res, d_err, s->shard_n, 1u, 0u, nullptr, 0u, nullptr);
+                       (uint64_t)cap, d_counts, d_res, d_err, s->shard_n, 1u, 0u, nullptr, 0u, nullptr, nullptr);
     HIPC(hipGetLastError());
   }
   return 0;
@@ -1081,7 +1100,8 @@ int shard_level(Snapshot* s, const kg_frec* d_in, size_t n_in, const uint32_t* d
 // from d_counts[cur][0] on the device) and writes buffer cur ^ 1; from the second level on, queries
 // answered IsMember (esc_mode 1: or escalated) drop their records through the done bitmap.
 int shard_levels(Snapshot* s, int levels, kg_frec* d_buf[2], size_t cap, uint32_t* d_counts[2], int start,
-                 uint8_t* d_res, uint32_t* d_err, size_t slots, int esc_mode, int* end, hipStream_t stream) {
+                 uint8_t* d_res, uint32_t* d_err, size_t slots, int esc_mode, int* end, hipStream_t stream,
+                 unsigned long long* need) {
   HIPC(hipSetDevice(s->device));
   if (!stream) stream = s->stream;
   if (s->shard_n != 1) return set_error(-2, "kg_shard_levels runs one-rank batches (shard_n = %u)", s->shard_n);
@@ -1110,6 +1130,7 @@ int shard_levels(Snapshot* s, int levels, kg_frec* d_buf[2], size_t cap, uint32_
   if (!c->cnt8) HIPC(hipMalloc((void**)&c->cnt8, 32 * 4));
   HIPC(hipMemsetAsync(c->cnt8, 0, 32 * 4, stream));
   uint32_t* sub[2] = {c->cnt8, c->cnt8 + 16};
+  uint32_t* maxsub = c->cnt8 + 12;  // the largest sub-bucket count of any level (k_shard_heavy / _prep)
   // Without escalation the levels need no done bitmap -- every query is this rank's, so a level
   // reads its results directly when pruning is on (slots > 0; off when a query can still end in an
   // error an IsMember must not hide) -- and no k_shard_prep launch per level: each level's k_shard_heavy
@@ -1127,7 +1148,7 @@ int shard_levels(Snapshot* s, int levels, kg_frec* d_buf[2], size_t cap, uint32_
       hk.pk = pk2[k & 1];
     } else {
       hipLaunchKernelGGL(k_shard_prep, dim3(std::max<uint32_t>(1, (w + 255) / 256)), dim3(256), 0, stream,
-                         (uint32_t)slots, d_res, d_err, esc, w, c->bits, sub[nx], SUB, heavy.pk);
+                         (uint32_t)slots, d_res, d_err, esc, w, c->bits, sub[nx], SUB, heavy.pk, maxsub);
       HIPC(hipGetLastError());
     }
     const bool seg_in = k > 0;
@@ -1140,13 +1161,13 @@ int shard_levels(Snapshot* s, int levels, kg_frec* d_buf[2], size_t cap, uint32_
     // direct: the level after this one writes sub[cur] (this level's input counters) and pk2[(k+1) & 1]
     hipLaunchKernelGGL(k_shard_heavy, dim3((uint32_t)s->n_cu * 4), dim3(256), 0, stream, s->ds, hk, d_buf[nx], seg,
                        sub[nx], d_res, d_err, s->shard_n, SUB, pack, direct && seg_in ? sub[cur] : nullptr,
-                       direct && seg_in ? SUB : 0u, direct ? pk2[(k + 1) & 1] : nullptr);
+                       direct && seg_in ? SUB : 0u, direct ? pk2[(k + 1) & 1] : nullptr, maxsub);
     HIPC(hipGetLastError());
     cur = nx;
   }
   if (levels > 0) {  // the caller's counters: records left in the last buffer, flags of both
     hipLaunchKernelGGL(k_shard_fold, dim3(1), dim3(64), 0, stream, sub[cur], sub[cur ^ 1], SUB, d_counts[cur],
-                       d_counts[0]);
+                       d_counts[0], (const uint32_t*)maxsub, (const uint32_t*)d_counts[start & 1], need);
     HIPC(hipGetLastError());
   }
   if (end) *end = cur;
@@ -1237,7 +1258,7 @@ int shard_back_level(Snapshot* s, const kg_frec* d_in, size_t n_in, const uint32
                        c->qcnt ? s->shard_back_budget : 0u, s->shard_vis_mode ? 1u : 0u);
     HIPC(hipGetLastError());
     hipLaunchKernelGGL(k_shard_heavy, dim3((uint32_t)s->n_cu * 4), dim3(256), 0, stream, s->ds, heavy, d_out,
-                       (uint64_t)cap, d_counts, d_res, d_err, 1u, 1u, 0u, nullptr, 0u, nullptr);
+                       (uint64_t)cap, d_counts, d_res, d_err, 1u, 1u, 0u, nullptr, 0u, nullptr, nullptr);
     HIPC(hipGetLastError());
   }
   return 0;

@@ -64,8 +64,17 @@ struct ShardComm {
   size_t dq_cap = 0;
   void* pinned = nullptr;  // host staging: host-memory transports and readbacks
   size_t pinned_bytes = 0;
-  size_t bucket = 0;     // B, learned from the previous batch
-  uint64_t st[8] = {};   // kg_shard_comm_stats
+  size_t bucket = 0;     // one rank's device loop: B, learned from the previous batch
+  // the exchange protocol: B_k records per destination for exchange k (k = 0 .. gdepth; the seed
+  // writes exchange 0's buckets, level k - 1 exchange k's), each learned from the largest bucket
+  // exchange k needed in the previous batch -- levels differ by orders of magnitude, and every
+  // destination of exchange k gets B_k records on the wire whatever it holds
+  std::vector<size_t> lb;
+  unsigned long long* red = nullptr;  // [8 + levels]: the end-of-batch all-reduce (tot[5] | per-exchange largest)
+  size_t red_cap = 0;
+  std::vector<uint64_t> lvl_last, lb_last;  // the last batch: per exchange its largest bucket and B_k
+  std::mutex host_mu;    // kg_check_batch (host buffers): one batch at a time through dq / dout / derr
+  uint64_t st[16] = {};  // kg_shard_comm_stats (kg_shard_comm_stats_ex: all 16)
   hipEvent_t ev[2] = {nullptr, nullptr};
   ~ShardComm();
 };
@@ -79,6 +88,7 @@ ShardComm::~ShardComm() {
   hipFree(recv);
   hipFree(cnt);
   hipFree(acc);
+  hipFree(red);
   hipFree(bits);
   hipFree(bits_all);
   hipFree(res);
@@ -92,14 +102,22 @@ ShardComm::~ShardComm() {
 }
 
 void shard_comms_free(Snapshot* s) {
-  std::lock_guard<std::mutex> lk(s->comm_mu);
-  for (ShardComm* c : s->comms) delete c;
-  s->comms.clear();
+  std::vector<std::shared_ptr<ShardComm>> v;
+  {
+    std::lock_guard<std::mutex> lk(s->comm_mu);
+    v.swap(s->comms);
+    s->n_comms.store(0, std::memory_order_release);
+  }
+  v.clear();  // each binding is destroyed when its last caller lets go of it
 }
 
-ShardComm* shard_comm_of(Snapshot* s, hipStream_t st) {
+// The binding of stream st (shared: kg_shard_comm_release or a re-bind on st only drops the list's
+// reference, and a caller inside a batch keeps the object alive until it returns).  Snapshots with
+// nothing bound -- the replicated path -- take no lock.
+std::shared_ptr<ShardComm> shard_comm_of(Snapshot* s, hipStream_t st) {
+  if (s->n_comms.load(std::memory_order_acquire) == 0) return nullptr;
   std::lock_guard<std::mutex> lk(s->comm_mu);
-  for (ShardComm* c : s->comms)
+  for (const auto& c : s->comms)
     if (c->bound == st) return c;
   return nullptr;
 }
@@ -233,21 +251,27 @@ static int h_alltoall2(ShardComm* c, const void* s0, void* r0, size_t b0, const 
 }
 
 // ------------------------------------------------------------------ small kernels
-// Per level before the exchange (keto_amd/sharded.py _check_fixed's device accumulators): acc[0] |=
-// overflow flags (c[N], or a bucket past B), acc[1] = largest bucket, acc[2] += records sent.
-__global__ void k_sc_acc(const uint32_t* __restrict__ c, uint32_t N, uint32_t B, unsigned long long* acc) {
+// Per exchange k before it runs (keto_amd/sharded.py _check_fixed's device accumulators): acc[0] |=
+// overflow flags (c[N], or a bucket past B_k), acc[1] = largest bucket, acc[2] += records sent,
+// acc[3] += records sent to other ranks (what crosses xGMI), *lvl = exchange k's largest bucket (the
+// counters keep counting past B_k, so an overflowed bucket reports what it would have needed).
+__global__ void k_sc_acc(const uint32_t* __restrict__ c, uint32_t N, uint32_t B, uint32_t me, unsigned long long* acc,
+                         unsigned long long* lvl) {
   const uint32_t i = threadIdx.x;
   const uint32_t v = i < N ? c[i] : 0u;
-  unsigned long long fl = (i < N && v > B) ? 1ull : 0ull, mx = v, sum = v;
+  unsigned long long fl = (i < N && v > B) ? 1ull : 0ull, mx = v, sum = v, wire = i != me ? v : 0u;
   for (int off = 32; off; off >>= 1) {
     fl |= __shfl_xor(fl, off, 64);
     mx = max(mx, __shfl_xor(mx, off, 64));
     sum += __shfl_xor(sum, off, 64);
+    wire += __shfl_xor(wire, off, 64);
   }
   if (i == 0) {
     acc[0] |= fl | c[N];
     acc[1] = max(acc[1], mx);
     acc[2] += sum;
+    acc[3] += wire;
+    *lvl = mx;
   }
 }
 
@@ -271,18 +295,28 @@ __global__ void k_sc_final(const uint32_t* __restrict__ c, uint32_t N, uint32_t 
   }
 }
 
-// One rank (kg_shard_levels' device loop): tot = (bucket overflow, visited overflow, 0, records left, 0)
-// from the flags words of both buffers and the count of the last one.
+// One rank (kg_shard_levels' device loop): tot = (bucket overflow, visited overflow, -, records left, 0)
+// from the flags words of both buffers and the count of the last one; tot[2] = the bucket size the
+// levels needed, written by kg_shard_levels' fold.
 __global__ void k_sc_final1(const uint32_t* __restrict__ c0, const uint32_t* __restrict__ c1, int end,
                             unsigned long long* tot) {
   if (threadIdx.x == 0) {
     const uint32_t f = c0[1] | c1[1];
     tot[0] = f & 1u;
     tot[1] = (f >> 1) & 1u;
-    tot[2] = 0;
     tot[3] = end ? c1[0] : c0[0];
     tot[4] = 0;
   }
+}
+
+// 1 + the largest relation id of any node (the general phase's region gather asks owners for every
+// relation of an object, so every relation a row can carry must be named).
+__global__ void k_sc_rel_span(const uint32_t* __restrict__ nd_rel, uint64_t n, unsigned int* out) {
+  uint32_t m = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    m = max(m, nd_rel[i] + 1u);
+  for (int off = 32; off; off >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, off, 64));
+  if ((threadIdx.x & 63) == 0 && m) atomicMax(out, m);
 }
 
 // tot[4] = 1 when some query of [0, n) ended KG_ERROR / KG_ERR_NOT_IMPLEMENTED (general phase).
@@ -346,7 +380,9 @@ static int comm_setup(Snapshot* s, ShardComm* c) {
   return 0;
 }
 
+// Takes ownership of c (freed on failure).
 static int bind(Snapshot* s, ShardComm* c, hipStream_t st) {
+  std::shared_ptr<ShardComm> sp(c);
   if ((uint32_t)c->world != s->shard_n || (uint32_t)c->rank != s->shard_rank)
     return set_error(-2, "transport is rank %d of %d, the snapshot was built as shard %u of %u", c->rank, c->world,
                      s->shard_rank, s->shard_n);
@@ -355,18 +391,40 @@ static int bind(Snapshot* s, ShardComm* c, hipStream_t st) {
   c->bucket = s->shard_bucket0;
   c->device = s->device;
   if (int rc = comm_setup(s, c)) return rc;
+  std::shared_ptr<ShardComm> old;  // a previous binding of st: destroyed outside the lock, once unused
   std::lock_guard<std::mutex> lk(s->comm_mu);
   for (auto it = s->comms.begin(); it != s->comms.end(); ++it)
     if ((*it)->bound == st) {
-      delete *it;
+      old = *it;
       s->comms.erase(it);
       break;
     }
-  s->comms.push_back(c);
+  s->comms.push_back(sp);
+  s->n_comms.store((int)s->comms.size(), std::memory_order_release);
   return 0;
 }
 
 // ------------------------------------------------------------------ the general phase
+// s->rel_span (1 + the largest relation id of any node; collective callers all compute their own)
+static int rel_span(Snapshot* s, hipStream_t st) {
+  if (s->rel_span || !s->ds.n_nodes) return 0;
+  unsigned int* d = nullptr;
+  HIPC(hipMalloc((void**)&d, 4));
+  unsigned int h = 0;
+  int rc = hipMemsetAsync(d, 0, 4, st) != hipSuccess;
+  if (!rc) {
+    const uint64_t nn = s->ds.n_nodes;
+    hipLaunchKernelGGL(k_sc_rel_span, dim3((uint32_t)std::min<uint64_t>((nn + 255) / 256, 4096)), dim3(256), 0, st,
+                       s->ds.nd_rel, nn, d);
+    rc = hipGetLastError() != hipSuccess || hipMemcpyAsync(&h, d, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+         hipStreamSynchronize(st) != hipSuccess;
+  }
+  hipFree(d);
+  if (rc) return set_error(-1, "relation span of the snapshot's nodes");
+  s->rel_span = std::max(h, 1u);
+  return 0;
+}
+
 template <int W>
 using Row = std::array<uint64_t, W>;
 
@@ -409,7 +467,10 @@ static int gather_region(Snapshot* s, ShardComm* c, const std::vector<std::pair<
   for (const auto& o : starts) reqset.insert(Row<3>{(uint64_t)c->rank, o.first, o.second});
   std::vector<Row<3>> req(reqset.begin(), reqset.end());
   std::set<Row<3>> seen;  // (home, ns, obj) this owner has shipped
-  const uint32_t nrel = std::max<uint32_t>(s->ds.n_rel, 1);
+  // every relation a row can carry: the program's / dict's relation count does not bound the ids a
+  // snapshot built without a dict (or with undeclared relations) stores
+  if (int rc = rel_span(s, c->run)) return rc;
+  const uint32_t nrel = std::max<uint32_t>(std::max<uint32_t>(s->ds.n_rel, s->rel_span), 1);
   for (int hop = 0; hop < gdepth + 2; hop++) {
     std::vector<int> dest(req.size());
     for (size_t i = 0; i < req.size(); i++) dest[i] = (int)shard_owner((uint32_t)req[i][1], (uint32_t)req[i][2], N);
@@ -493,12 +554,16 @@ static int general_phase(Snapshot* s, ShardComm* c, const kg_query* d_q, size_t 
   if (!rc && (hipMalloc(&dq, m * sizeof(kg_query)) != hipSuccess || hipMalloc(&dout, m) != hipSuccess ||
               hipMalloc(&derr, m * 4) != hipSuccess))
     rc = set_error(-1, "general phase buffers");
-  if (!rc && hipMemcpy(dq, oq.data(), m * sizeof(kg_query), hipMemcpyHostToDevice) != hipSuccess)
+  // everything on the region snapshot's own stream (non-blocking: the null stream would not wait for
+  // it), completed before the results are read
+  if (!rc && hipMemcpyAsync(dq, oq.data(), m * sizeof(kg_query), hipMemcpyHostToDevice, g->stream) != hipSuccess)
     rc = set_error(-1, "general phase H2D");
-  if (!rc) rc = check_batch_device(g, g->workspace(nullptr), dq, m, gdepth, dout, derr, nullptr);
-  if (!rc && (hipMemcpy(r.data(), dout, m, hipMemcpyDeviceToHost) != hipSuccess ||
-              hipMemcpy(e.data(), derr, m * 4, hipMemcpyDeviceToHost) != hipSuccess))
+  if (!rc) rc = check_batch_device(g, g->workspace(g->stream), dq, m, gdepth, dout, derr, nullptr);
+  if (!rc && (hipMemcpyAsync(r.data(), dout, m, hipMemcpyDeviceToHost, g->stream) != hipSuccess ||
+              hipMemcpyAsync(e.data(), derr, m * 4, hipMemcpyDeviceToHost, g->stream) != hipSuccess ||
+              hipStreamSynchronize(g->stream) != hipSuccess))
     rc = set_error(-1, "general phase D2H");
+  if (g->stream) (void)hipStreamSynchronize(g->stream);  // nothing of g's still running when it is freed
   hipFree(dq);
   hipFree(dout);
   hipFree(derr);
@@ -520,11 +585,19 @@ static int general_phase(Snapshot* s, ShardComm* c, const kg_query* d_q, size_t 
 // phase) and the single-GPU expand runs on a snapshot of them -- the same rows in the same shard order
 // per (ns, obj, rel), so the same trees.
 int shard_expand(Snapshot* s, const kg_set* roots, size_t n, int32_t gdepth, kg_tree_buf* out) {
-  ShardComm* c = shard_comm_of(s, nullptr);
+  std::shared_ptr<ShardComm> cp = shard_comm_of(s, nullptr);
+  ShardComm* c = cp.get();
   if (!c) return set_error(-2, "sharded snapshot: bind a transport to its own stream first (kg_shard_comm_init)");
   std::lock_guard<std::mutex> lk(c->mu);
   HIPC(hipSetDevice(s->device));
   if (gdepth < 1) gdepth = 5;  // config.schema.json:308-315 default
+  if (c->world == 1 && !s->shard_force_exchange && s->shard_local) {
+    // one rank holds every row: nothing to gather (local-first, as shard_check)
+    void* bufs = nullptr;
+    const int rc = expand_batch(s, s->stream, &bufs, roots, n, gdepth, out);
+    if (bufs) expand_bufs_free(bufs);
+    return rc;
+  }
   std::vector<std::pair<uint32_t, uint32_t>> starts;
   for (size_t i = 0; i < n; i++)
     if (roots[i].sns != KG_SUBJECT_ID) starts.emplace_back(roots[i].sns, roots[i].sobj);
@@ -546,95 +619,210 @@ int shard_expand(Snapshot* s, const kg_set* roots, size_t n, int32_t gdepth, kg_
 }
 
 // ------------------------------------------------------------------ one batch
+// Device buffers a failed step left half-grown are dropped on EVERY rank together, so the next batch
+// finds the same allocation state on all of them (allocation decisions stay symmetric: a rank that
+// allocates alone would wait in the all-reduce below for ranks that never get there).
+static void drop_buffers(ShardComm* c) {
+  for (kg_frec** p : {&c->buf[0], &c->buf[1], &c->recv}) {
+    hipFree(*p);
+    *p = nullptr;
+  }
+  c->recs = 0;
+  hipFree(c->bits);
+  hipFree(c->bits_all);
+  c->bits = c->bits_all = nullptr;
+  c->words_cap = c->all_cap = 0;
+}
+
+// Bucket buffers may take this much (kg_snapshot_tune "shard_max_bytes"; default a quarter of the free
+// HBM, counting what the buffers being replaced hold).
+static uint64_t bucket_byte_cap(const Snapshot* s, const ShardComm* c) {
+  if (s->shard_max_bytes) return s->shard_max_bytes;
+  size_t fr = 0, total = 0;
+  if (hipMemGetInfo(&fr, &total) != hipSuccess) return ~0ull;
+  return (fr + 3 * c->recs * sizeof(kg_frec)) / 4;
+}
+
+// Grows the buffers of one run of the protocol.  Collective when `xch`: every rank reaches this with
+// the same B and the same history, so all of them allocate (and agree) on the same runs; a failure on
+// any rank -- a cap or an out-of-memory -- is returned by all of them.
+static int grow_run(Snapshot* s, ShardComm* c, bool xch, size_t B, uint32_t words) {
+  const size_t N = (size_t)c->world;
+  const bool g_bits = !c->bits || !c->bits_all || (size_t)words + 1 > c->words_cap || N * words + 1 > c->all_cap;
+  const bool g_recs = N * B > c->recs || !c->buf[0];
+  if (!g_bits && !g_recs) return 0;
+  uint64_t f = 0;
+  const uint64_t bytes = 3ull * N * B * sizeof(kg_frec), cap = bucket_byte_cap(s, c);
+  if (g_recs) {
+    for (kg_frec** p : {&c->buf[0], &c->buf[1], &c->recv}) {
+      hipFree(*p);
+      *p = nullptr;
+    }
+    c->recs = 0;
+    if (bytes > cap) f = 1;
+    for (kg_frec** p : {&c->buf[0], &c->buf[1], &c->recv})
+      if (!f && hipMalloc((void**)p, N * B * sizeof(kg_frec)) != hipSuccess) f = 2;
+    if (!f) c->recs = N * B;
+  }
+  if (!f && g_bits &&
+      (grow((void**)&c->bits, &c->words_cap, (size_t)words + 1, 4) ||
+       grow((void**)&c->bits_all, &c->all_cap, N * words + 1, 4)))
+    f = 2;
+  const uint64_t mine = f;
+  if (xch) {
+    if (int rc = h_allreduce_max(c, &f, 1)) return rc;
+    c->st[2]++;
+  }
+  if (!f) return 0;
+  drop_buffers(c);
+  if (f == 1 && mine)
+    return set_error(KG_ERR_RESOURCE_CODE,
+                     "sharded batch: bucket buffers of %zu records per destination need %.3g GB, over the %.3g GB "
+                     "cap (kg_snapshot_tune shard_max_bytes)", B, bytes / 1e9, cap / 1e9);
+  return set_error(KG_ERR_RESOURCE_CODE, "sharded batch: buffer allocation failed on %s",
+                   mine ? "this rank" : "another rank");
+}
+
 int shard_check(Snapshot* s, ShardComm* c, const kg_query* d_q, size_t n, int32_t gdepth, uint8_t* d_out,
                 uint32_t* d_err, kg_stats* stats) {
   std::lock_guard<std::mutex> lk(c->mu);
   HIPC(hipSetDevice(s->device));
   if (gdepth < 1) gdepth = 5;  // config.schema.json:308-315 default (as kg_shard_seed)
-  if (n > 0x7FFFFFFFull) return set_error(-2, "batch too large");
   hipStream_t st = c->run;
   const uint32_t N = (uint32_t)c->world;
+  // the exchange protocol runs at N > 1, and at N = 1 when forced (kg_snapshot_tune
+  // "shard_force_exchange": the same RCCL calls as N > 1, each rank its own peer)
+  const bool xch = N > 1 || s->shard_force_exchange;
   memset(c->st, 0, sizeof c->st);
+  if (!xch && s->shard_local) {
+    // Local-first, one rank: every row is this rank's, so no record of the level protocol would ever
+    // leave it -- the batch runs the replica engine's tier chain (k_resolve -> k_stream4 -> k_back ->
+    // grid tiers / rewrite interpreter) on the bound stream's workspace instead of level-synchronous
+    // records with a (query, node) CAS each (kg_snapshot_tune "shard_local" 0: the device
+    // level loop below).
+    c->st[10] = 0;
+    Workspace* w = s->workspace(st);
+    std::lock_guard<std::mutex> wl(w->mu);
+    return check_batch_device(s, w, d_q, n, gdepth, d_out, d_err, stats);
+  }
+  c->st[10] = xch ? 2 : 1;
   if (stats) {
     memset(stats, 0, sizeof *stats);
     for (auto& e : c->ev)
       if (!e) HIPC(hipEventCreate(&e));
     HIPC(hipEventRecord(c->ev[0], st));
   }
-  // the largest result-slot count of any rank: the done bitmap's width (host round trip 1; one rank
-  // needs none)
+  // Before the first collective, what only this rank can know: whether it can run its batch at all
+  // and its result buffers (sized by its own batch).  The agreement all-reduce then carries a failure
+  // flag beside the largest result-slot count of any rank (the done bitmap's width), so a rank that
+  // cannot go on never leaves the others waiting in a later collective (host round trip 1; one rank
+  // without the exchange needs none).
   const size_t slots = shard_result_slots(s, n);
-  uint64_t smax = slots;
-  if (N > 1) {
-    if (int rc = h_allreduce_max(c, &smax, 1)) return rc;
-    c->st[2]++;
-  }
-  const uint32_t words = (uint32_t)((smax + 31) / 32);
-  if (grow((void**)&c->bits, &c->words_cap, (size_t)words + 1, 4)) return -1;
-  if (grow((void**)&c->bits_all, &c->all_cap, (size_t)N * words + 1, 4)) return -1;
-  size_t have = c->slots_cap;
-  if (slots > have || !c->res) {
+  uint64_t bad = (n > 0x7FFFFFFFull || slots > shard_slot_limit()) ? 1 : 0;
+  if (!bad && (slots > c->slots_cap || !c->res)) {
     hipFree(c->res);
     hipFree(c->err);
     c->res = nullptr;
     c->err = nullptr;
     c->slots_cap = 0;
     const size_t m = std::max<size_t>(slots, 1024);
-    HIPC(hipMalloc((void**)&c->res, m));
-    HIPC(hipMalloc((void**)&c->err, m * 4));
-    c->slots_cap = m;
+    if (hipMalloc((void**)&c->res, m) != hipSuccess || hipMalloc((void**)&c->err, m * 4) != hipSuccess) bad = 2;
+    else c->slots_cap = m;
+  }
+  uint64_t agree[2] = {slots, bad};
+  if (xch) {
+    if (int rc = h_allreduce_max(c, agree, 2)) return rc;
+    c->st[2]++;
+  }
+  if (agree[1]) {
+    if (bad == 1) return set_error(-2, "sharded batch too large (%zu queries, %zu result slots > %zu)", n, slots,
+                                   shard_slot_limit());
+    return set_error(bad ? KG_ERR_RESOURCE_CODE : -2, "sharded batch: %s", bad ? "result buffers" :
+                     "another rank cannot run its batch (too large, or out of memory)");
+  }
+  const uint64_t smax = agree[0];
+  const uint32_t words = (uint32_t)((smax + 31) / 32);
+  const size_t B0 = std::min<size_t>(2 * smax / N + 1024, 1ull << 26);
+  // exchanges k = 0 .. L - 1 (L = gdepth + 1); lb[L] bounds what the last level emits (nothing)
+  const int L = gdepth + 1;
+  if (xch && (int)c->lb.size() != L + 1) c->lb.assign((size_t)L + 1, c->bucket ? c->bucket : B0);
+  if (xch && c->red_cap < (size_t)(8 + L)) {
+    hipFree(c->red);
+    c->red = nullptr;
+    c->red_cap = 0;
+    uint64_t f = hipMalloc((void**)&c->red, (size_t)(8 + L) * 8) != hipSuccess ? 1 : 0;
+    const uint64_t mine = f;
+    if (int rc = h_allreduce_max(c, &f, 1)) return rc;
+    c->st[2]++;
+    if (f) {
+      hipFree(c->red);
+      c->red = nullptr;
+      return set_error(KG_ERR_RESOURCE_CODE, "sharded batch: reduction buffer (%s)", mine ? "this rank" : "another rank");
+    }
+    c->red_cap = (size_t)(8 + L);
   }
   uint32_t* counts[2] = {c->cnt, c->cnt + (N + 1)};
   uint32_t* rcv = c->cnt + 2 * (N + 1);
   unsigned long long* acc = c->acc;
-  unsigned long long* tot = c->acc + 4;
+  // tot[0..4] = (bucket overflow, visited overflow, largest bucket / bucket needed, records left, a
+  // query needs the general phase), then per exchange its largest bucket
+  unsigned long long* tot = xch ? c->red : c->acc + 4;
+  unsigned long long* lvl = xch ? c->red + 8 : nullptr;
+  const size_t nred = xch ? (size_t)(8 + L) : 5;
+  std::vector<uint64_t> h(nred + 2);
+  // reruns after a bucket overflow are bounded (kg_snapshot_tune "shard_max_reruns"); the visited table
+  // grows 4x per visited-overflow rerun up to 2^34 keys, its own bound
+  uint32_t run = 0;
   for (;;) {
-    const size_t B = c->bucket ? c->bucket : std::min<size_t>(2 * smax / N + 1024, 1ull << 26);
-    c->bucket = B;
-    if ((size_t)N * B > c->recs) {
-      for (kg_frec** p : {&c->buf[0], &c->buf[1], &c->recv}) {
-        hipFree(*p);
-        *p = nullptr;
-      }
-      c->recs = 0;
-      for (kg_frec** p : {&c->buf[0], &c->buf[1], &c->recv}) HIPC(hipMalloc((void**)p, (size_t)N * B * sizeof(kg_frec)));
-      c->recs = (size_t)N * B;
-    }
+    size_t B;
+    if (xch) B = *std::max_element(c->lb.begin(), c->lb.end());
+    else B = c->bucket ? c->bucket : B0;
+    if (!xch) c->bucket = B;
+    if (int rc = grow_run(s, c, xch, B, words)) return rc;
     HIPC(hipMemsetAsync(acc, 0, 12 * 8, st));
+    if (xch) HIPC(hipMemsetAsync(c->red, 0, (size_t)(8 + L) * 8, st));
     // both count buffers start clear: the flags word counts[k][N] accumulates over the levels that
     // write buffer k, and shard_seed / shard_level clear only what they write
     HIPC(hipMemsetAsync(c->cnt, 0, (3 * (size_t)N + 2) * 4, st));
-    if (int rc = shard_seed(s, d_q, n, gdepth, c->buf[0], B, counts[0], c->res, c->err, st)) return rc;
+    if (int rc = shard_seed(s, d_q, n, gdepth, c->buf[0], xch ? c->lb[0] : B, counts[0], c->res, c->err, st))
+      return rc;
     int cur = 0;
-    if (N == 1) {
-      // one rank: nothing to exchange -- gdepth levels back to back in the device loop (per-XCD
-      // sub-buckets, hub rows grid-wide; kg_shard_levels), hit reports stay local
+    if (!xch) {
+      // one rank, device loop: nothing to exchange -- gdepth levels back to back (per-XCD sub-buckets,
+      // hub rows grid-wide; kg_shard_levels), hit reports stay local; the loop reports the bucket
+      // size its levels needed (tot[2]), so an overflow reruns once at the right size
       kg_frec* bufs[2] = {c->buf[0], c->buf[1]};
-      if (int rc = shard_levels(s, gdepth, bufs, B, counts, 0, c->res, c->err, c->prune ? slots : 0, 0, &cur, st))
+      if (int rc = shard_levels(s, gdepth, bufs, B, counts, 0, c->res, c->err, c->prune ? slots : 0, 0, &cur, st,
+                                tot + 2))
         return rc;
       c->st[0] += (uint64_t)gdepth;
       hipLaunchKernelGGL(k_sc_final1, dim3(1), dim3(64), 0, st, counts[0], counts[1], cur, tot);
       HIPC(hipGetLastError());
     }
-    for (int k = 0; N > 1 && k <= gdepth; k++) {
-      hipLaunchKernelGGL(k_sc_acc, dim3(1), dim3(64), 0, st, counts[cur], N, (uint32_t)B, acc);
+    uint64_t wire = 0;  // bytes this rank puts on the wire (every destination but itself gets B_k records)
+    for (int k = 0; xch && k < L; k++) {
+      const size_t Bk = c->lb[(size_t)k], Bn = c->lb[(size_t)k + 1];
+      hipLaunchKernelGGL(k_sc_acc, dim3(1), dim3(64), 0, st, counts[cur], N, (uint32_t)Bk, (uint32_t)c->rank, acc,
+                         lvl + k);
       HIPC(hipGetLastError());
-      if (int rc = x_alltoall2(c, counts[cur], rcv, 4, c->buf[cur], c->recv, B * sizeof(kg_frec))) return rc;
+      if (int rc = x_alltoall2(c, counts[cur], rcv, 4, c->buf[cur], c->recv, Bk * sizeof(kg_frec))) return rc;
+      wire += (uint64_t)(N - 1) * (4 + Bk * sizeof(kg_frec));
       const uint32_t* done = nullptr;
       if (c->prune && k > 0) {
         if (int rc = shard_done(s, slots, c->res, c->err, 0, c->bits, words, st)) return rc;
         if (int rc = x_allgather(c, c->bits, c->bits_all, (size_t)words * 4)) return rc;
+        wire += (uint64_t)(N - 1) * words * 4;
         done = c->bits_all;
       }
       const int nx = cur ^ 1;
-      if (int rc = shard_level(s, c->recv, (size_t)N * B, rcv, c->buf[nx], B, counts[nx], c->res, c->err, done, words,
-                               st, N, B))
+      if (int rc = shard_level(s, c->recv, (size_t)N * Bk, rcv, c->buf[nx], Bn, counts[nx], c->res, c->err, done, words,
+                               st, N, Bk))
         return rc;
       cur = nx;
       c->st[0]++;
     }
-    if (N > 1) {
-      hipLaunchKernelGGL(k_sc_final, dim3(1), dim3(64), 0, st, counts[cur], N, (uint32_t)B, acc, tot);
+    if (xch) {
+      hipLaunchKernelGGL(k_sc_final, dim3(1), dim3(64), 0, st, counts[cur], N, (uint32_t)c->lb[(size_t)L], acc, tot);
       HIPC(hipGetLastError());
     }
     // results final before the all-reduce, which then also carries "a query needs the general phase"
@@ -644,18 +832,42 @@ int shard_check(Snapshot* s, ShardComm* c, const kg_query* d_q, size_t n, int32_
                          tot);
       HIPC(hipGetLastError());
     }
-    if (N > 1)
-      if (int rc = x_allreduce_max(c, tot, 5)) return rc;
-    uint64_t h[8];
-    HIPC(hipMemcpyAsync(h, tot, 5 * 8, hipMemcpyDeviceToHost, st));
-    HIPC(hipMemcpyAsync(h + 5, acc + 2, 8, hipMemcpyDeviceToHost, st));
+    if (xch)
+      if (int rc = x_allreduce_max(c, tot, nred)) return rc;
+    HIPC(hipMemcpyAsync(h.data(), tot, nred * 8, hipMemcpyDeviceToHost, st));
+    HIPC(hipMemcpyAsync(h.data() + nred, acc + 2, 16, hipMemcpyDeviceToHost, st));
     HIPC(hipStreamSynchronize(st));  // host round trip 2
     c->st[2]++;
-    const uint64_t big = h[2];
-    if (h[0] || h[1]) {  // dropped records somewhere: every rank reruns with more room
-      if (h[0]) {  // (one rank: the device loop does not report its largest bucket)
+    if (h[0] || h[1] || s->shard_force_overflow) {  // dropped records somewhere: every rank reruns with more room
+      const bool bucket_over = h[0] || s->shard_force_overflow;
+      if (bucket_over && run++ >= s->shard_max_reruns) {
+        drop_buffers(c);
+        return set_error(KG_ERR_RESOURCE_CODE,
+                         "sharded batch still overflows after %u reruns (bucket %zu records per destination, "
+                         "visited table 2^%d keys; kg_snapshot_tune shard_max_reruns)", run - 1, B, s->shard_vis_log2);
+      }
+      if (bucket_over) {
         c->st[3]++;
-        c->bucket = std::max<size_t>(2 * B, (size_t)(big * 1.25) + 1024);
+        if (xch) {
+          // every exchange that overflowed gets what it needed (its counter counted past B_k) plus a
+          // quarter; records it dropped were missing downstream, so the later exchanges double too
+          bool after = false;
+          for (int k = 0; k <= L; k++) {
+            const uint64_t need = k < L ? h[8 + (size_t)k] : h[2];
+            size_t& b = c->lb[(size_t)k];
+            const size_t want = std::min<size_t>((size_t)(need * 1.25) + 1024, 1ull << 30);
+            if (after) b = std::max(b, std::min<size_t>(2 * b, 1ull << 30));
+            if (need > b) {
+              b = std::max(b, want);
+              after = true;
+            }
+          }
+          if (s->shard_force_overflow) c->lb.assign(c->lb.size(), std::min<size_t>(2 * B, 1ull << 30));
+        } else {
+          // the device loop's fold reported the bucket its levels needed (0: not known -- double)
+          const uint64_t need = h[2];
+          c->bucket = need ? std::max<size_t>(B + 1024, (size_t)(need * 1.25) + 1024) : 2 * B;
+        }
       }
       if (h[1]) {
         c->st[4]++;
@@ -664,15 +876,26 @@ int shard_check(Snapshot* s, ShardComm* c, const kg_query* d_q, size_t n, int32_
       }
       continue;
     }
-    if (h[3]) return set_error(-1, "sharded batch: records left after %d levels", N > 1 ? gdepth + 1 : gdepth);
-    // next batch: buckets 25 % above the largest one this batch needed (shrinking slowly)
-    if (N > 1 && big * 2 < B) c->bucket = std::max<size_t>(1024, std::min<size_t>(B, (size_t)(big * 1.25) + 1024));
-    c->st[1] = h[5];
+    if (h[3]) return set_error(-1, "sharded batch: records left after %d levels", xch ? L : gdepth);
+    if (xch) {
+      // next batch: each exchange's bucket 25 % above what it needed this batch (shrinking slowly)
+      c->st[9] = wire;
+      for (int k = 0; k <= L; k++) {
+        const uint64_t need = k < L ? h[8 + (size_t)k] : 0;
+        size_t& b = c->lb[(size_t)k];
+        if (need * 2 < b) b = std::max<size_t>(1024, std::min<size_t>(b, (size_t)(need * 1.25) + 1024));
+      }
+      c->lvl_last.assign(h.begin() + 8, h.begin() + 8 + L);
+      c->lb_last.assign(c->lb.begin(), c->lb.begin() + L);
+    }
+    c->st[1] = h[nred];
+    c->st[8] = h[nred + 1];
     if (h[4])
       if (int rc = general_phase(s, c, d_q, n, gdepth)) return rc;
     break;
   }
-  c->st[7] = c->bucket;
+  c->st[7] = xch ? *std::max_element(c->lb.begin(), c->lb.end()) : c->bucket;
+  c->st[11] = xch ? (uint64_t)L : 0;
   if (n) {
     HIPC(hipMemcpyAsync(d_out, c->res, n, hipMemcpyDeviceToDevice, st));
     if (d_err) HIPC(hipMemcpyAsync(d_err, c->err, n * 4, hipMemcpyDeviceToDevice, st));
@@ -687,9 +910,11 @@ int shard_check(Snapshot* s, ShardComm* c, const kg_query* d_q, size_t n, int32_
   return 0;
 }
 
-// Host buffers: staged through the binding's device buffers, on the bound stream.
+// Host buffers: staged through the binding's device buffers, on the bound stream (one host batch at a
+// time per binding: the staging buffers are the binding's).
 static int shard_check_host(Snapshot* s, ShardComm* c, const kg_query* q, size_t n, int32_t gdepth, uint8_t* out,
                             uint32_t* err, kg_stats* stats) {
+  std::lock_guard<std::mutex> hl(c->host_mu);
   {
     std::lock_guard<std::mutex> lk(c->mu);
     HIPC(hipSetDevice(s->device));
@@ -721,9 +946,17 @@ static int shard_check_host(Snapshot* s, ShardComm* c, const kg_query* q, size_t
 
 int shard_check_host_entry(Snapshot* s, const kg_query* q, size_t n, int32_t gdepth, uint8_t* out, uint32_t* err,
                            kg_stats* stats) {
-  ShardComm* c = shard_comm_of(s, nullptr);
+  std::shared_ptr<ShardComm> c = shard_comm_of(s, nullptr);
   if (!c) return set_error(-2, "sharded snapshot: bind a transport to its own stream first (kg_shard_comm_init)");
-  return shard_check_host(s, c, q, n, gdepth, out, err, stats);
+  return shard_check_host(s, c.get(), q, n, gdepth, out, err, stats);
+}
+
+int shard_check_entry(Snapshot* s, hipStream_t stream, const kg_query* d_q, size_t n, int32_t gdepth, uint8_t* d_out,
+                      uint32_t* d_err, kg_stats* stats, bool* handled) {
+  std::shared_ptr<ShardComm> c = shard_comm_of(s, stream);
+  *handled = c != nullptr;
+  if (!c) return 0;
+  return shard_check(s, c.get(), d_q, n, gdepth, d_out, d_err, stats);
 }
 
 }  // namespace kg
@@ -761,11 +994,7 @@ int kg_shard_comm_init(kg_snapshot* sp, const void* id, int rank, int world, voi
       return set_error(-1, "ncclCommInitRank: %s", ncclGetErrorString(r));
     }
     c->t = kg_shard_transport{c, rank, world, 0, kg::rccl_alltoall2, kg::rccl_allgather, kg::rccl_allreduce_max};
-    if (int rc = kg::bind(s, c, (hipStream_t)stream)) {
-      delete c;
-      return rc;
-    }
-    return 0;
+    return kg::bind(s, c, (hipStream_t)stream);  // owns c
   } catch (...) {
     return set_error(-4, "kg_shard_comm_init: exception");
   }
@@ -782,11 +1011,7 @@ int kg_shard_transport_attach(kg_snapshot* sp, const kg_shard_transport* t, void
     c->rank = t->rank;
     c->world = t->world;
     c->t = *t;
-    if (int rc = kg::bind(s, c, (hipStream_t)stream)) {
-      delete c;
-      return rc;
-    }
-    return 0;
+    return kg::bind(s, c, (hipStream_t)stream);  // owns c
   } catch (...) {
     return set_error(-4, "kg_shard_transport_attach: exception");
   }
@@ -795,23 +1020,45 @@ int kg_shard_transport_attach(kg_snapshot* sp, const kg_shard_transport* t, void
 int kg_shard_comm_release(kg_snapshot* sp, void* stream) {
   if (!sp) return set_error(-2, "NULL snapshot");
   kg::Snapshot* s = reinterpret_cast<kg::Snapshot*>(sp);
+  std::shared_ptr<kg::ShardComm> gone;  // destroyed outside the lock, once no caller is inside a batch with it
   std::lock_guard<std::mutex> lk(s->comm_mu);
   for (auto it = s->comms.begin(); it != s->comms.end(); ++it)
     if ((*it)->bound == (hipStream_t)stream) {
-      delete *it;
+      gone = *it;
       s->comms.erase(it);
+      s->n_comms.store((int)s->comms.size(), std::memory_order_release);
       return 0;
     }
   return set_error(-2, "no transport bound to this stream");
 }
 
-int kg_shard_comm_stats(const kg_snapshot* sp, void* stream, uint64_t out8[8]) {
-  if (!sp || !out8) return set_error(-2, "NULL argument");
+int kg_shard_comm_stats_ex(const kg_snapshot* sp, void* stream, uint64_t* out, size_t n) {
+  if (!sp || (n && !out)) return set_error(-2, "NULL argument");
   kg::Snapshot* s = const_cast<kg::Snapshot*>(reinterpret_cast<const kg::Snapshot*>(sp));
-  kg::ShardComm* c = kg::shard_comm_of(s, (hipStream_t)stream);
+  std::shared_ptr<kg::ShardComm> c = kg::shard_comm_of(s, (hipStream_t)stream);
   if (!c) return set_error(-2, "no transport bound to this stream");
-  memcpy(out8, c->st, sizeof c->st);
+  std::lock_guard<std::mutex> lk(c->mu);
+  const size_t m = sizeof c->st / sizeof c->st[0];
+  for (size_t i = 0; i < n; i++) out[i] = i < m ? c->st[i] : 0;
   return 0;
+}
+
+int kg_shard_comm_stats(const kg_snapshot* sp, void* stream, uint64_t out8[8]) {
+  return kg_shard_comm_stats_ex(sp, stream, out8, 8);
+}
+
+int64_t kg_shard_comm_levels(const kg_snapshot* sp, void* stream, uint64_t* out, size_t cap) {
+  if (!sp || (cap && !out)) return set_error(-2, "NULL argument");
+  kg::Snapshot* s = const_cast<kg::Snapshot*>(reinterpret_cast<const kg::Snapshot*>(sp));
+  std::shared_ptr<kg::ShardComm> c = kg::shard_comm_of(s, (hipStream_t)stream);
+  if (!c) return set_error(-2, "no transport bound to this stream");
+  std::lock_guard<std::mutex> lk(c->mu);
+  const size_t L = c->lvl_last.size();
+  for (size_t k = 0; k < L && 2 * k + 1 < cap; k++) {
+    out[2 * k] = c->lb_last[k];
+    out[2 * k + 1] = c->lvl_last[k];
+  }
+  return (int64_t)L;
 }
 
 }  // extern "C"

@@ -5,6 +5,7 @@
 #include <atomic>
 #include <condition_variable>
 #include <list>
+#include <memory>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -245,9 +246,17 @@ struct Snapshot {
   // can be in flight at once; created by the first kg_shard_seed on a stream
   std::vector<ShardCtx*> shard_ctxs;
   ShardCtx* shard_ctx(hipStream_t st, bool create = true);  // st == NULL: the snapshot's stream
-  // sharded batches inside the library (kg_shard_comm.hip): a transport per stream
+  // sharded batches inside the library (kg_shard_comm.hip): a transport per stream, reference-counted
+  // (a caller inside a batch keeps its binding alive across kg_shard_comm_release / a re-bind)
   std::mutex comm_mu;
-  std::vector<ShardComm*> comms;
+  std::vector<std::shared_ptr<ShardComm>> comms;
+  std::atomic<int> n_comms{0};  // comms.size(): the replicated path's lock-free "nothing bound" test
+  int shard_force_exchange = 0;  // kg_snapshot_tune("shard_force_exchange"): one rank runs the N > 1 protocol
+  int shard_local = 1;           // kg_snapshot_tune("shard_local"): one rank runs the replica tier chain
+  uint32_t shard_max_reruns = 4;  // kg_snapshot_tune("shard_max_reruns"): overflow reruns per batch
+  uint64_t shard_max_bytes = 0;   // kg_snapshot_tune("shard_max_bytes"): bucket buffers cap (0: 1/4 of free HBM)
+  int shard_force_overflow = 0;   // kg_snapshot_tune("shard_force_overflow"): tests -- every run overflows
+  uint32_t rel_span = 0;          // 1 + the largest relation id of any node (0: not yet computed)
   ProgCopy prog_copy;  // the program the snapshot was built with (the general phase's region snapshots)
   uint32_t* shard_held = nullptr;  // holder bitmap OR-ed over every rank (kg_shard_held), or null
   uint32_t shard_held_n = 0;
@@ -350,7 +359,8 @@ int shard_level(Snapshot* s, const kg_frec* d_in, size_t n_in, const uint32_t* d
 int shard_done(Snapshot* s, size_t n, const uint8_t* d_res, const uint32_t* d_err, int with_esc, uint32_t* d_bits,
                uint32_t words, hipStream_t stream);
 int shard_levels(Snapshot* s, int levels, kg_frec* d_buf[2], size_t cap, uint32_t* d_counts[2], int start,
-                 uint8_t* d_res, uint32_t* d_err, size_t slots, int esc_mode, int* end, hipStream_t stream);
+                 uint8_t* d_res, uint32_t* d_err, size_t slots, int esc_mode, int* end, hipStream_t stream,
+                 unsigned long long* need = nullptr);  // *need: the bucket size the levels needed
 int shard_back_list(Snapshot* s, size_t n, const uint8_t* d_res, const uint32_t* d_err, kg_frec* d_list, size_t cap,
                     uint32_t* d_counts, hipStream_t stream);
 int shard_back_seed(Snapshot* s, const kg_frec* d_list, size_t m, const uint32_t* d_m, kg_frec* d_out, size_t cap,
@@ -363,12 +373,15 @@ int shard_refwd_seed(Snapshot* s, size_t n, const uint8_t* d_res, const uint32_t
 int shard_held(Snapshot* s, uint32_t* d_bits, size_t words, int import, hipStream_t stream);
 int shard_finish(Snapshot* s, size_t n, uint8_t* d_res, uint32_t* d_err, hipStream_t stream);
 size_t shard_result_slots(const Snapshot* s, size_t n);
+size_t shard_slot_limit();  // result slots one sharded batch can address (query index bits of kg_frec.q)
 int shard_bad_nodes(Snapshot* s, uint64_t* count);
 // kg_shard_comm.hip: sharded batches inside the library
 void shard_comms_free(Snapshot* s);
-ShardComm* shard_comm_of(Snapshot* s, hipStream_t st);  // the transport bound to st, or null
+std::shared_ptr<ShardComm> shard_comm_of(Snapshot* s, hipStream_t st);  // the transport bound to st, or null
 int shard_check(Snapshot* s, ShardComm* c, const kg_query* d_q, size_t n, int32_t gdepth, uint8_t* d_out,
                 uint32_t* d_err, kg_stats* stats);
+int shard_check_entry(Snapshot* s, hipStream_t st, const kg_query* d_q, size_t n, int32_t gdepth, uint8_t* d_out,
+                      uint32_t* d_err, kg_stats* stats, bool* handled);  // kg_check_batch_device on a bound stream
 int shard_expand(Snapshot* s, const kg_set* roots, size_t n, int32_t gdepth, kg_tree_buf* out);  // collective
 int shard_check_host_entry(Snapshot* s, const kg_query* q, size_t n, int32_t gdepth, uint8_t* out, uint32_t* err,
                            kg_stats* stats);  // kg_check_batch on a sharded snapshot (its own stream's binding)

@@ -69,7 +69,7 @@ __global__ void k_nmap_insert(NSlot* nm, uint64_t slots, const uint32_t* nd_ns, 
       nm[i].len = (uint32_t)(adj_off[v + 1] - adj_off[v]);
       const uint2 g = sig[v];
       nm[i].sig = g.y;
-      // node flags (k_resolve's impurity test without a random nflags read) + signature bits 0-15
+      // node flags (k_resolve's impurity test without a random nflags read) + signature bits 0-11 in bits 20-31
       nm[i].pad1 = (flags ? flags[v] : 0u) | (g.x & SIG_LO);
       return;
     }

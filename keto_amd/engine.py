@@ -188,7 +188,13 @@ class Snapshot:
         return {"union_nodes": int(a[0]), "new_nodes": int(a[1]), "check_rows": int(a[2])}
 
     def tune(self, key: str, value: int) -> None:
-        """Engine knobs (kg_snapshot_tune): "tiers" = 0 grid / 1 LDS workgroup + grid / 2 workgroup tiers."""
+        """Engine knobs (kg_snapshot_tune; keto_amd/csrc/kg_abi.cpp tune_one lists them with their ranges):
+        tier chain -- back, back_wgs, back_edges, stream_ecap, stream_wgs, stream_steal, stream_chunk,
+        resolve_unheld, grid_wgs, grid_bidir, grid_cap, grid_reserve, grid_ms, grid_ms_words, grid_ms_bytes,
+        grid_ms_tg_cap, grid_ms_cap, interp_wgs, interp_cap2, device_sync, host_sync, max_lanes;
+        expand -- expand_tail; hash-sharded -- shard_local, shard_force_exchange, shard_max_reruns,
+        shard_max_bytes, shard_force_overflow (tests), shard_bucket, shard_vis, shard_vis_mode, shard_wgs,
+        shard_heavy, shard_pack, shard_budget, shard_back_budget."""
         _lib.check(_lib.load().kg_snapshot_tune(self._h, key.encode(), int(value)), "kg_snapshot_tune")
         self.__dict__.setdefault("tuned", {})[key] = int(value)  # what the Python drivers need to know
 

@@ -320,12 +320,23 @@ class LibShardedChecker:
             raise ValueError("sharded expand runs on the snapshot's own stream (snapshot_stream=True)")
         return ExpandEngine(self.snapshot, Config(gdepth)).build_trees_ids(roots)
 
+    STAT_KEYS = ("levels", "records_sent", "host_syncs", "reruns_bucket", "reruns_visited", "general_queries",
+                 "general_rows", "bucket", "records_to_peers", "wire_bytes", "path", "exchanges")
+    PATHS = {0: "local-first (replica tier chain)", 1: "one-rank device level loop", 2: "exchange protocol"}
+
     def stats(self) -> dict:
-        out = (C.c_uint64 * 8)()
-        _lib.check(self.L.kg_shard_comm_stats(self.snapshot.handle, self._sp, out), "kg_shard_comm_stats")
-        keys = ("levels", "records_sent", "host_syncs", "reruns_bucket", "reruns_visited", "general_queries",
-                "general_rows", "bucket")
-        return dict(zip(keys, (int(x) for x in out)))
+        """kg_shard_comm_stats_ex of the last batch (include/ketogpu.h)."""
+        out = (C.c_uint64 * 16)()
+        _lib.check(self.L.kg_shard_comm_stats_ex(self.snapshot.handle, self._sp, out, 16), "kg_shard_comm_stats_ex")
+        return dict(zip(self.STAT_KEYS, (int(x) for x in out)))
+
+    def levels(self) -> list:
+        """Per exchange of the last batch: (B_k records per destination, largest bucket)."""
+        out = (C.c_uint64 * 256)()
+        n = int(self.L.kg_shard_comm_levels(self.snapshot.handle, self._sp, out, 256))
+        if n < 0:
+            _lib.check(n, "kg_shard_comm_levels")
+        return [(int(out[2 * k]), int(out[2 * k + 1])) for k in range(min(n, 128))]
 
     def close(self):
         if self.snapshot.handle:

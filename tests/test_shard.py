@@ -6,6 +6,7 @@ sizes, the all-to-all of records, hit reports to the home rank, termination and 
 rerun.  GPU: the HIP local steps (kg_shard_seed / kg_shard_level) at world_size 1 and 2 (two
 processes on one GPU, gloo exchange) against the same oracle, bit-exact."""
 import os
+import time
 import socket
 import sys
 
@@ -177,12 +178,14 @@ class _LibAdapter:
         from keto_amd.sharded import LibShardedChecker
         self.chk = LibShardedChecker(snap, rank, world, dist_, transport=transport)
         self.levels = self.host_syncs = self.back_levels = self.general_queries = 0
+        self.path = None
         self.reruns = {1: 0, 2: 0}
 
     def check(self, dq, gmax):
         r = self.chk.check(dq, gmax)
         st = self.chk.stats()
         self.levels = st["levels"]
+        self.path = st["path"]
         self.host_syncs += st["host_syncs"]
         self.reruns[1] += st["reruns_bucket"]
         self.reruns[2] += st["reruns_visited"]
@@ -190,14 +193,27 @@ class _LibAdapter:
         return r
 
 
+# (host round trips, levels) of a clean in-library batch by path: local-first tier chain, one-rank device
+# level loop, exchange protocol (gdepth + 1 exchanges; the agreement all-reduce and the end-of-batch one)
+LIB_PATH_COST = {0: lambda g: (0, 0), 1: lambda g: (1, g), 2: lambda g: (2, g + 1)}
+
+
 def _checker(driver, snap, rank, world, dist_, cap=256):
-    """driver "py": keto_amd.sharded.ShardedChecker over the kg_shard_* steps; "lib": the in-library batch
-    over RCCL (world 1) or the gloo host transport (world > 1: ranks share the one GPU, which RCCL does
-    not allow); "lib-rccl" / "lib-host": that transport explicitly."""
+    """driver "py": keto_amd.sharded.ShardedChecker over the kg_shard_* steps; "lib[-rccl|-host][-loop]
+    [-forced]": the in-library batch over RCCL (default at world 1) or the gloo host transport (default at
+    world > 1: ranks share the one GPU, which RCCL does not allow).  World 1 runs local-first (the replica
+    tier chain) unless "-loop" (kg_snapshot_tune shard_local 0: the one-rank device level loop) or
+    "-forced" (shard_force_exchange 1: the N > 1 exchange protocol over the transport, each rank its own
+    peer)."""
     from keto_amd.sharded import HipShardOps, ShardedChecker
     if driver == "py":
         return ShardedChecker(HipShardOps(snap), rank, world, dist_, device="cuda", cap=cap)
-    transport = driver.split("-")[1] if "-" in driver else ("rccl" if world == 1 else "host")
+    parts = driver.split("-")
+    transport = "rccl" if "rccl" in parts else ("host" if "host" in parts else ("rccl" if world == 1 else "host"))
+    if "loop" in parts:
+        snap.tune("shard_local", 0)
+    if "forced" in parts:
+        snap.tune("shard_force_exchange", 1)
     return _LibAdapter(snap, rank, world, dist_, transport)
 
 
@@ -571,7 +587,8 @@ def _synth_worker(rank, world, port, n_tuples, n_q, gmax, backend, outq, preset=
     res, err = chk.check(mq, gmax)
     assert (res.cpu().numpy() == res0).all() and (err.cpu().numpy() == err0).all()  # the rerun batch = a clean one
     outq.put((rank, mine, res.cpu().numpy(), err.cpu().numpy(), chk.levels, chk.host_syncs - s0,
-              dq.cpu().numpy() if rank == 0 else None, snap.materialized(), chk.back_levels, dict(chk.reruns)))
+              dq.cpu().numpy() if rank == 0 else None, snap.materialized(), chk.back_levels, dict(chk.reruns),
+              getattr(chk, "path", None)))
     if dist_:
         dist.destroy_process_group()
 
@@ -645,14 +662,16 @@ def _run_synth(world, backend, n_tuples, n_q, gmax, preset, budget=None, back_bu
     exp, oerr, _ = o.check_batch(q[:, :6], q[:, 6].view(np.int32), gmax, POLICY_CANONICAL, nthreads=8)
     assert (oerr == 0).all()
     res = np.zeros(n_q, np.uint8)
-    for rank, mine, r, e, levels, syncs, _, mat, back_levels, reruns in got:
+    for rank, mine, r, e, levels, syncs, _, mat, back_levels, reruns, path in got:
         assert (e == 0).all(), (rank, np.nonzero(e)[0][:10])
         res[mine] = r
         if world == 1 and backend is None and driver == "py":
             assert syncs == 1 and levels == gmax  # one host round trip for the whole batch
-        if driver != "py":  # in-library: the agreement all-reduce and the end-of-batch one, no rerun
-            # (one rank: only the end-of-batch readback, gdepth levels in the device loop)
-            assert (syncs, levels) == ((1, gmax) if world == 1 else (2, gmax + 1)), (syncs, levels)
+        if driver != "py":  # in-library, no rerun: the path's host round trips and levels
+            want = 0 if (world == 1 and "loop" not in driver and "forced" not in driver) else (
+                1 if world == 1 and "loop" in driver else 2)
+            assert path == want, (path, want, driver)
+            assert (syncs, levels) == LIB_PATH_COST[path](gmax), (syncs, levels, path)
         if budget is not None and budget <= 8 and not preset:
             assert back_levels > 0  # the backward phase ran
         if preset:
@@ -668,14 +687,21 @@ def _run_synth(world, backend, n_tuples, n_q, gmax, preset, budget=None, back_bu
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("world,backend,preset,driver", [(1, None, 0, "lib"), (1, None, 1, "lib"),
+                                                         (1, None, 0, "lib-loop"), (1, None, 1, "lib-loop"),
+                                                         (1, None, 0, "lib-rccl-forced"),
+                                                         (1, None, 1, "lib-rccl-forced"),
                                                          (2, "gloo", 0, "lib"), (2, "gloo", 1, "lib"),
-                                                         (1, "gloo", 0, "lib-host")])
+                                                         (1, "gloo", 0, "lib-host"), (1, "gloo", 0, "lib-host-forced")])
 def test_sharded_in_library_vs_oracle(world, backend, preset, driver):
     """The hash-sharded batch inside libketogpu.so (kg_shard_comm.hip: one kg_check_batch_device call per
     batch, as a Go host makes it): C4's generator (preset 0) and C3's (preset 1: union nodes across ranks,
-    split formulas) at world 1 over RCCL and at world 2 over the gloo host transport (two ranks on one
-    GPU), bit-exact with the oracle on the whole graph; two host round trips per batch, gdepth + 1 levels
-    (one rank: one round trip, gdepth levels in the device loop)."""
+    split formulas), bit-exact with the oracle on the whole graph:
+      world 1 local-first -- the replica tier chain on the rank's rows (no level protocol, no round trip);
+      world 1 "-loop" -- the one-rank device level loop (one round trip, gdepth levels);
+      world 1 "-rccl-forced" -- the N > 1 exchange protocol over a real RCCL communicator (self send /
+        recv, all-gather, all-reduce: the transport code of an 8-GPU run, on one GPU; VERDICT r4 item 1);
+      world 2 over the gloo host transport (two ranks on one GPU) and world 1 "-host-forced";
+    the exchange protocol: two host round trips per batch, gdepth + 1 exchanges."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     _run_synth(world, backend, 300_000 if preset == 0 else 150_000, 20_000 if preset == 0 else 6000, 10, preset=preset,
@@ -686,7 +712,7 @@ def test_sharded_in_library_vs_oracle(world, backend, preset, driver):
 @pytest.mark.parametrize("world,backend,vis,bucket", [(1, None, 10, None), (2, "gloo", 10, None),
                                                       (2, "gloo", None, 64), (1, "nccl", 11, None),
                                                       ("lib", None, 10, None), ("lib", None, None, 64),
-                                                      ("lib2", "gloo", 10, 64)])
+                                                      ("lib-forced", None, 10, 64), ("lib2", "gloo", 10, 64)])
 def test_sharded_visited_overflow_reruns(world, backend, vis, bucket):
     """Regression (round 3: "records left after 10 levels" on C3 sharded, an overflow flag OR-ed into a
     sub-bucket count in kg_shard.hip): a C3-shaped graph with a per-batch (query, node) visited table
@@ -697,9 +723,191 @@ def test_sharded_visited_overflow_reruns(world, backend, vis, bucket):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     driver = "py"
-    if world in ("lib", "lib2"):  # the same through the in-library batch (kg_shard_comm.hip)
-        driver, world = "lib", (1 if world == "lib" else 2)
+    if world in ("lib", "lib2"):  # the same through the in-library batch (kg_shard_comm.hip; world 1: its
+        # device level loop -- local-first never builds the per-batch (query, node) table or buckets)
+        driver, world = ("lib-loop", 1) if world == "lib" else ("lib", 2)
+    elif world == "lib-forced":  # world 1, the exchange protocol over RCCL
+        driver, world = "lib-rccl-forced", 1
     _run_synth(world, backend, 150_000, 6000, 10, preset=1, vis=vis, bucket=bucket, driver=driver)
+
+
+def _bound_worker(rank, world, port, outq, driver, mode):
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+    from keto_amd import _lib
+    from keto_amd.engine import Snapshot
+    dist_ = None
+    torch.cuda.set_device(0)
+    if world > 1:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dist_ = dist
+    snap = Snapshot.synthetic(150_000, seed=20250131, shard=(rank, world))
+    n_q = 8000
+    dq = torch.empty((n_q, 7), dtype=torch.int32, device="cuda")
+    _lib.check(_lib.load().kg_synth_queries(snap.handle, 77, n_q, dq.data_ptr()), "kg_synth_queries")
+    mine = np.array_split(np.arange(n_q), world)[rank]
+    mq = dq[mine[0]:mine[-1] + 1].contiguous()
+    snap.tune("shard_bucket", 64)  # far too small: the first run overflows
+    if mode == "overflow":  # every run reports a bucket overflow: a persistent one
+        snap.tune("shard_force_overflow", 1)
+        snap.tune("shard_max_reruns", 3)
+    else:  # the bucket the batch needs is over the buffer cap
+        snap.tune("shard_max_bytes", 1 << 16)
+    chk = _checker(driver, snap, rank, world, dist_)
+    t0 = time.time()
+    try:
+        chk.check(mq, 10)
+        outcome = "ok"
+    except _lib.KetoGPUError as e:
+        outcome = str(e)
+    took = time.time() - t0
+    # the binding stays usable: the same batch with sane limits
+    snap.tune("shard_force_overflow", 0)
+    snap.tune("shard_max_bytes", 0)
+    res, err = chk.check(mq, 10)
+    outq.put((rank, outcome, took, mine, res.cpu().numpy(), err.cpu().numpy(), dq.cpu().numpy() if rank == 0 else None))
+    if dist_:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("driver,world", [("lib-loop", 1), ("lib-rccl-forced", 1), ("lib", 2)])
+@pytest.mark.parametrize("mode", ["overflow", "bytes"])
+def test_sharded_rerun_bound(driver, world, mode):
+    """the overflow rerun loop is bounded.  A persistent bucket overflow
+    (kg_snapshot_tune shard_force_overflow) ends after shard_max_reruns reruns, and a bucket larger than
+    the buffer cap (shard_max_bytes) ends at once -- every rank returns KG_ERR_RESOURCE (-4) together, in
+    seconds, with no out-of-memory and no rank left waiting in a collective; the binding then answers the
+    same batch bit-exact with the oracle.  World 1 in the device loop and over RCCL (the exchange
+    protocol), world 2 over gloo."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from keto_amd.engine import Snapshot
+    ctx = mp.get_context("spawn")
+    outq = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_bound_worker, args=(r, world, port, outq, driver, mode)) for r in range(world)]
+    for p in ps:
+        p.start()
+    got = [outq.get(timeout=110) for _ in range(world)]
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    want = "after 3 reruns" if mode == "overflow" else "cap"
+    for rank, outcome, took, *_ in got:
+        assert "(-4)" in outcome and want in outcome, (rank, outcome)
+        assert took < 60, took
+    q = [g[6] for g in got if g[6] is not None][0].view(np.uint32)
+    full = Snapshot.synthetic(150_000, seed=20250131)
+    exp = _expected(full.export(), 0xFFFFFFFF, q, 10)
+    res = np.zeros(len(q), np.uint8)
+    for _, _, _, mine, r, e, _ in got:
+        assert (e == 0).all()
+        res[mine] = r
+    bad = np.nonzero(res != exp)[0]
+    assert bad.size == 0, bad[:8]
+
+
+def _nodict_graph():
+    """Rows in a relation no dict and no program names (the dict is NULL, so the snapshot's relation count
+    comes from the program): n1:b#zz@u1 decides n1:a#r2@u1 (r2 = computed r0, r0 -> (n1:b#zz)) through
+    checkDirect before astRelationFor's error for the undeclared zz (engine.go:183-207) -- only when the
+    general phase's region gather brings the zz rows (gather_region asked for relations
+    [0, n_rel) only)."""
+    sys.path.insert(0, ROOT)
+    from keto_amd.engine import queries_array
+    from keto_amd.ketoapi import RelationTuple
+    from keto_amd.mapper import Interner
+    from keto_amd.namespace import ComputedSubjectSet, Namespace, Relation, SubjectSetRewrite, compile_program
+    it = Interner()
+    nss = [Namespace("n1", [Relation("r0"), Relation("r1"), Relation("r2", rewrite=SubjectSetRewrite([
+        ComputedSubjectSet("r0")]))])]
+    prog = compile_program(nss, it)
+    rows = []
+    for i in range(40):
+        rows += [f"n1:a{i}#r0@(n1:b{i}#zz)", f"n1:b{i}#zz@u{i % 7}", f"n1:a{i}#r1@u{(i + 1) % 7}",
+                 f"n1:c{i}#r0@(n1:a{(i + 3) % 40}#r2)"]
+    tuples = [RelationTuple.from_string(x) for x in rows]
+    t6 = it.tuples_array(tuples)
+    assert it.rel_id("zz") > max(it.rel_id(r) for r in ("r0", "r1", "r2"))
+    qs = []
+    for i in range(40):
+        for u in range(8):
+            for rel, obj in (("r2", "a"), ("r0", "c"), ("r0", "a")):
+                qs.append(RelationTuple.from_string(f"n1:{obj}{i}#{rel}@u{u}"))
+    q6 = np.asarray([it.tuple_ids(t) for t in qs], np.uint32)
+    return it, t6, queries_array(q6, np.zeros(len(qs), np.int64)), prog
+
+
+def _nodict_worker(rank, world, port, outq, driver):
+    sys.path.insert(0, ROOT)
+    import ctypes as C
+    import torch.distributed as dist
+    from keto_amd import _lib
+    from keto_amd.engine import Snapshot
+    dist_ = None
+    torch.cuda.set_device(0)
+    if world > 1:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dist_ = dist
+    it, t6, q, prog = _nodict_graph()
+    L = _lib.load()
+    holder = Snapshot(None, it, prog, 0, _handle=C.c_void_p(), shard=(rank, world))
+    pc = holder._prog(prog)
+    t = np.ascontiguousarray(t6, np.uint32)
+    h = C.c_void_p()
+    _lib.check(L.kg_snapshot_create_shard(t.ctypes.data_as(C.c_void_p), t.shape[0], None, C.byref(pc), 0, rank, world,
+                                          C.byref(h)), "kg_snapshot_create_shard (NULL dict)")
+    holder._h = h
+    mine = np.array_split(np.arange(len(q)), world)[rank]
+    chk = _checker(driver, holder, rank, world, dist_)
+    out = {}
+    for gmax in (3, 6):
+        res, err = chk.check(torch.from_numpy(q[mine].view(np.int32).copy()).cuda(), gmax)
+        out[gmax] = (mine, res.cpu().numpy(), err.cpu().numpy())
+    outq.put((rank, out, chk.general_queries))
+    if dist_:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,driver", [(1, "lib-rccl-forced"), (2, "lib"), (1, "lib")])
+def test_sharded_general_phase_null_dict(world, driver):
+    """a snapshot created with a NULL dict whose rows use a relation the program never
+    names.  The general phase gathers every relation's rows of an object (rel_span: 1 + the largest
+    relation id of any node), so the answers and error codes equal the oracle's on the program as
+    written; world 1 local-first answers without any gather."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from oracle.oracle import POLICY_CANONICAL, Oracle
+    ctx = mp.get_context("spawn")
+    outq = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_nodict_worker, args=(r, world, port, outq, driver)) for r in range(world)]
+    for p in ps:
+        p.start()
+    got = [outq.get(timeout=110) for _ in range(world)]
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    it, t6, q, prog = _nodict_graph()
+    o = Oracle(t6, 0xFFFFFFFF, prog)
+    if driver != "lib" or world > 1:
+        assert sum(g[2] for g in got) > 0  # the general phase answered some
+    for gmax in (3, 6):
+        exp, oerr, _ = o.check_batch(q[:, :6], q[:, 6].view(np.int32), gmax, POLICY_CANONICAL)
+        res = np.zeros(len(q), np.uint8)
+        err = np.zeros(len(q), np.int64)
+        for _, out, _ in got:
+            mine, r, e = out[gmax]
+            res[mine], err[mine] = r, e
+        bad = np.nonzero((res != exp) | (err != oerr))[0]
+        assert bad.size == 0, [(q[i].tolist(), int(res[i]), int(exp[i]), int(err[i]), int(oerr[i])) for i in bad[:8]]
+        assert (exp == 1).any() and (oerr != 0).any()
 
 
 @pytest.mark.gpu
