@@ -53,6 +53,8 @@ def parse(argv=None):
     ap.add_argument("--batch", type=int, default=1_000_000, help="checks per step per GPU")
     ap.add_argument("--global-depth", type=int, default=10)
     ap.add_argument("--seed", type=int, default=20250131)
+    ap.add_argument("--stream-gate", type=int, default=0,
+                    help="kg_snapshot_tune stream_gate: k_stream4 launches of different batches at once (0 = no cap)")
     ap.add_argument("--stream-ecap", type=int, default=512, help="kg_snapshot_tune stream_ecap (stream-tier edges per query, 0 = none)")
     ap.add_argument("--sharded-steps", type=int, default=20,
                     help="check mode: timed batches of the hash-sharded sub-line (the C4 engine through "
@@ -183,6 +185,8 @@ def apply_tune(snap, a) -> None:
     the parity test with exactly this set)."""
     snap.tune("back", a.back)
     snap.tune("stream_ecap", a.stream_ecap)
+    if a.stream_gate:
+        snap.tune("stream_gate", a.stream_gate)
     if a.resolve_unheld != 1:
         snap.tune("resolve_unheld", a.resolve_unheld)
     snap.tune("device_sync", a.device_sync)
@@ -307,8 +311,35 @@ def bench_expand(a):
             L.kg_tree_free(C.byref(buf))
         out["largest_root"] = {"records": n_big, "walk_kernel_ms": float(min(walk)),
                                "expand_tail": a.expand_tail}
+    # roofline of the expand launch chain (8 B per row opened, 4 B per edge read, 12 B per
+    # emitted tree node), from one more call's records (every step expands the same roots) over the
+    # calls' mean device time (HIP events around k_expand_lds / _hash / _hbm + k_expand_compact on the
+    # call's stream; several calls overlap, so a call's time is contended wall time)
+    buf = _lib.kg_tree_buf()
+    _lib.check(L.kg_expand_batch(snap.handle, roots.ctypes.data_as(C.c_void_p), a.roots, depth, C.byref(buf)),
+               "kg_expand_batch")
+    rec = np.ctypeslib.as_array(C.cast(buf.nodes, C.POINTER(C.c_uint8)), shape=(int(buf.n_nodes) * 20,)).view(
+        np.dtype([("type", "u1"), ("is_set", "u1"), ("pad", "<u2"), ("ns", "<u4"), ("obj", "<u4"), ("rel", "<u4"),
+                  ("n_children", "<u4")])) if buf.n_nodes else None
+    L.kg_tree_free(C.byref(buf))
+    if rec is not None:
+        unions = rec["type"] == 1  # kg_tree_node type 1 = union (include/ketogpu.h)
+        R, E, T = int(unions.sum()), int(rec["n_children"][unions].sum()), int(len(rec))
+        byts = 8 * R + 4 * E + 12 * T
+        ms = kms / a.steps
+        out["roofline"] = {"kernel": "k_expand_lds/_hash/_hbm + k_expand_compact (one call's chain)", "bound": "hbm",
+                           "achieved": byts / (ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                           "frac": byts / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "traffic": None,
+                           "bytes_model": "8*unions(rows opened) + 4*children(edges read) + 12*tree records",
+                           "bytes_per_call": byts, "rows_opened": R, "edges_read": E, "records": T,
+                           "call_kernel_ms": ms}
+    orc = None
+    if rank == 0 and ((a.parity_roots > 0 and off is not None) or (world == 1 and a.cpu_seconds > 0)):
+        orc = expand_oracle(snap)
     if rank == 0 and a.parity_roots > 0 and off is not None:
-        out["parity"] = expand_parity(snap, roots, np.diff(off.astype(np.int64)), depth, a)
+        out["parity"] = expand_parity(snap, roots, np.diff(off.astype(np.int64)), depth, a, orc)
+    if rank == 0 and world == 1 and a.cpu_seconds > 0:
+        out["cpu_baseline"] = expand_cpu_baseline(orc, roots, depth, a)
     if rank == 0:
         print(json.dumps(out), flush=True)
         if out.get("parity") and out["parity"]["mismatches"]:
@@ -320,12 +351,10 @@ def bench_expand(a):
         dist.destroy_process_group()
 
 
-def expand_parity(snap, roots: np.ndarray, sizes: np.ndarray, depth: int, a) -> dict:
-    """C5 trees vs the oracle's BuildTree (oracle/keto_oracle.c, expand/engine.go:35-104) on the snapshot's
-    own rows: the 10 largest roots of the timed batch plus a seeded sample of the rest, same pre-order and
-    same child order (rows are in shard order on both sides)."""
+def expand_oracle(snap):
+    """The oracle (oracle/keto_oracle.c) over the snapshot's own rows in shard order, for the C5 parity
+    leg and CPU baseline; its node arrays ride along as .nd."""
     from keto_amd import _lib
-    from keto_amd.engine import ExpandEngine, Config
     from oracle.oracle import Oracle
     L = _lib.load()
     t0 = time.perf_counter()
@@ -338,7 +367,57 @@ def expand_parity(snap, roots: np.ndarray, sizes: np.ndarray, depth: int, a) -> 
     _lib.check(L.kg_snapshot_export_csr(snap.handle, p(row_off), p(row_subj), p(nd[0]), p(nd[1]), p(nd[2])),
                "kg_snapshot_export_csr")
     orc = Oracle.from_csr(0, nd[0], nd[1], nd[2], row_off, row_subj, nthreads=16)
-    del row_subj
+    orc.nd = nd
+    orc.build_s = time.perf_counter() - t0
+    return orc
+
+
+def expand_cpu_baseline(orc, roots: np.ndarray, depth: int, a) -> dict:
+    """BuildTree (oracle/keto_oracle.c ko_expand_node: expand/engine.go:35-104, one visited set per request,
+    rows in shard order) over the C5 roots on the host cores: a bounded sample of the same roots (grown
+    until ~--cpu-seconds of work), at the usable CPU count (ctypes releases the GIL: one root per call,
+    a thread pool) and at 1 thread."""
+    from concurrent.futures import ThreadPoolExecutor
+    cpus = effective_cpus()
+    eff = cpus["effective"]
+
+    def run(n, th):
+        t = time.perf_counter()
+        nodes = [int(r[1]) for r in roots[:n]]  # synthetic group#member: node id == object id
+        dp = [int(np.int32(np.uint32(r[3]))) for r in roots[:n]]
+        if th == 1:
+            for x, d in zip(nodes, dp):
+                orc.expand_node(x, d, depth)
+        else:
+            with ThreadPoolExecutor(th) as ex:
+                list(ex.map(lambda xd: orc.expand_node(xd[0], xd[1], depth), zip(nodes, dp)))
+        return time.perf_counter() - t
+
+    res = {}
+    for th, budget in ((eff, a.cpu_seconds / 2), (1, a.cpu_seconds / 4)):
+        n = 64
+        t = run(n, th)
+        while t < budget / 4 and n < len(roots):
+            n = min(len(roots), n * 4)
+            t = run(n, th)
+        res[th] = (n / t, n, t)
+    best = max(res, key=lambda k: res[k][0])
+    v, n, t = res[best]
+    return {"value": v, "unit": "trees/s", "cores": best, "kind": "port",
+            "sample": f"the first {n} of the {len(roots)} C5 roots ({t:.1f} s), BuildTree with one visited set per "
+                      f"request (oracle/keto_oracle.c ko_expand_node), {best} host threads (best of {sorted(res)})",
+            "by_threads": {str(k): r[0] for k, r in sorted(res.items())}, "value_1thread": res[1][0],
+            "cpus": cpus, "host_cpu": host_cpu()}
+
+
+def expand_parity(snap, roots: np.ndarray, sizes: np.ndarray, depth: int, a, orc=None) -> dict:
+    """C5 trees vs the oracle's BuildTree (oracle/keto_oracle.c, expand/engine.go:35-104) on the snapshot's
+    own rows: the 10 largest roots of the timed batch plus a seeded sample of the rest, same pre-order and
+    same child order (rows are in shard order on both sides)."""
+    from keto_amd.engine import ExpandEngine, Config
+    t0 = time.perf_counter()
+    orc = orc or expand_oracle(snap)
+    nd = orc.nd
     rng = np.random.default_rng(a.seed)
     top = np.argsort(sizes)[-10:]
     rest = rng.choice(len(roots), size=min(len(roots), max(0, a.parity_roots - 10)), replace=False)
@@ -1261,10 +1340,63 @@ def host_path(L, snap, dq_all, n_distinct, a, P) -> dict:
     if errors:
         raise errors[0]
     ms = np.array(lat) * 1e3
-    return {"value": B * a.host_calls * P / el, "unit": "checks/s", "callers": P, "calls": len(lat),
-            "checks_per_call": B, "p50_call_ms": float(np.percentile(ms, 50)),
-            "p99_call_ms": float(np.percentile(ms, 99)),
-            "what": "kg_check_batch on 1 M-check host batches: PCIe both ways included (not the headline value)"}
+    dense = {"value": B * a.host_calls * P / el, "unit": "checks/s", "callers": P, "calls": len(lat),
+             "checks_per_call": B, "p50_call_ms": float(np.percentile(ms, 50)),
+             "p99_call_ms": float(np.percentile(ms, 99)),
+             "bytes_per_check": {"in": 28, "out": 5},
+             "what": "kg_check_batch on 1 M-check host batches: PCIe both ways included (not the headline value)"}
+    # the narrow boundary: kg_check_batch_packed (16-B queries in, 1-B answers out, error codes sparse),
+    # every answer checked against the dense call's
+    pks = [_lib.pack_queries(x) for x in qs]
+    ref = []
+    lat2, errors = [], []
+    ready = threading.Barrier(P + 1)
+
+    def worker2(p):
+        try:
+            o = np.empty(B, np.uint8)
+            idx = np.empty(1024, np.uint32)
+            code = np.empty(1024, np.uint32)
+            ne = C.c_size_t(0)
+
+            def call():
+                _lib.check(L.kg_check_batch_packed(snap.handle, pks[p].ctypes.data_as(C.c_void_p), B, a.global_depth,
+                                                   o.ctypes.data_as(C.c_void_p), idx.ctypes.data_as(C.c_void_p),
+                                                   code.ctypes.data_as(C.c_void_p), 1024, C.byref(ne), None),
+                           "kg_check_batch_packed")
+            call()
+            ready.wait()
+            for _ in range(a.host_calls):
+                s0 = time.perf_counter()
+                call()
+                lat2.append(time.perf_counter() - s0)
+            ref.append((p, o.copy(), int(ne.value)))
+        except Exception as x:  # noqa: BLE001
+            errors.append(x)
+            ready.abort()
+
+    th = [threading.Thread(target=worker2, args=(p,)) for p in range(P)]
+    [t.start() for t in th]
+    ready.wait()
+    t0 = time.perf_counter()
+    [t.join() for t in th]
+    el2 = time.perf_counter() - t0
+    if errors:
+        raise errors[0]
+    # answers of the packed calls vs kg_check_batch on the same host batch
+    o = np.empty(B, np.uint8)
+    e = np.empty(B, np.uint32)
+    mism = 0
+    for p, got, ne in ref:
+        _lib.check(L.kg_check_batch(snap.handle, qs[p].ctypes.data_as(C.c_void_p), B, a.global_depth,
+                                    o.ctypes.data_as(C.c_void_p), e.ctypes.data_as(C.c_void_p), None), "kg_check_batch")
+        mism += int((got != o).sum()) + abs(ne - int((o == 2).sum()))
+    ms2 = np.array(lat2) * 1e3
+    dense["packed"] = {"value": B * a.host_calls * P / el2, "unit": "checks/s", "callers": P, "calls": len(lat2),
+                       "p50_call_ms": float(np.percentile(ms2, 50)), "p99_call_ms": float(np.percentile(ms2, 99)),
+                       "bytes_per_check": {"in": 16, "out": 1}, "mismatches_vs_dense": mism,
+                       "what": "kg_check_batch_packed (kg_query_packed in, answers + sparse error codes out)"}
+    return dense
 
 
 class CheckOracle:

@@ -49,6 +49,33 @@ typedef struct {
   int32_t max_depth;
 } kg_query;
 
+/* The same request in 16 bytes (kg_check_batch_packed: the host boundary moves 16 B per check in
+ * instead of 28).  Namespace and relation ids < 4095 (KG_PACK_ID_MAX), the subject-id marker
+ * KG_PACK_SUBJECT_ID in the subject namespace field, request max-depth 0..65535 (0: use global; the
+ * configured max_read_depth's own range, embedx/config.schema.json:308-315; a negative depth is 0):
+ *   obj, sobj  as in kg_tuple
+ *   w2         ns (bits 0-11) | rel (bits 12-23) | sns bits 0-7 (bits 24-31)
+ *   w3         sns bits 8-11 (bits 0-3) | srel (bits 4-15) | max_depth (bits 16-31) */
+typedef struct {
+  uint32_t obj, sobj, w2, w3;
+} kg_query_packed;
+#define KG_PACK_ID_MAX 4094u
+#define KG_PACK_SUBJECT_ID 4095u
+/* Returns 0, or -2 when an id does not fit (use kg_check_batch). */
+static inline int kg_pack_query(const kg_query* q, kg_query_packed* p) {
+  const uint32_t sns = q->t.sns == 0xFFFFFFFFu ? KG_PACK_SUBJECT_ID : q->t.sns;
+  const uint32_t srel = q->t.sns == 0xFFFFFFFFu ? 0u : q->t.srel;
+  const uint32_t d = q->max_depth <= 0 ? 0u : (q->max_depth > 65535 ? 65535u : (uint32_t)q->max_depth);
+  if (q->t.ns > KG_PACK_ID_MAX || q->t.rel > KG_PACK_ID_MAX || (sns != KG_PACK_SUBJECT_ID && sns > KG_PACK_ID_MAX) ||
+      srel > KG_PACK_ID_MAX)
+    return -2;
+  p->obj = q->t.obj;
+  p->sobj = q->t.sobj;
+  p->w2 = q->t.ns | (q->t.rel << 12) | ((sns & 0xFFu) << 24);
+  p->w3 = (sns >> 8) | (srel << 4) | (d << 16);
+  return 0;
+}
+
 /* An expand root: a subject set, or a subject id (sns = KG_SUBJECT_ID) -- BuildTree's Subject. */
 typedef struct {
   uint32_t sns, sobj, srel;
@@ -275,6 +302,14 @@ int kg_snapshot_export_csr(const kg_snapshot* s, uint64_t* row_off, uint32_t* ro
  * The batch is split over the replicas in contiguous chunks of >= 16384 queries. */
 int kg_check_batch(kg_snapshot* s, const kg_query* q, size_t n, int32_t global_max_depth, uint8_t* out,
                    uint32_t* err_code, kg_stats* stats);
+/* kg_check_batch with the narrow boundary (round 5): 16-B packed queries in (kg_query_packed, unpacked
+ * on the device), 1 B per answer out, and the error codes only of the checks answered KG_ERROR, as a
+ * sparse list: *n_err = how many there are; the first min(n_err, err_cap) of them, by ascending index,
+ * in err_index[] / err_code[] (both may be NULL when err_cap is 0).  Same engine, answers and
+ * threading as kg_check_batch: the reference's BatchCheck (one CheckIsMember per request,
+ * internal/check/engine.go:54-60; error codes as kg_check_batch's err_code). */
+int kg_check_batch_packed(kg_snapshot* s, const kg_query_packed* q, size_t n, int32_t global_max_depth, uint8_t* out,
+                          uint32_t* err_index, uint32_t* err_code, size_t err_cap, size_t* n_err, kg_stats* stats);
 /* Device-resident variant (replica 0 only: the pointers belong to its device): d_q / d_out / d_err are device pointers (HBM), stream is a
  * hipStream_t (NULL = the snapshot's stream).  Returns once the batch is enqueued; when queries
  * reach the grid tier the call waits for the wave tiers (the grid tier's size is read back), and

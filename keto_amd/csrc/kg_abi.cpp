@@ -412,6 +412,11 @@ static int tune_one(Snapshot* s, const char* key, int64_t value) {
     s->shard_bucket0 = (uint32_t)value;
     return 0;
   }
+  if (strcmp(key, "stream_gate") == 0) {
+    if (value < 0 || value > 8) return set_error(-2, "stream_gate must be in [0, 8]");
+    s->stream_gate = (int)value;
+    return 0;
+  }
   if (strcmp(key, "shard_force_exchange") == 0) {
     if (value < 0 || value > 1) return set_error(-2, "shard_force_exchange must be 0 or 1");
     s->shard_force_exchange = (int)value;
@@ -672,21 +677,25 @@ struct LaneLease {
   ~LaneLease() { s->lanes_release(v); }
 };
 
+// The sparse error output of kg_check_batch_packed.
+struct SparseErr {
+  uint32_t* idx;
+  uint32_t* code;
+  size_t cap;
+  size_t* n;
+};
+
 // Host buffers in and out: the batch is split over the snapshot's replicas (one contiguous chunk
 // each, none smaller than MIN_PER_REPLICA queries), every chunk on this thread's lane of its
 // replica.  All chunks are staged and enqueued before the first wait, so the devices run
 // concurrently; queries are staged through pinned memory in slices so the H2D copy of one slice
-// overlaps the staging of the next.
-int kg_check_batch(kg_snapshot* sp, const kg_query* q, size_t n, int32_t global_max_depth, uint8_t* out,
-                   uint32_t* err_code, kg_stats* stats) {
-  KG_GUARD_BEGIN
+// overlaps the staging of the next.  Packed queries (pq) cross PCIe as 16 B and are unpacked on the
+// device; with `sp` only the answers cross back, plus the (index, code) pairs of the KG_ERROR ones.
+static int check_host(Snapshot* s, const kg_query* q, const kg_query_packed* pq, size_t n, int32_t global_max_depth,
+                      uint8_t* out, uint32_t* err_code, SparseErr* sp, kg_stats* stats) {
   constexpr size_t MIN_PER_REPLICA = 16384, SLICE = 65536;
-  if (!sp) return set_error(-2, "NULL snapshot");
-  if (n && (!q || !out)) return set_error(-2, "NULL buffer");
-  Snapshot* s = reinterpret_cast<Snapshot*>(sp);
-  if (s->shard_n > 1 || kg::shard_comm_of(s, nullptr))  // hash-sharded: the whole batch in kg_shard_comm.hip
-    return kg::shard_check_host_entry(s, q, n, global_max_depth, out, err_code, stats);
   if (stats) memset(stats, 0, sizeof *stats);
+  if (sp) *sp->n = 0;
   if (n == 0) return 0;
   if (n > 0x7FFFFFFFull) return set_error(-2, "batch too large");
   std::vector<kg::Lane*>* lanes = s->lanes_acquire();
@@ -706,25 +715,31 @@ int kg_check_batch(kg_snapshot* sp, const kg_query* q, size_t n, int32_t global_
   for (size_t i = 0; i < R && !rc; i++) {
     kg::Lane* L = lane(i);
     const size_t m = b[i + 1] - b[i];
-    if ((rc = L->reserve(m))) break;
+    if ((rc = pq ? L->reserve_packed(m) : L->reserve(m))) break;
     HIPC(hipSetDevice(L->device));
+    const size_t rec = pq ? sizeof(kg_query_packed) : sizeof(kg_query);
+    char* hs = reinterpret_cast<char*>(L->h_q);
+    char* ds = pq ? reinterpret_cast<char*>(L->d_pk) : reinterpret_cast<char*>(L->d_q);
+    const char* src = pq ? reinterpret_cast<const char*>(pq + b[i]) : reinterpret_cast<const char*>(q + b[i]);
     for (size_t o = 0; o < m; o += SLICE) {
       const size_t k = std::min(SLICE, m - o);
-      memcpy(L->h_q + o, q + b[i] + o, k * sizeof(kg_query));
-      if (hipMemcpyAsync(L->d_q + o, L->h_q + o, k * sizeof(kg_query), hipMemcpyHostToDevice, L->stream) != hipSuccess) {
+      memcpy(hs + o * rec, src + o * rec, k * rec);
+      if (hipMemcpyAsync(ds + o * rec, hs + o * rec, k * rec, hipMemcpyHostToDevice, L->stream) != hipSuccess) {
         rc = set_error(-1, "H2D copy failed");
         break;
       }
     }
+    if (!rc && pq) rc = kg::unpack_queries(L->d_pk, m, L->d_q, L->stream);
     if (rc) break;
     L->w->mu.lock();
     rc = kg::check_batch_begin(L->rep, L->w, L->d_q, m, global_max_depth, L->d_out, L->d_err, stats ? &st[i] : nullptr,
                                &bp[i]);
     begun++;
     if (!rc && (hipMemcpyAsync(L->h_out, L->d_out, m, hipMemcpyDeviceToHost, L->stream) != hipSuccess ||
-                hipMemcpyAsync(L->h_err, L->d_err, m * 4, hipMemcpyDeviceToHost, L->stream) != hipSuccess))
+                (!sp && hipMemcpyAsync(L->h_err, L->d_err, m * 4, hipMemcpyDeviceToHost, L->stream) != hipSuccess)))
       rc = set_error(-1, "D2H copy failed");
   }
+  std::vector<std::pair<uint32_t, uint32_t>> errs;  // sparse: (index, code) over every chunk
   for (size_t i = 0; i < begun; i++) {
     kg::Lane* L = lane(i);
     const size_t m = b[i + 1] - b[i];
@@ -735,12 +750,30 @@ int kg_check_batch(kg_snapshot* sp, const kg_query* q, size_t n, int32_t global_
       int r2 = kg::check_batch_end(L->rep, L->w, &bp[i], &reran, blocking);
       if (!r2 && reran &&  // the grid tier rewrote results after the first copy: copy them again
           (hipMemcpyAsync(L->h_out, L->d_out, m, hipMemcpyDeviceToHost, L->stream) != hipSuccess ||
-           hipMemcpyAsync(L->h_err, L->d_err, m * 4, hipMemcpyDeviceToHost, L->stream) != hipSuccess))
+           (!sp && hipMemcpyAsync(L->h_err, L->d_err, m * 4, hipMemcpyDeviceToHost, L->stream) != hipSuccess)))
         r2 = set_error(-1, "D2H copy failed");
+      const size_t pre = std::min(m, kg::Lane::EL_PREFETCH);
+      if (!r2 && sp) {  // the error list of the final answers, its count and first pairs read back with them
+        r2 = kg::error_list(L->d_out, L->d_err, m, (uint32_t)b[i], L->d_el, m, L->stream);
+        if (!r2 && hipMemcpyAsync(L->h_el, L->d_el, (2 + 2 * pre) * 4, hipMemcpyDeviceToHost, L->stream) != hipSuccess)
+          r2 = set_error(-1, "D2H copy failed");
+      }
       if (!r2) r2 = L->w->wait(L->stream, blocking);  // the error text is set by wait()
       if (!r2) {
         memcpy(out + b[i], L->h_out, m);
-        if (err_code) memcpy(err_code + b[i], L->h_err, m * 4);
+        if (err_code && !sp) memcpy(err_code + b[i], L->h_err, m * 4);
+      }
+      if (!r2 && sp) {
+        const size_t cnt = std::min<size_t>(L->h_el[0], m);
+        std::vector<uint32_t> more;
+        const uint32_t* pairs = L->h_el + 2;
+        if (cnt > pre) {  // rare: more errors than the prefetch held
+          more.resize(2 * cnt);
+          if (hipMemcpy(more.data(), L->d_el + 2, 2 * cnt * 4, hipMemcpyDeviceToHost) != hipSuccess)
+            r2 = set_error(-1, "D2H copy failed");
+          pairs = more.data();
+        }
+        for (size_t k = 0; !r2 && k < cnt; k++) errs.emplace_back(pairs[2 * k], pairs[2 * k + 1]);
       }
       rc = r2;
     } else {
@@ -748,6 +781,14 @@ int kg_check_batch(kg_snapshot* sp, const kg_query* q, size_t n, int32_t global_
       (void)hipStreamSynchronize(L->stream);
     }
     L->w->mu.unlock();
+  }
+  if (!rc && sp) {
+    std::sort(errs.begin(), errs.end());
+    *sp->n = errs.size();
+    for (size_t k = 0; k < errs.size() && k < sp->cap; k++) {
+      if (sp->idx) sp->idx[k] = errs[k].first;
+      if (sp->code) sp->code[k] = errs[k].second;
+    }
   }
   if (!rc && stats) {  // counters add up over replicas; device time is the slowest replica's
     for (size_t i = 0; i < R; i++) {
@@ -765,6 +806,52 @@ int kg_check_batch(kg_snapshot* sp, const kg_query* q, size_t n, int32_t global_
     stats->light_ms = lm;
   }
   return rc;
+}
+
+int kg_check_batch(kg_snapshot* sp, const kg_query* q, size_t n, int32_t global_max_depth, uint8_t* out,
+                   uint32_t* err_code, kg_stats* stats) {
+  KG_GUARD_BEGIN
+  if (!sp) return set_error(-2, "NULL snapshot");
+  if (n && (!q || !out)) return set_error(-2, "NULL buffer");
+  Snapshot* s = reinterpret_cast<Snapshot*>(sp);
+  if (s->shard_n > 1 || kg::shard_comm_of(s, nullptr))  // hash-sharded: the whole batch in kg_shard_comm.hip
+    return kg::shard_check_host_entry(s, q, n, global_max_depth, out, err_code, stats);
+  return check_host(s, q, nullptr, n, global_max_depth, out, err_code, nullptr, stats);
+  KG_GUARD_END
+}
+
+int kg_check_batch_packed(kg_snapshot* sp, const kg_query_packed* q, size_t n, int32_t global_max_depth, uint8_t* out,
+                          uint32_t* err_index, uint32_t* err_code, size_t err_cap, size_t* n_err, kg_stats* stats) {
+  KG_GUARD_BEGIN
+  if (!sp || !n_err) return set_error(-2, "NULL argument");
+  if (n && (!q || !out)) return set_error(-2, "NULL buffer");
+  if (err_cap && (!err_index || !err_code)) return set_error(-2, "err_cap > 0 needs err_index and err_code");
+  Snapshot* s = reinterpret_cast<Snapshot*>(sp);
+  SparseErr spe{err_index, err_code, err_cap, n_err};
+  if (s->shard_n > 1 || kg::shard_comm_of(s, nullptr)) {
+    // hash-sharded: unpacked on the host, the whole batch in kg_shard_comm.hip (not the narrow path)
+    std::vector<kg_query> w(n);
+    for (size_t i = 0; i < n; i++) {
+      const kg_query_packed& p = q[i];
+      const uint32_t sns = (p.w2 >> 24) | ((p.w3 & 0xFu) << 8);
+      w[i].t = kg_tuple{p.w2 & 0xFFFu, p.obj, (p.w2 >> 12) & 0xFFFu, sns == KG_PACK_SUBJECT_ID ? KG_SUBJECT_ID : sns,
+                        p.sobj, (p.w3 >> 4) & 0xFFFu};
+      w[i].max_depth = (int32_t)(p.w3 >> 16);
+    }
+    std::vector<uint32_t> e(n);
+    if (int rc = kg::shard_check_host_entry(s, w.data(), n, global_max_depth, out, e.data(), stats)) return rc;
+    *n_err = 0;
+    for (size_t i = 0; i < n; i++)
+      if (out[i] == KG_ERROR) {
+        if (*n_err < err_cap) {
+          err_index[*n_err] = (uint32_t)i;
+          err_code[*n_err] = e[i];
+        }
+        ++*n_err;
+      }
+    return 0;
+  }
+  return check_host(s, nullptr, q, n, global_max_depth, out, nullptr, &spe, stats);
   KG_GUARD_END
 }
 

@@ -923,9 +923,25 @@ int check_batch_begin(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n, 
       // starting at its label blockIdx & 7, so every label must occur for every range to be drained
       const uint32_t grid =
           std::max<uint32_t>(8u, (uint32_t)std::min<uint64_t>((uint64_t)s->n_cu * per_cu, (n + 31) / 32 + 8));
-      hipLaunchKernelGGL((k_stream4<9, 256>), dim3(grid), dim3(256), 0, stream, s->ds, LqList{lq, ctl->light8, lq_cap},
-                         ctl->heads, d_out, rq, heavy, &ctl->heavy_count, ctl, ecap,
-                         std::max<uint32_t>(1u, std::min<uint32_t>(s->stream_chunk, S4_CHUNK)), s->stream_steal);
+      const int gate = std::min(s->stream_gate, Snapshot::GATE_RING - 1);
+      std::unique_lock<std::mutex> gl(s->gate_mu, std::defer_lock);
+      if (gate > 0) {
+        // at most `gate` stream launches at once: this one starts after the launch `gate` tickets back
+        // has finished (a device-side wait; the host does not block)
+        gl.lock();
+        const uint64_t t = s->gate_ticket++;
+        for (auto& e : s->gate_ev)
+          if (!e) HIPC(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        if (t >= (uint64_t)gate) HIPC(hipStreamWaitEvent(stream, s->gate_ev[(t - gate) % Snapshot::GATE_RING], 0));
+        hipLaunchKernelGGL((k_stream4<9, 256>), dim3(grid), dim3(256), 0, stream, s->ds,
+                           LqList{lq, ctl->light8, lq_cap}, ctl->heads, d_out, rq, heavy, &ctl->heavy_count, ctl, ecap,
+                           std::max<uint32_t>(1u, std::min<uint32_t>(s->stream_chunk, S4_CHUNK)), s->stream_steal);
+        HIPC(hipEventRecord(s->gate_ev[t % Snapshot::GATE_RING], stream));
+      } else {
+        hipLaunchKernelGGL((k_stream4<9, 256>), dim3(grid), dim3(256), 0, stream, s->ds,
+                           LqList{lq, ctl->light8, lq_cap}, ctl->heads, d_out, rq, heavy, &ctl->heavy_count, ctl, ecap,
+                           std::max<uint32_t>(1u, std::min<uint32_t>(s->stream_chunk, S4_CHUNK)), s->stream_steal);
+      }
     }
     HIPC(hipGetLastError());
     if (stats) HIPC(hipEventRecord(l1, stream));
@@ -1059,6 +1075,60 @@ int check_batch_device(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n,
   BatchPending bp;
   if (int rc = check_batch_begin(s, w, d_q, n, global_max_depth, d_out, d_err, stats, &bp)) return rc;
   return check_batch_end(s, w, &bp, nullptr, s->device_sync != 0);
+}
+
+// ---- the narrow host boundary (kg_check_batch_packed): 16-B queries in, sparse error codes out
+// One query per thread; a 16-B load and a 28-B store, both coalesced (HBM-streaming, no reuse).
+__global__ __launch_bounds__(256) void k_unpack(const uint4* __restrict__ pk, uint32_t n, kg_query* __restrict__ q) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint4 v = pk[i];
+  const uint32_t sns = (v.z >> 24) | ((v.w & 0xFu) << 8);
+  kg_query x;
+  x.t.ns = v.z & 0xFFFu;
+  x.t.obj = v.x;
+  x.t.rel = (v.z >> 12) & 0xFFFu;
+  x.t.sns = sns == KG_PACK_SUBJECT_ID ? KG_SUBJECT_ID : sns;
+  x.t.sobj = v.y;
+  x.t.srel = (v.w >> 4) & 0xFFFu;
+  x.max_depth = (int32_t)(v.w >> 16);
+  q[i] = x;
+}
+
+// The checks answered KG_ERROR as (base + index, code) pairs after a count word: list[0] = count,
+// pairs from list[2].  One device atomic per wave with an error (errors are rare).
+__global__ __launch_bounds__(256) void k_err_list(const uint8_t* __restrict__ out, const uint32_t* __restrict__ err,
+                                                  uint32_t n, uint32_t base, uint32_t* list, uint32_t cap) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool e = i < n && out[i] == KG_ERROR;
+  const uint64_t m = __ballot(e);
+  if (!m) return;
+  const int lead = __ffsll((unsigned long long)m) - 1;
+  uint32_t at = 0;
+  if (lane_id() == lead) at = atomicAdd(list, (uint32_t)__popcll(m));
+  at = __shfl(at, lead, 64) + lanes_below(m);
+  if (e && at < cap) {
+    list[2 + 2 * (size_t)at] = base + i;
+    list[3 + 2 * (size_t)at] = err[i];
+  }
+}
+
+int unpack_queries(const kg_query_packed* d_pk, size_t n, kg_query* d_q, hipStream_t stream) {
+  if (!n) return 0;
+  hipLaunchKernelGGL(k_unpack, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, stream, (const uint4*)d_pk,
+                     (uint32_t)n, d_q);
+  HIPC(hipGetLastError());
+  return 0;
+}
+
+int error_list(const uint8_t* d_out, const uint32_t* d_err, size_t n, uint32_t base, uint32_t* d_list, size_t cap,
+               hipStream_t stream) {
+  HIPC(hipMemsetAsync(d_list, 0, 8, stream));
+  if (!n) return 0;
+  hipLaunchKernelGGL(k_err_list, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, stream, d_out, d_err, (uint32_t)n,
+                     base, d_list, (uint32_t)cap);
+  HIPC(hipGetLastError());
+  return 0;
 }
 
 }  // namespace kg

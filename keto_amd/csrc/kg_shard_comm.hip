@@ -840,7 +840,9 @@ int shard_check(Snapshot* s, ShardComm* c, const kg_query* d_q, size_t n, int32_
     c->st[2]++;
     if (h[0] || h[1] || s->shard_force_overflow) {  // dropped records somewhere: every rank reruns with more room
       const bool bucket_over = h[0] || s->shard_force_overflow;
-      if (bucket_over && run++ >= s->shard_max_reruns) {
+      // a run whose visited table overflowed too dropped records for that reason as well, so its
+      // bucket counts are lower bounds: only runs without it count against the bucket-rerun bound
+      if (bucket_over && !h[1] && run++ >= s->shard_max_reruns) {
         drop_buffers(c);
         return set_error(KG_ERR_RESOURCE_CODE,
                          "sharded batch still overflows after %u reruns (bucket %zu records per destination, "
@@ -848,25 +850,30 @@ int shard_check(Snapshot* s, ShardComm* c, const kg_query* d_q, size_t n, int32_
       }
       if (bucket_over) {
         c->st[3]++;
+        const size_t top = 1ull << 30;
         if (xch) {
-          // every exchange that overflowed gets what it needed (its counter counted past B_k) plus a
-          // quarter; records it dropped were missing downstream, so the later exchanges double too
+          // every exchange that overflowed gets at least what it needed (its counter counted past
+          // B_k) plus a quarter, and at least twice its old size; records it dropped were missing
+          // downstream, so the counts of every later exchange are lower bounds: they get at least the
+          // largest size any overflowed exchange now has (levels are the same order of magnitude)
+          size_t grown = 0;
           bool after = false;
           for (int k = 0; k <= L; k++) {
-            const uint64_t need = k < L ? h[8 + (size_t)k] : h[2];
+            const uint64_t need = k < L ? h[8 + (size_t)k] : 0;
             size_t& b = c->lb[(size_t)k];
-            const size_t want = std::min<size_t>((size_t)(need * 1.25) + 1024, 1ull << 30);
-            if (after) b = std::max(b, std::min<size_t>(2 * b, 1ull << 30));
-            if (need > b) {
-              b = std::max(b, want);
+            if (need > b || (s->shard_force_overflow && !h[0])) {
+              b = std::min(top, std::max((size_t)(need * 1.25) + 1024, 2 * b));
+              grown = std::max(grown, b);
               after = true;
+            } else if (after) {
+              b = std::min(top, std::max(b, grown));
             }
           }
-          if (s->shard_force_overflow) c->lb.assign(c->lb.size(), std::min<size_t>(2 * B, 1ull << 30));
         } else {
-          // the device loop's fold reported the bucket its levels needed (0: not known -- double)
+          // the device loop's fold reported the bucket its levels needed (a lower bound past the first
+          // level that dropped records): that plus a quarter, and at least twice the old size
           const uint64_t need = h[2];
-          c->bucket = need ? std::max<size_t>(B + 1024, (size_t)(need * 1.25) + 1024) : 2 * B;
+          c->bucket = std::min(top, std::max<size_t>(2 * B, (size_t)(need * 1.25) + 1024));
         }
       }
       if (h[1]) {

@@ -201,7 +201,14 @@ struct Lane {
   uint32_t* d_err = nullptr;
   size_t cap = 0;
   void* exp = nullptr;  // expand buffers of this lane (kg_expand.hip)
+  // kg_check_batch_packed: packed queries on the device (staged through h_q) and the error list
+  kg_query_packed* d_pk = nullptr;
+  uint32_t* d_el = nullptr;  // count word, pad, then (index, code) pairs: room for every query of the chunk
+  uint32_t* h_el = nullptr;  // pinned: the count and the first EL_PREFETCH pairs, read back with the answers
+  size_t pk_cap = 0;
+  static constexpr size_t EL_PREFETCH = 4096;
   int reserve(size_t n);
+  int reserve_packed(size_t n);
   ~Lane();
 };
 
@@ -297,6 +304,16 @@ struct Snapshot {
   int grid_ms_words = 8;     // kg_snapshot_tune("grid_ms_words"): 64-bit words per MS-BFS mask (64 queries each)
   uint32_t grid_ms_tg_cap = 256;  // kg_snapshot_tune("grid_ms_tg_cap"): holders above which MS-BFS probes dset instead
   uint64_t grid_ms_cap = 0;  // kg_snapshot_tune("grid_ms_cap"): MS-BFS entries per level buffer (0 = 16 Mi; tests)
+  // kg_snapshot_tune("stream_gate"): at most this many k_stream4 launches of different batches run at
+  // once (0: no cap).  Each launch waits, on the device, for the one `stream_gate` tickets before it
+  // (an event ring, tickets taken in launch order under gate_mu), so more batches can be in flight
+  // (their k_resolve / k_back / grid phases overlapping) without more stream launches contending for
+  // the LDS and the random-request path.
+  int stream_gate = 0;
+  static constexpr int GATE_RING = 16;
+  std::mutex gate_mu;
+  uint64_t gate_ticket = 0;
+  hipEvent_t gate_ev[GATE_RING] = {};
   int grid_bidir = 0;  // kg_snapshot_tune("grid_bidir"): grid slots whose subject has <= this many holders alternate
                        // forward and backward turns (0: none, forward only)
   // replicas: the same snapshot on more devices (kg_snapshot_create's device mask); this object is
@@ -345,6 +362,11 @@ int check_batch_begin(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n, 
                       uint8_t* d_out, uint32_t* d_err, kg_stats* stats, BatchPending* bp);
 int check_batch_end(Snapshot* s, Workspace* w, BatchPending* bp, bool* reran, bool blocking = false);
 int synth_queries(Snapshot* s, uint64_t seed, size_t n, kg_query* d_q);
+// kg_check_batch_packed: packed queries -> kg_query on the device; the KG_ERROR answers of [0, n) as
+// (base + index, code) pairs after a count word (d_list: 2 + 2 * cap words)
+int unpack_queries(const kg_query_packed* d_pk, size_t n, kg_query* d_q, hipStream_t stream);
+int error_list(const uint8_t* d_out, const uint32_t* d_err, size_t n, uint32_t base, uint32_t* d_list, size_t cap,
+               hipStream_t stream);
 // kg_formula.hip: split a batch's decomposable queries into leaf checks / combine their results
 int formula_split(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n, int32_t gdepth, const kg_query** q2,
                   size_t* n2, const uint32_t** n_extra, uint8_t** out2, uint32_t** err2, const uint2** ref);

@@ -250,6 +250,8 @@ Snapshot::~Snapshot() {
   for (auto& a : allocs) hipFree(a.first);
   for (Workspace* w : wss) delete w;
   for (ShardCtx* c : shard_ctxs) delete c;
+  for (hipEvent_t e : gate_ev)
+    if (e) hipEventDestroy(e);
   giant.release();
   if (stream) hipStreamDestroy(stream);
 }
@@ -304,6 +306,9 @@ Lane::~Lane() {
   if (d_q) hipFree(d_q);
   if (d_out) hipFree(d_out);
   if (d_err) hipFree(d_err);
+  if (d_pk) hipFree(d_pk);
+  if (d_el) hipFree(d_el);
+  if (h_el) hipHostFree(h_el);
   if (exp) expand_bufs_free(exp);
   // the stream's workspace belongs to the replica (freed with it); the stream itself is ours
   if (stream) hipStreamDestroy(stream);
@@ -330,6 +335,23 @@ int Lane::reserve(size_t n) {
   HIPC(hipMalloc(&d_out, c));
   HIPC(hipMalloc(&d_err, c * 4));
   cap = c;
+  return 0;
+}
+
+int Lane::reserve_packed(size_t n) {
+  if (int rc = reserve(n)) return rc;  // h_q stages the packed queries, d_q holds them unpacked
+  if (n <= pk_cap && d_pk) return 0;
+  HIPC(hipSetDevice(device));
+  HIPC(hipStreamSynchronize(stream));
+  if (d_pk) hipFree(d_pk);
+  if (d_el) hipFree(d_el);
+  d_pk = nullptr;
+  d_el = nullptr;
+  pk_cap = 0;
+  if (!h_el) HIPC(hipHostMalloc(&h_el, (2 + 2 * EL_PREFETCH) * 4, hipHostMallocDefault));
+  HIPC(hipMalloc(&d_pk, cap * sizeof(kg_query_packed)));
+  HIPC(hipMalloc(&d_el, (2 + 2 * cap) * 4));
+  pk_cap = cap;
   return 0;
 }
 

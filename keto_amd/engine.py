@@ -276,6 +276,24 @@ class Engine:
         self.last_stats = st.as_dict() if with_stats else None
         return out, err
 
+    def batch_check_packed(self, q: np.ndarray, err_cap: Optional[int] = None) -> Tuple[np.ndarray, np.ndarray, int]:
+        """The narrow boundary (kg_check_batch_packed): q (n,7) uint32 kg_query rows are packed to 16 B
+        (pack_queries = the header's kg_pack_query), answers come back as bytes and the error codes as
+        (index, code) pairs of the KG_ERROR answers only.  Returns (result u8, pairs (k, 2) u32, n_err)."""
+        pk = _lib.pack_queries(q)
+        n = pk.shape[0]
+        cap = n if err_cap is None else int(err_cap)
+        out = np.zeros(n, np.uint8)
+        idx = np.zeros(max(cap, 1), np.uint32)
+        code = np.zeros(max(cap, 1), np.uint32)
+        n_err = C.c_size_t(0)
+        rc = _lib.load().kg_check_batch_packed(self.snapshot.handle, _ptr(pk), n, self.config.max_read_depth, _ptr(out),
+                                               _ptr(idx) if cap else None, _ptr(code) if cap else None, cap,
+                                               C.byref(n_err), None)
+        _lib.check(rc, "kg_check_batch_packed")
+        k = min(cap, int(n_err.value))
+        return out, np.stack([idx[:k], code[:k]], axis=1), int(n_err.value)
+
     def batch_check(self, tuples: Sequence[RelationTuple], max_depths) -> Tuple[List[bool], List[Optional[CheckError]]]:
         """BatchCheck(ctx, []*RelationTuple, maxDepth []int) ([]bool, []error) -- SURVEY.md 8b."""
         it = self.snapshot.interner

@@ -428,6 +428,47 @@ def test_random_rewrites_vs_oracle(seed, unions, mat, monkeypatch):
         assert m["union_nodes"] > 0, m
 
 
+@pytest.mark.parametrize("seed", [0, 5])
+def test_packed_boundary_vs_oracle(seed):
+    """kg_check_batch_packed (16-B packed queries in, answers as bytes, error codes as
+    sparse (index, code) pairs of the KG_ERROR answers): the same answers and codes as kg_check_batch and
+    the oracle, on random programs with undeclared relations (many errors) -- 20 k queries, so the error
+    list outgrows its read-back prefetch (4096 pairs) and the queries span several staging slices; and
+    a truncated list (err_cap 5) keeps the full count and the first pairs by index."""
+    from keto_amd import _lib
+    from keto_amd.namespace import compile_program
+    rng = np.random.default_rng(700 + seed)
+    nss, rels = ["a", "b", "c"], ["r0", "r1", "r2", "r3"]
+    it = Interner()
+    namespaces = random_program(rng, nss, rels)
+    prog = compile_program(namespaces, it, lower_ttu=False)
+    n_obj = 60
+    tuples = []
+    for _ in range(600):
+        ns, obj = rng.choice(nss), f"o{rng.integers(n_obj)}"
+        rel = rng.choice(rels) if rng.random() < 0.9 else "undeclared"
+        s = f"({rng.choice(nss)}:o{rng.integers(n_obj)}#{rng.choice(rels + ['undeclared'])})" if rng.random() < 0.5 \
+            else f"u{rng.integers(25)}"
+        tuples.append(RelationTuple.from_string(f"{ns}:{obj}#{rel}@{s}"))
+    reg = Registry(tuples, namespaces, interner=it)
+    qs = random_queries(rng, nss, rels + ["undeclared"], 2000, n_obj=n_obj, n_users=25)
+    q6 = np.tile(np.asarray([it.tuple_ids(t) for t in qs], np.uint32), (10, 1))
+    depths = np.tile(rng.integers(-1, 7, len(qs)), 10)
+    q = queries_array(q6, depths)
+    oracle = Oracle(it.tuples_array(tuples), it.wildcard_rel, prog)
+    for gmax in (2, 5):
+        e = Engine(reg.snapshot, Config(gmax))
+        out, err = e.batch_check_ids(q)
+        pout, pairs, n_err = e.batch_check_packed(q)
+        exp, oerr, _ = oracle.check_batch(q6, depths, gmax, POLICY_CANONICAL)
+        assert (pout == out).all() and (out == exp).all() and (err.astype(np.int64) == oerr).all()
+        bad = np.nonzero(out == _lib.KG_ERROR)[0]
+        assert n_err == bad.size > 4096, (n_err, bad.size)
+        assert (pairs[:, 0] == bad).all() and (pairs[:, 1] == err[bad]).all()
+        t_out, t_pairs, t_n = e.batch_check_packed(q, err_cap=5)
+        assert (t_out == out).all() and t_n == n_err and (t_pairs == pairs[:5]).all()
+
+
 def test_relation_not_found_and_cycle():
     nss = [Namespace("d", [Relation("a"), Relation("b", rewrite=SubjectSetRewrite([ComputedSubjectSet("c")])),
                            Relation("c", rewrite=SubjectSetRewrite([ComputedSubjectSet("b")]))])]

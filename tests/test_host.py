@@ -86,7 +86,9 @@ def test_library_exports_every_declared_symbol():
     build()  # cross-compiles for gfx950 on a CPU-only host too
     with open(os.path.join(ROOT, "include", "ketogpu.h")) as f:
         hdr = f.read()
-    declared = set(re.findall(r"\b(kg_[a-z_]+)\s*\(", hdr))
+    # header-only helpers (static inline, e.g. kg_pack_query) are not library symbols
+    inline = set(re.findall(r"static inline \w+ (kg_[a-z_]+)\s*\(", hdr))
+    declared = set(re.findall(r"\b(kg_[a-z_]+)\s*\(", hdr)) - inline
     assert declared == set(_lib.EXPORTS), declared ^ set(_lib.EXPORTS)
     L = _lib.load()
     for name in declared:
@@ -136,3 +138,48 @@ def test_ttu_lowering_preserves_semantics(seed):
         e1, r1, _ = o1.check_batch(q6, depths, gmax, POLICY_CANONICAL)
         e2, r2, _ = o2.check_batch(q6, depths, gmax, POLICY_CANONICAL)
         assert (e1 == e2).all() and (r1 == r2).all(), gmax
+
+
+def test_pack_queries_matches_header(tmp_path):
+    """keto_amd._lib.pack_queries (what the tests and bench feed kg_check_batch_packed) equals the header's
+    kg_pack_query (what a cgo caller compiles), and a restatement of the device unpack (kg_check.hip
+    k_unpack) restores every field -- depths clamped to 0..65535, a subject id's relation ignored."""
+    import ctypes as C
+    import subprocess
+    from keto_amd import _lib
+    src = tmp_path / "pack.c"
+    src.write_text('#include "ketogpu.h"\n'
+                   'int pack_all(const kg_query* q, unsigned long n, kg_query_packed* p) {\n'
+                   '  for (unsigned long i = 0; i < n; i++) if (kg_pack_query(q + i, p + i)) return -1;\n'
+                   '  return 0; }\n')
+    so = tmp_path / "pack.so"
+    subprocess.run(["gcc", "-O1", "-shared", "-fPIC", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(so)],
+                   check=True)
+    lib = C.CDLL(str(so))
+    rng = np.random.default_rng(5)
+    n = 5000
+    q = np.zeros((n, 7), np.uint32)
+    q[:, 0] = rng.integers(0, 4095, n)
+    q[:, 1] = rng.integers(0, 2 ** 32, n, dtype=np.uint64).astype(np.uint32)
+    q[:, 2] = rng.integers(0, 4095, n)
+    sid = rng.random(n) < 0.5
+    q[:, 3] = np.where(sid, 0xFFFFFFFF, rng.integers(0, 4095, n))
+    q[:, 4] = rng.integers(0, 2 ** 32, n, dtype=np.uint64).astype(np.uint32)
+    q[:, 5] = rng.integers(0, 4095, n)
+    q[:, 6] = rng.integers(-5, 70000, n).astype(np.int32).view(np.uint32)
+    got = _lib.pack_queries(q)
+    want = np.zeros((n, 4), np.uint32)
+    assert lib.pack_all(q.ctypes.data_as(C.c_void_p), C.c_ulong(n), want.ctypes.data_as(C.c_void_p)) == 0
+    assert (got == want).all()
+    # the device unpack, restated
+    w2, w3 = got[:, 2].astype(np.int64), got[:, 3].astype(np.int64)
+    sns = (w2 >> 24) | ((w3 & 0xF) << 8)
+    assert ((w2 & 0xFFF) == q[:, 0]).all() and (((w2 >> 12) & 0xFFF) == q[:, 2]).all()
+    assert (np.where(sns == 4095, 0xFFFFFFFF, sns) == q[:, 3]).all()
+    assert (((w3 >> 4) & 0xFFF)[~sid] == q[~sid, 5]).all() and (((w3 >> 4) & 0xFFF)[sid] == 0).all()
+    assert ((w3 >> 16) == np.clip(q[:, 6].view(np.int32), 0, 65535)).all()
+    assert (got[:, 0] == q[:, 1]).all() and (got[:, 1] == q[:, 4]).all()
+    bad = q[:1].copy()
+    bad[0, 0] = 5000
+    with pytest.raises(ValueError):
+        _lib.pack_queries(bad)

@@ -503,15 +503,18 @@ def _general_gpu_worker(rank, world, port, outq, kind, driver="py"):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("kind,world,driver", [("impure", 1, "py"), ("opl", 1, "py"), ("opl", 2, "py"),
-                                               ("order", 1, "py"), ("order", 2, "py"), ("impure", 1, "lib"),
-                                               ("opl", 1, "lib"), ("opl", 2, "lib"), ("order", 1, "lib"),
-                                               ("order", 2, "lib"), ("impure", 2, "lib")])
+                                               ("order", 1, "py"), ("order", 2, "py"),
+                                               ("impure", 1, "lib-rccl-forced"), ("opl", 1, "lib-rccl-forced"),
+                                               ("order", 1, "lib-rccl-forced"), ("opl", 1, "lib"),
+                                               ("opl", 2, "lib"), ("order", 2, "lib"), ("impure", 2, "lib")])
 def test_sharded_general_rewrites_vs_oracle(kind, world, driver):
     """Every rewrite in the hash-sharded mode: the reference parser's full example (a `view` formula
     recursive through tuple-to-subject-set, `not`, nested traverse) and a program with a computed
     rewrite and undeclared relations.  Queries the level protocol ends as NOT_IMPLEMENTED go to the
     general phase (their rows gathered to the home rank, the single-GPU engine's interpreter on them):
-    answers and error codes bit-exact with the oracle evaluating the program as written."""
+    answers and error codes bit-exact with the oracle evaluating the program as written -- at world 2
+    over gloo and at world 1 through the exchange protocol over RCCL; world 1 local-first answers every
+    query with the replica tier chain (interpreter included)."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from oracle.oracle import POLICY_CANONICAL, Oracle
@@ -532,7 +535,8 @@ def test_sharded_general_rewrites_vs_oracle(kind, world, driver):
     else:
         it, t6, q, prog_ref, _ = _impure_graph(5)
     o = Oracle(t6, it.wildcard_rel, prog_ref)
-    assert sum(g[2] for g in got) > 0
+    if driver != "lib" or world > 1:  # (world 1 local-first: the interpreter answers them, no general phase)
+        assert sum(g[2] for g in got) > 0
     for gmax in (2, 5, 8):
         exp, oerr, _ = o.check_batch(q[:, :6], q[:, 6].view(np.int32), gmax, POLICY_CANONICAL)
         res = np.zeros(len(q), np.uint8)
