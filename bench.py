@@ -60,7 +60,10 @@ def parse(argv=None):
                     help="check mode: timed batches of the hash-sharded sub-line (the C4 engine through "
                          "kg_check_batch_device over RCCL, one shard per rank; 0 = off)")
     ap.add_argument("--sharded-warmup", type=int, default=4)
-    ap.add_argument("--sharded-inflight", type=int, default=4, help="sharded batches in flight per rank")
+    ap.add_argument("--sharded-inflight", type=int, default=0,
+                    help="sharded batches in flight per rank, each with its own communicator (0: 4 at one rank, 1 "
+                         "across ranks -- streams share HIP's hardware queues, and collectives of different "
+                         "communicators queued in different orders on different ranks can deadlock)")
     ap.add_argument("--sharded-timeout", type=float, default=300.0,
                     help="watchdog of the sharded sub-line: past it rank 0 prints the line without it")
     ap.add_argument("--shard-budget", type=int, default=0,
@@ -1212,7 +1215,7 @@ def sharded_leg(a, snap, size_param, dist, rank, world, local, backend, orc) -> 
                                    doc_alpha=alpha, group_alpha=alpha)
     t_build = time.time() - t0
     transport = "rccl" if backend == "nccl" else "host"
-    P = max(1, a.sharded_inflight)
+    P = a.sharded_inflight if a.sharded_inflight > 0 else (4 if world == 1 else 1)
     groups = [None] * P
     if dist is not None and P > 1:
         groups = [dist.new_group(list(range(world))) for _ in range(P)]

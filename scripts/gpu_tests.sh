@@ -2,13 +2,14 @@
 # usage: gpurun -- 'bash scripts/gpu_tests.sh'
 #   env: TESTS="tests -m gpu" (pytest args), TAG=r2a (log suffix), BENCH=1 (0 skips the default
 #        bench), BENCH_EXTRA (args of the default bench), BENCH2 (args of a second bench run),
-#        PYTEST_X ("" runs past failures; default -x), PYTEST_TIMEOUT (seconds, 900)
+#        PYTEST_X ("" runs past failures; default -x), PYTEST_TIMEOUT (seconds, 900), KEXPR (pytest -k
+#        expression, may hold spaces)
 set -u
 TAG=${TAG:-r2}
 TESTS=${TESTS:-tests -m gpu}
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
-timeout -k 10 ${PYTEST_TIMEOUT:-900} python -u -m pytest $TESTS -q -rs ${PYTEST_X--x} --timeout 180 --timeout-method thread --durations 15 > gpurun_out/pytest_${TAG}.log 2>&1; rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/pytest_${TAG}.log
+timeout -k 10 ${PYTEST_TIMEOUT:-900} python -u -m pytest $TESTS ${KEXPR:+-k "$KEXPR"} -q -rs ${PYTEST_X--x} --timeout 180 --timeout-method thread --durations 15 > gpurun_out/pytest_${TAG}.log 2>&1; rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/pytest_${TAG}.log
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_${TAG}.log 2>&1; rc=$?; echo "smoke rc=$rc"
 [ $rc -eq 0 ] || exit $rc
