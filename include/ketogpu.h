@@ -474,8 +474,9 @@ int kg_shard_bad_nodes(const kg_snapshot* s, uint64_t* count);
  * batch: one all-reduce that agrees on the slot count (the done bitmap's width) and one at the end
  * (overflow flags, largest bucket, records left, "a query needs the general phase") -- two host
  * round trips per batch, none per level.  A bucket or visited-table overflow on any rank reruns the
- * batch on every rank with room to spare.  Escalation (kg_snapshot_tune "shard_budget") is not
- * available here (keto_amd/sharded.py drives it through the kg_shard_* steps above).
+ * batch on every rank with room to spare.  Escalation (kg_snapshot_tune "shard_budget", round 5) runs
+ * here too: a backward phase over all-gathered fixed buckets of the escalated queries and a final forward
+ * phase for the queries past both budgets (keto_amd/sharded.py ShardedChecker is the restatement).
  *
  * kg_shard_comm_init binds an RCCL communicator (over xGMI on one node) to the batches the
  * snapshot runs on `stream` (NULL: the snapshot's own stream, which kg_check_batch uses); several
@@ -526,7 +527,7 @@ int kg_shard_comm_release(kg_snapshot* s, void* stream);
  * kg_shard_comm_stats_ex gives up to 16: [8] records this rank sent to OTHER ranks (what crosses
  * xGMI), [9] bytes it put on the wire (every other rank gets B_k records per exchange, plus counts
  * and done bitmaps), [10] path (0 local-first tier chain, 1 one-rank device loop, 2 exchange
- * protocol), [11] exchanges. */
+ * protocol), [11] exchanges, [12] levels of the escalation phases (backward + final forward). */
 int kg_shard_comm_stats(const kg_snapshot* s, void* stream, uint64_t out8[8]);
 int kg_shard_comm_stats_ex(const kg_snapshot* s, void* stream, uint64_t* out, size_t n);
 /* Per exchange k of the last batch: out[2k] = B_k (records per destination it was sent with),

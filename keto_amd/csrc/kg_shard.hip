@@ -470,6 +470,29 @@ __device__ __forceinline__ void back_child(const DevSnap& s, const kg_frec& pr, 
   }
 }
 
+// Segmented input (n_seg > 1: the receive buffer of a fixed-split all-to-all or all-gather -- segment k
+// holds min(d_n_in[k], seg_cap) records from in[k * seg_cap]): every thread of the workgroup calls
+// seg_total once (it stages the segments' prefix sums in LDS) and seg_src per record.
+__device__ __forceinline__ uint64_t seg_total(uint64_t* s_segpre, uint32_t n_seg, const uint32_t* d_n_in,
+                                              uint64_t seg_cap) {
+  if (threadIdx.x == 0) {
+    uint64_t a = 0;
+    for (uint32_t k = 0; k < n_seg; k++) {
+      s_segpre[k] = a;
+      a += min((uint64_t)d_n_in[k], seg_cap);
+    }
+    s_segpre[n_seg] = a;
+  }
+  __syncthreads();
+  return s_segpre[n_seg];
+}
+
+__device__ __forceinline__ uint64_t seg_src(const uint64_t* s_segpre, uint32_t n_seg, uint64_t seg_cap, uint64_t i) {
+  uint32_t k = 0;
+  while (k + 1 < n_seg && s_segpre[k + 1] <= i) k++;
+  return (uint64_t)k * seg_cap + (i - s_segpre[k]);
+}
+
 // One workgroup handles 256 received records per iteration; their set rows are expanded
 // edge-parallel (block scan of the row lengths, LDS owner search).  A row longer than SHARD_HEAVY
 // (a hub) is not expanded by its workgroup -- one workgroup would hold the level for the whole row --
@@ -494,34 +517,15 @@ __global__ __launch_bounds__(256) void k_shard_level(DevSnap s, const kg_frec* _
   const uint32_t me = s.shard_rank;
   // record count: from the previous level's counter on the device (clamped to the bucket: a count
   // past it means dropped records, which the caller's overflow check turns into a rerun)
-  uint64_t n_in;
-  if (n_seg > 1) {
-    if (tid == 0) {
-      uint64_t a = 0;
-      for (uint32_t k = 0; k < n_seg; k++) {
-        s_segpre[k] = a;
-        a += min((uint64_t)d_n_in[k], seg_cap);
-      }
-      s_segpre[n_seg] = a;
-    }
-    __syncthreads();
-    n_in = s_segpre[n_seg];
-  } else {
-    n_in = d_n_in ? min((uint64_t)*d_n_in, n_bound) : n_bound;
-  }
+  const uint64_t n_in =
+      n_seg > 1 ? seg_total(s_segpre, n_seg, d_n_in, seg_cap) : (d_n_in ? min((uint64_t)*d_n_in, n_bound) : n_bound);
   for (uint64_t base = (uint64_t)blockIdx.x * 256; base < n_in; base += (uint64_t)gridDim.x * 256) {
     const uint64_t i = base + tid;
     kg_frec r{0, NONE, 0, 0};
     bool hit_out = false, err_out = false, esc_out = false;
     uint64_t rb = 0, len = 0;
     if (i < n_in) {
-      uint64_t src = i;
-      if (n_seg > 1) {
-        uint32_t k = 0;
-        while (k + 1 < n_seg && s_segpre[k + 1] <= i) k++;
-        src = (uint64_t)k * seg_cap + (i - s_segpre[k]);
-      }
-      r = in[src];
+      r = in[n_seg > 1 ? seg_src(s_segpre, n_seg, seg_cap, i) : i];
       const bool probe = !(r.depth & D_NOPROBE), own = (r.depth & D_OWN) != 0;
       const bool packed = pack && (r.depth & D_ROW) != 0;  // r.node = the row's begin, the length in the depth word
       r.depth &= D_MASK;
@@ -668,17 +672,18 @@ __global__ __launch_bounds__(256) void k_shard_refwd_seed(DevSnap s, uint32_t n,
 // forward phase's root probe.
 __global__ __launch_bounds__(256) void k_shard_back_seed(DevSnap s, const kg_frec* __restrict__ list, uint64_t m_bound,
                                                          const uint32_t* d_m, kg_frec* out, uint64_t cap,
-                                                         uint32_t* counts) {
+                                                         uint32_t* counts, uint32_t n_seg, uint64_t seg_cap) {
   __shared__ uint32_t s_pref[256], s_wsum[4], s_first[256];
   __shared__ kg_frec s_rec[256];
+  __shared__ uint64_t s_segpre[KG_SHARD_MAX_RANKS + 1];
   const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
-  const uint64_t m = d_m ? min((uint64_t)*d_m, m_bound) : m_bound;
+  const uint64_t m = n_seg > 1 ? seg_total(s_segpre, n_seg, d_m, seg_cap) : (d_m ? min((uint64_t)*d_m, m_bound) : m_bound);
   for (uint64_t base = (uint64_t)blockIdx.x * 256; base < m; base += (uint64_t)gridDim.x * 256) {
     const uint64_t i = base + tid;
     uint32_t cnt = 0, first = 0;
     kg_frec r{0, NONE, NONE, 0};
     if (i < m) {
-      const kg_frec e = list[i];
+      const kg_frec e = list[n_seg > 1 ? seg_src(s_segpre, n_seg, seg_cap, i) : i];
       if (e.depth >= 2) {  // holders at distance 0 lead to the root within D - 1 hops only if D - 1 >= 1
         const uint2 h = holders_find(s, e.subj);
         first = h.x;
@@ -726,20 +731,22 @@ __global__ __launch_bounds__(256) void k_shard_back_level(DevSnap s, const kg_fr
                                                           uint64_t vmask, const uint32_t* __restrict__ done,
                                                           uint32_t done_wpr, HeavyList heavy, uint32_t* qcnt,
                                                           uint32_t budget,
-                                                          uint32_t lossy) {
+                                                          uint32_t lossy, uint32_t n_seg, uint64_t seg_cap) {
   __shared__ uint32_t s_pref[256], s_wsum[4];
   __shared__ uint64_t s_rb[256];
   __shared__ kg_frec s_rec[256];
+  __shared__ uint64_t s_segpre[KG_SHARD_MAX_RANKS + 1];
   const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
   const uint32_t me = s.shard_rank;
-  const uint64_t n_in = d_n_in ? min((uint64_t)*d_n_in, n_bound) : n_bound;
+  const uint64_t n_in =
+      n_seg > 1 ? seg_total(s_segpre, n_seg, d_n_in, seg_cap) : (d_n_in ? min((uint64_t)*d_n_in, n_bound) : n_bound);
   for (uint64_t base = (uint64_t)blockIdx.x * 256; base < n_in; base += (uint64_t)gridDim.x * 256) {
     const uint64_t i = base + tid;
     kg_frec r{0, NONE, 0, 0};
     uint64_t rb = 0, len = 0;
     bool esc_out = false;
     if (i < n_in) {
-      r = in[i];
+      r = in[n_seg > 1 ? seg_src(s_segpre, n_seg, seg_cap, i) : i];
       if (r.node == KG_FREC_HIT) {
         if ((r.q >> Q_BITS) == me) res[r.q & Q_MASK] = KG_IS_MEMBER;
       } else if (r.node == KG_FREC_ESC) {
@@ -917,7 +924,7 @@ __global__ void k_shard_fold(const uint32_t* __restrict__ sub_end, const uint32_
   }
   counts_end[0] = left;
   counts0[1] |= sub_end[n_sub] | sub_other[n_sub];
-  if (need) *need = max((unsigned long long)mx * n_sub, seeded);
+  if (need) *need = max(*need, max((unsigned long long)mx * n_sub, seeded));
 }
 
 __global__ void k_shard_finish(uint32_t n, uint8_t* res, uint32_t* err, ShardFormula F) {
@@ -1020,7 +1027,7 @@ static HeavyList heavy_list(ShardCtx* c) {
 
 // Escalation is on for snapshots without a namespace program (errors below the root cannot occur)
 // whose reverse indexes exist, with a non-zero budget.
-static bool shard_escalates(const Snapshot* s) { return s->shard_budget && !s->ds.relflags && s->ds.radj; }
+bool shard_escalates(const Snapshot* s) { return s->shard_budget && !s->ds.relflags && s->ds.radj; }
 
 int shard_seed(Snapshot* s, const kg_query* d_q, size_t n, int32_t gdepth, kg_frec* d_out, size_t cap,
                uint32_t* d_counts, uint8_t* d_res, uint32_t* d_err, hipStream_t stream) {
@@ -1226,14 +1233,14 @@ int shard_refwd_seed(Snapshot* s, size_t n, const uint8_t* d_res, const uint32_t
 }
 
 int shard_back_seed(Snapshot* s, const kg_frec* d_list, size_t m, const uint32_t* d_m, kg_frec* d_out, size_t cap,
-                    uint32_t* d_counts, hipStream_t stream) {
+                    uint32_t* d_counts, hipStream_t stream, uint32_t n_seg, size_t seg_cap) {
   HIPC(hipSetDevice(s->device));
   if (!stream) stream = s->stream;
   HIPC(hipMemsetAsync(d_counts, 0, 8, stream));
   if (m && s->ds.radj) {
     const uint32_t grid = (uint32_t)std::min<uint64_t>((m + 255) / 256, (uint64_t)s->n_cu * s->shard_wgs);
     hipLaunchKernelGGL(k_shard_back_seed, dim3(grid), dim3(256), 0, stream, s->ds, d_list, (uint64_t)m, d_m, d_out,
-                       (uint64_t)cap, d_counts);
+                       (uint64_t)cap, d_counts, n_seg, (uint64_t)seg_cap);
     HIPC(hipGetLastError());
   }
   return 0;
@@ -1241,7 +1248,7 @@ int shard_back_seed(Snapshot* s, const kg_frec* d_list, size_t m, const uint32_t
 
 int shard_back_level(Snapshot* s, const kg_frec* d_in, size_t n_in, const uint32_t* d_n_in, kg_frec* d_out, size_t cap,
                      uint32_t* d_counts, uint8_t* d_res, uint32_t* d_err, const uint32_t* d_done, uint32_t done_words,
-                     hipStream_t stream) {
+                     hipStream_t stream, uint32_t n_seg, size_t seg_cap) {
   HIPC(hipSetDevice(s->device));
   if (!stream) stream = s->stream;
   ShardCtx* c = s->shard_ctx(stream);  // this stream's batch state (batches in flight on other streams)
@@ -1255,7 +1262,7 @@ int shard_back_level(Snapshot* s, const kg_frec* d_in, size_t n_in, const uint32
     hipLaunchKernelGGL(k_shard_back_level, dim3(grid), dim3(256), 0, stream, s->ds, d_in, (uint64_t)n_in, d_n_in, d_out,
                        (uint64_t)cap, d_counts, d_res, d_err, (uint64_t*)c->vis, c->vis_slots - 1, d_done,
                        d_done ? done_words : 0u, heavy, (uint32_t*)c->qcnt,
-                       c->qcnt ? s->shard_back_budget : 0u, s->shard_vis_mode ? 1u : 0u);
+                       c->qcnt ? s->shard_back_budget : 0u, s->shard_vis_mode ? 1u : 0u, n_seg, (uint64_t)seg_cap);
     HIPC(hipGetLastError());
     hipLaunchKernelGGL(k_shard_heavy, dim3((uint32_t)s->n_cu * 4), dim3(256), 0, stream, s->ds, heavy, d_out,
                        (uint64_t)cap, d_counts, d_res, d_err, 1u, 1u, 0u, nullptr, 0u, nullptr, nullptr);

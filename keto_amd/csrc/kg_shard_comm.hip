@@ -70,6 +70,7 @@ struct ShardComm {
   // exchange k needed in the previous batch -- levels differ by orders of magnitude, and every
   // destination of exchange k gets B_k records on the wire whatever it holds
   std::vector<size_t> lb;
+  size_t bb = 0;  // escalation: records per rank of a backward-phase all-gather, learned like B_k
   unsigned long long* red = nullptr;  // [8 + levels]: the end-of-batch all-reduce (tot[5] | per-exchange largest)
   size_t red_cap = 0;
   std::vector<uint64_t> lvl_last, lb_last;  // the last batch: per exchange its largest bucket and B_k
@@ -251,6 +252,10 @@ static int h_alltoall2(ShardComm* c, const void* s0, void* r0, size_t b0, const 
 }
 
 // ------------------------------------------------------------------ small kernels
+// acc words (32, cleared per run): [0] flags, [1] largest bucket, [2] records sent, [3] records to other
+// ranks, [4..11] tot of the one-rank loop, [12..19] host all-reduce scratch, then:
+constexpr int ACC_LEFT = 20;  // records left at the end of the phases before the last
+constexpr int ACC_BACK = 21;  // largest backward-phase bucket
 // Per exchange k before it runs (keto_amd/sharded.py _check_fixed's device accumulators): acc[0] |=
 // overflow flags (c[N], or a bucket past B_k), acc[1] = largest bucket, acc[2] += records sent,
 // acc[3] += records sent to other ranks (what crosses xGMI), *lvl = exchange k's largest bucket (the
@@ -271,7 +276,7 @@ __global__ void k_sc_acc(const uint32_t* __restrict__ c, uint32_t N, uint32_t B,
     acc[1] = max(acc[1], mx);
     acc[2] += sum;
     acc[3] += wire;
-    *lvl = mx;
+    *lvl = max(*lvl, mx);  // exchange k runs once per forward phase (twice with escalation)
   }
 }
 
@@ -290,8 +295,44 @@ __global__ void k_sc_final(const uint32_t* __restrict__ c, uint32_t N, uint32_t 
     tot[0] = f & 1ull;
     tot[1] = (f >> 1) & 1ull;
     tot[2] = acc[1];
-    tot[3] = sum;
+    tot[3] = sum + acc[ACC_LEFT];
     tot[4] = 0;
+    tot[5] = acc[ACC_BACK];
+  }
+}
+
+// End of a forward phase that another phase follows (escalation): its flags and the records it left
+// (none, in a clean run) go to the accumulators k_sc_final reads.
+__global__ void k_sc_phase_end(const uint32_t* __restrict__ c, uint32_t N, uint32_t B, unsigned long long* acc) {
+  const uint32_t i = threadIdx.x;
+  const uint32_t v = i < N ? c[i] : 0u;
+  unsigned long long fl = (i < N && v > B) ? 1ull : 0ull, sum = v;
+  for (int off = 32; off; off >>= 1) {
+    fl |= __shfl_xor(fl, off, 64);
+    sum += __shfl_xor(sum, off, 64);
+  }
+  if (i == 0) {
+    acc[0] |= fl | c[N];
+    acc[ACC_LEFT] += sum;
+  }
+}
+
+// The one-rank device loop's version: counts (left, flags) of its two buffers, `cur` the last one.
+__global__ void k_sc_loop_end(const uint32_t* __restrict__ c0, const uint32_t* __restrict__ c1, int cur,
+                              unsigned long long* acc) {
+  if (threadIdx.x == 0) {
+    acc[0] |= c0[1] | c1[1];
+    acc[ACC_LEFT] += cur ? c1[0] : c0[0];
+  }
+}
+
+// A backward-phase bucket (count, flags): its overflow and its size (the largest one sizes the next
+// batch's backward buckets); with `left`, the records it holds are records left (the phase's last).
+__global__ void k_sc_back(const uint32_t* __restrict__ cb, uint32_t B, int left, unsigned long long* acc) {
+  if (threadIdx.x == 0) {
+    acc[0] |= cb[1] | (cb[0] > B ? 1u : 0u);
+    acc[ACC_BACK] = max(acc[ACC_BACK], (unsigned long long)cb[0]);
+    if (left) acc[ACC_LEFT] += cb[0];
   }
 }
 
@@ -299,13 +340,14 @@ __global__ void k_sc_final(const uint32_t* __restrict__ c, uint32_t N, uint32_t 
 // from the flags words of both buffers and the count of the last one; tot[2] = the bucket size the
 // levels needed, written by kg_shard_levels' fold.
 __global__ void k_sc_final1(const uint32_t* __restrict__ c0, const uint32_t* __restrict__ c1, int end,
-                            unsigned long long* tot) {
+                            const unsigned long long* acc, unsigned long long* tot) {
   if (threadIdx.x == 0) {
-    const uint32_t f = c0[1] | c1[1];
+    const unsigned long long f = c0[1] | c1[1] | acc[0];
     tot[0] = f & 1u;
     tot[1] = (f >> 1) & 1u;
-    tot[3] = end ? c1[0] : c0[0];
+    tot[3] = (end ? c1[0] : c0[0]) + acc[ACC_LEFT];
     tot[4] = 0;
+    tot[5] = acc[ACC_BACK];
   }
 }
 
@@ -353,7 +395,7 @@ static int grow(void** p, size_t* have, size_t want, size_t unit) {
 static int comm_setup(Snapshot* s, ShardComm* c) {
   HIPC(hipMalloc((void**)&c->acc, 32 * 8));
   HIPC(hipMemsetAsync(c->acc, 0, 32 * 8, c->run));
-  HIPC(hipMalloc((void**)&c->cnt, (3 * (size_t)KG_SHARD_MAX_RANKS + 2) * 4));
+  HIPC(hipMalloc((void**)&c->cnt, (4 * (size_t)KG_SHARD_MAX_RANKS + 8) * 4));
   uint64_t bad = 0;
   if (int rc = shard_bad_nodes(s, &bad)) return rc;
   size_t words = 0;
@@ -763,13 +805,22 @@ int shard_check(Snapshot* s, ShardComm* c, const kg_query* d_q, size_t n, int32_
   }
   uint32_t* counts[2] = {c->cnt, c->cnt + (N + 1)};
   uint32_t* rcv = c->cnt + 2 * (N + 1);
+  // the backward phase's (count, flags) pairs and received counts (escalation)
+  uint32_t* cb[2] = {c->cnt + 3 * N + 2, c->cnt + 3 * N + 4};
+  uint32_t* rcvb = c->cnt + 3 * N + 6;
   unsigned long long* acc = c->acc;
-  // tot[0..4] = (bucket overflow, visited overflow, largest bucket / bucket needed, records left, a
-  // query needs the general phase), then per exchange its largest bucket
+  // tot[0..5] = (bucket overflow, visited overflow, largest bucket / bucket needed, records left, a
+  // query needs the general phase, largest backward bucket), then per exchange its largest bucket
   unsigned long long* tot = xch ? c->red : c->acc + 4;
   unsigned long long* lvl = xch ? c->red + 8 : nullptr;
-  const size_t nred = xch ? (size_t)(8 + L) : 5;
+  const size_t nred = xch ? (size_t)(8 + L) : 6;
   std::vector<uint64_t> h(nred + 2);
+  // Escalation (kg_snapshot_tune "shard_budget"; no namespace program): the forward phase drops a query
+  // past its set-edge budget on a rank (ESC), a backward phase from the subjects' holders answers it, and
+  // queries past the backward budget too (ESC2) walk forward once more from their roots without one
+  // (keto_amd/sharded.py ShardedChecker's three phases; the single-GPU k_stream4 -> k_back -> grid chain)
+  const bool esc = shard_escalates(s);
+  if (esc && !c->bb) c->bb = B0;
   // reruns after a bucket overflow are bounded (kg_snapshot_tune "shard_max_reruns"); the visited table
   // grows 4x per visited-overflow rerun up to 2^34 keys, its own bound
   uint32_t run = 0;
@@ -778,48 +829,116 @@ int shard_check(Snapshot* s, ShardComm* c, const kg_query* d_q, size_t n, int32_
     if (xch) B = *std::max_element(c->lb.begin(), c->lb.end());
     else B = c->bucket ? c->bucket : B0;
     if (!xch) c->bucket = B;
+    if (esc) B = std::max(B, c->bb);  // the backward phase all-gathers N buckets of bb into recv
     if (int rc = grow_run(s, c, xch, B, words)) return rc;
-    HIPC(hipMemsetAsync(acc, 0, 12 * 8, st));
+    HIPC(hipMemsetAsync(acc, 0, 32 * 8, st));
     if (xch) HIPC(hipMemsetAsync(c->red, 0, (size_t)(8 + L) * 8, st));
-    // both count buffers start clear: the flags word counts[k][N] accumulates over the levels that
+    // every count buffer starts clear: the flags word counts[k][N] accumulates over the levels that
     // write buffer k, and shard_seed / shard_level clear only what they write
-    HIPC(hipMemsetAsync(c->cnt, 0, (3 * (size_t)N + 2) * 4, st));
+    HIPC(hipMemsetAsync(c->cnt, 0, (4 * (size_t)N + 6) * 4, st));
     if (int rc = shard_seed(s, d_q, n, gdepth, c->buf[0], xch ? c->lb[0] : B, counts[0], c->res, c->err, st))
       return rc;
     int cur = 0;
+    uint64_t wire = 0;  // bytes this rank puts on the wire (every destination but itself gets B_k records)
+    c->st[12] = 0;
     if (!xch) {
       // one rank, device loop: nothing to exchange -- gdepth levels back to back (per-XCD sub-buckets,
       // hub rows grid-wide; kg_shard_levels), hit reports stay local; the loop reports the bucket
       // size its levels needed (tot[2]), so an overflow reruns once at the right size
       kg_frec* bufs[2] = {c->buf[0], c->buf[1]};
-      if (int rc = shard_levels(s, gdepth, bufs, B, counts, 0, c->res, c->err, c->prune ? slots : 0, 0, &cur, st,
-                                tot + 2))
+      if (int rc = shard_levels(s, gdepth, bufs, B, counts, 0, c->res, c->err, c->prune ? slots : 0, esc ? 1 : 0, &cur,
+                                st, tot + 2))
         return rc;
       c->st[0] += (uint64_t)gdepth;
-      hipLaunchKernelGGL(k_sc_final1, dim3(1), dim3(64), 0, st, counts[0], counts[1], cur, tot);
+      if (esc) {
+        hipLaunchKernelGGL(k_sc_loop_end, dim3(1), dim3(64), 0, st, counts[0], counts[1], cur, acc);
+        HIPC(hipGetLastError());
+        // backward: this rank's escalated queries (the list) -> their subjects' holders -> gdepth
+        // reverse levels, the done bitmap counting members and queries past the backward budget
+        if (int rc = shard_back_list(s, slots, c->res, c->err, c->recv, B, cb[0], st)) return rc;
+        hipLaunchKernelGGL(k_sc_back, dim3(1), dim3(64), 0, st, cb[0], (uint32_t)B, 0, acc);
+        if (int rc = shard_back_seed(s, c->recv, B, cb[0], bufs[0], B, cb[1], st)) return rc;
+        hipLaunchKernelGGL(k_sc_back, dim3(1), dim3(64), 0, st, cb[1], (uint32_t)B, 0, acc);
+        uint32_t* cbl[2] = {cb[1], cb[0]};  // the seed wrote buffer 0 with cb[1]
+        int bc = 0;
+        for (int k = 0; k < gdepth; k++) {
+          if (int rc = shard_done(s, slots, c->res, c->err, 2, c->bits, words, st)) return rc;
+          if (int rc = shard_back_level(s, bufs[bc], B, cbl[bc], bufs[bc ^ 1], B, cbl[bc ^ 1], c->res, c->err, c->bits,
+                                        words, st))
+            return rc;
+          hipLaunchKernelGGL(k_sc_back, dim3(1), dim3(64), 0, st, cbl[bc ^ 1], (uint32_t)B, k == gdepth - 1 ? 1 : 0,
+                             acc);
+          bc ^= 1;
+          c->st[12]++;
+        }
+        // final forward phase: queries past both budgets, re-seeded at their roots, no budget
+        if (int rc = shard_refwd_seed(s, slots, c->res, c->err, bufs[0], B, counts[0], st)) return rc;
+        HIPC(hipMemsetAsync(counts[1], 0, (N + 1) * 4, st));
+        if (int rc = shard_levels(s, gdepth, bufs, B, counts, 0, c->res, c->err, c->prune ? slots : 0, 0, &cur, st,
+                                  tot + 2))
+          return rc;
+        c->st[12] += (uint64_t)gdepth;
+      }
+      hipLaunchKernelGGL(k_sc_final1, dim3(1), dim3(64), 0, st, counts[0], counts[1], cur, acc, tot);
       HIPC(hipGetLastError());
     }
-    uint64_t wire = 0;  // bytes this rank puts on the wire (every destination but itself gets B_k records)
-    for (int k = 0; xch && k < L; k++) {
-      const size_t Bk = c->lb[(size_t)k], Bn = c->lb[(size_t)k + 1];
-      hipLaunchKernelGGL(k_sc_acc, dim3(1), dim3(64), 0, st, counts[cur], N, (uint32_t)Bk, (uint32_t)c->rank, acc,
-                         lvl + k);
-      HIPC(hipGetLastError());
-      if (int rc = x_alltoall2(c, counts[cur], rcv, 4, c->buf[cur], c->recv, Bk * sizeof(kg_frec))) return rc;
-      wire += (uint64_t)(N - 1) * (4 + Bk * sizeof(kg_frec));
-      const uint32_t* done = nullptr;
-      if (c->prune && k > 0) {
-        if (int rc = shard_done(s, slots, c->res, c->err, 0, c->bits, words, st)) return rc;
-        if (int rc = x_allgather(c, c->bits, c->bits_all, (size_t)words * 4)) return rc;
-        wire += (uint64_t)(N - 1) * words * 4;
-        done = c->bits_all;
+    // the forward exchange protocol: L exchanges, then (escalation) the backward phase over all-gathers
+    // and a second forward pass for the queries past both budgets
+    for (int phase = 0; xch && phase < (esc ? 2 : 1); phase++) {
+      for (int k = 0; k < L; k++) {
+        const size_t Bk = c->lb[(size_t)k], Bn = c->lb[(size_t)k + 1];
+        hipLaunchKernelGGL(k_sc_acc, dim3(1), dim3(64), 0, st, counts[cur], N, (uint32_t)Bk, (uint32_t)c->rank, acc,
+                           lvl + k);
+        HIPC(hipGetLastError());
+        if (int rc = x_alltoall2(c, counts[cur], rcv, 4, c->buf[cur], c->recv, Bk * sizeof(kg_frec))) return rc;
+        wire += (uint64_t)(N - 1) * (4 + Bk * sizeof(kg_frec));
+        const uint32_t* done = nullptr;
+        if (c->prune && k > 0) {
+          // the forward phase of an escalating batch: escalated queries are done here too
+          if (int rc = shard_done(s, slots, c->res, c->err, esc && phase == 0 ? 1 : 0, c->bits, words, st)) return rc;
+          if (int rc = x_allgather(c, c->bits, c->bits_all, (size_t)words * 4)) return rc;
+          wire += (uint64_t)(N - 1) * words * 4;
+          done = c->bits_all;
+        }
+        const int nx = cur ^ 1;
+        if (int rc = shard_level(s, c->recv, (size_t)N * Bk, rcv, c->buf[nx], Bn, counts[nx], c->res, c->err, done,
+                                 words, st, N, Bk))
+          return rc;
+        cur = nx;
+        c->st[phase ? 12 : 0]++;
       }
-      const int nx = cur ^ 1;
-      if (int rc = shard_level(s, c->recv, (size_t)N * Bk, rcv, c->buf[nx], Bn, counts[nx], c->res, c->err, done, words,
-                               st, N, Bk))
-        return rc;
-      cur = nx;
-      c->st[0]++;
+      if (!esc || phase == 1) break;
+      hipLaunchKernelGGL(k_sc_phase_end, dim3(1), dim3(64), 0, st, counts[cur], N, (uint32_t)c->lb[(size_t)L], acc);
+      HIPC(hipGetLastError());
+      // backward phase: every rank sees every backward record (a node's parents sit in their owners'
+      // rows, and every rank holds the reverse set-adjacency of its own rows), so each level all-gathers
+      // fixed buckets of bb records with their counts; gdepth levels after the seed drain it (rest depths
+      // fall by one per level; the last one only delivers hit / escalation reports)
+      const size_t bb = c->bb;
+      if (int rc = shard_back_list(s, slots, c->res, c->err, c->buf[0], bb, cb[0], st)) return rc;
+      hipLaunchKernelGGL(k_sc_back, dim3(1), dim3(64), 0, st, cb[0], (uint32_t)bb, 0, acc);
+      if (int rc = x_allgather(c, cb[0], rcvb, 4)) return rc;
+      if (int rc = x_allgather(c, c->buf[0], c->recv, bb * sizeof(kg_frec))) return rc;
+      wire += (uint64_t)(N - 1) * (4 + bb * sizeof(kg_frec));
+      if (int rc = shard_back_seed(s, c->recv, (size_t)N * bb, rcvb, c->buf[1], bb, cb[1], st, N, bb)) return rc;
+      hipLaunchKernelGGL(k_sc_back, dim3(1), dim3(64), 0, st, cb[1], (uint32_t)bb, 0, acc);
+      int bc = 1;
+      for (int k = 0; k < gdepth; k++) {
+        if (int rc = x_allgather(c, cb[bc], rcvb, 4)) return rc;
+        if (int rc = x_allgather(c, c->buf[bc], c->recv, bb * sizeof(kg_frec))) return rc;
+        if (int rc = shard_done(s, slots, c->res, c->err, 2, c->bits, words, st)) return rc;
+        if (int rc = x_allgather(c, c->bits, c->bits_all, (size_t)words * 4)) return rc;
+        wire += (uint64_t)(N - 1) * (8 + bb * sizeof(kg_frec) + words * 4);
+        if (int rc = shard_back_level(s, c->recv, (size_t)N * bb, rcvb, c->buf[bc ^ 1], bb, cb[bc ^ 1], c->res, c->err,
+                                      c->bits_all, words, st, N, bb))
+          return rc;
+        hipLaunchKernelGGL(k_sc_back, dim3(1), dim3(64), 0, st, cb[bc ^ 1], (uint32_t)bb, k == gdepth - 1 ? 1 : 0, acc);
+        bc ^= 1;
+        c->st[12]++;
+      }
+      // final forward phase: this rank's queries past both budgets, re-seeded at their roots' owners
+      if (int rc = shard_refwd_seed(s, slots, c->res, c->err, c->buf[0], c->lb[0], counts[0], st)) return rc;
+      cur = 0;
     }
     if (xch) {
       hipLaunchKernelGGL(k_sc_final, dim3(1), dim3(64), 0, st, counts[cur], N, (uint32_t)c->lb[(size_t)L], acc, tot);
@@ -876,6 +995,7 @@ int shard_check(Snapshot* s, ShardComm* c, const kg_query* d_q, size_t n, int32_
           c->bucket = std::min(top, std::max<size_t>(2 * B, (size_t)(need * 1.25) + 1024));
         }
       }
+      if (esc && h[5] > c->bb) c->bb = std::min<size_t>(1ull << 30, std::max((size_t)(h[5] * 1.25) + 1024, 2 * c->bb));
       if (h[1]) {
         c->st[4]++;
         if (s->shard_vis_log2 >= 34) return set_error(KG_ERR_RESOURCE_CODE, "sharded visited table overflow");
@@ -884,6 +1004,7 @@ int shard_check(Snapshot* s, ShardComm* c, const kg_query* d_q, size_t n, int32_
       continue;
     }
     if (h[3]) return set_error(-1, "sharded batch: records left after %d levels", xch ? L : gdepth);
+    if (esc && h[5] * 2 < c->bb) c->bb = std::max<size_t>(1024, std::min<size_t>(c->bb, (size_t)(h[5] * 1.25) + 1024));
     if (xch) {
       // next batch: each exchange's bucket 25 % above what it needed this batch (shrinking slowly)
       c->st[9] = wire;

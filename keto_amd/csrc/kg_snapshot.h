@@ -386,10 +386,11 @@ int shard_levels(Snapshot* s, int levels, kg_frec* d_buf[2], size_t cap, uint32_
 int shard_back_list(Snapshot* s, size_t n, const uint8_t* d_res, const uint32_t* d_err, kg_frec* d_list, size_t cap,
                     uint32_t* d_counts, hipStream_t stream);
 int shard_back_seed(Snapshot* s, const kg_frec* d_list, size_t m, const uint32_t* d_m, kg_frec* d_out, size_t cap,
-                    uint32_t* d_counts, hipStream_t stream);
+                    uint32_t* d_counts, hipStream_t stream, uint32_t n_seg = 1, size_t seg_cap = 0);
 int shard_back_level(Snapshot* s, const kg_frec* d_in, size_t n_in, const uint32_t* d_n_in, kg_frec* d_out, size_t cap,
                      uint32_t* d_counts, uint8_t* d_res, uint32_t* d_err, const uint32_t* d_done, uint32_t done_words,
-                     hipStream_t stream);
+                     hipStream_t stream, uint32_t n_seg = 1, size_t seg_cap = 0);
+bool shard_escalates(const Snapshot* s);  // the escalation phases run (shard_budget, no program, reverse index)
 int shard_refwd_seed(Snapshot* s, size_t n, const uint8_t* d_res, const uint32_t* d_err, kg_frec* d_out, size_t cap,
                      uint32_t* d_counts, hipStream_t stream);
 int shard_held(Snapshot* s, uint32_t* d_bits, size_t words, int import, hipStream_t stream);
