@@ -323,7 +323,7 @@ def bench_expand(a):
                "kg_expand_batch")
     rec = np.ctypeslib.as_array(C.cast(buf.nodes, C.POINTER(C.c_uint8)), shape=(int(buf.n_nodes) * 20,)).view(
         np.dtype([("type", "u1"), ("is_set", "u1"), ("pad", "<u2"), ("ns", "<u4"), ("obj", "<u4"), ("rel", "<u4"),
-                  ("n_children", "<u4")])) if buf.n_nodes else None
+                  ("n_children", "<u4")])).copy() if buf.n_nodes else None
     L.kg_tree_free(C.byref(buf))
     if rec is not None:
         unions = rec["type"] == 1  # kg_tree_node type 1 = union (include/ketogpu.h)
