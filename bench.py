@@ -60,6 +60,14 @@ def parse(argv=None):
                     help="check mode: timed batches of the hash-sharded sub-line (the C4 engine through "
                          "kg_check_batch_device over RCCL, one shard per rank; 0 = off)")
     ap.add_argument("--sharded-warmup", type=int, default=4)
+    ap.add_argument("--expand-steps", type=int, default=6,
+                    help="check mode, one rank: timed calls of the C5 expand sub-line over the headline graph (0 = off)")
+    ap.add_argument("--expand-inflight", type=int, default=4)
+    ap.add_argument("--c3-steps", type=int, default=20,
+                    help="check mode, one rank: timed batches of the C3 sub-line (OPL rewrites; 0 = off)")
+    ap.add_argument("--c3-tuples", type=float, default=1e7, help="C3 sub-line graph size (BASELINE configs[2]: 10M)")
+    ap.add_argument("--c3-inflight", type=int, default=6)
+    ap.add_argument("--c3-parity", type=int, default=200_000)
     ap.add_argument("--sharded-inflight", type=int, default=0,
                     help="sharded batches in flight per rank, each with its own communicator (0: 4 at one rank, 1 "
                          "across ranks -- streams share HIP's hardware queues, and collectives of different "
@@ -236,51 +244,8 @@ def bench_expand(a):
     roots = hot_group_roots(snap.synth_ids(), a.roots)
     depth = a.global_depth if a.global_depth != 10 else 5
 
-    def step():
-        buf = _lib.kg_tree_buf()
-        _lib.check(L.kg_expand_batch(snap.handle, roots.ctypes.data_as(C.c_void_p), a.roots, depth, C.byref(buf)),
-                   "kg_expand_batch")
-        off = np.ctypeslib.as_array(buf.root_off, shape=(a.roots + 1,)).copy() if buf.root_off else None
-        res = (buf.n_nodes, buf.kernel_ms, off)
-        L.kg_tree_free(C.byref(buf))
-        return res
-
     P = max(1, a.inflight)  # batches in flight: P host threads, each on its own lane (stream + buffers)
-    import threading
-    nw = min(P, a.steps)
-    results = [None] * a.steps
-    errors = []
-    warm = threading.Barrier(nw + 1)  # every lane warmed up
-    go = threading.Barrier(nw + 1)    # timed region starts (after the ranks' barrier)
-
-    def worker(p):
-        try:
-            for _ in range(max(1, -(-a.warmup // nw))):  # warm-up: this thread's lane and buffers
-                step()
-        except Exception as e:  # noqa: BLE001 -- re-raised below
-            errors.append(e)
-        warm.wait()
-        go.wait()
-        try:
-            for k in range(p, a.steps, nw):
-                if not errors:
-                    results[k] = step()
-        except Exception as e:  # noqa: BLE001
-            errors.append(e)
-
-    th = [threading.Thread(target=worker, args=(p,)) for p in range(nw)]
-    for t in th:
-        t.start()
-    warm.wait()
-    if dist:
-        dist.barrier()
-    t0 = time.perf_counter()
-    go.wait()
-    for t in th:
-        t.join()
-    el = time.perf_counter() - t0
-    if errors:
-        raise errors[0]
+    el, results = expand_steps(L, snap, roots, depth, P, a.steps, a.warmup, dist)
     el, _ = aggregate(dist, el, 0.0, f"cuda:{local}" if a.backend == "nccl" else None)
     nodes = sum(r[0] for r in results)
     kms = sum(r[1] for r in results)
@@ -314,28 +279,9 @@ def bench_expand(a):
             L.kg_tree_free(C.byref(buf))
         out["largest_root"] = {"records": n_big, "walk_kernel_ms": float(min(walk)),
                                "expand_tail": a.expand_tail}
-    # roofline of the expand launch chain (8 B per row opened, 4 B per edge read, 12 B per
-    # emitted tree node), from one more call's records (every step expands the same roots) over the
-    # calls' mean device time (HIP events around k_expand_lds / _hash / _hbm + k_expand_compact on the
-    # call's stream; several calls overlap, so a call's time is contended wall time)
-    buf = _lib.kg_tree_buf()
-    _lib.check(L.kg_expand_batch(snap.handle, roots.ctypes.data_as(C.c_void_p), a.roots, depth, C.byref(buf)),
-               "kg_expand_batch")
-    rec = np.ctypeslib.as_array(C.cast(buf.nodes, C.POINTER(C.c_uint8)), shape=(int(buf.n_nodes) * 20,)).view(
-        np.dtype([("type", "u1"), ("is_set", "u1"), ("pad", "<u2"), ("ns", "<u4"), ("obj", "<u4"), ("rel", "<u4"),
-                  ("n_children", "<u4")])).copy() if buf.n_nodes else None
-    L.kg_tree_free(C.byref(buf))
-    if rec is not None:
-        unions = rec["type"] == 1  # kg_tree_node type 1 = union (include/ketogpu.h)
-        R, E, T = int(unions.sum()), int(rec["n_children"][unions].sum()), int(len(rec))
-        byts = 8 * R + 4 * E + 12 * T
-        ms = kms / a.steps
-        out["roofline"] = {"kernel": "k_expand_lds/_hash/_hbm + k_expand_compact (one call's chain)", "bound": "hbm",
-                           "achieved": byts / (ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                           "frac": byts / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "traffic": None,
-                           "bytes_model": "8*unions(rows opened) + 4*children(edges read) + 12*tree records",
-                           "bytes_per_call": byts, "rows_opened": R, "edges_read": E, "records": T,
-                           "call_kernel_ms": ms}
+    rf = expand_roofline(L, snap, roots, depth, kms / a.steps)
+    if rf:
+        out["roofline"] = rf
     orc = None
     if rank == 0 and ((a.parity_roots > 0 and off is not None) or (world == 1 and a.cpu_seconds > 0)):
         orc = expand_oracle(snap)
@@ -352,6 +298,84 @@ def bench_expand(a):
             sys.exit(1)
     if dist:
         dist.destroy_process_group()
+
+
+def expand_steps(L, snap, roots: np.ndarray, depth: int, P: int, steps: int, warmup: int, dist=None):
+    """C5's timed region: P host threads, each on its own lane (stream + cached buffers), run `steps`
+    kg_expand_batch calls over the same roots after a warm-up, between barriers.  Returns (elapsed s,
+    per call (tree records, kernel ms, root offsets))."""
+    from keto_amd import _lib
+    n = len(roots)
+
+    def step():
+        buf = _lib.kg_tree_buf()
+        _lib.check(L.kg_expand_batch(snap.handle, roots.ctypes.data_as(C.c_void_p), n, depth, C.byref(buf)),
+                   "kg_expand_batch")
+        off = np.ctypeslib.as_array(buf.root_off, shape=(n + 1,)).copy() if buf.root_off else None
+        res = (buf.n_nodes, buf.kernel_ms, off)
+        L.kg_tree_free(C.byref(buf))
+        return res
+
+    nw = min(P, steps)
+    results = [None] * steps
+    errors = []
+    warm = threading.Barrier(nw + 1)  # every lane warmed up
+    go = threading.Barrier(nw + 1)    # timed region starts (after the ranks' barrier)
+
+    def worker(p):
+        try:
+            for _ in range(max(1, -(-warmup // nw))):  # warm-up: this thread's lane and buffers
+                step()
+        except Exception as e:  # noqa: BLE001 -- re-raised below
+            errors.append(e)
+        warm.wait()
+        go.wait()
+        try:
+            for k in range(p, steps, nw):
+                if not errors:
+                    results[k] = step()
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    th = [threading.Thread(target=worker, args=(p,)) for p in range(nw)]
+    for t in th:
+        t.start()
+    warm.wait()
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    go.wait()
+    for t in th:
+        t.join()
+    el = time.perf_counter() - t0
+    if errors:
+        raise errors[0]
+    return el, results
+
+
+def expand_roofline(L, snap, roots: np.ndarray, depth: int, call_ms: float):
+    """Roofline of the expand launch chain (8 B per row opened, 4 B per edge read, 12 B per
+    emitted tree node), from one more call's records (every step expands the same roots) over the calls'
+    mean device time (HIP events around k_expand_lds / _hash / _hbm + k_expand_compact on the call's
+    stream; several calls overlap, so a call's time is contended wall time)."""
+    from keto_amd import _lib
+    buf = _lib.kg_tree_buf()
+    _lib.check(L.kg_expand_batch(snap.handle, roots.ctypes.data_as(C.c_void_p), len(roots), depth, C.byref(buf)),
+               "kg_expand_batch")
+    rec = np.ctypeslib.as_array(C.cast(buf.nodes, C.POINTER(C.c_uint8)), shape=(int(buf.n_nodes) * 20,)).view(
+        np.dtype([("type", "u1"), ("is_set", "u1"), ("pad", "<u2"), ("ns", "<u4"), ("obj", "<u4"), ("rel", "<u4"),
+                  ("n_children", "<u4")])).copy() if buf.n_nodes else None
+    L.kg_tree_free(C.byref(buf))
+    if rec is None or call_ms <= 0:
+        return None
+    unions = rec["type"] == 1  # kg_tree_node type 1 = union (include/ketogpu.h)
+    R, E, T = int(unions.sum()), int(rec["n_children"][unions].sum()), int(len(rec))
+    byts = 8 * R + 4 * E + 12 * T
+    gbs = byts / (call_ms * 1e-3) / 1e9
+    return {"kernel": "k_expand_lds/_hash/_hbm + k_expand_compact (one call's chain)", "bound": "hbm",
+            "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS, "traffic": None,
+            "bytes_model": "8*unions(rows opened) + 4*children(edges read) + 12*tree records",
+            "bytes_per_call": byts, "rows_opened": R, "edges_read": E, "records": T, "call_kernel_ms": call_ms}
 
 
 def expand_oracle(snap):
@@ -1160,24 +1184,38 @@ def main():
         if world == 1 and a.cpu_seconds > 0:
             out["cpu_baseline"] = cpu_baseline(orc, q0, a, cpus)
     bad = a.parity > 0 and rank == 0 and out["parity"]["mismatches"] + out["parity"]["canonical_mismatches"]
-    if a.sharded_steps > 0 and a.preset == 0 and not a.heavy_tail:
-        # the hash-sharded C4 engine beside the replica headline; a watchdog keeps a
-        # hung collective from costing the whole line: rank 0 then prints it without the sub-line
-        def on_timeout():
-            if rank == 0:
-                out["sharded"] = {"error": "sharded sub-line did not finish within %.0f s" % a.sharded_timeout}
-                print(json.dumps(out), flush=True)
-            os._exit(1 if bad else 0)
+    # the other configurations beside the headline, on the driver's own runs (C3 and C5 had
+    # builder-run numbers only): one rank -- C5 expand over the headline graph, C3 at its config size;
+    # every rank -- the hash-sharded C4 engine (item 1).  A watchdog keeps a hung collective from costing
+    # the whole line: rank 0 then prints it without the unfinished sub-line.
+    current = [None]
+
+    def on_timeout():
+        if rank == 0:
+            out[current[0] or "sub_lines"] = {"error": "did not finish within %.0f s" % a.sharded_timeout}
+            print(json.dumps(out), flush=True)
+        os._exit(1 if bad else 0)
+
+    def sub_line(name, fn):
+        current[0] = name
         wd = threading.Timer(a.sharded_timeout, on_timeout)
         wd.daemon = True
         wd.start()
         try:
-            out["sharded"] = sharded_leg(a, snap, size_param, dist, rank, world, local, backend, orc)
+            out[name] = fn()
         except Exception as e:  # noqa: BLE001 -- reported in the line; the replica headline stands
-            out["sharded"] = {"error": f"{type(e).__name__}: {e}"}
+            out[name] = {"error": f"{type(e).__name__}: {e}"}
         wd.cancel()
-        sp = [x.get("parity") for x in (out["sharded"], out["sharded"].get("exchange") or {}) if x.get("parity")]
-        bad = bad or any(x["mismatches"] + x["canonical_mismatches"] for x in sp)
+        subs = [out[name]] + [v for v in out[name].values() if isinstance(v, dict)]
+        return any(x["parity"]["mismatches"] + x["parity"].get("canonical_mismatches", 0)
+                   for x in subs if isinstance(x.get("parity"), dict) and "mismatches" in x["parity"])
+
+    if world == 1 and a.preset == 0 and not a.heavy_tail and a.expand_steps > 0:
+        bad = sub_line("expand", lambda: expand_leg(a, snap, orc)) or bad
+    if world == 1 and a.preset == 0 and not a.heavy_tail and a.c3_steps > 0:
+        bad = sub_line("c3", lambda: c3_leg(a, local)) or bad
+    if a.sharded_steps > 0 and a.preset == 0 and not a.heavy_tail:
+        bad = sub_line("sharded", lambda: sharded_leg(a, snap, size_param, dist, rank, world, local, backend, orc)) or bad
     if rank == 0:
         print(json.dumps(out), flush=True)
         if bad:
@@ -1187,6 +1225,110 @@ def main():
             sys.exit(1)
     if dist:
         dist.destroy_process_group()
+
+
+def expand_leg(a, snap, orc) -> dict:
+    """Config C5 (BASELINE.json configs[4]) beside the headline, on the headline's own graph: BuildTree of
+    the --roots most popular group#member sets at the global max_read_depth 5, one
+    kg_expand_batch call per step (trees to host memory), --expand-inflight calls in flight; roofline of
+    the expand chain and parity against the oracle's BuildTree (the 10 largest roots + a sample).  The
+    full C5 bench (16 calls in flight over 16 HIP hardware queues, CPU baseline) is --mode expand."""
+    from keto_amd import _lib
+    from keto_amd.synth import hot_group_roots
+    L = _lib.load()
+    roots = hot_group_roots(snap.synth_ids(), a.roots)
+    depth = 5
+    P, K = max(1, a.expand_inflight), a.expand_steps
+    el, results = expand_steps(L, snap, roots, depth, P, K, P)
+    nodes = sum(r[0] for r in results)
+    kms = sum(r[1] for r in results)
+    off = results[-1][2]
+    res = {"metric": "expand trees/sec (C5: batched BuildTree, hot group#member roots)",
+           "value": len(roots) * K / el, "unit": "trees/s", "steps": K, "inflight": P, "ms_per_step": el / K * 1e3,
+           "tree_nodes_per_s": nodes / el, "kernel_ms_per_call": kms / K,
+           "config": {"workload": "C5: %d hot roots of the headline graph, max_read_depth %d" % (len(roots), depth)}}
+    rf = expand_roofline(L, snap, roots, depth, kms / K)
+    if rf:
+        res["roofline"] = rf
+    if orc is not None and a.parity_roots > 0 and off is not None:
+        o = orc.o
+        o.nd = orc.nd
+        res["parity"] = expand_parity(snap, roots, np.diff(off.astype(np.int64)), depth, a, o)
+    return res
+
+
+def c3_leg(a, local) -> dict:
+    """Config C3 (BASELINE.json configs[2]: the generator graph at --c3-tuples, default its 10M, plus the
+    folder forest and the OPL namespace view / edit / share) beside the headline: 1 M checks per batch
+    through kg_check_batch_device, --c3-inflight batches in flight (C3's occupancy set: stream_wgs 3,
+    grid_wgs 4, back_wgs 1), distinct batches, parity of the first timed batch against the oracle
+    evaluating the program (Go-order DFS + canonical policy)."""
+    import copy
+    import torch
+    from keto_amd import _lib
+    L = _lib.load()
+    a3 = copy.copy(a)
+    a3.preset, a3.stream_wgs, a3.grid_wgs, a3.back_wgs = 1, 3, 4, 1
+    t0 = time.time()
+    snap3, _ = build_synthetic(a3, a.c3_tuples, device=local)
+    apply_tune(snap3, a3)
+    t_build = time.time() - t0
+    dev = f"cuda:{local}"
+    B, P, K = a.batch, max(1, a.c3_inflight), a.c3_steps
+    W = P
+    streams = [torch.cuda.Stream(local) for _ in range(P)]
+    dqs = []
+    for k in range(W + K):
+        d = torch.empty((B, 7), dtype=torch.int32, device=dev)
+        _lib.check(L.kg_synth_queries(snap3.handle, 700000 + 7919 * k, B, d.data_ptr()), "kg_synth_queries")
+        dqs.append(d)
+    outs = [torch.empty(B, dtype=torch.uint8, device=dev) for _ in range(W + K)]
+    errs = [torch.empty(B, dtype=torch.int32, device=dev) for _ in range(P)]
+    st = _lib.kg_stats()
+
+    def phase(k0, n):
+        errors = []
+
+        def worker(p):
+            try:
+                for k in range(p, n, P):
+                    _lib.check(L.kg_check_batch_device(snap3.handle, dqs[k0 + k].data_ptr(), B, a.global_depth,
+                                                       outs[k0 + k].data_ptr(), errs[p].data_ptr(),
+                                                       C.byref(st) if (p == 0 and k == 0) else None,
+                                                       C.c_void_p(streams[p].cuda_stream)), "kg_check_batch_device")
+                streams[p].synchronize()
+            except Exception as x:  # noqa: BLE001
+                errors.append(x)
+
+        th = [threading.Thread(target=worker, args=(p,)) for p in range(min(P, n))]
+        [t.start() for t in th]
+        [t.join() for t in th]
+        if errors:
+            raise errors[0]
+
+    phase(0, W)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    phase(W, K)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t1
+    assert (torch.cat(errs).cpu().numpy() == 0).all(), "unexpected errors in the synthetic C3 batch"
+    r0 = outs[W].cpu().numpy()
+    res = {"metric": "permission checks/sec (C3: OPL view/edit/share rewrites)", "value": B * K / el,
+           "unit": "checks/s", "steps": K, "inflight": P, "ms_per_step": el / K * 1e3,
+           "config": {"workload": "C3 generator @ %.4g tuples (rows), %d checks/step, max_read_depth %d"
+                                  % (snap3.info()["rows"], B, a.global_depth),
+                      "materialized": snap3.materialized(), "tune": dict(snap3.__dict__.get("tuned", {}))},
+           "allowed_fraction": float(r0.mean()), "snapshot_build_s": t_build,
+           "tiers": {"light": int(st.n_light), "back": int(st.n_back), "grid": int(st.n_grid),
+                     "general": int(st.n_general), "no_holder": int(st.n_no_holder)}}
+    if a.c3_parity > 0:
+        orc3 = CheckOracle(snap3, a3, effective_cpus()["effective"])
+        res["parity"] = orc3.parity(dqs[W].cpu().numpy().view(np.uint32), r0, a.c3_parity,
+                                    min(a.parity_canonical, a.c3_parity))
+        orc3.o.close()
+    snap3.close()
+    return res
 
 
 def sharded_leg(a, snap, size_param, dist, rank, world, local, backend, orc) -> dict:
@@ -1421,6 +1563,7 @@ class CheckOracle:
         _lib.check(L.kg_snapshot_export_csr(snap.handle, p(row_off), p(row_subj), p(nd[0]), p(nd[1]), p(nd[2])),
                    "kg_snapshot_export_csr")
         self.by_node = a.preset == 0
+        self.nd = nd  # node triples (the C5 expand parity's root check)
         t = time.perf_counter()
         self.o = Oracle.from_csr(0, nd[0], nd[1], nd[2], row_off, row_subj, with_node_map=not self.by_node,
                                  nthreads=min(nthreads, 64))
