@@ -12,10 +12,11 @@ INFLIGHT=${INFLIGHT:-4}
 EXTRA="--preset $PRESET --tuples $TUPLES --inflight $INFLIGHT ${EXTRA:-}"
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG} -o run --output-format csv -- python3 bench.py --steps 40 --warmup 6 --cpu-seconds 0 --parity 0 --latency-batches 0 --host-calls 0 $EXTRA > gpurun_out/prof_${TAG}.log 2>&1; rc=$?; echo "prof rc=$rc"
+NOSUB="--expand-steps 0 --c3-steps 0 --sharded-steps 0"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG} -o run --output-format csv -- python3 bench.py --steps 40 --warmup 6 --cpu-seconds 0 --parity 0 --latency-batches 0 --host-calls 0 $NOSUB $EXTRA > gpurun_out/prof_${TAG}.log 2>&1; rc=$?; echo "prof rc=$rc"
 [ $rc -eq 0 ] || exit $rc
 python3 scripts/timeline.py gpurun_out/prof_${TAG}/run_kernel_trace.csv > gpurun_out/timeline_${TAG}.txt || true
-B="python3 bench.py --steps 4 --warmup 2 --cpu-seconds 0 --parity 0 --latency-batches 0 --host-calls 0 $EXTRA"
+B="python3 bench.py --steps 4 --warmup 2 --cpu-seconds 0 --parity 0 --latency-batches 0 --host-calls 0 $NOSUB $EXTRA"
 RX="k_stream4|k_resolve|k_back|k_grid_level|k_fsplit"
 timeout -s KILL 150 rocprofv3 --kernel-include-regex "$RX" --pmc FETCH_SIZE -d gpurun_out/pmc_${TAG}_fetch -o run --output-format csv -- $B > gpurun_out/pmc_${TAG}_fetch.log 2>&1; rc=$?; echo "fetch rc=$rc"
 [ $rc -eq 0 ] || exit $rc
