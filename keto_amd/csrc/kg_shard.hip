@@ -78,7 +78,8 @@ constexpr int SV_PROBES = 64;
 // query past both (ESC2_BIT) is walked forward once more without any budget (kg_shard_refwd_seed) --
 // the single-GPU engine's stream -> backward -> grid tier chain.
 constexpr uint32_t ESC_BIT = 0x40000000u, ESC2_BIT = 0x20000000u;
-constexpr int QCNT_LOG2 = 22;  // per-rank edge counters, hashed by query (a collision only escalates early)
+constexpr int QCNT_LOG2 = 22;  // per-rank edge counters, hashed by query (a collision only escalates early:
+                               // every query whose row a full counter drops is marked escalated)
 // A received record whose set row is longer than this is expanded by the whole grid (k_shard_heavy).
 constexpr uint32_t SHARD_HEAVY = 4096, SHARD_HEAVY_CAP = 1u << 20;
 constexpr uint32_t HEAVY_TILE = 256;              // edges per k_shard_heavy tile
@@ -578,11 +579,16 @@ __global__ __launch_bounds__(256) void k_shard_level(DevSnap s, const kg_frec* _
             if (len && budget) {  // escalation: this rank's set-edge count of the query passes the budget
               const uint32_t add = (uint32_t)min(len, (uint64_t)budget);
               const uint32_t old = atomicAdd(&qcnt[mix64(r.q) & ((1u << QCNT_LOG2) - 1)], add);
-              if (old < budget && old + add >= budget) {
+              if (old + add >= budget) {
+                // escalated: the backward phase answers it.  Counters are hashed by query, so a slot can
+                // be past the budget because of ANOTHER query: every record whose row is dropped marks its
+                // own query (not only the one that crossed the threshold) -- a dropped row of an unmarked
+                // query would end its walk as NotMember (round 5: 2-4 missed members in 20 k C4 checks at
+                // budget 2)
                 if ((r.q >> Q_BITS) == me) atomicOr(&err[r.q & Q_MASK], ESC_BIT);
                 else esc_out = true;
+                len = 0;
               }
-              if (old + add >= budget) len = 0;  // escalated: the backward phase answers it
             }
           }
         }
@@ -764,11 +770,11 @@ __global__ __launch_bounds__(256) void k_shard_back_level(DevSnap s, const kg_fr
           if (len && budget) {  // the reverse search's own budget: past it, the final forward phase
             const uint32_t add = (uint32_t)min(len, (uint64_t)budget);
             const uint32_t old = atomicAdd(&qcnt[mix64(r.q) & ((1u << QCNT_LOG2) - 1)], add);
-            if (old < budget && old + add >= budget) {
+            if (old + add >= budget) {  // (every query whose row is dropped is marked: see k_shard_level)
               if ((r.q >> Q_BITS) == me) atomicOr(&err[r.q & Q_MASK], ESC2_BIT);
               else esc_out = true;
+              len = 0;
             }
-            if (old + add >= budget) len = 0;
           }
         }
       }

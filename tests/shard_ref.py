@@ -197,12 +197,11 @@ class CpuShardOps:
                     old = self.qcnt.get(q, 0)
                     add = min(len(kids), self.budget)
                     self.qcnt[q] = old + add
-                    if old < self.budget <= old + add:
+                    if old + add >= self.budget:  # every dropped row marks its query (kg_shard.hip k_shard_level)
                         if home == self.rank:
                             err[qi] = int(err[qi]) | ESC_BIT
                         else:
                             self._emit(out, cap, counts, home, [q, ESC, 0, 0])
-                    if old + add >= self.budget:
                         kids = []
                 for c in kids:
                     self._emit(out, cap, counts, self.owner[c], [q, c, np.uint32(subj).view(np.int32), d - 1])
@@ -257,12 +256,11 @@ class CpuShardOps:
                 old = self.qcnt.get(q, 0)
                 add = min(len(parents), self.back_budget)
                 self.qcnt[q] = old + add
-                if old < self.back_budget <= old + add:
+                if old + add >= self.back_budget:  # every dropped row marks its query (k_shard_back_level)
                     if home == self.rank:
                         err[qi] = int(err[qi]) | ESC2_BIT
                     else:
                         self._emit(out, cap, counts, 0, [q, ESC, 0, 0], 1)
-                if old + add >= self.back_budget:
                     parents = []
             for p in parents:
                 if p == root:
