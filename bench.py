@@ -56,7 +56,7 @@ def parse(argv=None):
     ap.add_argument("--stream-gate", type=int, default=0,
                     help="kg_snapshot_tune stream_gate: k_stream4 launches of different batches at once (0 = no cap)")
     ap.add_argument("--stream-ecap", type=int, default=512, help="kg_snapshot_tune stream_ecap (stream-tier edges per query, 0 = none)")
-    ap.add_argument("--sharded-steps", type=int, default=20,
+    ap.add_argument("--sharded-steps", type=int, default=60,
                     help="check mode: timed batches of the hash-sharded sub-line (the C4 engine through "
                          "kg_check_batch_device over RCCL, one shard per rank; 0 = off)")
     ap.add_argument("--sharded-warmup", type=int, default=4)
@@ -402,22 +402,17 @@ def expand_oracle(snap):
 def expand_cpu_baseline(orc, roots: np.ndarray, depth: int, a) -> dict:
     """BuildTree (oracle/keto_oracle.c ko_expand_node: expand/engine.go:35-104, one visited set per request,
     rows in shard order) over the C5 roots on the host cores: a bounded sample of the same roots (grown
-    until ~--cpu-seconds of work), at the usable CPU count (ctypes releases the GIL: one root per call,
-    a thread pool) and at 1 thread."""
-    from concurrent.futures import ThreadPoolExecutor
+    until ~--cpu-seconds of work), at the usable CPU count and at 1 thread -- one C call per pass
+    (ko_expand_nodes_batch: pthreads take 16-root chunks; no Python per root)."""
     cpus = effective_cpus()
     eff = cpus["effective"]
 
-    def run(n, th):
+    nodes = np.ascontiguousarray(roots[:, 1]).astype(np.uint32)  # synthetic group#member: node id == object id
+    dp = np.ascontiguousarray(roots[:, 3]).view(np.int32) if roots.dtype == np.uint32 else roots[:, 3].astype(np.int32)
+
+    def run(n, th):  # one C call: the roots spread over th pthreads, no Python per root
         t = time.perf_counter()
-        nodes = [int(r[1]) for r in roots[:n]]  # synthetic group#member: node id == object id
-        dp = [int(np.int32(np.uint32(r[3]))) for r in roots[:n]]
-        if th == 1:
-            for x, d in zip(nodes, dp):
-                orc.expand_node(x, d, depth)
-        else:
-            with ThreadPoolExecutor(th) as ex:
-                list(ex.map(lambda xd: orc.expand_node(xd[0], xd[1], depth), zip(nodes, dp)))
+        orc.expand_nodes_batch(nodes[:n], dp[:n], depth, th)
         return time.perf_counter() - t
 
     res = {}
@@ -432,7 +427,7 @@ def expand_cpu_baseline(orc, roots: np.ndarray, depth: int, a) -> dict:
     v, n, t = res[best]
     return {"value": v, "unit": "trees/s", "cores": best, "kind": "port",
             "sample": f"the first {n} of the {len(roots)} C5 roots ({t:.1f} s), BuildTree with one visited set per "
-                      f"request (oracle/keto_oracle.c ko_expand_node), {best} host threads (best of {sorted(res)})",
+                      f"request (oracle/keto_oracle.c ko_expand_nodes_batch: ko_expand_node per root), {best} host threads (best of {sorted(res)})",
             "by_threads": {str(k): r[0] for k, r in sorted(res.items())}, "value_1thread": res[1][0],
             "cpus": cpus, "host_cpu": host_cpu()}
 
@@ -1254,6 +1249,13 @@ def expand_leg(a, snap, orc) -> dict:
         o = orc.o
         o.nd = orc.nd
         res["parity"] = expand_parity(snap, roots, np.diff(off.astype(np.int64)), depth, a, o)
+    if orc is not None and a.cpu_seconds > 0:  # a bounded sample: a third of the headline's CPU budget
+        import copy
+        ac = copy.copy(a)
+        ac.cpu_seconds = a.cpu_seconds / 3
+        o = orc.o
+        o.nd = orc.nd
+        res["cpu_baseline"] = expand_cpu_baseline(o, roots, depth, ac)
     return res
 
 
@@ -1369,28 +1371,48 @@ def sharded_leg(a, snap, size_param, dist, rank, world, local, backend, orc) -> 
         _lib.check(L.kg_synth_queries(snap.handle, 900000 + rank + 7919 * k, B, d.data_ptr()), "kg_synth_queries")
         dqs.append(d)
 
-    def run_phase(k0, n, lat=None, keep=None):
+    res_k = torch.empty((K, B), dtype=torch.uint8, device=dev)  # every timed batch keeps its own results
+    err_p = [torch.empty(B, dtype=torch.int32, device=dev) for _ in range(P)]
+    res_p = [torch.empty(B, dtype=torch.uint8, device=dev) for _ in range(P)]
+    torch.cuda.synchronize()  # queries and buffers exist before the checkers' streams use them
+
+    def run_phase(k0, n, lat=None, timed=False):
+        """Batches k0 .. k0+n-1 round-robin over the P checkers.  Throughput phases enqueue back to back
+        (each thread synchronises its stream once at the end); `lat` phases wait for every batch."""
         errors = []
+        nth = min(P, max(n, 1))
+        ready = threading.Barrier(nth + 1)  # threads exist before the clock starts (as the headline's `go`)
 
         def worker(p):
             try:
-                with torch.cuda.stream(chks[p].stream):
-                    for k in range(p, n, P):
-                        s0 = time.perf_counter()
-                        r, e = chks[p].check(dqs[k0 + k], a.global_depth)
-                        torch.cuda.current_stream().synchronize()
-                        if lat is not None:
-                            lat[k] = time.perf_counter() - s0
-                        if keep is not None and k == 0:
-                            keep.append((r.cpu().numpy(), e.cpu().numpy()))
+                c = chks[p]
+                ready.wait()
+                for k in range(p, n, P):
+                    # what a Go host calls: kg_check_batch_device on the stream the communicator is bound to
+                    s0 = time.perf_counter()
+                    o = res_k[k] if timed else res_p[p]
+                    c._check_t(L.kg_check_batch_device(ssnap.handle, dqs[k0 + k].data_ptr(), B, a.global_depth,
+                                                       o.data_ptr(), err_p[p].data_ptr(), None, c._sp),
+                               "kg_check_batch_device (sharded)")
+                    if lat is not None:
+                        c.stream.synchronize()
+                        lat[k] = time.perf_counter() - s0
+                c.stream.synchronize()
             except Exception as x:  # noqa: BLE001 -- re-raised below
                 errors.append(x)
+                ready.abort()
 
-        th = [threading.Thread(target=worker, args=(p,)) for p in range(min(P, max(n, 1)))]
+        th = [threading.Thread(target=worker, args=(p,)) for p in range(nth)]
         [t.start() for t in th]
+        try:
+            ready.wait()
+        except threading.BrokenBarrierError:
+            pass
+        t_go = time.perf_counter()
         [t.join() for t in th]
         if errors:
             raise errors[0]
+        return t_go
 
     def measure(tag):
         run_phase(0, W)
@@ -1398,9 +1420,7 @@ def sharded_leg(a, snap, size_param, dist, rank, world, local, backend, orc) -> 
         if dist:
             dist.barrier()
         torch.cuda.synchronize()
-        lat, keep = [0.0] * K, []
-        t1 = time.perf_counter()
-        run_phase(W, K, lat, keep)
+        t1 = run_phase(W, K, timed=True)
         torch.cuda.synchronize()
         if dist:
             dist.barrier()
@@ -1408,11 +1428,20 @@ def sharded_leg(a, snap, size_param, dist, rank, world, local, backend, orc) -> 
         el, _ = aggregate(dist, time.perf_counter() - t1, 0.0, dev if backend == "nccl" else None)
         st = chks[0].stats()
         lv = chks[0].levels()
-        r0, e0 = keep[0]
-        assert (e0 == 0).all() and (r0 <= 1).all(), "unexpected errors in the synthetic batch"
+        r0 = res_k[0].cpu().numpy()
+        e_all = torch.stack(err_p).cpu().numpy()
+        assert (e_all == 0).all() and (res_k <= 1).all().item(), "unexpected errors in the synthetic batch"
+        # latency: after the throughput phase, KL more batches at the same in-flight depth, each waited for
+        # by its thread (enqueue -> results on the host)
+        KL = min(K, max(P, 8))
+        lat = [0.0] * KL
+        if dist:
+            dist.barrier()
+        run_phase(0, KL, lat)
         res = {"value": world * B * K / el, "unit": "checks/s", "steps": K, "warmup": W, "inflight": P,
                "ms_per_step": el / K * 1e3, "p99_batch_ms": float(np.percentile(np.array(lat) * 1e3, 99)),
                "p50_batch_ms": float(np.percentile(np.array(lat) * 1e3, 50)),
+               "latency_batches": KL,
                "path": LibShardedChecker.PATHS.get(st["path"], st["path"]),
                "levels_per_batch": st["levels"], "host_syncs_per_batch": st["host_syncs"],
                "records_sent_per_batch": st["records_sent"], "records_to_peers_per_batch": st["records_to_peers"],

@@ -291,13 +291,17 @@ class LibShardedChecker:
             raise _lib.KetoGPUError(f"{what}: transport callback failed: {self._t.error!r}")
         _lib.check(rc, what)
 
-    def check(self, dq, gdepth: int):
+    def check(self, dq, gdepth: int, res=None, err=None):
         """dq: (n, 7) int32 kg_query rows of THIS rank's queries (device tensor).  Returns (res u8, err i32)
-        device tensors, ordered after the caller's current stream's work."""
+        device tensors, ordered after the caller's current stream's work; `res` / `err` (>= n u8 / i32 device
+        tensors) are written in place when given."""
         import torch
         n = int(dq.shape[0])
-        res = torch.empty(max(n, 1), dtype=torch.uint8, device=dq.device)
-        err = torch.empty(max(n, 1), dtype=torch.int32, device=dq.device)
+        if res is None:
+            res = torch.empty(max(n, 1), dtype=torch.uint8, device=dq.device)
+        if err is None:
+            err = torch.empty(max(n, 1), dtype=torch.int32, device=dq.device)
+        assert res.numel() >= n and err.numel() >= n and res.dtype == torch.uint8 and err.dtype == torch.int32
         if self.snapshot_stream:  # the library's own stream: order through the device
             torch.cuda.synchronize()
         else:

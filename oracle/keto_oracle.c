@@ -608,3 +608,51 @@ int64_t ko_expand_node(const ko_index* ix, uint32_t node, int rest_depth, int gl
   if (!ok) return 0;
   return t.overflow ? -t.n : t.n;
 }
+
+/* Batch of ko_expand_node over `n` root nodes on `nthreads` threads (the C5 CPU baseline: every tree is
+ * built into a per-thread buffer, as BuildTree's result would be serialised, then dropped).  counts[i] =
+ * records of root i (0 = nil).  Returns 0, or -1 if a buffer could not be allocated. */
+typedef struct {
+  const ko_index* ix; const uint32_t* node; const int32_t* depth; uint64_t n; int global; int64_t* counts;
+  uint64_t next; pthread_mutex_t* mu; int fail;
+} expand_arg;
+
+static void* expand_worker(void* p) {
+  expand_arg* a = (expand_arg*)p;
+  int64_t cap = 1 << 16;
+  int32_t* buf = (int32_t*)malloc((size_t)cap * 6 * sizeof(int32_t));
+  for (;;) {
+    pthread_mutex_lock(a->mu);
+    uint64_t i0 = a->next; a->next += 16;
+    pthread_mutex_unlock(a->mu);
+    if (i0 >= a->n || !buf) break;
+    uint64_t i1 = i0 + 16 < a->n ? i0 + 16 : a->n;
+    for (uint64_t i = i0; i < i1 && buf; i++) {
+      int64_t r = ko_expand_node(a->ix, a->node[i], a->depth[i], a->global, buf, cap);
+      while (r < 0 && r != -1) { /* grow to the size it asked for and rebuild */
+        cap = -r + 1024;
+        free(buf);
+        buf = (int32_t*)malloc((size_t)cap * 6 * sizeof(int32_t));
+        if (!buf) break;
+        r = ko_expand_node(a->ix, a->node[i], a->depth[i], a->global, buf, cap);
+      }
+      a->counts[i] = r;
+    }
+  }
+  if (!buf) { pthread_mutex_lock(a->mu); a->fail = 1; pthread_mutex_unlock(a->mu); }
+  free(buf);
+  return NULL;
+}
+
+int ko_expand_nodes_batch(const ko_index* ix, const uint32_t* node, const int32_t* depth, uint64_t n, int global,
+                          int nthreads, int64_t* counts) {
+  if (!ix->finalized) return -1;
+  pthread_mutex_t mu = PTHREAD_MUTEX_INITIALIZER;
+  expand_arg a = {ix, node, depth, n, global, counts, 0, &mu, 0};
+  if (nthreads < 1) nthreads = 1;
+  pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * nthreads);
+  for (int t = 0; t < nthreads; t++) pthread_create(&th[t], NULL, expand_worker, &a);
+  for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+  free(th);
+  return a.fail ? -1 : 0;
+}

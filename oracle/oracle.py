@@ -56,6 +56,7 @@ def lib():
         L.ko_expand.argtypes = [vp, u32, u32, u32, C.c_int, C.c_int, vp, i64]
         L.ko_expand_node.restype = i64
         L.ko_expand_node.argtypes = [vp, u32, C.c_int, C.c_int, vp, i64]
+        L.ko_expand_nodes_batch.argtypes = [vp, vp, vp, u64, C.c_int, C.c_int, vp]
         _lib = L
     return _lib
 
@@ -165,6 +166,19 @@ class Oracle:
             if n >= 0:
                 return buf[:n] if n > 0 else None
             cap = -n + 16
+
+    def expand_nodes_batch(self, nodes: np.ndarray, depths: np.ndarray, global_max: int, nthreads: int = 1) -> np.ndarray:
+        """expand_node over many roots on `nthreads` threads (ko_expand_nodes_batch); returns each root's
+        record count (0 = nil).  The trees themselves are built and dropped (the C5 CPU baseline)."""
+        nodes = np.ascontiguousarray(nodes, np.uint32)
+        d = np.ascontiguousarray(depths, np.int32)
+        if nodes.size and int(nodes.max()) >= self.n_nodes:
+            raise ValueError("node out of range")
+        counts = np.zeros(nodes.shape[0], np.int64)
+        if lib().ko_expand_nodes_batch(self.h, _p(nodes), _p(d), nodes.shape[0], int(global_max), int(nthreads),
+                                       _p(counts)) != 0:
+            raise MemoryError("ko_expand_nodes_batch")
+        return counts
 
 
 def records_to_tree(rec: Optional[np.ndarray], interner):

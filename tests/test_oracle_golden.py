@@ -32,3 +32,31 @@ def test_oracle_expand(fn, case):
             assert got == exp
         else:
             assert trees_equal_unordered(got, exp), (got, exp)
+
+
+@pytest.mark.parametrize("threads", [1, 4])
+def test_oracle_expand_nodes_batch(threads):
+    """ko_expand_nodes_batch (the C5 CPU baseline) builds the same trees as ko_expand_node, root by root,
+    including a tree larger than a worker's first buffer (70 k records: the grow-and-rebuild path)."""
+    import numpy as np
+    SET = 0x80000000
+    rng = np.random.default_rng(3)
+    n = 400
+    rows = [[] for _ in range(n)]
+    for v in range(n - 1):
+        for _ in range(int(rng.integers(0, 6))):
+            c = int(rng.integers(0, n - 1))
+            rows[v].append(SET | c if rng.random() < 0.6 else 1000 + c)
+    rows[n - 1] = [5000 + i for i in range(70000)]  # one wide row: 70 001 records at depth >= 2
+    off = np.zeros(n + 1, np.uint64)
+    off[1:] = np.cumsum([len(r) for r in rows])
+    subj = np.array([s for r in rows for s in r], np.uint32)
+    nd = np.arange(n, dtype=np.uint32)
+    o = Oracle.from_csr(0, np.zeros(n, np.uint32), nd, np.ones(n, np.uint32), off, subj)
+    nodes = np.concatenate([np.arange(n, dtype=np.uint32), [n - 1, 7]]).astype(np.uint32)
+    depths = np.array([int(x) % 6 for x in range(len(nodes))], np.int32)
+    got = o.expand_nodes_batch(nodes, depths, 5, threads)
+    for i, (v, d) in enumerate(zip(nodes, depths)):
+        rec = o.expand_node(int(v), int(d), 5)
+        assert got[i] == (0 if rec is None else len(rec)), (i, v, d)
+    assert got.max() == 70001
