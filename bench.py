@@ -96,7 +96,8 @@ def parse(argv=None):
     ap.add_argument("--host-sync", type=int, default=1,
                     help="kg_snapshot_tune host_sync (--mode host: 1 = kg_check_batch waits asleep, 0 = spins)")
     ap.add_argument("--resolve-unheld", type=int, default=1,
-                    help="kg_snapshot_tune resolve_unheld (1: k_resolve skips the node map for subjects no row holds)")
+                    help="kg_snapshot_tune resolve_unheld (1: k_resolve skips the node map for subjects no row holds; "
+                         "2: reads the holder bit only for queries headed for the stream tier)")
     ap.add_argument("--stream-steal", type=int, default=4,
                     help="kg_snapshot_tune stream_steal (XCD ranges a k_stream4 wave dequeues from, 1..8)")
     ap.add_argument("--stream-chunk", type=int, default=64,
@@ -172,6 +173,8 @@ def parse(argv=None):
                          "a Go host makes it; py = keto_amd.sharded.ShardedChecker driving the kg_shard_* steps "
                          "(needed for --shard-budget)")
     ap.add_argument("--roots", type=int, default=100_000, help="expand roots per step (C5)")
+    ap.add_argument("--expand-gw", type=int, default=1,
+                    help="kg_snapshot_tune expand_gw (1: large expand roots gather their neighbourhood, then walk the copy)")
     ap.add_argument("--expand-tail", type=int, default=1,
                     help="kg_snapshot_tune expand_tail (1: passes 2/3 walk with LDS-cached frames; 0: round 2's walk)")
     ap.add_argument("--delta", type=int, default=1000, help="--mode refresh: rows per transaction")
@@ -240,6 +243,7 @@ def bench_expand(a):
     L = _lib.load()
     snap, _ = build_synthetic(a, a.tuples, device=local)
     snap.tune("expand_tail", a.expand_tail)
+    snap.tune("expand_gw", a.expand_gw)
     from keto_amd.synth import hot_group_roots
     roots = hot_group_roots(snap.synth_ids(), a.roots)
     depth = a.global_depth if a.global_depth != 10 else 5
@@ -257,7 +261,7 @@ def bench_expand(a):
            "config": {"workload": "C5: %d hot roots @ %.4g tuples (rows), max_read_depth %d" % (a.roots, snap.info()["rows"],
                                                                                             depth),
                       "inflight_per_gpu": P, "hw_queues": a.hw_queues, "parallelism": f"replica{world}",
-                      "expand_tail": a.expand_tail},
+                      "expand_tail": a.expand_tail, "expand_gw": a.expand_gw},
            "tree_nodes_per_step": nodes / a.steps, "tree_nodes_per_s": nodes / el,
            "kernel_ms_per_step": kms / a.steps}
     if off is not None:
@@ -1233,6 +1237,7 @@ def expand_leg(a, snap, orc) -> dict:
     L = _lib.load()
     roots = hot_group_roots(snap.synth_ids(), a.roots)
     depth = 5
+    snap.tune("expand_gw", a.expand_gw)
     P, K = max(1, a.expand_inflight), a.expand_steps
     el, results = expand_steps(L, snap, roots, depth, P, K, P)
     nodes = sum(r[0] for r in results)

@@ -237,8 +237,10 @@ int kg_snapshot_materialized(const kg_snapshot* s, uint64_t* out3);
  * goes straight to the grid tier; default); 0 = off.
  * key "stream_ecap": edges a query may enqueue in the stream tier before it is handed to the
  * backward / grid tiers (default 512; 0 = no budget) -- cuts the stream kernel's tail of long walks.
- * key "resolve_unheld" (0/1): without a namespace program, k_resolve reads a subject id's holder
- * bit before the node map and answers an unheld subject NotMember without the lookup (default 1).
+ * key "resolve_unheld" (0..2): without a namespace program, k_resolve reads a subject id's holder
+ * bit before the node map and answers an unheld subject NotMember without the lookup (default 1);
+ * 2 = the bit is read only by queries that the node map and the root probe leave for the stream
+ * tier; 0 = the bit beside the node-map lookup for every query.
  * key "device_sync" (0/1): the same for kg_check_batch_device when it waits (stats or a grid-tier
  * readback; default 1: asleep -- 5.6 -> 5.8 x 10^9 checks/s with 4 batches in flight).  key "host_sync" (0/1): kg_check_batch waits for its device work asleep on a blocking-sync event
  * (1, default: no core spins per in-flight batch) or spinning in hipStreamSynchronize (0).

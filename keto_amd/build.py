@@ -28,37 +28,43 @@ def stale() -> bool:
     return any(os.path.getmtime(p) > t for p in deps)
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and not stale():
+def build(force: bool = False, verbose: bool = False, out: str = LIB, defines=()) -> str:
+    """out / defines: an A/B variant of the library (e.g. keto_amd/lib/ab/x.so with -DKG_NT_RANDOM=1),
+    loaded by bench.py through KG_LIB_PATH; the in-tree library is built without defines."""
+    if out == LIB and not force and not stale():
         return LIB
-    os.makedirs(LIB_DIR, exist_ok=True)
+    obj_dir = os.path.join(os.path.dirname(out), ".obj_" + os.path.basename(out))
+    os.makedirs(obj_dir, exist_ok=True)
     objs = []
     jobs = []
     for src in sources():
-        obj = os.path.join(LIB_DIR, os.path.basename(src) + ".o")
+        obj = os.path.join(obj_dir, os.path.basename(src) + ".o")
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-c", "-x", "hip", src, "-o", obj,
                "-I", os.path.join(ROOT, "include"), "-Wall", "-Wno-unused-function", "-Wno-unused-result"]
+        cmd += ["-D" + d for d in defines]
         jobs.append((cmd, src))
         objs.append(obj)
     procs = [(subprocess.Popen(c, stdout=subprocess.PIPE, stderr=subprocess.STDOUT), s) for c, s in jobs]
     failed = False
     for p, s in procs:
-        out, _ = p.communicate()
+        log, _ = p.communicate()
         if p.returncode != 0 or verbose:
-            sys.stderr.write(out.decode(errors="replace"))
+            sys.stderr.write(log.decode(errors="replace"))
         if p.returncode != 0:
             failed = True
     if failed:
         raise RuntimeError("hipcc failed")
-    tmp = LIB + ".tmp"
+    tmp = out + ".tmp"
     # RCCL: the hash-sharded mode's transport over xGMI (kg_shard_comm.hip)
     subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs +
                    ["-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib", "-lpthread"], check=True)
-    os.replace(tmp, LIB)
+    os.replace(tmp, out)
     for o in objs:
         os.remove(o)
-    build_tools()
-    return LIB
+    os.rmdir(obj_dir)
+    if out == LIB:
+        build_tools()
+    return out
 
 
 TOOLS_LIB = os.path.join(ROOT, "tools", "lib", "libkg_loadgen.so")
@@ -74,4 +80,8 @@ def build_tools() -> str:
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose="-v" in sys.argv))
+    # python -m keto_amd.build [--force] [-v] [--out PATH -DNAME=V ...]
+    av = sys.argv[1:]
+    out = av[av.index("--out") + 1] if "--out" in av else LIB
+    print(build(force="--force" in av, verbose="-v" in av, out=os.path.abspath(out),
+                defines=[x[2:] for x in av if x.startswith("-D")]))

@@ -488,7 +488,7 @@ static int tune_one(Snapshot* s, const char* key, int64_t value) {
     return 0;
   }
   if (strcmp(key, "resolve_unheld") == 0) {
-    if (value < 0 || value > 1) return set_error(-2, "resolve_unheld must be 0 or 1");
+    if (value < 0 || value > 2) return set_error(-2, "resolve_unheld must be 0, 1 or 2");
     s->resolve_unheld = (int)value;
     return 0;
   }
@@ -526,6 +526,11 @@ static int tune_one(Snapshot* s, const char* key, int64_t value) {
   if (strcmp(key, "grid_cap") == 0) {
     if (value < 0 || value > (1ll << 34)) return set_error(-2, "grid_cap must be in [0, 2^34]");
     s->grid_small_cap = (uint64_t)value;
+    return 0;
+  }
+  if (strcmp(key, "expand_gw") == 0 || strcmp(key, "expand_skip_lds") == 0) {
+    if (value < 0 || value > 1) return set_error(-2, "%s must be 0 or 1", key);
+    (strcmp(key, "expand_gw") == 0 ? s->expand_gw : s->expand_skip_lds) = (int)value;
     return 0;
   }
   if (strcmp(key, "expand_tail") == 0) {

@@ -140,6 +140,22 @@ __device__ void block_append_lq(bool pred, const LQuery& v, LQuery* list, uint32
 }
 
 // ------------------------------------------------------------------ k_resolve
+// kg_query is 28 B: seven dword loads (non-temporal under KG_NT_RANDOM, as ld_once)
+__device__ __forceinline__ kg_query ld_once_q(const kg_query* p) {
+#if KG_NT_RANDOM
+  static_assert(sizeof(kg_query) == 28, "seven dwords");
+  uint32_t w[7];
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(p);
+#pragma unroll
+  for (int k = 0; k < 7; k++) w[k] = __builtin_nontemporal_load(src + k);
+  kg_query x;
+  __builtin_memcpy(&x, w, sizeof x);
+  return x;
+#else
+  return *p;
+#endif
+}
+
 // Light-routed queries go to the stream tier as LQuery records in 8 shards of lq_cap entries (shard
 // blockIdx & 7) and skip rq[i]; only queries that later tiers read by index (GENERAL) are written to
 // rq (the stream tier writes the RQuery of a query it hands on).
@@ -155,7 +171,7 @@ __global__ __launch_bounds__(256) void k_resolve(DevSnap s, const kg_query* __re
   bool did_probe = false, no_holder = false;
   LQuery lq{};
   if (valid) {
-    kg_query x = q[i];
+    kg_query x = ld_once_q(q + i);
     // node map and (for a subject id) holder hash: the first slots of both are loaded together,
     // so the common case is one round trip for both lookups
     const bool key_ok = nmap_key_ok(x.t.ns, x.t.rel, x.t.obj);
@@ -170,14 +186,17 @@ __global__ __launch_bounds__(256) void k_resolve(DevSnap s, const kg_query* __re
     const uint64_t hi = mix64(subj) & s.hmask;
     HSlot h0{};
     uint32_t hw = 0;
-    if (use_bits) hw = subj < s.hbits_n ? s.hbits[subj >> 5] : 0u;
-    else if (want_h) h0 = s.hslots[hi];
+    // no_holder_filter 3 (lazy): the bit is read only by queries still headed for the stream tier
+    // after the node map and the root probe -- about half of them -- instead of by every query
+    const bool lazy = no_holder_filter == 3;
+    if (use_bits && !lazy) hw = subj < s.hbits_n ? ld_once(s.hbits + (subj >> 5)) : 0u;
+    else if (want_h && !use_bits) h0 = s.hslots[hi];
     // without a namespace program nothing can end as an error, so a subject that no row holds is
     // NotMember whatever the root: the bit (an Infinity-Cache hit) is read first and such a query
     // never touches the node map (~13 % of the C2 batch; one random HBM line each)
     const bool unheld = no_holder_filter == 2 && use_bits && !s.relflags && !((hw >> (subj & 31)) & 1u);
     NSlot n0{};
-    if (key_ok && !unheld) n0 = s.nmap[ni];
+    if (key_ok && !unheld) n0 = ld_once(s.nmap + ni);
     uint32_t node = NONE, rb = 0, rl = 0, rsig_lo = 0xFFFFFFFFu, rsig = 0xFFFFFFFFu, nfl = 0;
     if (unheld) {
       no_holder = true;
@@ -225,7 +244,11 @@ __global__ __launch_bounds__(256) void k_resolve(DevSnap s, const kg_query* __re
       // depth that cannot reach any child (D < 2) finishes the query before the wave tier.  The
       // row signature in the node-map slot rules out most misses without touching dset.
       // an unset holder bit rules the probe out as well (the exact tuple would make subj a holder)
-      const bool nobit = use_bits && !((hw >> (subj & 31)) & 1u);
+      // lazy: the bit matters only if the query would go on (d >= 2, a row, no direct hit); its load
+      // is issued beside the root probe's
+      const bool lazy_bit = lazy && use_bits && d >= 2 && rl > 0;
+      if (lazy_bit) hw = subj < s.hbits_n ? ld_once(s.hbits + (subj >> 5)) : 0u;
+      const bool nobit = use_bits && (!lazy || lazy_bit) && !((hw >> (subj & 31)) & 1u);
       did_probe = subj != NONE && !nobit && sig_maybe(rsig_lo, rsig, subj_sig(subj));
       member = did_probe && dset_probe(s, node, subj);
       if (member || d < 2 || rl == 0) route = ROUTE_DONE;
@@ -476,7 +499,7 @@ __global__ __launch_bounds__(256) void k_stream4(DevSnap s, LqList wl, uint32_t*
     const bool act = (uint32_t)lane < taken;
     const AdjX x = s.adjx[act ? ob + ((uint32_t)lane - ox) : 0u];  // adjx[0] exists (n_set_edges + 1)
     const ulonglong2 pb =
-        *reinterpret_cast<const ulonglong2*>(s.dset + (pvalid ? dset_home(pkey, s.dset_nb) : 0ull) * DSET_BUCKET);
+        ld_once(reinterpret_cast<const ulonglong2*>(s.dset + (pvalid ? dset_home(pkey, s.dset_nb) : 0ull) * DSET_BUCKET));
     const uint32_t slot = (om >> 11) & 31u, d = om >> 25, g = (om >> 16) & S2_GEN;
     const uint4 ss = L.s_ss[slot];  // LDS, under the gathers' latency: Bloom mask, visited-cache salt
     const uint2 ssig = make_uint2(ss.x, ss.y);
@@ -910,7 +933,7 @@ int check_batch_begin(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n, 
     const bool use_back = s->back_tier && s->ds.radj;
     const uint32_t nblk = (uint32_t)((n + 255) / 256);
     hipLaunchKernelGGL(k_resolve, dim3(nblk), dim3(256), 0, stream, s->ds, d_q, (uint32_t)n, (uint32_t)n_base, n_extra,
-                       global_max_depth, rq, d_out, d_err, gen, use_back ? (s->resolve_unheld ? 2 : 1) : 0, ctl, lq,
+                       global_max_depth, rq, d_out, d_err, gen, use_back ? (s->resolve_unheld == 2 ? 3 : s->resolve_unheld ? 2 : 1) : 0, ctl, lq,
                        lq_cap);
     HIPC(hipGetLastError());
     if (stats) HIPC(hipEventRecord(l0, stream));

@@ -18,6 +18,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <cstdio>
 #include <cstring>
 #include <mutex>
 #include <vector>
@@ -48,6 +49,10 @@ struct ExpCtl {
   uint32_t p3_count, p3_head;  // pass-3 (full bitmap) queue: pass-2 overflows
   uint32_t pad;
   unsigned long long records;
+  // gather-walk passes (expand_gw): the small slots take the pass-1 overflows (p2), the large slots
+  // what outgrew a small slot (ga), the hash pass what outgrew a large one (gb)
+  uint32_t gs_head, ga_count, ga_head, gb_count, gb_head, pad2[3];
+  unsigned long long gw_ticks[4];  // longest gather / walk of one root, small and large slots (wall clock, 100 MHz)
 };
 
 // Per-root result of the DFS: first chunk and record count (0 records = nil tree).
@@ -450,7 +455,7 @@ __device__ int expand_root_x(const DevSnap& s, Store& st, const kg_set& root, in
 __global__ __launch_bounds__(256) void k_expand_lds(DevSnap s, const kg_set* __restrict__ roots, uint32_t n,
                                                     int32_t global, ExpCtl* ctl, RootOut* outs, kg_tree_node* arena,
                                                     uint32_t* next, uint32_t n_chunks, ExpFrame* stacks,
-                                                    uint32_t stack_cap, uint32_t* p2_list) {
+                                                    uint32_t stack_cap, uint32_t* p2_list, int skip) {
   __shared__ WaveLds lds_all[4];
   const int wave = threadIdx.x >> 6, lane = lane_id();
   LdsStore st{&lds_all[wave]};
@@ -463,7 +468,7 @@ __global__ __launch_bounds__(256) void k_expand_lds(DevSnap s, const kg_set* __r
     ri = __shfl(ri, 0, 64);
     if (ri >= n) break;
     uint32_t nr = 0;
-    const int r = expand_root(s, st, roots[ri], global, stack, S, nr);
+    const int r = skip ? EXP_OVERFLOW : expand_root(s, st, roots[ri], global, stack, S, nr);
     if (lane == 0) {
       if (r == EXP_OVERFLOW) {
         p2_list[atomicAdd(&ctl->p2_count, 1u)] = ri;
@@ -518,13 +523,14 @@ __device__ void expand_slot_loop(const DevSnap& s, const kg_set* __restrict__ ro
 __global__ __launch_bounds__(64) void k_expand_hash(DevSnap s, const kg_set* __restrict__ roots, int32_t global,
                                                     ExpCtl* ctl, RootOut* outs, kg_tree_node* arena, uint32_t* next,
                                                     uint32_t n_chunks, ExpFrame* stacks, uint32_t stack_cap,
-                                                    const uint32_t* p2_list, uint32_t* tabs, uint64_t tsize,
-                                                    uint32_t* lists, uint64_t cap, uint32_t* p3_list, int cached) {
+                                                    const uint32_t* qlist, const uint32_t* qcount, uint32_t* qhead,
+                                                    uint32_t* tabs, uint64_t tsize, uint32_t* lists, uint64_t cap,
+                                                    uint32_t* p3_list, int cached) {
   __shared__ uint32_t pref[64];
   uint32_t* tab = tabs + (size_t)blockIdx.x * tsize;
   HashStore st{tab, (uint32_t)(tsize - 1), lists + (size_t)blockIdx.x * cap, cap, pref};
-  expand_slot_loop(s, roots, global, ctl, outs, arena, next, n_chunks, stacks + (size_t)blockIdx.x * stack_cap, p2_list,
-                   ctl->p2_count, &ctl->p2_head, st, tab, tsize, p3_list, cached);
+  expand_slot_loop(s, roots, global, ctl, outs, arena, next, n_chunks, stacks + (size_t)blockIdx.x * stack_cap, qlist,
+                   *qcount, qhead, st, tab, tsize, p3_list, cached);
 }
 
 __global__ __launch_bounds__(64) void k_expand_hbm(DevSnap s, const kg_set* __restrict__ roots, int32_t global,
@@ -536,6 +542,325 @@ __global__ __launch_bounds__(64) void k_expand_hbm(DevSnap s, const kg_set* __re
   GlobalStore st{bm, list, cap, pref};
   expand_slot_loop(s, roots, global, ctl, outs, arena, next, n_chunks, stack, p3_list, ctl->p3_count, &ctl->p3_head, st,
                    bm, words, nullptr, cached);
+}
+
+// ------------------------------------------------------------------ gather-then-walk (pass 2)
+// A large root's pre-order walk is one wave's chain of dependent round trips: per expanded set, the
+// 64-wide row chunk (row_subj), then the children's row ranges, node triples and visited lookups --
+// two trips to HBM, ~2.8 us, so C5's largest tree (~115 k records) took ~42 ms alone.  Here a
+// workgroup first GATHERS the root's neighbourhood in parallel and the walk then runs on that copy:
+//   * level-synchronous BFS from the root to distance D-2 (the nodes the walk can expand: a node
+//     expanded at rest depth >= 2 lies on a path of length <= D-2).  Every node within distance
+//     D-1 that has rows gets a dense LOCAL id (an open-addressing map, epoch-tagged so it is never
+//     cleared); every node within D-2 also gets its row COPIED into the slot's entry array, each
+//     entry carrying everything the walk needs: the leaf record's triple, the child's local id, its
+//     row length (the union record's child count) and the first entry of its copied row;
+//   * a level's entries are one contiguous range (rows are allocated by a bump counter while the
+//     level before runs), so the next level is edge-parallel over that range: a run-head mark per
+//     row start and the head of each 64-entry tile find an entry's source row position;
+//   * the walk (one wave) is expand_root_x's order over the copy: one trip per chunk (the slot's
+//     recently written lines, L2 / MALL) and the visited set is an LDS bitmap over local ids.
+// The output is identical to expand_root's (same candidates in the same order).  A root that outgrows
+// a slot (entries, local ids, map probes) goes on to the next pass: small slots -> large slots ->
+// the hash pass (expand_slot_loop) -> the whole-graph bitmap pass.
+struct GwEnt {
+  uint32_t sub;   // the row subject as stored (SET_BIT | node, or a subject id)
+  uint32_t loc;   // the child set's local id (a set with rows), else NONE; during the gather: its map slot
+  uint32_t ns, obj, rel;  // the leaf record's triple (KG_SUBJECT_ID, id, 0 for a subject id)
+  uint32_t len;   // the child's row length (its union record's child count)
+  uint32_t cb;    // first entry of the child's copied row (NONE: not copied, never expanded)
+  uint32_t pad;
+};
+static_assert(sizeof(GwEnt) == 32, "two 16-B loads per entry");
+
+struct GwSlots {
+  GwEnt* ent;           // [slot][ent_cap]
+  uint64_t* hsrc;       // [slot][ent_cap] source row position of a run head
+  uint32_t* hmark;      // [slot][ent_cap] epoch at a run head
+  uint32_t* tfirst;     // [slot][ent_cap / 64 + 1] run head of each 64-entry tile's first entry
+  unsigned long long* map;  // [slot][2 * map_cap] key (epoch << 32 | node), value (cb << 32 | local id)
+  uint32_t* epoch;      // [slot]
+  uint32_t ent_cap, map_cap;  // map_cap: a power of two
+};
+
+__device__ __forceinline__ uint32_t ld_sc1(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t ld_sc1(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long ld_sc1(const unsigned long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+constexpr int GW_PROBES = 64;
+// The map slot of `node` for this root (inserting it; *won: this thread inserted it), or -1 (probe bound).
+__device__ __forceinline__ int64_t gw_insert(unsigned long long* map, uint32_t mask, uint32_t epoch, uint32_t node,
+                                             bool* won) {
+  const unsigned long long key = ((unsigned long long)epoch << 32) | node;
+  uint32_t h = (uint32_t)mix64(node) & mask;
+  *won = false;
+  for (int p = 0; p < GW_PROBES; p++) {
+    unsigned long long cur = ld_sc1(&map[2 * (size_t)h]);
+    for (;;) {
+      if (cur == key) return h;
+      if ((uint32_t)(cur >> 32) == epoch) break;  // another node of this root
+      const unsigned long long old = atomicCAS(&map[2 * (size_t)h], cur, key);
+      if (old == cur) {
+        *won = true;
+        return h;
+      }
+      cur = old;
+    }
+    h = (h + 1) & mask;
+  }
+  return -1;
+}
+
+// Marks the run [cb, cb + len) as copied from row position r0: head mark + the tile heads it starts.
+__device__ __forceinline__ void gw_run(const GwSlots& g, uint64_t* hsrc, uint32_t* hmark, uint32_t* tfirst,
+                                       uint32_t epoch, uint32_t cb, uint32_t len, uint64_t r0) {
+  hsrc[cb] = r0;
+  hmark[cb] = epoch;
+  for (uint32_t t = (cb + 63) / 64; t * 64 < cb + len; t++) tfirst[t] = cb;
+}
+
+template <uint32_t LOC_CAP>
+__global__ __launch_bounds__(256) void k_expand_gw(DevSnap s, const kg_set* __restrict__ roots, int32_t global,
+                                                   ExpCtl* ctl, RootOut* outs, kg_tree_node* arena, uint32_t* next,
+                                                   uint32_t n_chunks, ExpFrame* stacks, uint32_t stack_cap,
+                                                   const uint32_t* qlist, const uint32_t* qcount, uint32_t* qhead,
+                                                   uint32_t* ovf_list, uint32_t* ovf_count, GwSlots g) {
+  __shared__ uint32_t vis[LOC_CAP / 32];
+  __shared__ uint32_t s_k, s_nloc, s_nent, s_bad, s_epoch;
+  __shared__ ExpFrame s_fr[XF];
+  const int lane = lane_id(), wave = threadIdx.x >> 6;
+  const size_t slot = blockIdx.x;
+  GwEnt* E = g.ent + slot * g.ent_cap;
+  uint64_t* hsrc = g.hsrc + slot * g.ent_cap;
+  uint32_t* hmark = g.hmark + slot * g.ent_cap;
+  uint32_t* tfirst = g.tfirst + slot * (g.ent_cap / 64 + 1);
+  unsigned long long* map = g.map + slot * 2 * (size_t)g.map_cap;
+  ExpFrame* gstack = stacks + slot * stack_cap;
+  const uint32_t mmask = g.map_cap - 1;
+  const uint32_t count = *qcount;  // written by an earlier kernel of the chain
+  Stream S{arena, next, n_chunks, ctl, 0, 0, 0, true};
+  unsigned long long recs = 0;
+  for (;;) {
+    if (threadIdx.x == 0) s_k = atomicAdd(qhead, 1u);
+    __syncthreads();
+    const uint32_t k = s_k;
+    if (k >= count) break;
+    const uint32_t ri = qlist[k];
+    const kg_set root = roots[ri];
+    int32_t d0 = root.max_depth;
+    if (d0 <= 0 || global < d0) d0 = global;  // engine.go:37-39
+    const uint32_t rn = root.sns == KG_SUBJECT_ID ? NONE : nmap_find(s, root.sns, root.srel, root.sobj);
+    const uint64_t rb0 = rn == NONE ? 0 : s.row_off[rn];
+    const uint64_t len0 = rn == NONE ? 0 : s.row_off[rn + 1] - rb0;
+    // pass 1 answers these itself; anything else unusual is left to the passes after this one
+    bool bad = rn == NONE || len0 == 0 || d0 <= 1 || len0 > g.ent_cap;
+    const unsigned long long t0 = wall_clock64();
+    if (!bad) {
+      if (threadIdx.x == 0) {
+        s_epoch = ++g.epoch[slot];  // only this workgroup touches its slot
+        s_nloc = 1;
+        s_nent = (uint32_t)len0;
+        s_bad = 0;
+        bool won;
+        const int64_t h = gw_insert(map, mmask, s_epoch, rn, &won);
+        if (h < 0) s_bad = 1;
+        else map[2 * (size_t)h + 1] = 0ull;  // copied at entry 0, local id 0
+      }
+      __syncthreads();
+      const uint32_t epoch = s_epoch;
+      if (threadIdx.x == 0) {
+        hsrc[0] = rb0;
+        hmark[0] = epoch;
+      }
+      for (uint32_t t = threadIdx.x; t * 64 < len0; t += 256) tfirst[t] = 0;
+      __syncthreads();
+      uint32_t lo = 0, hi = (uint32_t)len0;
+      for (int lv = 0; lv <= d0 - 2 && lo < hi && !s_bad; lv++) {
+        const bool alloc_next = lv + 1 <= d0 - 2;  // the children's rows are copied (the walk may expand them)
+        // phase 1: every entry of the level's rows, 64-entry tiles per wave
+        for (uint32_t t = lo / 64 + wave; t * 64 < hi; t += 4) {
+          const uint32_t e = t * 64 + lane;
+          const bool valid = e >= lo && e < hi;
+          const bool head = valid && ld_sc1(&hmark[e]) == epoch;
+          uint32_t hv = head ? e + 1 : 0u;
+          if (lane == 0 && !head) hv = ld_sc1(&tfirst[t]) + 1;
+          const uint32_t hpos = wave_incl_scan<DppMax>(hv) - 1;  // the run this entry belongs to
+          if (valid) {
+            const uint64_t src = ld_sc1(&hsrc[hpos]) + (e - hpos);
+            const uint32_t sub = s.row_subj[src];
+            const bool is_set = (sub & SET_BIT) != 0;
+            const uint32_t c = is_set ? sub & ~SET_BIT : 0u;
+            const uint64_t r0 = s.row_off[c], r1 = s.row_off[c + 1];
+            const uint32_t ns = s.nd_ns[c], ob = s.nd_obj[c], rl = s.nd_rel[c];
+            const uint32_t len = is_set ? (uint32_t)(r1 - r0) : 0u;
+            GwEnt x{sub, NONE, is_set ? ns : (uint32_t)KG_SUBJECT_ID, is_set ? ob : sub, is_set ? rl : 0u, len, NONE, 0};
+            if (len > 0) {
+              bool won;
+              const int64_t h = gw_insert(map, mmask, epoch, c, &won);
+              if (h < 0) {
+                s_bad = 1;
+              } else {
+                x.loc = (uint32_t)h;  // resolved to the local id in phase 2
+                if (won) {
+                  const uint32_t loc = atomicAdd(&s_nloc, 1u);
+                  uint32_t cb = NONE;
+                  if (loc >= LOC_CAP) s_bad = 1;
+                  if (alloc_next) {
+                    cb = atomicAdd(&s_nent, len);
+                    if ((uint64_t)cb + len > g.ent_cap) {
+                      s_bad = 1;
+                      cb = NONE;
+                    } else {
+                      gw_run(g, hsrc, hmark, tfirst, epoch, cb, len, r0);
+                    }
+                  }
+                  map[2 * (size_t)h + 1] = ((unsigned long long)cb << 32) | loc;
+                }
+              }
+            }
+            E[e] = x;
+          }
+        }
+        __syncthreads();
+        if (s_bad) break;
+        // phase 2: the children's local ids and copied rows, now that every insert of the level is done
+        for (uint32_t e = lo + threadIdx.x; e < hi; e += 256) {
+          const uint32_t sub = ld_sc1(&E[e].sub), len = ld_sc1(&E[e].len);
+          if ((sub & SET_BIT) && len > 0) {
+            const unsigned long long v = ld_sc1(&map[2 * (size_t)ld_sc1(&E[e].loc) + 1]);
+            E[e].loc = (uint32_t)v;
+            E[e].cb = (uint32_t)(v >> 32);
+          }
+        }
+        __syncthreads();
+        lo = hi;
+        hi = s_nent;
+      }
+      bad = s_bad != 0;
+    }
+    if (bad) {
+      if (threadIdx.x == 0) ovf_list[atomicAdd(ovf_count, 1u)] = ri;
+      __syncthreads();
+      continue;
+    }
+    // the walk: wave 0 over the copy; the visited bitmap covers the root's local ids
+    const unsigned long long t1 = wall_clock64();
+    if (threadIdx.x == 0) atomicMax(&ctl->gw_ticks[LOC_CAP > 16384 ? 2 : 0], t1 - t0);
+    const uint32_t nloc = s_nloc;
+    for (uint32_t w = threadIdx.x; w < (nloc + 31) / 32; w += 256) vis[w] = 0;
+    __syncthreads();
+    if (wave == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the copy was written by every wave: drop stale L1 lines
+      int status = EXP_OK;
+      uint32_t cnt = 0;
+      S.ok = true;
+      S.pos = 0;
+      S.first = S.cur = alloc_chunk(S);
+      if (!S.ok) status = EXP_ARENA;
+      if (status == EXP_OK) {
+        if (lane == 0) vis[0] = 1u;
+        emit(S, lane == 0, rec_set(s, 1, rn, (uint32_t)len0));
+        cnt = 1;
+        int sp = 0;
+        ExpFrame F{0, 0, 0, (uint32_t)len0, d0};
+        for (;;) {
+          const uint64_t eb = F.rb, ee = F.rb + F.len;
+          const bool can_expand = F.d - 1 >= 2;
+          bool pushed = false;
+          while (eb + F.cursor < ee) {
+            const uint64_t at0 = eb + F.cursor;
+            const uint32_t width = (uint32_t)min<uint64_t>(64, ee - at0);
+            const bool valid = (uint32_t)lane < width;
+            const GwEnt x = E[valid ? at0 + lane : at0];
+            const bool is_set = valid && (x.sub & SET_BIT);
+            const bool has_loc = is_set && x.loc != NONE;
+            bool cand = false;
+            if (has_loc && can_expand) cand = !((vis[x.loc >> 5] >> (x.loc & 31)) & 1u);
+            const uint64_t mc = __ballot(cand);
+            const uint32_t p = mc ? (uint32_t)(__ffsll((unsigned long long)mc) - 1) : 64u;
+            const bool leaf = valid && (uint32_t)lane < p;
+            // rest depth <= 1 below: child sets become leaves but are still marked (BuildTree marks
+            // before it looks at the depth); sets without rows need no mark
+            if (!can_expand && leaf && has_loc) atomicOr(&vis[x.loc >> 5], 1u << (x.loc & 31));
+            kg_tree_node r;
+            r.type = 2;
+            r.is_set = is_set ? 1 : 0;
+            r.pad = 0;
+            r.ns = x.ns;
+            r.obj = x.obj;
+            r.rel = x.rel;
+            r.n_children = 0;
+            emit(S, leaf, r);
+            cnt += __popcll(__ballot(leaf));
+            if (!S.ok) {
+              status = EXP_ARENA;
+              break;
+            }
+            if (p == 64u) {
+              F.cursor += width;
+              continue;
+            }
+            // p is wave-uniform (a ballot's first lane): v_readlane, no LDS round trip per field
+            auto rl = [&](uint32_t v) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)p); };
+            const uint32_t cloc = rl(x.loc), ccb = rl(x.cb), clen = rl(x.len);
+            kg_tree_node u;
+            u.type = 1;
+            u.is_set = 1;
+            u.pad = 0;
+            u.ns = rl(x.ns);
+            u.obj = rl(x.obj);
+            u.rel = rl(x.rel);
+            u.n_children = clen;
+            F.cursor += p + 1;
+            if (ccb == NONE || sp >= 0x7FFF) {  // cannot happen (see the header); left to the next pass
+              status = EXP_OVERFLOW;
+              break;
+            }
+            if (lane == 0) vis[cloc >> 5] |= 1u << (cloc & 31);
+            emit(S, lane == 0, u);
+            cnt++;
+            if (!S.ok) {
+              status = EXP_ARENA;
+              break;
+            }
+            if (lane == 0) {
+              if (sp < XF) s_fr[sp] = F;
+              else gstack[sp] = F;
+            }
+            sp++;
+            __builtin_amdgcn_wave_barrier();
+            F = ExpFrame{ccb, cloc, 0, clen, F.d - 1};
+            pushed = true;
+            break;
+          }
+          if (status != EXP_OK) break;
+          if (pushed) continue;
+          if (sp == 0) break;
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+          sp--;
+          F = sp < XF ? s_fr[sp] : gstack[sp];
+        }
+      }
+      if (lane == 0) {
+        atomicMax(&ctl->gw_ticks[LOC_CAP > 16384 ? 3 : 1], wall_clock64() - t1);
+        if (status == EXP_OVERFLOW) {
+          ovf_list[atomicAdd(ovf_count, 1u)] = ri;
+        } else {
+          outs[ri] = RootOut{S.first, cnt};
+          recs += cnt;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0 && recs) atomicAdd(&ctl->records, recs);
 }
 
 __global__ void k_expand_compact(const RootOut* outs, uint32_t n, const uint64_t* off, const kg_tree_node* arena,
@@ -575,6 +900,9 @@ struct ExpandBufs {
   size_t dst_cap = 0;
   uint64_t* d_off = nullptr;
   size_t off_cap = 0;
+  void* gw[2] = {nullptr, nullptr};  // gather-walk slots: small, large (allocated once, epochs zeroed)
+  GwSlots gws[2] = {};
+  uint32_t gw_slots[2] = {0, 0};
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   hipEvent_t sync_ev = nullptr;  // blocking-sync: a caller waits asleep (16 batches in flight, 16 CPUs)
   // Waits for everything enqueued on st so far without spinning a core.
@@ -588,7 +916,7 @@ struct ExpandBufs {
   ~ExpandBufs() {
     if (device >= 0) hipSetDevice(device);
     for (void* p : {(void*)d_roots, (void*)outs, (void*)p2, (void*)ctl, (void*)stacks, (void*)bm, (void*)arena,
-                    (void*)next, (void*)dst, (void*)d_off})
+                    (void*)next, (void*)dst, (void*)d_off, gw[0], gw[1]})
       if (p) hipFree(p);
     for (auto& e : ev)
       if (e) hipEventDestroy(e);
@@ -661,6 +989,43 @@ static hipError_t grow(T** p, size_t& have, size_t need) {
   return e;
 }
 
+// Gather-walk slot classes: (slots, entries, map slots) -- local ids are the kernel's LOC_CAP.  Small:
+// the bulk of the pass-1 overflows (~1 k C5 roots of 0.5-10 k records); large: the few giant trees.
+constexpr uint32_t GW_LOC[2] = {16384, 262144};
+static hipError_t gw_alloc(ExpandBufs& B, int k, uint32_t slots, uint32_t ent_cap, hipStream_t stream) {
+  if (B.gw[k]) return hipSuccess;
+  const uint32_t map_cap = 2 * GW_LOC[k];
+  const size_t tf = ent_cap / 64 + 1;
+  const size_t per = (size_t)ent_cap * (sizeof(GwEnt) + 8 + 4) + tf * 4 + (size_t)map_cap * 16;
+  char* p = nullptr;
+  hipError_t e = hipMalloc((void**)&p, per * slots + (size_t)slots * 4 + 256);
+  if (e != hipSuccess) return e;
+  GwSlots g{};
+  g.ent_cap = ent_cap;
+  g.map_cap = map_cap;
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    char* q = p + off;
+    off += (bytes + 255) & ~size_t(255);
+    return q;
+  };
+  g.map = (unsigned long long*)take((size_t)slots * map_cap * 16);
+  g.hmark = (uint32_t*)take((size_t)slots * ent_cap * 4);
+  g.epoch = (uint32_t*)take((size_t)slots * 4);
+  const size_t zero = off;  // keys, run marks and epochs start at 0 (epoch 0 is never used)
+  g.ent = (GwEnt*)take((size_t)slots * ent_cap * sizeof(GwEnt));
+  g.hsrc = (uint64_t*)take((size_t)slots * ent_cap * 8);
+  g.tfirst = (uint32_t*)take((size_t)slots * tf * 4);
+  if ((e = hipMemsetAsync(p, 0, zero, stream)) != hipSuccess) {
+    hipFree(p);
+    return e;
+  }
+  B.gw[k] = p;
+  B.gws[k] = g;
+  B.gw_slots[k] = slots;
+  return hipSuccess;
+}
+
 int expand_batch(Snapshot* s, hipStream_t stream, void** bufs, const kg_set* roots, size_t n, int32_t global,
                  kg_tree_buf* out) {
   memset(out, 0, sizeof *out);
@@ -674,6 +1039,8 @@ int expand_batch(Snapshot* s, hipStream_t stream, void** bufs, const kg_set* roo
   ExpandBufs& B = *static_cast<ExpandBufs*>(*bufs);
   B.device = s->device;
   const uint32_t stack_cap = (uint32_t)std::min<int64_t>(0x8000, (int64_t)global + 2);
+  const bool gw_on = s->expand_gw != 0;
+  const uint32_t gw_n[2] = {std::max<uint32_t>(1, (uint32_t)s->n_cu / 2), 4};
   const uint32_t grid1 = (uint32_t)s->n_cu * 2, slots1 = grid1 * 4;
   const uint64_t nn = std::max<uint32_t>(s->ds.n_nodes, 1), words = ((nn + 31) / 32 + 1 + 3) & ~3ull;
   // pass 2: 2 slots per CU, each a visited hash + list of up to 256 Ki nodes (~5 MB a slot, <= 2 GiB;
@@ -694,14 +1061,17 @@ int expand_batch(Snapshot* s, hipStream_t stream, void** bufs, const kg_set* roo
     const size_t cap = std::max(n, 2 * B.n_cap);
     B.n_cap = 0;
     if ((e = grow(&B.d_roots, a, cap * sizeof(kg_set))) != hipSuccess || (e = grow(&B.outs, b, cap * sizeof(RootOut))) != hipSuccess ||
-        (e = grow(&B.p2, c, cap * 8)) != hipSuccess)
+        (e = grow(&B.p2, c, cap * 16)) != hipSuccess)  // p2 | p3 | ga | gb queues
       fail("hipMalloc", e);
     else
       B.n_cap = cap;
   }
   if (!rc && !B.ctl && (e = hipMalloc(&B.ctl, sizeof(ExpCtl))) != hipSuccess) fail("hipMalloc", e);
-  if (!rc && (e = grow(&B.stacks, B.stacks_bytes, (size_t)(slots1 + slots2 + 1) * stack_cap * sizeof(ExpFrame))) != hipSuccess)
+  if (!rc && (e = grow(&B.stacks, B.stacks_bytes,
+                       (size_t)(slots1 + slots2 + 1 + gw_n[0] + gw_n[1]) * stack_cap * sizeof(ExpFrame))) != hipSuccess)
     fail("hipMalloc", e);
+  for (int k = 0; k < 2 && gw_on && !rc; k++)
+    if ((e = gw_alloc(B, k, gw_n[k], k == 0 ? 65536u : (2u << 20), stream)) != hipSuccess) fail("hipMalloc(gather-walk)", e);
   if (!rc && (e = grow(&B.bm, B.bm_bytes, (clear_words + (size_t)slots2 * cap2 + nn) * 4)) != hipSuccess)
     fail("hipMalloc", e);
   for (auto& x : B.ev)
@@ -729,10 +1099,26 @@ int expand_batch(Snapshot* s, hipStream_t stream, void** bufs, const kg_set* roo
     }
     (void)hipEventRecord(B.ev[0], stream);
     hipLaunchKernelGGL(k_expand_lds, dim3(grid1), dim3(256), 0, stream, s->ds, B.d_roots, (uint32_t)n, global, B.ctl,
-                       B.outs, B.arena, B.next, n_chunks, B.stacks, stack_cap, B.p2);
+                       B.outs, B.arena, B.next, n_chunks, B.stacks, stack_cap, B.p2, s->expand_skip_lds);
+    // pass-1 overflows: gather-walk small slots -> large slots -> the hash pass (or straight to it)
+    uint32_t* q_hash = B.p2;
+    uint32_t* c_hash = &B.ctl->p2_count;
+    uint32_t* h_hash = &B.ctl->p2_head;
+    if (gw_on) {
+      ExpFrame* gst = B.stacks + (size_t)(slots1 + slots2 + 1) * stack_cap;
+      hipLaunchKernelGGL(k_expand_gw<GW_LOC[0]>, dim3(gw_n[0]), dim3(256), 0, stream, s->ds, B.d_roots, global, B.ctl,
+                         B.outs, B.arena, B.next, n_chunks, gst, stack_cap, B.p2, &B.ctl->p2_count, &B.ctl->gs_head,
+                         B.p2 + 2 * n, &B.ctl->ga_count, B.gws[0]);
+      hipLaunchKernelGGL(k_expand_gw<GW_LOC[1]>, dim3(gw_n[1]), dim3(256), 0, stream, s->ds, B.d_roots, global, B.ctl,
+                         B.outs, B.arena, B.next, n_chunks, gst + (size_t)gw_n[0] * stack_cap, stack_cap, B.p2 + 2 * n,
+                         &B.ctl->ga_count, &B.ctl->ga_head, B.p2 + 3 * n, &B.ctl->gb_count, B.gws[1]);
+      q_hash = B.p2 + 3 * n;
+      c_hash = &B.ctl->gb_count;
+      h_hash = &B.ctl->gb_head;
+    }
     hipLaunchKernelGGL(k_expand_hash, dim3(slots2), dim3(64), 0, stream, s->ds, B.d_roots, global, B.ctl, B.outs,
-                       B.arena, B.next, n_chunks, B.stacks + (size_t)slots1 * stack_cap, stack_cap, B.p2, B.bm, tsize,
-                       lists, cap2, B.p2 + n, s->expand_tail);
+                       B.arena, B.next, n_chunks, B.stacks + (size_t)slots1 * stack_cap, stack_cap, q_hash, c_hash,
+                       h_hash, B.bm, tsize, lists, cap2, B.p2 + n, s->expand_tail);
     hipLaunchKernelGGL(k_expand_hbm, dim3(1), dim3(64), 0, stream, s->ds, B.d_roots, global, B.ctl, B.outs, B.arena,
                        B.next, n_chunks, B.stacks + (size_t)(slots1 + slots2) * stack_cap, B.p2 + n,
                        B.bm + (size_t)slots2 * tsize, words, lists + (size_t)slots2 * cap2, nn, s->expand_tail);
@@ -746,7 +1132,13 @@ int expand_batch(Snapshot* s, hipStream_t stream, void** bufs, const kg_set* roo
       fail("expand", e);
       break;
     }
-    if (!h.overflow) break;
+    if (!h.overflow) {
+      if (getenv("KG_EXPAND_TRACE"))  // diagnostics: the longest gather / walk of one root per slot class
+        fprintf(stderr, "kg expand: gw small gather %.1f us walk %.1f us (queue %u) | large gather %.1f us walk %.1f us (queue %u) | hash queue %u\n",
+                h.gw_ticks[0] / 100.0, h.gw_ticks[1] / 100.0, h.p2_count, h.gw_ticks[2] / 100.0, h.gw_ticks[3] / 100.0,
+                h.ga_count, h.gb_count);
+      break;
+    }
     if (n_chunks >= (1u << 30) || attempt > 8) {
       rc = set_error(KG_ERR_RESOURCE, "expand output exceeds the arena");
       break;

@@ -277,7 +277,13 @@ struct Snapshot {
   uint32_t shard_back_budget = 1u << 14;  // kg_snapshot_tune("shard_back_budget"): reverse edges per query and rank
   int back_tier = 2;  // kg_snapshot_tune("back"): backward tier (1: wave + workgroup widths, 2: wave only) + no-holder filter
   uint32_t stream_ecap = 512;  // kg_snapshot_tune("stream_ecap"): stream-tier edge budget per query (0 = none)
-  int resolve_unheld = 1;  // kg_snapshot_tune("resolve_unheld"): k_resolve reads the holder bit before the node map
+  // kg_snapshot_tune("resolve_unheld"): 1 = k_resolve reads the holder bit before the node map (a subject
+  // no row holds skips it); 2 = reads it only for queries headed for the stream tier; 0 = beside the map
+  int resolve_unheld = 1;
+  // kg_snapshot_tune("expand_gw"): pass-1 overflows of kg_expand_batch run gather-then-walk (1) or the
+  // hash pass directly (0); "expand_skip_lds" (tests): every root skips the LDS pass
+  int expand_gw = 1;
+  int expand_skip_lds = 0;
   uint32_t stream_steal = 4;   // kg_snapshot_tune("stream_steal"): XCD ranges a k_stream4 wave dequeues from (1..8)
   uint32_t stream_chunk = 64;  // kg_snapshot_tune("stream_chunk"): k_stream4 queries per dequeue (1..64)
   // Occupancy defaults (library-wide, measured with several batches in flight, the way a server keeps

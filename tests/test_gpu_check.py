@@ -187,7 +187,8 @@ def _torch():
 
 
 @pytest.mark.parametrize("n_tuples,gmax,ecap,unheld", [(200_000, 10, 512, 1), (300_000, 5, 512, 1), (300_000, 10, 512, 0),
-                                                        (300_000, 10, 32, 1), (300_000, 5, 0, 0)])
+                                                        (300_000, 10, 32, 1), (300_000, 5, 0, 0), (300_000, 10, 512, 2),
+                                                        (300_000, 5, 32, 2)])
 def test_synthetic_graph_vs_oracle(n_tuples, gmax, ecap, unheld):
     """ecap: the stream tier's per-query edge budget (32: most long walks go on to the backward and
     grid tiers; 0: no budget, every walk finishes in the stream tier)."""
@@ -195,7 +196,7 @@ def test_synthetic_graph_vs_oracle(n_tuples, gmax, ecap, unheld):
     from keto_amd import _lib
     snap = Snapshot.synthetic(n_tuples, seed=20250131)
     snap.tune("stream_ecap", ecap)
-    snap.tune("resolve_unheld", unheld)  # 0: the node map is read for every query (round-1 order)
+    snap.tune("resolve_unheld", unheld)  # 0: the node map is read for every query (round-1 order); 2: lazy bit
     n = 20000
     dq = torch.empty((n, 7), dtype=torch.int32, device="cuda")
     _lib.check(_lib.load().kg_synth_queries(snap.handle, 7, n, dq.data_ptr()), "kg_synth_queries")

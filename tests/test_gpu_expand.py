@@ -39,8 +39,12 @@ def _records(rec):
     return None if rec is None else np.asarray(rec, np.int64)
 
 
+GW_MODES = [(1, 0), (1, 1), (0, 1)]  # (expand_gw, expand_skip_lds): default; gather-walk on every root; hash pass on every root
+
+
+@pytest.mark.parametrize("gw,skip", GW_MODES, ids=["default", "gw-all", "hash-all"])
 @pytest.mark.parametrize("seed", range(5))
-def test_random_expand_vs_oracle(seed):
+def test_random_expand_vs_oracle(seed, gw, skip):
     rng = np.random.default_rng(50 + seed)
     n_obj = 30 + 30 * seed
     tuples = []
@@ -53,6 +57,8 @@ def test_random_expand_vs_oracle(seed):
             s = f"u{rng.integers(30)}"
         tuples.append(RelationTuple.from_string(f"{ns}:{obj}#{rel}@{s}"))
     reg = Registry(tuples, [])
+    reg.snapshot.tune("expand_gw", gw)
+    reg.snapshot.tune("expand_skip_lds", skip)
     it = reg.interner
     oracle = Oracle(it.tuples_array(tuples), it.wildcard_rel)
     roots = []
@@ -73,13 +79,16 @@ def test_random_expand_vs_oracle(seed):
             _cmp_records(exp, g, (r, gmax))
 
 
-def test_expand_overflow_tier_and_wide_rows():
-    # a root whose visited set exceeds the LDS tier (pass 2, HBM bitmap) and rows wider than a wave
+@pytest.mark.parametrize("gw", [1, 0])
+def test_expand_overflow_tier_and_wide_rows(gw):
+    # a root whose visited set exceeds the LDS tier (pass 2: gather-walk or the HBM hash) and rows wider
+    # than a wave
     tuples = [RelationTuple.from_string(f"g:root#m@(g:c{i}#m)") for i in range(900)]
     tuples += [RelationTuple.from_string(f"g:c{i}#m@(g:d{i % 300}#m)") for i in range(900)]
     tuples += [RelationTuple.from_string(f"g:d{i}#m@u{i}") for i in range(300)]
     tuples += [RelationTuple.from_string(f"g:c{i}#m@x{i}") for i in range(0, 900, 7)]
     reg = Registry(tuples, [])
+    reg.snapshot.tune("expand_gw", gw)
     it = reg.interner
     oracle = Oracle(it.tuples_array(tuples), it.wildcard_rel)
     ex = reg.expand_engine()
@@ -88,6 +97,38 @@ def test_expand_overflow_tier_and_wide_rows():
         got = ex.build_tree(SubjectSet("g", "root", "m"), 0)
         exp = oracle_tree(oracle.expand(it.ns_id("g"), it.obj_id("root"), it.rel_id("m"), 0, gmax), it)
         assert got == exp, gmax
+
+
+def test_expand_gather_walk_large_slot_and_cycles():
+    """A neighbourhood too large for a small gather-walk slot (96 k copied entries > 64 Ki): the root
+    moves on to a large slot.  Shared grandchildren, back edges to the root and to a middle layer, and
+    subject ids in every row make the visited order matter; depths 2..6 (the copy's reach D-2 and the
+    local ids' reach D-1 both vary)."""
+    tuples = [RelationTuple.from_string(f"g:root#m@(g:c{i}#m)") for i in range(320)]
+    for i in range(320):
+        for j in range(300):
+            tuples.append(RelationTuple.from_string(f"g:c{i}#m@(g:d{(i * 7 + j * 13) % 2000}#m)"))
+        tuples.append(RelationTuple.from_string(f"g:c{i}#m@u{i}"))
+    for k in range(2000):
+        tuples.append(RelationTuple.from_string(f"g:d{k}#m@(g:e{k % 50}#m)"))
+        tuples.append(RelationTuple.from_string(f"g:d{k}#m@v{k}"))
+        if k % 97 == 0:
+            tuples.append(RelationTuple.from_string(f"g:d{k}#m@(g:root#m)"))
+            tuples.append(RelationTuple.from_string(f"g:d{k}#m@(g:c{k % 320}#m)"))
+    for k in range(50):
+        tuples.append(RelationTuple.from_string(f"g:e{k}#m@(g:c{k}#m)"))
+        tuples.append(RelationTuple.from_string(f"g:e{k}#m@w{k}"))
+    reg = Registry(tuples, [])
+    it = reg.interner
+    oracle = Oracle(it.tuples_array(tuples), it.wildcard_rel)
+    for gw in (1, 0):
+        reg.snapshot.tune("expand_gw", gw)
+        ex = reg.expand_engine()
+        for gmax in (2, 3, 4, 6):
+            ex.config.max_read_depth = gmax
+            got = ex.build_tree(SubjectSet("g", "root", "m"), 0)
+            exp = oracle_tree(oracle.expand(it.ns_id("g"), it.obj_id("root"), it.rel_id("m"), 0, gmax), it)
+            assert got == exp, (gw, gmax)
 
 
 def _cmp_records(exp, g, what):
@@ -105,14 +146,17 @@ def _cmp_records(exp, g, what):
     assert e2.shape == g2.shape and (e2 == g2).all(), what
 
 
-@pytest.mark.parametrize("n_tuples,gmax", [(300_000, 5), (1_000_000, 3)])
-def test_c5_hot_group_roots_vs_oracle(n_tuples, gmax):
+@pytest.mark.parametrize("n_tuples,gmax,gw,skip", [(300_000, 5, 1, 0), (1_000_000, 3, 1, 0), (300_000, 5, 1, 1),
+                                                    (300_000, 5, 0, 0)])
+def test_c5_hot_group_roots_vs_oracle(n_tuples, gmax, gw, skip):
     """Config C5's workload at reduced size: the generator's most popular group#member roots (the
     roots bench.py --mode expand times), expanded at the global depth, against the oracle's
     BuildTree on the snapshot's own rows -- same pre-order, same child order, every root."""
     from keto_amd.engine import Snapshot
     from keto_amd.synth import hot_group_roots
     snap = Snapshot.synthetic(n_tuples, seed=20250131)
+    snap.tune("expand_gw", gw)
+    snap.tune("expand_skip_lds", skip)
     roots = hot_group_roots(snap.synth_ids(), 1500)
     ex = ExpandEngine(snap)
     ex.config.max_read_depth = gmax
