@@ -426,12 +426,17 @@ def expand_cpu_baseline(orc, roots: np.ndarray, depth: int, a) -> dict:
         while t < budget / 4 and n < len(roots):
             n = min(len(roots), n * 4)
             t = run(n, th)
-        res[th] = (n / t, n, t)
+        passes, tt = 1, t
+        while tt < budget / 2:  # the whole set is quick on many cores: repeat it until the budget is spent
+            tt += run(n, th)
+            passes += 1
+        res[th] = (n * passes / tt, n, tt, passes)
     best = max(res, key=lambda k: res[k][0])
-    v, n, t = res[best]
+    v, n, t, passes = res[best]
     return {"value": v, "unit": "trees/s", "cores": best, "kind": "port",
-            "sample": f"the first {n} of the {len(roots)} C5 roots ({t:.1f} s), BuildTree with one visited set per "
-                      f"request (oracle/keto_oracle.c ko_expand_nodes_batch: ko_expand_node per root), {best} host threads (best of {sorted(res)})",
+            "sample": f"{passes} pass(es) over the first {n} of the {len(roots)} C5 roots ({t:.1f} s), BuildTree with one "
+                      f"visited set per request (oracle/keto_oracle.c ko_expand_nodes_batch: ko_expand_node per root), "
+                      f"{best} host threads (best of {sorted(res)})",
             "by_threads": {str(k): r[0] for k, r in sorted(res.items())}, "value_1thread": res[1][0],
             "cpus": cpus, "host_cpu": host_cpu()}
 

@@ -53,6 +53,7 @@ struct ExpCtl {
   // what outgrew a small slot (ga), the hash pass what outgrew a large one (gb)
   uint32_t gs_head, ga_count, ga_head, gb_count, gb_head, pad2[3];
   unsigned long long gw_ticks[4];  // longest gather / walk of one root, small and large slots (wall clock, 100 MHz)
+  unsigned long long gw_stat[8];   // diagnostics (sums over roots): chunks, unions at rest depth 2 / 3 / 4 / >= 5, pops, entries gathered
 };
 
 // Per-root result of the DFS: first chunk and record count (0 records = nil tree).
@@ -634,6 +635,11 @@ __global__ __launch_bounds__(256) void k_expand_gw(DevSnap s, const kg_set* __re
   __shared__ uint32_t vis[LOC_CAP / 32];
   __shared__ uint32_t s_k, s_nloc, s_nent, s_bad, s_epoch;
   __shared__ ExpFrame s_fr[XF];
+  // each frame level's last chunk (as expand_root_x): a pop resumes the parent's chunk from LDS, so an
+  // expanded set costs one trip to the copy (its own row), not two
+  __shared__ GwEnt s_ch[XF][64];
+  __shared__ uint64_t s_cbase[XF];
+  __shared__ uint32_t s_cn[XF];
   const int lane = lane_id(), wave = threadIdx.x >> 6;
   const size_t slot = blockIdx.x;
   GwEnt* E = g.ent + slot * g.ent_cap;
@@ -768,6 +774,9 @@ __global__ __launch_bounds__(256) void k_expand_gw(DevSnap s, const kg_set* __re
         emit(S, lane == 0, rec_set(s, 1, rn, (uint32_t)len0));
         cnt = 1;
         int sp = 0;
+        uint32_t st_chunks = 0, st_u[4] = {0, 0, 0, 0}, st_pops = 0;
+        if (lane < XF) s_cn[lane] = 0;
+        __builtin_amdgcn_wave_barrier();
         ExpFrame F{0, 0, 0, (uint32_t)len0, d0};
         for (;;) {
           const uint64_t eb = F.rb, ee = F.rb + F.len;
@@ -775,9 +784,26 @@ __global__ __launch_bounds__(256) void k_expand_gw(DevSnap s, const kg_set* __re
           bool pushed = false;
           while (eb + F.cursor < ee) {
             const uint64_t at0 = eb + F.cursor;
-            const uint32_t width = (uint32_t)min<uint64_t>(64, ee - at0);
+            const bool cached = sp < XF && s_cn[sp] && at0 >= s_cbase[sp] && at0 < s_cbase[sp] + s_cn[sp];
+            uint32_t width;
+            GwEnt x;
+            if (cached) {
+              const uint32_t k0 = (uint32_t)(at0 - s_cbase[sp]);
+              width = s_cn[sp] - k0;
+              x = s_ch[sp][(uint32_t)lane < width ? k0 + lane : k0];
+            } else {
+              width = (uint32_t)min<uint64_t>(64, ee - at0);
+              x = E[(uint32_t)lane < width ? at0 + lane : at0];
+              st_chunks++;
+              if (sp < XF) {
+                s_ch[sp][lane] = x;
+                if (lane == 0) {
+                  s_cbase[sp] = at0;
+                  s_cn[sp] = width;
+                }
+              }
+            }
             const bool valid = (uint32_t)lane < width;
-            const GwEnt x = E[valid ? at0 + lane : at0];
             const bool is_set = valid && (x.sub & SET_BIT);
             const bool has_loc = is_set && x.loc != NONE;
             bool cand = false;
@@ -823,6 +849,7 @@ __global__ __launch_bounds__(256) void k_expand_gw(DevSnap s, const kg_set* __re
               break;
             }
             if (lane == 0) vis[cloc >> 5] |= 1u << (cloc & 31);
+            st_u[min(3, max(0, F.d - 1 - 2))]++;
             emit(S, lane == 0, u);
             cnt++;
             if (!S.ok) {
@@ -834,6 +861,7 @@ __global__ __launch_bounds__(256) void k_expand_gw(DevSnap s, const kg_set* __re
               else gstack[sp] = F;
             }
             sp++;
+            if (lane == 0 && sp < XF) s_cn[sp] = 0;  // the child's level starts without a cached chunk
             __builtin_amdgcn_wave_barrier();
             F = ExpFrame{ccb, cloc, 0, clen, F.d - 1};
             pushed = true;
@@ -845,7 +873,14 @@ __global__ __launch_bounds__(256) void k_expand_gw(DevSnap s, const kg_set* __re
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
           sp--;
+          st_pops++;
           F = sp < XF ? s_fr[sp] : gstack[sp];
+        }
+        if (lane == 0) {
+          atomicAdd(&ctl->gw_stat[0], (unsigned long long)st_chunks);
+          for (int q = 0; q < 4; q++) atomicAdd(&ctl->gw_stat[1 + q], (unsigned long long)st_u[q]);
+          atomicAdd(&ctl->gw_stat[5], (unsigned long long)st_pops);
+          atomicAdd(&ctl->gw_stat[6], (unsigned long long)s_nent);
         }
       }
       if (lane == 0) {
@@ -1137,6 +1172,9 @@ int expand_batch(Snapshot* s, hipStream_t stream, void** bufs, const kg_set* roo
         fprintf(stderr, "kg expand: gw small gather %.1f us walk %.1f us (queue %u) | large gather %.1f us walk %.1f us (queue %u) | hash queue %u\n",
                 h.gw_ticks[0] / 100.0, h.gw_ticks[1] / 100.0, h.p2_count, h.gw_ticks[2] / 100.0, h.gw_ticks[3] / 100.0,
                 h.ga_count, h.gb_count);
+      if (getenv("KG_EXPAND_TRACE"))
+        fprintf(stderr, "kg expand: gw walk chunks %llu unions d2 %llu d3 %llu d4 %llu d5+ %llu pops %llu entries %llu records %llu\n",
+                h.gw_stat[0], h.gw_stat[1], h.gw_stat[2], h.gw_stat[3], h.gw_stat[4], h.gw_stat[5], h.gw_stat[6], h.records);
       break;
     }
     if (n_chunks >= (1u << 30) || attempt > 8) {
