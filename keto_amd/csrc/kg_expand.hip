@@ -51,7 +51,7 @@ struct ExpCtl {
   unsigned long long records;
   // gather-walk passes (expand_gw): the small slots take the pass-1 overflows (p2), the large slots
   // what outgrew a small slot (ga), the hash pass what outgrew a large one (gb)
-  uint32_t gs_head, ga_count, ga_head, gb_count, gb_head, pad2[3];
+  uint32_t gs_head, ga_count, ga_head, gb_count, gb_head, gw_small_done, pad2[2];
   unsigned long long gw_ticks[4];  // longest gather / walk of one root, small and large slots (wall clock, 100 MHz)
   unsigned long long gw_stat[8];   // diagnostics (sums over roots): chunks, unions at rest depth 2 / 3 / 4 / >= 5, pops, entries gathered
 };
@@ -582,7 +582,9 @@ struct GwSlots {
   unsigned long long* map;  // [slot][2 * map_cap] key (epoch << 32 | node), value (cb << 32 | local id)
   uint32_t* epoch;      // [slot]
   uint32_t ent_cap, map_cap;  // map_cap: a power of two
+  uint32_t loc_cap;           // local ids (<= GW_LDS_LOC, the walk's LDS bitmap)
 };
+constexpr uint32_t GW_LDS_LOC = 262144;
 
 __device__ __forceinline__ uint32_t ld_sc1(const uint32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -626,38 +628,82 @@ __device__ __forceinline__ void gw_run(const GwSlots& g, uint64_t* hsrc, uint32_
   for (uint32_t t = (cb + 63) / 64; t * 64 < cb + len; t++) tfirst[t] = cb;
 }
 
-template <uint32_t LOC_CAP>
+// A root handed on: ga (from a small slot; published as ri + 1 for the waiting large slots) or gb (from
+// a large slot; read by the hash pass, a later kernel).
+__device__ __forceinline__ void gw_publish(uint32_t* list, uint32_t* count, uint32_t ri, bool big) {
+  const uint32_t at = atomicAdd(count, 1u);
+  if (big) list[at] = ri;
+  else atomicExch(&list[at], ri + 1);
+}
+
+// One launch, two slot classes: workgroups [0, n_big) hold large slots, the rest small ones.  Every
+// workgroup takes pass-1 overflows (p2) from one queue; a root that outgrows a small slot is published
+// on the ga queue, which the large slots drain once p2 is empty -- so the giant trees start as soon as
+// a large slot is free instead of after the whole small-slot pass (two launches: ~12 + ~25 ms per C5
+// call in series).  A large slot waits for ga items with s_sleep and leaves when every small
+// workgroup has finished and the queue is drained (small workgroups never wait: the exit is reached).
+// What outgrows a large slot goes on to the hash pass (gb).
 __global__ __launch_bounds__(256) void k_expand_gw(DevSnap s, const kg_set* __restrict__ roots, int32_t global,
                                                    ExpCtl* ctl, RootOut* outs, kg_tree_node* arena, uint32_t* next,
                                                    uint32_t n_chunks, ExpFrame* stacks, uint32_t stack_cap,
-                                                   const uint32_t* qlist, const uint32_t* qcount, uint32_t* qhead,
-                                                   uint32_t* ovf_list, uint32_t* ovf_count, GwSlots g) {
-  __shared__ uint32_t vis[LOC_CAP / 32];
-  __shared__ uint32_t s_k, s_nloc, s_nent, s_bad, s_epoch;
+                                                   const uint32_t* p2_list, uint32_t* ga_list, uint32_t* gb_list,
+                                                   uint32_t n_big, GwSlots g_small, GwSlots g_big) {
+  __shared__ uint32_t vis[GW_LDS_LOC / 32];
+  __shared__ uint32_t s_k, s_nloc, s_nent, s_bad, s_epoch, s_ri, s_src, s_p2dry;
   __shared__ ExpFrame s_fr[XF];
-  // each frame level's last chunk (as expand_root_x): a pop resumes the parent's chunk from LDS, so an
-  // expanded set costs one trip to the copy (its own row), not two
-  __shared__ GwEnt s_ch[XF][64];
-  __shared__ uint64_t s_cbase[XF];
-  __shared__ uint32_t s_cn[XF];
+  // The walk's records are staged in LDS and leave one full arena chunk at a time: on CDNA a wave's
+  // vmcnt counts stores as well as loads, so a record store per step made every next load of the copy
+  // wait for the previous step's stores as well (the walk's step was ~1 us)
+  __shared__ uint4 s_out[CHUNK * sizeof(kg_tree_node) / 16];
   const int lane = lane_id(), wave = threadIdx.x >> 6;
-  const size_t slot = blockIdx.x;
+  const bool big = blockIdx.x < n_big;
+  const GwSlots& g = big ? g_big : g_small;
+  const size_t slot = big ? blockIdx.x : blockIdx.x - n_big;
+  const uint32_t n_small = gridDim.x - n_big;
+  uint32_t* ovf_list = big ? gb_list : ga_list;
+  uint32_t* ovf_count = big ? &ctl->gb_count : &ctl->ga_count;
   GwEnt* E = g.ent + slot * g.ent_cap;
   uint64_t* hsrc = g.hsrc + slot * g.ent_cap;
   uint32_t* hmark = g.hmark + slot * g.ent_cap;
   uint32_t* tfirst = g.tfirst + slot * (g.ent_cap / 64 + 1);
   unsigned long long* map = g.map + slot * 2 * (size_t)g.map_cap;
-  ExpFrame* gstack = stacks + slot * stack_cap;
+  ExpFrame* gstack = stacks + (size_t)blockIdx.x * stack_cap;
   const uint32_t mmask = g.map_cap - 1;
-  const uint32_t count = *qcount;  // written by an earlier kernel of the chain
+  const uint32_t p2_count = ctl->p2_count;  // written by pass 1 (the previous kernel)
   Stream S{arena, next, n_chunks, ctl, 0, 0, 0, true};
   unsigned long long recs = 0;
+  if (threadIdx.x == 0) s_p2dry = 0;
   for (;;) {
-    if (threadIdx.x == 0) s_k = atomicAdd(qhead, 1u);
+    if (threadIdx.x == 0) {
+      uint32_t src = 0, ri = 0;
+      if (!s_p2dry) {
+        const uint32_t k = atomicAdd(&ctl->gs_head, 1u);
+        if (k < p2_count) {
+          src = 1;
+          ri = p2_list[k];
+        } else {
+          s_p2dry = 1;
+        }
+      }
+      if (!src && big) {
+        const uint32_t k = atomicAdd(&ctl->ga_head, 1u);
+        for (;;) {
+          const uint32_t v = ld_sc1(&ga_list[k]);  // ri + 1 once published (the list is zeroed per call)
+          if (v) {
+            src = 2;
+            ri = v - 1;
+            break;
+          }
+          if (ld_sc1(&ctl->gw_small_done) == n_small && ld_sc1(&ctl->ga_count) <= k) break;
+          __builtin_amdgcn_s_sleep(16);
+        }
+      }
+      s_src = src;
+      s_ri = ri;
+    }
     __syncthreads();
-    const uint32_t k = s_k;
-    if (k >= count) break;
-    const uint32_t ri = qlist[k];
+    if (!s_src) break;
+    const uint32_t ri = s_ri;
     const kg_set root = roots[ri];
     int32_t d0 = root.max_depth;
     if (d0 <= 0 || global < d0) d0 = global;  // engine.go:37-39
@@ -716,7 +762,7 @@ __global__ __launch_bounds__(256) void k_expand_gw(DevSnap s, const kg_set* __re
                 if (won) {
                   const uint32_t loc = atomicAdd(&s_nloc, 1u);
                   uint32_t cb = NONE;
-                  if (loc >= LOC_CAP) s_bad = 1;
+                  if (loc >= g.loc_cap) s_bad = 1;
                   if (alloc_next) {
                     cb = atomicAdd(&s_nent, len);
                     if ((uint64_t)cb + len > g.ent_cap) {
@@ -751,13 +797,13 @@ __global__ __launch_bounds__(256) void k_expand_gw(DevSnap s, const kg_set* __re
       bad = s_bad != 0;
     }
     if (bad) {
-      if (threadIdx.x == 0) ovf_list[atomicAdd(ovf_count, 1u)] = ri;
+      if (threadIdx.x == 0) gw_publish(ovf_list, ovf_count, ri, big);
       __syncthreads();
       continue;
     }
     // the walk: wave 0 over the copy; the visited bitmap covers the root's local ids
     const unsigned long long t1 = wall_clock64();
-    if (threadIdx.x == 0) atomicMax(&ctl->gw_ticks[LOC_CAP > 16384 ? 2 : 0], t1 - t0);
+    if (threadIdx.x == 0) atomicMax(&ctl->gw_ticks[big ? 2 : 0], t1 - t0);
     const uint32_t nloc = s_nloc;
     for (uint32_t w = threadIdx.x; w < (nloc + 31) / 32; w += 256) vis[w] = 0;
     __syncthreads();
@@ -766,17 +812,51 @@ __global__ __launch_bounds__(256) void k_expand_gw(DevSnap s, const kg_set* __re
       int status = EXP_OK;
       uint32_t cnt = 0;
       S.ok = true;
-      S.pos = 0;
-      S.first = S.cur = alloc_chunk(S);
-      if (!S.ok) status = EXP_ARENA;
+      S.first = S.cur = NONE;
+      uint32_t nbuf = 0;  // records staged in s_out (wave-uniform)
+      kg_tree_node* sbuf = reinterpret_cast<kg_tree_node*>(s_out);
+      // staged -> a new arena chunk (linked after the root's previous one); n records, n <= CHUNK
+      auto flush = [&](uint32_t n) {
+        uint32_t c = 0;
+        if (lane == 0) c = atomicAdd(&ctl->arena_head, 1u);
+        c = __shfl(c, 0, 64);
+        if (c >= S.n_chunks) {
+          if (lane == 0) ctl->overflow = 1;
+          S.ok = false;
+          return;
+        }
+        if (lane == 0) {
+          S.next[c] = NONE;
+          if (S.cur != NONE) S.next[S.cur] = c;
+        }
+        if (S.first == NONE) S.first = c;
+        S.cur = c;
+        uint4* dst = reinterpret_cast<uint4*>(S.arena + (size_t)c * CHUNK);
+        const uint32_t words = (n * (uint32_t)sizeof(kg_tree_node) + 15) / 16;
+        for (uint32_t i = lane; i < words; i += 64) dst[i] = s_out[i];
+      };
+      // lanes with pred append one record each, in lane order
+      auto emit_l = [&](bool pred, const kg_tree_node& rr) {
+        const uint64_t m = __ballot(pred);
+        if (!m || !S.ok) return;
+        const uint32_t k = __popcll(m), rank = lanes_below(m), room = CHUNK - nbuf;
+        if (pred && rank < room) sbuf[nbuf + rank] = rr;
+        if (k < room) {
+          nbuf += k;
+          return;
+        }
+        __builtin_amdgcn_wave_barrier();
+        flush(CHUNK);
+        __builtin_amdgcn_wave_barrier();
+        if (pred && rank >= room) sbuf[rank - room] = rr;
+        nbuf = k - room;
+      };
       if (status == EXP_OK) {
         if (lane == 0) vis[0] = 1u;
-        emit(S, lane == 0, rec_set(s, 1, rn, (uint32_t)len0));
+        emit_l(lane == 0, rec_set(s, 1, rn, (uint32_t)len0));
         cnt = 1;
         int sp = 0;
         uint32_t st_chunks = 0, st_u[4] = {0, 0, 0, 0}, st_pops = 0;
-        if (lane < XF) s_cn[lane] = 0;
-        __builtin_amdgcn_wave_barrier();
         ExpFrame F{0, 0, 0, (uint32_t)len0, d0};
         for (;;) {
           const uint64_t eb = F.rb, ee = F.rb + F.len;
@@ -784,36 +864,14 @@ __global__ __launch_bounds__(256) void k_expand_gw(DevSnap s, const kg_set* __re
           bool pushed = false;
           while (eb + F.cursor < ee) {
             const uint64_t at0 = eb + F.cursor;
-            const bool cached = sp < XF && s_cn[sp] && at0 >= s_cbase[sp] && at0 < s_cbase[sp] + s_cn[sp];
-            uint32_t width;
-            GwEnt x;
-            if (cached) {
-              const uint32_t k0 = (uint32_t)(at0 - s_cbase[sp]);
-              width = s_cn[sp] - k0;
-              x = s_ch[sp][(uint32_t)lane < width ? k0 + lane : k0];
-            } else {
-              width = (uint32_t)min<uint64_t>(64, ee - at0);
-              x = E[(uint32_t)lane < width ? at0 + lane : at0];
-              st_chunks++;
-              if (sp < XF) {
-                s_ch[sp][lane] = x;
-                if (lane == 0) {
-                  s_cbase[sp] = at0;
-                  s_cn[sp] = width;
-                }
-              }
-            }
+            // (caching each frame level's chunk in LDS, as expand_root_x does, measured slower here: the
+            // walk is bound by its own instruction chain, ~1 us per chunk, not by the copy's latency)
+            const uint32_t width = (uint32_t)min<uint64_t>(64, ee - at0);
             const bool valid = (uint32_t)lane < width;
+            const GwEnt x = E[valid ? at0 + lane : at0];
+            st_chunks++;
             const bool is_set = valid && (x.sub & SET_BIT);
             const bool has_loc = is_set && x.loc != NONE;
-            bool cand = false;
-            if (has_loc && can_expand) cand = !((vis[x.loc >> 5] >> (x.loc & 31)) & 1u);
-            const uint64_t mc = __ballot(cand);
-            const uint32_t p = mc ? (uint32_t)(__ffsll((unsigned long long)mc) - 1) : 64u;
-            const bool leaf = valid && (uint32_t)lane < p;
-            // rest depth <= 1 below: child sets become leaves but are still marked (BuildTree marks
-            // before it looks at the depth); sets without rows need no mark
-            if (!can_expand && leaf && has_loc) atomicOr(&vis[x.loc >> 5], 1u << (x.loc & 31));
             kg_tree_node r;
             r.type = 2;
             r.is_set = is_set ? 1 : 0;
@@ -822,50 +880,101 @@ __global__ __launch_bounds__(256) void k_expand_gw(DevSnap s, const kg_set* __re
             r.obj = x.obj;
             r.rel = x.rel;
             r.n_children = 0;
-            emit(S, leaf, r);
-            cnt += __popcll(__ballot(leaf));
-            if (!S.ok) {
-              status = EXP_ARENA;
+            bool leave = false;
+            // lanes [lo, width) of the chunk are still to be emitted; a candidate whose children all sit
+            // at rest depth 1 is expanded inline, and the chunk continues from registers
+            for (uint32_t lo = 0;;) {
+              bool cand = false;
+              if (has_loc && can_expand && (uint32_t)lane >= lo) cand = !((vis[x.loc >> 5] >> (x.loc & 31)) & 1u);
+              const uint64_t mc = __ballot(cand);
+              const uint32_t p = mc ? (uint32_t)(__ffsll((unsigned long long)mc) - 1) : 64u;
+              const bool leaf = valid && (uint32_t)lane >= lo && (uint32_t)lane < p;
+              // rest depth <= 1 below: child sets become leaves but are still marked (BuildTree marks
+              // before it looks at the depth); sets without rows need no mark
+              if (!can_expand && leaf && has_loc) atomicOr(&vis[x.loc >> 5], 1u << (x.loc & 31));
+              emit_l(leaf, r);
+              cnt += __popcll(__ballot(leaf));
+              if (!S.ok) {
+                status = EXP_ARENA;
+                leave = true;
+                break;
+              }
+              if (p == 64u) {
+                F.cursor = (uint32_t)(at0 - eb) + width;
+                break;
+              }
+              // p is wave-uniform (a ballot's first lane): v_readlane, no LDS round trip per field
+              auto rl = [&](uint32_t v) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)p); };
+              const uint32_t cloc = rl(x.loc), ccb = rl(x.cb), clen = rl(x.len);
+              kg_tree_node u;
+              u.type = 1;
+              u.is_set = 1;
+              u.pad = 0;
+              u.ns = rl(x.ns);
+              u.obj = rl(x.obj);
+              u.rel = rl(x.rel);
+              u.n_children = clen;
+              if (ccb == NONE || sp >= 0x7FFF) {  // cannot happen (see the header); left to the next pass
+                status = EXP_OVERFLOW;
+                leave = true;
+                break;
+              }
+              if (lane == 0) vis[cloc >> 5] |= 1u << (cloc & 31);
+              st_u[min(3, max(0, F.d - 1 - 2))]++;
+              emit_l(lane == 0, u);
+              cnt++;
+              if (!S.ok) {
+                status = EXP_ARENA;
+                leave = true;
+                break;
+              }
+              if (F.d - 1 == 2) {
+                // the child's children are at rest depth 1: all leaves, the sets among them marked
+                for (uint64_t c0 = ccb; c0 < (uint64_t)ccb + clen; c0 += 64) {
+                  const uint32_t cw = (uint32_t)min<uint64_t>(64, (uint64_t)ccb + clen - c0);
+                  const bool cv = (uint32_t)lane < cw;
+                  const GwEnt y = E[cv ? c0 + lane : c0];
+                  st_chunks++;
+                  const bool yset = cv && (y.sub & SET_BIT);
+                  if (yset && y.loc != NONE) atomicOr(&vis[y.loc >> 5], 1u << (y.loc & 31));
+                  kg_tree_node ry;
+                  ry.type = 2;
+                  ry.is_set = yset ? 1 : 0;
+                  ry.pad = 0;
+                  ry.ns = y.ns;
+                  ry.obj = y.obj;
+                  ry.rel = y.rel;
+                  ry.n_children = 0;
+                  emit_l(cv, ry);
+                  cnt += cw;
+                  if (!S.ok) break;
+                }
+                if (!S.ok) {
+                  status = EXP_ARENA;
+                  leave = true;
+                  break;
+                }
+                lo = p + 1;
+                if (lo >= width) {
+                  F.cursor = (uint32_t)(at0 - eb) + width;
+                  break;
+                }
+                continue;
+              }
+              // a deeper child: push (the parent's chunk is reloaded from the copy on the pop)
+              F.cursor = (uint32_t)(at0 - eb) + p + 1;
+              if (lane == 0) {
+                if (sp < XF) s_fr[sp] = F;
+                else gstack[sp] = F;
+              }
+              sp++;
+              __builtin_amdgcn_wave_barrier();
+              F = ExpFrame{ccb, cloc, 0, clen, F.d - 1};
+              pushed = true;
+              leave = true;
               break;
             }
-            if (p == 64u) {
-              F.cursor += width;
-              continue;
-            }
-            // p is wave-uniform (a ballot's first lane): v_readlane, no LDS round trip per field
-            auto rl = [&](uint32_t v) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)p); };
-            const uint32_t cloc = rl(x.loc), ccb = rl(x.cb), clen = rl(x.len);
-            kg_tree_node u;
-            u.type = 1;
-            u.is_set = 1;
-            u.pad = 0;
-            u.ns = rl(x.ns);
-            u.obj = rl(x.obj);
-            u.rel = rl(x.rel);
-            u.n_children = clen;
-            F.cursor += p + 1;
-            if (ccb == NONE || sp >= 0x7FFF) {  // cannot happen (see the header); left to the next pass
-              status = EXP_OVERFLOW;
-              break;
-            }
-            if (lane == 0) vis[cloc >> 5] |= 1u << (cloc & 31);
-            st_u[min(3, max(0, F.d - 1 - 2))]++;
-            emit(S, lane == 0, u);
-            cnt++;
-            if (!S.ok) {
-              status = EXP_ARENA;
-              break;
-            }
-            if (lane == 0) {
-              if (sp < XF) s_fr[sp] = F;
-              else gstack[sp] = F;
-            }
-            sp++;
-            if (lane == 0 && sp < XF) s_cn[sp] = 0;  // the child's level starts without a cached chunk
-            __builtin_amdgcn_wave_barrier();
-            F = ExpFrame{ccb, cloc, 0, clen, F.d - 1};
-            pushed = true;
-            break;
+            if (leave) break;
           }
           if (status != EXP_OK) break;
           if (pushed) continue;
@@ -876,6 +985,11 @@ __global__ __launch_bounds__(256) void k_expand_gw(DevSnap s, const kg_set* __re
           st_pops++;
           F = sp < XF ? s_fr[sp] : gstack[sp];
         }
+        if (status == EXP_OK && S.ok && nbuf) {
+          __builtin_amdgcn_wave_barrier();
+          flush(nbuf);
+        }
+        if (status == EXP_OK && !S.ok) status = EXP_ARENA;
         if (lane == 0) {
           atomicAdd(&ctl->gw_stat[0], (unsigned long long)st_chunks);
           for (int q = 0; q < 4; q++) atomicAdd(&ctl->gw_stat[1 + q], (unsigned long long)st_u[q]);
@@ -884,9 +998,9 @@ __global__ __launch_bounds__(256) void k_expand_gw(DevSnap s, const kg_set* __re
         }
       }
       if (lane == 0) {
-        atomicMax(&ctl->gw_ticks[LOC_CAP > 16384 ? 3 : 1], wall_clock64() - t1);
+        atomicMax(&ctl->gw_ticks[big ? 3 : 1], wall_clock64() - t1);
         if (status == EXP_OVERFLOW) {
-          ovf_list[atomicAdd(ovf_count, 1u)] = ri;
+          gw_publish(ovf_list, ovf_count, ri, big);
         } else {
           outs[ri] = RootOut{S.first, cnt};
           recs += cnt;
@@ -895,7 +1009,13 @@ __global__ __launch_bounds__(256) void k_expand_gw(DevSnap s, const kg_set* __re
     }
     __syncthreads();
   }
-  if (threadIdx.x == 0 && recs) atomicAdd(&ctl->records, recs);
+  if (threadIdx.x == 0) {
+    if (recs) atomicAdd(&ctl->records, recs);
+    if (!big) {  // this workgroup's ga publications happen-before its count (the large slots' exit test)
+      __threadfence();
+      atomicAdd(&ctl->gw_small_done, 1u);
+    }
+  }
 }
 
 __global__ void k_expand_compact(const RootOut* outs, uint32_t n, const uint64_t* off, const kg_tree_node* arena,
@@ -1024,9 +1144,9 @@ static hipError_t grow(T** p, size_t& have, size_t need) {
   return e;
 }
 
-// Gather-walk slot classes: (slots, entries, map slots) -- local ids are the kernel's LOC_CAP.  Small:
+// Gather-walk slot classes: (slots, entries, map slots, local ids).  Small:
 // the bulk of the pass-1 overflows (~1 k C5 roots of 0.5-10 k records); large: the few giant trees.
-constexpr uint32_t GW_LOC[2] = {16384, 262144};
+constexpr uint32_t GW_LOC[2] = {16384, GW_LDS_LOC};
 static hipError_t gw_alloc(ExpandBufs& B, int k, uint32_t slots, uint32_t ent_cap, hipStream_t stream) {
   if (B.gw[k]) return hipSuccess;
   const uint32_t map_cap = 2 * GW_LOC[k];
@@ -1038,6 +1158,7 @@ static hipError_t gw_alloc(ExpandBufs& B, int k, uint32_t slots, uint32_t ent_ca
   GwSlots g{};
   g.ent_cap = ent_cap;
   g.map_cap = map_cap;
+  g.loc_cap = GW_LOC[k];
   size_t off = 0;
   auto take = [&](size_t bytes) {
     char* q = p + off;
@@ -1128,7 +1249,8 @@ int expand_batch(Snapshot* s, hipStream_t stream, void** bufs, const kg_set* roo
     }
     // every attempt starts from clear visited bitmaps (an arena overflow aborts roots mid-way)
     if ((e = hipMemsetAsync(B.bm, 0, clear_words * 4, stream)) != hipSuccess ||
-        (e = hipMemsetAsync(B.ctl, 0, sizeof(ExpCtl), stream)) != hipSuccess) {
+        (e = hipMemsetAsync(B.ctl, 0, sizeof(ExpCtl), stream)) != hipSuccess ||
+        (gw_on && (e = hipMemsetAsync(B.p2 + 2 * n, 0, n * 4, stream)) != hipSuccess)) {  // ga: published as ri + 1
       fail("memset", e);
       break;
     }
@@ -1141,12 +1263,9 @@ int expand_batch(Snapshot* s, hipStream_t stream, void** bufs, const kg_set* roo
     uint32_t* h_hash = &B.ctl->p2_head;
     if (gw_on) {
       ExpFrame* gst = B.stacks + (size_t)(slots1 + slots2 + 1) * stack_cap;
-      hipLaunchKernelGGL(k_expand_gw<GW_LOC[0]>, dim3(gw_n[0]), dim3(256), 0, stream, s->ds, B.d_roots, global, B.ctl,
-                         B.outs, B.arena, B.next, n_chunks, gst, stack_cap, B.p2, &B.ctl->p2_count, &B.ctl->gs_head,
-                         B.p2 + 2 * n, &B.ctl->ga_count, B.gws[0]);
-      hipLaunchKernelGGL(k_expand_gw<GW_LOC[1]>, dim3(gw_n[1]), dim3(256), 0, stream, s->ds, B.d_roots, global, B.ctl,
-                         B.outs, B.arena, B.next, n_chunks, gst + (size_t)gw_n[0] * stack_cap, stack_cap, B.p2 + 2 * n,
-                         &B.ctl->ga_count, &B.ctl->ga_head, B.p2 + 3 * n, &B.ctl->gb_count, B.gws[1]);
+      hipLaunchKernelGGL(k_expand_gw, dim3(gw_n[0] + gw_n[1]), dim3(256), 0, stream, s->ds, B.d_roots, global, B.ctl,
+                         B.outs, B.arena, B.next, n_chunks, gst, stack_cap, B.p2, B.p2 + 2 * n, B.p2 + 3 * n, gw_n[1],
+                         B.gws[0], B.gws[1]);
       q_hash = B.p2 + 3 * n;
       c_hash = &B.ctl->gb_count;
       h_hash = &B.ctl->gb_head;
