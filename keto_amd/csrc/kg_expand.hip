@@ -647,7 +647,7 @@ __global__ __launch_bounds__(256) void k_expand_gw(DevSnap s, const kg_set* __re
                                                    ExpCtl* ctl, RootOut* outs, kg_tree_node* arena, uint32_t* next,
                                                    uint32_t n_chunks, ExpFrame* stacks, uint32_t stack_cap,
                                                    const uint32_t* p2_list, uint32_t* ga_list, uint32_t* gb_list,
-                                                   uint32_t n_big, GwSlots g_small, GwSlots g_big) {
+                                                   uint32_t n_roots, uint32_t n_big, GwSlots g_small, GwSlots g_big) {
   __shared__ uint32_t vis[GW_LDS_LOC / 32];
   __shared__ uint32_t s_k, s_nloc, s_nent, s_bad, s_epoch, s_ri, s_src, s_p2dry;
   __shared__ ExpFrame s_fr[XF];
@@ -687,7 +687,8 @@ __global__ __launch_bounds__(256) void k_expand_gw(DevSnap s, const kg_set* __re
       }
       if (!src && big) {
         const uint32_t k = atomicAdd(&ctl->ga_head, 1u);
-        for (;;) {
+        // the list holds n_roots entries at most: a ticket past it can never be served
+        for (; k < n_roots;) {
           const uint32_t v = ld_sc1(&ga_list[k]);  // ri + 1 once published (the list is zeroed per call)
           if (v) {
             src = 2;
@@ -1264,8 +1265,8 @@ int expand_batch(Snapshot* s, hipStream_t stream, void** bufs, const kg_set* roo
     if (gw_on) {
       ExpFrame* gst = B.stacks + (size_t)(slots1 + slots2 + 1) * stack_cap;
       hipLaunchKernelGGL(k_expand_gw, dim3(gw_n[0] + gw_n[1]), dim3(256), 0, stream, s->ds, B.d_roots, global, B.ctl,
-                         B.outs, B.arena, B.next, n_chunks, gst, stack_cap, B.p2, B.p2 + 2 * n, B.p2 + 3 * n, gw_n[1],
-                         B.gws[0], B.gws[1]);
+                         B.outs, B.arena, B.next, n_chunks, gst, stack_cap, B.p2, B.p2 + 2 * n, B.p2 + 3 * n,
+                         (uint32_t)n, gw_n[1], B.gws[0], B.gws[1]);
       q_hash = B.p2 + 3 * n;
       c_hash = &B.ctl->gb_count;
       h_hash = &B.ctl->gb_head;
