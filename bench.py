@@ -50,7 +50,9 @@ def parse(argv=None):
     ap.add_argument("--heavy-tail", action="store_true",
                     help="out-degree law P(k) ~ k^-1.5 (Pareto tail index 0.5 for docs and groups, SURVEY.md 8d) "
                          "instead of the default 1.3 / 1.1; ~40x the rows per node")
-    ap.add_argument("--batch", type=int, default=1_000_000, help="checks per step per GPU")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="checks per step per GPU (default 1 M; 62,500 with --heavy-tail, its latency point: "
+                         "DESIGN.md 7f)")
     ap.add_argument("--global-depth", type=int, default=10)
     ap.add_argument("--seed", type=int, default=20250131)
     ap.add_argument("--stream-gate", type=int, default=0,
@@ -133,7 +135,8 @@ def parse(argv=None):
                          "queues and serialise")
     ap.add_argument("--inflight", type=int, default=None,
                     help="batches in flight per GPU: one HIP stream (own workspace) and one host thread each "
-                         "(default 4; 16 for --mode expand, whose batches end in long sequential roots)")
+                         "(default 4; 16 for --mode expand, whose batches end in long sequential roots; 2 with "
+                         "--heavy-tail)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline time budget (0 = skip)")
     ap.add_argument("--parity", type=int, default=1_000_000,
                     help="checks of the first timed batch compared with the oracle (Go-order DFS; 0 = skip).  Any "
@@ -181,8 +184,10 @@ def parse(argv=None):
     a = ap.parse_args(argv)
     if a.hw_queues is None:
         a.hw_queues = 16 if a.mode == "expand" else 0
+    if a.batch is None:
+        a.batch = 62_500 if a.heavy_tail else 1_000_000
     if a.inflight is None:
-        a.inflight = 16 if a.mode == "expand" else 4
+        a.inflight = 16 if a.mode == "expand" else (2 if a.heavy_tail else 4)
     if a.back_wgs is None:
         a.back_wgs = 1 if a.preset else 3
     if a.grid_wgs is None:
