@@ -267,7 +267,10 @@ int kg_snapshot_materialized(const kg_snapshot* s, uint64_t* out3);
  * overflow reruns in tests).
  * key "grid_bidir" (0..2^31-1, default 0): grid-tier slots whose subject has at most this many
  * holders alternate forward and backward turns (0: forward only).  key "expand_tail" (0/1, default
- * 1): the expand walk caches a root's last frontier in LDS.  Hash-sharded mode: key "shard_wgs"
+ * 1): the expand walk caches a root's last frontier in LDS.  key "expand_gw" (0/1, default 1): roots
+ * that outgrow the LDS pass gather their neighbourhood in parallel and walk the copy (small and large
+ * workgroup slots, then the hash pass); "expand_skip_lds" (0/1, tests): every root skips the LDS pass.
+ * Hash-sharded mode: key "shard_wgs"
  * (1..64, default 8) k_shard_level workgroups per CU; "shard_heavy" (default 64) set rows longer than
  * this go to k_shard_heavy, which spreads their edges over the grid (0: every row); "shard_vis_mode"
  * 0 = exact (query, node) CAS table (default), 1 = lossy direct-mapped cache; "shard_pack" (0/1,
