@@ -1007,7 +1007,7 @@ def main():
     # own result buffers (ctypes releases the GIL).  Every step checks a DISTINCT synthetic batch
     # (warm-up and timed steps alike), so no batch re-touches rows and probe lines a previous step
     # already pulled into L2 / the Infinity Cache.
-    streams = [torch.cuda.current_stream(local)] + [torch.cuda.Stream(local) for _ in range(P - 1)]
+    streams = inflight_streams(local, P)
     warm = max(a.warmup, P)  # every stream's workspace is allocated before the timed region
     n_batches = warm + a.steps
     n_distinct = min(n_batches, a.replay) if a.replay > 0 else n_batches
@@ -1293,7 +1293,7 @@ def c3_leg(a, local) -> dict:
     dev = f"cuda:{local}"
     B, P, K = a.batch, max(1, a.c3_inflight), a.c3_steps
     W = P
-    streams = [torch.cuda.Stream(local) for _ in range(P)]
+    streams = inflight_streams(local, P)
     dqs = []
     for k in range(W + K):
         d = torch.empty((B, 7), dtype=torch.int32, device=dev)
@@ -1348,6 +1348,19 @@ def c3_leg(a, local) -> dict:
     return res
 
 
+_STREAMS = {}
+
+
+def inflight_streams(local: int, P: int) -> list:
+    """The process's batches-in-flight streams on device `local`, created once and shared by the headline
+    and the sub-lines (the current stream first, as the headline always used it)."""
+    import torch
+    v = _STREAMS.setdefault(local, [torch.cuda.current_stream(local)])
+    while len(v) < P:
+        v.append(torch.cuda.Stream(local))
+    return v[:P]
+
+
 def sharded_leg(a, snap, size_param, dist, rank, world, local, backend, orc) -> dict:
     """Config C4 hash-sharded (BASELINE.json configs[3]) beside the replica headline: rank r
     holds only the rows of the objects hash(ns, obj) mod N == r of the same generator graph, and every
@@ -1378,7 +1391,12 @@ def sharded_leg(a, snap, size_param, dist, rank, world, local, backend, orc) -> 
     groups = [None] * P
     if dist is not None and P > 1:
         groups = [dist.new_group(list(range(world))) for _ in range(P)]
-    chks = [LibShardedChecker(ssnap, rank, world, dist, group=groups[p], transport=transport) for p in range(P)]
+    # the headline's streams: HIP maps streams onto its hardware queues (4 by default) round-robin as they
+    # are created, so fresh streams here could share queues with each other and serialise.  Not the
+    # current (null) stream: a transport bound to it would catch the library's null-stream calls.
+    streams = inflight_streams(local, P + 1)[1:]
+    chks = [LibShardedChecker(ssnap, rank, world, dist, group=groups[p], transport=transport, stream=streams[p])
+            for p in range(P)]
     B, K, W = a.batch, a.sharded_steps, max(a.sharded_warmup, P)
     dqs = []
     for k in range(W + K):  # distinct batches, drawn from the full graph (the replica snapshot)

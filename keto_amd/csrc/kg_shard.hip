@@ -892,6 +892,60 @@ __global__ void k_shard_done(uint32_t n, const uint8_t* __restrict__ res, const 
   bits[w] = b;
 }
 
+// One launch before each exchange of the N > 1 protocol (kg_shard_comm.hip), replacing four: block 0's
+// first wave folds the outgoing bucket counts into the batch accumulators (acc: flags | largest | sent
+// | sent to peers; lvl: this exchange's largest bucket), block 0 zeroes the level's output counters and
+// the hub-row head, and every thread packs one word of the done bitmap (words = 0: none).
+__global__ void k_shard_pre(const uint32_t* __restrict__ cc, uint32_t N, uint32_t B, uint32_t me,
+                            unsigned long long* acc, unsigned long long* lvl, uint32_t* zero_counts,
+                            unsigned long long* heavy_pk, uint32_t n, const uint8_t* __restrict__ res,
+                            const uint32_t* __restrict__ err, uint32_t esc_mask, uint32_t words, uint32_t* bits) {
+  if (blockIdx.x == 0) {
+    if (threadIdx.x < 64) {
+      const uint32_t i = threadIdx.x;
+      const uint32_t v = i < N ? cc[i] : 0u;
+      unsigned long long fl = (i < N && v > B) ? 1ull : 0ull, mx = v, sum = v, wire = i != me ? v : 0u;
+      for (int off = 32; off; off >>= 1) {
+        fl |= __shfl_xor(fl, off, 64);
+        mx = max(mx, __shfl_xor(mx, off, 64));
+        sum += __shfl_xor(sum, off, 64);
+        wire += __shfl_xor(wire, off, 64);
+      }
+      if (i == 0) {
+        acc[0] |= fl | cc[N];
+        acc[1] = max(acc[1], mx);
+        acc[2] += sum;
+        acc[3] += wire;
+        *lvl = max(*lvl, mx);
+      }
+    }
+    for (uint32_t i = threadIdx.x; i < N; i += blockDim.x) zero_counts[i] = 0;
+    if (threadIdx.x == 0 && heavy_pk) *heavy_pk = 0;
+  }
+  const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
+  if (w < words) {
+    uint32_t b = 0;
+    for (uint32_t k = 0; k < 32; k++) {
+      const uint32_t i = w * 32 + k;
+      if (i < n && (res[i] == KG_IS_MEMBER || (esc_mask && (err[i] & esc_mask)))) b |= 1u << k;
+    }
+    bits[w] = b;
+  }
+}
+
+int shard_pre_level(Snapshot* s, hipStream_t stream, const uint32_t* d_cur, uint32_t N, uint32_t B, uint32_t me,
+                    unsigned long long* acc, unsigned long long* lvl, uint32_t* d_next_counts, size_t n,
+                    const uint8_t* d_res, const uint32_t* d_err, int with_esc, uint32_t* d_bits, uint32_t words) {
+  HIPC(hipSetDevice(s->device));
+  if (N > 64) return set_error(-2, "shard_pre_level: at most 64 ranks");
+  if (words && words < (n + 31) / 32) return set_error(-2, "done bitmap too small (%u words for %zu queries)", words, n);
+  const uint32_t blocks = std::max<uint32_t>(1, (words + 255) / 256);
+  hipLaunchKernelGGL(k_shard_pre, dim3(blocks), dim3(256), 0, stream, d_cur, N, B, me, acc, lvl, d_next_counts,
+                     shard_heavy_head(s, stream), (uint32_t)n, d_res, d_err, with_esc ? ESC_BIT : 0u, words, d_bits);
+  HIPC(hipGetLastError());
+  return 0;
+}
+
 // One launch before each level of kg_shard_levels: the done bitmap from the results so far
 // (k_shard_done's packing; words = 0 at the first level) and the level's zeroed bucket counter and
 // hub-row count -- what the per-level driver did with a kernel and two fills.
@@ -1080,19 +1134,26 @@ int shard_seed(Snapshot* s, const kg_query* d_q, size_t n, int32_t gdepth, kg_fr
   return 0;
 }
 
+unsigned long long* shard_heavy_head(Snapshot* s, hipStream_t stream) {
+  if (hipSetDevice(s->device) != hipSuccess) return nullptr;
+  ShardCtx* c = s->shard_ctx(stream ? stream : s->stream);
+  return c ? (unsigned long long*)heavy_list(c).pk : nullptr;
+}
+
 int shard_level(Snapshot* s, const kg_frec* d_in, size_t n_in, const uint32_t* d_n_in, kg_frec* d_out, size_t cap,
                 uint32_t* d_counts, uint8_t* d_res, uint32_t* d_err, const uint32_t* d_done, uint32_t done_words,
-                hipStream_t stream, uint32_t n_seg, size_t seg_cap) {
+                hipStream_t stream, uint32_t n_seg, size_t seg_cap, bool prezeroed) {
   HIPC(hipSetDevice(s->device));
   if (!stream) stream = s->stream;
   ShardCtx* c = s->shard_ctx(stream);  // this stream's batch state (batches in flight on other streams)
   if (!c) return set_error(-4, "sharded batch state");
   // the bucket sizes restart; the flags word (counts[shard_n]: dropped records, visited table full)
-  // accumulates over the batch's levels, so the caller reads it once at the end
-  HIPC(hipMemsetAsync(d_counts, 0, s->shard_n * 4, stream));
+  // accumulates over the batch's levels, so the caller reads it once at the end.  prezeroed: the
+  // caller's kernel before this level already cleared the bucket counters and the hub-row head.
+  if (!prezeroed) HIPC(hipMemsetAsync(d_counts, 0, s->shard_n * 4, stream));
   if (n_in) {
     const HeavyList heavy = heavy_list(c);
-    HIPC(hipMemsetAsync(heavy.pk, 0, 8, stream));
+    if (!prezeroed) HIPC(hipMemsetAsync(heavy.pk, 0, 8, stream));
     const uint32_t grid = (uint32_t)std::min<uint64_t>((n_in + 255) / 256, (uint64_t)s->n_cu * s->shard_wgs);
     hipLaunchKernelGGL(k_shard_level, dim3(grid), dim3(256), 0, stream, s->ds, d_in, (uint64_t)n_in, d_n_in, d_out,
                        (uint64_t)cap, d_counts, d_res, d_err, (uint64_t*)c->vis, c->vis_slots - 1,

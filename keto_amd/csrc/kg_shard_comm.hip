@@ -256,30 +256,11 @@ static int h_alltoall2(ShardComm* c, const void* s0, void* r0, size_t b0, const 
 // ranks, [4..11] tot of the one-rank loop, [12..19] host all-reduce scratch, then:
 constexpr int ACC_LEFT = 20;  // records left at the end of the phases before the last
 constexpr int ACC_BACK = 21;  // largest backward-phase bucket
-// Per exchange k before it runs (keto_amd/sharded.py _check_fixed's device accumulators): acc[0] |=
-// overflow flags (c[N], or a bucket past B_k), acc[1] = largest bucket, acc[2] += records sent,
-// acc[3] += records sent to other ranks (what crosses xGMI), *lvl = exchange k's largest bucket (the
-// counters keep counting past B_k, so an overflowed bucket reports what it would have needed).
-__global__ void k_sc_acc(const uint32_t* __restrict__ c, uint32_t N, uint32_t B, uint32_t me, unsigned long long* acc,
-                         unsigned long long* lvl) {
-  const uint32_t i = threadIdx.x;
-  const uint32_t v = i < N ? c[i] : 0u;
-  unsigned long long fl = (i < N && v > B) ? 1ull : 0ull, mx = v, sum = v, wire = i != me ? v : 0u;
-  for (int off = 32; off; off >>= 1) {
-    fl |= __shfl_xor(fl, off, 64);
-    mx = max(mx, __shfl_xor(mx, off, 64));
-    sum += __shfl_xor(sum, off, 64);
-    wire += __shfl_xor(wire, off, 64);
-  }
-  if (i == 0) {
-    acc[0] |= fl | c[N];
-    acc[1] = max(acc[1], mx);
-    acc[2] += sum;
-    acc[3] += wire;
-    *lvl = max(*lvl, mx);  // exchange k runs once per forward phase (twice with escalation)
-  }
-}
-
+// Per exchange k before it runs (kg_shard.hip k_shard_pre; keto_amd/sharded.py _check_fixed's device
+// accumulators): acc[0] |= overflow flags (c[N], or a bucket past B_k), acc[1] = largest bucket,
+// acc[2] += records sent, acc[3] += records sent to other ranks (what crosses xGMI), *lvl = exchange
+// k's largest bucket (the counters keep counting past B_k, so an overflowed bucket reports what it
+// would have needed).
 // After the last level: tot = (bucket overflow, visited overflow, largest bucket, records left, 0).
 __global__ void k_sc_final(const uint32_t* __restrict__ c, uint32_t N, uint32_t B, unsigned long long* acc,
                            unsigned long long* tot) {
@@ -887,22 +868,24 @@ int shard_check(Snapshot* s, ShardComm* c, const kg_query* d_q, size_t n, int32_
     for (int phase = 0; xch && phase < (esc ? 2 : 1); phase++) {
       for (int k = 0; k < L; k++) {
         const size_t Bk = c->lb[(size_t)k], Bn = c->lb[(size_t)k + 1];
-        hipLaunchKernelGGL(k_sc_acc, dim3(1), dim3(64), 0, st, counts[cur], N, (uint32_t)Bk, (uint32_t)c->rank, acc,
-                           lvl + k);
-        HIPC(hipGetLastError());
+        const int nx = cur ^ 1;
+        // one kernel: the outgoing counts into the accumulators, the level's output counters and hub
+        // head cleared, and (from the second exchange) the done bitmap -- the escalating forward phase
+        // counts escalated queries as done too
+        const bool with_done = c->prune && k > 0;
+        if (int rc = shard_pre_level(s, st, counts[cur], N, (uint32_t)Bk, (uint32_t)c->rank, acc, lvl + k, counts[nx],
+                                     slots, c->res, c->err, esc && phase == 0 ? 1 : 0, c->bits, with_done ? words : 0u))
+          return rc;
         if (int rc = x_alltoall2(c, counts[cur], rcv, 4, c->buf[cur], c->recv, Bk * sizeof(kg_frec))) return rc;
         wire += (uint64_t)(N - 1) * (4 + Bk * sizeof(kg_frec));
         const uint32_t* done = nullptr;
-        if (c->prune && k > 0) {
-          // the forward phase of an escalating batch: escalated queries are done here too
-          if (int rc = shard_done(s, slots, c->res, c->err, esc && phase == 0 ? 1 : 0, c->bits, words, st)) return rc;
+        if (with_done) {
           if (int rc = x_allgather(c, c->bits, c->bits_all, (size_t)words * 4)) return rc;
           wire += (uint64_t)(N - 1) * words * 4;
           done = c->bits_all;
         }
-        const int nx = cur ^ 1;
         if (int rc = shard_level(s, c->recv, (size_t)N * Bk, rcv, c->buf[nx], Bn, counts[nx], c->res, c->err, done,
-                                 words, st, N, Bk))
+                                 words, st, N, Bk, true))
           return rc;
         cur = nx;
         c->st[phase ? 12 : 0]++;

@@ -383,7 +383,13 @@ int shard_seed(Snapshot* s, const kg_query* d_q, size_t n, int32_t gdepth, kg_fr
                uint32_t* d_counts, uint8_t* d_res, uint32_t* d_err, hipStream_t stream);
 int shard_level(Snapshot* s, const kg_frec* d_in, size_t n_in, const uint32_t* d_n_in, kg_frec* d_out, size_t cap,
                 uint32_t* d_counts, uint8_t* d_res, uint32_t* d_err, const uint32_t* d_done, uint32_t done_words,
-                hipStream_t stream, uint32_t n_seg = 1, size_t seg_cap = 0);
+                hipStream_t stream, uint32_t n_seg = 1, size_t seg_cap = 0, bool prezeroed = false);
+// the stream's hub-row list head (zeroed before each level; kg_shard_comm's fused pre-level kernel)
+unsigned long long* shard_heavy_head(Snapshot* s, hipStream_t stream);
+// the exchange protocol's fused pre-exchange kernel (accumulators, next counters, hub head, done bitmap)
+int shard_pre_level(Snapshot* s, hipStream_t stream, const uint32_t* d_cur, uint32_t N, uint32_t B, uint32_t me,
+                    unsigned long long* acc, unsigned long long* lvl, uint32_t* d_next_counts, size_t n,
+                    const uint8_t* d_res, const uint32_t* d_err, int with_esc, uint32_t* d_bits, uint32_t words);
 int shard_done(Snapshot* s, size_t n, const uint8_t* d_res, const uint32_t* d_err, int with_esc, uint32_t* d_bits,
                uint32_t words, hipStream_t stream);
 int shard_levels(Snapshot* s, int levels, kg_frec* d_buf[2], size_t cap, uint32_t* d_counts[2], int start,
