@@ -147,7 +147,7 @@ def parse(argv=None):
     ap.add_argument("--latency-batches", type=int, default=240,
                     help="batches of the separate latency phase (after the timed region, same batches in flight): "
                          "p50 / p99 batch latency, submit to done")
-    ap.add_argument("--host-calls", type=int, default=6,
+    ap.add_argument("--host-calls", type=int, default=20,
                     help="kg_check_batch calls per in-flight thread in the host-path leg (1 M-check host batches, "
                          "PCIe both ways; 0 = skip)")
     ap.add_argument("--stats-every", type=int, default=1,
