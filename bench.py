@@ -71,9 +71,10 @@ def parse(argv=None):
     ap.add_argument("--c3-inflight", type=int, default=6)
     ap.add_argument("--c3-parity", type=int, default=200_000)
     ap.add_argument("--sharded-inflight", type=int, default=0,
-                    help="sharded batches in flight per rank, each with its own communicator (0: 4 at one rank, 1 "
-                         "across ranks -- streams share HIP's hardware queues, and collectives of different "
-                         "communicators queued in different orders on different ranks can deadlock)")
+                    help="sharded batches in flight per rank, each with its own communicator (0: 3 at one rank -- "
+                         "4 measured 20 %% slower, 6 slower still (DESIGN.md 7f) -- and 1 across ranks: streams "
+                         "share HIP's hardware queues, and collectives of different communicators queued in "
+                         "different orders on different ranks can deadlock)")
     ap.add_argument("--sharded-timeout", type=float, default=300.0,
                     help="watchdog of the sharded sub-line: past it rank 0 prints the line without it")
     ap.add_argument("--shard-budget", type=int, default=0,
@@ -147,6 +148,8 @@ def parse(argv=None):
     ap.add_argument("--latency-batches", type=int, default=240,
                     help="batches of the separate latency phase (after the timed region, same batches in flight): "
                          "p50 / p99 batch latency, submit to done")
+    ap.add_argument("--stream-base", type=int, default=0,
+                    help="diagnostics: the headline's in-flight streams start at this one (0 = the current stream)")
     ap.add_argument("--host-calls", type=int, default=20,
                     help="kg_check_batch calls per in-flight thread in the host-path leg (1 M-check host batches, "
                          "PCIe both ways; 0 = skip)")
@@ -1007,7 +1010,7 @@ def main():
     # own result buffers (ctypes releases the GIL).  Every step checks a DISTINCT synthetic batch
     # (warm-up and timed steps alike), so no batch re-touches rows and probe lines a previous step
     # already pulled into L2 / the Infinity Cache.
-    streams = inflight_streams(local, P)
+    streams = inflight_streams(local, P + a.stream_base)[a.stream_base:]  # --stream-base: diagnostics
     warm = max(a.warmup, P)  # every stream's workspace is allocated before the timed region
     n_batches = warm + a.steps
     n_distinct = min(n_batches, a.replay) if a.replay > 0 else n_batches
@@ -1387,7 +1390,7 @@ def sharded_leg(a, snap, size_param, dist, rank, world, local, backend, orc) -> 
                                    doc_alpha=alpha, group_alpha=alpha)
     t_build = time.time() - t0
     transport = "rccl" if backend == "nccl" else "host"
-    P = a.sharded_inflight if a.sharded_inflight > 0 else (4 if world == 1 else 1)
+    P = a.sharded_inflight if a.sharded_inflight > 0 else (3 if world == 1 else 1)
     groups = [None] * P
     if dist is not None and P > 1:
         groups = [dist.new_group(list(range(world))) for _ in range(P)]
