@@ -64,7 +64,8 @@ def parse(argv=None):
     ap.add_argument("--sharded-warmup", type=int, default=4)
     ap.add_argument("--expand-steps", type=int, default=6,
                     help="check mode, one rank: timed calls of the C5 expand sub-line over the headline graph (0 = off)")
-    ap.add_argument("--expand-inflight", type=int, default=4)
+    ap.add_argument("--expand-inflight", type=int, default=8,
+                    help="check mode: kg_expand_batch calls in flight in the C5 sub-line (one library lane each)")
     ap.add_argument("--c3-steps", type=int, default=20,
                     help="check mode, one rank: timed batches of the C3 sub-line (OPL rewrites; 0 = off)")
     ap.add_argument("--c3-tuples", type=float, default=1e7, help="C3 sub-line graph size (BASELINE configs[2]: 10M)")
@@ -132,8 +133,8 @@ def parse(argv=None):
     ap.add_argument("--interp-wgs", type=int, default=6, help="kg_snapshot_tune interp_wgs (rewrite-path LDS pass WGs per CU)")
     ap.add_argument("--hw-queues", type=int, default=None,
                     help="HIP hardware queues for this process (GPU_MAX_HW_QUEUES, 1..32; 0 = HIP's default, 4; "
-                         "default 16 for --mode expand, else 0): batches in flight beyond the queue count share "
-                         "queues and serialise")
+                         "default 16): streams map onto queues round-robin as they are created, and in-flight "
+                         "streams that share a queue serialise (DESIGN.md 7f)")
     ap.add_argument("--inflight", type=int, default=None,
                     help="batches in flight per GPU: one HIP stream (own workspace) and one host thread each "
                          "(default 4; 16 for --mode expand, whose batches end in long sequential roots; 2 with "
@@ -186,7 +187,7 @@ def parse(argv=None):
     ap.add_argument("--delta", type=int, default=1000, help="--mode refresh: rows per transaction")
     a = ap.parse_args(argv)
     if a.hw_queues is None:
-        a.hw_queues = 16 if a.mode == "expand" else 0
+        a.hw_queues = 16
     if a.batch is None:
         a.batch = 62_500 if a.heavy_tail else 1_000_000
     if a.inflight is None:
