@@ -647,8 +647,7 @@ __global__ __launch_bounds__(256) void k_expand_gw(DevSnap s, const kg_set* __re
                                                    ExpCtl* ctl, RootOut* outs, kg_tree_node* arena, uint32_t* next,
                                                    uint32_t n_chunks, ExpFrame* stacks, uint32_t stack_cap,
                                                    const uint32_t* p2_list, uint32_t* ga_list, uint32_t* gb_list,
-                                                   uint32_t n_roots, uint32_t n_big, GwSlots g_small, GwSlots g_big,
-                                                   int dbg) {
+                                                   uint32_t n_roots, uint32_t n_big, GwSlots g_small, GwSlots g_big) {
   __shared__ uint32_t vis[GW_LDS_LOC / 32];
   __shared__ uint32_t s_k, s_nloc, s_nent, s_bad, s_epoch, s_ri, s_src, s_p2dry;
   __shared__ ExpFrame s_fr[XF];
@@ -840,7 +839,7 @@ __global__ __launch_bounds__(256) void k_expand_gw(DevSnap s, const kg_set* __re
       // lanes with pred append one record each, in lane order
       auto emit_l = [&](bool pred, const kg_tree_node& rr) {
         const uint64_t m = __ballot(pred);
-        if (!m || !S.ok || (dbg & 1)) return;  // dbg 1: timing without the records (diagnostics only)
+        if (!m || !S.ok) return;
         const uint32_t k = __popcll(m), rank = lanes_below(m), room = CHUNK - nbuf;
         if (pred && rank < room) sbuf[nbuf + rank] = rr;
         if (k < room) {
@@ -1267,7 +1266,7 @@ int expand_batch(Snapshot* s, hipStream_t stream, void** bufs, const kg_set* roo
       ExpFrame* gst = B.stacks + (size_t)(slots1 + slots2 + 1) * stack_cap;
       hipLaunchKernelGGL(k_expand_gw, dim3(gw_n[0] + gw_n[1]), dim3(256), 0, stream, s->ds, B.d_roots, global, B.ctl,
                          B.outs, B.arena, B.next, n_chunks, gst, stack_cap, B.p2, B.p2 + 2 * n, B.p2 + 3 * n,
-                         (uint32_t)n, gw_n[1], B.gws[0], B.gws[1], getenv("KG_GW_DBG") ? atoi(getenv("KG_GW_DBG")) : 0);
+                         (uint32_t)n, gw_n[1], B.gws[0], B.gws[1]);
       q_hash = B.p2 + 3 * n;
       c_hash = &B.ctl->gb_count;
       h_hash = &B.ctl->gb_head;

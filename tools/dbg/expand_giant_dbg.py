@@ -1,4 +1,5 @@
-# diagnostics: the C5 giant root's walk time with and without record emission (KG_GW_DBG=1 drops records)
+# diagnostics: a hot C5 root's gather / walk times (KG_EXPAND_TRACE).  Round 5 timed the walk without its
+# record emission with a temporary KG_GW_DBG switch in k_expand_gw (17 % of the walk); the switch is gone.
 import ctypes as C, os, subprocess, sys
 code = r'''
 import ctypes as C, sys, os, numpy as np
