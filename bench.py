@@ -58,10 +58,14 @@ def parse(argv=None):
     ap.add_argument("--stream-gate", type=int, default=0,
                     help="kg_snapshot_tune stream_gate: k_stream4 launches of different batches at once (0 = no cap)")
     ap.add_argument("--stream-ecap", type=int, default=512, help="kg_snapshot_tune stream_ecap (stream-tier edges per query, 0 = none)")
-    ap.add_argument("--sharded-steps", type=int, default=60,
+    ap.add_argument("--sharded-steps", type=int, default=20,
                     help="check mode: timed batches of the hash-sharded sub-line (the C4 engine through "
                          "kg_check_batch_device over RCCL, one shard per rank; 0 = off)")
     ap.add_argument("--sharded-warmup", type=int, default=4)
+    ap.add_argument("--sharded-batch", type=int, default=4_000_000,
+                    help="checks per sharded batch per rank (0: --batch).  C4 names 1-8 M; across ranks one batch "
+                         "is in flight per rank, and 4 M amortises the exchanges' fixed cost: one-rank exchange "
+                         "protocol 0.80 / 1.19 / 1.29 x 10^9 checks/s at 1 / 4 / 8 M (DESIGN.md 7f)")
     ap.add_argument("--expand-steps", type=int, default=6,
                     help="check mode, one rank: timed calls of the C5 expand sub-line over the headline graph (0 = off)")
     ap.add_argument("--expand-inflight", type=int, default=8,
@@ -1401,7 +1405,7 @@ def sharded_leg(a, snap, size_param, dist, rank, world, local, backend, orc) -> 
     streams = inflight_streams(local, P + 1)[1:]
     chks = [LibShardedChecker(ssnap, rank, world, dist, group=groups[p], transport=transport, stream=streams[p])
             for p in range(P)]
-    B, K, W = a.batch, a.sharded_steps, max(a.sharded_warmup, P)
+    B, K, W = a.sharded_batch or a.batch, a.sharded_steps, max(a.sharded_warmup, P)
     dqs = []
     for k in range(W + K):  # distinct batches, drawn from the full graph (the replica snapshot)
         d = torch.empty((B, 7), dtype=torch.int32, device=dev)
