@@ -99,6 +99,9 @@ def parse(argv=None):
                     help="kg_snapshot_tune shard_vis: log2 of the sharded mode's (query, node) visited table (0: library default)")
     ap.add_argument("--shard-vis-mode", type=int, default=0,
                     help="kg_snapshot_tune shard_vis_mode (sharded (query, node) dedup: 0 exact CAS table, 1 lossy cache)")
+    ap.add_argument("--shard-remote-meta", type=int, default=1,
+                    help="kg_snapshot_tune shard_remote_meta (N > 1: owners' row length + signature of remote "
+                         "children in adjx at bind time, so remote leaves that cannot hit are never sent)")
     ap.add_argument("--device-sync", type=int, default=1,
                     help="kg_snapshot_tune device_sync (1: kg_check_batch_device waits asleep instead of spinning)")
     ap.add_argument("--host-sync", type=int, default=1,
@@ -1393,6 +1396,7 @@ def sharded_leg(a, snap, size_param, dist, rank, world, local, backend, orc) -> 
         alpha = 0.5 if a.heavy_tail else 0.0
         ssnap = Snapshot.synthetic(size_param, seed=a.seed, device=local, shard=(rank, world), preset=a.preset,
                                    doc_alpha=alpha, group_alpha=alpha)
+        ssnap.tune("shard_remote_meta", a.shard_remote_meta)  # applied when the checkers bind below
     t_build = time.time() - t0
     transport = "rccl" if backend == "nccl" else "host"
     P = a.sharded_inflight if a.sharded_inflight > 0 else (3 if world == 1 else 1)
@@ -1500,7 +1504,8 @@ def sharded_leg(a, snap, size_param, dist, rank, world, local, backend, orc) -> 
            "n_gpus": world, "transport": "RCCL over xGMI" if transport == "rccl" else "host (gloo)",
            "config": {"workload": "C4: the headline's generator graph hash-sharded by object over %d rank(s), "
                                   "%d checks/step/rank, max_read_depth %d" % (world, B, a.global_depth),
-                      "rows_on_rank": ssnap.info()["rows"], "parallelism": f"shard{world}"},
+                      "rows_on_rank": ssnap.info()["rows"], "parallelism": f"shard{world}",
+                      "remote_meta": a.shard_remote_meta if world > 1 else None},
            "snapshot_build_s": t_build, "scaling": "weak"}
     out.update(measure("default"))
     if world == 1:

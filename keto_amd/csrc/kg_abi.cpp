@@ -427,6 +427,11 @@ static int tune_one(Snapshot* s, const char* key, int64_t value) {
     s->shard_local = (int)value;
     return 0;
   }
+  if (strcmp(key, "shard_remote_meta") == 0) {
+    if (value < 0 || value > 1) return set_error(-2, "shard_remote_meta must be 0 or 1");
+    s->shard_remote_meta = (int)value;
+    return 0;
+  }
   if (strcmp(key, "shard_max_reruns") == 0) {
     if (value < 0 || value > 64) return set_error(-2, "shard_max_reruns must be in [0, 64]");
     s->shard_max_reruns = (uint32_t)value;

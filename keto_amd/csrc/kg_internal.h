@@ -198,7 +198,13 @@ struct DevSnap {
   // hash-sharded mode: this snapshot holds the rows of the nodes with shard_owner == shard_rank
   uint32_t shard_rank, shard_n;
   const uint8_t* nowner;  // [n_nodes] owner rank of every node (shard_n > 1)
+  // shard_n > 1, set when a transport is bound (kg_shard_comm.hip comm_setup): an adjx record whose
+  // child another rank owns has begin = ADJX_REMOTE | owner and the OWNER's row length and signature
+  // in lsig / sig (all-reduced at bind time), so the sender decides like for a local child -- no
+  // nowner read per edge, and a remote child that can neither hit nor expand is never sent
+  uint32_t remote_meta;
 };
+constexpr uint32_t ADJX_REMOTE = 0x80000000u;
 
 // The child's exact set-row length (one adj_off read for rows of ADJX_LEN_SAT edges or more).
 __device__ __forceinline__ uint32_t adjx_len(const DevSnap& s, const AdjX& x) {

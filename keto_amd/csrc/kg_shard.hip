@@ -405,7 +405,23 @@ __device__ __forceinline__ void shard_child(const DevSnap& s, const kg_frec& pr,
                                             bool pack = false) {
   const uint32_t child = ax.node;
   if (pr.depth >= 2) {
-    dest = s.nowner ? s.nowner[child] : 0u;
+    if (s.remote_meta) {
+      dest = (ax.begin & ADJX_REMOTE) ? (ax.begin & 0xFFu) : me;
+      if (dest != me && !s.relflags) {
+        // a remote child with its owner's row length and signature (remote_meta): the same decision
+        // as for a local one, taken here -- a record goes out only if the owner's checkDirect can hit
+        // (it probes) or the child can still expand; the rest never travel.  With a namespace
+        // program every child travels (the owner checks its relation for errors)
+        const bool may = pr.subj != NONE && sig_maybe(ax.lsig, ax.sig, subj_sig(pr.subj));
+        if (may || (adjx_len16(ax) && pr.depth >= 3)) {
+          c = kg_frec{pr.q, child, pr.subj, (pr.depth - 1) | (may ? 0 : D_NOPROBE)};
+          send = true;
+        }
+        return;
+      }
+    } else {
+      dest = s.nowner ? s.nowner[child] : 0u;
+    }
     if (dest == me && !s.relflags) {
       // a locally owned child without a namespace program: its checkDirect (depth - 2 >= 0) is
       // probed here, and a record goes out only if the child can still expand (a set row and
@@ -1051,6 +1067,64 @@ int shard_bad_nodes(Snapshot* s, uint64_t* count) {
   HIPC(hipStreamSynchronize(s->stream));
   HIPC(hipFree(d));
   *count = h;
+  return 0;
+}
+
+// Remote child metadata (DevSnap::remote_meta).  Per node, this rank's set-row length and check-row
+// signature in AdjX's lsig / sig layout: non-zero only for nodes this rank owns (a node's rows all sit
+// on its owner), so a max all-reduce over the ranks leaves every rank the owners' values.
+__global__ void k_shard_meta(DevSnap s, const uint64_t* __restrict__ coff, const uint32_t* __restrict__ csub,
+                             uint64_t* meta) {
+  for (uint64_t v = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; v < s.n_nodes;
+       v += (uint64_t)gridDim.x * blockDim.x) {
+    uint2 m = make_uint2(0u, 0u);
+    for (uint64_t i = coff[v], e = coff[v + 1]; i < e && (m.x != SIG_LO || m.y != 0xFFFFFFFFu); i++) {
+      const uint2 b = subj_sig(csub[i]);
+      m.x |= b.x;
+      m.y |= b.y;
+    }
+    const uint64_t len = s.adj_off[v + 1] - s.adj_off[v];
+    const uint32_t lsig = (uint32_t)min(len, (uint64_t)ADJX_LEN_SAT) | (m.x & SIG_LO);
+    meta[v] = (uint64_t)lsig | ((uint64_t)m.y << 32);
+  }
+}
+
+// Every local set edge to a child another rank owns: the owner in `begin` (ADJX_REMOTE | rank) and the
+// owner's row length and signature (all-reduced meta).  Local children keep their records.
+__global__ void k_shard_adjx_remote(DevSnap s, AdjX* adjx, uint64_t n_edges, const uint64_t* __restrict__ meta) {
+  for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < n_edges;
+       e += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t c = adjx[e].node;
+    const uint32_t o = s.nowner[c];
+    if (o != s.shard_rank) {
+      const uint64_t m = meta[c];
+      adjx[e] = AdjX{c, ADJX_REMOTE | o, (uint32_t)m, (uint32_t)(m >> 32)};
+    }
+  }
+}
+
+int shard_meta_local(Snapshot* s, uint64_t* d_meta, hipStream_t st) {
+  HIPC(hipSetDevice(s->device));
+  if (!s->ds.n_nodes) return 0;
+  const uint64_t* coff = s->ds.crow_off ? s->ds.crow_off : s->ds.row_off;
+  const uint32_t* csub = s->ds.crow_off ? s->ds.crow_subj : s->ds.row_subj;
+  hipLaunchKernelGGL(k_shard_meta, dim3((uint32_t)std::min<uint64_t>((s->ds.n_nodes + 255) / 256, 65536)), dim3(256),
+                     0, st, s->ds, coff, csub, d_meta);
+  HIPC(hipGetLastError());
+  return 0;
+}
+
+int shard_meta_apply(Snapshot* s, const uint64_t* d_meta, hipStream_t st) {
+  HIPC(hipSetDevice(s->device));
+  if (s->shard_n < 2 || !s->ds.nowner) return set_error(-2, "remote child metadata: not a hash-sharded snapshot");
+  if (s->n_set_edges >= ADJX_REMOTE) return 0;  // row begins need bit 31: keep the nowner reads
+  if (s->n_set_edges) {
+    hipLaunchKernelGGL(k_shard_adjx_remote, dim3(4096), dim3(256), 0, st, s->ds, const_cast<AdjX*>(s->ds.adjx),
+                       s->n_set_edges, d_meta);
+    HIPC(hipGetLastError());
+  }
+  HIPC(hipStreamSynchronize(st));
+  s->ds.remote_meta = 1;
   return 0;
 }
 

@@ -381,10 +381,29 @@ static int comm_setup(Snapshot* s, ShardComm* c) {
   if (int rc = shard_bad_nodes(s, &bad)) return rc;
   size_t words = 0;
   if (c->world > 1) words = ((size_t)s->ds.hbits_n + 31) / 32;
-  uint64_t v[2] = {bad, words};
-  if (int rc = h_allreduce_max(c, v, 2)) return rc;
+  // remote child metadata (DevSnap::remote_meta) runs when every rank wants it (not yet done, knob on)
+  // and every rank has the same node id space (node ids are global: kg_snapshot.hip create_from_tuples)
+  const uint64_t nn = s->ds.n_nodes;
+  uint64_t* dmeta = nullptr;  // allocated before the agreement: a rank without it makes every rank skip
+  if (c->world > 1 && !s->ds.remote_meta && s->shard_remote_meta && nn &&
+      hipMalloc((void**)&dmeta, nn * 8) != hipSuccess) {
+    (void)hipGetLastError();
+    dmeta = nullptr;
+  }
+  const uint64_t skip = dmeta ? 0 : 1;
+  uint64_t v[4] = {bad, words, nn, 0xFFFFFFFFull - nn};
+  v[3] |= skip << 40;
+  if (int rc = h_allreduce_max(c, v, 4)) {
+    hipFree(dmeta);
+    return rc;
+  }
   c->prune = v[0] == 0;
   words = (size_t)v[1];
+  const bool meta = !(v[3] >> 40) && v[2] == 0xFFFFFFFFull - (v[3] & 0xFFFFFFFFull);
+  if (!meta) {
+    hipFree(dmeta);
+    dmeta = nullptr;
+  }
   if (c->world > 1 && words) {
     uint32_t *mine = nullptr, *all = nullptr;
     HIPC(hipMalloc((void**)&mine, words * 4));
@@ -398,6 +417,20 @@ static int comm_setup(Snapshot* s, ShardComm* c) {
     }
     hipFree(mine);
     hipFree(all);
+    if (rc) {
+      hipFree(dmeta);
+      return rc;
+    }
+  }
+  if (dmeta) {
+    // one max all-reduce of 8 B per node: each node's (row length, signature) word is non-zero on its
+    // owner only.  A failed step leaves this rank on the nowner path: more records, the same answers
+    uint64_t* d = dmeta;
+    int rc = shard_meta_local(s, d, c->run);
+    if (!rc) rc = x_allreduce_max(c, reinterpret_cast<unsigned long long*>(d), nn);
+    if (!rc) rc = shard_meta_apply(s, d, c->run);  // synchronises
+    else (void)hipStreamSynchronize(c->run);
+    hipFree(d);
     if (rc) return rc;
   }
   return 0;

@@ -260,6 +260,7 @@ struct Snapshot {
   std::atomic<int> n_comms{0};  // comms.size(): the replicated path's lock-free "nothing bound" test
   int shard_force_exchange = 0;  // kg_snapshot_tune("shard_force_exchange"): one rank runs the N > 1 protocol
   int shard_local = 1;           // kg_snapshot_tune("shard_local"): one rank runs the replica tier chain
+  int shard_remote_meta = 1;     // kg_snapshot_tune("shard_remote_meta"): bind-time remote child metadata (DevSnap)
   uint32_t shard_max_reruns = 4;  // kg_snapshot_tune("shard_max_reruns"): overflow reruns per batch
   uint64_t shard_max_bytes = 0;   // kg_snapshot_tune("shard_max_bytes"): bucket buffers cap (0: 1/4 of free HBM)
   int shard_force_overflow = 0;   // kg_snapshot_tune("shard_force_overflow"): tests -- every run overflows
@@ -406,6 +407,10 @@ bool shard_escalates(const Snapshot* s);  // the escalation phases run (shard_bu
 int shard_refwd_seed(Snapshot* s, size_t n, const uint8_t* d_res, const uint32_t* d_err, kg_frec* d_out, size_t cap,
                      uint32_t* d_counts, hipStream_t stream);
 int shard_held(Snapshot* s, uint32_t* d_bits, size_t words, int import, hipStream_t stream);
+// remote child metadata (DevSnap::remote_meta): this rank's per-node (row length, signature) words,
+// then -- after the caller's max all-reduce -- the owners' values written into adjx
+int shard_meta_local(Snapshot* s, uint64_t* d_meta, hipStream_t st);
+int shard_meta_apply(Snapshot* s, const uint64_t* d_meta, hipStream_t st);
 int shard_finish(Snapshot* s, size_t n, uint8_t* d_res, uint32_t* d_err, hipStream_t stream);
 size_t shard_result_slots(const Snapshot* s, size_t n);
 size_t shard_slot_limit();  // result slots one sharded batch can address (query index bits of kg_frec.q)

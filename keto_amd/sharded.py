@@ -239,9 +239,12 @@ class GlooTransport:
     def _allreduce(self, ctx, buf, count, stream):
         try:
             a = np.ctypeslib.as_array(buf, shape=(count,))
-            t = self.torch.from_numpy(a.astype(np.int64))  # counts and flags < 2^63
+            # unsigned max as a signed one: flipping bit 63 maps u64 order onto i64 order (the remote
+            # child metadata words use all 64 bits)
+            top = np.uint64(1 << 63)
+            t = self.torch.from_numpy((a ^ top).view(np.int64).copy())
             self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX, group=self.group)
-            a[:] = t.numpy().astype(np.uint64)
+            a[:] = t.numpy().view(np.uint64) ^ top
             return 0
         except Exception as x:  # noqa: BLE001
             self.error = x

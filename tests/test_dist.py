@@ -60,3 +60,37 @@ def test_bench_spawns_ranks_without_launcher():
     line = json.loads(r.stdout.decode().strip().splitlines()[-1])
     assert line["n_gpus"] == 3 and line["config"]["parallelism"] == "replica3"
     assert line["units"] == 3 * 5 * 100
+
+
+def _max_worker(rank, world, port, q):
+    sys.path.insert(0, ROOT)
+    import ctypes
+    import numpy as np
+    import torch.distributed as dist
+    from keto_amd.sharded import GlooTransport
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    t = GlooTransport(dist, rank, world)
+    # the remote child metadata words use all 64 bits: one rank holds a value >= 2^63, the other 0
+    vals = [[0, 5, 1 << 63, (1 << 64) - 1], [(1 << 63) | 7, 3, 0, 1]][rank]
+    a = np.array(vals, dtype=np.uint64)
+    rc = t._allreduce(None, a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), len(vals), None)
+    q.put((rank, rc, [int(x) for x in a]))
+    dist.destroy_process_group()
+
+
+def test_gloo_transport_allreduce_is_unsigned_max():
+    """kg_shard_transport.allreduce_max_u64 is an unsigned max (include/ketogpu.h); the gloo transport
+    used to reduce as int64, which drops any word with bit 63 set."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_max_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(120)
+        assert p.exitcode == 0
+    want = [(1 << 63) | 7, 5, 1 << 63, (1 << 64) - 1]
+    assert sorted(q.get(timeout=10) for _ in range(2)) == [(0, 0, want), (1, 0, want)]
