@@ -282,7 +282,7 @@ __device__ __forceinline__ SeedQ seed_query(const DevSnap& s, const kg_query* __
   // node map (k_resolve's resolve_unheld order)
   const bool unheld = held && !s.relflags && sid &&
                       (subj == NONE || subj >= held_n || !((held[subj >> 5] >> (subj & 31)) & 1u));
-  uint32_t node = NONE, rsig_lo = 0xFFFFFFFFu, rsig = 0xFFFFFFFFu, rlen = 0;
+  uint32_t node = NONE, rsig_lo = 0xFFFFFFFFu, rsig = 0xFFFFFFFFu, rlen = 0, rbeg = 0;
   if (!unheld && nmap_key_ok(x.t.ns, x.t.rel, x.t.obj)) {
     const uint64_t key = nmap_key(x.t.ns, x.t.rel, x.t.obj);
     const NSlot* sl = nmap_slot(s, key, hash_home(key, s.nmap_n));
@@ -291,6 +291,7 @@ __device__ __forceinline__ SeedQ seed_query(const DevSnap& s, const kg_query* __
       rsig = sl->sig;
       rsig_lo = (uint32_t)sl->pad1;  // signature bits 0-11 in bits 20-31
       rlen = sl->len;
+      rbeg = sl->beg;
     }
   }
   if (!sid) {
@@ -328,9 +329,14 @@ __device__ __forceinline__ SeedQ seed_query(const DevSnap& s, const kg_query* __
     // an unknown subject can never be held, but with a namespace program the query can still
     // reach a rewrite (an error), so it is seeded all the same (its probes are skipped)
     o.act = true;
-    o.dest = s.nowner ? s.nowner[node] : 0u;
-    // signatures are built from this rank's rows: only a locally owned node's rules a probe out
-    const bool may = subj == NONE || o.dest != s.shard_rank || sig_maybe(rsig_lo, rsig, subj_sig(subj));
+    // remote_meta: the slot of a root another rank owns carries the owner and the owner's row length and
+    // signature (k_shard_nmap_remote), so it is judged like a local one: a record only if the owner's
+    // checkDirect can hit or the root can expand
+    const bool rmeta = s.remote_meta && (rbeg & ADJX_REMOTE) && !s.relflags;
+    o.dest = s.remote_meta ? ((rbeg & ADJX_REMOTE) ? (rbeg & 0xFFu) : s.shard_rank) : (s.nowner ? s.nowner[node] : 0u);
+    // otherwise signatures are built from this rank's rows: only a locally owned node's rules a probe out
+    const bool may = subj == NONE || (o.dest != s.shard_rank && !rmeta) || sig_maybe(rsig_lo, rsig, subj_sig(subj));
+    if (rmeta && subj != NONE && !may && (rlen == 0 || d < 2)) o.act = false;
     o.r = kg_frec{(s.shard_rank << Q_BITS) | i, node, subj, d | (may ? 0 : D_NOPROBE)};
     if (o.dest == s.shard_rank && !s.relflags) {
       // a locally owned root without a namespace program (as shard_child): checkDirect here, a
@@ -694,7 +700,8 @@ __global__ __launch_bounds__(256) void k_shard_refwd_seed(DevSnap s, uint32_t n,
 // forward phase's root probe.
 __global__ __launch_bounds__(256) void k_shard_back_seed(DevSnap s, const kg_frec* __restrict__ list, uint64_t m_bound,
                                                          const uint32_t* d_m, kg_frec* out, uint64_t cap,
-                                                         uint32_t* counts, uint32_t n_seg, uint64_t seg_cap) {
+                                                         uint32_t* counts, uint32_t n_seg, uint64_t seg_cap,
+                                                         uint32_t budget) {
   __shared__ uint32_t s_pref[256], s_wsum[4], s_first[256];
   __shared__ kg_frec s_rec[256];
   __shared__ uint64_t s_segpre[KG_SHARD_MAX_RANKS + 1];
@@ -703,6 +710,7 @@ __global__ __launch_bounds__(256) void k_shard_back_seed(DevSnap s, const kg_fre
   for (uint64_t base = (uint64_t)blockIdx.x * 256; base < m; base += (uint64_t)gridDim.x * 256) {
     const uint64_t i = base + tid;
     uint32_t cnt = 0, first = 0;
+    bool esc = false;
     kg_frec r{0, NONE, NONE, 0};
     if (i < m) {
       const kg_frec e = list[n_seg > 1 ? seg_src(s_segpre, n_seg, seg_cap, i) : i];
@@ -711,8 +719,16 @@ __global__ __launch_bounds__(256) void k_shard_back_seed(DevSnap s, const kg_fre
         first = h.x;
         cnt = h.y;
         r = kg_frec{e.q, NONE, e.node, e.depth - 1};  // subj carries the root from here on
+        // a subject held by more rows on this rank than the reverse-edge budget allows (a popular
+        // subject: its reverse search would start wider than the forward walk it replaces) goes
+        // straight to the final forward phase -- an ESC report to its home, through the all-gather
+        if (budget && cnt > budget) {
+          cnt = 0;
+          esc = true;
+        }
       }
     }
+    emit(esc, 0u, kg_frec{r.q, KG_FREC_ESC, 0u, 0}, out, cap, counts, 1u);
     s_first[tid] = first;
     s_rec[tid] = r;
     uint32_t v = cnt, x = v, total = 0, before = 0;
@@ -1103,6 +1119,23 @@ __global__ void k_shard_adjx_remote(DevSnap s, AdjX* adjx, uint64_t n_edges, con
   }
 }
 
+// The node-map slot of a node another rank owns, likewise (the seed's root): beg = ADJX_REMOTE | owner,
+// len and the signature words the owner's.  The slot's flags byte stays.
+__global__ void k_shard_nmap_remote(DevSnap s, NSlot* nm, uint64_t slots, const uint64_t* __restrict__ meta) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < slots; i += (uint64_t)gridDim.x * blockDim.x) {
+    if (nm[i].key == EMPTY64) continue;
+    const uint32_t v = nm[i].node;
+    const uint32_t o = s.nowner[v];
+    if (o == s.shard_rank) continue;
+    const uint64_t m = meta[v];
+    const uint32_t lsig = (uint32_t)m;
+    nm[i].beg = ADJX_REMOTE | o;
+    nm[i].len = lsig & ADJX_LEN_SAT;
+    nm[i].sig = (uint32_t)(m >> 32);
+    nm[i].pad1 = (nm[i].pad1 & 0xFFull) | (lsig & SIG_LO);
+  }
+}
+
 int shard_meta_local(Snapshot* s, uint64_t* d_meta, hipStream_t st) {
   HIPC(hipSetDevice(s->device));
   if (!s->ds.n_nodes) return 0;
@@ -1121,6 +1154,11 @@ int shard_meta_apply(Snapshot* s, const uint64_t* d_meta, hipStream_t st) {
   if (s->n_set_edges) {
     hipLaunchKernelGGL(k_shard_adjx_remote, dim3(4096), dim3(256), 0, st, s->ds, const_cast<AdjX*>(s->ds.adjx),
                        s->n_set_edges, d_meta);
+    HIPC(hipGetLastError());
+  }
+  if (s->ds.nmap_n) {
+    hipLaunchKernelGGL(k_shard_nmap_remote, dim3(4096), dim3(256), 0, st, s->ds, const_cast<NSlot*>(s->ds.nmap),
+                       s->ds.nmap_n, d_meta);
     HIPC(hipGetLastError());
   }
   HIPC(hipStreamSynchronize(st));
@@ -1381,7 +1419,7 @@ int shard_back_seed(Snapshot* s, const kg_frec* d_list, size_t m, const uint32_t
   if (m && s->ds.radj) {
     const uint32_t grid = (uint32_t)std::min<uint64_t>((m + 255) / 256, (uint64_t)s->n_cu * s->shard_wgs);
     hipLaunchKernelGGL(k_shard_back_seed, dim3(grid), dim3(256), 0, stream, s->ds, d_list, (uint64_t)m, d_m, d_out,
-                       (uint64_t)cap, d_counts, n_seg, (uint64_t)seg_cap);
+                       (uint64_t)cap, d_counts, n_seg, (uint64_t)seg_cap, s->shard_back_budget);
     HIPC(hipGetLastError());
   }
   return 0;
