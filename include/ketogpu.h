@@ -489,7 +489,12 @@ int kg_shard_bad_nodes(const kg_snapshot* s, uint64_t* count);
  * collectively with the id rank 0 got from kg_shard_unique_id (the host broadcasts the 128 bytes);
  * the snapshot must have been created for (rank, world) (kg_snapshot_create_shard / _synthetic_shard).
  * It also installs the OR of every rank's holder bitmap (kg_shard_held) and agrees whether any rank
- * can end a check in an error (kg_shard_bad_nodes). */
+ * can end a check in an error (kg_shard_bad_nodes).  Round 5: the first binding of a snapshot at
+ * world > 1 also writes the OWNER's set-row length and row signature of every remote child into this
+ * rank's adjacency records and node map (one max all-reduce of 8 B per node; kg_snapshot_tune
+ * "shard_remote_meta" 0 skips it), so a remote child that can neither hit nor expand is never sent
+ * and no per-edge owner lookup is made -- the same answers with fewer records (a transport's
+ * allreduce_max_u64 must compare all 64 bits unsigned). */
 #define KG_SHARD_UNIQUE_ID_BYTES 128
 int kg_shard_unique_id(void* id);
 int kg_shard_comm_init(kg_snapshot* s, const void* id, int rank, int world, void* stream);
