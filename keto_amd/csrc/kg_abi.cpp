@@ -402,6 +402,11 @@ int kg_snapshot_materialized(const kg_snapshot* sp, uint64_t* out3) {
 
 static int tune_one(Snapshot* s, const char* key, int64_t value) {
   std::lock_guard<std::mutex> lk(s->mu);
+  if (strcmp(key, "shard_vis_q") == 0) {
+    if (value < 0 || value > 256) return set_error(-2, "shard_vis_q must be in [0, 256]");
+    s->shard_vis_q = (uint32_t)value;
+    return 0;
+  }
   if (strcmp(key, "shard_vis") == 0) {
     if (value < 10 || value > 34) return set_error(-2, "shard_vis must be in [10, 34]");
     s->shard_vis_log2 = (int)value;

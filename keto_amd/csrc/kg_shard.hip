@@ -1170,10 +1170,18 @@ size_t shard_slot_limit() { return Q_MASK; }
 
 size_t shard_result_slots(const Snapshot* s, size_t n) { return s->n_fplans ? n * (2 + (size_t)s->fp_leaves) : n; }
 
-static int shard_vis_prepare(Snapshot* s, ShardCtx* c, hipStream_t stream) {
+static int shard_vis_prepare(Snapshot* s, ShardCtx* c, hipStream_t stream, size_t n) {
   // per-batch (query, node) table of 2^shard_vis_log2 slots (kg_snapshot_tune "shard_vis",
-  // default 2^23 = 64 MiB); an overflow is reported in the flags and the driver grows it
-  const uint64_t slots = 1ull << s->shard_vis_log2;
+  // default 2^23 = 64 MiB); an overflow is reported in the flags and the driver grows it.  At least
+  // shard_vis_q slots per query of the batch (kg_snapshot_tune "shard_vis_q"; 0: the fixed size): the
+  // table only grew on an overflow -- a probe chain past SV_PROBES -- so it ran nearly full, and each
+  // record's device-scope CAS walked a long chain
+  uint64_t slots = 1ull << s->shard_vis_log2;
+  if (s->shard_vis_q && n) {
+    uint64_t want = 1;
+    while (want < (uint64_t)n * s->shard_vis_q && want < (1ull << 34)) want <<= 1;
+    slots = std::max(slots, want);
+  }
   if (c->vis && c->vis_slots != slots) {
     HIPC(hipFree(c->vis));
     c->vis = nullptr;
@@ -1210,7 +1218,7 @@ int shard_seed(Snapshot* s, const kg_query* d_q, size_t n, int32_t gdepth, kg_fr
   if (!stream) stream = s->stream;
   ShardCtx* c = s->shard_ctx(stream);  // this stream's batch state (batches in flight on other streams)
   if (!c) return set_error(-4, "sharded batch state");
-  if (int rc = shard_vis_prepare(s, c, stream)) return rc;
+  if (int rc = shard_vis_prepare(s, c, stream, n)) return rc;
   HIPC(hipMemsetAsync(d_counts, 0, (s->shard_n + 1) * 4, stream));
   c->final = false;
   c->gdepth = gdepth;

@@ -269,6 +269,7 @@ struct Snapshot {
   uint32_t* shard_held = nullptr;  // holder bitmap OR-ed over every rank (kg_shard_held), or null
   uint32_t shard_held_n = 0;
   int shard_vis_log2 = 23;
+  uint32_t shard_vis_q = 0;  // kg_snapshot_tune("shard_vis_q"): visited-table slots per query of a batch (at least)
   uint32_t shard_bucket0 = 0;  // kg_snapshot_tune("shard_bucket"): first bucket size of new in-library bindings (0: by batch)
   uint32_t shard_wgs = 8;  // kg_snapshot_tune("shard_wgs"): k_shard_level workgroups per CU
   int shard_pack = 0;  // kg_snapshot_tune("shard_pack"): packed local records in kg_shard_levels (D_ROW; measured neutral)
