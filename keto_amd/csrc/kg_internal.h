@@ -165,7 +165,7 @@ struct DevSnap {
   uint32_t wildcard_rel;
   const uint64_t* adj_off;
   const uint32_t* adj;
-  const AdjX* adjx;  // parallel to adj
+  const AdjX* adjx;  // one record per set edge: parallel to adj, or laid out hot-first (adjx_off)
   const uint64_t* row_off;
   const uint32_t* row_subj;
   const uint64_t* crow_off;  // check rows (nullptr: row_off / row_subj)
@@ -203,6 +203,10 @@ struct DevSnap {
   // in lsig / sig (all-reduced at bind time), so the sender decides like for a local child -- no
   // nowner read per edge, and a remote child that can neither hit nor expand is never sent
   uint32_t remote_meta;
+  // adjx laid out hot-first (kg_snapshot.hip build_hash_tables): the adjx begin of every node's set
+  // row -- what nmap slots and adjx records carry; adj_off still gives lengths and the adj rows.
+  // nullptr: adjx is parallel to adj (begin = adj_off)
+  const uint32_t* adjx_off;
 };
 constexpr uint32_t ADJX_REMOTE = 0x80000000u;
 

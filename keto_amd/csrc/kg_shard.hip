@@ -578,6 +578,7 @@ __global__ __launch_bounds__(256) void k_shard_level(DevSnap s, const kg_frec* _
             s.dset + (want_p ? dset_home(dkey, s.dset_nb) : 0ull) * DSET_BUCKET);
         const uint32_t an = packed ? 0u : r.node;
         const uint64_t a0 = s.adj_off[an], a1 = s.adj_off[an + 1];
+        const uint64_t xb = s.adjx_off ? (uint64_t)s.adjx_off[an] : a0;  // the row's begin in adjx
         const uint64_t vkey = ((uint64_t)r.q << 32) | (packed ? (0x80000000u | r.node) : r.node);
         const int ins = lossy ? sv_insert_lossy(vis, vmask, vkey) : sv_insert(vis, vmask, vkey);
         // the flags word follows the (sub-)bucket counters: counts[out_sub] in the one-rank sub mode
@@ -596,7 +597,7 @@ __global__ __launch_bounds__(256) void k_shard_level(DevSnap s, const kg_frec* _
             // children at depth - 1 >= 1 can still be probed; children at depth 0 cannot, but
             // checkIsAllowed(child, 0) still evaluates astRelationFor (engine.go:199-206), so with a
             // namespace program their relation flags are checked (shard_child) for the error report
-            rb = packed ? (uint64_t)r.node : a0;
+            rb = packed ? (uint64_t)r.node : xb;
             len = packed ? (uint64_t)pk_len : a1 - a0;
             if (len && budget) {  // escalation: this rank's set-edge count of the query passes the budget
               const uint32_t add = (uint32_t)min(len, (uint64_t)budget);

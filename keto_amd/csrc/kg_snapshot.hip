@@ -54,7 +54,7 @@ __global__ void k_dset_insert_rows(uint64_t* dset, uint64_t nb, const uint64_t* 
 }
 
 __global__ void k_nmap_insert(NSlot* nm, uint64_t slots, const uint32_t* nd_ns, const uint32_t* nd_obj,
-                              const uint32_t* nd_rel, const uint64_t* adj_off, const uint2* sig,
+                              const uint32_t* nd_rel, const uint64_t* adj_off, const uint32_t* xoff, const uint2* sig,
                               const uint8_t* flags, uint32_t n_nodes) {
   uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
   if (v >= n_nodes) return;
@@ -65,7 +65,7 @@ __global__ void k_nmap_insert(NSlot* nm, uint64_t slots, const uint32_t* nd_ns, 
         atomicCAS((unsigned long long*)&nm[i].key, (unsigned long long)EMPTY64, (unsigned long long)key);
     if (old == EMPTY64 || old == key) {
       nm[i].node = v;
-      nm[i].beg = (uint32_t)adj_off[v];
+      nm[i].beg = xoff ? xoff[v] : (uint32_t)adj_off[v];
       nm[i].len = (uint32_t)(adj_off[v + 1] - adj_off[v]);
       const uint2 g = sig[v];
       nm[i].sig = g.y;
@@ -104,6 +104,42 @@ __global__ void k_build_adjx(const uint32_t* adj, const uint64_t* adj_off, const
     const uint64_t b = adj_off[c], x = adj_off[c + 1];
     const uint2 g = sig[c];
     adjx[e] = AdjX{c, (uint32_t)b, (uint32_t)std::min<uint64_t>(x - b, ADJX_LEN_SAT) | (g.x & SIG_LO), g.y};
+  }
+}
+
+// Hot-first adjx (round 5): the set rows are laid out in descending in-degree order of their nodes, so
+// the rows a query batch keeps re-reading -- the popular groups every walk runs into -- share 128-B
+// lines and stay in L2 / the Infinity Cache instead of sitting one per line among cold rows.  Node ids
+// do not change; xoff[v] is v's row begin in adjx (nmap slots and adjx records carry it).
+__global__ void k_hot_keys(const unsigned long long* indeg, uint32_t n, uint32_t* keys, uint32_t* vals) {
+  for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < n; v += gridDim.x * blockDim.x) {
+    const unsigned long long d = indeg[v];
+    keys[v] = ~(uint32_t)(d < 0xFFFFFFFFull ? d : 0xFFFFFFFFull);  // ascending sort = descending in-degree
+    vals[v] = v;
+  }
+}
+__global__ void k_hot_lens(const uint32_t* order, const uint64_t* adj_off, uint32_t n, uint64_t* len) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint32_t v = order[i];
+    len[i] = adj_off[v + 1] - adj_off[v];
+  }
+}
+__global__ void k_hot_scatter(const uint32_t* order, const uint64_t* pos, uint32_t n, uint32_t* xoff) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+    xoff[order[i]] = (uint32_t)pos[i];
+}
+// One thread per node: its row's records at xoff[u] (long rows are build-time only)
+__global__ void k_build_adjx_hot(const uint32_t* adj, const uint64_t* adj_off, const uint32_t* xoff, const uint2* sig,
+                                 uint32_t n, AdjX* adjx) {
+  for (uint32_t u = blockIdx.x * blockDim.x + threadIdx.x; u < n; u += gridDim.x * blockDim.x) {
+    const uint64_t b0 = adj_off[u], b1 = adj_off[u + 1];
+    AdjX* out = adjx + xoff[u];
+    for (uint64_t e = b0; e < b1; e++) {
+      const uint32_t c = adj[e];
+      const uint64_t l = adj_off[c + 1] - adj_off[c];
+      const uint2 g = sig[c];
+      out[e - b0] = AdjX{c, xoff[c], (uint32_t)std::min<uint64_t>(l, ADJX_LEN_SAT) | (g.x & SIG_LO), g.y};
+    }
   }
 }
 
@@ -471,11 +507,52 @@ int Snapshot::build_hash_tables() {
     hipLaunchKernelGGL(k_node_sig, dim3((ds.n_nodes + 255) / 256), dim3(256), 0, stream, coff, csub, ds.n_nodes, sig);
     HIPC(hipGetLastError());
   }
-  if (n_set_edges) {
+  // hot-first layout unless KG_ADJX_ORDER=0 (node order, adjx parallel to adj)
+  const char* order_env = getenv("KG_ADJX_ORDER");
+  const bool hot = n_set_edges && ds.n_nodes && !(order_env && atoi(order_env) == 0);
+  uint32_t* xoff = nullptr;
+  if (hot) {
+    const uint32_t nn = ds.n_nodes;
+    if (alloc((void**)&xoff, ((size_t)nn + 1) * 4)) return -1;
+    unsigned long long* indeg = nullptr;
+    uint32_t *k0, *k1, *v0, *v1;
+    uint64_t *len, *pos;
+    HIPC(hipMalloc(&indeg, (size_t)nn * 8));
+    HIPC(hipMalloc(&k0, (size_t)nn * 4));
+    HIPC(hipMalloc(&k1, (size_t)nn * 4));
+    HIPC(hipMalloc(&v0, (size_t)nn * 4));
+    HIPC(hipMalloc(&v1, (size_t)nn * 4));
+    HIPC(hipMemsetAsync(indeg, 0, (size_t)nn * 8, stream));
+    hipLaunchKernelGGL(k_indeg, dim3(4096), dim3(256), 0, stream, ds.adj, n_set_edges, indeg);
+    hipLaunchKernelGGL(k_hot_keys, dim3(4096), dim3(256), 0, stream, indeg, nn, k0, v0);
+    HIPC(hipGetLastError());
+    hipcub::DoubleBuffer<uint32_t> kb(k0, k1), vb(v0, v1);
+    size_t tmp_bytes = 0;
+    HIPC(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, kb, vb, (size_t)nn, 0, 32, stream));
+    void* tmp = nullptr;
+    size_t scan_bytes = 0;
+    HIPC(hipFree(indeg));  // reuse its bytes: lengths and positions in sorted order (u64 each)
+    HIPC(hipMalloc(&len, ((size_t)nn + 1) * 8));
+    HIPC(hipMalloc(&pos, ((size_t)nn + 1) * 8));
+    HIPC(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, len, pos, (size_t)nn, stream));
+    HIPC(hipMalloc(&tmp, std::max(tmp_bytes, scan_bytes) + 16));
+    HIPC(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, kb, vb, (size_t)nn, 0, 32, stream));
+    hipLaunchKernelGGL(k_hot_lens, dim3(4096), dim3(256), 0, stream, vb.Current(), ds.adj_off, nn, len);
+    HIPC(hipGetLastError());
+    HIPC(hipcub::DeviceScan::ExclusiveSum(tmp, scan_bytes, len, pos, (size_t)nn, stream));
+    hipLaunchKernelGGL(k_hot_scatter, dim3(4096), dim3(256), 0, stream, vb.Current(), pos, nn, xoff);
+    HIPC(hipGetLastError());
+    HIPC(hipMemsetAsync(xoff + nn, 0, 4, stream));
+    hipLaunchKernelGGL(k_build_adjx_hot, dim3(4096), dim3(256), 0, stream, ds.adj, ds.adj_off, xoff, sig, nn, adjx);
+    HIPC(hipGetLastError());
+    HIPC(hipStreamSynchronize(stream));
+    for (void* p : {(void*)k0, (void*)k1, (void*)v0, (void*)v1, (void*)len, (void*)pos, tmp}) HIPC(hipFree(p));
+  } else if (n_set_edges) {
     hipLaunchKernelGGL(k_build_adjx, dim3(2048), dim3(256), 0, stream, ds.adj, ds.adj_off, sig, n_set_edges, adjx);
     HIPC(hipGetLastError());
   }
   ds.adjx = adjx;
+  ds.adjx_off = xoff;
   const uint64_t n_rows = n_check_rows;
   // load <= 0.25 keys per slot: a miss (the common probe) reads one bucket with probability ~0.9.
   // A table that would take more than a fifth of the device's HBM runs at 0.375 instead (and the
@@ -504,7 +581,7 @@ int Snapshot::build_hash_tables() {
                          stream, dset, buckets, coff, csub, ds.n_nodes, n_rows);
     HIPC(hipGetLastError());
     hipLaunchKernelGGL(k_nmap_insert, dim3(grid), dim3(256), 0, stream, nm, slots, ds.nd_ns, ds.nd_obj,
-                       ds.nd_rel, ds.adj_off, sig, ds.nflags, ds.n_nodes);
+                       ds.nd_rel, ds.adj_off, xoff, sig, ds.nflags, ds.n_nodes);
     HIPC(hipGetLastError());
   }
   HIPC(hipStreamSynchronize(stream));
@@ -853,6 +930,7 @@ int Snapshot::create_synthetic(const kg_synth_params* p, const kg_rewrite_prog* 
   if (!synth_make_layout(L, T, p->seed, p->n_layers, p->max_degree, p->set_fraction, p->doc_set_fraction, p->preset,
                          p->doc_alpha, p->group_alpha))
     return set_error(-2, "synthetic graph too large");
+  if (const char* e = getenv("KG_SYNTH_IDENTITY")) L.pick_identity = atoi(e) ? 1u : 0u;  // experiment only
   synth = L;
   is_synth = true;
   wildcard_rel = 0;

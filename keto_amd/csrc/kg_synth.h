@@ -45,6 +45,9 @@ struct SynthLayout {
   SynthBlock b[SYNTH_MAX_BLOCKS];
   // ids (interned by keto_amd.synth in this order)
   uint32_t ns_doc, ns_group, ns_user, ns_folder;
+  // experiment (env KG_SYNTH_IDENTITY=1, kg_snapshot.hip): popularity rank r IS the id -- hot groups and
+  // users at the front of their ranges, the layout an in-degree relabelling of the snapshot would give
+  uint32_t pick_identity;
   uint32_t rel_viewer, rel_member, rel_editor, rel_owner, rel_parents, rel_blocked, rel_view, rel_edit, rel_share;
 };
 
@@ -53,11 +56,11 @@ __host__ __device__ __forceinline__ uint64_t shash(uint64_t seed, uint64_t a, ui
   return mix64(seed ^ mix64(a * 0x9E3779B97F4A7C15ull + b * 0xD1B54A32D192ED03ull + 0x632BE59BD9B4E019ull));
 }
 // log-uniform rank (Zipf(~1) popularity) mapped through an affine permutation of [0, n)
-__host__ __device__ __forceinline__ uint32_t synth_pick(uint64_t h, uint32_t n) {
+__host__ __device__ __forceinline__ uint32_t synth_pick(uint64_t h, uint32_t n, uint32_t identity = 0) {
   double u = u01(h);
   uint64_t r = (uint64_t)floor(exp(u * log((double)n + 1.0))) - 1;
   if (r >= n) r = n - 1;
-  return (uint32_t)((r * 2654435761ull + 12345ull) % n);
+  return identity ? (uint32_t)r : (uint32_t)((r * 2654435761ull + 12345ull) % n);
 }
 
 __host__ __device__ __forceinline__ int synth_block_of(const SynthLayout& L, uint32_t v) {
@@ -90,14 +93,14 @@ __host__ __device__ __forceinline__ uint32_t synth_subject(const SynthLayout& L,
   if (B.set_kind != SK_NONE && u01(h1) < B.p_set) {
     switch (B.set_kind) {
       case SK_GROUP_LAYER:
-        return SET_BIT | (L.group_node0 + B.set_arg * L.group_per_layer + synth_pick(h2, L.group_per_layer));
+        return SET_BIT | (L.group_node0 + B.set_arg * L.group_per_layer + synth_pick(h2, L.group_per_layer, L.pick_identity));
       case SK_FOLDER_ANY:
         return SET_BIT | (L.folder_any_node0 + (uint32_t)(h2 % L.n_folders));
       case SK_FOLDER_PARENT:  // 4-ary forest: folder i's parent is (i-1)/4
         return SET_BIT | (L.folder_any_node0 + (v - B.node0 - 1) / 4);
     }
   }
-  return L.user_obj0 + synth_pick(h2, L.n_users);
+  return L.user_obj0 + synth_pick(h2, L.n_users, L.pick_identity);
 }
 
 __host__ __device__ __forceinline__ void synth_node(const SynthLayout& L, uint32_t v, uint32_t& ns, uint32_t& obj,
