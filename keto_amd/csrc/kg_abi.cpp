@@ -402,6 +402,11 @@ int kg_snapshot_materialized(const kg_snapshot* sp, uint64_t* out3) {
 
 static int tune_one(Snapshot* s, const char* key, int64_t value) {
   std::lock_guard<std::mutex> lk(s->mu);
+  if (strcmp(key, "shard_level_occ") == 0) {
+    if (value != 0 && value != 6 && value != 8) return set_error(-2, "shard_level_occ must be 0, 6 or 8");
+    s->shard_level_occ = (int)value;
+    return 0;
+  }
   if (strcmp(key, "shard_vis_q") == 0) {
     if (value < 0 || value > 256) return set_error(-2, "shard_vis_q must be in [0, 256]");
     s->shard_vis_q = (uint32_t)value;

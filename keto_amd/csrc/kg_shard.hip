@@ -524,7 +524,10 @@ __device__ __forceinline__ uint64_t seg_src(const uint64_t* s_segpre, uint32_t n
 // in-workgroup expansion overlaps other workgroups' record processing, profiles/r2s8_*.)
 // Segmented input (n_seg > 1): the receive buffer of a fixed-split all-to-all -- segment k holds
 // d_n_in[k] records (clamped to seg_cap) from in[k * seg_cap]; the level walks their concatenation.
-__global__ __launch_bounds__(256) void k_shard_level(DevSnap s, const kg_frec* __restrict__ in, uint64_t n_bound,
+// MINW: minimum waves per SIMD the compiler must allow (kg_snapshot_tune "shard_level_occ"): 1 lets it
+// take 82 VGPRs (5 waves per SIMD), 6 fits 78, 8 fits 64 with a small spill
+template <int MINW>
+__global__ __launch_bounds__(256, MINW) void k_shard_level(DevSnap s, const kg_frec* __restrict__ in, uint64_t n_bound,
                                                      const uint32_t* d_n_in, kg_frec* out, uint64_t cap, uint32_t* counts, uint8_t* res,
                                                      uint32_t* err, uint64_t* vis, uint64_t vmask,
                                                      const uint32_t* __restrict__ done, uint32_t done_wpr,
@@ -1261,6 +1264,15 @@ unsigned long long* shard_heavy_head(Snapshot* s, hipStream_t stream) {
   return c ? (unsigned long long*)heavy_list(c).pk : nullptr;
 }
 
+#define KG_SHARD_LEVEL_LAUNCH(OCC, ...)                                        \
+  do {                                                                         \
+    switch (OCC) {                                                             \
+      case 8: hipLaunchKernelGGL(k_shard_level<8>, __VA_ARGS__); break;        \
+      case 6: hipLaunchKernelGGL(k_shard_level<6>, __VA_ARGS__); break;        \
+      default: hipLaunchKernelGGL(k_shard_level<1>, __VA_ARGS__); break;       \
+    }                                                                          \
+  } while (0)
+
 int shard_level(Snapshot* s, const kg_frec* d_in, size_t n_in, const uint32_t* d_n_in, kg_frec* d_out, size_t cap,
                 uint32_t* d_counts, uint8_t* d_res, uint32_t* d_err, const uint32_t* d_done, uint32_t done_words,
                 hipStream_t stream, uint32_t n_seg, size_t seg_cap, bool prezeroed) {
@@ -1276,14 +1288,18 @@ int shard_level(Snapshot* s, const kg_frec* d_in, size_t n_in, const uint32_t* d
     const HeavyList heavy = heavy_list(c);
     if (!prezeroed) HIPC(hipMemsetAsync(heavy.pk, 0, 8, stream));
     const uint32_t grid = (uint32_t)std::min<uint64_t>((n_in + 255) / 256, (uint64_t)s->n_cu * s->shard_wgs);
-    hipLaunchKernelGGL(k_shard_level, dim3(grid), dim3(256), 0, stream, s->ds, d_in, (uint64_t)n_in, d_n_in, d_out,
+    // packed local records (kg_snapshot_tune "shard_pack"), as the one-rank loop: a locally owned child
+    // travels with its adjx row instead of its node id, so its level reads no adj_off pair
+    const uint32_t budget = shard_escalates(s) && c->qcnt && !c->final ? s->shard_budget : 0u;
+    const uint32_t pack = (s->shard_pack && !s->ds.relflags && !s->ds.nflags && budget == 0 &&
+                           s->ds.n_nodes < 0x80000000u && c->gdepth > 0 && c->gdepth < 256) ? 1u : 0u;
+    KG_SHARD_LEVEL_LAUNCH(s->shard_level_occ, dim3(grid), dim3(256), 0, stream, s->ds, d_in, (uint64_t)n_in, d_n_in, d_out,
                        (uint64_t)cap, d_counts, d_res, d_err, (uint64_t*)c->vis, c->vis_slots - 1,
                        d_done, d_done ? done_words : 0u, heavy, (uint32_t*)c->qcnt,
-                       shard_escalates(s) && c->qcnt && !c->final ? s->shard_budget : 0u,
-                       s->shard_vis_mode ? 1u : 0u, n_seg, (uint64_t)seg_cap, s->shard_heavy, 1u, 0u, 0u);
+                       budget, s->shard_vis_mode ? 1u : 0u, n_seg, (uint64_t)seg_cap, s->shard_heavy, 1u, pack, 0u);
     HIPC(hipGetLastError());
     hipLaunchKernelGGL(k_shard_heavy, dim3((uint32_t)s->n_cu * 4), dim3(256), 0, stream, s->ds, heavy, d_out,
-                       (uint64_t)cap, d_counts, d_res, d_err, s->shard_n, 1u, 0u, nullptr, 0u, nullptr, nullptr);
+                       (uint64_t)cap, d_counts, d_res, d_err, s->shard_n, 1u, pack, nullptr, 0u, nullptr, nullptr);
     HIPC(hipGetLastError());
   }
   return 0;
@@ -1347,7 +1363,7 @@ int shard_levels(Snapshot* s, int levels, kg_frec* d_buf[2], size_t cap, uint32_
       HIPC(hipGetLastError());
     }
     const bool seg_in = k > 0;
-    hipLaunchKernelGGL(k_shard_level, dim3(grid), dim3(256), 0, stream, s->ds, d_buf[cur], (uint64_t)cap,
+    KG_SHARD_LEVEL_LAUNCH(s->shard_level_occ, dim3(grid), dim3(256), 0, stream, s->ds, d_buf[cur], (uint64_t)cap,
                        seg_in ? sub[cur] : d_counts[cur], d_buf[nx], seg, sub[nx], d_res, d_err, (uint64_t*)c->vis,
                        c->vis_slots - 1, k > 0 && !direct ? (const uint32_t*)c->bits : nullptr, direct ? 0u : w, hk,
                        (uint32_t*)c->qcnt, budget, s->shard_vis_mode ? 1u : 0u, seg_in ? SUB : 1u,

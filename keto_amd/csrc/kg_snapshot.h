@@ -271,6 +271,7 @@ struct Snapshot {
   int shard_vis_log2 = 23;
   uint32_t shard_vis_q = 0;  // kg_snapshot_tune("shard_vis_q"): visited-table slots per query of a batch (at least)
   uint32_t shard_bucket0 = 0;  // kg_snapshot_tune("shard_bucket"): first bucket size of new in-library bindings (0: by batch)
+  int shard_level_occ = 0;  // kg_snapshot_tune("shard_level_occ"): k_shard_level built for 0 (compiler's choice), 6 or 8 waves per SIMD
   uint32_t shard_wgs = 8;  // kg_snapshot_tune("shard_wgs"): k_shard_level workgroups per CU
   int shard_pack = 0;  // kg_snapshot_tune("shard_pack"): packed local records in kg_shard_levels (D_ROW; measured neutral)
   uint32_t shard_heavy = 64;  // kg_snapshot_tune("shard_heavy"): set rows longer than this go to k_shard_heavy (r3p A/B)

@@ -80,7 +80,7 @@ def main():
 
     # library defaults to restore (the knobs these A/Bs touch)
     defaults.update({"shard_budget": 0, "shard_back_budget": 1 << 14, "shard_vis_mode": 0, "shard_heavy": 64,
-                     "shard_wgs": 8, "shard_vis": 23, "shard_local": 1})
+                     "shard_wgs": 8, "shard_vis": 23, "shard_local": 1, "shard_level_occ": 0, "shard_pack": 0})
     for rnd in range(x.rounds):
         for cfg in x.configs:
             el, st = run(cfg)
