@@ -215,6 +215,35 @@ def test_synthetic_graph_vs_oracle(n_tuples, gmax, ecap, unheld):
     assert (dfs == exp).all()
 
 
+@pytest.mark.parametrize("ecap", [512, 32])
+def test_adjx_layouts_vs_oracle(ecap, monkeypatch):
+    """The snapshot's adjx in node order (KG_ADJX_ORDER=0: parallel to adj) and hot-first (the default,
+    round 5: rows in descending in-degree order, begins from DevSnap::adjx_off): the same answers, equal
+    to the oracle's -- through the stream tier and, at ecap 32, the backward and grid tiers that follow
+    adjx records and node-map row begins too."""
+    torch = _torch()
+    from keto_amd import _lib
+    n, gmax = 20000, 10
+    outs = []
+    for order in ("0", "1"):
+        monkeypatch.setenv("KG_ADJX_ORDER", order)  # read when the snapshot builds its hash tables
+        snap = Snapshot.synthetic(300_000, seed=20250131)
+        snap.tune("stream_ecap", ecap)
+        dq = torch.empty((n, 7), dtype=torch.int32, device="cuda")
+        _lib.check(_lib.load().kg_synth_queries(snap.handle, 11, n, dq.data_ptr()), "kg_synth_queries")
+        q = dq.cpu().numpy().view(np.uint32)
+        out, err = Engine(snap, Config(gmax)).batch_check_ids(q)
+        assert (err == 0).all()
+        outs.append(out)
+        if order == "1":
+            exp, _, _ = Oracle(snap.export(), 0).check_batch(q[:, :6], q[:, 6].view(np.int32), gmax, POLICY_CANONICAL,
+                                                              nthreads=8)
+            assert (out == exp).all(), np.nonzero(out != exp)[0][:10]
+        snap.close()
+    assert (outs[0] == outs[1]).all()
+    assert 0.05 < outs[1].mean() < 0.95
+
+
 @pytest.mark.parametrize("stream_wgs,grid_wgs", [(1, 1), (3, 8)])
 def test_occupancy_knobs_vs_oracle(stream_wgs, grid_wgs):
     """k_stream4 / k_grid_level workgroups per CU (defaults 2 / 2): fewer or more waves draining the

@@ -753,6 +753,60 @@ def test_sharded_visited_overflow_reruns(world, backend, vis, bucket):
     _run_synth(world, backend, 150_000, 6000, 10, preset=1, vis=vis, bucket=bucket, driver=driver)
 
 
+def _meta_worker(rank, world, port, outq, n_tuples, n_q, gmax):
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+    from keto_amd import _lib
+    from keto_amd.engine import Snapshot
+    torch.cuda.set_device(0)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    out = {}
+    for meta in (1, 0):
+        snap = Snapshot.synthetic(n_tuples, seed=20250131, shard=(rank, world))
+        snap.tune("shard_remote_meta", meta)  # read when the transport binds (collective)
+        dq = torch.empty((n_q, 7), dtype=torch.int32, device="cuda")
+        _lib.check(_lib.load().kg_synth_queries(snap.handle, 31, n_q, dq.data_ptr()), "kg_synth_queries")
+        mine = np.array_split(np.arange(n_q), world)[rank]
+        chk = _checker("lib", snap, rank, world, dist)
+        r, e = chk.check(dq[mine[0]:mine[-1] + 1].contiguous(), gmax)
+        st = chk.chk.stats()
+        out[meta] = (r.cpu().numpy(), e.cpu().numpy(), st["records_sent"], st["records_to_peers"])
+        chk.chk.close()
+        snap.close()
+    outq.put((rank, out))
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_sharded_remote_meta_same_answers_fewer_records():
+    """Remote child metadata (round 5, kg_shard_comm.hip comm_setup): the first binding all-reduces every
+    owner's (set-row length, row signature) word into the other ranks' adjacency records and node map,
+    so a remote child that can neither hit nor expand is never sent.  Two ranks on one GPU over gloo,
+    C4's generator: the same answers and error codes with the metadata on and off (the oracle check of
+    this configuration is test_sharded_in_library_vs_oracle[2-gloo-0-lib]), and fewer records sent and
+    fewer crossing to the other rank with it on."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    world = 2
+    ctx = mp.get_context("spawn")
+    outq = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_meta_worker, args=(r, world, port, outq, 300_000, 20_000, 10)) for r in range(world)]
+    for p in ps:
+        p.start()
+    got = [outq.get(timeout=110) for _ in range(world)]
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    for rank, out in got:
+        (r1, e1, sent1, peers1), (r0, e0, sent0, peers0) = out[1], out[0]
+        assert (r1 == r0).all() and (e1 == e0).all(), rank
+        assert (e1 == 0).all() and 0.05 < r1.mean() < 0.95
+        assert sent1 < sent0 and peers1 < peers0, (rank, sent1, sent0, peers1, peers0)
+
+
 def _bound_worker(rank, world, port, outq, driver, mode):
     sys.path.insert(0, ROOT)
     import torch.distributed as dist
