@@ -194,7 +194,9 @@ class Snapshot:
         grid_ms_tg_cap, grid_ms_cap, interp_wgs, interp_cap2, device_sync, host_sync, max_lanes;
         expand -- expand_tail; hash-sharded -- shard_local, shard_force_exchange, shard_max_reruns,
         shard_max_bytes, shard_force_overflow (tests), shard_bucket, shard_vis, shard_vis_mode, shard_wgs,
-        shard_heavy, shard_pack, shard_budget, shard_back_budget."""
+        shard_heavy, shard_pack, shard_budget, shard_back_budget, shard_remote_meta (read at the first binding),
+        shard_vis_q, shard_level_occ; plus stream_gate, expand_gw.  Build-time, from the environment:
+        KG_ADJX_ORDER=0 lays adjx out in node order instead of hot-first."""
         _lib.check(_lib.load().kg_snapshot_tune(self._h, key.encode(), int(value)), "kg_snapshot_tune")
         self.__dict__.setdefault("tuned", {})[key] = int(value)  # what the Python drivers need to know
 
