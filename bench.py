@@ -99,6 +99,10 @@ def parse(argv=None):
                     help="kg_snapshot_tune shard_vis: log2 of the sharded mode's (query, node) visited table (0: library default)")
     ap.add_argument("--shard-vis-mode", type=int, default=0,
                     help="kg_snapshot_tune shard_vis_mode (sharded (query, node) dedup: 0 exact CAS table, 1 lossy cache)")
+    ap.add_argument("--packed", type=int, default=0,
+                    help="check mode: the headline's queries as 16-B kg_query_packed in HBM through "
+                         "kg_check_batch_packed_device (k_resolve reads them itself) instead of 28-B kg_query "
+                         "through kg_check_batch_device")
     ap.add_argument("--shard-remote-meta", type=int, default=1,
                     help="kg_snapshot_tune shard_remote_meta (N > 1: owners' row length + signature of remote "
                          "children in adjx at bind time, so remote leaves that cannot hit are never sent)")
@@ -847,6 +851,24 @@ def bench_host(a):
 ROWS_PER_T = {(0, False): 0.94513, (1, False): 1.3400, (0, True): 119.92, (1, True): 119.92}
 
 
+def pack_queries_device(dq):
+    """kg_pack_query (include/ketogpu.h) over an (n, 7) int32 kg_query tensor on the device: (n, 4) int32
+    kg_query_packed rows (the bit layout of keto_amd._lib.pack_queries, which tests pin to the header)."""
+    import torch
+    q = dq.to(torch.int64) & 0xFFFFFFFF
+    ns, obj, rel, sns, sobj, srel, d = (q[:, j] for j in range(7))
+    sid = sns == 0xFFFFFFFF
+    assert bool((ns <= 4094).all()) and bool((rel <= 4094).all()) and bool(((sns <= 4094) | sid).all()), \
+        "ids do not fit kg_query_packed"
+    snsp = torch.where(sid, torch.full_like(sns, 4095), sns)
+    srelp = torch.where(sid, torch.zeros_like(srel), srel)
+    dd = torch.where(d >= 0x80000000, torch.zeros_like(d), d).clamp(0, 65535)  # a negative depth is 0
+    w2 = ns | (rel << 12) | ((snsp & 0xFF) << 24)
+    w3 = (snsp >> 8) | (srelp << 4) | (dd << 16)
+    out = torch.stack([obj, sobj, w2, w3], 1)
+    return torch.where(out >= 0x80000000, out - (1 << 32), out).to(torch.int32).contiguous()
+
+
 def build_synthetic(a, target_rows: float, **kw):
     """Snapshot.synthetic sized so that it holds at least `target_rows` rows: the generator's size
     parameter is the row target over the measured rows-per-parameter ratio (+0.2 %), and a build that
@@ -1030,13 +1052,16 @@ def main():
     derrs = [torch.empty(B, dtype=torch.int32, device=dev) for _ in range(P)]
     dq = dq_all[warm % n_distinct]
     timed_out = torch.empty((a.steps, B), dtype=torch.uint8, device=dev)
+    # --packed: the same queries as 16-B kg_query_packed rows (kg_pack_query, on the device)
+    dp_all = torch.stack([pack_queries_device(dq_all[k]) for k in range(n_distinct)]) if a.packed else None
+    check_fn = L.kg_check_batch_packed_device if a.packed else L.kg_check_batch_device
+    qbatch = (lambda k: dp_all[k % n_distinct]) if a.packed else (lambda k: dq_all[k % n_distinct])
 
     def step(p, k, st=None):
         o = timed_out[k - warm] if k >= warm else douts[p]  # every timed batch keeps its own results
-        rc = L.kg_check_batch_device(snap.handle, dq_all[k % n_distinct].data_ptr(), B, a.global_depth, o.data_ptr(),
-                                     derrs[p].data_ptr(), C.byref(st) if st is not None else None,
-                                     C.c_void_p(streams[p].cuda_stream))
-        _lib.check(rc, "kg_check_batch_device")
+        rc = check_fn(snap.handle, qbatch(k).data_ptr(), B, a.global_depth, o.data_ptr(),
+                      derrs[p].data_ptr(), C.byref(st) if st is not None else None, C.c_void_p(streams[p].cuda_stream))
+        _lib.check(rc, "kg_check_batch_packed_device" if a.packed else "kg_check_batch_device")
 
     def run_steps(k0, K, stats=None, lat=None):
         """Starts P host threads that run steps k0 .. k0+K-1 round-robin over the P streams once `go` is set."""
@@ -1110,6 +1135,8 @@ def main():
         for k in range(n_ld):
             _lib.check(L.kg_synth_queries(snap.handle, 500000 + rank + 7919 * k, B, dq_lat[k].data_ptr()),
                        "kg_synth_queries")
+        if a.packed:
+            dq_lat = torch.stack([pack_queries_device(dq_lat[k]) for k in range(n_ld)])
         lat = [0.0] * lat_n
         errors = []
 
@@ -1118,9 +1145,9 @@ def main():
                 st = _lib.kg_stats()
                 for k in range(p, lat_n, P):
                     s0 = time.perf_counter()
-                    _lib.check(L.kg_check_batch_device(snap.handle, dq_lat[k % n_ld].data_ptr(), B, a.global_depth,
-                                                       douts[p].data_ptr(), derrs[p].data_ptr(), C.byref(st),
-                                                       C.c_void_p(streams[p].cuda_stream)), "kg_check_batch_device")
+                    _lib.check(check_fn(snap.handle, dq_lat[k % n_ld].data_ptr(), B, a.global_depth,
+                                        douts[p].data_ptr(), derrs[p].data_ptr(), C.byref(st),
+                                        C.c_void_p(streams[p].cuda_stream)), "check (latency phase)")
                     lat[k] = time.perf_counter() - s0  # a batch with stats returns once its results are in
             except Exception as e:  # noqa: BLE001
                 errors.append(e)
@@ -1159,7 +1186,7 @@ def main():
                    "tuples": info["rows"], "tuples_target": a.tuples, "generator_size_param": size_param,
                    "nodes": info["nodes"], "set_edges": info["set_edges"],
                    "batch_per_gpu": B, "global_max_read_depth": a.global_depth, "parallelism": f"replica{world}",
-                   "inflight_per_gpu": P, "device_gb": info["device_bytes"] / 1e9,
+                   "inflight_per_gpu": P, "queries": ("16-B kg_query_packed, kg_check_batch_packed_device" if a.packed else "28-B kg_query, kg_check_batch_device"), "device_gb": info["device_bytes"] / 1e9,
                    "hbm_free_gb_after_build": free_after_build / 1e9,
                    "materialized": snap.materialized(), "tune": dict(snap.__dict__.get("tuned", {}))},
         "gteps": edges / elapsed / 1e9,

@@ -324,6 +324,13 @@ int kg_check_batch_packed(kg_snapshot* s, const kg_query_packed* q, size_t n, in
  * stream are serialised.  kg_check_batch uses the snapshot's own stream. */
 int kg_check_batch_device(kg_snapshot* s, const kg_query* d_q, size_t n, int32_t global_max_depth,
                           uint8_t* d_out, uint32_t* d_err, kg_stats* stats, void* stream);
+/* kg_check_batch_device with 16-B packed queries in HBM (round 5): without a namespace program the
+ * request-mapping kernel reads them itself (16 B per check instead of 28: the batch's only coalesced
+ * stream of the first tier); with one they are unpacked on the device first.  Same answers, error
+ * codes, streams and waiting as kg_check_batch_device; on a hash-sharded snapshot the call unpacks
+ * into a buffer of its own and completes before it returns. */
+int kg_check_batch_packed_device(kg_snapshot* s, const kg_query_packed* d_q, size_t n, int32_t global_max_depth,
+                                 uint8_t* d_out, uint32_t* d_err, kg_stats* stats, void* stream);
 /* Device-side synthetic check batch for a synthetic snapshot: 50% positive (reverse walks) and
  * 50% uniform doc#viewer@user queries, max_depth in {0,1..10}.  d_q is a device buffer. */
 int kg_synth_queries(kg_snapshot* s, uint64_t seed, size_t n, kg_query* d_q);

@@ -103,7 +103,7 @@ class kg_synth_params(C.Structure):
 EXPORTS = ["kg_snapshot_create", "kg_snapshot_create_on", "kg_snapshot_synthetic", "kg_snapshot_synthetic_on",
            "kg_snapshot_replicas", "kg_snapshot_destroy", "kg_snapshot_info", "kg_snapshot_materialized", "kg_snapshot_tune", "kg_synth_ids",
            "kg_snapshot_create_ordered", "kg_snapshot_apply",
-           "kg_snapshot_export", "kg_snapshot_rows", "kg_snapshot_export_csr", "kg_check_batch", "kg_check_batch_device", "kg_synth_queries", "kg_expand_batch",
+           "kg_snapshot_export", "kg_snapshot_rows", "kg_snapshot_export_csr", "kg_check_batch", "kg_check_batch_device", "kg_check_batch_packed_device", "kg_synth_queries", "kg_expand_batch",
            "kg_tree_free", "kg_last_error", "kg_version", "kg_check_batch_packed", "kg_shard_owner", "kg_snapshot_create_shard",
            "kg_snapshot_synthetic_shard", "kg_shard_seed", "kg_shard_level", "kg_shard_level_seg", "kg_shard_finish",
            "kg_shard_done", "kg_shard_levels", "kg_shard_back_list", "kg_shard_back_seed", "kg_shard_back_level", "kg_shard_refwd_seed",
@@ -117,35 +117,6 @@ ALLTOALL2_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size
                            C.c_void_p)
 ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p)
 ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_uint64), C.c_size_t, C.c_void_p)
-
-
-KG_PACK_ID_MAX = 4094
-KG_PACK_SUBJECT_ID = 4095
-
-
-def pack_queries(q: "np.ndarray") -> "np.ndarray":
-    """kg_pack_query (include/ketogpu.h) over an (n, 7) uint32 kg_query array: (n, 4) uint32 kg_query_packed
-    rows.  Raises ValueError when an id does not fit (namespace / relation ids <= KG_PACK_ID_MAX)."""
-    import numpy as np
-    q = np.ascontiguousarray(q, dtype=np.uint32).reshape(-1, 7)
-    sid = q[:, 3] == 0xFFFFFFFF
-    sns = np.where(sid, KG_PACK_SUBJECT_ID, q[:, 3]).astype(np.uint64)
-    srel = np.where(sid, 0, q[:, 5]).astype(np.uint64)
-    d = q[:, 6].view(np.int32).astype(np.int64)
-    d = np.clip(d, 0, 65535).astype(np.uint64)
-    if (q[:, 0] > KG_PACK_ID_MAX).any() or (q[:, 2] > KG_PACK_ID_MAX).any() or \
-            ((sns > KG_PACK_ID_MAX) & ~sid).any() or (srel > KG_PACK_ID_MAX).any():
-        raise ValueError("an id does not fit kg_query_packed (use kg_check_batch)")
-    out = np.empty((len(q), 4), np.uint32)
-    out[:, 0] = q[:, 1]
-    out[:, 1] = q[:, 4]
-    out[:, 2] = (q[:, 0].astype(np.uint64) | (q[:, 2].astype(np.uint64) << 12) | ((sns & 0xFF) << 24)).astype(np.uint32)
-    out[:, 3] = ((sns >> 8) | (srel << 4) | (d << 16)).astype(np.uint32)
-    return out
-
-
-class kg_tuple(C.Structure):
-    _fields_ = [(k, C.c_uint32) for k in ("ns", "obj", "rel", "sns", "sobj", "srel")]
 
 
 class kg_check_node(C.Structure):
@@ -207,6 +178,7 @@ def load(path: str = LIB_PATH):
     L.kg_check_batch.argtypes = [vp, vp, sz, i32, vp, vp, C.POINTER(kg_stats)]
     L.kg_check_batch_device.argtypes = [vp, vp, sz, i32, vp, vp, C.POINTER(kg_stats), vp]
     L.kg_check_batch_packed.argtypes = [vp, vp, sz, i32, vp, vp, vp, sz, C.POINTER(sz), C.POINTER(kg_stats)]
+    L.kg_check_batch_packed_device.argtypes = [vp, vp, sz, i32, vp, vp, C.POINTER(kg_stats), vp]
     L.kg_synth_queries.argtypes = [vp, u64, sz, vp]
     L.kg_expand_batch.argtypes = [vp, vp, sz, i32, C.POINTER(kg_tree_buf)]
     L.kg_tree_free.argtypes = [C.POINTER(kg_tree_buf)]
@@ -256,7 +228,8 @@ def load(path: str = LIB_PATH):
     for name in ("kg_snapshot_create", "kg_snapshot_create_on", "kg_snapshot_synthetic", "kg_snapshot_synthetic_on",
                  "kg_snapshot_replicas", "kg_snapshot_info", "kg_snapshot_materialized", "kg_snapshot_tune",
                  "kg_snapshot_create_ordered", "kg_snapshot_apply", "kg_synth_ids", "kg_check_batch", "kg_check_batch_packed",
-                 "kg_check_batch_device", "kg_synth_queries", "kg_expand_batch", "kg_snapshot_create_shard",
+                 "kg_check_batch_device", "kg_check_batch_packed_device", "kg_synth_queries", "kg_expand_batch",
+                 "kg_snapshot_create_shard",
                  "kg_snapshot_synthetic_shard", "kg_shard_seed", "kg_shard_level", "kg_shard_level_seg", "kg_shard_finish",
                  "kg_shard_done", "kg_shard_levels", "kg_shard_back_list", "kg_shard_back_seed", "kg_shard_back_level", "kg_shard_refwd_seed",
                  "kg_shard_held_words", "kg_shard_held", "kg_batcher_create", "kg_batcher_check", "kg_batcher_stats",

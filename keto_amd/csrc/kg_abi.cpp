@@ -690,6 +690,31 @@ int kg_check_batch_device(kg_snapshot* sp, const kg_query* d_q, size_t n, int32_
   KG_GUARD_END
 }
 
+int kg_check_batch_packed_device(kg_snapshot* sp, const kg_query_packed* d_q, size_t n, int32_t global_max_depth,
+                                 uint8_t* d_out, uint32_t* d_err, kg_stats* stats, void* stream) {
+  KG_GUARD_BEGIN
+  if (!sp) return set_error(-2, "NULL snapshot");
+  if (n && !d_q) return set_error(-2, "d_q is NULL");
+  Snapshot* s = reinterpret_cast<Snapshot*>(sp);
+  if (s->shard_n > 1 || kg::shard_comm_of(s, (hipStream_t)stream)) {
+    // hash-sharded: the seed reads kg_query records -- unpacked into a buffer of this call, then the
+    // usual sharded batch (completed before the buffer is freed)
+    HIPC(hipSetDevice(s->device));
+    hipStream_t st = stream ? (hipStream_t)stream : s->stream;
+    kg_query* dq = nullptr;
+    if (n) HIPC(hipMalloc(&dq, n * sizeof(kg_query)));
+    int rc = n ? kg::unpack_queries(d_q, n, dq, st) : 0;
+    if (!rc) rc = kg_check_batch_device(sp, dq, n, global_max_depth, d_out, d_err, stats, stream);
+    if (hipStreamSynchronize(st) != hipSuccess && !rc) rc = set_error(-1, "packed sharded batch");
+    hipFree(dq);
+    return rc;
+  }
+  kg::Workspace* w = s->workspace((hipStream_t)stream);
+  std::lock_guard<std::mutex> lk(w->mu);
+  return kg::check_batch_device(s, w, nullptr, n, global_max_depth, d_out, d_err, stats, d_q);
+  KG_GUARD_END
+}
+
 // A checked-out lane set goes back to the snapshot's pool when the call returns (any path).
 struct LaneLease {
   Snapshot* s;

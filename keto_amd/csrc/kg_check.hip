@@ -159,7 +159,23 @@ __device__ __forceinline__ kg_query ld_once_q(const kg_query* p) {
 // Light-routed queries go to the stream tier as LQuery records in 8 shards of lq_cap entries (shard
 // blockIdx & 7) and skip rq[i]; only queries that later tiers read by index (GENERAL) are written to
 // rq (the stream tier writes the RQuery of a query it hands on).
-__global__ __launch_bounds__(256) void k_resolve(DevSnap s, const kg_query* __restrict__ q, uint32_t n,
+// kg_query_packed (include/ketogpu.h) -> kg_query, in registers
+__device__ __forceinline__ kg_query unpack_query(const uint4 v) {
+  const uint32_t sns = (v.z >> 24) | ((v.w & 0xFu) << 8);
+  kg_query x;
+  x.t.ns = v.z & 0xFFFu;
+  x.t.obj = v.x;
+  x.t.rel = (v.z >> 12) & 0xFFFu;
+  x.t.sns = sns == KG_PACK_SUBJECT_ID ? KG_SUBJECT_ID : sns;
+  x.t.sobj = v.y;
+  x.t.srel = (v.w >> 4) & 0xFFFu;
+  x.max_depth = (int32_t)(v.w >> 16);
+  return x;
+}
+
+// pq != nullptr: the batch's queries are packed (16 B each, kg_check_batch_packed_device) and q is unused
+__global__ __launch_bounds__(256) void k_resolve(DevSnap s, const kg_query* __restrict__ q, const uint4* __restrict__ pq,
+                                                 uint32_t n,
                                                  uint32_t n_base, const uint32_t* __restrict__ n_extra,
                                                  int32_t global, RQuery* __restrict__ rq, uint8_t* __restrict__ out,
                                                  uint32_t* __restrict__ err, uint32_t* gen_list,
@@ -171,7 +187,7 @@ __global__ __launch_bounds__(256) void k_resolve(DevSnap s, const kg_query* __re
   bool did_probe = false, no_holder = false;
   LQuery lq{};
   if (valid) {
-    kg_query x = ld_once_q(q + i);
+    kg_query x = pq ? unpack_query(pq[i]) : ld_once_q(q + i);
     // node map and (for a subject id) holder hash: the first slots of both are loaded together,
     // so the common case is one round trip for both lookups
     const bool key_ok = nmap_key_ok(x.t.ns, x.t.rel, x.t.obj);
@@ -855,7 +871,8 @@ static size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 // and returns without waiting; check_batch_end waits for the stream, finishes the grid tier if its
 // first round overflowed (rare: a rerun with fewer slots) and fills the statistics.
 int check_batch_begin(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n, int32_t global_max_depth,
-                      uint8_t* d_out, uint32_t* d_err, kg_stats* stats, BatchPending* bp) {
+                      uint8_t* d_out, uint32_t* d_err, kg_stats* stats, BatchPending* bp,
+                      const kg_query_packed* d_pk) {
   *bp = BatchPending{};
   bp->stats = stats;
   bp->d_out = d_out;
@@ -864,6 +881,26 @@ int check_batch_begin(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n, 
   if (n > 0x7FFFFFFFull) return set_error(-2, "batch too large");
   HIPC(hipSetDevice(s->device));
   hipStream_t stream = w->stream;
+  // packed queries: k_resolve unpacks them in registers when it is the only reader of the queries --
+  // without a namespace program there is no formula split and no general route; otherwise they are
+  // unpacked into the workspace first
+  const uint4* pq = nullptr;
+  if (d_pk && n) {
+    if (s->n_fplans || s->ds.relflags || s->ds.nflags) {
+      if (n > w->unpacked_n) {
+        if (w->unpacked) hipFree(w->unpacked);
+        w->unpacked = nullptr;
+        w->unpacked_n = 0;
+        HIPC(hipMalloc(&w->unpacked, n * sizeof(kg_query)));
+        w->unpacked_n = n;
+      }
+      if (int rc = unpack_queries(d_pk, n, w->unpacked, stream)) return rc;
+      d_q = w->unpacked;
+    } else {
+      pq = reinterpret_cast<const uint4*>(d_pk);
+      d_q = nullptr;
+    }
+  }
   // boolean rewrites over rewrite-free leaves (kg_formula.hip): the batch runs as the originals plus
   // their leaf sub-checks; check_batch_end combines the leaves into the requested results
   const uint32_t* n_extra = nullptr;
@@ -932,7 +969,7 @@ int check_batch_begin(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n, 
   if (n) {
     const bool use_back = s->back_tier && s->ds.radj;
     const uint32_t nblk = (uint32_t)((n + 255) / 256);
-    hipLaunchKernelGGL(k_resolve, dim3(nblk), dim3(256), 0, stream, s->ds, d_q, (uint32_t)n, (uint32_t)n_base, n_extra,
+    hipLaunchKernelGGL(k_resolve, dim3(nblk), dim3(256), 0, stream, s->ds, d_q, pq, (uint32_t)n, (uint32_t)n_base, n_extra,
                        global_max_depth, rq, d_out, d_err, gen, use_back ? (s->resolve_unheld == 2 ? 3 : s->resolve_unheld ? 2 : 1) : 0, ctl, lq,
                        lq_cap);
     HIPC(hipGetLastError());
@@ -1094,9 +1131,9 @@ int check_batch_end(Snapshot* s, Workspace* w, BatchPending* bp, bool* reran, bo
 }
 
 int check_batch_device(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n, int32_t global_max_depth,
-                       uint8_t* d_out, uint32_t* d_err, kg_stats* stats) {
+                       uint8_t* d_out, uint32_t* d_err, kg_stats* stats, const kg_query_packed* d_pk) {
   BatchPending bp;
-  if (int rc = check_batch_begin(s, w, d_q, n, global_max_depth, d_out, d_err, stats, &bp)) return rc;
+  if (int rc = check_batch_begin(s, w, d_q, n, global_max_depth, d_out, d_err, stats, &bp, d_pk)) return rc;
   return check_batch_end(s, w, &bp, nullptr, s->device_sync != 0);
 }
 
@@ -1105,17 +1142,7 @@ int check_batch_device(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n,
 __global__ __launch_bounds__(256) void k_unpack(const uint4* __restrict__ pk, uint32_t n, kg_query* __restrict__ q) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const uint4 v = pk[i];
-  const uint32_t sns = (v.z >> 24) | ((v.w & 0xFu) << 8);
-  kg_query x;
-  x.t.ns = v.z & 0xFFFu;
-  x.t.obj = v.x;
-  x.t.rel = (v.z >> 12) & 0xFFFu;
-  x.t.sns = sns == KG_PACK_SUBJECT_ID ? KG_SUBJECT_ID : sns;
-  x.t.sobj = v.y;
-  x.t.srel = (v.w >> 4) & 0xFFFu;
-  x.max_depth = (int32_t)(v.w >> 16);
-  q[i] = x;
+  q[i] = unpack_query(pk[i]);
 }
 
 // The checks answered KG_ERROR as (base + index, code) pairs after a count word: list[0] = count,

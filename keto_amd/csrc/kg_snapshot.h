@@ -62,6 +62,8 @@ struct Workspace {
   hipEvent_t sync_ev = nullptr;  // blocking-sync event (host-buffer batches wait on it asleep)
   int wait(hipStream_t st, bool blocking);  // waits for st: spin (hipStreamSynchronize) or asleep
   void* pinned = nullptr;  // 64 KiB of pinned host memory for small device->host readbacks
+  kg_query* unpacked = nullptr;  // packed device batches that need the original queries (a program)
+  size_t unpacked_n = 0;
   void* host_buf(size_t bytes);
   ~Workspace();
 };
@@ -365,10 +367,13 @@ struct Snapshot {
 };
 
 // kg_check.hip
+// d_pk (packed queries, d_q unused): read by k_resolve itself when nothing else of the batch needs the
+// original queries (no namespace program), else unpacked into the workspace first
 int check_batch_device(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n, int32_t global_max_depth,
-                       uint8_t* d_out, uint32_t* d_err, kg_stats* stats);
+                       uint8_t* d_out, uint32_t* d_err, kg_stats* stats, const kg_query_packed* d_pk = nullptr);
 int check_batch_begin(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n, int32_t global_max_depth,
-                      uint8_t* d_out, uint32_t* d_err, kg_stats* stats, BatchPending* bp);
+                      uint8_t* d_out, uint32_t* d_err, kg_stats* stats, BatchPending* bp,
+                      const kg_query_packed* d_pk = nullptr);
 int check_batch_end(Snapshot* s, Workspace* w, BatchPending* bp, bool* reran, bool blocking = false);
 int synth_queries(Snapshot* s, uint64_t seed, size_t n, kg_query* d_q);
 // kg_check_batch_packed: packed queries -> kg_query on the device; the KG_ERROR answers of [0, n) as

@@ -323,6 +323,7 @@ Workspace::~Workspace() {
   ms.release();
   if (interp_pool) hipFree(interp_pool);
   if (split) hipFree(split);
+  if (unpacked) hipFree(unpacked);
   if (pinned) hipHostFree(pinned);
   for (auto& e : ev)
     if (e) hipEventDestroy(e);

@@ -458,6 +458,41 @@ def test_random_rewrites_vs_oracle(seed, unions, mat, monkeypatch):
         assert m["union_nodes"] > 0, m
 
 
+@pytest.mark.parametrize("preset", [0, 1])
+def test_packed_device_vs_device(preset):
+    """kg_check_batch_packed_device (round 5: 16-B queries in HBM): without a namespace program (C2's
+    generator) k_resolve reads the packed rows itself; with one (C3's OPL program: formula split, union
+    nodes) they are unpacked on the device first.  Answers and error codes equal kg_check_batch_device's
+    on the same queries, and the oracle's."""
+    torch = _torch()
+    import sys
+    import os
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    from keto_amd import _lib
+    L = _lib.load()
+    n, gmax = 20000, 10
+    snap = Snapshot.synthetic(300_000 if preset == 0 else 150_000, seed=20250131, preset=preset)
+    dq = torch.empty((n, 7), dtype=torch.int32, device="cuda")
+    _lib.check(L.kg_synth_queries(snap.handle, 13, n, dq.data_ptr()), "kg_synth_queries")
+    dp = bench.pack_queries_device(dq)
+    o1 = torch.empty(n, dtype=torch.uint8, device="cuda")
+    e1 = torch.empty(n, dtype=torch.int32, device="cuda")
+    o2, e2 = torch.empty_like(o1), torch.empty_like(e1)
+    _lib.check(L.kg_check_batch_device(snap.handle, dq.data_ptr(), n, gmax, o1.data_ptr(), e1.data_ptr(), None, None),
+               "kg_check_batch_device")
+    _lib.check(L.kg_check_batch_packed_device(snap.handle, dp.data_ptr(), n, gmax, o2.data_ptr(), e2.data_ptr(), None,
+                                              None), "kg_check_batch_packed_device")
+    torch.cuda.synchronize()
+    a, b = o1.cpu().numpy(), o2.cpu().numpy()
+    assert (a == b).all() and (e1.cpu().numpy() == e2.cpu().numpy()).all()
+    q = dq.cpu().numpy().view(np.uint32)
+    exp, oerr, _ = Oracle(snap.export(), 0, snap.program if preset else None).check_batch(
+        q[:, :6], q[:, 6].view(np.int32), gmax, POLICY_CANONICAL, nthreads=8)
+    assert (b == exp).all() and (oerr == 0).all()
+    assert 0.05 < b.mean() < 0.95
+
+
 @pytest.mark.parametrize("seed", [0, 5])
 def test_packed_boundary_vs_oracle(seed):
     """kg_check_batch_packed (16-B packed queries in, answers as bytes, error codes as

@@ -183,3 +183,27 @@ def test_pack_queries_matches_header(tmp_path):
     bad[0, 0] = 5000
     with pytest.raises(ValueError):
         _lib.pack_queries(bad)
+
+
+def test_bench_device_packer_matches_pack_queries():
+    """bench.py packs the headline's device-resident queries with torch ops (pack_queries_device); they
+    must be the header's kg_pack_query rows bit for bit, as keto_amd._lib.pack_queries is (pinned above):
+    subject ids and subject sets, depths below 0, inside 1..65535 and above it."""
+    import sys
+    import torch
+    sys.path.insert(0, ROOT)
+    import bench
+    from keto_amd import _lib
+    rng = np.random.default_rng(11)
+    n = 20000
+    q = np.zeros((n, 7), np.uint32)
+    q[:, 0] = rng.integers(0, 4095, n)
+    q[:, 1] = rng.integers(0, 2 ** 31 - 1, n)
+    q[:, 2] = rng.integers(0, 4095, n)
+    sid = rng.random(n) < 0.5
+    q[:, 3] = np.where(sid, 0xFFFFFFFF, rng.integers(0, 4095, n))
+    q[:, 4] = rng.integers(0, 2 ** 31 - 1, n)
+    q[:, 5] = rng.integers(0, 4095, n)
+    q[:, 6] = rng.integers(-5, 70000, n).astype(np.int32).view(np.uint32)
+    got = bench.pack_queries_device(torch.from_numpy(q.view(np.int32))).numpy().view(np.uint32)
+    assert (got == _lib.pack_queries(q)).all()
