@@ -102,9 +102,8 @@ def parse(argv=None):
     ap.add_argument("--packed", type=int, default=0,
                     help="check mode: the headline's queries as 16-B kg_query_packed in HBM through "
                          "kg_check_batch_packed_device (k_resolve reads them itself) instead of 28-B kg_query "
-                         "through kg_check_batch_device.  Off: the packing's copies before the clock shift "
-                         "which HIP hardware queues the in-flight streams get, two of them share one and the "
-                         "line measures that, not the path (DESIGN.md 5d)")
+                         "through kg_check_batch_device (packed by the library on the snapshot's stream, "
+                         "DESIGN.md 5d)")
     ap.add_argument("--shard-remote-meta", type=int, default=1,
                     help="kg_snapshot_tune shard_remote_meta (N > 1: owners' row length + signature of remote "
                          "children in adjx at bind time, so remote leaves that cannot hit are never sent)")
@@ -1057,10 +1056,13 @@ def main():
     # --packed: the same queries as 16-B kg_query_packed rows (kg_pack_query, on the device)
     dp_all = None
     if a.packed:
+        # packed by the library on the snapshot's own stream (kg_synth_queries' stream): no torch kernel or
+        # copy touches a stream before the in-flight streams' first batches, which would shift the HIP
+        # hardware queues they are bound to at their first launch
         dp_all = torch.empty((n_distinct, B, 4), dtype=torch.int32, device=dev)
-        for k in range(n_distinct):  # packed on the host (kg_pack_query's numpy twin), before the clock
-            dp_all[k].copy_(torch.from_numpy(_lib.pack_queries(dq_all[k].cpu().numpy().view(np.uint32)).view(np.int32)))
-        torch.cuda.synchronize()
+        for k in range(n_distinct):
+            _lib.check(L.kg_pack_queries_device(snap.handle, dq_all[k].data_ptr(), B, dp_all[k].data_ptr(), None),
+                       "kg_pack_queries_device")
     check_fn = L.kg_check_batch_packed_device if a.packed else L.kg_check_batch_device
     qbatch = (lambda k: dp_all[k % n_distinct]) if a.packed else (lambda k: dq_all[k % n_distinct])
 
@@ -1143,8 +1145,11 @@ def main():
             _lib.check(L.kg_synth_queries(snap.handle, 500000 + rank + 7919 * k, B, dq_lat[k].data_ptr()),
                        "kg_synth_queries")
         if a.packed:
-            dq_lat = torch.from_numpy(np.stack([_lib.pack_queries(dq_lat[k].cpu().numpy().view(np.uint32)).view(np.int32)
-                                                for k in range(n_ld)])).to(dev)
+            dp_lat = torch.empty((n_ld, B, 4), dtype=torch.int32, device=dev)
+            for k in range(n_ld):
+                _lib.check(L.kg_pack_queries_device(snap.handle, dq_lat[k].data_ptr(), B, dp_lat[k].data_ptr(), None),
+                           "kg_pack_queries_device")
+            dq_lat = dp_lat
         lat = [0.0] * lat_n
         errors = []
 

@@ -331,6 +331,9 @@ int kg_check_batch_device(kg_snapshot* s, const kg_query* d_q, size_t n, int32_t
  * into a buffer of its own and completes before it returns. */
 int kg_check_batch_packed_device(kg_snapshot* s, const kg_query_packed* d_q, size_t n, int32_t global_max_depth,
                                  uint8_t* d_out, uint32_t* d_err, kg_stats* stats, void* stream);
+/* kg_pack_query over device-resident queries (d_q[n] -> d_pk[n]) on `stream` (NULL: the snapshot's);
+ * returns once done, -2 when an id does not fit. */
+int kg_pack_queries_device(kg_snapshot* s, const kg_query* d_q, size_t n, kg_query_packed* d_pk, void* stream);
 /* Device-side synthetic check batch for a synthetic snapshot: 50% positive (reverse walks) and
  * 50% uniform doc#viewer@user queries, max_depth in {0,1..10}.  d_q is a device buffer. */
 int kg_synth_queries(kg_snapshot* s, uint64_t seed, size_t n, kg_query* d_q);

@@ -103,8 +103,8 @@ class kg_synth_params(C.Structure):
 EXPORTS = ["kg_snapshot_create", "kg_snapshot_create_on", "kg_snapshot_synthetic", "kg_snapshot_synthetic_on",
            "kg_snapshot_replicas", "kg_snapshot_destroy", "kg_snapshot_info", "kg_snapshot_materialized", "kg_snapshot_tune", "kg_synth_ids",
            "kg_snapshot_create_ordered", "kg_snapshot_apply",
-           "kg_snapshot_export", "kg_snapshot_rows", "kg_snapshot_export_csr", "kg_check_batch", "kg_check_batch_device", "kg_check_batch_packed_device", "kg_synth_queries", "kg_expand_batch",
-           "kg_tree_free", "kg_last_error", "kg_version", "kg_check_batch_packed", "kg_shard_owner", "kg_snapshot_create_shard",
+           "kg_snapshot_export", "kg_snapshot_rows", "kg_snapshot_export_csr", "kg_check_batch", "kg_check_batch_device", "kg_check_batch_packed_device", "kg_pack_queries_device", "kg_synth_queries",
+           "kg_expand_batch", "kg_tree_free", "kg_last_error", "kg_version", "kg_check_batch_packed", "kg_shard_owner", "kg_snapshot_create_shard",
            "kg_snapshot_synthetic_shard", "kg_shard_seed", "kg_shard_level", "kg_shard_level_seg", "kg_shard_finish",
            "kg_shard_done", "kg_shard_levels", "kg_shard_back_list", "kg_shard_back_seed", "kg_shard_back_level", "kg_shard_refwd_seed",
            "kg_shard_held_words", "kg_shard_held", "kg_shard_result_slots", "kg_shard_bad_nodes", "kg_batcher_create", "kg_batcher_check", "kg_batcher_stats", "kg_batcher_reset_stats", "kg_batcher_destroy",
@@ -179,6 +179,7 @@ def load(path: str = LIB_PATH):
     L.kg_check_batch_device.argtypes = [vp, vp, sz, i32, vp, vp, C.POINTER(kg_stats), vp]
     L.kg_check_batch_packed.argtypes = [vp, vp, sz, i32, vp, vp, vp, sz, C.POINTER(sz), C.POINTER(kg_stats)]
     L.kg_check_batch_packed_device.argtypes = [vp, vp, sz, i32, vp, vp, C.POINTER(kg_stats), vp]
+    L.kg_pack_queries_device.argtypes = [vp, vp, sz, vp, vp]
     L.kg_synth_queries.argtypes = [vp, u64, sz, vp]
     L.kg_expand_batch.argtypes = [vp, vp, sz, i32, C.POINTER(kg_tree_buf)]
     L.kg_tree_free.argtypes = [C.POINTER(kg_tree_buf)]
@@ -228,8 +229,8 @@ def load(path: str = LIB_PATH):
     for name in ("kg_snapshot_create", "kg_snapshot_create_on", "kg_snapshot_synthetic", "kg_snapshot_synthetic_on",
                  "kg_snapshot_replicas", "kg_snapshot_info", "kg_snapshot_materialized", "kg_snapshot_tune",
                  "kg_snapshot_create_ordered", "kg_snapshot_apply", "kg_synth_ids", "kg_check_batch", "kg_check_batch_packed",
-                 "kg_check_batch_device", "kg_check_batch_packed_device", "kg_synth_queries", "kg_expand_batch",
-                 "kg_snapshot_create_shard",
+                 "kg_check_batch_device", "kg_check_batch_packed_device", "kg_pack_queries_device", "kg_synth_queries",
+                 "kg_expand_batch", "kg_snapshot_create_shard",
                  "kg_snapshot_synthetic_shard", "kg_shard_seed", "kg_shard_level", "kg_shard_level_seg", "kg_shard_finish",
                  "kg_shard_done", "kg_shard_levels", "kg_shard_back_list", "kg_shard_back_seed", "kg_shard_back_level", "kg_shard_refwd_seed",
                  "kg_shard_held_words", "kg_shard_held", "kg_batcher_create", "kg_batcher_check", "kg_batcher_stats",

@@ -715,6 +715,28 @@ int kg_check_batch_packed_device(kg_snapshot* sp, const kg_query_packed* d_q, si
   KG_GUARD_END
 }
 
+int kg_pack_queries_device(kg_snapshot* sp, const kg_query* d_q, size_t n, kg_query_packed* d_pk, void* stream) {
+  KG_GUARD_BEGIN
+  if (!sp) return set_error(-2, "NULL snapshot");
+  if (n && (!d_q || !d_pk)) return set_error(-2, "NULL buffer");
+  if (n > 0x7FFFFFFFull) return set_error(-2, "batch too large");
+  Snapshot* s = reinterpret_cast<Snapshot*>(sp);
+  HIPC(hipSetDevice(s->device));
+  hipStream_t st = stream ? (hipStream_t)stream : s->stream;
+  uint32_t* d_bad = nullptr;
+  HIPC(hipMalloc(&d_bad, 4));
+  uint32_t bad = 0;
+  int rc = hipMemsetAsync(d_bad, 0, 4, st) != hipSuccess ? set_error(-1, "pack: memset") : 0;
+  if (!rc) rc = kg::pack_queries(d_q, n, d_pk, d_bad, st);
+  if (!rc && (hipMemcpyAsync(&bad, d_bad, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+              hipStreamSynchronize(st) != hipSuccess))
+    rc = set_error(-1, "pack: readback");
+  hipFree(d_bad);
+  if (!rc && bad) rc = set_error(-2, "an id does not fit kg_query_packed (use kg_check_batch_device)");
+  return rc;
+  KG_GUARD_END
+}
+
 // A checked-out lane set goes back to the snapshot's pool when the call returns (any path).
 struct LaneLease {
   Snapshot* s;

@@ -1163,6 +1163,31 @@ __global__ __launch_bounds__(256) void k_err_list(const uint8_t* __restrict__ ou
   }
 }
 
+// kg_pack_query on the device (kg_pack_queries_device): 28-B load, 16-B store per thread; an id that
+// does not fit sets *bad
+__global__ __launch_bounds__(256) void k_pack(const kg_query* __restrict__ q, uint32_t n, uint4* __restrict__ pk,
+                                              uint32_t* bad) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const kg_query x = q[i];
+  const uint32_t sns = x.t.sns == KG_SUBJECT_ID ? KG_PACK_SUBJECT_ID : x.t.sns;
+  const uint32_t srel = x.t.sns == KG_SUBJECT_ID ? 0u : x.t.srel;
+  const uint32_t d = x.max_depth <= 0 ? 0u : (x.max_depth > 65535 ? 65535u : (uint32_t)x.max_depth);
+  if (x.t.ns > KG_PACK_ID_MAX || x.t.rel > KG_PACK_ID_MAX || (sns != KG_PACK_SUBJECT_ID && sns > KG_PACK_ID_MAX) ||
+      srel > KG_PACK_ID_MAX)
+    atomicOr(bad, 1u);
+  pk[i] = make_uint4(x.t.obj, x.t.sobj, x.t.ns | (x.t.rel << 12) | ((sns & 0xFFu) << 24),
+                     (sns >> 8) | (srel << 4) | (d << 16));
+}
+
+int pack_queries(const kg_query* d_q, size_t n, kg_query_packed* d_pk, uint32_t* d_bad, hipStream_t stream) {
+  if (!n) return 0;
+  hipLaunchKernelGGL(k_pack, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, stream, d_q, (uint32_t)n, (uint4*)d_pk,
+                     d_bad);
+  HIPC(hipGetLastError());
+  return 0;
+}
+
 int unpack_queries(const kg_query_packed* d_pk, size_t n, kg_query* d_q, hipStream_t stream) {
   if (!n) return 0;
   hipLaunchKernelGGL(k_unpack, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, stream, (const uint4*)d_pk,

@@ -379,6 +379,7 @@ int synth_queries(Snapshot* s, uint64_t seed, size_t n, kg_query* d_q);
 // kg_check_batch_packed: packed queries -> kg_query on the device; the KG_ERROR answers of [0, n) as
 // (base + index, code) pairs after a count word (d_list: 2 + 2 * cap words)
 int unpack_queries(const kg_query_packed* d_pk, size_t n, kg_query* d_q, hipStream_t stream);
+int pack_queries(const kg_query* d_q, size_t n, kg_query_packed* d_pk, uint32_t* d_bad, hipStream_t stream);
 int error_list(const uint8_t* d_out, const uint32_t* d_err, size_t n, uint32_t base, uint32_t* d_list, size_t cap,
                hipStream_t stream);
 // kg_formula.hip: split a batch's decomposable queries into leaf checks / combine their results

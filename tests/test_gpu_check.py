@@ -476,6 +476,9 @@ def test_packed_device_vs_device(preset):
     dq = torch.empty((n, 7), dtype=torch.int32, device="cuda")
     _lib.check(L.kg_synth_queries(snap.handle, 13, n, dq.data_ptr()), "kg_synth_queries")
     dp = bench.pack_queries_device(dq)
+    dl = torch.empty_like(dp)  # the library's packer (kg_pack_queries_device) gives the same rows
+    _lib.check(L.kg_pack_queries_device(snap.handle, dq.data_ptr(), n, dl.data_ptr(), None), "kg_pack_queries_device")
+    assert torch.equal(dl.cpu(), dp.cpu())
     o1 = torch.empty(n, dtype=torch.uint8, device="cuda")
     e1 = torch.empty(n, dtype=torch.int32, device="cuda")
     o2, e2 = torch.empty_like(o1), torch.empty_like(e1)
