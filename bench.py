@@ -75,6 +75,11 @@ def parse(argv=None):
     ap.add_argument("--c3-tuples", type=float, default=1e7, help="C3 sub-line graph size (BASELINE configs[2]: 10M)")
     ap.add_argument("--c3-inflight", type=int, default=6)
     ap.add_argument("--c3-parity", type=int, default=200_000)
+    ap.add_argument("--heavy-steps", type=int, default=20,
+                    help="check mode, one rank: timed batches of the heavy-tail sub-line (SURVEY.md 8d's out-degree "
+                         "law P(k) ~ k^-1.5 at 1.2e8 tuples, 62.5 k checks per batch, 2 in flight; a child "
+                         "`bench.py --heavy-tail` run; 0 = off)")
+    ap.add_argument("--heavy-parity", type=int, default=62_500, help="heavy-tail sub-line: checks compared with the oracle")
     ap.add_argument("--sharded-inflight", type=int, default=0,
                     help="sharded batches in flight per rank, each with its own communicator (0: 3 at one rank -- "
                          "4 measured 20 %% slower, 6 slower still (DESIGN.md 7f) -- and 1 across ranks: streams "
@@ -378,7 +383,7 @@ def expand_steps(L, snap, roots: np.ndarray, depth: int, P: int, steps: int, war
     return el, results
 
 
-def expand_roofline(L, snap, roots: np.ndarray, depth: int, call_ms: float):
+def expand_roofline(L, snap, roots: np.ndarray, depth: int, call_ms: float, traffic=None):
     """Roofline of the expand launch chain (8 B per row opened, 4 B per edge read, 12 B per
     emitted tree node), from one more call's records (every step expands the same roots) over the calls'
     mean device time (HIP events around k_expand_lds / _hash / _hbm + k_expand_compact on the call's
@@ -397,8 +402,8 @@ def expand_roofline(L, snap, roots: np.ndarray, depth: int, call_ms: float):
     R, E, T = int(unions.sum()), int(rec["n_children"][unions].sum()), int(len(rec))
     byts = 8 * R + 4 * E + 12 * T
     gbs = byts / (call_ms * 1e-3) / 1e9
-    return {"kernel": "k_expand_lds/_hash/_hbm + k_expand_compact (one call's chain)", "bound": "hbm",
-            "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS, "traffic": None,
+    return {"kernel": "k_expand_lds/_gw/_hash/_hbm + k_expand_compact (one call's chain)", "bound": "hbm",
+            "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS, "traffic": traffic,
             "bytes_model": "8*unions(rows opened) + 4*children(edges read) + 12*tree records",
             "bytes_per_call": byts, "rows_opened": R, "edges_read": E, "records": T, "call_kernel_ms": call_ms}
 
@@ -1127,12 +1132,12 @@ def main():
     stats = [x for x in stats if x is not None]
     elapsed, edges = aggregate(dist, elapsed, float(sum(s.edges_read for s in stats)) * a.steps / len(stats),
                                f"cuda:{local}" if backend == "nccl" else None)
-    l_bytes = np.array([8 * s.light_rows_opened + 4 * s.light_edges_read + 16 * s.light_probes for s in stats], float)
-    l_reqs = np.array([s.light_rows_opened + s.light_probes for s in stats], float)
-    l_ms = np.array([s.light_ms for s in stats], float)
-    achieved = float(l_bytes.mean() / (l_ms.mean() * 1e-3) / 1e9)
-    req_rate = float(l_reqs.mean() / (l_ms.mean() * 1e-3))
-    traffic = pmc_traffic(STREAM_KERNEL, int(a.tuples), B, a.preset, P)
+    tag = "h" if a.heavy_tail else ""
+    rf_stream = stream_roofline(stats, pmc_traffic(STREAM_KERNEL, int(a.tuples), B, a.preset, P, tag))
+    rf_tail = tail_roofline(stats, lambda k: pmc_traffic(k, int(a.tuples), B, a.preset, P, tag))
+    # the headline keeps k_stream4's roofline (its kernel since round 1); the heavy-tail point reports its
+    # dominant kernel by device time per batch (k_ms_level); every measured kernel is in "rooflines"
+    rf_main = dominant(rf_stream, rf_tail) if a.heavy_tail else rf_stream
 
     # ---- latency phase (outside the timed region): the same P batches in flight, every batch waited for
     # (submit -> results on the host side of the stream), distinct query batches
@@ -1195,7 +1200,10 @@ def main():
         "data": "synthetic (device-generated Drive-like tuple graph, seed %d)" % a.seed,
         "config": {"workload": "%s generator @ %.4g tuples (rows), %d checks/step/GPU, max_read_depth %d"
                                % ("C2/C4" if a.preset == 0 else "C3 (OPL view/edit/share)", info["rows"], B,
-                                  a.global_depth) + (", out-degree law P(k)~k^-1.5" if a.heavy_tail else ""),
+                                  a.global_depth) + (", out-degree law P(k)~k^-1.5" if a.heavy_tail else
+                                  "; out-degrees truncated Pareto, tail index 1.3 (docs) / 1.1 (groups), "
+                                  "mean ~4-10 per row (SURVEY.md 8d's Zipf 1.5 is the heavy sub-line); "
+                                  "doc roots uniform (not Zipf popularity); positives by forward random walks"),
                    "tuples": info["rows"], "tuples_target": a.tuples, "generator_size_param": size_param,
                    "nodes": info["nodes"], "set_edges": info["set_edges"],
                    "batch_per_gpu": B, "global_max_read_depth": a.global_depth, "parallelism": f"replica{world}",
@@ -1223,14 +1231,8 @@ def main():
                            "back": {"rows": int(stats[-1].back_rows), "edges": int(stats[-1].back_edges)}},
         "stream_diag": stream_diag(stats[-1]),
         "snapshot_build_s": t_build,
-        "roofline": {"kernel": STREAM_KERNEL, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "bytes_model": "8*rows_opened + 4*edges_read + 16*direct_probes (per k_stream launch; R/E/P counted in-kernel)",
-                     "launch_ms": float(l_ms.mean()), "bytes_per_launch": float(l_bytes.mean()),
-                     # the random-request view: one row open and one dset probe are one random line each;
-                     # ceiling = independent random 16-B loads/s measured by tools/randprobe.hip on MI355X
-                     "requests_per_launch": float(l_reqs.mean()), "request_rate": req_rate,
-                     "request_peak": RAND_REQ_PEAK, "request_frac": req_rate / RAND_REQ_PEAK},
+        "roofline": rf_main,
+        "rooflines": {r["kernel"]: r for r in (rf_stream, rf_tail) if r},
         "host_path": host,
     }
     orc = None
@@ -1274,6 +1276,8 @@ def main():
         bad = sub_line("expand", lambda: expand_leg(a, snap, orc)) or bad
     if world == 1 and a.preset == 0 and not a.heavy_tail and a.c3_steps > 0:
         bad = sub_line("c3", lambda: c3_leg(a, local)) or bad
+    if world == 1 and a.preset == 0 and not a.heavy_tail and a.heavy_steps > 0:
+        bad = sub_line("heavy", lambda: heavy_leg(a)) or bad
     if a.sharded_steps > 0 and a.preset == 0 and not a.heavy_tail:
         bad = sub_line("sharded", lambda: sharded_leg(a, snap, size_param, dist, rank, world, local, backend, orc)) or bad
     if rank == 0:
@@ -1308,7 +1312,8 @@ def expand_leg(a, snap, orc) -> dict:
            "value": len(roots) * K / el, "unit": "trees/s", "steps": K, "inflight": P, "ms_per_step": el / K * 1e3,
            "tree_nodes_per_s": nodes / el, "kernel_ms_per_call": kms / K,
            "config": {"workload": "C5: %d hot roots of the headline graph, max_read_depth %d" % (len(roots), depth)}}
-    rf = expand_roofline(L, snap, roots, depth, kms / K)
+    # traffic: PMC bytes of every k_expand* dispatch per call (scripts/gpu_r6_prof.sh, same roots and calls in flight)
+    rf = expand_roofline(L, snap, roots, depth, kms / K, pmc_traffic("k_expand", int(a.tuples), len(roots), 0, P, "x"))
     if rf:
         res["roofline"] = rf
     if orc is not None and a.parity_roots > 0 and off is not None:
@@ -1322,6 +1327,36 @@ def expand_leg(a, snap, orc) -> dict:
         o = orc.o
         o.nd = orc.nd
         res["cpu_baseline"] = expand_cpu_baseline(o, roots, depth, ac)
+    return res
+
+
+def heavy_leg(a) -> dict:
+    """SURVEY.md 8d's literal degree law beside the headline: the heavy-tail point
+    (out-degrees P(k) ~ k^-1.5, 1.2e8 tuples, 62.5 k checks per batch, 2 in flight -- its p99 point,
+    DESIGN.md 7f) as a child `bench.py --heavy-tail` run on the same GPU (the parent idles meanwhile), with
+    its own timed region, latency phase, parity against the oracle, CPU baseline and the roofline of its
+    dominant kernel (k_ms_level, HIP events per launch)."""
+    import subprocess
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--heavy-tail", "--steps", str(a.heavy_steps), "--warmup", "4",
+           "--cpu-seconds", str(a.cpu_seconds / 3), "--parity", str(a.heavy_parity), "--parity-canonical",
+           str(min(a.heavy_parity, 10_000)), "--latency-batches", "120", "--host-calls", "0",
+           "--hw-queues", str(a.hw_queues), "--seed", str(a.seed), "--global-depth", str(a.global_depth)]
+    env = dict(os.environ)
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK"):
+        env.pop(k, None)
+    t0 = time.time()
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, env=env, timeout=max(60.0, a.sharded_timeout - 20))
+    lines = [x for x in r.stdout.decode(errors="replace").splitlines() if x.startswith("{")]
+    if not lines:
+        raise RuntimeError("heavy-tail run printed no line (rc %d): %s" % (r.returncode, r.stderr.decode(errors="replace")[-600:]))
+    d = json.loads(lines[-1])
+    keep = ("metric", "value", "unit", "steps", "warmup", "ms_per_step", "config", "gteps", "p99_batch_ms", "steady",
+            "batch_ms", "edges_per_batch", "allowed_fraction", "tiers", "work_per_batch", "snapshot_build_s",
+            "roofline", "rooflines", "parity", "cpu_baseline")
+    res = {k: d[k] for k in keep if k in d}
+    res["config"]["workload"] += ("; popularity: doc roots uniform (not Zipf), positives by forward random walks, "
+                                  "out-degrees Pareto tail index 0.5 for docs and groups")
+    res["child"] = {"cmd": " ".join(cmd[1:]), "rc": r.returncode, "seconds": time.time() - t0}
     return res
 
 
@@ -1352,17 +1387,19 @@ def c3_leg(a, local) -> dict:
         dqs.append(d)
     outs = [torch.empty(B, dtype=torch.uint8, device=dev) for _ in range(W + K)]
     errs = [torch.empty(B, dtype=torch.int32, device=dev) for _ in range(P)]
-    st = _lib.kg_stats()
+    NS = 2 * P  # the stats phase (after the timed region): every batch with kernel stats, same P in flight
+    sts = [_lib.kg_stats() for _ in range(NS)]
 
-    def phase(k0, n):
+    def phase(k0, n, with_stats=False):
         errors = []
 
         def worker(p):
             try:
                 for k in range(p, n, P):
-                    _lib.check(L.kg_check_batch_device(snap3.handle, dqs[k0 + k].data_ptr(), B, a.global_depth,
-                                                       outs[k0 + k].data_ptr(), errs[p].data_ptr(),
-                                                       C.byref(st) if (p == 0 and k == 0) else None,
+                    kk = (k0 + k) % (W + K)
+                    _lib.check(L.kg_check_batch_device(snap3.handle, dqs[kk].data_ptr(), B, a.global_depth,
+                                                       outs[kk].data_ptr(), errs[p].data_ptr(),
+                                                       C.byref(sts[k]) if with_stats else None,
                                                        C.c_void_p(streams[p].cuda_stream)), "kg_check_batch_device")
                 streams[p].synchronize()
             except Exception as x:  # noqa: BLE001
@@ -1382,6 +1419,13 @@ def c3_leg(a, local) -> dict:
     el = time.perf_counter() - t1
     assert (torch.cat(errs).cpu().numpy() == 0).all(), "unexpected errors in the synthetic C3 batch"
     r0 = outs[W].cpu().numpy()
+    q0 = dqs[W].cpu().numpy().view(np.uint32)
+    phase(0, NS, with_stats=True)  # batches 0 .. NS-1 again (their results are not read)
+    torch.cuda.synchronize()
+    st = sts[0]
+    tr = lambda k: pmc_traffic(k, int(a.c3_tuples), B, 1, P)
+    rf_stream = stream_roofline(sts, tr(STREAM_KERNEL))
+    rf_tail = tail_roofline(sts, tr)
     res = {"metric": "permission checks/sec (C3: OPL view/edit/share rewrites)", "value": B * K / el,
            "unit": "checks/s", "steps": K, "inflight": P, "ms_per_step": el / K * 1e3,
            "config": {"workload": "C3 generator @ %.4g tuples (rows), %d checks/step, max_read_depth %d"
@@ -1389,11 +1433,24 @@ def c3_leg(a, local) -> dict:
                       "materialized": snap3.materialized(), "tune": dict(snap3.__dict__.get("tuned", {}))},
            "allowed_fraction": float(r0.mean()), "snapshot_build_s": t_build,
            "tiers": {"light": int(st.n_light), "back": int(st.n_back), "grid": int(st.n_grid),
-                     "general": int(st.n_general), "no_holder": int(st.n_no_holder)}}
-    if a.c3_parity > 0:
-        orc3 = CheckOracle(snap3, a3, effective_cpus()["effective"])
-        res["parity"] = orc3.parity(dqs[W].cpu().numpy().view(np.uint32), r0, a.c3_parity,
-                                    min(a.parity_canonical, a.c3_parity))
+                     "general": int(st.n_general), "no_holder": int(st.n_no_holder)},
+           # the dominant kernel by device time per batch (HIP events of a separate stats phase: every batch
+           # waited for, same batches in flight); every measured kernel in "rooflines"
+           "roofline": dominant(rf_stream, rf_tail),
+           "rooflines": {r["kernel"]: r for r in (rf_stream, rf_tail) if r},
+           "kernel_ms_per_batch": {"k_fsplit": float(np.mean([s.split_ms for s in sts])),
+                                   "k_stream4": rf_stream["ms_per_batch"],
+                                   **({rf_tail["kernel"]: rf_tail["ms_per_batch"]} if rf_tail else {}),
+                                   "batch_span": float(np.mean([s.kernel_ms for s in sts]))},
+           "stats_batches": NS}
+    if a.c3_parity > 0 or a.cpu_seconds > 0:
+        cpus = effective_cpus()
+        orc3 = CheckOracle(snap3, a3, cpus["effective"])
+        if a.c3_parity > 0:
+            res["parity"] = orc3.parity(q0, r0, a.c3_parity, min(a.parity_canonical, a.c3_parity))
+        if a.cpu_seconds > 0:  # a bounded sample: a third of the headline's CPU budget
+            a3.cpu_seconds = a.cpu_seconds / 3
+            res["cpu_baseline"] = cpu_baseline(orc3, q0, a3, cpus)
         orc3.o.close()
     snap3.close()
     return res
@@ -1724,11 +1781,72 @@ def stream_diag(s) -> dict:
             "max_wave_us": s.light_wave_max_ticks / 100.0, "span_us": s.light_span_ticks / 100.0}
 
 
-def pmc_traffic(kernel: str, tuples: int, batch: int, preset: int, inflight: int):
+TAIL_KERNELS = {1: "k_grid_level<0>", 2: "k_ms_level<8>"}
+
+
+def stream_roofline(stats: list, traffic) -> dict:
+    """k_stream4 (one launch per batch): the SURVEY.md 8d byte model over its in-kernel counters, per
+    launch, against its HIP-event launch time."""
+    b = np.array([8 * s.light_rows_opened + 4 * s.light_edges_read + 16 * s.light_probes for s in stats], float)
+    r = np.array([s.light_rows_opened + s.light_probes for s in stats], float)
+    ms = np.array([s.light_ms for s in stats], float)
+    ach = float(b.mean() / (ms.mean() * 1e-3) / 1e9)
+    rate = float(r.mean() / (ms.mean() * 1e-3))
+    return {"kernel": STREAM_KERNEL, "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": ach / HBM_PEAK_GBS, "traffic": traffic,
+            "bytes_model": "8*rows_opened + 4*edges_read + 16*direct_probes (per k_stream launch; R/E/P counted in-kernel)",
+            "launch_ms": float(ms.mean()), "bytes_per_launch": float(b.mean()), "launches_per_batch": 1,
+            "ms_per_batch": float(ms.mean()),
+            # the random-request view: one row open and one dset probe are one random line each;
+            # ceiling = independent random 16-B loads/s measured by tools/randprobe.hip on MI355X
+            "requests_per_launch": float(r.mean()), "request_rate": rate, "request_peak": RAND_REQ_PEAK,
+            "request_frac": rate / RAND_REQ_PEAK}
+
+
+def tail_roofline(stats: list, traffic_of) -> dict | None:
+    """The tail tier's level kernel (kg_stats tail_*): k_grid_level (per-query grid tier; the 8d byte model
+    over its counters) or k_ms_level (MS-BFS; per edge with work its 16-B adjx record + 4-B hop stamp, per
+    active (edge, 64-query word) the child's 8-B VIS + 8-B TG words -- one row read per (group, node)
+    entry, i.e. per 512 queries, not per query).  Launch time = the HIP-event durations of the timed
+    launches (the first 64 of a batch) / their count; bytes per launch = the batch's bytes / launches."""
+    st = [s for s in stats if s.tail_launches > 0 and s.tail_ms > 0]
+    if not st:
+        return None
+    kind = max(int(s.tail_kind) for s in st)
+    if kind == 2:
+        b = np.array([20 * s.ms_edges_loaded + 16 * s.ms_words_active for s in st], float)
+        model = ("20*ms_edges_loaded + 16*ms_words_active (k_ms_level: adjx record + hop stamp per edge with work, "
+                 "child VIS + TG word per active (edge, 64-query word); counted in-kernel)")
+    else:
+        b = np.array([8 * s.tail_rows + 4 * s.tail_edges + 16 * s.tail_probes + 16 * s.tail_logged for s in st], float)
+        model = "8*rows_opened + 4*edges_read + 16*direct_probes + 16*level_entries (grid tier share; counted in-kernel)"
+    launches = np.array([s.tail_launches for s in st], float)
+    timed = np.minimum(launches, 64)
+    ms = np.array([s.tail_ms for s in st], float)
+    launch_ms = float(ms.sum() / timed.sum())
+    bpl = float(b.sum() / launches.sum())
+    ach = bpl / (launch_ms * 1e-3) / 1e9
+    name = TAIL_KERNELS.get(kind, "tail")
+    return {"kernel": name, "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": ach / HBM_PEAK_GBS, "traffic": traffic_of(name), "bytes_model": model, "launch_ms": launch_ms,
+            "bytes_per_launch": bpl, "launches_per_batch": float(launches.mean()),
+            "ms_per_batch": float(launch_ms * launches.mean()),
+            **({"ms_edges_loaded_per_batch": float(np.mean([s.ms_edges_loaded for s in st])),
+                "ms_words_active_per_batch": float(np.mean([s.ms_words_active for s in st])),
+                "edge_visits_per_batch": float(np.mean([s.tail_edges for s in st]))} if kind == 2 else
+               {"edges_per_batch": float(np.mean([s.tail_edges for s in st]))})}
+
+
+def dominant(*rfs) -> dict:
+    """The roofline of the kernel with the most device time per batch."""
+    return max([r for r in rfs if r], key=lambda r: r["ms_per_batch"])
+
+
+def pmc_traffic(kernel: str, tuples: int, batch: int, preset: int, inflight: int, tag: str = ""):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc passes
-    (profiles/pmc_<kernel>_p<preset>.json, scripts/gpu_profile.sh), if taken on this exact workload;
+    (profiles/pmc_<kernel>_p<preset><tag>.json, scripts/gpu_profile.sh), if taken on this exact workload;
     else None."""
-    p = os.path.join(ROOT, "profiles", f"pmc_{kernel.split('<')[0]}_p{preset}.json")
+    p = os.path.join(ROOT, "profiles", f"pmc_{kernel.split('<')[0]}_p{preset}{tag}.json")
     try:
         with open(p) as f:
             d = json.load(f)

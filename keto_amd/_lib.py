@@ -77,7 +77,11 @@ class kg_stats(C.Structure):
                 ("n_back", C.c_uint64), ("n_no_holder", C.c_uint64), ("back_rows", C.c_uint64),
                 ("back_edges", C.c_uint64), ("light_steps", C.c_uint64), ("light_waves", C.c_uint64),
                 ("light_wave_ticks", C.c_uint64),
-                ("light_span_ticks", C.c_uint64), ("light_wave_max_ticks", C.c_uint64)]
+                ("light_span_ticks", C.c_uint64), ("light_wave_max_ticks", C.c_uint64),
+                ("tail_ms", C.c_double), ("tail_launches", C.c_uint64), ("tail_kind", C.c_uint64),
+                ("tail_rows", C.c_uint64), ("tail_edges", C.c_uint64), ("tail_probes", C.c_uint64),
+                ("tail_logged", C.c_uint64), ("ms_edges_loaded", C.c_uint64), ("ms_words_active", C.c_uint64),
+                ("split_ms", C.c_double)]
 
     def as_dict(self) -> dict:
         return {n: getattr(self, n) for n, _ in self._fields_}

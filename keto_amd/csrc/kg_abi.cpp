@@ -548,6 +548,11 @@ static int tune_one(Snapshot* s, const char* key, int64_t value) {
     (strcmp(key, "expand_gw") == 0 ? s->expand_gw : s->expand_skip_lds) = (int)value;
     return 0;
   }
+  if (strcmp(key, "expand_gw_wait_us") == 0) {
+    if (value < 0 || value > 10000000) return set_error(-2, "expand_gw_wait_us must be in [0, 10^7]");
+    s->expand_gw_wait_us = (uint32_t)value;
+    return 0;
+  }
   if (strcmp(key, "expand_tail") == 0) {
     if (value < 0 || value > 1) return set_error(-2, "expand_tail must be 0 or 1");
     s->expand_tail = (int)value;
@@ -864,13 +869,20 @@ static int check_host(Snapshot* s, const kg_query* q, const kg_query_packed* pq,
       const uint64_t* y = reinterpret_cast<const uint64_t*>(&x);
       for (size_t f = 0; f < sizeof(kg_stats) / 8; f++) d[f] += y[f];
     }
-    double km = 0, lm = 0;
+    double km = 0, lm = 0, tm = 0, sm = 0;
+    uint64_t tk = 0;
     for (size_t i = 0; i < R; i++) {
       km = std::max(km, st[i].kernel_ms);
       lm = std::max(lm, st[i].light_ms);
+      tm = std::max(tm, st[i].tail_ms);
+      sm = std::max(sm, st[i].split_ms);
+      tk = std::max(tk, st[i].tail_kind);  // a kind, not a count
     }
+    stats->tail_kind = tk;
     stats->kernel_ms = km;
     stats->light_ms = lm;
+    stats->tail_ms = tm;
+    stats->split_ms = sm;
   }
   return rc;
 }
@@ -891,6 +903,7 @@ int kg_check_batch_packed(kg_snapshot* sp, const kg_query_packed* q, size_t n, i
                           uint32_t* err_index, uint32_t* err_code, size_t err_cap, size_t* n_err, kg_stats* stats) {
   KG_GUARD_BEGIN
   if (!sp || !n_err) return set_error(-2, "NULL argument");
+  *n_err = 0;  // defined on every return, failures included
   if (n && (!q || !out)) return set_error(-2, "NULL buffer");
   if (err_cap && (!err_index || !err_code)) return set_error(-2, "err_cap > 0 needs err_index and err_code");
   Snapshot* s = reinterpret_cast<Snapshot*>(sp);

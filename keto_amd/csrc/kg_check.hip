@@ -881,6 +881,15 @@ int check_batch_begin(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n, 
   if (n > 0x7FFFFFFFull) return set_error(-2, "batch too large");
   HIPC(hipSetDevice(s->device));
   hipStream_t stream = w->stream;
+  // timing of a batch with stats: the whole batch (ev 0-1), k_stream4 (2-3), the formula split (4-5)
+  // and each tail-tier level launch (Workspace::lev_mark)
+  if (stats && !w->ev[0])
+    for (auto& e : w->ev) HIPC(hipEventCreate(&e));
+  w->lev_on = stats != nullptr;
+  w->lev_n = 0;
+  w->lev_kind = 0;
+  w->lev_launches = 0;
+  if (stats) HIPC(hipEventRecord(w->ev[0], stream));
   // packed queries: k_resolve unpacks them in registers when it is the only reader of the queries --
   // without a namespace program there is no formula split and no general route; otherwise they are
   // unpacked into the workspace first
@@ -911,7 +920,9 @@ int check_batch_begin(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n, 
     uint8_t* out2;
     uint32_t* err2;
     const uint2* ref;
+    if (stats) HIPC(hipEventRecord(w->ev[4], stream));
     if (int rc = formula_split(s, w, d_q, n, global_max_depth, &q2, &n2, &n_extra, &out2, &err2, &ref)) return rc;
+    if (stats) HIPC(hipEventRecord(w->ev[5], stream));
     bp->split = true;
     bp->f_n = n;
     bp->f_out = d_out;
@@ -961,10 +972,7 @@ int check_batch_begin(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n, 
   bool grid_pending = false;
   const uint32_t *grid_list = nullptr, *grid_count = nullptr;
 
-  if (stats && !w->ev[0])
-    for (auto& e : w->ev) HIPC(hipEventCreate(&e));
-  hipEvent_t e0 = w->ev[0], e1 = w->ev[1], l0 = w->ev[2], l1 = w->ev[3];
-  if (stats) HIPC(hipEventRecord(e0, stream));
+  hipEvent_t e1 = w->ev[1], l0 = w->ev[2], l1 = w->ev[3];
   HIPC(hipMemsetAsync(ctl, 0, sizeof(Ctl), stream));
   if (n) {
     const bool use_back = s->back_tier && s->ds.radj;
@@ -1085,9 +1093,30 @@ int check_batch_end(Snapshot* s, Workspace* w, BatchPending* bp, bool* reran, bo
       return -1;
   }
   if (stats) {
-    float ms = 0, lms = 0;
+    float ms = 0, lms = 0, sms = 0;
     HIPC(hipEventElapsedTime(&ms, w->ev[0], w->ev[1]));
     if (bp->n) HIPC(hipEventElapsedTime(&lms, w->ev[2], w->ev[3]));
+    if (bp->split) HIPC(hipEventElapsedTime(&sms, w->ev[4], w->ev[5]));
+    double tms = 0;
+    for (int k = 0; k < w->lev_n; k++) {
+      float x = 0;
+      if (w->lev_ev[2 * k] && w->lev_ev[2 * k + 1] &&
+          hipEventElapsedTime(&x, w->lev_ev[2 * k], w->lev_ev[2 * k + 1]) == hipSuccess)
+        tms += x;
+      else
+        (void)hipGetLastError();
+    }
+    w->lev_on = false;
+    stats->tail_ms = tms;
+    stats->tail_launches = w->lev_launches;
+    stats->tail_kind = (uint64_t)w->lev_kind;
+    stats->tail_rows = gs.rows;
+    stats->tail_edges = gs.edges;
+    stats->tail_probes = gs.probes;
+    stats->tail_logged = gs.logged;
+    stats->ms_edges_loaded = gs.ms_eload;
+    stats->ms_words_active = gs.ms_wact;
+    stats->split_ms = sms;
     Ctl h;
     memcpy(&h, bp->ctl_host, sizeof(Ctl));
     for (int x = 0; x < 8; x++)

@@ -629,11 +629,14 @@ __device__ __forceinline__ void gw_run(const GwSlots& g, uint64_t* hsrc, uint32_
 }
 
 // A root handed on: ga (from a small slot; published as ri + 1 for the waiting large slots) or gb (from
-// a large slot; read by the hash pass, a later kernel).
-__device__ __forceinline__ void gw_publish(uint32_t* list, uint32_t* count, uint32_t ri, bool big) {
+// a large slot; read by the hash pass, a later kernel).  A ga entry whose ticket holder gave up waiting
+// (GW_ABANDON, see k_expand_gw) goes to gb instead: the hash pass expands any root.
+#define GW_ABANDON 0xFFFFFFFFu
+__device__ __forceinline__ void gw_publish(uint32_t* list, uint32_t* count, uint32_t ri, bool big, uint32_t* gb_list,
+                                           uint32_t* gb_count) {
   const uint32_t at = atomicAdd(count, 1u);
   if (big) list[at] = ri;
-  else atomicExch(&list[at], ri + 1);
+  else if (atomicCAS(&list[at], 0u, ri + 1) == GW_ABANDON) gb_list[atomicAdd(gb_count, 1u)] = ri;
 }
 
 // One launch, two slot classes: workgroups [0, n_big) hold large slots, the rest small ones.  Every
@@ -642,12 +645,17 @@ __device__ __forceinline__ void gw_publish(uint32_t* list, uint32_t* count, uint
 // a large slot is free instead of after the whole small-slot pass (two launches: ~12 + ~25 ms per C5
 // call in series).  A large slot waits for ga items with s_sleep and leaves when every small
 // workgroup has finished and the queue is drained (small workgroups never wait: the exit is reached).
-// What outgrows a large slot goes on to the hash pass (gb).
+// The wait is bounded (`wait_ticks`, kg_snapshot_tune("expand_gw_wait_us")): the small workgroups are
+// dispatched after the large ones and need free CUs, so with other kernels holding the CUs a large slot
+// must not depend on them forever.  Past the bound it abandons its ticket (CAS 0 -> GW_ABANDON; a root
+// published there later goes to the hash pass) and leaves.  What outgrows a large slot goes on to the
+// hash pass (gb).
 __global__ __launch_bounds__(256) void k_expand_gw(DevSnap s, const kg_set* __restrict__ roots, int32_t global,
                                                    ExpCtl* ctl, RootOut* outs, kg_tree_node* arena, uint32_t* next,
                                                    uint32_t n_chunks, ExpFrame* stacks, uint32_t stack_cap,
                                                    const uint32_t* p2_list, uint32_t* ga_list, uint32_t* gb_list,
-                                                   uint32_t n_roots, uint32_t n_big, GwSlots g_small, GwSlots g_big) {
+                                                   uint32_t n_roots, uint32_t n_big, GwSlots g_small, GwSlots g_big,
+                                                   uint64_t wait_ticks) {
   __shared__ uint32_t vis[GW_LDS_LOC / 32];
   __shared__ uint32_t s_k, s_nloc, s_nent, s_bad, s_epoch, s_ri, s_src, s_p2dry;
   __shared__ ExpFrame s_fr[XF];
@@ -687,6 +695,7 @@ __global__ __launch_bounds__(256) void k_expand_gw(DevSnap s, const kg_set* __re
       }
       if (!src && big) {
         const uint32_t k = atomicAdd(&ctl->ga_head, 1u);
+        const uint64_t w0 = wall_clock64();
         // the list holds n_roots entries at most: a ticket past it can never be served
         for (; k < n_roots;) {
           const uint32_t v = ld_sc1(&ga_list[k]);  // ri + 1 once published (the list is zeroed per call)
@@ -696,6 +705,14 @@ __global__ __launch_bounds__(256) void k_expand_gw(DevSnap s, const kg_set* __re
             break;
           }
           if (ld_sc1(&ctl->gw_small_done) == n_small && ld_sc1(&ctl->ga_count) <= k) break;
+          if (wall_clock64() - w0 >= wait_ticks) {  // give the ticket up; a publication that won the race is ours
+            const uint32_t old = atomicCAS(&ga_list[k], 0u, GW_ABANDON);
+            if (old) {
+              src = 2;
+              ri = old - 1;
+            }
+            break;
+          }
           __builtin_amdgcn_s_sleep(16);
         }
       }
@@ -798,7 +815,7 @@ __global__ __launch_bounds__(256) void k_expand_gw(DevSnap s, const kg_set* __re
       bad = s_bad != 0;
     }
     if (bad) {
-      if (threadIdx.x == 0) gw_publish(ovf_list, ovf_count, ri, big);
+      if (threadIdx.x == 0) gw_publish(ovf_list, ovf_count, ri, big, gb_list, &ctl->gb_count);
       __syncthreads();
       continue;
     }
@@ -1001,7 +1018,7 @@ __global__ __launch_bounds__(256) void k_expand_gw(DevSnap s, const kg_set* __re
       if (lane == 0) {
         atomicMax(&ctl->gw_ticks[big ? 3 : 1], wall_clock64() - t1);
         if (status == EXP_OVERFLOW) {
-          gw_publish(ovf_list, ovf_count, ri, big);
+          gw_publish(ovf_list, ovf_count, ri, big, gb_list, &ctl->gb_count);
         } else {
           outs[ri] = RootOut{S.first, cnt};
           recs += cnt;
@@ -1016,6 +1033,17 @@ __global__ __launch_bounds__(256) void k_expand_gw(DevSnap s, const kg_set* __re
       __threadfence();
       atomicAdd(&ctl->gw_small_done, 1u);
     }
+  }
+}
+
+// After k_expand_gw: ga entries no large slot ever held a ticket for (every large slot gave up waiting
+// before they were published) go to the hash pass.  Entries below the last ticket were taken, or
+// abandoned and redirected by their publisher (gw_publish); stream order makes the kernel race-free.
+__global__ void k_gw_sweep(ExpCtl* ctl, const uint32_t* ga_list, uint32_t* gb_list) {
+  const uint32_t cnt = ctl->ga_count, head = ctl->ga_head;
+  for (uint32_t i = min(head, cnt) + threadIdx.x; i < cnt; i += blockDim.x) {
+    const uint32_t v = ga_list[i];
+    if (v && v != GW_ABANDON) gb_list[atomicAdd(&ctl->gb_count, 1u)] = v - 1;
   }
 }
 
@@ -1196,7 +1224,7 @@ int expand_batch(Snapshot* s, hipStream_t stream, void** bufs, const kg_set* roo
   ExpandBufs& B = *static_cast<ExpandBufs*>(*bufs);
   B.device = s->device;
   const uint32_t stack_cap = (uint32_t)std::min<int64_t>(0x8000, (int64_t)global + 2);
-  const bool gw_on = s->expand_gw != 0;
+  bool gw_on = s->expand_gw != 0;
   const uint32_t gw_n[2] = {std::max<uint32_t>(1, (uint32_t)s->n_cu / 2), 4};
   const uint32_t grid1 = (uint32_t)s->n_cu * 2, slots1 = grid1 * 4;
   const uint64_t nn = std::max<uint32_t>(s->ds.n_nodes, 1), words = ((nn + 31) / 32 + 1 + 3) & ~3ull;
@@ -1227,8 +1255,12 @@ int expand_batch(Snapshot* s, hipStream_t stream, void** bufs, const kg_set* roo
   if (!rc && (e = grow(&B.stacks, B.stacks_bytes,
                        (size_t)(slots1 + slots2 + 1 + gw_n[0] + gw_n[1]) * stack_cap * sizeof(ExpFrame))) != hipSuccess)
     fail("hipMalloc", e);
+  // gather-walk slots (~0.9 GB a lane); without them the pass-1 overflows go to the hash pass directly
   for (int k = 0; k < 2 && gw_on && !rc; k++)
-    if ((e = gw_alloc(B, k, gw_n[k], k == 0 ? 65536u : (2u << 20), stream)) != hipSuccess) fail("hipMalloc(gather-walk)", e);
+    if (gw_alloc(B, k, gw_n[k], k == 0 ? 65536u : (2u << 20), stream) != hipSuccess) {
+      (void)hipGetLastError();
+      gw_on = false;
+    }
   if (!rc && (e = grow(&B.bm, B.bm_bytes, (clear_words + (size_t)slots2 * cap2 + nn) * 4)) != hipSuccess)
     fail("hipMalloc", e);
   for (auto& x : B.ev)
@@ -1266,7 +1298,8 @@ int expand_batch(Snapshot* s, hipStream_t stream, void** bufs, const kg_set* roo
       ExpFrame* gst = B.stacks + (size_t)(slots1 + slots2 + 1) * stack_cap;
       hipLaunchKernelGGL(k_expand_gw, dim3(gw_n[0] + gw_n[1]), dim3(256), 0, stream, s->ds, B.d_roots, global, B.ctl,
                          B.outs, B.arena, B.next, n_chunks, gst, stack_cap, B.p2, B.p2 + 2 * n, B.p2 + 3 * n,
-                         (uint32_t)n, gw_n[1], B.gws[0], B.gws[1]);
+                         (uint32_t)n, gw_n[1], B.gws[0], B.gws[1], (uint64_t)s->expand_gw_wait_us * 100);  // 100 MHz clock
+      hipLaunchKernelGGL(k_gw_sweep, dim3(1), dim3(256), 0, stream, B.ctl, B.p2 + 2 * n, B.p2 + 3 * n);
       q_hash = B.p2 + 3 * n;
       c_hash = &B.ctl->gb_count;
       h_hash = &B.ctl->gb_head;

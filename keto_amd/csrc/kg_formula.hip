@@ -31,7 +31,12 @@
 namespace kg {
 
 // ------------------------------------------------------------------ device
-__global__ __launch_bounds__(256) void k_fsplit(DevSnap s, const int32_t* __restrict__ fidx,
+// One thread per request, 1024 per workgroup, ONE slot reservation per workgroup: the leaf queries go
+// to one contiguous range after the batch, so every reservation hits the same counter, and same-address
+// atomics serialise at the memory side (~11 ns each, MI355X_MICROARCH.md).  Per wave (round 5) that was
+// 15.6 k atomics per 1 M requests, 185 us of a C3 batch (profiles/r6a_c3_timeline.txt).
+constexpr uint32_t FS_BLOCK = 1024;
+__global__ __launch_bounds__(FS_BLOCK) void k_fsplit(DevSnap s, const int32_t* __restrict__ fidx,
                                                 const FPlan* __restrict__ plans, const kg_query* __restrict__ q,
                                                 uint32_t n, int32_t global, kg_query* __restrict__ q2,
                                                 uint2* __restrict__ ref, uint32_t* n_extra) {
@@ -67,12 +72,25 @@ __global__ __launch_bounds__(256) void k_fsplit(DevSnap s, const int32_t* __rest
       }
     }
   }
-  // wave-aggregated slot reservation for the leaf queries
+  // workgroup-aggregated slot reservation for the leaf queries
+  __shared__ uint32_t s_wsum[FS_BLOCK / 64], s_base;
+  const uint32_t wave = threadIdx.x >> 6;
   uint32_t total = 0;
-  const uint32_t off = wave_excl_scan(take, &total);
-  uint32_t wbase = 0;
-  if (lane_id() == 0 && total) wbase = atomicAdd(n_extra, total);
-  wbase = __shfl(wbase, 0, 64);
+  uint32_t off = wave_excl_scan(take, &total);
+  if (lane_id() == 0) s_wsum[wave] = total;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+    for (uint32_t k = 0; k < FS_BLOCK / 64; k++) {
+      const uint32_t c = s_wsum[k];
+      s_wsum[k] = t;
+      t += c;
+    }
+    s_base = t ? atomicAdd(n_extra, t) : 0u;
+  }
+  __syncthreads();
+  off += s_wsum[wave];
+  const uint32_t wbase = s_base;
   if (!valid) return;
   uint2 r = make_uint2(NONE, NONE);
   if (take) {
@@ -266,7 +284,7 @@ int formula_split(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n, int3
   uint2* r = (uint2*)(b + off[3]);
   uint32_t* cnt = (uint32_t*)(b + off[4]);
   HIPC(hipMemsetAsync(cnt, 0, 4, w->stream));
-  hipLaunchKernelGGL(k_fsplit, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, w->stream, s->ds, s->d_fidx,
+  hipLaunchKernelGGL(k_fsplit, dim3((uint32_t)((n + FS_BLOCK - 1) / FS_BLOCK)), dim3(FS_BLOCK), 0, w->stream, s->ds, s->d_fidx,
                      (const FPlan*)s->d_fplans, d_q, (uint32_t)n, gdepth, q, r, cnt);
   HIPC(hipGetLastError());
   *q2 = q;

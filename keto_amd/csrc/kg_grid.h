@@ -8,6 +8,7 @@ namespace kg {
 
 struct GridStats {
   unsigned long long rows = 0, edges = 0, probes = 0, done = 0, logged = 0;
+  unsigned long long ms_eload = 0, ms_wact = 0;  // k_ms_level: adjx records loaded, active (edge, word) pairs
 };
 
 // phase 1 with dsum (zeroed, 256-B aligned, GRID_SUM_WORDS): the first round keeps its counters there

@@ -568,15 +568,19 @@ int grid_tier(Snapshot* s, Workspace* w, const RQuery* rq, const uint32_t* qlist
         hipLaunchKernelGGL(k_grid_settle, dim3(slot_blocks), dim3(256), 0, stream, v.sl, d_count, done, G, t, 0);
         HIPC(hipGetLastError());
       }
+      w->lev_mark(stream, false, 1);
       hipLaunchKernelGGL(k_grid_level<0>, dim3(lgrid), dim3(256), 0, stream, s->ds, v.lg, t, v.sl, v.H, v.hcap - 1,
                          epoch, v.ctl);
       HIPC(hipGetLastError());
+      w->lev_mark(stream, true, 1);
       if (bidir && 2 * t + 1 <= global_max_depth - 1) {
         hipLaunchKernelGGL(k_grid_settle, dim3(slot_blocks), dim3(256), 0, stream, v.sl, d_count, done, G, t, 1);
         HIPC(hipGetLastError());
+        w->lev_mark(stream, false, 1);
         hipLaunchKernelGGL(k_grid_level<1>, dim3(lgrid), dim3(256), 0, stream, s->ds, v.blg, t, v.sl, v.H,
                            v.hcap - 1, epoch, v.ctl);
         HIPC(hipGetLastError());
+        w->lev_mark(stream, true, 1);
       }
     }
     hipLaunchKernelGGL(k_grid_finish, dim3(slot_blocks), dim3(256), 0, stream, v.sl, d_count, done, G, out, err, v.ctl,

@@ -44,13 +44,14 @@ constexpr int MS_EDGE_BITS = 36;
 constexpr uint64_t MS_EDGE_MASK = (1ull << MS_EDGE_BITS) - 1;
 constexpr uint64_t MS_ENTRY_MAX = (1ull << (64 - MS_EDGE_BITS)) - 1;
 constexpr int MS_HOPS = 32;  // depth masks per group (global max depth <= 32 here)
-// edges per tile of k_ms_level: K lanes per edge, two edges per lane group
-constexpr uint32_t ms_tile_edges(int K) { return 2u * 256u / (uint32_t)K; }
+// edges per tile of k_ms_level: one lane per edge (the LDS staging is (TE + 2) x K words x 2)
+constexpr uint32_t ms_tile_edges(int K) { return K <= 8 ? 256u : 128u; }
 
 struct MsCtl {
   unsigned long long packed[2];  // per level buffer: entries << 36 | edges
   unsigned long long edges, logged;
   uint32_t overflow, pad;
+  unsigned long long eload, wact;  // k_ms_level: adjx records loaded, (edge, 64-query word) pairs with work
 };
 
 // A group is 64 * K queries; every per-node mask is K consecutive 64-bit words (node-major), so the
@@ -65,6 +66,7 @@ struct MsView {
   uint32_t* stamp;  // [G][n]: 1 + the last hop the node was appended at (one entry per hop)
   uint64_t* hit;   // [G][K]
   uint64_t* many;  // [G][K]: queries whose subject has more than tg_cap holders (probed, no TG bits)
+  uint32_t* gmany;  // [G]: 1 when any word of many[g] is non-zero
   uint32_t* qs;    // [G][64K] tagged subject
   uint32_t tg_cap;
   uint64_t* pm;    // [G][MS_HOPS][K]
@@ -184,6 +186,7 @@ __global__ void k_ms_masks(MsView v) {
   if (h == 0) {
     v.hit[(size_t)g * K + k] = 0;
     v.many[(size_t)g * K + k] = 0;
+    if (k == 0) v.gmany[g] = 0;
   }
 }
 
@@ -199,7 +202,10 @@ __global__ __launch_bounds__(256) void k_ms_holders(DevSnap s, const RQuery* __r
   const uint32_t g = i / Q, b = i % Q;
   const uint64_t bit = 1ull << (b & 63);
   if (hr.y > v.tg_cap) {
-    if (lane_id() == 0) atomicOr((unsigned long long*)&v.many[(size_t)g * K + (b >> 6)], (unsigned long long)bit);
+    if (lane_id() == 0) {
+      atomicOr((unsigned long long*)&v.many[(size_t)g * K + (b >> 6)], (unsigned long long)bit);
+      v.gmany[g] = 1u;
+    }
     return;
   }
   for (uint32_t k = lane_id(); k < hr.y; k += 64)
@@ -216,11 +222,15 @@ __device__ __forceinline__ uint64_t ms_entry_of(const uint64_t* ex, uint64_t lo,
 }
 
 // Level L: the frontier (hop L) in buffer cur is expanded into hop L+1, appended to buffer cur ^ 1.
-// K lanes per edge (lane k owns mask word k), TE = 2 * 256 / K edges per tile (two per lane group:
-// both edges' loads are issued before either is used).  A tile's entries are staged in LDS with
-// their frontier masks (already filtered by depth and answered queries at tile start), so a word
-// with nothing to propagate costs no memory access, and an edge whose K words are all empty is not
-// even loaded.
+// ONE lane per edge (round 6; rounds 3-5 ran K lanes per edge, one mask word each, 2 edges per lane
+// group: a 64-edge tile per workgroup iteration, whose chain of dependent round trips -- tile map,
+// staged entries, adjx record, child masks, hop stamp, two append atomics on one counter -- was the
+// level's time at ~6 us per tile, profiles/r6a_heavy_kernel_stats.csv).  A lane loads its edge's adjx
+// record, then the child's K VIS words (and its TG words only when a new bit may use them) as 16-B
+// loads, and does the K words' logic itself: TE = 256 edges per tile (128 at K = 16), one append per
+// tile.  A tile's entries are staged in LDS with their frontier masks already filtered by depth and
+// answered queries at tile start (`want`: may probe the child at hop L+1, `s_em`: may expand it), so an
+// edge whose K words are all empty is not even loaded.
 //
 // Per edge the updates are blind ORs on the masks loaded once (no returning atomic on the chain): the
 // bits new to the child are `want & ~vis` as loaded.  Two edges of one level that reach the same
@@ -230,40 +240,27 @@ __device__ __forceinline__ uint64_t ms_entry_of(const uint64_t* ex, uint64_t lo,
 // one returning atomic is the node's hop stamp (one level entry per (group, node, hop)), skipped when
 // the loaded stamp already says so.
 template <int K>
-__device__ __forceinline__ void ms_edge(const DevSnap& s, const MsView& v, uint32_t n, int L, int nx, uint64_t want,
-                                        uint64_t many, uint64_t em, uint32_t g, uint32_t k, const AdjX& x, bool& app,
-                                        uint32_t& child, uint32_t& cb, uint32_t& clen, uint64_t vis0, uint64_t tg0,
-                                        uint32_t st0) {
-  const uint64_t nw = want & ~vis0;
-  if (!nw) return;
-  const size_t at = ((size_t)g * n + x.node) * K + k;
-  atomicOr((unsigned long long*)&v.vis[at], (unsigned long long)nw);
-  // checkDirect: TG bits for subjects with few holders, dset probes for popular ones
-  uint64_t hits = nw & ~many & tg0;
-  for (uint64_t m = nw & many; m; m &= m - 1) {
-    const uint32_t subj = v.qs[(size_t)g * 64 * K + k * 64 + __builtin_ctzll(m)];
-    if (sig_maybe(x.lsig, x.sig, subj_sig(subj)) && dset_probe(s, x.node, subj)) hits |= m & (~m + 1);
-  }
-  if (hits) atomicOr((unsigned long long*)&v.hit[(size_t)g * K + k], (unsigned long long)hits);
-  // expansion: those that may expand it
-  const uint64_t ex = adjx_len16(x) ? (nw & em) : 0ull;
-  if (ex) {
-    atomicOr((unsigned long long*)&v.fr[nx][at], (unsigned long long)ex);
-    const uint32_t want_st = (uint32_t)L + 2;
-    app = st0 < want_st && atomicMax(&v.stamp[(size_t)g * n + x.node], want_st) < want_st;
-    child = x.node;
-    cb = x.begin;
-    clen = adjx_len(s, x);
+__device__ __forceinline__ void ms_load_words(const uint64_t* p, uint64_t (&w)[K]) {
+  if constexpr (K == 1) {
+    w[0] = p[0];
+  } else {
+    const uint4* q = reinterpret_cast<const uint4*>(p);  // K words of one node: 8K-byte aligned
+#pragma unroll
+    for (int j = 0; j < K / 2; j++) {
+      const uint4 x = q[j];
+      w[2 * j] = (uint64_t)x.x | ((uint64_t)x.y << 32);
+      w[2 * j + 1] = (uint64_t)x.z | ((uint64_t)x.w << 32);
+    }
   }
 }
 
-// (256, 5): at least 5 waves per SIMD -- at 97 VGPRs the level ran 4 and the heavy-tail point lost 12 %
-// (profiles/r4bis_heavy_tail_bisect.jsonl)
+// (256, 4): 4 workgroups per CU fit the LDS (~36 KB each)
 template <int K>
-__global__ __launch_bounds__(256, 5) void k_ms_level(DevSnap s, MsView v, int L, int cur) {
+__global__ __launch_bounds__(256, 4) void k_ms_level(DevSnap s, MsView v, int L, int cur) {
   constexpr uint32_t TE = ms_tile_edges(K);
-  __shared__ uint64_t s_beg[TE + 2], s_f[TE + 2][K], s_pm[TE + 2][K], s_em[TE + 2][K], s_many[TE + 2][K];
-  __shared__ uint32_t s_g[TE + 2], s_rb[TE + 2];
+  __shared__ uint64_t s_want[TE + 2][K], s_em[TE + 2][K];
+  __shared__ uint64_t s_beg[TE + 2];
+  __shared__ uint32_t s_g[TE + 2], s_rb[TE + 2], s_gm[TE + 2];
   __shared__ uint64_t s_j0, s_cnt;
   if (v.ctl->overflow) return;
   const int nx = cur ^ 1;
@@ -275,7 +272,9 @@ __global__ __launch_bounds__(256, 5) void k_ms_level(DevSnap s, MsView v, int L,
   }
   const uint32_t n = v.n;
   const int h0 = min(L, MS_HOPS - 1), h1 = min(L + 1, MS_HOPS - 1);
-  const uint32_t my_e = threadIdx.x / K, k = threadIdx.x % K;
+  const uint32_t want_st = (uint32_t)L + 2;
+  // work counters (kg_stats ms_edges_loaded / ms_words_active): per lane, one atomic per wave at the end
+  unsigned long long c_eload = 0, c_wact = 0;
   for (uint64_t t0 = (uint64_t)blockIdx.x * TE; t0 < total; t0 += (uint64_t)gridDim.x * TE) {
     const uint64_t t1 = t0 + TE < total ? t0 + TE : total;
     if (threadIdx.x == 0) {
@@ -301,57 +300,89 @@ __global__ __launch_bounds__(256, 5) void k_ms_level(DevSnap s, MsView v, int L,
         s_beg[i] = v.ex[cur][q];
         s_rb[i] = v.erb[cur][q];
         s_g[i] = g;
+        s_gm[i] = v.gmany[g];
       }
-      s_f[i][kk] = v.fr[cur][((size_t)g * n + v.en[cur][q]) * K + kk] & v.em[((size_t)g * MS_HOPS + h0) * K + kk] &
-                   ~v.hit[(size_t)g * K + kk];
-      s_pm[i][kk] = v.pm[((size_t)g * MS_HOPS + h1) * K + kk];
+      // the queries of the word that reach the child first at hop L+1 and may still probe there (a
+      // later arrival has less rest depth: its probe and expansion are subsets of the first one's)
+      s_want[i][kk] = v.fr[cur][((size_t)g * n + v.en[cur][q]) * K + kk] & v.em[((size_t)g * MS_HOPS + h0) * K + kk] &
+                      ~v.hit[(size_t)g * K + kk] & v.pm[((size_t)g * MS_HOPS + h1) * K + kk];
       s_em[i][kk] = v.em[((size_t)g * MS_HOPS + h1) * K + kk];
-      s_many[i][kk] = v.many[(size_t)g * K + kk];
     }
     __syncthreads();
-    // two edges per lane group: e and e + TE / 2
-    uint64_t want[2] = {0ull, 0ull};
-    uint32_t ent[2] = {0u, 0u};
-    AdjX x[2];
-#pragma unroll
-    for (int h = 0; h < 2; h++) {
-      const uint64_t e = t0 + my_e + (uint64_t)h * (TE / 2);
-      if (e < t1) {
-        uint32_t lo = 0, hi = (uint32_t)cnt;
-        while (hi - lo > 1) {
-          const uint32_t mid = (lo + hi) >> 1;
-          if (s_beg[mid] <= e) lo = mid;
-          else hi = mid;
-        }
-        ent[h] = lo;
-        // the queries of the word that reach the child first at hop L+1 and may still probe there (a
-        // later arrival has less rest depth: its probe and expansion are subsets of the first one's)
-        want[h] = s_f[lo][k] & s_pm[lo][k];
+    const uint64_t e = t0 + threadIdx.x;
+    bool app = false;
+    uint32_t child = 0, cb = 0, clen = 0, g = 0;
+    if (threadIdx.x < TE && e < t1) {
+      uint32_t lo = 0, hi = (uint32_t)cnt;
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (s_beg[mid] <= e) lo = mid;
+        else hi = mid;
       }
-      // unconditional load (adjx[0] exists), predicated afterwards: both edges' gathers in flight at once
-      x[h] = s.adjx[want[h] ? s_rb[ent[h]] + (uint32_t)(e - s_beg[ent[h]]) : 0u];
-    }
-    // the child's masks and hop stamp, both edges' loads issued before either is used
-    uint64_t vis0[2], tg0[2];
-    uint32_t st0[2];
+      g = s_g[lo];
+      uint64_t want[K];
+      uint64_t any = 0;
 #pragma unroll
-    for (int h = 0; h < 2; h++) {
-      const uint32_t g = s_g[ent[h]], c = want[h] ? x[h].node : 0u;
-      const size_t at = ((size_t)g * n + c) * K + k;
-      vis0[h] = v.vis[at];
-      tg0[h] = v.tg[at];
-      st0[h] = v.stamp[(size_t)g * n + c];
-    }
+      for (int k = 0; k < K; k++) {
+        want[k] = s_want[lo][k];
+        any |= want[k];
+        c_wact += want[k] ? 1u : 0u;
+      }
+      if (any) {
+        c_eload++;
+        const AdjX x = s.adjx[s_rb[lo] + (uint32_t)(e - s_beg[lo])];
+        const size_t base = ((size_t)g * n + x.node) * K;
+        uint64_t vis0[K];
+        ms_load_words<K>(v.vis + base, vis0);
+        const uint32_t st0 = v.stamp[(size_t)g * n + x.node];
+        uint64_t nw[K], anynw = 0;
 #pragma unroll
-    for (int h = 0; h < 2; h++) {
-      bool app = false;
-      uint32_t child = 0, cb = 0, clen = 0;
-      const uint32_t g = s_g[ent[h]];
-      if (want[h])
-        ms_edge<K>(s, v, n, L, nx, want[h], s_many[ent[h]][k], s_em[ent[h]][k], g, k, x[h], app, child, cb, clen,
-                   vis0[h], tg0[h], st0[h]);
-      ms_append<TE>(v, nx, app, g, child, cb, clen);
+        for (int k = 0; k < K; k++) {
+          nw[k] = want[k] & ~vis0[k];
+          anynw |= nw[k];
+        }
+        if (anynw) {
+          // checkDirect: TG bits for subjects with few holders, dset probes for popular ones
+          uint64_t many[K];
+#pragma unroll
+          for (int k = 0; k < K; k++) many[k] = s_gm[lo] ? v.many[(size_t)g * K + k] : 0ull;
+          uint64_t tg0[K];
+          ms_load_words<K>(v.tg + base, tg0);
+          const bool can_expand = adjx_len16(x) != 0;
+          uint64_t anyex = 0;
+#pragma unroll
+          for (int k = 0; k < K; k++) {
+            if (!nw[k]) continue;
+            atomicOr((unsigned long long*)&v.vis[base + k], (unsigned long long)nw[k]);
+            uint64_t hits = nw[k] & ~many[k] & tg0[k];
+            for (uint64_t m = nw[k] & many[k]; m; m &= m - 1) {
+              const uint32_t subj = v.qs[(size_t)g * 64 * K + k * 64 + __builtin_ctzll(m)];
+              if (sig_maybe(x.lsig, x.sig, subj_sig(subj)) && dset_probe(s, x.node, subj)) hits |= m & (~m + 1);
+            }
+            if (hits) atomicOr((unsigned long long*)&v.hit[(size_t)g * K + k], (unsigned long long)hits);
+            // expansion: those that may expand it
+            const uint64_t ex = can_expand ? (nw[k] & s_em[lo][k]) : 0ull;
+            if (ex) atomicOr((unsigned long long*)&v.fr[nx][base + k], (unsigned long long)ex);
+            anyex |= ex;
+          }
+          if (anyex) {
+            app = st0 < want_st && atomicMax(&v.stamp[(size_t)g * n + x.node], want_st) < want_st;
+            child = x.node;
+            cb = x.begin;
+            clen = adjx_len(s, x);
+          }
+        }
+      }
     }
+    ms_append<TE>(v, nx, app, g, child, cb, clen);
+  }
+  for (int off = 32; off; off >>= 1) {
+    c_eload += __shfl_xor(c_eload, off, 64);
+    c_wact += __shfl_xor(c_wact, off, 64);
+  }
+  if (lane_id() == 0 && c_wact) {
+    atomicAdd(&v.ctl->eload, c_eload);
+    atomicAdd(&v.ctl->wact, c_wact);
   }
 }
 
@@ -383,7 +414,7 @@ size_t ms_group_bytes(uint32_t n, int K) {
 // Pool layout for G groups of K words and level buffers of `cap` entries.
 int ms_layout(GridPool* P, uint32_t n, int K, uint32_t G, uint64_t cap, MsView* v) {
   const size_t gn = (size_t)G * n * K * 8;
-  const size_t need = 4 * gn + (size_t)G * n * 4 + (size_t)G * K * (16 + 2 * MS_HOPS * 8 + 64 * 12) +
+  const size_t need = 4 * gn + (size_t)G * n * 4 + (size_t)G * K * (16 + 2 * MS_HOPS * 8 + 64 * 12) + (size_t)G * 4 + 8 +
                       2 * (cap * (4 + 4 + 4 + 8) + MS_TILE_CAP * 4) + sizeof(MsCtl) + 8192;
   if (need > P->bytes) {
     P->release();
@@ -406,6 +437,8 @@ int ms_layout(GridPool* P, uint32_t n, int K, uint32_t G, uint64_t cap, MsView* 
   p += (size_t)G * K * 8;
   v->many = (uint64_t*)p;
   p += (size_t)G * K * 8;
+  v->gmany = (uint32_t*)p;
+  p += ((size_t)G * 4 + 7) & ~size_t(7);
   v->pm = (uint64_t*)p;
   p += (size_t)G * MS_HOPS * K * 8;
   v->em = (uint64_t*)p;
@@ -488,8 +521,10 @@ int ms_rounds(Snapshot* s, Workspace* w, const RQuery* rq, const uint32_t* qlist
       HIPC(hipGetLastError());
       for (int L = 0; L < levels; L++) {
         const int cur = L & 1;
+        w->lev_mark(stream, false, 2);
         hipLaunchKernelGGL(k_ms_level<K>, dim3(lgrid), dim3(256), 0, stream, s->ds, v, L, cur);
         HIPC(hipGetLastError());
+        w->lev_mark(stream, true, 2);
         hipLaunchKernelGGL(k_ms_clear<K>, dim3((uint32_t)s->n_cu * 4), dim3(256), 0, stream, v, cur);
         HIPC(hipGetLastError());
         HIPC(hipMemsetAsync(&v.ctl->packed[cur], 0, 8, stream));
@@ -509,6 +544,8 @@ int ms_rounds(Snapshot* s, Workspace* w, const RQuery* rq, const uint32_t* qlist
     if (gs) {
       gs->rows += h.logged;
       gs->edges += h.edges;
+      gs->ms_eload += h.eload;
+      gs->ms_wact += h.wact;
     }
     if (h.overflow) {
       if (G == 1) {  // one group alone overflows the level buffers: the per-query rounds take the list

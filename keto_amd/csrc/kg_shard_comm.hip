@@ -77,6 +77,7 @@ struct ShardComm {
   std::mutex host_mu;    // kg_check_batch (host buffers): one batch at a time through dq / dout / derr
   uint64_t st[16] = {};  // kg_shard_comm_stats (kg_shard_comm_stats_ex: all 16)
   hipEvent_t ev[2] = {nullptr, nullptr};
+  void* xbufs = nullptr;  // one rank's local-first expand: device buffers kept across calls (under mu)
   ~ShardComm();
 };
 
@@ -84,6 +85,7 @@ ShardComm::~ShardComm() {
   if (device >= 0) hipSetDevice(device);
   if (run) hipStreamSynchronize(run);
   if (nccl) ncclCommDestroy(nccl);
+  if (xbufs) expand_bufs_free(xbufs);
   hipFree(buf[0]);
   hipFree(buf[1]);
   hipFree(recv);
@@ -390,6 +392,12 @@ static int comm_setup(Snapshot* s, ShardComm* c) {
     (void)hipGetLastError();
     dmeta = nullptr;
   }
+  // a host-memory transport stages the all-reduce through pinned memory: taken now, so a rank that
+  // cannot have it makes every rank skip instead of failing alone inside the collective below
+  if (dmeta && c->t.host_memory && !pinned_at_least(c, nn * 8)) {
+    hipFree(dmeta);
+    dmeta = nullptr;
+  }
   const uint64_t skip = dmeta ? 0 : 1;
   uint64_t v[4] = {bad, words, nn, 0xFFFFFFFFull - nn};
   v[3] |= skip << 40;
@@ -424,11 +432,17 @@ static int comm_setup(Snapshot* s, ShardComm* c) {
   }
   if (dmeta) {
     // one max all-reduce of 8 B per node: each node's (row length, signature) word is non-zero on its
-    // owner only.  A failed step leaves this rank on the nowner path: more records, the same answers
+    // owner only.  Every rank reaches both collectives whatever its own step did: a rank whose local
+    // step failed contributes zeros and a failure flag, and the second all-reduce makes every rank skip
+    // the metadata together (the nowner path: more records, the same answers).  Only a failed
+    // collective (the transport itself) or a failed apply on this rank fails the bind.
     uint64_t* d = dmeta;
-    int rc = shard_meta_local(s, d, c->run);
-    if (!rc) rc = x_allreduce_max(c, reinterpret_cast<unsigned long long*>(d), nn);
-    if (!rc) rc = shard_meta_apply(s, d, c->run);  // synchronises
+    const int lrc = shard_meta_local(s, d, c->run);
+    if (lrc && hipMemsetAsync(d, 0, nn * 8, c->run) != hipSuccess) (void)hipGetLastError();
+    int rc = x_allreduce_max(c, reinterpret_cast<unsigned long long*>(d), nn);
+    uint64_t failed = lrc != 0;
+    if (!rc) rc = h_allreduce_max(c, &failed, 1);
+    if (!rc && !failed) rc = shard_meta_apply(s, d, c->run);  // synchronises
     else (void)hipStreamSynchronize(c->run);
     hipFree(d);
     if (rc) return rc;
@@ -648,11 +662,9 @@ int shard_expand(Snapshot* s, const kg_set* roots, size_t n, int32_t gdepth, kg_
   HIPC(hipSetDevice(s->device));
   if (gdepth < 1) gdepth = 5;  // config.schema.json:308-315 default
   if (c->world == 1 && !s->shard_force_exchange && s->shard_local) {
-    // one rank holds every row: nothing to gather (local-first, as shard_check)
-    void* bufs = nullptr;
-    const int rc = expand_batch(s, s->stream, &bufs, roots, n, gdepth, out);
-    if (bufs) expand_bufs_free(bufs);
-    return rc;
+    // one rank holds every row: nothing to gather (local-first, as shard_check); the buffers stay on
+    // the comm for the next call (held under c->mu, like every other comm buffer)
+    return expand_batch(s, s->stream, &c->xbufs, roots, n, gdepth, out);
   }
   std::vector<std::pair<uint32_t, uint32_t>> starts;
   for (size_t i = 0; i < n; i++)
@@ -977,7 +989,10 @@ int shard_check(Snapshot* s, ShardComm* c, const kg_query* d_q, size_t n, int32_
       const bool bucket_over = h[0] || s->shard_force_overflow;
       // a run whose visited table overflowed too dropped records for that reason as well, so its
       // bucket counts are lower bounds: only runs without it count against the bucket-rerun bound
-      if (bucket_over && !h[1] && run++ >= s->shard_max_reruns) {
+      // an exchange downstream of one that dropped records reports a lower bound, so each rerun may
+      // fix one more exchange: the default (0) allows max(4, L + 1) reruns
+      const uint32_t max_reruns = s->shard_max_reruns ? s->shard_max_reruns : std::max<uint32_t>(4, xch ? (uint32_t)L + 1 : 0u);
+      if (bucket_over && !h[1] && run++ >= max_reruns) {
         drop_buffers(c);
         return set_error(KG_ERR_RESOURCE_CODE,
                          "sharded batch still overflows after %u reruns (bucket %zu records per destination, "

@@ -58,7 +58,30 @@ struct Workspace {
   void* interp_pool = nullptr;
   size_t interp_pool_bytes = 0;
   uint64_t interp_layout = 0;  // (pass-2 slots, pass-1 slots, list cap) the pool was last laid out for
-  hipEvent_t ev[4] = {};  // batch timing events (created on first use)
+  hipEvent_t ev[6] = {};  // batch timing events (created on first use)
+  // tail-tier level launches (k_grid_level / k_ms_level) of a batch with stats: one event pair each,
+  // summed in check_batch_end (kg_stats::tail_ms); launches past LEV_EV are counted, not timed
+  static constexpr int LEV_EV = 64;
+  hipEvent_t lev_ev[2 * LEV_EV] = {};
+  int lev_n = 0, lev_kind = 0;
+  uint64_t lev_launches = 0;
+  bool lev_on = false;
+  // record the start (end = false) or end (end = true) of one level launch
+  void lev_mark(hipStream_t st, bool end, int kind) {
+    if (!lev_on) return;
+    if (!end) {
+      lev_kind = kind;
+      lev_launches++;
+    }
+    if (lev_n >= LEV_EV) return;
+    hipEvent_t& e = lev_ev[2 * lev_n + (end ? 1 : 0)];
+    if (!e && hipEventCreate(&e) != hipSuccess) {
+      (void)hipGetLastError();
+      e = nullptr;
+    }
+    if (e) (void)hipEventRecord(e, st);
+    if (end) lev_n++;
+  }
   hipEvent_t sync_ev = nullptr;  // blocking-sync event (host-buffer batches wait on it asleep)
   int wait(hipStream_t st, bool blocking);  // waits for st: spin (hipStreamSynchronize) or asleep
   void* pinned = nullptr;  // 64 KiB of pinned host memory for small device->host readbacks
@@ -263,7 +286,7 @@ struct Snapshot {
   int shard_force_exchange = 0;  // kg_snapshot_tune("shard_force_exchange"): one rank runs the N > 1 protocol
   int shard_local = 1;           // kg_snapshot_tune("shard_local"): one rank runs the replica tier chain
   int shard_remote_meta = 1;     // kg_snapshot_tune("shard_remote_meta"): bind-time remote child metadata (DevSnap)
-  uint32_t shard_max_reruns = 4;  // kg_snapshot_tune("shard_max_reruns"): overflow reruns per batch
+  uint32_t shard_max_reruns = 0;  // kg_snapshot_tune("shard_max_reruns"): overflow reruns per batch (0: max(4, exchanges))
   uint64_t shard_max_bytes = 0;   // kg_snapshot_tune("shard_max_bytes"): bucket buffers cap (0: 1/4 of free HBM)
   int shard_force_overflow = 0;   // kg_snapshot_tune("shard_force_overflow"): tests -- every run overflows
   uint32_t rel_span = 0;          // 1 + the largest relation id of any node (0: not yet computed)
@@ -289,6 +312,8 @@ struct Snapshot {
   // hash pass directly (0); "expand_skip_lds" (tests): every root skips the LDS pass
   int expand_gw = 1;
   int expand_skip_lds = 0;
+  // k_expand_gw: longest wait (us) of a large slot for a small slot's hand-on before it gives its ticket up
+  uint32_t expand_gw_wait_us = 100000;
   uint32_t stream_steal = 4;   // kg_snapshot_tune("stream_steal"): XCD ranges a k_stream4 wave dequeues from (1..8)
   uint32_t stream_chunk = 64;  // kg_snapshot_tune("stream_chunk"): k_stream4 queries per dequeue (1..64)
   // Occupancy defaults (library-wide, measured with several batches in flight, the way a server keeps

@@ -327,6 +327,8 @@ Workspace::~Workspace() {
   if (pinned) hipHostFree(pinned);
   for (auto& e : ev)
     if (e) hipEventDestroy(e);
+  for (auto& e : lev_ev)
+    if (e) hipEventDestroy(e);
 }
 
 void* Workspace::host_buf(size_t bytes) {

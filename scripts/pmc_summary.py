@@ -40,18 +40,31 @@ def main():
     ap.add_argument("--preset", type=int, default=0)
     ap.add_argument("--inflight", type=int, default=4)
     ap.add_argument("--skip", type=int, default=1, help="leading (warmup) dispatches to drop")
+    ap.add_argument("--anchor", default="",
+                    help="a kernel chain: bytes of every dispatch matching --kernel, per dispatch of this kernel "
+                         "(one per call), e.g. --kernel k_expand --anchor k_expand_lds (no dispatch skipped)")
     ap.add_argument("--out")
     a = ap.parse_args()
-    fetch = per_dispatch(a.fetch, a.kernel, "FETCH_SIZE")[a.skip:]
-    write = per_dispatch(a.write, a.kernel, "WRITE_SIZE")[a.skip:]
-    if not fetch or not write:
-        raise SystemExit(f"no {a.kernel} dispatches with FETCH_SIZE/WRITE_SIZE under {a.fetch} / {a.write}")
-    f_kib = sum(fetch) / len(fetch)
-    w_kib = sum(write) / len(write)
+    if a.anchor:
+        fetch = per_dispatch(a.fetch, a.kernel, "FETCH_SIZE")
+        write = per_dispatch(a.write, a.kernel, "WRITE_SIZE")
+        calls_f = len(per_dispatch(a.fetch, a.anchor, "FETCH_SIZE"))
+        calls_w = len(per_dispatch(a.write, a.anchor, "WRITE_SIZE"))
+        if not calls_f or not calls_w:
+            raise SystemExit(f"no {a.anchor} dispatches under {a.fetch} / {a.write}")
+        f_kib = sum(fetch) / calls_f
+        w_kib = sum(write) / calls_w
+    else:
+        fetch = per_dispatch(a.fetch, a.kernel, "FETCH_SIZE")[a.skip:]
+        write = per_dispatch(a.write, a.kernel, "WRITE_SIZE")[a.skip:]
+        if not fetch or not write:
+            raise SystemExit(f"no {a.kernel} dispatches with FETCH_SIZE/WRITE_SIZE under {a.fetch} / {a.write}")
+        f_kib = sum(fetch) / len(fetch)
+        w_kib = sum(write) / len(write)
     out = {
         "kernel": a.kernel, "tuples": int(a.tuples), "batch": a.batch, "preset": a.preset,
         "inflight": a.inflight,
-        "dispatches": {"fetch": len(fetch), "write": len(write)},
+        "dispatches": {"fetch": len(fetch), "write": len(write)}, "anchor": a.anchor or None,
         "fetch_size_kib_raw": f_kib, "write_size_kib_raw": w_kib,
         "hbm_bytes_per_launch": (2 * f_kib + w_kib) * 1024.0,
         "correction": "2 x FETCH_SIZE + WRITE_SIZE (MI355X_MICROARCH.md HBM section, gfx950)",

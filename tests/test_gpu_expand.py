@@ -121,14 +121,17 @@ def test_expand_gather_walk_large_slot_and_cycles():
     reg = Registry(tuples, [])
     it = reg.interner
     oracle = Oracle(it.tuples_array(tuples), it.wildcard_rel)
-    for gw in (1, 0):
+    # (expand_gw, expand_gw_wait_us): default; large slots that never wait (their tickets are
+    # abandoned and the roots go to the hash pass); no gather-walk
+    for gw, wait in ((1, 100000), (1, 0), (0, 100000)):
         reg.snapshot.tune("expand_gw", gw)
+        reg.snapshot.tune("expand_gw_wait_us", wait)
         ex = reg.expand_engine()
         for gmax in (2, 3, 4, 6):
             ex.config.max_read_depth = gmax
             got = ex.build_tree(SubjectSet("g", "root", "m"), 0)
             exp = oracle_tree(oracle.expand(it.ns_id("g"), it.obj_id("root"), it.rel_id("m"), 0, gmax), it)
-            assert got == exp, (gw, gmax)
+            assert got == exp, (gw, wait, gmax)
 
 
 def _cmp_records(exp, g, what):
@@ -146,9 +149,10 @@ def _cmp_records(exp, g, what):
     assert e2.shape == g2.shape and (e2 == g2).all(), what
 
 
-@pytest.mark.parametrize("n_tuples,gmax,gw,skip", [(300_000, 5, 1, 0), (1_000_000, 3, 1, 0), (300_000, 5, 1, 1),
-                                                    (300_000, 5, 0, 0)])
-def test_c5_hot_group_roots_vs_oracle(n_tuples, gmax, gw, skip):
+@pytest.mark.parametrize("n_tuples,gmax,gw,skip,wait", [(300_000, 5, 1, 0, 100000), (1_000_000, 3, 1, 0, 100000),
+                                                         (300_000, 5, 1, 1, 100000), (300_000, 5, 0, 0, 100000),
+                                                         (300_000, 5, 1, 0, 0), (300_000, 5, 1, 0, 50)])
+def test_c5_hot_group_roots_vs_oracle(n_tuples, gmax, gw, skip, wait):
     """Config C5's workload at reduced size: the generator's most popular group#member roots (the
     roots bench.py --mode expand times), expanded at the global depth, against the oracle's
     BuildTree on the snapshot's own rows -- same pre-order, same child order, every root."""
@@ -157,6 +161,7 @@ def test_c5_hot_group_roots_vs_oracle(n_tuples, gmax, gw, skip):
     snap = Snapshot.synthetic(n_tuples, seed=20250131)
     snap.tune("expand_gw", gw)
     snap.tune("expand_skip_lds", skip)
+    snap.tune("expand_gw_wait_us", wait)  # 0 / 50 us: large slots give their tickets up
     roots = hot_group_roots(snap.synth_ids(), 1500)
     ex = ExpandEngine(snap)
     ex.config.max_read_depth = gmax
