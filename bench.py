@@ -55,8 +55,6 @@ def parse(argv=None):
                          "DESIGN.md 7f)")
     ap.add_argument("--global-depth", type=int, default=10)
     ap.add_argument("--seed", type=int, default=20250131)
-    ap.add_argument("--stream-gate", type=int, default=0,
-                    help="kg_snapshot_tune stream_gate: k_stream4 launches of different batches at once (0 = no cap)")
     ap.add_argument("--stream-ecap", type=int, default=512, help="kg_snapshot_tune stream_ecap (stream-tier edges per query, 0 = none)")
     ap.add_argument("--sharded-steps", type=int, default=20,
                     help="check mode: timed batches of the hash-sharded sub-line (the C4 engine through "
@@ -93,17 +91,11 @@ def parse(argv=None):
     ap.add_argument("--shard-back-budget", type=int, default=1 << 14,
                     help="kg_snapshot_tune shard_back_budget (reverse edges per query and rank before the final "
                          "forward phase takes it)")
-    ap.add_argument("--shard-wgs", type=int, default=0,
-                    help="kg_snapshot_tune shard_wgs: sharded level kernel workgroups per CU (0: library default)")
-    ap.add_argument("--shard-pack", type=int, default=-1,
-                    help="kg_snapshot_tune shard_pack: packed local records in the one-rank level loop (-1 library default)")
     ap.add_argument("--shard-heavy", type=int, default=-1,
                     help="kg_snapshot_tune shard_heavy: set rows longer than this are expanded grid-wide (k_shard_heavy; "
                          "0: every expansion; -1: the library default)")
     ap.add_argument("--shard-vis", type=int, default=0,
                     help="kg_snapshot_tune shard_vis: log2 of the sharded mode's (query, node) visited table (0: library default)")
-    ap.add_argument("--shard-vis-mode", type=int, default=0,
-                    help="kg_snapshot_tune shard_vis_mode (sharded (query, node) dedup: 0 exact CAS table, 1 lossy cache)")
     ap.add_argument("--packed", type=int, default=0,
                     help="check mode: the headline's queries as 16-B kg_query_packed in HBM through "
                          "kg_check_batch_packed_device (k_resolve reads them itself) instead of 28-B kg_query "
@@ -112,17 +104,8 @@ def parse(argv=None):
     ap.add_argument("--shard-remote-meta", type=int, default=1,
                     help="kg_snapshot_tune shard_remote_meta (N > 1: owners' row length + signature of remote "
                          "children in adjx at bind time, so remote leaves that cannot hit are never sent)")
-    ap.add_argument("--device-sync", type=int, default=1,
-                    help="kg_snapshot_tune device_sync (1: kg_check_batch_device waits asleep instead of spinning)")
-    ap.add_argument("--host-sync", type=int, default=1,
-                    help="kg_snapshot_tune host_sync (--mode host: 1 = kg_check_batch waits asleep, 0 = spins)")
-    ap.add_argument("--resolve-unheld", type=int, default=1,
-                    help="kg_snapshot_tune resolve_unheld (1: k_resolve skips the node map for subjects no row holds; "
-                         "2: reads the holder bit only for queries headed for the stream tier)")
     ap.add_argument("--stream-steal", type=int, default=4,
                     help="kg_snapshot_tune stream_steal (XCD ranges a k_stream4 wave dequeues from, 1..8)")
-    ap.add_argument("--stream-chunk", type=int, default=64,
-                    help="kg_snapshot_tune stream_chunk (k_stream4 queries per dequeue, 1..64)")
     ap.add_argument("--grid-wgs", type=int, default=None,
                     help="kg_snapshot_tune grid_wgs (k_grid_level WGs per CU; default 2 for C2/C4, 4 for C3: "
                          "profiles/r4w_grid_stream_wgs_ab.jsonl)")
@@ -135,19 +118,14 @@ def parse(argv=None):
                     help="kg_snapshot_tune grid_ms_bytes: MS-BFS mask budget per workspace in bytes (0: library default)")
     ap.add_argument("--grid-ms-tg-cap", type=int, default=256,
                     help="kg_snapshot_tune grid_ms_tg_cap: holders above which MS-BFS probes a query's subject in dset")
-    ap.add_argument("--grid-bidir", type=int, default=0,
-                    help="kg_snapshot_tune grid_bidir: grid slots whose subject has <= this many holders "
-                         "alternate forward and backward turns (0: forward only)")
     ap.add_argument("--stream-wgs", type=int, default=None,
                     help="kg_snapshot_tune stream_wgs (k_stream4 WGs per CU; default 2 for C2/C4 -- LDS left to the "
                          "other batches' tail tiers, profiles/r4w_grid_stream_wgs_ab.jsonl -- and 3 for C3)")
-    ap.add_argument("--back", type=int, default=2, help="kg_snapshot_tune back (1 backward tier wave+WG widths, 2 wave width only, 0 off)")
     ap.add_argument("--back-wgs", type=int, default=None,
                     help="kg_snapshot_tune back_wgs (k_back WGs per CU; default 3 for C2/C4 with 4 batches in "
                          "flight, 1 for C3 with 6: profiles/r4s_back_wgs_ab.jsonl, r2bwc3_back_wgs_c3_ab.jsonl)")
     ap.add_argument("--back-edges", type=int, default=0,
                     help="kg_snapshot_tune back_edges (k_back reverse-edge budget per query, 0 = library default 2^12)")
-    ap.add_argument("--interp-wgs", type=int, default=6, help="kg_snapshot_tune interp_wgs (rewrite-path LDS pass WGs per CU)")
     ap.add_argument("--hw-queues", type=int, default=None,
                     help="HIP hardware queues for this process (GPU_MAX_HW_QUEUES, 1..32; 0 = HIP's default, 4; "
                          "default 16): streams map onto queues round-robin as they are created, and in-flight "
@@ -199,8 +177,6 @@ def parse(argv=None):
     ap.add_argument("--roots", type=int, default=100_000, help="expand roots per step (C5)")
     ap.add_argument("--expand-gw", type=int, default=1,
                     help="kg_snapshot_tune expand_gw (1: large expand roots gather their neighbourhood, then walk the copy)")
-    ap.add_argument("--expand-tail", type=int, default=1,
-                    help="kg_snapshot_tune expand_tail (1: passes 2/3 walk with LDS-cached frames; 0: round 2's walk)")
     ap.add_argument("--delta", type=int, default=1000, help="--mode refresh: rows per transaction")
     a = ap.parse_args(argv)
     if a.hw_queues is None:
@@ -223,18 +199,9 @@ def parse(argv=None):
 def apply_tune(snap, a) -> None:
     """The engine knobs of the check bench (tests/test_gpu_check.py::test_bench_tune_set_vs_oracle runs
     the parity test with exactly this set)."""
-    snap.tune("back", a.back)
     snap.tune("stream_ecap", a.stream_ecap)
-    if a.stream_gate:
-        snap.tune("stream_gate", a.stream_gate)
-    if a.resolve_unheld != 1:
-        snap.tune("resolve_unheld", a.resolve_unheld)
-    snap.tune("device_sync", a.device_sync)
     snap.tune("stream_steal", a.stream_steal)
-    if a.stream_chunk != 64:
-        snap.tune("stream_chunk", a.stream_chunk)
     snap.tune("grid_wgs", a.grid_wgs)
-    snap.tune("grid_bidir", a.grid_bidir)
     snap.tune("grid_ms", a.grid_ms)
     snap.tune("grid_ms_words", a.grid_ms_words)
     snap.tune("grid_ms_tg_cap", a.grid_ms_tg_cap)
@@ -245,8 +212,6 @@ def apply_tune(snap, a) -> None:
     if a.back_edges:
         snap.tune("back_edges", a.back_edges)
     snap.tune("grid_reserve", 1)  # a server pays this once at start-up, not inside some request's batch
-    if snap.program is not None and not snap.program.empty:
-        snap.tune("interp_wgs", a.interp_wgs)
 
 
 def bench_expand(a):
@@ -268,7 +233,6 @@ def bench_expand(a):
         dist.init_process_group(a.backend, rank=rank, world_size=world)
     L = _lib.load()
     snap, _ = build_synthetic(a, a.tuples, device=local)
-    snap.tune("expand_tail", a.expand_tail)
     snap.tune("expand_gw", a.expand_gw)
     from keto_amd.synth import hot_group_roots
     roots = hot_group_roots(snap.synth_ids(), a.roots)
@@ -287,7 +251,7 @@ def bench_expand(a):
            "config": {"workload": "C5: %d hot roots @ %.4g tuples (rows), max_read_depth %d" % (a.roots, snap.info()["rows"],
                                                                                             depth),
                       "inflight_per_gpu": P, "hw_queues": a.hw_queues, "parallelism": f"replica{world}",
-                      "expand_tail": a.expand_tail, "expand_gw": a.expand_gw},
+                      "expand_gw": a.expand_gw},
            "tree_nodes_per_step": nodes / a.steps, "tree_nodes_per_s": nodes / el,
            "kernel_ms_per_step": kms / a.steps}
     if off is not None:
@@ -307,8 +271,7 @@ def bench_expand(a):
             walk.append(buf.kernel_ms)
             n_big = int(buf.n_nodes)
             L.kg_tree_free(C.byref(buf))
-        out["largest_root"] = {"records": n_big, "walk_kernel_ms": float(min(walk)),
-                               "expand_tail": a.expand_tail}
+        out["largest_root"] = {"records": n_big, "walk_kernel_ms": float(min(walk))}
     rf = expand_roofline(L, snap, roots, depth, kms / a.steps)
     if rf:
         out["roofline"] = rf
@@ -597,15 +560,10 @@ def bench_sharded(a):
     t_build = time.time() - t_build
     snap.tune("shard_budget", a.shard_budget)
     snap.tune("shard_back_budget", a.shard_back_budget)
-    snap.tune("shard_vis_mode", a.shard_vis_mode)
     if a.shard_vis:
         snap.tune("shard_vis", a.shard_vis)
     if a.shard_heavy >= 0:
         snap.tune("shard_heavy", a.shard_heavy)
-    if a.shard_pack >= 0:
-        snap.tune("shard_pack", a.shard_pack)
-    if a.shard_wgs:
-        snap.tune("shard_wgs", a.shard_wgs)
     B = a.batch
     P = max(1, a.inflight)
     n_distinct = max(P, 2)
@@ -702,8 +660,8 @@ def bench_sharded(a):
            "levels_per_batch": cs["levels"], "backward_levels_per_batch": cs["back_levels"],
            "final_levels_per_batch": cs["final_levels"], "shard_budget": a.shard_budget,
            "host_syncs_per_batch": sum(syncs) / max(1, a.steps),
-           "bucket": cs["bucket"], "shard_back_budget": a.shard_back_budget, "shard_vis_mode": a.shard_vis_mode,
-           "shard_heavy": a.shard_heavy, "shard_pack": a.shard_pack, "records_exchanged_per_batch": recs / a.steps,
+           "bucket": cs["bucket"], "shard_back_budget": a.shard_back_budget,
+           "shard_heavy": a.shard_heavy, "records_exchanged_per_batch": recs / a.steps,
            **({"level_records": cs["level_records"]} if cs["level_records"] else {}),
            "snapshot_build_s": t_build}
     bad = 0
@@ -743,7 +701,6 @@ def bench_host(a):
     devices = list(range(n_dev))
     t_build = time.time()
     snap, _ = build_synthetic(a, a.tuples, devices=devices)
-    snap.tune("host_sync", a.host_sync)
     snap.tune("stream_wgs", a.stream_wgs)
     snap.tune("back_wgs", a.back_wgs)
     snap.tune("grid_wgs", a.grid_wgs)
@@ -845,7 +802,7 @@ def bench_host(a):
            "dtype": "u32", "data": "synthetic (device-generated Drive-like tuple graph, seed %d)" % a.seed,
            "config": {"workload": "C2/C4 generator @ %.3g tuples, %d-check host batches, %d caller threads, "
                                   "max_read_depth %d" % (a.tuples, B, T, a.global_depth),
-                      "replicas": devices, "parallelism": "replicas in one process", "host_sync": a.host_sync},
+                      "replicas": devices, "parallelism": "replicas in one process"},
            "p50_call_ms": float(np.percentile(np.array(lat) * 1e3, 50)),
            "p99_call_ms": float(np.percentile(np.array(lat) * 1e3, 99)),
            "batcher": batcher, "snapshot_build_s": t_build}

@@ -29,7 +29,7 @@ def stale() -> bool:
 
 
 def build(force: bool = False, verbose: bool = False, out: str = LIB, defines=()) -> str:
-    """out / defines: an A/B variant of the library (e.g. keto_amd/lib/ab/x.so with -DKG_NT_RANDOM=1),
+    """out / defines: an A/B variant of the library (e.g. keto_amd/lib/ab/x.so with a -D define),
     loaded by bench.py through KG_LIB_PATH; the in-tree library is built without defines."""
     if out == LIB and not force and not stale():
         return LIB

@@ -402,16 +402,8 @@ int kg_snapshot_materialized(const kg_snapshot* sp, uint64_t* out3) {
 
 static int tune_one(Snapshot* s, const char* key, int64_t value) {
   std::lock_guard<std::mutex> lk(s->mu);
-  if (strcmp(key, "shard_level_occ") == 0) {
-    if (value != 0 && value != 6 && value != 8) return set_error(-2, "shard_level_occ must be 0, 6 or 8");
-    s->shard_level_occ = (int)value;
-    return 0;
-  }
-  if (strcmp(key, "shard_vis_q") == 0) {
-    if (value < 0 || value > 256) return set_error(-2, "shard_vis_q must be in [0, 256]");
-    s->shard_vis_q = (uint32_t)value;
-    return 0;
-  }
+
+
   if (strcmp(key, "shard_vis") == 0) {
     if (value < 10 || value > 34) return set_error(-2, "shard_vis must be in [10, 34]");
     s->shard_vis_log2 = (int)value;
@@ -422,11 +414,7 @@ static int tune_one(Snapshot* s, const char* key, int64_t value) {
     s->shard_bucket0 = (uint32_t)value;
     return 0;
   }
-  if (strcmp(key, "stream_gate") == 0) {
-    if (value < 0 || value > 8) return set_error(-2, "stream_gate must be in [0, 8]");
-    s->stream_gate = (int)value;
-    return 0;
-  }
+
   if (strcmp(key, "shard_force_exchange") == 0) {
     if (value < 0 || value > 1) return set_error(-2, "shard_force_exchange must be 0 or 1");
     s->shard_force_exchange = (int)value;
@@ -457,11 +445,7 @@ static int tune_one(Snapshot* s, const char* key, int64_t value) {
     s->shard_force_overflow = (int)value;
     return 0;
   }
-  if (strcmp(key, "shard_pack") == 0) {
-    if (value < 0 || value > 1) return set_error(-2, "shard_pack must be 0 or 1");
-    s->shard_pack = (int)value;
-    return 0;
-  }
+
   if (strcmp(key, "stream_ecap") == 0) {
     if (value < 0 || value > 0xFFFFFFFFll) return set_error(-2, "stream_ecap must be in [0, 2^32)");
     s->stream_ecap = (uint32_t)value;
@@ -472,51 +456,27 @@ static int tune_one(Snapshot* s, const char* key, int64_t value) {
     s->shard_budget = (uint32_t)value;
     return 0;
   }
-  if (strcmp(key, "shard_wgs") == 0) {
-    if (value < 1 || value > 64) return set_error(-2, "shard_wgs must be in [1, 64]");
-    s->shard_wgs = (uint32_t)value;
-    return 0;
-  }
+
   if (strcmp(key, "shard_heavy") == 0) {
     if (value < 0 || value > 0xFFFFFFFFll) return set_error(-2, "shard_heavy must be in [0, 2^32)");
     s->shard_heavy = (uint32_t)value;
     return 0;
   }
-  if (strcmp(key, "shard_vis_mode") == 0) {
-    if (value < 0 || value > 1) return set_error(-2, "shard_vis_mode must be 0 or 1");
-    s->shard_vis_mode = (int)value;
-    return 0;
-  }
-  if (strcmp(key, "device_sync") == 0) {
-    if (value < 0 || value > 1) return set_error(-2, "device_sync must be 0 or 1");
-    s->device_sync = (int)value;
-    return 0;
-  }
-  if (strcmp(key, "host_sync") == 0) {
-    if (value < 0 || value > 1) return set_error(-2, "host_sync must be 0 or 1");
-    s->host_sync = (int)value;
-    return 0;
-  }
+
+
+
   if (strcmp(key, "shard_back_budget") == 0) {
     if (value < 0 || value > 0xFFFFFFFFll) return set_error(-2, "shard_back_budget must be in [0, 2^32)");
     s->shard_back_budget = (uint32_t)value;
     return 0;
   }
-  if (strcmp(key, "resolve_unheld") == 0) {
-    if (value < 0 || value > 2) return set_error(-2, "resolve_unheld must be 0, 1 or 2");
-    s->resolve_unheld = (int)value;
-    return 0;
-  }
+
   if (strcmp(key, "stream_steal") == 0) {
     if (value < 1 || value > 8) return set_error(-2, "stream_steal must be in [1, 8]");
     s->stream_steal = (uint32_t)value;
     return 0;
   }
-  if (strcmp(key, "stream_chunk") == 0) {
-    if (value < 1 || value > 64) return set_error(-2, "stream_chunk must be in [1, 64]");
-    s->stream_chunk = (uint32_t)value;
-    return 0;
-  }
+
   if (strcmp(key, "stream_wgs") == 0) {
     if (value < 0 || value > 8) return set_error(-2, "stream_wgs must be in [0, 8]");
     s->stream_wgs = (int)value;
@@ -527,11 +487,7 @@ static int tune_one(Snapshot* s, const char* key, int64_t value) {
     s->grid_wgs = (int)value;
     return 0;
   }
-  if (strcmp(key, "interp_wgs") == 0) {
-    if (value < 1 || value > 8) return set_error(-2, "interp_wgs must be in [1, 8]");
-    s->interp_wgs = (int)value;
-    return 0;
-  }
+
   if (strcmp(key, "interp_cap2") == 0) {
     if (value < 0 || value > (1 << 22)) return set_error(-2, "interp_cap2 must be in [0, 4194304]");
     s->interp_cap2 = (uint32_t)value;
@@ -553,11 +509,7 @@ static int tune_one(Snapshot* s, const char* key, int64_t value) {
     s->expand_gw_wait_us = (uint32_t)value;
     return 0;
   }
-  if (strcmp(key, "expand_tail") == 0) {
-    if (value < 0 || value > 1) return set_error(-2, "expand_tail must be 0 or 1");
-    s->expand_tail = (int)value;
-    return 0;
-  }
+
   if (strcmp(key, "grid_ms") == 0) {
     if (value < 0 || value > 1) return set_error(-2, "grid_ms must be 0 or 1");
     s->grid_ms = (int)value;
@@ -584,12 +536,7 @@ static int tune_one(Snapshot* s, const char* key, int64_t value) {
     s->grid_ms_cap = (uint64_t)value;
     return 0;
   }
-  if (strcmp(key, "grid_bidir") == 0) {
-    // 0 off, 1 on (a slot is bidirectional when its subject has <= 1024 holders), > 1: that holder cap
-    if (value < 0 || value > 0x7FFFFFFF) return set_error(-2, "grid_bidir must be in [0, 2^31)");
-    s->grid_bidir = (int)value;
-    return 0;
-  }
+
   if (strcmp(key, "max_lanes") == 0) {
     if (value < 1 || value > 1024) return set_error(-2, "max_lanes in [1, 1024]");
     {
@@ -609,11 +556,7 @@ static int tune_one(Snapshot* s, const char* key, int64_t value) {
     s->back_wgs = (int)value;
     return 0;
   }
-  if (strcmp(key, "back") == 0) {
-    if (value < 0 || value > 2) return set_error(-2, "back must be 0, 1 or 2");
-    s->back_tier = (int)value;
-    return 0;
-  }
+
   return set_error(-2, "unknown knob '%s'", key);
 }
 
@@ -818,8 +761,9 @@ static int check_host(Snapshot* s, const kg_query* q, const kg_query_packed* pq,
     if (!rc) {
       hipSetDevice(L->device);
       bool reran = false;
-      const bool blocking = s->host_sync != 0;
-      int r2 = kg::check_batch_end(L->rep, L->w, &bp[i], &reran, blocking);
+      // asleep on a blocking-sync event, not spinning (round 2: one spinning core per in-flight batch
+      // competed with the server's threads; the "host_sync" knob was removed in round 6)
+      int r2 = kg::check_batch_end(L->rep, L->w, &bp[i], &reran, true);
       if (!r2 && reran &&  // the grid tier rewrote results after the first copy: copy them again
           (hipMemcpyAsync(L->h_out, L->d_out, m, hipMemcpyDeviceToHost, L->stream) != hipSuccess ||
            (!sp && hipMemcpyAsync(L->h_err, L->d_err, m * 4, hipMemcpyDeviceToHost, L->stream) != hipSuccess)))
@@ -830,7 +774,7 @@ static int check_host(Snapshot* s, const kg_query* q, const kg_query_packed* pq,
         if (!r2 && hipMemcpyAsync(L->h_el, L->d_el, (2 + 2 * pre) * 4, hipMemcpyDeviceToHost, L->stream) != hipSuccess)
           r2 = set_error(-1, "D2H copy failed");
       }
-      if (!r2) r2 = L->w->wait(L->stream, blocking);  // the error text is set by wait()
+      if (!r2) r2 = L->w->wait(L->stream, true);  // the error text is set by wait()
       if (!r2) {
         memcpy(out + b[i], L->h_out, m);
         if (err_code && !sp) memcpy(err_code + b[i], L->h_err, m * 4);

@@ -19,33 +19,12 @@ namespace kg {
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
 // Loads of random lines a batch touches about once (node-map slots, dset buckets, holder-bitmap
-// words, the query records): with KG_NT_RANDOM they carry the non-temporal hint, so they do not
-// push the rows of hot groups out of the XCD's L2 (an A/B knob: built as a separate library).
-#ifndef KG_NT_RANDOM
-#define KG_NT_RANDOM 0
-#endif
-typedef unsigned long long kg_u64x2 __attribute__((ext_vector_type(2)));
+// words, the query records): plain loads.  (A non-temporal variant, built as a separate library with
+// KG_NT_RANDOM, measured 6 % slower in round 5 -- profiles/r5nt_nontemporal_random_ab.jsonl -- and was
+// removed in round 6.)
 template <class T>
 __device__ __forceinline__ T ld_once(const T* p) {
-#if KG_NT_RANDOM
-  static_assert(sizeof(T) % 16 == 0 || sizeof(T) == 4 || sizeof(T) == 8, "16-B multiple, 4 or 8 bytes");
-  T v;
-  if constexpr (sizeof(T) == 4) {
-    const uint32_t x = __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(p));
-    __builtin_memcpy(&v, &x, 4);
-  } else if constexpr (sizeof(T) == 8) {
-    const uint64_t x = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(p));
-    __builtin_memcpy(&v, &x, 8);
-  } else {
-    kg_u64x2 w[sizeof(T) / 16];
-#pragma unroll
-    for (int k = 0; k < (int)(sizeof(T) / 16); k++) w[k] = __builtin_nontemporal_load(reinterpret_cast<const kg_u64x2*>(p) + k);
-    __builtin_memcpy(&v, w, sizeof(T));
-  }
-  return v;
-#else
   return *p;
-#endif
 }
 
 // Node-map lookup: the slot of (ns, rel, obj), or nullptr.  The first slot is passed in when the

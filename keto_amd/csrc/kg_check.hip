@@ -42,7 +42,8 @@ static_assert(ST_N <= 32, "per-XCD counter shards hold 32 counters");
 struct Ctl {
   uint32_t light_count, gen_count, heavy_count, giant_count;
   uint32_t heavy_head, giant_head, gen_head, pad0;  // heavy: the stream tier's hand-ons (k_back's input)
-  uint32_t back_head, fwd_count, back2_head, back2_count;  // k_back<64> / k_back<256> lists and heads
+  uint32_t back_head, fwd_count, back2_head, back2_count;  // (back_head, back2_head, fwd_count unused since round 6)
+  uint32_t bheads[1][8 * 32];  // k_back<64>: dequeue heads of the list's 8 ranges, one 128-B line each
   uint32_t heads[8 * 32];   // per-XCD dequeue heads of the stream tier, one 128-B line each
   uint32_t light8[8 * 32];  // per-XCD shard sizes of the stream tier's work list (k_resolve appends)
   unsigned long long st[ST_N];
@@ -140,21 +141,8 @@ __device__ void block_append_lq(bool pred, const LQuery& v, LQuery* list, uint32
 }
 
 // ------------------------------------------------------------------ k_resolve
-// kg_query is 28 B: seven dword loads (non-temporal under KG_NT_RANDOM, as ld_once)
-__device__ __forceinline__ kg_query ld_once_q(const kg_query* p) {
-#if KG_NT_RANDOM
-  static_assert(sizeof(kg_query) == 28, "seven dwords");
-  uint32_t w[7];
-  const uint32_t* src = reinterpret_cast<const uint32_t*>(p);
-#pragma unroll
-  for (int k = 0; k < 7; k++) w[k] = __builtin_nontemporal_load(src + k);
-  kg_query x;
-  __builtin_memcpy(&x, w, sizeof x);
-  return x;
-#else
-  return *p;
-#endif
-}
+// kg_query is 28 B (one record per thread)
+__device__ __forceinline__ kg_query ld_once_q(const kg_query* p) { return *p; }
 
 // Light-routed queries go to the stream tier as LQuery records in 8 shards of lq_cap entries (shard
 // blockIdx & 7) and skip rq[i]; only queries that later tiers read by index (GENERAL) are written to
@@ -202,10 +190,7 @@ __global__ __launch_bounds__(256) void k_resolve(DevSnap s, const kg_query* __re
     const uint64_t hi = mix64(subj) & s.hmask;
     HSlot h0{};
     uint32_t hw = 0;
-    // no_holder_filter 3 (lazy): the bit is read only by queries still headed for the stream tier
-    // after the node map and the root probe -- about half of them -- instead of by every query
-    const bool lazy = no_holder_filter == 3;
-    if (use_bits && !lazy) hw = subj < s.hbits_n ? ld_once(s.hbits + (subj >> 5)) : 0u;
+    if (use_bits) hw = subj < s.hbits_n ? ld_once(s.hbits + (subj >> 5)) : 0u;
     else if (want_h && !use_bits) h0 = s.hslots[hi];
     // without a namespace program nothing can end as an error, so a subject that no row holds is
     // NotMember whatever the root: the bit (an Infinity-Cache hit) is read first and such a query
@@ -260,11 +245,7 @@ __global__ __launch_bounds__(256) void k_resolve(DevSnap s, const kg_query* __re
       // depth that cannot reach any child (D < 2) finishes the query before the wave tier.  The
       // row signature in the node-map slot rules out most misses without touching dset.
       // an unset holder bit rules the probe out as well (the exact tuple would make subj a holder)
-      // lazy: the bit matters only if the query would go on (d >= 2, a row, no direct hit); its load
-      // is issued beside the root probe's
-      const bool lazy_bit = lazy && use_bits && d >= 2 && rl > 0;
-      if (lazy_bit) hw = subj < s.hbits_n ? ld_once(s.hbits + (subj >> 5)) : 0u;
-      const bool nobit = use_bits && (!lazy || lazy_bit) && !((hw >> (subj & 31)) & 1u);
+      const bool nobit = use_bits && !((hw >> (subj & 31)) & 1u);
       did_probe = subj != NONE && !nobit && sig_maybe(rsig_lo, rsig, subj_sig(subj));
       member = did_probe && dset_probe(s, node, subj);
       if (member || d < 2 || rl == 0) route = ROUTE_DONE;
@@ -334,7 +315,7 @@ __device__ __forceinline__ uint32_t wave_or(uint32_t v) {
 //   * work comes as LQuery records (k_resolve writes the resolved query into the list itself), and a
 //     dequeue is PIPELINED over steps: step t issues the head atomic, step t+1 issues the coalesced
 //     record load, the records are used from step t+2 on -- both round trips hide under the steps'
-//     gathers, so chunks can be small (kg_snapshot_tune "stream_chunk")
+//     gathers, so chunks can be small
 //   * per-slot bookkeeping without returning LDS atomics: a query is finished when the FIFO position
 //     of its last appended entry (s_last, an atomicMax) lies behind the head -- no decrement per
 //     consumed entry and no increment per append; the edge budget is an atomicAdd read once, at the
@@ -628,8 +609,9 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t* wsum, 
 // on to the forward grid tier, which redoes it from scratch (results never depend on the tier).
 // Paths from a LIGHT root only cross rewrite-free nodes (k_resolve's routing), so any backward
 // path that reaches the root is a forward path of the same length.
-// Two widths: k_back<64> runs one query per WAVE (visited hash 512 / list 256 in LDS, 12 queries
-// in flight per CU), its overflow goes to k_back<256>, one query per WORKGROUP (8192 / 4096).
+// k_back<64> runs one query per WAVE (visited hash 512 / list 256 in LDS, 12 queries in flight per
+// CU); its overflow goes to the grid tier.  (Rounds 2-5 also built a workgroup-per-query width,
+// k_back<256>, behind it -- an A/B knob that never beat this chain; the template keeps W generic.)
 template <int W>
 struct BackCfg;
 // EDGES: reverse edges one query may read here.  A level that reaches hub groups reads their whole
@@ -642,11 +624,6 @@ template <>
 struct BackCfg<64> {
   static constexpr uint32_t VLOG2 = 9, CAP = 256;  // larger caps only lengthen the tail (1024: -9 % checks/s)
   static constexpr uint32_t EDGES = 1u << 12;
-};
-template <>
-struct BackCfg<256> {
-  static constexpr uint32_t VLOG2 = 13, CAP = 4096;
-  static constexpr uint32_t EDGES = 1u << 17;
 };
 
 template <int W>
@@ -708,15 +685,29 @@ __global__ __launch_bounds__(256) void k_back(DevSnap s, const RQuery* __restric
   const int t = threadIdx.x % W;  // thread within the query group
   const uint32_t qcount = *qcount_p;
   unsigned long long st_rows = 0, st_edges = 0, st_done = 0;
-  // the first query of every group is static (group g takes g); later ones are dequeued past the
-  // groups' count, so groups beyond the list and the list's end cost no atomic on the one hot word
+  // the first query of every group is static (group g takes g); the rest of the list is cut into 8
+  // ranges, each dequeued through its own head on a line of its own (qhead[r * 32]): a group starts at
+  // its XCD's range and moves on when that one is dry.  One hot word saturates near 90 M dequeues/s
+  // (MI355X_MICROARCH.md "dequeue"): ~9 k dequeues per C3 batch on one word were ~100 us of k_back.
   const uint32_t n_groups = gridDim.x * (256 / W), g0 = blockIdx.x * (256 / W) + threadIdx.x / W;
+  const uint32_t rest = qcount > n_groups ? qcount - n_groups : 0u, rlen = (rest + 7) / 8;
+  uint32_t r_at = blockIdx.x & 7, r_tried = 0;
   for (bool first = true;; first = false) {
     if (first) {
       if (t == 0) L.qi = g0;
     } else {
-      if (n_groups >= qcount) break;  // the static round took every query
-      if (t == 0) L.qi = n_groups + atomicAdd(qhead, 1u);
+      if (!rest) break;  // the static round took every query
+      if (t == 0) {
+        uint32_t qi = NONE;
+        for (; r_tried < 8; r_tried++, r_at = (r_at + 1) & 7) {
+          const uint32_t k = atomicAdd(&qhead[r_at * 32], 1u);
+          if (k < rlen && r_at * rlen + k < rest) {
+            qi = n_groups + r_at * rlen + k;
+            break;
+          }
+        }
+        L.qi = qi;
+      }
     }
     bk_sync<W>();
     const uint32_t hi = L.qi;
@@ -964,7 +955,6 @@ int check_batch_begin(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n, 
   LQuery* lq = (LQuery*)(base + off[1]);
   uint32_t* gen = (uint32_t*)(base + off[2]);
   uint32_t* heavy = (uint32_t*)(base + off[3]);
-  uint32_t* giant = (uint32_t*)(base + off[4]);
   uint32_t* p2 = (uint32_t*)(base + off[5]);
   uint32_t* back2 = (uint32_t*)(base + off[6]);
   Ctl* ctl = (Ctl*)(base + off[7]);
@@ -975,10 +965,10 @@ int check_batch_begin(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n, 
   hipEvent_t e1 = w->ev[1], l0 = w->ev[2], l1 = w->ev[3];
   HIPC(hipMemsetAsync(ctl, 0, sizeof(Ctl), stream));
   if (n) {
-    const bool use_back = s->back_tier && s->ds.radj;
+    const bool use_back = s->ds.radj != nullptr;
     const uint32_t nblk = (uint32_t)((n + 255) / 256);
     hipLaunchKernelGGL(k_resolve, dim3(nblk), dim3(256), 0, stream, s->ds, d_q, pq, (uint32_t)n, (uint32_t)n_base, n_extra,
-                       global_max_depth, rq, d_out, d_err, gen, use_back ? (s->resolve_unheld == 2 ? 3 : s->resolve_unheld ? 2 : 1) : 0, ctl, lq,
+                       global_max_depth, rq, d_out, d_err, gen, use_back ? 2 : 0, ctl, lq,
                        lq_cap);
     HIPC(hipGetLastError());
     if (stats) HIPC(hipEventRecord(l0, stream));
@@ -991,25 +981,8 @@ int check_batch_begin(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n, 
       // starting at its label blockIdx & 7, so every label must occur for every range to be drained
       const uint32_t grid =
           std::max<uint32_t>(8u, (uint32_t)std::min<uint64_t>((uint64_t)s->n_cu * per_cu, (n + 31) / 32 + 8));
-      const int gate = std::min(s->stream_gate, Snapshot::GATE_RING - 1);
-      std::unique_lock<std::mutex> gl(s->gate_mu, std::defer_lock);
-      if (gate > 0) {
-        // at most `gate` stream launches at once: this one starts after the launch `gate` tickets back
-        // has finished (a device-side wait; the host does not block)
-        gl.lock();
-        const uint64_t t = s->gate_ticket++;
-        for (auto& e : s->gate_ev)
-          if (!e) HIPC(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        if (t >= (uint64_t)gate) HIPC(hipStreamWaitEvent(stream, s->gate_ev[(t - gate) % Snapshot::GATE_RING], 0));
-        hipLaunchKernelGGL((k_stream4<9, 256>), dim3(grid), dim3(256), 0, stream, s->ds,
-                           LqList{lq, ctl->light8, lq_cap}, ctl->heads, d_out, rq, heavy, &ctl->heavy_count, ctl, ecap,
-                           std::max<uint32_t>(1u, std::min<uint32_t>(s->stream_chunk, S4_CHUNK)), s->stream_steal);
-        HIPC(hipEventRecord(s->gate_ev[t % Snapshot::GATE_RING], stream));
-      } else {
-        hipLaunchKernelGGL((k_stream4<9, 256>), dim3(grid), dim3(256), 0, stream, s->ds,
-                           LqList{lq, ctl->light8, lq_cap}, ctl->heads, d_out, rq, heavy, &ctl->heavy_count, ctl, ecap,
-                           std::max<uint32_t>(1u, std::min<uint32_t>(s->stream_chunk, S4_CHUNK)), s->stream_steal);
-      }
+      hipLaunchKernelGGL((k_stream4<9, 256>), dim3(grid), dim3(256), 0, stream, s->ds, LqList{lq, ctl->light8, lq_cap},
+                         ctl->heads, d_out, rq, heavy, &ctl->heavy_count, ctl, ecap, S4_CHUNK, s->stream_steal);
     }
     HIPC(hipGetLastError());
     if (stats) HIPC(hipEventRecord(l1, stream));
@@ -1018,22 +991,15 @@ int check_batch_begin(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n, 
       const uint32_t* fwd_list = heavy;
       const uint32_t* fwd_count = &ctl->heavy_count;
       if (use_back) {
-        // wave per query (~48 KiB LDS per workgroup: 3 per CU), its overflow to the workgroup-per-query
-        // width (~52 KiB: 3 per CU), whose overflow goes to the grid tier
+        // one query per wave (~48 KiB LDS per workgroup: 3 per CU); its overflow goes to the grid tier
+        // (the workgroup-per-query width k_back<256> between them measured no better and was removed
+        // in round 6 with the "back" knob)
         hipLaunchKernelGGL(k_back<64>, dim3((uint32_t)s->n_cu * s->back_wgs), dim3(256), 0, stream, s->ds, rq, heavy,
-                           &ctl->heavy_count, &ctl->back_head, d_out, d_err, back2, &ctl->back2_count, ctl,
+                           &ctl->heavy_count, ctl->bheads[0], d_out, d_err, back2, &ctl->back2_count, ctl,
                            (uint32_t)s->back_edges);
         HIPC(hipGetLastError());
-        if (s->back_tier == 2) {  // wave width only: its overflow goes straight to the grid tier
-          fwd_list = back2;
-          fwd_count = &ctl->back2_count;
-        } else {
-          hipLaunchKernelGGL(k_back<256>, dim3((uint32_t)s->n_cu * s->back_wgs), dim3(256), 0, stream, s->ds, rq, back2,
-                             &ctl->back2_count, &ctl->back2_head, d_out, d_err, giant, &ctl->fwd_count, ctl, 0u);
-          HIPC(hipGetLastError());
-          fwd_list = giant;
-          fwd_count = &ctl->fwd_count;
-        }
+        fwd_list = back2;
+        fwd_count = &ctl->back2_count;
       }
       // first grid round enqueued without waiting; its readback is checked after the batch's one sync
       const int rc = grid_tier(s, w, rq, fwd_list, fwd_count, global_max_depth, d_out, d_err, stream, &bp->gs, 1, true,
@@ -1163,7 +1129,7 @@ int check_batch_device(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n,
                        uint8_t* d_out, uint32_t* d_err, kg_stats* stats, const kg_query_packed* d_pk) {
   BatchPending bp;
   if (int rc = check_batch_begin(s, w, d_q, n, global_max_depth, d_out, d_err, stats, &bp, d_pk)) return rc;
-  return check_batch_end(s, w, &bp, nullptr, s->device_sync != 0);
+  return check_batch_end(s, w, &bp, nullptr, true);
 }
 
 // ---- the narrow host boundary (kg_check_batch_packed): 16-B queries in, sparse error codes out

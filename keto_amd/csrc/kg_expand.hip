@@ -54,7 +54,38 @@ struct ExpCtl {
   uint32_t gs_head, ga_count, ga_head, gb_count, gb_head, gw_small_done, pad2[2];
   unsigned long long gw_ticks[4];  // longest gather / walk of one root, small and large slots (wall clock, 100 MHz)
   unsigned long long gw_stat[8];   // diagnostics (sums over roots): chunks, unions at rest depth 2 / 3 / 4 / >= 5, pops, entries gathered
+  // round 6: the arena's chunks and pass 1's roots are cut into 8 ranges, each claimed through its own
+  // head on a 128-B line of its own.  One word saturates near 90 M atomics/s (MI355X_MICROARCH.md
+  // "dequeue"): a C5 call's ~100 k root dequeues and ~100 k chunk claims on two words were a ~1.1 ms
+  // floor under k_expand_lds.
+  alignas(128) uint32_t ahead[8 * 32];
+  uint32_t rhead[8 * 32];
 };
+
+__device__ __forceinline__ uint32_t ld_sc1(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t ld_sc1(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long ld_sc1(const unsigned long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// A free arena chunk (lane 0 only): from the range of this workgroup's XCD label, then the others;
+// NONE when all eight are used up.
+__device__ __forceinline__ uint32_t claim_chunk(ExpCtl* ctl, uint32_t n_chunks) {
+  const uint32_t per = (n_chunks + 7) / 8;
+  uint32_t sh = blockIdx.x & 7;
+  for (int k = 0; k < 8; k++, sh = (sh + 1) & 7) {
+    const uint32_t lo = sh * per, hi = min(n_chunks, lo + per);
+    if (lo >= hi) continue;
+    if (ld_sc1(&ctl->ahead[sh * 32]) >= hi - lo) continue;  // dry: no atomic
+    const uint32_t c = atomicAdd(&ctl->ahead[sh * 32], 1u);
+    if (c < hi - lo) return lo + c;
+  }
+  return NONE;
+}
 
 // Per-root result of the DFS: first chunk and record count (0 records = nil tree).
 struct RootOut {
@@ -73,7 +104,7 @@ struct Stream {
 
 __device__ __forceinline__ uint32_t alloc_chunk(Stream& S) {
   uint32_t c = 0;
-  if (lane_id() == 0) c = atomicAdd(&S.ctl->arena_head, 1u);
+  if (lane_id() == 0) c = claim_chunk(S.ctl, S.n_chunks);
   c = __shfl(c, 0, 64);
   if (c >= S.n_chunks) {
     if (lane_id() == 0) S.ctl->overflow = 1;
@@ -463,9 +494,21 @@ __global__ __launch_bounds__(256) void k_expand_lds(DevSnap s, const kg_set* __r
   ExpFrame* stack = stacks + (size_t)(blockIdx.x * 4 + wave) * stack_cap;
   Stream S{arena, next, n_chunks, ctl, 0, 0, 0, true};
   unsigned long long recs = 0;
+  // roots in 8 ranges, each dequeued through its own head (ExpCtl::rhead): this XCD's range first
+  const uint32_t rper = (n + 7) / 8;
+  uint32_t r_at = blockIdx.x & 7, r_tried = 0;
   for (;;) {
-    uint32_t ri = 0;
-    if (lane == 0) ri = atomicAdd(&ctl->head, 1u);
+    uint32_t ri = NONE;
+    if (lane == 0)
+      for (; r_tried < 8; r_tried++, r_at = (r_at + 1) & 7) {
+        const uint32_t lo = r_at * rper, hi = min(n, lo + rper);
+        if (lo >= hi || ld_sc1(&ctl->rhead[r_at * 32]) >= hi - lo) continue;
+        const uint32_t k = atomicAdd(&ctl->rhead[r_at * 32], 1u);
+        if (k < hi - lo) {
+          ri = lo + k;
+          break;
+        }
+      }
     ri = __shfl(ri, 0, 64);
     if (ri >= n) break;
     uint32_t nr = 0;
@@ -491,7 +534,7 @@ template <class Store>
 __device__ void expand_slot_loop(const DevSnap& s, const kg_set* __restrict__ roots, int32_t global, ExpCtl* ctl,
                                  RootOut* outs, kg_tree_node* arena, uint32_t* next, uint32_t n_chunks,
                                  ExpFrame* stack, const uint32_t* qlist, uint32_t count, uint32_t* head, Store& st,
-                                 uint32_t* clear_base, uint64_t clear_words, uint32_t* p3_list, int cached) {
+                                 uint32_t* clear_base, uint64_t clear_words, uint32_t* p3_list) {
   __shared__ ExpLds X;
   const int lane = lane_id();
   Stream S{arena, next, n_chunks, ctl, 0, 0, 0, true};
@@ -503,8 +546,9 @@ __device__ void expand_slot_loop(const DevSnap& s, const kg_set* __restrict__ ro
     if (k >= count) break;
     const uint32_t ri = qlist[k];
     uint32_t nr = 0;
-    const int r = cached ? expand_root_x(s, st, roots[ri], global, stack, S, nr, X)
-                         : expand_root(s, st, roots[ri], global, stack, S, nr);
+    // the walk with LDS-cached frames (round 3; the "expand_tail" knob that kept round 2's walk beside
+    // it was removed in round 6)
+    const int r = expand_root_x(s, st, roots[ri], global, stack, S, nr, X);
     if (r == EXP_OVERFLOW && p3_list) {
       uint4* b4 = reinterpret_cast<uint4*>(clear_base);  // clear_words: multiple of 4, 16-B aligned
       for (uint64_t i = lane; i < clear_words / 4; i += 64) b4[i] = make_uint4(0, 0, 0, 0);
@@ -526,23 +570,22 @@ __global__ __launch_bounds__(64) void k_expand_hash(DevSnap s, const kg_set* __r
                                                     uint32_t n_chunks, ExpFrame* stacks, uint32_t stack_cap,
                                                     const uint32_t* qlist, const uint32_t* qcount, uint32_t* qhead,
                                                     uint32_t* tabs, uint64_t tsize, uint32_t* lists, uint64_t cap,
-                                                    uint32_t* p3_list, int cached) {
+                                                    uint32_t* p3_list) {
   __shared__ uint32_t pref[64];
   uint32_t* tab = tabs + (size_t)blockIdx.x * tsize;
   HashStore st{tab, (uint32_t)(tsize - 1), lists + (size_t)blockIdx.x * cap, cap, pref};
   expand_slot_loop(s, roots, global, ctl, outs, arena, next, n_chunks, stacks + (size_t)blockIdx.x * stack_cap, qlist,
-                   *qcount, qhead, st, tab, tsize, p3_list, cached);
+                   *qcount, qhead, st, tab, tsize, p3_list);
 }
 
 __global__ __launch_bounds__(64) void k_expand_hbm(DevSnap s, const kg_set* __restrict__ roots, int32_t global,
                                                    ExpCtl* ctl, RootOut* outs, kg_tree_node* arena, uint32_t* next,
                                                    uint32_t n_chunks, ExpFrame* stack, const uint32_t* p3_list,
-                                                   uint32_t* bm, uint64_t words, uint32_t* list, uint64_t cap,
-                                                   int cached) {
+                                                   uint32_t* bm, uint64_t words, uint32_t* list, uint64_t cap) {
   __shared__ uint32_t pref[64];
   GlobalStore st{bm, list, cap, pref};
   expand_slot_loop(s, roots, global, ctl, outs, arena, next, n_chunks, stack, p3_list, ctl->p3_count, &ctl->p3_head, st,
-                   bm, words, nullptr, cached);
+                   bm, words, nullptr);
 }
 
 // ------------------------------------------------------------------ gather-then-walk (pass 2)
@@ -586,15 +629,6 @@ struct GwSlots {
 };
 constexpr uint32_t GW_LDS_LOC = 262144;
 
-__device__ __forceinline__ uint32_t ld_sc1(const uint32_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint64_t ld_sc1(const uint64_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ unsigned long long ld_sc1(const unsigned long long* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 constexpr int GW_PROBES = 64;
 // The map slot of `node` for this root (inserting it; *won: this thread inserted it), or -1 (probe bound).
@@ -836,7 +870,7 @@ __global__ __launch_bounds__(256) void k_expand_gw(DevSnap s, const kg_set* __re
       // staged -> a new arena chunk (linked after the root's previous one); n records, n <= CHUNK
       auto flush = [&](uint32_t n) {
         uint32_t c = 0;
-        if (lane == 0) c = atomicAdd(&ctl->arena_head, 1u);
+        if (lane == 0) c = claim_chunk(ctl, S.n_chunks);
         c = __shfl(c, 0, 64);
         if (c >= S.n_chunks) {
           if (lane == 0) ctl->overflow = 1;
@@ -1306,10 +1340,10 @@ int expand_batch(Snapshot* s, hipStream_t stream, void** bufs, const kg_set* roo
     }
     hipLaunchKernelGGL(k_expand_hash, dim3(slots2), dim3(64), 0, stream, s->ds, B.d_roots, global, B.ctl, B.outs,
                        B.arena, B.next, n_chunks, B.stacks + (size_t)slots1 * stack_cap, stack_cap, q_hash, c_hash,
-                       h_hash, B.bm, tsize, lists, cap2, B.p2 + n, s->expand_tail);
+                       h_hash, B.bm, tsize, lists, cap2, B.p2 + n);
     hipLaunchKernelGGL(k_expand_hbm, dim3(1), dim3(64), 0, stream, s->ds, B.d_roots, global, B.ctl, B.outs, B.arena,
                        B.next, n_chunks, B.stacks + (size_t)(slots1 + slots2) * stack_cap, B.p2 + n,
-                       B.bm + (size_t)slots2 * tsize, words, lists + (size_t)slots2 * cap2, nn, s->expand_tail);
+                       B.bm + (size_t)slots2 * tsize, words, lists + (size_t)slots2 * cap2, nn);
     (void)hipEventRecord(B.ev[1], stream);
     if ((e = hipGetLastError()) != hipSuccess) {
       fail("launch", e);

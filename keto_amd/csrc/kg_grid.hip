@@ -16,20 +16,10 @@
 // Semantics are those of k_stream / k_medium (kg_check.hip): bounded reachability with every node
 // probed once at its shallowest depth.  A round that overflows the log is rerun with fewer slots.
 //
-// Bidirectional mode (kg_snapshot_tune "grid_bidir" = holder cap; default 0 = off): the queries that reach this tier are the
-// ones whose forward search is huge -- on a heavy-tailed graph every root reaches whole layers within
-// two hops (SURVEY.md 8d's degree law: ~1.2 M edge visits per query).  Each round alternates a forward
-// turn (the log above) with a BACKWARD turn over a second log: backward turn 0 reads the subject's
-// holders (hold[], engine.go:159-163's exact tuples seen from the subject), turn j their parents
-// through the reverse set-adjacency.  Forward turn t runs while 2t <= D-1 and backward turn t while
-// 2t+1 <= D-1, so every node either side has recorded can close a path of <= D-1 hops with every node
-// the other side has recorded: a forward child found in the backward set, or a backward parent that is
-// the root or in the forward set, is a hit (checkExpandSubject's "first IsMember wins").  A side whose
-// frontier runs dry while its turns are still active has its whole closure: nothing the other side
-// finds later can be new to it, so the query is NotMember at once (a root that reaches no holder, or a
-// subject no ancestor chain leads up from to the root).  Both sides share the visited table (a
-// direction bit in the key).  Typical heavy-tail negatives -- subjects held only by rows nothing points
-// at -- end after one backward turn instead of a forward walk over whole layers.
+// (Rounds 3-5 also had a bidirectional mode -- backward turns from the subject's holders alternating
+// with the forward ones, kg_snapshot_tune "grid_bidir" -- off by default since it measured slower on
+// both C2 and the heavy-tail point (profiles/r3d_heavy_grid_bidir_ab.jsonl); removed in
+// round 6.)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -56,41 +46,30 @@ struct GridLv {
 };
 
 struct GridCtl {
-  GridLv lv[3];   // forward log
-  GridLv blv[3];  // backward log (bidirectional mode)
+  GridLv lv[3];   // the log's level counters
   uint32_t overflow, pad;
   unsigned long long logged;  // entries over all levels (stats: rows opened)
   unsigned long long edges;   // edges over all levels (stats)
   unsigned long long probes8[8][16];  // per-XCD shards (one 128-B line each)
 };
 
-// Per-slot state of a round.  hit: 0 live, 1 IsMember, 2 NotMember decided early (a side's closure
-// ran dry).  lastf / lastb: the last turn that appended to the side's next level.
+// Per-slot state of a round.  hit: 0 live, 1 IsMember.
 struct GridSlots {
   uint32_t* q;     // query index
   uint2* info;     // (tagged subject, rest depth of the root)
   uint32_t* hit;
-  uint32_t* root;  // root node (a backward parent equal to it closes a path)
-  uint32_t* lastf;
-  uint32_t* lastb;
-  uint32_t* bd;    // 1: this slot runs bidirectional turns, 0: forward only
 };
 
-// Turn activity for a slot of rest depth D (bd = 0: forward only, the classic schedule).
-__device__ __forceinline__ bool fwd_active(uint32_t bd, int t, int D) { return bd ? 2 * t <= D - 1 : t + 1 <= D - 1; }
-__device__ __forceinline__ bool back_active(uint32_t bd, int t, int D) { return bd && 2 * t + 1 <= D - 1; }
-
 // Visited sets of all slots in ONE open-addressing table of 64-bit keys
-//   epoch (15) | direction (1: backward) | slot (16) | node (32)
+//   epoch (15) | 0 (1) | slot (16) | node (32)
 // Entries of older epochs (earlier rounds / batches) count as empty, so the table is never
 // cleared between rounds; it is zeroed once per 32767 rounds.  Within a round an entry never
 // changes once written, so a (possibly stale) plain load that shows this round's epoch is final.
 constexpr int GH_PROBES = 128;
 constexpr int GH_EPOCH_SHIFT = 49;
-constexpr uint64_t GH_BACK = 1ull << 48;
 constexpr uint32_t GH_EPOCH_WRAP = 0x8000;
-__device__ __forceinline__ uint64_t gh_key(uint64_t epoch, bool back, uint32_t slot, uint32_t node) {
-  return (epoch << GH_EPOCH_SHIFT) | (back ? GH_BACK : 0ull) | ((uint64_t)slot << 32) | node;
+__device__ __forceinline__ uint64_t gh_key(uint64_t epoch, uint32_t slot, uint32_t node) {
+  return (epoch << GH_EPOCH_SHIFT) | ((uint64_t)slot << 32) | node;
 }
 __device__ __forceinline__ int gh_insert(uint64_t* H, uint64_t mask, uint64_t key) {
   const uint64_t ep = key >> GH_EPOCH_SHIFT;
@@ -107,18 +86,6 @@ __device__ __forceinline__ int gh_insert(uint64_t* H, uint64_t mask, uint64_t ke
     h = (h + 1) & mask;
   }
   return -1;  // probe bound: the round is rerun with fewer slots
-}
-// Membership only (the other direction's set): 1 present, 0 absent, -1 probe bound (rerun).
-__device__ __forceinline__ int gh_contains(const uint64_t* H, uint64_t mask, uint64_t key) {
-  const uint64_t ep = key >> GH_EPOCH_SHIFT;
-  uint64_t h = mix64(key & ((1ull << GH_EPOCH_SHIFT) - 1)) & mask;
-  for (int p = 0; p < GH_PROBES; p++) {
-    const uint64_t cur = H[h];
-    if (cur == key) return 1;
-    if ((cur >> GH_EPOCH_SHIFT) != ep) return 0;  // an empty slot of this round ends the probe
-    h = (h + 1) & mask;
-  }
-  return -1;
 }
 
 struct GridLog {
@@ -177,60 +144,113 @@ __device__ __forceinline__ void grid_append(GridCtl* ctl, GridLv* lvs, const Gri
   __syncthreads();
 }
 
+// k_grid_level's appends, buffered in LDS across the workgroup's tiles and flushed with ONE packed
+// atomic per GB_BUF entries (round 6): every append of a level hits the same counter, and same-address
+// atomics serialise at the memory side (~11 ns each, MI355X_MICROARCH.md "dequeue") -- one per 256-edge
+// tile with an append was the level's floor on C3 (~52 us per level, profiles/r6a_c3_timeline.txt).
+constexpr uint32_t GB_BUF = 1024;
+struct GridBuf {
+  uint32_t slot[GB_BUF], rb[GB_BUF], len[GB_BUF], pre[GB_BUF];
+  uint32_t n, edges;
+  uint32_t wcnt[4], wedge[4];
+  unsigned long long old;
+};
+
+__device__ void grid_flush(GridCtl* ctl, GridLv* lvs, const GridLog& lg, int nl, int np, uint64_t next_base,
+                           GridBuf& B) {
+  if (threadIdx.x == 0)
+    B.old = atomicAdd(&lvs[nl].packed, (unsigned long long)(((uint64_t)B.n << EDGE_BITS) | B.edges));
+  __syncthreads();
+  const uint64_t at0 = B.old >> EDGE_BITS, ex0 = B.old & EDGE_MASK;
+  for (uint32_t i = threadIdx.x; i < B.n; i += blockDim.x) {
+    const uint64_t at = at0 + i, ex = ex0 + B.pre[i], gi = next_base + at;
+    const uint32_t len = B.len[i];
+    if (gi < lg.cap && at < ENTRY_MAX && ex + len <= EDGE_MASK) {
+      lg.slot[gi] = B.slot[i];
+      lg.rb[gi] = B.rb[i];
+      lg.ex[gi] = ex;
+      // tiles whose first edge lies in [ex, ex + len): exactly one entry writes each tile
+      for (uint64_t t = (ex + GT - 1) / GT; t * GT < ex + len && t < TILE_CAP; t++) lg.tile_first[np][t] = (uint32_t)at;
+    } else {
+      ctl->overflow = 1;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    B.n = 0;
+    B.edges = 0;
+  }
+  __syncthreads();
+}
+
+// Every thread of the workgroup (256) calls it; flushes first when the tile's appends do not fit.
+__device__ __forceinline__ void grid_push(GridCtl* ctl, GridLv* lvs, const GridLog& lg, int nl, int np,
+                                          uint64_t next_base, GridBuf& B, bool app, uint32_t slot, uint32_t rb,
+                                          uint32_t len) {
+  const int lane = lane_id(), wave = threadIdx.x >> 6;
+  const uint64_t m = __ballot(app);
+  uint32_t x = app ? len : 0u;
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t y = __shfl_up(x, off, 64);
+    if (lane >= off) x += y;
+  }
+  if (lane == 63) {
+    B.wcnt[wave] = (uint32_t)__popcll(m);
+    B.wedge[wave] = x;
+  }
+  __syncthreads();
+  const uint32_t tc = B.wcnt[0] + B.wcnt[1] + B.wcnt[2] + B.wcnt[3];
+  const uint32_t te = B.wedge[0] + B.wedge[1] + B.wedge[2] + B.wedge[3];
+  uint32_t n0 = B.n, e0 = B.edges;  // read by every thread before a flush changes them
+  if (tc && (n0 + tc > GB_BUF || e0 + te < e0)) {
+    grid_flush(ctl, lvs, lg, nl, np, next_base, B);
+    n0 = 0;
+    e0 = 0;
+  }
+  if (app) {
+    uint32_t at = n0 + lanes_below(m), pre = e0 + x - len;
+    for (int w = 0; w < wave; w++) {
+      at += B.wcnt[w];
+      pre += B.wedge[w];
+    }
+    B.slot[at] = slot;
+    B.rb[at] = rb;
+    B.len[at] = len;
+    B.pre[at] = pre;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    B.n = n0 + tc;
+    B.edges = e0 + te;
+  }
+  __syncthreads();
+}
+
 // slots of a round: queries [base, base + G) of the list, clamped to its device-side length
 __device__ __forceinline__ uint32_t round_slots(const uint32_t* d_count, uint32_t base, uint32_t G) {
   const uint32_t c = *d_count;
   return c > base ? min(G, c - base) : 0u;
 }
 
-// Level 0: the roots (already probed by k_resolve), one per slot; in bidirectional mode also the
-// backward log's level 0: one pseudo-entry per slot whose "edges" are the subject's holders.
-__global__ __launch_bounds__(256) void k_grid_init(DevSnap s, const RQuery* __restrict__ rq,
-                                                   const uint32_t* __restrict__ qlist, const uint32_t* d_count,
-                                                   uint32_t base, uint32_t G, GridLog lg, GridLog blg, GridSlots sl,
-                                                   uint64_t* H, uint64_t mask, uint64_t epoch, GridCtl* ctl,
-                                                   uint32_t hb) {
+// Level 0: the roots (already probed by k_resolve), one per slot.
+__global__ __launch_bounds__(256) void k_grid_init(const RQuery* __restrict__ rq, const uint32_t* __restrict__ qlist,
+                                                   const uint32_t* d_count, uint32_t base, uint32_t G, GridLog lg,
+                                                   GridSlots sl, uint64_t* H, uint64_t mask, uint64_t epoch,
+                                                   GridCtl* ctl) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   const bool valid = i < round_slots(d_count, base, G);
-  uint32_t rb = 0, len = 0, hb0 = 0, hn = 0;
+  uint32_t rb = 0, len = 0;
   if (valid) {
     const uint32_t qi = qlist[base + i];
     const RQuery q = rq[qi];
     sl.q[i] = qi;
     sl.info[i] = make_uint2(q.subj, (uint32_t)q.depth);
     sl.hit[i] = 0;  // the root was already probed (k_resolve)
-    sl.root[i] = q.node;
-    sl.lastf[i] = 0;
-    sl.lastb[i] = NONE;
-    sl.bd[i] = 0;
-    if (gh_insert(H, mask, gh_key(epoch, false, i, q.node)) < 0) ctl->overflow = 1;
+    if (gh_insert(H, mask, gh_key(epoch, i, q.node)) < 0) ctl->overflow = 1;
     rb = q.beg;
     len = q.len;
-    if (hb) {
-      // bidirectional only for subjects with at most hb holders: backward turn 0 reads every holder
-      // and turn 1 their parents, which for a popular subject is most of the reverse graph, while its
-      // forward search usually hits within a hop or two
-      const uint2 hr = holders_find(s, q.subj);
-      if (hr.y > 0 && hr.y <= hb) {
-        hb0 = hr.x;
-        hn = hr.y;
-        sl.bd[i] = 1;
-        sl.lastb[i] = 0;
-      }
-    }
   }
   grid_append(ctl, ctl->lv, lg, 0, 0, 0, valid, i, rb, len);
-  if (hb) grid_append(ctl, ctl->blv, blg, 0, 0, 0, valid && hn > 0, i, hb0, hn);
-}
-
-// Before a turn: a live slot whose side `back` has an active turn t but appended nothing at turn t-1
-// has that side's whole closure (BFS stopped by itself, not by depth) -- NotMember (see the header).
-__global__ void k_grid_settle(GridSlots sl, const uint32_t* d_count, uint32_t base, uint32_t G, int t, int back) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= round_slots(d_count, base, G) || sl.hit[i] || !sl.bd[i]) return;
-  const int D = (int)sl.info[i].y;
-  if (back ? (back_active(1, t, D) && sl.lastb[i] != (uint32_t)t) : (fwd_active(1, t, D) && sl.lastf[i] != (uint32_t)t))
-    sl.hit[i] = 2;
 }
 
 // Largest j in [lo, hi) with ex[base + j] <= e: the entry holding edge e (search in the log).
@@ -243,21 +263,28 @@ __device__ __forceinline__ uint64_t entry_of(const uint64_t* ex, uint64_t base, 
   return lo;
 }
 
-// One level: one thread per edge, one GT-edge tile per workgroup iteration.  back = 0: a forward
-// turn over the forward log (edges = adjx records: children); back = 1: a backward turn over the
-// backward log (edges = reverse-adjacency parents, or at turn 0 the subject's holders).
-template <int BACK>
+// One level: one thread per edge, one GT-edge tile per workgroup iteration.  Level L expands the
+// nodes found at hop L (rest depth D - L >= 2) into hop L + 1: every child is probed (checkDirect at
+// its shallowest depth) and kept for the next level while D - (L + 1) >= 2 and its set row is non-empty.
 __global__ __launch_bounds__(256) void k_grid_level(DevSnap s, GridLog lg, int level, GridSlots sl, uint64_t* H,
                                                     uint64_t mask, uint64_t epoch, GridCtl* ctl) {
   __shared__ uint64_t s_beg[GT + 2];
   __shared__ uint32_t s_slot[GT + 2], s_rb[GT + 2];
-  // per entry: its slot's state at tile start (subject, rest depth, hit | bidir << 8, root) -- one
-  // load per entry instead of four per edge, and a slot already answered skips its edges' loads
+  // per entry: its slot's state at tile start (subject, rest depth; hit) -- one load per entry instead
+  // of two per edge, and a slot already answered skips its edges' loads
   __shared__ uint2 s_info[GT + 2];
-  __shared__ uint32_t s_hb[GT + 2], s_root[GT + 2];
+  __shared__ uint32_t s_hit[GT + 2];
   __shared__ uint64_t s_j0, s_cnt;
-  if (ctl->overflow) return;  // the round is void (entries past the log were dropped)
-  GridLv* lvs = BACK ? ctl->blv : ctl->lv;
+  __shared__ uint32_t s_void;
+  __shared__ GridBuf B;
+  if (threadIdx.x == 0) {
+    s_void = ctl->overflow;  // one read for the whole workgroup (the loop below has barriers)
+    B.n = 0;
+    B.edges = 0;
+  }
+  __syncthreads();
+  if (s_void) return;  // the round is void (entries past the log were dropped)
+  GridLv* lvs = ctl->lv;
   const int cl3 = level % 3, nl = (level + 1) % 3, zl = (level + 2) % 3;
   const uint64_t lb = lvs[cl3].base, packed = lvs[cl3].packed;
   const uint64_t n = packed >> EDGE_BITS, total = packed & EDGE_MASK;
@@ -296,16 +323,15 @@ __global__ __launch_bounds__(256) void k_grid_level(DevSnap s, GridLog lg, int l
         s_slot[i] = sl_i;
         s_rb[i] = lg.rb[lb + j0 + i];
         s_info[i] = sl.info[sl_i];
-        s_hb[i] = sl.hit[sl_i] | (sl.bd[sl_i] << 8);
-        if (BACK) s_root[i] = sl.root[sl_i];
+        s_hit[i] = sl.hit[sl_i];
       }
     __syncthreads();
     const uint64_t e = t0 + threadIdx.x;
-    bool act = e < t1, app = false;
-    uint32_t slot = 0, cb = 0, clen = 0, child = 0;
-    if (act) {
+    bool app = false;
+    uint32_t slot = 0, cb = 0, clen = 0;
+    if (e < t1) {
       uint64_t beg;
-      uint32_t rb, hit, bidir, root;
+      uint32_t rb, hit;
       uint2 si;  // (tagged subject, rest depth of the root)
       if (use_lds) {
         uint32_t lo = 0, hi = (uint32_t)cnt;  // largest i < cnt with s_beg[i] <= e
@@ -318,9 +344,7 @@ __global__ __launch_bounds__(256) void k_grid_level(DevSnap s, GridLog lg, int l
         slot = s_slot[lo];
         rb = s_rb[lo];
         si = s_info[lo];
-        hit = s_hb[lo] & 0xFF;
-        bidir = s_hb[lo] >> 8;
-        root = BACK ? s_root[lo] : 0u;
+        hit = s_hit[lo];
       } else {
         const uint64_t j = entry_of(lg.ex, lb, j0, j0 + cnt, e);
         beg = lg.ex[lb + j];
@@ -328,78 +352,32 @@ __global__ __launch_bounds__(256) void k_grid_level(DevSnap s, GridLog lg, int l
         rb = lg.rb[lb + j];
         hit = sl.hit[slot];
         si = sl.info[slot];
-        bidir = sl.bd[slot];
-        root = BACK ? sl.root[slot] : 0u;
       }
       const int D = (int)si.y;
-      if (!BACK) {
-        if (hit) {
-          act = false;  // answered at tile start: the edge is not even loaded
-        } else {
-          const AdjX x = s.adjx[rb + (e - beg)];
-          child = x.node;
-          cb = x.begin;
-          clen = adjx_len(s, x);
-          // forward turn `level` finds hop level+1: it is expanded at forward turn level+1 and may be met
-          // by backward turn `level` (both need a set row)
-          const bool next_f = fwd_active(bidir, level + 1, D), meet_b = back_active(bidir, level, D);
-          const bool keep = clen > 0 && (next_f || meet_b);
-          bool fresh = true;
-          if (keep) {
-            const int ins = gh_insert(H, mask, gh_key(epoch, false, slot, child));
-            if (ins < 0) ctl->overflow = 1;
-            fresh = ins > 0;
-          }
-          if (fresh) {
-            if (sig_maybe(x.lsig, x.sig, subj_sig(si.x))) {  // the signature rules out most misses
-              probes++;
-              if (dset_probe(s, child, si.x)) atomicExch(&sl.hit[slot], 1u);
-            }
-            // the backward set of hops 1..level-1 (backward turns 0..level-1 ran; hop 0 = the
-            // holders, which the probe above covers)
-            if (bidir && level >= 2) {
-              const int c = gh_contains(H, mask, gh_key(epoch, true, slot, child));
-              if (c < 0) ctl->overflow = 1;
-              if (c > 0) atomicExch(&sl.hit[slot], 1u);
-            }
-            app = keep && next_f;
-          }
+      if (!hit) {  // answered at tile start: the edge is not even loaded
+        const AdjX x = s.adjx[rb + (e - beg)];
+        cb = x.begin;
+        clen = adjx_len(s, x);
+        // hop level+1 is expanded at the next level while its rest depth D - (level + 1) >= 2
+        const bool keep = clen > 0 && level + 2 <= D - 1;
+        bool fresh = true;
+        if (keep) {
+          const int ins = gh_insert(H, mask, gh_key(epoch, slot, x.node));
+          if (ins < 0) ctl->overflow = 1;
+          fresh = ins > 0;
         }
-      } else {
-        // backward turn `level`: hop `level` parents (turn 0: the holders themselves)
-        if (hit) {
-          act = false;
-        } else {
-          const uint32_t p = level == 0 ? s.hold[rb + (e - beg)] : s.radj[rb + (e - beg)];
-          child = p;
-          if (p == root) {
-            atomicExch(&sl.hit[slot], 1u);
-          } else {
-            const int ins = gh_insert(H, mask, gh_key(epoch, true, slot, p));
-            if (ins < 0) ctl->overflow = 1;
-            if (ins > 0) {
-              // the forward set (hops 0..level+1, nodes with a set row): a parent in it closes a path
-              const int c = gh_contains(H, mask, gh_key(epoch, false, slot, p));
-              if (c < 0) ctl->overflow = 1;
-              if (c > 0) atomicExch(&sl.hit[slot], 1u);
-              if (back_active(bidir, level + 1, D)) {
-                const uint64_t r0 = s.radj_off[p], r1 = s.radj_off[p + 1];
-                cb = (uint32_t)r0;
-                clen = (uint32_t)(r1 - r0);
-                app = clen > 0;
-              }
-            }
+        if (fresh) {
+          if (sig_maybe(x.lsig, x.sig, subj_sig(si.x))) {  // the signature rules out most misses
+            probes++;
+            if (dset_probe(s, x.node, si.x)) atomicExch(&sl.hit[slot], 1u);
           }
+          app = keep;
         }
       }
     }
-    const bool do_app = act && app;
-    if (do_app) {
-      if (BACK) sl.lastb[slot] = (uint32_t)level + 1;
-      else sl.lastf[slot] = (uint32_t)level + 1;
-    }
-    grid_append(ctl, lvs, lg, nl, (level + 1) & 1, next_base, do_app, slot, cb, clen);
+    grid_push(ctl, lvs, lg, nl, (level + 1) & 1, next_base, B, app, slot, cb, clen);
   }
+  if (B.n) grid_flush(ctl, lvs, lg, nl, (level + 1) & 1, next_base, B);
   for (int off = 32; off; off >>= 1) probes += __shfl_xor(probes, off, 64);
   if (lane == 0 && probes) atomicAdd(&ctl->probes8[blockIdx.x & 7][threadIdx.x >> 6], (unsigned long long)probes);
 }
@@ -431,21 +409,18 @@ constexpr uint32_t G0 = 0xFFFF;  // slot field is 16 bits
 struct GridView {  // pointers into a pool laid out for `cap` log entries (per direction)
   uint64_t cap = 0, hcap = 0;
   uint64_t* H = nullptr;
-  GridLog lg{}, blg{};
+  GridLog lg{};
   GridSlots sl{};
   GridCtl* ctl = nullptr;       // the running round's counters
   GridCtl* ctl_pool = nullptr;  // the pool's own block
 };
 
-// two: a backward log too (bidirectional rounds), and a visited table for both directions' nodes;
-// the table is sized for twice the logged entries (load <= 0.5).  The snapshot's full-size pool (one
-// query that overflowed a workspace's pool) runs forward only: two node-sized logs at C3's ~10^9 nodes
-// would take ~60 GB.
-static int grid_layout(GridPool* P, uint64_t cap, hipStream_t stream, GridView* v, bool two = true) {
+// One log and a visited table sized for twice the logged entries (load <= 0.5).
+static int grid_layout(GridPool* P, uint64_t cap, hipStream_t stream, GridView* v) {
   uint64_t hcap = 1;
-  while (hcap < (two ? 4 : 2) * cap) hcap <<= 1;
+  while (hcap < 2 * cap) hcap <<= 1;
   const size_t log_bytes = cap * (4 + 4 + 8) + 2 * TILE_CAP * 4;
-  const size_t need = hcap * 8 + (two ? 2 : 1) * log_bytes + (size_t)G0 * 32 + sizeof(GridCtl) + 4096;
+  const size_t need = hcap * 8 + log_bytes + (size_t)G0 * 16 + sizeof(GridCtl) + 4096;
   if (need > P->bytes) {
     P->release();
     HIPC(hipMalloc(&P->mem, need));
@@ -458,30 +433,23 @@ static int grid_layout(GridPool* P, uint64_t cap, hipStream_t stream, GridView* 
   v->hcap = hcap;
   v->H = (uint64_t*)p;
   p += hcap * 8;
-  v->blg = GridLog{};
-  for (GridLog* lg : {&v->lg, &v->blg}) {
-    if (lg == &v->blg && !two) break;
-    lg->cap = cap;
-    lg->ex = (uint64_t*)p;
-    p += cap * 8;
-    lg->slot = (uint32_t*)p;
-    p += cap * 4;
-    lg->rb = (uint32_t*)p;
-    p += cap * 4;
-    lg->tile_first[0] = (uint32_t*)p;
-    p += TILE_CAP * 4;
-    lg->tile_first[1] = (uint32_t*)p;
-    p += TILE_CAP * 4;
-  }
+  GridLog* lg = &v->lg;
+  lg->cap = cap;
+  lg->ex = (uint64_t*)p;
+  p += cap * 8;
+  lg->slot = (uint32_t*)p;
+  p += cap * 4;
+  lg->rb = (uint32_t*)p;
+  p += cap * 4;
+  lg->tile_first[0] = (uint32_t*)p;
+  p += TILE_CAP * 4;
+  lg->tile_first[1] = (uint32_t*)p;
+  p += TILE_CAP * 4;
   v->sl.info = (uint2*)p;
   p += (size_t)G0 * 8;
   v->sl.q = (uint32_t*)p;
   v->sl.hit = v->sl.q + G0;
-  v->sl.root = v->sl.hit + G0;
-  v->sl.lastf = v->sl.root + G0;
-  v->sl.lastb = v->sl.lastf + G0;
-  v->sl.bd = v->sl.lastb + G0;
-  p += (size_t)G0 * 24;
+  p += (size_t)G0 * 8;
   v->ctl = v->ctl_pool = (GridCtl*)(((uintptr_t)p + 255) & ~uintptr_t(255));
   return 0;
 }
@@ -490,7 +458,7 @@ int grid_reserve(Snapshot* s) {
   HIPC(hipSetDevice(s->device));
   std::lock_guard<std::mutex> lk(s->giant_mu);
   GridView v;
-  if (int rc = grid_layout(&s->giant, grid_full_cap(s), s->stream, &v, false)) return rc;
+  if (int rc = grid_layout(&s->giant, grid_full_cap(s), s->stream, &v)) return rc;
   HIPC(hipStreamSynchronize(s->stream));
   return 0;
 }
@@ -528,9 +496,6 @@ int grid_tier(Snapshot* s, Workspace* w, const RQuery* rq, const uint32_t* qlist
   const uint64_t full_cap = grid_full_cap(s);
   const uint64_t small_cap = std::min<uint64_t>(full_cap, s->grid_small_cap ? s->grid_small_cap : 16ull << 20);
   GridPool* gp = &w->grid;
-  // bidirectional turns need the reverse indexes (holders, reverse set-adjacency)
-  const int bidir_ok = s->grid_bidir && s->ds.radj && s->ds.hold && s->ds.hslots ? 1 : 0;
-  const uint32_t hold_cap = (uint32_t)s->grid_bidir;  // holders a bidirectional slot's subject may have
   std::unique_lock<std::mutex> giant_lk(s->giant_mu, std::defer_lock);
   GridView v;
   if (int rc = grid_layout(gp, small_cap, stream, &v)) return rc;
@@ -546,7 +511,6 @@ int grid_tier(Snapshot* s, Workspace* w, const RQuery* rq, const uint32_t* qlist
       gp->epoch = 1;
     }
     const uint64_t epoch = gp->epoch;
-    const int bidir = bidir_ok && gp != &s->giant ? 1 : 0;  // the full-size pool has no backward log
     const uint32_t slot_blocks = (G + 255) / 256;
     const uint32_t lgrid = (uint32_t)s->n_cu * s->grid_wgs;
     // the first round of a batch keeps its counters in the caller's zeroed Ctl (kg_grid.h), later
@@ -554,34 +518,19 @@ int grid_tier(Snapshot* s, Workspace* w, const RQuery* rq, const uint32_t* qlist
     const bool fold = phase == 1 && dsum;
     v.ctl = fold ? reinterpret_cast<GridCtl*>(dsum) : v.ctl_pool;
     if (!fold) HIPC(hipMemsetAsync(v.ctl, 0, sizeof(GridCtl), stream));
-    hipLaunchKernelGGL(k_grid_init, dim3(slot_blocks), dim3(256), 0, stream, s->ds, rq, qlist, d_count, done, G, v.lg,
-                       v.blg, v.sl, v.H, v.hcap - 1, epoch, v.ctl, bidir ? hold_cap : 0u);
+    hipLaunchKernelGGL(k_grid_init, dim3(slot_blocks), dim3(256), 0, stream, rq, qlist, d_count, done, G, v.lg, v.sl,
+                       v.H, v.hcap - 1, epoch, v.ctl);
     HIPC(hipGetLastError());
     // Levels run back to back on the device (sizes never come back to the host; an empty level
-    // costs one near-empty launch).  Forward only: level k expands nodes at rest depth D-k >= 2, so
-    // at most global_max_depth-1 levels exist.  Bidirectional: forward turn t while 2t <= D-1,
-    // backward turn t while 2t+1 <= D-1, alternating, each side's dry closure settled before its turn.
-    // forward-only slots take up to D-1 forward turns; bidirectional ones alternate while 2t(+1) <= D-1
+    // costs one near-empty launch): level k expands nodes at rest depth D-k >= 2, so at most
+    // global_max_depth-1 levels exist
     const int max_levels = std::max(1, global_max_depth - 1);
     for (int t = 0; t < max_levels; t++) {
-      if (bidir && t > 0 && 2 * t <= global_max_depth - 1) {
-        hipLaunchKernelGGL(k_grid_settle, dim3(slot_blocks), dim3(256), 0, stream, v.sl, d_count, done, G, t, 0);
-        HIPC(hipGetLastError());
-      }
       w->lev_mark(stream, false, 1);
-      hipLaunchKernelGGL(k_grid_level<0>, dim3(lgrid), dim3(256), 0, stream, s->ds, v.lg, t, v.sl, v.H, v.hcap - 1,
-                         epoch, v.ctl);
+      hipLaunchKernelGGL(k_grid_level, dim3(lgrid), dim3(256), 0, stream, s->ds, v.lg, t, v.sl, v.H, v.hcap - 1, epoch,
+                         v.ctl);
       HIPC(hipGetLastError());
       w->lev_mark(stream, true, 1);
-      if (bidir && 2 * t + 1 <= global_max_depth - 1) {
-        hipLaunchKernelGGL(k_grid_settle, dim3(slot_blocks), dim3(256), 0, stream, v.sl, d_count, done, G, t, 1);
-        HIPC(hipGetLastError());
-        w->lev_mark(stream, false, 1);
-        hipLaunchKernelGGL(k_grid_level<1>, dim3(lgrid), dim3(256), 0, stream, s->ds, v.blg, t, v.sl, v.H,
-                           v.hcap - 1, epoch, v.ctl);
-        HIPC(hipGetLastError());
-        w->lev_mark(stream, true, 1);
-      }
     }
     hipLaunchKernelGGL(k_grid_finish, dim3(slot_blocks), dim3(256), 0, stream, v.sl, d_count, done, G, out, err, v.ctl,
                        fold ? dsum : nullptr);
@@ -613,7 +562,7 @@ int grid_tier(Snapshot* s, Workspace* w, const RQuery* rq, const uint32_t* qlist
         // one query alone overflowed the workspace pool: rerun it in the shared full-size pool
         giant_lk.lock();
         gp = &s->giant;
-        if (int rc = grid_layout(gp, full_cap, stream, &v, false)) return rc;
+        if (int rc = grid_layout(gp, full_cap, stream, &v)) return rc;
         continue;
       }
       G = std::max<uint32_t>(1, std::min(G, cnt) / 4);

@@ -133,6 +133,89 @@ __device__ __forceinline__ void ms_append(const MsView& v, int b, bool app, uint
   __syncthreads();
 }
 
+// The level kernel's appends, buffered in LDS across its tiles and flushed with ONE packed atomic per
+// MS_BUF entries (round 6): every append hits the same counter, and same-address atomics serialise at
+// the memory side (~11 ns each, MI355X_MICROARCH.md "dequeue"); one per tile was ~0.8 M per heavy-tail
+// batch.  The entries of one flush keep their order, so edge offsets are the buffer's own prefix sums.
+constexpr uint32_t MS_BUF = 512;
+struct MsBuf {
+  uint32_t g[MS_BUF], node[MS_BUF], rb[MS_BUF], len[MS_BUF], pre[MS_BUF];
+  uint32_t n, edges;
+  uint32_t wcnt[4], wedge[4];
+  unsigned long long old;
+};
+
+template <uint32_t TE>
+__device__ void ms_flush(const MsView& v, int b, MsBuf& B) {
+  if (threadIdx.x == 0)
+    B.old = atomicAdd(&v.ctl->packed[b], (unsigned long long)(((uint64_t)B.n << MS_EDGE_BITS) | B.edges));
+  __syncthreads();
+  const uint64_t at0 = B.old >> MS_EDGE_BITS, e00 = B.old & MS_EDGE_MASK;
+  for (uint32_t i = threadIdx.x; i < B.n; i += blockDim.x) {
+    const uint64_t at = at0 + i, e0 = e00 + B.pre[i];
+    const uint32_t len = B.len[i];
+    if (at < v.cap && at < MS_ENTRY_MAX && e0 + len <= MS_EDGE_MASK) {
+      v.eg[b][at] = B.g[i];
+      v.en[b][at] = B.node[i];
+      v.erb[b][at] = B.rb[i];
+      v.ex[b][at] = e0;
+      for (uint64_t t = (e0 + TE - 1) / TE; t * TE < e0 + len && t < MS_TILE_CAP; t++) v.tf[b][t] = (uint32_t)at;
+    } else {
+      v.ctl->overflow = 1;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    B.n = 0;
+    B.edges = 0;
+  }
+  __syncthreads();
+}
+
+// Every thread of the workgroup calls it (256 threads); flushes first when the tile's appends do not fit.
+template <uint32_t TE>
+__device__ __forceinline__ void ms_push(const MsView& v, int b, MsBuf& B, bool app, uint32_t g, uint32_t node,
+                                        uint32_t rb, uint32_t len) {
+  const int lane = lane_id(), wave = threadIdx.x >> 6;
+  const uint64_t m = __ballot(app);
+  uint32_t x = app ? len : 0u;
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t y = __shfl_up(x, off, 64);
+    if (lane >= off) x += y;
+  }
+  if (lane == 63) {
+    B.wcnt[wave] = (uint32_t)__popcll(m);
+    B.wedge[wave] = x;
+  }
+  __syncthreads();
+  const uint32_t tc = B.wcnt[0] + B.wcnt[1] + B.wcnt[2] + B.wcnt[3];
+  const uint32_t te = B.wedge[0] + B.wedge[1] + B.wedge[2] + B.wedge[3];
+  uint32_t n0 = B.n, e0 = B.edges;  // read by every thread before a flush changes them
+  if (tc && (n0 + tc > MS_BUF || e0 + te < e0)) {
+    ms_flush<TE>(v, b, B);
+    n0 = 0;
+    e0 = 0;
+  }
+  if (app) {
+    uint32_t at = n0 + lanes_below(m), pre = e0 + x - len;
+    for (int w = 0; w < wave; w++) {
+      at += B.wcnt[w];
+      pre += B.wedge[w];
+    }
+    B.g[at] = g;
+    B.node[at] = node;
+    B.rb[at] = rb;
+    B.len[at] = len;
+    B.pre[at] = pre;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    B.n = n0 + tc;
+    B.edges = e0 + te;
+  }
+  __syncthreads();
+}
+
 // The round's queries: bit b of group g = query base + 64K g + b (word b / 64).  Roots are hop 0
 // (k_resolve probed them); each (group, root) pair becomes one level-0 entry.
 template <int K>
@@ -254,15 +337,23 @@ __device__ __forceinline__ void ms_load_words(const uint64_t* p, uint64_t (&w)[K
   }
 }
 
-// (256, 4): 4 workgroups per CU fit the LDS (~36 KB each)
+// (256, 4): 4 workgroups per CU fit the LDS (~33 KB each: staged want words + the append buffer)
 template <int K>
 __global__ __launch_bounds__(256, 4) void k_ms_level(DevSnap s, MsView v, int L, int cur) {
   constexpr uint32_t TE = ms_tile_edges(K);
-  __shared__ uint64_t s_want[TE + 2][K], s_em[TE + 2][K];
+  __shared__ uint64_t s_want[TE + 2][K];
   __shared__ uint64_t s_beg[TE + 2];
   __shared__ uint32_t s_g[TE + 2], s_rb[TE + 2], s_gm[TE + 2];
   __shared__ uint64_t s_j0, s_cnt;
-  if (v.ctl->overflow) return;
+  __shared__ uint32_t s_void;
+  __shared__ MsBuf B;
+  if (threadIdx.x == 0) {
+    s_void = v.ctl->overflow;  // one read for the whole workgroup (the loop below has barriers)
+    B.n = 0;
+    B.edges = 0;
+  }
+  __syncthreads();
+  if (s_void) return;
   const int nx = cur ^ 1;
   const uint64_t packed = v.ctl->packed[cur];
   const uint64_t n_e = packed >> MS_EDGE_BITS, total = packed & MS_EDGE_MASK;
@@ -306,7 +397,6 @@ __global__ __launch_bounds__(256, 4) void k_ms_level(DevSnap s, MsView v, int L,
       // later arrival has less rest depth: its probe and expansion are subsets of the first one's)
       s_want[i][kk] = v.fr[cur][((size_t)g * n + v.en[cur][q]) * K + kk] & v.em[((size_t)g * MS_HOPS + h0) * K + kk] &
                       ~v.hit[(size_t)g * K + kk] & v.pm[((size_t)g * MS_HOPS + h1) * K + kk];
-      s_em[i][kk] = v.em[((size_t)g * MS_HOPS + h1) * K + kk];
     }
     __syncthreads();
     const uint64_t e = t0 + threadIdx.x;
@@ -360,8 +450,8 @@ __global__ __launch_bounds__(256, 4) void k_ms_level(DevSnap s, MsView v, int L,
               if (sig_maybe(x.lsig, x.sig, subj_sig(subj)) && dset_probe(s, x.node, subj)) hits |= m & (~m + 1);
             }
             if (hits) atomicOr((unsigned long long*)&v.hit[(size_t)g * K + k], (unsigned long long)hits);
-            // expansion: those that may expand it
-            const uint64_t ex = can_expand ? (nw[k] & s_em[lo][k]) : 0ull;
+            // expansion: those that may expand it at hop L+1 (a tiny per-group table: L1 / L2 hits)
+            const uint64_t ex = can_expand ? (nw[k] & v.em[((size_t)g * MS_HOPS + h1) * K + k]) : 0ull;
             if (ex) atomicOr((unsigned long long*)&v.fr[nx][base + k], (unsigned long long)ex);
             anyex |= ex;
           }
@@ -374,8 +464,9 @@ __global__ __launch_bounds__(256, 4) void k_ms_level(DevSnap s, MsView v, int L,
         }
       }
     }
-    ms_append<TE>(v, nx, app, g, child, cb, clen);
+    ms_push<TE>(v, nx, B, app, g, child, cb, clen);
   }
+  if (B.n) ms_flush<TE>(v, nx, B);
   for (int off = 32; off; off >>= 1) {
     c_eload += __shfl_xor(c_eload, off, 64);
     c_wact += __shfl_xor(c_wact, off, 64);

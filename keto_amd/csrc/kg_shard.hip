@@ -40,12 +40,8 @@ constexpr int32_t D_NOPROBE = 1 << 30;
 // bit 29: the record checks the own part of a split formula query's node (its rows as a plain node,
 // the node's rewrite evaluated by the formula instead)
 constexpr int32_t D_OWN = 1 << 29, D_MASK = D_OWN - 1;
-// A packed local record (one-rank levels, no namespace program, kg_snapshot_tune "shard_pack"): node
-// holds the child's set-row begin (< 2^31) and depth holds D_ROW | len << 8 | rest depth (< 256), so
-// the receiving level reads no adj_off pair; its visited key is (q, 2^31 | begin) -- a row begin
-// identifies its node (rows are disjoint), and plain keys keep node ids < 2^31.
-constexpr int32_t D_ROW = 1 << 28;
-constexpr uint32_t PK_LEN_BITS = 20;
+// (Round 5's packed local records -- the child's set-row begin in place of its node id, knob
+// "shard_pack" -- measured neutral and were removed in round 6, profiles/r5k_level_occupancy_pack_ab.jsonl.)
 
 // Rewrite materialisation runs in this mode too (union nodes are plain; kg_augment.hip), so a node
 // needs the interpreter -- unavailable across shards: an error -- when its own relation has a
@@ -160,18 +156,8 @@ __device__ __forceinline__ int sv_insert(uint64_t* T, uint64_t mask, uint64_t ke
   return -1;
 }
 
-// Lossy variant (kg_snapshot_tune "shard_vis_mode" 1): a direct-mapped cache of keys with blind
-// writes -- one load and one store instead of a device-scope CAS probe chain.  A collision or a
-// race only lets a (query, node) record be processed again, at the same or a later level, i.e. with
-// the same or a smaller rest depth: it explores a subset of what the first arrival did (extra work,
-// the same answers), and rest depths still fall every level, so batches still terminate.  It never
-// reports a key this batch did not insert (the table starts empty).  1 fresh, 0 seen.
-__device__ __forceinline__ int sv_insert_lossy(uint64_t* T, uint64_t mask, uint64_t key) {
-  uint64_t* slot = &T[mix64(key) & mask];
-  if (*slot == key) return 0;
-  *slot = key;
-  return 1;
-}
+// (Round 5's lossy direct-mapped variant of this table, knob "shard_vis_mode", measured flat and was
+// removed in round 6, profiles/r5e_visited_table_size_ab.jsonl.)
 
 // Workgroup-aggregated append of one record per active thread to the bucket of its destination
 // rank: ballots per wave into LDS counters, then ONE device atomic per (workgroup, destination) --
@@ -407,8 +393,7 @@ __global__ __launch_bounds__(256) void k_shard_seed(DevSnap s, const kg_query* _
 // One set-adjacency edge (parent record pr -> child ax) of an expansion: the child's record for its
 // owner, a hit / error report for the query's home, or nothing.
 __device__ __forceinline__ void shard_child(const DevSnap& s, const kg_frec& pr, const AdjX& ax, uint32_t me,
-                                            uint8_t* res, uint32_t* err, kg_frec& c, uint32_t& dest, bool& send,
-                                            bool pack = false) {
+                                            uint8_t* res, uint32_t* err, kg_frec& c, uint32_t& dest, bool& send) {
   const uint32_t child = ax.node;
   if (pr.depth >= 2) {
     if (s.remote_meta) {
@@ -444,10 +429,7 @@ __device__ __forceinline__ void shard_child(const DevSnap& s, const kg_frec& pr,
         dest = pr.q >> Q_BITS;
         send = true;
       } else if (alen && pr.depth >= 3) {
-        if (pack && ax.begin < 0x80000000u && alen < ADJX_LEN_SAT && alen < (1u << PK_LEN_BITS) && pr.depth - 1 < 256)
-          c = kg_frec{pr.q, ax.begin, pr.subj, (int32_t)((alen << 8) | (uint32_t)(pr.depth - 1)) | D_ROW | D_NOPROBE};
-        else
-          c = kg_frec{pr.q, child, pr.subj, (pr.depth - 1) | D_NOPROBE};
+        c = kg_frec{pr.q, child, pr.subj, (pr.depth - 1) | D_NOPROBE};
         send = true;
       }
     } else {
@@ -524,17 +506,16 @@ __device__ __forceinline__ uint64_t seg_src(const uint64_t* s_segpre, uint32_t n
 // in-workgroup expansion overlaps other workgroups' record processing, profiles/r2s8_*.)
 // Segmented input (n_seg > 1): the receive buffer of a fixed-split all-to-all -- segment k holds
 // d_n_in[k] records (clamped to seg_cap) from in[k * seg_cap]; the level walks their concatenation.
-// MINW: minimum waves per SIMD the compiler must allow (kg_snapshot_tune "shard_level_occ"): 1 lets it
-// take 82 VGPRs (5 waves per SIMD), 6 fits 78, 8 fits 64 with a small spill
-template <int MINW>
-__global__ __launch_bounds__(256, MINW) void k_shard_level(DevSnap s, const kg_frec* __restrict__ in, uint64_t n_bound,
+// (The compiler's choice of registers: forcing 6 or 8 waves per SIMD -- round 5's "shard_level_occ"
+// knob -- measured no better, profiles/r5k_level_occupancy_pack_ab.jsonl.)
+__global__ __launch_bounds__(256) void k_shard_level(DevSnap s, const kg_frec* __restrict__ in, uint64_t n_bound,
                                                      const uint32_t* d_n_in, kg_frec* out, uint64_t cap, uint32_t* counts, uint8_t* res,
                                                      uint32_t* err, uint64_t* vis, uint64_t vmask,
                                                      const uint32_t* __restrict__ done, uint32_t done_wpr,
                                                      HeavyList heavy,
-                                                     uint32_t* qcnt, uint32_t budget, uint32_t lossy, uint32_t n_seg,
+                                                     uint32_t* qcnt, uint32_t budget, uint32_t n_seg,
                                                      uint64_t seg_cap, uint32_t heavy_min, uint32_t out_sub,
-                                                     uint32_t pack, uint32_t res_done) {
+                                                     uint32_t res_done) {
   __shared__ uint32_t s_pref[256], s_wsum[4];
   __shared__ uint64_t s_rb[256];
   __shared__ kg_frec s_rec[256];
@@ -553,13 +534,7 @@ __global__ __launch_bounds__(256, MINW) void k_shard_level(DevSnap s, const kg_f
     if (i < n_in) {
       r = in[n_seg > 1 ? seg_src(s_segpre, n_seg, seg_cap, i) : i];
       const bool probe = !(r.depth & D_NOPROBE), own = (r.depth & D_OWN) != 0;
-      const bool packed = pack && (r.depth & D_ROW) != 0;  // r.node = the row's begin, the length in the depth word
       r.depth &= D_MASK;
-      uint32_t pk_len = 0;
-      if (packed) {
-        pk_len = ((uint32_t)r.depth >> 8) & ((1u << PK_LEN_BITS) - 1);
-        r.depth &= 0xFF;
-      }
       if (r.node == KG_FREC_HIT) {
         if ((r.q >> Q_BITS) == me) res[r.q & Q_MASK] = KG_IS_MEMBER;
       } else if (r.node == KG_FREC_ESC) {
@@ -579,14 +554,13 @@ __global__ __launch_bounds__(256, MINW) void k_shard_level(DevSnap s, const kg_f
         const uint64_t dkey = dset_key(r.node, r.subj);
         const ulonglong2 pb = *reinterpret_cast<const ulonglong2*>(
             s.dset + (want_p ? dset_home(dkey, s.dset_nb) : 0ull) * DSET_BUCKET);
-        const uint32_t an = packed ? 0u : r.node;
-        const uint64_t a0 = s.adj_off[an], a1 = s.adj_off[an + 1];
-        const uint64_t xb = s.adjx_off ? (uint64_t)s.adjx_off[an] : a0;  // the row's begin in adjx
-        const uint64_t vkey = ((uint64_t)r.q << 32) | (packed ? (0x80000000u | r.node) : r.node);
-        const int ins = lossy ? sv_insert_lossy(vis, vmask, vkey) : sv_insert(vis, vmask, vkey);
+        const uint64_t a0 = s.adj_off[r.node], a1 = s.adj_off[r.node + 1];
+        const uint64_t xb = s.adjx_off ? (uint64_t)s.adjx_off[r.node] : a0;  // the row's begin in adjx
+        const uint64_t vkey = ((uint64_t)r.q << 32) | r.node;
+        const int ins = sv_insert(vis, vmask, vkey);
         // the flags word follows the (sub-)bucket counters: counts[out_sub] in the one-rank sub mode
         if (ins < 0) atomicOr(&counts[out_sub > 1 ? out_sub : s.shard_n], 2u);
-        if (ins > 0 && !own && !packed && node_bad(s, r.node)) {  // a rewrite / undeclared relation
+        if (ins > 0 && !own && node_bad(s, r.node)) {  // a rewrite / undeclared relation
           if ((r.q >> Q_BITS) == me) atomicMax(&err[r.q & Q_MASK], (uint32_t)KG_ERR_NOT_IMPLEMENTED);
           else err_out = true;
         } else if (ins > 0) {
@@ -600,8 +574,8 @@ __global__ __launch_bounds__(256, MINW) void k_shard_level(DevSnap s, const kg_f
             // children at depth - 1 >= 1 can still be probed; children at depth 0 cannot, but
             // checkIsAllowed(child, 0) still evaluates astRelationFor (engine.go:199-206), so with a
             // namespace program their relation flags are checked (shard_child) for the error report
-            rb = packed ? (uint64_t)r.node : xb;
-            len = packed ? (uint64_t)pk_len : a1 - a0;
+            rb = xb;
+            len = a1 - a0;
             if (len && budget) {  // escalation: this rank's set-edge count of the query passes the budget
               const uint32_t add = (uint32_t)min(len, (uint64_t)budget);
               const uint32_t old = atomicAdd(&qcnt[mix64(r.q) & ((1u << QCNT_LOG2) - 1)], add);
@@ -653,7 +627,7 @@ __global__ __launch_bounds__(256, MINW) void k_shard_level(DevSnap s, const kg_f
       bool send = false;
       if (e < total) {
         const int own = owner_search(s_pref, 256, e);
-        shard_child(s, s_rec[own], s.adjx[s_rb[own] + (e - s_pref[own])], me, res, err, c, dest, send, pack != 0);
+        shard_child(s, s_rec[own], s.adjx[s_rb[own] + (e - s_pref[own])], me, res, err, c, dest, send);
       }
       emit(send, dest, c, out, cap, counts, s.shard_n, out_sub);
     }
@@ -773,7 +747,7 @@ __global__ __launch_bounds__(256) void k_shard_back_level(DevSnap s, const kg_fr
                                                           uint64_t vmask, const uint32_t* __restrict__ done,
                                                           uint32_t done_wpr, HeavyList heavy, uint32_t* qcnt,
                                                           uint32_t budget,
-                                                          uint32_t lossy, uint32_t n_seg, uint64_t seg_cap) {
+                                                          uint32_t n_seg, uint64_t seg_cap) {
   __shared__ uint32_t s_pref[256], s_wsum[4];
   __shared__ uint64_t s_rb[256];
   __shared__ kg_frec s_rec[256];
@@ -798,7 +772,7 @@ __global__ __launch_bounds__(256) void k_shard_back_level(DevSnap s, const kg_fr
         // answered IsMember by an earlier level
       } else {
         const uint64_t vkey = ((uint64_t)r.q << 32) | r.node;
-        const int ins = lossy ? sv_insert_lossy(vis, vmask, vkey) : sv_insert(vis, vmask, vkey);
+        const int ins = sv_insert(vis, vmask, vkey);
         if (ins < 0) atomicOr(&counts[1], 2u);
         if (ins > 0 && r.depth >= 1) {
           rb = s.radj_off[r.node];
@@ -851,7 +825,7 @@ __global__ __launch_bounds__(256) void k_shard_back_level(DevSnap s, const kg_fr
 // tile's rows staged in LDS.
 __global__ __launch_bounds__(256) void k_shard_heavy(DevSnap s, HeavyList heavy, kg_frec* out, uint64_t cap,
                                                      uint32_t* counts, uint8_t* res, uint32_t* err, uint32_t nranks,
-                                                     uint32_t out_sub, uint32_t pack, uint32_t* zero_counts,
+                                                     uint32_t out_sub, uint32_t* zero_counts,
                                                      uint32_t zero_n, unsigned long long* zero_pk,
                                                      uint32_t* maxacc) {
   static_assert(HEAVY_TILE == 256, "one edge per thread");
@@ -908,7 +882,7 @@ __global__ __launch_bounds__(256) void k_shard_heavy(DevSnap s, HeavyList heavy,
       const HeavyRow H = heavy.rows[r0 + lo];
       const uint64_t k = e - H.e0;
       if (H.pad) back_child(s, H.r, s.radj[H.rb + k], me, res, c, send);  // a reverse row (backward phase)
-      else shard_child(s, H.r, s.adjx[H.rb + k], me, res, err, c, dest, send, pack != 0);
+      else shard_child(s, H.r, s.adjx[H.rb + k], me, res, err, c, dest, send);
     }
     emit(send, dest, c, out, cap, counts, nranks, out_sub);  // ends with a barrier: s_r0 is free again
   }
@@ -1176,16 +1150,9 @@ size_t shard_result_slots(const Snapshot* s, size_t n) { return s->n_fplans ? n 
 
 static int shard_vis_prepare(Snapshot* s, ShardCtx* c, hipStream_t stream, size_t n) {
   // per-batch (query, node) table of 2^shard_vis_log2 slots (kg_snapshot_tune "shard_vis",
-  // default 2^23 = 64 MiB); an overflow is reported in the flags and the driver grows it.  At least
-  // shard_vis_q slots per query of the batch (kg_snapshot_tune "shard_vis_q"; 0: the fixed size): the
-  // table only grew on an overflow -- a probe chain past SV_PROBES -- so it ran nearly full, and each
-  // record's device-scope CAS walked a long chain
-  uint64_t slots = 1ull << s->shard_vis_log2;
-  if (s->shard_vis_q && n) {
-    uint64_t want = 1;
-    while (want < (uint64_t)n * s->shard_vis_q && want < (1ull << 34)) want <<= 1;
-    slots = std::max(slots, want);
-  }
+  // default 2^23 = 64 MiB); an overflow is reported in the flags and the driver grows it
+  (void)n;
+  const uint64_t slots = 1ull << s->shard_vis_log2;
   if (c->vis && c->vis_slots != slots) {
     HIPC(hipFree(c->vis));
     c->vis = nullptr;
@@ -1264,15 +1231,6 @@ unsigned long long* shard_heavy_head(Snapshot* s, hipStream_t stream) {
   return c ? (unsigned long long*)heavy_list(c).pk : nullptr;
 }
 
-#define KG_SHARD_LEVEL_LAUNCH(OCC, ...)                                        \
-  do {                                                                         \
-    switch (OCC) {                                                             \
-      case 8: hipLaunchKernelGGL(k_shard_level<8>, __VA_ARGS__); break;        \
-      case 6: hipLaunchKernelGGL(k_shard_level<6>, __VA_ARGS__); break;        \
-      default: hipLaunchKernelGGL(k_shard_level<1>, __VA_ARGS__); break;       \
-    }                                                                          \
-  } while (0)
-
 int shard_level(Snapshot* s, const kg_frec* d_in, size_t n_in, const uint32_t* d_n_in, kg_frec* d_out, size_t cap,
                 uint32_t* d_counts, uint8_t* d_res, uint32_t* d_err, const uint32_t* d_done, uint32_t done_words,
                 hipStream_t stream, uint32_t n_seg, size_t seg_cap, bool prezeroed) {
@@ -1288,18 +1246,14 @@ int shard_level(Snapshot* s, const kg_frec* d_in, size_t n_in, const uint32_t* d
     const HeavyList heavy = heavy_list(c);
     if (!prezeroed) HIPC(hipMemsetAsync(heavy.pk, 0, 8, stream));
     const uint32_t grid = (uint32_t)std::min<uint64_t>((n_in + 255) / 256, (uint64_t)s->n_cu * s->shard_wgs);
-    // packed local records (kg_snapshot_tune "shard_pack"), as the one-rank loop: a locally owned child
-    // travels with its adjx row instead of its node id, so its level reads no adj_off pair
     const uint32_t budget = shard_escalates(s) && c->qcnt && !c->final ? s->shard_budget : 0u;
-    const uint32_t pack = (s->shard_pack && !s->ds.relflags && !s->ds.nflags && budget == 0 &&
-                           s->ds.n_nodes < 0x80000000u && c->gdepth > 0 && c->gdepth < 256) ? 1u : 0u;
-    KG_SHARD_LEVEL_LAUNCH(s->shard_level_occ, dim3(grid), dim3(256), 0, stream, s->ds, d_in, (uint64_t)n_in, d_n_in, d_out,
+    hipLaunchKernelGGL(k_shard_level, dim3(grid), dim3(256), 0, stream, s->ds, d_in, (uint64_t)n_in, d_n_in, d_out,
                        (uint64_t)cap, d_counts, d_res, d_err, (uint64_t*)c->vis, c->vis_slots - 1,
                        d_done, d_done ? done_words : 0u, heavy, (uint32_t*)c->qcnt,
-                       budget, s->shard_vis_mode ? 1u : 0u, n_seg, (uint64_t)seg_cap, s->shard_heavy, 1u, pack, 0u);
+                       budget, n_seg, (uint64_t)seg_cap, s->shard_heavy, 1u, 0u);
     HIPC(hipGetLastError());
     hipLaunchKernelGGL(k_shard_heavy, dim3((uint32_t)s->n_cu * 4), dim3(256), 0, stream, s->ds, heavy, d_out,
-                       (uint64_t)cap, d_counts, d_res, d_err, s->shard_n, 1u, pack, nullptr, 0u, nullptr, nullptr);
+                       (uint64_t)cap, d_counts, d_res, d_err, s->shard_n, 1u, nullptr, 0u, nullptr, nullptr);
     HIPC(hipGetLastError());
   }
   return 0;
@@ -1334,10 +1288,6 @@ int shard_levels(Snapshot* s, int levels, kg_frec* d_buf[2], size_t cap, uint32_
   // sub mode): level 0 reads the seed's bucket, every later level the SUB segments of the one before
   const uint32_t SUB = cap >= 8 * 256 ? 8u : 1u;
   const uint64_t seg = cap / SUB;
-  // packed local records (D_ROW): only here, where every record stays on this rank and is read by the
-  // next level of this loop; not with a namespace program (node flags) or an escalation budget
-  const uint32_t pack = (s->shard_pack && !s->ds.relflags && !s->ds.nflags && budget == 0 &&
-                         s->ds.n_nodes < 0x80000000u && c->gdepth > 0 && c->gdepth < 256) ? 1u : 0u;
   if (!c->cnt8) HIPC(hipMalloc((void**)&c->cnt8, 32 * 4));
   HIPC(hipMemsetAsync(c->cnt8, 0, 32 * 4, stream));
   uint32_t* sub[2] = {c->cnt8, c->cnt8 + 16};
@@ -1363,15 +1313,15 @@ int shard_levels(Snapshot* s, int levels, kg_frec* d_buf[2], size_t cap, uint32_
       HIPC(hipGetLastError());
     }
     const bool seg_in = k > 0;
-    KG_SHARD_LEVEL_LAUNCH(s->shard_level_occ, dim3(grid), dim3(256), 0, stream, s->ds, d_buf[cur], (uint64_t)cap,
+    hipLaunchKernelGGL(k_shard_level, dim3(grid), dim3(256), 0, stream, s->ds, d_buf[cur], (uint64_t)cap,
                        seg_in ? sub[cur] : d_counts[cur], d_buf[nx], seg, sub[nx], d_res, d_err, (uint64_t*)c->vis,
                        c->vis_slots - 1, k > 0 && !direct ? (const uint32_t*)c->bits : nullptr, direct ? 0u : w, hk,
-                       (uint32_t*)c->qcnt, budget, s->shard_vis_mode ? 1u : 0u, seg_in ? SUB : 1u,
-                       seg_in ? seg : (uint64_t)0, s->shard_heavy, SUB, pack, direct && k > 0 && slots ? 1u : 0u);
+                       (uint32_t*)c->qcnt, budget, seg_in ? SUB : 1u, seg_in ? seg : (uint64_t)0, s->shard_heavy, SUB,
+                       direct && k > 0 && slots ? 1u : 0u);
     HIPC(hipGetLastError());
     // direct: the level after this one writes sub[cur] (this level's input counters) and pk2[(k+1) & 1]
     hipLaunchKernelGGL(k_shard_heavy, dim3((uint32_t)s->n_cu * 4), dim3(256), 0, stream, s->ds, hk, d_buf[nx], seg,
-                       sub[nx], d_res, d_err, s->shard_n, SUB, pack, direct && seg_in ? sub[cur] : nullptr,
+                       sub[nx], d_res, d_err, s->shard_n, SUB, direct && seg_in ? sub[cur] : nullptr,
                        direct && seg_in ? SUB : 0u, direct ? pk2[(k + 1) & 1] : nullptr, maxsub);
     HIPC(hipGetLastError());
     cur = nx;
@@ -1466,10 +1416,10 @@ int shard_back_level(Snapshot* s, const kg_frec* d_in, size_t n_in, const uint32
     hipLaunchKernelGGL(k_shard_back_level, dim3(grid), dim3(256), 0, stream, s->ds, d_in, (uint64_t)n_in, d_n_in, d_out,
                        (uint64_t)cap, d_counts, d_res, d_err, (uint64_t*)c->vis, c->vis_slots - 1, d_done,
                        d_done ? done_words : 0u, heavy, (uint32_t*)c->qcnt,
-                       c->qcnt ? s->shard_back_budget : 0u, s->shard_vis_mode ? 1u : 0u, n_seg, (uint64_t)seg_cap);
+                       c->qcnt ? s->shard_back_budget : 0u, n_seg, (uint64_t)seg_cap);
     HIPC(hipGetLastError());
     hipLaunchKernelGGL(k_shard_heavy, dim3((uint32_t)s->n_cu * 4), dim3(256), 0, stream, s->ds, heavy, d_out,
-                       (uint64_t)cap, d_counts, d_res, d_err, 1u, 1u, 0u, nullptr, 0u, nullptr, nullptr);
+                       (uint64_t)cap, d_counts, d_res, d_err, 1u, 1u, nullptr, 0u, nullptr, nullptr);
     HIPC(hipGetLastError());
   }
   return 0;

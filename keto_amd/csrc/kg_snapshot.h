@@ -294,20 +294,12 @@ struct Snapshot {
   uint32_t* shard_held = nullptr;  // holder bitmap OR-ed over every rank (kg_shard_held), or null
   uint32_t shard_held_n = 0;
   int shard_vis_log2 = 23;
-  uint32_t shard_vis_q = 0;  // kg_snapshot_tune("shard_vis_q"): visited-table slots per query of a batch (at least)
   uint32_t shard_bucket0 = 0;  // kg_snapshot_tune("shard_bucket"): first bucket size of new in-library bindings (0: by batch)
-  int shard_level_occ = 0;  // kg_snapshot_tune("shard_level_occ"): k_shard_level built for 0 (compiler's choice), 6 or 8 waves per SIMD
-  uint32_t shard_wgs = 8;  // kg_snapshot_tune("shard_wgs"): k_shard_level workgroups per CU
-  int shard_pack = 0;  // kg_snapshot_tune("shard_pack"): packed local records in kg_shard_levels (D_ROW; measured neutral)
+  uint32_t shard_wgs = 8;  // k_shard_level workgroups per CU
   uint32_t shard_heavy = 64;  // kg_snapshot_tune("shard_heavy"): set rows longer than this go to k_shard_heavy (r3p A/B)
-  int shard_vis_mode = 0;  // kg_snapshot_tune("shard_vis_mode"): (query, node) dedup 0 = exact CAS table, 1 = lossy cache
   uint32_t shard_budget = 0;       // kg_snapshot_tune("shard_budget"): forward set edges per query and rank (0 = off)
   uint32_t shard_back_budget = 1u << 14;  // kg_snapshot_tune("shard_back_budget"): reverse edges per query and rank
-  int back_tier = 2;  // kg_snapshot_tune("back"): backward tier (1: wave + workgroup widths, 2: wave only) + no-holder filter
   uint32_t stream_ecap = 512;  // kg_snapshot_tune("stream_ecap"): stream-tier edge budget per query (0 = none)
-  // kg_snapshot_tune("resolve_unheld"): 1 = k_resolve reads the holder bit before the node map (a subject
-  // no row holds skips it); 2 = reads it only for queries headed for the stream tier; 0 = beside the map
-  int resolve_unheld = 1;
   // kg_snapshot_tune("expand_gw"): pass-1 overflows of kg_expand_batch run gather-then-walk (1) or the
   // hash pass directly (0); "expand_skip_lds" (tests): every root skips the LDS pass
   int expand_gw = 1;
@@ -315,7 +307,6 @@ struct Snapshot {
   // k_expand_gw: longest wait (us) of a large slot for a small slot's hand-on before it gives its ticket up
   uint32_t expand_gw_wait_us = 100000;
   uint32_t stream_steal = 4;   // kg_snapshot_tune("stream_steal"): XCD ranges a k_stream4 wave dequeues from (1..8)
-  uint32_t stream_chunk = 64;  // kg_snapshot_tune("stream_chunk"): k_stream4 queries per dequeue (1..64)
   // Occupancy defaults (library-wide, measured with several batches in flight, the way a server keeps
   // them: C2 and C3 A/Bs in profiles/r2gw_tier_wgs_sweep.jsonl, r2v_occupancy_sweep.jsonl,
   // r2bw_back_wgs_ab.jsonl; a one-batch-at-a-time caller loses < 5 % with them)
@@ -323,10 +314,8 @@ struct Snapshot {
   // (the LDS a third stream workgroup held now serves the other batches' tail tiers): 7.00 -> 7.20 x 10^9;
   // C3 keeps 4 / 3 through bench.py
   int grid_wgs = 2;          // kg_snapshot_tune("grid_wgs"): k_grid_level workgroups per CU
-  int device_sync = 1;      // kg_snapshot_tune("device_sync"): kg_check_batch_device waits asleep (1) or spinning (0)
-  int host_sync = 1;        // kg_snapshot_tune("host_sync"): kg_check_batch waits asleep (1) or spinning (0)
   int stream_wgs = 2;        // kg_snapshot_tune("stream_wgs"): k_stream4 workgroups per CU (LDS left to other batches)
-  int interp_wgs = 6;        // kg_snapshot_tune("interp_wgs"): k_interp_lds workgroups (4 waves) per CU (6 fit the LDS)
+  int interp_wgs = 6;        // k_interp_lds workgroups (4 waves) per CU (6 fit the LDS)
   uint32_t interp_cap2 = 0;  // kg_snapshot_tune("interp_cap2"): pass-2 BFS list cap of the rewrite path (0 = 256 Ki)
   // k_back workgroups per CU (1..3, LDS allows 3; C3 prefers 1).  3: one wave per query for up to 3 Ki
   // hand-ons (C2 hands on ~2.2 k per 1 M batch: at 2, ~170 of them waited for a second pass on a
@@ -334,24 +323,11 @@ struct Snapshot {
   int back_wgs = 3;          // kg_snapshot_tune("back_wgs")
   uint32_t back_edges = 0;   // kg_snapshot_tune("back_edges"): k_back<64>'s reverse-edge budget per query (0 = 2^12)
   uint64_t grid_small_cap = 0;  // kg_snapshot_tune("grid_cap"): workspace grid-log entries (0 = 16 Mi; tests)
-  int expand_tail = 1;  // kg_snapshot_tune("expand_tail"): expand passes 2/3 walk with LDS-cached frames (0: round 2)
   int grid_ms = 1;  // kg_snapshot_tune("grid_ms"): grid-tier queries as MS-BFS when the dense masks fit (0: off)
   size_t grid_ms_bytes = 1ull << 30;  // kg_snapshot_tune("grid_ms_bytes"): MS-BFS mask budget per workspace
   int grid_ms_words = 8;     // kg_snapshot_tune("grid_ms_words"): 64-bit words per MS-BFS mask (64 queries each)
   uint32_t grid_ms_tg_cap = 256;  // kg_snapshot_tune("grid_ms_tg_cap"): holders above which MS-BFS probes dset instead
   uint64_t grid_ms_cap = 0;  // kg_snapshot_tune("grid_ms_cap"): MS-BFS entries per level buffer (0 = 16 Mi; tests)
-  // kg_snapshot_tune("stream_gate"): at most this many k_stream4 launches of different batches run at
-  // once (0: no cap).  Each launch waits, on the device, for the one `stream_gate` tickets before it
-  // (an event ring, tickets taken in launch order under gate_mu), so more batches can be in flight
-  // (their k_resolve / k_back / grid phases overlapping) without more stream launches contending for
-  // the LDS and the random-request path.
-  int stream_gate = 0;
-  static constexpr int GATE_RING = 16;
-  std::mutex gate_mu;
-  uint64_t gate_ticket = 0;
-  hipEvent_t gate_ev[GATE_RING] = {};
-  int grid_bidir = 0;  // kg_snapshot_tune("grid_bidir"): grid slots whose subject has <= this many holders alternate
-                       // forward and backward turns (0: none, forward only)
   // replicas: the same snapshot on more devices (kg_snapshot_create's device mask); this object is
   // replica 0 and owns the others.  Host-buffer batches and expands are split over all of them.
   std::vector<Snapshot*> peers;

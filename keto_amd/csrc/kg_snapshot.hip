@@ -286,8 +286,6 @@ Snapshot::~Snapshot() {
   for (auto& a : allocs) hipFree(a.first);
   for (Workspace* w : wss) delete w;
   for (ShardCtx* c : shard_ctxs) delete c;
-  for (hipEvent_t e : gate_ev)
-    if (e) hipEventDestroy(e);
   giant.release();
   if (stream) hipStreamDestroy(stream);
 }

@@ -188,14 +188,13 @@ class Snapshot:
         return {"union_nodes": int(a[0]), "new_nodes": int(a[1]), "check_rows": int(a[2])}
 
     def tune(self, key: str, value: int) -> None:
-        """Engine knobs (kg_snapshot_tune; keto_amd/csrc/kg_abi.cpp tune_one lists them with their ranges):
-        tier chain -- back, back_wgs, back_edges, stream_ecap, stream_wgs, stream_steal, stream_chunk,
-        resolve_unheld, grid_wgs, grid_bidir, grid_cap, grid_reserve, grid_ms, grid_ms_words, grid_ms_bytes,
-        grid_ms_tg_cap, grid_ms_cap, interp_wgs, interp_cap2, device_sync, host_sync, max_lanes;
-        expand -- expand_tail; hash-sharded -- shard_local, shard_force_exchange, shard_max_reruns,
-        shard_max_bytes, shard_force_overflow (tests), shard_bucket, shard_vis, shard_vis_mode, shard_wgs,
-        shard_heavy, shard_pack, shard_budget, shard_back_budget, shard_remote_meta (read at the first binding),
-        shard_vis_q, shard_level_occ; plus stream_gate, expand_gw.  Build-time, from the environment:
+        """Engine knobs (kg_snapshot_tune; keto_amd/csrc/kg_abi.cpp tune_one lists them with their ranges;
+        29 since round 6 removed the ones that measured flat): tier chain -- back_wgs, back_edges, stream_ecap,
+        stream_wgs, stream_steal, grid_wgs, grid_cap, grid_reserve, grid_ms, grid_ms_words, grid_ms_bytes,
+        grid_ms_tg_cap, grid_ms_cap, interp_cap2, max_lanes; expand -- expand_gw, expand_gw_wait_us,
+        expand_skip_lds (tests); hash-sharded -- shard_local, shard_force_exchange, shard_max_reruns,
+        shard_max_bytes, shard_force_overflow (tests), shard_bucket, shard_vis, shard_heavy, shard_budget,
+        shard_back_budget, shard_remote_meta (read at the first binding).  Build-time, from the environment:
         KG_ADJX_ORDER=0 lays adjx out in node order instead of hot-first."""
         _lib.check(_lib.load().kg_snapshot_tune(self._h, key.encode(), int(value)), "kg_snapshot_tune")
         self.__dict__.setdefault("tuned", {})[key] = int(value)  # what the Python drivers need to know

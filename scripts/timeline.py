@@ -5,7 +5,7 @@ import re
 import sys
 
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
-short = lambda n: re.sub(r"\(.*", "", n).replace("kg::", "").replace("void ", "")[:40]
+short = lambda n: re.sub(r"\(.*", "", n.replace("(anonymous namespace)::", "")).replace("kg::", "").replace("void ", "")[:40]
 # batches start at k_resolve (ANCHOR: another kernel, e.g. k_shard_seed); show the last complete one
 anchor = os.environ.get("ANCHOR", "k_resolve")
 starts = [i for i, r in enumerate(rows) if anchor in r["Kernel_Name"]]

@@ -19,8 +19,7 @@ def test_defaults_and_tune_set():
     assert a.parity >= 1_000_000 and a.latency_batches >= 200
     s = _FakeSnap()
     bench.apply_tune(s, a)
-    for k in ("stream_ecap", "stream_steal", "back_wgs", "stream_wgs", "grid_wgs", "grid_reserve",
-              "device_sync"):
+    for k in ("stream_ecap", "stream_steal", "back_wgs", "stream_wgs", "grid_wgs", "grid_reserve"):
         assert k in s.tuned, k
     c3 = bench.parse(["--preset", "1"])
     assert c3.back_wgs == 1 and c3.grid_wgs == 4 and c3.stream_wgs == 3

@@ -57,13 +57,12 @@ def test_random_graphs_vs_oracle(seed):
     rng = np.random.default_rng(seed)
     it, tuples, nss, rels = random_graph(rng, n_obj=40 + 20 * (seed % 6), n_rows=200 + 150 * (seed % 6))
     reg = Registry(tuples, [], interner=it)
-    # k_stream4 knobs (results never depend on them): a tiny per-query edge budget (queries overflow
-    # into the backward / grid tiers mid-search), dequeue chunks of 1 / 16 / 64 queries, one / four /
-    # eight XCD steal ranges, and the backward tier off / wave + workgroup / wave only
+    # tier knobs (results never depend on them): a tiny per-query edge budget (queries overflow into
+    # the backward / grid tiers mid-search), one / four / eight XCD steal ranges, and a backward tier
+    # that hands nearly every query on (a one-edge reverse budget: the grid tier answers them)
     reg.snapshot.tune("stream_ecap", 6 if seed % 5 == 2 else 0)
-    reg.snapshot.tune("stream_chunk", 1 if seed % 4 == 1 else (16 if seed % 4 == 3 else 64))
     reg.snapshot.tune("stream_steal", 1 if seed % 3 == 1 else (8 if seed % 3 == 2 else 4))
-    reg.snapshot.tune("back", seed % 3)
+    reg.snapshot.tune("back_edges", 1 if seed % 4 == 3 else 0)
     qs = random_queries(rng, nss, rels, 3000, n_obj=40 + 20 * (seed % 6))
     depths = rng.integers(-1, 9, len(qs))
     q6 = np.asarray([it.tuple_ids(t) for t in qs], np.uint32)
@@ -81,8 +80,8 @@ def test_random_graphs_vs_oracle(seed):
         assert (out[inv] == dfs[inv]).all()
 
 
-@pytest.mark.parametrize("chunk,ecap", [(64, 512), (1, 512), (16, 0), (64, 3)])
-def test_stream_tier_long_rows_and_dense_cycles(chunk, ecap):
+@pytest.mark.parametrize("ecap", [512, 0, 3])
+def test_stream_tier_long_rows_and_dense_cycles(ecap):
     """Rows longer than a FIFO entry holds (2047 edges), dense cycles (the direct-mapped visited cache
     evicts and re-expands), many queries per wave on one hub: exact vs the oracle."""
     rng = np.random.default_rng(77)
@@ -93,7 +92,6 @@ def test_stream_tier_long_rows_and_dense_cycles(chunk, ecap):
     tuples += [RelationTuple.from_string(f"g:k{i}#m@u{i}") for i in range(0, 40, 5)]
     tuples += [RelationTuple.from_string(f"g:c{i}#m@v{i % 97}") for i in range(0, 2500, 11)]
     reg = Registry(tuples, [])
-    reg.snapshot.tune("stream_chunk", chunk)
     reg.snapshot.tune("stream_ecap", ecap)
     it = reg.interner
     qs = [RelationTuple.from_string(f"g:{r}#m@{u}") for r in ["hub", "k0", "k3", "c5", "c17", "c999"]
@@ -128,10 +126,11 @@ def test_heavy_path_overflow_star():
     assert e.last_stats["n_heavy"] + e.last_stats["n_back"] >= 1
 
 
-@pytest.mark.parametrize("back,grid_cap", [(0, 0), (1, 0), (2, 0), (0, 600), (0, 5000)])
-def test_tail_tiers_backward_and_grid(back, grid_cap):
-    # > 512 enqueued edges leaves the stream tier; with back=1/2 the backward tier (reverse search
-    # from the subject's holders) answers first and hands on what outgrows it to the grid tier
+@pytest.mark.parametrize("back_edges,grid_cap", [(1, 0), (0, 0), (1, 600), (1, 5000)])
+def test_tail_tiers_backward_and_grid(back_edges, grid_cap):
+    # > 512 enqueued edges leaves the stream tier; the backward tier (reverse search from the
+    # subject's holders) answers first and hands on what outgrows it to the grid tier -- with a
+    # one-edge reverse budget (back_edges 1) nearly everything goes on to the grid tier
     tuples = [RelationTuple.from_string(f"g:root#m@(g:c{i}#m)") for i in range(5000)]
     tuples += [RelationTuple.from_string(f"g:c{i}#m@(g:d{i % 1500}#m)") for i in range(5000)]
     tuples += [RelationTuple.from_string(f"g:d{i}#m@(g:e{i % 400}#m)") for i in range(1500)]
@@ -145,7 +144,7 @@ def test_tail_tiers_backward_and_grid(back, grid_cap):
     tuples += [RelationTuple.from_string(f"g:e{i}#m@pop") for i in range(400)]
     reg = Registry(tuples, [])
     e = reg.permission_engine()
-    e.snapshot.tune("back", back)
+    e.snapshot.tune("back_edges", back_edges)
     # grid_cap: the workspace's grid log holds 600 / 5000 entries, so rounds overflow, rerun with
     # fewer slots, and the queries that overflow it alone run in the shared full-size pool (the
     # per-query rounds: MS-BFS off); grid_cap 0 runs the grid tier's queries as MS-BFS (kg_msbfs.hip)
@@ -186,17 +185,15 @@ def _torch():
     return torch
 
 
-@pytest.mark.parametrize("n_tuples,gmax,ecap,unheld", [(200_000, 10, 512, 1), (300_000, 5, 512, 1), (300_000, 10, 512, 0),
-                                                        (300_000, 10, 32, 1), (300_000, 5, 0, 0), (300_000, 10, 512, 2),
-                                                        (300_000, 5, 32, 2)])
-def test_synthetic_graph_vs_oracle(n_tuples, gmax, ecap, unheld):
+@pytest.mark.parametrize("n_tuples,gmax,ecap", [(200_000, 10, 512), (300_000, 5, 512), (300_000, 10, 32),
+                                                 (300_000, 5, 0), (300_000, 5, 32)])
+def test_synthetic_graph_vs_oracle(n_tuples, gmax, ecap):
     """ecap: the stream tier's per-query edge budget (32: most long walks go on to the backward and
     grid tiers; 0: no budget, every walk finishes in the stream tier)."""
     torch = _torch()
     from keto_amd import _lib
     snap = Snapshot.synthetic(n_tuples, seed=20250131)
     snap.tune("stream_ecap", ecap)
-    snap.tune("resolve_unheld", unheld)  # 0: the node map is read for every query (round-1 order); 2: lazy bit
     n = 20000
     dq = torch.empty((n, 7), dtype=torch.int32, device="cuda")
     _lib.check(_lib.load().kg_synth_queries(snap.handle, 7, n, dq.data_ptr()), "kg_synth_queries")
@@ -792,15 +789,14 @@ def test_bench_tune_set_vs_oracle(preset, n_tuples):
         assert 0.05 < (out == 1).mean() < 0.95
 
 
-@pytest.mark.parametrize("ms,bidir,grid_cap,seed,tg_cap", [
-    (0, 1024, 0, 0, 256), (0, 1024, 0, 1, 256), (0, 0, 0, 0, 256), (0, 1024, 700, 2, 256), (0, 2, 0, 3, 256),
-    (0, 64, 0, 4, 256), (8, 0, 0, 0, 256), (1, 0, 0, 1, 256), (1, 0, 40, 2, 256), (2, 0, 300, 3, 256),
-    (8, 1024, 0, 5, 256), (16, 0, 0, 6, 256), (4, 0, 120, 7, 256), (8, 0, 0, 8, 0), (1, 0, 0, 9, 3)])
-def test_grid_bidirectional_dense_vs_oracle(ms, bidir, grid_cap, seed, tg_cap):
+@pytest.mark.parametrize("ms,grid_cap,seed,tg_cap", [
+    (0, 0, 0, 256), (0, 0, 1, 256), (0, 700, 2, 256), (0, 60, 3, 256), (0, 0, 4, 256), (8, 0, 0, 256), (1, 0, 1, 256),
+    (1, 40, 2, 256), (2, 300, 3, 256), (8, 0, 5, 256), (16, 0, 6, 256), (4, 120, 7, 256), (8, 0, 8, 0), (1, 0, 9, 3)])
+def test_grid_dense_vs_oracle(ms, grid_cap, seed, tg_cap):
     """The grid tier on dense graphs with cycles, hubs and subjects held only by rows nothing points
-    at: a tiny stream-tier edge budget and the backward tier off send nearly every query there; every
-    depth 2..9 is bit-exact with the oracle.  ms 0: the per-query rounds (kg_grid.hip), bidirectional
-    or forward only, with a log small enough that rounds overflow and rerun (grid_cap); ms 1: the
+    at: a tiny stream-tier edge budget and a one-edge backward budget send nearly every query there;
+    every depth 2..9 is bit-exact with the oracle.  ms 0: the per-query rounds (kg_grid.hip), with a
+    log small enough that rounds overflow and rerun (grid_cap); ms 1: the
     multi-source bit-parallel BFS (kg_msbfs.hip, 64 x ms queries per group), with
     level buffers small enough that rounds overflow and rerun with fewer groups, or that one group
     overflows them alone and the list falls back to the per-query rounds (grid_cap as grid_ms_cap);
@@ -823,8 +819,7 @@ def test_grid_bidirectional_dense_vs_oracle(ms, bidir, grid_cap, seed, tg_cap):
     reg = Registry(tuples, [])
     snap = reg.snapshot
     snap.tune("stream_ecap", 3)
-    snap.tune("back", 0)
-    snap.tune("grid_bidir", bidir)
+    snap.tune("back_edges", 1)  # the backward tier hands nearly every query on to the grid tier
     snap.tune("grid_ms", 1 if ms else 0)
     if ms:
         snap.tune("grid_ms_words", ms)

@@ -219,7 +219,7 @@ def _checker(driver, snap, rank, world, dist_, cap=256):
 
 
 # ------------------------------------------------------------------ GPU (HIP local steps)
-def _gpu_worker(rank, world, port, seed, outq, budget=None, back_budget=None, vis_mode=0):
+def _gpu_worker(rank, world, port, seed, outq, budget=None, back_budget=None):
     sys.path.insert(0, ROOT)
     import torch.distributed as dist
     from keto_amd.engine import Snapshot
@@ -237,7 +237,6 @@ def _gpu_worker(rank, world, port, seed, outq, budget=None, back_budget=None, vi
         snap.tune("shard_budget", budget)
     if back_budget is not None:
         snap.tune("shard_back_budget", back_budget)
-    snap.tune("shard_vis_mode", vis_mode)
     mine = np.array_split(np.arange(len(q)), world)[rank]
     chk = ShardedChecker(HipShardOps(snap), rank, world, dist_, device="cuda", cap=256)
     out = {}
@@ -250,11 +249,11 @@ def _gpu_worker(rank, world, port, seed, outq, budget=None, back_budget=None, vi
         dist.destroy_process_group()
 
 
-def _run_gpu(world, seed, budget=None, back_budget=None, vis_mode=0):
+def _run_gpu(world, seed, budget=None, back_budget=None):
     ctx = mp.get_context("spawn")
     outq = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_gpu_worker, args=(r, world, port, seed, outq, budget, back_budget, vis_mode))
+    ps = [ctx.Process(target=_gpu_worker, args=(r, world, port, seed, outq, budget, back_budget))
           for r in range(world)]
     for p in ps:
         p.start()
@@ -274,18 +273,16 @@ def _run_gpu(world, seed, budget=None, back_budget=None, vis_mode=0):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,budget,back_budget,vis_mode", [(1, None, None, 0), (2, None, None, 0), (1, 1, None, 0),
-                                                              (2, 2, None, 0), (1, 0, None, 0), (1, 1, 2, 0),
-                                                              (2, 1, 2, 0), (1, None, None, 1), (2, None, None, 1),
-                                                              (2, 1, 2, 1)])
-def test_sharded_hip_vs_oracle(world, budget, back_budget, vis_mode):
+@pytest.mark.parametrize("world,budget,back_budget", [(1, None, None), (2, None, None), (1, 1, None), (2, 2, None),
+                                                     (1, 0, None), (1, 1, 2), (2, 1, 2)])
+def test_sharded_hip_vs_oracle(world, budget, back_budget):
     """Random graphs (cycles, subject sets as subjects), against the oracle.  Budgets 1 / 2 escalate
     nearly every query that expands to the backward phase (reverse search from the subject's holders
     over all-gathered records); 0 turns escalation off; back_budget 2 sends most of them on to the
     final forward phase."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    _run_gpu(world, seed=11, budget=budget, back_budget=back_budget, vis_mode=vis_mode)
+    _run_gpu(world, seed=11, budget=budget, back_budget=back_budget)
 
 
 # ------------------------------------------------------------------ rewrites reached in sharded mode
@@ -552,7 +549,7 @@ def test_sharded_general_rewrites_vs_oracle(kind, world, driver):
 
 # ------------------------------------------------------------------ config C4 generator, sharded
 def _synth_worker(rank, world, port, n_tuples, n_q, gmax, backend, outq, preset=0, budget=None, back_budget=None,
-                  vis_mode=0, heavy=None, pack=None, vis=None, bucket=None, driver="py"):
+                  heavy=None, vis=None, bucket=None, driver="py"):
     sys.path.insert(0, ROOT)
     import torch.distributed as dist
     from keto_amd import _lib
@@ -570,11 +567,8 @@ def _synth_worker(rank, world, port, n_tuples, n_q, gmax, backend, outq, preset=
         snap.tune("shard_budget", budget)
     if back_budget is not None:
         snap.tune("shard_back_budget", back_budget)
-    snap.tune("shard_vis_mode", vis_mode)
     if heavy is not None:
         snap.tune("shard_heavy", heavy)
-    if pack is not None:
-        snap.tune("shard_pack", pack)
     if vis is not None:  # a per-batch visited table of 2^vis (query, node) keys: overflows, reruns larger
         snap.tune("shard_vis", vis)
     dq = torch.empty((n_q, 7), dtype=torch.int32, device="cuda")
@@ -599,14 +593,13 @@ def _synth_worker(rank, world, port, n_tuples, n_q, gmax, backend, outq, preset=
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,backend,budget,back_budget,vis_mode,heavy",
-                         [(1, None, None, None, 0, None), (1, "nccl", None, None, 0, None),
-                          (2, "gloo", None, None, 0, None), (1, None, 8, None, 0, None),
-                          (1, "nccl", 8, 64, 0, None), (2, "gloo", 8, 64, 0, None),
-                          (1, None, None, None, 1, None), (2, "gloo", None, None, 1, None),
-                          (1, None, None, None, 0, 256), (2, "gloo", None, None, 0, 256), (1, None, 8, 64, 0, 256),
-                          (1, None, None, None, 0, 0), (2, "gloo", None, None, 0, 0), (1, "nccl", None, None, 0, 0)])
-def test_sharded_c4_generator_vs_oracle(world, backend, budget, back_budget, vis_mode, heavy):
+@pytest.mark.parametrize("world,backend,budget,back_budget,heavy",
+                         [(1, None, None, None, None), (1, "nccl", None, None, None),
+                          (2, "gloo", None, None, None), (1, None, 8, None, None),
+                          (1, "nccl", 8, 64, None), (2, "gloo", 8, 64, None),
+                          (1, None, None, None, 256), (2, "gloo", None, None, 256), (1, None, 8, 64, 256),
+                          (1, None, None, None, 0), (2, "gloo", None, None, 0), (1, "nccl", None, None, 0)])
+def test_sharded_c4_generator_vs_oracle(world, backend, budget, back_budget, heavy):
     """Config C4's generator, hash-sharded: world 1 with every level on the device (no host round
     trip per level), world 1 through torch.distributed over RCCL ("nccl": the metadata and record
     all-to-alls run on device tensors), and world 2 (two ranks on one GPU, gloo).  Against the
@@ -616,8 +609,7 @@ def test_sharded_c4_generator_vs_oracle(world, backend, budget, back_budget, vis
     grid-wide hub kernel (k_shard_heavy's tile map), in the forward and the backward phase."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    _run_synth(world, backend, 300_000, 20_000, 10, preset=0, budget=budget, back_budget=back_budget, vis_mode=vis_mode,
-               heavy=heavy)
+    _run_synth(world, backend, 300_000, 20_000, 10, preset=0, budget=budget, back_budget=back_budget, heavy=heavy)
 
 
 @pytest.mark.gpu
@@ -638,15 +630,13 @@ def test_sharded_in_library_escalation_vs_oracle(world, backend, driver, budget,
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("pack,heavy,gmax", [(0, None, 10), (1, None, 10), (1, 0, 10), (1, 256, 5), (0, 0, 5)])
-def test_sharded_packed_records_vs_oracle(pack, heavy, gmax):
-    """kg_snapshot_tune("shard_pack"): in the one-rank device level loop a locally owned child travels as
-    a packed record (its set-row begin and length instead of its node id: the next level reads no
-    adj_off pair; its visited key lives in a separate half of the key space).  On and off, with every
-    row / rows over 256 edges through the hub kernel, bit-exact with the oracle."""
+@pytest.mark.parametrize("heavy,gmax", [(None, 10), (0, 10), (256, 5), (0, 5)])
+def test_sharded_one_rank_levels_vs_oracle(heavy, gmax):
+    """The one-rank device level loop with every row / rows over 256 edges through the hub kernel and
+    at two global depths, bit-exact with the oracle."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    _run_synth(1, None, 300_000, 20_000, gmax, preset=0, heavy=heavy, pack=pack)
+    _run_synth(1, None, 300_000, 20_000, gmax, preset=0, heavy=heavy)
 
 
 @pytest.mark.gpu
@@ -662,15 +652,15 @@ def test_sharded_c3_rewrites_vs_oracle(world, backend):
     _run_synth(world, backend, 150_000, 6000, 10, preset=1)
 
 
-def _run_synth(world, backend, n_tuples, n_q, gmax, preset, budget=None, back_budget=None, vis_mode=0, heavy=None,
-               pack=None, vis=None, bucket=None, driver="py"):
+def _run_synth(world, backend, n_tuples, n_q, gmax, preset, budget=None, back_budget=None, heavy=None,
+               vis=None, bucket=None, driver="py"):
     from keto_amd.engine import Snapshot
     from oracle.oracle import POLICY_CANONICAL, Oracle
     ctx = mp.get_context("spawn")
     outq = ctx.Queue()
     port = _free_port()
     ps = [ctx.Process(target=_synth_worker, args=(r, world, port, n_tuples, n_q, gmax, backend, outq, preset, budget,
-                                                  back_budget, vis_mode, heavy, pack, vis, bucket, driver))
+                                                  back_budget, heavy, vis, bucket, driver))
           for r in range(world)]
     for p in ps:
         p.start()
