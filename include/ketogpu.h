@@ -136,7 +136,7 @@ typedef struct {
   uint64_t light_span_ticks;            /* k_stream4: first wave start to last wave end  */
   uint64_t light_wave_max_ticks;        /* k_stream4: longest wave lifetime              */
   /* the tail tier's level kernels (round 6): the grid tier's k_grid_level or the MS-BFS k_ms_level */
-  double tail_ms;                       /* summed device time of those launches (HIP events per launch) */
+  double tail_ms;                       /* summed device time of those launches (HIP events per launch; only with kg_snapshot_tune "level_events" 1) */
   uint64_t tail_launches;               /* level launches of the batch (the first 64 are timed)          */
   uint64_t tail_kind;                   /* 0 none, 1 k_grid_level, 2 k_ms_level                          */
   uint64_t tail_rows, tail_edges, tail_probes, tail_logged; /* the tail tier's share of the counters    */

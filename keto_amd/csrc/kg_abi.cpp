@@ -500,8 +500,14 @@ static int tune_one(Snapshot* s, const char* key, int64_t value) {
     return 0;
   }
   if (strcmp(key, "expand_gw") == 0 || strcmp(key, "expand_skip_lds") == 0) {
-    if (value < 0 || value > 1) return set_error(-2, "%s must be 0 or 1", key);
+    if (value < 0 || value > (strcmp(key, "expand_gw") == 0 ? 1 : 2))
+      return set_error(-2, "%s must be 0 or 1 (expand_skip_lds: 0, 1 or 2)", key);
     (strcmp(key, "expand_gw") == 0 ? s->expand_gw : s->expand_skip_lds) = (int)value;
+    return 0;
+  }
+  if (strcmp(key, "level_events") == 0) {
+    if (value < 0 || value > 1) return set_error(-2, "level_events must be 0 or 1");
+    s->level_events = (int)value;
     return 0;
   }
   if (strcmp(key, "expand_gw_wait_us") == 0) {

@@ -876,7 +876,10 @@ int check_batch_begin(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n, 
   // and each tail-tier level launch (Workspace::lev_mark)
   if (stats && !w->ev[0])
     for (auto& e : w->ev) HIPC(hipEventCreate(&e));
-  w->lev_on = stats != nullptr;
+  // per-launch level events only when asked for (kg_snapshot_tune "level_events"): an event record
+  // between back-to-back launches leaves a gap in the stream (round 6: -15 % on the headline with
+  // stats on every batch)
+  w->lev_on = stats != nullptr && s->level_events != 0;
   w->lev_n = 0;
   w->lev_kind = 0;
   w->lev_launches = 0;

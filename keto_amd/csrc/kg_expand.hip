@@ -60,6 +60,8 @@ struct ExpCtl {
   // floor under k_expand_lds.
   alignas(128) uint32_t ahead[8 * 32];
   uint32_t rhead[8 * 32];
+  uint32_t qhead[8 * 32];  // the 64-lane pass's heads over pass 0's overflow list
+  uint32_t p0_count, pad3[31];
 };
 
 __device__ __forceinline__ uint32_t ld_sc1(const uint32_t* p) {
@@ -484,28 +486,281 @@ __device__ int expand_root_x(const DevSnap& s, Store& st, const kg_set& root, in
   return status;
 }
 
-__global__ __launch_bounds__(256) void k_expand_lds(DevSnap s, const kg_set* __restrict__ roots, uint32_t n,
+// ------------------------------------------------------------------ pass 0: 16-lane walkers (round 6)
+// C5's ~100 k hot roots average ~45 records (a handful of expanded sets each): one 64-lane wave per
+// root left most lanes idle on every row chunk and paid a whole wave's chain of dependent round trips
+// per root.  Here a wave runs FOUR roots at once, one per 16-lane group, with expand_root's exact
+// pre-order (the same chunk scan, 16 entries at a time, first-candidate rule, one visited set per
+// request).  Each walker has its own LDS visited hash and record stream; a root that outgrows the
+// small hash or SW_RECS records is given up (its chunks are abandoned) and redone by the 64-lane pass.
+constexpr int SW = 16;
+constexpr int SW_VL2 = 9;           // visited-hash slots per walker (512)
+constexpr uint32_t SW_CAP = 224;    // visited sets per walker (hash load <= ~0.5)
+constexpr uint32_t SW_RECS = 2048;  // records per root before it is handed to the 64-lane pass
+__device__ __forceinline__ int sw_lane() { return lane_id() & (SW - 1); }
+__device__ __forceinline__ int sw_base() { return lane_id() & ~(SW - 1); }
+__device__ __forceinline__ uint32_t sw_bits(uint64_t m) { return (uint32_t)(m >> sw_base()) & 0xFFFFu; }
+__device__ __forceinline__ uint32_t sw_below(uint32_t m) { return (uint32_t)__popc(m & ((1u << sw_lane()) - 1)); }
+
+struct SubStore {
+  uint32_t* vis;  // 1 << SW_VL2 slots
+  __device__ void reset() const {
+    for (int i = sw_lane() * 4; i < (1 << SW_VL2); i += SW * 4)
+      *reinterpret_cast<uint4*>(&vis[i]) = make_uint4(NONE, NONE, NONE, NONE);
+    __builtin_amdgcn_wave_barrier();
+  }
+  __device__ bool insert(uint32_t key) const {
+    uint32_t h = (key * 2654435761u) >> (32 - SW_VL2);
+    for (int p = 0; p < (1 << SW_VL2); p++) {
+      const uint32_t old = atomicCAS(&vis[h], NONE, key);
+      if (old == NONE) return true;
+      if (old == key) return false;
+      h = (h + 1) & ((1u << SW_VL2) - 1);
+    }
+    return true;
+  }
+  __device__ bool contains(uint32_t key) const {
+    uint32_t h = (key * 2654435761u) >> (32 - SW_VL2);
+    for (int p = 0; p < (1 << SW_VL2); p++) {
+      const uint32_t k = vis[h];
+      if (k == key) return true;
+      if (k == NONE) return false;
+      h = (h + 1) & ((1u << SW_VL2) - 1);
+    }
+    return false;
+  }
+};
+
+// group-uniform values: S.cur / S.pos / S.first / S.ok are the same in the walker's 16 lanes
+__device__ __forceinline__ uint32_t sw_alloc_chunk(Stream& S) {
+  uint32_t c = 0;
+  if (sw_lane() == 0) c = claim_chunk(S.ctl, S.n_chunks);
+  c = __shfl(c, sw_base(), 64);
+  if (c >= S.n_chunks) {
+    if (sw_lane() == 0) S.ctl->overflow = 1;
+    S.ok = false;
+    return NONE;
+  }
+  if (sw_lane() == 0) S.next[c] = NONE;
+  return c;
+}
+
+__device__ __forceinline__ void sw_emit(Stream& S, bool pred, const kg_tree_node& r) {
+  const uint32_t m = sw_bits(__ballot(pred));
+  if (!m || !S.ok) return;
+  const uint32_t cnt = (uint32_t)__popc(m), rank = sw_below(m);
+  const uint32_t room = CHUNK - S.pos;
+  uint32_t nxt = NONE;
+  if (cnt > room) {
+    nxt = sw_alloc_chunk(S);
+    if (!S.ok) return;
+    if (sw_lane() == 0) S.next[S.cur] = nxt;
+  }
+  if (pred) {
+    if (rank < room) S.arena[(size_t)S.cur * CHUNK + S.pos + rank] = r;
+    else S.arena[(size_t)nxt * CHUNK + (rank - room)] = r;
+  }
+  if (cnt > room) {
+    S.cur = nxt;
+    S.pos = cnt - room;
+  } else {
+    S.pos += cnt;
+  }
+}
+
+// marks `node` (lanes with `offer`); false when the walker's visited cap would be passed
+__device__ __forceinline__ bool sw_add(const SubStore& st, bool offer, uint32_t node, uint32_t& n_vis) {
+  const bool fresh = offer && st.insert(node);
+  const uint32_t cnt = (uint32_t)__popc(sw_bits(__ballot(fresh)));
+  if (n_vis + cnt > SW_CAP) return false;
+  n_vis += cnt;
+  return true;
+}
+
+// expand_root (above) on one 16-lane walker: identical records in identical order, or EXP_OVERFLOW
+__device__ int expand_root_sw(const DevSnap& s, const SubStore& st, const kg_set& root, int32_t global,
+                              ExpFrame* stack, uint32_t stack_cap, Stream& S, uint32_t& n_records) {
+  const int gl = sw_lane(), gb = sw_base();
+  S.ok = true;
+  S.pos = 0;
+  S.first = S.cur = sw_alloc_chunk(S);
+  n_records = 0;
+  if (!S.ok) return EXP_ARENA;
+  int32_t d = root.max_depth;
+  if (d <= 0 || global < d) d = global;  // engine.go:37-39
+  if (root.sns == KG_SUBJECT_ID) {       // SubjectID -> Leaf
+    sw_emit(S, gl == 0, rec_subject(s, root.sobj < 0x7FFFFFFFu ? root.sobj : 0x7FFFFFFFu));
+    n_records = 1;
+    return S.ok ? EXP_OK : EXP_ARENA;
+  }
+  const uint32_t rn = nmap_find(s, root.sns, root.srel, root.sobj);
+  if (rn == NONE) return EXP_OK;  // no rows anywhere: nil
+  st.reset();
+  uint32_t n_vis = 0;
+  sw_add(st, gl == 0, rn, n_vis);  // marks the root visited
+  const uint64_t rb0 = s.row_off[rn], re0 = s.row_off[rn + 1];
+  if (rb0 == re0) return EXP_OK;  // no rows: nil
+  if (d <= 1) {
+    sw_emit(S, gl == 0, rec_set(s, 2, rn, 0));
+    n_records = 1;
+    return S.ok ? EXP_OK : EXP_ARENA;
+  }
+  sw_emit(S, gl == 0, rec_set(s, 1, rn, (uint32_t)(re0 - rb0)));
+  uint32_t count = 1;
+  uint32_t sp = 0;
+  ExpFrame F{rb0, rn, 0, (uint32_t)(re0 - rb0), d};
+  int status = EXP_OK;
+  for (;;) {
+    const uint64_t rb = F.rb, re = F.rb + F.len;
+    const bool can_expand = F.d - 1 >= 2;
+    bool pushed = false;
+    while (rb + F.cursor < re) {
+      if (count > SW_RECS) {
+        status = EXP_OVERFLOW;
+        break;
+      }
+      const uint64_t i = rb + F.cursor + gl;
+      const bool valid = i < re;
+      const uint32_t sub = valid ? s.row_subj[i] : 0;
+      bool cand = false;
+      uint64_t crb = 0, cre = 0;
+      if (valid && can_expand && (sub & SET_BIT)) {
+        const uint32_t c = sub & ~SET_BIT;
+        crb = s.row_off[c];
+        cre = s.row_off[c + 1];
+        cand = cre > crb && !st.contains(c);
+      }
+      const uint32_t mc = sw_bits(__ballot(cand));
+      const uint32_t p = mc ? (uint32_t)(__ffs(mc) - 1) : (uint32_t)SW;
+      const bool leaf = valid && (uint32_t)gl < p;
+      if (!can_expand && !sw_add(st, leaf && (sub & SET_BIT), sub & ~SET_BIT, n_vis)) {
+        status = EXP_OVERFLOW;
+        break;
+      }
+      sw_emit(S, leaf, rec_subject(s, sub));
+      count += (uint32_t)__popc(sw_bits(__ballot(leaf)));
+      if (!S.ok) return EXP_ARENA;
+      if (p == (uint32_t)SW) {
+        F.cursor += (uint32_t)min<uint64_t>(SW, re - (rb + F.cursor));
+        continue;
+      }
+      const int src = gb + (int)p;
+      const uint32_t csub = __shfl(sub, src, 64);
+      const uint32_t cnode = csub & ~SET_BIT;
+      const uint32_t clen = (uint32_t)__shfl((uint32_t)(cre - crb), src, 64);
+      const uint64_t cbeg = ((uint64_t)(uint32_t)__shfl((uint32_t)(crb >> 32), src, 64) << 32) |
+                            (uint32_t)__shfl((uint32_t)crb, src, 64);
+      F.cursor += p + 1;
+      const uint32_t before = n_vis;
+      if (!sw_add(st, gl == 0, cnode, n_vis)) {
+        status = EXP_OVERFLOW;
+        break;
+      }
+      if (n_vis == before) {  // already visited: BuildTree -> nil -> Leaf{row subject}
+        sw_emit(S, gl == 0, rec_subject(s, csub));
+        count++;
+        if (!S.ok) return EXP_ARENA;
+        continue;
+      }
+      sw_emit(S, gl == 0, rec_set(s, 1, cnode, clen));
+      count++;
+      if (!S.ok) return EXP_ARENA;
+      if (sp >= stack_cap) {
+        status = EXP_OVERFLOW;
+        break;
+      }
+      if (gl == 0) stack[sp] = F;
+      sp++;
+      F = ExpFrame{cbeg, cnode, 0, clen, F.d - 1};
+      pushed = true;
+      break;
+    }
+    if (status != EXP_OK) break;
+    if (pushed) continue;
+    if (sp == 0) break;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    sp--;
+    F = stack[sp];
+  }
+  n_records = count;
+  return status;
+}
+
+// Pass 0: every root, 16 walkers per workgroup; what a walker gives up goes to the p0 list (the 64-lane
+// pass).  Roots are dequeued through ExpCtl::rhead (8 ranges), one walker at a time.
+__global__ __launch_bounds__(256) void k_expand_sub(DevSnap s, const kg_set* __restrict__ roots, uint32_t n,
                                                     int32_t global, ExpCtl* ctl, RootOut* outs, kg_tree_node* arena,
                                                     uint32_t* next, uint32_t n_chunks, ExpFrame* stacks,
-                                                    uint32_t stack_cap, uint32_t* p2_list, int skip) {
-  __shared__ WaveLds lds_all[4];
-  const int wave = threadIdx.x >> 6, lane = lane_id();
-  LdsStore st{&lds_all[wave]};
-  ExpFrame* stack = stacks + (size_t)(blockIdx.x * 4 + wave) * stack_cap;
+                                                    uint32_t stack_cap, uint32_t* p0_list) {
+  __shared__ uint32_t vis_all[256 / SW][1 << SW_VL2];
+  __shared__ unsigned long long s_recs;
+  if (threadIdx.x == 0) s_recs = 0;
+  __syncthreads();
+  const int walker = threadIdx.x / SW, gl = sw_lane();
+  const SubStore st{vis_all[walker]};
+  ExpFrame* stack = stacks + ((size_t)blockIdx.x * (256 / SW) + walker) * stack_cap;
   Stream S{arena, next, n_chunks, ctl, 0, 0, 0, true};
   unsigned long long recs = 0;
-  // roots in 8 ranges, each dequeued through its own head (ExpCtl::rhead): this XCD's range first
   const uint32_t rper = (n + 7) / 8;
   uint32_t r_at = blockIdx.x & 7, r_tried = 0;
   for (;;) {
     uint32_t ri = NONE;
-    if (lane == 0)
+    if (gl == 0)
       for (; r_tried < 8; r_tried++, r_at = (r_at + 1) & 7) {
         const uint32_t lo = r_at * rper, hi = min(n, lo + rper);
         if (lo >= hi || ld_sc1(&ctl->rhead[r_at * 32]) >= hi - lo) continue;
         const uint32_t k = atomicAdd(&ctl->rhead[r_at * 32], 1u);
         if (k < hi - lo) {
           ri = lo + k;
+          break;
+        }
+      }
+    ri = __shfl(ri, sw_base(), 64);
+    if (ri >= n) break;
+    uint32_t nr = 0;
+    const int r = expand_root_sw(s, st, roots[ri], global, stack, stack_cap, S, nr);
+    if (gl == 0) {
+      if (r == EXP_OVERFLOW) {
+        p0_list[atomicAdd(&ctl->p0_count, 1u)] = ri;
+        outs[ri] = RootOut{NONE, 0};
+      } else {
+        outs[ri] = RootOut{S.first, nr};
+        recs += nr;
+      }
+    }
+  }
+  if (gl == 0 && recs) atomicAdd(&s_recs, recs);  // one device atomic per workgroup, not per walker
+  __syncthreads();
+  if (threadIdx.x == 0 && s_recs) atomicAdd(&ctl->records, s_recs);
+}
+
+__global__ __launch_bounds__(256) void k_expand_lds(DevSnap s, const kg_set* __restrict__ roots, uint32_t n,
+                                                    int32_t global, ExpCtl* ctl, RootOut* outs, kg_tree_node* arena,
+                                                    uint32_t* next, uint32_t n_chunks, ExpFrame* stacks,
+                                                    uint32_t stack_cap, uint32_t* p2_list, int skip,
+                                                    const uint32_t* qlist) {
+  __shared__ WaveLds lds_all[4];
+  const int wave = threadIdx.x >> 6, lane = lane_id();
+  LdsStore st{&lds_all[wave]};
+  ExpFrame* stack = stacks + (size_t)(blockIdx.x * 4 + wave) * stack_cap;
+  Stream S{arena, next, n_chunks, ctl, 0, 0, 0, true};
+  unsigned long long recs = 0;
+  // roots in 8 ranges, each dequeued through its own head (ExpCtl::rhead; with qlist -- pass 0's
+  // overflows, ctl->p0_count of them -- ExpCtl::qhead): this XCD's range first
+  const uint32_t cnt = qlist ? ctl->p0_count : n;
+  uint32_t* heads = qlist ? ctl->qhead : ctl->rhead;
+  const uint32_t rper = (cnt + 7) / 8;
+  uint32_t r_at = blockIdx.x & 7, r_tried = 0;
+  for (;;) {
+    uint32_t ri = NONE;
+    if (lane == 0)
+      for (; r_tried < 8; r_tried++, r_at = (r_at + 1) & 7) {
+        const uint32_t lo = r_at * rper, hi = min(cnt, lo + rper);
+        if (lo >= hi || ld_sc1(&heads[r_at * 32]) >= hi - lo) continue;
+        const uint32_t k = atomicAdd(&heads[r_at * 32], 1u);
+        if (k < hi - lo) {
+          ri = qlist ? qlist[lo + k] : lo + k;
           break;
         }
       }
@@ -1111,6 +1366,10 @@ struct ExpandBufs {
   size_t stacks_bytes = 0;
   uint32_t* bm = nullptr;  // [pass-2 tables | pass-3 bitmap] | pass-2 lists | pass-3 list
   size_t bm_bytes = 0;
+  // the pass-2 tables and the pass-3 bitmap need clearing: fresh memory, or a call that ended early (an
+  // arena rerun or an error can leave keys behind; a completed call leaves them clear -- every root's
+  // walk removes its keys, an overflowing one zeroes its table)
+  bool bm_dirty = true;
   kg_tree_node* arena = nullptr;
   uint32_t* next = nullptr;
   uint32_t chunks = 0;
@@ -1261,6 +1520,10 @@ int expand_batch(Snapshot* s, hipStream_t stream, void** bufs, const kg_set* roo
   bool gw_on = s->expand_gw != 0;
   const uint32_t gw_n[2] = {std::max<uint32_t>(1, (uint32_t)s->n_cu / 2), 4};
   const uint32_t grid1 = (uint32_t)s->n_cu * 2, slots1 = grid1 * 4;
+  // pass 0 (16-lane walkers, 16 per workgroup) unless expand_skip_lds says otherwise (1: no LDS pass
+  // at all, 2: the 64-lane pass takes every root)
+  const bool sub_on = s->expand_skip_lds == 0;
+  const uint32_t grid0 = (uint32_t)s->n_cu * 2, slots0 = sub_on ? grid0 * (256 / SW) : 0u;
   const uint64_t nn = std::max<uint32_t>(s->ds.n_nodes, 1), words = ((nn + 31) / 32 + 1 + 3) & ~3ull;
   // pass 2: 2 slots per CU, each a visited hash + list of up to 256 Ki nodes (~5 MB a slot, <= 2 GiB;
   // 4 per CU measured the same on C5)
@@ -1269,7 +1532,7 @@ int expand_batch(Snapshot* s, hipStream_t stream, void** bufs, const kg_set* roo
   while (tsize < 2 * cap2 + 128) tsize <<= 1;
   const uint32_t slots2 =
       (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)s->n_cu * 2, (2ull << 30) / ((tsize + cap2) * 4)));
-  uint32_t n_chunks = (uint32_t)std::min<uint64_t>(1u << 22, std::max<uint64_t>(4096, n * 2 + slots1));
+  uint32_t n_chunks = (uint32_t)std::min<uint64_t>(1u << 22, std::max<uint64_t>(4096, n * 2 + slots1 + slots0));
   n_chunks = std::max(n_chunks, B.chunks);  // an arena that grew for earlier calls stays grown
   const size_t clear_words = (size_t)slots2 * tsize + words;
   int rc = 0;
@@ -1280,14 +1543,14 @@ int expand_batch(Snapshot* s, hipStream_t stream, void** bufs, const kg_set* roo
     const size_t cap = std::max(n, 2 * B.n_cap);
     B.n_cap = 0;
     if ((e = grow(&B.d_roots, a, cap * sizeof(kg_set))) != hipSuccess || (e = grow(&B.outs, b, cap * sizeof(RootOut))) != hipSuccess ||
-        (e = grow(&B.p2, c, cap * 16)) != hipSuccess)  // p2 | p3 | ga | gb queues
+        (e = grow(&B.p2, c, cap * 20)) != hipSuccess)  // p2 | p3 | ga | gb | p0 queues
       fail("hipMalloc", e);
     else
       B.n_cap = cap;
   }
   if (!rc && !B.ctl && (e = hipMalloc(&B.ctl, sizeof(ExpCtl))) != hipSuccess) fail("hipMalloc", e);
   if (!rc && (e = grow(&B.stacks, B.stacks_bytes,
-                       (size_t)(slots1 + slots2 + 1 + gw_n[0] + gw_n[1]) * stack_cap * sizeof(ExpFrame))) != hipSuccess)
+                       (size_t)(slots1 + slots2 + 1 + gw_n[0] + gw_n[1] + slots0) * stack_cap * sizeof(ExpFrame))) != hipSuccess)
     fail("hipMalloc", e);
   // gather-walk slots (~0.9 GB a lane); without them the pass-1 overflows go to the hash pass directly
   for (int k = 0; k < 2 && gw_on && !rc; k++)
@@ -1295,8 +1558,12 @@ int expand_batch(Snapshot* s, hipStream_t stream, void** bufs, const kg_set* roo
       (void)hipGetLastError();
       gw_on = false;
     }
-  if (!rc && (e = grow(&B.bm, B.bm_bytes, (clear_words + (size_t)slots2 * cap2 + nn) * 4)) != hipSuccess)
-    fail("hipMalloc", e);
+  {
+    const uint32_t* bm0 = B.bm;
+    if (!rc && (e = grow(&B.bm, B.bm_bytes, (clear_words + (size_t)slots2 * cap2 + nn) * 4)) != hipSuccess)
+      fail("hipMalloc", e);
+    if (B.bm != bm0) B.bm_dirty = true;
+  }
   for (auto& x : B.ev)
     if (!rc && !x && (e = hipEventCreate(&x)) != hipSuccess) fail("hipEventCreate", e);
   uint32_t* lists = B.bm + clear_words;
@@ -1314,16 +1581,22 @@ int expand_batch(Snapshot* s, hipStream_t stream, void** bufs, const kg_set* roo
       }
       B.chunks = n_chunks;
     }
-    // every attempt starts from clear visited bitmaps (an arena overflow aborts roots mid-way)
-    if ((e = hipMemsetAsync(B.bm, 0, clear_words * 4, stream)) != hipSuccess ||
+    // every attempt starts from clear visited tables (an arena overflow aborts roots mid-way); a lane whose
+    // last call completed has them clear already (C5: ~1.6 GB of memset per call before round 6)
+    if (((B.bm_dirty || attempt > 0) && (e = hipMemsetAsync(B.bm, 0, clear_words * 4, stream)) != hipSuccess) ||
         (e = hipMemsetAsync(B.ctl, 0, sizeof(ExpCtl), stream)) != hipSuccess ||
         (gw_on && (e = hipMemsetAsync(B.p2 + 2 * n, 0, n * 4, stream)) != hipSuccess)) {  // ga: published as ri + 1
       fail("memset", e);
       break;
     }
     (void)hipEventRecord(B.ev[0], stream);
+    if (sub_on)
+      hipLaunchKernelGGL(k_expand_sub, dim3(grid0), dim3(256), 0, stream, s->ds, B.d_roots, (uint32_t)n, global, B.ctl,
+                         B.outs, B.arena, B.next, n_chunks,
+                         B.stacks + (size_t)(slots1 + slots2 + 1 + gw_n[0] + gw_n[1]) * stack_cap, stack_cap, B.p2 + 4 * n);
     hipLaunchKernelGGL(k_expand_lds, dim3(grid1), dim3(256), 0, stream, s->ds, B.d_roots, (uint32_t)n, global, B.ctl,
-                       B.outs, B.arena, B.next, n_chunks, B.stacks, stack_cap, B.p2, s->expand_skip_lds);
+                       B.outs, B.arena, B.next, n_chunks, B.stacks, stack_cap, B.p2, s->expand_skip_lds == 1 ? 1 : 0,
+                       sub_on ? (const uint32_t*)(B.p2 + 4 * n) : nullptr);
     // pass-1 overflows: gather-walk small slots -> large slots -> the hash pass (or straight to it)
     uint32_t* q_hash = B.p2;
     uint32_t* c_hash = &B.ctl->p2_count;
@@ -1370,6 +1643,7 @@ int expand_batch(Snapshot* s, hipStream_t stream, void** bufs, const kg_set* roo
     }
     n_chunks *= 4;  // grow the arena and rerun (outputs are rewritten from scratch)
   }
+  B.bm_dirty = rc != 0 || h.overflow != 0;  // only a completed call leaves the tables clear
   std::vector<RootOut> ho(n);
   if (!rc && (e = hipMemcpyAsync(ho.data(), B.outs, n * sizeof(RootOut), hipMemcpyDeviceToHost, stream)) != hipSuccess)
     fail("D2H", e);
@@ -1417,6 +1691,7 @@ int expand_batch(Snapshot* s, hipStream_t stream, void** bufs, const kg_set* roo
     out->kernel_ms = (double)a + (double)b;
   }
   if (rc) {
+    B.bm_dirty = true;
     if (out->pinned) tree_pool_put(out->nodes, total * sizeof(kg_tree_node));
     free(out->root_off);
     memset(out, 0, sizeof *out);

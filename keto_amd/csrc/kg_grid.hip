@@ -32,7 +32,7 @@
 
 namespace kg {
 
-constexpr uint32_t GT = 256;                 // edges per tile = threads per workgroup
+constexpr uint32_t GT = 512;                 // edges per tile: two per thread of the 256-thread workgroup
 constexpr uint64_t TILE_CAP = 1ull << 24;    // tiles per level with a tile_first entry (beyond: log search)
 constexpr int EDGE_BITS = 36;                // packed level counter: entries (28 bits) | edges (36 bits)
 constexpr uint64_t EDGE_MASK = (1ull << EDGE_BITS) - 1;
@@ -148,7 +148,7 @@ __device__ __forceinline__ void grid_append(GridCtl* ctl, GridLv* lvs, const Gri
 // atomic per GB_BUF entries (round 6): every append of a level hits the same counter, and same-address
 // atomics serialise at the memory side (~11 ns each, MI355X_MICROARCH.md "dequeue") -- one per 256-edge
 // tile with an append was the level's floor on C3 (~52 us per level, profiles/r6a_c3_timeline.txt).
-constexpr uint32_t GB_BUF = 1024;
+constexpr uint32_t GB_BUF = 512;
 struct GridBuf {
   uint32_t slot[GB_BUF], rb[GB_BUF], len[GB_BUF], pre[GB_BUF];
   uint32_t n, edges;
@@ -263,7 +263,42 @@ __device__ __forceinline__ uint64_t entry_of(const uint64_t* ex, uint64_t base, 
   return lo;
 }
 
-// One level: one thread per edge, one GT-edge tile per workgroup iteration.  Level L expands the
+// Two visited-set inserts whose first probes are issued together (k_grid_level: a thread's two edges).
+__device__ __forceinline__ void gh_insert2(uint64_t* H, uint64_t mask, bool a0, uint64_t k0, bool a1, uint64_t k1,
+                                           int& r0, int& r1) {
+  const uint64_t h0 = mix64(k0 & ((1ull << GH_EPOCH_SHIFT) - 1)) & mask, h1 = mix64(k1 & ((1ull << GH_EPOCH_SHIFT) - 1)) & mask;
+  const uint64_t c0 = a0 ? H[h0] : 0ull, c1 = a1 ? H[h1] : 0ull;
+  r0 = r1 = 0;
+  // the common case: the home slot is this key (seen) or empty of this round (CAS it)
+  const uint64_t ep0 = k0 >> GH_EPOCH_SHIFT, ep1 = k1 >> GH_EPOCH_SHIFT;
+  bool done0 = !a0, done1 = !a1;
+  if (a0 && c0 == k0) done0 = true;
+  if (a1 && c1 == k1) done1 = true;
+  if (!done0 && (c0 >> GH_EPOCH_SHIFT) != ep0) {
+    const uint64_t old = atomicCAS((unsigned long long*)&H[h0], (unsigned long long)c0, (unsigned long long)k0);
+    if (old == c0) {
+      r0 = 1;
+      done0 = true;
+    } else if (old == k0) {
+      done0 = true;
+    }
+  }
+  if (!done1 && (c1 >> GH_EPOCH_SHIFT) != ep1) {
+    const uint64_t old = atomicCAS((unsigned long long*)&H[h1], (unsigned long long)c1, (unsigned long long)k1);
+    if (old == c1) {
+      r1 = 1;
+      done1 = true;
+    } else if (old == k1) {
+      done1 = true;
+    }
+  }
+  if (!done0) r0 = gh_insert(H, mask, k0);  // the general probe from the home slot
+  if (!done1) r1 = gh_insert(H, mask, k1);
+}
+
+// One level: two edges per thread (e and e + 256), one GT = 512-edge tile per workgroup iteration
+// (round 6; one edge per thread before: a tile's chain of dependent trips -- tile map, staged
+// entries, adjx, visited CAS, probe, append -- now covers twice the edges).  Level L expands the
 // nodes found at hop L (rest depth D - L >= 2) into hop L + 1: every child is probed (checkDirect at
 // its shallowest depth) and kept for the next level while D - (L + 1) >= 2 and its set row is non-empty.
 __global__ __launch_bounds__(256) void k_grid_level(DevSnap s, GridLog lg, int level, GridSlots sl, uint64_t* H,
@@ -326,56 +361,69 @@ __global__ __launch_bounds__(256) void k_grid_level(DevSnap s, GridLog lg, int l
         s_hit[i] = sl.hit[sl_i];
       }
     __syncthreads();
-    const uint64_t e = t0 + threadIdx.x;
-    bool app = false;
-    uint32_t slot = 0, cb = 0, clen = 0;
-    if (e < t1) {
-      uint64_t beg;
-      uint32_t rb, hit;
-      uint2 si;  // (tagged subject, rest depth of the root)
-      if (use_lds) {
-        uint32_t lo = 0, hi = (uint32_t)cnt;  // largest i < cnt with s_beg[i] <= e
-        while (hi - lo > 1) {
-          const uint32_t mid = (lo + hi) >> 1;
-          if (s_beg[mid] <= e) lo = mid;
-          else hi = mid;
-        }
-        beg = s_beg[lo];
-        slot = s_slot[lo];
-        rb = s_rb[lo];
-        si = s_info[lo];
-        hit = s_hit[lo];
-      } else {
-        const uint64_t j = entry_of(lg.ex, lb, j0, j0 + cnt, e);
-        beg = lg.ex[lb + j];
-        slot = lg.slot[lb + j];
-        rb = lg.rb[lb + j];
-        hit = sl.hit[slot];
-        si = sl.info[slot];
-      }
-      const int D = (int)si.y;
-      if (!hit) {  // answered at tile start: the edge is not even loaded
-        const AdjX x = s.adjx[rb + (e - beg)];
-        cb = x.begin;
-        clen = adjx_len(s, x);
-        // hop level+1 is expanded at the next level while its rest depth D - (level + 1) >= 2
-        const bool keep = clen > 0 && level + 2 <= D - 1;
-        bool fresh = true;
-        if (keep) {
-          const int ins = gh_insert(H, mask, gh_key(epoch, slot, x.node));
-          if (ins < 0) ctl->overflow = 1;
-          fresh = ins > 0;
-        }
-        if (fresh) {
-          if (sig_maybe(x.lsig, x.sig, subj_sig(si.x))) {  // the signature rules out most misses
-            probes++;
-            if (dset_probe(s, x.node, si.x)) atomicExch(&sl.hit[slot], 1u);
+    // both edges' entry, then both adjx loads in flight at once (an inactive edge reads adjx[0])
+    bool act[2];
+    uint32_t slot[2] = {0u, 0u}, subj[2] = {0u, 0u};
+    int D[2] = {0, 0};
+    AdjX x[2];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const uint64_t e = t0 + threadIdx.x + (uint64_t)h * 256;
+      uint64_t beg = 0;
+      uint32_t rb = 0, hit = 1;
+      if (e < t1) {
+        if (use_lds) {
+          uint32_t lo = 0, hi = (uint32_t)cnt;  // largest i < cnt with s_beg[i] <= e
+          while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (s_beg[mid] <= e) lo = mid;
+            else hi = mid;
           }
-          app = keep;
+          beg = s_beg[lo];
+          slot[h] = s_slot[lo];
+          rb = s_rb[lo];
+          subj[h] = s_info[lo].x;
+          D[h] = (int)s_info[lo].y;
+          hit = s_hit[lo];
+        } else {
+          const uint64_t j = entry_of(lg.ex, lb, j0, j0 + cnt, e);
+          beg = lg.ex[lb + j];
+          slot[h] = lg.slot[lb + j];
+          rb = lg.rb[lb + j];
+          const uint2 si = sl.info[slot[h]];
+          subj[h] = si.x;
+          D[h] = (int)si.y;
+          hit = sl.hit[slot[h]];
         }
       }
+      act[h] = !hit;  // answered at tile start (or no edge): the edge is not even loaded
+      x[h] = s.adjx[act[h] ? rb + (uint32_t)(e - beg) : 0u];
     }
-    grid_push(ctl, lvs, lg, nl, (level + 1) & 1, next_base, B, app, slot, cb, clen);
+    uint32_t clen[2], cb[2];
+    bool keep[2];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      cb[h] = x[h].begin;
+      clen[h] = act[h] ? adjx_len(s, x[h]) : 0u;
+      // hop level+1 is expanded at the next level while its rest depth D - (level + 1) >= 2
+      keep[h] = act[h] && clen[h] > 0 && level + 2 <= D[h] - 1;
+    }
+    int ins[2];
+    gh_insert2(H, mask, keep[0], gh_key(epoch, slot[0], x[0].node), keep[1], gh_key(epoch, slot[1], x[1].node), ins[0],
+               ins[1]);
+    bool app[2];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      if (keep[h] && ins[h] < 0) ctl->overflow = 1;
+      const bool fresh = act[h] && (!keep[h] || ins[h] > 0);
+      if (fresh && sig_maybe(x[h].lsig, x[h].sig, subj_sig(subj[h]))) {  // the signature rules out most misses
+        probes++;
+        if (dset_probe(s, x[h].node, subj[h])) atomicExch(&sl.hit[slot[h]], 1u);
+      }
+      app[h] = fresh && keep[h];
+    }
+    grid_push(ctl, lvs, lg, nl, (level + 1) & 1, next_base, B, app[0], slot[0], cb[0], clen[0]);
+    grid_push(ctl, lvs, lg, nl, (level + 1) & 1, next_base, B, app[1], slot[1], cb[1], clen[1]);
   }
   if (B.n) grid_flush(ctl, lvs, lg, nl, (level + 1) & 1, next_base, B);
   for (int off = 32; off; off >>= 1) probes += __shfl_xor(probes, off, 64);

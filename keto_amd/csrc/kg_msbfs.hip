@@ -48,7 +48,7 @@ constexpr int MS_HOPS = 32;  // depth masks per group (global max depth <= 32 he
 constexpr uint32_t ms_tile_edges(int K) { return K <= 8 ? 256u : 128u; }
 
 struct MsCtl {
-  unsigned long long packed[2];  // per level buffer: entries << 36 | edges
+  unsigned long long packed[3];  // per level buffer (2: the compacted level): entries << 36 | edges
   unsigned long long edges, logged;
   uint32_t overflow, pad;
   unsigned long long eload, wact;  // k_ms_level: adjx records loaded, (edge, 64-query word) pairs with work
@@ -73,11 +73,13 @@ struct MsView {
   uint64_t* em;    // [G][MS_HOPS][K]
   uint32_t* qi;    // [G][64K] query index (NONE: empty bit)
   uint32_t* qd;    // [G][64K] rest depth
-  uint32_t* eg[2];  // entry group
-  uint32_t* en[2];  // entry node
-  uint32_t* erb[2];  // entry row start (adjx)
-  uint64_t* ex[2];  // entry edge offset within its level
-  uint32_t* tf[2];  // tile -> first entry
+  // level buffers 0 / 1 alternate (level L reads L & 1, appends to the other); buffer 2 holds level
+  // L's live entries after k_ms_compact, which k_ms_level walks
+  uint32_t* eg[3];  // entry group
+  uint32_t* en[3];  // entry node
+  uint32_t* erb[3];  // entry row start (adjx)
+  uint64_t* ex[3];  // entry edge offset within its level
+  uint32_t* tf[3];  // tile -> first entry
   MsCtl* ctl;
 };
 
@@ -339,7 +341,9 @@ __device__ __forceinline__ void ms_load_words(const uint64_t* p, uint64_t (&w)[K
 
 // (256, 4): 4 workgroups per CU fit the LDS (~33 KB each: staged want words + the append buffer)
 template <int K>
-__global__ __launch_bounds__(256, 4) void k_ms_level(DevSnap s, MsView v, int L, int cur) {
+// cur: the entry buffer walked (2: the compacted level); the frontier masks of hop L are fr[L & 1] and
+// hop L+1's go to fr[nx = (L & 1) ^ 1]
+__global__ __launch_bounds__(256, 4) void k_ms_level(DevSnap s, MsView v, int L, int cur, int nx) {
   constexpr uint32_t TE = ms_tile_edges(K);
   __shared__ uint64_t s_want[TE + 2][K];
   __shared__ uint64_t s_beg[TE + 2];
@@ -354,7 +358,6 @@ __global__ __launch_bounds__(256, 4) void k_ms_level(DevSnap s, MsView v, int L,
   }
   __syncthreads();
   if (s_void) return;
-  const int nx = cur ^ 1;
   const uint64_t packed = v.ctl->packed[cur];
   const uint64_t n_e = packed >> MS_EDGE_BITS, total = packed & MS_EDGE_MASK;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -395,7 +398,7 @@ __global__ __launch_bounds__(256, 4) void k_ms_level(DevSnap s, MsView v, int L,
       }
       // the queries of the word that reach the child first at hop L+1 and may still probe there (a
       // later arrival has less rest depth: its probe and expansion are subsets of the first one's)
-      s_want[i][kk] = v.fr[cur][((size_t)g * n + v.en[cur][q]) * K + kk] & v.em[((size_t)g * MS_HOPS + h0) * K + kk] &
+      s_want[i][kk] = v.fr[nx ^ 1][((size_t)g * n + v.en[cur][q]) * K + kk] & v.em[((size_t)g * MS_HOPS + h0) * K + kk] &
                       ~v.hit[(size_t)g * K + kk] & v.pm[((size_t)g * MS_HOPS + h1) * K + kk];
     }
     __syncthreads();
@@ -477,15 +480,81 @@ __global__ __launch_bounds__(256, 4) void k_ms_level(DevSnap s, MsView v, int L,
   }
 }
 
-// After level L: the level's frontier masks are cleared (the buffer is the level after next's).
+// Before level L: the entries of buffer `cur` that still have work -- a frontier bit that may probe at
+// hop L+1 and whose query is not answered yet -- are copied to buffer 2 (any order: a level's updates
+// are order-free), which the level walks.  On the heavy-tail point 84 % of the logged edges belonged
+// to entries whose queries had all been answered when their level began (round 6: 243 M edge slots per
+// batch, 40 M loaded): a dead entry still held a whole row's worth of tile lanes.
+template <int K>
+__global__ __launch_bounds__(256) void k_ms_compact(MsView v, int L, int cur) {
+  __shared__ MsBuf B;
+  __shared__ uint32_t s_void;
+  if (threadIdx.x == 0) {
+    s_void = v.ctl->overflow;
+    B.n = 0;
+    B.edges = 0;
+  }
+  __syncthreads();
+  if (s_void) return;
+  constexpr uint32_t TE = ms_tile_edges(K);
+  const uint64_t packed = v.ctl->packed[cur];
+  const uint64_t n_e = packed >> MS_EDGE_BITS, total = packed & MS_EDGE_MASK;
+  const int h0 = min(L, MS_HOPS - 1), h1 = min(L + 1, MS_HOPS - 1);
+  const uint32_t n = v.n;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t b0 = (uint64_t)blockIdx.x * blockDim.x; b0 < n_e; b0 += stride) {
+    const uint64_t q = b0 + threadIdx.x;
+    bool live = false;
+    uint32_t g = 0, node = 0, rb = 0, len = 0;
+    if (q < n_e) {
+      g = v.eg[cur][q];
+      node = v.en[cur][q];
+      rb = v.erb[cur][q];
+      const uint64_t e0 = v.ex[cur][q], e1 = q + 1 < n_e ? v.ex[cur][q + 1] : total;
+      len = (uint32_t)(e1 - e0);
+      uint64_t any = 0;
+#pragma unroll
+      for (int k = 0; k < K; k++)
+        any |= v.fr[cur][((size_t)g * n + node) * K + k] & v.em[((size_t)g * MS_HOPS + h0) * K + k] &
+               ~v.hit[(size_t)g * K + k] & v.pm[((size_t)g * MS_HOPS + h1) * K + k];
+      live = any != 0 && len > 0;
+    }
+    ms_push<TE>(v, 2, B, live, g, node, rb, len);
+  }
+  if (B.n) ms_flush<TE>(v, 2, B);
+}
+
+// After level L: the level's frontier masks are cleared (the buffer is the level after next's): one
+// thread per entry, its K words as 16-B stores (one per word of 8 B before round 6: ~4 ms of a heavy-tail
+// batch in k_ms_clear, profiles/r6c_heavy_kernel_stats.csv).
 template <int K>
 __global__ __launch_bounds__(256) void k_ms_clear(MsView v, int cur) {
   const uint64_t n_e = v.ctl->packed[cur] >> MS_EDGE_BITS;
-  const uint64_t lim = (n_e < v.cap ? n_e : v.cap) * K;
-  for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < lim; w += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t q = w / K;
-    v.fr[cur][((size_t)v.eg[cur][q] * v.n + v.en[cur][q]) * K + w % K] = 0;
+  const uint64_t lim = n_e < v.cap ? n_e : v.cap;
+  for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < lim; q += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t* w = v.fr[cur] + ((size_t)v.eg[cur][q] * v.n + v.en[cur][q]) * K;
+    if constexpr (K == 1) {
+      w[0] = 0;
+    } else {
+#pragma unroll
+      for (int j = 0; j < K / 2; j++) reinterpret_cast<uint4*>(w)[j] = make_uint4(0, 0, 0, 0);
+    }
   }
+}
+
+// A round's masks start clear: 16-B stores over the whole chip (the runtime's fill kernel moved
+// ~1.3 TB/s on these GB-sized arrays: ~2.7 ms of fills per heavy-tail batch, profiles/r6c_heavy_*).
+__global__ __launch_bounds__(256) void k_ms_zero(uint4* a, uint4* b, uint4* c, uint4* d, uint64_t n16, uint4* e,
+                                                 uint64_t e16) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  const uint4 z = make_uint4(0, 0, 0, 0);
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride) {
+    a[i] = z;
+    b[i] = z;
+    c[i] = z;
+    d[i] = z;
+  }
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < e16; i += stride) e[i] = z;
 }
 
 template <int K>
@@ -502,60 +571,50 @@ size_t ms_group_bytes(uint32_t n, int K) {
   return (size_t)n * (8 * 4 * K + 4) + (size_t)K * (16 + 2 * MS_HOPS * 8 + 64 * 12);
 }
 
-// Pool layout for G groups of K words and level buffers of `cap` entries.
+// Pool layout for G groups of K words and level buffers of `cap` entries.  Every array starts on a
+// 256-B boundary (k_ms_zero and the mask loads use 16-B accesses).
 int ms_layout(GridPool* P, uint32_t n, int K, uint32_t G, uint64_t cap, MsView* v) {
-  const size_t gn = (size_t)G * n * K * 8;
-  const size_t need = 4 * gn + (size_t)G * n * 4 + (size_t)G * K * (16 + 2 * MS_HOPS * 8 + 64 * 12) + (size_t)G * 4 + 8 +
-                      2 * (cap * (4 + 4 + 4 + 8) + MS_TILE_CAP * 4) + sizeof(MsCtl) + 8192;
+  auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
+  const size_t gn = al((size_t)G * n * K * 8);
+  const size_t small = al((size_t)G * K * 8);
+  const size_t need = 4 * gn + 2 * small + al((size_t)G * 4) + 2 * al((size_t)G * MS_HOPS * K * 8) +
+                      3 * al((size_t)G * 64 * K * 4) + al((size_t)G * n * 4) +
+                      3 * (al(cap * 8) + 3 * al(cap * 4) + al(MS_TILE_CAP * 4)) + al(sizeof(MsCtl)) + 8192;
   if (need > P->bytes) {
     P->release();
     HIPC(hipMalloc(&P->mem, need));
     P->bytes = need;
   }
   char* p = (char*)P->mem;
+  auto take = [&](size_t bytes) {
+    char* q = p;
+    p += al(bytes);
+    return q;
+  };
   v->n = n;
   v->G = G;
   v->cap = cap;
-  v->vis = (uint64_t*)p;
-  p += gn;
-  v->fr[0] = (uint64_t*)p;
-  p += gn;
-  v->fr[1] = (uint64_t*)p;
-  p += gn;
-  v->tg = (uint64_t*)p;
-  p += gn;
-  v->hit = (uint64_t*)p;
-  p += (size_t)G * K * 8;
-  v->many = (uint64_t*)p;
-  p += (size_t)G * K * 8;
-  v->gmany = (uint32_t*)p;
-  p += ((size_t)G * 4 + 7) & ~size_t(7);
-  v->pm = (uint64_t*)p;
-  p += (size_t)G * MS_HOPS * K * 8;
-  v->em = (uint64_t*)p;
-  p += (size_t)G * MS_HOPS * K * 8;
-  v->qi = (uint32_t*)p;
-  p += (size_t)G * 64 * K * 4;
-  v->qd = (uint32_t*)p;
-  p += (size_t)G * 64 * K * 4;
-  v->qs = (uint32_t*)p;
-  p += (size_t)G * 64 * K * 4;
-  v->stamp = (uint32_t*)p;
-  p += (size_t)G * n * 4;
-  p = (char*)(((uintptr_t)p + 255) & ~uintptr_t(255));
-  for (int b = 0; b < 2; b++) {
-    v->ex[b] = (uint64_t*)p;
-    p += cap * 8;
-    v->eg[b] = (uint32_t*)p;
-    p += cap * 4;
-    v->en[b] = (uint32_t*)p;
-    p += cap * 4;
-    v->erb[b] = (uint32_t*)p;
-    p += cap * 4;
-    v->tf[b] = (uint32_t*)p;
-    p += MS_TILE_CAP * 4;
+  v->vis = (uint64_t*)take(gn);
+  v->fr[0] = (uint64_t*)take(gn);
+  v->fr[1] = (uint64_t*)take(gn);
+  v->tg = (uint64_t*)take(gn);
+  v->hit = (uint64_t*)take((size_t)G * K * 8);
+  v->many = (uint64_t*)take((size_t)G * K * 8);
+  v->gmany = (uint32_t*)take((size_t)G * 4);
+  v->pm = (uint64_t*)take((size_t)G * MS_HOPS * K * 8);
+  v->em = (uint64_t*)take((size_t)G * MS_HOPS * K * 8);
+  v->qi = (uint32_t*)take((size_t)G * 64 * K * 4);
+  v->qd = (uint32_t*)take((size_t)G * 64 * K * 4);
+  v->qs = (uint32_t*)take((size_t)G * 64 * K * 4);
+  v->stamp = (uint32_t*)take((size_t)G * n * 4);
+  for (int b = 0; b < 3; b++) {
+    v->ex[b] = (uint64_t*)take(cap * 8);
+    v->eg[b] = (uint32_t*)take(cap * 4);
+    v->en[b] = (uint32_t*)take(cap * 4);
+    v->erb[b] = (uint32_t*)take(cap * 4);
+    v->tf[b] = (uint32_t*)take(MS_TILE_CAP * 4);
   }
-  v->ctl = (MsCtl*)(((uintptr_t)p + 255) & ~uintptr_t(255));
+  v->ctl = (MsCtl*)take(sizeof(MsCtl));
   return 0;
 }
 
@@ -597,11 +656,11 @@ int ms_rounds(Snapshot* s, Workspace* w, const RQuery* rq, const uint32_t* qlist
       const size_t gn = (size_t)G * n * K * 8;
       // the round's masks start clear (frontier buffers are cleared level by level, but an
       // overflowed round may leave them dirty)
-      HIPC(hipMemsetAsync(v.vis, 0, gn, stream));
-      HIPC(hipMemsetAsync(v.fr[0], 0, gn, stream));
-      HIPC(hipMemsetAsync(v.fr[1], 0, gn, stream));
-      HIPC(hipMemsetAsync(v.tg, 0, gn, stream));
-      HIPC(hipMemsetAsync(v.stamp, 0, (size_t)G * n * 4, stream));
+      // arrays start on 256-B boundaries and are padded to them (ms_layout): whole 16-B words
+      hipLaunchKernelGGL(k_ms_zero, dim3((uint32_t)s->n_cu * 8), dim3(256), 0, stream, (uint4*)v.vis, (uint4*)v.fr[0],
+                         (uint4*)v.fr[1], (uint4*)v.tg, (uint64_t)((gn + 15) / 16), (uint4*)v.stamp,
+                         (uint64_t)(((size_t)G * n * 4 + 15) / 16));
+      HIPC(hipGetLastError());
       HIPC(hipMemsetAsync(v.ctl, 0, sizeof(MsCtl), stream));
       const uint32_t qblocks = (G * Q + 255) / 256;
       hipLaunchKernelGGL(k_ms_init<K>, dim3(qblocks), dim3(256), 0, stream, rq, qlist, d_count, done, v);
@@ -612,8 +671,11 @@ int ms_rounds(Snapshot* s, Workspace* w, const RQuery* rq, const uint32_t* qlist
       HIPC(hipGetLastError());
       for (int L = 0; L < levels; L++) {
         const int cur = L & 1;
+        HIPC(hipMemsetAsync(&v.ctl->packed[2], 0, 8, stream));
+        hipLaunchKernelGGL(k_ms_compact<K>, dim3((uint32_t)s->n_cu * 2), dim3(256), 0, stream, v, L, cur);
+        HIPC(hipGetLastError());
         w->lev_mark(stream, false, 2);
-        hipLaunchKernelGGL(k_ms_level<K>, dim3(lgrid), dim3(256), 0, stream, s->ds, v, L, cur);
+        hipLaunchKernelGGL(k_ms_level<K>, dim3(lgrid), dim3(256), 0, stream, s->ds, v, L, 2, cur ^ 1);
         HIPC(hipGetLastError());
         w->lev_mark(stream, true, 2);
         hipLaunchKernelGGL(k_ms_clear<K>, dim3((uint32_t)s->n_cu * 4), dim3(256), 0, stream, v, cur);

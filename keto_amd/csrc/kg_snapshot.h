@@ -301,9 +301,13 @@ struct Snapshot {
   uint32_t shard_back_budget = 1u << 14;  // kg_snapshot_tune("shard_back_budget"): reverse edges per query and rank
   uint32_t stream_ecap = 512;  // kg_snapshot_tune("stream_ecap"): stream-tier edge budget per query (0 = none)
   // kg_snapshot_tune("expand_gw"): pass-1 overflows of kg_expand_batch run gather-then-walk (1) or the
-  // hash pass directly (0); "expand_skip_lds" (tests): every root skips the LDS pass
+  // hash pass directly (0); "expand_skip_lds" (tests): 1 = every root skips the LDS passes, 2 = the
+  // 16-lane walkers (pass 0) are skipped and the 64-lane pass takes every root
   int expand_gw = 1;
   int expand_skip_lds = 0;
+  // kg_snapshot_tune("level_events"): batches with stats time every tail-tier level launch with a HIP
+  // event pair (kg_stats tail_ms); off by default -- the records leave gaps between the launches
+  int level_events = 0;
   // k_expand_gw: longest wait (us) of a large slot for a small slot's hand-on before it gives its ticket up
   uint32_t expand_gw_wait_us = 100000;
   uint32_t stream_steal = 4;   // kg_snapshot_tune("stream_steal"): XCD ranges a k_stream4 wave dequeues from (1..8)

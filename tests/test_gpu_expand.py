@@ -39,10 +39,12 @@ def _records(rec):
     return None if rec is None else np.asarray(rec, np.int64)
 
 
-GW_MODES = [(1, 0), (1, 1), (0, 1)]  # (expand_gw, expand_skip_lds): default; gather-walk on every root; hash pass on every root
+# (expand_gw, expand_skip_lds): default (16-lane walkers, then the 64-lane pass, gather-walk, hash pass);
+# gather-walk on every root; hash pass on every root; the 64-lane pass on every root
+GW_MODES = [(1, 0), (1, 1), (0, 1), (1, 2)]
 
 
-@pytest.mark.parametrize("gw,skip", GW_MODES, ids=["default", "gw-all", "hash-all"])
+@pytest.mark.parametrize("gw,skip", GW_MODES, ids=["default", "gw-all", "hash-all", "lds64-all"])
 @pytest.mark.parametrize("seed", range(5))
 def test_random_expand_vs_oracle(seed, gw, skip):
     rng = np.random.default_rng(50 + seed)
@@ -151,7 +153,8 @@ def _cmp_records(exp, g, what):
 
 @pytest.mark.parametrize("n_tuples,gmax,gw,skip,wait", [(300_000, 5, 1, 0, 100000), (1_000_000, 3, 1, 0, 100000),
                                                          (300_000, 5, 1, 1, 100000), (300_000, 5, 0, 0, 100000),
-                                                         (300_000, 5, 1, 0, 0), (300_000, 5, 1, 0, 50)])
+                                                         (300_000, 5, 1, 0, 0), (300_000, 5, 1, 0, 50),
+                                                         (300_000, 5, 1, 2, 100000)])
 def test_c5_hot_group_roots_vs_oracle(n_tuples, gmax, gw, skip, wait):
     """Config C5's workload at reduced size: the generator's most popular group#member roots (the
     roots bench.py --mode expand times), expanded at the global depth, against the oracle's
