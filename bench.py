@@ -1093,14 +1093,14 @@ def main():
     rf_stream = stream_roofline(stats, pmc_traffic(STREAM_KERNEL, int(a.tuples), B, a.preset, P, tag))
     # the tail tier's level launches are timed one by one (kg_snapshot_tune "level_events") in a stats phase
     # of their own after the timed region: an event pair per launch leaves gaps in the stream
-    snap.tune("level_events", 1)
+    level_events(snap, 1)
     n_t = min(2 * P, warm)  # warm-up batch indices: their results go to the scratch outputs, not timed_out
     tstats = [_lib.kg_stats() for _ in range(n_t)]
     go, th, errs_t = run_steps(0, n_t, tstats)
     go.set()
     finish(th, errs_t)
     torch.cuda.synchronize()
-    snap.tune("level_events", 0)
+    level_events(snap, 0)
     rf_tail = tail_roofline(tstats, lambda k: pmc_traffic(k, int(a.tuples), B, a.preset, P, tag))
     # the headline keeps k_stream4's roofline (its kernel since round 1); the heavy-tail point reports its
     # dominant kernel by device time per batch (k_ms_level); every measured kernel is in "rooflines"
@@ -1387,10 +1387,10 @@ def c3_leg(a, local) -> dict:
     assert (torch.cat(errs).cpu().numpy() == 0).all(), "unexpected errors in the synthetic C3 batch"
     r0 = outs[W].cpu().numpy()
     q0 = dqs[W].cpu().numpy().view(np.uint32)
-    snap3.tune("level_events", 1)  # the tail tier's launches timed one by one (outside the timed region)
+    level_events(snap3, 1)  # the tail tier's launches timed one by one (outside the timed region)
     phase(0, NS, with_stats=True)  # batches 0 .. NS-1 again (their results are not read)
     torch.cuda.synchronize()
-    snap3.tune("level_events", 0)
+    level_events(snap3, 0)
     st = sts[0]
     tr = lambda k: pmc_traffic(k, int(a.c3_tuples), B, 1, P)
     rf_stream = stream_roofline(sts, tr(STREAM_KERNEL))
@@ -1804,6 +1804,16 @@ def tail_roofline(stats: list, traffic_of) -> dict | None:
                 "ms_words_active_per_batch": float(np.mean([s.ms_words_active for s in st])),
                 "edge_visits_per_batch": float(np.mean([s.tail_edges for s in st]))} if kind == 2 else
                {"edges_per_batch": float(np.mean([s.tail_edges for s in st]))})}
+
+
+def level_events(snap, on: int) -> None:
+    """kg_snapshot_tune("level_events"): HIP events around every tail-tier level launch of batches with stats
+    (round 6; a library without the knob -- an A/B build -- just reports no tail roofline)."""
+    from keto_amd import _lib
+    try:
+        snap.tune("level_events", on)
+    except _lib.KetoGPUError:
+        pass
 
 
 def dominant(*rfs) -> dict:

@@ -60,9 +60,10 @@ struct MsView {
   uint32_t n;      // nodes
   uint32_t G;      // groups of this round
   uint64_t cap;    // entries per level buffer
-  uint64_t* vis;   // [G][n][K]
+  // VIS and TG of one (group, node) share one 16K-byte record (round 6; separate arrays before): the
+  // level reads both for an edge with new bits, so they are one random line (K = 8: 128 B) instead of two
+  uint64_t* vt;    // [G][n][2K]: VIS words, then TG words
   uint64_t* fr[2];  // [G][n][K] each
-  uint64_t* tg;    // [G][n][K]
   uint32_t* stamp;  // [G][n]: 1 + the last hop the node was appended at (one entry per hop)
   uint64_t* hit;   // [G][K]
   uint64_t* many;  // [G][K]: queries whose subject has more than tg_cap holders (probed, no TG bits)
@@ -242,7 +243,7 @@ __global__ __launch_bounds__(256) void k_ms_init(const RQuery* __restrict__ rq, 
       len = q.len;
       const uint64_t bit = 1ull << (b & 63);
       const size_t at = ((size_t)g * v.n + node) * K + (b >> 6);
-      atomicOr((unsigned long long*)&v.vis[at], (unsigned long long)bit);
+      atomicOr((unsigned long long*)&v.vt[((size_t)g * v.n + node) * 2 * K + (b >> 6)], (unsigned long long)bit);
       atomicOr((unsigned long long*)&v.fr[0][at], (unsigned long long)bit);
       app = len > 0 && atomicMax(&v.stamp[(size_t)g * v.n + node], 1u) < 1u;
     }
@@ -294,7 +295,8 @@ __global__ __launch_bounds__(256) void k_ms_holders(DevSnap s, const RQuery* __r
     return;
   }
   for (uint32_t k = lane_id(); k < hr.y; k += 64)
-    atomicOr((unsigned long long*)&v.tg[((size_t)g * v.n + s.hold[hr.x + k]) * K + (b >> 6)], (unsigned long long)bit);
+    atomicOr((unsigned long long*)&v.vt[((size_t)g * v.n + s.hold[hr.x + k]) * 2 * K + K + (b >> 6)],
+             (unsigned long long)bit);
 }
 
 __device__ __forceinline__ uint64_t ms_entry_of(const uint64_t* ex, uint64_t lo, uint64_t hi, uint64_t e) {
@@ -424,9 +426,9 @@ __global__ __launch_bounds__(256, 4) void k_ms_level(DevSnap s, MsView v, int L,
       if (any) {
         c_eload++;
         const AdjX x = s.adjx[s_rb[lo] + (uint32_t)(e - s_beg[lo])];
-        const size_t base = ((size_t)g * n + x.node) * K;
+        const size_t base = ((size_t)g * n + x.node) * K, vbase = 2 * base;  // fr / vt record of the child
         uint64_t vis0[K];
-        ms_load_words<K>(v.vis + base, vis0);
+        ms_load_words<K>(v.vt + vbase, vis0);
         const uint32_t st0 = v.stamp[(size_t)g * n + x.node];
         uint64_t nw[K], anynw = 0;
 #pragma unroll
@@ -440,13 +442,13 @@ __global__ __launch_bounds__(256, 4) void k_ms_level(DevSnap s, MsView v, int L,
 #pragma unroll
           for (int k = 0; k < K; k++) many[k] = s_gm[lo] ? v.many[(size_t)g * K + k] : 0ull;
           uint64_t tg0[K];
-          ms_load_words<K>(v.tg + base, tg0);
+          ms_load_words<K>(v.vt + vbase + K, tg0);
           const bool can_expand = adjx_len16(x) != 0;
           uint64_t anyex = 0;
 #pragma unroll
           for (int k = 0; k < K; k++) {
             if (!nw[k]) continue;
-            atomicOr((unsigned long long*)&v.vis[base + k], (unsigned long long)nw[k]);
+            atomicOr((unsigned long long*)&v.vt[vbase + k], (unsigned long long)nw[k]);
             uint64_t hits = nw[k] & ~many[k] & tg0[k];
             for (uint64_t m = nw[k] & many[k]; m; m &= m - 1) {
               const uint32_t subj = v.qs[(size_t)g * 64 * K + k * 64 + __builtin_ctzll(m)];
@@ -544,17 +546,16 @@ __global__ __launch_bounds__(256) void k_ms_clear(MsView v, int cur) {
 
 // A round's masks start clear: 16-B stores over the whole chip (the runtime's fill kernel moved
 // ~1.3 TB/s on these GB-sized arrays: ~2.7 ms of fills per heavy-tail batch, profiles/r6c_heavy_*).
-__global__ __launch_bounds__(256) void k_ms_zero(uint4* a, uint4* b, uint4* c, uint4* d, uint64_t n16, uint4* e,
-                                                 uint64_t e16) {
+struct MsZero {
+  uint4* p[4];
+  uint64_t n16[4];
+};
+__global__ __launch_bounds__(256) void k_ms_zero(MsZero z4) {
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   const uint4 z = make_uint4(0, 0, 0, 0);
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride) {
-    a[i] = z;
-    b[i] = z;
-    c[i] = z;
-    d[i] = z;
-  }
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < e16; i += stride) e[i] = z;
+#pragma unroll
+  for (int r = 0; r < 4; r++)
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < z4.n16[r]; i += stride) z4.p[r][i] = z;
 }
 
 template <int K>
@@ -594,10 +595,9 @@ int ms_layout(GridPool* P, uint32_t n, int K, uint32_t G, uint64_t cap, MsView* 
   v->n = n;
   v->G = G;
   v->cap = cap;
-  v->vis = (uint64_t*)take(gn);
+  v->vt = (uint64_t*)take(2 * gn);
   v->fr[0] = (uint64_t*)take(gn);
   v->fr[1] = (uint64_t*)take(gn);
-  v->tg = (uint64_t*)take(gn);
   v->hit = (uint64_t*)take((size_t)G * K * 8);
   v->many = (uint64_t*)take((size_t)G * K * 8);
   v->gmany = (uint32_t*)take((size_t)G * 4);
@@ -657,9 +657,9 @@ int ms_rounds(Snapshot* s, Workspace* w, const RQuery* rq, const uint32_t* qlist
       // the round's masks start clear (frontier buffers are cleared level by level, but an
       // overflowed round may leave them dirty)
       // arrays start on 256-B boundaries and are padded to them (ms_layout): whole 16-B words
-      hipLaunchKernelGGL(k_ms_zero, dim3((uint32_t)s->n_cu * 8), dim3(256), 0, stream, (uint4*)v.vis, (uint4*)v.fr[0],
-                         (uint4*)v.fr[1], (uint4*)v.tg, (uint64_t)((gn + 15) / 16), (uint4*)v.stamp,
-                         (uint64_t)(((size_t)G * n * 4 + 15) / 16));
+      const MsZero z4{{(uint4*)v.vt, (uint4*)v.fr[0], (uint4*)v.fr[1], (uint4*)v.stamp},
+                      {(2 * gn + 15) / 16, (gn + 15) / 16, (gn + 15) / 16, ((size_t)G * n * 4 + 15) / 16}};
+      hipLaunchKernelGGL(k_ms_zero, dim3((uint32_t)s->n_cu * 8), dim3(256), 0, stream, z4);
       HIPC(hipGetLastError());
       HIPC(hipMemsetAsync(v.ctl, 0, sizeof(MsCtl), stream));
       const uint32_t qblocks = (G * Q + 255) / 256;
