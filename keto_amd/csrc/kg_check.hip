@@ -323,12 +323,19 @@ __device__ __forceinline__ uint32_t wave_or(uint32_t v) {
 //   * the range bounds of the 8 per-XCD list shards are read once, into lanes 0..7
 //   * queries handed on write their RQuery for the next tiers (k_resolve no longer does)
 constexpr uint32_t S4_CHUNK = 64;
+// Edges per lane and step (round 6): the step is bound by its chain of dependent LDS and HBM round
+// trips, not by issue (~150 VALU per step at 4 waves per SIMD, ~2.5 us per step), and LDS caps the
+// waves per CU; two edges per lane double the gathers and probes one round trip carries.
+// (-DKG_STREAM_EPL=1 builds the one-edge step for A/Bs.)
+#ifndef KG_STREAM_EPL
+#define KG_STREAM_EPL 2
+#endif
 
-template <int VLOG2, int QC>
+template <int VLOG2, int QC, int EPL>
 struct Stream4Lds {
   unsigned long long vt[1 << VLOG2];  // direct-mapped visited cache (0 = empty)
   uint32_t e_beg[QC], e_meta[QC];     // FIFO ring
-  uint32_t pref[65];                  // edge-owner marks (+1 dummy)
+  uint32_t pref[64 * EPL + 1];        // edge-owner marks (+1 dummy)
   uint32_t s_state[32], s_qi[32], s_subj[32], s_last[32], s_edg[32];
   uint32_t s_node[32], s_depth[32], s_beg[32], s_len[32];
   uint4 s_ss[32];  // per slot: the subject's Bloom mask (2 words), the visited-cache salt of (slot, generation)
@@ -340,12 +347,13 @@ struct LqList {
   uint32_t cap;
 };
 
-template <int VLOG2, int QC>
+template <int VLOG2, int QC, int EPL>
 __global__ __launch_bounds__(256) void k_stream4(DevSnap s, LqList wl, uint32_t* heads, uint8_t* __restrict__ out,
                                                  RQuery* __restrict__ rq, uint32_t* next_list, uint32_t* next_count,
                                                  Ctl* ctl, uint32_t ecap, uint32_t chunk, uint32_t ranges) {
-  using Lds = Stream4Lds<VLOG2, QC>;
-  constexpr uint32_t WIN = 64u;
+  using Lds = Stream4Lds<VLOG2, QC, EPL>;
+  static_assert(EPL == 1 || EPL == 2, "one or two edges per lane and step");
+  constexpr uint32_t WIN = 64u * EPL;
   constexpr uint32_t VT = 1u << VLOG2;
   static_assert(QC <= 256 && (QC & (QC - 1)) == 0, "FIFO ring of <= 256 entries (9-bit generations stay unique)");
   const uint64_t t_start = wall_clock64();
@@ -373,8 +381,14 @@ __global__ __launch_bounds__(256) void k_stream4(DevSnap s, LqList wl, uint32_t*
   uint32_t c_left = 0, c_pos = 0;
   LQuery cq{};             // current chunk
   uint32_t head = 0, tail = 0, head_off = 0;
-  bool pend = false;
-  uint32_t pend_node = 0, pend_slot = 0, pend_gen = 0;
+  // the previous step's children awaiting their checkDirect probe: one per edge a lane gathered
+  bool pend[EPL];
+  uint32_t pend_node[EPL], pend_slot[EPL], pend_gen[EPL];
+#pragma unroll
+  for (int h = 0; h < EPL; h++) {
+    pend[h] = false;
+    pend_node[h] = pend_slot[h] = pend_gen[h] = 0;
+  }
   // per-lane counters: each grows by at most one per step, and a wave's steps stay far below 2^32
   uint32_t st_rows = 0, st_edges = 0, st_probes = 0, st_done = 0, st_steps = 0;
   for (;;) {
@@ -450,7 +464,8 @@ __global__ __launch_bounds__(256) void k_stream4(DevSnap s, LqList wl, uint32_t*
       continue;
     }
     __builtin_amdgcn_wave_barrier();
-    // ---- window: up to 64 FIFO entries from the head, up to WIN edges of them
+    // ---- window: up to 64 FIFO entries from the head, up to WIN = 64 * EPL edges of them (edge e on
+    // lane e % 64, in the lane's pass e / 64)
     // Every load of the step below is unconditional (lanes without work read a valid dummy slot) and
     // predicated afterwards: a load inside a branch whose value is merged after the branch makes the
     // compiler wait for it inside the branch -- k_stream2's gather was waited for before its probe
@@ -461,7 +476,14 @@ __global__ __launch_bounds__(256) void k_stream4(DevSnap s, LqList wl, uint32_t*
     const uint32_t sl0 = (emeta >> 11) & 31u;
     const uint32_t st0 = L.s_state[sl0];
     // the previous step's children: probe validity and keys (LDS reads independent of the gathers)
-    const uint32_t pst = L.s_state[pend_slot], psubj = L.s_subj[pend_slot];
+    bool pvalid[EPL];
+    uint64_t pkey[EPL];
+#pragma unroll
+    for (int h = 0; h < EPL; h++) {
+      const uint32_t pst = L.s_state[pend_slot[h]], psubj = L.s_subj[pend_slot[h]];
+      pvalid[h] = pend[h] && pst == pend_gen[h];
+      pkey[h] = dset_key(pend_node[h], psubj);
+    }
     const bool inwin = (uint32_t)lane < avail;
     const bool live = inwin && ((active >> sl0) & 1u) && (st0 == ((emeta >> 16) & S2_GEN));  // no HIT/OVER
     uint32_t elen = live ? (emeta & 0x7FFu) : 0u;
@@ -470,11 +492,10 @@ __global__ __launch_bounds__(256) void k_stream4(DevSnap s, LqList wl, uint32_t*
       elen = live ? elen - head_off : 0u;
     }
     if (!inwin) emeta = 0;
-    const bool pvalid = pend && pst == pend_gen;
-    const uint64_t pkey = dset_key(pend_node, psubj);
     uint32_t total;
     const uint32_t excl = wave_excl_scan(elen, &total);
-    L.pref[lane] = 0;
+#pragma unroll
+    for (int h = 0; h < EPL; h++) L.pref[lane + 64 * h] = 0;
     __builtin_amdgcn_wave_barrier();
     const uint32_t taken = min(total, WIN);
     L.pref[(elen > 0 && excl < taken) ? excl : WIN] = (uint32_t)lane + 1;
@@ -488,18 +509,37 @@ __global__ __launch_bounds__(256) void k_stream4(DevSnap s, LqList wl, uint32_t*
     }
     __builtin_amdgcn_wave_barrier();
     // ---- this step's edge gathers and the previous step's probes, all issued before any wait
-    const uint32_t m = wave_incl_scan<DppMax>(L.pref[lane]);
-    const int own = ((int)m - 1) & 63;
-    const uint32_t ob = __shfl(ebeg, own, 64);
-    const uint32_t om = __shfl(emeta, own, 64);
-    const uint32_t ox = __shfl(excl, own, 64);
-    const bool act = (uint32_t)lane < taken;
-    const AdjX x = s.adjx[act ? ob + ((uint32_t)lane - ox) : 0u];  // adjx[0] exists (n_set_edges + 1)
-    const ulonglong2 pb =
-        ld_once(reinterpret_cast<const ulonglong2*>(s.dset + (pvalid ? dset_home(pkey, s.dset_nb) : 0ull) * DSET_BUCKET));
-    const uint32_t slot = (om >> 11) & 31u, d = om >> 25, g = (om >> 16) & S2_GEN;
-    const uint4 ss = L.s_ss[slot];  // LDS, under the gathers' latency: Bloom mask, visited-cache salt
-    const uint2 ssig = make_uint2(ss.x, ss.y);
+    AdjX x[EPL];
+    uint32_t om[EPL];
+    bool act[EPL];
+    uint32_t mcarry = 0;  // owner marks of the earlier passes' edges (a max-scan carried across passes)
+#pragma unroll
+    for (int h = 0; h < EPL; h++) {
+      uint32_t m = wave_incl_scan<DppMax>(L.pref[lane + 64 * h]);
+      if (h > 0) m = max(m, mcarry);
+      if (h + 1 < EPL) mcarry = (uint32_t)__builtin_amdgcn_readlane((int)m, 63);
+      const int own = ((int)m - 1) & 63;
+      const uint32_t ob = __shfl(ebeg, own, 64);
+      om[h] = __shfl(emeta, own, 64);
+      const uint32_t ox = __shfl(excl, own, 64);
+      const uint32_t e = (uint32_t)lane + 64u * h;
+      act[h] = e < taken;
+      x[h] = s.adjx[act[h] ? ob + (e - ox) : 0u];  // adjx[0] exists (n_set_edges + 1)
+    }
+    ulonglong2 pb[EPL];
+#pragma unroll
+    for (int h = 0; h < EPL; h++)
+      pb[h] = ld_once(
+          reinterpret_cast<const ulonglong2*>(s.dset + (pvalid[h] ? dset_home(pkey[h], s.dset_nb) : 0ull) * DSET_BUCKET));
+    uint32_t slot[EPL], d[EPL], g[EPL];
+    uint4 ss[EPL];
+#pragma unroll
+    for (int h = 0; h < EPL; h++) {
+      slot[h] = (om[h] >> 11) & 31u;
+      d[h] = om[h] >> 25;
+      g[h] = (om[h] >> 16) & S2_GEN;
+      ss[h] = L.s_ss[slot[h]];  // LDS, under the gathers' latency: Bloom mask, visited-cache salt
+    }
     head += ncons;
     st_edges += (lane == 0) ? taken : 0u;
     st_steps += (lane == 0) ? 1u : 0u;
@@ -507,44 +547,65 @@ __global__ __launch_bounds__(256) void k_stream4(DevSnap s, LqList wl, uint32_t*
     // walked by the lanes that need it under a wave-uniform branch
     // bitwise, not short-circuit: a branch on pvalid split the bucket's 16-B load in two, one half
     // issued and waited for inside the branch
-    bool hit = pvalid & ((pb.x == pkey) | (pb.y == pkey));
-    {
-      const bool more = pvalid & !hit & (pb.y != EMPTY64);
+    bool hit[EPL];
+#pragma unroll
+    for (int h = 0; h < EPL; h++) {
+      hit[h] = pvalid[h] & ((pb[h].x == pkey[h]) | (pb[h].y == pkey[h]));
+      const bool more = pvalid[h] & !hit[h] & (pb[h].y != EMPTY64);
       if (__ballot(more)) {
-        if (more) hit = dset_probe(s, pend_node, (uint32_t)pkey);
+        if (more) hit[h] = dset_probe(s, pend_node[h], (uint32_t)pkey[h]);
       }
+      st_probes += pvalid[h] ? 1u : 0u;
     }
-    st_probes += pvalid ? 1u : 0u;
     // ---- children: kept ones (rest >= 2 after the hop, non-empty set row) are marked + appended;
-    // every child new to the query is probed next step
-    const uint32_t xlen = adjx_len16(x);  // saturated at ADJX_LEN_SAT: any such row is long here
-    const bool keepc = act && d >= 3 && xlen > 0;  // x of an inactive lane is adjx[0]: never used
-    const bool longrow = keepc && xlen > S2_LONG;
-    const unsigned long long key =
-        (1ull << 63) | ((unsigned long long)g << 37) | ((unsigned long long)slot << 32) | x.node;
-    const uint32_t hv = ((x.node * 0x9E3779B1u) ^ ss.z) >> (32 - VLOG2);
-    const unsigned long long old = keepc ? L.vt[hv] : 0ull;
-    const bool fresh = keepc && !longrow && old != key;
-    if (fresh) L.vt[hv] = key;
-    const uint64_t am = __ballot(fresh);
-    const uint32_t room = QC - (tail - head);
-    const uint32_t pos = __popcll(am & ((1ull << lane) - 1));
-    const bool appended = fresh && pos < room;
-    if (appended) {
-      const uint32_t at = tail + pos;
-      L.e_beg[at & (QC - 1)] = x.begin;
-      L.e_meta[at & (QC - 1)] = xlen | (om & 0x01FFF800u) | ((d - 1) << 25);
-      atomicMax(&L.s_last[slot], at);   // no return: read at the finish check
-      atomicAdd(&L.s_edg[slot], xlen);  // edge budget, likewise
+    // every child new to the query is probed next step.  Pass 0's edges precede pass 1's in FIFO
+    // order, so marks and appends go pass by pass: a node met twice in one step is kept at its first
+    // (shallowest) occurrence and the FIFO stays in BFS order per query.
+    bool keepc[EPL], fresh[EPL];
+    uint32_t xlen[EPL];
+#pragma unroll
+    for (int h = 0; h < EPL; h++) {
+      xlen[h] = adjx_len16(x[h]);  // saturated at ADJX_LEN_SAT: any such row is long here
+      keepc[h] = act[h] && d[h] >= 3 && xlen[h] > 0;  // x of an inactive lane is adjx[0]: never used
+      const bool longrow = keepc[h] && xlen[h] > S2_LONG;
+      const unsigned long long key =
+          (1ull << 63) | ((unsigned long long)g[h] << 37) | ((unsigned long long)slot[h] << 32) | x[h].node;
+      const uint32_t hv = ((x[h].node * 0x9E3779B1u) ^ ss[h].z) >> (32 - VLOG2);
+      const unsigned long long old = keepc[h] ? L.vt[hv] : 0ull;
+      fresh[h] = keepc[h] && !longrow && old != key;
+      if (fresh[h]) L.vt[hv] = key;
+      if (longrow) atomicOr(&L.s_state[slot[h]], S2_OVER);  // row too long for a FIFO entry
     }
-    if (longrow || (fresh && !appended)) atomicOr(&L.s_state[slot], S2_OVER);  // row too long / FIFO full
-    tail += min((uint32_t)__popcll(am), room);
-    if (hit) atomicOr(&L.s_state[pend_slot], S2_HIT);
-    pend = act && (keepc ? appended : true) && sig_maybe(x.lsig, x.sig, ssig);
-    pend_node = x.node;
-    pend_slot = slot;
-    pend_gen = g;
-    const uint32_t pslots = wave_or(pend ? 1u << slot : 0u);
+    const uint32_t room = QC - (tail - head);
+    uint32_t nfresh = 0;
+    bool appended[EPL];
+#pragma unroll
+    for (int h = 0; h < EPL; h++) {
+      const uint64_t am = __ballot(fresh[h]);
+      const uint32_t pos = nfresh + (uint32_t)__popcll(am & ((1ull << lane) - 1));
+      nfresh += (uint32_t)__popcll(am);
+      appended[h] = fresh[h] && pos < room;
+      if (appended[h]) {
+        const uint32_t at = tail + pos;
+        L.e_beg[at & (QC - 1)] = x[h].begin;
+        L.e_meta[at & (QC - 1)] = xlen[h] | (om[h] & 0x01FFF800u) | ((d[h] - 1) << 25);
+        atomicMax(&L.s_last[slot[h]], at);   // no return: read at the finish check
+        atomicAdd(&L.s_edg[slot[h]], xlen[h]);  // edge budget, likewise
+      }
+      if (fresh[h] && !appended[h]) atomicOr(&L.s_state[slot[h]], S2_OVER);  // FIFO full
+    }
+    tail += min(nfresh, room);
+    uint32_t pmask = 0;
+#pragma unroll
+    for (int h = 0; h < EPL; h++) {
+      if (hit[h]) atomicOr(&L.s_state[pend_slot[h]], S2_HIT);
+      pend[h] = act[h] && (keepc[h] ? appended[h] : true) && sig_maybe(x[h].lsig, x[h].sig, make_uint2(ss[h].x, ss[h].y));
+      pend_node[h] = x[h].node;
+      pend_slot[h] = slot[h];
+      pend_gen[h] = g[h];
+      pmask |= pend[h] ? 1u << slot[h] : 0u;
+    }
+    const uint32_t pslots = wave_or(pmask);
     __builtin_amdgcn_wave_barrier();
     // ---- finished queries
     bool done = false;
@@ -570,7 +631,9 @@ __global__ __launch_bounds__(256) void k_stream4(DevSnap s, LqList wl, uint32_t*
     }
     const uint32_t freed = (uint32_t)__ballot(done);
     active &= ~freed;
-    if (pend && ((freed >> pend_slot) & 1u)) pend = false;
+#pragma unroll
+    for (int h = 0; h < EPL; h++)
+      if (pend[h] && ((freed >> pend_slot[h]) & 1u)) pend[h] = false;
     __builtin_amdgcn_wave_barrier();
   }
   const unsigned long long t_end = wall_clock64(), life = lane == 0 ? t_end - t_start : 0ull;
@@ -984,7 +1047,7 @@ int check_batch_begin(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n, 
       // starting at its label blockIdx & 7, so every label must occur for every range to be drained
       const uint32_t grid =
           std::max<uint32_t>(8u, (uint32_t)std::min<uint64_t>((uint64_t)s->n_cu * per_cu, (n + 31) / 32 + 8));
-      hipLaunchKernelGGL((k_stream4<9, 256>), dim3(grid), dim3(256), 0, stream, s->ds, LqList{lq, ctl->light8, lq_cap},
+      hipLaunchKernelGGL((k_stream4<9, 256, KG_STREAM_EPL>), dim3(grid), dim3(256), 0, stream, s->ds, LqList{lq, ctl->light8, lq_cap},
                          ctl->heads, d_out, rq, heavy, &ctl->heavy_count, ctl, ecap, S4_CHUNK, s->stream_steal);
     }
     HIPC(hipGetLastError());

@@ -15,6 +15,7 @@
 // of an HBM arena (bump allocator), then a compaction kernel lays each root out contiguously.
 // Visited sets live in LDS (pass 1); roots that outgrow LDS rerun with an HBM bitmap (pass 2).
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <cstdlib>
@@ -1352,6 +1353,21 @@ __global__ void k_expand_compact(const RootOut* outs, uint32_t n, const uint64_t
   }
 }
 
+// Device-resident trees (kg_expand_batch_device): every root's record count as a u64 (a stack overflow
+// counts 0 and is tallied in cnt[n + 1]); cnt[n] = 0, so the exclusive sum over n + 1 entries ends in the
+// total.  One thread per root, coalesced.
+__global__ void k_root_counts(const RootOut* outs, uint32_t n, unsigned long long* cnt) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r > n) return;
+  if (r == n) {
+    cnt[n] = 0;
+    return;
+  }
+  const uint32_t c = outs[r].count;
+  if (c == 0xFFFFFFFFu) atomicAdd(&cnt[n + 1], 1ull);
+  cnt[r] = c == 0xFFFFFFFFu ? 0ull : c;
+}
+
 // Device buffers of one lane's expand calls (kg_expand_batch: one lane per calling thread and
 // replica), grown on demand and kept: hipMalloc / hipFree per call stall the device and would
 // serialise concurrent callers.
@@ -1377,6 +1393,10 @@ struct ExpandBufs {
   size_t dst_cap = 0;
   uint64_t* d_off = nullptr;
   size_t off_cap = 0;
+  unsigned long long* cnt = nullptr;  // device-resident trees: per-root counts (+ total, + overflow tally)
+  size_t cnt_cap = 0;
+  void* scan_tmp = nullptr;  // hipcub scan temporary
+  size_t scan_cap = 0;
   void* gw[2] = {nullptr, nullptr};  // gather-walk slots: small, large (allocated once, epochs zeroed)
   GwSlots gws[2] = {};
   uint32_t gw_slots[2] = {0, 0};
@@ -1393,7 +1413,7 @@ struct ExpandBufs {
   ~ExpandBufs() {
     if (device >= 0) hipSetDevice(device);
     for (void* p : {(void*)d_roots, (void*)outs, (void*)p2, (void*)ctl, (void*)stacks, (void*)bm, (void*)arena,
-                    (void*)next, (void*)dst, (void*)d_off, gw[0], gw[1]})
+                    (void*)next, (void*)dst, (void*)d_off, (void*)cnt, scan_tmp, gw[0], gw[1]})
       if (p) hipFree(p);
     for (auto& e : ev)
       if (e) hipEventDestroy(e);
@@ -1454,6 +1474,56 @@ void tree_pool_put(void* p, size_t bytes) {
   (void)hipHostFree(p);
 }
 
+// Device-resident tree outputs (kg_expand_batch_device) come from a per-device pool of the same size
+// classes, returned by kg_tree_free: hipMalloc / hipFree per call stall the device.  At most
+// DEV_POOL_KEEP bytes per device stay cached (C5: ~90 MB of records per call, 16 calls in flight).
+namespace {
+constexpr size_t DEV_POOL_KEEP = 16ull << 30;
+struct DevFree {
+  int device;
+  size_t cls;
+  void* p;
+};
+std::vector<DevFree> dev_free;
+size_t dev_cached[64] = {};
+}  // namespace
+
+void* tree_dev_get(int device, size_t bytes) {
+  const size_t c = pool_class(bytes);
+  {
+    std::lock_guard<std::mutex> lk(pool_mu);
+    for (size_t i = 0; i < dev_free.size(); i++)
+      if (dev_free[i].device == device && dev_free[i].cls == c) {
+        void* p = dev_free[i].p;
+        dev_free[i] = dev_free.back();
+        dev_free.pop_back();
+        dev_cached[device & 63] -= c;
+        return p;
+      }
+  }
+  void* p = nullptr;
+  if (hipSetDevice(device) != hipSuccess || hipMalloc(&p, c) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  return p;
+}
+
+void tree_dev_put(int device, void* p, size_t bytes) {
+  if (!p) return;
+  const size_t c = pool_class(bytes);
+  {
+    std::lock_guard<std::mutex> lk(pool_mu);
+    if (dev_cached[device & 63] + c <= DEV_POOL_KEEP) {
+      dev_free.push_back(DevFree{device, c, p});
+      dev_cached[device & 63] += c;
+      return;
+    }
+  }
+  (void)hipSetDevice(device);
+  (void)hipFree(p);
+}
+
 // Replaces *p with a buffer of at least `need` bytes (contents not kept).
 template <class T>
 static hipError_t grow(T** p, size_t& have, size_t need) {
@@ -1505,14 +1575,26 @@ static hipError_t gw_alloc(ExpandBufs& B, int k, uint32_t slots, uint32_t ent_ca
 }
 
 int expand_batch(Snapshot* s, hipStream_t stream, void** bufs, const kg_set* roots, size_t n, int32_t global,
-                 kg_tree_buf* out) {
+                 kg_tree_buf* out, bool dev_io) {
   memset(out, 0, sizeof *out);
   if (global < 1) global = 5;
-  out->root_off = (uint64_t*)calloc(n + 1, 8);
-  out->n_roots = n;
-  if (!out->root_off) return set_error(-4, "host allocation failed");
-  if (n == 0) return 0;
   HIPC(hipSetDevice(s->device));
+  out->n_roots = n;
+  if (dev_io) {
+    // device-resident trees: root_off (n + 1 entries) and the records in the device pool
+    out->pinned = KG_TREE_DEVICE | (uint64_t)(s->device & 0xFF);
+    out->root_off = (uint64_t*)tree_dev_get(s->device, (n + 1) * 8);
+    if (!out->root_off) return set_error(-4, "device allocation failed");
+    if (n == 0) {
+      HIPC(hipMemsetAsync(out->root_off, 0, 8, stream));
+      HIPC(hipStreamSynchronize(stream));
+      return 0;
+    }
+  } else {
+    out->root_off = (uint64_t*)calloc(n + 1, 8);
+    if (!out->root_off) return set_error(-4, "host allocation failed");
+    if (n == 0) return 0;
+  }
   if (!*bufs) *bufs = new ExpandBufs();
   ExpandBufs& B = *static_cast<ExpandBufs*>(*bufs);
   B.device = s->device;
@@ -1567,7 +1649,9 @@ int expand_batch(Snapshot* s, hipStream_t stream, void** bufs, const kg_set* roo
   for (auto& x : B.ev)
     if (!rc && !x && (e = hipEventCreate(&x)) != hipSuccess) fail("hipEventCreate", e);
   uint32_t* lists = B.bm + clear_words;
-  if (!rc && (e = hipMemcpyAsync(B.d_roots, roots, n * sizeof(kg_set), hipMemcpyHostToDevice, stream)) != hipSuccess)
+  // the roots: the caller's device array (dev_io) or staged from host memory
+  const kg_set* d_roots = dev_io ? roots : B.d_roots;
+  if (!dev_io && !rc && (e = hipMemcpyAsync(B.d_roots, roots, n * sizeof(kg_set), hipMemcpyHostToDevice, stream)) != hipSuccess)
     fail("H2D", e);
   ExpCtl h{};
   for (int attempt = 0; !rc; attempt++) {
@@ -1591,10 +1675,10 @@ int expand_batch(Snapshot* s, hipStream_t stream, void** bufs, const kg_set* roo
     }
     (void)hipEventRecord(B.ev[0], stream);
     if (sub_on)
-      hipLaunchKernelGGL(k_expand_sub, dim3(grid0), dim3(256), 0, stream, s->ds, B.d_roots, (uint32_t)n, global, B.ctl,
+      hipLaunchKernelGGL(k_expand_sub, dim3(grid0), dim3(256), 0, stream, s->ds, d_roots, (uint32_t)n, global, B.ctl,
                          B.outs, B.arena, B.next, n_chunks,
                          B.stacks + (size_t)(slots1 + slots2 + 1 + gw_n[0] + gw_n[1]) * stack_cap, stack_cap, B.p2 + 4 * n);
-    hipLaunchKernelGGL(k_expand_lds, dim3(grid1), dim3(256), 0, stream, s->ds, B.d_roots, (uint32_t)n, global, B.ctl,
+    hipLaunchKernelGGL(k_expand_lds, dim3(grid1), dim3(256), 0, stream, s->ds, d_roots, (uint32_t)n, global, B.ctl,
                        B.outs, B.arena, B.next, n_chunks, B.stacks, stack_cap, B.p2, s->expand_skip_lds == 1 ? 1 : 0,
                        sub_on ? (const uint32_t*)(B.p2 + 4 * n) : nullptr);
     // pass-1 overflows: gather-walk small slots -> large slots -> the hash pass (or straight to it)
@@ -1603,7 +1687,7 @@ int expand_batch(Snapshot* s, hipStream_t stream, void** bufs, const kg_set* roo
     uint32_t* h_hash = &B.ctl->p2_head;
     if (gw_on) {
       ExpFrame* gst = B.stacks + (size_t)(slots1 + slots2 + 1) * stack_cap;
-      hipLaunchKernelGGL(k_expand_gw, dim3(gw_n[0] + gw_n[1]), dim3(256), 0, stream, s->ds, B.d_roots, global, B.ctl,
+      hipLaunchKernelGGL(k_expand_gw, dim3(gw_n[0] + gw_n[1]), dim3(256), 0, stream, s->ds, d_roots, global, B.ctl,
                          B.outs, B.arena, B.next, n_chunks, gst, stack_cap, B.p2, B.p2 + 2 * n, B.p2 + 3 * n,
                          (uint32_t)n, gw_n[1], B.gws[0], B.gws[1], (uint64_t)s->expand_gw_wait_us * 100);  // 100 MHz clock
       hipLaunchKernelGGL(k_gw_sweep, dim3(1), dim3(256), 0, stream, B.ctl, B.p2 + 2 * n, B.p2 + 3 * n);
@@ -1611,10 +1695,10 @@ int expand_batch(Snapshot* s, hipStream_t stream, void** bufs, const kg_set* roo
       c_hash = &B.ctl->gb_count;
       h_hash = &B.ctl->gb_head;
     }
-    hipLaunchKernelGGL(k_expand_hash, dim3(slots2), dim3(64), 0, stream, s->ds, B.d_roots, global, B.ctl, B.outs,
+    hipLaunchKernelGGL(k_expand_hash, dim3(slots2), dim3(64), 0, stream, s->ds, d_roots, global, B.ctl, B.outs,
                        B.arena, B.next, n_chunks, B.stacks + (size_t)slots1 * stack_cap, stack_cap, q_hash, c_hash,
                        h_hash, B.bm, tsize, lists, cap2, B.p2 + n);
-    hipLaunchKernelGGL(k_expand_hbm, dim3(1), dim3(64), 0, stream, s->ds, B.d_roots, global, B.ctl, B.outs, B.arena,
+    hipLaunchKernelGGL(k_expand_hbm, dim3(1), dim3(64), 0, stream, s->ds, d_roots, global, B.ctl, B.outs, B.arena,
                        B.next, n_chunks, B.stacks + (size_t)(slots1 + slots2) * stack_cap, B.p2 + n,
                        B.bm + (size_t)slots2 * tsize, words, lists + (size_t)slots2 * cap2, nn);
     (void)hipEventRecord(B.ev[1], stream);
@@ -1644,6 +1728,54 @@ int expand_batch(Snapshot* s, hipStream_t stream, void** bufs, const kg_set* roo
     n_chunks *= 4;  // grow the arena and rerun (outputs are rewritten from scratch)
   }
   B.bm_dirty = rc != 0 || h.overflow != 0;  // only a completed call leaves the tables clear
+  if (dev_io) {
+    // offsets by a device scan of the roots' counts; the total and the overflow tally come back in one
+    // readback, then the records are compacted into the output (no host pass over the roots)
+    uint64_t tail[2] = {0, 0};
+    size_t tmp_need = 0;
+    if (!rc && (e = grow(&B.cnt, B.cnt_cap, (n + 2) * 8)) != hipSuccess) fail("hipMalloc", e);
+    if (!rc && (e = hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_need, B.cnt, (unsigned long long*)out->root_off,
+                                                     (int)(n + 1), stream)) != hipSuccess)
+      fail("scan", e);
+    if (!rc && (e = grow((char**)&B.scan_tmp, B.scan_cap, tmp_need)) != hipSuccess) fail("hipMalloc", e);
+    if (!rc && (e = hipMemsetAsync(B.cnt + n + 1, 0, 8, stream)) != hipSuccess) fail("memset", e);
+    if (!rc) {
+      hipLaunchKernelGGL(k_root_counts, dim3((uint32_t)((n + 1 + 255) / 256)), dim3(256), 0, stream, B.outs, (uint32_t)n,
+                         B.cnt);
+      if ((e = hipcub::DeviceScan::ExclusiveSum(B.scan_tmp, tmp_need, B.cnt, (unsigned long long*)out->root_off,
+                                                (int)(n + 1), stream)) != hipSuccess ||
+          (e = hipMemcpyAsync(&tail[0], out->root_off + n, 8, hipMemcpyDeviceToHost, stream)) != hipSuccess ||
+          (e = hipMemcpyAsync(&tail[1], B.cnt + n + 1, 8, hipMemcpyDeviceToHost, stream)) != hipSuccess ||
+          (e = B.wait(stream)) != hipSuccess)
+        fail("root offsets", e);
+    }
+    if (!rc && tail[1]) rc = set_error(KG_ERR_RESOURCE, "%llu expand root(s) exceeded the stack", (unsigned long long)tail[1]);
+    const uint64_t total = rc ? 0 : tail[0];
+    if (!rc && total) {
+      out->nodes = (kg_tree_node*)tree_dev_get(s->device, total * sizeof(kg_tree_node));
+      if (!out->nodes) rc = set_error(-4, "device allocation failed");
+    }
+    if (!rc && total) {
+      (void)hipEventRecord(B.ev[2], stream);
+      hipLaunchKernelGGL(k_expand_compact, dim3((uint32_t)((n + 3) / 4)), dim3(256), 0, stream, B.outs, (uint32_t)n,
+                         out->root_off, B.arena, B.next, out->nodes);
+      (void)hipEventRecord(B.ev[3], stream);
+      if ((e = hipGetLastError()) != hipSuccess || (e = B.wait(stream)) != hipSuccess) fail("compact", e);
+    }
+    out->n_nodes = total;
+    if (!rc) {
+      float a = 0, b = 0;
+      (void)hipEventElapsedTime(&a, B.ev[0], B.ev[1]);
+      if (total) (void)hipEventElapsedTime(&b, B.ev[2], B.ev[3]);
+      out->kernel_ms = (double)a + (double)b;
+    } else {
+      B.bm_dirty = true;
+      tree_dev_put(s->device, out->nodes, total * sizeof(kg_tree_node));
+      tree_dev_put(s->device, out->root_off, (n + 1) * 8);
+      memset(out, 0, sizeof *out);
+    }
+    return rc;
+  }
   std::vector<RootOut> ho(n);
   if (!rc && (e = hipMemcpyAsync(ho.data(), B.outs, n * sizeof(RootOut), hipMemcpyDeviceToHost, stream)) != hipSuccess)
     fail("D2H", e);

@@ -84,6 +84,7 @@ struct Workspace {
   }
   hipEvent_t sync_ev = nullptr;  // blocking-sync event (host-buffer batches wait on it asleep)
   int wait(hipStream_t st, bool blocking);  // waits for st: spin (hipStreamSynchronize) or asleep
+  void* exp = nullptr;  // expand buffers of kg_expand_batch_device calls on this stream (kg_expand.hip)
   void* pinned = nullptr;  // 64 KiB of pinned host memory for small device->host readbacks
   kg_query* unpacked = nullptr;  // packed device batches that need the original queries (a program)
   size_t unpacked_n = 0;
@@ -442,10 +443,15 @@ int shard_check_host_entry(Snapshot* s, const kg_query* q, size_t n, int32_t gde
 int grid_reserve(Snapshot* s);  // allocates the shared full-size grid pool now (kg_snapshot_tune "grid_reserve")
 // kg_expand.hip
 // runs on `stream` with the lane's cached device buffers (*bufs, created on first use)
+// dev_io: roots is a device pointer and the trees stay in HBM (kg_expand_batch_device: out->nodes /
+// out->root_off device buffers of the per-device output pool, out->pinned = KG_TREE_DEVICE | device)
 int expand_batch(Snapshot* s, hipStream_t stream, void** bufs, const kg_set* roots, size_t n, int32_t global,
-                 kg_tree_buf* out);
+                 kg_tree_buf* out, bool dev_io = false);
 void expand_bufs_free(void* bufs);
 void* tree_pool_get(size_t bytes);  // pinned host memory for tree outputs (kg_tree_free returns it)
 void tree_pool_put(void* p, size_t bytes);
+constexpr uint64_t KG_TREE_DEVICE = 0x100;  // kg_tree_buf.pinned: device-resident trees (low byte: the device)
+void* tree_dev_get(int device, size_t bytes);  // device memory for device-resident tree outputs
+void tree_dev_put(int device, void* p, size_t bytes);
 
 }  // namespace kg

@@ -327,6 +327,7 @@ Workspace::~Workspace() {
     if (e) hipEventDestroy(e);
   for (auto& e : lev_ev)
     if (e) hipEventDestroy(e);
+  if (exp) expand_bufs_free(exp);
 }
 
 void* Workspace::host_buf(size_t bytes) {

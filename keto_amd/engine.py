@@ -372,20 +372,36 @@ class ExpandEngine:
         self.snapshot = snapshot
         self.config = config or Config()
 
-    def build_trees_ids(self, roots: np.ndarray) -> List[Optional[np.ndarray]]:
+    def build_trees_ids(self, roots: np.ndarray, device: bool = False) -> List[Optional[np.ndarray]]:
         """roots: (n,4) uint32 kg_set rows (sns, sobj, srel, max_depth).  Returns per root the pre-order
-        records (m, 6) = (type, is_set, ns, obj, rel, n_children), or None for a nil tree."""
+        records (m, 6) = (type, is_set, ns, obj, rel, n_children), or None for a nil tree.  device: through
+        kg_expand_batch_device (roots and trees in HBM; the trees are copied back here to be returned)."""
         roots = np.ascontiguousarray(roots, np.uint32).reshape(-1, 4)
         buf = _lib.kg_tree_buf()
         L = _lib.load()
-        rc = L.kg_expand_batch(self.snapshot.handle, _ptr(roots), roots.shape[0], self.config.max_read_depth,
-                               C.byref(buf))
-        _lib.check(rc, "kg_expand_batch")
+        if device:
+            import torch
+            dev = torch.device("cuda", self.snapshot.device)
+            droots = torch.from_numpy(roots.view(np.int32)).to(dev)
+            rc = L.kg_expand_batch_device(self.snapshot.handle, C.c_void_p(droots.data_ptr()), roots.shape[0],
+                                          self.config.max_read_depth, C.byref(buf),
+                                          C.c_void_p(torch.cuda.current_stream(dev).cuda_stream))
+            _lib.check(rc, "kg_expand_batch_device")
+        else:
+            rc = L.kg_expand_batch(self.snapshot.handle, _ptr(roots), roots.shape[0], self.config.max_read_depth,
+                                   C.byref(buf))
+            _lib.check(rc, "kg_expand_batch")
         try:
             n = int(buf.n_nodes)
-            recs = np.ctypeslib.as_array(C.cast(buf.nodes, C.POINTER(C.c_uint32)), shape=(n * 5,)).reshape(n, 5) \
-                if n else np.zeros((0, 5), np.uint32)
-            offs = np.ctypeslib.as_array(buf.root_off, shape=(roots.shape[0] + 1,)).copy()
+            if device:
+                recs = np.zeros((n, 5), np.uint32)
+                offs = np.zeros(roots.shape[0] + 1, np.uint64)
+                _lib.device_to_host(recs, buf.nodes, n * 20)
+                _lib.device_to_host(offs, buf.root_off, offs.nbytes)
+            else:
+                recs = np.ctypeslib.as_array(C.cast(buf.nodes, C.POINTER(C.c_uint32)), shape=(n * 5,)).reshape(n, 5) \
+                    if n else np.zeros((0, 5), np.uint32)
+                offs = np.ctypeslib.as_array(buf.root_off, shape=(roots.shape[0] + 1,)).copy()
             out: List[Optional[np.ndarray]] = []
             for r in range(roots.shape[0]):
                 a, b = int(offs[r]), int(offs[r + 1])

@@ -199,3 +199,44 @@ def test_expand_lane_memory_stays_flat():
     free1 = torch.cuda.mem_get_info(0)[0]
     assert free0 - free1 < (64 << 20), (free0, free1)
     assert all((a is None and b is None) or (a == b).all() for a, b in zip(first, again))
+
+
+@pytest.mark.parametrize("gw,skip", [(1, 0), (0, 1)], ids=["default", "hash-all"])
+def test_expand_device_io_vs_oracle(gw, skip):
+    """kg_expand_batch_device (roots and trees in HBM, offsets by a device scan): the same trees as the
+    host-buffer call and the oracle's BuildTree, on C5 roots (giant trees included) and on random roots
+    with nil trees and subject-id roots; an empty batch; the device output pool reused across calls."""
+    import torch
+    from keto_amd import _lib
+    from keto_amd.engine import Snapshot
+    from keto_amd.synth import hot_group_roots
+    snap = Snapshot.synthetic(300_000, seed=20250131)
+    snap.tune("expand_gw", gw)
+    snap.tune("expand_skip_lds", skip)
+    roots = hot_group_roots(snap.synth_ids(), 1500)
+    rng = np.random.default_rng(7)
+    extra = roots[rng.choice(len(roots), 64)].copy()
+    extra[:16, 1] = 0x7FFFFFF0  # unknown objects: nil trees
+    extra[16:24, 0] = SUBJECT_ID  # subject-id roots: a leaf each
+    roots = np.concatenate([roots, extra])
+    ex = ExpandEngine(snap)
+    ex.config.max_read_depth = 5
+    host = ex.build_trees_ids(roots)
+    oracle = Oracle(snap.export(), 0)
+    for k in range(2):  # the second call reuses the pool's buffers
+        dev = ex.build_trees_ids(roots, device=True)
+        for r, h, d in zip(roots, host, dev):
+            assert (h is None) == (d is None) and (h is None or (h == d).all()), r.tolist()
+    for r, d in zip(roots[:200], dev[:200]):
+        if r[0] != SUBJECT_ID:
+            _cmp_records(oracle.expand(int(r[0]), int(r[1]), int(r[2]), 0, 5), d, r.tolist())
+    assert sum(d is not None and len(d) > 512 for d in dev) > 0
+    # empty batch: root_off = [0]
+    L = _lib.load()
+    buf = _lib.kg_tree_buf()
+    z = torch.zeros((1, 4), dtype=torch.int32, device="cuda:0")
+    _lib.check(L.kg_expand_batch_device(snap.handle, z.data_ptr(), 0, 5, buf, None), "kg_expand_batch_device")
+    off = np.ones(1, np.uint64)
+    _lib.device_to_host(off, buf.root_off, 8)
+    assert buf.n_nodes == 0 and off[0] == 0
+    L.kg_tree_free(buf)
