@@ -1584,6 +1584,7 @@ def sharded_leg(a, snap, size_param, dist, rank, world, local, backend, orc) -> 
                "latency_batches": KL,
                "path": LibShardedChecker.PATHS.get(st["path"], st["path"]),
                "levels_per_batch": st["levels"], "host_syncs_per_batch": st["host_syncs"],
+               "exchanges_per_batch": st["exchanges"], "exchange_reruns": st["exchange_reruns"],
                "records_sent_per_batch": st["records_sent"], "records_to_peers_per_batch": st["records_to_peers"],
                "wire_bytes_per_batch": st["wire_bytes"], "reruns_last_batch": st["reruns_bucket"] + st["reruns_visited"],
                "allowed_fraction": float(r0.mean())}

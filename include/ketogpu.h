@@ -555,7 +555,9 @@ int kg_shard_comm_release(kg_snapshot* s, void* stream);
  * kg_shard_comm_stats_ex gives up to 16: [8] records this rank sent to OTHER ranks (what crosses
  * xGMI), [9] bytes it put on the wire (every other rank gets B_k records per exchange, plus counts
  * and done bitmaps), [10] path (0 local-first tier chain, 1 one-rank device loop, 2 exchange
- * protocol), [11] exchanges, [12] levels of the escalation phases (backward + final forward). */
+ * protocol), [11] exchanges the last batch ran (learned: the previous batch's last non-empty exchange
+ * + 2, at most gdepth + 1), [12] levels of the escalation phases (backward + final forward), [13] 1 when
+ * the last batch had records left after the learned exchanges and reran with all of them. */
 int kg_shard_comm_stats(const kg_snapshot* s, void* stream, uint64_t out8[8]);
 int kg_shard_comm_stats_ex(const kg_snapshot* s, void* stream, uint64_t* out, size_t n);
 /* Per exchange k of the last batch: out[2k] = B_k (records per destination it was sent with),

@@ -74,6 +74,10 @@ struct ShardComm {
   unsigned long long* red = nullptr;  // [8 + levels]: the end-of-batch all-reduce (tot[5] | per-exchange largest)
   size_t red_cap = 0;
   std::vector<uint64_t> lvl_last, lb_last;  // the last batch: per exchange its largest bucket and B_k
+  // exchanges a batch runs (round 6): learned from the last batch -- its last
+  // non-empty exchange + 2 -- instead of always gdepth + 1 (the trailing ones carried nothing and cost
+  // ~37 us each); a batch that still has records after them reruns with all of them (0: not learned yet)
+  int lx = 0;
   std::mutex host_mu;    // kg_check_batch (host buffers): one batch at a time through dq / dout / derr
   uint64_t st[16] = {};  // kg_shard_comm_stats (kg_shard_comm_stats_ex: all 16)
   hipEvent_t ev[2] = {nullptr, nullptr};
@@ -910,8 +914,10 @@ int shard_check(Snapshot* s, ShardComm* c, const kg_query* d_q, size_t n, int32_
     }
     // the forward exchange protocol: L exchanges, then (escalation) the backward phase over all-gathers
     // and a second forward pass for the queries past both budgets
+    // exchanges of this run: the learned count (no escalation: its phases keep all L)
+    const int LX = (xch && !esc && c->lx > 0) ? std::min(L, c->lx) : L;
     for (int phase = 0; xch && phase < (esc ? 2 : 1); phase++) {
-      for (int k = 0; k < L; k++) {
+      for (int k = 0; k < LX; k++) {
         const size_t Bk = c->lb[(size_t)k], Bn = c->lb[(size_t)k + 1];
         const int nx = cur ^ 1;
         // one kernel: the outgoing counts into the accumulators, the level's output counters and hub
@@ -969,7 +975,9 @@ int shard_check(Snapshot* s, ShardComm* c, const kg_query* d_q, size_t n, int32_
       cur = 0;
     }
     if (xch) {
-      hipLaunchKernelGGL(k_sc_final, dim3(1), dim3(64), 0, st, counts[cur], N, (uint32_t)c->lb[(size_t)L], acc, tot);
+      // what the last exchange run left for the next one: bounded by that exchange's bucket (LX < L) or
+      // by nothing (LX = L: lb[L] -- the last level emits nothing)
+      hipLaunchKernelGGL(k_sc_final, dim3(1), dim3(64), 0, st, counts[cur], N, (uint32_t)c->lb[(size_t)LX], acc, tot);
       HIPC(hipGetLastError());
     }
     // results final before the all-reduce, which then also carries "a query needs the general phase"
@@ -985,6 +993,11 @@ int shard_check(Snapshot* s, ShardComm* c, const kg_query* d_q, size_t n, int32_
     HIPC(hipMemcpyAsync(h.data() + nred, acc + 2, 16, hipMemcpyDeviceToHost, st));
     HIPC(hipStreamSynchronize(st));  // host round trip 2
     c->st[2]++;
+    if (xch && LX < L && h[3]) {  // records left after the learned exchanges: rerun with all of them
+      c->lx = L;
+      c->st[13]++;
+      continue;
+    }
     if (h[0] || h[1] || s->shard_force_overflow) {  // dropped records somewhere: every rank reruns with more room
       const bool bucket_over = h[0] || s->shard_force_overflow;
       // a run whose visited table overflowed too dropped records for that reason as well, so its
@@ -1046,6 +1059,11 @@ int shard_check(Snapshot* s, ShardComm* c, const kg_query* d_q, size_t n, int32_
       }
       c->lvl_last.assign(h.begin() + 8, h.begin() + 8 + L);
       c->lb_last.assign(c->lb.begin(), c->lb.begin() + L);
+      int last = -1;  // the last exchange that carried records (per-exchange largest bucket, max over ranks)
+      for (int k = 0; k < LX; k++)
+        if (h[8 + (size_t)k]) last = k;
+      c->lx = std::min(L, last + 2);
+      c->st[11] = (uint64_t)LX;
     }
     c->st[1] = h[nred];
     c->st[8] = h[nred + 1];
@@ -1054,7 +1072,7 @@ int shard_check(Snapshot* s, ShardComm* c, const kg_query* d_q, size_t n, int32_
     break;
   }
   c->st[7] = xch ? *std::max_element(c->lb.begin(), c->lb.end()) : c->bucket;
-  c->st[11] = xch ? (uint64_t)L : 0;
+  if (!xch) c->st[11] = 0;
   if (n) {
     HIPC(hipMemcpyAsync(d_out, c->res, n, hipMemcpyDeviceToDevice, st));
     if (d_err) HIPC(hipMemcpyAsync(d_err, c->err, n * 4, hipMemcpyDeviceToDevice, st));

@@ -328,7 +328,8 @@ class LibShardedChecker:
         return ExpandEngine(self.snapshot, Config(gdepth)).build_trees_ids(roots)
 
     STAT_KEYS = ("levels", "records_sent", "host_syncs", "reruns_bucket", "reruns_visited", "general_queries",
-                 "general_rows", "bucket", "records_to_peers", "wire_bytes", "path", "exchanges", "escalation_levels")
+                 "general_rows", "bucket", "records_to_peers", "wire_bytes", "path", "exchanges", "escalation_levels",
+                 "exchange_reruns")
     PATHS = {0: "local-first (replica tier chain)", 1: "one-rank device level loop", 2: "exchange protocol"}
 
     def stats(self) -> dict:

@@ -195,7 +195,9 @@ class _LibAdapter:
 
 
 # (host round trips, levels) of a clean in-library batch by path: local-first tier chain, one-rank device
-# level loop, exchange protocol (gdepth + 1 exchanges; the agreement all-reduce and the end-of-batch one)
+# level loop, exchange protocol (at most gdepth + 1 exchanges -- a batch after the first runs the count
+# learned from the one before, its last non-empty exchange + 2; the agreement all-reduce and the
+# end-of-batch one)
 LIB_PATH_COST = {0: lambda g: (0, 0), 1: lambda g: (1, g), 2: lambda g: (2, g + 1)}
 
 
@@ -683,7 +685,9 @@ def _run_synth(world, backend, n_tuples, n_q, gmax, preset, budget=None, back_bu
             want = 0 if (world == 1 and "loop" not in driver and "forced" not in driver) else (
                 1 if world == 1 and "loop" in driver else 2)
             assert path == want, (path, want, driver)
-            assert (syncs, levels) == LIB_PATH_COST[path](gmax), (syncs, levels, path)
+            want_syncs, want_levels = LIB_PATH_COST[path](gmax)
+            assert syncs == want_syncs, (syncs, levels, path)
+            assert (levels == want_levels) if path != 2 else (2 <= levels <= want_levels), (syncs, levels, path)
         if budget is not None and budget <= 8 and not preset:
             assert back_levels > 0  # the backward phase ran
         if preset:
@@ -1175,3 +1179,46 @@ def test_sharded_expand_vs_oracle(world, transport):
                 _cmp_records(exp, g, (r.tolist(), gmax))
                 n_trees += g is not None
     assert n_trees > 100
+
+
+def _learned_worker(outq, n_tuples, n_q):
+    sys.path.insert(0, ROOT)
+    from keto_amd import _lib
+    from keto_amd.engine import Snapshot
+    torch.cuda.set_device(0)
+    snap = Snapshot.synthetic(n_tuples, seed=20250131, shard=(0, 1))
+    dq = torch.empty((n_q, 7), dtype=torch.int32, device="cuda")
+    _lib.check(_lib.load().kg_synth_queries(snap.handle, 77, n_q, dq.data_ptr()), "kg_synth_queries")
+    chk = _checker("lib-rccl-forced", snap, 0, 1, None, cap=1 << 14)
+    out = []
+    for gmax in (3, 3, 10, 10):  # a shallow batch teaches few exchanges; the deep one after it reruns
+        r, e = chk.check(dq, gmax)
+        st = chk.chk.stats()
+        out.append((gmax, r.cpu().numpy(), e.cpu().numpy(), st["exchanges"], st["exchange_reruns"]))
+    outq.put((dq.cpu().numpy(), out))
+
+
+@pytest.mark.gpu
+def test_sharded_learned_exchanges_rerun():
+    """The exchange protocol runs the number of exchanges the previous batch needed (its last non-empty
+    one + 2) instead of gdepth + 1.  A gdepth-3 batch learns <= 4; the gdepth-10
+    batch after it has records left after them and reruns with all 11 exchanges, then the next one runs
+    the learned count with no rerun -- every answer equal to the oracle's (world 1 over RCCL, forced)."""
+    from keto_amd.engine import Snapshot
+    from oracle.oracle import POLICY_CANONICAL, Oracle
+    ctx = mp.get_context("spawn")
+    outq = ctx.Queue()
+    p = ctx.Process(target=_learned_worker, args=(outq, 300_000, 20_000))
+    p.start()
+    dq, out = outq.get(timeout=110)
+    p.join(60)
+    assert p.exitcode == 0
+    q = dq.view(np.uint32)
+    full = Snapshot.synthetic(300_000, seed=20250131)
+    o = Oracle(full.export(), 0)
+    for k, (gmax, r, e, xch, reruns) in enumerate(out):
+        exp, oerr, _ = o.check_batch(q[:, :6], q[:, 6].view(np.int32), gmax, POLICY_CANONICAL, nthreads=8)
+        assert (e == 0).all() and (r == exp).all(), (k, gmax, np.nonzero(r != exp)[0][:8])
+        assert xch <= gmax + 1, (k, xch)
+    assert out[2][4] == 1 and out[2][3] == 11, out[2][3:]  # records left after the learned count: one rerun
+    assert out[3][4] == 0 and out[3][3] <= 11, out[3][3:]  # learned from the deep batch: no rerun
