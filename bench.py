@@ -149,8 +149,11 @@ def parse(argv=None):
     ap.add_argument("--host-calls", type=int, default=20,
                     help="kg_check_batch calls per in-flight thread in the host-path leg (1 M-check host batches, "
                          "PCIe both ways; 0 = skip)")
-    ap.add_argument("--stats-every", type=int, default=1,
-                    help="collect kernel stats on every k-th timed batch (1 = all; a batch with stats is waited for)")
+    ap.add_argument("--stats-every", type=int, default=10,
+                    help="collect kernel stats (HIP events around the batch and k_stream4, the in-kernel counters) on "
+                         "every k-th timed batch (1 = all).  Default 10: two of the driver's 20 steps -- the event "
+                         "records between a batch's launches cost ~9 %% of the 20-step line when every batch carries "
+                         "them (profiles/r6i_stats_every_ab.jsonl)")
     ap.add_argument("--replay", type=int, default=0,
                     help="cycle over this many distinct batches (0 = a distinct batch for every step; diagnostics)")
     ap.add_argument("--cpu-threads", type=int, default=0,
@@ -1090,8 +1093,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     # kernel stats (tier counts, in-kernel work counters, HIP-event kernel times) of every
-    # `stats_every`-th timed batch; a batch with stats waits for its results before its thread
-    # enqueues the next one
+    # `stats_every`-th timed batch (every kg_check_batch_device call waits for its batch anyway)
     stats = [_lib.kg_stats() if k % max(1, a.stats_every) == 0 else None for k in range(a.steps)]
     lat = [0.0] * a.steps
     go, th, errs = run_steps(warm, a.steps, stats, lat)

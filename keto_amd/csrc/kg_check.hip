@@ -863,6 +863,16 @@ __global__ __launch_bounds__(256) void k_back(DevSnap s, const RQuery* __restric
   block_stats<3>(ctl, idx, v);
 }
 
+// The rewrite interpreter's control block pointers (its counters live in the batch's zeroed Ctl).
+__global__ void k_ic_init(InterpCtl* ic, const uint32_t* gen_count, uint32_t* p2_list, Ctl* ctl) {
+  ic->gen_count = gen_count;
+  ic->p2_list = p2_list;
+  ic->st_general = &ctl->st[ST_GENERAL];
+  ic->st_rows = &ctl->st[ST_ROWS];
+  ic->st_edges = &ctl->st[ST_EDGES];
+  ic->st_probes = &ctl->st[ST_PROBES];
+}
+
 // ------------------------------------------------------------------ synthetic queries
 __global__ void k_synth_queries(SynthLayout L, DevSnap s, uint64_t seed, uint32_t n, kg_query* q) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1076,14 +1086,11 @@ int check_batch_begin(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n, 
       grid_count = fwd_count;
     }
     if (s->has_program) {
-      InterpCtl ic{};
-      ic.gen_count = &ctl->gen_count;
-      ic.p2_list = p2;
-      ic.st_general = &ctl->st[ST_GENERAL];
-      ic.st_rows = &ctl->st[ST_ROWS];
-      ic.st_edges = &ctl->st[ST_EDGES];
-      ic.st_probes = &ctl->st[ST_PROBES];
-      HIPC(hipMemcpyAsync(&ctl->ic, &ic, sizeof ic, hipMemcpyHostToDevice, stream));
+      // the interpreter's control block: its counters and heads were zeroed with the Ctl; the pointers are
+      // written by a one-thread kernel (round 6: a hipMemcpyAsync from this stack variable -- pageable
+      // memory -- held the host until the stream had drained, a gap before the interpreter passes of
+      // every C3 batch)
+      hipLaunchKernelGGL(k_ic_init, dim3(1), dim3(1), 0, stream, &ctl->ic, (const uint32_t*)&ctl->gen_count, p2, ctl);
       if (launch_general(s, w, d_q, rq, gen, &ctl->gen_count, &ctl->ic, d_out, d_err, (uint32_t)n, stream)) return -1;
     }
     // the requested results, stream-ordered before anything the caller enqueues after this call

@@ -92,6 +92,8 @@ struct GridLog {
   uint32_t* slot;  // slot of the entry
   uint32_t* rb;    // first adjx index of the node's set row
   uint64_t* ex;    // edge start of the entry within its level
+  uint2* info;     // the slot's (tagged subject, rest depth of the root), carried by every entry (round 6: a
+                   // level reads it with the entry instead of a dependent sl.info[slot] round trip)
   uint32_t* tile_first[2];  // level parity -> tile -> entry (level-relative)
   uint64_t cap;
 };
@@ -99,7 +101,8 @@ struct GridLog {
 // Workgroup-aggregated append of the lanes with `app` set (entry slot / row start rb / row length
 // len) to level counters lv[nl] (tile map tile_first[np]); every thread of the workgroup must call it.
 __device__ __forceinline__ void grid_append(GridCtl* ctl, GridLv* lvs, const GridLog& lg, int nl, int np,
-                                            uint64_t next_base, bool app, uint32_t slot, uint32_t rb, uint32_t len) {
+                                            uint64_t next_base, bool app, uint32_t slot, uint32_t rb, uint32_t len,
+                                            uint2 info) {
   __shared__ uint32_t s_wcnt[4];
   __shared__ uint64_t s_wedge[4];
   __shared__ unsigned long long s_old;
@@ -135,6 +138,7 @@ __device__ __forceinline__ void grid_append(GridCtl* ctl, GridLv* lvs, const Gri
       lg.slot[gi] = slot;
       lg.rb[gi] = rb;
       lg.ex[gi] = ex;
+      lg.info[gi] = info;
       // tiles whose first edge lies in [ex, ex + len): exactly one entry writes each tile
       for (uint64_t t = (ex + GT - 1) / GT; t * GT < ex + len && t < TILE_CAP; t++) lg.tile_first[np][t] = (uint32_t)at;
     } else {
@@ -151,6 +155,7 @@ __device__ __forceinline__ void grid_append(GridCtl* ctl, GridLv* lvs, const Gri
 constexpr uint32_t GB_BUF = 512;
 struct GridBuf {
   uint32_t slot[GB_BUF], rb[GB_BUF], len[GB_BUF], pre[GB_BUF];
+  uint2 info[GB_BUF];
   uint32_t n, edges;
   uint32_t wcnt[4], wedge[4];
   unsigned long long old;
@@ -169,6 +174,7 @@ __device__ void grid_flush(GridCtl* ctl, GridLv* lvs, const GridLog& lg, int nl,
       lg.slot[gi] = B.slot[i];
       lg.rb[gi] = B.rb[i];
       lg.ex[gi] = ex;
+      lg.info[gi] = B.info[i];
       // tiles whose first edge lies in [ex, ex + len): exactly one entry writes each tile
       for (uint64_t t = (ex + GT - 1) / GT; t * GT < ex + len && t < TILE_CAP; t++) lg.tile_first[np][t] = (uint32_t)at;
     } else {
@@ -186,7 +192,7 @@ __device__ void grid_flush(GridCtl* ctl, GridLv* lvs, const GridLog& lg, int nl,
 // Every thread of the workgroup (256) calls it; flushes first when the tile's appends do not fit.
 __device__ __forceinline__ void grid_push(GridCtl* ctl, GridLv* lvs, const GridLog& lg, int nl, int np,
                                           uint64_t next_base, GridBuf& B, bool app, uint32_t slot, uint32_t rb,
-                                          uint32_t len) {
+                                          uint32_t len, uint2 info) {
   const int lane = lane_id(), wave = threadIdx.x >> 6;
   const uint64_t m = __ballot(app);
   uint32_t x = app ? len : 0u;
@@ -217,6 +223,7 @@ __device__ __forceinline__ void grid_push(GridCtl* ctl, GridLv* lvs, const GridL
     B.rb[at] = rb;
     B.len[at] = len;
     B.pre[at] = pre;
+    B.info[at] = info;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -240,17 +247,19 @@ __global__ __launch_bounds__(256) void k_grid_init(const RQuery* __restrict__ rq
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   const bool valid = i < round_slots(d_count, base, G);
   uint32_t rb = 0, len = 0;
+  uint2 info = make_uint2(0u, 0u);
   if (valid) {
     const uint32_t qi = qlist[base + i];
     const RQuery q = rq[qi];
     sl.q[i] = qi;
-    sl.info[i] = make_uint2(q.subj, (uint32_t)q.depth);
+    info = make_uint2(q.subj, (uint32_t)q.depth);
+    sl.info[i] = info;
     sl.hit[i] = 0;  // the root was already probed (k_resolve)
     if (gh_insert(H, mask, gh_key(epoch, i, q.node)) < 0) ctl->overflow = 1;
     rb = q.beg;
     len = q.len;
   }
-  grid_append(ctl, ctl->lv, lg, 0, 0, 0, valid, i, rb, len);
+  grid_append(ctl, ctl->lv, lg, 0, 0, 0, valid, i, rb, len, info);
 }
 
 // Largest j in [lo, hi) with ex[base + j] <= e: the entry holding edge e (search in the log).
@@ -297,18 +306,21 @@ __device__ __forceinline__ void gh_insert2(uint64_t* H, uint64_t mask, bool a0, 
 }
 
 // One level: two edges per thread (e and e + 256), one GT = 512-edge tile per workgroup iteration
-// (round 6; one edge per thread before: a tile's chain of dependent trips -- tile map, staged
-// entries, adjx, visited CAS, probe, append -- now covers twice the edges).  Level L expands the
-// nodes found at hop L (rest depth D - L >= 2) into hop L + 1: every child is probed (checkDirect at
-// its shallowest depth) and kept for the next level while D - (L + 1) >= 2 and its set row is non-empty.
+// (round 6; one edge per thread before: a tile's chain of dependent trips covers twice the edges).  Level
+// L expands the nodes found at hop L (rest depth D - L >= 2) into hop L + 1: every child is probed
+// (checkDirect at its shallowest depth) and kept for the next level while D - (L + 1) >= 2 and its set
+// row is non-empty.
+// The tile's chain of dependent HBM round trips (round 6, second session: 7 -> 5): tile map -> entries
+// (slot, row, edge start and the slot's subject / depth, carried by the entry) -> the slot's answered
+// flag and the adjx record together (an answered slot's record is loaded for nothing) -> the visited-set
+// word and the child's first dset bucket together (a kept child already visited this round is probed
+// again: the same answer) -> the insert's CAS.  The C2 tail tier is a few hundred queries whose levels
+// are this chain plus a launch (~12-30 us each, profiles/r6i_headline_timed_timeline.txt).
 __global__ __launch_bounds__(256) void k_grid_level(DevSnap s, GridLog lg, int level, GridSlots sl, uint64_t* H,
                                                     uint64_t mask, uint64_t epoch, GridCtl* ctl) {
   __shared__ uint64_t s_beg[GT + 2];
   __shared__ uint32_t s_slot[GT + 2], s_rb[GT + 2];
-  // per entry: its slot's state at tile start (subject, rest depth; hit) -- one load per entry instead
-  // of two per edge, and a slot already answered skips its edges' loads
-  __shared__ uint2 s_info[GT + 2];
-  __shared__ uint32_t s_hit[GT + 2];
+  __shared__ uint2 s_info[GT + 2];  // per entry: its slot's (subject, rest depth of the root)
   __shared__ uint64_t s_j0, s_cnt;
   __shared__ uint32_t s_void;
   __shared__ GridBuf B;
@@ -354,24 +366,24 @@ __global__ __launch_bounds__(256) void k_grid_level(DevSnap s, GridLog lg, int l
     if (use_lds)
       for (uint32_t i = threadIdx.x; i < cnt; i += 256) {
         s_beg[i] = lg.ex[lb + j0 + i];
-        const uint32_t sl_i = lg.slot[lb + j0 + i];
-        s_slot[i] = sl_i;
+        s_slot[i] = lg.slot[lb + j0 + i];
         s_rb[i] = lg.rb[lb + j0 + i];
-        s_info[i] = sl.info[sl_i];
-        s_hit[i] = sl.hit[sl_i];
+        s_info[i] = lg.info[lb + j0 + i];
       }
     __syncthreads();
-    // both edges' entry, then both adjx loads in flight at once (an inactive edge reads adjx[0])
-    bool act[2];
-    uint32_t slot[2] = {0u, 0u}, subj[2] = {0u, 0u};
+    // both edges' entry (LDS), then their slots' answered flags and adjx records in flight at once
+    bool inr[2];
+    uint32_t slot[2] = {0u, 0u}, subj[2] = {0u, 0u}, hv[2];
     int D[2] = {0, 0};
     AdjX x[2];
 #pragma unroll
     for (int h = 0; h < 2; h++) {
       const uint64_t e = t0 + threadIdx.x + (uint64_t)h * 256;
       uint64_t beg = 0;
-      uint32_t rb = 0, hit = 1;
-      if (e < t1) {
+      uint32_t rb = 0;
+      inr[h] = e < t1;
+      if (inr[h]) {
+        uint2 info;
         if (use_lds) {
           uint32_t lo = 0, hi = (uint32_t)cnt;  // largest i < cnt with s_beg[i] <= e
           while (hi - lo > 1) {
@@ -382,31 +394,37 @@ __global__ __launch_bounds__(256) void k_grid_level(DevSnap s, GridLog lg, int l
           beg = s_beg[lo];
           slot[h] = s_slot[lo];
           rb = s_rb[lo];
-          subj[h] = s_info[lo].x;
-          D[h] = (int)s_info[lo].y;
-          hit = s_hit[lo];
+          info = s_info[lo];
         } else {
           const uint64_t j = entry_of(lg.ex, lb, j0, j0 + cnt, e);
           beg = lg.ex[lb + j];
           slot[h] = lg.slot[lb + j];
           rb = lg.rb[lb + j];
-          const uint2 si = sl.info[slot[h]];
-          subj[h] = si.x;
-          D[h] = (int)si.y;
-          hit = sl.hit[slot[h]];
+          info = lg.info[lb + j];
         }
+        subj[h] = info.x;
+        D[h] = (int)info.y;
       }
-      act[h] = !hit;  // answered at tile start (or no edge): the edge is not even loaded
-      x[h] = s.adjx[act[h] ? rb + (uint32_t)(e - beg) : 0u];
+      hv[h] = inr[h] ? sl.hit[slot[h]] : 1u;  // plain load: a stale 0 only costs this level's work
+      x[h] = s.adjx[inr[h] ? rb + (uint32_t)(e - beg) : 0u];
     }
+    bool act[2], keep[2], sigok[2];
     uint32_t clen[2], cb[2];
-    bool keep[2];
+    uint64_t pk[2];
+    ulonglong2 pb[2];
 #pragma unroll
     for (int h = 0; h < 2; h++) {
+      act[h] = inr[h] && hv[h] == 0;  // answered at tile start (or no edge): nothing more for this edge
       cb[h] = x[h].begin;
       clen[h] = act[h] ? adjx_len(s, x[h]) : 0u;
       // hop level+1 is expanded at the next level while its rest depth D - (level + 1) >= 2
       keep[h] = act[h] && clen[h] > 0 && level + 2 <= D[h] - 1;
+      // the signature rules out most misses; the first bucket of the rest is loaded now, beside the
+      // visited-set words below
+      sigok[h] = act[h] && sig_maybe(x[h].lsig, x[h].sig, subj_sig(subj[h]));
+      pk[h] = dset_key(x[h].node, subj[h]);
+      pb[h] = ld_once(
+          reinterpret_cast<const ulonglong2*>(s.dset + (sigok[h] ? dset_home(pk[h], s.dset_nb) : 0ull) * DSET_BUCKET));
     }
     int ins[2];
     gh_insert2(H, mask, keep[0], gh_key(epoch, slot[0], x[0].node), keep[1], gh_key(epoch, slot[1], x[1].node), ins[0],
@@ -416,14 +434,18 @@ __global__ __launch_bounds__(256) void k_grid_level(DevSnap s, GridLog lg, int l
     for (int h = 0; h < 2; h++) {
       if (keep[h] && ins[h] < 0) ctl->overflow = 1;
       const bool fresh = act[h] && (!keep[h] || ins[h] > 0);
-      if (fresh && sig_maybe(x[h].lsig, x[h].sig, subj_sig(subj[h]))) {  // the signature rules out most misses
+      if (fresh && sigok[h]) {
         probes++;
-        if (dset_probe(s, x[h].node, subj[h])) atomicExch(&sl.hit[slot[h]], 1u);
+        bool hit = pb[h].x == pk[h] || pb[h].y == pk[h];
+        if (!hit && pb[h].y != EMPTY64) hit = dset_probe(s, x[h].node, subj[h]);  // past a full first bucket
+        if (hit) atomicExch(&sl.hit[slot[h]], 1u);
       }
       app[h] = fresh && keep[h];
     }
-    grid_push(ctl, lvs, lg, nl, (level + 1) & 1, next_base, B, app[0], slot[0], cb[0], clen[0]);
-    grid_push(ctl, lvs, lg, nl, (level + 1) & 1, next_base, B, app[1], slot[1], cb[1], clen[1]);
+    grid_push(ctl, lvs, lg, nl, (level + 1) & 1, next_base, B, app[0], slot[0], cb[0], clen[0],
+              make_uint2(subj[0], (uint32_t)D[0]));
+    grid_push(ctl, lvs, lg, nl, (level + 1) & 1, next_base, B, app[1], slot[1], cb[1], clen[1],
+              make_uint2(subj[1], (uint32_t)D[1]));
   }
   if (B.n) grid_flush(ctl, lvs, lg, nl, (level + 1) & 1, next_base, B);
   for (int off = 32; off; off >>= 1) probes += __shfl_xor(probes, off, 64);
@@ -467,7 +489,7 @@ struct GridView {  // pointers into a pool laid out for `cap` log entries (per d
 static int grid_layout(GridPool* P, uint64_t cap, hipStream_t stream, GridView* v) {
   uint64_t hcap = 1;
   while (hcap < 2 * cap) hcap <<= 1;
-  const size_t log_bytes = cap * (4 + 4 + 8) + 2 * TILE_CAP * 4;
+  const size_t log_bytes = cap * (4 + 4 + 8 + 8) + 2 * TILE_CAP * 4;
   const size_t need = hcap * 8 + log_bytes + (size_t)G0 * 16 + sizeof(GridCtl) + 4096;
   if (need > P->bytes) {
     P->release();
@@ -489,6 +511,8 @@ static int grid_layout(GridPool* P, uint64_t cap, hipStream_t stream, GridView* 
   p += cap * 4;
   lg->rb = (uint32_t*)p;
   p += cap * 4;
+  lg->info = (uint2*)p;
+  p += cap * 8;
   lg->tile_first[0] = (uint32_t*)p;
   p += TILE_CAP * 4;
   lg->tile_first[1] = (uint32_t*)p;
