@@ -198,7 +198,8 @@ __global__ __launch_bounds__(256) void k_resolve(DevSnap s, const kg_query* __re
     const bool unheld = no_holder_filter == 2 && use_bits && !s.relflags && !((hw >> (subj & 31)) & 1u);
     NSlot n0{};
     if (key_ok && !unheld) n0 = ld_once(s.nmap + ni);
-    uint32_t node = NONE, rb = 0, rl = 0, rsig_lo = 0xFFFFFFFFu, rsig = 0xFFFFFFFFu, nfl = 0;
+    uint32_t node = NONE, rb = 0, rl = 0, rsig_lo = 0xFFFFFFFFu, rsig = 0xFFFFFFFFu, nfl = 0, icnt = 0;
+    uint4 il0 = make_uint4(NONE, NONE, NONE, NONE), il1 = il0;  // the slot's inline check-row subjects
     if (unheld) {
       no_holder = true;
     } else if (key_ok) {
@@ -220,6 +221,9 @@ __global__ __launch_bounds__(256) void k_resolve(DevSnap s, const kg_query* __re
         rsig = v.sig;
         rsig_lo = (uint32_t)v.pad1;  // signature bits 0-11 in bits 20-31
         nfl = (uint32_t)(v.pad1 & 0xFFu);
+        icnt = nslot_inline(v.pad1);
+        il0 = make_uint4(v.inl[0], v.inl[1], v.inl[2], v.inl[3]);
+        il1 = make_uint4(v.inl[4], v.inl[5], v.inl[6], v.inl[7]);
       }
     }
     if (!sid) {
@@ -246,8 +250,14 @@ __global__ __launch_bounds__(256) void k_resolve(DevSnap s, const kg_query* __re
       // row signature in the node-map slot rules out most misses without touching dset.
       // an unset holder bit rules the probe out as well (the exact tuple would make subj a holder)
       const bool nobit = use_bits && !((hw >> (subj & 31)) & 1u);
-      did_probe = subj != NONE && !nobit && sig_maybe(rsig_lo, rsig, subj_sig(subj));
-      member = did_probe && dset_probe(s, node, subj);
+      if (icnt) {
+        // the whole check row is in the slot (NONE past its length; NONE is never a subject): exact, no dset line
+        member = subj != NONE && ((il0.x == subj) | (il0.y == subj) | (il0.z == subj) | (il0.w == subj) |
+                                  (il1.x == subj) | (il1.y == subj) | (il1.z == subj) | (il1.w == subj));
+      } else {
+        did_probe = subj != NONE && !nobit && sig_maybe(rsig_lo, rsig, subj_sig(subj));
+        member = did_probe && dset_probe(s, node, subj);
+      }
       if (member || d < 2 || rl == 0) route = ROUTE_DONE;
       // a subject that no row holds cannot be reached from any root (checkDirect never hits)
       if (route == ROUTE_LIGHT && no_holder_filter) {

@@ -146,14 +146,23 @@ struct AdjX {
 };
 __host__ __device__ __forceinline__ uint32_t adjx_len16(const AdjX& x) { return x.lsig & ADJX_LEN_SAT; }
 
-// Node-map slot: key (ns,rel,obj), node id and the node's set-adjacency row, one 32-B slot so a
-// request mapping is one random line.  key == EMPTY64: free.
-struct NSlot {
+// Node-map slot: key (ns,rel,obj), node id and the node's set-adjacency row, and -- when the node's check
+// row has at most NSLOT_INL subjects -- those subjects themselves, one 64-B slot (one 64-B sector) so a
+// request mapping is one random read and the root's checkDirect (engine.go:148-177) needs no dset line
+// for most roots (round 6: doc rows average a few subjects; k_resolve probed dset for ~27 % of the C2
+// batch).  key == EMPTY64: free.
+constexpr uint32_t NSLOT_INL = 8;
+struct alignas(64) NSlot {
   uint64_t key;
   uint32_t node, beg, len;
   uint32_t sig;  // signature bits 12-43 of the node's row subjects (as AdjX.sig): k_resolve's root probe filter
-  uint64_t pad1;  // low byte: the node's flags (nflags; 0 without a namespace program); bits 20-31: signature bits 0-11
+  // low byte: the node's flags (nflags; 0 without a namespace program); bits 8-11: 1 + the number of inline
+  // check-row subjects (0: not inlined -- probe dset); bits 20-31: signature bits 0-11
+  uint64_t pad1;
+  uint32_t inl[NSLOT_INL];  // the inline check-row subjects (tagged), NONE past the count
 };
+static_assert(sizeof(NSlot) == 64, "one 64-B sector per node-map slot");
+__host__ __device__ __forceinline__ uint32_t nslot_inline(uint64_t pad1) { return (uint32_t)(pad1 >> 8) & 0xFu; }
 // Holder-hash slot: tagged subject -> hold[first, first + count).  key == NONE: free.
 struct HSlot {
   uint32_t key, first, count, pad;

@@ -269,6 +269,7 @@ __device__ __forceinline__ SeedQ seed_query(const DevSnap& s, const kg_query* __
   const bool unheld = held && !s.relflags && sid &&
                       (subj == NONE || subj >= held_n || !((held[subj >> 5] >> (subj & 31)) & 1u));
   uint32_t node = NONE, rsig_lo = 0xFFFFFFFFu, rsig = 0xFFFFFFFFu, rlen = 0, rbeg = 0;
+  const NSlot* rsl = nullptr;  // the root's slot: its inline check-row subjects (a local root's probe)
   if (!unheld && nmap_key_ok(x.t.ns, x.t.rel, x.t.obj)) {
     const uint64_t key = nmap_key(x.t.ns, x.t.rel, x.t.obj);
     const NSlot* sl = nmap_slot(s, key, hash_home(key, s.nmap_n));
@@ -278,6 +279,7 @@ __device__ __forceinline__ SeedQ seed_query(const DevSnap& s, const kg_query* __
       rsig_lo = (uint32_t)sl->pad1;  // signature bits 0-11 in bits 20-31
       rlen = sl->len;
       rbeg = sl->beg;
+      rsl = sl;
     }
   }
   if (!sid) {
@@ -327,7 +329,7 @@ __device__ __forceinline__ SeedQ seed_query(const DevSnap& s, const kg_query* __
     if (o.dest == s.shard_rank && !s.relflags) {
       // a locally owned root without a namespace program (as shard_child): checkDirect here, a
       // record only if the root can expand
-      if (may && d >= 1 && subj != NONE && dset_probe(s, node, subj)) {
+      if (may && d >= 1 && subj != NONE && nslot_probe(s, rsl, node, subj)) {
         res[i] = KG_IS_MEMBER;
         o.act = false;
       } else if (rlen == 0 || d < 2) {

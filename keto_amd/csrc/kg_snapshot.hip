@@ -55,7 +55,7 @@ __global__ void k_dset_insert_rows(uint64_t* dset, uint64_t nb, const uint64_t* 
 
 __global__ void k_nmap_insert(NSlot* nm, uint64_t slots, const uint32_t* nd_ns, const uint32_t* nd_obj,
                               const uint32_t* nd_rel, const uint64_t* adj_off, const uint32_t* xoff, const uint2* sig,
-                              const uint8_t* flags, uint32_t n_nodes) {
+                              const uint8_t* flags, uint32_t n_nodes, const uint64_t* coff, const uint32_t* csub) {
   uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
   if (v >= n_nodes) return;
   uint64_t key = nmap_key(nd_ns[v], nd_rel[v], nd_obj[v]);
@@ -69,8 +69,15 @@ __global__ void k_nmap_insert(NSlot* nm, uint64_t slots, const uint32_t* nd_ns, 
       nm[i].len = (uint32_t)(adj_off[v + 1] - adj_off[v]);
       const uint2 g = sig[v];
       nm[i].sig = g.y;
+      // a short check row rides in the slot (NSLOT_INL subjects at most); 1 + its length in bits 8-11
+      const uint64_t cb = coff[v], cl = coff[v + 1] - cb;
+      uint64_t inl = 0;
+      if (cl <= NSLOT_INL) {
+        inl = cl + 1;
+        for (uint32_t j = 0; j < NSLOT_INL; j++) nm[i].inl[j] = j < cl ? csub[cb + j] : NONE;
+      }
       // node flags (k_resolve's impurity test without a random nflags read) + signature bits 0-11 in bits 20-31
-      nm[i].pad1 = (flags ? flags[v] : 0u) | (g.x & SIG_LO);
+      nm[i].pad1 = (flags ? flags[v] : 0u) | (inl << 8) | (g.x & SIG_LO);
       return;
     }
     i = hash_next(i, slots);
@@ -583,7 +590,7 @@ int Snapshot::build_hash_tables() {
                          stream, dset, buckets, coff, csub, ds.n_nodes, n_rows);
     HIPC(hipGetLastError());
     hipLaunchKernelGGL(k_nmap_insert, dim3(grid), dim3(256), 0, stream, nm, slots, ds.nd_ns, ds.nd_obj,
-                       ds.nd_rel, ds.adj_off, xoff, sig, ds.nflags, ds.n_nodes);
+                       ds.nd_rel, ds.adj_off, xoff, sig, ds.nflags, ds.n_nodes, coff, csub);
     HIPC(hipGetLastError());
   }
   HIPC(hipStreamSynchronize(stream));
