@@ -68,12 +68,7 @@ __device__ __forceinline__ bool dset_probe(const DevSnap& s, uint32_t node, uint
 // checkDirect at a root whose node-map slot is at hand: its inline check-row subjects when the slot
 // carries them (the whole row), else the dset probe.
 __device__ __forceinline__ bool nslot_probe(const DevSnap& s, const NSlot* sl, uint32_t node, uint32_t subj) {
-  if (sl && nslot_inline(sl->pad1)) {
-    bool hit = false;
-#pragma unroll
-    for (uint32_t j = 0; j < NSLOT_INL; j++) hit |= sl->inl[j] == subj;
-    return hit;
-  }
+  if (sl && nslot_inline(sl->pad1)) return nslot_inline_has(nslot_inline(sl->pad1), sl->pad1, sl->sig, subj);
   return dset_probe(s, node, subj);
 }
 

@@ -199,7 +199,7 @@ __global__ __launch_bounds__(256) void k_resolve(DevSnap s, const kg_query* __re
     NSlot n0{};
     if (key_ok && !unheld) n0 = ld_once(s.nmap + ni);
     uint32_t node = NONE, rb = 0, rl = 0, rsig_lo = 0xFFFFFFFFu, rsig = 0xFFFFFFFFu, nfl = 0, icnt = 0;
-    uint4 il0 = make_uint4(NONE, NONE, NONE, NONE), il1 = il0;  // the slot's inline check-row subjects
+    uint64_t rpad = 0;
     if (unheld) {
       no_holder = true;
     } else if (key_ok) {
@@ -222,8 +222,7 @@ __global__ __launch_bounds__(256) void k_resolve(DevSnap s, const kg_query* __re
         rsig_lo = (uint32_t)v.pad1;  // signature bits 0-11 in bits 20-31
         nfl = (uint32_t)(v.pad1 & 0xFFu);
         icnt = nslot_inline(v.pad1);
-        il0 = make_uint4(v.inl[0], v.inl[1], v.inl[2], v.inl[3]);
-        il1 = make_uint4(v.inl[4], v.inl[5], v.inl[6], v.inl[7]);
+        rpad = v.pad1;
       }
     }
     if (!sid) {
@@ -251,9 +250,8 @@ __global__ __launch_bounds__(256) void k_resolve(DevSnap s, const kg_query* __re
       // an unset holder bit rules the probe out as well (the exact tuple would make subj a holder)
       const bool nobit = use_bits && !((hw >> (subj & 31)) & 1u);
       if (icnt) {
-        // the whole check row is in the slot (NONE past its length; NONE is never a subject): exact, no dset line
-        member = subj != NONE && ((il0.x == subj) | (il0.y == subj) | (il0.z == subj) | (il0.w == subj) |
-                                  (il1.x == subj) | (il1.y == subj) | (il1.z == subj) | (il1.w == subj));
+        // the whole check row is in the slot: exact, no dset line
+        member = subj != NONE && nslot_inline_has(icnt, rpad, rsig, subj);
       } else {
         did_probe = subj != NONE && !nobit && sig_maybe(rsig_lo, rsig, subj_sig(subj));
         member = did_probe && dset_probe(s, node, subj);

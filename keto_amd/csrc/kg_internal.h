@@ -146,23 +146,31 @@ struct AdjX {
 };
 __host__ __device__ __forceinline__ uint32_t adjx_len16(const AdjX& x) { return x.lsig & ADJX_LEN_SAT; }
 
-// Node-map slot: key (ns,rel,obj), node id and the node's set-adjacency row, and -- when the node's check
-// row has at most NSLOT_INL subjects -- those subjects themselves, one 64-B slot (one 64-B sector) so a
-// request mapping is one random read and the root's checkDirect (engine.go:148-177) needs no dset line
-// for most roots (round 6: doc rows average a few subjects; k_resolve probed dset for ~27 % of the C2
-// batch).  key == EMPTY64: free.
-constexpr uint32_t NSLOT_INL = 8;
-struct alignas(64) NSlot {
+// Node-map slot: key (ns,rel,obj), node id and the node's set-adjacency row, one 32-B slot so a
+// request mapping is one random line.  key == EMPTY64: free.
+// A check row of at most NSLOT_INL subjects rides in the slot itself (round 6): the first in pad1's high
+// word, the second in `sig` (such a row needs no Bloom signature) -- the root's checkDirect
+// (engine.go:148-177) then reads no dset line.  Doc rows are that short for ~3/4 of the C2 roots.
+// (A 64-B slot with up to 8 subjects cut k_resolve's fabric requests 10 % but cost the headline ~8 %:
+// twice the node map's footprint, profiles/r6m_*.)
+constexpr uint32_t NSLOT_INL = 2;
+struct NSlot {
   uint64_t key;
   uint32_t node, beg, len;
-  uint32_t sig;  // signature bits 12-43 of the node's row subjects (as AdjX.sig): k_resolve's root probe filter
-  // low byte: the node's flags (nflags; 0 without a namespace program); bits 8-11: 1 + the number of inline
-  // check-row subjects (0: not inlined -- probe dset); bits 20-31: signature bits 0-11
+  // signature bits 12-43 of the node's row subjects (as AdjX.sig): k_resolve's root probe filter; for an
+  // inline row of two subjects, the second subject
+  uint32_t sig;
+  // bits 0-7: the node's flags (nflags; 0 without a namespace program); bits 8-9: 1 + the number of
+  // inline check-row subjects (0: not inlined -- probe dset); bits 20-31: signature bits 0-11 (rows not
+  // inlined); bits 32-63: the first inline subject
   uint64_t pad1;
-  uint32_t inl[NSLOT_INL];  // the inline check-row subjects (tagged), NONE past the count
 };
-static_assert(sizeof(NSlot) == 64, "one 64-B sector per node-map slot");
-__host__ __device__ __forceinline__ uint32_t nslot_inline(uint64_t pad1) { return (uint32_t)(pad1 >> 8) & 0xFu; }
+static_assert(sizeof(NSlot) == 32, "one 32-B node-map slot");
+__host__ __device__ __forceinline__ uint32_t nslot_inline(uint64_t pad1) { return (uint32_t)(pad1 >> 8) & 3u; }
+// checkDirect against an inlined row (icnt = nslot_inline(pad1) >= 1): exact
+__host__ __device__ __forceinline__ bool nslot_inline_has(uint32_t icnt, uint64_t pad1, uint32_t sig, uint32_t subj) {
+  return (icnt >= 2 && (uint32_t)(pad1 >> 32) == subj) | (icnt == 3 && sig == subj);
+}
 // Holder-hash slot: tagged subject -> hold[first, first + count).  key == NONE: free.
 struct HSlot {
   uint32_t key, first, count, pad;

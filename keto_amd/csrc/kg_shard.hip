@@ -323,7 +323,11 @@ __device__ __forceinline__ SeedQ seed_query(const DevSnap& s, const kg_query* __
     const bool rmeta = s.remote_meta && (rbeg & ADJX_REMOTE) && !s.relflags;
     o.dest = s.remote_meta ? ((rbeg & ADJX_REMOTE) ? (rbeg & 0xFFu) : s.shard_rank) : (s.nowner ? s.nowner[node] : 0u);
     // otherwise signatures are built from this rank's rows: only a locally owned node's rules a probe out
-    const bool may = subj == NONE || (o.dest != s.shard_rank && !rmeta) || sig_maybe(rsig_lo, rsig, subj_sig(subj));
+    // an inlined slot (a short local check row) holds the row itself instead of its signature: exact
+    const uint32_t icnt = rsl ? nslot_inline(rsl->pad1) : 0u;
+    const bool sigm = icnt ? (subj != NONE && nslot_inline_has(icnt, rsl->pad1, rsl->sig, subj))
+                           : sig_maybe(rsig_lo, rsig, subj_sig(subj));
+    const bool may = subj == NONE || (o.dest != s.shard_rank && !rmeta) || sigm;
     if (rmeta && subj != NONE && !may && (rlen == 0 || d < 2)) o.act = false;
     o.r = kg_frec{(s.shard_rank << Q_BITS) | i, node, subj, d | (may ? 0 : D_NOPROBE)};
     if (o.dest == s.shard_rank && !s.relflags) {

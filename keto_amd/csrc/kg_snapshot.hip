@@ -68,16 +68,18 @@ __global__ void k_nmap_insert(NSlot* nm, uint64_t slots, const uint32_t* nd_ns, 
       nm[i].beg = xoff ? xoff[v] : (uint32_t)adj_off[v];
       nm[i].len = (uint32_t)(adj_off[v + 1] - adj_off[v]);
       const uint2 g = sig[v];
-      nm[i].sig = g.y;
-      // a short check row rides in the slot (NSLOT_INL subjects at most); 1 + its length in bits 8-11
+      // node flags (k_resolve's impurity test without a random nflags read) + signature bits 0-11 in bits 20-31,
+      // or a short check row in the slot (NSLOT_INL subjects at most: pad1's high word, then sig)
       const uint64_t cb = coff[v], cl = coff[v + 1] - cb;
-      uint64_t inl = 0;
+      const uint64_t fl = flags ? flags[v] : 0u;
       if (cl <= NSLOT_INL) {
-        inl = cl + 1;
-        for (uint32_t j = 0; j < NSLOT_INL; j++) nm[i].inl[j] = j < cl ? csub[cb + j] : NONE;
+        const uint32_t s0 = cl >= 1 ? csub[cb] : NONE, s1 = cl >= 2 ? csub[cb + 1] : NONE;
+        nm[i].sig = s1;
+        nm[i].pad1 = fl | ((cl + 1) << 8) | ((uint64_t)s0 << 32);
+      } else {
+        nm[i].sig = g.y;
+        nm[i].pad1 = fl | (g.x & SIG_LO);
       }
-      // node flags (k_resolve's impurity test without a random nflags read) + signature bits 0-11 in bits 20-31
-      nm[i].pad1 = (flags ? flags[v] : 0u) | (inl << 8) | (g.x & SIG_LO);
       return;
     }
     i = hash_next(i, slots);
