@@ -64,10 +64,13 @@ def parse(argv=None):
                     help="checks per sharded batch per rank (0: --batch).  C4 names 1-8 M; across ranks one batch "
                          "is in flight per rank, and 4 M amortises the exchanges' fixed cost: one-rank exchange "
                          "protocol 0.80 / 1.19 / 1.29 x 10^9 checks/s at 1 / 4 / 8 M (DESIGN.md 7f)")
-    ap.add_argument("--expand-steps", type=int, default=6,
-                    help="check mode, one rank: timed calls of the C5 expand sub-line over the headline graph (0 = off)")
-    ap.add_argument("--expand-inflight", type=int, default=8,
-                    help="check mode: kg_expand_batch calls in flight in the C5 sub-line (one library lane each)")
+    ap.add_argument("--expand-steps", type=int, default=24,
+                    help="check mode, one rank: timed calls of the C5 expand sub-line over the headline graph (0 = off; "
+                         "at least twice --expand-inflight, so every caller thread makes two calls)")
+    ap.add_argument("--expand-inflight", type=int, default=12,
+                    help="check mode: kg_expand_batch_device calls in flight in the C5 sub-line (one HIP stream each; "
+                         "a call's critical path is its largest root's walk on one workgroup, so calls overlap: "
+                         "8 / 12 / 16 gave 2.18 / 2.62 / 2.24 x 10^7 trees/s, profiles/r6m_c5_inflight.txt)")
     ap.add_argument("--c3-steps", type=int, default=20,
                     help="check mode, one rank: timed batches of the C3 sub-line (OPL rewrites; 0 = off)")
     ap.add_argument("--c3-tuples", type=float, default=1e7, help="C3 sub-line graph size (BASELINE configs[2]: 10M)")
@@ -149,6 +152,9 @@ def parse(argv=None):
     ap.add_argument("--host-calls", type=int, default=20,
                     help="kg_check_batch calls per in-flight thread in the host-path leg (1 M-check host batches, "
                          "PCIe both ways; 0 = skip)")
+    ap.add_argument("--stagger-us", type=float, default=0.0,
+                    help="diagnostics: in-flight caller p starts its first batch p * this many us after the others "
+                         "(timed region included), so the callers' tail tiers do not run in lockstep")
     ap.add_argument("--stats-every", type=int, default=10,
                     help="collect kernel stats (HIP events around the batch and k_stream4, the in-kernel counters) on "
                          "every k-th timed batch (1 = all).  Default 10: two of the driver's 20 steps -- the event "
@@ -1065,6 +1071,10 @@ def main():
         def worker(p):
             try:
                 go.wait()
+                if a.stagger_us > 0:  # caller p arrives p * stagger later (spin: sleep() is too coarse)
+                    t_go = time.perf_counter() + p * a.stagger_us * 1e-6
+                    while time.perf_counter() < t_go:
+                        pass
                 for k in range(p, K, P):
                     s0 = time.perf_counter()
                     step(p, k0 + k, stats[k] if stats is not None else None)  # stats => waits for its batch
