@@ -338,10 +338,6 @@ constexpr uint32_t S4_CHUNK = 64;
 #ifndef KG_STREAM_EPL
 #define KG_STREAM_EPL 2
 #endif
-// Two software-pipelined query groups per wave (k_stream6, round 6); -DKG_STREAM_DUAL=0 builds k_stream4.
-#ifndef KG_STREAM_DUAL
-#define KG_STREAM_DUAL 1
-#endif
 
 template <int VLOG2, int QC, int EPL>
 struct Stream4Lds {
@@ -652,358 +648,6 @@ __global__ __launch_bounds__(256) void k_stream4(DevSnap s, LqList wl, uint32_t*
   block_max3(ctl, ~(unsigned long long)t_start, t_end, t_end - t_start);
   const int idx[7] = {ST_LROWS, ST_LEDGES, ST_LPROBES, ST_LIGHT, ST_LSTEPS, ST_LWAVES, ST_LTICKS};
   const unsigned long long v[7] = {st_rows, st_edges, st_probes, st_done, st_steps, lane == 0 ? 1ull : 0ull, life};
-  block_stats<7>(ctl, idx, v);
-}
-
-// ------------------------------------------------------------------ k_stream6: two query groups per wave
-// The stream tier's step (k_stream4) is a chain of dependent LDS round trips and one HBM round trip, and
-// at 4 waves per SIMD (LDS and registers both cap it) the SIMD idles through most of it (round 6: ~3.5 us
-// per step, VALU busy ~30 %).  k_stream6 splits a wave's 32 query slots into two groups of 16, each with
-// its own FIFO of row entries, and software-pipelines them: a group's step is cut in two -- FRONT (the
-// window, its edges' adjx gathers and the previous children's dset probes ISSUED) and BACK (the loads
-// used: hits, children marked / appended, finished queries) -- and the wave runs
-//     front(0)  back(1)  front(1)  back(0)  ...
-// so one group's loads are in flight while the other group's results are processed.  Per group the
-// sequence front -> back -> front is the k_stream4 step, unchanged (same FIFO discipline, visited cache,
-// budgets and hand-ons); the groups share the visited cache (keys carry the slot) and the dequeue.
-template <int VLOG2, int QCG, int EPL>
-struct Stream6Lds {
-  unsigned long long vt[1 << VLOG2];   // direct-mapped visited cache (0 = empty), both groups
-  uint32_t e_beg[2][QCG], e_meta[2][QCG];  // a FIFO ring per group
-  uint32_t pref[2][64 * EPL + 1];      // edge-owner marks per group (+1 dummy)
-  uint32_t s_state[32], s_qi[32], s_subj[32], s_last[32], s_edg[32];  // slot 16 g + i: group g
-  uint32_t s_node[32], s_depth[32], s_beg[32], s_len[32];
-  uint4 s_ss[32];
-};
-
-// A group's wave-uniform FIFO state and its lanes' pending probes.
-// A lane's pending probe is (node, packed): packed = PEND | generation << 5 | slot (registers are what
-// caps the pipelined kernel's occupancy).
-constexpr uint32_t S6_PEND = 1u << 31;
-template <int EPL>
-struct S6Group {
-  uint32_t head, tail, head_off;
-  uint32_t pend_node[EPL], pend_sg[EPL];
-};
-__device__ __forceinline__ uint32_t s6_slot(uint32_t sg) { return sg & 31u; }
-__device__ __forceinline__ uint32_t s6_gen(uint32_t sg) { return (sg >> 5) & S2_GEN; }
-
-// One issued step of a group: what BACK needs of FRONT's window and loads.
-template <int EPL>
-struct S6Step {
-  bool live;       // a step is in flight
-  uint32_t taken;
-  AdjX x[EPL];
-  uint32_t om[EPL];
-  bool act[EPL];
-  bool pvalid[EPL];
-  uint32_t psubj[EPL];  // the pending probe's subject (its dset key is rebuilt from pend_node)
-  ulonglong2 pb[EPL];
-};
-
-template <int VLOG2, int QCG, int EPL>
-__device__ __forceinline__ void s6_front(const DevSnap& s, Stream6Lds<VLOG2, QCG, EPL>& L, int G, uint32_t active,
-                                         S6Group<EPL>& Gs, S6Step<EPL>& st, uint32_t& st_rows, uint32_t& st_edges,
-                                         uint32_t& st_steps) {
-  constexpr uint32_t WIN = 64u * EPL;
-  const int lane = lane_id();
-  const uint32_t gmask = 0xFFFFu << (16 * G);
-  st.live = false;
-  if ((active & gmask) == 0) {
-    Gs.head = Gs.tail;  // no query of this group holds its FIFO: whatever is left in it is stale
-    Gs.head_off = 0;
-    return;
-  }
-  st.live = true;
-  const uint32_t avail = Gs.tail - Gs.head;
-  const uint32_t at0 = (Gs.head + lane) & (QCG - 1);
-  uint32_t emeta = L.e_meta[G][at0], ebeg = L.e_beg[G][at0];
-  const uint32_t sl0 = (emeta >> 11) & 31u;
-  const uint32_t st0 = L.s_state[sl0];
-#pragma unroll
-  for (int h = 0; h < EPL; h++) {
-    const uint32_t ps = s6_slot(Gs.pend_sg[h]);
-    const uint32_t pst = L.s_state[ps];
-    st.psubj[h] = L.s_subj[ps];
-    st.pvalid[h] = (Gs.pend_sg[h] & S6_PEND) && pst == s6_gen(Gs.pend_sg[h]);
-  }
-  const bool inwin = (uint32_t)lane < avail;
-  const bool live = inwin && ((active >> sl0) & 1u) && (st0 == ((emeta >> 16) & S2_GEN));  // no HIT/OVER
-  uint32_t elen = live ? (emeta & 0x7FFu) : 0u;
-  if (lane == 0) {
-    ebeg += Gs.head_off;
-    elen = live ? elen - Gs.head_off : 0u;
-  }
-  if (!inwin) emeta = 0;
-  uint32_t total;
-  const uint32_t excl = wave_excl_scan(elen, &total);
-#pragma unroll
-  for (int h = 0; h < EPL; h++) L.pref[G][lane + 64 * h] = 0;
-  __builtin_amdgcn_wave_barrier();
-  const uint32_t taken = min(total, WIN);
-  L.pref[G][(elen > 0 && excl < taken) ? excl : WIN] = (uint32_t)lane + 1;
-  const bool consumed = (uint32_t)lane < avail && excl + elen <= taken;
-  const uint32_t ncons = __popcll(__ballot(consumed));  // a prefix of the window
-  st_rows += (consumed && live) ? 1u : 0u;
-  {
-    const uint32_t ex_n = (uint32_t)__builtin_amdgcn_readlane((int)excl, ncons & 63);
-    if (ncons < avail && ncons < 64 && ex_n < taken) Gs.head_off = (ncons == 0 ? Gs.head_off : 0u) + (taken - ex_n);
-    else if (ncons > 0) Gs.head_off = 0;
-  }
-  __builtin_amdgcn_wave_barrier();
-  uint32_t mcarry = 0;
-#pragma unroll
-  for (int h = 0; h < EPL; h++) {
-    uint32_t m = wave_incl_scan<DppMax>(L.pref[G][lane + 64 * h]);
-    if (h > 0) m = max(m, mcarry);
-    if (h + 1 < EPL) mcarry = (uint32_t)__builtin_amdgcn_readlane((int)m, 63);
-    const int own = ((int)m - 1) & 63;
-    const uint32_t ob = __shfl(ebeg, own, 64);
-    st.om[h] = __shfl(emeta, own, 64);
-    const uint32_t ox = __shfl(excl, own, 64);
-    const uint32_t e = (uint32_t)lane + 64u * h;
-    st.act[h] = e < taken;
-    st.x[h] = s.adjx[st.act[h] ? ob + (e - ox) : 0u];  // adjx[0] exists (n_set_edges + 1)
-  }
-#pragma unroll
-  for (int h = 0; h < EPL; h++)
-    st.pb[h] = ld_once(reinterpret_cast<const ulonglong2*>(
-        s.dset + (st.pvalid[h] ? dset_home(dset_key(Gs.pend_node[h], st.psubj[h]), s.dset_nb) : 0ull) * DSET_BUCKET));
-  st.taken = taken;
-  Gs.head += ncons;
-  st_edges += taken;  // wave-uniform (scalar registers); lane 0 reports them
-  st_steps += 1u;
-}
-
-// BACK of a group's step; returns the group's finished slots (bits of the 32-slot mask).
-template <int VLOG2, int QCG, int EPL>
-__device__ __forceinline__ uint32_t s6_back(const DevSnap& s, Stream6Lds<VLOG2, QCG, EPL>& L, int G, uint32_t active,
-                                            S6Group<EPL>& Gs, S6Step<EPL>& st, uint8_t* __restrict__ out,
-                                            RQuery* __restrict__ rq, uint32_t* next_list, uint32_t* next_count,
-                                            uint32_t ecap, uint32_t& st_probes, uint32_t& st_done) {
-  const int lane = lane_id();
-  if (!st.live) return 0u;
-  st.live = false;
-  uint32_t slot[EPL], d[EPL], g[EPL];
-  uint4 ss[EPL];
-#pragma unroll
-  for (int h = 0; h < EPL; h++) {
-    slot[h] = (st.om[h] >> 11) & 31u;
-    d[h] = st.om[h] >> 25;
-    g[h] = (st.om[h] >> 16) & S2_GEN;
-    ss[h] = L.s_ss[slot[h]];
-  }
-  bool hit[EPL];
-#pragma unroll
-  for (int h = 0; h < EPL; h++) {
-    const uint64_t pkey = dset_key(Gs.pend_node[h], st.psubj[h]);
-    hit[h] = st.pvalid[h] & ((st.pb[h].x == pkey) | (st.pb[h].y == pkey));
-    const bool more = st.pvalid[h] & !hit[h] & (st.pb[h].y != EMPTY64);
-    if (__ballot(more)) {
-      if (more) hit[h] = dset_probe(s, Gs.pend_node[h], st.psubj[h]);
-    }
-    st_probes += st.pvalid[h] ? 1u : 0u;
-  }
-  bool keepc[EPL], fresh[EPL];
-  uint32_t xlen[EPL];
-#pragma unroll
-  for (int h = 0; h < EPL; h++) {
-    xlen[h] = adjx_len16(st.x[h]);
-    keepc[h] = st.act[h] && d[h] >= 3 && xlen[h] > 0;
-    const bool longrow = keepc[h] && xlen[h] > S2_LONG;
-    const unsigned long long key =
-        (1ull << 63) | ((unsigned long long)g[h] << 37) | ((unsigned long long)slot[h] << 32) | st.x[h].node;
-    const uint32_t hv = ((st.x[h].node * 0x9E3779B1u) ^ ss[h].z) >> (32 - VLOG2);
-    const unsigned long long old = keepc[h] ? L.vt[hv] : 0ull;
-    fresh[h] = keepc[h] && !longrow && old != key;
-    if (fresh[h]) L.vt[hv] = key;
-    if (longrow) atomicOr(&L.s_state[slot[h]], S2_OVER);
-  }
-  const uint32_t room = QCG - (Gs.tail - Gs.head);
-  uint32_t nfresh = 0;
-  bool appended[EPL];
-#pragma unroll
-  for (int h = 0; h < EPL; h++) {
-    const uint64_t am = __ballot(fresh[h]);
-    const uint32_t pos = nfresh + (uint32_t)__popcll(am & ((1ull << lane) - 1));
-    nfresh += (uint32_t)__popcll(am);
-    appended[h] = fresh[h] && pos < room;
-    if (appended[h]) {
-      const uint32_t at = Gs.tail + pos;
-      L.e_beg[G][at & (QCG - 1)] = st.x[h].begin;
-      L.e_meta[G][at & (QCG - 1)] = xlen[h] | (st.om[h] & 0x01FFF800u) | ((d[h] - 1) << 25);
-      atomicMax(&L.s_last[slot[h]], at);
-      atomicAdd(&L.s_edg[slot[h]], xlen[h]);
-    }
-    if (fresh[h] && !appended[h]) atomicOr(&L.s_state[slot[h]], S2_OVER);
-  }
-  Gs.tail += min(nfresh, room);
-  uint32_t pmask = 0;
-#pragma unroll
-  for (int h = 0; h < EPL; h++) {
-    if (hit[h]) atomicOr(&L.s_state[s6_slot(Gs.pend_sg[h])], S2_HIT);
-    const bool pend = st.act[h] && (keepc[h] ? appended[h] : true) &&
-                      sig_maybe(st.x[h].lsig, st.x[h].sig, make_uint2(ss[h].x, ss[h].y));
-    Gs.pend_node[h] = st.x[h].node;
-    Gs.pend_sg[h] = (pend ? S6_PEND : 0u) | (g[h] << 5) | slot[h];
-    pmask |= pend ? 1u << slot[h] : 0u;
-  }
-  const uint32_t pslots = wave_or(pmask);
-  __builtin_amdgcn_wave_barrier();
-  // finished queries of this group (slots 16 G .. 16 G + 15, on lanes 0..15)
-  bool done = false;
-  const uint32_t sl = 16u * G + (uint32_t)lane;
-  if (lane < 16 && ((active >> sl) & 1u)) {
-    const uint32_t stt = L.s_state[sl];
-    const uint32_t last = L.s_last[sl], edg = L.s_edg[sl];
-    const uint32_t qi = L.s_qi[sl];
-    if (stt & S2_HIT) {
-      done = true;
-      out[qi] = KG_IS_MEMBER;  // NotMember was pre-written by k_resolve
-      st_done++;
-    } else if ((stt & S2_OVER) || (ecap != 0xFFFFFFFFu && edg > ecap)) {
-      done = true;
-      rq[qi] = RQuery{L.s_node[sl], L.s_subj[sl], (int32_t)L.s_depth[sl], ROUTE_LIGHT, L.s_beg[sl], L.s_len[sl]};
-      next_list[atomicAdd(next_count, 1u)] = qi;
-    } else if ((int32_t)(last - Gs.head) < 0 && !((pslots >> sl) & 1u)) {
-      done = true;  // every entry consumed, no probe pending: NotMember (pre-written)
-      st_done++;
-    }
-    if (done) L.s_state[sl] = ((stt & S2_GEN) + 1u) & S2_GEN;
-  }
-  const uint32_t freed = ((uint32_t)__ballot(done) & 0xFFFFu) << (16 * G);
-#pragma unroll
-  for (int h = 0; h < EPL; h++)
-    if ((freed >> s6_slot(Gs.pend_sg[h])) & 1u) Gs.pend_sg[h] &= ~S6_PEND;
-  __builtin_amdgcn_wave_barrier();
-  return freed;
-}
-
-template <int VLOG2, int QCG, int EPL>
-__global__ __launch_bounds__(256, 4) void k_stream6(DevSnap s, LqList wl, uint32_t* heads, uint8_t* __restrict__ out,
-                                                 RQuery* __restrict__ rq, uint32_t* next_list, uint32_t* next_count,
-                                                 Ctl* ctl, uint32_t ecap, uint32_t chunk, uint32_t ranges) {
-  using Lds = Stream6Lds<VLOG2, QCG, EPL>;
-  static_assert(EPL == 1 || EPL == 2, "one or two edges per lane and step");
-  constexpr uint32_t WIN = 64u * EPL;
-  constexpr uint32_t VT = 1u << VLOG2;
-  static_assert(QCG <= 256 && (QCG & (QCG - 1)) == 0, "FIFO rings of <= 256 entries (9-bit generations stay unique)");
-  const uint64_t t_start = wall_clock64();
-  __shared__ Lds lds_all[4];
-  Lds& L = lds_all[threadIdx.x >> 6];
-  const int lane = lane_id();
-  const uint32_t head0 = blockIdx.x & 7;
-  uint32_t head_sel = head0;
-  for (uint32_t i = lane; i < VT; i += 64) L.vt[i] = 0ull;
-  if (lane < 32) {
-    L.s_state[lane] = 0;
-    L.s_last[lane] = 0;
-    L.s_edg[lane] = 0;
-  }
-  if (lane < 2) L.pref[lane][WIN] = 0;
-  const uint32_t shard_n = lane < 8 ? wl.counts[lane * 32] : 0u;
-  __builtin_amdgcn_wave_barrier();
-  uint32_t active = 0;
-  uint32_t pf = 0, tk = 0, st_got = 0;
-  bool exhausted = false;
-  LQuery sq{};
-  uint32_t c_left = 0, c_pos = 0;
-  LQuery cq{};
-  S6Group<EPL> Gs[2];
-  S6Step<EPL> St[2];
-#pragma unroll
-  for (int G = 0; G < 2; G++) {
-    Gs[G].head = Gs[G].tail = Gs[G].head_off = 0;
-#pragma unroll
-    for (int h = 0; h < EPL; h++) Gs[G].pend_node[h] = Gs[G].pend_sg[h] = 0;
-    St[G].live = false;
-  }
-  uint32_t st_rows = 0, st_edges = 0, st_probes = 0, st_done = 0, st_steps = 0;
-  // refill the free slots of group G from the current chunk (their root entries need FIFO room)
-  auto refill = [&](int G) {
-    if (c_left == 0 && pf == 2) {
-      cq = sq;
-      c_left = st_got;
-      c_pos = 0;
-      pf = 0;
-    }
-    const uint32_t freem = ~active & (0xFFFFu << (16 * G));
-    const uint32_t want = __popc(freem);
-    const uint32_t got = min(want, c_left);
-    S6Group<EPL>& g = Gs[G];
-    if (got && (g.tail - g.head) + got <= QCG) {
-      const uint32_t r = __popc(freem & (lane < 32 ? (1u << lane) - 1u : 0xFFFFFFFFu));
-      const bool mine = lane < 32 && ((freem >> (lane & 31)) & 1u) && r < got;
-      const int src = mine ? (int)(c_pos + r) : lane;
-      const uint32_t qi = __shfl(cq.qi, src, 64), qnode = __shfl(cq.node, src, 64), qsubj = __shfl(cq.subj, src, 64),
-                     qbeg = __shfl(cq.beg, src, 64), qlen = __shfl(cq.len, src, 64);
-      const int32_t qdepth = __shfl(cq.depth, src, 64);
-      c_pos += got;
-      c_left -= got;
-      if (mine) {
-        const uint32_t slot = lane, gen = L.s_state[slot] & S2_GEN;
-        const bool over = qdepth > (int32_t)S2_DMAX || qlen > S2_LONG || qlen > ecap;
-        const uint32_t at = g.tail + r;
-        const uint32_t salt = (slot * 0x85EBCA77u) ^ (gen * 0xC2B2AE3Du);
-        L.s_qi[slot] = qi;
-        L.s_subj[slot] = qsubj;
-        const uint2 qm = subj_sig(qsubj);
-        L.s_ss[slot] = make_uint4(qm.x, qm.y, salt, 0u);
-        L.s_node[slot] = qnode;
-        L.s_depth[slot] = (uint32_t)qdepth;
-        L.s_beg[slot] = qbeg;
-        L.s_len[slot] = qlen;
-        L.s_edg[slot] = qlen;
-        L.s_last[slot] = at;
-        L.s_state[slot] = over ? (gen | S2_OVER) : gen;
-        const unsigned long long key =
-            (1ull << 63) | ((unsigned long long)gen << 37) | ((unsigned long long)slot << 32) | qnode;
-        L.vt[((qnode * 0x9E3779B1u) ^ salt) >> (32 - VLOG2)] = key;
-        L.e_beg[G][at & (QCG - 1)] = qbeg;
-        L.e_meta[G][at & (QCG - 1)] = s2_meta(over ? 0u : qlen, slot, gen, over ? 2u : (uint32_t)qdepth);
-      }
-      active |= (uint32_t)__ballot(mine);
-      g.tail += got;
-    }
-  };
-  auto dequeue = [&]() {
-    if (pf == 1) {
-      const uint32_t k = (uint32_t)__builtin_amdgcn_readfirstlane((int)tk);
-      const uint32_t h = head_sel & 7;
-      const uint32_t lo = h * wl.cap, hi = lo + (uint32_t)__builtin_amdgcn_readlane((int)shard_n, (int)h);
-      if (lo + k < hi) {
-        st_got = min(chunk, hi - (lo + k));
-        if ((uint32_t)lane < st_got) sq = wl.list[lo + k + (uint32_t)lane];
-        pf = 2;
-      } else {
-        pf = 0;
-        if (++head_sel >= head0 + ranges) exhausted = true;
-      }
-    }
-    if (pf == 0 && !exhausted) {
-      if (lane == 0) tk = atomicAdd(&heads[(head_sel & 7) * 32], chunk);
-      pf = 1;
-    }
-  };
-  for (;;) {
-    refill(0);
-    dequeue();
-    __builtin_amdgcn_wave_barrier();
-    s6_front<VLOG2, QCG, EPL>(s, L, 0, active, Gs[0], St[0], st_rows, st_edges, st_steps);
-    active &= ~s6_back<VLOG2, QCG, EPL>(s, L, 1, active, Gs[1], St[1], out, rq, next_list, next_count, ecap, st_probes,
-                                        st_done);
-    refill(1);
-    __builtin_amdgcn_wave_barrier();
-    s6_front<VLOG2, QCG, EPL>(s, L, 1, active, Gs[1], St[1], st_rows, st_edges, st_steps);
-    active &= ~s6_back<VLOG2, QCG, EPL>(s, L, 0, active, Gs[0], St[0], out, rq, next_list, next_count, ecap, st_probes,
-                                        st_done);
-    if (active == 0 && !St[1].live && exhausted && pf == 0 && c_left == 0) break;
-  }
-  const unsigned long long t_end = wall_clock64(), life = lane == 0 ? t_end - t_start : 0ull;
-  block_max3(ctl, ~(unsigned long long)t_start, t_end, t_end - t_start);
-  const int idx[7] = {ST_LROWS, ST_LEDGES, ST_LPROBES, ST_LIGHT, ST_LSTEPS, ST_LWAVES, ST_LTICKS};
-  const unsigned long long v[7] = {st_rows, lane == 0 ? st_edges : 0u, st_probes, st_done, lane == 0 ? st_steps : 0u,
-                                   lane == 0 ? 1ull : 0ull, life};
   block_stats<7>(ctl, idx, v);
 }
 
@@ -1421,14 +1065,8 @@ int check_batch_begin(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n, 
       // starting at its label blockIdx & 7, so every label must occur for every range to be drained
       const uint32_t grid =
           std::max<uint32_t>(8u, (uint32_t)std::min<uint64_t>((uint64_t)s->n_cu * per_cu, (n + 31) / 32 + 8));
-#if KG_STREAM_DUAL
-      hipLaunchKernelGGL((k_stream6<9, 128, KG_STREAM_EPL>), dim3(grid), dim3(256), 0, stream, s->ds,
-                         LqList{lq, ctl->light8, lq_cap}, ctl->heads, d_out, rq, heavy, &ctl->heavy_count, ctl, ecap,
-                         S4_CHUNK, s->stream_steal);
-#else
       hipLaunchKernelGGL((k_stream4<9, 256, KG_STREAM_EPL>), dim3(grid), dim3(256), 0, stream, s->ds, LqList{lq, ctl->light8, lq_cap},
                          ctl->heads, d_out, rq, heavy, &ctl->heavy_count, ctl, ecap, S4_CHUNK, s->stream_steal);
-#endif
     }
     HIPC(hipGetLastError());
     if (stats) HIPC(hipEventRecord(l1, stream));
