@@ -132,7 +132,10 @@ def parse(argv=None):
     ap.add_argument("--hw-queues", type=int, default=None,
                     help="HIP hardware queues for this process (GPU_MAX_HW_QUEUES, 1..32; 0 = HIP's default, 4; "
                          "default 16): streams map onto queues round-robin as they are created, and in-flight "
-                         "streams that share a queue serialise (DESIGN.md 7f)")
+                         "streams that share a queue serialise (DESIGN.md 7f).  32 helps C5's 12 callers (1.87 -> "
+                         "2.99 x 10^7 trees/s) but cost C3 (1.83 -> 1.00 x 10^9) and the sharded lines in the same "
+                         "process (profiles/r6o_c5_hw_queues.txt, r6q_hw_queues_default_line_ab.jsonl), so the C5 "
+                         "sub-line runs as a child process at 32")
     ap.add_argument("--inflight", type=int, default=None,
                     help="batches in flight per GPU: one HIP stream (own workspace) and one host thread each "
                          "(default 4; 16 for --mode expand, whose batches end in long sequential roots; 2 with "
@@ -152,9 +155,6 @@ def parse(argv=None):
     ap.add_argument("--host-calls", type=int, default=20,
                     help="kg_check_batch calls per in-flight thread in the host-path leg (1 M-check host batches, "
                          "PCIe both ways; 0 = skip)")
-    ap.add_argument("--stagger-us", type=float, default=0.0,
-                    help="diagnostics: in-flight caller p starts its first batch p * this many us after the others "
-                         "(timed region included), so the callers' tail tiers do not run in lockstep")
     ap.add_argument("--stats-every", type=int, default=10,
                     help="collect kernel stats (HIP events around the batch and k_stream4, the in-kernel counters) on "
                          "every k-th timed batch (1 = all).  Default 10: two of the driver's 20 steps -- the event "
@@ -287,7 +287,8 @@ def bench_expand(a):
             n_big = int(buf.n_nodes)
             L.kg_tree_free(C.byref(buf))
         out["largest_root"] = {"records": n_big, "walk_kernel_ms": float(min(walk))}
-    rf = expand_roofline(L, snap, roots, depth, kms / a.steps)
+    # traffic: PMC bytes of every k_expand* dispatch per call (scripts/gpu_r6_final.sh, same roots and callers)
+    rf = expand_roofline(L, snap, roots, depth, kms / a.steps, pmc_traffic("k_expand", int(a.tuples), a.roots, 0, P, "x"))
     if rf:
         out["roofline"] = rf
     orc = None
@@ -1071,10 +1072,6 @@ def main():
         def worker(p):
             try:
                 go.wait()
-                if a.stagger_us > 0:  # caller p arrives p * stagger later (spin: sleep() is too coarse)
-                    t_go = time.perf_counter() + p * a.stagger_us * 1e-6
-                    while time.perf_counter() < t_go:
-                        pass
                 for k in range(p, K, P):
                     s0 = time.perf_counter()
                     step(p, k0 + k, stats[k] if stats is not None else None)  # stats => waits for its batch
@@ -1272,7 +1269,7 @@ def main():
                    for x in subs if isinstance(x.get("parity"), dict) and "mismatches" in x["parity"])
 
     if world == 1 and a.preset == 0 and not a.heavy_tail and a.expand_steps > 0:
-        bad = sub_line("expand", lambda: expand_leg(a, snap, orc)) or bad
+        bad = sub_line("expand", lambda: expand_leg(a)) or bad
     if world == 1 and a.preset == 0 and not a.heavy_tail and a.c3_steps > 0:
         bad = sub_line("c3", lambda: c3_leg(a, local)) or bad
     if world == 1 and a.preset == 0 and not a.heavy_tail and a.heavy_steps > 0:
@@ -1290,51 +1287,36 @@ def main():
         dist.destroy_process_group()
 
 
-def expand_leg(a, snap, orc) -> dict:
-    """Config C5 (BASELINE.json configs[4]) beside the headline, on the headline's own graph: BuildTree of
-    the --roots most popular group#member sets at the global max_read_depth 5, one
-    kg_expand_batch call per step (trees to host memory), --expand-inflight calls in flight; roofline of
-    the expand chain and parity against the oracle's BuildTree (the 10 largest roots + a sample).  The
-    full C5 bench (16 calls in flight over 16 HIP hardware queues, CPU baseline) is --mode expand."""
-    from keto_amd import _lib
-    from keto_amd.synth import hot_group_roots
-    L = _lib.load()
-    roots = hot_group_roots(snap.synth_ids(), a.roots)
-    depth = 5
-    snap.tune("expand_gw", a.expand_gw)
-    P, K = max(1, a.expand_inflight), a.expand_steps
-    # the value: roots resident in HBM, trees left in HBM (kg_expand_batch_device, one HIP stream per caller)
-    el, results = expand_steps(L, snap, roots, depth, P, K, P, device=True)
-    nodes = sum(r[0] for r in results)
-    kms = sum(r[1] for r in results)
-    # the same calls through the host-buffer boundary (kg_expand_batch: roots over PCIe, trees back into pinned
-    # host memory) -- the PCIe-inclusive rate, reported beside the value
-    el_h, res_h = expand_steps(L, snap, roots, depth, P, K, P)
-    off = res_h[-1][2]
-    res = {"metric": "expand trees/sec (C5: batched BuildTree, hot group#member roots)",
-           "value": len(roots) * K / el, "unit": "trees/s", "steps": K, "inflight": P, "ms_per_step": el / K * 1e3,
-           "tree_nodes_per_s": nodes / el, "kernel_ms_per_call": kms / K,
-           "io": "kg_expand_batch_device: roots and trees in HBM",
-           "host_path": {"value": len(roots) * K / el_h, "unit": "trees/s", "ms_per_step": el_h / K * 1e3,
-                         "tree_bytes_per_call": int(res_h[-1][0]) * 20,
-                         "what": "kg_expand_batch (roots from / trees to pinned host memory, PCIe both ways): "
-                                 "not the value"},
-           "config": {"workload": "C5: %d hot roots of the headline graph, max_read_depth %d" % (len(roots), depth)}}
-    # traffic: PMC bytes of every k_expand* dispatch per call (scripts/gpu_r6_prof.sh, same roots and calls in flight)
-    rf = expand_roofline(L, snap, roots, depth, kms / K, pmc_traffic("k_expand", int(a.tuples), len(roots), 0, P, "x"))
-    if rf:
-        res["roofline"] = rf
-    if orc is not None and a.parity_roots > 0 and off is not None:
-        o = orc.o
-        o.nd = orc.nd
-        res["parity"] = expand_parity(snap, roots, np.diff(off.astype(np.int64)), depth, a, o)
-    if orc is not None and a.cpu_seconds > 0:  # a bounded sample: a third of the headline's CPU budget
-        import copy
-        ac = copy.copy(a)
-        ac.cpu_seconds = a.cpu_seconds / 3
-        o = orc.o
-        o.nd = orc.nd
-        res["cpu_baseline"] = expand_cpu_baseline(o, roots, depth, ac)
+def expand_leg(a) -> dict:
+    """Config C5 (BASELINE.json configs[4]) beside the headline: BuildTree of the --roots most popular
+    group#member sets of the headline's generator graph at the global max_read_depth 5, as a
+    child `bench.py --mode expand` run on the same GPU (the parent idles): --expand-inflight callers, each on
+    a HIP stream of its own through kg_expand_batch_device (roots and trees in HBM), --expand-steps calls in
+    the timed region, 32 hardware queues (the parent keeps 16, which C3 and the sharded lines need); the
+    host-buffer call (PCIe both ways) is reported beside it; roofline of the expand chain, parity against
+    the oracle's BuildTree (the 10 largest roots + a sample) and a CPU baseline."""
+    import subprocess
+    P = max(1, a.expand_inflight)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--mode", "expand", "--inflight", str(P),
+           "--steps", str(a.expand_steps), "--warmup", str(P), "--cpu-seconds", str(a.cpu_seconds / 3),
+           "--parity-roots", str(a.parity_roots), "--roots", str(a.roots), "--hw-queues", "32",
+           "--tuples", str(a.tuples), "--seed", str(a.seed), "--expand-gw", str(a.expand_gw)]
+    env = dict(os.environ)
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK"):
+        env.pop(k, None)
+    t0 = time.time()
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, env=env, timeout=max(60.0, a.sharded_timeout - 20))
+    lines = [x for x in r.stdout.decode(errors="replace").splitlines() if x.startswith("{")]
+    if not lines:
+        raise RuntimeError("expand run printed no line (rc %d): %s" % (r.returncode, r.stderr.decode(errors="replace")[-600:]))
+    d = json.loads(lines[-1])
+    keep = ("metric", "value", "unit", "steps", "warmup", "ms_per_step", "config", "io", "host_path", "tree_nodes_per_s",
+            "tree_nodes_per_step", "kernel_ms_per_step", "records_per_root", "largest_root", "roofline", "parity",
+            "cpu_baseline")
+    res = {k: d[k] for k in keep if k in d}
+    res["metric"] = "expand trees/sec (C5: batched BuildTree, hot group#member roots)"
+    res["inflight"] = P
+    res["child"] = {"cmd": " ".join(cmd[1:]), "rc": r.returncode, "seconds": time.time() - t0}
     return res
 
 

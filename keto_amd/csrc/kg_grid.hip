@@ -32,7 +32,12 @@
 
 namespace kg {
 
-constexpr uint32_t GT = 512;                 // edges per tile: two per thread of the 256-thread workgroup
+// edges per thread of k_grid_level's 256-thread workgroup (-DKG_GRID_EPT=4 builds 1024-edge tiles for A/Bs)
+#ifndef KG_GRID_EPT
+#define KG_GRID_EPT 2
+#endif
+constexpr int GEPT = KG_GRID_EPT;
+constexpr uint32_t GT = 256u * GEPT;          // edges per tile
 constexpr uint64_t TILE_CAP = 1ull << 24;    // tiles per level with a tile_first entry (beyond: log search)
 constexpr int EDGE_BITS = 36;                // packed level counter: entries (28 bits) | edges (36 bits)
 constexpr uint64_t EDGE_MASK = (1ull << EDGE_BITS) - 1;
@@ -372,12 +377,14 @@ __global__ __launch_bounds__(256) void k_grid_level(DevSnap s, GridLog lg, int l
       }
     __syncthreads();
     // both edges' entry (LDS), then their slots' answered flags and adjx records in flight at once
-    bool inr[2];
-    uint32_t slot[2] = {0u, 0u}, subj[2] = {0u, 0u}, hv[2];
-    int D[2] = {0, 0};
-    AdjX x[2];
+    bool inr[GEPT];
+    uint32_t slot[GEPT], subj[GEPT], hv[GEPT];
+    int D[GEPT];
+    AdjX x[GEPT];
 #pragma unroll
-    for (int h = 0; h < 2; h++) {
+    for (int h = 0; h < GEPT; h++) {
+      slot[h] = subj[h] = 0u;
+      D[h] = 0;
       const uint64_t e = t0 + threadIdx.x + (uint64_t)h * 256;
       uint64_t beg = 0;
       uint32_t rb = 0;
@@ -408,12 +415,12 @@ __global__ __launch_bounds__(256) void k_grid_level(DevSnap s, GridLog lg, int l
       hv[h] = inr[h] ? sl.hit[slot[h]] : 1u;  // plain load: a stale 0 only costs this level's work
       x[h] = s.adjx[inr[h] ? rb + (uint32_t)(e - beg) : 0u];
     }
-    bool act[2], keep[2], sigok[2];
-    uint32_t clen[2], cb[2];
-    uint64_t pk[2];
-    ulonglong2 pb[2];
+    bool act[GEPT], keep[GEPT], sigok[GEPT];
+    uint32_t clen[GEPT], cb[GEPT];
+    uint64_t pk[GEPT];
+    ulonglong2 pb[GEPT];
 #pragma unroll
-    for (int h = 0; h < 2; h++) {
+    for (int h = 0; h < GEPT; h++) {
       act[h] = inr[h] && hv[h] == 0;  // answered at tile start (or no edge): nothing more for this edge
       cb[h] = x[h].begin;
       clen[h] = act[h] ? adjx_len(s, x[h]) : 0u;
@@ -426,12 +433,14 @@ __global__ __launch_bounds__(256) void k_grid_level(DevSnap s, GridLog lg, int l
       pb[h] = ld_once(
           reinterpret_cast<const ulonglong2*>(s.dset + (sigok[h] ? dset_home(pk[h], s.dset_nb) : 0ull) * DSET_BUCKET));
     }
-    int ins[2];
-    gh_insert2(H, mask, keep[0], gh_key(epoch, slot[0], x[0].node), keep[1], gh_key(epoch, slot[1], x[1].node), ins[0],
-               ins[1]);
-    bool app[2];
+    int ins[GEPT];
 #pragma unroll
-    for (int h = 0; h < 2; h++) {
+    for (int h = 0; h < GEPT; h += 2)
+      gh_insert2(H, mask, keep[h], gh_key(epoch, slot[h], x[h].node), keep[h + 1], gh_key(epoch, slot[h + 1], x[h + 1].node),
+                 ins[h], ins[h + 1]);
+    bool app[GEPT];
+#pragma unroll
+    for (int h = 0; h < GEPT; h++) {
       if (keep[h] && ins[h] < 0) ctl->overflow = 1;
       const bool fresh = act[h] && (!keep[h] || ins[h] > 0);
       if (fresh && sigok[h]) {
@@ -442,10 +451,10 @@ __global__ __launch_bounds__(256) void k_grid_level(DevSnap s, GridLog lg, int l
       }
       app[h] = fresh && keep[h];
     }
-    grid_push(ctl, lvs, lg, nl, (level + 1) & 1, next_base, B, app[0], slot[0], cb[0], clen[0],
-              make_uint2(subj[0], (uint32_t)D[0]));
-    grid_push(ctl, lvs, lg, nl, (level + 1) & 1, next_base, B, app[1], slot[1], cb[1], clen[1],
-              make_uint2(subj[1], (uint32_t)D[1]));
+#pragma unroll
+    for (int h = 0; h < GEPT; h++)
+      grid_push(ctl, lvs, lg, nl, (level + 1) & 1, next_base, B, app[h], slot[h], cb[h], clen[h],
+                make_uint2(subj[h], (uint32_t)D[h]));
   }
   if (B.n) grid_flush(ctl, lvs, lg, nl, (level + 1) & 1, next_base, B);
   for (int off = 32; off; off >>= 1) probes += __shfl_xor(probes, off, 64);
