@@ -64,13 +64,14 @@ def parse(argv=None):
                     help="checks per sharded batch per rank (0: --batch).  C4 names 1-8 M; across ranks one batch "
                          "is in flight per rank, and 4 M amortises the exchanges' fixed cost: one-rank exchange "
                          "protocol 0.80 / 1.19 / 1.29 x 10^9 checks/s at 1 / 4 / 8 M (DESIGN.md 7f)")
-    ap.add_argument("--expand-steps", type=int, default=24,
+    ap.add_argument("--expand-steps", type=int, default=32,
                     help="check mode, one rank: timed calls of the C5 expand sub-line over the headline graph (0 = off; "
                          "at least twice --expand-inflight, so every caller thread makes two calls)")
-    ap.add_argument("--expand-inflight", type=int, default=12,
+    ap.add_argument("--expand-inflight", type=int, default=16,
                     help="check mode: kg_expand_batch_device calls in flight in the C5 sub-line (one HIP stream each; "
                          "a call's critical path is its largest root's walk on one workgroup, so calls overlap: "
-                         "8 / 12 / 16 gave 2.18 / 2.62 / 2.24 x 10^7 trees/s, profiles/r6m_c5_inflight.txt)")
+                         "12 / 16 / 20 gave 2.80 / 3.34 / 3.74 x 10^7 trees/s at 32 hardware queues, "
+                         "profiles/r6t_operating_points.txt)")
     ap.add_argument("--c3-steps", type=int, default=20,
                     help="check mode, one rank: timed batches of the C3 sub-line (OPL rewrites; 0 = off)")
     ap.add_argument("--c3-tuples", type=float, default=1e7, help="C3 sub-line graph size (BASELINE configs[2]: 10M)")
@@ -78,7 +79,7 @@ def parse(argv=None):
     ap.add_argument("--c3-parity", type=int, default=200_000)
     ap.add_argument("--heavy-steps", type=int, default=20,
                     help="check mode, one rank: timed batches of the heavy-tail sub-line (SURVEY.md 8d's out-degree "
-                         "law P(k) ~ k^-1.5 at 1.2e8 tuples, 62.5 k checks per batch, 2 in flight; a child "
+                         "law P(k) ~ k^-1.5 at 1.2e8 tuples, 62.5 k checks per batch, 4 in flight; a child "
                          "`bench.py --heavy-tail` run; 0 = off)")
     ap.add_argument("--heavy-parity", type=int, default=62_500, help="heavy-tail sub-line: checks compared with the oracle")
     ap.add_argument("--sharded-inflight", type=int, default=0,
@@ -193,7 +194,9 @@ def parse(argv=None):
     if a.batch is None:
         a.batch = 62_500 if a.heavy_tail else 1_000_000
     if a.inflight is None:
-        a.inflight = 16 if a.mode == "expand" else (2 if a.heavy_tail else 4)
+        # --heavy-tail: 4 (round 6: 2 / 3 / 4 / 6 in flight gave 6.2 / 9.1 / 12.0 / 10.3 x 10^6 checks/s at p99
+        # 21.4 / 21.5 / 22.4 / 40.6 ms per 62.5 k-check batch, profiles/r6t_operating_points.txt)
+        a.inflight = 16 if a.mode == "expand" else 4
     if a.back_wgs is None:
         a.back_wgs = 1 if a.preset else 3
     if a.grid_wgs is None:
@@ -1322,7 +1325,7 @@ def expand_leg(a) -> dict:
 
 def heavy_leg(a) -> dict:
     """SURVEY.md 8d's literal degree law beside the headline: the heavy-tail point
-    (out-degrees P(k) ~ k^-1.5, 1.2e8 tuples, 62.5 k checks per batch, 2 in flight -- its p99 point,
+    (out-degrees P(k) ~ k^-1.5, 1.2e8 tuples, 62.5 k checks per batch, 4 in flight -- its p99 point,
     DESIGN.md 7f) as a child `bench.py --heavy-tail` run on the same GPU (the parent idles meanwhile), with
     its own timed region, latency phase, parity against the oracle, CPU baseline and the roofline of its
     dominant kernel (k_ms_level, HIP events per launch)."""
