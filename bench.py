@@ -254,7 +254,10 @@ def bench_expand(a):
     # the value: roots and trees resident in HBM (kg_expand_batch_device); then the host-buffer boundary
     el, results = expand_steps(L, snap, roots, depth, P, a.steps, a.warmup, dist, device=True)
     el, _ = aggregate(dist, el, 0.0, f"cuda:{local}" if a.backend == "nccl" else None)
-    el_h, res_h = expand_steps(L, snap, roots, depth, P, a.steps, a.warmup, dist)
+    # host-buffer leg at <= 4 callers: every library lane holds ~3 GB of expand buffers, and 16 device lanes + 16
+    # host lanes beside the parent's and this child's 1e9-tuple graphs ran out of HBM (r6z closing run)
+    P_h = min(P, 4)
+    el_h, res_h = expand_steps(L, snap, roots, depth, P_h, a.steps, a.warmup, dist)
     el_h, _ = aggregate(dist, el_h, 0.0, f"cuda:{local}" if a.backend == "nccl" else None)
     nodes = sum(r[0] for r in results)
     kms = sum(r[1] for r in results)
@@ -269,7 +272,7 @@ def bench_expand(a):
                       "expand_gw": a.expand_gw},
            "tree_nodes_per_step": nodes / a.steps, "tree_nodes_per_s": nodes / el,
            "kernel_ms_per_step": kms / a.steps, "io": "kg_expand_batch_device: roots and trees in HBM",
-           "host_path": {"value": world * a.roots * a.steps / el_h, "unit": "trees/s", "ms_per_step": el_h / a.steps * 1e3,
+           "host_path": {"value": world * a.roots * a.steps / el_h, "unit": "trees/s", "ms_per_step": el_h / a.steps * 1e3, "inflight": P_h,
                          "what": "kg_expand_batch (roots from / trees to pinned host memory, PCIe both ways): "
                                  "not the value"}}
     if off is not None:
