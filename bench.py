@@ -35,7 +35,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 # independent random 16-B loads/s from HBM-sized tables (16-160 GiB) on one MI355X: tools/randprobe.hip,
 # profiles/r2_randprobe_sizes.jsonl (~37 G/s; the line, not the byte, is the unit of a random gather)
 RAND_REQ_PEAK = 37.0e9
-STREAM_KERNEL = "k_stream4<9,256,2>"
+STREAM_KERNEL = "k_stream4<8,256,2>"
 
 
 def parse(argv=None):

@@ -338,6 +338,17 @@ constexpr uint32_t S4_CHUNK = 64;
 #ifndef KG_STREAM_EPL
 #define KG_STREAM_EPL 2
 #endif
+// Visited-cache keys per wave (log2) and FIFO entries per wave.  256 keys (round 6; 512 before): 25.5 KB of
+// LDS per workgroup instead of 33.7 KB, so 5 workgroups per CU fit (the VGPR limit, 95 VGPRs) instead of 4 --
+// the same work per batch (rows, edges, probes and tiers unchanged) in a 13 % shorter launch; a 128-entry
+// FIFO instead measured slower (more queries handed on), profiles/r6z4_stream_lds_ab.jsonl.  -D overrides
+// build A/B variants.
+#ifndef KG_STREAM_VLOG2
+#define KG_STREAM_VLOG2 8
+#endif
+#ifndef KG_STREAM_QC
+#define KG_STREAM_QC 256
+#endif
 
 template <int VLOG2, int QC, int EPL>
 struct Stream4Lds {
@@ -1057,7 +1068,7 @@ int check_batch_begin(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n, 
     HIPC(hipGetLastError());
     if (stats) HIPC(hipEventRecord(l0, stream));
     {
-      // ~32 KiB of LDS per workgroup (4 waves: a 512-key visited cache and a 256-entry FIFO each);
+      // ~25 KiB of LDS per workgroup (4 waves: a 256-key visited cache and a 256-entry FIFO each);
       // stream_wgs per CU (default 2: the rest of the LDS serves the other batches in flight)
       const uint32_t per_cu = s->stream_wgs ? (uint32_t)s->stream_wgs : 2u;
       const uint32_t ecap = s->stream_ecap ? s->stream_ecap : 0xFFFFFFFFu;
@@ -1065,7 +1076,7 @@ int check_batch_begin(Snapshot* s, Workspace* w, const kg_query* d_q, size_t n, 
       // starting at its label blockIdx & 7, so every label must occur for every range to be drained
       const uint32_t grid =
           std::max<uint32_t>(8u, (uint32_t)std::min<uint64_t>((uint64_t)s->n_cu * per_cu, (n + 31) / 32 + 8));
-      hipLaunchKernelGGL((k_stream4<9, 256, KG_STREAM_EPL>), dim3(grid), dim3(256), 0, stream, s->ds, LqList{lq, ctl->light8, lq_cap},
+      hipLaunchKernelGGL((k_stream4<KG_STREAM_VLOG2, KG_STREAM_QC, KG_STREAM_EPL>), dim3(grid), dim3(256), 0, stream, s->ds, LqList{lq, ctl->light8, lq_cap},
                          ctl->heads, d_out, rq, heavy, &ctl->heavy_count, ctl, ecap, S4_CHUNK, s->stream_steal);
     }
     HIPC(hipGetLastError());

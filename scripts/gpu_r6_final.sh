@@ -1,10 +1,10 @@
 # Round-6 closing evidence at the final code: rocprofv3 kernel stats + timelines and PMC HBM traffic
 # (FETCH_SIZE / WRITE_SIZE, one pass each, summarised by scripts/pmc_summary.py into profiles/pmc_*.json,
 # which bench.py reads for roofline.traffic) of the headline (C2/C4), C3, the heavy-tail point and C5.
-# usage: gpurun -- 'TAG=r6z SK=k_stream6 bash scripts/gpu_r6_final.sh'   env: PARTS (default all), SK (stream kernel)
+# usage: gpurun -- 'TAG=r6z SK=k_stream4 bash scripts/gpu_r6_final.sh'   env: PARTS (default all), SK (stream kernel)
 set -u
 TAG=${TAG:-r6z}
-SK=${SK:-k_stream6}
+SK=${SK:-k_stream4}
 PARTS=${PARTS:-"c2 c3 heavy expand"}
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
