@@ -46,10 +46,10 @@ for P in $PARTS; do
     echo "heavy done"
     ;;
   expand)
-    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG}_expand -o run --output-format csv -- python3 bench.py --mode expand --inflight 16 --steps 32 --warmup 16 --cpu-seconds 0 --parity-roots 0 --hw-queues 32 > gpurun_out/prof_${TAG}_expand.log 2>&1 || { echo "expand trace failed"; exit 1; }
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG}_expand -o run --output-format csv -- python3 bench.py --mode expand --inflight 20 --steps 40 --warmup 20 --cpu-seconds 0 --parity-roots 0 --hw-queues 32 > gpurun_out/prof_${TAG}_expand.log 2>&1 || { echo "expand trace failed"; exit 1; }
     python3 scripts/busy.py gpurun_out/prof_${TAG}_expand/run_kernel_trace.csv "k_expand" > gpurun_out/busy_${TAG}_expand.txt || true
-    pmc expand "k_expand" --mode expand --inflight 16 --steps 16 --warmup 16 --cpu-seconds 0 --parity-roots 0 --hw-queues 32 || exit 1
-    python3 scripts/pmc_summary.py --kernel k_expand --anchor k_expand_lds --fetch gpurun_out/pmc_${TAG}_expand_fetch --write gpurun_out/pmc_${TAG}_expand_write --tuples 1e9 --batch 100000 --preset 0 --inflight 16 --out gpurun_out/pmc_k_expand_p0x.json > /dev/null || true
+    pmc expand "k_expand" --mode expand --inflight 20 --steps 20 --warmup 20 --cpu-seconds 0 --parity-roots 0 --hw-queues 32 || exit 1
+    python3 scripts/pmc_summary.py --kernel k_expand --anchor k_expand_lds --fetch gpurun_out/pmc_${TAG}_expand_fetch --write gpurun_out/pmc_${TAG}_expand_write --tuples 1e9 --batch 100000 --preset 0 --inflight 20 --out gpurun_out/pmc_k_expand_p0x.json > /dev/null || true
     echo "expand done"
     ;;
   esac
