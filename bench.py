@@ -76,9 +76,10 @@ def parse(argv=None):
     ap.add_argument("--c3-steps", type=int, default=20,
                     help="check mode, one rank: timed batches of the C3 sub-line (OPL rewrites; 0 = off)")
     ap.add_argument("--c3-tuples", type=float, default=1e7, help="C3 sub-line graph size (BASELINE configs[2]: 10M)")
-    ap.add_argument("--c3-inflight", type=int, default=3,
-                    help="C3 sub-line batches in flight: 3 / 4 / 6 gave 2.01 / 1.84 / 1.97 x 10^9 checks/s at p99 1.6 / 2.9 / 3.9 ms "
-                         "(profiles/r6z8_c3_inflight_ab.jsonl)")
+    ap.add_argument("--c3-inflight", type=int, default=6,
+                    help="C3 sub-line batches in flight: standalone 3 / 4 / 6 gave 2.01 / 1.84 / 1.97 x 10^9 checks/s at p99 "
+                         "1.6 / 2.9 / 3.9 ms (profiles/r6z8_c3_inflight_ab.jsonl), but inside the default line 3 was erratic "
+                         "(1.54-2.00 vs 1.98-2.05 x 10^9 at 6, profiles/r6z11_c3_subline.txt)")
     ap.add_argument("--c3-parity", type=int, default=200_000)
     ap.add_argument("--heavy-steps", type=int, default=20,
                     help="check mode, one rank: timed batches of the heavy-tail sub-line (SURVEY.md 8d's out-degree "
@@ -199,8 +200,8 @@ def parse(argv=None):
     if a.inflight is None:
         # --heavy-tail: 4 (round 6: 2 / 3 / 4 / 6 in flight gave 6.2 / 9.1 / 12.0 / 10.3 x 10^6 checks/s at p99
         # 21.4 / 21.5 / 22.4 / 40.6 ms per 62.5 k-check batch, profiles/r6t_operating_points.txt)
-        # --preset 1 (C3): 3 (3 / 4 / 6 gave 2.01 / 1.84 / 1.97 x 10^9, profiles/r6z8_c3_inflight_ab.jsonl)
-        a.inflight = 20 if a.mode == "expand" else (3 if a.preset else 4)
+        # --preset 1 (C3): 6, as the C3 sub-line (--c3-inflight)
+        a.inflight = 20 if a.mode == "expand" else (6 if a.preset else 4)
     if a.back_wgs is None:
         a.back_wgs = 1 if a.preset else 3
     if a.grid_wgs is None:

@@ -27,12 +27,12 @@ for P in $PARTS; do
     echo "c2 done"
     ;;
   c3)
-    timeout -k 10 240 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG}_c3 -o run --output-format csv -- python3 bench.py --preset 1 --tuples 1e7 --inflight 3 --steps 30 --warmup 6 $Q > gpurun_out/prof_${TAG}_c3.log 2>&1 || { echo "c3 trace failed"; exit 1; }
+    timeout -k 10 240 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG}_c3 -o run --output-format csv -- python3 bench.py --preset 1 --tuples 1e7 --inflight 6 --steps 30 --warmup 6 $Q > gpurun_out/prof_${TAG}_c3.log 2>&1 || { echo "c3 trace failed"; exit 1; }
     timeout -k 10 240 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG}_c3one -o run --output-format csv -- python3 bench.py --preset 1 --tuples 1e7 --inflight 1 --steps 10 --warmup 3 $Q > gpurun_out/prof_${TAG}_c3one.log 2>&1 || { echo "c3 one-batch trace failed"; exit 1; }
     ANCHOR=k_fsplit python3 scripts/timeline.py gpurun_out/prof_${TAG}_c3one/run_kernel_trace.csv > gpurun_out/timeline_${TAG}_c3.txt || true
-    pmc c3 "k_grid_level|${SK}|k_fsplit|k_back|k_resolve" --preset 1 --tuples 1e7 --inflight 3 --steps 6 --warmup 6 $Q || exit 1
+    pmc c3 "k_grid_level|${SK}|k_fsplit|k_back|k_resolve" --preset 1 --tuples 1e7 --inflight 6 --steps 6 --warmup 6 $Q || exit 1
     for K in k_grid_level $SK k_fsplit k_back k_resolve; do
-      python3 scripts/pmc_summary.py --kernel $K --fetch gpurun_out/pmc_${TAG}_c3_fetch --write gpurun_out/pmc_${TAG}_c3_write --tuples 1e7 --batch 1000000 --preset 1 --inflight 3 --out gpurun_out/pmc_${K}_p1.json > /dev/null || true
+      python3 scripts/pmc_summary.py --kernel $K --fetch gpurun_out/pmc_${TAG}_c3_fetch --write gpurun_out/pmc_${TAG}_c3_write --tuples 1e7 --batch 1000000 --preset 1 --inflight 6 --out gpurun_out/pmc_${K}_p1.json > /dev/null || true
     done
     echo "c3 done"
     ;;
