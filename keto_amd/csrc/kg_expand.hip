@@ -1166,6 +1166,10 @@ __global__ __launch_bounds__(256) void k_expand_gw(DevSnap s, const kg_set* __re
         int sp = 0;
         uint32_t st_chunks = 0, st_u[4] = {0, 0, 0, 0}, st_pops = 0;
         ExpFrame F{0, 0, 0, (uint32_t)len0, d0};
+        // a pushed child's first chunk, loaded as soon as the child is chosen (before its union record and
+        // the parent's leaves are emitted and the frame is pushed), so that work hides part of the load
+        GwEnt pre{};
+        bool have_pre = false;
         for (;;) {
           const uint64_t eb = F.rb, ee = F.rb + F.len;
           const bool can_expand = F.d - 1 >= 2;
@@ -1176,7 +1180,8 @@ __global__ __launch_bounds__(256) void k_expand_gw(DevSnap s, const kg_set* __re
             // walk is bound by its own instruction chain, ~1 us per chunk, not by the copy's latency)
             const uint32_t width = (uint32_t)min<uint64_t>(64, ee - at0);
             const bool valid = (uint32_t)lane < width;
-            const GwEnt x = E[valid ? at0 + lane : at0];
+            const GwEnt x = have_pre ? pre : E[valid ? at0 + lane : at0];
+            have_pre = false;
             st_chunks++;
             const bool is_set = valid && (x.sub & SET_BIT);
             const bool has_loc = is_set && x.loc != NONE;
@@ -1214,6 +1219,11 @@ __global__ __launch_bounds__(256) void k_expand_gw(DevSnap s, const kg_set* __re
               // p is wave-uniform (a ballot's first lane): v_readlane, no LDS round trip per field
               auto rl = [&](uint32_t v) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)p); };
               const uint32_t cloc = rl(x.loc), ccb = rl(x.cb), clen = rl(x.len);
+              // the child's first chunk (the pushed frame's first load; inline children read it below)
+              if (ccb != NONE) {
+                const uint32_t cw0 = min(64u, clen);
+                pre = E[(uint32_t)lane < cw0 ? (uint64_t)ccb + lane : (uint64_t)ccb];
+              }
               kg_tree_node u;
               u.type = 1;
               u.is_set = 1;
@@ -1241,7 +1251,7 @@ __global__ __launch_bounds__(256) void k_expand_gw(DevSnap s, const kg_set* __re
                 for (uint64_t c0 = ccb; c0 < (uint64_t)ccb + clen; c0 += 64) {
                   const uint32_t cw = (uint32_t)min<uint64_t>(64, (uint64_t)ccb + clen - c0);
                   const bool cv = (uint32_t)lane < cw;
-                  const GwEnt y = E[cv ? c0 + lane : c0];
+                  const GwEnt y = c0 == ccb ? pre : E[cv ? c0 + lane : c0];
                   st_chunks++;
                   const bool yset = cv && (y.sub & SET_BIT);
                   if (yset && y.loc != NONE) atomicOr(&vis[y.loc >> 5], 1u << (y.loc & 31));
@@ -1278,6 +1288,7 @@ __global__ __launch_bounds__(256) void k_expand_gw(DevSnap s, const kg_set* __re
               sp++;
               __builtin_amdgcn_wave_barrier();
               F = ExpFrame{ccb, cloc, 0, clen, F.d - 1};
+              have_pre = true;
               pushed = true;
               leave = true;
               break;
@@ -1291,6 +1302,7 @@ __global__ __launch_bounds__(256) void k_expand_gw(DevSnap s, const kg_set* __re
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
           sp--;
           st_pops++;
+          have_pre = false;  // (a pushed child always has rows, so its prefetched chunk was used)
           F = sp < XF ? s_fr[sp] : gstack[sp];
         }
         if (status == EXP_OK && S.ok && nbuf) {
