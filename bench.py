@@ -64,17 +64,19 @@ def parse(argv=None):
                     help="checks per sharded batch per rank (0: --batch).  C4 names 1-8 M; across ranks one batch "
                          "is in flight per rank, and 4 M amortises the exchanges' fixed cost: one-rank exchange "
                          "protocol 0.80 / 1.19 / 1.29 x 10^9 checks/s at 1 / 4 / 8 M (DESIGN.md 7f)")
-    ap.add_argument("--expand-steps", type=int, default=40,
+    ap.add_argument("--expand-steps", type=int, default=100,
                     help="check mode, one rank: timed calls of the C5 expand sub-line over the headline graph (0 = off; "
-                         "at least twice --expand-inflight, so every caller thread makes two calls)")
+                         "at least twice --expand-inflight).  100: five calls per caller thread -- a 40-call region (two "
+                         "per thread, ~0.1 s) read 2.55-3.78 x 10^7 trees/s on runs of the same code")
     ap.add_argument("--expand-inflight", type=int, default=20,
                     help="check mode: kg_expand_batch_device calls in flight in the C5 sub-line (one HIP stream each; "
                          "a call's critical path is its largest root's walk on one workgroup, so calls overlap: "
                          "12 / 16 / 20 gave 2.80 / 3.34 / 3.74 x 10^7 trees/s at 32 hardware queues, "
                          "profiles/r6t_operating_points.txt; 16 / 20 / 24 beside the headline graph 3.19 / 3.70 / "
                          "3.09 x 10^7, profiles/r6z9_c5_inflight.txt)")
-    ap.add_argument("--c3-steps", type=int, default=20,
-                    help="check mode, one rank: timed batches of the C3 sub-line (OPL rewrites; 0 = off)")
+    ap.add_argument("--c3-steps", type=int, default=60,
+                    help="check mode, one rank: timed batches of the C3 sub-line (OPL rewrites; 0 = off; 60: a ~30-ms "
+                         "region -- 20 batches were ~10 ms)")
     ap.add_argument("--c3-tuples", type=float, default=1e7, help="C3 sub-line graph size (BASELINE configs[2]: 10M)")
     ap.add_argument("--c3-inflight", type=int, default=6,
                     help="C3 sub-line batches in flight: standalone 3 / 4 / 6 gave 2.01 / 1.84 / 1.97 x 10^9 checks/s at p99 "
