@@ -1071,11 +1071,21 @@ def main():
     check_fn = L.kg_check_batch_packed_device if a.packed else L.kg_check_batch_device
     qbatch = (lambda k: dp_all[k % n_distinct]) if a.packed else (lambda k: dq_all[k % n_distinct])
 
+    # every pointer a step passes is taken here, once: a step's only Python work is the ctypes call itself
+    # (tensor views and data_ptr() per call were ~20 us of GIL-held work between a caller's batches)
+    q_ptrs = [qbatch(k).data_ptr() for k in range(n_batches)]
+    o_ptrs = [timed_out[k - warm].data_ptr() if k >= warm else None for k in range(n_batches)]
+    d_outp = [t.data_ptr() for t in douts]
+    e_ptrs = [t.data_ptr() for t in derrs]
+    s_ptrs = [C.c_void_p(st.cuda_stream) for st in streams]
+    c_name = "kg_check_batch_packed_device" if a.packed else "kg_check_batch_device"
+
     def step(p, k, st=None):
-        o = timed_out[k - warm] if k >= warm else douts[p]  # every timed batch keeps its own results
-        rc = check_fn(snap.handle, qbatch(k).data_ptr(), B, a.global_depth, o.data_ptr(),
-                      derrs[p].data_ptr(), C.byref(st) if st is not None else None, C.c_void_p(streams[p].cuda_stream))
-        _lib.check(rc, "kg_check_batch_packed_device" if a.packed else "kg_check_batch_device")
+        o = o_ptrs[k] if k >= warm else d_outp[p]  # every timed batch keeps its own results
+        rc = check_fn(snap.handle, q_ptrs[k], B, a.global_depth, o, e_ptrs[p], C.byref(st) if st is not None else None,
+                      s_ptrs[p])
+        if rc:
+            _lib.check(rc, c_name)
 
     def run_steps(k0, K, stats=None, lat=None):
         """Starts P host threads that run steps k0 .. k0+K-1 round-robin over the P streams once `go` is set."""
